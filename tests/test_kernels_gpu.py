@@ -1,0 +1,222 @@
+"""Numerics of every HIP kernel against a plain PyTorch fp32 reference of the same op."""
+import math
+
+import pytest
+import torch
+
+from xotorch_support_jetson_amd.ops import kernels as K
+from xotorch_support_jetson_amd.ops import reference as R
+from xotorch_support_jetson_amd.ops.rope import build_cos_sin
+
+pytestmark = pytest.mark.gpu
+
+
+def rel_err(a, b):
+  a, b = a.float(), b.float()
+  return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("D", [896, 2048, 8192])
+@pytest.mark.parametrize("with_res", [False, True])
+def test_rmsnorm(gpu, D, with_res):
+  torch.manual_seed(0)
+  x = torch.randn(37, D, device=gpu, dtype=torch.bfloat16)
+  w = torch.randn(D, device=gpu, dtype=torch.bfloat16)
+  res = torch.randn_like(x) if with_res else None
+  y, r = K.rmsnorm(x, w, 1e-5, res)
+  yr, rr = R.rmsnorm(x, w, 1e-5, res)
+  assert rel_err(y, yr) < 1e-2
+  if with_res:
+    assert torch.equal(r, rr)
+
+
+def test_rmsnorm_bwd(gpu):
+  torch.manual_seed(0)
+  x = torch.randn(40, 2048, device=gpu, dtype=torch.bfloat16)
+  w = torch.randn(2048, device=gpu, dtype=torch.bfloat16)
+  dy = torch.randn_like(x)
+  xr = x.float().requires_grad_()
+  wr = w.float().requires_grad_()
+  yr = xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-5) * wr
+  yr.backward(dy.float())
+  from xotorch_support_jetson_amd.ops._ext import require
+  dx = torch.empty_like(x)
+  dw = torch.zeros(2048, device=gpu, dtype=torch.float32)
+  require().rmsnorm_bwd(x, w, dy, dx, dw, 1e-5)
+  assert rel_err(dx, xr.grad) < 2e-2
+  assert rel_err(dw, wr.grad) < 1e-2
+
+
+def test_embedding_and_silu(gpu):
+  torch.manual_seed(0)
+  table = torch.randn(1000, 256, device=gpu, dtype=torch.bfloat16)
+  ids = torch.randint(0, 1000, (33,), device=gpu)
+  assert torch.equal(K.embedding(ids, table), table[ids])
+  gu = torch.randn(17, 2 * 512, device=gpu, dtype=torch.bfloat16)
+  assert rel_err(K.silu_mul(gu), R.silu_mul(gu)) < 1e-2
+
+
+@pytest.mark.parametrize("M,N,Kd", [(1, 1024, 2048), (7, 2048, 4096), (16, 512, 896), (33, 1024, 4096),
+                                    (64, 4096, 8192), (100, 1024, 2048), (128, 2048, 1024)])
+def test_gemm_skinny(gpu, M, N, Kd):
+  torch.manual_seed(0)
+  x = torch.randn(M, Kd, device=gpu, dtype=torch.bfloat16)
+  w = torch.randn(N, Kd, device=gpu, dtype=torch.bfloat16) / math.sqrt(Kd)
+  y = K.gemm(x, w, algo=1)
+  assert rel_err(y, R.linear(x, w)) < 1e-2
+  yf = K.gemm(x, w, algo=1, out_dtype=torch.float32)
+  assert rel_err(yf, R.linear(x, w)) < 1e-3
+
+
+def test_gemm_epilogues(gpu):
+  torch.manual_seed(0)
+  M, Kd, Fd = 24, 1024, 512
+  x = torch.randn(M, Kd, device=gpu, dtype=torch.bfloat16)
+  w = torch.randn(2 * Fd, Kd, device=gpu, dtype=torch.bfloat16) / 32
+  b = torch.randn(2 * Fd, device=gpu, dtype=torch.bfloat16)
+  r = torch.randn(M, 2 * Fd, device=gpu, dtype=torch.bfloat16)
+  y = K.gemm(x, w, bias=b, residual=r, epi="resid")
+  assert rel_err(y, R.linear(x, w, b) + r.float()) < 1e-2
+  # silu epilogue over 16-row interleaved gate/up
+  ys = K.gemm(x, w, epi="silu")
+  full = R.linear(x, w).view(M, Fd // 16, 2, 16)
+  ref = (torch.nn.functional.silu(full[:, :, 0]) * full[:, :, 1]).reshape(M, Fd)
+  assert rel_err(ys, ref) < 1e-2
+
+
+@pytest.mark.parametrize("M,N,Kd", [(256, 1024, 1024), (300, 520, 2048), (1024, 2048, 4096)])
+def test_gemm_tiled(gpu, M, N, Kd):
+  torch.manual_seed(0)
+  x = torch.randn(M, Kd, device=gpu, dtype=torch.bfloat16)
+  w = torch.randn(N, Kd, device=gpu, dtype=torch.bfloat16) / math.sqrt(Kd)
+  r = torch.randn(M, N, device=gpu, dtype=torch.bfloat16)
+  assert rel_err(K.gemm(x, w, algo=2), R.linear(x, w)) < 1e-2
+  assert rel_err(K.gemm(x, w, residual=r, epi="resid", algo=2), R.linear(x, w) + r.float()) < 1e-2
+
+
+def _make_cache(n_pages, Hkv, Dh, device):
+  kc = torch.randn(n_pages, Hkv, 64, Dh, device=device, dtype=torch.bfloat16)
+  vc = torch.randn(n_pages, Hkv, Dh, 64, device=device, dtype=torch.bfloat16)
+  return kc, vc
+
+
+@pytest.mark.parametrize("H,Hkv,Dh", [(32, 8, 64), (64, 8, 128), (14, 2, 64), (32, 8, 128)])
+def test_rope_kv_write(gpu, H, Hkv, Dh):
+  torch.manual_seed(0)
+  T = 19
+  cs = build_cos_sin(Dh, 4096, 500000.0, {"rope_type": "llama3", "factor": 32.0, "low_freq_factor": 1.0,
+                                          "high_freq_factor": 4.0, "original_max_position_embeddings": 8192},
+                     device=gpu)
+  qkv = torch.randn(T, (H + 2 * Hkv) * Dh, device=gpu, dtype=torch.bfloat16)
+  pos = torch.randint(0, 4000, (T,), device=gpu, dtype=torch.int32)
+  slots = torch.randperm(10 * 64, device=gpu)[:T].to(torch.int64)
+  slots[3] = -1
+  kc, vc = torch.zeros(10, Hkv, 64, Dh, device=gpu, dtype=torch.bfloat16), torch.zeros(10, Hkv, Dh, 64, device=gpu,
+                                                                                          dtype=torch.bfloat16)
+  kr, vr = kc.clone(), vc.clone()
+  q = K.rope_kv_write(qkv, pos, cs, slots, kc, vc, H, Hkv)
+  x = qkv.view(T, H + 2 * Hkv, Dh)
+  qr = R.rope(x[:, :H], pos, cs)
+  R.write_kv(R.rope(x[:, H:H + Hkv], pos, cs), x[:, H + Hkv:], slots, kr, vr)
+  assert rel_err(q, qr) < 1e-2
+  assert rel_err(kc, kr) < 1e-2
+  assert torch.equal(vc, vr)
+
+
+@pytest.mark.parametrize("H,Hkv,Dh", [(64, 8, 128), (32, 8, 64), (14, 2, 64), (32, 4, 128)])
+@pytest.mark.parametrize("ctx", [[1, 64, 65, 700], [2100, 5, 1300, 64]])
+def test_attn_decode(gpu, H, Hkv, Dh, ctx):
+  torch.manual_seed(0)
+  B = len(ctx)
+  maxb = 40
+  kc, vc = _make_cache(B * maxb + 3, Hkv, Dh, gpu)
+  bt = torch.randperm(B * maxb + 3, device=gpu)[:B * maxb].view(B, maxb).to(torch.int32).contiguous()
+  cl = torch.tensor(ctx, device=gpu, dtype=torch.int32)
+  q = torch.randn(B, H, Dh, device=gpu, dtype=torch.bfloat16)
+  scale = 1 / math.sqrt(Dh)
+  ref = R.attn_decode(q, kc, vc, bt, cl, scale)
+  for ppp in (4, 8):
+    ws = K.DecodeWorkspace(B, H, Dh, maxb * 64, gpu, pages_per_part=ppp)
+    out = K.attn_decode(q, kc, vc, bt, cl, scale, ws)
+    assert rel_err(out, ref) < 2e-2, ppp
+
+
+@pytest.mark.parametrize("H,Hkv,Dh", [(32, 8, 64), (64, 8, 128), (14, 2, 64)])
+def test_attn_prefill(gpu, H, Hkv, Dh):
+  torch.manual_seed(0)
+  qlens, ctxs = [5, 130, 1, 77], [5, 200, 64, 77]
+  B = len(qlens)
+  maxb = 8
+  kc, vc = _make_cache(B * maxb, Hkv, Dh, gpu)
+  bt = torch.randperm(B * maxb, device=gpu).view(B, maxb).to(torch.int32).contiguous()
+  cu = torch.tensor([0] + list(torch.tensor(qlens).cumsum(0)), device=gpu, dtype=torch.int32)
+  cl = torch.tensor(ctxs, device=gpu, dtype=torch.int32)
+  q = torch.randn(sum(qlens), H, Dh, device=gpu, dtype=torch.bfloat16)
+  scale = 1 / math.sqrt(Dh)
+  out = K.attn_prefill(q, kc, vc, bt, cu, cl, max(qlens), scale)
+  ref = R.attn_prefill(q, kc, vc, bt, cu, cl, scale)
+  assert rel_err(out, ref) < 2e-2
+
+
+def test_sample_greedy_and_topk(gpu):
+  torch.manual_seed(0)
+  B, V = 6, 128256
+  logits = torch.randn(B, V, device=gpu) * 3
+  so = torch.tensor([1234, 0], device=gpu, dtype=torch.int64)
+  greedy = K.sample(logits, torch.zeros(B, device=gpu), 35, so)
+  assert torch.equal(greedy.cpu(), logits.argmax(-1).int().cpu())
+  temps = torch.full((B,), 0.8, device=gpu)
+  mask = R.topk_mask(logits, 35)
+  seen = set()
+  for step in range(20):
+    so[1] = step
+    tok = K.sample(logits, temps, 35, so)
+    assert bool(mask[torch.arange(B, device=gpu), tok.long()].all())
+    seen.add(tuple(tok.tolist()))
+  assert len(seen) > 1  # actually random across offsets
+  # top_k = 1 is greedy even with temperature
+  assert torch.equal(K.sample(logits, temps, 1, so).cpu(), greedy.cpu())
+
+
+def test_sample_distribution(gpu):
+  # exponential race == categorical(softmax(l / T)) restricted to top-k
+  logits = torch.tensor([[2.0, 1.0, 0.5, 0.0, -1.0] + [-30.0] * 59], device=gpu)
+  B = 4096
+  lg = logits.expand(B, -1).contiguous()
+  so = torch.tensor([7, 3], device=gpu, dtype=torch.int64)
+  tok = K.sample(lg, torch.ones(B, device=gpu), 3, so)
+  counts = torch.bincount(tok.long(), minlength=64).float().cpu() / B
+  p = torch.softmax(torch.tensor([2.0, 1.0, 0.5]), 0)
+  assert counts[3:].sum() == 0
+  assert torch.allclose(counts[:3], p, atol=0.03)
+
+
+def test_cross_entropy_and_adamw(gpu):
+  torch.manual_seed(0)
+  from xotorch_support_jetson_amd.ops._ext import require
+  C = require()
+  T, V = 9, 50000
+  x = torch.randn(T, V, device=gpu, dtype=torch.bfloat16)
+  tgt = torch.randint(0, V, (T,), device=gpu, dtype=torch.int32)
+  tgt[2] = -100
+  loss, lse = torch.empty(T, device=gpu), torch.empty(T, device=gpu)
+  C.ce_fwd(x, tgt, loss, lse)
+  lr_, lser = R.cross_entropy(x, tgt)
+  assert torch.allclose(loss, lr_, atol=1e-3, rtol=1e-4)
+  dx = torch.empty_like(x)
+  C.ce_bwd(x, tgt, lse, torch.full((T,), 0.5, device=gpu), dx)
+  xr = x.float().requires_grad_()
+  l = torch.nn.functional.cross_entropy(xr, tgt.long(), ignore_index=-100, reduction="none")
+  (l * 0.5).sum().backward()
+  assert rel_err(dx, xr.grad) < 1e-2
+  # AdamW vs torch.optim.AdamW
+  p = torch.randn(1000, device=gpu)
+  g = torch.randn(1000, device=gpu)
+  m, v = torch.zeros_like(p), torch.zeros_like(p)
+  pt = p.clone().requires_grad_()
+  opt = torch.optim.AdamW([pt], lr=1e-2, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1)
+  for step in range(1, 4):
+    C.adamw(p, g, m, v, None, 1e-2, 0.9, 0.95, 1e-8, 0.1, step, 1.0)
+    pt.grad = g.clone()
+    opt.step()
+  assert torch.allclose(p, pt.detach(), atol=1e-5)

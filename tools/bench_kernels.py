@@ -1,0 +1,132 @@
+"""Kernel micro-benchmarks on one MI355X: decode/prefill GEMMs (vs hipBLASLt through torch.matmul),
+paged decode attention (HBM GB/s), prefill attention (TFLOP/s), RMSNorm, sampling.
+
+  python tools/bench_kernels.py [--quick] [--json out.json]
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from xotorch_support_jetson_amd.ops import kernels as K  # noqa: E402
+
+
+def timeit(fn, iters=20, warmup=3):
+  for _ in range(warmup):
+    fn()
+  torch.cuda.synchronize()
+  st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+  ts = []
+  for _ in range(iters):
+    st.record()
+    fn()
+    en.record()
+    en.synchronize()
+    ts.append(st.elapsed_time(en))
+  ts.sort()
+  return ts[len(ts) // 2] * 1e-3  # median seconds
+
+
+def main():
+  ap = argparse.ArgumentParser()
+  ap.add_argument("--quick", action="store_true")
+  ap.add_argument("--json", default=None)
+  args = ap.parse_args()
+  dev = torch.device("cuda:0")
+  res = {"gemm": [], "attn_decode": [], "attn_prefill": [], "misc": []}
+  torch.manual_seed(0)
+  # Llama-3-70B projections (N, K): qkv, o, gate_up, down, lm_head
+  shapes = [("qkv", 10240, 8192), ("o", 8192, 8192), ("gate_up", 57344, 8192), ("down", 8192, 28672),
+            ("lm_head", 128256, 8192)]
+  Ms = [1, 16, 32, 64, 128] if not args.quick else [16, 64, 128]
+  for name, N, Kd in shapes:
+    w = torch.randn(N, Kd, device=dev, dtype=torch.bfloat16) * 0.02
+    for M in Ms:
+      x = torch.randn(M, Kd, device=dev, dtype=torch.bfloat16)
+      epi = "silu" if name == "gate_up" else "none"
+      y_ours = K.gemm(x, w, epi=epi)
+      t_ours = timeit(lambda: K.gemm(x, w, epi=epi, out=y_ours))
+      yb = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+      t_blas = timeit(lambda: torch.matmul(x, w.t(), out=yb))
+      bytes_ = N * Kd * 2 + M * Kd * 2 + M * N * 2
+      r = dict(op=name, M=M, N=N, K=Kd, us_ours=t_ours * 1e6, us_hipblaslt=t_blas * 1e6,
+               gbps_ours=bytes_ / t_ours / 1e9, gbps_hipblaslt=bytes_ / t_blas / 1e9, speedup=t_blas / t_ours)
+      res["gemm"].append(r)
+      print(json.dumps(r), flush=True)
+    del w
+  # prefill GEMMs
+  for M, N, Kd in [(2048, 10240, 8192), (4096, 8192, 8192), (4096, 28672, 8192)]:
+    w = torch.randn(N, Kd, device=dev, dtype=torch.bfloat16) * 0.02
+    x = torch.randn(M, Kd, device=dev, dtype=torch.bfloat16)
+    y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    t_ours = timeit(lambda: K.gemm(x, w, out=y, algo=2), iters=10)
+    t_blas = timeit(lambda: torch.matmul(x, w.t(), out=y), iters=10)
+    fl = 2 * M * N * Kd
+    r = dict(op="prefill_gemm", M=M, N=N, K=Kd, tflops_ours=fl / t_ours / 1e12, tflops_hipblaslt=fl / t_blas / 1e12)
+    res["gemm"].append(r)
+    print(json.dumps(r), flush=True)
+    del w, x, y
+  # decode attention, Llama-70B heads
+  H, Hkv, Dh = 64, 8, 128
+  for B, ctx in [(1, 1024), (16, 2048), (64, 1024), (128, 1024), (128, 4096)]:
+    npg = -(-ctx // 64)
+    kc = torch.randn(B * npg, Hkv, 64, Dh, device=dev, dtype=torch.bfloat16)
+    vc = torch.randn(B * npg, Hkv, Dh, 64, device=dev, dtype=torch.bfloat16)
+    bt = torch.arange(B * npg, device=dev, dtype=torch.int32).view(B, npg)
+    cl = torch.full((B,), ctx, device=dev, dtype=torch.int32)
+    q = torch.randn(B, H, Dh, device=dev, dtype=torch.bfloat16)
+    ppp = K.choose_pages_per_part(B, Hkv, ctx)
+    ws = K.DecodeWorkspace(B, H, Dh, ctx, dev, ppp)
+    out = torch.empty_like(q)
+    t = timeit(lambda: K.attn_decode(q, kc, vc, bt, cl, 1 / math.sqrt(Dh), ws, out))
+    bytes_ = 2 * B * ctx * Hkv * Dh * 2
+    r = dict(B=B, ctx=ctx, us=t * 1e6, gbps=bytes_ / t / 1e9, pages_per_part=ppp)
+    res["attn_decode"].append(r)
+    print(json.dumps({"attn_decode": r}), flush=True)
+    del kc, vc
+  # prefill attention
+  for B, L in [(1, 2048), (4, 1024)]:
+    npg = -(-L // 64)
+    kc = torch.randn(B * npg, Hkv, 64, Dh, device=dev, dtype=torch.bfloat16)
+    vc = torch.randn(B * npg, Hkv, Dh, 64, device=dev, dtype=torch.bfloat16)
+    bt = torch.arange(B * npg, device=dev, dtype=torch.int32).view(B, npg)
+    cl = torch.full((B,), L, device=dev, dtype=torch.int32)
+    cu = torch.arange(0, B + 1, device=dev, dtype=torch.int32) * L
+    q = torch.randn(B * L, H, Dh, device=dev, dtype=torch.bfloat16)
+    out = torch.empty_like(q)
+    t = timeit(lambda: K.attn_prefill(q, kc, vc, bt, cu, cl, L, 1 / math.sqrt(Dh), out), iters=10)
+    fl = 4 * B * H * Dh * L * L / 2
+    qs = q.view(B, L, H, Dh).transpose(1, 2)
+    ks = torch.randn(B, Hkv, L, Dh, device=dev, dtype=torch.bfloat16).repeat_interleave(H // Hkv, 1)
+    vs = torch.randn_like(ks)
+    t_sdpa = timeit(lambda: torch.nn.functional.scaled_dot_product_attention(qs, ks, vs, is_causal=True), iters=10)
+    r = dict(B=B, L=L, tflops_ours=fl / t / 1e12, tflops_torch_sdpa=fl / t_sdpa / 1e12)
+    res["attn_prefill"].append(r)
+    print(json.dumps({"attn_prefill": r}), flush=True)
+  # rmsnorm + sampling
+  x = torch.randn(128, 8192, device=dev, dtype=torch.bfloat16)
+  w = torch.randn(8192, device=dev, dtype=torch.bfloat16)
+  r_ = torch.randn_like(x)
+  o, ro = torch.empty_like(x), torch.empty_like(x)
+  t = timeit(lambda: K.rmsnorm(x, w, 1e-5, r_, o, ro))
+  res["misc"].append(dict(op="rmsnorm_res_128x8192", us=t * 1e6))
+  logits = torch.randn(128, 128256, device=dev)
+  so = torch.tensor([1, 0], device=dev, dtype=torch.int64)
+  tok = torch.empty(128, device=dev, dtype=torch.int32)
+  t = timeit(lambda: K.sample(logits, torch.full((128,), 0.7, device=dev), 35, so, tok))
+  res["misc"].append(dict(op="sample_topk35_128x128256", us=t * 1e6))
+  t = timeit(lambda: K.sample(logits, torch.zeros(128, device=dev), 35, so, tok))
+  res["misc"].append(dict(op="sample_greedy_128x128256", us=t * 1e6))
+  print(json.dumps(res["misc"]), flush=True)
+  if args.json:
+    with open(args.json, "w") as f:
+      json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+  main()

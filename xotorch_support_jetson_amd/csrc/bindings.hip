@@ -1,0 +1,322 @@
+// Python bindings of the gfx950 kernel library.  Every entry point validates device, dtype,
+// contiguity and shapes before launching (a kernel never sees a shape it was not written for);
+// outputs are preallocated by the caller so all of these can be captured into a HIP graph.
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include "kernels.h"
+
+namespace {
+
+#define XCHECK(cond, ...) TORCH_CHECK(cond, "xot kernel: ", __VA_ARGS__)
+#define CHECK_GPU(x) XCHECK((x).is_cuda(), #x " must be a GPU tensor")
+#define CHECK_CONTIG(x) XCHECK((x).is_contiguous(), #x " must be contiguous")
+#define CHECK_DT(x, dt) XCHECK((x).scalar_type() == (dt), #x " must be " #dt)
+#define CHECK_BF16(x) \
+  CHECK_GPU(x);       \
+  CHECK_DT(x, at::kBFloat16)
+
+template <typename... Ts>
+bool all_contig_gpu(const Ts&... ts) {
+  return ((ts.is_contiguous() && ts.is_cuda()) && ...);
+}
+
+inline hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
+inline uint16_t* bf(const at::Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr()); }
+inline uint16_t* bf_opt(const c10::optional<at::Tensor>& t) {
+  return t.has_value() ? reinterpret_cast<uint16_t*>(t->data_ptr()) : nullptr;
+}
+
+void rmsnorm(const at::Tensor& x, const at::Tensor& w, at::Tensor& out, const c10::optional<at::Tensor>& res,
+             const c10::optional<at::Tensor>& res_out, double eps) {
+  CHECK_BF16(x);
+  CHECK_BF16(w);
+  CHECK_BF16(out);
+  CHECK_CONTIG(x);
+  CHECK_CONTIG(out);
+  const int64_t D = x.size(-1), rows = x.numel() / D;
+  XCHECK(D % 8 == 0 && D <= 16384, "rmsnorm: D must be a multiple of 8 and <= 16384");
+  XCHECK(w.numel() == D && out.numel() == x.numel(), "rmsnorm: shape mismatch");
+  if (res.has_value()) {
+    XCHECK(res_out.has_value(), "rmsnorm: residual needs residual_out");
+    CHECK_BF16((*res));
+    CHECK_BF16((*res_out));
+    XCHECK(res->is_contiguous() && res_out->is_contiguous(), "rmsnorm: residual must be contiguous");
+    XCHECK(res->numel() == x.numel() && res_out->numel() == x.numel(), "rmsnorm: residual shape mismatch");
+  }
+  xot::launch_rmsnorm(bf(x), bf_opt(res), bf(w), bf(out), bf_opt(res_out), (int)rows, (int)D, (float)eps,
+                      cur_stream());
+}
+
+void rmsnorm_bwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& dy, at::Tensor& dx, at::Tensor& dw,
+                 double eps) {
+  CHECK_BF16(x);
+  CHECK_BF16(w);
+  CHECK_BF16(dy);
+  CHECK_BF16(dx);
+  CHECK_GPU(dw);
+  CHECK_DT(dw, at::kFloat);
+  CHECK_CONTIG(x);
+  CHECK_CONTIG(dy);
+  CHECK_CONTIG(dx);
+  const int64_t D = x.size(-1), rows = x.numel() / D;
+  XCHECK(D % 8 == 0 && D <= 16384, "rmsnorm_bwd: bad D");
+  XCHECK(dy.numel() == x.numel() && dx.numel() == x.numel() && dw.numel() == D && w.numel() == D,
+         "rmsnorm_bwd: shape mismatch");
+  xot::launch_rmsnorm_bwd(bf(x), bf(w), bf(dy), bf(dx), dw.data_ptr<float>(), (int)rows, (int)D, (float)eps,
+                          cur_stream());
+}
+
+void embedding(const at::Tensor& ids, const at::Tensor& table, at::Tensor& out) {
+  CHECK_GPU(ids);
+  CHECK_DT(ids, at::kInt);
+  CHECK_BF16(table);
+  CHECK_BF16(out);
+  CHECK_CONTIG(ids);
+  CHECK_CONTIG(table);
+  CHECK_CONTIG(out);
+  const int64_t T = ids.numel(), D = table.size(1);
+  XCHECK(D % 8 == 0 && out.numel() == T * D, "embedding: shape mismatch");
+  xot::launch_embedding(ids.data_ptr<int32_t>(), bf(table), bf(out), (int)T, (int)D, (int)table.size(0),
+                        cur_stream());
+}
+
+void silu_mul(const at::Tensor& gu, at::Tensor& out) {
+  CHECK_BF16(gu);
+  CHECK_BF16(out);
+  CHECK_CONTIG(gu);
+  CHECK_CONTIG(out);
+  const int64_t F = out.size(-1), T = out.numel() / F;
+  XCHECK(F % 8 == 0 && gu.numel() == 2 * T * F && gu.size(-1) == 2 * F, "silu_mul: shape mismatch");
+  xot::launch_silu_mul(bf(gu), bf(out), (int)T, (int)F, cur_stream());
+}
+
+void silu_mul_bwd(const at::Tensor& gu, const at::Tensor& dout, at::Tensor& dgu) {
+  CHECK_BF16(gu);
+  CHECK_BF16(dout);
+  CHECK_BF16(dgu);
+  CHECK_CONTIG(gu);
+  CHECK_CONTIG(dout);
+  CHECK_CONTIG(dgu);
+  const int64_t F = dout.size(-1), T = dout.numel() / F;
+  XCHECK(F % 8 == 0 && gu.numel() == 2 * T * F && dgu.numel() == gu.numel(), "silu_mul_bwd: shape mismatch");
+  xot::launch_silu_mul_bwd(bf(gu), bf(dout), bf(dgu), (int)T, (int)F, cur_stream());
+}
+
+void rope_kv_write(const at::Tensor& qkv, const at::Tensor& pos, const at::Tensor& cos_sin, const at::Tensor& slots,
+                   at::Tensor& q_out, at::Tensor& k_cache, at::Tensor& v_cache, int64_t H, int64_t Hkv) {
+  CHECK_BF16(qkv);
+  CHECK_BF16(q_out);
+  CHECK_BF16(k_cache);
+  CHECK_BF16(v_cache);
+  CHECK_GPU(pos);
+  CHECK_DT(pos, at::kInt);
+  CHECK_GPU(slots);
+  CHECK_DT(slots, at::kLong);
+  CHECK_GPU(cos_sin);
+  CHECK_DT(cos_sin, at::kFloat);
+  XCHECK(all_contig_gpu(qkv, pos, cos_sin, slots, q_out), "rope_kv_write: non-contiguous");
+  XCHECK(k_cache.is_contiguous() && v_cache.is_contiguous(), "rope_kv_write: cache non-contiguous");
+  XCHECK(k_cache.dim() == 4 && v_cache.dim() == 4, "rope_kv_write: caches must be 4-D");
+  const int64_t T = pos.numel(), Dh = k_cache.size(3), BS = k_cache.size(2), nb = k_cache.size(0);
+  XCHECK(k_cache.size(1) == Hkv && v_cache.size(0) == nb && v_cache.size(1) == Hkv && v_cache.size(2) == Dh &&
+             v_cache.size(3) == BS,
+         "rope_kv_write: cache layout must be K[nb,Hkv,BS,Dh], V[nb,Hkv,Dh,BS]");
+  XCHECK(Dh % 8 == 0 && qkv.numel() == T * (H + 2 * Hkv) * Dh, "rope_kv_write: qkv shape mismatch");
+  XCHECK(q_out.numel() == T * H * Dh && slots.numel() == T, "rope_kv_write: q_out/slots shape mismatch");
+  XCHECK(cos_sin.dim() == 2 && cos_sin.size(1) == Dh, "rope_kv_write: cos_sin must be [max_pos, Dh]");
+  xot::launch_rope_kv_write(bf(qkv), pos.data_ptr<int32_t>(), cos_sin.data_ptr<float>(), slots.data_ptr<int64_t>(),
+                            bf(q_out), bf(k_cache), bf(v_cache), (int)T, (int)H, (int)Hkv, (int)Dh, (int)BS,
+                            (int)cos_sin.size(0), (long)(nb * BS), cur_stream());
+}
+
+void rope_apply(const at::Tensor& x, at::Tensor& y, const at::Tensor& pos, const at::Tensor& cos_sin, int64_t nh,
+                int64_t Dh, bool inverse) {
+  CHECK_BF16(x);
+  CHECK_BF16(y);
+  CHECK_GPU(pos);
+  CHECK_DT(pos, at::kInt);
+  CHECK_DT(cos_sin, at::kFloat);
+  XCHECK(x.dim() == 2 && y.dim() == 2 && x.stride(1) == 1 && y.stride(1) == 1, "rope_apply: x/y must be 2-D rows");
+  const int64_t T = x.size(0);
+  XCHECK(y.size(0) == T && pos.numel() == T && x.size(1) >= nh * Dh && y.size(1) >= nh * Dh && Dh % 8 == 0,
+         "rope_apply: shape mismatch");
+  XCHECK(cos_sin.dim() == 2 && cos_sin.size(1) == Dh && cos_sin.is_contiguous(), "rope_apply: bad cos_sin");
+  xot::launch_rope_apply(bf(x), bf(y), pos.data_ptr<int32_t>(), cos_sin.data_ptr<float>(), (int)T, (int)nh, (int)Dh,
+                         x.stride(0), y.stride(0), (int)cos_sin.size(0), inverse, cur_stream());
+}
+
+// epi: 0 none, 1 residual add, 2 silu(gate)*up (gate/up interleaved in 16-row tiles)
+// algo: 0 auto, 1 skinny, 2 tiled.  nt: n-tiles per wave for the skinny kernel (1 or 2)
+void gemm(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const c10::optional<at::Tensor>& bias,
+          const c10::optional<at::Tensor>& res, int64_t epi, int64_t algo, int64_t nt) {
+  CHECK_BF16(x);
+  CHECK_BF16(w);
+  CHECK_GPU(y);
+  XCHECK(x.dim() == 2 && w.dim() == 2 && y.dim() == 2, "gemm: x, w, y must be 2-D");
+  XCHECK(x.stride(1) == 1 && w.is_contiguous() && y.stride(1) == 1, "gemm: rows must be contiguous");
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
+  XCHECK(w.size(1) == K, "gemm: K mismatch");
+  const bool f32 = y.scalar_type() == at::kFloat;
+  XCHECK(f32 || y.scalar_type() == at::kBFloat16, "gemm: y must be bf16 or fp32");
+  XCHECK(y.size(0) == M && y.size(1) == (epi == 2 ? N / 2 : N), "gemm: y shape mismatch");
+  if (bias.has_value()) {
+    CHECK_BF16((*bias));
+    XCHECK(bias->numel() == N && bias->is_contiguous(), "gemm: bias shape mismatch");
+  }
+  int64_t ldr = 0;
+  if (epi == 1) {
+    XCHECK(res.has_value(), "gemm: residual epilogue needs res");
+    CHECK_BF16((*res));
+    XCHECK(res->dim() == 2 && res->size(0) == M && res->size(1) == N && res->stride(1) == 1, "gemm: res shape");
+    ldr = res->stride(0);
+  }
+  if (algo == 0) algo = (M <= 128 || epi == 2) ? 1 : 2;
+  int rc;
+  if (algo == 1)
+    rc = xot::launch_gemm_skinny(bf(x), (int)x.stride(0), bf(w), (int)K, bf_opt(bias), epi == 1 ? bf(*res) : nullptr,
+                                 (int)ldr, y.data_ptr(), (int)y.stride(0), f32, (int)epi, (int)M, (int)N, (int)K,
+                                 (int)nt, cur_stream());
+  else
+    rc = xot::launch_gemm_tiled(bf(x), (int)x.stride(0), bf(w), (int)K, bf_opt(bias), epi == 1 ? bf(*res) : nullptr,
+                                (int)ldr, y.data_ptr(), (int)y.stride(0), f32, (int)epi, (int)M, (int)N, (int)K,
+                                cur_stream());
+  XCHECK(rc == 0, "gemm: unsupported shape M=", M, " N=", N, " K=", K, " epi=", epi, " algo=", algo);
+}
+
+void attn_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
+                 const at::Tensor& block_tables, const at::Tensor& ctx_lens, at::Tensor& out, at::Tensor& ws_o,
+                 at::Tensor& ws_ml, int64_t pages_per_part, int64_t nparts, double scale) {
+  CHECK_BF16(q);
+  CHECK_BF16(k_cache);
+  CHECK_BF16(v_cache);
+  CHECK_BF16(out);
+  CHECK_DT(block_tables, at::kInt);
+  CHECK_DT(ctx_lens, at::kInt);
+  CHECK_DT(ws_o, at::kFloat);
+  CHECK_DT(ws_ml, at::kFloat);
+  XCHECK(all_contig_gpu(q, k_cache, v_cache, block_tables, ctx_lens, out, ws_o, ws_ml),
+         "attn_decode: all tensors must be contiguous GPU tensors");
+  XCHECK(q.dim() == 3 && k_cache.dim() == 4 && v_cache.dim() == 4, "attn_decode: q [B,H,Dh], caches 4-D");
+  const int64_t B = q.size(0), H = q.size(1), Dh = q.size(2), Hkv = k_cache.size(1), nb = k_cache.size(0);
+  XCHECK(k_cache.size(2) == 64 && k_cache.size(3) == Dh && v_cache.size(2) == Dh && v_cache.size(3) == 64 &&
+             v_cache.size(0) == nb && v_cache.size(1) == Hkv,
+         "attn_decode: cache layout K[nb,Hkv,64,Dh] V[nb,Hkv,Dh,64]");
+  XCHECK(block_tables.dim() == 2 && block_tables.size(0) >= B && ctx_lens.numel() >= B, "attn_decode: tables");
+  XCHECK(out.numel() == B * H * Dh, "attn_decode: out shape");
+  XCHECK(pages_per_part >= 1 && nparts >= 1, "attn_decode: bad partitioning");
+  if (nparts > 1)
+    XCHECK(ws_o.numel() >= B * H * nparts * Dh && ws_ml.numel() >= B * H * nparts * 2, "attn_decode: workspace small");
+  const int rc = xot::launch_attn_decode(bf(q), bf(k_cache), bf(v_cache), block_tables.data_ptr<int32_t>(),
+                                         (int)block_tables.size(1), ctx_lens.data_ptr<int32_t>(), bf(out),
+                                         ws_o.data_ptr<float>(), ws_ml.data_ptr<float>(), (int)B, (int)H, (int)Hkv,
+                                         (int)Dh, (int)pages_per_part, (int)nparts, (float)scale, (int)nb,
+                                         cur_stream());
+  XCHECK(rc == 0, "attn_decode: unsupported H=", H, " Hkv=", Hkv, " Dh=", Dh);
+}
+
+void attn_prefill(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
+                  const at::Tensor& block_tables, const at::Tensor& cu_q, const at::Tensor& ctx_lens, at::Tensor& out,
+                  int64_t max_qlen, double scale) {
+  CHECK_BF16(q);
+  CHECK_BF16(k_cache);
+  CHECK_BF16(v_cache);
+  CHECK_BF16(out);
+  CHECK_DT(block_tables, at::kInt);
+  CHECK_DT(cu_q, at::kInt);
+  CHECK_DT(ctx_lens, at::kInt);
+  XCHECK(all_contig_gpu(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, out),
+         "attn_prefill: all tensors must be contiguous GPU tensors");
+  XCHECK(q.dim() == 3, "attn_prefill: q must be [T,H,Dh]");
+  const int64_t H = q.size(1), Dh = q.size(2), Hkv = k_cache.size(1), nb = k_cache.size(0);
+  const int64_t B = ctx_lens.numel();
+  XCHECK(cu_q.numel() == B + 1 && block_tables.dim() == 2 && block_tables.size(0) >= B, "attn_prefill: tables");
+  XCHECK(k_cache.size(2) == 64 && k_cache.size(3) == Dh && v_cache.size(2) == Dh && v_cache.size(3) == 64,
+         "attn_prefill: cache layout");
+  XCHECK(out.numel() == q.numel(), "attn_prefill: out shape");
+  const int rc = xot::launch_attn_prefill(bf(q), bf(k_cache), bf(v_cache), block_tables.data_ptr<int32_t>(),
+                                          (int)block_tables.size(1), cu_q.data_ptr<int32_t>(),
+                                          ctx_lens.data_ptr<int32_t>(), bf(out), (int)B, (int)max_qlen, (int)H,
+                                          (int)Hkv, (int)Dh, (float)scale, (int)nb, cur_stream());
+  XCHECK(rc == 0, "attn_prefill: unsupported H=", H, " Hkv=", Hkv, " Dh=", Dh);
+}
+
+void sample(const at::Tensor& logits, const at::Tensor& temps, int64_t top_k, const at::Tensor& seed_off,
+            at::Tensor& out) {
+  CHECK_GPU(logits);
+  CHECK_DT(logits, at::kFloat);
+  CHECK_DT(temps, at::kFloat);
+  CHECK_DT(seed_off, at::kLong);
+  CHECK_DT(out, at::kInt);
+  XCHECK(logits.dim() == 2 && logits.stride(1) == 1, "sample: logits must be [B, V] with contiguous rows");
+  const int64_t B = logits.size(0), V = logits.size(1);
+  XCHECK(temps.numel() >= B && out.numel() >= B && seed_off.numel() >= 2, "sample: shape mismatch");
+  xot::launch_sample(logits.data_ptr<float>(), logits.stride(0), (int)B, (int)V, temps.data_ptr<float>(), (int)top_k,
+                     seed_off.data_ptr<int64_t>(), out.data_ptr<int32_t>(), cur_stream());
+}
+
+void ce_fwd(const at::Tensor& x, const at::Tensor& tgt, at::Tensor& loss, at::Tensor& lse) {
+  CHECK_GPU(x);
+  XCHECK(x.dim() == 2 && x.stride(1) == 1, "ce_fwd: x must be [T, V]");
+  const bool f32 = x.scalar_type() == at::kFloat;
+  XCHECK(f32 || x.scalar_type() == at::kBFloat16, "ce_fwd: x must be fp32 or bf16");
+  CHECK_DT(tgt, at::kInt);
+  CHECK_DT(loss, at::kFloat);
+  CHECK_DT(lse, at::kFloat);
+  const int64_t T = x.size(0);
+  XCHECK(tgt.numel() == T && loss.numel() == T && lse.numel() == T, "ce_fwd: shape mismatch");
+  xot::launch_ce_fwd(x.data_ptr(), f32, x.stride(0), (int)T, (int)x.size(1), tgt.data_ptr<int32_t>(),
+                     loss.data_ptr<float>(), lse.data_ptr<float>(), cur_stream());
+}
+
+void ce_bwd(const at::Tensor& x, const at::Tensor& tgt, const at::Tensor& lse, const at::Tensor& gscale,
+            at::Tensor& dx) {
+  CHECK_GPU(x);
+  XCHECK(x.dim() == 2 && x.stride(1) == 1 && dx.dim() == 2 && dx.stride(1) == 1, "ce_bwd: 2-D rows");
+  const bool f32 = x.scalar_type() == at::kFloat;
+  XCHECK(f32 || x.scalar_type() == at::kBFloat16, "ce_bwd: x must be fp32 or bf16");
+  CHECK_BF16(dx);
+  const int64_t T = x.size(0);
+  XCHECK(dx.size(0) == T && dx.size(1) == x.size(1) && tgt.numel() == T && lse.numel() == T && gscale.numel() == T,
+         "ce_bwd: shape mismatch");
+  xot::launch_ce_bwd(x.data_ptr(), f32, x.stride(0), (int)T, (int)x.size(1), tgt.data_ptr<int32_t>(),
+                     lse.data_ptr<float>(), gscale.data_ptr<float>(), bf(dx), dx.stride(0), cur_stream());
+}
+
+void adamw(at::Tensor& p, const at::Tensor& g, at::Tensor& m, at::Tensor& v, const c10::optional<at::Tensor>& p_bf16,
+           double lr, double b1, double b2, double eps, double wd, int64_t step, double gscale) {
+  CHECK_DT(p, at::kFloat);
+  CHECK_DT(m, at::kFloat);
+  CHECK_DT(v, at::kFloat);
+  const bool gf32 = g.scalar_type() == at::kFloat;
+  XCHECK(gf32 || g.scalar_type() == at::kBFloat16, "adamw: grad must be fp32 or bf16");
+  XCHECK(all_contig_gpu(p, g, m, v), "adamw: contiguous GPU tensors");
+  const int64_t n = p.numel();
+  XCHECK(g.numel() == n && m.numel() == n && v.numel() == n, "adamw: shape mismatch");
+  if (p_bf16.has_value()) {
+    CHECK_BF16((*p_bf16));
+    XCHECK(p_bf16->numel() == n && p_bf16->is_contiguous(), "adamw: p_bf16 shape");
+  }
+  xot::launch_adamw(p.data_ptr<float>(), g.data_ptr(), gf32, m.data_ptr<float>(), v.data_ptr<float>(),
+                    bf_opt(p_bf16), n, (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, (int)step,
+                    (float)gscale, cur_stream());
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "xot MI355X (gfx950) kernel library";
+  m.def("rmsnorm", &rmsnorm);
+  m.def("rmsnorm_bwd", &rmsnorm_bwd);
+  m.def("embedding", &embedding);
+  m.def("silu_mul", &silu_mul);
+  m.def("silu_mul_bwd", &silu_mul_bwd);
+  m.def("rope_kv_write", &rope_kv_write);
+  m.def("rope_apply", &rope_apply);
+  m.def("gemm", &gemm);
+  m.def("attn_decode", &attn_decode);
+  m.def("attn_prefill", &attn_prefill);
+  m.def("sample", &sample);
+  m.def("ce_fwd", &ce_fwd);
+  m.def("ce_bwd", &ce_bwd);
+  m.def("adamw", &adamw);
+}

@@ -1,0 +1,49 @@
+// Host-side launchers of the gfx950 kernel library (raw pointers + stream; no torch types so the
+// kernel translation units compile without the torch headers).  Launchers that can reject a shape
+// return -1 and launch nothing; the Python layer turns that into a loud error.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace xot {
+
+void launch_rmsnorm(const uint16_t* x, const uint16_t* res, const uint16_t* w, uint16_t* out, uint16_t* res_out,
+                    int rows, int D, float eps, hipStream_t s);
+void launch_rmsnorm_bwd(const uint16_t* x, const uint16_t* w, const uint16_t* dy, uint16_t* dx, float* dw, int rows,
+                        int D, float eps, hipStream_t s);
+void launch_embedding(const int32_t* ids, const uint16_t* table, uint16_t* out, int T, int D, int vocab,
+                      hipStream_t s);
+void launch_silu_mul(const uint16_t* gu, uint16_t* out, int T, int F, hipStream_t s);
+void launch_silu_mul_bwd(const uint16_t* gu, const uint16_t* dout, uint16_t* dgu, int T, int F, hipStream_t s);
+void launch_rope_kv_write(const uint16_t* qkv, const int32_t* pos, const float* cos_sin, const int64_t* slots,
+                          uint16_t* q_out, uint16_t* kc, uint16_t* vc, int T, int H, int Hkv, int Dh, int BS,
+                          int max_pos, long nslots, hipStream_t s);
+void launch_rope_apply(const uint16_t* x, uint16_t* y, const int32_t* pos, const float* cos_sin, int T, int nh,
+                       int Dh, long ldx, long ldy, int max_pos, bool inverse, hipStream_t s);
+
+int launch_gemm_skinny(const uint16_t* X, int ldx, const uint16_t* W, int ldw, const uint16_t* bias,
+                       const uint16_t* R, int ldr, void* Y, int ldy, bool out_f32, int epi, int M, int N, int K,
+                       int nt, hipStream_t s);
+int launch_gemm_tiled(const uint16_t* X, int ldx, const uint16_t* W, int ldw, const uint16_t* bias,
+                      const uint16_t* R, int ldr, void* Y, int ldy, bool out_f32, int epi, int M, int N, int K,
+                      hipStream_t s);
+
+int launch_attn_decode(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, const int32_t* block_tables,
+                       int max_blocks, const int32_t* ctx_lens, uint16_t* out, float* ws_o, float* ws_ml, int B,
+                       int H, int Hkv, int Dh, int pages_per_part, int nparts, float scale, int num_pages,
+                       hipStream_t s);
+int launch_attn_prefill(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, const int32_t* block_tables,
+                        int max_blocks, const int32_t* cu_q, const int32_t* ctx_lens, uint16_t* out, int B,
+                        int max_qlen, int H, int Hkv, int Dh, float scale, int num_pages, hipStream_t s);
+
+void launch_sample(const float* logits, long ld, int B, int V, const float* temps, int top_k,
+                   const int64_t* seed_off, int32_t* out, hipStream_t s);
+
+void launch_ce_fwd(const void* x, bool x_f32, long ld, int T, int V, const int32_t* tgt, float* loss, float* lse,
+                   hipStream_t s);
+void launch_ce_bwd(const void* x, bool x_f32, long ld, int T, int V, const int32_t* tgt, const float* lse,
+                   const float* gscale, uint16_t* dx, long ldd, hipStream_t s);
+void launch_adamw(float* p, const void* g, bool g_f32, float* m, float* v, uint16_t* p_bf16, long n, float lr,
+                  float b1, float b2, float eps, float wd, int step, float gscale, hipStream_t s);
+
+}  // namespace xot

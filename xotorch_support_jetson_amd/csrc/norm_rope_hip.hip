@@ -1,0 +1,332 @@
+#include "hip/hip_runtime.h"
+// Memory-bound row kernels: RMSNorm (+fused residual add), RMSNorm backward,
+// token-embedding gather, SiLU*mul (fwd/bwd) and rotary embedding
+// (fused with the paged KV-cache write for inference, plain/inverse for training).
+//
+// Reference parity: these replace the torchtune RMSNorm / RoPE / KVCache.update /
+// nn.Embedding / FeedForward activation that the reference runs through stock
+// torch ops (xotorch/inference/torch/models/general_mha.py:33-63,77-120,
+// xotorch/inference/torch/models/llm_utils.py:399-435,513-522).
+// All loads/stores are 16 B per lane (8 x bf16); reductions are wave64 shuffles.
+#include "common.h"
+#include "kernels.h"
+
+namespace xot {
+
+// ---------------------------------------------------------------- RMSNorm fwd
+// out = rmsnorm(x [+ res]) * w ; if res != null, res_out = bf16(x + res)
+template <int MAXC>
+__global__ __launch_bounds__(256) void rmsnorm_kernel(const uint16_t* __restrict__ x,
+                                                      const uint16_t* __restrict__ res,
+                                                      const uint16_t* __restrict__ w,
+                                                      uint16_t* __restrict__ out,
+                                                      uint16_t* __restrict__ res_out, int D, float eps) {
+  __shared__ float red[4];
+  const int row = blockIdx.x, tid = threadIdx.x, nchunk = D >> 3;
+  const size_t base = (size_t)row * D;
+  float v[MAXC][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXC; ++i) {
+    const int c = tid + i * 256;
+    if (c < nchunk) {
+      s16x8 a = ld16(x + base + c * 8);
+      if (res != nullptr) {
+        s16x8 b = ld16(res + base + c * 8);
+        s16x8 h;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) h[j] = (short)f2bf(bf2f(a[j]) + bf2f(b[j]));
+        st16(res_out + base + c * 8, h);
+        a = h;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        v[i][j] = bf2f(a[j]);
+        ss += v[i][j] * v[i][j];
+      }
+    }
+  }
+  ss = wave_sum(ss);
+  if ((tid & 63) == 0) red[tid >> 6] = ss;
+  __syncthreads();
+  ss = red[0] + red[1] + red[2] + red[3];
+  const float inv = rsqrtf(ss / (float)D + eps);
+#pragma unroll
+  for (int i = 0; i < MAXC; ++i) {
+    const int c = tid + i * 256;
+    if (c < nchunk) {
+      s16x8 wv = ld16(w + c * 8), o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (short)f2bf(v[i][j] * inv * bf2f(wv[j]));
+      st16(out + base + c * 8, o);
+    }
+  }
+}
+
+void launch_rmsnorm(const uint16_t* x, const uint16_t* res, const uint16_t* w, uint16_t* out,
+                    uint16_t* res_out, int rows, int D, float eps, hipStream_t s) {
+  if (rows <= 0) return;
+  const int nchunk = D / 8;
+  if (nchunk <= 256)
+   hipLaunchKernelGGL(( rmsnorm_kernel<1>), dim3(rows), dim3(256), 0, s, x, res, w, out, res_out, D, eps);
+  else if (nchunk <= 512)
+   hipLaunchKernelGGL(( rmsnorm_kernel<2>), dim3(rows), dim3(256), 0, s, x, res, w, out, res_out, D, eps);
+  else if (nchunk <= 1024)
+   hipLaunchKernelGGL(( rmsnorm_kernel<4>), dim3(rows), dim3(256), 0, s, x, res, w, out, res_out, D, eps);
+  else
+   hipLaunchKernelGGL(( rmsnorm_kernel<8>), dim3(rows), dim3(256), 0, s, x, res, w, out, res_out, D, eps);
+}
+
+// ---------------------------------------------------------------- RMSNorm bwd
+// y = x * inv * w  (inv = rsqrt(mean(x^2)+eps))
+// dx = inv * (w*dy - xhat * mean(xhat * w * dy)),  dw += sum_rows dy * xhat
+// ROWS rows per block so the dw partial sum is flushed once per block.
+constexpr int RMS_BWD_ROWS = 16;
+template <int MAXC>
+__global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const uint16_t* __restrict__ x,
+                                                          const uint16_t* __restrict__ w,
+                                                          const uint16_t* __restrict__ dy,
+                                                          uint16_t* __restrict__ dx, float* __restrict__ dw,
+                                                          int rows, int D, float eps) {
+  __shared__ float red[2][4];
+  const int tid = threadIdx.x, nchunk = D >> 3;
+  float dwacc[MAXC][8];
+#pragma unroll
+  for (int i = 0; i < MAXC; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dwacc[i][j] = 0.f;
+  const int r0 = blockIdx.x * RMS_BWD_ROWS;
+  for (int rr = 0; rr < RMS_BWD_ROWS; ++rr) {
+    const int row = r0 + rr;
+    if (row >= rows) break;
+    const size_t base = (size_t)row * D;
+    float xv[MAXC][8], gv[MAXC][8];
+    float ss = 0.f, dot = 0.f;
+#pragma unroll
+    for (int i = 0; i < MAXC; ++i) {
+      const int c = tid + i * 256;
+      if (c < nchunk) {
+        s16x8 a = ld16(x + base + c * 8), g = ld16(dy + base + c * 8), wv = ld16(w + c * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          xv[i][j] = bf2f(a[j]);
+          gv[i][j] = bf2f(g[j]);
+          ss += xv[i][j] * xv[i][j];
+          dot += xv[i][j] * gv[i][j] * bf2f(wv[j]);
+        }
+      }
+    }
+    ss = wave_sum(ss);
+    dot = wave_sum(dot);
+    if ((tid & 63) == 0) {
+      red[0][tid >> 6] = ss;
+      red[1][tid >> 6] = dot;
+    }
+    __syncthreads();
+    ss = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+    dot = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+    __syncthreads();
+    const float inv = rsqrtf(ss / (float)D + eps);
+    const float coef = dot * inv * inv / (float)D;  // mean(xhat*w*dy) * (1/inv) ... folded below
+#pragma unroll
+    for (int i = 0; i < MAXC; ++i) {
+      const int c = tid + i * 256;
+      if (c < nchunk) {
+        s16x8 wv = ld16(w + c * 8), o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float xhat = xv[i][j] * inv;
+          o[j] = (short)f2bf(inv * (bf2f(wv[j]) * gv[i][j] - xv[i][j] * coef));
+          dwacc[i][j] += gv[i][j] * xhat;
+        }
+        st16(dx + base + c * 8, o);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < MAXC; ++i) {
+    const int c = tid + i * 256;
+    if (c < nchunk) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) atomicAdd(dw + c * 8 + j, dwacc[i][j]);
+    }
+  }
+}
+
+void launch_rmsnorm_bwd(const uint16_t* x, const uint16_t* w, const uint16_t* dy, uint16_t* dx, float* dw,
+                        int rows, int D, float eps, hipStream_t s) {
+  if (rows <= 0) return;
+  const int nchunk = D / 8;
+  dim3 grid((rows + RMS_BWD_ROWS - 1) / RMS_BWD_ROWS);
+  if (nchunk <= 256)
+   hipLaunchKernelGGL(( rmsnorm_bwd_kernel<1>), dim3(grid), dim3(256), 0, s, x, w, dy, dx, dw, rows, D, eps);
+  else if (nchunk <= 512)
+   hipLaunchKernelGGL(( rmsnorm_bwd_kernel<2>), dim3(grid), dim3(256), 0, s, x, w, dy, dx, dw, rows, D, eps);
+  else if (nchunk <= 1024)
+   hipLaunchKernelGGL(( rmsnorm_bwd_kernel<4>), dim3(grid), dim3(256), 0, s, x, w, dy, dx, dw, rows, D, eps);
+  else
+   hipLaunchKernelGGL(( rmsnorm_bwd_kernel<8>), dim3(grid), dim3(256), 0, s, x, w, dy, dx, dw, rows, D, eps);
+}
+
+// ---------------------------------------------------------------- embedding
+__global__ __launch_bounds__(256) void embedding_kernel(const int32_t* __restrict__ ids,
+                                                        const uint16_t* __restrict__ table,
+                                                        uint16_t* __restrict__ out, int D, int vocab) {
+  const int t = blockIdx.x;
+  int id = ids[t];
+  id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);  // never read out of bounds
+  const uint16_t* src = table + (size_t)id * D;
+  uint16_t* dst = out + (size_t)t * D;
+  for (int c = threadIdx.x; c < (D >> 3); c += 256) st16(dst + c * 8, ld16(src + c * 8));
+}
+
+void launch_embedding(const int32_t* ids, const uint16_t* table, uint16_t* out, int T, int D, int vocab,
+                      hipStream_t s) {
+  if (T <= 0) return;
+ hipLaunchKernelGGL(( embedding_kernel), dim3(T), dim3(256), 0, s, ids, table, out, D, vocab);
+}
+
+// ---------------------------------------------------------------- SiLU * mul
+// gu: [T, 2F] = [gate | up]; out [T, F] = silu(gate) * up
+__global__ __launch_bounds__(256) void silu_mul_kernel(const uint16_t* __restrict__ gu, uint16_t* __restrict__ out,
+                                                       int F, long total_chunks) {
+  const int fc = F >> 3;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total_chunks; i += (long)gridDim.x * 256) {
+    const long t = i / fc, c = i % fc;
+    s16x8 g = ld16(gu + t * 2 * F + c * 8), u = ld16(gu + t * 2 * F + F + c * 8), o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (short)f2bf(silu(bf2f(g[j])) * bf2f(u[j]));
+    st16(out + t * F + c * 8, o);
+  }
+}
+
+// dgu[:, :F] = dout * up * dsilu(g),  dgu[:, F:] = dout * silu(g)
+__global__ __launch_bounds__(256) void silu_mul_bwd_kernel(const uint16_t* __restrict__ gu,
+                                                           const uint16_t* __restrict__ dout,
+                                                           uint16_t* __restrict__ dgu, int F, long total_chunks) {
+  const int fc = F >> 3;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total_chunks; i += (long)gridDim.x * 256) {
+    const long t = i / fc, c = i % fc;
+    s16x8 g = ld16(gu + t * 2 * F + c * 8), u = ld16(gu + t * 2 * F + F + c * 8), d = ld16(dout + t * F + c * 8);
+    s16x8 dg, du;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float gf = bf2f(g[j]), uf = bf2f(u[j]), df = bf2f(d[j]);
+      const float sg = 1.0f / (1.0f + __expf(-gf));
+      const float s = gf * sg;
+      dg[j] = (short)f2bf(df * uf * (sg * (1.0f + gf * (1.0f - sg))));
+      du[j] = (short)f2bf(df * s);
+    }
+    st16(dgu + t * 2 * F + c * 8, dg);
+    st16(dgu + t * 2 * F + F + c * 8, du);
+  }
+}
+
+static int grid_for(long chunks) {
+  long g = (chunks + 255) / 256;
+  return (int)(g < 4096 ? (g < 1 ? 1 : g) : 4096);
+}
+
+void launch_silu_mul(const uint16_t* gu, uint16_t* out, int T, int F, hipStream_t s) {
+  const long chunks = (long)T * (F / 8);
+  if (chunks <= 0) return;
+ hipLaunchKernelGGL(( silu_mul_kernel), dim3(grid_for(chunks)), dim3(256), 0, s, gu, out, F, chunks);
+}
+void launch_silu_mul_bwd(const uint16_t* gu, const uint16_t* dout, uint16_t* dgu, int T, int F, hipStream_t s) {
+  const long chunks = (long)T * (F / 8);
+  if (chunks <= 0) return;
+ hipLaunchKernelGGL(( silu_mul_bwd_kernel), dim3(grid_for(chunks)), dim3(256), 0, s, gu, dout, dgu, F, chunks);
+}
+
+// ---------------------------------------------------------------- RoPE
+// HF rotate-half convention (no torchtune q/k permute needed, cf. llm_utils.py:126-134):
+//   o[i]      = x[i] * cos[i] - x[i+h] * sin[i]
+//   o[i+h]    = x[i+h] * cos[i] + x[i] * sin[i]        (h = Dh/2)
+// cos_sin: [max_pos, Dh] fp32, row p = [cos(p*f_0..f_{h-1}) | sin(...)]
+__device__ __forceinline__ void rope4(const uint16_t* __restrict__ src, uint16_t* __restrict__ dst,
+                                      const float* __restrict__ cs, int i, int half, float sgn) {
+  const s16x4 a = *reinterpret_cast<const s16x4*>(src + i);
+  const s16x4 b = *reinterpret_cast<const s16x4*>(src + i + half);
+  const f32x4 c = *reinterpret_cast<const f32x4*>(cs + i);
+  const f32x4 sn = *reinterpret_cast<const f32x4*>(cs + half + i);
+  s16x4 oa, ob;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float x0 = bf2f(a[j]), x1 = bf2f(b[j]), sj = sgn * sn[j];
+    oa[j] = (short)f2bf(x0 * c[j] - x1 * sj);
+    ob[j] = (short)f2bf(x1 * c[j] + x0 * sj);
+  }
+  *reinterpret_cast<s16x4*>(dst + i) = oa;
+  *reinterpret_cast<s16x4*>(dst + i + half) = ob;
+}
+
+// qkv [T, (H + 2*Hkv) * Dh]  ->  q_out [T, H, Dh] (rotated), k -> k_cache (rotated), v -> v_cache
+// k_cache: [num_blocks, Hkv, BS, Dh]   v_cache: [num_blocks, Hkv, Dh, BS]  (V stored transposed
+// per page so the P.V MFMA B-operand is contiguous along keys)
+__global__ __launch_bounds__(256) void rope_kv_write_kernel(const uint16_t* __restrict__ qkv,
+                                                            const int32_t* __restrict__ pos,
+                                                            const float* __restrict__ cos_sin,
+                                                            const int64_t* __restrict__ slots,
+                                                            uint16_t* __restrict__ q_out, uint16_t* __restrict__ kc,
+                                                            uint16_t* __restrict__ vc, int H, int Hkv, int Dh, int BS,
+                                                            int max_pos, long nslots) {
+  const int t = blockIdx.x;
+  const int half = Dh >> 1, qpr = half >> 2;  // 4-wide pair-groups per head
+  int p = pos[t];
+  p = p < 0 ? 0 : (p >= max_pos ? max_pos - 1 : p);
+  const float* cs = cos_sin + (size_t)p * Dh;
+  const uint16_t* row = qkv + (size_t)t * (H + 2 * Hkv) * Dh;
+  const int64_t slot = slots[t] < nslots ? slots[t] : -1;  // out-of-range slot: skip the write
+  const long blk = slot >= 0 ? slot / BS : 0;
+  const int off = slot >= 0 ? (int)(slot % BS) : 0;
+  const int nrot = (H + Hkv) * qpr;
+  for (int w = threadIdx.x; w < nrot; w += 256) {
+    const int h = w / qpr, i = (w % qpr) * 4;
+    if (h < H) {
+      rope4(row + h * Dh, q_out + ((size_t)t * H + h) * Dh, cs, i, half, 1.f);
+    } else if (slot >= 0) {
+      const int kh = h - H;
+      uint16_t* dst = kc + (((size_t)blk * Hkv + kh) * BS + off) * Dh;
+      rope4(row + h * Dh, dst, cs, i, half, 1.f);
+    }
+  }
+  if (slot < 0) return;
+  const int nv = Hkv * Dh;
+  const uint16_t* vsrc = row + (H + Hkv) * Dh;
+  for (int w = threadIdx.x; w < nv; w += 256) {
+    const int kh = w / Dh, d = w % Dh;
+    vc[(((size_t)blk * Hkv + kh) * Dh + d) * BS + off] = vsrc[w];
+  }
+}
+
+void launch_rope_kv_write(const uint16_t* qkv, const int32_t* pos, const float* cos_sin, const int64_t* slots,
+                          uint16_t* q_out, uint16_t* kc, uint16_t* vc, int T, int H, int Hkv, int Dh, int BS,
+                          int max_pos, long nslots, hipStream_t s) {
+  if (T <= 0) return;
+ hipLaunchKernelGGL(( rope_kv_write_kernel), dim3(T), dim3(256), 0, s, qkv, pos, cos_sin, slots, q_out, kc, vc, H, Hkv, Dh, BS, max_pos, nslots);
+}
+
+// plain rotation of x [T, nh, Dh] (row stride ld elements between tokens) -> y (may alias x);
+// inverse=1 applies the transpose rotation (the backward of the forward rotation)
+__global__ __launch_bounds__(256) void rope_apply_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
+                                                         const int32_t* __restrict__ pos,
+                                                         const float* __restrict__ cos_sin, int nh, int Dh,
+                                                         long ldx, long ldy, int max_pos, float sgn) {
+  const int t = blockIdx.x;
+  const int half = Dh >> 1, qpr = half >> 2;
+  int p = pos[t];
+  p = p < 0 ? 0 : (p >= max_pos ? max_pos - 1 : p);
+  const float* cs = cos_sin + (size_t)p * Dh;
+  for (int w = threadIdx.x; w < nh * qpr; w += 256) {
+    const int h = w / qpr, i = (w % qpr) * 4;
+    rope4(x + t * ldx + h * Dh, y + t * ldy + h * Dh, cs, i, half, sgn);
+  }
+}
+
+void launch_rope_apply(const uint16_t* x, uint16_t* y, const int32_t* pos, const float* cos_sin, int T, int nh,
+                       int Dh, long ldx, long ldy, int max_pos, bool inverse, hipStream_t s) {
+  if (T <= 0) return;
+ hipLaunchKernelGGL(( rope_apply_kernel), dim3(T), dim3(256), 0, s, x, y, pos, cos_sin, nh, Dh, ldx, ldy, max_pos, inverse ? -1.f : 1.f);
+}
+
+}  // namespace xot

@@ -1,0 +1,140 @@
+// Training-path kernels: fused cross-entropy (forward + backward) and fused AdamW.
+//
+// The reference routes `xot train` through Node.enqueue_example -> engine.train(...) but never
+// implements the engine side (xotorch/orchestration/node.py:210-345, inference_engine.py:34-35);
+// these kernels are the loss/optimizer half of the train step this framework actually runs.
+#include "common.h"
+#include "kernels.h"
+
+namespace xot {
+
+template <typename T>
+__device__ __forceinline__ float ldf(const T* p, long i);
+template <>
+__device__ __forceinline__ float ldf<float>(const float* p, long i) { return p[i]; }
+template <>
+__device__ __forceinline__ float ldf<uint16_t>(const uint16_t* p, long i) { return bf2f(p[i]); }
+
+__device__ __forceinline__ void block_reduce_max_sum(float& m, float& s, float* sm, float* ss) {
+  // combine (max, sum-of-exp relative to max) across the 256-thread block
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float m2 = __shfl_xor(m, o, 64), s2 = __shfl_xor(s, o, 64);
+    const float mn = fmaxf(m, m2);
+    s = s * __expf(m - mn) + s2 * __expf(m2 - mn);
+    m = mn;
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    sm[w] = m;
+    ss[w] = s;
+  }
+  __syncthreads();
+  m = sm[0];
+  s = ss[0];
+  for (int i = 1; i < 4; ++i) {
+    const float mn = fmaxf(m, sm[i]);
+    s = s * __expf(m - mn) + ss[i] * __expf(sm[i] - mn);
+    m = mn;
+  }
+}
+
+// loss[t] = lse(x_t) - x_t[target_t]   (0 and lse=0 when target < 0: ignored position)
+template <typename T>
+__global__ __launch_bounds__(256) void ce_fwd_kernel(const T* __restrict__ x, long ld, int V,
+                                                     const int32_t* __restrict__ tgt, float* __restrict__ loss,
+                                                     float* __restrict__ lse) {
+  __shared__ float sm[4], ss[4];
+  const int t = blockIdx.x;
+  const T* row = x + (size_t)t * ld;
+  float m = -INFINITY, s = 0.f;
+  for (int i = threadIdx.x; i < V; i += 256) {
+    const float v = ldf(row, i);
+    if (v > m) {
+      s = s * __expf(m - v) + 1.f;
+      m = v;
+    } else {
+      s += __expf(v - m);
+    }
+  }
+  if (m == -INFINITY) s = 0.f;
+  block_reduce_max_sum(m, s, sm, ss);
+  if (threadIdx.x == 0) {
+    const float l = m + __logf(s);
+    const int y = tgt[t];
+    lse[t] = l;
+    loss[t] = (y >= 0 && y < V) ? l - ldf(row, y) : 0.f;
+  }
+}
+
+// dx[t, i] = gscale[t] * (softmax_i - [i == target])   (zero row for ignored positions)
+template <typename T>
+__global__ __launch_bounds__(256) void ce_bwd_kernel(const T* __restrict__ x, long ld, int V,
+                                                     const int32_t* __restrict__ tgt, const float* __restrict__ lse,
+                                                     const float* __restrict__ gscale, uint16_t* __restrict__ dx,
+                                                     long ldd) {
+  const int t = blockIdx.x;
+  const T* row = x + (size_t)t * ld;
+  uint16_t* drow = dx + (size_t)t * ldd;
+  const int y = tgt[t];
+  const bool ign = y < 0 || y >= V;
+  const float l = lse[t], gs = gscale[t];
+  for (int i = threadIdx.x; i < V; i += 256) {
+    const float p = __expf(ldf(row, i) - l);
+    drow[i] = ign ? (uint16_t)0 : f2bf(gs * (p - (i == y ? 1.f : 0.f)));
+  }
+}
+
+void launch_ce_fwd(const void* x, bool x_f32, long ld, int T, int V, const int32_t* tgt, float* loss, float* lse,
+                   hipStream_t s) {
+  if (T <= 0) return;
+  if (x_f32)
+    ce_fwd_kernel<float><<<T, 256, 0, s>>>((const float*)x, ld, V, tgt, loss, lse);
+  else
+    ce_fwd_kernel<uint16_t><<<T, 256, 0, s>>>((const uint16_t*)x, ld, V, tgt, loss, lse);
+}
+
+void launch_ce_bwd(const void* x, bool x_f32, long ld, int T, int V, const int32_t* tgt, const float* lse,
+                   const float* gscale, uint16_t* dx, long ldd, hipStream_t s) {
+  if (T <= 0) return;
+  if (x_f32)
+    ce_bwd_kernel<float><<<T, 256, 0, s>>>((const float*)x, ld, V, tgt, lse, gscale, dx, ldd);
+  else
+    ce_bwd_kernel<uint16_t><<<T, 256, 0, s>>>((const uint16_t*)x, ld, V, tgt, lse, gscale, dx, ldd);
+}
+
+// ---------------------------------------------------------------- AdamW
+// fp32 master weights + fp32 moments; grads in bf16 (model dtype) or fp32; writes the bf16 model copy.
+template <typename G>
+__global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const G* __restrict__ gr,
+                                                    float* __restrict__ m, float* __restrict__ v,
+                                                    uint16_t* __restrict__ p_bf16, long n, float lr, float b1,
+                                                    float b2, float eps, float wd, float bc1, float bc2,
+                                                    float gscale) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const float g = ldf(gr, i) * gscale;
+    const float mi = b1 * m[i] + (1.f - b1) * g;
+    const float vi = b2 * v[i] + (1.f - b2) * g * g;
+    m[i] = mi;
+    v[i] = vi;
+    float pi = p[i];
+    pi -= lr * ((mi / bc1) / (sqrtf(vi / bc2) + eps) + wd * pi);
+    p[i] = pi;
+    if (p_bf16 != nullptr) p_bf16[i] = f2bf(pi);
+  }
+}
+
+void launch_adamw(float* p, const void* g, bool g_f32, float* m, float* v, uint16_t* p_bf16, long n, float lr,
+                  float b1, float b2, float eps, float wd, int step, float gscale, hipStream_t s) {
+  if (n <= 0) return;
+  const float bc1 = 1.f - powf(b1, (float)step), bc2 = 1.f - powf(b2, (float)step);
+  long gsz = (n + 255) / 256;
+  const int grid = (int)(gsz > 8192 ? 8192 : gsz);
+  if (g_f32)
+    adamw_kernel<float><<<grid, 256, 0, s>>>(p, (const float*)g, m, v, p_bf16, n, lr, b1, b2, eps, wd, bc1, bc2, gscale);
+  else
+    adamw_kernel<uint16_t><<<grid, 256, 0, s>>>(p, (const uint16_t*)g, m, v, p_bf16, n, lr, b1, b2, eps, wd, bc1, bc2,
+                                                gscale);
+}
+
+}  // namespace xot

@@ -1,0 +1,211 @@
+"""Python entry points of the gfx950 kernel library.
+
+Each function takes torch tensors, allocates outputs when the caller did not preallocate them, and
+dispatches to the HIP kernel for GPU tensors or to the fp32 torch reference (`ops.reference`) for
+CPU tensors.  GPU tensors never take the reference path: if the extension is missing the call
+raises (see `ops._ext.require`).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import reference as ref
+from ._ext import require
+
+EPI = {"none": 0, "resid": 1, "silu": 2}
+PAGE = 64
+
+
+def _gpu(t: torch.Tensor) -> bool:
+  if t.is_cuda:
+    require()
+    return True
+  return False
+
+
+# ------------------------------------------------------------------ norms / elementwise
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: torch.Tensor | None = None,
+            out: torch.Tensor | None = None, residual_out: torch.Tensor | None = None):
+  """Returns (out, residual_out).  With `residual`, residual_out = x + residual (the new stream)."""
+  if not _gpu(x):
+    y, r = ref.rmsnorm(x, w, eps, residual)
+    if out is not None:
+      out.copy_(y)
+      y = out
+    if residual_out is not None and r is not None:
+      residual_out.copy_(r)
+      r = residual_out
+    return y, r
+  out = torch.empty_like(x) if out is None else out
+  if residual is not None and residual_out is None:
+    residual_out = torch.empty_like(x)
+  require().rmsnorm(x, w, out, residual, residual_out, float(eps))
+  return out, residual_out
+
+
+def embedding(ids: torch.Tensor, table: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+  if not _gpu(table):
+    y = table[ids.long().clamp(0, table.shape[0] - 1)]
+    if out is not None:
+      out.copy_(y.reshape(out.shape))
+      return out
+    return y
+  ids32 = ids.to(torch.int32).contiguous()
+  out = torch.empty(ids32.numel(), table.shape[1], dtype=table.dtype, device=table.device) if out is None else out
+  require().embedding(ids32, table, out)
+  return out
+
+
+def silu_mul(gu: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+  if not _gpu(gu):
+    return ref.silu_mul(gu)
+  Fd = gu.shape[-1] // 2
+  out = torch.empty(*gu.shape[:-1], Fd, dtype=gu.dtype, device=gu.device) if out is None else out
+  require().silu_mul(gu.contiguous(), out)
+  return out
+
+
+# ------------------------------------------------------------------ GEMM
+def gemm(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, residual: torch.Tensor | None = None,
+         epi: str = "none", out: torch.Tensor | None = None, out_dtype: torch.dtype | None = None, algo: int = 0,
+         nt: int = 0) -> torch.Tensor:
+  """y = x @ w.T (+bias) with fused epilogue: 'none' | 'resid' (y += residual) | 'silu'.
+
+  For 'silu' the weight rows must be gate/up interleaved in 16-row tiles (see
+  models.weights.interleave_gate_up); the output has w.shape[0] // 2 columns.
+  """
+  M, N = x.shape[0], w.shape[0]
+  ncol = N // 2 if epi == "silu" else N
+  if not _gpu(x):
+    y = ref.linear(x, w, bias)
+    if epi == "silu":
+      y = y.view(M, N // 32, 2, 16)
+      y = (torch.nn.functional.silu(y[:, :, 0]) * y[:, :, 1]).reshape(M, ncol)
+    elif epi == "resid":
+      y = y + residual.float()
+    dt = out_dtype or (out.dtype if out is not None else x.dtype)
+    if out is not None:
+      out.copy_(y.to(out.dtype))
+      return out
+    return y.to(dt)
+  if out is None:
+    out = torch.empty(M, ncol, dtype=out_dtype or x.dtype, device=x.device)
+  if nt == 0:
+    nt = 2 if (N // 32) >= 1024 else 1
+  require().gemm(x, w, out, bias, residual, EPI[epi], int(algo), int(nt))
+  return out
+
+
+# ------------------------------------------------------------------ RoPE + paged KV
+def rope_kv_write(qkv: torch.Tensor, pos: torch.Tensor, cos_sin: torch.Tensor, slots: torch.Tensor,
+                  k_cache: torch.Tensor, v_cache: torch.Tensor, H: int, Hkv: int,
+                  q_out: torch.Tensor | None = None) -> torch.Tensor:
+  """qkv [T, (H+2Hkv)*Dh] -> rotated q [T, H, Dh]; rotated k and v written into the paged caches."""
+  T = qkv.shape[0]
+  Dh = k_cache.shape[-1]
+  if not _gpu(qkv):
+    x = qkv.view(T, H + 2 * Hkv, Dh)
+    q = ref.rope(x[:, :H], pos, cos_sin)
+    k = ref.rope(x[:, H:H + Hkv], pos, cos_sin)
+    ref.write_kv(k, x[:, H + Hkv:], slots, k_cache, v_cache)
+    if q_out is not None:
+      q_out.copy_(q.view(q_out.shape))
+      return q_out
+    return q
+  q_out = torch.empty(T, H, Dh, dtype=qkv.dtype, device=qkv.device) if q_out is None else q_out
+  require().rope_kv_write(qkv, pos, cos_sin, slots, q_out, k_cache, v_cache, int(H), int(Hkv))
+  return q_out
+
+
+def rope_apply(x: torch.Tensor, pos: torch.Tensor, cos_sin: torch.Tensor, nh: int, Dh: int, inverse: bool = False,
+               out: torch.Tensor | None = None) -> torch.Tensor:
+  """x [T, >= nh*Dh] (2-D rows) -> rotated copy (or into `out`)."""
+  if not _gpu(x):
+    y = ref.rope(x[:, :nh * Dh].reshape(-1, nh, Dh), pos, cos_sin, inverse).reshape(x.shape[0], nh * Dh)
+    if out is not None:
+      out[:, :nh * Dh].copy_(y)
+      return out
+    return y
+  out = torch.empty(x.shape[0], nh * Dh, dtype=x.dtype, device=x.device) if out is None else out
+  require().rope_apply(x, out, pos, cos_sin, int(nh), int(Dh), bool(inverse))
+  return out
+
+
+# ------------------------------------------------------------------ attention
+class DecodeWorkspace:
+  """Split-KV scratch for attn_decode (sized once for the largest batch / context)."""
+
+  def __init__(self, max_batch: int, H: int, Dh: int, max_ctx: int, device, pages_per_part: int = 8):
+    self.pages_per_part = pages_per_part
+    self.nparts = max(1, -(-max_ctx // (PAGE * pages_per_part)))
+    self.o = torch.empty(max_batch * H * self.nparts * Dh, dtype=torch.float32, device=device)
+    self.ml = torch.empty(max_batch * H * self.nparts * 2, dtype=torch.float32, device=device)
+
+
+def choose_pages_per_part(batch: int, Hkv: int, max_ctx: int) -> int:
+  """Enough workgroups to cover 256 CUs several times, but >= 4 pages (one per wave) per partition."""
+  pages = max(1, -(-max_ctx // PAGE))
+  for ppp in (16, 8, 4):
+    if batch * Hkv * -(-pages // ppp) >= 1024:
+      return ppp
+  return 4
+
+
+def attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale: float, ws: DecodeWorkspace | None = None,
+                out: torch.Tensor | None = None) -> torch.Tensor:
+  if not _gpu(q):
+    y = ref.attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale)
+    if out is not None:
+      out.copy_(y.view(out.shape))
+      return out
+    return y
+  B, H, Dh = q.shape
+  if ws is None:
+    ws = DecodeWorkspace(B, H, Dh, block_tables.shape[1] * PAGE, q.device)
+  out = torch.empty_like(q) if out is None else out
+  require().attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, out, ws.o, ws.ml, ws.pages_per_part, ws.nparts,
+                        float(scale))
+  return out
+
+
+def attn_prefill(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, max_qlen: int, scale: float,
+                 out: torch.Tensor | None = None) -> torch.Tensor:
+  if not _gpu(q):
+    y = ref.attn_prefill(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale)
+    if out is not None:
+      out.copy_(y)
+      return out
+    return y
+  out = torch.empty_like(q) if out is None else out
+  require().attn_prefill(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, out, int(max_qlen), float(scale))
+  return out
+
+
+# ------------------------------------------------------------------ sampling
+def sample(logits: torch.Tensor, temps: torch.Tensor, top_k: int, seed_off: torch.Tensor,
+           out: torch.Tensor | None = None) -> torch.Tensor:
+  """Greedy when temp <= 1e-5, else top-k + exponential-race sampling (all on device)."""
+  if not _gpu(logits):
+    B = logits.shape[0]
+    res = torch.empty(B, dtype=torch.int32)
+    g = torch.Generator().manual_seed(int(seed_off[0]) * 1000003 + int(seed_off[1]))
+    for b in range(B):
+      t = float(temps[b])
+      row = logits[b].float()
+      if t <= 1e-5 or top_k == 1:
+        res[b] = int(row.argmax())
+        continue
+      row = row / max(t, 1e-5)
+      if 0 < top_k < row.numel():
+        kth = torch.topk(row, top_k).values[-1]
+        row = row.masked_fill(row < kth, float("-inf"))
+      probs = torch.softmax(row, -1)
+      q = torch.empty_like(probs).exponential_(1, generator=g)
+      res[b] = int((probs / q).argmax())
+    if out is not None:
+      out.copy_(res)
+      return out
+    return res
+  out = torch.empty(logits.shape[0], dtype=torch.int32, device=logits.device) if out is None else out
+  require().sample(logits, temps, int(top_k), seed_off, out)
+  return out

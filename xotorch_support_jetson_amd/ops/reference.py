@@ -1,0 +1,130 @@
+"""Plain-PyTorch fp32 implementations of every kernel in the library.
+
+These are (1) the numerical oracles the HIP kernels are tested against and (2) the compute path on
+CPU-only hosts (BASELINE config 1: Llama-3.2-1B on the CPU engine).  Semantics match the kernels
+exactly, including the paged KV layout (K [pages, Hkv, 64, Dh], V [pages, Hkv, Dh, 64]).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+PAGE = 64
+
+
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: torch.Tensor | None = None):
+  """Returns (normed, new_residual). new_residual = bf16(x + residual) when residual is given."""
+  if residual is not None:
+    x = (x.float() + residual.float()).to(x.dtype)
+  xf = x.float()
+  y = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps) * w.float()
+  return y.to(x.dtype), (x if residual is not None else None)
+
+
+def rope(x: torch.Tensor, pos: torch.Tensor, cos_sin: torch.Tensor, inverse: bool = False) -> torch.Tensor:
+  """x [T, nh, Dh]; HF rotate-half convention."""
+  Dh = x.shape[-1]
+  half = Dh // 2
+  cs = cos_sin[pos.long()].to(x.device)  # [T, Dh]
+  cos, sin = cs[:, None, :half], cs[:, None, half:]
+  if inverse:
+    sin = -sin
+  xf = x.float()
+  x0, x1 = xf[..., :half], xf[..., half:]
+  return torch.cat([x0 * cos - x1 * sin, x1 * cos + x0 * sin], dim=-1).to(x.dtype)
+
+
+def silu_mul(gu: torch.Tensor) -> torch.Tensor:
+  Fd = gu.shape[-1] // 2
+  g, u = gu[..., :Fd].float(), gu[..., Fd:].float()
+  return (F.silu(g) * u).to(gu.dtype)
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Tensor:
+  y = x.float() @ w.float().t()
+  if bias is not None:
+    y = y + bias.float()
+  return y
+
+
+def write_kv(k: torch.Tensor, v: torch.Tensor, slots: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor):
+  """k, v [T, Hkv, Dh] -> paged caches at global slots (slot < 0 skipped)."""
+  BS = k_cache.shape[2]
+  ok = slots >= 0
+  s = slots[ok].long()
+  blk, off = s // BS, s % BS
+  k_cache[blk, :, off, :] = k[ok].to(k_cache.dtype)
+  v_cache[blk, :, :, off] = v[ok].to(v_cache.dtype)
+
+
+def gather_kv(k_cache, v_cache, table, n):
+  """Dense [n, Hkv, Dh] K and V for one sequence from its block table."""
+  BS = k_cache.shape[2]
+  npg = (n + BS - 1) // BS
+  pages = table[:npg].long()
+  k = k_cache[pages].permute(0, 2, 1, 3).reshape(npg * BS, k_cache.shape[1], k_cache.shape[3])[:n]
+  v = v_cache[pages].permute(0, 3, 1, 2).reshape(npg * BS, v_cache.shape[1], v_cache.shape[2])[:n]
+  return k, v
+
+
+def _attend(q, k, v, scale, causal_offset: int | None):
+  # q [S, H, Dh], k/v [T, Hkv, Dh]
+  H, Hkv = q.shape[1], k.shape[1]
+  G = H // Hkv
+  kf = k.float().repeat_interleave(G, dim=1)
+  vf = v.float().repeat_interleave(G, dim=1)
+  s = torch.einsum("shd,thd->hst", q.float(), kf) * scale
+  if causal_offset is not None:
+    S, T = q.shape[0], k.shape[0]
+    qpos = torch.arange(S, device=q.device)[:, None] + causal_offset
+    kpos = torch.arange(T, device=q.device)[None, :]
+    s = s.masked_fill(kpos > qpos, float("-inf"))
+  p = torch.softmax(s, dim=-1)
+  return torch.einsum("hst,thd->shd", p, vf)
+
+
+def attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale):
+  """q [B, H, Dh] -> [B, H, Dh]"""
+  out = torch.empty_like(q)
+  for b in range(q.shape[0]):
+    n = int(ctx_lens[b])
+    if n <= 0:
+      out[b] = 0
+      continue
+    k, v = gather_kv(k_cache, v_cache, block_tables[b], n)
+    out[b] = _attend(q[b:b + 1], k, v, scale, None)[0].to(q.dtype)
+  return out
+
+
+def attn_prefill(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale):
+  """q [T, H, Dh] (new tokens of all sequences) -> [T, H, Dh]; causal against the cached context."""
+  out = torch.empty_like(q)
+  for b in range(ctx_lens.numel()):
+    q0, q1 = int(cu_q[b]), int(cu_q[b + 1])
+    if q1 <= q0:
+      continue
+    n = int(ctx_lens[b])
+    k, v = gather_kv(k_cache, v_cache, block_tables[b], n)
+    out[q0:q1] = _attend(q[q0:q1], k, v, scale, n - (q1 - q0)).to(q.dtype)
+  return out
+
+
+def sample_greedy(logits: torch.Tensor) -> torch.Tensor:
+  return logits.float().argmax(dim=-1).to(torch.int32)
+
+
+def topk_mask(logits: torch.Tensor, k: int) -> torch.Tensor:
+  """Boolean mask of entries >= the k-th largest value (ties kept), per row."""
+  kth = torch.topk(logits.float(), k, dim=-1).values[:, -1:]
+  return logits.float() >= kth
+
+
+def cross_entropy(logits: torch.Tensor, targets: torch.Tensor):
+  """Per-row loss (0 where target < 0) and lse."""
+  lf = logits.float()
+  lse = torch.logsumexp(lf, dim=-1)
+  valid = targets >= 0
+  tgt = targets.clamp(min=0).long()
+  picked = lf.gather(1, tgt[:, None])[:, 0]
+  loss = torch.where(valid, lse - picked, torch.zeros_like(lse))
+  return loss, lse
