@@ -1,0 +1,150 @@
+#!/usr/bin/env python3
+"""Headline benchmark: output tokens/sec (whole node), Llama-3-70B ring-sharded across N MI355X.
+
+  python bench.py --gpus N --steps K --warmup W            (N=1 runs in-process)
+  torchrun --nproc-per-node N bench.py --gpus N ...         (one rank per GPU, RCCL p2p ring)
+
+Each rank holds 80/N consecutive layers (ring memory-weighted partitioner).  The node serves
+N micro-batches of --batch-per-gpu sequences each (weak scaling: per-GPU work per step is fixed:
+80 layer-passes x batch-per-gpu tokens), so the ring is full and all GPUs work concurrently.
+Prompts (--prompt-len tokens, synthetic ids) are prefilled through the real model, then W untimed
+decode rounds, then K timed rounds; one round = every sequence in the node generates one token
+(sampled on device with temperature / top-k 35, the reference's sampler).  Weights are random-init
+bf16 with the exact Llama-3-70B architecture (no checkpoint download on the GPU box).
+Timing: barrier + device sync on both sides of the K rounds, max over ranks.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+
+def log(*a):
+  print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+  ap = argparse.ArgumentParser()
+  ap.add_argument("--gpus", type=int, default=1)
+  ap.add_argument("--steps", type=int, default=16)
+  ap.add_argument("--warmup", type=int, default=3)
+  ap.add_argument("--model", default="llama-3-70b")
+  ap.add_argument("--batch-per-gpu", type=int, default=int(os.environ.get("XOT_BENCH_BATCH", 128)))
+  ap.add_argument("--prompt-len", type=int, default=512)
+  ap.add_argument("--temperature", type=float, default=0.6)
+  ap.add_argument("--layers", type=int, default=0, help="debug only: truncate the model (result marked invalid)")
+  args = ap.parse_args()
+
+  from xotorch_support_jetson_amd.models.config import preset
+  from xotorch_support_jetson_amd.parallel.comm import P2PTransport, init_distributed
+  from xotorch_support_jetson_amd.parallel.pipeline import MicroBatch, RingStage, run_decode_steps
+  from xotorch_support_jetson_amd.runtime.runner import ShardRunner
+  from xotorch_support_jetson_amd.topology.ring_memory_weighted_partitioning_strategy import equal_layer_shards
+  import torch.distributed as dist
+
+  rank, world, dev = init_distributed()
+  if world != args.gpus:
+    raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+  cfg = preset(args.model)
+  if args.layers:
+    cfg = cfg.with_layers(args.layers)
+  shards = equal_layer_shards(args.model, cfg.num_layers, world)
+  assert len(shards) == world, shards
+  shard = shards[rank]
+  M = world  # micro-batches in flight = stages, so the ring is always full
+  B = args.batch_per_gpu
+  max_ctx = args.prompt_len + args.warmup + args.steps + 8
+  pages_per_seq = -(-max_ctx // 64)
+  t0 = time.time()
+  runner = ShardRunner(cfg, shard, dev, num_pages=M * B * pages_per_seq + 16, max_batch=B, max_ctx=max_ctx,
+                       seed=0)
+  torch.cuda.synchronize()
+  t_init = time.time() - t0
+  log(f"[rank {rank}] shard {shard.start_layer}-{shard.end_layer} weights {runner.weights.nbytes() / 1e9:.1f} GB "
+      f"kv {runner.kv.nbytes() / 1e9:.1f} GB init {t_init:.1f}s")
+
+  transport = P2PTransport(rank, world)
+  stage = RingStage(runner, rank, world, transport)
+  g = torch.Generator().manual_seed(1234)
+  mbs = []
+  for m in range(M):
+    rids = [f"mb{m}-r{i}" for i in range(B)]
+    prompt = torch.randint(0, cfg.vocab_size, (B, args.prompt_len), generator=g, dtype=torch.int32)
+    mbs.append(MicroBatch(rids, prompt=prompt, temps=torch.full((B,), args.temperature, device=dev)))
+
+  # ---- prefill (real forward through every stage)
+  if world > 1:
+    dist.barrier()
+  torch.cuda.synchronize()
+  t0 = time.time()
+  first = [stage.prefill(mb) for mb in mbs]
+  transport.drain()
+  torch.cuda.synchronize()
+  t_prefill = time.time() - t0
+  log(f"[rank {rank}] prefill {M * B} x {args.prompt_len} tokens in {t_prefill:.1f}s")
+
+  # ---- warmup rounds (graph capture + GEMM policy tuning happen here)
+  toks = run_decode_steps(stage, mbs, args.warmup, first_tokens=first if stage.last else None)
+  transport.drain()
+  torch.cuda.synchronize()
+  log(f"[rank {rank}] warmup done")
+
+  # ---- timed rounds
+  if world > 1:
+    dist.barrier()
+  torch.cuda.synchronize()
+  t0 = time.perf_counter()
+  toks = run_decode_steps(stage, mbs, args.steps, first_tokens=toks if stage.last else None)
+  transport.drain()
+  torch.cuda.synchronize()
+  if world > 1:
+    dist.barrier()
+  elapsed = time.perf_counter() - t0
+  if world > 1:
+    e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    dist.all_reduce(e, op=dist.ReduceOp.MAX)
+    elapsed = float(e.item())
+
+  total_tokens = args.steps * M * B
+  tps = total_tokens / elapsed
+  ms_step = elapsed / args.steps * 1e3
+  if rank == 0:
+    out = {
+      "metric": "output tokens/sec (whole node) Llama-3-70B ring-sharded across 1/2/4/8 MI355X",
+      "value": round(tps, 2),
+      "unit": "tokens/s",
+      "n_gpus": world,
+      "steps": args.steps,
+      "warmup": args.warmup,
+      "ms_per_step": round(ms_step, 3),
+      "higher_is_better": True,
+      "scaling": "weak",
+      "vs_baseline": None,
+      "dtype": "bf16",
+      "data": "synthetic prompts, random-init weights (exact Llama-3-70B architecture)",
+      "config": {
+        "model": args.model if not args.layers else f"{args.model}-TRUNCATED-{args.layers}L-INVALID",
+        "global_batch": M * B,
+        "seq_len": args.prompt_len,
+        "parallelism": f"pp{world} (ring, {M} micro-batches x {B})",
+        "batch_per_gpu": B,
+        "decode_context": f"{args.prompt_len + args.warmup}..{args.prompt_len + args.warmup + args.steps}",
+        "sampling": f"temperature {args.temperature}, top-k 35 (on-device)",
+      },
+      "extra": {"prefill_s": round(t_prefill, 2), "init_s": round(t_init, 2),
+                "tokens_per_s_per_gpu": round(tps / world, 2),
+                "reference_derived_ceiling_tok_s": 0.57 if world == 8 else (2.3 if world == 2 else None)},
+    }
+    print(json.dumps(out), flush=True)
+  if world > 1:
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+  main()

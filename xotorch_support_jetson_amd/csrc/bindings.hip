@@ -80,14 +80,19 @@ void embedding(const at::Tensor& ids, const at::Tensor& table, at::Tensor& out) 
                         cur_stream());
 }
 
-void silu_mul(const at::Tensor& gu, at::Tensor& out) {
+void silu_mul(const at::Tensor& gu, at::Tensor& out, bool interleaved16) {
   CHECK_BF16(gu);
   CHECK_BF16(out);
   CHECK_CONTIG(gu);
   CHECK_CONTIG(out);
   const int64_t F = out.size(-1), T = out.numel() / F;
   XCHECK(F % 8 == 0 && gu.numel() == 2 * T * F && gu.size(-1) == 2 * F, "silu_mul: shape mismatch");
-  xot::launch_silu_mul(bf(gu), bf(out), (int)T, (int)F, cur_stream());
+  if (interleaved16) {
+    XCHECK(F % 16 == 0, "silu_mul: interleaved layout needs F % 16 == 0");
+    xot::launch_silu_mul_il(bf(gu), bf(out), (int)T, (int)F, cur_stream());
+  } else {
+    xot::launch_silu_mul(bf(gu), bf(out), (int)T, (int)F, cur_stream());
+  }
 }
 
 void silu_mul_bwd(const at::Tensor& gu, const at::Tensor& dout, at::Tensor& dgu) {

@@ -14,6 +14,7 @@ void launch_rmsnorm_bwd(const uint16_t* x, const uint16_t* w, const uint16_t* dy
 void launch_embedding(const int32_t* ids, const uint16_t* table, uint16_t* out, int T, int D, int vocab,
                       hipStream_t s);
 void launch_silu_mul(const uint16_t* gu, uint16_t* out, int T, int F, hipStream_t s);
+void launch_silu_mul_il(const uint16_t* gu, uint16_t* out, int T, int F, hipStream_t s);
 void launch_silu_mul_bwd(const uint16_t* gu, const uint16_t* dout, uint16_t* dgu, int T, int F, hipStream_t s);
 void launch_rope_kv_write(const uint16_t* qkv, const int32_t* pos, const float* cos_sin, const int64_t* slots,
                           uint16_t* q_out, uint16_t* kc, uint16_t* vc, int T, int H, int Hkv, int Dh, int BS,

@@ -221,6 +221,22 @@ __global__ __launch_bounds__(256) void silu_mul_bwd_kernel(const uint16_t* __res
   }
 }
 
+// gu: [T, 2F] with gate/up interleaved in 16-column tiles (the fused gate_up weight layout):
+// cols [32j, 32j+16) = gate_{16j..16j+15}, [32j+16, 32j+32) = up_{16j..}; out [T, F]
+__global__ __launch_bounds__(256) void silu_mul_il_kernel(const uint16_t* __restrict__ gu, uint16_t* __restrict__ out,
+                                                          int F, long total_chunks) {
+  const int fc = F >> 3;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total_chunks; i += (long)gridDim.x * 256) {
+    const long t = i / fc;
+    const int o = (int)(i % fc) * 8, j = o >> 4, w = o & 15;
+    const uint16_t* row = gu + t * 2 * F;
+    s16x8 g = ld16(row + 32 * j + w), u = ld16(row + 32 * j + 16 + w), r;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) r[k] = (short)f2bf(silu(bf2f(g[k])) * bf2f(u[k]));
+    st16(out + t * F + o, r);
+  }
+}
+
 static int grid_for(long chunks) {
   long g = (chunks + 255) / 256;
   return (int)(g < 4096 ? (g < 1 ? 1 : g) : 4096);
@@ -230,6 +246,11 @@ void launch_silu_mul(const uint16_t* gu, uint16_t* out, int T, int F, hipStream_
   const long chunks = (long)T * (F / 8);
   if (chunks <= 0) return;
   silu_mul_kernel<<<grid_for(chunks), 256, 0, s>>>(gu, out, F, chunks);
+}
+void launch_silu_mul_il(const uint16_t* gu, uint16_t* out, int T, int F, hipStream_t s) {
+  const long chunks = (long)T * (F / 8);
+  if (chunks <= 0) return;
+  silu_mul_il_kernel<<<grid_for(chunks), 256, 0, s>>>(gu, out, F, chunks);
 }
 void launch_silu_mul_bwd(const uint16_t* gu, const uint16_t* dout, uint16_t* dgu, int T, int F, hipStream_t s) {
   const long chunks = (long)T * (F / 8);

@@ -1,0 +1,143 @@
+"""Model configuration: HF `config.json` -> typed ModelConfig, plus built-in presets.
+
+Presets carry the public HF architecture numbers for the BASELINE.json configs so the framework can
+build random-init models of the exact shape offline (there is no network on the GPU box).
+Reference: load_model_config (xotorch/inference/torch/models/llm_utils.py:30-77); unlike it, the
+layer count comes from config.json and is validated against the model card.
+"""
+from __future__ import annotations
+
+import json
+from dataclasses import asdict, dataclass, field, replace
+from pathlib import Path
+from typing import Optional
+
+
+@dataclass(frozen=True)
+class ModelConfig:
+  model_type: str  # llama | qwen2 | mistral | mixtral
+  vocab_size: int
+  hidden_size: int
+  intermediate_size: int
+  num_layers: int
+  num_heads: int
+  num_kv_heads: int
+  head_dim: int
+  rms_norm_eps: float = 1e-5
+  rope_theta: float = 500000.0
+  rope_scaling: Optional[dict] = None
+  max_position_embeddings: int = 8192
+  tie_word_embeddings: bool = False
+  attention_bias: bool = False
+  num_experts: int = 0  # >0: MoE (Mixtral) MLP
+  num_experts_per_tok: int = 0
+  bos_token_id: int = 128000
+  eos_token_ids: tuple = (128001, 128009)
+
+  @property
+  def qkv_size(self) -> int:
+    return (self.num_heads + 2 * self.num_kv_heads) * self.head_dim
+
+  @property
+  def is_moe(self) -> bool:
+    return self.num_experts > 0
+
+  def params_per_layer(self) -> int:
+    D, F = self.hidden_size, self.intermediate_size
+    attn = D * self.qkv_size + self.num_heads * self.head_dim * D
+    mlp = 3 * D * F * max(1, self.num_experts) + (D * self.num_experts if self.is_moe else 0)
+    return attn + mlp + 2 * D
+
+  def num_params(self) -> int:
+    emb = self.vocab_size * self.hidden_size
+    return self.num_layers * self.params_per_layer() + emb * (1 if self.tie_word_embeddings else 2) + self.hidden_size
+
+  def to_dict(self) -> dict:
+    d = asdict(self)
+    d["eos_token_ids"] = list(self.eos_token_ids)
+    return d
+
+  def with_layers(self, n: int) -> "ModelConfig":
+    return replace(self, num_layers=n)
+
+
+def from_hf_config(cfg: dict) -> ModelConfig:
+  mt = cfg.get("model_type", "llama")
+  H = int(cfg["num_attention_heads"])
+  D = int(cfg["hidden_size"])
+  eos = cfg.get("eos_token_id", 2)
+  eos_ids = tuple(eos) if isinstance(eos, (list, tuple)) else (int(eos),)
+  return ModelConfig(
+    model_type=mt,
+    vocab_size=int(cfg["vocab_size"]),
+    hidden_size=D,
+    intermediate_size=int(cfg["intermediate_size"]),
+    num_layers=int(cfg["num_hidden_layers"]),
+    num_heads=H,
+    num_kv_heads=int(cfg.get("num_key_value_heads", H)),
+    head_dim=int(cfg.get("head_dim") or D // H),
+    rms_norm_eps=float(cfg.get("rms_norm_eps", 1e-5)),
+    rope_theta=float(cfg.get("rope_theta", 10000.0)),
+    rope_scaling=cfg.get("rope_scaling"),
+    max_position_embeddings=int(cfg.get("max_position_embeddings", 8192)),
+    tie_word_embeddings=bool(cfg.get("tie_word_embeddings", False)),
+    attention_bias=bool(cfg.get("attention_bias", mt == "qwen2")),
+    num_experts=int(cfg.get("num_local_experts", 0)),
+    num_experts_per_tok=int(cfg.get("num_experts_per_tok", 0)),
+    bos_token_id=int(cfg.get("bos_token_id", 1) or 1),
+    eos_token_ids=eos_ids,
+  )
+
+
+def load_config(model_dir: str | Path) -> ModelConfig:
+  with open(Path(model_dir) / "config.json") as f:
+    return from_hf_config(json.load(f))
+
+
+_L3 = dict(rope_type="llama3", factor=32.0, low_freq_factor=1.0, high_freq_factor=4.0,
+           original_max_position_embeddings=8192)
+_L31 = dict(_L3, factor=8.0)
+
+PRESETS: dict[str, ModelConfig] = {
+  "llama-3.2-1b": ModelConfig("llama", 128256, 2048, 8192, 16, 32, 8, 64, 1e-5, 500000.0, _L3, 131072, True),
+  "llama-3.2-3b": ModelConfig("llama", 128256, 3072, 8192, 28, 24, 8, 128, 1e-5, 500000.0, _L3, 131072, True),
+  "llama-3-8b": ModelConfig("llama", 128256, 4096, 14336, 32, 32, 8, 128, 1e-5, 500000.0, None, 8192, False),
+  "llama-3.1-8b": ModelConfig("llama", 128256, 4096, 14336, 32, 32, 8, 128, 1e-5, 500000.0, _L31, 131072, False),
+  "llama-3-70b": ModelConfig("llama", 128256, 8192, 28672, 80, 64, 8, 128, 1e-5, 500000.0, None, 8192, False),
+  "llama-3.1-70b": ModelConfig("llama", 128256, 8192, 28672, 80, 64, 8, 128, 1e-5, 500000.0, _L31, 131072, False),
+  "llama-3.3-70b": ModelConfig("llama", 128256, 8192, 28672, 80, 64, 8, 128, 1e-5, 500000.0, _L31, 131072, False),
+  "qwen-2.5-0.5b": ModelConfig("qwen2", 151936, 896, 4864, 24, 14, 2, 64, 1e-6, 1000000.0, None, 32768, True, True,
+                               bos_token_id=151643, eos_token_ids=(151645, 151643)),
+  "qwen-2.5-1.5b": ModelConfig("qwen2", 151936, 1536, 8960, 28, 12, 2, 128, 1e-6, 1000000.0, None, 32768, True, True,
+                               bos_token_id=151643, eos_token_ids=(151645, 151643)),
+  "qwen-2.5-7b": ModelConfig("qwen2", 152064, 3584, 18944, 28, 28, 4, 128, 1e-6, 1000000.0, None, 32768, False, True,
+                             bos_token_id=151643, eos_token_ids=(151645, 151643)),
+  "mistral-7b": ModelConfig("mistral", 32768, 4096, 14336, 32, 32, 8, 128, 1e-5, 1000000.0, None, 32768, False,
+                            bos_token_id=1, eos_token_ids=(2,)),
+  "mixtral-8x7b": ModelConfig("mixtral", 32000, 4096, 14336, 32, 32, 8, 128, 1e-5, 1000000.0, None, 32768, False,
+                              num_experts=8, num_experts_per_tok=2, bos_token_id=1, eos_token_ids=(2,)),
+  "mistral-nemo": ModelConfig("mistral", 131072, 5120, 14336, 40, 32, 8, 128, 1e-5, 1000000.0, None, 131072, False,
+                              bos_token_id=1, eos_token_ids=(2,)),
+  # small shapes for tests / CPU plumbing
+  "tiny-llama": ModelConfig("llama", 512, 256, 512, 4, 4, 2, 64, 1e-5, 10000.0, None, 2048, False,
+                            bos_token_id=1, eos_token_ids=(2,)),
+  "tiny-llama-d64": ModelConfig("llama", 1024, 256, 512, 6, 4, 2, 64, 1e-5, 10000.0, _L3, 4096, True,
+                                bos_token_id=1, eos_token_ids=(2,)),
+  "tiny-qwen": ModelConfig("qwen2", 512, 256, 512, 4, 4, 2, 64, 1e-6, 1000000.0, None, 2048, True, True,
+                           bos_token_id=1, eos_token_ids=(2,)),
+  "tiny-mixtral": ModelConfig("mixtral", 512, 256, 512, 4, 4, 2, 64, 1e-5, 10000.0, None, 2048, False,
+                              num_experts=4, num_experts_per_tok=2, bos_token_id=1, eos_token_ids=(2,)),
+}
+# aliases of the reference's model cards that share an architecture
+for _alias, _base in {"llama-3.1-70b-bf16": "llama-3.1-70b", "nemotron-70b": "llama-3.1-70b",
+                      "deepseek-r1-distill-llama-70b": "llama-3.1-70b", "deepseek-r1-distill-llama-8b": "llama-3.1-8b",
+                      "qwen-2.5-coder-1.5b": "qwen-2.5-1.5b", "qwen-2.5-coder-7b": "qwen-2.5-7b",
+                      "qwen-2.5-math-7b": "qwen-2.5-7b", "deepseek-r1-distill-qwen-1.5b": "qwen-2.5-1.5b",
+                      "deepseek-r1-distill-qwen-7b": "qwen-2.5-7b"}.items():
+  PRESETS.setdefault(_alias, PRESETS[_base])
+
+
+def preset(model_id: str) -> ModelConfig:
+  if model_id not in PRESETS:
+    raise KeyError(f"no built-in architecture preset for {model_id!r}; provide a config.json")
+  return PRESETS[model_id]

@@ -1,0 +1,185 @@
+"""Forward pass of one pipeline shard of a dense (Llama/Qwen2/Mistral) or MoE (Mixtral) decoder.
+
+Per layer, all on the kernel library (ops.*), with the residual stream `h` carried in place:
+  xn  = rmsnorm(h, ln1)
+  qkv = xn @ qkv_w.T (+b)                          fused QKV GEMM
+  q   = rope(qkv.q); cache <- rope(qkv.k), qkv.v   one kernel, paged write (slot mapping)
+  a   = attention(q, paged cache)                  decode: split-KV GQA; prefill: causal varlen
+  h   = h + a @ o_w.T                              residual add in the GEMM epilogue
+  xn  = rmsnorm(h, ln2)
+  act = silu(xn @ gate.T) * (xn @ up.T)            one GEMM (interleaved gate/up), SiLU in the epilogue
+  h   = h + act @ down.T                           residual add in the GEMM epilogue
+Last shard: rmsnorm + LM head on each sequence's LAST row only (the reference computes the head over
+every prompt row and keeps [:, -1], sharded_inference_engine.py:366), fp32 logits for the sampler.
+
+Hidden-state contract between shards: the output of this shard's end_layer (fixing the reference's
+off-by-one that returns the *input* of the last layer and IndexErrors on middle shards,
+llm_utils.py:404-440 / general_mha.py:209).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import List, Optional
+
+import torch
+
+from ..inference.shard import Shard
+from ..ops import kernels as K
+from ..ops.linear import linear
+from ..ops.rope import build_cos_sin
+from .config import ModelConfig
+from .weights import ShardWeights
+
+PAGE = 64
+
+
+@dataclass
+class StepInputs:
+  """Device-side description of one forward step over a batch of sequences (all int tensors)."""
+  positions: torch.Tensor  # [T] int32 absolute position of each new token
+  slots: torch.Tensor  # [T] int64 global KV slot of each new token (-1: do not write)
+  block_tables: torch.Tensor  # [B, max_blocks] int32
+  ctx_lens: torch.Tensor  # [B] int32 context length INCLUDING the new tokens
+  cu_q: torch.Tensor  # [B+1] int32 offsets of each sequence's new tokens in T
+  last_idx: torch.Tensor  # [B] int64 row of each sequence's last new token
+  max_qlen: int
+  decode: bool  # every sequence has exactly one new token
+
+  @property
+  def num_tokens(self) -> int:
+    return int(self.positions.numel())
+
+  @property
+  def batch(self) -> int:
+    return int(self.ctx_lens.numel())
+
+
+class KVCache:
+  """Per-shard paged KV pool: K [L, pages, Hkv, 64, Dh] and V [L, pages, Hkv, Dh, 64] (V page-transposed)."""
+
+  def __init__(self, c: ModelConfig, n_layers: int, num_pages: int, device, dtype=torch.bfloat16):
+    self.num_pages = num_pages
+    self.k = torch.zeros(n_layers, num_pages, c.num_kv_heads, PAGE, c.head_dim, device=device, dtype=dtype)
+    self.v = torch.zeros(n_layers, num_pages, c.num_kv_heads, c.head_dim, PAGE, device=device, dtype=dtype)
+
+  @staticmethod
+  def bytes_per_page(c: ModelConfig, n_layers: int) -> int:
+    return 2 * n_layers * c.num_kv_heads * PAGE * c.head_dim * 2
+
+  def nbytes(self) -> int:
+    return 2 * self.k.numel() * self.k.element_size()
+
+
+class ShardModel:
+  def __init__(self, weights: ShardWeights, kv: KVCache, max_batch: int = 256, max_ctx: int = 8192):
+    self.w = weights
+    self.c: ModelConfig = weights.config
+    self.shard: Shard = weights.shard
+    self.kv = kv
+    self.device = kv.k.device
+    c = self.c
+    self.scale = 1.0 / math.sqrt(c.head_dim)
+    max_pos = max(max_ctx, 16)
+    self.cos_sin = build_cos_sin(c.head_dim, max_pos, c.rope_theta, c.rope_scaling, self.device)
+    self.layer_ids: List[int] = list(self.shard.layers())
+    self.max_batch = max_batch
+    self.max_ctx = max_ctx
+    self.ws = None
+    if self.device.type == "cuda":
+      ppp = K.choose_pages_per_part(max_batch, c.num_kv_heads, max_ctx)
+      self.ws = K.DecodeWorkspace(max_batch, c.num_heads, c.head_dim, max_ctx, self.device, ppp)
+
+  # ------------------------------------------------------------------ helpers
+  def _attention(self, q: torch.Tensor, li: int, inp: StepInputs) -> torch.Tensor:
+    kc, vc = self.kv.k[li], self.kv.v[li]
+    if inp.decode:
+      return K.attn_decode(q, kc, vc, inp.block_tables, inp.ctx_lens, self.scale, self.ws)
+    return K.attn_prefill(q, kc, vc, inp.block_tables, inp.cu_q, inp.ctx_lens, inp.max_qlen, self.scale)
+
+  def _mlp(self, xn: torch.Tensor, lw, h: torch.Tensor) -> torch.Tensor:
+    c = self.c
+    if not c.is_moe:
+      act = linear(xn, lw.gu_w, epi="silu")
+      return linear(act, lw.down_w, residual=h, epi="resid", out=h)
+    return self._moe(xn, lw, h)
+
+  def _moe(self, xn: torch.Tensor, lw, h: torch.Tensor) -> torch.Tensor:
+    """Mixtral sparse MoE: softmax top-k routing, tokens grouped per expert, expert GEMMs on the
+    kernel library (gate/up with fused SiLU epilogue), weighted scatter-add back into h."""
+    c = self.c
+    logits = linear(xn, lw.router, out_dtype=torch.float32)  # [T, E]
+    probs = torch.softmax(logits, dim=-1)
+    topw, topi = torch.topk(probs, c.num_experts_per_tok, dim=-1)
+    topw = topw / topw.sum(-1, keepdim=True)
+    T = xn.shape[0]
+    flat_e = topi.reshape(-1)
+    order = torch.argsort(flat_e, stable=True)
+    tok = order // c.num_experts_per_tok
+    counts = torch.bincount(flat_e, minlength=c.num_experts).tolist()
+    out = torch.zeros(T, c.hidden_size, device=xn.device, dtype=torch.float32)
+    start = 0
+    wflat = topw.reshape(-1)[order]
+    for e, n in enumerate(counts):
+      if n == 0:
+        continue
+      idx = tok[start:start + n]
+      xe = xn.index_select(0, idx)
+      act = linear(xe, lw.gu_w[e], epi="silu")
+      ye = linear(act, lw.down_w[e], out_dtype=torch.float32)
+      out.index_add_(0, idx, ye * wflat[start:start + n, None])
+      start += n
+    h += out.to(h.dtype)
+    return h
+
+  # ------------------------------------------------------------------ forward
+  @torch.inference_mode()
+  def forward(self, x: torch.Tensor, inp: StepInputs) -> torch.Tensor:
+    """x: token ids [T] (first shard) or hidden [T, D] bf16.  Returns hidden [T, D] (non-last shard)
+    or fp32 logits [B, V] of each sequence's last token (last shard)."""
+    c, w = self.c, self.w
+    if self.shard.is_first_layer():
+      h = K.embedding(x, w.embed)
+    else:
+      h = x.contiguous().clone() if x.dtype == torch.bfloat16 else x.to(torch.bfloat16).contiguous()
+    for j, li in enumerate(self.layer_ids):
+      lw = w.layers[li]
+      xn, _ = K.rmsnorm(h, lw.ln1, c.rms_norm_eps)
+      qkv = linear(xn, lw.qkv_w, bias=lw.qkv_b)
+      q = K.rope_kv_write(qkv, inp.positions, self.cos_sin, inp.slots, self.kv.k[j], self.kv.v[j], c.num_heads,
+                          c.num_kv_heads)
+      a = self._attention(q, j, inp).view(h.shape[0], c.num_heads * c.head_dim)
+      h = linear(a, lw.o_w, residual=h, epi="resid", out=h)
+      xn, _ = K.rmsnorm(h, lw.ln2, c.rms_norm_eps)
+      h = self._mlp(xn, lw, h)
+    if not self.shard.is_last_layer():
+      return h
+    hl = h.index_select(0, inp.last_idx) if not inp.decode else h
+    xn, _ = K.rmsnorm(hl, w.norm, c.rms_norm_eps)
+    return linear(xn, w.lm_head, out_dtype=torch.float32)
+
+
+def make_step_inputs(seqs: List[tuple], device, block_width: Optional[int] = None) -> StepInputs:
+  """Host helper: seqs = [(positions list, slots list, block_table list, ctx_len)] -> StepInputs."""
+  pos, slots, cu, last = [], [], [0], []
+  width = block_width or max(1, max(len(s[2]) for s in seqs))
+  tables = torch.zeros(len(seqs), width, dtype=torch.int32)
+  ctx = torch.zeros(len(seqs), dtype=torch.int32)
+  for b, (p, s, bt, n) in enumerate(seqs):
+    pos += list(p)
+    slots += list(s)
+    cu.append(cu[-1] + len(p))
+    last.append(cu[-1] - 1)
+    tables[b, :len(bt)] = torch.tensor(bt, dtype=torch.int32)
+    ctx[b] = n
+  qlens = [cu[i + 1] - cu[i] for i in range(len(seqs))]
+  return StepInputs(
+    positions=torch.tensor(pos, dtype=torch.int32, device=device),
+    slots=torch.tensor(slots, dtype=torch.int64, device=device),
+    block_tables=tables.to(device),
+    ctx_lens=ctx.to(device),
+    cu_q=torch.tensor(cu, dtype=torch.int32, device=device),
+    last_idx=torch.tensor(last, dtype=torch.int64, device=device),
+    max_qlen=max(qlens),
+    decode=all(q == 1 for q in qlens),
+  )

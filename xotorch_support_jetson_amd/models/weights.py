@@ -1,0 +1,252 @@
+"""Per-shard weights in the fused device layout, built from HF safetensors or random init.
+
+Device layout per decoder layer (all bf16, nn.Linear [out, in] rows):
+  qkv_w  [(H + 2 Hkv) Dh, D]   = cat(q_proj, k_proj, v_proj)     (+ qkv_b for Qwen2)
+  o_w    [D, H Dh]
+  gu_w   [2F, D]               gate/up interleaved in 16-row tiles (one MFMA n-tile each), so the
+                               GEMM epilogue computes silu(gate)*up without another pass
+  down_w [D, F]
+  ln1, ln2 [D]
+MoE (Mixtral): router [E, D], gu_w [E, 2F, D], down_w [E, D, F].
+Only this shard's layers are materialised (the reference allocates every shard's full embedding and
+LM head, general_mha.py:124-128; here the embedding lives on the first shard and the head on the last).
+HF names are kept for loading and checkpointing so any shard checkpoint can be re-partitioned.
+Reference parity: load_model_weights_torchtune (llm_utils.py:136-284) — without the q/k permute,
+because the RoPE kernel uses the HF rotate-half convention directly.
+"""
+from __future__ import annotations
+
+import json
+import os
+from dataclasses import dataclass, field
+from pathlib import Path
+from typing import Dict, Iterable, Optional
+
+import torch
+
+from ..inference.shard import Shard
+from .config import ModelConfig
+
+TILE = 16
+
+
+def interleave_gate_up(gate: torch.Tensor, up: torch.Tensor) -> torch.Tensor:
+  """[F, D] x2 -> [2F, D] with rows [g0..g15, u0..u15, g16..g31, u16..u31, ...]."""
+  Fd, D = gate.shape
+  assert Fd % TILE == 0, "intermediate size must be a multiple of 16"
+  return torch.stack([gate.view(Fd // TILE, TILE, D), up.view(Fd // TILE, TILE, D)], dim=1).reshape(2 * Fd, D)
+
+
+def split_gate_up(gu: torch.Tensor):
+  n2, D = gu.shape[-2], gu.shape[-1]
+  v = gu.reshape(*gu.shape[:-2], n2 // (2 * TILE), 2, TILE, D)
+  return v[..., 0, :, :].reshape(*gu.shape[:-2], n2 // 2, D), v[..., 1, :, :].reshape(*gu.shape[:-2], n2 // 2, D)
+
+
+@dataclass
+class LayerWeights:
+  qkv_w: torch.Tensor
+  o_w: torch.Tensor
+  gu_w: torch.Tensor
+  down_w: torch.Tensor
+  ln1: torch.Tensor
+  ln2: torch.Tensor
+  qkv_b: Optional[torch.Tensor] = None
+  router: Optional[torch.Tensor] = None  # MoE
+
+  def tensors(self) -> Dict[str, torch.Tensor]:
+    return {k: v for k, v in self.__dict__.items() if isinstance(v, torch.Tensor)}
+
+
+@dataclass
+class ShardWeights:
+  config: ModelConfig
+  shard: Shard
+  layers: Dict[int, LayerWeights] = field(default_factory=dict)
+  embed: Optional[torch.Tensor] = None  # first shard (and last, when tied)
+  norm: Optional[torch.Tensor] = None  # last shard
+  lm_head: Optional[torch.Tensor] = None  # last shard (aliases embed when tied)
+
+  def nbytes(self) -> int:
+    seen, total = set(), 0
+    for t in self.all_tensors():
+      if t.data_ptr() not in seen:
+        seen.add(t.data_ptr())
+        total += t.numel() * t.element_size()
+    return total
+
+  def all_tensors(self) -> Iterable[torch.Tensor]:
+    for lw in self.layers.values():
+      yield from lw.tensors().values()
+    for t in (self.embed, self.norm, self.lm_head):
+      if t is not None:
+        yield t
+
+  # ---------------------------------------------------------------- HF naming (checkpoints)
+  def to_hf_state_dict(self) -> Dict[str, torch.Tensor]:
+    c = self.config
+    H, Hkv, Dh = c.num_heads, c.num_kv_heads, c.head_dim
+    sd: Dict[str, torch.Tensor] = {}
+    for i, lw in self.layers.items():
+      p = f"model.layers.{i}."
+      q, k, v = lw.qkv_w.split([H * Dh, Hkv * Dh, Hkv * Dh], 0)
+      sd[p + "self_attn.q_proj.weight"], sd[p + "self_attn.k_proj.weight"], sd[p + "self_attn.v_proj.weight"] = q, k, v
+      if lw.qkv_b is not None:
+        qb, kb, vb = lw.qkv_b.split([H * Dh, Hkv * Dh, Hkv * Dh], 0)
+        sd[p + "self_attn.q_proj.bias"], sd[p + "self_attn.k_proj.bias"], sd[p + "self_attn.v_proj.bias"] = qb, kb, vb
+      sd[p + "self_attn.o_proj.weight"] = lw.o_w
+      sd[p + "input_layernorm.weight"] = lw.ln1
+      sd[p + "post_attention_layernorm.weight"] = lw.ln2
+      if c.is_moe:
+        sd[p + "block_sparse_moe.gate.weight"] = lw.router
+        g, u = split_gate_up(lw.gu_w)
+        for e in range(c.num_experts):
+          sd[p + f"block_sparse_moe.experts.{e}.w1.weight"] = g[e]
+          sd[p + f"block_sparse_moe.experts.{e}.w3.weight"] = u[e]
+          sd[p + f"block_sparse_moe.experts.{e}.w2.weight"] = lw.down_w[e]
+      else:
+        g, u = split_gate_up(lw.gu_w)
+        sd[p + "mlp.gate_proj.weight"], sd[p + "mlp.up_proj.weight"] = g, u
+        sd[p + "mlp.down_proj.weight"] = lw.down_w
+    if self.embed is not None:
+      sd["model.embed_tokens.weight"] = self.embed
+    if self.norm is not None:
+      sd["model.norm.weight"] = self.norm
+    if self.lm_head is not None and not (c.tie_word_embeddings and self.embed is not None and self.lm_head is self.embed):
+      sd["lm_head.weight"] = self.lm_head
+    return {k: v.contiguous() for k, v in sd.items()}
+
+
+def _needs_embed(c: ModelConfig, s: Shard) -> bool:
+  return s.is_first_layer() or (s.is_last_layer() and c.tie_word_embeddings)
+
+
+# -------------------------------------------------------------------- random init
+def random_weights(c: ModelConfig, shard: Shard, device: torch.device | str = "cpu", dtype=torch.bfloat16,
+                   seed: int = 0, std: float = 0.02) -> ShardWeights:
+  """Deterministic per-layer random weights: layer i is identical whichever shard holds it, so a
+  pipeline split reproduces the unsplit model exactly (the split-vs-full equivalence tests)."""
+  dev = torch.device(device)
+  D, Fd, E = c.hidden_size, c.intermediate_size, c.num_experts
+
+  def gen(tag: int):
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed * 1_000_003 + tag)
+    return g
+
+  def normal(shape, g, s=std):
+    return torch.empty(shape, device=dev, dtype=dtype).normal_(0.0, s, generator=g)
+
+  def norm_w(g):
+    return (1.0 + torch.empty(D, device=dev, dtype=torch.float32).normal_(0.0, 0.05, generator=g)).to(dtype)
+
+  sw = ShardWeights(c, shard)
+  for i in shard.layers():
+    g = gen(1000 + i)
+    out_std = std / (2 * c.num_layers) ** 0.5  # GPT-2 style residual-branch scaling keeps deep stacks stable
+    lw = LayerWeights(
+      qkv_w=normal((c.qkv_size, D), g),
+      o_w=normal((D, c.num_heads * c.head_dim), g, out_std),
+      gu_w=normal((E, 2 * Fd, D) if E else (2 * Fd, D), g),
+      down_w=normal((E, D, Fd) if E else (D, Fd), g, out_std),
+      ln1=norm_w(g),
+      ln2=norm_w(g),
+      qkv_b=normal((c.qkv_size,), g) if c.attention_bias else None,
+      router=normal((E, D), g, 0.1) if E else None,
+    )
+    sw.layers[i] = lw
+  if _needs_embed(c, shard):
+    sw.embed = normal((c.vocab_size, D), gen(1))
+  if shard.is_last_layer():
+    sw.norm = norm_w(gen(2))
+    sw.lm_head = sw.embed if c.tie_word_embeddings else normal((c.vocab_size, D), gen(3))
+  return sw
+
+
+# -------------------------------------------------------------------- HF safetensors
+def _weight_map(model_dir: Path) -> Dict[str, str]:
+  idx = model_dir / "model.safetensors.index.json"
+  if idx.exists():
+    return json.loads(idx.read_text())["weight_map"]
+  files = sorted(model_dir.glob("*.safetensors"))
+  if not files:
+    raise FileNotFoundError(f"no safetensors in {model_dir}")
+  from safetensors import safe_open
+  wm = {}
+  for f in files:
+    with safe_open(str(f), framework="pt") as sf:
+      for k in sf.keys():
+        wm[k] = f.name
+  return wm
+
+
+def needed_files(model_dir: Path, c: ModelConfig, shard: Shard) -> set:
+  """Safetensors files that hold this shard's tensors (for the downloader's allow patterns too)."""
+  wm = _weight_map(model_dir)
+  want = set()
+  for name, fname in wm.items():
+    if name.startswith("model.layers."):
+      if int(name.split(".")[2]) in shard.layers():
+        want.add(fname)
+    elif name.startswith("model.embed_tokens") and _needs_embed(c, shard):
+      want.add(fname)
+    elif (name.startswith("model.norm") or name.startswith("lm_head")) and shard.is_last_layer():
+      want.add(fname)
+  return want
+
+
+def load_hf_weights(model_dir: str | Path, c: ModelConfig, shard: Shard, device="cpu", dtype=torch.bfloat16) -> ShardWeights:
+  """Read only this shard's tensors (mmap'd safetensors, one tensor at a time) into the fused layout."""
+  from safetensors import safe_open
+  model_dir = Path(model_dir)
+  wm = _weight_map(model_dir)
+  handles = {}
+
+  def get(name: str) -> torch.Tensor:
+    fname = wm[name]
+    if fname not in handles:
+      handles[fname] = safe_open(str(model_dir / fname), framework="pt")
+    return handles[fname].get_tensor(name).to(device=device, dtype=dtype)
+
+  def has(name: str) -> bool:
+    return name in wm
+
+  sw = ShardWeights(c, shard)
+  for i in shard.layers():
+    p = f"model.layers.{i}."
+    qkv = torch.cat([get(p + f"self_attn.{n}_proj.weight") for n in "qkv"], 0)
+    qkv_b = None
+    if has(p + "self_attn.q_proj.bias"):
+      qkv_b = torch.cat([get(p + f"self_attn.{n}_proj.bias") for n in "qkv"], 0)
+    if c.is_moe:
+      pm = p + "block_sparse_moe."
+      gu = torch.stack([interleave_gate_up(get(pm + f"experts.{e}.w1.weight"), get(pm + f"experts.{e}.w3.weight"))
+                        for e in range(c.num_experts)])
+      down = torch.stack([get(pm + f"experts.{e}.w2.weight") for e in range(c.num_experts)])
+      router = get(pm + "gate.weight")
+    else:
+      gu = interleave_gate_up(get(p + "mlp.gate_proj.weight"), get(p + "mlp.up_proj.weight"))
+      down = get(p + "mlp.down_proj.weight")
+      router = None
+    sw.layers[i] = LayerWeights(qkv.contiguous(), get(p + "self_attn.o_proj.weight"), gu.contiguous(), down,
+                                get(p + "input_layernorm.weight"), get(p + "post_attention_layernorm.weight"), qkv_b,
+                                router)
+  if _needs_embed(c, shard):
+    sw.embed = get("model.embed_tokens.weight")
+  if shard.is_last_layer():
+    sw.norm = get("model.norm.weight")
+    if has("lm_head.weight") and not c.tie_word_embeddings:
+      sw.lm_head = get("lm_head.weight")
+    else:
+      sw.lm_head = sw.embed
+  return sw
+
+
+def from_hf_state_dict(sd: Dict[str, torch.Tensor], c: ModelConfig, shard: Shard, device="cpu",
+                       dtype=torch.bfloat16) -> ShardWeights:
+  """Inverse of ShardWeights.to_hf_state_dict (used by checkpoint resume)."""
+  import tempfile
+  from safetensors.torch import save_file
+  with tempfile.TemporaryDirectory() as d:
+    save_file({k: v.contiguous() for k, v in sd.items()}, os.path.join(d, "model.safetensors"))
+    return load_hf_weights(d, c, shard, device, dtype)

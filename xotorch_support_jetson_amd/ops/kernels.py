@@ -56,12 +56,22 @@ def embedding(ids: torch.Tensor, table: torch.Tensor, out: torch.Tensor | None =
   return out
 
 
-def silu_mul(gu: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+def silu_mul(gu: torch.Tensor, out: torch.Tensor | None = None, interleaved16: bool = False) -> torch.Tensor:
+  """silu(gate) * up.  gu = [gate | up] halves, or 16-column interleaved tiles (fused gate_up layout)."""
   if not _gpu(gu):
-    return ref.silu_mul(gu)
+    if interleaved16:
+      M, N = gu.shape
+      g = gu.view(M, N // 32, 2, 16)
+      y = (torch.nn.functional.silu(g[:, :, 0].float()) * g[:, :, 1].float()).reshape(M, N // 2).to(gu.dtype)
+    else:
+      y = ref.silu_mul(gu)
+    if out is not None:
+      out.copy_(y)
+      return out
+    return y
   Fd = gu.shape[-1] // 2
   out = torch.empty(*gu.shape[:-1], Fd, dtype=gu.dtype, device=gu.device) if out is None else out
-  require().silu_mul(gu.contiguous(), out)
+  require().silu_mul(gu.contiguous(), out, bool(interleaved16))
   return out
 
 

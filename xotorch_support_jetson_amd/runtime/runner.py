@@ -1,0 +1,213 @@
+"""ShardRunner: one pipeline shard on one device — weights, paged KV pool, request bookkeeping,
+step-input construction and HIP-graph replay of decode steps.
+
+Requests are independent: each owns pages in the shard's KV pool (native C++ BlockManager), so any
+number of sequences can be in flight on a shard and a ring stage can interleave micro-batches.
+Decode steps of a given padded batch size are captured once into a HIP graph (torch.cuda.CUDAGraph
+is hipGraph on ROCm) and replayed: one host launch per shard step instead of ~10 kernels per layer.
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, List, Optional, Sequence
+
+import torch
+
+from ..inference.shard import Shard
+from ..models.config import ModelConfig
+from ..models.transformer import KVCache, ShardModel, StepInputs
+from ..models.weights import ShardWeights, random_weights
+from ..ops import linear as linear_mod
+
+PAGE = 64
+
+
+def _block_manager(num_pages: int):
+  try:
+    from .. import _runtime
+    return _runtime.BlockManager(num_pages, PAGE)
+  except ImportError:
+    from .block_manager_py import BlockManager  # pure-python fallback for hosts without the build
+    return BlockManager(num_pages, PAGE)
+
+
+def _bucket(n: int) -> int:
+  for b in (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 160, 192, 256, 320, 384, 512):
+    if n <= b:
+      return b
+  return n
+
+
+class ShardRunner:
+  def __init__(self, config: ModelConfig, shard: Shard, device: torch.device | str = "cpu",
+               weights: Optional[ShardWeights] = None, num_pages: Optional[int] = None, max_batch: int = 128,
+               max_ctx: int = 4096, kv_mem_fraction: float = 0.85, seed: int = 0, use_graphs: Optional[bool] = None):
+    self.config = config
+    self.shard = shard
+    self.device = torch.device(device)
+    if self.device.type == "cuda":
+      torch.cuda.set_device(self.device)
+    self.weights = weights if weights is not None else random_weights(config, shard, self.device, seed=seed)
+    n_layers = shard.get_layer_count()
+    per_page = KVCache.bytes_per_page(config, n_layers)
+    if num_pages is None:
+      if self.device.type == "cuda":
+        free, _ = torch.cuda.mem_get_info(self.device)
+        reserve = 4 << 30  # activations, workspaces, graphs
+        num_pages = int(max(free - reserve, per_page * 64) * kv_mem_fraction) // per_page
+      else:
+        num_pages = max(64, (max_batch * max_ctx) // PAGE // 4)
+      num_pages = min(num_pages, max_batch * (-(-max_ctx // PAGE)) + 16)
+    self.kv = KVCache(config, n_layers, num_pages, self.device)
+    self.bm = _block_manager(num_pages)
+    self.max_ctx = max_ctx
+    self.max_batch = max_batch
+    self.width = -(-max_ctx // PAGE)
+    self.model = ShardModel(self.weights, self.kv, max_batch=max_batch, max_ctx=max_ctx)
+    if use_graphs is None:
+      use_graphs = self.device.type == "cuda" and os.environ.get("XOT_GRAPHS", "1") == "1"
+    self.use_graphs = use_graphs
+    self._graphs: Dict[int, dict] = {}
+    self._tables_host = torch.zeros(max_batch, self.width, dtype=torch.int32)
+    self._ctx_host = torch.zeros(max_batch, dtype=torch.int32)
+    self._staged = None  # event marking completion of the last async H2D copy out of the pinned buffers
+    if self.device.type == "cuda":
+      self._tables_host = self._tables_host.pin_memory()
+      self._ctx_host = self._ctx_host.pin_memory()
+
+  def _reuse_staging(self) -> None:
+    """The pinned staging buffers may still be read by an in-flight async copy: wait for it."""
+    if self._staged is not None:
+      self._staged.synchronize()
+      self._staged = None
+
+  def _mark_staged(self) -> None:
+    if self.device.type == "cuda":
+      self._staged = torch.cuda.Event()
+      self._staged.record()
+
+  # ------------------------------------------------------------------ bookkeeping
+  def has(self, rid: str) -> bool:
+    return self.bm.has(rid)
+
+  def num_tokens(self, rid: str) -> int:
+    return self.bm.num_tokens(rid) if self.bm.has(rid) else 0
+
+  def free(self, rid: str) -> None:
+    self.bm.free(rid)
+
+  def can_admit(self, rid: str, n_new: int) -> bool:
+    return self.bm.can_append(rid, n_new) and self.num_tokens(rid) + n_new <= self.max_ctx
+
+  def truncate(self, rid: str, n: int) -> None:
+    self.bm.truncate(rid, n)
+
+  # ------------------------------------------------------------------ step inputs
+  def _prepare(self, rids: Sequence[str], qlens: Sequence[int]) -> StepInputs:
+    if len(rids) > self.max_batch:
+      raise ValueError(f"batch {len(rids)} exceeds max_batch {self.max_batch}")
+    self._reuse_staging()
+    pos: List[int] = []
+    slots: List[int] = []
+    cu = [0]
+    for rid, n in zip(rids, qlens):
+      start = self.num_tokens(rid)
+      if start + n > self.max_ctx:
+        raise ValueError(f"request {rid}: context {start + n} exceeds max_ctx {self.max_ctx}")
+      slots += self.bm.append(rid, n)
+      pos += range(start, start + n)
+      cu.append(cu[-1] + n)
+    B = len(rids)
+    self.bm.fill_batch(list(rids), self._tables_host[:B].numpy(), self._ctx_host[:B].numpy())
+    dev = self.device
+    nb = non_blocking = dev.type == "cuda"
+    inp = StepInputs(
+      positions=torch.tensor(pos, dtype=torch.int32).to(dev, non_blocking=nb),
+      slots=torch.tensor(slots, dtype=torch.int64).to(dev, non_blocking=nb),
+      block_tables=self._tables_host[:B].to(dev, non_blocking=non_blocking),
+      ctx_lens=self._ctx_host[:B].to(dev, non_blocking=non_blocking),
+      cu_q=torch.tensor(cu, dtype=torch.int32).to(dev, non_blocking=nb),
+      last_idx=torch.tensor([c - 1 for c in cu[1:]], dtype=torch.int64).to(dev, non_blocking=nb),
+      max_qlen=max(qlens),
+      decode=all(q == 1 for q in qlens),
+    )
+    self._mark_staged()
+    return inp
+
+  # ------------------------------------------------------------------ forward
+  def forward(self, rids: Sequence[str], qlens: Sequence[int], x: torch.Tensor) -> torch.Tensor:
+    """Run this shard for the given requests.  x = token ids [sum(qlens)] (first shard) or hidden
+    [sum(qlens), D].  Allocates KV slots for the new tokens.  Returns hidden [T, D] or, on the last
+    shard, fp32 logits [len(rids), V] of each request's last token."""
+    x = x.to(self.device, non_blocking=True)
+    if self.use_graphs and all(q == 1 for q in qlens) and len(rids) <= self.max_batch:
+      return self._decode_graph(rids, x)
+    inp = self._prepare(rids, qlens)
+    return self.model.forward(x, inp)
+
+  # ------------------------------------------------------------------ graphs
+  def _decode_graph(self, rids: Sequence[str], x: torch.Tensor) -> torch.Tensor:
+    B = len(rids)
+    Bp = min(_bucket(B), self.max_batch)
+    g = self._graphs.get(Bp)
+    if g is None:
+      g = self._capture(Bp)
+    # host bookkeeping -> static buffers
+    self._reuse_staging()
+    pos, slots = [], []
+    for rid in rids:
+      start = self.num_tokens(rid)
+      if start + 1 > self.max_ctx:
+        raise ValueError(f"request {rid}: context exceeds max_ctx {self.max_ctx}")
+      slots += self.bm.append(rid, 1)
+      pos.append(start)
+    self.bm.fill_batch(list(rids), self._tables_host[:B].numpy(), self._ctx_host[:B].numpy())
+    pad = Bp - B
+    g["pos"].copy_(torch.tensor(pos + [0] * pad, dtype=torch.int32), non_blocking=True)
+    g["slots"].copy_(torch.tensor(slots + [-1] * pad, dtype=torch.int64), non_blocking=True)
+    self._ctx_host[B:Bp] = 0
+    g["tables"].copy_(self._tables_host[:Bp], non_blocking=True)
+    g["ctx"].copy_(self._ctx_host[:Bp], non_blocking=True)
+    self._mark_staged()
+    if self.shard.is_first_layer():
+      g["x"][:B].copy_(x.view(-1).to(torch.int32))
+      if pad:
+        g["x"][B:].zero_()
+    else:
+      g["x"][:B].copy_(x)
+    g["graph"].replay()
+    return g["out"][:B]
+
+  def _capture(self, Bp: int) -> dict:
+    dev = self.device
+    c = self.config
+    g = {
+      "pos": torch.zeros(Bp, dtype=torch.int32, device=dev),
+      "slots": torch.full((Bp,), -1, dtype=torch.int64, device=dev),
+      "tables": torch.zeros(Bp, self.width, dtype=torch.int32, device=dev),
+      "ctx": torch.zeros(Bp, dtype=torch.int32, device=dev),
+      "cu": torch.arange(Bp + 1, dtype=torch.int32, device=dev),
+      "last": torch.arange(Bp, dtype=torch.int64, device=dev),
+    }
+    if self.shard.is_first_layer():
+      g["x"] = torch.zeros(Bp, dtype=torch.int32, device=dev)
+    else:
+      g["x"] = torch.zeros(Bp, c.hidden_size, dtype=torch.bfloat16, device=dev)
+    inp = StepInputs(g["pos"], g["slots"], g["tables"], g["ctx"], g["cu"], g["last"], 1, True)
+    # warm up eagerly (also settles the GEMM policy for these shapes) on a side stream
+    s = torch.cuda.Stream(dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):
+      for _ in range(2):
+        self.model.forward(g["x"], inp)
+    torch.cuda.current_stream(dev).wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    linear_mod.policy.capturing = True
+    try:
+      with torch.cuda.graph(graph):
+        g["out"] = self.model.forward(g["x"], inp)
+    finally:
+      linear_mod.policy.capturing = False
+    g["graph"] = graph
+    self._graphs[Bp] = g
+    return g
