@@ -220,3 +220,37 @@ def test_cross_entropy_and_adamw(gpu):
     pt.grad = g.clone()
     opt.step()
   assert torch.allclose(p, pt.detach(), atol=1e-5)
+
+
+@pytest.mark.parametrize("M", [1, 5, 16, 33, 64, 100, 128, 200])
+@pytest.mark.parametrize("epi,ntw,splits", [("none", 1, 1), ("none", 2, 1), ("none", 1, 4), ("resid", 1, 2),
+                                            ("silu", 2, 1), ("silu", 2, 2), ("none", 4, 1), ("silu", 4, 2),
+                                            ("resid", 4, 2)])
+def test_gemm_stream(gpu, M, epi, ntw, splits):
+  from xotorch_support_jetson_amd.ops._ext import require
+  torch.manual_seed(0)
+  N, Kd = 1024, 2048
+  x = torch.randn(M, Kd, device=gpu, dtype=torch.bfloat16)
+  w = torch.randn(N, Kd, device=gpu, dtype=torch.bfloat16) / math.sqrt(Kd)
+  b = torch.randn(N, device=gpu, dtype=torch.bfloat16)
+  r = torch.randn(M, N, device=gpu, dtype=torch.bfloat16)
+  ws = torch.empty(splits * M * N, device=gpu, dtype=torch.float32)
+  full = R.linear(x, w, b)
+  if epi == "silu":
+    f = full.view(M, N // 32, 2, 16)
+    ref = (torch.nn.functional.silu(f[:, :, 0]) * f[:, :, 1]).reshape(M, N // 2)
+    y = torch.empty(M, N // 2, device=gpu, dtype=torch.bfloat16)
+  elif epi == "resid":
+    ref = full + r.float()
+    y = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+  else:
+    ref = full
+    y = torch.empty(M, N, device=gpu, dtype=torch.float32)
+  require().gemm_stream(x, w, y, b, r if epi == "resid" else None, ws, K.EPI[epi], ntw, splits, False)
+  assert rel_err(y, ref) < 1e-2
+  if M <= 128:
+    from xotorch_support_jetson_amd.ops.weights_layout import shuffle_for_stream
+    y2 = torch.empty_like(y)
+    require().gemm_stream(x, shuffle_for_stream(w), y2, b, r if epi == "resid" else None, ws, K.EPI[epi], ntw,
+                          splits, True)
+    assert rel_err(y2, ref) < 1e-2

@@ -9,6 +9,6 @@ run() {  # run <name> <seconds> <cmd...>
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
   return 0
 }
-run t2 300 python -m pytest tests/test_kernels_gpu.py tests/test_runner_gpu.py -x -q
-run bench_small 300 python bench.py --steps 5 --warmup 2 --layers 8 --batch-per-gpu 64
+run t2 300 python -m pytest tests/ -m gpu -x -q
 run bench_full 600 python bench.py --steps 10 --warmup 3
+run bench_b256 600 python bench.py --steps 10 --warmup 3 --batch-per-gpu 256

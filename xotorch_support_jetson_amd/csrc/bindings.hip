@@ -188,6 +188,52 @@ void gemm(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const c10::op
   XCHECK(rc == 0, "gemm: unsupported shape M=", M, " N=", N, " K=", K, " epi=", epi, " algo=", algo);
 }
 
+// Decode GEMM v2 (LDS-shared X, streamed W, optional split-K over `splits` workgroup slices with
+// an fp32 workspace of >= splits*M*N floats).  ntw: 16-row n-tiles per wave (1 or 2).
+void gemm_stream(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const c10::optional<at::Tensor>& bias,
+                 const c10::optional<at::Tensor>& res, const c10::optional<at::Tensor>& ws, int64_t epi, int64_t ntw,
+                 int64_t splits, bool wshuf) {
+  CHECK_BF16(x);
+  CHECK_BF16(w);
+  CHECK_GPU(y);
+  XCHECK(x.dim() == 2 && w.dim() == 2 && y.dim() == 2, "gemm_stream: x, w, y must be 2-D");
+  XCHECK(x.stride(1) == 1 && w.is_contiguous() && y.stride(1) == 1, "gemm_stream: rows must be contiguous");
+  // a pre-shuffled weight keeps its logical [N, K] shape (the layout is a permutation of the storage)
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
+  XCHECK(w.size(1) == K, "gemm_stream: K mismatch");
+  const bool f32 = y.scalar_type() == at::kFloat;
+  XCHECK(f32 || y.scalar_type() == at::kBFloat16, "gemm_stream: y must be bf16 or fp32");
+  XCHECK(y.size(0) == M && y.size(1) == (epi == 2 ? N / 2 : N), "gemm_stream: y shape mismatch");
+  XCHECK(M <= 256, "gemm_stream: M must be <= 256");
+  if (bias.has_value()) {
+    CHECK_BF16((*bias));
+    XCHECK(bias->numel() == N && bias->is_contiguous(), "gemm_stream: bias shape mismatch");
+  }
+  int64_t ldr = 0;
+  if (epi == 1) {
+    XCHECK(res.has_value(), "gemm_stream: residual epilogue needs res");
+    CHECK_BF16((*res));
+    XCHECK(res->dim() == 2 && res->size(0) == M && res->size(1) == N && res->stride(1) == 1, "gemm_stream: res shape");
+    ldr = res->stride(0);
+  }
+  float* wsp = nullptr;
+  long ws_elems = 0;
+  if (ws.has_value()) {
+    CHECK_GPU((*ws));
+    CHECK_DT((*ws), at::kFloat);
+    XCHECK(ws->is_contiguous(), "gemm_stream: ws must be contiguous");
+    wsp = ws->data_ptr<float>();
+    ws_elems = ws->numel();
+  }
+  if (splits > 1 && epi == 1) XCHECK(res->data_ptr() != nullptr, "gemm_stream: res");
+  const int rc = xot::launch_gemm_stream(bf(x), (int)x.stride(0), bf(w), (int)K, bf_opt(bias),
+                                         epi == 1 ? bf(*res) : nullptr, (int)ldr, y.data_ptr(), (int)y.stride(0), f32,
+                                         (int)epi, wsp, ws_elems, (int)M, (int)N, (int)K, (int)ntw, (int)splits,
+                                         wshuf, cur_stream());
+  XCHECK(rc == 0, "gemm_stream: unsupported shape M=", M, " N=", N, " K=", K, " epi=", epi, " ntw=", ntw,
+         " splits=", splits);
+}
+
 void attn_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
                  const at::Tensor& block_tables, const at::Tensor& ctx_lens, at::Tensor& out, at::Tensor& ws_o,
                  at::Tensor& ws_ml, int64_t pages_per_part, int64_t nparts, double scale) {
@@ -318,6 +364,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("rope_kv_write", &rope_kv_write);
   m.def("rope_apply", &rope_apply);
   m.def("gemm", &gemm);
+  m.def("gemm_stream", &gemm_stream);
   m.def("attn_decode", &attn_decode);
   m.def("attn_prefill", &attn_prefill);
   m.def("sample", &sample);

@@ -92,8 +92,8 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(const uint16_t* __rest
       acc[i][j] += red[2][i * NT + j][lane];
     }
 
-  if constexpr (EPI == EPI_SILU) {
-    // NT == 2: n-tile 0 = gate rows [16b, 16b+16), n-tile 1 = matching up rows
+  if constexpr (EPI == EPI_SILU && NT == 2) {
+    // n-tile 0 = gate rows [16b, 16b+16), n-tile 1 = matching up rows
     const int col = blockIdx.x * 16 + c;
     float bg = 0.f, bu = 0.f;
     if (bias != nullptr) {
@@ -113,7 +113,7 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(const uint16_t* __rest
             reinterpret_cast<uint16_t*>(Yv)[(size_t)m * ldy + col] = f2bf(v);
         }
       }
-  } else {
+  } else if constexpr (EPI != EPI_SILU) {
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
       const int col = n0 + 16 * j + c;
@@ -178,6 +178,331 @@ int launch_gemm_skinny(const uint16_t* X, int ldx, const uint16_t* W, int ldw, c
   if (epi == EPI_RESID) return skinny_dispatch<EPI_RESID, false>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, M, N, K, nt, s);
   return out_f32 ? skinny_dispatch<EPI_NONE, true>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, M, N, K, nt, s)
                  : skinny_dispatch<EPI_NONE, false>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, M, N, K, nt, s);
+}
+
+// ------------------------------------------------------------------------------------ stream
+// Decode GEMM v2.  Workgroup = 4 waves side by side along N (wave w owns W rows
+// [n0 + 16*NTW*w, +16*NTW)), all M rows (<= 16*MT), K range [blockIdx.y*kper, +kper).
+// Per k-chunk (KC = 32*KS):
+//   X[:, chunk]  : cooperatively register-staged into an XOR-swizzled LDS double buffer
+//                  (physical 16-B slot = logical ^ (row & (CPR-1))) -> the 16-lane ds_read_b128
+//                  groups of the A-fragment reads hit 16 distinct bank quads
+//   W rows       : streamed once, straight to VGPRs, two chunks in flight (prefetch depth 2)
+// MFMA k-order is permuted per lane group (group g owns k in [8*KS*g, 8*KS*(g+1)) of the chunk)
+// so each lane reads 16*KS contiguous bytes of its weight row per chunk.
+// SPLIT: fp32 partial slabs ws[blockIdx.y][M][N], finished by splitk_reduce_kernel (epilogue there).
+template <int MT, int NTW, int KS, int EPI, bool OUT_F32, bool SPLIT, bool WSHUF, int OCC>
+__global__ __launch_bounds__(256, OCC) void gemm_stream_kernel(const uint16_t* __restrict__ X, int ldx,
+                                                             const uint16_t* __restrict__ W, int ldw,
+                                                             const uint16_t* __restrict__ bias,
+                                                             const uint16_t* __restrict__ R, int ldr,
+                                                             void* __restrict__ Yv, int ldy,
+                                                             float* __restrict__ ws, int M, int N, int kper) {
+  constexpr int KC = 32 * KS;
+  constexpr int CPR = KC / 8;  // 16-B chunks per row per k-chunk
+  constexpr int ROWS = 16 * MT;
+  constexpr int XPT = ROWS * CPR / 256;  // staging chunks per thread
+  static_assert(XPT >= 1, "tile too small for 256 threads");
+  __shared__ __attribute__((aligned(16))) uint16_t xs[2][ROWS * KC];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, c = lane & 15;
+  const int n0 = blockIdx.x * (64 * NTW) + wave * 16 * NTW;
+  const int kb = blockIdx.y * kper;
+  const int nch = kper / KC;
+
+  // W pointers.  Row-major: lane (g, c) streams row n0+16j+c, k in [8*KS*g, 8*KS*(g+1)) of each chunk.
+  // Pre-shuffled (WSHUF, KS == 4): tiles [N/16][K/128][s][lane][8] so instruction s of a wave reads
+  // 1 KB of contiguous memory (see ops.weights_layout.shuffle_for_stream).
+  const uint16_t* wp[NTW];
+  constexpr int WSTEP = WSHUF ? 16 * KC : KC;  // elements between consecutive chunks of one lane
+#pragma unroll
+  for (int j = 0; j < NTW; ++j) {
+    if constexpr (WSHUF)
+      wp[j] = W + ((size_t)((n0 >> 4) + j) * (ldw / KC) + kb / KC) * (16 * KC) + lane * 8;
+    else
+      wp[j] = W + (size_t)(n0 + 16 * j + c) * ldw + kb + g * 8 * KS;
+  }
+
+  // staging geometry of this thread's XPT chunks, recomputed on use (keeps VGPRs for the pipeline):
+  // chunk q = tid + 256*i -> row q / CPR, logical 16-B slot q % CPR
+  const uint16_t* xbase = X + kb;
+  auto xload = [&](s16x8 (&xr)[XPT], int ch) {
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const int q = tid + 256 * i, row = q / CPR, cc = q % CPR;
+      const bool ok = row < M;
+      s16x8 v = ld16(xbase + (size_t)(ok ? row : 0) * ldx + ch * KC + cc * 8);
+      xr[i] = ok ? v : s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  };
+  auto xstore = [&](const s16x8 (&xr)[XPT], int buf) {
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const int q = tid + 256 * i, row = q / CPR, cc = q % CPR;
+      st16(&xs[buf][row * KC + ((cc ^ (row & (CPR - 1))) * 8)], xr[i]);
+    }
+  };
+  auto wload = [&](s16x8 (&wr)[NTW][KS], int ch) {
+#pragma unroll
+    for (int j = 0; j < NTW; ++j)
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+        wr[j][s] = __builtin_nontemporal_load(
+            reinterpret_cast<const s16x8*>(wp[j] + ch * WSTEP + (WSHUF ? 512 * s : 8 * s)));
+  };
+
+  f32x4 acc[MT][NTW];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // nch is even and >= 2 (checked by the dispatcher): prologue loads chunks 0 and 1
+  s16x8 xr[XPT];
+  s16x8 wa[NTW][KS], wb[NTW][KS];
+  xload(xr, 0);
+  wload(wa, 0);
+  xstore(xr, 0);
+  xload(xr, 1);
+  wload(wb, 1);
+  __syncthreads();
+
+  auto compute = [&](const s16x8 (&wr)[NTW][KS], int buf) {
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        const int row = 16 * i + c;
+        const int phys = (g * KS + s) ^ (row & (CPR - 1));
+        const s16x8 a = ld16(&xs[buf][row * KC + phys * 8]);
+#pragma unroll
+        for (int j = 0; j < NTW; ++j) acc[i][j] = mfma16(a, wr[j][s], acc[i][j]);
+      }
+    }
+  };
+
+  // Steady state: two chunks per trip (static register double buffer), every load unconditional so
+  // hipcc's waitcnt pass keeps counted vmcnt(N) waits across the back-edge instead of draining to 0.
+  int ch = 0;
+  for (; ch + 2 < nch; ch += 2) {
+    compute(wa, 0);
+    xstore(xr, 1);
+    __syncthreads();
+    xload(xr, ch + 2);
+    wload(wa, ch + 2);
+    compute(wb, 1);
+    xstore(xr, 0);
+    __syncthreads();
+    xload(xr, ch + 3);
+    wload(wb, ch + 3);
+  }
+  // tail: chunks nch-2 (wa, buf 0) and nch-1 (wb / xr)
+  compute(wa, 0);
+  xstore(xr, 1);
+  __syncthreads();
+  compute(wb, 1);
+
+  if constexpr (SPLIT) {
+    float* slab = ws + (size_t)blockIdx.y * M * N;
+#pragma unroll
+    for (int j = 0; j < NTW; ++j)
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = 16 * i + 4 * g + r;
+          if (m < M) slab[(size_t)m * N + n0 + 16 * j + c] = acc[i][j][r];
+        }
+  } else if constexpr (EPI == EPI_SILU && NTW >= 2) {
+#pragma unroll
+    for (int p = 0; p < NTW / 2; ++p) {  // pair (gate tile 2p, up tile 2p+1) -> 16 output columns
+      const int col = (n0 >> 1) + 16 * p + c;
+      float bg = 0.f, bu = 0.f;
+      if (bias != nullptr) {
+        bg = bf2f(bias[n0 + 32 * p + c]);
+        bu = bf2f(bias[n0 + 32 * p + 16 + c]);
+      }
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = 16 * i + 4 * g + r;
+          if (m < M) {
+            const float v = silu(acc[i][2 * p][r] + bg) * (acc[i][2 * p + 1][r] + bu);
+            if constexpr (OUT_F32)
+              reinterpret_cast<float*>(Yv)[(size_t)m * ldy + col] = v;
+            else
+              reinterpret_cast<uint16_t*>(Yv)[(size_t)m * ldy + col] = f2bf(v);
+          }
+        }
+    }
+  } else if constexpr (EPI != EPI_SILU) {
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+      const int col = n0 + 16 * j + c;
+      const float b = bias != nullptr ? bf2f(bias[col]) : 0.f;
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = 16 * i + 4 * g + r;
+          if (m < M) {
+            float v = acc[i][j][r] + b;
+            if constexpr (EPI == EPI_RESID) v += bf2f(R[(size_t)m * ldr + col]);
+            if constexpr (OUT_F32)
+              reinterpret_cast<float*>(Yv)[(size_t)m * ldy + col] = v;
+            else
+              reinterpret_cast<uint16_t*>(Yv)[(size_t)m * ldy + col] = f2bf(v);
+          }
+        }
+    }
+  }
+}
+
+// Sum S fp32 slabs [S][M][N] and apply the epilogue.  One thread per 8 output columns.
+template <int EPI, bool OUT_F32>
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, int S, int M, int N,
+                                                            const uint16_t* __restrict__ bias,
+                                                            const uint16_t* __restrict__ R, int ldr,
+                                                            void* __restrict__ Yv, int ldy) {
+  const int ncol = EPI == EPI_SILU ? N / 2 : N;
+  const long total = (long)M * (ncol / 8);
+  for (long t = blockIdx.x * 256L + threadIdx.x; t < total; t += (long)gridDim.x * 256) {
+    const int m = (int)(t / (ncol / 8));
+    const int o = (int)(t % (ncol / 8)) * 8;
+    float v[8];
+    if constexpr (EPI == EPI_SILU) {
+      const int j = o >> 4, w = o & 15;
+      float gs[8], us[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) gs[e] = us[e] = 0.f;
+      for (int s = 0; s < S; ++s) {
+        const float* row = ws + ((size_t)s * M + m) * N;
+        const f32x4 g0 = *reinterpret_cast<const f32x4*>(row + 32 * j + w);
+        const f32x4 g1 = *reinterpret_cast<const f32x4*>(row + 32 * j + w + 4);
+        const f32x4 u0 = *reinterpret_cast<const f32x4*>(row + 32 * j + 16 + w);
+        const f32x4 u1 = *reinterpret_cast<const f32x4*>(row + 32 * j + 16 + w + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          gs[e] += g0[e];
+          gs[e + 4] += g1[e];
+          us[e] += u0[e];
+          us[e + 4] += u1[e];
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float bg = bias ? bf2f(bias[32 * j + w + e]) : 0.f, bu = bias ? bf2f(bias[32 * j + 16 + w + e]) : 0.f;
+        v[e] = silu(gs[e] + bg) * (us[e] + bu);
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = 0.f;
+      for (int s = 0; s < S; ++s) {
+        const float* row = ws + ((size_t)s * M + m) * N + o;
+        const f32x4 a = *reinterpret_cast<const f32x4*>(row), b = *reinterpret_cast<const f32x4*>(row + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] += a[e];
+          v[e + 4] += b[e];
+        }
+      }
+      if (bias != nullptr) {
+        const s16x8 bb = ld16(bias + o);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += bf2f(bb[e]);
+      }
+      if constexpr (EPI == EPI_RESID) {
+        const s16x8 rr = ld16(R + (size_t)m * ldr + o);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += bf2f(rr[e]);
+      }
+    }
+    if constexpr (OUT_F32) {
+      float* y = reinterpret_cast<float*>(Yv) + (size_t)m * ldy + o;
+      *reinterpret_cast<f32x4*>(y) = f32x4{v[0], v[1], v[2], v[3]};
+      *reinterpret_cast<f32x4*>(y + 4) = f32x4{v[4], v[5], v[6], v[7]};
+    } else {
+      s16x8 out;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) out[e] = (short)f2bf(v[e]);
+      st16(reinterpret_cast<uint16_t*>(Yv) + (size_t)m * ldy + o, out);
+    }
+  }
+}
+
+template <int MT, int NTW, int KS, int EPI, bool F32, bool WSH>
+static void stream_launch(const uint16_t* X, int ldx, const uint16_t* W, int ldw, const uint16_t* bias,
+                          const uint16_t* R, int ldr, void* Y, int ldy, float* ws, int M, int N, int K, int S,
+                          hipStream_t st) {
+  // occupancy request: 2 workgroups/CU while the register budget allows it
+  constexpr int OCC = (MT * NTW >= 32) ? 1 : 2;
+  dim3 grid(N / (64 * NTW), S);
+  const int kper = K / S;
+  if (S == 1) {
+    gemm_stream_kernel<MT, NTW, KS, EPI, F32, false, WSH, OCC><<<grid, 256, 0, st>>>(X, ldx, W, ldw, bias, R, ldr,
+                                                                                     Y, ldy, nullptr, M, N, kper);
+  } else {
+    gemm_stream_kernel<MT, NTW, KS, EPI, F32, true, WSH, OCC><<<grid, 256, 0, st>>>(X, ldx, W, ldw, bias, R, ldr, Y,
+                                                                                    ldy, ws, M, N, kper);
+    const int ncol = EPI == EPI_SILU ? N / 2 : N;
+    long chunks = (long)M * (ncol / 8);
+    int blocks = (int)((chunks + 255) / 256);
+    if (blocks > 2048) blocks = 2048;
+    splitk_reduce_kernel<EPI, F32><<<blocks, 256, 0, st>>>(ws, S, M, N, bias, R, ldr, Y, ldy);
+  }
+}
+
+template <int EPI, bool F32>
+static int stream_dispatch(const uint16_t* X, int ldx, const uint16_t* W, int ldw, const uint16_t* bias,
+                           const uint16_t* R, int ldr, void* Y, int ldy, float* ws, long ws_elems, int M, int N,
+                           int K, int ntw, int S, bool wshuf, hipStream_t st) {
+  if (EPI == EPI_SILU && ntw == 1) ntw = 2;
+  if (ntw != 1 && ntw != 2 && ntw != 4) return -1;
+  const int mt = (M + 15) / 16;
+  if (ntw == 4 && mt <= 2) ntw = 2;
+  if (N % (64 * ntw) != 0 || S < 1) return -1;
+  const int KS = mt <= 8 ? 4 : 2;
+  if (K % (S * 64 * KS) != 0) return -1;  // an even number (>= 2) of k-chunks per workgroup
+  if (S > 1 && (ws == nullptr || ws_elems < (long)S * M * N)) return -1;
+  if (EPI == EPI_SILU && N % 32 != 0) return -1;
+  if (wshuf && (KS != 4 || K % 128 != 0)) return -1;
+#define XOT_ST2(MTV, KSV, WSH)                                                                              \
+  do {                                                                                                      \
+    if (ntw == 1 && EPI != EPI_SILU)                                                                        \
+      stream_launch<MTV, 1, KSV, EPI, F32, WSH>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, M, N, K, S, st);  \
+    else if (ntw == 4 && MTV >= 4)                                                                          \
+      stream_launch<MTV, 4, KSV, EPI, F32, WSH>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, M, N, K, S, st);  \
+    else                                                                                                    \
+      stream_launch<MTV, 2, KSV, EPI, F32, WSH>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, M, N, K, S, st);  \
+    return 0;                                                                                               \
+  } while (0)
+#define XOT_ST(MTV, KSV)                  \
+  do {                                    \
+    if (wshuf) XOT_ST2(MTV, KSV, true);   \
+    XOT_ST2(MTV, KSV, false);             \
+  } while (0)
+  if (mt <= 1) XOT_ST(1, 4);
+  if (mt <= 2) XOT_ST(2, 4);
+  if (mt <= 4) XOT_ST(4, 4);
+  if (mt <= 8) XOT_ST(8, 4);
+  if (mt <= 16 && !wshuf) XOT_ST2(16, 2, false);
+#undef XOT_ST
+#undef XOT_ST2
+  return -1;
+}
+
+int launch_gemm_stream(const uint16_t* X, int ldx, const uint16_t* W, int ldw, const uint16_t* bias,
+                       const uint16_t* R, int ldr, void* Y, int ldy, bool out_f32, int epi, float* ws, long ws_elems,
+                       int M, int N, int K, int ntw, int S, bool wshuf, hipStream_t s) {
+  if (M <= 0) return 0;
+  if (epi == EPI_SILU)
+    return out_f32 ? stream_dispatch<EPI_SILU, true>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, ntw, S, wshuf, s)
+                   : stream_dispatch<EPI_SILU, false>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, ntw, S, wshuf, s);
+  if (epi == EPI_RESID)
+    return out_f32 ? -1 : stream_dispatch<EPI_RESID, false>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, ntw, S, wshuf, s);
+  return out_f32 ? stream_dispatch<EPI_NONE, true>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, ntw, S, wshuf, s)
+                 : stream_dispatch<EPI_NONE, false>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, ntw, S, wshuf, s);
 }
 
 // ------------------------------------------------------------------------------------ tiled

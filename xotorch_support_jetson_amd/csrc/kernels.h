@@ -25,6 +25,9 @@ void launch_rope_apply(const uint16_t* x, uint16_t* y, const int32_t* pos, const
 int launch_gemm_skinny(const uint16_t* X, int ldx, const uint16_t* W, int ldw, const uint16_t* bias,
                        const uint16_t* R, int ldr, void* Y, int ldy, bool out_f32, int epi, int M, int N, int K,
                        int nt, hipStream_t s);
+int launch_gemm_stream(const uint16_t* X, int ldx, const uint16_t* W, int ldw, const uint16_t* bias,
+                       const uint16_t* R, int ldr, void* Y, int ldy, bool out_f32, int epi, float* ws, long ws_elems,
+                       int M, int N, int K, int ntw, int S, bool wshuf, hipStream_t s);
 int launch_gemm_tiled(const uint16_t* X, int ldx, const uint16_t* W, int ldw, const uint16_t* bias,
                       const uint16_t* R, int ldr, void* Y, int ldy, bool out_f32, int epi, int M, int N, int K,
                       hipStream_t s);

@@ -29,7 +29,7 @@ from ..ops import kernels as K
 from ..ops.linear import linear
 from ..ops.rope import build_cos_sin
 from .config import ModelConfig
-from .weights import ShardWeights
+from .weights import ShardWeights, expert
 
 PAGE = 64
 
@@ -125,8 +125,8 @@ class ShardModel:
         continue
       idx = tok[start:start + n]
       xe = xn.index_select(0, idx)
-      act = linear(xe, lw.gu_w[e], epi="silu")
-      ye = linear(act, lw.down_w[e], out_dtype=torch.float32)
+      act = linear(xe, expert(lw.gu_w, e), epi="silu")
+      ye = linear(act, expert(lw.down_w, e), out_dtype=torch.float32)
       out.index_add_(0, idx, ye * wflat[start:start + n, None])
       start += n
     h += out.to(h.dtype)

@@ -89,32 +89,88 @@ class ShardWeights:
     sd: Dict[str, torch.Tensor] = {}
     for i, lw in self.layers.items():
       p = f"model.layers.{i}."
-      q, k, v = lw.qkv_w.split([H * Dh, Hkv * Dh, Hkv * Dh], 0)
+      q, k, v = _rowmajor(lw.qkv_w).split([H * Dh, Hkv * Dh, Hkv * Dh], 0)
       sd[p + "self_attn.q_proj.weight"], sd[p + "self_attn.k_proj.weight"], sd[p + "self_attn.v_proj.weight"] = q, k, v
       if lw.qkv_b is not None:
         qb, kb, vb = lw.qkv_b.split([H * Dh, Hkv * Dh, Hkv * Dh], 0)
         sd[p + "self_attn.q_proj.bias"], sd[p + "self_attn.k_proj.bias"], sd[p + "self_attn.v_proj.bias"] = qb, kb, vb
-      sd[p + "self_attn.o_proj.weight"] = lw.o_w
+      sd[p + "self_attn.o_proj.weight"] = _rowmajor(lw.o_w)
       sd[p + "input_layernorm.weight"] = lw.ln1
       sd[p + "post_attention_layernorm.weight"] = lw.ln2
+      gu, down = _rowmajor(lw.gu_w), _rowmajor(lw.down_w)
       if c.is_moe:
         sd[p + "block_sparse_moe.gate.weight"] = lw.router
-        g, u = split_gate_up(lw.gu_w)
+        g, u = split_gate_up(gu)
         for e in range(c.num_experts):
           sd[p + f"block_sparse_moe.experts.{e}.w1.weight"] = g[e]
           sd[p + f"block_sparse_moe.experts.{e}.w3.weight"] = u[e]
-          sd[p + f"block_sparse_moe.experts.{e}.w2.weight"] = lw.down_w[e]
+          sd[p + f"block_sparse_moe.experts.{e}.w2.weight"] = down[e]
       else:
-        g, u = split_gate_up(lw.gu_w)
+        g, u = split_gate_up(gu)
         sd[p + "mlp.gate_proj.weight"], sd[p + "mlp.up_proj.weight"] = g, u
-        sd[p + "mlp.down_proj.weight"] = lw.down_w
+        sd[p + "mlp.down_proj.weight"] = down
     if self.embed is not None:
       sd["model.embed_tokens.weight"] = self.embed
     if self.norm is not None:
       sd["model.norm.weight"] = self.norm
-    if self.lm_head is not None and not (c.tie_word_embeddings and self.embed is not None and self.lm_head is self.embed):
-      sd["lm_head.weight"] = self.lm_head
+    if self.lm_head is not None and not c.tie_word_embeddings:
+      sd["lm_head.weight"] = _rowmajor(self.lm_head)
+    elif self.lm_head is not None and self.embed is None:
+      sd["model.embed_tokens.weight"] = _rowmajor(self.lm_head)  # tied head on a shard without the embedding
     return {k: v.contiguous() for k, v in sd.items()}
+
+
+def _rowmajor(t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+  """Row-major view of a possibly pre-shuffled device weight (2-D, or 3-D expert stacks)."""
+  if t is None or getattr(t, "xot_layout", "rowmajor") != "stream":
+    return t
+  from ..ops.weights_layout import unshuffle_from_stream
+  if t.dim() == 3:
+    return torch.stack([unshuffle_from_stream(t[e]) for e in range(t.shape[0])])
+  return unshuffle_from_stream(t)
+
+
+def expert(t: torch.Tensor, e: int) -> torch.Tensor:
+  """Expert e's [rows, K] weight, keeping the storage-layout tag of the stack."""
+  v = t[e]
+  if hasattr(t, "xot_layout"):
+    v.xot_layout = t.xot_layout
+  return v
+
+
+def prepare_for_decode(sw: "ShardWeights") -> "ShardWeights":
+  """Convert the projection weights of a GPU shard to the pre-shuffled stream layout (in place).
+  The embedding stays row-major (it is gathered); a tied LM head gets its own shuffled copy."""
+  from ..ops.weights_layout import can_shuffle, shuffle_for_stream
+  if sw.embed is not None and not sw.embed.is_cuda:
+    return sw
+  if sw.lm_head is None and not sw.layers:
+    return sw
+
+  def conv(t):
+    if t is None or not t.is_cuda or getattr(t, "xot_layout", "rowmajor") == "stream":
+      return t
+    if t.dim() == 3:
+      if not all(can_shuffle(t[e]) for e in range(t.shape[0])):
+        return t
+      out = torch.empty_like(t)
+      for e in range(t.shape[0]):
+        out[e] = shuffle_for_stream(t[e])
+    else:
+      if not can_shuffle(t):
+        return t
+      out = shuffle_for_stream(t)
+    out.xot_layout = "stream"
+    return out
+
+  for lw in sw.layers.values():
+    lw.qkv_w = conv(lw.qkv_w)
+    lw.o_w = conv(lw.o_w)
+    lw.gu_w = conv(lw.gu_w)
+    lw.down_w = conv(lw.down_w)
+  if sw.lm_head is not None:
+    sw.lm_head = conv(sw.lm_head)  # a tied head becomes a separate shuffled copy; embed stays row-major
+  return sw
 
 
 def _needs_embed(c: ModelConfig, s: Shard) -> bool:

@@ -16,7 +16,7 @@ import torch
 from ..inference.shard import Shard
 from ..models.config import ModelConfig
 from ..models.transformer import KVCache, ShardModel, StepInputs
-from ..models.weights import ShardWeights, random_weights
+from ..models.weights import ShardWeights, prepare_for_decode, random_weights
 from ..ops import linear as linear_mod
 
 PAGE = 64
@@ -48,6 +48,8 @@ class ShardRunner:
     if self.device.type == "cuda":
       torch.cuda.set_device(self.device)
     self.weights = weights if weights is not None else random_weights(config, shard, self.device, seed=seed)
+    if self.device.type == "cuda" and os.environ.get("XOT_SHUFFLE", "1") == "1":
+      prepare_for_decode(self.weights)  # projection weights -> pre-shuffled stream-GEMM layout
     n_layers = shard.get_layer_count()
     per_page = KVCache.bytes_per_page(config, n_layers)
     if num_pages is None:
@@ -65,7 +67,8 @@ class ShardRunner:
     self.width = -(-max_ctx // PAGE)
     self.model = ShardModel(self.weights, self.kv, max_batch=max_batch, max_ctx=max_ctx)
     if use_graphs is None:
-      use_graphs = self.device.type == "cuda" and os.environ.get("XOT_GRAPHS", "1") == "1"
+      # MoE routing sizes expert groups on the host (not capturable yet)
+      use_graphs = self.device.type == "cuda" and os.environ.get("XOT_GRAPHS", "1") == "1" and not config.is_moe
     self.use_graphs = use_graphs
     self._graphs: Dict[int, dict] = {}
     self._tables_host = torch.zeros(max_batch, self.width, dtype=torch.int32)
