@@ -60,7 +60,9 @@ class AsyncCallback(Generic[T]):
   def set(self, *args: T) -> None:
     self.result = args
     for fn in list(self.observers):
-      fn(*args)
+      out = fn(*args)
+      if asyncio.iscoroutine(out):  # async observers are scheduled on the running loop
+        asyncio.get_running_loop().create_task(out)
     try:
       asyncio.get_running_loop().create_task(self._notify())
     except RuntimeError:

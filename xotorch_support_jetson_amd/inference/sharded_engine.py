@@ -1,0 +1,217 @@
+"""ShardedInferenceEngine: the MI355X engine behind the Node (reference: TorchDynamicShardInferenceEngine,
+xotorch/inference/torch/sharded_inference_engine.py:37-424).
+
+Differences by design:
+  * one ShardRunner per shard: HIP kernels, paged per-request KV (concurrent requests do not clobber
+    each other as they do in the reference's single global cache), HIP-graph decode;
+  * the inference state shipped between peers is {"n_past": int} — positions and masks are derived
+    on the device (the reference JSON-ships tokens, positions and a [1,T,T] mask on every hop);
+  * hidden states travel as bf16 tensors; the last shard returns fp32 logits of the last token only;
+  * per-request temperature reaches the sampler (the reference drops the API temperature).
+Weights come from a local HF snapshot of the shard when present (safetensors, this shard's tensors
+only) and otherwise from the deterministic random init of the exact architecture (offline boxes).
+"""
+from __future__ import annotations
+
+import asyncio
+import os
+from concurrent.futures import ThreadPoolExecutor
+from pathlib import Path
+from typing import Optional, Tuple
+
+import numpy as np
+import torch
+
+from ..helpers import DEBUG
+from ..models import registry
+from ..models.config import ModelConfig, load_config, preset
+from .inference_engine import InferenceEngine
+from .shard import Shard
+from .tokenizers import _resolve_tokenizer
+
+TEMPERATURE = 0.6
+TOP_K = 35
+
+
+def default_device() -> torch.device:
+  env = os.environ.get("TORCH_DEVICE") or os.environ.get("XOT_DEVICE")
+  if env:
+    return torch.device(env)
+  if torch.cuda.is_available():
+    return torch.device("cuda", int(os.environ.get("LOCAL_RANK", 0)) % max(1, torch.cuda.device_count()))
+  return torch.device("cpu")
+
+
+class ShardedInferenceEngine(InferenceEngine):
+  def __init__(self, shard_downloader=None, device: Optional[torch.device] = None, seed: int = 1234):
+    self.shard: Optional[Shard] = None
+    self.shard_downloader = shard_downloader
+    self.device = device or default_device()
+    self.executor = ThreadPoolExecutor(max_workers=1, thread_name_prefix="xot-engine")
+    self.runner = None
+    self.config: Optional[ModelConfig] = None
+    self.tokenizer = None
+    self.model_path: Optional[Path] = None
+    self.seed = seed
+    self.seed_off = torch.tensor([seed, 0], dtype=torch.int64)
+    self._lock = asyncio.Lock()
+    self.trainer = None
+
+  # ------------------------------------------------------------------ helpers
+  async def _run(self, fn, *args):
+    return await asyncio.get_running_loop().run_in_executor(self.executor, fn, *args)
+
+  async def encode(self, shard: Shard, prompt: str) -> np.ndarray:
+    await self.ensure_shard(shard)
+    ids = self.tokenizer.encode(prompt)
+    return np.asarray(ids, dtype=np.int64)
+
+  async def decode(self, shard: Shard, tokens: np.ndarray) -> str:
+    await self.ensure_shard(shard)
+    return self.tokenizer.decode(np.asarray(tokens).reshape(-1).tolist())
+
+  async def sample(self, x, temp: float = TEMPERATURE, top_k: int = TOP_K) -> np.ndarray:
+    def _sample():
+      from ..ops import kernels as K
+      logits = torch.as_tensor(x) if not isinstance(x, torch.Tensor) else x
+      logits = logits.reshape(-1, logits.shape[-1]).to(self.device, torch.float32).contiguous()
+      temps = torch.full((logits.shape[0],), float(temp), dtype=torch.float32, device=self.device)
+      so = self.seed_off.to(self.device)
+      tok = K.sample(logits, temps, int(top_k), so)
+      self.seed_off[1] += 1
+      return tok.cpu().numpy().astype(np.int64)
+
+    return await self._run(_sample)
+
+  # ------------------------------------------------------------------ forward
+  async def infer_tensor(self, request_id: str, shard: Shard, input_data,
+                         inference_state: Optional[dict] = None) -> Tuple[object, Optional[dict]]:
+    await self.ensure_shard(shard)
+
+    def _infer():
+      if self.trainer is not None and self.trainer.dirty:
+        self.trainer.sync_to_inference()  # serve the weights training just produced
+      x = input_data if isinstance(input_data, torch.Tensor) else torch.as_tensor(np.asarray(input_data))
+      if x.dim() == 3:  # hidden [1, L, D]
+        L = x.shape[1]
+        xin = x.reshape(L, x.shape[2]).to(torch.bfloat16)
+      else:  # token ids [1, L]
+        xin = x.reshape(-1).to(torch.int32)
+        L = xin.numel()
+      try:
+        out = self.runner.forward([request_id], [L], xin)
+      except torch.cuda.OutOfMemoryError:
+        self.clear_model()
+        raise
+      n_past = self.runner.num_tokens(request_id)
+      state = {"n_past": n_past}
+      if self.shard.is_last_layer():
+        return out[-1:].float().cpu().numpy(), state  # [1, V] logits of the last token
+      return out.reshape(1, L, -1).cpu(), state  # bf16 hidden [1, L, D]
+
+    return await self._run(_infer)
+
+  async def finish_request(self, request_id: str) -> None:
+    if self.runner is not None:
+      await self._run(self.runner.free, request_id)
+
+  # ------------------------------------------------------------------ shard lifecycle
+  def _model_dir(self, shard: Shard) -> Optional[Path]:
+    repo = registry.get_repo(shard.model_id, "ShardedInferenceEngine")
+    if repo is None:
+      return None
+    from ..helpers import xot_home
+    p = xot_home() / "downloads" / repo.replace("/", "--")
+    return p if (p / "config.json").exists() else None
+
+  async def ensure_shard(self, shard: Shard):
+    if self.shard == shard and self.runner is not None:
+      return
+    async with self._lock:
+      if self.shard == shard and self.runner is not None:
+        return
+      model_dir = None
+      if self.shard_downloader is not None and shard.model_id not in registry.SYNTHETIC:
+        try:
+          model_dir = await self.shard_downloader.ensure_shard(shard, "ShardedInferenceEngine")
+        except Exception as e:
+          if DEBUG >= 1:
+            print(f"download of {shard.model_id} unavailable ({e}); using synthetic weights")
+      model_dir = Path(model_dir) if model_dir else self._model_dir(shard)
+      await self._run(self._build, shard, model_dir)
+
+  def _build(self, shard: Shard, model_dir: Optional[Path]):
+    from ..models.weights import load_hf_weights
+    from ..runtime.runner import ShardRunner
+    self.clear_model()
+    if model_dir is not None and (model_dir / "config.json").exists():
+      cfg = load_config(model_dir)
+      registry.validate_layers(shard.model_id, cfg.num_layers)
+    else:
+      cfg = preset(shard.model_id)
+    if cfg.num_layers != shard.n_layers:
+      cfg = cfg.with_layers(shard.n_layers)
+    weights = None
+    if model_dir is not None and any(model_dir.glob("*.safetensors")):
+      weights = load_hf_weights(model_dir, cfg, shard, self.device)
+    elif DEBUG >= 1:
+      print(f"[engine] {shard.model_id}: no local weights, random-init {cfg.model_type} shard {shard}")
+    max_ctx = int(os.environ.get("XOT_MAX_CTX", 8192 if self.device.type == "cuda" else 2048))
+    max_ctx = min(max_ctx, cfg.max_position_embeddings)
+    self.runner = ShardRunner(cfg, shard, self.device, weights=weights, max_batch=int(os.environ.get("XOT_MAX_BATCH", 64)),
+                              max_ctx=max_ctx, seed=0)
+    self.config = cfg
+    self.model_path = model_dir
+    self.tokenizer = _resolve_tokenizer(model_dir if model_dir is not None else
+                                        (registry.get_repo(shard.model_id, "ShardedInferenceEngine") or "byte"),
+                                        cfg.vocab_size)
+    self.shard = shard
+
+  def clear_model(self):
+    self.runner = None
+    self.shard = None
+    if self.device.type == "cuda":
+      torch.cuda.empty_cache()
+
+  @property
+  def eos_token_ids(self):
+    ids = set(self.config.eos_token_ids) if self.config else set()
+    tid = getattr(self.tokenizer, "eos_token_id", None)
+    if tid is not None:
+      ids.add(int(tid))
+    return ids
+
+  # ------------------------------------------------------------------ checkpoints / training
+  async def load_checkpoint(self, shard: Shard, path: str):
+    from ..train.checkpoint import load_shard_checkpoint
+    await self.ensure_shard(shard)
+    await self._run(load_shard_checkpoint, self, shard, path)
+
+  async def save_checkpoint(self, shard: Shard, path: str):
+    from ..train.checkpoint import save_shard_checkpoint
+    await self.ensure_shard(shard)
+    await self._run(save_shard_checkpoint, self, shard, path)
+
+  def _get_trainer(self):
+    from ..train.trainer import ShardTrainer
+    if self.trainer is None or self.trainer.shard != self.shard:
+      self.trainer = ShardTrainer(self.runner.weights, self.device)
+    return self.trainer
+
+  async def train(self, request_id, shard, example, target, length, train=True, loss="length_masked_ce"):
+    await self.ensure_shard(shard)
+    return await self._run(lambda: self._get_trainer().step(request_id, example, target, length, train=train,
+                                                            loss=loss))
+
+  async def train_forward(self, request_id, shard, example):
+    """Forward of a non-last pipeline stage for training (no KV cache): the activation to send on."""
+    await self.ensure_shard(shard)
+    return await self._run(lambda: self._get_trainer().train_forward(example))
+
+  async def eval_forward(self, request_id, shard, example):
+    return await self.train_forward(request_id, shard, example)
+
+  async def evaluate(self, request_id, shard, example, target, length, loss="length_masked_ce"):
+    await self.ensure_shard(shard)
+    return await self._run(lambda: self._get_trainer().step(request_id, example, target, length, train=False,
+                                                            evaluate=True))

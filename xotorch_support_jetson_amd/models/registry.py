@@ -64,6 +64,7 @@ _CARDS: List[tuple] = [
 ]
 
 model_cards: Dict[str, dict] = {mid: {"layers": n, "repo": {ENGINE: repo}} for mid, n, repo, _ in _CARDS}
+SYNTHETIC = {mid for mid, _, repo, _ in _CARDS if repo.startswith("synthetic/")}
 model_cards["dummy"] = {"layers": 8, "repo": {DUMMY: "dummy"}}
 pretty_name: Dict[str, str] = {mid: pretty for mid, _, _, pretty in _CARDS}
 pretty_name["dummy"] = "Dummy"

@@ -173,6 +173,42 @@ def prepare_for_decode(sw: "ShardWeights") -> "ShardWeights":
   return sw
 
 
+@torch.no_grad()
+def assign_weight(dst: Optional[torch.Tensor], src: torch.Tensor) -> None:
+  """Write a row-major `src` into `dst` IN PLACE, honouring dst's storage layout (pre-shuffled or
+  not).  In-place matters: captured HIP graphs hold the addresses of the inference weights."""
+  if dst is None:
+    return
+  src = src.to(device=dst.device, dtype=dst.dtype)
+  if getattr(dst, "xot_layout", "rowmajor") == "stream":
+    from ..ops.weights_layout import shuffle_for_stream
+    if dst.dim() == 3:
+      for e in range(dst.shape[0]):
+        dst[e].copy_(shuffle_for_stream(src[e]))
+    else:
+      dst.copy_(shuffle_for_stream(src))
+  else:
+    dst.copy_(src)
+
+
+@torch.no_grad()
+def copy_weights_into(dst: "ShardWeights", src: "ShardWeights") -> None:
+  """Copy every tensor of the row-major `src` shard into the live inference shard `dst` in place."""
+  for i, lw in dst.layers.items():
+    s = src.layers[i]
+    for name in ("qkv_w", "o_w", "gu_w", "down_w", "ln1", "ln2", "qkv_b", "router"):
+      if getattr(lw, name) is not None and getattr(s, name) is not None:
+        assign_weight(getattr(lw, name), getattr(s, name))
+  if dst.embed is not None and src.embed is not None:
+    assign_weight(dst.embed, src.embed)
+  if dst.norm is not None and src.norm is not None:
+    assign_weight(dst.norm, src.norm)
+  if dst.lm_head is not None and dst.lm_head is not dst.embed:
+    head = src.lm_head if src.lm_head is not None else src.embed
+    if head is not None:
+      assign_weight(dst.lm_head, head)
+
+
 def _needs_embed(c: ModelConfig, s: Shard) -> bool:
   return s.is_first_layer() or (s.is_last_layer() and c.tie_word_embeddings)
 

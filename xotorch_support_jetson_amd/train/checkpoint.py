@@ -1,0 +1,94 @@
+"""Per-shard checkpoints (reference design: node.py:230-252 + the unimplemented save_checkpoint).
+
+File: {dir}/{model_id}/{start:03d}-{end:03d}-of-{n:03d}-{iteration:06d}.safetensors with HF tensor names
+(un-shuffled, gate/up split), so a checkpoint written by one partition can be loaded by any other:
+loading picks every tensor of the requested layer range from all shard files of the newest iteration.
+Optimizer state (fp32 master weights + AdamW moments + step) goes to a `.optim.safetensors` sidecar.
+`--resume-checkpoint DIR` (parsed but never read by the reference) resumes from the newest iteration.
+"""
+from __future__ import annotations
+
+import re
+from pathlib import Path
+from typing import Dict, List, Optional, Tuple
+
+import torch
+
+from ..inference.shard import Shard
+
+_NAME = re.compile(r"^(\d{3})-(\d{3})-of-(\d{3})-(\d{6})\.safetensors$")
+
+
+def checkpoint_path(directory: str | Path, shard: Shard, iteration: int) -> Path:
+  return (Path(directory) / shard.model_id /
+          f"{shard.start_layer:03d}-{shard.end_layer:03d}-of-{shard.n_layers:03d}-{iteration:06d}.safetensors")
+
+
+def list_checkpoints(directory: str | Path, model_id: str) -> List[Tuple[int, int, int, int, Path]]:
+  d = Path(directory) / model_id
+  out = []
+  if d.exists():
+    for p in d.iterdir():
+      m = _NAME.match(p.name)
+      if m:
+        s, e, n, it = map(int, m.groups())
+        out.append((it, s, e, n, p))
+  return sorted(out)
+
+
+def save_shard_checkpoint(engine, shard: Shard, path: str | Path) -> Path:
+  from safetensors.torch import save_file
+  path = Path(path)
+  path.parent.mkdir(parents=True, exist_ok=True)
+  trainer = getattr(engine, "trainer", None)
+  if trainer is not None:
+    trainer.sync_to_inference()
+  sd = {k: v.detach().to("cpu").contiguous() for k, v in engine.runner.weights.to_hf_state_dict().items()}
+  save_file(sd, str(path), metadata={"format": "pt", "shard": shard.key()})
+  if trainer is not None:
+    osd = {k: v.detach().to("cpu").contiguous() for k, v in trainer.state_dict().items()}
+    save_file(osd, str(path.with_name(path.name.replace(".safetensors", ".optim.safetensors"))))
+  return path
+
+
+def _gather_tensors(files: List[Path], shard: Shard, tie: bool) -> Dict[str, torch.Tensor]:
+  from safetensors import safe_open
+  want: Dict[str, torch.Tensor] = {}
+  for f in files:
+    with safe_open(str(f), framework="pt") as sf:
+      for k in sf.keys():
+        if k.startswith("model.layers."):
+          if int(k.split(".")[2]) in shard.layers():
+            want[k] = sf.get_tensor(k)
+        elif k.startswith("model.embed_tokens"):
+          if shard.is_first_layer() or (shard.is_last_layer() and tie):
+            want[k] = sf.get_tensor(k)
+        elif (k.startswith("model.norm") or k.startswith("lm_head")) and shard.is_last_layer():
+          want[k] = sf.get_tensor(k)
+  return want
+
+
+def load_shard_checkpoint(engine, shard: Shard, path: str | Path) -> None:
+  from ..models.weights import copy_weights_into, from_hf_state_dict
+  path = Path(path)
+  cfg = engine.runner.config
+  if path.is_dir():
+    cks = list_checkpoints(path, shard.model_id)
+    if not cks:
+      raise FileNotFoundError(f"no checkpoints for {shard.model_id} under {path}")
+    latest = cks[-1][0]
+    files = [p for it, s, e, n, p in cks if it == latest]
+  else:
+    files = [path]
+  sd = _gather_tensors(files, shard, cfg.tie_word_embeddings)
+  w = from_hf_state_dict(sd, cfg, shard, device=engine.runner.device)
+  copy_weights_into(engine.runner.weights, w)  # in place: captured decode graphs keep their addresses
+  engine.trainer = None
+  # optimizer sidecar for this exact shard, if present
+  for f in files:
+    side = f.with_name(f.name.replace(".safetensors", ".optim.safetensors"))
+    m = _NAME.match(f.name)
+    if side.exists() and m and (int(m.group(1)), int(m.group(2))) == (shard.start_layer, shard.end_layer):
+      from safetensors.torch import load_file
+      tr = engine._get_trainer()
+      tr.load_state_dict({k: v.to(tr.device) for k, v in load_file(str(side)).items()})

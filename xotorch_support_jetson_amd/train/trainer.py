@@ -1,0 +1,219 @@
+"""Pipeline-stage trainer: the engine.train / engine.evaluate the reference's Node calls but never
+implements (xotorch/orchestration/node.py:299-345, inference_engine.py:34-35).
+
+Protocol (one micro-batch, synchronous, like the reference's SendExample recursion):
+  non-last stage:  out = train_forward(x)  -> next stage ... -> grad wrt out comes back
+                   step(x, grad_out, loss="back_gradient")  -> backward + AdamW, returns grad wrt x
+  last stage:      step(x, y, lengths)     -> length-masked CE, backward + AdamW, returns (loss, grad wrt x)
+The stage recomputes its forward inside `step` (activation checkpointing at stage granularity), so
+no activations are kept between the hops.
+
+Numerics: bf16 working weights (leaf tensors with grads), fp32 master weights + fp32 AdamW moments
+updated by the fused HIP AdamW kernel, which also refreshes the bf16 copy.  RMSNorm, SiLU*mul, RoPE and
+the cross-entropy run on the kernel library's forward/backward kernels; GEMMs on hipBLASLt; attention
+on torch SDPA (causal).  Updated weights are written back into the inference shard lazily
+(`sync_to_inference`) so `xot run` after `xot train` uses the trained model.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, Optional, Tuple
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from ..models.config import ModelConfig
+from ..models.weights import ShardWeights, _rowmajor, interleave_gate_up, split_gate_up
+from ..ops._ext import require
+from ..ops.rope import build_cos_sin
+from . import autograd_ops as A
+
+
+class ShardTrainer:
+  def __init__(self, weights: ShardWeights, device, lr: float = 1e-5, betas=(0.9, 0.95), eps: float = 1e-8,
+               weight_decay: float = 0.0, max_seq: int = 4096, grad_clip: float = 1.0):
+    self.w = weights
+    self.c: ModelConfig = weights.config
+    self.shard = weights.shard
+    self.device = torch.device(device)
+    self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
+    self.grad_clip = grad_clip
+    self.step_count = 0
+    self.dirty = False
+    self.cos_sin = build_cos_sin(self.c.head_dim, max_seq, self.c.rope_theta, self.c.rope_scaling, self.device)
+    if self.c.is_moe:
+      raise NotImplementedError("MoE fine-tuning is not implemented yet (dense Llama/Qwen/Mistral only)")
+    # training parameters (row-major, gate|up halves), bf16 leaves + fp32 master + moments
+    self.params: Dict[str, torch.Tensor] = {}
+    for i, lw in weights.layers.items():
+      g, u = split_gate_up(_rowmajor(lw.gu_w))
+      self._add(f"{i}.qkv", _rowmajor(lw.qkv_w))
+      if lw.qkv_b is not None:
+        self._add(f"{i}.qkv_b", lw.qkv_b)
+      self._add(f"{i}.o", _rowmajor(lw.o_w))
+      self._add(f"{i}.gu", torch.cat([g, u], 0))
+      self._add(f"{i}.down", _rowmajor(lw.down_w))
+      self._add(f"{i}.ln1", lw.ln1)
+      self._add(f"{i}.ln2", lw.ln2)
+    if weights.embed is not None and self.shard.is_first_layer():
+      self._add("embed", weights.embed)
+    if self.shard.is_last_layer():
+      self._add("norm", weights.norm)
+      if not self.c.tie_word_embeddings or "embed" not in self.params:
+        self._add("lm_head", _rowmajor(weights.lm_head))
+    self.master = {k: p.detach().float().clone() for k, p in self.params.items()}
+    self.m = {k: torch.zeros_like(v) for k, v in self.master.items()}
+    self.v = {k: torch.zeros_like(v) for k, v in self.master.items()}
+
+  def _add(self, name: str, t: torch.Tensor):
+    self.params[name] = t.detach().to(self.device, torch.bfloat16).clone().requires_grad_(True)
+
+  # ------------------------------------------------------------------ model
+  def forward(self, x: torch.Tensor) -> torch.Tensor:
+    """x: ids [B, L] (first stage) or hidden [B, L, D].  Returns hidden [B, L, D] or logits [B, L, V]."""
+    c, P = self.c, self.params
+    H, Hkv, Dh, D = c.num_heads, c.num_kv_heads, c.head_dim, c.hidden_size
+    if self.shard.is_first_layer():
+      ids = x.long().clamp(0, c.vocab_size - 1)
+      h = F.embedding(ids, P["embed"])
+    else:
+      h = x.to(torch.bfloat16)
+    B, L = h.shape[0], h.shape[1]
+    pos = torch.arange(L, device=self.device, dtype=torch.int32).repeat(B)
+    h = h.reshape(B * L, D)
+    for i in self.shard.layers():
+      xn = A.rmsnorm(h, P[f"{i}.ln1"], c.rms_norm_eps)
+      qkv = xn @ P[f"{i}.qkv"].t()
+      if f"{i}.qkv_b" in P:
+        qkv = qkv + P[f"{i}.qkv_b"]
+      q = A.rope(qkv[:, :H * Dh].contiguous(), pos, self.cos_sin, H, Dh)
+      k = A.rope(qkv[:, H * Dh:(H + Hkv) * Dh].contiguous(), pos, self.cos_sin, Hkv, Dh)
+      v = qkv[:, (H + Hkv) * Dh:]
+      q = q.view(B, L, H, Dh).transpose(1, 2)
+      k = k.view(B, L, Hkv, Dh).transpose(1, 2).repeat_interleave(H // Hkv, dim=1)
+      v = v.reshape(B, L, Hkv, Dh).transpose(1, 2).repeat_interleave(H // Hkv, dim=1)
+      a = F.scaled_dot_product_attention(q, k, v, is_causal=True)
+      a = a.transpose(1, 2).reshape(B * L, H * Dh)
+      h = h + a @ P[f"{i}.o"].t()
+      xn = A.rmsnorm(h, P[f"{i}.ln2"], c.rms_norm_eps)
+      h = h + A.silu_mul((xn @ P[f"{i}.gu"].t()).contiguous()) @ P[f"{i}.down"].t()
+    if not self.shard.is_last_layer():
+      return h.view(B, L, D)
+    xn = A.rmsnorm(h, P["norm"], c.rms_norm_eps)
+    head = P["lm_head"] if "lm_head" in P else P["embed"]
+    return (xn @ head.t()).view(B, L, -1)
+
+  # ------------------------------------------------------------------ steps
+  def _to(self, a, dtype=None):
+    t = a if isinstance(a, torch.Tensor) else torch.as_tensor(np.asarray(a))
+    return t.to(self.device, dtype) if dtype is not None else t.to(self.device)
+
+  @torch.no_grad()
+  def train_forward(self, example) -> torch.Tensor:
+    x = self._to(example)
+    return self.forward(x).detach().cpu()
+
+  def loss_of(self, logits: torch.Tensor, target, lengths) -> Tuple[torch.Tensor, int]:
+    B, L, V = logits.shape
+    y = self._to(target, torch.int64)
+    ln = self._to(lengths, torch.int64).view(-1)
+    mask = torch.arange(L, device=self.device)[None, :] < ln[:, None]
+    tgt = torch.where(mask, y, torch.full_like(y, -100)).view(-1).to(torch.int32)
+    n = int(mask.sum().item())
+    w = torch.full((B * L,), 1.0 / max(n, 1), device=self.device, dtype=torch.float32)
+    return A.cross_entropy(logits.reshape(B * L, V), tgt, w), n
+
+  def step(self, request_id, example, target, length, train: bool = True, evaluate: bool = False,
+           loss: str = "length_masked_ce"):
+    x = self._to(example)
+    need_in_grad = not self.shard.is_first_layer()
+    if need_in_grad:
+      x = x.to(torch.bfloat16).detach().requires_grad_(train)
+    if not train:
+      with torch.no_grad():
+        out = self.forward(x)
+        if self.shard.is_last_layer():
+          l, _ = self.loss_of(out, target, length)
+          return float(l)
+        return 0.0
+    for p in self.params.values():
+      p.grad = None
+    out = self.forward(x)
+    if self.shard.is_last_layer() and loss != "back_gradient":
+      lval, _ = self.loss_of(out, target, length)
+      lval.backward()
+      loss_out = float(lval.detach())
+    else:
+      g = self._to(target).to(out.dtype)
+      out.backward(g.view_as(out))
+      loss_out = 0.0
+    self._optimizer_step()
+    grad_in = x.grad.detach().cpu() if need_in_grad and x.grad is not None else None
+    return loss_out, grad_in
+
+  def _optimizer_step(self):
+    self.step_count += 1
+    grads = {k: p.grad for k, p in self.params.items() if p.grad is not None}
+    gnorm = torch.sqrt(sum((g.float() ** 2).sum() for g in grads.values())) if grads else torch.tensor(0.0)
+    scale = float(min(1.0, self.grad_clip / (float(gnorm) + 1e-6))) if self.grad_clip else 1.0
+    b1, b2 = self.betas
+    for k, g in grads.items():
+      p, m, v, pb = self.master[k], self.m[k], self.v[k], self.params[k]
+      if p.is_cuda:
+        require().adamw(p, g.contiguous(), m, v, pb.data, self.lr, b1, b2, self.eps, self.wd, self.step_count, scale)
+      else:
+        gf = g.float() * scale
+        m.mul_(b1).add_(gf, alpha=1 - b1)
+        v.mul_(b2).addcmul_(gf, gf, value=1 - b2)
+        bc1, bc2 = 1 - b1 ** self.step_count, 1 - b2 ** self.step_count
+        p.mul_(1 - self.lr * self.wd).addcdiv_(m / bc1, (v / bc2).sqrt_().add_(self.eps), value=-self.lr)
+        pb.data.copy_(p.to(pb.dtype))
+    self.dirty = True
+
+  # ------------------------------------------------------------------ write-back
+  @torch.no_grad()
+  def sync_to_inference(self) -> None:
+    """Copy the trained weights into the inference shard (re-interleave gate/up, re-shuffle on GPU)."""
+    if not self.dirty:
+      return
+    from ..models.weights import assign_weight
+    P = self.params
+    Fd = self.c.intermediate_size
+    for i, lw in self.w.layers.items():
+      gu = P[f"{i}.gu"].detach()
+      assign_weight(lw.qkv_w, P[f"{i}.qkv"].detach())
+      if f"{i}.qkv_b" in P:
+        assign_weight(lw.qkv_b, P[f"{i}.qkv_b"].detach())
+      assign_weight(lw.o_w, P[f"{i}.o"].detach())
+      assign_weight(lw.gu_w, interleave_gate_up(gu[:Fd].contiguous(), gu[Fd:].contiguous()))
+      assign_weight(lw.down_w, P[f"{i}.down"].detach())
+      assign_weight(lw.ln1, P[f"{i}.ln1"].detach())
+      assign_weight(lw.ln2, P[f"{i}.ln2"].detach())
+    if "embed" in P:
+      assign_weight(self.w.embed, P["embed"].detach())
+    if "norm" in P:
+      assign_weight(self.w.norm, P["norm"].detach())
+    head = P["lm_head"] if "lm_head" in P else P.get("embed")
+    if head is not None and self.w.lm_head is not None and self.w.lm_head is not self.w.embed:
+      assign_weight(self.w.lm_head, head.detach())
+    self.dirty = False
+
+  def state_dict(self) -> Dict[str, torch.Tensor]:
+    out = {}
+    for k in self.master:
+      out[f"master.{k}"] = self.master[k]
+      out[f"m.{k}"] = self.m[k]
+      out[f"v.{k}"] = self.v[k]
+    out["step"] = torch.tensor([self.step_count], dtype=torch.int64)
+    return out
+
+  def load_state_dict(self, sd: Dict[str, torch.Tensor]) -> None:
+    for k in self.master:
+      if f"master.{k}" in sd:
+        self.master[k].copy_(sd[f"master.{k}"])
+        self.m[k].copy_(sd[f"m.{k}"])
+        self.v[k].copy_(sd[f"v.{k}"])
+        self.params[k].data.copy_(self.master[k].to(torch.bfloat16))
+    if "step" in sd:
+      self.step_count = int(sd["step"][0])
