@@ -1,0 +1,186 @@
+"""CPU unit tests for the model registry, configs, block managers, wire codec, dataset, tokenizers,
+manual-discovery config (reference: test/test_model_helpers.py, test/test_tokenizers.py,
+xotorch/networking/manual/test_network_topology_config.py)."""
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from xotorch_support_jetson_amd.inference.shard import Shard
+from xotorch_support_jetson_amd.models import registry as R
+from xotorch_support_jetson_amd.models.config import PRESETS, from_hf_config
+
+
+# ---------------------------------------------------------------- registry / config
+def test_model_cards_and_shards():
+  E = R.ENGINE
+  assert R.build_base_shard("llama-3-70b", E) == Shard("llama-3-70b", 0, 0, 80)
+  assert R.build_full_shard("llama-3.2-1b", E) == Shard("llama-3.2-1b", 0, 15, 16)
+  assert R.build_base_shard("dummy", "DummyInferenceEngine").n_layers == 8
+  assert R.build_base_shard("no-such-model", E) is None
+  assert R.get_repo("llama-3.2-1b", E) == "unsloth/Llama-3.2-1B-Instruct"
+  assert R.get_pretty_name("llama-3.3-70b") == "Llama 3.3 70B"
+
+
+def test_supported_models_intersection():
+  both = R.get_supported_models([["mi355x"], ["mi355x", "dummy"]])
+  assert "llama-3-70b" in both and "dummy" not in both
+  assert R.get_supported_models([["dummy"]]) == ["dummy"]
+  assert len(R.get_supported_models()) == len(R.model_cards)
+
+
+def test_validate_layers_warns():
+  with pytest.warns(UserWarning):
+    assert R.validate_layers("llama-3.2-1b", 17) == 17
+
+
+def test_presets_match_hf_shapes():
+  c = PRESETS["llama-3-70b"]
+  assert (c.num_layers, c.hidden_size, c.num_heads, c.num_kv_heads, c.intermediate_size, c.vocab_size) == \
+         (80, 8192, 64, 8, 28672, 128256)
+  for name, cfg in PRESETS.items():
+    assert cfg.hidden_size == cfg.num_heads * cfg.head_dim or cfg.head_dim in (64, 128), name
+
+
+def test_config_from_hf_dict():
+  hf = {"architectures": ["LlamaForCausalLM"], "model_type": "llama", "hidden_size": 2048, "num_hidden_layers": 16,
+        "num_attention_heads": 32, "num_key_value_heads": 8, "intermediate_size": 8192, "vocab_size": 128256,
+        "rms_norm_eps": 1e-5, "rope_theta": 500000.0, "tie_word_embeddings": True,
+        "rope_scaling": {"rope_type": "llama3", "factor": 32.0, "low_freq_factor": 1.0, "high_freq_factor": 4.0,
+                         "original_max_position_embeddings": 8192}}
+  c = from_hf_config(hf)
+  assert c.head_dim == 64 and c.tie_word_embeddings and c.num_layers == 16
+
+
+# ---------------------------------------------------------------- block managers
+def _managers():
+  from xotorch_support_jetson_amd.runtime.block_manager_py import BlockManager as PyBM
+  out = [PyBM]
+  try:
+    from xotorch_support_jetson_amd import _runtime
+    out.append(_runtime.BlockManager)
+  except ImportError:
+    pass
+  return out
+
+
+@pytest.mark.parametrize("BM", _managers())
+def test_block_manager_semantics(BM):
+  bm = BM(8, 64)
+  assert bm.num_free == 8
+  s = bm.append("a", 100)
+  assert len(s) == 100 and bm.num_tokens("a") == 100
+  tab = bm.block_table("a")
+  assert len(tab) == 2
+  assert s[0] == tab[0] * 64 and s[99] == tab[1] * 64 + 35
+  assert bm.blocks_needed("a", 28) == 0 and bm.blocks_needed("a", 29) == 1
+  bm.append("b", 64)
+  assert bm.num_free == 5
+  assert not bm.can_append("c", 6 * 64)
+  bm.truncate("a", 10)
+  assert bm.num_free == 6 and bm.num_tokens("a") == 10
+  tables = np.zeros((2, 4), dtype=np.int32)
+  ctx = np.zeros(2, dtype=np.int32)
+  bm.fill_batch(["a", "b"], tables, ctx)
+  assert list(ctx) == [10, 64] and tables[0, 0] == bm.block_table("a")[0]
+  bm.free("a")
+  bm.append("a", 100)
+  bm.fork("a", "a2", 100)  # shares only the full pages: 64 tokens, 1 refcounted page
+  assert bm.num_tokens("a2") == 64 and bm.num_free == 5
+  bm.free("a")
+  assert bm.num_free == 6  # the shared page stays alive for a2
+  bm.free("a2")
+  bm.free("b")
+  assert bm.num_free == 8 and not bm.has("b")
+
+
+def test_block_manager_native_matches_python():
+  mgrs = _managers()
+  if len(mgrs) < 2:
+    pytest.skip("native runtime not built")
+  rng = np.random.default_rng(0)
+  a, b = mgrs[0](64, 64), mgrs[1](64, 64)
+  live = []
+  for step in range(300):
+    op = rng.integers(0, 3)
+    if op == 0 or not live:
+      rid = f"r{step}"
+      n = int(rng.integers(1, 200))
+      if a.can_append(rid, n):
+        assert a.append(rid, n) == b.append(rid, n)
+        live.append(rid)
+    elif op == 1:
+      rid = live[int(rng.integers(0, len(live)))]
+      if a.can_append(rid, 1):
+        assert a.append(rid, 1) == b.append(rid, 1)
+    else:
+      rid = live.pop(int(rng.integers(0, len(live))))
+      a.free(rid)
+      b.free(rid)
+    assert a.num_free == b.num_free
+
+
+# ---------------------------------------------------------------- wire codec
+def test_wire_roundtrip():
+  from xotorch_support_jetson_amd.networking.grpc import wire
+  x = np.arange(12, dtype=np.float32).reshape(3, 4)
+  y = wire.decode_tensor(wire.encode_tensor(x))
+  assert y.dtype == np.float32 and (y == x).all()
+  t = torch.randn(2, 3, 5).to(torch.bfloat16)
+  msg = wire.unpack(wire.pack({"tensor": wire.encode_tensor(t), "state": {"n_past": 3}}))
+  t2 = wire.decode_tensor(msg["tensor"])
+  assert t2.dtype == torch.bfloat16 and torch.equal(t2, t)
+  assert msg["state"] == {"n_past": 3}
+  assert wire.decode_tensor(wire.encode_tensor(None)) is None
+  ids = np.array([[1, 2, 3]], dtype=np.int64)
+  assert (wire.decode_tensor(wire.encode_tensor(ids)) == ids).all()
+
+
+# ---------------------------------------------------------------- dataset
+def test_dataset_batches():
+  from xotorch_support_jetson_amd.train.dataset import batch_with_lengths, iterate_batches, load_dataset
+  x, y, ln = batch_with_lengths([[1, 2, 3, 4], [5, 6]])
+  assert x.tolist() == [[1, 2, 3], [5, 6, 0]] and y.tolist() == [[2, 3, 4], [6, 0, 0]]
+  assert ln.tolist() == [3, 1]
+  train, valid, test = load_dataset(preprocess=lambda s: [ord(c) for c in s])
+  assert len(train) == 1000 and len(valid) == 100 and len(test) == 100
+  b1 = [b[0].shape for b in iterate_batches(train, 8, train=True, seed=1)]
+  assert len(b1) == 125
+  b2 = [b[0].shape for b in iterate_batches(train, 8, train=True, seed=1)]
+  assert b1 == b2  # seeded shuffle is reproducible
+
+
+# ---------------------------------------------------------------- tokenizers
+def test_tokenizers_offline():
+  from xotorch_support_jetson_amd.inference.tokenizers import ByteTokenizer, DummyTokenizer
+  bt = ByteTokenizer()
+  ids = bt.encode("héllo")
+  assert bt.decode(ids) == "héllo"
+  s = bt.apply_chat_template([{"role": "user", "content": "hi"}], tokenize=False, add_generation_prompt=True)
+  assert "hi" in s
+  dt = DummyTokenizer()
+  assert dt.eos_token_id == 69
+  assert isinstance(dt.decode(dt.encode("abc")), str)
+
+
+# ---------------------------------------------------------------- manual discovery config
+def test_network_topology_config(tmp_path):
+  from xotorch_support_jetson_amd.networking.manual.network_topology_config import NetworkTopology
+  good = {"peers": {"node1": {"address": "127.0.0.1", "port": 50051, "device_capabilities": {
+    "model": "MI355X", "chip": "AMD Instinct MI355X", "memory": 294912, "flops": {"fp32": 157.3, "fp16": 2516.6,
+                                                                                  "int8": 5033.2}}}}}
+  p = tmp_path / "good.json"
+  p.write_text(json.dumps(good))
+  t = NetworkTopology.from_path(str(p))
+  assert t.peers["node1"].port == 50051 and t.peers["node1"].device_capabilities.memory == 294912
+  bad = tmp_path / "bad.json"
+  bad.write_text("{not json")
+  with pytest.raises(ValueError, match="invalid JSON"):
+    NetworkTopology.from_path(str(bad))
+  missing = tmp_path / "missing_field.json"
+  missing.write_text(json.dumps({"peers": {"n": {"address": "x"}}}))
+  with pytest.raises(ValueError):
+    NetworkTopology.from_path(str(missing))
+  with pytest.raises(FileNotFoundError):
+    NetworkTopology.from_path(str(tmp_path / "nope.json"))

@@ -1,0 +1,123 @@
+"""ShardedInferenceEngine + ShardTrainer on CPU (reference: xotorch/inference/test_inference_engine.py —
+split inference == full inference; plus the training path the reference never implemented)."""
+import asyncio
+
+import numpy as np
+import pytest
+import torch
+
+from xotorch_support_jetson_amd.download.shard_download import NoopShardDownloader
+from xotorch_support_jetson_amd.inference.shard import Shard
+from xotorch_support_jetson_amd.inference.sharded_engine import ShardedInferenceEngine
+from xotorch_support_jetson_amd.train import checkpoint as ck
+
+MODEL = "tiny-llama"
+N = 4
+
+
+def run(c):
+  return asyncio.run(c)
+
+
+def eng():
+  return ShardedInferenceEngine(NoopShardDownloader(), device=torch.device("cpu"))
+
+
+def test_engine_split_equals_full():
+  async def main():
+    full, a, b = eng(), eng(), eng()
+    ids = np.random.default_rng(0).integers(0, 500, size=(1, 9))
+    f_out, f_state = await full.infer_tensor("r", Shard(MODEL, 0, N - 1, N), ids)
+    h, st = await a.infer_tensor("r", Shard(MODEL, 0, 1, N), ids)
+    s_out, _ = await b.infer_tensor("r", Shard(MODEL, 2, N - 1, N), h, st)
+    assert np.allclose(np.asarray(f_out, np.float32), np.asarray(s_out, np.float32), atol=1e-5)
+    # one decode step continues from the cached prefix
+    tok = np.asarray(await full.sample(f_out, temp=0.0)).reshape(1, 1)
+    f2, _ = await full.infer_tensor("r", Shard(MODEL, 0, N - 1, N), tok, f_state)
+    h2, st2 = await a.infer_tensor("r", Shard(MODEL, 0, 1, N), tok, st)
+    s2, _ = await b.infer_tensor("r", Shard(MODEL, 2, N - 1, N), h2, st2)
+    assert np.allclose(np.asarray(f2, np.float32), np.asarray(s2, np.float32), atol=1e-5)
+    await full.finish_request("r")
+    assert not full.runner.has("r")
+
+  run(main())
+
+
+def test_pipeline_training_matches_single_stage():
+  """Two-stage SendExample protocol (forward, back-gradient) gives the same loss and updated weights
+  as one stage holding all layers."""
+  async def main():
+    x = np.random.default_rng(1).integers(0, 500, size=(2, 12))
+    y = np.roll(x, -1, 1)
+    ln = np.array([12, 9])
+    full = eng()
+    fs = Shard(MODEL, 0, N - 1, N)
+    l_full, _ = await full.train("t", fs, x, y, ln)
+    s0, s1 = eng(), eng()
+    a, b = Shard(MODEL, 0, 1, N), Shard(MODEL, 2, N - 1, N)
+    h = await s0.train_forward("t", a, x)
+    l_split, g = await s1.train("t", b, h, y, ln)
+    _, g0 = await s0.train("t", a, x, g, ln, loss="back_gradient")
+    assert g0 is None
+    assert abs(l_full - l_split) < 1e-3
+    tf, t0, t1 = full.trainer, s0.trainer, s1.trainer
+    for k in ("0.qkv", "1.down", "embed"):
+      assert torch.allclose(tf.master[k], t0.master[k], atol=2e-6), k
+    for k in ("2.o", "3.gu", "norm"):
+      assert torch.allclose(tf.master[k], t1.master[k], atol=2e-6), k
+
+  run(main())
+
+
+def test_training_reduces_loss_and_checkpoint_roundtrip(tmp_path):
+  async def main():
+    e = eng()
+    s = Shard(MODEL, 0, N - 1, N)
+    await e.ensure_shard(s)
+    e.lr = 3e-3
+    rng = np.random.default_rng(2)
+    x = rng.integers(0, 64, size=(4, 16))
+    y = np.roll(x, -1, 1)
+    ln = np.full(4, 16)
+    losses = [(await e.train("t", s, x, y, ln))[0] for _ in range(12)]
+    assert losses[-1] < losses[0] * 0.9, losses
+    ev = await e.evaluate("e", s, x, y, ln)
+    assert abs(ev - losses[-1]) < 0.5
+    p = ck.checkpoint_path(tmp_path, s, 12)
+    await e.save_checkpoint(s, str(p))
+    assert p.exists() and p.with_name(p.name.replace(".safetensors", ".optim.safetensors")).exists()
+    assert ck.list_checkpoints(tmp_path, MODEL)[-1][0] == 12
+    out1, _ = await e.infer_tensor("q", s, x[:1])
+    e2 = eng()
+    await e2.ensure_shard(s)
+    await e2.load_checkpoint(s, str(tmp_path))
+    out2, _ = await e2.infer_tensor("q", s, x[:1])
+    assert np.array_equal(np.asarray(out1), np.asarray(out2))
+    assert e2.trainer is not None and e2.trainer.step_count == 12  # optimizer state resumed
+
+  run(main())
+
+
+def test_checkpoint_resharding(tmp_path):
+  """A checkpoint written by a 1-stage run loads into a 2-stage split (tensors gathered by layer)."""
+  async def main():
+    e = eng()
+    s = Shard(MODEL, 0, N - 1, N)
+    await e.ensure_shard(s)
+    ids = np.arange(7).reshape(1, 7)
+    ref, _ = await e.infer_tensor("q", s, ids)
+    await e.save_checkpoint(s, str(ck.checkpoint_path(tmp_path, s, 3)))
+    a, b = eng(), eng()
+    sa, sb = Shard(MODEL, 0, 1, N), Shard(MODEL, 2, N - 1, N)
+    await a.ensure_shard(sa)
+    await b.ensure_shard(sb)
+    # perturb, then restore from the checkpoint
+    for lw in a.runner.weights.layers.values():
+      lw.ln1.mul_(0.5)
+    await a.load_checkpoint(sa, str(tmp_path))
+    await b.load_checkpoint(sb, str(tmp_path))
+    h, st = await a.infer_tensor("q", sa, ids)
+    out, _ = await b.infer_tensor("q", sb, h, st)
+    assert np.allclose(np.asarray(ref, np.float32), np.asarray(out, np.float32), atol=1e-5)
+
+  run(main())

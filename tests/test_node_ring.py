@@ -1,0 +1,195 @@
+"""Multi-node ring over real gRPC on localhost with the dummy engine (reference:
+xotorch/orchestration/test_node.py, xotorch/inference/test_dummy_inference_engine.py), plus the
+ChatGPT-API contract against a live node."""
+import asyncio
+import json
+import socket
+
+import numpy as np
+import pytest
+
+from xotorch_support_jetson_amd.download.shard_download import NoopShardDownloader
+from xotorch_support_jetson_amd.inference.dummy_inference_engine import DummyInferenceEngine
+from xotorch_support_jetson_amd.inference.shard import Shard
+from xotorch_support_jetson_amd.networking.grpc.grpc_peer_handle import GRPCPeerHandle
+from xotorch_support_jetson_amd.networking.grpc.grpc_server import GRPCServer
+from xotorch_support_jetson_amd.networking.manual.manual_discovery import ManualDiscovery
+from xotorch_support_jetson_amd.orchestration.node import Node
+from xotorch_support_jetson_amd.topology.device_capabilities import DeviceCapabilities, DeviceFlops
+from xotorch_support_jetson_amd.topology.ring_memory_weighted_partitioning_strategy import \
+  RingMemoryWeightedPartitioningStrategy
+
+CAPS = {"model": "test", "chip": "test", "memory": 1000, "flops": {"fp32": 1.0, "fp16": 2.0, "int8": 4.0}}
+
+
+def free_port():
+  with socket.socket() as s:
+    s.bind(("127.0.0.1", 0))
+    return s.getsockname()[1]
+
+
+async def make_ring(tmp_path, ids, engines=None):
+  ports = {i: free_port() for i in ids}
+  cfg = {"peers": {i: {"address": "127.0.0.1", "port": ports[i], "device_capabilities": CAPS} for i in ids}}
+  path = tmp_path / "topology.json"
+  path.write_text(json.dumps(cfg))
+  nodes = []
+  for k, i in enumerate(ids):
+    eng = engines[k] if engines else DummyInferenceEngine()
+    disc = ManualDiscovery(str(path), i, create_peer_handle=lambda pid, addr, desc, caps: GRPCPeerHandle(pid, addr, desc,
+                                                                                                        caps),
+                           poll_interval=0.2)
+    node = Node(i, None, eng, disc, NoopShardDownloader(), RingMemoryWeightedPartitioningStrategy(),
+                max_generate_tokens=64, device_caps=DeviceCapabilities(**CAPS))
+    node.server = GRPCServer(node, "127.0.0.1", ports[i])
+    nodes.append(node)
+  for n in nodes:
+    await n.server.start()
+  await asyncio.gather(*(n.start(wait_for_peers=len(ids) - 1) for n in nodes))
+  for n in nodes:
+    await n.collect_topology(set())
+  return nodes
+
+
+async def stop_all(nodes):
+  for n in nodes:
+    await n.stop()
+
+
+def run(coro):
+  return asyncio.run(asyncio.wait_for(coro, timeout=60))
+
+
+def test_two_node_generation(tmp_path):
+  async def main():
+    nodes = await make_ring(tmp_path, ["node-a", "node-b"])
+    try:
+      a, b = nodes
+      assert {n for n, _ in a.current_topology.all_nodes()} == {"node-a", "node-b"}
+      # equal memory -> ring order by id descending: node-b holds layers 0-3, node-a 4-7
+      base = Shard("dummy", 0, 0, 8)
+      assert b.get_current_shard(base) == Shard("dummy", 0, 3, 8)
+      assert a.get_current_shard(base) == Shard("dummy", 4, 7, 8)
+      done = asyncio.Event()
+      got = []
+      seen_on_b = []
+
+      def on_tok(rid, toks, fin):
+        got.extend(toks)
+        if fin:
+          done.set()
+
+      a.on_token.register("t").on_next(on_tok)
+      b.on_token.register("t").on_next(lambda rid, toks, fin: seen_on_b.extend(toks))
+      await a.process_prompt(base, "x", request_id="r1")
+      await asyncio.wait_for(done.wait(), 20)
+      assert got[-1] == 69
+      assert all(y == x + 1 for x, y in zip(got[:-2], got[1:-1]))
+      await asyncio.sleep(0.3)
+      # results are routed to the request origin only (node-a), not broadcast per token
+      assert seen_on_b == []
+      # finished request released everywhere
+      assert "r1" not in a.outstanding_requests and "r1" not in b.outstanding_requests
+    finally:
+      await stop_all(nodes)
+
+  run(main())
+
+
+def test_request_params_reach_sampler(tmp_path):
+  class Recording(DummyInferenceEngine):
+    def __init__(self):
+      super().__init__()
+      self.temps = []
+
+    async def sample(self, x, temp=0.0, top_k=35):
+      self.temps.append((temp, top_k))
+      return await super().sample(x, temp, top_k)
+
+  async def main():
+    engs = [Recording(), Recording()]
+    nodes = await make_ring(tmp_path, ["n1", "n2"], engs)
+    try:
+      a = nodes[0]
+      done = asyncio.Event()
+      toks = []
+      a.on_token.register("t").on_next(lambda rid, t, fin: (toks.extend(t), fin and done.set()))
+      await a.process_prompt(Shard("dummy", 0, 0, 8), "x", request_id="r2",
+                             inference_state={"temperature": 0.7, "top_k": 5, "max_tokens": 3})
+      await asyncio.wait_for(done.wait(), 20)
+      assert len(toks) == 3  # max_tokens honoured
+      temps = engs[0].temps + engs[1].temps
+      assert temps and all(t == (0.7, 5) for t in temps)
+    finally:
+      await stop_all(nodes)
+
+  run(main())
+
+
+def test_three_node_training_example(tmp_path):
+  async def main():
+    engs = [DummyInferenceEngine() for _ in range(3)]
+    nodes = await make_ring(tmp_path, ["p1", "p2", "p3"], engs)
+    try:
+      base = Shard("dummy", 0, 0, 8)
+      x = np.zeros((2, 5), dtype=np.int64)
+      first = [n for n in nodes if n.get_current_shard(base).is_first_layer()][0]
+      loss = await first.enqueue_example(base, x, x, np.array([5, 4]), request_id="ex1", train=True)
+      assert loss is not None
+      assert all(e.trained for e in engs)  # every stage stepped
+      # checkpoint coordination: every peer saves its own shard file
+      await first.coordinate_save(base, 1, str(tmp_path / "ck"))
+      await asyncio.sleep(0.5)
+      assert sum(len(e.saved) for e in engs) == 3
+    finally:
+      await stop_all(nodes)
+
+  run(main())
+
+
+def test_chatgpt_api_contract(tmp_path):
+  from aiohttp.test_utils import TestClient, TestServer
+
+  from xotorch_support_jetson_amd.api.chatgpt_api import ChatGPTAPI
+
+  async def main():
+    nodes = await make_ring(tmp_path, ["solo"])
+    node = nodes[0]
+    api = ChatGPTAPI(node, "DummyInferenceEngine", response_timeout=30, default_model="dummy")
+    client = TestClient(TestServer(api.app))
+    await client.start_server()
+    try:
+      r = await client.get("/v1/models")
+      assert r.status == 200 and any(m["id"] == "dummy" for m in (await r.json())["data"])
+      r = await client.get("/healthcheck")
+      assert (await r.json()) == {"status": "ok"}
+      r = await client.get("/v1/topology")
+      assert "solo" in (await r.json())["nodes"]
+      body = {"model": "dummy", "messages": [{"role": "user", "content": "hi"}], "temperature": 0.0}
+      r = await client.post("/v1/chat/completions", json=body)
+      assert r.status == 200, await r.text()
+      d = await r.json()
+      assert d["object"] == "chat.completion" and d["choices"][0]["finish_reason"] == "stop"
+      assert d["usage"]["completion_tokens"] >= 1
+      # streaming: chunks then [DONE]
+      r = await client.post("/v1/chat/completions", json={**body, "stream": True})
+      text = await r.text()
+      lines = [l for l in text.split("\n") if l.startswith("data: ")]
+      assert lines[-1] == "data: [DONE]"
+      chunks = [json.loads(l[6:]) for l in lines[:-1]]
+      assert all(c["object"] == "chat.completion.chunk" for c in chunks)
+      assert chunks[-1]["choices"][0]["finish_reason"] == "stop"
+      r = await client.post("/v1/chat/completions", json={"model": "dummy", "messages": [{"content": "no role"}]})
+      assert r.status == 400
+      r = await client.post("/v1/chat/token/encode", json={"model": "dummy", "messages": [{"role": "user",
+                                                                                          "content": "abc"}]})
+      assert r.status == 200 and (await r.json())["num_tokens"] > 0
+      r = await client.get("/metrics")
+      assert r.status == 200
+      r = await client.options("/v1/chat/completions")
+      assert r.headers.get("Access-Control-Allow-Origin") == "*"
+    finally:
+      await client.close()
+      await stop_all(nodes)
+
+  run(main())

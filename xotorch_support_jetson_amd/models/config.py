@@ -65,8 +65,8 @@ def from_hf_config(cfg: dict) -> ModelConfig:
   mt = cfg.get("model_type", "llama")
   H = int(cfg["num_attention_heads"])
   D = int(cfg["hidden_size"])
-  eos = cfg.get("eos_token_id", 2)
-  eos_ids = tuple(eos) if isinstance(eos, (list, tuple)) else (int(eos),)
+  eos = cfg.get("eos_token_id")
+  eos_ids = tuple(eos) if isinstance(eos, (list, tuple)) else ((int(eos),) if eos is not None else (2,))
   return ModelConfig(
     model_type=mt,
     vocab_size=int(cfg["vocab_size"]),

@@ -106,6 +106,9 @@ class Node:
         elif st == "request_finished":
           rid = status.get("request_id")
           asyncio.get_running_loop().create_task(self._release_request(rid))
+      elif kind == "save_checkpoint" and status.get("node_id") != self.id:
+        asyncio.get_running_loop().create_task(self.coordinate_save(
+          Shard.from_dict(status["base_shard"]), int(status["iteration"]), status["destination"], broadcast=False))
       elif kind == "download_progress":
         self.node_download_progress[status.get("node_id")] = status.get("progress")
       if self.topology_viz:
@@ -264,7 +267,13 @@ class Node:
     self.outstanding_requests[request_id] = "waiting"
     return await self.forward_example(shard, example, target, length, train, request_id, 0)
 
-  async def coordinate_save(self, base_shard: Shard, iteration: int, destination: str):
+  async def coordinate_save(self, base_shard: Shard, iteration: int, destination: str, broadcast: bool = True):
+    """Save this peer's shard and (broadcast=True) tell every other peer to save theirs, so a ring
+    checkpoint covers all layers (the reference saves only the calling peer's shard, node.py:230-252)."""
+    if broadcast:
+      await self.broadcast_opaque_status("", json.dumps({
+        "type": "save_checkpoint", "node_id": self.id, "base_shard": base_shard.to_dict(), "iteration": iteration,
+        "destination": destination}))
     from ..train.checkpoint import checkpoint_path
     shard = self.get_current_shard(base_shard)
     model, sid = shard.model_id, shard.key()
