@@ -28,6 +28,11 @@ def log(*a):
   print(*a, file=sys.stderr, flush=True)
 
 
+def sync():
+  if torch.cuda.is_available():
+    torch.cuda.synchronize()
+
+
 def main():
   ap = argparse.ArgumentParser()
   ap.add_argument("--gpus", type=int, default=1)
@@ -63,7 +68,7 @@ def main():
   t0 = time.time()
   runner = ShardRunner(cfg, shard, dev, num_pages=M * B * pages_per_seq + 16, max_batch=B, max_ctx=max_ctx,
                        seed=0)
-  torch.cuda.synchronize()
+  sync()
   t_init = time.time() - t0
   log(f"[rank {rank}] shard {shard.start_layer}-{shard.end_layer} weights {runner.weights.nbytes() / 1e9:.1f} GB "
       f"kv {runner.kv.nbytes() / 1e9:.1f} GB init {t_init:.1f}s")
@@ -80,28 +85,28 @@ def main():
   # ---- prefill (real forward through every stage)
   if world > 1:
     dist.barrier()
-  torch.cuda.synchronize()
+  sync()
   t0 = time.time()
   first = [stage.prefill(mb) for mb in mbs]
   transport.drain()
-  torch.cuda.synchronize()
+  sync()
   t_prefill = time.time() - t0
   log(f"[rank {rank}] prefill {M * B} x {args.prompt_len} tokens in {t_prefill:.1f}s")
 
   # ---- warmup rounds (graph capture + GEMM policy tuning happen here)
   toks = run_decode_steps(stage, mbs, args.warmup, first_tokens=first if stage.last else None)
   transport.drain()
-  torch.cuda.synchronize()
+  sync()
   log(f"[rank {rank}] warmup done")
 
   # ---- timed rounds
   if world > 1:
     dist.barrier()
-  torch.cuda.synchronize()
+  sync()
   t0 = time.perf_counter()
   toks = run_decode_steps(stage, mbs, args.steps, first_tokens=toks if stage.last else None)
   transport.drain()
-  torch.cuda.synchronize()
+  sync()
   if world > 1:
     dist.barrier()
   elapsed = time.perf_counter() - t0

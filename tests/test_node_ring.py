@@ -193,3 +193,30 @@ def test_chatgpt_api_contract(tmp_path):
       await stop_all(nodes)
 
   run(main())
+
+
+def test_tinychat_served(tmp_path):
+  from aiohttp.test_utils import TestClient, TestServer
+
+  from xotorch_support_jetson_amd.api.chatgpt_api import ChatGPTAPI
+
+  async def main():
+    nodes = await make_ring(tmp_path, ["solo2"])
+    api = ChatGPTAPI(nodes[0], "DummyInferenceEngine", default_model="dummy")
+    client = TestClient(TestServer(api.app))
+    await client.start_server()
+    try:
+      r = await client.get("/")
+      assert r.status == 200 and "<html" in (await r.text())
+      for f in ("/index.js", "/index.css"):
+        r = await client.get(f)
+        assert r.status == 200, f
+      r = await client.get("/initial_models")
+      assert "dummy" in await r.json()
+      r = await client.get("/modelpool")
+      assert (await r.text()).rstrip().endswith("data: [DONE]")
+    finally:
+      await client.close()
+      await stop_all(nodes)
+
+  run(main())

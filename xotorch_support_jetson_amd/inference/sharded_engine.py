@@ -56,6 +56,7 @@ class ShardedInferenceEngine(InferenceEngine):
     self.seed_off = torch.tensor([seed, 0], dtype=torch.int64)
     self._lock = asyncio.Lock()
     self.trainer = None
+    self.lr = float(os.environ.get("XOT_LR", "1e-5"))  # `xot train --lr` sets this
 
   # ------------------------------------------------------------------ helpers
   async def _run(self, fn, *args):
@@ -195,7 +196,7 @@ class ShardedInferenceEngine(InferenceEngine):
   def _get_trainer(self):
     from ..train.trainer import ShardTrainer
     if self.trainer is None or self.trainer.shard != self.shard:
-      self.trainer = ShardTrainer(self.runner.weights, self.device)
+      self.trainer = ShardTrainer(self.runner.weights, self.device, lr=self.lr)
     return self.trainer
 
   async def train(self, request_id, shard, example, target, length, train=True, loss="length_masked_ce"):

@@ -249,6 +249,8 @@ def build_node(args):
   engine_name = args.inference_engine
   downloader = NoopShardDownloader() if engine_name == "dummy" else new_shard_downloader(args.max_parallel_downloads)
   engine = get_inference_engine(engine_name, downloader)
+  if hasattr(engine, "lr"):
+    engine.lr = args.lr
   print(f"Using inference engine: {type(engine).__name__} with shard downloader: {type(downloader).__name__}")
   port = args.node_port or find_available_port(args.node_host)
   node_id = args.node_id or get_or_create_node_id()

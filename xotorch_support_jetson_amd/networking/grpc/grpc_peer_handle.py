@@ -89,10 +89,9 @@ class GRPCPeerHandle(PeerHandle):
     resp = await self._call(name)(pack(msg), timeout=timeout)
     return unpack(resp) if resp else None
 
-  async def health_check(self) -> bool:
+  async def health_check(self, timeout: float = 3.0) -> bool:
     try:
-      await self._ensure_connected()
-      r = await self._rpc("HealthCheck", {}, timeout=5)
+      r = await asyncio.wait_for(self._rpc("HealthCheck", {}, timeout=timeout), timeout)
       return bool(r and r.get("is_healthy"))
     except asyncio.TimeoutError:
       return False
