@@ -9,6 +9,6 @@ run() {  # run <name> <seconds> <cmd...>
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
   return 0
 }
-run t2 420 python -m pytest tests/ -m gpu -q
-run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-run bench_full 600 python bench.py --steps 10 --warmup 3
+run t2 600 python -m pytest tests/ -m gpu -q
+run bench_b128 600 python bench.py --steps 10 --warmup 3 --batch-per-gpu 128
+run bench_b256 600 python bench.py --steps 10 --warmup 3 --batch-per-gpu 256

@@ -204,7 +204,7 @@ void gemm_stream(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const 
   const bool f32 = y.scalar_type() == at::kFloat;
   XCHECK(f32 || y.scalar_type() == at::kBFloat16, "gemm_stream: y must be bf16 or fp32");
   XCHECK(y.size(0) == M && y.size(1) == (epi == 2 ? N / 2 : N), "gemm_stream: y shape mismatch");
-  XCHECK(M <= 256, "gemm_stream: M must be <= 256");
+  XCHECK(M <= 65536, "gemm_stream: M must be <= 65536");
   if (bias.has_value()) {
     CHECK_BF16((*bias));
     XCHECK(bias->numel() == N && bias->is_contiguous(), "gemm_stream: bias shape mismatch");

@@ -191,22 +191,51 @@ int launch_gemm_skinny(const uint16_t* X, int ldx, const uint16_t* W, int ldw, c
 // MFMA k-order is permuted per lane group (group g owns k in [8*KS*g, 8*KS*(g+1)) of the chunk)
 // so each lane reads 16*KS contiguous bytes of its weight row per chunk.
 // SPLIT: fp32 partial slabs ws[blockIdx.y][M][N], finished by splitk_reduce_kernel (epilogue there).
-template <int MT, int NTW, int KS, int EPI, bool OUT_F32, bool SPLIT, bool WSHUF, int OCC>
-__global__ __launch_bounds__(256, OCC) void gemm_stream_kernel(const uint16_t* __restrict__ X, int ldx,
+// WM = 2: 8 waves as 2 (row halves) x 4 (column groups); both row halves use the same weight
+// fragments, so a CU streams each weight byte once for 2*16*MT rows (the M = 256 decode shape).
+template <int MT, int NTW, int KS, int EPI, bool OUT_F32, bool SPLIT, bool WSHUF, int OCC, int WM>
+__global__ __launch_bounds__(256 * WM, OCC) void gemm_stream_kernel(const uint16_t* __restrict__ X, int ldx,
                                                              const uint16_t* __restrict__ W, int ldw,
                                                              const uint16_t* __restrict__ bias,
                                                              const uint16_t* __restrict__ R, int ldr,
                                                              void* __restrict__ Yv, int ldy,
-                                                             float* __restrict__ ws, int M, int N, int kper) {
+                                                             float* __restrict__ ws, int M, int N, int kper,
+                                                             int mblocks) {
   constexpr int KC = 32 * KS;
   constexpr int CPR = KC / 8;  // 16-B chunks per row per k-chunk
-  constexpr int ROWS = 16 * MT;
-  constexpr int XPT = ROWS * CPR / 256;  // staging chunks per thread
+  constexpr int NTH = 256 * WM;
+  constexpr int ROWS = 16 * MT * WM;
+  constexpr int XPT = ROWS * CPR / NTH;  // staging chunks per thread
   static_assert(XPT >= 1, "tile too small for 256 threads");
-  __shared__ __attribute__((aligned(16))) uint16_t xs[2][ROWS * KC];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // X double buffer in dynamic LDS (2 x ROWS x KC bf16: 128 KB at ROWS = 256)
+  extern __shared__ __attribute__((aligned(16))) uint16_t xs_raw[];
+  auto xs = reinterpret_cast<uint16_t(*)[ROWS * KC]>(xs_raw);
+  const int tid = threadIdx.x, lane = tid & 63, wave = (tid >> 6) & 3, wrow = 16 * MT * (tid >> 8);
   const int g = lane >> 4, c = lane & 15;
-  const int n0 = blockIdx.x * (64 * NTW) + wave * 16 * NTW;
+  // M-blocking (M > ROWS): blockIdx.x = (column tile, row block).  The row blocks of one column tile
+  // get ids 8 apart, i.e. the same XCD under round-robin dispatch, and run together: the weight tile
+  // comes from HBM once and from that XCD's L2 for the other row blocks.
+  int bt = blockIdx.x, mb = 0;
+  if (mblocks > 1) {
+    const int ntiles = N / (64 * NTW);
+    if ((ntiles & 7) == 0) {
+      const int grp = 8 * mblocks, q = bt / grp, rem = bt % grp;
+      mb = rem >> 3;
+      bt = 8 * q + (rem & 7);
+    } else {
+      mb = bt % mblocks;
+      bt /= mblocks;
+    }
+  }
+  const int Mtot = M, m_base = mb * ROWS;
+  M = min(ROWS, Mtot - m_base);
+  X += (size_t)m_base * ldx;
+  if constexpr (EPI == EPI_RESID) R += (size_t)m_base * ldr;
+  if constexpr (OUT_F32)
+    Yv = reinterpret_cast<float*>(Yv) + (size_t)m_base * ldy;
+  else
+    Yv = reinterpret_cast<uint16_t*>(Yv) + (size_t)m_base * ldy;
+  const int n0 = bt * (64 * NTW) + wave * 16 * NTW;
   const int kb = blockIdx.y * kper;
   const int nch = kper / KC;
 
@@ -224,12 +253,12 @@ __global__ __launch_bounds__(256, OCC) void gemm_stream_kernel(const uint16_t* _
   }
 
   // staging geometry of this thread's XPT chunks, recomputed on use (keeps VGPRs for the pipeline):
-  // chunk q = tid + 256*i -> row q / CPR, logical 16-B slot q % CPR
+  // chunk q = tid + NTH*i -> row q / CPR, logical 16-B slot q % CPR
   const uint16_t* xbase = X + kb;
   auto xload = [&](s16x8 (&xr)[XPT], int ch) {
 #pragma unroll
     for (int i = 0; i < XPT; ++i) {
-      const int q = tid + 256 * i, row = q / CPR, cc = q % CPR;
+      const int q = tid + NTH * i, row = q / CPR, cc = q % CPR;
       const bool ok = row < M;
       s16x8 v = ld16(xbase + (size_t)(ok ? row : 0) * ldx + ch * KC + cc * 8);
       xr[i] = ok ? v : s16x8{0, 0, 0, 0, 0, 0, 0, 0};
@@ -238,7 +267,7 @@ __global__ __launch_bounds__(256, OCC) void gemm_stream_kernel(const uint16_t* _
   auto xstore = [&](const s16x8 (&xr)[XPT], int buf) {
 #pragma unroll
     for (int i = 0; i < XPT; ++i) {
-      const int q = tid + 256 * i, row = q / CPR, cc = q % CPR;
+      const int q = tid + NTH * i, row = q / CPR, cc = q % CPR;
       st16(&xs[buf][row * KC + ((cc ^ (row & (CPR - 1))) * 8)], xr[i]);
     }
   };
@@ -267,17 +296,28 @@ __global__ __launch_bounds__(256, OCC) void gemm_stream_kernel(const uint16_t* _
   wload(wb, 1);
   __syncthreads();
 
+  // A fragments are software-pipelined LDPF reads ahead of their MFMAs; the scheduling fences keep
+  // the compiler from hoisting the whole chunk's LDS reads (which costs 100+ VGPRs and spills).
+  constexpr int LDPF = 4;
   auto compute = [&](const s16x8 (&wr)[NTW][KS], int buf) {
+    const uint16_t* xb = &xs[buf][0];
+    auto afrag = [&](int t) {
+      const int s = t / MT, i = t % MT;
+      const int row = wrow + 16 * i + c;
+      const int phys = (g * KS + s) ^ (row & (CPR - 1));
+      return ld16(xb + row * KC + phys * 8);
+    };
+    s16x8 a[LDPF];
 #pragma unroll
-    for (int s = 0; s < KS; ++s) {
+    for (int t = 0; t < LDPF; ++t) a[t] = afrag(t);
 #pragma unroll
-      for (int i = 0; i < MT; ++i) {
-        const int row = 16 * i + c;
-        const int phys = (g * KS + s) ^ (row & (CPR - 1));
-        const s16x8 a = ld16(&xs[buf][row * KC + phys * 8]);
+    for (int t = 0; t < KS * MT; ++t) {
+      const int s = t / MT, i = t % MT;
+      const s16x8 cur = a[t % LDPF];
+      if (t + LDPF < KS * MT) a[t % LDPF] = afrag(t + LDPF);
 #pragma unroll
-        for (int j = 0; j < NTW; ++j) acc[i][j] = mfma16(a, wr[j][s], acc[i][j]);
-      }
+      for (int j = 0; j < NTW; ++j) acc[i][j] = mfma16(cur, wr[j][s], acc[i][j]);
+      __builtin_amdgcn_sched_barrier(0);
     }
   };
 
@@ -303,14 +343,14 @@ __global__ __launch_bounds__(256, OCC) void gemm_stream_kernel(const uint16_t* _
   compute(wb, 1);
 
   if constexpr (SPLIT) {
-    float* slab = ws + (size_t)blockIdx.y * M * N;
+    float* slab = ws + ((size_t)blockIdx.y * Mtot + m_base) * N;
 #pragma unroll
     for (int j = 0; j < NTW; ++j)
 #pragma unroll
       for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int m = 16 * i + 4 * g + r;
+          const int m = wrow + 16 * i + 4 * g + r;
           if (m < M) slab[(size_t)m * N + n0 + 16 * j + c] = acc[i][j][r];
         }
   } else if constexpr (EPI == EPI_SILU && NTW >= 2) {
@@ -326,7 +366,7 @@ __global__ __launch_bounds__(256, OCC) void gemm_stream_kernel(const uint16_t* _
       for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int m = 16 * i + 4 * g + r;
+          const int m = wrow + 16 * i + 4 * g + r;
           if (m < M) {
             const float v = silu(acc[i][2 * p][r] + bg) * (acc[i][2 * p + 1][r] + bu);
             if constexpr (OUT_F32)
@@ -345,7 +385,7 @@ __global__ __launch_bounds__(256, OCC) void gemm_stream_kernel(const uint16_t* _
       for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int m = 16 * i + 4 * g + r;
+          const int m = wrow + 16 * i + 4 * g + r;
           if (m < M) {
             float v = acc[i][j][r] + b;
             if constexpr (EPI == EPI_RESID) v += bf2f(R[(size_t)m * ldr + col]);
@@ -431,20 +471,32 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   }
 }
 
-template <int MT, int NTW, int KS, int EPI, bool F32, bool WSH>
+template <int MT, int NTW, int KS, int EPI, bool F32, bool WSH, int WM = 1>
 static void stream_launch(const uint16_t* X, int ldx, const uint16_t* W, int ldw, const uint16_t* bias,
                           const uint16_t* R, int ldr, void* Y, int ldy, float* ws, int M, int N, int K, int S,
                           hipStream_t st) {
   // occupancy request: 2 workgroups/CU while the register budget allows it
-  constexpr int OCC = (MT * NTW >= 32) ? 1 : 2;
-  dim3 grid(N / (64 * NTW), S);
+  constexpr int OCC = (MT * NTW >= 32 || WM > 1) ? 1 : 2;
+  constexpr int SMEM = 2 * 16 * MT * WM * 32 * KS * 2;
+  const int mblocks = (M + 16 * MT * WM - 1) / (16 * MT * WM);
+  dim3 grid(N / (64 * NTW) * mblocks, S);
   const int kper = K / S;
   if (S == 1) {
-    gemm_stream_kernel<MT, NTW, KS, EPI, F32, false, WSH, OCC><<<grid, 256, 0, st>>>(X, ldx, W, ldw, bias, R, ldr,
-                                                                                     Y, ldy, nullptr, M, N, kper);
+    auto kern = gemm_stream_kernel<MT, NTW, KS, EPI, F32, false, WSH, OCC, WM>;
+    if constexpr (SMEM > 65536) {
+      static bool attr = (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM) ==
+                          hipSuccess);
+      (void)attr;
+    }
+    kern<<<grid, 256 * WM, SMEM, st>>>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, nullptr, M, N, kper, mblocks);
   } else {
-    gemm_stream_kernel<MT, NTW, KS, EPI, F32, true, WSH, OCC><<<grid, 256, 0, st>>>(X, ldx, W, ldw, bias, R, ldr, Y,
-                                                                                    ldy, ws, M, N, kper);
+    auto kern = gemm_stream_kernel<MT, NTW, KS, EPI, F32, true, WSH, OCC, WM>;
+    if constexpr (SMEM > 65536) {
+      static bool attr = (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM) ==
+                          hipSuccess);
+      (void)attr;
+    }
+    kern<<<grid, 256 * WM, SMEM, st>>>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, M, N, kper, mblocks);
     const int ncol = EPI == EPI_SILU ? N / 2 : N;
     long chunks = (long)M * (ncol / 8);
     int blocks = (int)((chunks + 255) / 256);
@@ -462,7 +514,7 @@ static int stream_dispatch(const uint16_t* X, int ldx, const uint16_t* W, int ld
   const int mt = (M + 15) / 16;
   if (ntw == 4 && mt <= 2) ntw = 2;
   if (N % (64 * ntw) != 0 || S < 1) return -1;
-  const int KS = mt <= 8 ? 4 : 2;
+  const int KS = 4;
   if (K % (S * 64 * KS) != 0) return -1;  // an even number (>= 2) of k-chunks per workgroup
   if (S > 1 && (ws == nullptr || ws_elems < (long)S * M * N)) return -1;
   if (EPI == EPI_SILU && N % 32 != 0) return -1;
@@ -471,7 +523,7 @@ static int stream_dispatch(const uint16_t* X, int ldx, const uint16_t* W, int ld
   do {                                                                                                      \
     if (ntw == 1 && EPI != EPI_SILU)                                                                        \
       stream_launch<MTV, 1, KSV, EPI, F32, WSH>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, M, N, K, S, st);  \
-    else if (ntw == 4 && MTV >= 4)                                                                          \
+    else if (ntw == 4 && MTV >= 4 && MTV <= 8)                                                                    \
       stream_launch<MTV, 4, KSV, EPI, F32, WSH>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, M, N, K, S, st);  \
     else                                                                                                    \
       stream_launch<MTV, 2, KSV, EPI, F32, WSH>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, M, N, K, S, st);  \
@@ -486,7 +538,10 @@ static int stream_dispatch(const uint16_t* X, int ldx, const uint16_t* W, int ld
   if (mt <= 2) XOT_ST(2, 4);
   if (mt <= 4) XOT_ST(4, 4);
   if (mt <= 8) XOT_ST(8, 4);
-  if (mt <= 16 && !wshuf) XOT_ST2(16, 2, false);
+  // M > 128: 128-row blocks; the blocks of one column tile run on one XCD together (see the kernel).
+  // (256-row tiles -- MT = 16, or WM = 2 -- need > 256 registers per lane at this pipeline depth and
+  // spill; measured slower than the M-blocked 128-row tile.)
+  XOT_ST(8, 4);
 #undef XOT_ST
 #undef XOT_ST2
   return -1;

@@ -138,9 +138,13 @@ def expert(t: torch.Tensor, e: int) -> torch.Tensor:
   return v
 
 
-def prepare_for_decode(sw: "ShardWeights") -> "ShardWeights":
+def prepare_for_decode(sw: "ShardWeights", keep_rowmajor: Iterable[str] = ()) -> "ShardWeights":
   """Convert the projection weights of a GPU shard to the pre-shuffled stream layout (in place).
-  The embedding stays row-major (it is gathered); a tied LM head gets its own shuffled copy."""
+  The embedding stays row-major (it is gathered); a tied LM head gets its own shuffled copy.
+  `keep_rowmajor` names projections ("qkv", "o", "gu", "down") left row-major: at decode batches of
+  ~256 rows hipBLASLt beats the stream GEMM on the wide qkv / gate-up shapes, while the stream GEMM
+  keeps winning on o / down (tools/bench_gemm_m.py, profiles/bench_gemm_m_*.json)."""
+  keep = set(keep_rowmajor)
   from ..ops.weights_layout import can_shuffle, shuffle_for_stream
   if sw.embed is not None and not sw.embed.is_cuda:
     return sw
@@ -164,10 +168,14 @@ def prepare_for_decode(sw: "ShardWeights") -> "ShardWeights":
     return out
 
   for lw in sw.layers.values():
-    lw.qkv_w = conv(lw.qkv_w)
-    lw.o_w = conv(lw.o_w)
-    lw.gu_w = conv(lw.gu_w)
-    lw.down_w = conv(lw.down_w)
+    if "qkv" not in keep:
+      lw.qkv_w = conv(lw.qkv_w)
+    if "o" not in keep:
+      lw.o_w = conv(lw.o_w)
+    if "gu" not in keep:
+      lw.gu_w = conv(lw.gu_w)
+    if "down" not in keep:
+      lw.down_w = conv(lw.down_w)
   if sw.lm_head is not None:
     sw.lm_head = conv(sw.lm_head)  # a tied head becomes a separate shuffled copy; embed stays row-major
   return sw

@@ -3,13 +3,13 @@
 GPU weights of the decode path are stored PRE-SHUFFLED (ops.weights_layout.shuffle_for_stream;
 tagged `w.xot_layout == "stream"`).  Per call:
 
-  M <= 128 (decode, small prefill chunks)
+  M <= STREAM_MAX_M (decode batches, small prefill chunks)
         gemm_stream: the library's weight-streaming MFMA GEMM on the shuffled layout (1 KB coalesced
         weight loads per wave instruction, X shared through swizzled LDS) with the epilogue fused
-        (bias / residual add / SiLU*mul).  (ntw, split-K) is autotuned per shape on first use.
-  128 < M <= 256
-        the same kernel over 128-row slices (weights re-read once more, still cheaper than a copy)
-  M > 256 (prefill)
+        (bias / residual add / SiLU*mul).  (ntw, split-K) is autotuned per shape on first use.  Above
+        128 rows the launch holds ceil(M/128) row blocks per column tile, dispatched onto one XCD
+        together so the weight tile is read from HBM once.
+  M > STREAM_MAX_M (prefill)
         unshuffle the weight into a per-device scratch buffer and run hipBLASLt (torch.matmul/addmm)
         + the library's epilogue kernel; the copy is ~5 % of a long prefill GEMM.
 
@@ -28,6 +28,11 @@ import torch
 from . import kernels as K
 from ._ext import require
 from .weights_layout import can_shuffle, shuffle_for_stream, unshuffle_from_stream
+
+
+# largest M served by the stream GEMM (128-row blocks of one column tile share its weight reads through
+# L2); above it: unshuffled copy + hipBLASLt
+STREAM_MAX_M = int(os.environ.get("XOT_STREAM_MAX_M", "512"))
 
 
 def _m_bucket(M: int) -> int:
@@ -102,38 +107,52 @@ class GemmPolicy:
     with open(path, "w") as f:
       json.dump({json.dumps(list(k)): v for k, v in self.table.items()}, f, indent=1)
 
-  @staticmethod
-  def _time(fn) -> float:
+  _flush_buf = None
+
+  @classmethod
+  def _time(cls, fn) -> float:
+    """Cold-cache time of one call: a 512 MB write before each rep evicts the weight from L2 and the
+    256 MB MALL, as in a real forward pass where each layer's weights are read once per step."""
+    if cls._flush_buf is None:
+      cls._flush_buf = torch.empty(128 << 20, dtype=torch.float32, device=torch.cuda.current_device())
     fn()
     torch.cuda.synchronize()
     st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    best = float("inf")
-    for _ in range(3):
+    times = []
+    for _ in range(5):
+      cls._flush_buf.fill_(0.0)
       st.record()
-      for _ in range(3):
-        fn()
+      fn()
       en.record()
       en.synchronize()
-      best = min(best, st.elapsed_time(en))
-    return best
+      times.append(st.elapsed_time(en))
+    times.sort()
+    return times[1]
 
   def _no_tuning(self) -> bool:
     return self.capturing or torch.cuda.is_current_stream_capturing()
 
   # ---------------------------------------------------------------- row-major weights
-  def choose(self, x, w, bias, residual, epi, out_dtype) -> str:
+  def choose(self, x, w, bias, residual, epi, out_dtype):
+    """Row-major weight: hipBLASLt ("blas"), the library's skinny/tiled GEMM ("hip") or the stream
+    GEMM on the row-major layout (("stream", ntw, S)); cold-cache timed once per M bucket."""
     if self.mode in ("hip", "blas"):
       return self.mode
     M, Kd = x.shape
-    key = ("rm", _m_bucket(M), w.shape[0], Kd, epi, bias is not None)
+    N = w.shape[0]
+    key = ("rm", _m_bucket(M), N, Kd, epi, bias is not None)
     got = self.table.get(key)
     if got is not None:
       return got
     if self._no_tuning():
-      return "hip"
+      return "blas" if M > 128 else "hip"
+    cands = ["hip", "blas"]
+    if M <= 256:
+      cands += [("stream",) + c for c in self._stream_cands(M, N, Kd, epi)]
+      scratch.splitk(x.device, 8 * max(M, 128) * N)
     times = {}
     res_copy = residual.clone() if residual is not None else None
-    for impl in ("hip", "blas"):
+    for impl in cands:
       try:
         times[impl] = self._time(lambda: _run_rowmajor(impl, x, w, bias, res_copy, epi, None, out_dtype))
       except RuntimeError:
@@ -141,6 +160,17 @@ class GemmPolicy:
     got = min(times, key=times.get)
     self.table[key] = got
     return got
+
+  @staticmethod
+  def _stream_cands(M, N, Kd, epi):
+    cands = []
+    for ntw in ((2, 4) if epi == "silu" else (1, 2, 4)):
+      if N % (64 * ntw) or (ntw == 4 and M <= 32):
+        continue
+      for S in (1, 2, 4, 8):
+        if Kd % (S * 256) == 0 and (N // (64 * ntw)) * S <= 4096:
+          cands.append((ntw, S))
+    return cands
 
   # ---------------------------------------------------------------- shuffled weights
   def stream_cfg(self, x, w, bias, residual, epi, out_dtype) -> Tuple[int, int]:
@@ -150,18 +180,12 @@ class GemmPolicy:
     got = self.table.get(key)
     if got is not None:
       return got
-    cands = []
-    for ntw in ((2, 4) if epi == "silu" else (1, 2, 4)):
-      if N % (64 * ntw) or (ntw == 4 and M <= 32):
-        continue
-      for S in (1, 2, 4, 8):
-        if Kd % (S * 256) == 0 and (N // (64 * ntw)) * S <= 4096:
-          cands.append((ntw, S))
+    cands = self._stream_cands(M, N, Kd, epi)
     if not cands:
       raise RuntimeError(f"no stream-GEMM configuration for N={N} K={Kd}")
     if self._no_tuning():
       return self._heuristic(M, N, cands)
-    scratch.splitk(x.device, 8 * 128 * N)
+    scratch.splitk(x.device, 8 * max(M, 128) * N)
     y = torch.empty(M, N // 2 if epi == "silu" else N, dtype=out_dtype, device=x.device)
     times = {}
     for cfg in cands:
@@ -188,17 +212,22 @@ class GemmPolicy:
 policy = GemmPolicy()
 
 
-def _stream_call(x, w, bias, residual, epi, out, cfg):
+def _stream_call(x, w, bias, residual, epi, out, cfg, shuffled: bool = True):
   ntw, S = cfg
   M, N = x.shape[0], w.shape[0]
   ws = scratch.splitk(x.device, S * M * N) if S > 1 else None
-  require().gemm_stream(x, w, out, bias, residual, ws, K.EPI[epi], ntw, S, True)
+  require().gemm_stream(x, w, out, bias, residual, ws, K.EPI[epi], ntw, S, shuffled)
   return out
 
 
 def _run_rowmajor(impl, x, w, bias, residual, epi, out, out_dtype):
   if impl == "hip":
     return K.gemm(x, w, bias=bias, residual=residual, epi=epi, out=out, out_dtype=out_dtype)
+  if isinstance(impl, tuple) and impl[0] == "stream":
+    M, N = x.shape[0], w.shape[0]
+    if out is None:
+      out = torch.empty(M, N // 2 if epi == "silu" else N, dtype=out_dtype or x.dtype, device=x.device)
+    return _stream_call(x.contiguous(), w, bias, residual, epi, out, impl[1:], shuffled=False)
   return _blas(x, w, bias, residual, epi, out, out_dtype)
 
 
@@ -246,16 +275,12 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, r
   if layout_of(w) != "stream":
     impl = policy.choose(x, w, bias, residual, epi, dt)
     return _run_rowmajor(impl, x, w, bias, residual, epi, out, out_dtype)
-  if M > 256:
+  if M > STREAM_MAX_M:
     return _blas(x, scratch.dense_weight(w), bias, residual, epi, out, out_dtype)
   if out is None:
     out = torch.empty(M, N // 2 if epi == "silu" else N, dtype=dt, device=x.device)
   if x.stride(1) != 1:
     x = x.contiguous()
-  for lo in range(0, M, 128):  # rows are independent: 128-row slices share one tuned config
-    hi = min(M, lo + 128)
-    xs, ys = x[lo:hi], out[lo:hi]
-    rs = residual[lo:hi] if residual is not None else None
-    cfg = policy.stream_cfg(xs, w, bias, rs, epi, dt)
-    _stream_call(xs, w, bias, rs, epi, ys, cfg)
+  cfg = policy.stream_cfg(x, w, bias, residual, epi, dt)
+  _stream_call(x, w, bias, residual, epi, out, cfg)
   return out
