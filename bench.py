@@ -39,7 +39,7 @@ def main():
   ap.add_argument("--steps", type=int, default=16)
   ap.add_argument("--warmup", type=int, default=3)
   ap.add_argument("--model", default="llama-3-70b")
-  ap.add_argument("--batch-per-gpu", type=int, default=int(os.environ.get("XOT_BENCH_BATCH", 128)))
+  ap.add_argument("--batch-per-gpu", type=int, default=int(os.environ.get("XOT_BENCH_BATCH", 512)))
   ap.add_argument("--prompt-len", type=int, default=512)
   ap.add_argument("--temperature", type=float, default=0.6)
   ap.add_argument("--layers", type=int, default=0, help="debug only: truncate the model (result marked invalid)")

@@ -29,6 +29,7 @@ def init_distributed(backend: Optional[str] = None, timeout_s: int = 1800) -> tu
   """Init the default process group from torchrun-style env vars.  Returns (rank, world, device)."""
   rank, local, world = env_rank()
   if torch.cuda.is_available():
+    local = local % torch.cuda.device_count()  # more ranks than GPUs only in single-GPU rehearsals
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
   else:

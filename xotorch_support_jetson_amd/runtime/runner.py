@@ -211,7 +211,9 @@ class ShardRunner:
     graph = torch.cuda.CUDAGraph()
     linear_mod.policy.capturing = True
     try:
-      with torch.cuda.graph(graph):
+      # thread-local capture: the process-group watchdog thread keeps polling its RCCL events while
+      # this thread captures (global mode would make those queries fail)
+      with torch.cuda.graph(graph, capture_error_mode="thread_local"):
         g["out"] = self.model.forward(g["x"], inp)
     finally:
       linear_mod.policy.capturing = False
