@@ -254,3 +254,49 @@ def test_gemm_stream(gpu, M, epi, ntw, splits):
     require().gemm_stream(x, shuffle_for_stream(w), y2, b, r if epi == "resid" else None, ws, K.EPI[epi], ntw,
                           splits, True)
     assert rel_err(y2, ref) < 1e-2
+
+
+# ------------------------------------------------------------------ mixture of experts
+@pytest.mark.parametrize("T,E,k", [(1, 8, 2), (7, 8, 2), (100, 8, 2), (300, 4, 2), (64, 16, 4)])
+@pytest.mark.parametrize("shuffled", [False, True])
+def test_moe_layer(gpu, T, E, k, shuffled):
+  """route -> grouped gate/up (gathered rows, SiLU*mul) -> grouped down -> combine, vs an fp32
+  per-expert reference of the same Mixtral MoE block."""
+  from xotorch_support_jetson_amd.ops._ext import require
+  from xotorch_support_jetson_amd.ops.weights_layout import shuffle_for_stream
+  torch.manual_seed(T + E)
+  C = require()
+  D, F = 256, 512
+  x = torch.randn(T, D, device=gpu).to(torch.bfloat16)
+  h = torch.randn(T, D, device=gpu).to(torch.bfloat16)
+  router = torch.randn(T, E, device=gpu, dtype=torch.float32)
+  gu = (torch.randn(E, 2 * F, D, device=gpu) / math.sqrt(D)).to(torch.bfloat16)  # 16-row interleaved g/u
+  down = (torch.randn(E, D, F, device=gpu) / math.sqrt(F)).to(torch.bfloat16)
+  # fp32 reference
+  probs = torch.softmax(router, -1)
+  tw, ti = torch.topk(probs, k, -1)
+  tw = tw / tw.sum(-1, keepdim=True)
+  ref = h.float().clone()
+  for t in range(T):
+    for j in range(k):
+      e = int(ti[t, j])
+      g = (x[t].float() @ gu[e].float().t()).view(-1, 2, 16)
+      a = torch.nn.functional.silu(g[:, 0]) * g[:, 1]
+      ref[t] += tw[t, j] * (a.reshape(-1).to(torch.bfloat16).float() @ down[e].float().t())
+  topw = torch.empty(T * k, device=gpu)
+  topi = torch.empty(T * k, dtype=torch.int32, device=gpu)
+  slot_of = torch.empty_like(topi)
+  sorted_tok = torch.empty_like(topi)
+  off = torch.empty(E + 1, dtype=torch.int32, device=gpu)
+  C.moe_route(router, k, topw, topi, slot_of, sorted_tok, off)
+  assert torch.equal(torch.sort(topi.view(T, k).long(), -1)[0], torch.sort(ti, -1)[0])
+  assert int(off[-1]) == T * k and torch.equal(torch.sort(slot_of.long())[0], torch.arange(T * k, device=gpu))
+  gw = torch.stack([shuffle_for_stream(gu[e]) for e in range(E)]) if shuffled else gu
+  dw = torch.stack([shuffle_for_stream(down[e]) for e in range(E)]) if shuffled else down
+  act = torch.empty(T * k, F, dtype=torch.bfloat16, device=gpu)
+  C.gemm_moe(x, gw, act, off, sorted_tok, 2, T, shuffled)
+  y = torch.empty(T * k, D, dtype=torch.float32, device=gpu)
+  C.gemm_moe(act, dw, y, off, None, 0, T, shuffled)
+  out = h.clone()
+  C.moe_combine(y, slot_of, topw, out)
+  assert rel_err(out.float() - h.float(), ref - h.float()) < 3e-2  # the MoE contribution itself

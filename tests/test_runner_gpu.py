@@ -17,7 +17,7 @@ def test_split_equals_full_gpu(gpu, name):
   L = c.num_layers
   full = ShardRunner(c, Shard(name, 0, L - 1, L), gpu, max_batch=8, max_ctx=512, use_graphs=False)
   a = ShardRunner(c, Shard(name, 0, L // 2 - 1, L), gpu, max_batch=8, max_ctx=512, use_graphs=False)
-  b = ShardRunner(c, Shard(name, L // 2, L - 1, L), gpu, max_batch=8, max_ctx=512, use_graphs=not c.is_moe)
+  b = ShardRunner(c, Shard(name, L // 2, L - 1, L), gpu, max_batch=8, max_ctx=512, use_graphs=True)
   g = torch.Generator().manual_seed(0)
   ids = torch.randint(0, c.vocab_size, (30,), generator=g, dtype=torch.int32)
   rids, q = ["x", "y", "z"], [10, 15, 5]

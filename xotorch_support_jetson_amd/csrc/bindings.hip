@@ -234,6 +234,69 @@ void gemm_stream(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const 
          " splits=", splits);
 }
 
+// grouped expert GEMM: y[slot] = x[gather ? gather[slot] : slot] @ w[e].T for slots of expert e
+void gemm_moe(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const at::Tensor& off,
+              const c10::optional<at::Tensor>& gather, int64_t epi, int64_t max_rows, bool wshuf) {
+  CHECK_BF16(x);
+  CHECK_BF16(w);
+  CHECK_GPU(y);
+  CHECK_GPU(off);
+  CHECK_DT(off, at::kInt);
+  XCHECK(x.dim() == 2 && w.dim() == 3 && y.dim() == 2, "gemm_moe: x [rows, K], w [E, N, K], y [slots, N']");
+  XCHECK(x.stride(1) == 1 && w.is_contiguous() && y.is_contiguous() && off.is_contiguous(), "gemm_moe: layout");
+  const int64_t E = w.size(0), N = w.size(1), K = w.size(2);
+  XCHECK(x.size(1) == K, "gemm_moe: K mismatch");
+  XCHECK(off.numel() == E + 1, "gemm_moe: off must have E+1 entries");
+  XCHECK(epi == 0 || epi == 2, "gemm_moe: epilogue must be none or silu");
+  const bool f32 = y.scalar_type() == at::kFloat;
+  XCHECK(f32 || y.scalar_type() == at::kBFloat16, "gemm_moe: y must be bf16 or fp32");
+  XCHECK(y.size(1) == (epi == 2 ? N / 2 : N), "gemm_moe: y width mismatch");
+  XCHECK(max_rows >= 0 && max_rows <= y.size(0), "gemm_moe: max_rows must be <= slots");
+  const int* gp = nullptr;
+  if (gather.has_value()) {
+    CHECK_GPU((*gather));
+    CHECK_DT((*gather), at::kInt);
+    XCHECK(gather->is_contiguous() && gather->numel() == y.size(0), "gemm_moe: gather must have one entry per slot");
+    gp = gather->data_ptr<int>();
+  } else {
+    XCHECK(x.size(0) == y.size(0), "gemm_moe: without gather, x rows are slots");
+  }
+  const int rc = xot::launch_gemm_moe(bf(x), (int)x.stride(0), bf(w), y.data_ptr(), (int)y.stride(0), f32, (int)epi,
+                                      off.data_ptr<int>(), gp, (int)E, (int)max_rows, (int)N, (int)K, wshuf,
+                                      cur_stream());
+  XCHECK(rc == 0, "gemm_moe: unsupported shape N=", N, " K=", K, " epi=", epi);
+}
+
+void moe_route(const at::Tensor& logits, int64_t k, at::Tensor& topw, at::Tensor& topi, at::Tensor& slot_of,
+               at::Tensor& sorted_tok, at::Tensor& off) {
+  CHECK_GPU(logits);
+  CHECK_DT(logits, at::kFloat);
+  XCHECK(all_contig_gpu(logits, topw, topi, slot_of, sorted_tok, off), "moe_route: tensors must be contiguous GPU");
+  const int64_t T = logits.size(0), E = logits.size(1);
+  XCHECK(E >= 1 && E <= 64 && k >= 1 && k <= 8 && k <= E, "moe_route: need 1 <= k <= E <= 64, k <= 8");
+  CHECK_DT(topw, at::kFloat);
+  CHECK_DT(topi, at::kInt);
+  CHECK_DT(slot_of, at::kInt);
+  CHECK_DT(sorted_tok, at::kInt);
+  CHECK_DT(off, at::kInt);
+  XCHECK(topw.numel() == T * k && topi.numel() == T * k && slot_of.numel() == T * k && sorted_tok.numel() == T * k &&
+             off.numel() == E + 1,
+         "moe_route: output sizes");
+  xot::launch_moe_route(logits.data_ptr<float>(), (int)T, (int)E, (int)k, topw.data_ptr<float>(), topi.data_ptr<int>(),
+                        slot_of.data_ptr<int>(), sorted_tok.data_ptr<int>(), off.data_ptr<int>(), cur_stream());
+}
+
+void moe_combine(const at::Tensor& y, const at::Tensor& slot_of, const at::Tensor& topw, at::Tensor& h) {
+  CHECK_GPU(y);
+  CHECK_DT(y, at::kFloat);
+  CHECK_BF16(h);
+  XCHECK(all_contig_gpu(y, slot_of, topw, h), "moe_combine: tensors must be contiguous GPU");
+  const int64_t T = h.size(0), D = h.size(1), k = slot_of.numel() / T;
+  XCHECK(D % 8 == 0 && y.size(1) == D && y.size(0) == T * k && topw.numel() == T * k, "moe_combine: shapes");
+  xot::launch_moe_combine(y.data_ptr<float>(), slot_of.data_ptr<int>(), topw.data_ptr<float>(), bf(h), (int)T, (int)k,
+                          (int)D, cur_stream());
+}
+
 void attn_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
                  const at::Tensor& block_tables, const at::Tensor& ctx_lens, at::Tensor& out, at::Tensor& ws_o,
                  at::Tensor& ws_ml, int64_t pages_per_part, int64_t nparts, double scale) {
@@ -365,6 +428,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("rope_apply", &rope_apply);
   m.def("gemm", &gemm);
   m.def("gemm_stream", &gemm_stream);
+  m.def("gemm_moe", &gemm_moe);
+  m.def("moe_route", &moe_route);
+  m.def("moe_combine", &moe_combine);
   m.def("attn_decode", &attn_decode);
   m.def("attn_prefill", &attn_prefill);
   m.def("sample", &sample);

@@ -191,26 +191,32 @@ int launch_gemm_skinny(const uint16_t* X, int ldx, const uint16_t* W, int ldw, c
 // MFMA k-order is permuted per lane group (group g owns k in [8*KS*g, 8*KS*(g+1)) of the chunk)
 // so each lane reads 16*KS contiguous bytes of its weight row per chunk.
 // SPLIT: fp32 partial slabs ws[blockIdx.y][M][N], finished by splitk_reduce_kernel (epilogue there).
-// WM = 2: 8 waves as 2 (row halves) x 4 (column groups); both row halves use the same weight
-// fragments, so a CU streams each weight byte once for 2*16*MT rows (the M = 256 decode shape).
-template <int MT, int NTW, int KS, int EPI, bool OUT_F32, bool SPLIT, bool WSHUF, int OCC, int WM>
-__global__ __launch_bounds__(256 * WM, OCC) void gemm_stream_kernel(const uint16_t* __restrict__ X, int ldx,
+// MOE = 1 / 2: grouped (mixture-of-experts) GEMM.  blockIdx.z = expert e with weight W[e]
+// ([E][N][K], same layout per expert) and rows moe_off[e] .. moe_off[e+1] of the expert-sorted slot
+// order; MOE = 1 reads A in slot order, MOE = 2 gathers A row moe_gather[slot] (token rows).  Output
+// rows are slots.  Row blocks past an expert's count exit at once, so the grid can be sized for the
+// worst case on the host and the launch stays graph-capturable (no host sync on the routing).
+template <int MT, int NTW, int KS, int EPI, bool OUT_F32, bool SPLIT, bool WSHUF, int OCC, int MOE>
+__global__ __launch_bounds__(256, OCC) void gemm_stream_kernel(const uint16_t* __restrict__ X, int ldx,
                                                              const uint16_t* __restrict__ W, int ldw,
                                                              const uint16_t* __restrict__ bias,
                                                              const uint16_t* __restrict__ R, int ldr,
                                                              void* __restrict__ Yv, int ldy,
                                                              float* __restrict__ ws, int M, int N, int kper,
-                                                             int mblocks) {
+                                                             int mblocks, const int* __restrict__ moe_off,
+                                                             const int* __restrict__ moe_gather) {
   constexpr int KC = 32 * KS;
   constexpr int CPR = KC / 8;  // 16-B chunks per row per k-chunk
-  constexpr int NTH = 256 * WM;
-  constexpr int ROWS = 16 * MT * WM;
+  constexpr int NTH = 256;
+  constexpr int ROWS = 16 * MT;
   constexpr int XPT = ROWS * CPR / NTH;  // staging chunks per thread
   static_assert(XPT >= 1, "tile too small for 256 threads");
-  // X double buffer in dynamic LDS (2 x ROWS x KC bf16: 128 KB at ROWS = 256)
+  static_assert(MOE == 0 || !SPLIT, "grouped GEMM runs without split-K");
+  // X double buffer in dynamic LDS (2 x ROWS x KC bf16)
   extern __shared__ __attribute__((aligned(16))) uint16_t xs_raw[];
   auto xs = reinterpret_cast<uint16_t(*)[ROWS * KC]>(xs_raw);
-  const int tid = threadIdx.x, lane = tid & 63, wave = (tid >> 6) & 3, wrow = 16 * MT * (tid >> 8);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr int wrow = 0;
   const int g = lane >> 4, c = lane & 15;
   // M-blocking (M > ROWS): blockIdx.x = (column tile, row block).  The row blocks of one column tile
   // get ids 8 apart, i.e. the same XCD under round-robin dispatch, and run together: the weight tile
@@ -227,14 +233,22 @@ __global__ __launch_bounds__(256 * WM, OCC) void gemm_stream_kernel(const uint16
       bt /= mblocks;
     }
   }
+  int row0 = 0;  // first output row of this launch's row range
+  if constexpr (MOE != 0) {
+    const int e = blockIdx.z;
+    row0 = moe_off[e];
+    M = moe_off[e + 1] - row0;  // this expert's rows
+    W += (size_t)e * N * ldw;
+    if (mb * ROWS >= M) return;  // uniform over the workgroup, before any barrier
+  }
   const int Mtot = M, m_base = mb * ROWS;
   M = min(ROWS, Mtot - m_base);
-  X += (size_t)m_base * ldx;
-  if constexpr (EPI == EPI_RESID) R += (size_t)m_base * ldr;
+  if constexpr (MOE != 2) X += (size_t)(row0 + m_base) * ldx;
+  if constexpr (EPI == EPI_RESID) R += (size_t)(row0 + m_base) * ldr;
   if constexpr (OUT_F32)
-    Yv = reinterpret_cast<float*>(Yv) + (size_t)m_base * ldy;
+    Yv = reinterpret_cast<float*>(Yv) + (size_t)(row0 + m_base) * ldy;
   else
-    Yv = reinterpret_cast<uint16_t*>(Yv) + (size_t)m_base * ldy;
+    Yv = reinterpret_cast<uint16_t*>(Yv) + (size_t)(row0 + m_base) * ldy;
   const int n0 = bt * (64 * NTW) + wave * 16 * NTW;
   const int kb = blockIdx.y * kper;
   const int nch = kper / KC;
@@ -255,12 +269,21 @@ __global__ __launch_bounds__(256 * WM, OCC) void gemm_stream_kernel(const uint16
   // staging geometry of this thread's XPT chunks, recomputed on use (keeps VGPRs for the pipeline):
   // chunk q = tid + NTH*i -> row q / CPR, logical 16-B slot q % CPR
   const uint16_t* xbase = X + kb;
+  int srow[MOE == 2 ? XPT : 1];  // gathered source rows of this thread's staging chunks
+  if constexpr (MOE == 2) {
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const int row = (tid + NTH * i) / CPR;
+      srow[i] = row < M ? moe_gather[row0 + m_base + row] : 0;
+    }
+  }
   auto xload = [&](s16x8 (&xr)[XPT], int ch) {
 #pragma unroll
     for (int i = 0; i < XPT; ++i) {
       const int q = tid + NTH * i, row = q / CPR, cc = q % CPR;
       const bool ok = row < M;
-      s16x8 v = ld16(xbase + (size_t)(ok ? row : 0) * ldx + ch * KC + cc * 8);
+      const int src = MOE == 2 ? srow[i] : (ok ? row : 0);
+      s16x8 v = ld16(xbase + (size_t)src * ldx + ch * KC + cc * 8);
       xr[i] = ok ? v : s16x8{0, 0, 0, 0, 0, 0, 0, 0};
     }
   };
@@ -471,32 +494,32 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   }
 }
 
-template <int MT, int NTW, int KS, int EPI, bool F32, bool WSH, int WM = 1>
+template <int MT, int NTW, int KS, int EPI, bool F32, bool WSH>
 static void stream_launch(const uint16_t* X, int ldx, const uint16_t* W, int ldw, const uint16_t* bias,
                           const uint16_t* R, int ldr, void* Y, int ldy, float* ws, int M, int N, int K, int S,
                           hipStream_t st) {
   // occupancy request: 2 workgroups/CU while the register budget allows it
-  constexpr int OCC = (MT * NTW >= 32 || WM > 1) ? 1 : 2;
-  constexpr int SMEM = 2 * 16 * MT * WM * 32 * KS * 2;
-  const int mblocks = (M + 16 * MT * WM - 1) / (16 * MT * WM);
+  constexpr int OCC = (MT * NTW >= 32) ? 1 : 2;
+  constexpr int SMEM = 2 * 16 * MT * 32 * KS * 2;
+  const int mblocks = (M + 16 * MT - 1) / (16 * MT);
   dim3 grid(N / (64 * NTW) * mblocks, S);
   const int kper = K / S;
   if (S == 1) {
-    auto kern = gemm_stream_kernel<MT, NTW, KS, EPI, F32, false, WSH, OCC, WM>;
+    auto kern = gemm_stream_kernel<MT, NTW, KS, EPI, F32, false, WSH, OCC, 0>;
     if constexpr (SMEM > 65536) {
       static bool attr = (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM) ==
                           hipSuccess);
       (void)attr;
     }
-    kern<<<grid, 256 * WM, SMEM, st>>>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, nullptr, M, N, kper, mblocks);
+    kern<<<grid, 256, SMEM, st>>>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, nullptr, M, N, kper, mblocks, nullptr, nullptr);
   } else {
-    auto kern = gemm_stream_kernel<MT, NTW, KS, EPI, F32, true, WSH, OCC, WM>;
+    auto kern = gemm_stream_kernel<MT, NTW, KS, EPI, F32, true, WSH, OCC, 0>;
     if constexpr (SMEM > 65536) {
       static bool attr = (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM) ==
                           hipSuccess);
       (void)attr;
     }
-    kern<<<grid, 256 * WM, SMEM, st>>>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, M, N, kper, mblocks);
+    kern<<<grid, 256, SMEM, st>>>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, M, N, kper, mblocks, nullptr, nullptr);
     const int ncol = EPI == EPI_SILU ? N / 2 : N;
     long chunks = (long)M * (ncol / 8);
     int blocks = (int)((chunks + 255) / 256);
@@ -539,12 +562,60 @@ static int stream_dispatch(const uint16_t* X, int ldx, const uint16_t* W, int ld
   if (mt <= 4) XOT_ST(4, 4);
   if (mt <= 8) XOT_ST(8, 4);
   // M > 128: 128-row blocks; the blocks of one column tile run on one XCD together (see the kernel).
-  // (256-row tiles -- MT = 16, or WM = 2 -- need > 256 registers per lane at this pipeline depth and
-  // spill; measured slower than the M-blocked 128-row tile.)
+  // (256-row tiles -- MT = 16, or 8 waves as 2 row halves x 4 column groups -- need > 256 registers
+  // per lane at this pipeline depth and spill; both measured slower than the M-blocked 128-row tile.)
   XOT_ST(8, 4);
 #undef XOT_ST
 #undef XOT_ST2
   return -1;
+}
+
+// ------------------------------------------------------------------------------------ grouped (MoE)
+template <int MT, int EPI, bool F32, bool WSH, int MOE>
+static void moe_launch(const uint16_t* X, int ldx, const uint16_t* W, void* Y, int ldy, const int* off,
+                       const int* gather, int E, int max_rows, int N, int K, hipStream_t st) {
+  constexpr int NTW = 2, KS = 4;
+  constexpr int OCC = (MT * NTW >= 32) ? 1 : 2;
+  constexpr int SMEM = 2 * 16 * MT * 32 * KS * 2;
+  const int mblocks = (max_rows + 16 * MT - 1) / (16 * MT);
+  dim3 grid(N / (64 * NTW) * mblocks, 1, E);
+  gemm_stream_kernel<MT, NTW, KS, EPI, F32, false, WSH, OCC, MOE><<<grid, 256, SMEM, st>>>(
+      X, ldx, W, K, nullptr, nullptr, 0, Y, ldy, nullptr, max_rows, N, K, mblocks, off, gather);
+}
+
+template <int EPI, bool F32, bool WSH, int MOE>
+static void moe_mt(const uint16_t* X, int ldx, const uint16_t* W, void* Y, int ldy, const int* off,
+                   const int* gather, int E, int max_rows, int N, int K, hipStream_t st) {
+  if (max_rows <= 16)
+    moe_launch<1, EPI, F32, WSH, MOE>(X, ldx, W, Y, ldy, off, gather, E, max_rows, N, K, st);
+  else if (max_rows <= 64)
+    moe_launch<4, EPI, F32, WSH, MOE>(X, ldx, W, Y, ldy, off, gather, E, max_rows, N, K, st);
+  else
+    moe_launch<8, EPI, F32, WSH, MOE>(X, ldx, W, Y, ldy, off, gather, E, max_rows, N, K, st);
+}
+
+int launch_gemm_moe(const uint16_t* X, int ldx, const uint16_t* W, void* Y, int ldy, bool out_f32, int epi,
+                    const int* off, const int* gather, int E, int max_rows, int N, int K, bool wshuf,
+                    hipStream_t s) {
+  if (max_rows <= 0) return 0;
+  if (N % 128 != 0 || K % 256 != 0) return -1;
+  if (epi != EPI_NONE && epi != EPI_SILU) return -1;
+  if (epi == EPI_SILU && out_f32) return -1;
+#define XOT_MOE(EPIV, F32V)                                                                        \
+  do {                                                                                              \
+    if (wshuf) {                                                                                    \
+      if (gather) moe_mt<EPIV, F32V, true, 2>(X, ldx, W, Y, ldy, off, gather, E, max_rows, N, K, s);  \
+      else moe_mt<EPIV, F32V, true, 1>(X, ldx, W, Y, ldy, off, gather, E, max_rows, N, K, s);         \
+    } else {                                                                                        \
+      if (gather) moe_mt<EPIV, F32V, false, 2>(X, ldx, W, Y, ldy, off, gather, E, max_rows, N, K, s); \
+      else moe_mt<EPIV, F32V, false, 1>(X, ldx, W, Y, ldy, off, gather, E, max_rows, N, K, s);        \
+    }                                                                                               \
+    return 0;                                                                                       \
+  } while (0)
+  if (epi == EPI_SILU) XOT_MOE(EPI_SILU, false);
+  if (out_f32) XOT_MOE(EPI_NONE, true);
+  XOT_MOE(EPI_NONE, false);
+#undef XOT_MOE
 }
 
 int launch_gemm_stream(const uint16_t* X, int ldx, const uint16_t* W, int ldw, const uint16_t* bias,

@@ -1,0 +1,127 @@
+// Mixture-of-experts routing and combine for gfx950 (Mixtral-style top-k softmax gating).
+//
+// moe_route: one workgroup of 1024 threads.  Per token: softmax over the E router logits, top-k,
+// renormalised weights; per expert a count (LDS atomics), an exclusive scan to slot offsets, and each
+// (token, j) gets a slot in the expert-sorted order.  Slot order inside an expert is arbitrary: the
+// grouped GEMM treats rows independently and the combine sums each token's k slots in j order, so
+// results do not depend on it.  Everything stays on the device (graph-capturable).
+// moe_combine: h[t] += sum_j w[t, j] * y[slot_of[t, j]] with the expert outputs y in fp32.
+#include "common.h"
+#include "kernels.h"
+
+namespace xot {
+
+constexpr int MOE_MAX_E = 64;
+constexpr int MOE_MAX_K = 8;
+
+__global__ __launch_bounds__(1024) void moe_route_kernel(const float* __restrict__ logits, int T, int E, int k,
+                                                         float* __restrict__ topw, int32_t* __restrict__ topi,
+                                                         int32_t* __restrict__ slot_of,
+                                                         int32_t* __restrict__ sorted_tok, int32_t* __restrict__ off) {
+  __shared__ int cnt[MOE_MAX_E];
+  __shared__ int base[MOE_MAX_E + 1];
+  const int tid = threadIdx.x;
+  if (tid < MOE_MAX_E) cnt[tid] = 0;
+  __syncthreads();
+  for (int t = tid; t < T; t += blockDim.x) {
+    const float* lg = logits + (size_t)t * E;
+    float mx = -INFINITY;
+    for (int e = 0; e < E; ++e) mx = fmaxf(mx, lg[e]);
+    float sel_v[MOE_MAX_K];
+    int sel_i[MOE_MAX_K];
+    for (int j = 0; j < k; ++j) {
+      sel_v[j] = -INFINITY;
+      sel_i[j] = 0;
+    }
+    for (int e = 0; e < E; ++e) {  // insertion into the running top-k (ties -> lower expert id)
+      float v = lg[e];
+      int id = e;
+      for (int j = 0; j < k; ++j) {
+        if (v > sel_v[j]) {
+          const float tv = sel_v[j];
+          const int ti = sel_i[j];
+          sel_v[j] = v;
+          sel_i[j] = id;
+          v = tv;
+          id = ti;
+        }
+      }
+    }
+    // softmax restricted to the selected experts == top-k of the full softmax, renormalised
+    float den = 0.f;
+    for (int j = 0; j < k; ++j) den += __expf(sel_v[j] - mx);
+    for (int j = 0; j < k; ++j) {
+      topw[(size_t)t * k + j] = __expf(sel_v[j] - mx) / den;
+      topi[(size_t)t * k + j] = sel_i[j];
+      atomicAdd(&cnt[sel_i[j]], 1);
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int acc = 0;
+    for (int e = 0; e < E; ++e) {
+      base[e] = acc;
+      off[e] = acc;
+      acc += cnt[e];
+    }
+    off[E] = acc;
+  }
+  __syncthreads();
+  if (tid < E) cnt[tid] = 0;
+  __syncthreads();
+  for (int t = tid; t < T; t += blockDim.x) {
+    for (int j = 0; j < k; ++j) {
+      const int e = topi[(size_t)t * k + j];
+      const int pos = base[e] + atomicAdd(&cnt[e], 1);
+      slot_of[(size_t)t * k + j] = pos;
+      sorted_tok[pos] = t;
+    }
+  }
+}
+
+// one thread per 8 hidden columns of one token
+__global__ __launch_bounds__(256) void moe_combine_kernel(const float* __restrict__ y,
+                                                          const int32_t* __restrict__ slot_of,
+                                                          const float* __restrict__ topw, uint16_t* __restrict__ h,
+                                                          int T, int k, int D) {
+  const long total = (long)T * (D / 8);
+  for (long q = blockIdx.x * 256L + threadIdx.x; q < total; q += (long)gridDim.x * 256) {
+    const int t = (int)(q / (D / 8));
+    const int d = (int)(q % (D / 8)) * 8;
+    s16x8 hv = ld16(h + (size_t)t * D + d);
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = bf2f(hv[e]);
+    for (int j = 0; j < k; ++j) {
+      const float w = topw[(size_t)t * k + j];
+      const float* yr = y + (size_t)slot_of[(size_t)t * k + j] * D + d;
+      const f32x4 a = *reinterpret_cast<const f32x4*>(yr);
+      const f32x4 b = *reinterpret_cast<const f32x4*>(yr + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        acc[e] += w * a[e];
+        acc[4 + e] += w * b[e];
+      }
+    }
+    s16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (short)f2bf(acc[e]);
+    st16(h + (size_t)t * D + d, o);
+  }
+}
+
+void launch_moe_route(const float* logits, int T, int E, int k, float* topw, int32_t* topi, int32_t* slot_of,
+                      int32_t* sorted_tok, int32_t* off, hipStream_t s) {
+  moe_route_kernel<<<1, 1024, 0, s>>>(logits, T, E, k, topw, topi, slot_of, sorted_tok, off);
+}
+
+void launch_moe_combine(const float* y, const int32_t* slot_of, const float* topw, uint16_t* h, int T, int k, int D,
+                        hipStream_t s) {
+  const long chunks = (long)T * (D / 8);
+  int blocks = (int)((chunks + 255) / 256);
+  if (blocks > 4096) blocks = 4096;
+  if (blocks < 1) return;
+  moe_combine_kernel<<<blocks, 256, 0, s>>>(y, slot_of, topw, h, T, k, D);
+}
+
+}  // namespace xot

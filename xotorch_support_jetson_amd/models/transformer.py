@@ -26,7 +26,8 @@ import torch
 
 from ..inference.shard import Shard
 from ..ops import kernels as K
-from ..ops.linear import linear
+from ..ops._ext import require
+from ..ops.linear import layout_of, linear
 from ..ops.rope import build_cos_sin
 from .config import ModelConfig
 from .weights import ShardWeights, expert
@@ -109,6 +110,8 @@ class ShardModel:
     kernel library (gate/up with fused SiLU epilogue), weighted scatter-add back into h."""
     c = self.c
     logits = linear(xn, lw.router, out_dtype=torch.float32)  # [T, E]
+    if xn.is_cuda:
+      return self._moe_gpu(xn, lw, h, logits)
     probs = torch.softmax(logits, dim=-1)
     topw, topi = torch.topk(probs, c.num_experts_per_tok, dim=-1)
     topw = topw / topw.sum(-1, keepdim=True)
@@ -130,6 +133,28 @@ class ShardModel:
       out.index_add_(0, idx, ye * wflat[start:start + n, None])
       start += n
     h += out.to(h.dtype)
+    return h
+
+  def _moe_gpu(self, xn: torch.Tensor, lw, h: torch.Tensor, logits: torch.Tensor) -> torch.Tensor:
+    """Device-only MoE (graph-capturable): routing kernel (softmax top-k, per-expert slot order),
+    grouped gate/up GEMM gathering token rows with the SiLU*mul epilogue, grouped down GEMM into fp32
+    slots, combine kernel adding sum_j w_j * y_slot(j) into the residual stream."""
+    c = self.c
+    T, D = xn.shape
+    k, E, F = c.num_experts_per_tok, c.num_experts, c.intermediate_size
+    dev = xn.device
+    C = require()
+    topw = torch.empty(T * k, dtype=torch.float32, device=dev)
+    topi = torch.empty(T * k, dtype=torch.int32, device=dev)
+    slot_of = torch.empty(T * k, dtype=torch.int32, device=dev)
+    sorted_tok = torch.empty(T * k, dtype=torch.int32, device=dev)
+    off = torch.empty(E + 1, dtype=torch.int32, device=dev)
+    C.moe_route(logits.contiguous(), k, topw, topi, slot_of, sorted_tok, off)
+    act = torch.empty(T * k, F, dtype=torch.bfloat16, device=dev)
+    C.gemm_moe(xn, lw.gu_w, act, off, sorted_tok, K.EPI["silu"], T, layout_of(lw.gu_w) == "stream")
+    y = torch.empty(T * k, D, dtype=torch.float32, device=dev)
+    C.gemm_moe(act, lw.down_w, y, off, None, K.EPI["none"], T, layout_of(lw.down_w) == "stream")
+    C.moe_combine(y, slot_of, topw, h)
     return h
 
   # ------------------------------------------------------------------ forward

@@ -71,8 +71,8 @@ class ShardRunner:
     self.width = -(-max_ctx // PAGE)
     self.model = ShardModel(self.weights, self.kv, max_batch=max_batch, max_ctx=max_ctx)
     if use_graphs is None:
-      # MoE routing sizes expert groups on the host (not capturable yet)
-      use_graphs = self.device.type == "cuda" and os.environ.get("XOT_GRAPHS", "1") == "1" and not config.is_moe
+      # MoE routing runs on the device too (moe_route + grouped GEMMs), so every model is capturable
+      use_graphs = self.device.type == "cuda" and os.environ.get("XOT_GRAPHS", "1") == "1"
     self.use_graphs = use_graphs
     self._graphs: Dict[int, dict] = {}
     self._tables_host = torch.zeros(max_batch, self.width, dtype=torch.int32)
