@@ -37,6 +37,7 @@ def main():
   ap.add_argument("--quick", action="store_true")
   ap.add_argument("--json", default=None)
   ap.add_argument("--gemm-only", action="store_true")
+  ap.add_argument("--attn-only", action="store_true")
   args = ap.parse_args()
   dev = torch.device("cuda:0")
   res = {"gemm": [], "attn_decode": [], "attn_prefill": [], "misc": []}
@@ -45,7 +46,7 @@ def main():
   shapes = [("qkv", 10240, 8192), ("o", 8192, 8192), ("gate_up", 57344, 8192), ("down", 8192, 28672),
             ("lm_head", 128256, 8192)]
   Ms = [1, 16, 32, 64, 128] if not args.quick else [16, 64, 128]
-  for name, N, Kd in shapes:
+  for name, N, Kd in ([] if args.attn_only else shapes):
     w = torch.randn(N, Kd, device=dev, dtype=torch.bfloat16) * 0.02
     for M in Ms:
       x = torch.randn(M, Kd, device=dev, dtype=torch.bfloat16)
@@ -99,7 +100,7 @@ def main():
     del w, x, y
   # decode attention, Llama-70B heads
   H, Hkv, Dh = 64, 8, 128
-  for B, ctx in [(1, 1024), (16, 2048), (64, 1024), (128, 1024), (128, 4096)]:
+  for B, ctx in [(1, 1024), (1, 32768), (16, 2048), (64, 1024), (128, 1024), (128, 4096), (256, 525), (512, 525)]:
     npg = -(-ctx // 64)
     kc = torch.randn(B * npg, Hkv, 64, Dh, device=dev, dtype=torch.bfloat16)
     vc = torch.randn(B * npg, Hkv, Dh, 64, device=dev, dtype=torch.bfloat16)
