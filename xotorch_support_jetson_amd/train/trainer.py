@@ -114,15 +114,55 @@ class ShardTrainer:
     x = self._to(example)
     return self.forward(x).detach().cpu()
 
-  def loss_of(self, logits: torch.Tensor, target, lengths) -> Tuple[torch.Tensor, int]:
+  def loss_of(self, logits: torch.Tensor, target, lengths, denom: Optional[float] = None) -> Tuple[torch.Tensor, int]:
+    """Length-masked CE summed over valid tokens / denom (default: this batch's valid-token count)."""
     B, L, V = logits.shape
     y = self._to(target, torch.int64)
     ln = self._to(lengths, torch.int64).view(-1)
     mask = torch.arange(L, device=self.device)[None, :] < ln[:, None]
     tgt = torch.where(mask, y, torch.full_like(y, -100)).view(-1).to(torch.int32)
-    n = int(mask.sum().item())
-    w = torch.full((B * L,), 1.0 / max(n, 1), device=self.device, dtype=torch.float32)
+    if denom is None:
+      n = int(mask.sum().item())
+      denom = float(max(n, 1))
+    else:
+      n = -1  # not computed (no host sync)
+    w = torch.full((B * L,), 1.0 / denom, device=self.device, dtype=torch.float32)
     return A.cross_entropy(logits.reshape(B * L, V), tgt, w), n
+
+  # ------------------------------------------------------------------ accumulate / apply
+  # (pipeline schedules: forward every micro-batch, backward every micro-batch, then one optimizer
+  # step; see parallel/pipeline_train.py)
+  def zero_grad(self) -> None:
+    for p in self.params.values():
+      p.grad = None
+
+  def forward_train(self, x) -> Tuple[Optional[torch.Tensor], torch.Tensor]:
+    """Forward with autograd: returns (input leaf or None for token ids, output)."""
+    x = self._to(x)
+    leaf = None
+    if not self.shard.is_first_layer():
+      leaf = x.to(torch.bfloat16).detach().requires_grad_(True)
+      x = leaf
+    return leaf, self.forward(x)
+
+  def backward_accumulate(self, leaf, out, grad_out=None, target=None, length=None,
+                          denom: Optional[float] = None) -> Tuple[Optional[torch.Tensor], Optional[torch.Tensor]]:
+    """Accumulate parameter grads of one micro-batch.  Last stage: CE(out, target) / denom (returned
+    as a device scalar, no sync); other stages: out.backward(grad_out).  Returns (loss, grad wrt input)."""
+    loss = None
+    if grad_out is None:
+      loss, _ = self.loss_of(out, target, length, denom)
+      loss.backward()
+      loss = loss.detach()
+    else:
+      out.backward(grad_out.to(out.dtype).view_as(out))
+    return loss, (leaf.grad if leaf is not None else None)
+
+  def apply(self, grad_norm_sq_reduce=None, norm_exclude=()) -> None:
+    """One AdamW step on the accumulated grads.  `grad_norm_sq_reduce(t)` (e.g. an all-reduce over
+    the pipeline stages) turns the local squared grad norm into the global one for clipping;
+    `norm_exclude` names parameters counted by another stage (a tied head copy)."""
+    self._optimizer_step(grad_norm_sq_reduce, norm_exclude)
 
   def step(self, request_id, example, target, length, train: bool = True, evaluate: bool = False,
            loss: str = "length_masked_ce"):
@@ -152,10 +192,14 @@ class ShardTrainer:
     grad_in = x.grad.detach().cpu() if need_in_grad and x.grad is not None else None
     return loss_out, grad_in
 
-  def _optimizer_step(self):
+  def _optimizer_step(self, grad_norm_sq_reduce=None, norm_exclude=()):
     self.step_count += 1
     grads = {k: p.grad for k, p in self.params.items() if p.grad is not None}
-    gnorm = torch.sqrt(sum((g.float() ** 2).sum() for g in grads.values())) if grads else torch.tensor(0.0)
+    counted = [g for k, g in grads.items() if k not in norm_exclude]
+    sq = sum((g.float() ** 2).sum() for g in counted) if counted else torch.zeros((), device=self.device)
+    if grad_norm_sq_reduce is not None:
+      sq = grad_norm_sq_reduce(sq.reshape(1).float()).reshape(())
+    gnorm = torch.sqrt(sq)
     scale = float(min(1.0, self.grad_clip / (float(gnorm) + 1e-6))) if self.grad_clip else 1.0
     b1, b2 = self.betas
     for k, g in grads.items():
