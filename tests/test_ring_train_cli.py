@@ -1,0 +1,37 @@
+"""`xot train|eval --ring`: pipeline stages as local processes over the p2p ring (gloo here, RCCL on
+GPUs) with the Node path's checkpoint files and resume."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _xot(args, tmp_path):
+  env = dict(os.environ, PYTHONPATH=ROOT, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="2",
+             XOT_HOME=str(tmp_path / "home"))
+  r = subprocess.run([sys.executable, "-m", "xotorch_support_jetson_amd.main"] + args + ["--disable-tui"],
+                     capture_output=True, text=True, timeout=300, env=env, cwd=str(tmp_path))
+  assert r.returncode == 0, r.stderr[-3000:]
+  return r.stdout
+
+
+def test_ring_train_eval_resume(tmp_path):
+  ds = tmp_path / "ds"
+  ds.mkdir()
+  for split, n in (("train", 12), ("valid", 4), ("test", 4)):
+    with open(ds / f"{split}.jsonl", "w") as f:
+      for i in range(n):
+        f.write(json.dumps({"text": f"Q: select a from t{i}? A: SELECT a FROM t{i}"}) + "\n")
+  ck = tmp_path / "ck"
+  out = _xot(["train", "tiny-llama", "--ring", "--gpus", "2", "--iters", "2", "--batch-size", "4", "--micro-batch", "2",
+              "--save-every", "2", "--save-checkpoint-dir", str(ck), "--data", str(ds), "--lr", "1e-3"], tmp_path)
+  losses = [float(l.split("loss:")[1].split(",")[0]) for l in out.splitlines() if l.startswith("epoch")]
+  assert len(losses) == 2 and losses[1] < losses[0]
+  files = sorted(p.name for p in (ck / "tiny-llama").iterdir())
+  assert files == ["000-001-of-004-000002.optim.safetensors", "000-001-of-004-000002.safetensors",
+                   "002-003-of-004-000002.optim.safetensors", "002-003-of-004-000002.safetensors"]
+  ev = _xot(["eval", "tiny-llama", "--ring", "--gpus", "2", "--batch-size", "4", "--data", str(ds),
+             "--resume-checkpoint", str(ck)], tmp_path)
+  assert "resumed tiny-llama from iteration 2" in ev and "eval | loss=" in ev

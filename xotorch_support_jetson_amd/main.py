@@ -69,6 +69,9 @@ def build_parser() -> argparse.ArgumentParser:
   p.add_argument("--interface-type-filter", type=str, default=None, help="Comma separated interface types to allow")
   p.add_argument("--system-prompt", type=str, default=None, help="System prompt for the ChatGPT API")
   p.add_argument("--gpus", type=int, default=0, help="Spawn one peer process per local GPU (0 = single process)")
+  p.add_argument("--ring", action="store_true",
+                 help="train/eval: run the pipeline stages on the local GPUs over RCCL (no gRPC hops)")
+  p.add_argument("--micro-batch", type=int, default=1, help="--ring: sequences per pipeline micro-batch")
   p.add_argument("--no-api", action="store_true", help="Do not start the ChatGPT API on this peer")
   return p
 
@@ -353,6 +356,9 @@ async def async_main(args):
 def run(argv=None):
   argv = list(sys.argv[1:] if argv is None else argv)
   args = build_parser().parse_args(argv)
+  if args.ring and args.command in ("train", "eval"):
+    from .train.ring_train import run_ring
+    sys.exit(run_ring(args))
   if args.gpus and args.gpus > 1 and "XOT_PEER_RANK" not in os.environ:
     sys.exit(spawn_gpu_peers(args, argv))
   if DEBUG >= 0 and not args.no_api and os.environ.get("XOT_PEER_RANK", "0") == "0":

@@ -1,0 +1,175 @@
+"""`xot train|eval <model> --gpus N --ring`: training / evaluation with the pipeline shards on the local
+GPUs talking RCCL over xGMI (parallel/pipeline_train.py) instead of gRPC SendExample hops.
+
+Same data (`--data` JSONL dir, `batch_with_lengths`), same checkpoint files as the Node path
+(`train/checkpoint.py` names, HF tensor names, optimizer sidecars) so a ring-trained checkpoint
+loads into `xot run` on any partitioning and `--resume-checkpoint` works both ways.
+"""
+from __future__ import annotations
+
+import os
+import socket
+from pathlib import Path
+from typing import Optional
+
+import torch
+
+
+def _free_port() -> int:
+  with socket.socket() as s:
+    s.bind(("127.0.0.1", 0))
+    return s.getsockname()[1]
+
+
+def _model_dir(model_id: str) -> Optional[Path]:
+  from ..helpers import xot_home
+  from ..models import registry
+  repo = registry.get_repo(model_id, "ShardedInferenceEngine")
+  if repo is None:
+    return None
+  p = xot_home() / "downloads" / repo.replace("/", "--")
+  return p if (p / "config.json").exists() else None
+
+
+def _worker(rank: int, world: int, port: int, a: dict) -> None:
+  os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                    LOCAL_RANK=str(rank))
+  import torch.distributed as dist
+  from ..inference.tokenizers import _resolve_tokenizer
+  from ..models import registry
+  from ..models.config import load_config, preset
+  from ..models.weights import load_hf_weights, random_weights
+  from ..parallel.comm import P2PTransport, init_distributed
+  from ..parallel.pipeline_train import PipelineTrainer, TrainBatch
+  from ..topology.ring_memory_weighted_partitioning_strategy import equal_layer_shards
+  from ..train import checkpoint as ck
+  from ..train.dataset import DEFAULT_DATA, iterate_batches, load_dataset
+  from ..train.trainer import ShardTrainer
+
+  rank, world, dev = init_distributed()
+  model = a["model"]
+  mdir = _model_dir(model)
+  cfg = load_config(mdir) if mdir is not None else preset(model)
+  shard = equal_layer_shards(model, cfg.num_layers, world)[rank]
+  if mdir is not None and any(mdir.glob("*.safetensors")):
+    w = load_hf_weights(mdir, cfg, shard, dev)
+  else:
+    w = random_weights(cfg, shard, dev, seed=0)
+  if a.get("resume"):
+    files = ck.list_checkpoints(a["resume"], model)
+    if files:
+      latest = files[-1][0]
+      sd = ck._gather_tensors([p for it, s, e, n, p in files if it == latest], shard, cfg.tie_word_embeddings)
+      from ..models.weights import copy_weights_into, from_hf_state_dict
+      copy_weights_into(w, from_hf_state_dict(sd, cfg, shard, device=dev))
+      if rank == 0:
+        print(f"resumed {model} from iteration {latest}", flush=True)
+  tr = ShardTrainer(w, dev, lr=a["lr"], max_seq=4096)
+  if a.get("resume"):  # optimizer state of this exact shard, when the partitioning is unchanged
+    files = ck.list_checkpoints(a["resume"], model)
+    if files:
+      side = ck.checkpoint_path(a["resume"], shard, files[-1][0])
+      side = side.with_name(side.name.replace(".safetensors", ".optim.safetensors"))
+      if side.exists():
+        from safetensors.torch import load_file
+        tr.load_state_dict({k: v.to(dev) for k, v in load_file(str(side)).items()})
+  pt = PipelineTrainer(tr, rank, world, P2PTransport(rank, world))
+  tok = _resolve_tokenizer(mdir if mdir is not None else (registry.get_repo(model, "ShardedInferenceEngine") or "byte"),
+                           cfg.vocab_size)
+  train, valid, test = load_dataset(a["data"] or DEFAULT_DATA, lambda s: tok.encode(s))
+  bs, mb = a["batch_size"], max(1, a["micro_batch"])
+
+  def to_micro(batch):
+    x, y, ln = batch
+    out = []
+    for i in range(0, x.shape[0], mb):
+      out.append(TrainBatch(torch.from_numpy(x[i:i + mb]), torch.from_numpy(y[i:i + mb]),
+                            torch.from_numpy(ln[i:i + mb])))
+    return out
+
+  class _Shim:  # save_shard_checkpoint wants engine.runner.weights / engine.trainer
+    pass
+
+  if a["command"] == "eval":
+    tot, n = 0.0, 0
+    for batch in iterate_batches(test, bs):
+      micro = to_micro(batch)
+      loss = _eval(pt, micro)
+      tot += loss * float(batch[2].sum())
+      n += int(batch[2].sum())
+    if rank == 0:
+      print(f"eval | loss={tot / max(n, 1):.4f} tokens={n}", flush=True)
+  else:
+    step = 0
+    for epoch in range(a["iters"]):
+      tot, n = 0.0, 0
+      for batch in iterate_batches(train, bs, train=True, seed=epoch):
+        loss = pt.step(to_micro(batch))
+        tot += loss * float(batch[2].sum())
+        n += int(batch[2].sum())
+        step += 1
+      if rank == 0:
+        print(f"epoch {epoch + 1}/{a['iters']}\t| loss: {tot / max(n, 1):.4f}, tokens: {n}", flush=True)
+      if a["save_every"] > 0 and (epoch + 1) % a["save_every"] == 0 and a["save_dir"]:
+        tr.sync_to_inference()
+        shim = _Shim()
+        shim.runner = type("R", (), {"weights": w})()
+        shim.trainer = tr
+        path = ck.checkpoint_path(a["save_dir"], shard, epoch + 1)
+        ck.save_shard_checkpoint(shim, shard, path)
+        print(f"[rank {rank}] saved {path}", flush=True)
+  if world > 1:
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@torch.no_grad()
+def _eval(pt, micro) -> float:
+  """Forward-only pass of the pipeline; mean loss on the last stage, broadcast over the ring."""
+  import torch.distributed as dist
+  tr = pt.tr
+  denom = float(sum(int(b.lengths.sum()) for b in micro))
+  total = torch.zeros(1, device=pt.dev)
+  for b in micro:
+    mbs, L = b.x.shape
+    if pt.first:
+      inp = b.x.to(pt.dev)
+    else:
+      inp = torch.empty(mbs, L, pt.D, dtype=torch.bfloat16, device=pt.dev)
+      pt.t.irecv(inp, pt.prev).wait()
+    out = tr.forward(inp if pt.first else inp.to(torch.bfloat16))
+    if pt.last:
+      loss, _ = tr.loss_of(out, b.y, b.lengths, denom)
+      total += loss.float()
+    else:
+      pt.t.isend(out.contiguous(), pt.next)
+  pt.t.drain()
+  if pt.world > 1:
+    dist.all_reduce(total)
+  return float(total)
+
+
+def run_ring(args) -> int:
+  """Spawn one training process per GPU (torch.multiprocessing, RCCL process group)."""
+  import torch.multiprocessing as mp
+  n = args.gpus or max(1, torch.cuda.device_count())
+  a = {"model": args.model_name or args.default_model, "command": args.command, "data": args.data,
+       "batch_size": args.batch_size, "micro_batch": getattr(args, "micro_batch", 1), "iters": args.iters,
+       "save_every": args.save_every, "save_dir": args.save_checkpoint_dir, "resume": args.resume_checkpoint,
+       "lr": args.lr}
+  if not a["model"]:
+    print("Error: model name is required")
+    return 1
+  port = _free_port()
+  if n == 1:
+    _worker(0, 1, port, a)
+    return 0
+  ctx = mp.get_context("spawn")
+  procs = [ctx.Process(target=_worker, args=(r, n, port, a)) for r in range(n)]
+  for p in procs:
+    p.start()
+  rc = 0
+  for p in procs:
+    p.join()
+    rc = rc or (p.exitcode or 0)
+  return rc
