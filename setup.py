@@ -70,7 +70,8 @@ def ext_modules():
   kernels = HipExtension(name=f"{PKG}._C", sources=sorted(glob.glob(os.path.join(CSRC, "*.hip"))))
   runtime = Extension(  # plain C++17 + pybind11: no torch or HIP dependency on the host runtime
     name=f"{PKG}._runtime",
-    sources=sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp"))),
+    sources=sorted(f for f in glob.glob(os.path.join(CSRC, "runtime", "*.cpp"))
+                   if not os.path.basename(f).startswith("test_")),
     include_dirs=[pybind11.get_include(), os.path.join(HERE, CSRC, "runtime")],
     extra_compile_args=["-O3", "-std=c++17", "-fvisibility=hidden"],
     language="c++",
