@@ -220,3 +220,31 @@ def test_tinychat_served(tmp_path):
       await stop_all(nodes)
 
   run(main())
+
+
+def test_peer_failure_finishes_request_and_repartitions(tmp_path):
+  """A peer dies mid-ring: the request finishes at its origin instead of hanging, and the next request
+  runs on the surviving peer, which now holds every layer."""
+  async def main():
+    nodes = await make_ring(tmp_path, ["node-a", "node-b"])
+    a, b = nodes
+    try:
+      base = Shard("dummy", 0, 0, 8)
+      assert a.get_current_shard(base) == Shard("dummy", 4, 7, 8)
+      await b.stop()  # node-b (layers 0-3, the first stage) goes away
+      done = asyncio.Event()
+      a.on_token.register("t").on_next(lambda rid, toks, fin: fin and done.set())
+      await a.process_prompt(base, "x", request_id="dead")
+      await asyncio.wait_for(done.wait(), 10)
+      assert {n for n, _ in a.current_topology.all_nodes()} == {"node-a"}
+      assert a.get_current_shard(base) == Shard("dummy", 0, 7, 8)
+      done2 = asyncio.Event()
+      toks = []
+      a.on_token.register("t2").on_next(lambda rid, t, fin: rid == "alive" and (toks.extend(t), fin and done2.set()))
+      await a.process_prompt(base, "x", request_id="alive")
+      await asyncio.wait_for(done2.wait(), 10)
+      assert toks and toks[-1] == 69
+    finally:
+      await a.stop()
+
+  run(main())

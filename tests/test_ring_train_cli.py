@@ -5,12 +5,15 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _xot(args, tmp_path):
-  env = dict(os.environ, PYTHONPATH=ROOT, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="2",
-             XOT_HOME=str(tmp_path / "home"))
+def _xot(args, tmp_path, cpu=True):
+  env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2", XOT_HOME=str(tmp_path / "home"))
+  if cpu:
+    env.update(CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
   r = subprocess.run([sys.executable, "-m", "xotorch_support_jetson_amd.main"] + args + ["--disable-tui"],
                      capture_output=True, text=True, timeout=300, env=env, cwd=str(tmp_path))
   assert r.returncode == 0, r.stderr[-3000:]
@@ -35,3 +38,18 @@ def test_ring_train_eval_resume(tmp_path):
   ev = _xot(["eval", "tiny-llama", "--ring", "--gpus", "2", "--batch-size", "4", "--data", str(ds),
              "--resume-checkpoint", str(ck)], tmp_path)
   assert "resumed tiny-llama from iteration 2" in ev and "eval | loss=" in ev
+
+
+@pytest.mark.gpu
+def test_ring_train_gpu_single(gpu, tmp_path):
+  """The same CLI on one MI355X (world 1: the HIP training kernels + fused AdamW)."""
+  ds = tmp_path / "ds"
+  ds.mkdir()
+  for split, n in (("train", 8), ("valid", 2), ("test", 2)):
+    with open(ds / f"{split}.jsonl", "w") as f:
+      for i in range(n):
+        f.write(json.dumps({"text": f"Q: select a from t{i}? A: SELECT a FROM t{i}"}) + "\n")
+  out = _xot(["train", "tiny-llama", "--ring", "--gpus", "1", "--iters", "3", "--batch-size", "4", "--data", str(ds),
+              "--lr", "1e-3"], tmp_path, cpu=False)
+  losses = [float(l.split("loss:")[1].split(",")[0]) for l in out.splitlines() if l.startswith("epoch")]
+  assert len(losses) == 3 and losses[-1] < losses[0]

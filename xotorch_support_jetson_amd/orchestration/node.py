@@ -363,7 +363,11 @@ class Node:
     next_shard = self.get_current_shard(base_shard, target_index)
     if target_id == self.id:
       return await self.process_prompt(next_shard, prompt, request_id, inference_state)
-    await self._peer(target_id).send_prompt(next_shard, prompt, request_id=request_id, inference_state=inference_state)
+    try:
+      await self._peer(target_id).send_prompt(next_shard, prompt, request_id=request_id,
+                                              inference_state=inference_state)
+    except Exception as e:
+      await self._fail_request(request_id, target_id, e)
 
   async def forward_tensor(self, base_shard: Shard, tensor, request_id: str, target_index: int,
                            inference_state: Optional[dict] = None):
@@ -376,8 +380,39 @@ class Node:
         await self._peer(target_id).send_tensor(next_shard, tensor, request_id=request_id,
                                                 inference_state=inference_state)
     except Exception as e:
-      print(f"Error forwarding tensor for {request_id} to {target_id}: {e}")
-      self.outstanding_requests.pop(request_id, None)
+      await self._fail_request(request_id, target_id, e)
+
+  async def _fail_request(self, request_id: str, peer_id: str, err: Exception) -> None:
+    """A hop to `peer_id` failed (peer gone or unreachable): the request cannot continue because that
+    peer holds part of its KV cache.  Finish it at its origin (the API answers with the tokens so far
+    instead of hanging until its timeout), free its pages on the live peers, and refresh peers and
+    topology so the next request is re-partitioned over the peers that are still up (the reference
+    logs the error and leaves the request hanging, node.py:424-443)."""
+    print(f"Error forwarding {request_id} to {peer_id}: {err}; finishing the request and re-partitioning")
+    self.outstanding_requests.pop(request_id, None)
+    origin = self.request_origin.get(request_id) or self.id
+    buf = self.buffered_token_output.get(request_id, ([], False))
+    self.buffered_token_output[request_id] = (buf[0], True)
+    if origin == self.id:
+      self.trigger_on_token_callbacks(request_id, [], True)
+    else:
+      try:
+        await asyncio.wait_for(self._peer(origin).send_result(request_id, [], True), timeout=5.0)
+      except Exception:
+        pass
+    dead = [p for p in self.peers if p.id() == peer_id]
+    self.peers = [p for p in self.peers if p.id() != peer_id]
+    for p in dead:
+      try:
+        await asyncio.wait_for(p.disconnect(), timeout=2.0)
+      except Exception:
+        pass
+    try:
+      await self.collect_topology(set())
+    except Exception:
+      pass
+    asyncio.create_task(self.broadcast_opaque_status(request_id, json.dumps(
+      {"type": "node_status", "node_id": self.id, "status": "request_finished", "request_id": request_id})))
 
   def _peer(self, node_id: str) -> PeerHandle:
     for p in self.peers:
@@ -452,21 +487,24 @@ class Node:
   async def collect_topology(self, visited: set, max_depth: int = 4) -> Topology:
     next_topology = Topology()
     next_topology.update_node(self.id, self.device_capabilities)
-    for p in self.peers:
-      next_topology.update_node(p.id(), p.device_capabilities())
-      next_topology.add_edge(self.id, p.id(), p.description())
     visited = set(visited) | {self.id}
-    if max_depth > 0:
-      for p in self.peers:
-        if p.id() in visited:
-          continue
+    for p in self.peers:
+      if max_depth > 0 and p.id() not in visited:
         try:
           other = await asyncio.wait_for(p.collect_topology(visited | {p.id()}, max_depth - 1), timeout=5.0)
-          next_topology.merge(p.id(), other)
-          visited.add(p.id())
         except Exception as e:
+          # an unreachable peer leaves the topology (and so the partitioning) until discovery and a
+          # successful collection bring it back
           if DEBUG >= 2:
             print(f"Error collecting topology from {p.id()}: {e}")
+          continue
+        next_topology.update_node(p.id(), p.device_capabilities())
+        next_topology.add_edge(self.id, p.id(), p.description())
+        next_topology.merge(p.id(), other)
+        visited.add(p.id())
+      else:
+        next_topology.update_node(p.id(), p.device_capabilities())
+        next_topology.add_edge(self.id, p.id(), p.description())
     next_topology.active_node_id = self.topology.active_node_id
     self.topology = next_topology
     if self.topology_viz:
