@@ -66,7 +66,7 @@ def test_training_gpu_matches_cpu(gpu):
         await e.train("t", a, x, g, ln, loss="back_gradient")
         losses.append(l)
       logits, _ = await e2.infer_tensor("q", b, (await e.infer_tensor("q", a, x[:1]))[0])
-      out[dev] = (losses, np.asarray(logits, np.float32))
+      out[dev] = (losses, np.asarray(torch.as_tensor(logits).float().cpu(), np.float32))
     lc, lg = out["cpu"][0], out["cuda:0"][0]
     assert np.allclose(lc, lg, rtol=2e-2), (lc, lg)
     assert lg[-1] < lg[0]

@@ -248,3 +248,35 @@ def test_peer_failure_finishes_request_and_repartitions(tmp_path):
       await a.stop()
 
   run(main())
+
+
+def test_api_concurrent_requests_real_engine(tmp_path):
+  """Concurrent chat completions on one peer with the real engine (tiny synthetic Llama on CPU): all
+  complete, with per-request max_tokens, through the continuously batched engine."""
+  import torch
+  from aiohttp.test_utils import TestClient, TestServer
+
+  from xotorch_support_jetson_amd.api.chatgpt_api import ChatGPTAPI
+  from xotorch_support_jetson_amd.inference.sharded_engine import ShardedInferenceEngine
+
+  async def main():
+    eng = ShardedInferenceEngine(NoopShardDownloader(), device=torch.device("cpu"))
+    nodes = await make_ring(tmp_path, ["solo3"], engines=[eng])
+    api = ChatGPTAPI(nodes[0], "ShardedInferenceEngine", response_timeout=60, default_model="tiny-llama")
+    client = TestClient(TestServer(api.app))
+    await client.start_server()
+    try:
+      async def ask(i):
+        r = await client.post("/v1/chat/completions", json={
+          "model": "tiny-llama", "messages": [{"role": "user", "content": f"hello {i}"}], "max_tokens": 3 + i,
+          "temperature": 0.0})
+        assert r.status == 200, await r.text()
+        return await r.json()
+      outs = await asyncio.gather(*(ask(i) for i in range(4)))
+      for i, d in enumerate(outs):
+        assert d["usage"]["completion_tokens"] <= 3 + i
+    finally:
+      await client.close()
+      await stop_all(nodes)
+
+  run(main())

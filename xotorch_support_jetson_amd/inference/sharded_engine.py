@@ -57,6 +57,8 @@ class ShardedInferenceEngine(InferenceEngine):
     self._lock = asyncio.Lock()
     self.trainer = None
     self.lr = float(os.environ.get("XOT_LR", "1e-5"))  # `xot train --lr` sets this
+    self._queue: list = []  # (request id, shard, input, future) waiting for the next batched step
+    self._draining = False
 
   # ------------------------------------------------------------------ helpers
   async def _run(self, fn, *args):
@@ -84,33 +86,75 @@ class ShardedInferenceEngine(InferenceEngine):
 
     return await self._run(_sample)
 
-  # ------------------------------------------------------------------ forward
+  # ------------------------------------------------------------------ forward (continuously batched)
   async def infer_tensor(self, request_id: str, shard: Shard, input_data,
                          inference_state: Optional[dict] = None) -> Tuple[object, Optional[dict]]:
+    """Queue one request's step; concurrent requests on this peer run as ONE batched forward
+    (prefill chunks and decode tokens mixed, varlen attention; a pure-decode batch replays the
+    HIP graph of its batch bucket).  The reference runs every request on its own, one token at a
+    time, through a single global KV cache (sharded_inference_engine.py:230-370)."""
     await self.ensure_shard(shard)
+    fut = asyncio.get_running_loop().create_future()
+    self._queue.append((request_id, shard, input_data, fut))
+    if not self._draining:
+      self._draining = True
+      asyncio.create_task(self._drain())
+    return await fut
 
-    def _infer():
-      if self.trainer is not None and self.trainer.dirty:
-        self.trainer.sync_to_inference()  # serve the weights training just produced
-      x = input_data if isinstance(input_data, torch.Tensor) else torch.as_tensor(np.asarray(input_data))
+  async def _drain(self):
+    try:
+      while self._queue:
+        cap = self.runner.max_batch if self.runner is not None else 1
+        batch, self._queue = self._queue[:cap], self._queue[cap:]
+        ok = [it for it in batch if it[1] == self.shard]
+        for it in batch:
+          if it[1] != self.shard and not it[3].done():
+            it[3].set_exception(RuntimeError(f"shard {it[1]} is not loaded on this peer (have {self.shard})"))
+        if not ok:
+          continue
+        try:
+          results = await self._run(self._infer_batch, [(rid, x) for rid, _, x, _ in ok])
+          for (_, _, _, fut), r in zip(ok, results):
+            if not fut.done():
+              fut.set_result(r)
+        except Exception as e:  # noqa: BLE001 - delivered to every waiter of the batch
+          for _, _, _, fut in ok:
+            if not fut.done():
+              fut.set_exception(e)
+    finally:
+      self._draining = False
+
+  def _infer_batch(self, items):
+    if self.trainer is not None and self.trainer.dirty:
+      self.trainer.sync_to_inference()  # serve the weights training just produced
+    rids, qlens, xs = [], [], []
+    for rid, inp in items:
+      x = inp if isinstance(inp, torch.Tensor) else torch.as_tensor(np.asarray(inp))
       if x.dim() == 3:  # hidden [1, L, D]
         L = x.shape[1]
-        xin = x.reshape(L, x.shape[2]).to(torch.bfloat16)
+        xs.append(x.reshape(L, x.shape[2]).to(torch.bfloat16))
       else:  # token ids [1, L]
-        xin = x.reshape(-1).to(torch.int32)
-        L = xin.numel()
-      try:
-        out = self.runner.forward([request_id], [L], xin)
-      except torch.cuda.OutOfMemoryError:
-        self.clear_model()
-        raise
-      n_past = self.runner.num_tokens(request_id)
-      state = {"n_past": n_past}
-      if self.shard.is_last_layer():
-        return out[-1:].float().cpu().numpy(), state  # [1, V] logits of the last token
-      return out.reshape(1, L, -1).cpu(), state  # bf16 hidden [1, L, D]
-
-    return await self._run(_infer)
+        xs.append(x.reshape(-1).to(torch.int32))
+        L = xs[-1].numel()
+      rids.append(rid)
+      qlens.append(L)
+    try:
+      out = self.runner.forward(rids, qlens, torch.cat(xs))
+    except torch.cuda.OutOfMemoryError:
+      self.clear_model()
+      raise
+    res = []
+    if self.shard.is_last_layer():
+      # [B, V] fp32 logits of each request's last token; they stay on the device for the sampler
+      for i, rid in enumerate(rids):
+        res.append((out[i:i + 1], {"n_past": self.runner.num_tokens(rid)}))
+      return res
+    off = 0
+    outc = out.cpu()
+    for rid, L in zip(rids, qlens):
+      res.append((outc[off:off + L].reshape(1, L, -1), {"n_past": self.runner.num_tokens(rid)}))
+      off += L
+    return res
 
   async def finish_request(self, request_id: str) -> None:
     if self.runner is not None:
