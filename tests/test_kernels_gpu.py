@@ -225,7 +225,7 @@ def test_cross_entropy_and_adamw(gpu):
 @pytest.mark.parametrize("M", [1, 5, 16, 33, 64, 100, 128, 200, 256, 300, 513])
 @pytest.mark.parametrize("epi,ntw,splits", [("none", 1, 1), ("none", 2, 1), ("none", 1, 4), ("resid", 1, 2),
                                             ("silu", 2, 1), ("silu", 2, 2), ("none", 4, 1), ("silu", 4, 2),
-                                            ("resid", 4, 2)])
+                                            ("resid", 4, 2), ("resid", 2, 8), ("silu", 2, 8)])
 def test_gemm_stream(gpu, M, epi, ntw, splits):
   from xotorch_support_jetson_amd.ops._ext import require
   torch.manual_seed(0)
@@ -248,6 +248,13 @@ def test_gemm_stream(gpu, M, epi, ntw, splits):
     y = torch.empty(M, N, device=gpu, dtype=torch.float32)
   require().gemm_stream(x, w, y, b, r if epi == "resid" else None, ws, K.EPI[epi], ntw, splits, False)
   assert rel_err(y, ref) < 1e-2
+  if splits > 1:  # in-launch combine (tickets), twice: the counters must come back to zero
+    tk = torch.zeros(4096, dtype=torch.int32, device=gpu)
+    for _ in range(2):
+      y.zero_()
+      require().gemm_stream(x, w, y, b, r if epi == "resid" else None, ws, K.EPI[epi], ntw, splits, False, tk)
+      assert rel_err(y, ref) < 1e-2
+    assert int(tk.abs().sum()) == 0
   if True:  # pre-shuffled layout, every M (M > 128 runs the XCD-paired 128-row blocks)
     from xotorch_support_jetson_amd.ops.weights_layout import shuffle_for_stream
     y2 = torch.empty_like(y)

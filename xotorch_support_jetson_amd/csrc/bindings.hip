@@ -192,7 +192,7 @@ void gemm(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const c10::op
 // an fp32 workspace of >= splits*M*N floats).  ntw: 16-row n-tiles per wave (1 or 2).
 void gemm_stream(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const c10::optional<at::Tensor>& bias,
                  const c10::optional<at::Tensor>& res, const c10::optional<at::Tensor>& ws, int64_t epi, int64_t ntw,
-                 int64_t splits, bool wshuf) {
+                 int64_t splits, bool wshuf, const c10::optional<at::Tensor>& tickets) {
   CHECK_BF16(x);
   CHECK_BF16(w);
   CHECK_GPU(y);
@@ -226,10 +226,19 @@ void gemm_stream(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const 
     ws_elems = ws->numel();
   }
   if (splits > 1 && epi == 1) XCHECK(res->data_ptr() != nullptr, "gemm_stream: res");
+  int* tk = nullptr;
+  long tk_n = 0;
+  if (tickets.has_value()) {  // zero-initialised int32 counters for the in-launch split-K combine
+    CHECK_GPU((*tickets));
+    CHECK_DT((*tickets), at::kInt);
+    XCHECK(tickets->is_contiguous(), "gemm_stream: tickets must be contiguous");
+    tk = tickets->data_ptr<int>();
+    tk_n = tickets->numel();
+  }
   const int rc = xot::launch_gemm_stream(bf(x), (int)x.stride(0), bf(w), (int)K, bf_opt(bias),
                                          epi == 1 ? bf(*res) : nullptr, (int)ldr, y.data_ptr(), (int)y.stride(0), f32,
                                          (int)epi, wsp, ws_elems, (int)M, (int)N, (int)K, (int)ntw, (int)splits,
-                                         wshuf, cur_stream());
+                                         wshuf, tk, tk_n, cur_stream());
   XCHECK(rc == 0, "gemm_stream: unsupported shape M=", M, " N=", N, " K=", K, " epi=", epi, " ntw=", ntw,
          " splits=", splits);
 }
@@ -427,7 +436,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("rope_kv_write", &rope_kv_write);
   m.def("rope_apply", &rope_apply);
   m.def("gemm", &gemm);
-  m.def("gemm_stream", &gemm_stream);
+  m.def("gemm_stream", &gemm_stream, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("bias"), py::arg("res"),
+        py::arg("ws"), py::arg("epi"), py::arg("ntw"), py::arg("splits"), py::arg("wshuf"),
+        py::arg("tickets") = py::none());
   m.def("gemm_moe", &gemm_moe);
   m.def("moe_route", &moe_route);
   m.def("moe_combine", &moe_combine);

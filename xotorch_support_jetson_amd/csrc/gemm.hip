@@ -190,7 +190,74 @@ int launch_gemm_skinny(const uint16_t* X, int ldx, const uint16_t* W, int ldw, c
 //   W rows       : streamed once, straight to VGPRs, two chunks in flight (prefetch depth 2)
 // MFMA k-order is permuted per lane group (group g owns k in [8*KS*g, 8*KS*(g+1)) of the chunk)
 // so each lane reads 16*KS contiguous bytes of its weight row per chunk.
-// SPLIT: fp32 partial slabs ws[blockIdx.y][M][N], finished by splitk_reduce_kernel (epilogue there).
+// Sum the S fp32 slabs of one output row at 8 output columns [o, o+8) and apply the epilogue.
+// wsrow = slab 0 of this row (slabs are sstride floats apart); rrow / yrow = this row of R / Y.
+template <int EPI, bool OUT_F32>
+__device__ __forceinline__ void splitk_out8(const float* __restrict__ wsrow, size_t sstride, int S, int o,
+                                            const uint16_t* __restrict__ bias, const uint16_t* __restrict__ rrow,
+                                            void* __restrict__ yrow) {
+  float v[8];
+  if constexpr (EPI == EPI_SILU) {
+    const int j = o >> 4, w = o & 15;
+    float gs[8], us[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) gs[e] = us[e] = 0.f;
+    for (int s = 0; s < S; ++s) {
+      const float* row = wsrow + s * sstride;
+      const f32x4 g0 = *reinterpret_cast<const f32x4*>(row + 32 * j + w);
+      const f32x4 g1 = *reinterpret_cast<const f32x4*>(row + 32 * j + w + 4);
+      const f32x4 u0 = *reinterpret_cast<const f32x4*>(row + 32 * j + 16 + w);
+      const f32x4 u1 = *reinterpret_cast<const f32x4*>(row + 32 * j + 16 + w + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        gs[e] += g0[e];
+        gs[e + 4] += g1[e];
+        us[e] += u0[e];
+        us[e + 4] += u1[e];
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float bg = bias ? bf2f(bias[32 * j + w + e]) : 0.f, bu = bias ? bf2f(bias[32 * j + 16 + w + e]) : 0.f;
+      v[e] = silu(gs[e] + bg) * (us[e] + bu);
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = 0.f;
+    for (int s = 0; s < S; ++s) {
+      const float* row = wsrow + s * sstride + o;
+      const f32x4 a = *reinterpret_cast<const f32x4*>(row), b = *reinterpret_cast<const f32x4*>(row + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] += a[e];
+        v[e + 4] += b[e];
+      }
+    }
+    if (bias != nullptr) {
+      const s16x8 bb = ld16(bias + o);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += bf2f(bb[e]);
+    }
+    if constexpr (EPI == EPI_RESID) {
+      const s16x8 rr = ld16(rrow + o);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += bf2f(rr[e]);
+    }
+  }
+  if constexpr (OUT_F32) {
+    float* y = reinterpret_cast<float*>(yrow) + o;
+    *reinterpret_cast<f32x4*>(y) = f32x4{v[0], v[1], v[2], v[3]};
+    *reinterpret_cast<f32x4*>(y + 4) = f32x4{v[4], v[5], v[6], v[7]};
+  } else {
+    s16x8 out;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) out[e] = (short)f2bf(v[e]);
+    st16(reinterpret_cast<uint16_t*>(yrow) + o, out);
+  }
+}
+
+// SPLIT: fp32 partial slabs ws[blockIdx.y][M][N], finished by splitk_reduce_kernel or -- with tickets -- by the
+// last-arriving workgroup of each tile inside the same launch (epilogue there).
 // MOE = 1 / 2: grouped (mixture-of-experts) GEMM.  blockIdx.z = expert e with weight W[e]
 // ([E][N][K], same layout per expert) and rows moe_off[e] .. moe_off[e+1] of the expert-sorted slot
 // order; MOE = 1 reads A in slot order, MOE = 2 gathers A row moe_gather[slot] (token rows).  Output
@@ -204,7 +271,8 @@ __global__ __launch_bounds__(256, OCC) void gemm_stream_kernel(const uint16_t* _
                                                              void* __restrict__ Yv, int ldy,
                                                              float* __restrict__ ws, int M, int N, int kper,
                                                              int mblocks, const int* __restrict__ moe_off,
-                                                             const int* __restrict__ moe_gather) {
+                                                             const int* __restrict__ moe_gather,
+                                                             int* __restrict__ tickets) {
   constexpr int KC = 32 * KS;
   constexpr int CPR = KC / 8;  // 16-B chunks per row per k-chunk
   constexpr int NTH = 256;
@@ -376,6 +444,41 @@ __global__ __launch_bounds__(256, OCC) void gemm_stream_kernel(const uint16_t* _
           const int m = wrow + 16 * i + 4 * g + r;
           if (m < M) slab[(size_t)m * N + n0 + 16 * j + c] = acc[i][j][r];
         }
+    if (tickets != nullptr) {
+      // In-launch combine: the split that arrives last for this (column tile, row block) sums every
+      // slab of the tile and applies the epilogue (no second kernel).  Publish: stores drained,
+      // agent-scope release, relaxed ticket; reducer: agent-scope acquire before reading the slabs.
+      // The reducer resets the ticket, so the zero-initialised counters stay valid across launches
+      // and HIP-graph replays.
+      const int S = gridDim.y, tile = bt * mblocks + mb;
+      int* flag = reinterpret_cast<int*>(xs_raw);  // LDS is free again after the last compute phase
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int t = __hip_atomic_fetch_add(&tickets[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = t == S - 1;
+        if (last) {
+          __hip_atomic_store(&tickets[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        *flag = last;
+      }
+      __syncthreads();
+      if (*flag == 0) return;
+      const int c0 = bt * (64 * NTW);  // first weight row (output column before SiLU pairing)
+      constexpr int OCOLS = EPI == EPI_SILU ? 32 * NTW : 64 * NTW;
+      const int oc0 = EPI == EPI_SILU ? c0 / 2 : c0;
+      for (int q = tid; q < M * (OCOLS / 8); q += NTH) {
+        const int m = q / (OCOLS / 8), o = oc0 + (q % (OCOLS / 8)) * 8;
+        void* yrow = OUT_F32 ? (void*)(reinterpret_cast<float*>(Yv) + (size_t)m * ldy)
+                             : (void*)(reinterpret_cast<uint16_t*>(Yv) + (size_t)m * ldy);
+        splitk_out8<EPI, OUT_F32>(ws + ((size_t)m_base + m) * N, (size_t)Mtot * N, S, o, bias,
+                                  EPI == EPI_RESID ? R + (size_t)m * ldr : nullptr, yrow);
+      }
+    }
   } else if constexpr (EPI == EPI_SILU && NTW >= 2) {
 #pragma unroll
     for (int p = 0; p < NTW / 2; ++p) {  // pair (gate tile 2p, up tile 2p+1) -> 16 output columns
@@ -433,71 +536,17 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   for (long t = blockIdx.x * 256L + threadIdx.x; t < total; t += (long)gridDim.x * 256) {
     const int m = (int)(t / (ncol / 8));
     const int o = (int)(t % (ncol / 8)) * 8;
-    float v[8];
-    if constexpr (EPI == EPI_SILU) {
-      const int j = o >> 4, w = o & 15;
-      float gs[8], us[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) gs[e] = us[e] = 0.f;
-      for (int s = 0; s < S; ++s) {
-        const float* row = ws + ((size_t)s * M + m) * N;
-        const f32x4 g0 = *reinterpret_cast<const f32x4*>(row + 32 * j + w);
-        const f32x4 g1 = *reinterpret_cast<const f32x4*>(row + 32 * j + w + 4);
-        const f32x4 u0 = *reinterpret_cast<const f32x4*>(row + 32 * j + 16 + w);
-        const f32x4 u1 = *reinterpret_cast<const f32x4*>(row + 32 * j + 16 + w + 4);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          gs[e] += g0[e];
-          gs[e + 4] += g1[e];
-          us[e] += u0[e];
-          us[e + 4] += u1[e];
-        }
-      }
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float bg = bias ? bf2f(bias[32 * j + w + e]) : 0.f, bu = bias ? bf2f(bias[32 * j + 16 + w + e]) : 0.f;
-        v[e] = silu(gs[e] + bg) * (us[e] + bu);
-      }
-    } else {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = 0.f;
-      for (int s = 0; s < S; ++s) {
-        const float* row = ws + ((size_t)s * M + m) * N + o;
-        const f32x4 a = *reinterpret_cast<const f32x4*>(row), b = *reinterpret_cast<const f32x4*>(row + 4);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          v[e] += a[e];
-          v[e + 4] += b[e];
-        }
-      }
-      if (bias != nullptr) {
-        const s16x8 bb = ld16(bias + o);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] += bf2f(bb[e]);
-      }
-      if constexpr (EPI == EPI_RESID) {
-        const s16x8 rr = ld16(R + (size_t)m * ldr + o);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] += bf2f(rr[e]);
-      }
-    }
-    if constexpr (OUT_F32) {
-      float* y = reinterpret_cast<float*>(Yv) + (size_t)m * ldy + o;
-      *reinterpret_cast<f32x4*>(y) = f32x4{v[0], v[1], v[2], v[3]};
-      *reinterpret_cast<f32x4*>(y + 4) = f32x4{v[4], v[5], v[6], v[7]};
-    } else {
-      s16x8 out;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) out[e] = (short)f2bf(v[e]);
-      st16(reinterpret_cast<uint16_t*>(Yv) + (size_t)m * ldy + o, out);
-    }
+    void* yrow = OUT_F32 ? (void*)(reinterpret_cast<float*>(Yv) + (size_t)m * ldy)
+                         : (void*)(reinterpret_cast<uint16_t*>(Yv) + (size_t)m * ldy);
+    splitk_out8<EPI, OUT_F32>(ws + (size_t)m * N, (size_t)M * N, S, o, bias,
+                              EPI == EPI_RESID ? R + (size_t)m * ldr : nullptr, yrow);
   }
 }
 
 template <int MT, int NTW, int KS, int EPI, bool F32, bool WSH>
 static void stream_launch(const uint16_t* X, int ldx, const uint16_t* W, int ldw, const uint16_t* bias,
                           const uint16_t* R, int ldr, void* Y, int ldy, float* ws, int M, int N, int K, int S,
-                          hipStream_t st) {
+                          int* tickets, hipStream_t st) {
   // occupancy request: 2 workgroups/CU while the register budget allows it
   constexpr int OCC = (MT * NTW >= 32) ? 1 : 2;
   constexpr int SMEM = 2 * 16 * MT * 32 * KS * 2;
@@ -511,7 +560,8 @@ static void stream_launch(const uint16_t* X, int ldx, const uint16_t* W, int ldw
                           hipSuccess);
       (void)attr;
     }
-    kern<<<grid, 256, SMEM, st>>>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, nullptr, M, N, kper, mblocks, nullptr, nullptr);
+    kern<<<grid, 256, SMEM, st>>>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, nullptr, M, N, kper, mblocks, nullptr, nullptr,
+                                  nullptr);
   } else {
     auto kern = gemm_stream_kernel<MT, NTW, KS, EPI, F32, true, WSH, OCC, 0>;
     if constexpr (SMEM > 65536) {
@@ -519,7 +569,9 @@ static void stream_launch(const uint16_t* X, int ldx, const uint16_t* W, int ldw
                           hipSuccess);
       (void)attr;
     }
-    kern<<<grid, 256, SMEM, st>>>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, M, N, kper, mblocks, nullptr, nullptr);
+    kern<<<grid, 256, SMEM, st>>>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, M, N, kper, mblocks, nullptr, nullptr,
+                                  tickets);
+    if (tickets != nullptr) return;  // combined in-launch
     const int ncol = EPI == EPI_SILU ? N / 2 : N;
     long chunks = (long)M * (ncol / 8);
     int blocks = (int)((chunks + 255) / 256);
@@ -531,7 +583,7 @@ static void stream_launch(const uint16_t* X, int ldx, const uint16_t* W, int ldw
 template <int EPI, bool F32>
 static int stream_dispatch(const uint16_t* X, int ldx, const uint16_t* W, int ldw, const uint16_t* bias,
                            const uint16_t* R, int ldr, void* Y, int ldy, float* ws, long ws_elems, int M, int N,
-                           int K, int ntw, int S, bool wshuf, hipStream_t st) {
+                           int K, int ntw, int S, bool wshuf, int* tickets, long tickets_n, hipStream_t st) {
   if (EPI == EPI_SILU && ntw == 1) ntw = 2;
   if (ntw != 1 && ntw != 2 && ntw != 4) return -1;
   const int mt = (M + 15) / 16;
@@ -540,16 +592,18 @@ static int stream_dispatch(const uint16_t* X, int ldx, const uint16_t* W, int ld
   const int KS = 4;
   if (K % (S * 64 * KS) != 0) return -1;  // an even number (>= 2) of k-chunks per workgroup
   if (S > 1 && (ws == nullptr || ws_elems < (long)S * M * N)) return -1;
+  // in-launch split-K combine needs one ticket per (column tile, 128-row block)
+  if (S == 1 || tickets_n < (long)(N / (64 * ntw)) * ((M + 127) / 128)) tickets = nullptr;
   if (EPI == EPI_SILU && N % 32 != 0) return -1;
   if (wshuf && (KS != 4 || K % 128 != 0)) return -1;
 #define XOT_ST2(MTV, KSV, WSH)                                                                              \
   do {                                                                                                      \
     if (ntw == 1 && EPI != EPI_SILU)                                                                        \
-      stream_launch<MTV, 1, KSV, EPI, F32, WSH>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, M, N, K, S, st);  \
+      stream_launch<MTV, 1, KSV, EPI, F32, WSH>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, M, N, K, S, tickets, st);  \
     else if (ntw == 4 && MTV >= 4 && MTV <= 8)                                                                    \
-      stream_launch<MTV, 4, KSV, EPI, F32, WSH>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, M, N, K, S, st);  \
+      stream_launch<MTV, 4, KSV, EPI, F32, WSH>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, M, N, K, S, tickets, st);  \
     else                                                                                                    \
-      stream_launch<MTV, 2, KSV, EPI, F32, WSH>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, M, N, K, S, st);  \
+      stream_launch<MTV, 2, KSV, EPI, F32, WSH>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, M, N, K, S, tickets, st);  \
     return 0;                                                                                               \
   } while (0)
 #define XOT_ST(MTV, KSV)                  \
@@ -580,7 +634,7 @@ static void moe_launch(const uint16_t* X, int ldx, const uint16_t* W, void* Y, i
   const int mblocks = (max_rows + 16 * MT - 1) / (16 * MT);
   dim3 grid(N / (64 * NTW) * mblocks, 1, E);
   gemm_stream_kernel<MT, NTW, KS, EPI, F32, false, WSH, OCC, MOE><<<grid, 256, SMEM, st>>>(
-      X, ldx, W, K, nullptr, nullptr, 0, Y, ldy, nullptr, max_rows, N, K, mblocks, off, gather);
+      X, ldx, W, K, nullptr, nullptr, 0, Y, ldy, nullptr, max_rows, N, K, mblocks, off, gather, nullptr);
 }
 
 template <int EPI, bool F32, bool WSH, int MOE>
@@ -620,15 +674,16 @@ int launch_gemm_moe(const uint16_t* X, int ldx, const uint16_t* W, void* Y, int 
 
 int launch_gemm_stream(const uint16_t* X, int ldx, const uint16_t* W, int ldw, const uint16_t* bias,
                        const uint16_t* R, int ldr, void* Y, int ldy, bool out_f32, int epi, float* ws, long ws_elems,
-                       int M, int N, int K, int ntw, int S, bool wshuf, hipStream_t s) {
+                       int M, int N, int K, int ntw, int S, bool wshuf, int* tickets, long tickets_n,
+                       hipStream_t s) {
   if (M <= 0) return 0;
   if (epi == EPI_SILU)
-    return out_f32 ? stream_dispatch<EPI_SILU, true>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, ntw, S, wshuf, s)
-                   : stream_dispatch<EPI_SILU, false>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, ntw, S, wshuf, s);
+    return out_f32 ? stream_dispatch<EPI_SILU, true>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, ntw, S, wshuf, tickets, tickets_n, s)
+                   : stream_dispatch<EPI_SILU, false>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, ntw, S, wshuf, tickets, tickets_n, s);
   if (epi == EPI_RESID)
-    return out_f32 ? -1 : stream_dispatch<EPI_RESID, false>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, ntw, S, wshuf, s);
-  return out_f32 ? stream_dispatch<EPI_NONE, true>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, ntw, S, wshuf, s)
-                 : stream_dispatch<EPI_NONE, false>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, ntw, S, wshuf, s);
+    return out_f32 ? -1 : stream_dispatch<EPI_RESID, false>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, ntw, S, wshuf, tickets, tickets_n, s);
+  return out_f32 ? stream_dispatch<EPI_NONE, true>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, ntw, S, wshuf, tickets, tickets_n, s)
+                 : stream_dispatch<EPI_NONE, false>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, ntw, S, wshuf, tickets, tickets_n, s);
 }
 
 // ------------------------------------------------------------------------------------ tiled

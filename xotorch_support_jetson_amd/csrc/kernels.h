@@ -27,7 +27,8 @@ int launch_gemm_skinny(const uint16_t* X, int ldx, const uint16_t* W, int ldw, c
                        int nt, hipStream_t s);
 int launch_gemm_stream(const uint16_t* X, int ldx, const uint16_t* W, int ldw, const uint16_t* bias,
                        const uint16_t* R, int ldr, void* Y, int ldy, bool out_f32, int epi, float* ws, long ws_elems,
-                       int M, int N, int K, int ntw, int S, bool wshuf, hipStream_t s);
+                       int M, int N, int K, int ntw, int S, bool wshuf, int* tickets, long tickets_n,
+                       hipStream_t s);
 // grouped GEMM over experts: rows of expert e are off[e]..off[e+1] (slot order), W is [E][N][K]
 int launch_gemm_moe(const uint16_t* X, int ldx, const uint16_t* W, void* Y, int ldy, bool out_f32, int epi,
                     const int* off, const int* gather, int E, int max_rows, int N, int K, bool wshuf,

@@ -30,6 +30,12 @@ from ._ext import require
 from .weights_layout import can_shuffle, shuffle_for_stream, unshuffle_from_stream
 
 
+# XOT_SPLITK_IN_LAUNCH=1: split-K partial sums combined by the last-arriving workgroup of each tile
+# (one launch instead of GEMM + reduce kernel).  Off by default: measured no faster at batch 1
+# (graph launches of the small reduce kernel are cheap) and ~3 % slower at batch 512 (the reducing
+# workgroup is a serial tail on one CU).
+SPLITK_IN_LAUNCH = os.environ.get("XOT_SPLITK_IN_LAUNCH", "0") == "1"
+
 # largest M served by the stream GEMM (128-row blocks of one column tile share its weight reads through
 # L2); above it: unshuffled copy + hipBLASLt
 STREAM_MAX_M = int(os.environ.get("XOT_STREAM_MAX_M", "512"))
@@ -64,6 +70,7 @@ class _Scratch:
   def __init__(self):
     self.ws: Dict[int, torch.Tensor] = {}
     self.dense: Dict[int, torch.Tensor] = {}
+    self.tk: Dict[int, torch.Tensor] = {}
 
   def splitk(self, device, n: int) -> torch.Tensor:
     idx = device.index or 0
@@ -73,6 +80,18 @@ class _Scratch:
         raise RuntimeError("split-K workspace must be sized before graph capture")
       t = torch.empty(max(n, 1 << 20), dtype=torch.float32, device=device)
       self.ws[idx] = t
+    return t
+
+  def tickets(self, device, n: int) -> torch.Tensor:
+    """Zero-initialised int32 tile counters of the in-launch split-K combine (the last arriver of a
+    tile resets its counter, so the buffer stays zeroed between launches and graph replays)."""
+    idx = device.index or 0
+    t = self.tk.get(idx)
+    if t is None or t.numel() < n:
+      if torch.cuda.is_current_stream_capturing():
+        raise RuntimeError("split-K tickets must be sized before graph capture")
+      t = torch.zeros(max(n, 1 << 16), dtype=torch.int32, device=device)
+      self.tk[idx] = t
     return t
 
   def dense_weight(self, w: torch.Tensor) -> torch.Tensor:
@@ -216,7 +235,8 @@ def _stream_call(x, w, bias, residual, epi, out, cfg, shuffled: bool = True):
   ntw, S = cfg
   M, N = x.shape[0], w.shape[0]
   ws = scratch.splitk(x.device, S * M * N) if S > 1 else None
-  require().gemm_stream(x, w, out, bias, residual, ws, K.EPI[epi], ntw, S, shuffled)
+  tk = scratch.tickets(x.device, (N // 64) * (-(-M // 128))) if S > 1 and SPLITK_IN_LAUNCH else None
+  require().gemm_stream(x, w, out, bias, residual, ws, K.EPI[epi], ntw, S, shuffled, tk)
   return out
 
 
