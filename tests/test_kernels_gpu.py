@@ -178,6 +178,34 @@ def test_sample_greedy_and_topk(gpu):
   assert torch.equal(K.sample(logits, temps, 1, so).cpu(), greedy.cpu())
 
 
+def test_sample_split_path_matches_single_block(gpu):
+  """Small batches take the two-stage (64 chunk workgroups + merge) path; for the same seed and row
+  index it must pick the same tokens as the one-workgroup-per-row path used for large batches."""
+  torch.manual_seed(1)
+  V = 128256
+  small = torch.randn(6, V, device=gpu) * 3
+  big = torch.cat([small, torch.randn(60, V, device=gpu) * 3])  # 66 rows -> single-block path
+  for temp, k in ((0.0, 35), (0.7, 35), (1.0, 64), (0.5, 7)):
+    so = torch.tensor([99, 5], device=gpu, dtype=torch.int64)
+    a = K.sample(small, torch.full((6,), temp, device=gpu), k, so)
+    b = K.sample(big, torch.full((66,), temp, device=gpu), k, so)
+    assert torch.equal(a.cpu(), b[:6].cpu()), (temp, k)
+
+
+def test_sample_split_distribution(gpu):
+  base = torch.full((128256,), -30.0, device=gpu)
+  base[[10, 70000, 128000]] = torch.tensor([2.0, 1.0, 0.5], device=gpu)
+  lg = base.expand(8, -1).contiguous()
+  counts = torch.zeros(128256, device=gpu)
+  for off in range(250):
+    tok = K.sample(lg, torch.ones(8, device=gpu), 3, torch.tensor([3, off], device=gpu, dtype=torch.int64))
+    counts += torch.bincount(tok.long(), minlength=128256).float()
+  c = counts.cpu() / counts.sum().cpu()
+  p = torch.softmax(torch.tensor([2.0, 1.0, 0.5]), 0)
+  assert abs(float(c[10]) - float(p[0])) < 0.03 and abs(float(c[70000]) - float(p[1])) < 0.03
+  assert float(c[10] + c[70000] + c[128000]) == 1.0
+
+
 def test_sample_distribution(gpu):
   # exponential race == categorical(softmax(l / T)) restricted to top-k
   logits = torch.tensor([[2.0, 1.0, 0.5, 0.0, -1.0] + [-30.0] * 59], device=gpu)

@@ -373,8 +373,12 @@ void sample(const at::Tensor& logits, const at::Tensor& temps, int64_t top_k, co
   XCHECK(logits.dim() == 2 && logits.stride(1) == 1, "sample: logits must be [B, V] with contiguous rows");
   const int64_t B = logits.size(0), V = logits.size(1);
   XCHECK(temps.numel() >= B && out.numel() >= B && seed_off.numel() >= 2, "sample: shape mismatch");
+  // candidate scratch of the split path for small batches (graph-safe caching-allocator tensors)
+  auto ck = at::empty({B * xot::SAMPLE_CAND_PER_ROW}, logits.options().dtype(at::kInt));
+  auto ci = at::empty({B * xot::SAMPLE_CAND_PER_ROW}, logits.options().dtype(at::kInt));
   xot::launch_sample(logits.data_ptr<float>(), logits.stride(0), (int)B, (int)V, temps.data_ptr<float>(), (int)top_k,
-                     seed_off.data_ptr<int64_t>(), out.data_ptr<int32_t>(), cur_stream());
+                     seed_off.data_ptr<int64_t>(), out.data_ptr<int32_t>(),
+                     reinterpret_cast<uint32_t*>(ck.data_ptr<int>()), ci.data_ptr<int>(), cur_stream());
 }
 
 void ce_fwd(const at::Tensor& x, const at::Tensor& tgt, at::Tensor& loss, at::Tensor& lse) {

@@ -33,6 +33,40 @@ __device__ __forceinline__ void argmax_combine(float& v, int& i, float v2, int i
   }
 }
 
+// Radix-select step, run by wave 0: find the bin holding the krem-th largest key (bins scanned from
+// 255 down) with a wave suffix scan instead of a 256-long dependent LDS chain (which alone cost
+// ~25 us per row).  Writes the refined prefix and the remaining rank to shv[0], shv[1].
+__device__ __forceinline__ void pick_bin(const int* hist, uint32_t krem, uint32_t prefix, int shift, uint32_t* shv) {
+  const int l = threadIdx.x;  // 0..63
+  const int b0 = 255 - 4 * l;
+  const int c0 = hist[b0], c1 = hist[b0 - 1], c2 = hist[b0 - 2], c3 = hist[b0 - 3];
+  const int sum = c0 + c1 + c2 + c3;
+  int incl = sum;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(incl, o, 64);
+    if (l >= o) incl += t;
+  }
+  const int excl = incl - sum;
+  const bool hit = (uint32_t)excl < krem && krem <= (uint32_t)incl;
+  const unsigned long long m = __ballot(hit);
+  const int L = m ? __ffsll((long long)m) - 1 : 63;
+  if (l == L) {
+    const int cs[4] = {c0, c1, c2, c3};
+    uint32_t cum = excl;
+    int bin = b0 - 3;
+    for (int j = 0; j < 4; ++j) {
+      if (b0 - j == 0 || cum + (uint32_t)cs[j] >= krem) {
+        bin = b0 - j;
+        break;
+      }
+      cum += cs[j];
+    }
+    shv[0] = prefix | ((uint32_t)bin << shift);
+    shv[1] = krem - cum;
+  }
+}
+
 __global__ __launch_bounds__(1024) void sample_kernel(const float* __restrict__ logits, long ld, int V,
                                                       const float* __restrict__ temps, int top_k,
                                                       const int64_t* __restrict__ seed_off,
@@ -40,7 +74,7 @@ __global__ __launch_bounds__(1024) void sample_kernel(const float* __restrict__ 
   __shared__ int hist[256];
   __shared__ float rv[16];
   __shared__ int ri[16];
-  __shared__ uint32_t sh_prefix, sh_krem;
+  __shared__ uint32_t shv1[2];
   const int row = blockIdx.x, tid = threadIdx.x;
   const float* x = logits + (size_t)row * ld;
   const float temp = temps[row];
@@ -59,19 +93,11 @@ __global__ __launch_bounds__(1024) void sample_kernel(const float* __restrict__ 
         if ((k & hmask) == prefix) atomicAdd(&hist[(k >> shift) & 255], 1);
       }
       __syncthreads();
-      if (tid == 0) {
-        uint32_t cum = 0;
-        int bin = 255;
-        for (; bin > 0; --bin) {
-          if (cum + (uint32_t)hist[bin] >= krem) break;
-          cum += hist[bin];
-        }
-        sh_prefix = prefix | ((uint32_t)bin << shift);
-        sh_krem = krem - cum;
-      }
+      if (tid < 64) pick_bin(hist, krem, prefix, shift, shv1);
       __syncthreads();
-      prefix = sh_prefix;
-      krem = sh_krem;
+      prefix = shv1[0];
+      krem = shv1[1];
+      __syncthreads();
     }
     thresh = prefix;  // exact key of the k-th largest value
   }
@@ -113,9 +139,178 @@ __global__ __launch_bounds__(1024) void sample_kernel(const float* __restrict__ 
   }
 }
 
+// ---------------------------------------------------------------------------- small batches
+// With few rows a single workgroup per row leaves the chip idle and is latency-bound (~150 us for
+// one 128k-vocab row).  Split each row over SG chunk workgroups: stage 1 keeps every chunk's top-k
+// (key, index) candidates (for greedy rows: the chunk argmax); stage 2, one workgroup per row,
+// selects the global k-th largest among the SG*k candidates and runs the same exponential race on
+// the eligible ones.  Every element >= the global k-th largest is in its chunk's top-k, so both
+// paths pick the same token for the same (seed, offset) except under exact float ties at the cut.
+constexpr int SG = 64;       // chunks per row
+constexpr int SK = 64;       // max top_k on this path
+constexpr int SCH = 2048;    // max chunk length (V <= SG * SCH)
+
+// block-wide 4-pass radix select over n keys in LDS: the key of the krem-th largest
+__device__ uint32_t radix_kth(const uint32_t* keys, int n, uint32_t krem, int* hist, uint32_t* shv) {
+  const int tid = threadIdx.x;
+  uint32_t prefix = 0;
+  for (int pass = 0; pass < 4; ++pass) {
+    const int shift = 24 - 8 * pass;
+    const uint32_t hmask = pass == 0 ? 0u : (0xFFFFFFFFu << (shift + 8));
+    for (int i = tid; i < 256; i += blockDim.x) hist[i] = 0;
+    __syncthreads();
+    for (int i = tid; i < n; i += blockDim.x) {
+      const uint32_t k = keys[i];
+      if ((k & hmask) == prefix) atomicAdd(&hist[(k >> shift) & 255], 1);
+    }
+    __syncthreads();
+    if (tid < 64) pick_bin(hist, krem, prefix, shift, shv);
+    __syncthreads();
+    prefix = shv[0];
+    krem = shv[1];
+    __syncthreads();
+  }
+  return prefix;
+}
+
+__global__ __launch_bounds__(256) void sample_stage1_kernel(const float* __restrict__ logits, long ld, int V,
+                                                            const float* __restrict__ temps, int top_k,
+                                                            uint32_t* __restrict__ cand_key,
+                                                            int32_t* __restrict__ cand_idx) {
+  __shared__ uint32_t keys[SCH];
+  __shared__ int hist[256];
+  __shared__ uint32_t shv[2];
+  __shared__ int cnt;
+  __shared__ float rv[4];
+  __shared__ int ri[4];
+  const int chunk = blockIdx.x, row = blockIdx.y, tid = threadIdx.x;
+  const int len = (V + SG - 1) / SG, beg = chunk * len, n = max(0, min(len, V - beg));
+  const float* x = logits + (size_t)row * ld + beg;
+  uint32_t* ck = cand_key + ((size_t)row * SG + chunk) * SK;
+  int32_t* ci = cand_idx + ((size_t)row * SG + chunk) * SK;
+  const bool greedy = temps[row] <= 1e-5f || top_k == 1;
+  if (greedy) {  // chunk argmax -> candidate slot 0
+    float best = -INFINITY;
+    int bidx = 0x7fffffff;
+    for (int i = tid; i < n; i += 256) argmax_combine(best, bidx, x[i], beg + i);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float v2 = __shfl_xor(best, o, 64);
+      const int i2 = __shfl_xor(bidx, o, 64);
+      argmax_combine(best, bidx, v2, i2);
+    }
+    if ((tid & 63) == 0) {
+      rv[tid >> 6] = best;
+      ri[tid >> 6] = bidx;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      float bv = rv[0];
+      int bi = ri[0];
+      for (int w = 1; w < 4; ++w) argmax_combine(bv, bi, rv[w], ri[w]);
+      ck[0] = fkey(bv);
+      ci[0] = bi;
+    }
+    return;
+  }
+  for (int i = tid; i < n; i += 256) keys[i] = fkey(x[i]);
+  if (tid == 0) cnt = 0;
+  __syncthreads();
+  const int kk = min(top_k, n);
+  const uint32_t th = kk > 0 ? radix_kth(keys, n, (uint32_t)kk, hist, shv) : 0xFFFFFFFFu;
+  // emit the chunk's top-kk (keys > th first, then ties at th up to kk)
+  for (int i = tid; i < n; i += 256)
+    if (keys[i] > th) {
+      const int p = atomicAdd(&cnt, 1);
+      ck[p] = keys[i];
+      ci[p] = beg + i;
+    }
+  __syncthreads();
+  for (int i = tid; i < n; i += 256)
+    if (keys[i] == th) {
+      const int p = atomicAdd(&cnt, 1);
+      if (p < kk) {
+        ck[p] = keys[i];
+        ci[p] = beg + i;
+      }
+    }
+  __syncthreads();
+  for (int p = min(cnt, kk) + tid; p < SK; p += 256) {  // unused slots
+    ck[p] = 0;
+    ci[p] = -1;
+  }
+}
+
+__global__ __launch_bounds__(256) void sample_stage2_kernel(const float* __restrict__ temps, int top_k,
+                                                            const int64_t* __restrict__ seed_off,
+                                                            const uint32_t* __restrict__ cand_key,
+                                                            const int32_t* __restrict__ cand_idx, int V,
+                                                            int32_t* __restrict__ out) {
+  __shared__ uint32_t keys[SG * SK];
+  __shared__ int hist[256];
+  __shared__ uint32_t shv[2];
+  __shared__ float rv[4];
+  __shared__ int ri[4];
+  const int row = blockIdx.x, tid = threadIdx.x;
+  const uint32_t* ck = cand_key + (size_t)row * SG * SK;
+  const int32_t* ci = cand_idx + (size_t)row * SG * SK;
+  const float temp = temps[row];
+  const bool greedy = temp <= 1e-5f || top_k == 1;
+  const int n = SG * SK;
+  for (int i = tid; i < n; i += 256) keys[i] = (greedy && (i % SK) != 0) ? 0u : (ci[i] < 0 ? 0u : ck[i]);
+  // (unused slots hold key 0, below every real key, so they never reach the top-k)
+  __syncthreads();
+  uint32_t th = 0;
+  if (!greedy) th = radix_kth(keys, n, (uint32_t)top_k, hist, shv);
+  const float invt = greedy ? 1.f : 1.f / fmaxf(temp, 1e-5f);
+  const uint64_t seed = (uint64_t)seed_off[0], off = (uint64_t)seed_off[1];
+  const uint64_t base = splitmix64(seed ^ splitmix64(off * 0x632be59bd9b4e019ull + (uint64_t)row));
+  float best = -INFINITY;
+  int bidx = 0x7fffffff;
+  for (int i = tid; i < n; i += 256) {
+    const int idx = ci[i];
+    if (idx < 0 || keys[i] < th || (greedy && (i % SK) != 0)) continue;
+    // invert fkey to recover the logit
+    const uint32_t k = keys[i];
+    const float v = __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
+    float sc;
+    if (greedy) {
+      sc = v;
+    } else {
+      const uint64_t h = splitmix64(base + (uint64_t)idx);
+      const float u = ((float)(h >> 40) + 0.5f) * (1.0f / 16777216.0f);
+      sc = v * invt - __logf(-__logf(u));
+    }
+    argmax_combine(best, bidx, sc, idx);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float v2 = __shfl_xor(best, o, 64);
+    const int i2 = __shfl_xor(bidx, o, 64);
+    argmax_combine(best, bidx, v2, i2);
+  }
+  if ((tid & 63) == 0) {
+    rv[tid >> 6] = best;
+    ri[tid >> 6] = bidx;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    float bv = rv[0];
+    int bi = ri[0];
+    for (int w = 1; w < 4; ++w) argmax_combine(bv, bi, rv[w], ri[w]);
+    out[row] = bi >= V ? 0 : bi;
+  }
+}
+
 void launch_sample(const float* logits, long ld, int B, int V, const float* temps, int top_k,
-                   const int64_t* seed_off, int32_t* out, hipStream_t s) {
+                   const int64_t* seed_off, int32_t* out, uint32_t* cand_key, int32_t* cand_idx, hipStream_t s) {
   if (B <= 0) return;
+  const bool split = cand_key != nullptr && B < 64 && top_k > 0 && top_k <= SK && V <= SG * SCH && V >= SG * SK;
+  if (split) {
+    sample_stage1_kernel<<<dim3(SG, B), 256, 0, s>>>(logits, ld, V, temps, top_k, cand_key, cand_idx);
+    sample_stage2_kernel<<<B, 256, 0, s>>>(temps, top_k, seed_off, cand_key, cand_idx, V, out);
+    return;
+  }
   sample_kernel<<<B, 1024, 0, s>>>(logits, ld, V, temps, top_k, seed_off, out);
 }
 
