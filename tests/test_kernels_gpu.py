@@ -291,6 +291,51 @@ def test_gemm_stream(gpu, M, epi, ntw, splits):
     assert rel_err(y2, ref) < 1e-2
 
 
+@pytest.mark.parametrize("M", [1, 77, 256, 300, 512, 700])
+@pytest.mark.parametrize("epi,bn,splits", [("none", 256, 1), ("none", 128, 1), ("resid", 256, 1), ("silu", 256, 1),
+                                           ("silu", 128, 1), ("none", 256, 3), ("resid", 128, 2), ("silu", 256, 5)])
+def test_gemm_big(gpu, M, epi, bn, splits):
+  """Large-M LDS-DMA GEMM on the pre-shuffled layout vs the fp32 reference: masked row tiles, both
+  column tilings, uneven split-K ranges, every epilogue, fp32 and bf16 outputs."""
+  from xotorch_support_jetson_amd.ops._ext import require
+  from xotorch_support_jetson_amd.ops.weights_layout import shuffle_for_stream
+  torch.manual_seed(M + bn + splits)
+  N, Kd = 1024, 1280  # 20 k stages: splits of 3 and 5 get unequal ranges
+  x = torch.randn(M, Kd, device=gpu, dtype=torch.bfloat16)
+  w = torch.randn(N, Kd, device=gpu, dtype=torch.bfloat16) / math.sqrt(Kd)
+  b = torch.randn(N, device=gpu, dtype=torch.bfloat16)
+  r = torch.randn(M, N, device=gpu, dtype=torch.bfloat16)
+  ws = torch.empty(splits * M * N, device=gpu, dtype=torch.float32)
+  full = R.linear(x, w, b)
+  if epi == "silu":
+    f = full.view(M, N // 32, 2, 16)
+    ref = (torch.nn.functional.silu(f[:, :, 0]) * f[:, :, 1]).reshape(M, N // 2)
+    y = torch.empty(M, N // 2, device=gpu, dtype=torch.bfloat16)
+  elif epi == "resid":
+    ref = full + r.float()
+    y = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+  else:
+    ref = full
+    y = torch.empty(M, N, device=gpu, dtype=torch.float32)
+  require().gemm_big(x, shuffle_for_stream(w), y, b, r if epi == "resid" else None, ws, K.EPI[epi], bn, splits)
+  assert rel_err(y, ref) < 1e-2
+
+
+def test_gemm_big_exact_layout(gpu):
+  """Integer-valued operands (exact in bf16 and fp32): every output element must match bit for bit,
+  which pins the fragment maps, the LDS swizzle and the shuffled-layout k order."""
+  from xotorch_support_jetson_amd.ops._ext import require
+  from xotorch_support_jetson_amd.ops.weights_layout import shuffle_for_stream
+  g = torch.Generator(device="cpu").manual_seed(5)
+  M, N, Kd = 300, 512, 384
+  x = torch.randint(-3, 4, (M, Kd), generator=g).to(torch.bfloat16).to(gpu)
+  w = torch.randint(-3, 4, (N, Kd), generator=g).to(torch.bfloat16).to(gpu)
+  y = torch.empty(M, N, device=gpu, dtype=torch.float32)
+  require().gemm_big(x, shuffle_for_stream(w), y, None, None, None, 0, 256, 1)
+  ref = x.float() @ w.float().t()
+  assert torch.equal(y, ref)
+
+
 # ------------------------------------------------------------------ mixture of experts
 @pytest.mark.parametrize("T,E,k", [(1, 8, 2), (7, 8, 2), (100, 8, 2), (300, 4, 2), (64, 16, 4)])
 @pytest.mark.parametrize("shuffled", [False, True])

@@ -42,7 +42,8 @@ def _worker(rank, world, port, q, MODEL):
     shard = equal_layer_shards(MODEL, c.num_layers, world)[rank]
     tr = ShardTrainer(random_weights(c, shard, "cpu", seed=3), "cpu", lr=1e-3)
     losses = _run(tr, rank, world, P2PTransport(rank, world))
-    q.put((rank, losses, {k: v.clone() for k, v in tr.master.items()}))
+    # numpy, not torch tensors: a queued tensor is an fd into this process, gone once it exits
+    q.put((rank, losses, {k: v.detach().float().numpy().copy() for k, v in tr.master.items()}))
     dist.barrier()
   finally:
     dist.destroy_process_group()
@@ -84,8 +85,8 @@ def test_pipeline_training_two_ranks_matches_single(MODEL):
   for r in (0, 1):
     for a, b in zip(res[r][0], ref_losses):
       assert abs(a - b) < tol, (r, res[r][0], ref_losses)
-  merged = {**res[0][1], **res[1][1]}
+  merged = {k: torch.from_numpy(v) for k, v in {**res[0][1], **res[1][1]}.items()}
   for k, v in full.master.items():
     assert torch.allclose(v, merged[k], atol=1e-6 if tol < 1e-3 else 2e-3, rtol=1e-5), k
   if c.tie_word_embeddings:  # the last stage's head copy took the same update as the embedding
-    assert torch.allclose(res[1][1]["lm_head"], res[0][1]["embed"], atol=1e-7)
+    assert torch.allclose(merged["lm_head"], torch.from_numpy(res[0][1]["embed"]), atol=1e-7)

@@ -60,11 +60,11 @@ def main():
       ncol = N // 2 if epi == "silu" else N
       out = torch.empty(M, ncol, dtype=torch.bfloat16, device=dev)
       L.STREAM_MAX_M = 1 << 30
-      cfg = L.policy.stream_cfg(x, ws, None, res, epi, torch.bfloat16)
-      us_stream = t_us(lambda i: L._stream_call(x, wsl[i], None, res, epi, out, cfg), nc)
+      cfg = L.policy.shuffled_cfg(x, ws, None, res, epi, torch.bfloat16)
+      us_stream = t_us(lambda i: L._shuffled_call(x, wsl[i], None, res, epi, out, cfg), nc)
       # correctness vs hipBLASLt on the row-major weight
       ref = L._blas(x, w, None, res, epi, None, torch.bfloat16)
-      L._stream_call(x, ws, None, res, epi, out, cfg)
+      L._shuffled_call(x, ws, None, res, epi, out, cfg)
       err = ((out.float() - ref.float()).abs().max() / ref.float().abs().max()).item()
       us_blas = t_us(lambda i: L._blas(x, wl[i], None, res, epi, None, torch.bfloat16), nc)
       us_unshuf = t_us(lambda i: L.scratch.dense_weight(wsl[i]), nc)

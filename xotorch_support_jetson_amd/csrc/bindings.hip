@@ -243,6 +243,50 @@ void gemm_stream(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const 
          " splits=", splits);
 }
 
+// Large-M GEMM on the pre-shuffled weight layout (prefill chunks, decode batches > 128 rows).
+// bn: 256 or 128 output columns per workgroup; splits > 1 needs an fp32 workspace of splits*M*N.
+void gemm_big(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const c10::optional<at::Tensor>& bias,
+              const c10::optional<at::Tensor>& res, const c10::optional<at::Tensor>& ws, int64_t epi, int64_t bn,
+              int64_t splits) {
+  CHECK_BF16(x);
+  CHECK_BF16(w);
+  CHECK_GPU(y);
+  XCHECK(x.dim() == 2 && w.dim() == 2 && y.dim() == 2, "gemm_big: x, w, y must be 2-D");
+  XCHECK(x.stride(1) == 1 && x.stride(0) % 8 == 0 && w.is_contiguous() && y.stride(1) == 1,
+         "gemm_big: rows must be contiguous and 16-B aligned");
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
+  XCHECK(w.size(1) == K, "gemm_big: K mismatch");
+  const bool f32 = y.scalar_type() == at::kFloat;
+  XCHECK(f32 || y.scalar_type() == at::kBFloat16, "gemm_big: y must be bf16 or fp32");
+  XCHECK(y.size(0) == M && y.size(1) == (epi == 2 ? N / 2 : N), "gemm_big: y shape mismatch");
+  XCHECK(M <= (1 << 24), "gemm_big: M too large");
+  if (bias.has_value()) {
+    CHECK_BF16((*bias));
+    XCHECK(bias->numel() == N && bias->is_contiguous(), "gemm_big: bias shape mismatch");
+  }
+  int64_t ldr = 0;
+  if (epi == 1) {
+    XCHECK(res.has_value(), "gemm_big: residual epilogue needs res");
+    CHECK_BF16((*res));
+    XCHECK(res->dim() == 2 && res->size(0) == M && res->size(1) == N && res->stride(1) == 1, "gemm_big: res shape");
+    ldr = res->stride(0);
+  }
+  float* wsp = nullptr;
+  long ws_elems = 0;
+  if (ws.has_value()) {
+    CHECK_GPU((*ws));
+    CHECK_DT((*ws), at::kFloat);
+    XCHECK(ws->is_contiguous(), "gemm_big: ws must be contiguous");
+    wsp = ws->data_ptr<float>();
+    ws_elems = ws->numel();
+  }
+  const int rc = xot::launch_gemm_big(bf(x), (int)x.stride(0), bf(w), bf_opt(bias), epi == 1 ? bf(*res) : nullptr,
+                                      (int)ldr, y.data_ptr(), (int)y.stride(0), f32, (int)epi, wsp, ws_elems, (int)M,
+                                      (int)N, (int)K, (int)bn, (int)splits, cur_stream());
+  XCHECK(rc == 0, "gemm_big: unsupported shape M=", M, " N=", N, " K=", K, " epi=", epi, " bn=", bn,
+         " splits=", splits);
+}
+
 // grouped expert GEMM: y[slot] = x[gather ? gather[slot] : slot] @ w[e].T for slots of expert e
 void gemm_moe(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const at::Tensor& off,
               const c10::optional<at::Tensor>& gather, int64_t epi, int64_t max_rows, bool wshuf) {
@@ -443,6 +487,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_stream", &gemm_stream, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("bias"), py::arg("res"),
         py::arg("ws"), py::arg("epi"), py::arg("ntw"), py::arg("splits"), py::arg("wshuf"),
         py::arg("tickets") = py::none());
+  m.def("gemm_big", &gemm_big, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("bias"), py::arg("res"),
+        py::arg("ws"), py::arg("epi"), py::arg("bn"), py::arg("splits"));
   m.def("gemm_moe", &gemm_moe);
   m.def("moe_route", &moe_route);
   m.def("moe_combine", &moe_combine);

@@ -15,11 +15,10 @@
 // Reference parity: replaces the q/k/v/o projections and FeedForward w1/w2/w3 of the torchtune
 // layers built in xotorch/inference/torch/models/general_mha.py:77-120 and llm_utils.py:513-522.
 #include "common.h"
+#include "gemm_common.h"
 #include "kernels.h"
 
 namespace xot {
-
-enum { EPI_NONE = 0, EPI_RESID = 1, EPI_SILU = 2 };
 
 template <int MT, int NT, int KS, int EPI, bool OUT_F32>
 __global__ __launch_bounds__(256) void gemm_skinny_kernel(const uint16_t* __restrict__ X, int ldx,
@@ -190,72 +189,6 @@ int launch_gemm_skinny(const uint16_t* X, int ldx, const uint16_t* W, int ldw, c
 //   W rows       : streamed once, straight to VGPRs, two chunks in flight (prefetch depth 2)
 // MFMA k-order is permuted per lane group (group g owns k in [8*KS*g, 8*KS*(g+1)) of the chunk)
 // so each lane reads 16*KS contiguous bytes of its weight row per chunk.
-// Sum the S fp32 slabs of one output row at 8 output columns [o, o+8) and apply the epilogue.
-// wsrow = slab 0 of this row (slabs are sstride floats apart); rrow / yrow = this row of R / Y.
-template <int EPI, bool OUT_F32>
-__device__ __forceinline__ void splitk_out8(const float* __restrict__ wsrow, size_t sstride, int S, int o,
-                                            const uint16_t* __restrict__ bias, const uint16_t* __restrict__ rrow,
-                                            void* __restrict__ yrow) {
-  float v[8];
-  if constexpr (EPI == EPI_SILU) {
-    const int j = o >> 4, w = o & 15;
-    float gs[8], us[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) gs[e] = us[e] = 0.f;
-    for (int s = 0; s < S; ++s) {
-      const float* row = wsrow + s * sstride;
-      const f32x4 g0 = *reinterpret_cast<const f32x4*>(row + 32 * j + w);
-      const f32x4 g1 = *reinterpret_cast<const f32x4*>(row + 32 * j + w + 4);
-      const f32x4 u0 = *reinterpret_cast<const f32x4*>(row + 32 * j + 16 + w);
-      const f32x4 u1 = *reinterpret_cast<const f32x4*>(row + 32 * j + 16 + w + 4);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        gs[e] += g0[e];
-        gs[e + 4] += g1[e];
-        us[e] += u0[e];
-        us[e + 4] += u1[e];
-      }
-    }
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float bg = bias ? bf2f(bias[32 * j + w + e]) : 0.f, bu = bias ? bf2f(bias[32 * j + 16 + w + e]) : 0.f;
-      v[e] = silu(gs[e] + bg) * (us[e] + bu);
-    }
-  } else {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = 0.f;
-    for (int s = 0; s < S; ++s) {
-      const float* row = wsrow + s * sstride + o;
-      const f32x4 a = *reinterpret_cast<const f32x4*>(row), b = *reinterpret_cast<const f32x4*>(row + 4);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        v[e] += a[e];
-        v[e + 4] += b[e];
-      }
-    }
-    if (bias != nullptr) {
-      const s16x8 bb = ld16(bias + o);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] += bf2f(bb[e]);
-    }
-    if constexpr (EPI == EPI_RESID) {
-      const s16x8 rr = ld16(rrow + o);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] += bf2f(rr[e]);
-    }
-  }
-  if constexpr (OUT_F32) {
-    float* y = reinterpret_cast<float*>(yrow) + o;
-    *reinterpret_cast<f32x4*>(y) = f32x4{v[0], v[1], v[2], v[3]};
-    *reinterpret_cast<f32x4*>(y + 4) = f32x4{v[4], v[5], v[6], v[7]};
-  } else {
-    s16x8 out;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) out[e] = (short)f2bf(v[e]);
-    st16(reinterpret_cast<uint16_t*>(yrow) + o, out);
-  }
-}
-
 // SPLIT: fp32 partial slabs ws[blockIdx.y][M][N], finished by splitk_reduce_kernel or -- with tickets -- by the
 // last-arriving workgroup of each tile inside the same launch (epilogue there).
 // MOE = 1 / 2: grouped (mixture-of-experts) GEMM.  blockIdx.z = expert e with weight W[e]
@@ -323,7 +256,8 @@ __global__ __launch_bounds__(256, OCC) void gemm_stream_kernel(const uint16_t* _
 
   // W pointers.  Row-major: lane (g, c) streams row n0+16j+c, k in [8*KS*g, 8*KS*(g+1)) of each chunk.
   // Pre-shuffled (WSHUF, KS == 4): tiles [N/16][K/128][s][lane][8] so instruction s of a wave reads
-  // 1 KB of contiguous memory (see ops.weights_layout.shuffle_for_stream).
+  // 1 KB of contiguous memory holding the MFMA B fragments of k [32s, 32s+32) in natural order (lane
+  // (g, c): row c, k 32s+8g..+8; see ops.weights_layout.shuffle_for_stream).
   const uint16_t* wp[NTW];
   constexpr int WSTEP = WSHUF ? 16 * KC : KC;  // elements between consecutive chunks of one lane
 #pragma unroll
@@ -395,7 +329,8 @@ __global__ __launch_bounds__(256, OCC) void gemm_stream_kernel(const uint16_t* _
     auto afrag = [&](int t) {
       const int s = t / MT, i = t % MT;
       const int row = wrow + 16 * i + c;
-      const int phys = (g * KS + s) ^ (row & (CPR - 1));
+      // row-major W: lane group g owns k [8*KS*g, +8*KS) of the chunk; pre-shuffled W: natural MFMA order
+      const int phys = (WSHUF ? (4 * s + g) : (g * KS + s)) ^ (row & (CPR - 1));
       return ld16(xb + row * KC + phys * 8);
     };
     s16x8 a[LDPF];
@@ -522,24 +457,6 @@ __global__ __launch_bounds__(256, OCC) void gemm_stream_kernel(const uint16_t* _
           }
         }
     }
-  }
-}
-
-// Sum S fp32 slabs [S][M][N] and apply the epilogue.  One thread per 8 output columns.
-template <int EPI, bool OUT_F32>
-__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, int S, int M, int N,
-                                                            const uint16_t* __restrict__ bias,
-                                                            const uint16_t* __restrict__ R, int ldr,
-                                                            void* __restrict__ Yv, int ldy) {
-  const int ncol = EPI == EPI_SILU ? N / 2 : N;
-  const long total = (long)M * (ncol / 8);
-  for (long t = blockIdx.x * 256L + threadIdx.x; t < total; t += (long)gridDim.x * 256) {
-    const int m = (int)(t / (ncol / 8));
-    const int o = (int)(t % (ncol / 8)) * 8;
-    void* yrow = OUT_F32 ? (void*)(reinterpret_cast<float*>(Yv) + (size_t)m * ldy)
-                         : (void*)(reinterpret_cast<uint16_t*>(Yv) + (size_t)m * ldy);
-    splitk_out8<EPI, OUT_F32>(ws + (size_t)m * N, (size_t)M * N, S, o, bias,
-                              EPI == EPI_RESID ? R + (size_t)m * ldr : nullptr, yrow);
   }
 }
 

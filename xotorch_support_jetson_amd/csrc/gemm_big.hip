@@ -1,0 +1,324 @@
+// Large-M projection GEMM on the pre-shuffled weight layout:  Y[M,N] = X[M,K] . W[N,K]^T
+//
+// Serves decode batches above 128 rows and prefill chunks -- the compute-bound regime, where the
+// weight-streaming kernel (gemm.hip) runs out of MFMA issue rate.  Structure (CDNA4, wave64):
+//   * workgroup tile 256 (M) x BN (N) x 64 (K), 8 waves (512 threads) as WM x WN; a wave owns
+//     (256/WM) x (BN/WN) of the output = MT x NT tiles of v_mfma_f32_16x16x32_bf16
+//   * both operands staged HBM/L2 -> LDS by LDS-DMA (global_load_lds_dwordx4, 1 KB per wave
+//     instruction, no VGRP round trip), two stages: stage t+1 is issued before the MFMAs of stage t
+//     and retired by one counted wait + one barrier per 64-deep k step
+//   * W tiles: the shuffled layout stores the MFMA B fragments of 16 rows x 32 k as 1 KB, so a
+//     16-row group's 64-deep stage is 2 KB of contiguous memory copied verbatim; fragment reads are
+//     ds_read_b128 at lane*16 (conflict-free)
+//   * X tiles: [256 rows][64 k] with 128-B rows; 16-B slot XOR-swizzled by (row >> 1) & 7 (applied
+//     to the per-lane global source address, so the LDS-DMA image stays lane-linear) -> the 16-lane
+//     groups of every A-fragment ds_read_b128 hit 16 distinct bank quads
+//   * XCD-aware block order: consecutive tile ids (the row tiles of one column tile, then the next
+//     column tiles) are dispatched to the same XCD, so a weight tile is read from HBM once and the
+//     activation rows stay in that XCD's L2
+//   * fused epilogues (bias, residual add, SiLU(gate)*up on 16-row interleaved gate/up weights) or
+//     split-K fp32 slabs reduced by splitk_reduce_kernel
+//
+// Reference parity: the q/k/v/o and w1/w2/w3 projections of xotorch/inference/torch/models/
+// general_mha.py:77-120 and llm_utils.py:513-522 (torchtune nn.Linear), at serving batch sizes.
+#include "common.h"
+#include "gemm_common.h"
+#include "kernels.h"
+
+namespace xot {
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef __attribute__((address_space(1))) void* glb_ptr_t;
+
+// one LDS-DMA wave instruction: lane l copies 16 B from its own global address to lds_base + 16*l
+template <int AUX = 0>
+__device__ __forceinline__ void glds16(const void* g, void* lds_base) {
+  __builtin_amdgcn_global_load_lds((glb_ptr_t)g, (lds_ptr_t)lds_base, 16, 0, AUX);
+}
+
+constexpr int GB_BM = 256;
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// ABL (tools/lab only): 1 = k loop without MFMAs, 2 = without stage loads, 3 = stage loads not overlapped
+// AUXA / AUXB: cache-policy bits of the X / W LDS-DMA loads (sc0 = 1, nt = 2, sc1 = 16)
+template <int BN, int WM, int WN, int BK, int NBUF, int EPI, bool OUT_F32, bool SPLIT, int ABL = 0, int AUXA = 0,
+          int AUXB = 3, bool PRIO = false>
+__global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __restrict__ X, int ldx,
+                                                          const uint16_t* __restrict__ W,
+                                                          const uint16_t* __restrict__ bias,
+                                                          const uint16_t* __restrict__ R, int ldr,
+                                                          void* __restrict__ Yv, int ldy, float* __restrict__ ws,
+                                                          int M, int N, int K, int S) {
+  static_assert(WM * WN == 8, "8 waves");
+  static_assert(BK == 32 || BK == 64, "k stage of 32 or 64");
+  constexpr int BM = GB_BM;
+  constexpr int MT = BM / (16 * WM), NT = BN / (16 * WN);
+  static_assert(EPI != EPI_SILU || NT % 2 == 0, "SiLU epilogue pairs gate/up n-tiles");
+  constexpr int KS = BK / 32;                          // MFMA k-steps (and 1 KB W blocks per row group) per stage
+  constexpr int SPR = BK / 8;                          // 16-B slots per X row in LDS
+  constexpr int A_ELEMS = BM * BK, B_ELEMS = BN * BK;  // bf16 elements per stage
+  constexpr int STAGE = A_ELEMS + B_ELEMS;
+  constexpr int A_INSTR = A_ELEMS * 2 / 1024 / 8;      // 1 KB LDS-DMA instructions per wave per stage
+  constexpr int B_INSTR = B_ELEMS * 2 / 1024 / 8;
+  constexpr int NI = A_INSTR + B_INSTR;
+  constexpr int PD = NBUF - 1;                         // stages in flight ahead of the one computed
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, c = lane & 15;
+  const int wm = wave / WN, wn = wave % WN;
+
+  // ---- tile of this workgroup (bijective XCD remap, then split-major / column / row order)
+  const int mtiles = (M + BM - 1) / BM, ntiles = N / BN;
+  const int nwg = mtiles * ntiles * S;
+  int b = blockIdx.x;
+  {
+    const int xcd = b & 7, q = nwg >> 3, r = nwg & 7;
+    b = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+  }
+  const int mt = b % mtiles, nt = (b / mtiles) % ntiles, split = b / (mtiles * ntiles);
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int T_all = K / BK;
+  const int t_beg = (int)((long)split * T_all / S), t_end = (int)((long)(split + 1) * T_all / S);
+  const int T = t_end - t_beg;
+
+  // X LDS image: rows of BK bf16, 16-B slot XOR-swizzled so the 16 lanes of each A-fragment
+  // ds_read_b128 group land on 16 distinct bank quads (2 rows per 256-B bank row at BK = 64, 4 at 32).
+  auto aswz = [](int row) -> int {
+    if constexpr (SPR == 8) {
+      return (row >> 1) & 7;
+    } else {
+      constexpr int lut = 0 | (2 << 2) | (3 << 4) | (1 << 6);  // {0, 2, 3, 1}
+      return (lut >> (2 * ((row >> 2) & 3))) & 3;
+    }
+  };
+
+  // ---- LDS-DMA source addresses (advance with the k stage)
+  // X: instruction i of wave w covers rows (1024 / (2*BK)) * (A_INSTR*w + i) .. ; lane -> row +lane/SPR,
+  // physical slot lane%SPR holding logical slot (lane%SPR) ^ aswz(row).
+  const uint16_t* asrc[A_INSTR];
+#pragma unroll
+  for (int i = 0; i < A_INSTR; ++i) {
+    const int row = (64 / SPR) * (A_INSTR * wave + i) + lane / SPR;
+    const int slot = (lane % SPR) ^ aswz(row);
+    const int grow = min(m0 + row, M - 1);  // rows past M load valid memory; their outputs are masked
+    asrc[i] = X + (size_t)grow * ldx + slot * 8;
+  }
+  // W: instruction q = B_INSTR*w + i copies 1 KB block q % KS of row group q / KS for this stage.
+  const size_t kchunks = K / 128;
+  const uint16_t* bsrc[B_INSTR];
+#pragma unroll
+  for (int i = 0; i < B_INSTR; ++i) {
+    const int q = B_INSTR * wave + i;
+    bsrc[i] = W + ((size_t)((n0 >> 4) + q / KS) * kchunks) * 2048 + (q % KS) * 512 + lane * 8;
+  }
+
+  auto issue = [&](int t, int buf) {  // stage t (absolute k step) -> LDS buffer buf
+    uint16_t* As = smem + buf * STAGE;
+    uint16_t* Bs = As + A_ELEMS;
+    const int k0 = t * BK;
+    const size_t woff = (size_t)(k0 >> 7) * 2048 + ((k0 & 127) >> 5) * 512;
+#pragma unroll
+    for (int i = 0; i < A_INSTR; ++i) glds16<AUXA>(asrc[i] + k0, As + (A_INSTR * wave + i) * 512);
+#pragma unroll
+    for (int i = 0; i < B_INSTR; ++i) glds16<AUXB>(bsrc[i] + woff, Bs + (B_INSTR * wave + i) * 512);
+  };
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // fragment read offsets (elements) inside a stage
+  int aoff[MT][KS];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    const int row = wm * (MT * 16) + 16 * i + c;
+#pragma unroll
+    for (int s2 = 0; s2 < KS; ++s2) aoff[i][s2] = row * BK + (((4 * s2 + g) ^ aswz(row)) * 8);
+  }
+  const int boff = (wn * NT) * KS * 512 + lane * 8;  // + (16-row group j)*KS*512 + s2*512
+
+  // Per stage: B fragments of all k-steps first, then the A fragments in a ring LDPF deep so each
+  // ds_read_b128 is in flight under the MFMAs of the previous row tile (the scheduling fence keeps
+  // the compiler from hoisting all reads up front, which costs registers and serialises on lgkmcnt).
+  constexpr int LDPF = 3;
+  auto compute = [&](int buf) {
+    const uint16_t* As = smem + buf * STAGE;
+    const uint16_t* Bs = As + A_ELEMS;
+    s16x8 bf[KS][NT];
+#pragma unroll
+    for (int s2 = 0; s2 < KS; ++s2)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) bf[s2][j] = ld16(Bs + boff + (j * KS + s2) * 512);
+    s16x8 af[LDPF];
+#pragma unroll
+    for (int u = 0; u < LDPF; ++u) af[u] = ld16(As + aoff[u % MT][u / MT]);
+#pragma unroll
+    for (int u = 0; u < KS * MT; ++u) {
+      const int s2 = u / MT, i = u % MT;
+      const s16x8 cur = af[u % LDPF];
+      if (u + LDPF < KS * MT) af[u % LDPF] = ld16(As + aoff[(u + LDPF) % MT][(u + LDPF) / MT]);
+      if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int j = 0; j < NT; ++j) acc[i][j] = mfma16(cur, bf[s2][j], acc[i][j]);
+      if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  // Barrier without the vmcnt(0) drain __syncthreads() would add: LDS-DMA stages stay in flight.
+  // The asm statements are compiler fences (no LDS access moves across the barrier).
+  auto barrier = []() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  // wait until at most k younger stages of this wave are still in flight
+  auto wait_stages = [](int k) {
+    if (PD >= 4 && k >= 3) wait_vm<(PD >= 4 ? 3 * NI : 0)>();
+    else if (PD >= 3 && k >= 2) wait_vm<(PD >= 3 ? 2 * NI : 0)>();
+    else if (PD >= 2 && k >= 1) wait_vm<(PD >= 2 ? NI : 0)>();
+    else wait_vm<0>();
+  };
+
+  if (T > 0) {
+    // prologue: stages 0 .. PD-1 in flight, stage 0 landed
+#pragma unroll
+    for (int p = 0; p < PD; ++p)
+      if (p < T) issue(t_beg + p, p);
+    wait_stages(min(PD - 1, T - 1));
+    barrier();
+    for (int t = 0; t < T; ++t) {
+      // refill the buffer computed in iteration t-1 (every wave is past that iteration's barrier)
+      if (ABL != 2 && t + PD < T) issue(t_beg + t + PD, (t + PD) % NBUF);
+      if constexpr (ABL == 3) wait_vm<0>();
+      if constexpr (ABL != 1) compute(t % NBUF);
+      // stage t+1 landed for this wave; the barrier makes it landed for all
+      wait_stages(min(PD - 1, T - 2 - t));
+      barrier();
+    }
+  }
+
+  // ---- epilogue
+  const int rbase = m0 + wm * (MT * 16);
+  const int cbase = n0 + wn * (NT * 16);
+  if constexpr (SPLIT) {
+    float* slab = ws + (size_t)split * M * N;
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = rbase + 16 * i + 4 * g + r;
+        if (m < M) {
+#pragma unroll
+          for (int j = 0; j < NT; ++j) slab[(size_t)m * N + cbase + 16 * j + c] = acc[i][j][r];
+        }
+      }
+  } else if constexpr (EPI == EPI_SILU) {
+#pragma unroll
+    for (int p = 0; p < NT / 2; ++p) {  // (gate tile 2p, up tile 2p+1) -> 16 output columns
+      const int col = (cbase >> 1) + 16 * p + c;
+      float bg = 0.f, bu = 0.f;
+      if (bias != nullptr) {
+        bg = bf2f(bias[cbase + 32 * p + c]);
+        bu = bf2f(bias[cbase + 32 * p + 16 + c]);
+      }
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = rbase + 16 * i + 4 * g + r;
+          if (m < M) {
+            const float v = silu(acc[i][2 * p][r] + bg) * (acc[i][2 * p + 1][r] + bu);
+            if constexpr (OUT_F32)
+              reinterpret_cast<float*>(Yv)[(size_t)m * ldy + col] = v;
+            else
+              reinterpret_cast<uint16_t*>(Yv)[(size_t)m * ldy + col] = f2bf(v);
+          }
+        }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int col = cbase + 16 * j + c;
+      const float bv = bias != nullptr ? bf2f(bias[col]) : 0.f;
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = rbase + 16 * i + 4 * g + r;
+          if (m < M) {
+            float v = acc[i][j][r] + bv;
+            if constexpr (EPI == EPI_RESID) v += bf2f(R[(size_t)m * ldr + col]);
+            if constexpr (OUT_F32)
+              reinterpret_cast<float*>(Yv)[(size_t)m * ldy + col] = v;
+            else
+              reinterpret_cast<uint16_t*>(Yv)[(size_t)m * ldy + col] = f2bf(v);
+          }
+        }
+    }
+  }
+}
+
+template <int BN, int WM, int WN, int BK, int NBUF, int EPI, bool F32>
+static void big_launch(const uint16_t* X, int ldx, const uint16_t* W, const uint16_t* bias, const uint16_t* R,
+                       int ldr, void* Y, int ldy, float* ws, int M, int N, int K, int S, hipStream_t st) {
+  constexpr int SMEM = NBUF * (GB_BM + BN) * BK * 2;
+  static_assert(SMEM <= 160 * 1024, "LDS");
+  const int nwg = ((M + GB_BM - 1) / GB_BM) * (N / BN) * S;
+  if (S == 1) {
+    auto kern = gemm_big_kernel<BN, WM, WN, BK, NBUF, EPI, F32, false>;
+    static bool attr = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM) ==
+                       hipSuccess;
+    (void)attr;
+    kern<<<nwg, 512, SMEM, st>>>(X, ldx, W, bias, R, ldr, Y, ldy, nullptr, M, N, K, 1);
+  } else {
+    auto kern = gemm_big_kernel<BN, WM, WN, BK, NBUF, EPI, false, true>;
+    static bool attr = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM) ==
+                       hipSuccess;
+    (void)attr;
+    kern<<<nwg, 512, SMEM, st>>>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, S);
+    const int ncol = EPI == EPI_SILU ? N / 2 : N;
+    const long chunks = (long)M * (ncol / 8);
+    int blocks = (int)((chunks + 255) / 256);
+    if (blocks > 2048) blocks = 2048;
+    splitk_reduce_kernel<EPI, F32><<<blocks, 256, 0, st>>>(ws, S, M, N, bias, R, ldr, Y, ldy);
+  }
+}
+
+template <int EPI, bool F32>
+static int big_dispatch(const uint16_t* X, int ldx, const uint16_t* W, const uint16_t* bias, const uint16_t* R,
+                        int ldr, void* Y, int ldy, float* ws, long ws_elems, int M, int N, int K, int bn, int S,
+                        hipStream_t st) {
+  if (bn == 256)
+    big_launch<256, 2, 4, 32, 4, EPI, F32>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, S, st);
+  else if (bn == 128)
+    big_launch<128, 4, 2, 64, 3, EPI, F32>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, S, st);
+  else
+    return -1;
+  return 0;
+}
+
+int launch_gemm_big(const uint16_t* X, int ldx, const uint16_t* W, const uint16_t* bias, const uint16_t* R, int ldr,
+                    void* Y, int ldy, bool out_f32, int epi, float* ws, long ws_elems, int M, int N, int K, int bn,
+                    int S, hipStream_t s) {
+  if (M <= 0) return 0;
+  if ((bn != 128 && bn != 256) || N % bn != 0 || K % 128 != 0 || S < 1 || S > K / 64) return -1;
+  if (S > 1 && (ws == nullptr || ws_elems < (long)S * M * N)) return -1;
+  if (epi == EPI_SILU && N % 32 != 0) return -1;
+  if (epi == EPI_SILU)
+    return out_f32 ? big_dispatch<EPI_SILU, true>(X, ldx, W, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, bn, S, s)
+                   : big_dispatch<EPI_SILU, false>(X, ldx, W, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, bn, S, s);
+  if (epi == EPI_RESID)
+    return out_f32 ? -1 : big_dispatch<EPI_RESID, false>(X, ldx, W, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, bn, S, s);
+  return out_f32 ? big_dispatch<EPI_NONE, true>(X, ldx, W, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, bn, S, s)
+                 : big_dispatch<EPI_NONE, false>(X, ldx, W, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, bn, S, s);
+}
+
+}  // namespace xot

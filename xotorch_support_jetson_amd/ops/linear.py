@@ -1,21 +1,20 @@
 """Projection dispatch for the transformer: y = x @ W.T with a fused epilogue.
 
-GPU weights of the decode path are stored PRE-SHUFFLED (ops.weights_layout.shuffle_for_stream;
-tagged `w.xot_layout == "stream"`).  Per call:
+GPU weights are stored PRE-SHUFFLED (ops.weights_layout.shuffle_for_stream; tagged
+`w.xot_layout == "stream"`): 16-row x 32-k MFMA B-fragment blocks, 1 KB each.  Two library kernels
+consume that layout, both with the epilogue fused (bias / residual add / SiLU*mul):
 
-  M <= STREAM_MAX_M (decode batches, small prefill chunks)
-        gemm_stream: the library's weight-streaming MFMA GEMM on the shuffled layout (1 KB coalesced
-        weight loads per wave instruction, X shared through swizzled LDS) with the epilogue fused
-        (bias / residual add / SiLU*mul).  (ntw, split-K) is autotuned per shape on first use.  Above
-        128 rows the launch holds ceil(M/128) row blocks per column tile, dispatched onto one XCD
-        together so the weight tile is read from HBM once.
-  M > STREAM_MAX_M (prefill)
-        unshuffle the weight into a per-device scratch buffer and run hipBLASLt (torch.matmul/addmm)
-        + the library's epilogue kernel; the copy is ~5 % of a long prefill GEMM.
+  gemm_stream  decode-shaped M: weight-streaming MFMA GEMM (1 KB coalesced weight loads per wave
+               instruction straight to registers, X shared through swizzled LDS, optional split-K).
+  gemm_big     compute-bound M (large decode batches, prefill chunks): 256 x {256,128} x 64 tiles,
+               both operands staged by LDS-DMA, 8 waves, XCD-aware tile order, optional split-K.
+  ("blas")     long prefill chunks may instead copy the weight back to row-major scratch and run
+               hipBLASLt when that measures faster (copy included in the timing).
 
-Row-major (un-shuffled) GPU weights use the GemmPolicy (own skinny/tiled kernels vs hipBLASLt, timed
-once per shape).  CPU tensors use the fp32 reference.  Autotuning never runs inside a HIP-graph
-capture (the runner warms every captured shape up eagerly first).
+The configuration ((kernel, ntw|bn, split-K) per M bucket and shape) is chosen by cold-cache timing on
+first use; inside a HIP-graph capture a heuristic stands in (the runner warms every captured shape up
+eagerly first, so the timed choice is normally cached).  Row-major GPU weights use the GemmPolicy
+(own skinny/tiled kernels vs hipBLASLt).  CPU tensors use the fp32 reference.
 """
 from __future__ import annotations
 
@@ -36,9 +35,10 @@ from .weights_layout import can_shuffle, shuffle_for_stream, unshuffle_from_stre
 # workgroup is a serial tail on one CU).
 SPLITK_IN_LAUNCH = os.environ.get("XOT_SPLITK_IN_LAUNCH", "0") == "1"
 
-# largest M served by the stream GEMM (128-row blocks of one column tile share its weight reads through
-# L2); above it: unshuffled copy + hipBLASLt
+# largest M for which the stream GEMM is a candidate (above it only gemm_big is timed)
 STREAM_MAX_M = int(os.environ.get("XOT_STREAM_MAX_M", "512"))
+# smallest M for which gemm_big is a candidate
+BIG_MIN_M = int(os.environ.get("XOT_BIG_MIN_M", "65"))
 
 
 def _m_bucket(M: int) -> int:
@@ -104,7 +104,7 @@ class _Scratch:
       self.dense[idx] = t
     N, Kd = w.shape
     v = t[:n].view(N // 16, 16, Kd // 128, 4, 4, 8)
-    v.copy_(w.view(N // 16, Kd // 128, 4, 4, 16, 8).permute(0, 4, 1, 3, 2, 5))
+    v.copy_(w.view(N // 16, Kd // 128, 4, 4, 16, 8).permute(0, 4, 1, 2, 3, 5))
     return t[:n].view(N, Kd)
 
 
@@ -192,24 +192,45 @@ class GemmPolicy:
     return cands
 
   # ---------------------------------------------------------------- shuffled weights
-  def stream_cfg(self, x, w, bias, residual, epi, out_dtype) -> Tuple[int, int]:
+  @staticmethod
+  def _big_cands(M, N, Kd):
+    cands = []
+    tiles0 = -(-M // 256)
+    for bn in (256, 128):
+      if N % bn:
+        continue
+      tiles = tiles0 * (N // bn)
+      for S in (1, 2, 3, 4, 6, 8):
+        if S > 1 and (tiles >= 256 or tiles * S > 1024 or Kd // 64 < 2 * S):
+          continue
+        cands.append(("big", bn, S))
+    return cands
+
+  def shuffled_cfg(self, x, w, bias, residual, epi, out_dtype) -> Tuple:
+    """(kernel, ntw | bn, split-K) for a pre-shuffled weight at this M bucket."""
     M, Kd = x.shape
     N = w.shape[0]
-    key = ("st", _m_bucket(M), N, Kd, epi, bias is not None, str(out_dtype))
+    key = ("sh", _m_bucket(M), N, Kd, epi, bias is not None, str(out_dtype))
     got = self.table.get(key)
     if got is not None:
       return got
-    cands = self._stream_cands(M, N, Kd, epi)
+    cands = []
+    if M <= STREAM_MAX_M:
+      cands += [("stream",) + c for c in self._stream_cands(M, N, Kd, epi)]
+    if M >= BIG_MIN_M and Kd % 128 == 0:
+      cands += self._big_cands(M, N, Kd)
+    if M > STREAM_MAX_M and self.mode != "hip":
+      cands.append(("blas",))  # long prefill chunks: un-shuffled scratch copy + hipBLASLt
     if not cands:
-      raise RuntimeError(f"no stream-GEMM configuration for N={N} K={Kd}")
+      raise RuntimeError(f"no GEMM configuration for pre-shuffled N={N} K={Kd} M={M}")
     if self._no_tuning():
       return self._heuristic(M, N, cands)
-    scratch.splitk(x.device, 8 * max(M, 128) * N)
+    scratch.splitk(x.device, max(_ws_elems(c, M, N) for c in cands))
     y = torch.empty(M, N // 2 if epi == "silu" else N, dtype=out_dtype, device=x.device)
     times = {}
     for cfg in cands:
       try:
-        times[cfg] = self._time(lambda: _stream_call(x, w, bias, residual, epi, y, cfg))
+        times[cfg] = self._time(lambda: _shuffled_call(x, w, bias, residual, epi, y, cfg))
       except RuntimeError:
         pass
     got = min(times, key=times.get) if times else cands[0]
@@ -218,14 +239,31 @@ class GemmPolicy:
 
   @staticmethod
   def _heuristic(M, N, cands):
-    # enough workgroups to cover 256 CUs a few times
-    best = None
-    for ntw, S in cands:
-      wg = (N // (64 * ntw)) * S
-      score = abs(wg - 768)
+    if not any(c[0] in ("big", "stream") for c in cands):
+      return cands[0]
+    if M <= 128 or not any(c[0] == "big" for c in cands):
+      best = None  # stream GEMM: enough workgroups to cover 256 CUs a few times
+      for c in cands:
+        if c[0] != "stream":
+          continue
+        wg = (N // (64 * c[1])) * c[2]
+        score = abs(wg - 768)
+        if best is None or score < best[0]:
+          best = (score, c)
+      return best[1]
+    best = None  # big GEMM: split K until the tiles cover the CUs once
+    for c in cands:
+      if c[0] != "big":
+        continue
+      tiles = -(-M // 256) * (N // c[1]) * c[2]
+      score = abs(tiles - 256) + (0 if c[1] == 256 else 64)
       if best is None or score < best[0]:
-        best = (score, (ntw, S))
+        best = (score, c)
     return best[1]
+
+
+def _ws_elems(cfg, M, N) -> int:
+  return cfg[2] * M * N if len(cfg) == 3 and cfg[2] > 1 else 0
 
 
 policy = GemmPolicy()
@@ -237,6 +275,18 @@ def _stream_call(x, w, bias, residual, epi, out, cfg, shuffled: bool = True):
   ws = scratch.splitk(x.device, S * M * N) if S > 1 else None
   tk = scratch.tickets(x.device, (N // 64) * (-(-M // 128))) if S > 1 and SPLITK_IN_LAUNCH else None
   require().gemm_stream(x, w, out, bias, residual, ws, K.EPI[epi], ntw, S, shuffled, tk)
+  return out
+
+
+def _shuffled_call(x, w, bias, residual, epi, out, cfg):
+  if cfg[0] == "blas":
+    return _blas(x, scratch.dense_weight(w), bias, residual, epi, out, out.dtype if out is not None else None)
+  if cfg[0] == "stream":
+    return _stream_call(x, w, bias, residual, epi, out, cfg[1:])
+  _, bn, S = cfg
+  M, N = x.shape[0], w.shape[0]
+  ws = scratch.splitk(x.device, S * M * N) if S > 1 else None
+  require().gemm_big(x, w, out, bias, residual, ws, K.EPI[epi], bn, S)
   return out
 
 
@@ -295,12 +345,10 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, r
   if layout_of(w) != "stream":
     impl = policy.choose(x, w, bias, residual, epi, dt)
     return _run_rowmajor(impl, x, w, bias, residual, epi, out, out_dtype)
-  if M > STREAM_MAX_M:
-    return _blas(x, scratch.dense_weight(w), bias, residual, epi, out, out_dtype)
   if out is None:
     out = torch.empty(M, N // 2 if epi == "silu" else N, dtype=dt, device=x.device)
-  if x.stride(1) != 1:
+  if x.stride(1) != 1 or x.stride(0) % 8:
     x = x.contiguous()
-  cfg = policy.stream_cfg(x, w, bias, residual, epi, dt)
-  _stream_call(x, w, bias, residual, epi, out, cfg)
+  cfg = policy.shuffled_cfg(x, w, bias, residual, epi, dt)
+  _shuffled_call(x, w, bias, residual, epi, out, cfg)
   return out

@@ -49,10 +49,11 @@ class ShardRunner:
       torch.cuda.set_device(self.device)
     self.weights = weights if weights is not None else random_weights(config, shard, self.device, seed=seed)
     if self.device.type == "cuda" and os.environ.get("XOT_SHUFFLE", "1") == "1":
-      # projection weights -> pre-shuffled stream-GEMM layout; with decode batches above 128 rows the
-      # wide qkv / gate-up projections stay row-major for hipBLASLt (XOT_ROWMAJOR_PROJ overrides)
+      # projection weights -> pre-shuffled MFMA-fragment layout (gemm_stream for decode-shaped M,
+      # gemm_big for large batches); with decode batches above 128 rows the gate/up projection stays
+      # row-major, where hipBLASLt measures faster (ops/linear.py; XOT_ROWMAJOR_PROJ overrides)
       env = os.environ.get("XOT_ROWMAJOR_PROJ")
-      keep = [p for p in env.split(",") if p] if env is not None else (["qkv", "gu"] if max_batch > 128 else [])
+      keep = [p for p in env.split(",") if p] if env is not None else (["gu"] if max_batch > 128 else [])
       prepare_for_decode(self.weights, keep_rowmajor=keep)
     n_layers = shard.get_layer_count()
     per_page = KVCache.bytes_per_page(config, n_layers)
