@@ -135,10 +135,13 @@ def test_attn_decode(gpu, H, Hkv, Dh, ctx):
   q = torch.randn(B, H, Dh, device=gpu, dtype=torch.bfloat16)
   scale = 1 / math.sqrt(Dh)
   ref = R.attn_decode(q, kc, vc, bt, cl, scale)
-  for ppp in (4, 8):
-    ws = K.DecodeWorkspace(B, H, Dh, maxb * 64, gpu, pages_per_part=ppp)
-    out = K.attn_decode(q, kc, vc, bt, cl, scale, ws)
-    assert rel_err(out, ref) < 2e-2, ppp
+  for algo in (0, 1, 2):  # workgroup kernel; wave kernel without / with page prefetch
+    for ppp in (1, 3, 4, 8, None):  # None: per-call choice from the batch
+      if algo == 0 and ppp in (1, 3):
+        continue
+      ws = K.DecodeWorkspace(B, H, Dh, maxb * 64, gpu, pages_per_part=ppp, algo=algo)
+      out = K.attn_decode(q, kc, vc, bt, cl, scale, ws)
+      assert rel_err(out, ref) < 2e-2, (algo, ppp)
 
 
 @pytest.mark.parametrize("H,Hkv,Dh", [(32, 8, 64), (64, 8, 128), (14, 2, 64)])

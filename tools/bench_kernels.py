@@ -107,12 +107,15 @@ def main():
     bt = torch.arange(B * npg, device=dev, dtype=torch.int32).view(B, npg)
     cl = torch.full((B,), ctx, device=dev, dtype=torch.int32)
     q = torch.randn(B, H, Dh, device=dev, dtype=torch.bfloat16)
-    ppp = K.choose_pages_per_part(B, Hkv, ctx)
-    ws = K.DecodeWorkspace(B, H, Dh, ctx, dev, ppp)
     out = torch.empty_like(q)
-    t = timeit(lambda: K.attn_decode(q, kc, vc, bt, cl, 1 / math.sqrt(Dh), ws, out))
     bytes_ = 2 * B * ctx * Hkv * Dh * 2
-    r = dict(B=B, ctx=ctx, us=t * 1e6, gbps=bytes_ / t / 1e9, pages_per_part=ppp)
+    r = dict(B=B, ctx=ctx)
+    for algo in (0, 1, 2, -1):
+      ws = K.DecodeWorkspace(B, H, Dh, ctx, dev, algo=algo)
+      t = timeit(lambda: K.attn_decode(q, kc, vc, bt, cl, 1 / math.sqrt(Dh), ws, out))
+      r[f"us_a{algo}"] = round(t * 1e6, 1)
+      r[f"gbps_a{algo}"] = round(bytes_ / t / 1e9, 1)
+      r[f"ppp_a{algo}"] = ws.partition(B, Hkv, npg)[0]
     res["attn_decode"].append(r)
     print(json.dumps({"attn_decode": r}), flush=True)
     del kc, vc

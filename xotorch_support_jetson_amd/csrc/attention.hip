@@ -206,14 +206,183 @@ __global__ __launch_bounds__(DH) void attn_decode_reduce_kernel(const float* __r
   out[(size_t)bh * DH + d] = f2bf(L > 0.f ? O / L : 0.f);
 }
 
+// ---------------------------------------------------------------------------- decode, wave per unit
+// One wave owns one (sequence, KV head, KV partition) unit -- no intra-workgroup combine, and units are
+// balanced to the page.  Transposed formulation: S^T = K . Q^T (A = 16 keys of K, B = the G query
+// heads as columns) so each lane's accumulator column IS one query head: the running max / sum /
+// rescale are lane-local scalars, and the probabilities P^T come out of the S^T accumulators already
+// in the B-operand layout of O^T += V^T . P^T.  The key held by MFMA row c of score tile t is chosen
+// so that this works with contiguous V^T reads: tile t = 2kk + h, row c = 4q + r holds key
+// 32kk + 8q + 4h + r, hence lane group g of the P^T operand owns keys 32kk + 8g .. +8 and reads one
+// 16-byte run of the transposed V page.  No LDS.
+// PF: prefetch the next page's K / V into registers under the current page's math.
+template <int DH, bool PF>
+__global__ __launch_bounds__(256) void attn_decode_wave_kernel(
+    const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
+    const int32_t* __restrict__ block_tables, int max_blocks, const int32_t* __restrict__ ctx_lens,
+    uint16_t* __restrict__ out, float* __restrict__ ws_o, float* __restrict__ ws_ml, int B, int H, int Hkv,
+    int pages_per_part, int nparts, float scale_log2, int num_pages) {
+  constexpr int KS = DH / 32;   // k-steps of S^T over the head dim
+  constexpr int NDT = DH / 16;  // 16-row d tiles of O^T
+  const int lane = threadIdx.x & 63;
+  const int g = lane >> 4, c = lane & 15;
+  const int unit = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (unit >= B * Hkv * nparts) return;  // whole wave
+  const int part = unit % nparts, kvh = (unit / nparts) % Hkv, b = unit / (nparts * Hkv);
+  const int G = H / Hkv;
+  const int ctx = min(max(ctx_lens[b], 0), max_blocks * PAGE);
+  const int npages = (ctx + PAGE - 1) / PAGE;
+  const int p_begin = part * pages_per_part;
+  const int p_end = min(npages, p_begin + pages_per_part);
+
+  // Q^T (B operand): column c = query head kvh*G + c; lane group g owns d in [8*KS*g, 8*KS*(g+1)).
+  s16x8 qf[KS];
+  {
+    const bool ok = c < G;
+    const uint16_t* qp = q + ((size_t)b * H + kvh * G + (ok ? c : 0)) * DH + g * 8 * KS;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      s16x8 v = ld16(qp + 8 * s);
+      qf[s] = ok ? v : s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  }
+  float m = NEG_BIG, l = 0.f;
+  f32x4 o[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int32_t* bt = block_tables + (size_t)b * max_blocks;
+  // K page [64 keys][DH]: score tile t = 2kk + h, lane (g, c) reads key 32kk + 8(c/4) + 4h + c%4,
+  //   d [8*KS*g, +8*KS) (contiguous 16*KS bytes)
+  // V^T page [DH][64 keys]: d tile dt, k-step kk, lane (g, c) reads d 16dt + c, keys 32kk + 8g .. +8
+  const int krow = 8 * (c >> 2) + (c & 3);
+  auto load = [&](int p, s16x8 (&kf)[4][KS], s16x8 (&vf)[NDT][2]) {
+    const long page = min(max(bt[p], 0), num_pages - 1);
+    const uint16_t* kb = kc + ((size_t)page * Hkv + kvh) * PAGE * DH + krow * DH + g * 8 * KS;
+    const uint16_t* vb = vc + ((size_t)page * Hkv + kvh) * DH * PAGE + c * PAGE + 8 * g;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int s = 0; s < KS; ++s) kf[t][s] = ld16(kb + (32 * (t >> 1) + 4 * (t & 1)) * DH + 8 * s);
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) vf[dt][kk] = ld16(vb + 16 * dt * PAGE + 32 * kk);
+  };
+  auto compute = [&](int p, const s16x8 (&kf)[4][KS], const s16x8 (&vf)[NDT][2]) {
+    f32x4 st[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      st[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < KS; ++s) st[t] = mfma16(kf[t][s], qf[s], st[t]);
+    }
+    const int key0 = p * PAGE + 8 * g;  // + 32kk + 4h + r
+    float mx = NEG_BIG;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = key0 + 32 * (t >> 1) + 4 * (t & 1) + r < ctx ? st[t][r] * scale_log2 : -INFINITY;
+        st[t][r] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mn = fmaxf(m, mx);
+    const float alpha = exp2f(m - mn);
+    m = mn;
+    l *= alpha;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) o[dt] *= alpha;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      s16x8 pf;
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float pv = exp2f(st[2 * kk + h][r] - mn);
+          l += pv;
+          pf[4 * h + r] = (short)f2bf(pv);
+        }
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) o[dt] = mfma16(vf[dt][kk], pf, o[dt]);
+    }
+  };
+
+  if constexpr (PF) {
+    s16x8 ka[4][KS], kb2[4][KS];
+    s16x8 va[NDT][2], vb2[NDT][2];
+    int p = p_begin;
+    if (p < p_end) load(p, ka, va);
+    for (; p + 1 < p_end; p += 2) {
+      load(p + 1, kb2, vb2);
+      compute(p, ka, va);
+      if (p + 2 < p_end) load(p + 2, ka, va);
+      compute(p + 1, kb2, vb2);
+    }
+    if (p < p_end) compute(p, ka, va);
+  } else {
+    for (int p = p_begin; p < p_end; ++p) {
+      s16x8 kf[4][KS], vf[NDT][2];
+      load(p, kf, vf);
+      compute(p, kf, vf);
+    }
+  }
+
+  // lane (g, c): head c, d rows 16dt + 4g + r
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+  if (c >= G) return;
+  const int h = kvh * G + c;
+  if (nparts == 1) {
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    uint16_t* op = out + ((size_t)b * H + h) * DH + 4 * g;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) {
+      s16x4 v;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = (short)f2bf(o[dt][r] * inv);
+      *reinterpret_cast<s16x4*>(op + 16 * dt) = v;
+    }
+  } else {
+    const size_t idx = ((size_t)b * H + h) * nparts + part;
+    float* wo = ws_o + idx * DH + 4 * g;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) *reinterpret_cast<f32x4*>(wo + 16 * dt) = o[dt];
+    if (g == 0) {
+      ws_ml[idx * 2] = m;
+      ws_ml[idx * 2 + 1] = l;
+    }
+  }
+}
+
 int launch_attn_decode(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, const int32_t* block_tables,
                        int max_blocks, const int32_t* ctx_lens, uint16_t* out, float* ws_o, float* ws_ml, int B,
-                       int H, int Hkv, int Dh, int pages_per_part, int nparts, float scale, int num_pages,
+                       int H, int Hkv, int Dh, int pages_per_part, int nparts, float scale, int num_pages, int algo,
                        hipStream_t s) {
   if (B <= 0) return 0;
   if (H % Hkv != 0 || H / Hkv > 16) return -1;
   dim3 grid(nparts, Hkv, B);
   const float sl = scale * LOG2E;
+  if (algo != 0) {  // wave per (sequence, KV head, partition)
+    const int units = B * Hkv * nparts, wgs = (units + 3) / 4;
+#define XOT_WAVE(DHV, PFV)                                                                                       \
+  attn_decode_wave_kernel<DHV, PFV><<<wgs, 256, 0, s>>>(q, kc, vc, block_tables, max_blocks, ctx_lens, out, ws_o, \
+                                                        ws_ml, B, H, Hkv, pages_per_part, nparts, sl, num_pages)
+    if (Dh == 128) {
+      if (algo == 2) XOT_WAVE(128, true); else XOT_WAVE(128, false);
+      if (nparts > 1) attn_decode_reduce_kernel<128><<<B * H, 128, 0, s>>>(ws_o, ws_ml, ctx_lens, out, H, nparts, pages_per_part);
+    } else if (Dh == 64) {
+      if (algo == 2) XOT_WAVE(64, true); else XOT_WAVE(64, false);
+      if (nparts > 1) attn_decode_reduce_kernel<64><<<B * H, 64, 0, s>>>(ws_o, ws_ml, ctx_lens, out, H, nparts, pages_per_part);
+    } else {
+      return -1;
+    }
+#undef XOT_WAVE
+    return 0;
+  }
   if (Dh == 128) {
     attn_decode_kernel<128><<<grid, 256, 0, s>>>(q, kc, vc, block_tables, max_blocks, ctx_lens, out, ws_o, ws_ml,
                                                  H, Hkv, pages_per_part, nparts, sl, num_pages);

@@ -352,7 +352,7 @@ void moe_combine(const at::Tensor& y, const at::Tensor& slot_of, const at::Tenso
 
 void attn_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
                  const at::Tensor& block_tables, const at::Tensor& ctx_lens, at::Tensor& out, at::Tensor& ws_o,
-                 at::Tensor& ws_ml, int64_t pages_per_part, int64_t nparts, double scale) {
+                 at::Tensor& ws_ml, int64_t pages_per_part, int64_t nparts, double scale, int64_t algo) {
   CHECK_BF16(q);
   CHECK_BF16(k_cache);
   CHECK_BF16(v_cache);
@@ -376,7 +376,7 @@ void attn_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tenso
   const int rc = xot::launch_attn_decode(bf(q), bf(k_cache), bf(v_cache), block_tables.data_ptr<int32_t>(),
                                          (int)block_tables.size(1), ctx_lens.data_ptr<int32_t>(), bf(out),
                                          ws_o.data_ptr<float>(), ws_ml.data_ptr<float>(), (int)B, (int)H, (int)Hkv,
-                                         (int)Dh, (int)pages_per_part, (int)nparts, (float)scale, (int)nb,
+                                         (int)Dh, (int)pages_per_part, (int)nparts, (float)scale, (int)nb, (int)algo,
                                          cur_stream());
   XCHECK(rc == 0, "attn_decode: unsupported H=", H, " Hkv=", Hkv, " Dh=", Dh);
 }
@@ -492,7 +492,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_moe", &gemm_moe);
   m.def("moe_route", &moe_route);
   m.def("moe_combine", &moe_combine);
-  m.def("attn_decode", &attn_decode);
+  m.def("attn_decode", &attn_decode, py::arg("q"), py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"),
+        py::arg("ctx_lens"), py::arg("out"), py::arg("ws_o"), py::arg("ws_ml"), py::arg("pages_per_part"),
+        py::arg("nparts"), py::arg("scale"), py::arg("algo") = 2);
   m.def("attn_prefill", &attn_prefill);
   m.def("sample", &sample);
   m.def("ce_fwd", &ce_fwd);

@@ -297,7 +297,7 @@ static int big_dispatch(const uint16_t* X, int ldx, const uint16_t* W, const uin
                         int ldr, void* Y, int ldy, float* ws, long ws_elems, int M, int N, int K, int bn, int S,
                         hipStream_t st) {
   if (bn == 256)
-    big_launch<256, 2, 4, 32, 4, EPI, F32>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, S, st);
+    big_launch<256, 2, 4, 64, 2, EPI, F32>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, S, st);
   else if (bn == 128)
     big_launch<128, 4, 2, 64, 3, EPI, F32>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, S, st);
   else

@@ -47,7 +47,7 @@ int launch_gemm_tiled(const uint16_t* X, int ldx, const uint16_t* W, int ldw, co
 
 int launch_attn_decode(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, const int32_t* block_tables,
                        int max_blocks, const int32_t* ctx_lens, uint16_t* out, float* ws_o, float* ws_ml, int B,
-                       int H, int Hkv, int Dh, int pages_per_part, int nparts, float scale, int num_pages,
+                       int H, int Hkv, int Dh, int pages_per_part, int nparts, float scale, int num_pages, int algo,
                        hipStream_t s);
 int launch_attn_prefill(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, const int32_t* block_tables,
                         int max_blocks, const int32_t* cu_q, const int32_t* ctx_lens, uint16_t* out, int B,

@@ -88,8 +88,7 @@ class ShardModel:
     self.max_ctx = max_ctx
     self.ws = None
     if self.device.type == "cuda":
-      ppp = K.choose_pages_per_part(max_batch, c.num_kv_heads, max_ctx)
-      self.ws = K.DecodeWorkspace(max_batch, c.num_heads, c.head_dim, max_ctx, self.device, ppp)
+      self.ws = K.DecodeWorkspace(max_batch, c.num_heads, c.head_dim, max_ctx, self.device)
 
   # ------------------------------------------------------------------ helpers
   def _attention(self, q: torch.Tensor, li: int, inp: StepInputs) -> torch.Tensor:

@@ -7,6 +7,8 @@ raises (see `ops._ext.require`).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import reference as ref
@@ -142,23 +144,63 @@ def rope_apply(x: torch.Tensor, pos: torch.Tensor, cos_sin: torch.Tensor, nh: in
 
 
 # ------------------------------------------------------------------ attention
-class DecodeWorkspace:
-  """Split-KV scratch for attn_decode (sized once for the largest batch / context)."""
-
-  def __init__(self, max_batch: int, H: int, Dh: int, max_ctx: int, device, pages_per_part: int = 8):
-    self.pages_per_part = pages_per_part
-    self.nparts = max(1, -(-max_ctx // (PAGE * pages_per_part)))
-    self.o = torch.empty(max_batch * H * self.nparts * Dh, dtype=torch.float32, device=device)
-    self.ml = torch.empty(max_batch * H * self.nparts * 2, dtype=torch.float32, device=device)
+# 0: workgroup per (sequence, KV head, partition), waves split pages + LDS combine
+# 1 / 2: wave per (sequence, KV head, partition), transposed S^T (lane = query head), no LDS;
+#        2 prefetches the next page under the current one
+# -1 (default): 0 below 64 (sequence, KV head) pairs -- few long sequences, where the workgroup
+#        kernel's 4-wave page split needs fewer partitions -- else 2 (measured: tools/bench_kernels.py)
+DECODE_ALGO = int(os.environ.get("XOT_ATTN_DECODE", "-1"))
 
 
-def choose_pages_per_part(batch: int, Hkv: int, max_ctx: int) -> int:
-  """Enough workgroups to cover 256 CUs several times, but >= 4 pages (one per wave) per partition."""
+def resolve_decode_algo(batch: int, Hkv: int, algo: int | None = None) -> int:
+  algo = DECODE_ALGO if algo is None else algo
+  if algo < 0:
+    return 0 if batch * Hkv < 64 else 2
+  return algo
+
+
+def choose_pages_per_part(batch: int, Hkv: int, max_ctx: int, algo: int | None = None) -> int:
+  """KV pages per split-KV partition for a decode step of `batch` sequences."""
+  algo = resolve_decode_algo(batch, Hkv, algo)
   pages = max(1, -(-max_ctx // PAGE))
-  for ppp in (16, 8, 4):
-    if batch * Hkv * -(-pages // ppp) >= 1024:
-      return ppp
-  return 4
+  if algo == 0:  # enough workgroups to cover 256 CUs several times, >= 4 pages (one per wave) each
+    for ppp in (16, 8, 4):
+      if batch * Hkv * -(-pages // ppp) >= 1024:
+        return ppp
+    return 4
+  # one wave per unit: >= 2048 waves in flight (8 per CU), partitions of >= 2 pages
+  nparts = max(1, min(max(pages // 2, 1), -(-2048 // max(batch * Hkv, 1))))
+  return -(-pages // nparts)
+
+
+class DecodeWorkspace:
+  """Split-KV scratch for attn_decode, sized for every batch up to max_batch at this context bound.
+  The partitioning is chosen per call from the actual batch (static per captured graph)."""
+
+  def __init__(self, max_batch: int, H: int, Dh: int, max_ctx: int, device, pages_per_part: int | None = None,
+               algo: int | None = None):
+    self.algo = DECODE_ALGO if algo is None else algo
+    self.max_ctx = max_ctx
+    self.Hkv_hint = None
+    self.fixed_ppp = pages_per_part
+    pages = max(1, -(-max_ctx // PAGE))
+    worst = 1
+    for b in range(1, max_batch + 1):
+      for hkv in (1, 2, 4, 8, 16):
+        ppp = pages_per_part or choose_pages_per_part(b, hkv, max_ctx, self.algo)
+        worst = max(worst, b * -(-pages // ppp))
+    self.units = worst  # max over batch of batch * nparts
+    self.o = torch.empty(worst * H * Dh, dtype=torch.float32, device=device)
+    self.ml = torch.empty(worst * H * 2, dtype=torch.float32, device=device)
+
+  def partition(self, batch: int, Hkv: int, width_pages: int):
+    """(pages per partition, partitions, kernel) for this call."""
+    algo = resolve_decode_algo(batch, Hkv, self.algo)
+    ppp = self.fixed_ppp or choose_pages_per_part(batch, Hkv, width_pages * PAGE, algo)
+    nparts = max(1, -(-width_pages // ppp))
+    if batch * nparts > self.units:
+      raise RuntimeError(f"decode workspace sized for {self.units} units, need {batch * nparts}")
+    return ppp, nparts, algo
 
 
 def attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale: float, ws: DecodeWorkspace | None = None,
@@ -170,11 +212,13 @@ def attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale: float, ws: D
       return out
     return y
   B, H, Dh = q.shape
+  width = block_tables.shape[1]
   if ws is None:
-    ws = DecodeWorkspace(B, H, Dh, block_tables.shape[1] * PAGE, q.device)
+    ws = DecodeWorkspace(B, H, Dh, width * PAGE, q.device)
+  ppp, nparts, algo = ws.partition(B, k_cache.shape[1], width)
   out = torch.empty_like(q) if out is None else out
-  require().attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, out, ws.o, ws.ml, ws.pages_per_part, ws.nparts,
-                        float(scale))
+  require().attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, out, ws.o, ws.ml, ppp, nparts, float(scale),
+                        algo)
   return out
 
 
