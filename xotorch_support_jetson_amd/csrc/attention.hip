@@ -226,7 +226,9 @@ __global__ __launch_bounds__(256) void attn_decode_wave_kernel(
   constexpr int NDT = DH / 16;  // 16-row d tiles of O^T
   const int lane = threadIdx.x & 63;
   const int g = lane >> 4, c = lane & 15;
-  const int unit = blockIdx.x * 4 + (threadIdx.x >> 6);
+  // wave-uniform unit id in an SGPR: page indices and block-table reads stay scalar (s_load, counted by
+  // lgkmcnt), so they never force a vmcnt(0) drain of the K / V prefetch
+  const int unit = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
   if (unit >= B * Hkv * nparts) return;  // whole wave
   const int part = unit % nparts, kvh = (unit / nparts) % Hkv, b = unit / (nparts * Hkv);
   const int G = H / Hkv;
@@ -235,14 +237,15 @@ __global__ __launch_bounds__(256) void attn_decode_wave_kernel(
   const int p_begin = part * pages_per_part;
   const int p_end = min(npages, p_begin + pages_per_part);
 
-  // Q^T (B operand): column c = query head kvh*G + c; lane group g owns d in [8*KS*g, 8*KS*(g+1)).
+  // Q^T (B operand): column c = query head kvh*G + c; k-step s, lane group g: d 32s + 8g .. +8
+  // (natural MFMA order, so each K load instruction below reads 64 contiguous bytes of 16 rows).
   s16x8 qf[KS];
   {
     const bool ok = c < G;
-    const uint16_t* qp = q + ((size_t)b * H + kvh * G + (ok ? c : 0)) * DH + g * 8 * KS;
+    const uint16_t* qp = q + ((size_t)b * H + kvh * G + (ok ? c : 0)) * DH + g * 8;
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
-      s16x8 v = ld16(qp + 8 * s);
+      s16x8 v = ld16(qp + 32 * s);
       qf[s] = ok ? v : s16x8{0, 0, 0, 0, 0, 0, 0, 0};
     }
   }
@@ -253,17 +256,17 @@ __global__ __launch_bounds__(256) void attn_decode_wave_kernel(
 
   const int32_t* bt = block_tables + (size_t)b * max_blocks;
   // K page [64 keys][DH]: score tile t = 2kk + h, lane (g, c) reads key 32kk + 8(c/4) + 4h + c%4,
-  //   d [8*KS*g, +8*KS) (contiguous 16*KS bytes)
+  //   d 32s + 8g .. +8 for k-step s
   // V^T page [DH][64 keys]: d tile dt, k-step kk, lane (g, c) reads d 16dt + c, keys 32kk + 8g .. +8
   const int krow = 8 * (c >> 2) + (c & 3);
   auto load = [&](int p, s16x8 (&kf)[4][KS], s16x8 (&vf)[NDT][2]) {
     const long page = min(max(bt[p], 0), num_pages - 1);
-    const uint16_t* kb = kc + ((size_t)page * Hkv + kvh) * PAGE * DH + krow * DH + g * 8 * KS;
+    const uint16_t* kb = kc + ((size_t)page * Hkv + kvh) * PAGE * DH + krow * DH + g * 8;
     const uint16_t* vb = vc + ((size_t)page * Hkv + kvh) * DH * PAGE + c * PAGE + 8 * g;
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int s = 0; s < KS; ++s) kf[t][s] = ld16(kb + (32 * (t >> 1) + 4 * (t & 1)) * DH + 8 * s);
+      for (int s = 0; s < KS; ++s) kf[t][s] = ld16(kb + (32 * (t >> 1) + 4 * (t & 1)) * DH + 32 * s);
 #pragma unroll
     for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
