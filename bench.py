@@ -120,7 +120,8 @@ def main():
   ms_step = elapsed / args.steps * 1e3
   if rank == 0:
     out = {
-      "metric": "output tokens/sec (whole node) Llama-3-70B ring-sharded across 1/2/4/8 MI355X",
+      "metric": ("output tokens/sec (whole node) Llama-3-70B ring-sharded across 1/2/4/8 MI355X"
+                 if args.model == "llama-3-70b" else f"output tokens/sec (whole node) {args.model} ring-sharded"),
       "value": round(tps, 2),
       "unit": "tokens/s",
       "n_gpus": world,

@@ -378,8 +378,9 @@ def test_moe_layer(gpu, T, E, k, shuffled):
   dw = torch.stack([shuffle_for_stream(down[e]) for e in range(E)]) if shuffled else down
   act = torch.empty(T * k, F, dtype=torch.bfloat16, device=gpu)
   C.gemm_moe(x, gw, act, off, sorted_tok, 2, T, shuffled)
-  y = torch.empty(T * k, D, dtype=torch.float32, device=gpu)
-  C.gemm_moe(act, dw, y, off, None, 0, T, shuffled)
-  out = h.clone()
-  C.moe_combine(y, slot_of, topw, out)
-  assert rel_err(out.float() - h.float(), ref - h.float()) < 3e-2  # the MoE contribution itself
+  for S in (1, 2):  # down projection whole, and split over K into two fp32 slabs summed by the combine
+    y = torch.empty(S * T * k, D, dtype=torch.float32, device=gpu)
+    C.gemm_moe(act, dw, y, off, None, 0, T, shuffled, S)
+    out = h.clone()
+    C.moe_combine(y, slot_of, topw, out, S)
+    assert rel_err(out.float() - h.float(), ref - h.float()) < 3e-2, S  # the MoE contribution itself

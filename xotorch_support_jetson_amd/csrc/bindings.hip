@@ -288,8 +288,10 @@ void gemm_big(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const c10
 }
 
 // grouped expert GEMM: y[slot] = x[gather ? gather[slot] : slot] @ w[e].T for slots of expert e
+// splits > 1 (fp32 output, no epilogue): K slice s writes rows [s*slots, (s+1)*slots) of y ([splits*slots, N]),
+// summed by moe_combine(..., splits)
 void gemm_moe(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const at::Tensor& off,
-              const c10::optional<at::Tensor>& gather, int64_t epi, int64_t max_rows, bool wshuf) {
+              const c10::optional<at::Tensor>& gather, int64_t epi, int64_t max_rows, bool wshuf, int64_t splits) {
   CHECK_BF16(x);
   CHECK_BF16(w);
   CHECK_GPU(y);
@@ -304,20 +306,22 @@ void gemm_moe(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const at:
   const bool f32 = y.scalar_type() == at::kFloat;
   XCHECK(f32 || y.scalar_type() == at::kBFloat16, "gemm_moe: y must be bf16 or fp32");
   XCHECK(y.size(1) == (epi == 2 ? N / 2 : N), "gemm_moe: y width mismatch");
-  XCHECK(max_rows >= 0 && max_rows <= y.size(0), "gemm_moe: max_rows must be <= slots");
+  XCHECK(splits >= 1 && y.size(0) % splits == 0, "gemm_moe: y rows must be splits * slots");
+  const int64_t slots = y.size(0) / splits;
+  XCHECK(max_rows >= 0 && max_rows <= slots, "gemm_moe: max_rows must be <= slots");
   const int* gp = nullptr;
   if (gather.has_value()) {
     CHECK_GPU((*gather));
     CHECK_DT((*gather), at::kInt);
-    XCHECK(gather->is_contiguous() && gather->numel() == y.size(0), "gemm_moe: gather must have one entry per slot");
+    XCHECK(gather->is_contiguous() && gather->numel() == slots, "gemm_moe: gather must have one entry per slot");
     gp = gather->data_ptr<int>();
   } else {
-    XCHECK(x.size(0) == y.size(0), "gemm_moe: without gather, x rows are slots");
+    XCHECK(x.size(0) == slots, "gemm_moe: without gather, x rows are slots");
   }
   const int rc = xot::launch_gemm_moe(bf(x), (int)x.stride(0), bf(w), y.data_ptr(), (int)y.stride(0), f32, (int)epi,
                                       off.data_ptr<int>(), gp, (int)E, (int)max_rows, (int)N, (int)K, wshuf,
-                                      cur_stream());
-  XCHECK(rc == 0, "gemm_moe: unsupported shape N=", N, " K=", K, " epi=", epi);
+                                      (int)splits, (long)(slots * y.size(1)), cur_stream());
+  XCHECK(rc == 0, "gemm_moe: unsupported shape N=", N, " K=", K, " epi=", epi, " splits=", splits);
 }
 
 void moe_route(const at::Tensor& logits, int64_t k, at::Tensor& topw, at::Tensor& topi, at::Tensor& slot_of,
@@ -339,15 +343,17 @@ void moe_route(const at::Tensor& logits, int64_t k, at::Tensor& topw, at::Tensor
                         slot_of.data_ptr<int>(), sorted_tok.data_ptr<int>(), off.data_ptr<int>(), cur_stream());
 }
 
-void moe_combine(const at::Tensor& y, const at::Tensor& slot_of, const at::Tensor& topw, at::Tensor& h) {
+void moe_combine(const at::Tensor& y, const at::Tensor& slot_of, const at::Tensor& topw, at::Tensor& h,
+                 int64_t splits) {
   CHECK_GPU(y);
   CHECK_DT(y, at::kFloat);
   CHECK_BF16(h);
   XCHECK(all_contig_gpu(y, slot_of, topw, h), "moe_combine: tensors must be contiguous GPU");
   const int64_t T = h.size(0), D = h.size(1), k = slot_of.numel() / T;
-  XCHECK(D % 8 == 0 && y.size(1) == D && y.size(0) == T * k && topw.numel() == T * k, "moe_combine: shapes");
+  XCHECK(splits >= 1 && D % 8 == 0 && y.size(1) == D && y.size(0) == splits * T * k && topw.numel() == T * k,
+         "moe_combine: shapes");
   xot::launch_moe_combine(y.data_ptr<float>(), slot_of.data_ptr<int>(), topw.data_ptr<float>(), bf(h), (int)T, (int)k,
-                          (int)D, cur_stream());
+                          (int)D, (int)splits, (long)(T * k * D), cur_stream());
 }
 
 void attn_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
@@ -489,9 +495,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("tickets") = py::none());
   m.def("gemm_big", &gemm_big, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("bias"), py::arg("res"),
         py::arg("ws"), py::arg("epi"), py::arg("bn"), py::arg("splits"));
-  m.def("gemm_moe", &gemm_moe);
+  m.def("gemm_moe", &gemm_moe, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("off"), py::arg("gather"),
+        py::arg("epi"), py::arg("max_rows"), py::arg("wshuf"), py::arg("splits") = 1);
   m.def("moe_route", &moe_route);
-  m.def("moe_combine", &moe_combine);
+  m.def("moe_combine", &moe_combine, py::arg("y"), py::arg("slot_of"), py::arg("topw"), py::arg("h"),
+        py::arg("splits") = 1);
   m.def("attn_decode", &attn_decode, py::arg("q"), py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"),
         py::arg("ctx_lens"), py::arg("out"), py::arg("ws_o"), py::arg("ws_ml"), py::arg("pages_per_part"),
         py::arg("nparts"), py::arg("scale"), py::arg("algo") = 2);

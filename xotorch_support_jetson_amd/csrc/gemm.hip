@@ -205,7 +205,7 @@ __global__ __launch_bounds__(256, OCC) void gemm_stream_kernel(const uint16_t* _
                                                              float* __restrict__ ws, int M, int N, int kper,
                                                              int mblocks, const int* __restrict__ moe_off,
                                                              const int* __restrict__ moe_gather,
-                                                             int* __restrict__ tickets) {
+                                                             int* __restrict__ tickets, long ysplit) {
   constexpr int KC = 32 * KS;
   constexpr int CPR = KC / 8;  // 16-B chunks per row per k-chunk
   constexpr int NTH = 256;
@@ -241,6 +241,11 @@ __global__ __launch_bounds__(256, OCC) void gemm_stream_kernel(const uint16_t* _
     M = moe_off[e + 1] - row0;  // this expert's rows
     W += (size_t)e * N * ldw;
     if (mb * ROWS >= M) return;  // uniform over the workgroup, before any barrier
+  }
+  // grouped GEMM split over K: K slice blockIdx.y writes its own fp32 slab of Y (ysplit elements apart),
+  // summed by the consumer (moe_combine_kernel)
+  if constexpr (MOE != 0) {
+    if (ysplit != 0) Yv = reinterpret_cast<float*>(Yv) + (size_t)blockIdx.y * ysplit;
   }
   const int Mtot = M, m_base = mb * ROWS;
   M = min(ROWS, Mtot - m_base);
@@ -478,7 +483,7 @@ static void stream_launch(const uint16_t* X, int ldx, const uint16_t* W, int ldw
       (void)attr;
     }
     kern<<<grid, 256, SMEM, st>>>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, nullptr, M, N, kper, mblocks, nullptr, nullptr,
-                                  nullptr);
+                                  nullptr, 0L);
   } else {
     auto kern = gemm_stream_kernel<MT, NTW, KS, EPI, F32, true, WSH, OCC, 0>;
     if constexpr (SMEM > 65536) {
@@ -487,7 +492,7 @@ static void stream_launch(const uint16_t* X, int ldx, const uint16_t* W, int ldw
       (void)attr;
     }
     kern<<<grid, 256, SMEM, st>>>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, M, N, kper, mblocks, nullptr, nullptr,
-                                  tickets);
+                                  tickets, 0L);
     if (tickets != nullptr) return;  // combined in-launch
     const int ncol = EPI == EPI_SILU ? N / 2 : N;
     long chunks = (long)M * (ncol / 8);
@@ -544,44 +549,46 @@ static int stream_dispatch(const uint16_t* X, int ldx, const uint16_t* W, int ld
 // ------------------------------------------------------------------------------------ grouped (MoE)
 template <int MT, int EPI, bool F32, bool WSH, int MOE>
 static void moe_launch(const uint16_t* X, int ldx, const uint16_t* W, void* Y, int ldy, const int* off,
-                       const int* gather, int E, int max_rows, int N, int K, hipStream_t st) {
+                       const int* gather, int E, int max_rows, int N, int K, int S, long ysplit, hipStream_t st) {
   constexpr int NTW = 2, KS = 4;
   constexpr int OCC = (MT * NTW >= 32) ? 1 : 2;
   constexpr int SMEM = 2 * 16 * MT * 32 * KS * 2;
   const int mblocks = (max_rows + 16 * MT - 1) / (16 * MT);
-  dim3 grid(N / (64 * NTW) * mblocks, 1, E);
+  dim3 grid(N / (64 * NTW) * mblocks, S, E);
   gemm_stream_kernel<MT, NTW, KS, EPI, F32, false, WSH, OCC, MOE><<<grid, 256, SMEM, st>>>(
-      X, ldx, W, K, nullptr, nullptr, 0, Y, ldy, nullptr, max_rows, N, K, mblocks, off, gather, nullptr);
+      X, ldx, W, K, nullptr, nullptr, 0, Y, ldy, nullptr, max_rows, N, K / S, mblocks, off, gather, nullptr,
+      S > 1 ? ysplit : 0L);
 }
 
 template <int EPI, bool F32, bool WSH, int MOE>
 static void moe_mt(const uint16_t* X, int ldx, const uint16_t* W, void* Y, int ldy, const int* off,
-                   const int* gather, int E, int max_rows, int N, int K, hipStream_t st) {
+                   const int* gather, int E, int max_rows, int N, int K, int S, long ysplit, hipStream_t st) {
   if (max_rows <= 16)
-    moe_launch<1, EPI, F32, WSH, MOE>(X, ldx, W, Y, ldy, off, gather, E, max_rows, N, K, st);
+    moe_launch<1, EPI, F32, WSH, MOE>(X, ldx, W, Y, ldy, off, gather, E, max_rows, N, K, S, ysplit, st);
   else if (max_rows <= 64)
-    moe_launch<4, EPI, F32, WSH, MOE>(X, ldx, W, Y, ldy, off, gather, E, max_rows, N, K, st);
+    moe_launch<4, EPI, F32, WSH, MOE>(X, ldx, W, Y, ldy, off, gather, E, max_rows, N, K, S, ysplit, st);
   else
-    moe_launch<8, EPI, F32, WSH, MOE>(X, ldx, W, Y, ldy, off, gather, E, max_rows, N, K, st);
+    moe_launch<8, EPI, F32, WSH, MOE>(X, ldx, W, Y, ldy, off, gather, E, max_rows, N, K, S, ysplit, st);
 }
 
 int launch_gemm_moe(const uint16_t* X, int ldx, const uint16_t* W, void* Y, int ldy, bool out_f32, int epi,
-                    const int* off, const int* gather, int E, int max_rows, int N, int K, bool wshuf,
-                    hipStream_t s) {
+                    const int* off, const int* gather, int E, int max_rows, int N, int K, bool wshuf, int S,
+                    long ysplit, hipStream_t s) {
   if (max_rows <= 0) return 0;
-  if (N % 128 != 0 || K % 256 != 0) return -1;
+  if (N % 128 != 0 || S < 1 || K % (256 * S) != 0) return -1;
   if (epi != EPI_NONE && epi != EPI_SILU) return -1;
   if (epi == EPI_SILU && out_f32) return -1;
-#define XOT_MOE(EPIV, F32V)                                                                        \
-  do {                                                                                              \
-    if (wshuf) {                                                                                    \
-      if (gather) moe_mt<EPIV, F32V, true, 2>(X, ldx, W, Y, ldy, off, gather, E, max_rows, N, K, s);  \
-      else moe_mt<EPIV, F32V, true, 1>(X, ldx, W, Y, ldy, off, gather, E, max_rows, N, K, s);         \
-    } else {                                                                                        \
-      if (gather) moe_mt<EPIV, F32V, false, 2>(X, ldx, W, Y, ldy, off, gather, E, max_rows, N, K, s); \
-      else moe_mt<EPIV, F32V, false, 1>(X, ldx, W, Y, ldy, off, gather, E, max_rows, N, K, s);        \
-    }                                                                                               \
-    return 0;                                                                                       \
+  if (S > 1 && (epi != EPI_NONE || !out_f32)) return -1;  // K slices write fp32 partial slabs
+#define XOT_MOE(EPIV, F32V)                                                                                     \
+  do {                                                                                                          \
+    if (wshuf) {                                                                                                \
+      if (gather) moe_mt<EPIV, F32V, true, 2>(X, ldx, W, Y, ldy, off, gather, E, max_rows, N, K, S, ysplit, s);  \
+      else moe_mt<EPIV, F32V, true, 1>(X, ldx, W, Y, ldy, off, gather, E, max_rows, N, K, S, ysplit, s);         \
+    } else {                                                                                                    \
+      if (gather) moe_mt<EPIV, F32V, false, 2>(X, ldx, W, Y, ldy, off, gather, E, max_rows, N, K, S, ysplit, s); \
+      else moe_mt<EPIV, F32V, false, 1>(X, ldx, W, Y, ldy, off, gather, E, max_rows, N, K, S, ysplit, s);        \
+    }                                                                                                           \
+    return 0;                                                                                                   \
   } while (0)
   if (epi == EPI_SILU) XOT_MOE(EPI_SILU, false);
   if (out_f32) XOT_MOE(EPI_NONE, true);

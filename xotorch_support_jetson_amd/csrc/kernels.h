@@ -35,12 +35,12 @@ int launch_gemm_big(const uint16_t* X, int ldx, const uint16_t* W, const uint16_
                     int S, hipStream_t s);
 // grouped GEMM over experts: rows of expert e are off[e]..off[e+1] (slot order), W is [E][N][K]
 int launch_gemm_moe(const uint16_t* X, int ldx, const uint16_t* W, void* Y, int ldy, bool out_f32, int epi,
-                    const int* off, const int* gather, int E, int max_rows, int N, int K, bool wshuf,
-                    hipStream_t s);
+                    const int* off, const int* gather, int E, int max_rows, int N, int K, bool wshuf, int S,
+                    long ysplit, hipStream_t s);
 void launch_moe_route(const float* logits, int T, int E, int k, float* topw, int32_t* topi, int32_t* slot_of,
                       int32_t* sorted_tok, int32_t* off, hipStream_t s);
 void launch_moe_combine(const float* y, const int32_t* slot_of, const float* topw, uint16_t* h, int T, int k, int D,
-                        hipStream_t s);
+                        int S, long ysplit, hipStream_t s);
 int launch_gemm_tiled(const uint16_t* X, int ldx, const uint16_t* W, int ldw, const uint16_t* bias,
                       const uint16_t* R, int ldr, void* Y, int ldy, bool out_f32, int epi, int M, int N, int K,
                       hipStream_t s);

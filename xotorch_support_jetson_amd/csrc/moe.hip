@@ -83,7 +83,7 @@ __global__ __launch_bounds__(1024) void moe_route_kernel(const float* __restrict
 __global__ __launch_bounds__(256) void moe_combine_kernel(const float* __restrict__ y,
                                                           const int32_t* __restrict__ slot_of,
                                                           const float* __restrict__ topw, uint16_t* __restrict__ h,
-                                                          int T, int k, int D) {
+                                                          int T, int k, int D, int S, long ysplit) {
   const long total = (long)T * (D / 8);
   for (long q = blockIdx.x * 256L + threadIdx.x; q < total; q += (long)gridDim.x * 256) {
     const int t = (int)(q / (D / 8));
@@ -95,12 +95,14 @@ __global__ __launch_bounds__(256) void moe_combine_kernel(const float* __restric
     for (int j = 0; j < k; ++j) {
       const float w = topw[(size_t)t * k + j];
       const float* yr = y + (size_t)slot_of[(size_t)t * k + j] * D + d;
-      const f32x4 a = *reinterpret_cast<const f32x4*>(yr);
-      const f32x4 b = *reinterpret_cast<const f32x4*>(yr + 4);
+      for (int sl = 0; sl < S; ++sl, yr += ysplit) {  // K-slice partial slabs of the grouped down GEMM
+        const f32x4 a = *reinterpret_cast<const f32x4*>(yr);
+        const f32x4 b = *reinterpret_cast<const f32x4*>(yr + 4);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        acc[e] += w * a[e];
-        acc[4 + e] += w * b[e];
+        for (int e = 0; e < 4; ++e) {
+          acc[e] += w * a[e];
+          acc[4 + e] += w * b[e];
+        }
       }
     }
     s16x8 o;
@@ -116,12 +118,12 @@ void launch_moe_route(const float* logits, int T, int E, int k, float* topw, int
 }
 
 void launch_moe_combine(const float* y, const int32_t* slot_of, const float* topw, uint16_t* h, int T, int k, int D,
-                        hipStream_t s) {
+                        int S, long ysplit, hipStream_t s) {
   const long chunks = (long)T * (D / 8);
   int blocks = (int)((chunks + 255) / 256);
   if (blocks > 4096) blocks = 4096;
   if (blocks < 1) return;
-  moe_combine_kernel<<<blocks, 256, 0, s>>>(y, slot_of, topw, h, T, k, D);
+  moe_combine_kernel<<<blocks, 256, 0, s>>>(y, slot_of, topw, h, T, k, D, S, ysplit);
 }
 
 }  // namespace xot

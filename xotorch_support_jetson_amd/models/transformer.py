@@ -151,9 +151,14 @@ class ShardModel:
     C.moe_route(logits.contiguous(), k, topw, topi, slot_of, sorted_tok, off)
     act = torch.empty(T * k, F, dtype=torch.bfloat16, device=dev)
     C.gemm_moe(xn, lw.gu_w, act, off, sorted_tok, K.EPI["silu"], T, layout_of(lw.gu_w) == "stream")
-    y = torch.empty(T * k, D, dtype=torch.float32, device=dev)
-    C.gemm_moe(act, lw.down_w, y, off, None, K.EPI["none"], T, layout_of(lw.down_w) == "stream")
-    C.moe_combine(y, slot_of, topw, h)
+    # down projection split over K (fp32 partial slabs summed by the combine): the grouped GEMM only has
+    # (experts hit) x N/128 workgroups with work, too few to stream the expert weights at full HBM rate
+    S = 4 if T * k <= 64 else 2
+    if F % (256 * S):
+      S = 1
+    y = torch.empty(S * T * k, D, dtype=torch.float32, device=dev)
+    C.gemm_moe(act, lw.down_w, y, off, None, K.EPI["none"], T, layout_of(lw.down_w) == "stream", S)
+    C.moe_combine(y, slot_of, topw, h, S)
     return h
 
   # ------------------------------------------------------------------ forward

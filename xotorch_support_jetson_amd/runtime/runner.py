@@ -53,7 +53,8 @@ class ShardRunner:
       # gemm_big for large batches); with decode batches above 128 rows the gate/up projection stays
       # row-major, where hipBLASLt measures faster (ops/linear.py; XOT_ROWMAJOR_PROJ overrides)
       env = os.environ.get("XOT_ROWMAJOR_PROJ")
-      keep = [p for p in env.split(",") if p] if env is not None else (["gu"] if max_batch > 128 else [])
+      keep = [p for p in env.split(",") if p] if env is not None else (
+          ["gu"] if max_batch > 128 and not config.is_moe else [])  # grouped expert GEMMs want the shuffled layout
       prepare_for_decode(self.weights, keep_rowmajor=keep)
     n_layers = shard.get_layer_count()
     per_page = KVCache.bytes_per_page(config, n_layers)
