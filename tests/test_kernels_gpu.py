@@ -384,3 +384,14 @@ def test_moe_layer(gpu, T, E, k, shuffled):
     out = h.clone()
     C.moe_combine(y, slot_of, topw, out, S)
     assert rel_err(out.float() - h.float(), ref - h.float()) < 3e-2, S  # the MoE contribution itself
+  if shuffled:  # the same block on gemm_big tiles (128-, 192- and 256-row tiles per expert)
+    for bm in (128, 192, 256):
+      act2 = torch.empty_like(act)
+      C.gemm_moe(x, gw, act2, off, sorted_tok, 2, T, True, 1, bm)
+      assert rel_err(act2, act) < 1e-2, bm
+      for S in (1, 2):
+        y = torch.empty(S * T * k, D, dtype=torch.float32, device=gpu)
+        C.gemm_moe(act2, dw, y, off, None, 0, T, True, S, bm)
+        out = h.clone()
+        C.moe_combine(y, slot_of, topw, out, S)
+        assert rel_err(out.float() - h.float(), ref - h.float()) < 3e-2, (bm, S)

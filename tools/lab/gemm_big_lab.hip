@@ -15,10 +15,10 @@ template <int BN, int BK, int NBUF, int ABL, int AA = 0, int AB = 0, bool PRIO =
 float run(const uint16_t* X, const uint16_t* W, uint16_t* Y, float* ws, int M, int N, int K, int S, size_t wstride,
           int ncopies) {
   constexpr int WM = BN == 256 ? 2 : 4, WN = 8 / WM;
-  constexpr int SMEM = NBUF * (GB_BM + BN) * BK * 2;
+  constexpr int SMEM = NBUF * (256 + BN) * BK * 2;
   const int nwg = ((M + 255) / 256) * (N / BN) * S;
-  auto k1 = gemm_big_kernel<BN, WM, WN, BK, NBUF, EPI_NONE, false, false, ABL, AA, AB, PRIO>;
-  auto k2 = gemm_big_kernel<BN, WM, WN, BK, NBUF, EPI_NONE, false, true, ABL, AA, AB, PRIO>;
+  auto k1 = gemm_big_kernel<256, BN, WM, WN, BK, NBUF, EPI_NONE, false, false, 0, ABL, AA, AB, PRIO>;
+  auto k2 = gemm_big_kernel<256, BN, WM, WN, BK, NBUF, EPI_NONE, false, true, 0, ABL, AA, AB, PRIO>;
   CK(hipFuncSetAttribute((const void*)k1, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM));
   CK(hipFuncSetAttribute((const void*)k2, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM));
   hipEvent_t a, b;
@@ -28,8 +28,8 @@ float run(const uint16_t* X, const uint16_t* W, uint16_t* Y, float* ws, int M, i
   for (int r = 0; r < 12; ++r) {
     const uint16_t* Wc = W + (size_t)(r % ncopies) * wstride;
     CK(hipEventRecord(a));
-    if (S == 1) k1<<<nwg, 512, SMEM>>>(X, K, Wc, nullptr, nullptr, 0, Y, N, nullptr, M, N, K, 1);
-    else k2<<<nwg, 512, SMEM>>>(X, K, Wc, nullptr, nullptr, 0, Y, N, ws, M, N, K, S);
+    if (S == 1) k1<<<nwg, 512, SMEM>>>(X, K, Wc, nullptr, nullptr, 0, Y, N, nullptr, M, N, K, 1, nullptr, nullptr, 0L);
+    else k2<<<nwg, 512, SMEM>>>(X, K, Wc, nullptr, nullptr, 0, Y, N, ws, M, N, K, S, nullptr, nullptr, 0L);
     CK(hipEventRecord(b));
     CK(hipEventSynchronize(b));
     float ms;

@@ -290,8 +290,10 @@ void gemm_big(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const c10
 // grouped expert GEMM: y[slot] = x[gather ? gather[slot] : slot] @ w[e].T for slots of expert e
 // splits > 1 (fp32 output, no epilogue): K slice s writes rows [s*slots, (s+1)*slots) of y ([splits*slots, N]),
 // summed by moe_combine(..., splits)
+// big_bm = 128 / 256: gemm_big tiles (pre-shuffled weights), else the weight-streaming kernel
 void gemm_moe(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const at::Tensor& off,
-              const c10::optional<at::Tensor>& gather, int64_t epi, int64_t max_rows, bool wshuf, int64_t splits) {
+              const c10::optional<at::Tensor>& gather, int64_t epi, int64_t max_rows, bool wshuf, int64_t splits,
+              int64_t big_bm) {
   CHECK_BF16(x);
   CHECK_BF16(w);
   CHECK_GPU(y);
@@ -318,9 +320,17 @@ void gemm_moe(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const at:
   } else {
     XCHECK(x.size(0) == slots, "gemm_moe: without gather, x rows are slots");
   }
-  const int rc = xot::launch_gemm_moe(bf(x), (int)x.stride(0), bf(w), y.data_ptr(), (int)y.stride(0), f32, (int)epi,
-                                      off.data_ptr<int>(), gp, (int)E, (int)max_rows, (int)N, (int)K, wshuf,
-                                      (int)splits, (long)(slots * y.size(1)), cur_stream());
+  int rc;
+  if (big_bm > 0) {
+    XCHECK(wshuf, "gemm_moe: the big-tile path needs pre-shuffled expert weights");
+    rc = xot::launch_gemm_moe_big(bf(x), (int)x.stride(0), bf(w), y.data_ptr(), (int)y.stride(0), f32, (int)epi,
+                                  off.data_ptr<int>(), gp, (int)E, (int)max_rows, (int)N, (int)K, (int)splits,
+                                  (long)(slots * y.size(1)), (int)big_bm, cur_stream());
+  } else {
+    rc = xot::launch_gemm_moe(bf(x), (int)x.stride(0), bf(w), y.data_ptr(), (int)y.stride(0), f32, (int)epi,
+                              off.data_ptr<int>(), gp, (int)E, (int)max_rows, (int)N, (int)K, wshuf, (int)splits,
+                              (long)(slots * y.size(1)), cur_stream());
+  }
   XCHECK(rc == 0, "gemm_moe: unsupported shape N=", N, " K=", K, " epi=", epi, " splits=", splits);
 }
 
@@ -496,7 +506,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_big", &gemm_big, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("bias"), py::arg("res"),
         py::arg("ws"), py::arg("epi"), py::arg("bn"), py::arg("splits"));
   m.def("gemm_moe", &gemm_moe, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("off"), py::arg("gather"),
-        py::arg("epi"), py::arg("max_rows"), py::arg("wshuf"), py::arg("splits") = 1);
+        py::arg("epi"), py::arg("max_rows"), py::arg("wshuf"), py::arg("splits") = 1, py::arg("big_bm") = 0);
   m.def("moe_route", &moe_route);
   m.def("moe_combine", &moe_combine, py::arg("y"), py::arg("slot_of"), py::arg("topw"), py::arg("h"),
         py::arg("splits") = 1);

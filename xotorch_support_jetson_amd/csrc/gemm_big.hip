@@ -36,7 +36,6 @@ __device__ __forceinline__ void glds16(const void* g, void* lds_base) {
   __builtin_amdgcn_global_load_lds((glb_ptr_t)g, (lds_ptr_t)lds_base, 16, 0, AUX);
 }
 
-constexpr int GB_BM = 256;
 
 template <int N>
 __device__ __forceinline__ void wait_vm() {
@@ -45,17 +44,25 @@ __device__ __forceinline__ void wait_vm() {
 
 // ABL (tools/lab only): 1 = k loop without MFMAs, 2 = without stage loads, 3 = stage loads not overlapped
 // AUXA / AUXB: cache-policy bits of the X / W LDS-DMA loads (sc0 = 1, nt = 2, sc1 = 16)
-template <int BN, int WM, int WN, int BK, int NBUF, int EPI, bool OUT_F32, bool SPLIT, int ABL = 0, int AUXA = 0,
-          int AUXB = 3, bool PRIO = false>
+// MOE = 1 / 2: grouped GEMM over experts (blockIdx.y = expert e, weight W[e], rows moe_off[e] ..
+// moe_off[e+1] of the expert-sorted slot order; MOE 2 gathers X row moe_gather[slot]); M is the
+// worst-case rows per expert (row tiles past an expert's count exit at once, so the grid is fixed and
+// graph-capturable).  A K split writes fp32 partial slabs ysplit elements apart (summed by the consumer).
+template <int BM, int BN, int WM, int WN, int BK, int NBUF, int EPI, bool OUT_F32, bool SPLIT, int MOE = 0, int ABL = 0,
+          int AUXA = 0, int AUXB = 3, bool PRIO = false>
 __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __restrict__ X, int ldx,
                                                           const uint16_t* __restrict__ W,
                                                           const uint16_t* __restrict__ bias,
                                                           const uint16_t* __restrict__ R, int ldr,
                                                           void* __restrict__ Yv, int ldy, float* __restrict__ ws,
-                                                          int M, int N, int K, int S) {
+                                                          int M, int N, int K, int S,
+                                                          const int* __restrict__ moe_off = nullptr,
+                                                          const int* __restrict__ moe_gather = nullptr,
+                                                          long ysplit = 0) {
   static_assert(WM * WN == 8, "8 waves");
   static_assert(BK == 32 || BK == 64, "k stage of 32 or 64");
-  constexpr int BM = GB_BM;
+  static_assert(BM == 128 || BM == 192 || BM == 256, "row tile of 128, 192 or 256");
+  static_assert(MOE == 0 || (!SPLIT && EPI != EPI_RESID), "grouped GEMM: no slab reduce, no residual");
   constexpr int MT = BM / (16 * WM), NT = BN / (16 * WN);
   static_assert(EPI != EPI_SILU || NT % 2 == 0, "SiLU epilogue pairs gate/up n-tiles");
   constexpr int KS = BK / 32;                          // MFMA k-steps (and 1 KB W blocks per row group) per stage
@@ -82,6 +89,15 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
   }
   const int mt = b % mtiles, nt = (b / mtiles) % ntiles, split = b / (mtiles * ntiles);
   const int m0 = mt * BM, n0 = nt * BN;
+  int row0 = 0, Mv = M;  // first output row (slot) and valid rows of this launch's row range
+  if constexpr (MOE != 0) {
+    const int e = blockIdx.y;
+    row0 = moe_off[e];
+    Mv = moe_off[e + 1] - row0;
+    W += (size_t)e * N * K;
+    if (m0 >= Mv) return;  // uniform over the workgroup, before any barrier
+    if (ysplit != 0) Yv = reinterpret_cast<float*>(Yv) + (size_t)split * ysplit;
+  }
   const int T_all = K / BK;
   const int t_beg = (int)((long)split * T_all / S), t_end = (int)((long)(split + 1) * T_all / S);
   const int T = t_end - t_beg;
@@ -105,7 +121,9 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
   for (int i = 0; i < A_INSTR; ++i) {
     const int row = (64 / SPR) * (A_INSTR * wave + i) + lane / SPR;
     const int slot = (lane % SPR) ^ aswz(row);
-    const int grow = min(m0 + row, M - 1);  // rows past M load valid memory; their outputs are masked
+    int grow = min(m0 + row, Mv - 1);  // rows past the end load valid memory; their outputs are masked
+    if constexpr (MOE == 1) grow += row0;
+    if constexpr (MOE == 2) grow = moe_gather[row0 + grow];
     asrc[i] = X + (size_t)grow * ldx + slot * 8;
   }
   // W: instruction q = B_INSTR*w + i copies 1 KB block q % KS of row group q / KS for this stage.
@@ -207,6 +225,12 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
 
   // ---- epilogue
   const int rbase = m0 + wm * (MT * 16);
+  if constexpr (MOE != 0) {  // output rows are slots
+    if constexpr (OUT_F32)
+      Yv = reinterpret_cast<float*>(Yv) + (size_t)row0 * ldy;
+    else
+      Yv = reinterpret_cast<uint16_t*>(Yv) + (size_t)row0 * ldy;
+  }
   const int cbase = n0 + wn * (NT * 16);
   if constexpr (SPLIT) {
     float* slab = ws + (size_t)split * M * N;
@@ -215,7 +239,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int m = rbase + 16 * i + 4 * g + r;
-        if (m < M) {
+        if (m < Mv) {
 #pragma unroll
           for (int j = 0; j < NT; ++j) slab[(size_t)m * N + cbase + 16 * j + c] = acc[i][j][r];
         }
@@ -234,7 +258,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int m = rbase + 16 * i + 4 * g + r;
-          if (m < M) {
+          if (m < Mv) {
             const float v = silu(acc[i][2 * p][r] + bg) * (acc[i][2 * p + 1][r] + bu);
             if constexpr (OUT_F32)
               reinterpret_cast<float*>(Yv)[(size_t)m * ldy + col] = v;
@@ -253,7 +277,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int m = rbase + 16 * i + 4 * g + r;
-          if (m < M) {
+          if (m < Mv) {
             float v = acc[i][j][r] + bv;
             if constexpr (EPI == EPI_RESID) v += bf2f(R[(size_t)m * ldr + col]);
             if constexpr (OUT_F32)
@@ -266,24 +290,24 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
   }
 }
 
-template <int BN, int WM, int WN, int BK, int NBUF, int EPI, bool F32>
+template <int BM, int BN, int WM, int WN, int BK, int NBUF, int EPI, bool F32>
 static void big_launch(const uint16_t* X, int ldx, const uint16_t* W, const uint16_t* bias, const uint16_t* R,
                        int ldr, void* Y, int ldy, float* ws, int M, int N, int K, int S, hipStream_t st) {
-  constexpr int SMEM = NBUF * (GB_BM + BN) * BK * 2;
+  constexpr int SMEM = NBUF * (BM + BN) * BK * 2;
   static_assert(SMEM <= 160 * 1024, "LDS");
-  const int nwg = ((M + GB_BM - 1) / GB_BM) * (N / BN) * S;
+  const int nwg = ((M + BM - 1) / BM) * (N / BN) * S;
   if (S == 1) {
-    auto kern = gemm_big_kernel<BN, WM, WN, BK, NBUF, EPI, F32, false>;
+    auto kern = gemm_big_kernel<BM, BN, WM, WN, BK, NBUF, EPI, F32, false>;
     static bool attr = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM) ==
                        hipSuccess;
     (void)attr;
-    kern<<<nwg, 512, SMEM, st>>>(X, ldx, W, bias, R, ldr, Y, ldy, nullptr, M, N, K, 1);
+    kern<<<nwg, 512, SMEM, st>>>(X, ldx, W, bias, R, ldr, Y, ldy, nullptr, M, N, K, 1, nullptr, nullptr, 0L);
   } else {
-    auto kern = gemm_big_kernel<BN, WM, WN, BK, NBUF, EPI, false, true>;
+    auto kern = gemm_big_kernel<BM, BN, WM, WN, BK, NBUF, EPI, false, true>;
     static bool attr = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM) ==
                        hipSuccess;
     (void)attr;
-    kern<<<nwg, 512, SMEM, st>>>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, S);
+    kern<<<nwg, 512, SMEM, st>>>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, S, nullptr, nullptr, 0L);
     const int ncol = EPI == EPI_SILU ? N / 2 : N;
     const long chunks = (long)M * (ncol / 8);
     int blocks = (int)((chunks + 255) / 256);
@@ -297,9 +321,9 @@ static int big_dispatch(const uint16_t* X, int ldx, const uint16_t* W, const uin
                         int ldr, void* Y, int ldy, float* ws, long ws_elems, int M, int N, int K, int bn, int S,
                         hipStream_t st) {
   if (bn == 256)
-    big_launch<256, 2, 4, 64, 2, EPI, F32>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, S, st);
+    big_launch<256, 256, 2, 4, 64, 2, EPI, F32>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, S, st);
   else if (bn == 128)
-    big_launch<128, 4, 2, 64, 3, EPI, F32>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, S, st);
+    big_launch<256, 128, 4, 2, 64, 3, EPI, F32>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, S, st);
   else
     return -1;
   return 0;
@@ -319,6 +343,54 @@ int launch_gemm_big(const uint16_t* X, int ldx, const uint16_t* W, const uint16_
     return out_f32 ? -1 : big_dispatch<EPI_RESID, false>(X, ldx, W, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, bn, S, s);
   return out_f32 ? big_dispatch<EPI_NONE, true>(X, ldx, W, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, bn, S, s)
                  : big_dispatch<EPI_NONE, false>(X, ldx, W, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, bn, S, s);
+}
+
+// ------------------------------------------------------------------------------------ grouped (MoE)
+template <int BM, int EPI, bool F32, int MOE>
+static void big_moe_launch(const uint16_t* X, int ldx, const uint16_t* W, void* Y, int ldy, const int* off,
+                           const int* gather, int E, int max_rows, int N, int K, int S, long ysplit, hipStream_t st) {
+  constexpr int BN = 256, WM = 2, WN = 4, BK = 64, NBUF = 2;
+  constexpr int SMEM = NBUF * (BM + BN) * BK * 2;
+  auto kern = gemm_big_kernel<BM, BN, WM, WN, BK, NBUF, EPI, F32, false, MOE>;
+  static bool attr = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM) ==
+                     hipSuccess;
+  (void)attr;
+  dim3 grid(((max_rows + BM - 1) / BM) * (N / BN) * S, E);
+  kern<<<grid, 512, SMEM, st>>>(X, ldx, W, nullptr, nullptr, 0, Y, ldy, nullptr, max_rows, N, K, S, off, gather,
+                                S > 1 ? ysplit : 0L);
+}
+
+template <int EPI, bool F32>
+static void big_moe_bm(const uint16_t* X, int ldx, const uint16_t* W, void* Y, int ldy, const int* off,
+                       const int* gather, int E, int max_rows, int N, int K, int S, long ysplit, int bm,
+                       hipStream_t st) {
+  if (bm == 128) {
+    if (gather) big_moe_launch<128, EPI, F32, 2>(X, ldx, W, Y, ldy, off, gather, E, max_rows, N, K, S, ysplit, st);
+    else big_moe_launch<128, EPI, F32, 1>(X, ldx, W, Y, ldy, off, gather, E, max_rows, N, K, S, ysplit, st);
+  } else if (bm == 192) {
+    if (gather) big_moe_launch<192, EPI, F32, 2>(X, ldx, W, Y, ldy, off, gather, E, max_rows, N, K, S, ysplit, st);
+    else big_moe_launch<192, EPI, F32, 1>(X, ldx, W, Y, ldy, off, gather, E, max_rows, N, K, S, ysplit, st);
+  } else {
+    if (gather) big_moe_launch<256, EPI, F32, 2>(X, ldx, W, Y, ldy, off, gather, E, max_rows, N, K, S, ysplit, st);
+    else big_moe_launch<256, EPI, F32, 1>(X, ldx, W, Y, ldy, off, gather, E, max_rows, N, K, S, ysplit, st);
+  }
+}
+
+int launch_gemm_moe_big(const uint16_t* X, int ldx, const uint16_t* W, void* Y, int ldy, bool out_f32, int epi,
+                        const int* off, const int* gather, int E, int max_rows, int N, int K, int S, long ysplit,
+                        int bm, hipStream_t s) {
+  if (max_rows <= 0) return 0;
+  if ((bm != 128 && bm != 192 && bm != 256) || N % 256 != 0 || K % 128 != 0 || S < 1 || S > K / 64) return -1;
+  if (epi != EPI_NONE && epi != EPI_SILU) return -1;
+  if (epi == EPI_SILU && out_f32) return -1;
+  if (S > 1 && (epi != EPI_NONE || !out_f32)) return -1;  // K slices write fp32 partial slabs
+  if (epi == EPI_SILU)
+    big_moe_bm<EPI_SILU, false>(X, ldx, W, Y, ldy, off, gather, E, max_rows, N, K, S, ysplit, bm, s);
+  else if (out_f32)
+    big_moe_bm<EPI_NONE, true>(X, ldx, W, Y, ldy, off, gather, E, max_rows, N, K, S, ysplit, bm, s);
+  else
+    big_moe_bm<EPI_NONE, false>(X, ldx, W, Y, ldy, off, gather, E, max_rows, N, K, S, ysplit, bm, s);
+  return 0;
 }
 
 }  // namespace xot

@@ -33,6 +33,10 @@ int launch_gemm_stream(const uint16_t* X, int ldx, const uint16_t* W, int ldw, c
 int launch_gemm_big(const uint16_t* X, int ldx, const uint16_t* W, const uint16_t* bias, const uint16_t* R, int ldr,
                     void* Y, int ldy, bool out_f32, int epi, float* ws, long ws_elems, int M, int N, int K, int bn,
                     int S, hipStream_t s);
+// grouped expert GEMM on gemm_big tiles (bm = 128 or 256 rows per tile; large per-expert row counts)
+int launch_gemm_moe_big(const uint16_t* X, int ldx, const uint16_t* W, void* Y, int ldy, bool out_f32, int epi,
+                        const int* off, const int* gather, int E, int max_rows, int N, int K, int S, long ysplit,
+                        int bm, hipStream_t s);
 // grouped GEMM over experts: rows of expert e are off[e]..off[e+1] (slot order), W is [E][N][K]
 int launch_gemm_moe(const uint16_t* X, int ldx, const uint16_t* W, void* Y, int ldy, bool out_f32, int epi,
                     const int* off, const int* gather, int E, int max_rows, int N, int K, bool wshuf, int S,

@@ -19,6 +19,7 @@ llm_utils.py:404-440 / general_mha.py:209).
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from typing import List, Optional
 
@@ -32,6 +33,8 @@ from ..ops.rope import build_cos_sin
 from .config import ModelConfig
 from .weights import ShardWeights, expert
 
+# average rows per expert above which the grouped expert GEMMs run on gemm_big tiles
+MOE_BIG_MIN_ROWS = float(os.environ.get("XOT_MOE_BIG_MIN_ROWS", "24"))
 PAGE = 64
 
 
@@ -149,15 +152,22 @@ class ShardModel:
     sorted_tok = torch.empty(T * k, dtype=torch.int32, device=dev)
     off = torch.empty(E + 1, dtype=torch.int32, device=dev)
     C.moe_route(logits.contiguous(), k, topw, topi, slot_of, sorted_tok, off)
+    shuffled = layout_of(lw.gu_w) == "stream" and layout_of(lw.down_w) == "stream"
+    # rows per expert decide the kernel: the weight-streaming GEMM for decode-sized groups, gemm_big
+    # tiles (128 or 256 rows) once the groups are compute-bound
+    rows = T * k / E
+    # measured (tools/bench_moe.py, Mixtral shapes): 192-row tiles when one tile holds an expert's
+    # ~100-160 rows, 256 otherwise (a tile's rows past the expert's count are masked MFMA work)
+    bm = 0 if not shuffled or rows < MOE_BIG_MIN_ROWS else (192 if 96 < rows <= 160 else 256)
     act = torch.empty(T * k, F, dtype=torch.bfloat16, device=dev)
-    C.gemm_moe(xn, lw.gu_w, act, off, sorted_tok, K.EPI["silu"], T, layout_of(lw.gu_w) == "stream")
+    C.gemm_moe(xn, lw.gu_w, act, off, sorted_tok, K.EPI["silu"], T, layout_of(lw.gu_w) == "stream", 1, bm)
     # down projection split over K (fp32 partial slabs summed by the combine): the grouped GEMM only has
-    # (experts hit) x N/128 workgroups with work, too few to stream the expert weights at full HBM rate
-    S = 4 if T * k <= 64 else 2
+    # (experts hit) x N/tile workgroups with work, too few to stream the expert weights at full HBM rate
+    S = (4 if T * k <= 64 else 2) if bm == 0 else (4 if bm == 192 else 2)
     if F % (256 * S):
       S = 1
     y = torch.empty(S * T * k, D, dtype=torch.float32, device=dev)
-    C.gemm_moe(act, lw.down_w, y, off, None, K.EPI["none"], T, layout_of(lw.down_w) == "stream", S)
+    C.gemm_moe(act, lw.down_w, y, off, None, K.EPI["none"], T, layout_of(lw.down_w) == "stream", S, bm)
     C.moe_combine(y, slot_of, topw, h, S)
     return h
 
