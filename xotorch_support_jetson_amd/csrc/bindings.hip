@@ -192,7 +192,7 @@ void gemm(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const c10::op
 // an fp32 workspace of >= splits*M*N floats).  ntw: 16-row n-tiles per wave (1 or 2).
 void gemm_stream(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const c10::optional<at::Tensor>& bias,
                  const c10::optional<at::Tensor>& res, const c10::optional<at::Tensor>& ws, int64_t epi, int64_t ntw,
-                 int64_t splits, bool wshuf, const c10::optional<at::Tensor>& tickets) {
+                 int64_t splits, bool wshuf, const c10::optional<at::Tensor>& tickets, bool reduce) {
   CHECK_BF16(x);
   CHECK_BF16(w);
   CHECK_GPU(y);
@@ -238,7 +238,7 @@ void gemm_stream(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const 
   const int rc = xot::launch_gemm_stream(bf(x), (int)x.stride(0), bf(w), (int)K, bf_opt(bias),
                                          epi == 1 ? bf(*res) : nullptr, (int)ldr, y.data_ptr(), (int)y.stride(0), f32,
                                          (int)epi, wsp, ws_elems, (int)M, (int)N, (int)K, (int)ntw, (int)splits,
-                                         wshuf, tk, tk_n, cur_stream());
+                                         wshuf, tk, tk_n, reduce, cur_stream());
   XCHECK(rc == 0, "gemm_stream: unsupported shape M=", M, " N=", N, " K=", K, " epi=", epi, " ntw=", ntw,
          " splits=", splits);
 }
@@ -247,7 +247,7 @@ void gemm_stream(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const 
 // bn: 256 or 128 output columns per workgroup; splits > 1 needs an fp32 workspace of splits*M*N.
 void gemm_big(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const c10::optional<at::Tensor>& bias,
               const c10::optional<at::Tensor>& res, const c10::optional<at::Tensor>& ws, int64_t epi, int64_t bn,
-              int64_t splits) {
+              int64_t splits, bool reduce) {
   CHECK_BF16(x);
   CHECK_BF16(w);
   CHECK_GPU(y);
@@ -282,9 +282,30 @@ void gemm_big(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const c10
   }
   const int rc = xot::launch_gemm_big(bf(x), (int)x.stride(0), bf(w), bf_opt(bias), epi == 1 ? bf(*res) : nullptr,
                                       (int)ldr, y.data_ptr(), (int)y.stride(0), f32, (int)epi, wsp, ws_elems, (int)M,
-                                      (int)N, (int)K, (int)bn, (int)splits, cur_stream());
+                                      (int)N, (int)K, (int)bn, (int)splits, reduce, cur_stream());
   XCHECK(rc == 0, "gemm_big: unsupported shape M=", M, " N=", N, " K=", K, " epi=", epi, " bn=", bn,
          " splits=", splits);
+}
+
+// h [rows, D] += bias + sum_s ws[s] (the split-K slabs of a residual projection, fp32 [S][rows][D]);
+// out = rmsnorm(h) * w: the projection's reduce, the residual add and the next RMSNorm in one pass.
+void splitk_resid_rmsnorm(const at::Tensor& ws, int64_t splits, const c10::optional<at::Tensor>& bias, at::Tensor& h,
+                          const at::Tensor& w, at::Tensor& out, double eps) {
+  CHECK_GPU(ws);
+  CHECK_DT(ws, at::kFloat);
+  CHECK_BF16(h);
+  CHECK_BF16(w);
+  CHECK_BF16(out);
+  XCHECK(all_contig_gpu(ws, h, w, out), "splitk_resid_rmsnorm: tensors must be contiguous GPU");
+  const int64_t rows = h.size(0), D = h.size(1);
+  XCHECK(h.dim() == 2 && D % 8 == 0 && w.numel() == D && out.numel() == rows * D, "splitk_resid_rmsnorm: shapes");
+  XCHECK(splits >= 1 && ws.numel() >= splits * rows * D, "splitk_resid_rmsnorm: workspace too small");
+  if (bias.has_value()) {
+    CHECK_BF16((*bias));
+    XCHECK(bias->numel() == D && bias->is_contiguous(), "splitk_resid_rmsnorm: bias");
+  }
+  xot::launch_splitk_resid_rmsnorm(ws.data_ptr<float>(), (int)splits, bf_opt(bias), bf(h), bf(w), bf(out), (int)rows,
+                                   (int)D, (float)eps, cur_stream());
 }
 
 // grouped expert GEMM: y[slot] = x[gather ? gather[slot] : slot] @ w[e].T for slots of expert e
@@ -502,9 +523,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm", &gemm);
   m.def("gemm_stream", &gemm_stream, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("bias"), py::arg("res"),
         py::arg("ws"), py::arg("epi"), py::arg("ntw"), py::arg("splits"), py::arg("wshuf"),
-        py::arg("tickets") = py::none());
+        py::arg("tickets") = py::none(), py::arg("reduce") = true);
   m.def("gemm_big", &gemm_big, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("bias"), py::arg("res"),
-        py::arg("ws"), py::arg("epi"), py::arg("bn"), py::arg("splits"));
+        py::arg("ws"), py::arg("epi"), py::arg("bn"), py::arg("splits"), py::arg("reduce") = true);
+  m.def("splitk_resid_rmsnorm", &splitk_resid_rmsnorm);
   m.def("gemm_moe", &gemm_moe, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("off"), py::arg("gather"),
         py::arg("epi"), py::arg("max_rows"), py::arg("wshuf"), py::arg("splits") = 1, py::arg("big_bm") = 0);
   m.def("moe_route", &moe_route);

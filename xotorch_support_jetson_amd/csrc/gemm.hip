@@ -468,7 +468,7 @@ __global__ __launch_bounds__(256, OCC) void gemm_stream_kernel(const uint16_t* _
 template <int MT, int NTW, int KS, int EPI, bool F32, bool WSH>
 static void stream_launch(const uint16_t* X, int ldx, const uint16_t* W, int ldw, const uint16_t* bias,
                           const uint16_t* R, int ldr, void* Y, int ldy, float* ws, int M, int N, int K, int S,
-                          int* tickets, hipStream_t st) {
+                          int* tickets, bool reduce, hipStream_t st) {
   // occupancy request: 2 workgroups/CU while the register budget allows it
   constexpr int OCC = (MT * NTW >= 32) ? 1 : 2;
   constexpr int SMEM = 2 * 16 * MT * 32 * KS * 2;
@@ -493,7 +493,7 @@ static void stream_launch(const uint16_t* X, int ldx, const uint16_t* W, int ldw
     }
     kern<<<grid, 256, SMEM, st>>>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, M, N, kper, mblocks, nullptr, nullptr,
                                   tickets, 0L);
-    if (tickets != nullptr) return;  // combined in-launch
+    if (tickets != nullptr || !reduce) return;  // combined in-launch / slabs left for the consumer
     const int ncol = EPI == EPI_SILU ? N / 2 : N;
     long chunks = (long)M * (ncol / 8);
     int blocks = (int)((chunks + 255) / 256);
@@ -505,7 +505,8 @@ static void stream_launch(const uint16_t* X, int ldx, const uint16_t* W, int ldw
 template <int EPI, bool F32>
 static int stream_dispatch(const uint16_t* X, int ldx, const uint16_t* W, int ldw, const uint16_t* bias,
                            const uint16_t* R, int ldr, void* Y, int ldy, float* ws, long ws_elems, int M, int N,
-                           int K, int ntw, int S, bool wshuf, int* tickets, long tickets_n, hipStream_t st) {
+                           int K, int ntw, int S, bool wshuf, int* tickets, long tickets_n, bool reduce,
+                           hipStream_t st) {
   if (EPI == EPI_SILU && ntw == 1) ntw = 2;
   if (ntw != 1 && ntw != 2 && ntw != 4) return -1;
   const int mt = (M + 15) / 16;
@@ -515,17 +516,17 @@ static int stream_dispatch(const uint16_t* X, int ldx, const uint16_t* W, int ld
   if (K % (S * 64 * KS) != 0) return -1;  // an even number (>= 2) of k-chunks per workgroup
   if (S > 1 && (ws == nullptr || ws_elems < (long)S * M * N)) return -1;
   // in-launch split-K combine needs one ticket per (column tile, 128-row block)
-  if (S == 1 || tickets_n < (long)(N / (64 * ntw)) * ((M + 127) / 128)) tickets = nullptr;
+  if (S == 1 || !reduce || tickets_n < (long)(N / (64 * ntw)) * ((M + 127) / 128)) tickets = nullptr;
   if (EPI == EPI_SILU && N % 32 != 0) return -1;
   if (wshuf && (KS != 4 || K % 128 != 0)) return -1;
 #define XOT_ST2(MTV, KSV, WSH)                                                                              \
   do {                                                                                                      \
     if (ntw == 1 && EPI != EPI_SILU)                                                                        \
-      stream_launch<MTV, 1, KSV, EPI, F32, WSH>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, M, N, K, S, tickets, st);  \
+      stream_launch<MTV, 1, KSV, EPI, F32, WSH>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, M, N, K, S, tickets, reduce, st);  \
     else if (ntw == 4 && MTV >= 4 && MTV <= 8)                                                                    \
-      stream_launch<MTV, 4, KSV, EPI, F32, WSH>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, M, N, K, S, tickets, st);  \
+      stream_launch<MTV, 4, KSV, EPI, F32, WSH>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, M, N, K, S, tickets, reduce, st);  \
     else                                                                                                    \
-      stream_launch<MTV, 2, KSV, EPI, F32, WSH>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, M, N, K, S, tickets, st);  \
+      stream_launch<MTV, 2, KSV, EPI, F32, WSH>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, M, N, K, S, tickets, reduce, st);  \
     return 0;                                                                                               \
   } while (0)
 #define XOT_ST(MTV, KSV)                  \
@@ -598,16 +599,16 @@ int launch_gemm_moe(const uint16_t* X, int ldx, const uint16_t* W, void* Y, int 
 
 int launch_gemm_stream(const uint16_t* X, int ldx, const uint16_t* W, int ldw, const uint16_t* bias,
                        const uint16_t* R, int ldr, void* Y, int ldy, bool out_f32, int epi, float* ws, long ws_elems,
-                       int M, int N, int K, int ntw, int S, bool wshuf, int* tickets, long tickets_n,
+                       int M, int N, int K, int ntw, int S, bool wshuf, int* tickets, long tickets_n, bool reduce,
                        hipStream_t s) {
   if (M <= 0) return 0;
   if (epi == EPI_SILU)
-    return out_f32 ? stream_dispatch<EPI_SILU, true>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, ntw, S, wshuf, tickets, tickets_n, s)
-                   : stream_dispatch<EPI_SILU, false>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, ntw, S, wshuf, tickets, tickets_n, s);
+    return out_f32 ? stream_dispatch<EPI_SILU, true>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, ntw, S, wshuf, tickets, tickets_n, reduce, s)
+                   : stream_dispatch<EPI_SILU, false>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, ntw, S, wshuf, tickets, tickets_n, reduce, s);
   if (epi == EPI_RESID)
-    return out_f32 ? -1 : stream_dispatch<EPI_RESID, false>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, ntw, S, wshuf, tickets, tickets_n, s);
-  return out_f32 ? stream_dispatch<EPI_NONE, true>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, ntw, S, wshuf, tickets, tickets_n, s)
-                 : stream_dispatch<EPI_NONE, false>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, ntw, S, wshuf, tickets, tickets_n, s);
+    return out_f32 ? -1 : stream_dispatch<EPI_RESID, false>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, ntw, S, wshuf, tickets, tickets_n, reduce, s);
+  return out_f32 ? stream_dispatch<EPI_NONE, true>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, ntw, S, wshuf, tickets, tickets_n, reduce, s)
+                 : stream_dispatch<EPI_NONE, false>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, ntw, S, wshuf, tickets, tickets_n, reduce, s);
 }
 
 // ------------------------------------------------------------------------------------ tiled

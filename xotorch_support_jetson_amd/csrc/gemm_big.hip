@@ -292,7 +292,8 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
 
 template <int BM, int BN, int WM, int WN, int BK, int NBUF, int EPI, bool F32>
 static void big_launch(const uint16_t* X, int ldx, const uint16_t* W, const uint16_t* bias, const uint16_t* R,
-                       int ldr, void* Y, int ldy, float* ws, int M, int N, int K, int S, hipStream_t st) {
+                       int ldr, void* Y, int ldy, float* ws, int M, int N, int K, int S, bool reduce,
+                       hipStream_t st) {
   constexpr int SMEM = NBUF * (BM + BN) * BK * 2;
   static_assert(SMEM <= 160 * 1024, "LDS");
   const int nwg = ((M + BM - 1) / BM) * (N / BN) * S;
@@ -308,6 +309,7 @@ static void big_launch(const uint16_t* X, int ldx, const uint16_t* W, const uint
                        hipSuccess;
     (void)attr;
     kern<<<nwg, 512, SMEM, st>>>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, S, nullptr, nullptr, 0L);
+    if (!reduce) return;  // slabs left for the consumer (fused reduce + residual + RMSNorm)
     const int ncol = EPI == EPI_SILU ? N / 2 : N;
     const long chunks = (long)M * (ncol / 8);
     int blocks = (int)((chunks + 255) / 256);
@@ -319,11 +321,11 @@ static void big_launch(const uint16_t* X, int ldx, const uint16_t* W, const uint
 template <int EPI, bool F32>
 static int big_dispatch(const uint16_t* X, int ldx, const uint16_t* W, const uint16_t* bias, const uint16_t* R,
                         int ldr, void* Y, int ldy, float* ws, long ws_elems, int M, int N, int K, int bn, int S,
-                        hipStream_t st) {
+                        bool reduce, hipStream_t st) {
   if (bn == 256)
-    big_launch<256, 256, 2, 4, 64, 2, EPI, F32>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, S, st);
+    big_launch<256, 256, 2, 4, 64, 2, EPI, F32>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, S, reduce, st);
   else if (bn == 128)
-    big_launch<256, 128, 4, 2, 64, 3, EPI, F32>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, S, st);
+    big_launch<256, 128, 4, 2, 64, 3, EPI, F32>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, S, reduce, st);
   else
     return -1;
   return 0;
@@ -331,18 +333,18 @@ static int big_dispatch(const uint16_t* X, int ldx, const uint16_t* W, const uin
 
 int launch_gemm_big(const uint16_t* X, int ldx, const uint16_t* W, const uint16_t* bias, const uint16_t* R, int ldr,
                     void* Y, int ldy, bool out_f32, int epi, float* ws, long ws_elems, int M, int N, int K, int bn,
-                    int S, hipStream_t s) {
+                    int S, bool reduce, hipStream_t s) {
   if (M <= 0) return 0;
   if ((bn != 128 && bn != 256) || N % bn != 0 || K % 128 != 0 || S < 1 || S > K / 64) return -1;
   if (S > 1 && (ws == nullptr || ws_elems < (long)S * M * N)) return -1;
   if (epi == EPI_SILU && N % 32 != 0) return -1;
   if (epi == EPI_SILU)
-    return out_f32 ? big_dispatch<EPI_SILU, true>(X, ldx, W, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, bn, S, s)
-                   : big_dispatch<EPI_SILU, false>(X, ldx, W, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, bn, S, s);
+    return out_f32 ? big_dispatch<EPI_SILU, true>(X, ldx, W, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, bn, S, reduce, s)
+                   : big_dispatch<EPI_SILU, false>(X, ldx, W, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, bn, S, reduce, s);
   if (epi == EPI_RESID)
-    return out_f32 ? -1 : big_dispatch<EPI_RESID, false>(X, ldx, W, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, bn, S, s);
-  return out_f32 ? big_dispatch<EPI_NONE, true>(X, ldx, W, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, bn, S, s)
-                 : big_dispatch<EPI_NONE, false>(X, ldx, W, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, bn, S, s);
+    return out_f32 ? -1 : big_dispatch<EPI_RESID, false>(X, ldx, W, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, bn, S, reduce, s);
+  return out_f32 ? big_dispatch<EPI_NONE, true>(X, ldx, W, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, bn, S, reduce, s)
+                 : big_dispatch<EPI_NONE, false>(X, ldx, W, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, bn, S, reduce, s);
 }
 
 // ------------------------------------------------------------------------------------ grouped (MoE)

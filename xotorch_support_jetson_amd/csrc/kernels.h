@@ -27,12 +27,15 @@ int launch_gemm_skinny(const uint16_t* X, int ldx, const uint16_t* W, int ldw, c
                        int nt, hipStream_t s);
 int launch_gemm_stream(const uint16_t* X, int ldx, const uint16_t* W, int ldw, const uint16_t* bias,
                        const uint16_t* R, int ldr, void* Y, int ldy, bool out_f32, int epi, float* ws, long ws_elems,
-                       int M, int N, int K, int ntw, int S, bool wshuf, int* tickets, long tickets_n,
+                       int M, int N, int K, int ntw, int S, bool wshuf, int* tickets, long tickets_n, bool reduce,
                        hipStream_t s);
 // large-M GEMM on the pre-shuffled layout (256 x bn x 64 LDS-DMA tiles, 8 waves; split-K via ws)
 int launch_gemm_big(const uint16_t* X, int ldx, const uint16_t* W, const uint16_t* bias, const uint16_t* R, int ldr,
                     void* Y, int ldy, bool out_f32, int epi, float* ws, long ws_elems, int M, int N, int K, int bn,
-                    int S, hipStream_t s);
+                    int S, bool reduce, hipStream_t s);
+// h += bias + sum of S fp32 split-K slabs [S][rows][D] (in place, bf16), out = rmsnorm(h) * w
+void launch_splitk_resid_rmsnorm(const float* ws, int S, const uint16_t* bias, uint16_t* h, const uint16_t* w,
+                                 uint16_t* out, int rows, int D, float eps, hipStream_t s);
 // grouped expert GEMM on gemm_big tiles (bm = 128 or 256 rows per tile; large per-expert row counts)
 int launch_gemm_moe_big(const uint16_t* X, int ldx, const uint16_t* W, void* Y, int ldy, bool out_f32, int epi,
                         const int* off, const int* gather, int E, int max_rows, int N, int K, int S, long ysplit,

@@ -76,6 +76,84 @@ void launch_rmsnorm(const uint16_t* x, const uint16_t* res, const uint16_t* w, u
     rmsnorm_kernel<8><<<rows, 256, 0, s>>>(x, res, w, out, res_out, D, eps);
 }
 
+// ---------------------------------------------------------------- split-K reduce + residual + RMSNorm
+// One workgroup per row: h = bf16(h + bias + sum_s ws[s][row]) (in place), out = rmsnorm(h) * w.  Replaces
+// the split-K reduce kernel of a residual projection (o_proj / down_proj) and the RMSNorm that follows it.
+template <int MAXC>
+__global__ __launch_bounds__(256) void splitk_resid_rmsnorm_kernel(const float* __restrict__ ws, int S,
+                                                                   size_t sstride, const uint16_t* __restrict__ bias,
+                                                                   uint16_t* __restrict__ h,
+                                                                   const uint16_t* __restrict__ w,
+                                                                   uint16_t* __restrict__ out, int D, float eps) {
+  __shared__ float red[4];
+  const int row = blockIdx.x, tid = threadIdx.x, nchunk = D >> 3;
+  const size_t base = (size_t)row * D;
+  float v[MAXC][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXC; ++i) {
+    const int c = tid + i * 256;
+    if (c < nchunk) {
+      const s16x8 a = ld16(h + base + c * 8);
+      float acc[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = bf2f(a[j]);
+      if (bias != nullptr) {
+        const s16x8 bv = ld16(bias + c * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += bf2f(bv[j]);
+      }
+      const float* sp = ws + base + c * 8;
+      for (int sl = 0; sl < S; ++sl, sp += sstride) {
+        const f32x4 p0 = *reinterpret_cast<const f32x4*>(sp), p1 = *reinterpret_cast<const f32x4*>(sp + 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          acc[j] += p0[j];
+          acc[4 + j] += p1[j];
+        }
+      }
+      s16x8 hv;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        hv[j] = (short)f2bf(acc[j]);
+        v[i][j] = bf2f(hv[j]);  // normalise the stored (bf16) stream, as the unfused path does
+        ss += v[i][j] * v[i][j];
+      }
+      st16(h + base + c * 8, hv);
+    }
+  }
+  ss = wave_sum(ss);
+  if ((tid & 63) == 0) red[tid >> 6] = ss;
+  __syncthreads();
+  ss = red[0] + red[1] + red[2] + red[3];
+  const float inv = rsqrtf(ss / (float)D + eps);
+#pragma unroll
+  for (int i = 0; i < MAXC; ++i) {
+    const int c = tid + i * 256;
+    if (c < nchunk) {
+      s16x8 wv = ld16(w + c * 8), o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (short)f2bf(v[i][j] * inv * bf2f(wv[j]));
+      st16(out + base + c * 8, o);
+    }
+  }
+}
+
+void launch_splitk_resid_rmsnorm(const float* ws, int S, const uint16_t* bias, uint16_t* h, const uint16_t* w,
+                                 uint16_t* out, int rows, int D, float eps, hipStream_t s) {
+  if (rows <= 0) return;
+  const int nchunk = D / 8;
+  const size_t ss = (size_t)rows * D;
+  if (nchunk <= 256)
+    splitk_resid_rmsnorm_kernel<1><<<rows, 256, 0, s>>>(ws, S, ss, bias, h, w, out, D, eps);
+  else if (nchunk <= 512)
+    splitk_resid_rmsnorm_kernel<2><<<rows, 256, 0, s>>>(ws, S, ss, bias, h, w, out, D, eps);
+  else if (nchunk <= 1024)
+    splitk_resid_rmsnorm_kernel<4><<<rows, 256, 0, s>>>(ws, S, ss, bias, h, w, out, D, eps);
+  else
+    splitk_resid_rmsnorm_kernel<8><<<rows, 256, 0, s>>>(ws, S, ss, bias, h, w, out, D, eps);
+}
+
 // ---------------------------------------------------------------- RMSNorm bwd
 // y = x * inv * w  (inv = rsqrt(mean(x^2)+eps))
 // dx = inv * (w*dy - xhat * mean(xhat * w * dy)),  dw += sum_rows dy * xhat

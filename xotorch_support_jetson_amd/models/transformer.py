@@ -28,7 +28,7 @@ import torch
 from ..inference.shard import Shard
 from ..ops import kernels as K
 from ..ops._ext import require
-from ..ops.linear import layout_of, linear
+from ..ops.linear import layout_of, linear, linear_resid_norm
 from ..ops.rope import build_cos_sin
 from .config import ModelConfig
 from .weights import ShardWeights, expert
@@ -100,12 +100,17 @@ class ShardModel:
       return K.attn_decode(q, kc, vc, inp.block_tables, inp.ctx_lens, self.scale, self.ws)
     return K.attn_prefill(q, kc, vc, inp.block_tables, inp.cu_q, inp.ctx_lens, inp.max_qlen, self.scale)
 
-  def _mlp(self, xn: torch.Tensor, lw, h: torch.Tensor) -> torch.Tensor:
+  def _mlp(self, xn: torch.Tensor, lw, h: torch.Tensor, next_norm: Optional[torch.Tensor]):
+    """h += MLP(xn) in place; returns rmsnorm(h) * next_norm (None if there is no following norm)."""
     c = self.c
     if not c.is_moe:
       act = linear(xn, lw.gu_w, epi="silu")
-      return linear(act, lw.down_w, residual=h, epi="resid", out=h)
-    return self._moe(xn, lw, h)
+      if next_norm is not None:
+        return linear_resid_norm(act, lw.down_w, h, next_norm, c.rms_norm_eps)
+      linear(act, lw.down_w, residual=h, epi="resid", out=h)
+      return None
+    self._moe(xn, lw, h)
+    return K.rmsnorm(h, next_norm, c.rms_norm_eps)[0] if next_norm is not None else None
 
   def _moe(self, xn: torch.Tensor, lw, h: torch.Tensor) -> torch.Tensor:
     """Mixtral sparse MoE: softmax top-k routing, tokens grouped per expert, expert GEMMs on the
@@ -181,20 +186,26 @@ class ShardModel:
       h = K.embedding(x, w.embed)
     else:
       h = x.contiguous().clone() if x.dtype == torch.bfloat16 else x.to(torch.bfloat16).contiguous()
+    last = self.shard.is_last_layer()
+    n = len(self.layer_ids)
+    xn, _ = K.rmsnorm(h, w.layers[self.layer_ids[0]].ln1, c.rms_norm_eps) if n else (None, None)
     for j, li in enumerate(self.layer_ids):
       lw = w.layers[li]
-      xn, _ = K.rmsnorm(h, lw.ln1, c.rms_norm_eps)
       qkv = linear(xn, lw.qkv_w, bias=lw.qkv_b)
       q = K.rope_kv_write(qkv, inp.positions, self.cos_sin, inp.slots, self.kv.k[j], self.kv.v[j], c.num_heads,
                           c.num_kv_heads)
       a = self._attention(q, j, inp).view(h.shape[0], c.num_heads * c.head_dim)
-      h = linear(a, lw.o_w, residual=h, epi="resid", out=h)
-      xn, _ = K.rmsnorm(h, lw.ln2, c.rms_norm_eps)
-      h = self._mlp(xn, lw, h)
-    if not self.shard.is_last_layer():
+      # o_proj + residual + post-attention norm (one fused pass when the projection runs split-K)
+      xn = linear_resid_norm(a, lw.o_w, h, lw.ln2, c.rms_norm_eps)
+      # the norm that follows this layer: the next layer's input norm, or the final norm (decode: every row
+      # is a sequence's last token) -- fused into the down projection's reduce the same way
+      nxt = w.layers[self.layer_ids[j + 1]].ln1 if j + 1 < n else (w.norm if last and inp.decode else None)
+      xn = self._mlp(xn, lw, h, nxt)
+    if not last:
       return h
-    hl = h.index_select(0, inp.last_idx) if not inp.decode else h
-    xn, _ = K.rmsnorm(hl, w.norm, c.rms_norm_eps)
+    if not inp.decode or n == 0:
+      hl = h.index_select(0, inp.last_idx) if not inp.decode else h
+      xn, _ = K.rmsnorm(hl, w.norm, c.rms_norm_eps)
     return linear(xn, w.lm_head, out_dtype=torch.float32)
 
 

@@ -352,3 +352,34 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, r
   cfg = policy.shuffled_cfg(x, w, bias, residual, epi, dt)
   _shuffled_call(x, w, bias, residual, epi, out, cfg)
   return out
+
+
+# XOT_FUSE_NORM=0: keep the split-K reduce and the following RMSNorm as separate kernels
+FUSE_NORM = os.environ.get("XOT_FUSE_NORM", "1") == "1"
+
+
+def linear_resid_norm(x: torch.Tensor, w: torch.Tensor, h: torch.Tensor, ln_w: torch.Tensor, eps: float,
+                      bias: torch.Tensor | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
+  """h += x @ w.T (+ bias) in place (the residual stream) and return rmsnorm(h) * ln_w.
+
+  When the projection runs split-K on the pre-shuffled layout, the GEMM leaves its fp32 slabs and one
+  kernel does the slab reduce, the residual add and the RMSNorm (instead of reduce + norm kernels)."""
+  if FUSE_NORM and x.is_cuda and layout_of(w) == "stream":
+    if x.stride(1) != 1 or x.stride(0) % 8:
+      x = x.contiguous()
+    M, N = x.shape[0], w.shape[0]
+    cfg = policy.shuffled_cfg(x, w, bias, h, "resid", h.dtype)
+    if cfg[0] in ("stream", "big") and cfg[2] > 1:
+      S = cfg[2]
+      ws = scratch.splitk(x.device, S * M * N)
+      C = require()
+      if cfg[0] == "stream":
+        C.gemm_stream(x, w, h, None, h, ws, K.EPI["resid"], cfg[1], S, True, None, False)
+      else:
+        C.gemm_big(x, w, h, None, h, ws, K.EPI["resid"], cfg[1], S, False)
+      out = torch.empty_like(h) if out is None else out
+      C.splitk_resid_rmsnorm(ws, S, bias, h, ln_w, out, float(eps))
+      return out
+  linear(x, w, bias=bias, residual=h, epi="resid", out=h)
+  return K.rmsnorm(h, ln_w, eps, out=out)[0]
+
