@@ -296,7 +296,9 @@ def test_gemm_stream(gpu, M, epi, ntw, splits):
 
 @pytest.mark.parametrize("M", [1, 77, 256, 300, 512, 700])
 @pytest.mark.parametrize("epi,bn,splits", [("none", 256, 1), ("none", 128, 1), ("resid", 256, 1), ("silu", 256, 1),
-                                           ("silu", 128, 1), ("none", 256, 3), ("resid", 128, 2), ("silu", 256, 5)])
+                                           ("silu", 128, 1), ("none", 256, 3), ("resid", 128, 2), ("silu", 256, 5),
+                                           ("none", 1256, 1), ("resid", 1256, 1), ("silu", 1256, 1), ("none", 1256, 3),
+                                           ("resid", 1256, 4)])
 def test_gemm_big(gpu, M, epi, bn, splits):
   """Large-M LDS-DMA GEMM on the pre-shuffled layout vs the fp32 reference: masked row tiles, both
   column tilings, uneven split-K ranges, every epilogue, fp32 and bf16 outputs."""
@@ -334,9 +336,11 @@ def test_gemm_big_exact_layout(gpu):
   x = torch.randint(-3, 4, (M, Kd), generator=g).to(torch.bfloat16).to(gpu)
   w = torch.randint(-3, 4, (N, Kd), generator=g).to(torch.bfloat16).to(gpu)
   y = torch.empty(M, N, device=gpu, dtype=torch.float32)
-  require().gemm_big(x, shuffle_for_stream(w), y, None, None, None, 0, 256, 1)
   ref = x.float() @ w.float().t()
-  assert torch.equal(y, ref)
+  for bn in (256, 128, 1256):  # 1256: ping-pong schedule of the 256 x 256 tile
+    y.zero_()
+    require().gemm_big(x, shuffle_for_stream(w), y, None, None, None, 0, bn, 1)
+    assert torch.equal(y, ref), bn
 
 
 # ------------------------------------------------------------------ mixture of experts

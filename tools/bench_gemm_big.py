@@ -66,10 +66,10 @@ def main():
       ref = L._blas(x, wl[0], None, res, epi, None, torch.bfloat16).float()
       flop = 2 * M * N * Kd
       big = {}
-      for bn in (256, 128):
-        if N % bn:
+      for bn in (256, 1256, 128):
+        if N % (bn % 1000):
           continue
-        tiles = -(-M // 256) * (N // bn)
+        tiles = -(-M // 256) * (N // (bn % 1000))
         for S in (1, 2, 3, 4, 6, 8):
           if S > 1 and (tiles * S > 1024 or S * M * N > ws_buf.numel()):
             continue

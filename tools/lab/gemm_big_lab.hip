@@ -11,14 +11,17 @@ using namespace xot;
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
 
-template <int BN, int BK, int NBUF, int ABL, int AA = 0, int AB = 0, bool PRIO = false>
+static int g_ldx_pad = 0;  // extra elements per X row (L2 channel spread experiment)
+
+template <int BN, int BK, int NBUF, int ABL, int AA = 0, int AB = 0, bool PRIO = false, bool PP = false>
 float run(const uint16_t* X, const uint16_t* W, uint16_t* Y, float* ws, int M, int N, int K, int S, size_t wstride,
           int ncopies) {
+  const int ldx = K + g_ldx_pad;
   constexpr int WM = BN == 256 ? 2 : 4, WN = 8 / WM;
   constexpr int SMEM = NBUF * (256 + BN) * BK * 2;
   const int nwg = ((M + 255) / 256) * (N / BN) * S;
-  auto k1 = gemm_big_kernel<256, BN, WM, WN, BK, NBUF, EPI_NONE, false, false, 0, ABL, AA, AB, PRIO>;
-  auto k2 = gemm_big_kernel<256, BN, WM, WN, BK, NBUF, EPI_NONE, false, true, 0, ABL, AA, AB, PRIO>;
+  auto k1 = gemm_big_kernel<256, BN, WM, WN, BK, NBUF, EPI_NONE, false, false, 0, ABL, AA, AB, PRIO, PP>;
+  auto k2 = gemm_big_kernel<256, BN, WM, WN, BK, NBUF, EPI_NONE, false, true, 0, ABL, AA, AB, PRIO, PP>;
   CK(hipFuncSetAttribute((const void*)k1, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM));
   CK(hipFuncSetAttribute((const void*)k2, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM));
   hipEvent_t a, b;
@@ -28,8 +31,8 @@ float run(const uint16_t* X, const uint16_t* W, uint16_t* Y, float* ws, int M, i
   for (int r = 0; r < 12; ++r) {
     const uint16_t* Wc = W + (size_t)(r % ncopies) * wstride;
     CK(hipEventRecord(a));
-    if (S == 1) k1<<<nwg, 512, SMEM>>>(X, K, Wc, nullptr, nullptr, 0, Y, N, nullptr, M, N, K, 1, nullptr, nullptr, 0L);
-    else k2<<<nwg, 512, SMEM>>>(X, K, Wc, nullptr, nullptr, 0, Y, N, ws, M, N, K, S, nullptr, nullptr, 0L);
+    if (S == 1) k1<<<nwg, 512, SMEM>>>(X, ldx, Wc, nullptr, nullptr, 0, Y, N, nullptr, M, N, K, 1, nullptr, nullptr, 0L);
+    else k2<<<nwg, 512, SMEM>>>(X, ldx, Wc, nullptr, nullptr, 0, Y, N, ws, M, N, K, S, nullptr, nullptr, 0L);
     CK(hipEventRecord(b));
     CK(hipEventSynchronize(b));
     float ms;
@@ -65,17 +68,36 @@ int main(int argc, char** argv) {
   const int nc = (int)std::max<size_t>(2, (1ull << 30) / (wsz * 2) + 1);
   uint16_t *X, *W, *Y;
   float* ws;
-  CK(hipMalloc(&X, (size_t)M * K * 2));
+  CK(hipMalloc(&X, (size_t)M * (K + 1024) * 2));
   CK(hipMalloc(&W, wsz * 2 * nc));
   CK(hipMalloc(&Y, (size_t)M * N * 4));
   CK(hipMalloc(&ws, (size_t)S * M * N * 4));
-  CK(hipMemset(X, 0x3c, (size_t)M * K * 2));
+  CK(hipMemset(X, 0x3c, (size_t)M * (K + 1024) * 2));
   CK(hipMemset(W, 0x3c, wsz * 2 * nc));
   if (only < 0 || only == 0) sweep<256, 64, 2>(X, W, Y, ws, M, N, K, S, wsz, nc, abl);
   if (only < 0 || only == 1) sweep<256, 32, 4>(X, W, Y, ws, M, N, K, S, wsz, nc, abl);
   if (only < 0 || only == 2) sweep<256, 32, 3>(X, W, Y, ws, M, N, K, S, wsz, nc, abl);
   if (only < 0 || only == 3) sweep<128, 64, 3>(X, W, Y, ws, M, N, K, S, wsz, nc, abl);
   if (only < 0 || only == 4) sweep<128, 32, 4>(X, W, Y, ws, M, N, K, S, wsz, nc, abl);
+  if (only == 6) {  // ping-pong schedule vs the one-barrier-per-stage loop
+    const double flop = 2.0 * M * N * K;
+    for (int rep = 0; rep < 2; ++rep) {
+      const float a = run<256, 64, 2, 0, 0, 3>(X, W, Y, ws, M, N, K, S, wsz, nc);
+      const float b = run<256, 64, 2, 0, 0, 3, false, true>(X, W, Y, ws, M, N, K, S, wsz, nc);
+      printf("M=%d N=%d K=%d S=%d base %.1f us (%.0f TF/s)  pp %.1f us (%.0f TF/s)\n", M, N, K, S, a, flop / a / 1e6, b,
+             flop / b / 1e6);
+    }
+  }
+  if (only == 7) {  // X row stride padding
+    const double flop = 2.0 * M * N * K;
+    for (int pad : {0, 64, 128, 512, 0}) {
+      g_ldx_pad = pad;
+      const float a = run<256, 64, 2, 0, 0, 3>(X, W, Y, ws, M, N, K, S, wsz, nc);
+      const float b = run<256, 64, 2, 1, 0, 3>(X, W, Y, ws, M, N, K, S, wsz, nc);
+      printf("ldx pad %4d: full %.1f us (%.0f TF/s)  no-mfma %.1f us\n", pad, a, flop / a / 1e6, b);
+    }
+    g_ldx_pad = 0;
+  }
   if (only == 8) {  // s_setprio around the MFMA clusters
     const double flop = 2.0 * M * N * K;
     for (int rep = 0; rep < 2; ++rep) {

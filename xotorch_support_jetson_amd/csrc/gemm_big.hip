@@ -48,8 +48,14 @@ __device__ __forceinline__ void wait_vm() {
 // moe_off[e+1] of the expert-sorted slot order; MOE 2 gathers X row moe_gather[slot]); M is the
 // worst-case rows per expert (row tiles past an expert's count exit at once, so the grid is fixed and
 // graph-capturable).  A K split writes fp32 partial slabs ysplit elements apart (summed by the consumer).
+// PP: two-group ping-pong schedule (BM = BN = 256, 2 x 4 waves, BK = 64, 2 buffers): each 64-deep stage
+// is 4 phases of 16 MFMAs (one 64 x 32 quadrant of the wave's 128 x 64 tile); phase = {fragment reads ->
+// barrier -> MFMAs -> barrier}; the row-half-1 waves run one barrier behind, so on every SIMD one wave's
+// MFMAs overlap the other's LDS reads.  A stage is read only in its phases 0-2 (A halves in 0 and 2, B
+// halves in 0 and 1), so in phase 3 the stage two ahead is issued into the buffer being finished, and
+// the stage one ahead is retired by a counted vmcnt (LDS-DMA stays in flight across the barriers).
 template <int BM, int BN, int WM, int WN, int BK, int NBUF, int EPI, bool OUT_F32, bool SPLIT, int MOE = 0, int ABL = 0,
-          int AUXA = 0, int AUXB = 3, bool PRIO = false>
+          int AUXA = 0, int AUXB = 3, bool PRIO = false, bool PP = false>
 __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __restrict__ X, int ldx,
                                                           const uint16_t* __restrict__ W,
                                                           const uint16_t* __restrict__ bias,
@@ -205,7 +211,83 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
     else wait_vm<0>();
   };
 
-  if (T > 0) {
+  if constexpr (PP) {
+    static_assert(BM == 256 && BN == 256 && WM == 2 && WN == 4 && BK == 64 && NBUF == 2 && ABL == 0, "PP geometry");
+    auto bar = []() {  // raw barrier (no vmcnt / lgkmcnt drain); the asm statements are compiler fences
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    };
+    s16x8 af[4][2], bq[2][2][2];
+    auto read_a = [&](int buf, int qm) {
+      const uint16_t* As = smem + buf * STAGE;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) af[i][s2] = ld16(As + aoff[4 * qm + i][s2]);
+    };
+    auto read_b = [&](int buf, int qn) {
+      const uint16_t* Bs = smem + buf * STAGE + A_ELEMS;
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) bq[qn][j][s2] = ld16(Bs + boff + ((2 * qn + j) * KS + s2) * 512);
+    };
+    auto quad = [&](int qm, int qn) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[4 * qm + i][2 * qn + j] = mfma16(af[i][s2], bq[qn][j][s2], acc[4 * qm + i][2 * qn + j]);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    if (T > 0) {
+      issue(t_beg, 0);
+      if (T > 1) {
+        issue(t_beg + 1, 1);
+        wait_vm<NI>();
+      } else {
+        wait_vm<0>();
+      }
+      bar();
+      // wave-uniform branch (an EXEC-masked s_barrier would still execute)
+      const int half = __builtin_amdgcn_readfirstlane(wm);
+      if (half == 1) bar();  // row-half 1 runs one barrier behind
+      for (int t = 0; t < T; ++t) {
+        const int buf = t & 1;
+        read_a(buf, 0);  // phase 0
+        read_b(buf, 0);
+        bar();
+        quad(0, 0);
+        bar();
+        read_b(buf, 1);  // phase 1 (last B read of this stage)
+        bar();
+        quad(0, 1);
+        bar();
+        read_a(buf, 1);  // phase 2 (last A read of this stage)
+        bar();
+        quad(1, 1);
+        bar();
+        // phase 3: every wave finished reading this buffer two barriers ago -> refill it with stage t+2;
+        // retire stage t+1 (the younger stage t+2 stays in flight)
+        if (t + 2 < T) {
+          issue(t_beg + t + 2, buf);
+          wait_vm<NI>();
+        } else {
+          wait_vm<0>();
+        }
+        bar();
+        quad(1, 0);
+        bar();
+      }
+      if (half == 0) bar();  // balance the barrier count
+    }
+  } else if (T > 0) {
     // prologue: stages 0 .. PD-1 in flight, stage 0 landed
 #pragma unroll
     for (int p = 0; p < PD; ++p)
@@ -290,7 +372,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
   }
 }
 
-template <int BM, int BN, int WM, int WN, int BK, int NBUF, int EPI, bool F32>
+template <int BM, int BN, int WM, int WN, int BK, int NBUF, int EPI, bool F32, bool PP = false>
 static void big_launch(const uint16_t* X, int ldx, const uint16_t* W, const uint16_t* bias, const uint16_t* R,
                        int ldr, void* Y, int ldy, float* ws, int M, int N, int K, int S, bool reduce,
                        hipStream_t st) {
@@ -298,13 +380,13 @@ static void big_launch(const uint16_t* X, int ldx, const uint16_t* W, const uint
   static_assert(SMEM <= 160 * 1024, "LDS");
   const int nwg = ((M + BM - 1) / BM) * (N / BN) * S;
   if (S == 1) {
-    auto kern = gemm_big_kernel<BM, BN, WM, WN, BK, NBUF, EPI, F32, false>;
+    auto kern = gemm_big_kernel<BM, BN, WM, WN, BK, NBUF, EPI, F32, false, 0, 0, 0, 3, false, PP>;
     static bool attr = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM) ==
                        hipSuccess;
     (void)attr;
     kern<<<nwg, 512, SMEM, st>>>(X, ldx, W, bias, R, ldr, Y, ldy, nullptr, M, N, K, 1, nullptr, nullptr, 0L);
   } else {
-    auto kern = gemm_big_kernel<BM, BN, WM, WN, BK, NBUF, EPI, false, true>;
+    auto kern = gemm_big_kernel<BM, BN, WM, WN, BK, NBUF, EPI, false, true, 0, 0, 0, 3, false, PP>;
     static bool attr = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM) ==
                        hipSuccess;
     (void)attr;
@@ -324,6 +406,8 @@ static int big_dispatch(const uint16_t* X, int ldx, const uint16_t* W, const uin
                         bool reduce, hipStream_t st) {
   if (bn == 256)
     big_launch<256, 256, 2, 4, 64, 2, EPI, F32>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, S, reduce, st);
+  else if (bn == 1256)  // ping-pong schedule of the 256 x 256 tile
+    big_launch<256, 256, 2, 4, 64, 2, EPI, F32, true>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, S, reduce, st);
   else if (bn == 128)
     big_launch<256, 128, 4, 2, 64, 3, EPI, F32>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, S, reduce, st);
   else
@@ -335,7 +419,8 @@ int launch_gemm_big(const uint16_t* X, int ldx, const uint16_t* W, const uint16_
                     void* Y, int ldy, bool out_f32, int epi, float* ws, long ws_elems, int M, int N, int K, int bn,
                     int S, bool reduce, hipStream_t s) {
   if (M <= 0) return 0;
-  if ((bn != 128 && bn != 256) || N % bn != 0 || K % 128 != 0 || S < 1 || S > K / 64) return -1;
+  const int tile_n = bn == 1256 ? 256 : bn;
+  if ((bn != 128 && bn != 256 && bn != 1256) || N % tile_n != 0 || K % 128 != 0 || S < 1 || S > K / 64) return -1;
   if (S > 1 && (ws == nullptr || ws_elems < (long)S * M * N)) return -1;
   if (epi == EPI_SILU && N % 32 != 0) return -1;
   if (epi == EPI_SILU)

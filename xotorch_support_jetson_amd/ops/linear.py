@@ -196,10 +196,10 @@ class GemmPolicy:
   def _big_cands(M, N, Kd):
     cands = []
     tiles0 = -(-M // 256)
-    for bn in (256, 128):
-      if N % bn:
+    for bn in (256, 1256, 128):  # 1256: the 256 x 256 tile on the two-group ping-pong schedule
+      if N % (bn % 1000):
         continue
-      tiles = tiles0 * (N // bn)
+      tiles = tiles0 * (N // (bn % 1000))
       for S in (1, 2, 3, 4, 6, 8):
         if S > 1 and (tiles >= 256 or tiles * S > 1024 or Kd // 64 < 2 * S):
           continue
@@ -255,8 +255,8 @@ class GemmPolicy:
     for c in cands:
       if c[0] != "big":
         continue
-      tiles = -(-M // 256) * (N // c[1]) * c[2]
-      score = abs(tiles - 256) + (0 if c[1] == 256 else 64)
+      tiles = -(-M // 256) * (N // (c[1] % 1000)) * c[2]
+      score = abs(tiles - 256) + (0 if c[1] == 1256 else 64)
       if best is None or score < best[0]:
         best = (score, c)
     return best[1]
