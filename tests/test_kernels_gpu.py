@@ -399,3 +399,26 @@ def test_moe_layer(gpu, T, E, k, shuffled):
         out = h.clone()
         C.moe_combine(y, slot_of, topw, out, S)
         assert rel_err(out.float() - h.float(), ref - h.float()) < 3e-2, (bm, S)
+
+
+@pytest.mark.parametrize("B,L,H,Hkv,Dh", [(1, 64, 4, 1, 64), (2, 100, 8, 2, 128), (1, 300, 8, 8, 64),
+                                          (2, 257, 16, 4, 128)])
+def test_attention_train_fwd_bwd(gpu, B, L, H, Hkv, Dh):
+  """Training attention kernels (fwd, dQ, dK/dV) vs fp32 torch autograd of causal GQA attention, with
+  q / k / v given as strided row views of one fused qkv tensor (as the trainer passes them)."""
+  from xotorch_support_jetson_amd.train import autograd_ops as A
+  torch.manual_seed(L + H)
+  qkv = (torch.randn(B * L, (H + 2 * Hkv) * Dh, device=gpu) * 0.5).to(torch.bfloat16).requires_grad_()
+  q = qkv[:, :H * Dh]
+  k = qkv[:, H * Dh:(H + Hkv) * Dh]
+  v = qkv[:, (H + Hkv) * Dh:]
+  o = A.attention(q, k, v, B, L, H, Hkv, Dh)
+  do = torch.randn_like(o)
+  o.backward(do)
+  g = qkv.grad.float().clone()
+  x = qkv.detach().float().requires_grad_()
+  ref = A._attn_ref(x[:, :H * Dh], x[:, H * Dh:(H + Hkv) * Dh], x[:, (H + Hkv) * Dh:], B, L, H, Hkv, Dh)
+  ref.backward(do.float())
+  assert rel_err(o, ref) < 2e-2
+  for name, sl in (("dq", slice(0, H * Dh)), ("dk", slice(H * Dh, (H + Hkv) * Dh)), ("dv", slice((H + Hkv) * Dh, None))):
+    assert rel_err(g[:, sl], x.grad[:, sl]) < 3e-2, name

@@ -1,0 +1,415 @@
+// Causal self-attention for the training step (flash-style, no S x S matrix), MFMA 16x16x32 bf16.
+//
+// Tensors are token-major slices of the projection outputs: Q [B*L, ldq] holding H heads of DH,
+// K / V [B*L, ldk / ldv] holding Hkv heads (GQA: query head h reads KV head h / (H / Hkv)).
+// Sequences are right-padded to L; causality alone keeps valid queries off padded keys.
+//
+//  fwd   grid (L/64, H, B): 4 waves x 16 query rows.  Per 64-key tile: K rows and V^T staged in LDS,
+//        S = Q.K^T, online softmax in the log2 domain, P through LDS into P.V.  Writes O and the
+//        per-row log2-sum-exp (lse2 = max + log2 sum, scores pre-scaled by scale*log2(e)).
+//  dq    grid (L/64, H, B): recomputes P from lse2, dP = dO.V^T, dS = P (dP - delta); dQ += dS.K.
+//        Also computes delta = rowsum(dO * O) for its rows and stores it for the dK/dV pass.
+//  dkdv  grid (L/64, Hkv, B): 4 waves x 16 keys; sweeps the G query heads x query tiles >= its key
+//        tile: S^T = K.Q^T, dP^T = V.dO^T with the query on the lane (lse2 / delta are lane-local);
+//        P^T and dS^T go through LDS into dV += P^T.dO and dK += dS^T.Q.  dK / dV need no cross-
+//        workgroup sum (each workgroup owns its keys), dQ needs none either (separate pass).
+//
+// Replaces torch SDPA in the reference-parity train step (the reference never implemented training:
+// xotorch/inference/inference_engine.py:34-35; the torchtune attention it would have used is
+// MultiHeadAttention via xotorch/inference/torch/models/general_mha.py:77-120).
+#include "common.h"
+#include "kernels.h"
+
+namespace xot {
+
+namespace {
+constexpr int TT = 64;  // query / key tile
+constexpr float NEG = -1e30f;
+constexpr float L2E = 1.4426950408889634f;
+
+__device__ __forceinline__ void wave_sync_lds() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// Stage a [64 rows][DH] token-major tile (rows row0.., clamped to L-1) into LDS as rows (ld RLD) and/or
+// transposed (ld TLD).  256 threads, 16-byte global loads.
+template <int DH, int RLD, int TLD, bool ROWS, bool TRANS>
+__device__ __forceinline__ void stage_tile(const uint16_t* __restrict__ src, long ld, int row0, int L,
+                                           uint16_t* rows, uint16_t* trans) {
+  constexpr int CPR = DH / 8;
+  for (int q = threadIdx.x; q < TT * CPR; q += 256) {
+    const int r = q / CPR, cc = q % CPR;
+    const int gr = min(row0 + r, L - 1);
+    const s16x8 v = ld16(src + (long)gr * ld + cc * 8);
+    if constexpr (ROWS) st16(rows + r * RLD + cc * 8, v);
+    if constexpr (TRANS) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) trans[(cc * 8 + e) * TLD + r] = (uint16_t)v[e];
+    }
+  }
+}
+}  // namespace
+
+// ---------------------------------------------------------------------------------------- forward
+template <int DH>
+__global__ __launch_bounds__(256) void attn_train_fwd_kernel(const uint16_t* __restrict__ Q, long ldq,
+                                                             const uint16_t* __restrict__ K, long ldk,
+                                                             const uint16_t* __restrict__ V, long ldv,
+                                                             uint16_t* __restrict__ O, long ldo,
+                                                             float* __restrict__ lse2, int L, int H, int Hkv,
+                                                             float scale) {
+  constexpr int KS = DH / 32, NDT = DH / 16;
+  constexpr int KLD = DH + 8, VLD = TT + 8, PLD = TT + 8;
+  __shared__ __attribute__((aligned(16))) uint16_t ks[TT * KLD];
+  __shared__ __attribute__((aligned(16))) uint16_t vt[DH * VLD];
+  __shared__ __attribute__((aligned(16))) uint16_t pl[4][16 * PLD];
+  const int qt = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const int kvh = h / (H / Hkv);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
+  const int q0 = qt * TT, qrow = q0 + 16 * wave;
+  const uint16_t* Qb = Q + (long)b * L * ldq + h * DH;
+  const uint16_t* Kb = K + (long)b * L * ldk + kvh * DH;
+  const uint16_t* Vb = V + (long)b * L * ldv + kvh * DH;
+  const float sl = scale * L2E;
+
+  s16x8 qf[KS];
+  {
+    const uint16_t* qp = Qb + (long)min(qrow + c, L - 1) * ldq + 8 * g;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) qf[s] = ld16(qp + 32 * s);
+  }
+  float m[4], l[4];
+  f32x4 o[NDT];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    m[r] = NEG;
+    l[r] = 0.f;
+  }
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  uint16_t* pw = pl[wave];
+
+  for (int kt = 0; kt <= qt; ++kt) {
+    const int k0 = kt * TT;
+    __syncthreads();  // previous tile's LDS reads done
+    stage_tile<DH, KLD, VLD, true, false>(Kb, ldk, k0, L, ks, nullptr);
+    stage_tile<DH, KLD, VLD, false, true>(Vb, ldv, k0, L, nullptr, vt);
+    __syncthreads();
+    f32x4 sc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      sc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < KS; ++s) sc[t] = mfma16(qf[s], ld16(ks + (16 * t + c) * KLD + 32 * s + 8 * g), sc[t]);
+    }
+    float mt[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) mt[r] = NEG;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = k0 + 16 * t + c, qi = qrow + 4 * g + r;
+        const float v = (key <= qi && key < L) ? sc[t][r] * sl : -INFINITY;
+        sc[t][r] = v;
+        mt[r] = fmaxf(mt[r], v);
+      }
+    float alpha[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      mt[r] = group16_max(mt[r]);
+      const float mn = fmaxf(m[r], mt[r]);
+      alpha[r] = exp2f(m[r] - mn);
+      m[r] = mn;
+      l[r] *= alpha[r];
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = exp2f(sc[t][r] - m[r]);
+        l[r] += p;
+        pw[(4 * g + r) * PLD + 16 * t + c] = f2bf(p);
+      }
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[dt][r] *= alpha[r];
+    wave_sync_lds();
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const s16x8 pa = ld16(pw + c * PLD + 32 * kk + 8 * g);
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) o[dt] = mfma16(pa, ld16(vt + (16 * dt + c) * VLD + 32 * kk + 8 * g), o[dt]);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    l[r] = group16_sum(l[r]);
+    const int qi = qrow + 4 * g + r;
+    if (qi >= L) continue;
+    const float inv = l[r] > 0.f ? 1.f / l[r] : 0.f;
+    uint16_t* op = O + ((long)b * L + qi) * ldo + h * DH + c;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) op[16 * dt] = f2bf(o[dt][r] * inv);
+    if (c == 0) lse2[((long)b * H + h) * L + qi] = m[r] + log2f(l[r]);
+  }
+}
+
+// ---------------------------------------------------------------------------------------- dQ (+ delta)
+template <int DH>
+__global__ __launch_bounds__(256) void attn_train_dq_kernel(const uint16_t* __restrict__ Q, long ldq,
+                                                            const uint16_t* __restrict__ K, long ldk,
+                                                            const uint16_t* __restrict__ V, long ldv,
+                                                            const uint16_t* __restrict__ O, long ldo,
+                                                            const uint16_t* __restrict__ dO, long lddo,
+                                                            const float* __restrict__ lse2, float* __restrict__ delta,
+                                                            uint16_t* __restrict__ dQ, long lddq, int L, int H,
+                                                            int Hkv, float scale) {
+  constexpr int KS = DH / 32, NDT = DH / 16;
+  constexpr int KLD = DH + 8, TLD = TT + 8, PLD = TT + 8;
+  __shared__ __attribute__((aligned(16))) uint16_t ks[TT * KLD];   // K rows (S = Q.K^T)
+  __shared__ __attribute__((aligned(16))) uint16_t vs[TT * KLD];   // V rows (dP = dO.V^T)
+  __shared__ __attribute__((aligned(16))) uint16_t kt_[DH * TLD];  // K^T (dQ += dS.K)
+  __shared__ __attribute__((aligned(16))) uint16_t pl[4][16 * PLD];
+  __shared__ float dl[4][16];
+  const int qt = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const int kvh = h / (H / Hkv);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
+  const int q0 = qt * TT, qrow = q0 + 16 * wave;
+  const uint16_t* Kb = K + (long)b * L * ldk + kvh * DH;
+  const uint16_t* Vb = V + (long)b * L * ldv + kvh * DH;
+  const float sl = scale * L2E;
+
+  s16x8 qf[KS], df[KS];
+  float dsum = 0.f;
+  {
+    const long row = (long)b * L + min(qrow + c, L - 1);
+    const uint16_t* qp = Q + row * ldq + h * DH + 8 * g;
+    const uint16_t* dp = dO + row * lddo + h * DH + 8 * g;
+    const uint16_t* opp = O + row * ldo + h * DH + 8 * g;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      qf[s] = ld16(qp + 32 * s);
+      df[s] = ld16(dp + 32 * s);
+      const s16x8 ov = ld16(opp + 32 * s);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dsum += bf2f(df[s][e]) * bf2f(ov[e]);
+    }
+  }
+  // delta of row c: sum over the 4 lane groups; broadcast to the C layout (rows 4g + r) through LDS
+  dsum += __shfl_xor(dsum, 16, 64);
+  dsum += __shfl_xor(dsum, 32, 64);
+  if (g == 0) {
+    dl[wave][c] = dsum;
+    if (qrow + c < L) delta[((long)b * H + h) * L + qrow + c] = dsum;
+  }
+  wave_sync_lds();
+  float del[4], lse[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    del[r] = dl[wave][4 * g + r];
+    const int qi = min(qrow + 4 * g + r, L - 1);
+    lse[r] = lse2[((long)b * H + h) * L + qi];
+  }
+  f32x4 dq[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) dq[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  uint16_t* pw = pl[wave];
+
+  for (int kt = 0; kt <= qt; ++kt) {
+    const int k0 = kt * TT;
+    __syncthreads();
+    stage_tile<DH, KLD, TLD, true, true>(Kb, ldk, k0, L, ks, kt_);
+    stage_tile<DH, KLD, TLD, true, false>(Vb, ldv, k0, L, vs, nullptr);
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      f32x4 sc = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        sc = mfma16(qf[s], ld16(ks + (16 * t + c) * KLD + 32 * s + 8 * g), sc);
+        dp = mfma16(df[s], ld16(vs + (16 * t + c) * KLD + 32 * s + 8 * g), dp);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = k0 + 16 * t + c, qi = qrow + 4 * g + r;
+        const float p = (key <= qi && key < L) ? exp2f(sc[r] * sl - lse[r]) : 0.f;
+        pw[(4 * g + r) * PLD + 16 * t + c] = f2bf(p * (dp[r] - del[r]));
+      }
+    }
+    wave_sync_lds();
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const s16x8 da = ld16(pw + c * PLD + 32 * kk + 8 * g);
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) dq[dt] = mfma16(da, ld16(kt_ + (16 * dt + c) * TLD + 32 * kk + 8 * g), dq[dt]);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int qi = qrow + 4 * g + r;
+    if (qi >= L) continue;
+    uint16_t* op = dQ + ((long)b * L + qi) * lddq + h * DH + c;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) op[16 * dt] = f2bf(dq[dt][r] * scale);
+  }
+}
+
+// ---------------------------------------------------------------------------------------- dK, dV
+template <int DH>
+__global__ __launch_bounds__(256) void attn_train_dkdv_kernel(const uint16_t* __restrict__ Q, long ldq,
+                                                              const uint16_t* __restrict__ K, long ldk,
+                                                              const uint16_t* __restrict__ V, long ldv,
+                                                              const uint16_t* __restrict__ dO, long lddo,
+                                                              const float* __restrict__ lse2,
+                                                              const float* __restrict__ delta,
+                                                              uint16_t* __restrict__ dK, long lddk,
+                                                              uint16_t* __restrict__ dV, long lddv, int L, int H,
+                                                              int Hkv, float scale) {
+  constexpr int KS = DH / 32, NDT = DH / 16;
+  constexpr int RLD = DH + 8, TLD = TT + 8, PLD = TT + 8;
+  extern __shared__ __attribute__((aligned(16))) uint16_t sm[];
+  uint16_t* qs = sm;                 // Q rows       [64][RLD]
+  uint16_t* ds_ = qs + TT * RLD;     // dO rows      [64][RLD]
+  uint16_t* qt_ = ds_ + TT * RLD;    // Q^T          [DH][TLD]
+  uint16_t* dt_ = qt_ + DH * TLD;    // dO^T         [DH][TLD]
+  uint16_t* pt = dt_ + DH * TLD;     // P^T / dS^T   [4 waves][2][16][PLD]
+  float* ld_ = reinterpret_cast<float*>(pt + 4 * 2 * 16 * PLD);  // lse2[64], delta[64]
+  const int kt = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
+  const int G = H / Hkv;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
+  const int k0 = kt * TT, krow = k0 + 16 * wave;
+  const float sl = scale * L2E;
+
+  s16x8 kf[KS], vf[KS];
+  {
+    const long row = (long)b * L + min(krow + c, L - 1);
+    const uint16_t* kp = K + row * ldk + kvh * DH + 8 * g;
+    const uint16_t* vp = V + row * ldv + kvh * DH + 8 * g;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      kf[s] = ld16(kp + 32 * s);
+      vf[s] = ld16(vp + 32 * s);
+    }
+  }
+  f32x4 dk[NDT], dv[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) dk[dt] = dv[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  uint16_t* pw = pt + wave * 2 * 16 * PLD;  // [0]: P^T, [1]: dS^T
+  const int nq = (L + TT - 1) / TT;
+
+  for (int hh = 0; hh < G; ++hh) {
+    const int h = kvh * G + hh;
+    const uint16_t* Qb = Q + (long)b * L * ldq + h * DH;
+    const uint16_t* Db = dO + (long)b * L * lddo + h * DH;
+    for (int qt = kt; qt < nq; ++qt) {
+      const int q0 = qt * TT;
+      __syncthreads();
+      stage_tile<DH, RLD, TLD, true, true>(Qb, ldq, q0, L, qs, qt_);
+      stage_tile<DH, RLD, TLD, true, true>(Db, lddo, q0, L, ds_, dt_);
+      if (threadIdx.x < TT) {
+        const int qi = min(q0 + (int)threadIdx.x, L - 1);
+        ld_[threadIdx.x] = lse2[((long)b * H + h) * L + qi];
+        ld_[TT + threadIdx.x] = delta[((long)b * H + h) * L + qi];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {  // 16-query sub-tiles: query on the lane (column c)
+        f32x4 st = f32x4{0.f, 0.f, 0.f, 0.f}, dpt = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          st = mfma16(kf[s], ld16(qs + (16 * t + c) * RLD + 32 * s + 8 * g), st);
+          dpt = mfma16(vf[s], ld16(ds_ + (16 * t + c) * RLD + 32 * s + 8 * g), dpt);
+        }
+        const int qi = q0 + 16 * t + c;
+        const float lq = ld_[16 * t + c], dq = ld_[TT + 16 * t + c];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = krow + 4 * g + r;
+          const float p = (key <= qi && qi < L) ? exp2f(st[r] * sl - lq) : 0.f;
+          pw[(4 * g + r) * PLD + 16 * t + c] = f2bf(p);
+          pw[16 * PLD + (4 * g + r) * PLD + 16 * t + c] = f2bf(p * (dpt[r] - dq));
+        }
+      }
+      wave_sync_lds();
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const s16x8 pa = ld16(pw + c * PLD + 32 * kk + 8 * g);
+        const s16x8 sa = ld16(pw + 16 * PLD + c * PLD + 32 * kk + 8 * g);
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) {
+          dv[dt] = mfma16(pa, ld16(dt_ + (16 * dt + c) * TLD + 32 * kk + 8 * g), dv[dt]);
+          dk[dt] = mfma16(sa, ld16(qt_ + (16 * dt + c) * TLD + 32 * kk + 8 * g), dk[dt]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int key = krow + 4 * g + r;
+    if (key >= L) continue;
+    uint16_t* kp = dK + ((long)b * L + key) * lddk + kvh * DH + c;
+    uint16_t* vp = dV + ((long)b * L + key) * lddv + kvh * DH + c;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) {
+      kp[16 * dt] = f2bf(dk[dt][r] * scale);
+      vp[16 * dt] = f2bf(dv[dt][r]);
+    }
+  }
+}
+
+template <int DH>
+static size_t dkdv_smem() {
+  return (size_t)(2 * TT * (DH + 8) + 2 * DH * (TT + 8) + 4 * 2 * 16 * (TT + 8)) * 2 + 2 * TT * sizeof(float);
+}
+
+int launch_attn_train_fwd(const uint16_t* q, long ldq, const uint16_t* k, long ldk, const uint16_t* v, long ldv,
+                          uint16_t* o, long ldo, float* lse2, int B, int L, int H, int Hkv, int Dh, float scale,
+                          hipStream_t s) {
+  if (B <= 0 || L <= 0) return 0;
+  if (H % Hkv != 0) return -1;
+  dim3 grid((L + TT - 1) / TT, H, B);
+  if (Dh == 128)
+    attn_train_fwd_kernel<128><<<grid, 256, 0, s>>>(q, ldq, k, ldk, v, ldv, o, ldo, lse2, L, H, Hkv, scale);
+  else if (Dh == 64)
+    attn_train_fwd_kernel<64><<<grid, 256, 0, s>>>(q, ldq, k, ldk, v, ldv, o, ldo, lse2, L, H, Hkv, scale);
+  else
+    return -1;
+  return 0;
+}
+
+int launch_attn_train_bwd(const uint16_t* q, long ldq, const uint16_t* k, long ldk, const uint16_t* v, long ldv,
+                          const uint16_t* o, long ldo, const uint16_t* dout, long lddo, const float* lse2,
+                          float* delta, uint16_t* dq, long lddq, uint16_t* dk, long lddk, uint16_t* dv, long lddv,
+                          int B, int L, int H, int Hkv, int Dh, float scale, hipStream_t s) {
+  if (B <= 0 || L <= 0) return 0;
+  if (H % Hkv != 0) return -1;
+  dim3 gq((L + TT - 1) / TT, H, B), gk((L + TT - 1) / TT, Hkv, B);
+  if (Dh == 128) {
+    attn_train_dq_kernel<128><<<gq, 256, 0, s>>>(q, ldq, k, ldk, v, ldv, o, ldo, dout, lddo, lse2, delta, dq, lddq,
+                                                  L, H, Hkv, scale);
+    static bool attr = hipFuncSetAttribute((const void*)attn_train_dkdv_kernel<128>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)dkdv_smem<128>()) ==
+                       hipSuccess;
+    (void)attr;
+    attn_train_dkdv_kernel<128><<<gk, 256, dkdv_smem<128>(), s>>>(q, ldq, k, ldk, v, ldv, dout, lddo, lse2, delta, dk,
+                                                                  lddk, dv, lddv, L, H, Hkv, scale);
+  } else if (Dh == 64) {
+    attn_train_dq_kernel<64><<<gq, 256, 0, s>>>(q, ldq, k, ldk, v, ldv, o, ldo, dout, lddo, lse2, delta, dq, lddq,
+                                                 L, H, Hkv, scale);
+    static bool attr = hipFuncSetAttribute((const void*)attn_train_dkdv_kernel<64>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)dkdv_smem<64>()) ==
+                       hipSuccess;
+    (void)attr;
+    attn_train_dkdv_kernel<64><<<gk, 256, dkdv_smem<64>(), s>>>(q, ldq, k, ldk, v, ldv, dout, lddo, lse2, delta, dk,
+                                                                lddk, dv, lddv, L, H, Hkv, scale);
+  } else {
+    return -1;
+  }
+  return 0;
+}
+
+}  // namespace xot

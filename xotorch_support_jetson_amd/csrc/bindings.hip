@@ -418,6 +418,52 @@ void attn_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tenso
   XCHECK(rc == 0, "attn_decode: unsupported H=", H, " Hkv=", Hkv, " Dh=", Dh);
 }
 
+// training attention: 2-D token-major views ([B*L, n*Dh] rows, unit inner stride; row strides may differ,
+// e.g. slices of the fused qkv projection)
+static void check_rows(const at::Tensor& t, int64_t rows, int64_t cols, const char* what) {
+  CHECK_BF16(t);
+  XCHECK(t.dim() == 2 && t.size(0) == rows && t.size(1) == cols && t.stride(1) == 1 && t.stride(0) % 8 == 0,
+         "attn_train: bad ", what, " view");
+}
+
+void attn_train_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, at::Tensor& o, at::Tensor& lse2,
+                    int64_t B, int64_t L, int64_t H, int64_t Hkv, int64_t Dh, double scale) {
+  check_rows(q, B * L, H * Dh, "q");
+  check_rows(k, B * L, Hkv * Dh, "k");
+  check_rows(v, B * L, Hkv * Dh, "v");
+  check_rows(o, B * L, H * Dh, "o");
+  CHECK_GPU(lse2);
+  CHECK_DT(lse2, at::kFloat);
+  XCHECK(lse2.is_contiguous() && lse2.numel() == B * H * L, "attn_train_fwd: lse2 [B, H, L]");
+  const int rc = xot::launch_attn_train_fwd(bf(q), q.stride(0), bf(k), k.stride(0), bf(v), v.stride(0), bf(o),
+                                            o.stride(0), lse2.data_ptr<float>(), (int)B, (int)L, (int)H, (int)Hkv,
+                                            (int)Dh, (float)scale, cur_stream());
+  XCHECK(rc == 0, "attn_train_fwd: unsupported H=", H, " Hkv=", Hkv, " Dh=", Dh);
+}
+
+void attn_train_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, const at::Tensor& o,
+                    const at::Tensor& dout, const at::Tensor& lse2, at::Tensor& delta, at::Tensor& dq, at::Tensor& dk,
+                    at::Tensor& dv, int64_t B, int64_t L, int64_t H, int64_t Hkv, int64_t Dh, double scale) {
+  check_rows(q, B * L, H * Dh, "q");
+  check_rows(k, B * L, Hkv * Dh, "k");
+  check_rows(v, B * L, Hkv * Dh, "v");
+  check_rows(o, B * L, H * Dh, "o");
+  check_rows(dout, B * L, H * Dh, "dout");
+  check_rows(dq, B * L, H * Dh, "dq");
+  check_rows(dk, B * L, Hkv * Dh, "dk");
+  check_rows(dv, B * L, Hkv * Dh, "dv");
+  CHECK_DT(lse2, at::kFloat);
+  CHECK_DT(delta, at::kFloat);
+  XCHECK(lse2.is_contiguous() && delta.is_contiguous() && lse2.numel() == B * H * L && delta.numel() == B * H * L,
+         "attn_train_bwd: lse2 / delta [B, H, L]");
+  const int rc = xot::launch_attn_train_bwd(bf(q), q.stride(0), bf(k), k.stride(0), bf(v), v.stride(0), bf(o),
+                                            o.stride(0), bf(dout), dout.stride(0), lse2.data_ptr<float>(),
+                                            delta.data_ptr<float>(), bf(dq), dq.stride(0), bf(dk), dk.stride(0),
+                                            bf(dv), dv.stride(0), (int)B, (int)L, (int)H, (int)Hkv, (int)Dh,
+                                            (float)scale, cur_stream());
+  XCHECK(rc == 0, "attn_train_bwd: unsupported H=", H, " Hkv=", Hkv, " Dh=", Dh);
+}
+
 void attn_prefill(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
                   const at::Tensor& block_tables, const at::Tensor& cu_q, const at::Tensor& ctx_lens, at::Tensor& out,
                   int64_t max_qlen, double scale) {
@@ -536,6 +582,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("ctx_lens"), py::arg("out"), py::arg("ws_o"), py::arg("ws_ml"), py::arg("pages_per_part"),
         py::arg("nparts"), py::arg("scale"), py::arg("algo") = 2);
   m.def("attn_prefill", &attn_prefill);
+  m.def("attn_train_fwd", &attn_train_fwd);
+  m.def("attn_train_bwd", &attn_train_bwd);
   m.def("sample", &sample);
   m.def("ce_fwd", &ce_fwd);
   m.def("ce_bwd", &ce_bwd);

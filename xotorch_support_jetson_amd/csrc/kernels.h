@@ -60,6 +60,15 @@ int launch_attn_prefill(const uint16_t* q, const uint16_t* kc, const uint16_t* v
                         int max_blocks, const int32_t* cu_q, const int32_t* ctx_lens, uint16_t* out, int B,
                         int max_qlen, int H, int Hkv, int Dh, float scale, int num_pages, hipStream_t s);
 
+// causal self-attention for training (token-major Q / K / V slices, GQA); lse2 [B, H, L] fp32 (log2 domain)
+int launch_attn_train_fwd(const uint16_t* q, long ldq, const uint16_t* k, long ldk, const uint16_t* v, long ldv,
+                          uint16_t* o, long ldo, float* lse2, int B, int L, int H, int Hkv, int Dh, float scale,
+                          hipStream_t s);
+int launch_attn_train_bwd(const uint16_t* q, long ldq, const uint16_t* k, long ldk, const uint16_t* v, long ldv,
+                          const uint16_t* o, long ldo, const uint16_t* dout, long lddo, const float* lse2,
+                          float* delta, uint16_t* dq, long lddq, uint16_t* dk, long lddk, uint16_t* dv, long lddv,
+                          int B, int L, int H, int Hkv, int Dh, float scale, hipStream_t s);
+
 void launch_sample(const float* logits, long ld, int B, int V, const float* temps, int top_k,
                    const int64_t* seed_off, int32_t* out, uint32_t* cand_key, int32_t* cand_idx, hipStream_t s);
 constexpr int SAMPLE_CAND_PER_ROW = 64 * 64;  // split path scratch: chunks x max top-k

@@ -4,7 +4,9 @@
   SiluMulFn    [gate | up] -> silu(gate) * up, backward silu_mul_bwd kernel
   RopeFn       rotate-half RoPE; backward = the inverse rotation (same kernel, sin negated)
   CrossEntropyFn  per-row loss with ignore (-100) and per-row weights; forward ce_fwd, backward ce_bwd
-Projections use torch.matmul (hipBLASLt) and attention uses torch SDPA in the training path.
+  AttentionFn  causal GQA self-attention: attn_train_fwd (flash-style, saves O and the row log2-sum-exp),
+               backward attn_train_bwd (dQ pass with delta = rowsum(dO*O), then the dK/dV pass)
+Projections use torch.matmul (hipBLASLt).
 """
 from __future__ import annotations
 
@@ -124,6 +126,55 @@ class CrossEntropyFn(torch.autograd.Function):
     oh = F.one_hot(targets.clamp(min=0).long(), logits.shape[-1]).float()
     d = (p - oh) * gs[:, None] * valid[:, None].float()
     return d.to(logits.dtype), None, None
+
+
+class AttentionFn(torch.autograd.Function):
+  """q [B*L, H*Dh], k / v [B*L, Hkv*Dh] (token-major, may be strided row views) -> o [B*L, H*Dh]."""
+
+  @staticmethod
+  def forward(ctx, q, k, v, B, L, H, Hkv, Dh):
+    scale = Dh ** -0.5
+    ctx.dims = (B, L, H, Hkv, Dh, scale)
+    if _gpu(q):
+      o = torch.empty(B * L, H * Dh, dtype=q.dtype, device=q.device)
+      lse2 = torch.empty(B * H * L, dtype=torch.float32, device=q.device)
+      require().attn_train_fwd(q, k, v, o, lse2, B, L, H, Hkv, Dh, scale)
+      ctx.save_for_backward(q, k, v, o, lse2)
+      return o
+    ctx.save_for_backward(q, k, v)
+    return _attn_ref(q, k, v, B, L, H, Hkv, Dh)
+
+  @staticmethod
+  def backward(ctx, do):
+    B, L, H, Hkv, Dh, scale = ctx.dims
+    if _gpu(do):
+      q, k, v, o, lse2 = ctx.saved_tensors
+      dq = torch.empty(B * L, H * Dh, dtype=q.dtype, device=q.device)
+      dk = torch.empty(B * L, Hkv * Dh, dtype=q.dtype, device=q.device)
+      dv = torch.empty_like(dk)
+      delta = torch.empty_like(lse2)
+      require().attn_train_bwd(q, k, v, o, do.contiguous().to(q.dtype), lse2, delta, dq, dk, dv, B, L, H, Hkv, Dh,
+                               scale)
+      return dq, dk, dv, None, None, None, None, None
+    q, k, v = ctx.saved_tensors
+    with torch.enable_grad():
+      qr, kr, vr = (t.detach().float().requires_grad_() for t in (q, k, v))
+      y = _attn_ref(qr, kr, vr, B, L, H, Hkv, Dh)
+      y.backward(do.float())
+    return qr.grad.to(q.dtype), kr.grad.to(k.dtype), vr.grad.to(v.dtype), None, None, None, None, None
+
+
+def _attn_ref(q, k, v, B, L, H, Hkv, Dh):
+  """fp32 causal GQA attention (reference / CPU path)."""
+  qh = q.float().reshape(B, L, H, Dh).transpose(1, 2)
+  kh = k.float().reshape(B, L, Hkv, Dh).transpose(1, 2).repeat_interleave(H // Hkv, dim=1)
+  vh = v.float().reshape(B, L, Hkv, Dh).transpose(1, 2).repeat_interleave(H // Hkv, dim=1)
+  a = F.scaled_dot_product_attention(qh, kh, vh, is_causal=True)
+  return a.transpose(1, 2).reshape(B * L, H * Dh).to(q.dtype)
+
+
+def attention(q, k, v, B, L, H, Hkv, Dh):
+  return AttentionFn.apply(q, k, v, B, L, H, Hkv, Dh)
 
 
 def rmsnorm(x, w, eps):

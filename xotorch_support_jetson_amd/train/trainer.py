@@ -9,9 +9,9 @@ The stage recomputes its forward inside `step` (activation checkpointing at stag
 no activations are kept between the hops.
 
 Numerics: bf16 working weights (leaf tensors with grads), fp32 master weights + fp32 AdamW moments
-updated by the fused HIP AdamW kernel, which also refreshes the bf16 copy.  RMSNorm, SiLU*mul, RoPE and
-the cross-entropy run on the kernel library's forward/backward kernels; GEMMs on hipBLASLt; attention
-on torch SDPA (causal).  Updated weights are written back into the inference shard lazily
+updated by the fused HIP AdamW kernel, which also refreshes the bf16 copy.  RMSNorm, SiLU*mul, RoPE,
+the causal GQA attention (flash-style fwd / dQ / dK-dV kernels) and the cross-entropy run on the kernel
+library's forward/backward kernels; GEMMs on hipBLASLt.  Updated weights are written back into the inference shard lazily
 (`sync_to_inference`) so `xot run` after `xot train` uses the trained model.
 """
 from __future__ import annotations
@@ -90,11 +90,7 @@ class ShardTrainer:
       q = A.rope(qkv[:, :H * Dh].contiguous(), pos, self.cos_sin, H, Dh)
       k = A.rope(qkv[:, H * Dh:(H + Hkv) * Dh].contiguous(), pos, self.cos_sin, Hkv, Dh)
       v = qkv[:, (H + Hkv) * Dh:]
-      q = q.view(B, L, H, Dh).transpose(1, 2)
-      k = k.view(B, L, Hkv, Dh).transpose(1, 2).repeat_interleave(H // Hkv, dim=1)
-      v = v.reshape(B, L, Hkv, Dh).transpose(1, 2).repeat_interleave(H // Hkv, dim=1)
-      a = F.scaled_dot_product_attention(q, k, v, is_causal=True)
-      a = a.transpose(1, 2).reshape(B * L, H * Dh)
+      a = A.attention(q, k, v, B, L, H, Hkv, Dh)  # flash-style HIP kernels (fwd + dQ + dK/dV)
       h = h + a @ P[f"{i}.o"].t()
       xn = A.rmsnorm(h, P[f"{i}.ln2"], c.rms_norm_eps)
       h = h + A.silu_mul((xn @ P[f"{i}.gu"].t()).contiguous()) @ P[f"{i}.down"].t()
