@@ -4,6 +4,10 @@
 // K / V [B*L, ldk / ldv] holding Hkv heads (GQA: query head h reads KV head h / (H / Hkv)).
 // Sequences are right-padded to L; causality alone keeps valid queries off padded keys.
 //
+// Operands that MFMA reads "by column" (V for P.V, K for dS.K, Q / dO for the dK / dV products) come from
+// pre-transposed [B, heads, DH, Lp] images (attn_train_transpose_kernel), so every staging copy is 16
+// bytes wide; the next tile is loaded into registers under the current tile's math.
+//
 //  fwd   grid (L/64, H, B): 4 waves x 16 query rows.  Per 64-key tile: K rows and V^T staged in LDS,
 //        S = Q.K^T, online softmax in the log2 domain, P through LDS into P.V.  Writes O and the
 //        per-row log2-sum-exp (lse2 = max + log2 sum, scores pre-scaled by scale*log2(e)).
@@ -33,30 +37,57 @@ __device__ __forceinline__ void wave_sync_lds() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
-// Stage a [64 rows][DH] token-major tile (rows row0.., clamped to L-1) into LDS as rows (ld RLD) and/or
-// transposed (ld TLD).  256 threads, 16-byte global loads.
-template <int DH, int RLD, int TLD, bool ROWS, bool TRANS>
-__device__ __forceinline__ void stage_tile(const uint16_t* __restrict__ src, long ld, int row0, int L,
-                                           uint16_t* rows, uint16_t* trans) {
-  constexpr int CPR = DH / 8;
-  for (int q = threadIdx.x; q < TT * CPR; q += 256) {
-    const int r = q / CPR, cc = q % CPR;
-    const int gr = min(row0 + r, L - 1);
-    const s16x8 v = ld16(src + (long)gr * ld + cc * 8);
-    if constexpr (ROWS) st16(rows + r * RLD + cc * 8, v);
-    if constexpr (TRANS) {
+// Register-staged tile copies (256 threads, 16-byte chunks): load() issues the global loads into registers
+// (in flight under the current tile's math), store() writes them to LDS after the barrier.
+//   rows tile:  [64 tokens][DH] of a token-major source (ld elements per token), tokens clamped to L-1
+//   trans tile: [DH][64 tokens] of a pre-transposed [.., DH, Lp] image (zero past L)
+template <int DH>
+struct RowsTile {
+  static constexpr int N = TT * DH / 8 / 256;  // chunks per thread
+  s16x8 v[N];
+  __device__ __forceinline__ void load(const uint16_t* __restrict__ src, long ld, int row0, int L) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) trans[(cc * 8 + e) * TLD + r] = (uint16_t)v[e];
+    for (int i = 0; i < N; ++i) {
+      const int q = threadIdx.x + 256 * i, r = q / (DH / 8), cc = q % (DH / 8);
+      v[i] = ld16(src + (long)min(row0 + r, L - 1) * ld + cc * 8);
     }
   }
-}
+  template <int RLD>
+  __device__ __forceinline__ void store(uint16_t* dst) const {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int q = threadIdx.x + 256 * i, r = q / (DH / 8), cc = q % (DH / 8);
+      st16(dst + r * RLD + cc * 8, v[i]);
+    }
+  }
+};
+template <int DH>
+struct TransTile {
+  static constexpr int N = DH * TT / 8 / 256;
+  s16x8 v[N];
+  __device__ __forceinline__ void load(const uint16_t* __restrict__ srcT, int Lp, int tok0) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int q = threadIdx.x + 256 * i, d = q / (TT / 8), cc = q % (TT / 8);
+      v[i] = ld16(srcT + (long)d * Lp + tok0 + cc * 8);
+    }
+  }
+  template <int TLD>
+  __device__ __forceinline__ void store(uint16_t* dst) const {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int q = threadIdx.x + 256 * i, d = q / (TT / 8), cc = q % (TT / 8);
+      st16(dst + d * TLD + cc * 8, v[i]);
+    }
+  }
+};
 }  // namespace
 
 // ---------------------------------------------------------------------------------------- forward
 template <int DH>
 __global__ __launch_bounds__(256) void attn_train_fwd_kernel(const uint16_t* __restrict__ Q, long ldq,
                                                              const uint16_t* __restrict__ K, long ldk,
-                                                             const uint16_t* __restrict__ V, long ldv,
+                                                             const uint16_t* __restrict__ VT, int Lp,
                                                              uint16_t* __restrict__ O, long ldo,
                                                              float* __restrict__ lse2, int L, int H, int Hkv,
                                                              float scale) {
@@ -69,14 +100,13 @@ __global__ __launch_bounds__(256) void attn_train_fwd_kernel(const uint16_t* __r
   const int kvh = h / (H / Hkv);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
   const int q0 = qt * TT, qrow = q0 + 16 * wave;
-  const uint16_t* Qb = Q + (long)b * L * ldq + h * DH;
   const uint16_t* Kb = K + (long)b * L * ldk + kvh * DH;
-  const uint16_t* Vb = V + (long)b * L * ldv + kvh * DH;
+  const uint16_t* VTb = VT + ((long)b * Hkv + kvh) * DH * Lp;
   const float sl = scale * L2E;
 
   s16x8 qf[KS];
   {
-    const uint16_t* qp = Qb + (long)min(qrow + c, L - 1) * ldq + 8 * g;
+    const uint16_t* qp = Q + ((long)b * L + min(qrow + c, L - 1)) * ldq + h * DH + 8 * g;
 #pragma unroll
     for (int s = 0; s < KS; ++s) qf[s] = ld16(qp + 32 * s);
   }
@@ -91,12 +121,20 @@ __global__ __launch_bounds__(256) void attn_train_fwd_kernel(const uint16_t* __r
   for (int dt = 0; dt < NDT; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
   uint16_t* pw = pl[wave];
 
+  RowsTile<DH> kr;
+  TransTile<DH> vr;
+  kr.load(Kb, ldk, 0, L);
+  vr.load(VTb, Lp, 0);
   for (int kt = 0; kt <= qt; ++kt) {
     const int k0 = kt * TT;
-    __syncthreads();  // previous tile's LDS reads done
-    stage_tile<DH, KLD, VLD, true, false>(Kb, ldk, k0, L, ks, nullptr);
-    stage_tile<DH, KLD, VLD, false, true>(Vb, ldv, k0, L, nullptr, vt);
+    __syncthreads();  // every wave is done with the previous tile
+    kr.template store<KLD>(ks);
+    vr.template store<VLD>(vt);
     __syncthreads();
+    if (kt < qt) {  // next tile in flight under this tile's math
+      kr.load(Kb, ldk, k0 + TT, L);
+      vr.load(VTb, Lp, k0 + TT);
+    }
     f32x4 sc[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -162,9 +200,10 @@ __global__ __launch_bounds__(256) void attn_train_fwd_kernel(const uint16_t* __r
 template <int DH>
 __global__ __launch_bounds__(256) void attn_train_dq_kernel(const uint16_t* __restrict__ Q, long ldq,
                                                             const uint16_t* __restrict__ K, long ldk,
+                                                            const uint16_t* __restrict__ KT,
                                                             const uint16_t* __restrict__ V, long ldv,
                                                             const uint16_t* __restrict__ O, long ldo,
-                                                            const uint16_t* __restrict__ dO, long lddo,
+                                                            const uint16_t* __restrict__ dO, long lddo, int Lp,
                                                             const float* __restrict__ lse2, float* __restrict__ delta,
                                                             uint16_t* __restrict__ dQ, long lddq, int L, int H,
                                                             int Hkv, float scale) {
@@ -181,7 +220,14 @@ __global__ __launch_bounds__(256) void attn_train_dq_kernel(const uint16_t* __re
   const int q0 = qt * TT, qrow = q0 + 16 * wave;
   const uint16_t* Kb = K + (long)b * L * ldk + kvh * DH;
   const uint16_t* Vb = V + (long)b * L * ldv + kvh * DH;
+  const uint16_t* KTb = KT + ((long)b * Hkv + kvh) * DH * Lp;
   const float sl = scale * L2E;
+
+  RowsTile<DH> kr, vr;
+  TransTile<DH> ktr;
+  kr.load(Kb, ldk, 0, L);
+  vr.load(Vb, ldv, 0, L);
+  ktr.load(KTb, Lp, 0);
 
   s16x8 qf[KS], df[KS];
   float dsum = 0.f;
@@ -211,8 +257,7 @@ __global__ __launch_bounds__(256) void attn_train_dq_kernel(const uint16_t* __re
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     del[r] = dl[wave][4 * g + r];
-    const int qi = min(qrow + 4 * g + r, L - 1);
-    lse[r] = lse2[((long)b * H + h) * L + qi];
+    lse[r] = lse2[((long)b * H + h) * L + min(qrow + 4 * g + r, L - 1)];
   }
   f32x4 dq[NDT];
 #pragma unroll
@@ -222,9 +267,15 @@ __global__ __launch_bounds__(256) void attn_train_dq_kernel(const uint16_t* __re
   for (int kt = 0; kt <= qt; ++kt) {
     const int k0 = kt * TT;
     __syncthreads();
-    stage_tile<DH, KLD, TLD, true, true>(Kb, ldk, k0, L, ks, kt_);
-    stage_tile<DH, KLD, TLD, true, false>(Vb, ldv, k0, L, vs, nullptr);
+    kr.template store<KLD>(ks);
+    vr.template store<KLD>(vs);
+    ktr.template store<TLD>(kt_);
     __syncthreads();
+    if (kt < qt) {
+      kr.load(Kb, ldk, k0 + TT, L);
+      vr.load(Vb, ldv, k0 + TT, L);
+      ktr.load(KTb, Lp, k0 + TT);
+    }
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       f32x4 sc = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -261,9 +312,11 @@ __global__ __launch_bounds__(256) void attn_train_dq_kernel(const uint16_t* __re
 // ---------------------------------------------------------------------------------------- dK, dV
 template <int DH>
 __global__ __launch_bounds__(256) void attn_train_dkdv_kernel(const uint16_t* __restrict__ Q, long ldq,
+                                                              const uint16_t* __restrict__ QT,
                                                               const uint16_t* __restrict__ K, long ldk,
                                                               const uint16_t* __restrict__ V, long ldv,
                                                               const uint16_t* __restrict__ dO, long lddo,
+                                                              const uint16_t* __restrict__ dOT, int Lp,
                                                               const float* __restrict__ lse2,
                                                               const float* __restrict__ delta,
                                                               uint16_t* __restrict__ dK, long lddk,
@@ -283,6 +336,23 @@ __global__ __launch_bounds__(256) void attn_train_dkdv_kernel(const uint16_t* __
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
   const int k0 = kt * TT, krow = k0 + 16 * wave;
   const float sl = scale * L2E;
+  const int nq = (L + TT - 1) / TT, per_head = nq - kt, iters = G * per_head;
+
+  RowsTile<DH> qr, dr;
+  TransTile<DH> qtr, dtr;
+  float lsv = 0.f, dlv = 0.f;
+  auto load = [&](int it) {  // (head, query tile) of iteration it into registers
+    const int h = kvh * G + it / per_head, q0 = (kt + it % per_head) * TT;
+    qr.load(Q + (long)b * L * ldq + h * DH, ldq, q0, L);
+    dr.load(dO + (long)b * L * lddo + h * DH, lddo, q0, L);
+    qtr.load(QT + ((long)b * H + h) * DH * Lp, Lp, q0);
+    dtr.load(dOT + ((long)b * H + h) * DH * Lp, Lp, q0);
+    if (threadIdx.x < TT) {
+      const long idx = ((long)b * H + h) * L + min(q0 + (int)threadIdx.x, L - 1);
+      lsv = lse2[idx];
+      dlv = delta[idx];
+    }
+  };
 
   s16x8 kf[KS], vf[KS];
   {
@@ -299,51 +369,48 @@ __global__ __launch_bounds__(256) void attn_train_dkdv_kernel(const uint16_t* __
 #pragma unroll
   for (int dt = 0; dt < NDT; ++dt) dk[dt] = dv[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
   uint16_t* pw = pt + wave * 2 * 16 * PLD;  // [0]: P^T, [1]: dS^T
-  const int nq = (L + TT - 1) / TT;
 
-  for (int hh = 0; hh < G; ++hh) {
-    const int h = kvh * G + hh;
-    const uint16_t* Qb = Q + (long)b * L * ldq + h * DH;
-    const uint16_t* Db = dO + (long)b * L * lddo + h * DH;
-    for (int qt = kt; qt < nq; ++qt) {
-      const int q0 = qt * TT;
-      __syncthreads();
-      stage_tile<DH, RLD, TLD, true, true>(Qb, ldq, q0, L, qs, qt_);
-      stage_tile<DH, RLD, TLD, true, true>(Db, lddo, q0, L, ds_, dt_);
-      if (threadIdx.x < TT) {
-        const int qi = min(q0 + (int)threadIdx.x, L - 1);
-        ld_[threadIdx.x] = lse2[((long)b * H + h) * L + qi];
-        ld_[TT + threadIdx.x] = delta[((long)b * H + h) * L + qi];
+  if (iters > 0) load(0);
+  for (int it = 0; it < iters; ++it) {
+    const int q0 = (kt + it % per_head) * TT;
+    __syncthreads();
+    qr.template store<RLD>(qs);
+    dr.template store<RLD>(ds_);
+    qtr.template store<TLD>(qt_);
+    dtr.template store<TLD>(dt_);
+    if (threadIdx.x < TT) {
+      ld_[threadIdx.x] = lsv;
+      ld_[TT + threadIdx.x] = dlv;
+    }
+    __syncthreads();
+    if (it + 1 < iters) load(it + 1);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {  // 16-query sub-tiles: query on the lane (column c)
+      f32x4 st = f32x4{0.f, 0.f, 0.f, 0.f}, dpt = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        st = mfma16(kf[s], ld16(qs + (16 * t + c) * RLD + 32 * s + 8 * g), st);
+        dpt = mfma16(vf[s], ld16(ds_ + (16 * t + c) * RLD + 32 * s + 8 * g), dpt);
       }
-      __syncthreads();
+      const int qi = q0 + 16 * t + c;
+      const float lq = ld_[16 * t + c], dq = ld_[TT + 16 * t + c];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {  // 16-query sub-tiles: query on the lane (column c)
-        f32x4 st = f32x4{0.f, 0.f, 0.f, 0.f}, dpt = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s = 0; s < KS; ++s) {
-          st = mfma16(kf[s], ld16(qs + (16 * t + c) * RLD + 32 * s + 8 * g), st);
-          dpt = mfma16(vf[s], ld16(ds_ + (16 * t + c) * RLD + 32 * s + 8 * g), dpt);
-        }
-        const int qi = q0 + 16 * t + c;
-        const float lq = ld_[16 * t + c], dq = ld_[TT + 16 * t + c];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int key = krow + 4 * g + r;
-          const float p = (key <= qi && qi < L) ? exp2f(st[r] * sl - lq) : 0.f;
-          pw[(4 * g + r) * PLD + 16 * t + c] = f2bf(p);
-          pw[16 * PLD + (4 * g + r) * PLD + 16 * t + c] = f2bf(p * (dpt[r] - dq));
-        }
+      for (int r = 0; r < 4; ++r) {
+        const int key = krow + 4 * g + r;
+        const float p = (key <= qi && qi < L) ? exp2f(st[r] * sl - lq) : 0.f;
+        pw[(4 * g + r) * PLD + 16 * t + c] = f2bf(p);
+        pw[16 * PLD + (4 * g + r) * PLD + 16 * t + c] = f2bf(p * (dpt[r] - dq));
       }
-      wave_sync_lds();
+    }
+    wave_sync_lds();
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const s16x8 pa = ld16(pw + c * PLD + 32 * kk + 8 * g);
-        const s16x8 sa = ld16(pw + 16 * PLD + c * PLD + 32 * kk + 8 * g);
+    for (int kk = 0; kk < 2; ++kk) {
+      const s16x8 pa = ld16(pw + c * PLD + 32 * kk + 8 * g);
+      const s16x8 sa = ld16(pw + 16 * PLD + c * PLD + 32 * kk + 8 * g);
 #pragma unroll
-        for (int dt = 0; dt < NDT; ++dt) {
-          dv[dt] = mfma16(pa, ld16(dt_ + (16 * dt + c) * TLD + 32 * kk + 8 * g), dv[dt]);
-          dk[dt] = mfma16(sa, ld16(qt_ + (16 * dt + c) * TLD + 32 * kk + 8 * g), dk[dt]);
-        }
+      for (int dt = 0; dt < NDT; ++dt) {
+        dv[dt] = mfma16(pa, ld16(dt_ + (16 * dt + c) * TLD + 32 * kk + 8 * g), dv[dt]);
+        dk[dt] = mfma16(sa, ld16(qt_ + (16 * dt + c) * TLD + 32 * kk + 8 * g), dk[dt]);
       }
     }
   }
@@ -361,54 +428,90 @@ __global__ __launch_bounds__(256) void attn_train_dkdv_kernel(const uint16_t* __
   }
 }
 
+// ---------------------------------------------------------------------------------------- transpose
+// X [B*L, ldx] token-major, n heads of DH -> XT [B, n, DH, Lp] (tokens contiguous, zero for t >= L).
+template <int DH>
+__global__ __launch_bounds__(256) void attn_train_transpose_kernel(const uint16_t* __restrict__ X, long ldx,
+                                                                   uint16_t* __restrict__ XT, int L, int Lp, int n) {
+  constexpr int TLD = TT + 8;
+  __shared__ __attribute__((aligned(16))) uint16_t tl[DH * TLD];
+  const int t0 = blockIdx.x * TT, hd = blockIdx.y, b = blockIdx.z;
+  for (int q = threadIdx.x; q < TT * (DH / 8); q += 256) {  // read 64 tokens x DH (16-B loads)
+    const int r = q / (DH / 8), cc = q % (DH / 8);
+    s16x8 v = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    if (t0 + r < L) v = ld16(X + ((long)b * L + t0 + r) * ldx + hd * DH + cc * 8);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) tl[(cc * 8 + e) * TLD + r] = (uint16_t)v[e];
+  }
+  __syncthreads();
+  uint16_t* out = XT + (((long)b * n + hd) * DH) * Lp + t0;
+  for (int q = threadIdx.x; q < DH * (TT / 8); q += 256) {  // write DH rows x 64 tokens (16-B stores)
+    const int d = q / (TT / 8), cc = q % (TT / 8);
+    st16(out + (long)d * Lp + cc * 8, ld16(tl + d * TLD + cc * 8));
+  }
+}
+
 template <int DH>
 static size_t dkdv_smem() {
   return (size_t)(2 * TT * (DH + 8) + 2 * DH * (TT + 8) + 4 * 2 * 16 * (TT + 8)) * 2 + 2 * TT * sizeof(float);
 }
 
-int launch_attn_train_fwd(const uint16_t* q, long ldq, const uint16_t* k, long ldk, const uint16_t* v, long ldv,
-                          uint16_t* o, long ldo, float* lse2, int B, int L, int H, int Hkv, int Dh, float scale,
-                          hipStream_t s) {
+int launch_attn_train_transpose(const uint16_t* x, long ldx, uint16_t* xt, int B, int L, int Lp, int n, int Dh,
+                                hipStream_t s) {
   if (B <= 0 || L <= 0) return 0;
-  if (H % Hkv != 0) return -1;
-  dim3 grid((L + TT - 1) / TT, H, B);
+  if (Lp % TT != 0 || Lp < L) return -1;
+  dim3 grid(Lp / TT, n, B);
   if (Dh == 128)
-    attn_train_fwd_kernel<128><<<grid, 256, 0, s>>>(q, ldq, k, ldk, v, ldv, o, ldo, lse2, L, H, Hkv, scale);
+    attn_train_transpose_kernel<128><<<grid, 256, 0, s>>>(x, ldx, xt, L, Lp, n);
   else if (Dh == 64)
-    attn_train_fwd_kernel<64><<<grid, 256, 0, s>>>(q, ldq, k, ldk, v, ldv, o, ldo, lse2, L, H, Hkv, scale);
+    attn_train_transpose_kernel<64><<<grid, 256, 0, s>>>(x, ldx, xt, L, Lp, n);
   else
     return -1;
   return 0;
 }
 
-int launch_attn_train_bwd(const uint16_t* q, long ldq, const uint16_t* k, long ldk, const uint16_t* v, long ldv,
-                          const uint16_t* o, long ldo, const uint16_t* dout, long lddo, const float* lse2,
+int launch_attn_train_fwd(const uint16_t* q, long ldq, const uint16_t* k, long ldk, const uint16_t* vt, int Lp,
+                          uint16_t* o, long ldo, float* lse2, int B, int L, int H, int Hkv, int Dh, float scale,
+                          hipStream_t s) {
+  if (B <= 0 || L <= 0) return 0;
+  if (H % Hkv != 0 || Lp % TT != 0 || Lp < L) return -1;
+  dim3 grid((L + TT - 1) / TT, H, B);
+  if (Dh == 128)
+    attn_train_fwd_kernel<128><<<grid, 256, 0, s>>>(q, ldq, k, ldk, vt, Lp, o, ldo, lse2, L, H, Hkv, scale);
+  else if (Dh == 64)
+    attn_train_fwd_kernel<64><<<grid, 256, 0, s>>>(q, ldq, k, ldk, vt, Lp, o, ldo, lse2, L, H, Hkv, scale);
+  else
+    return -1;
+  return 0;
+}
+
+int launch_attn_train_bwd(const uint16_t* q, long ldq, const uint16_t* qt, const uint16_t* k, long ldk,
+                          const uint16_t* kt, const uint16_t* v, long ldv, const uint16_t* o, long ldo,
+                          const uint16_t* dout, long lddo, const uint16_t* doutt, int Lp, const float* lse2,
                           float* delta, uint16_t* dq, long lddq, uint16_t* dk, long lddk, uint16_t* dv, long lddv,
                           int B, int L, int H, int Hkv, int Dh, float scale, hipStream_t s) {
   if (B <= 0 || L <= 0) return 0;
-  if (H % Hkv != 0) return -1;
+  if (H % Hkv != 0 || Lp % TT != 0 || Lp < L) return -1;
   dim3 gq((L + TT - 1) / TT, H, B), gk((L + TT - 1) / TT, Hkv, B);
-  if (Dh == 128) {
-    attn_train_dq_kernel<128><<<gq, 256, 0, s>>>(q, ldq, k, ldk, v, ldv, o, ldo, dout, lddo, lse2, delta, dq, lddq,
-                                                  L, H, Hkv, scale);
-    static bool attr = hipFuncSetAttribute((const void*)attn_train_dkdv_kernel<128>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)dkdv_smem<128>()) ==
-                       hipSuccess;
-    (void)attr;
-    attn_train_dkdv_kernel<128><<<gk, 256, dkdv_smem<128>(), s>>>(q, ldq, k, ldk, v, ldv, dout, lddo, lse2, delta, dk,
-                                                                  lddk, dv, lddv, L, H, Hkv, scale);
-  } else if (Dh == 64) {
-    attn_train_dq_kernel<64><<<gq, 256, 0, s>>>(q, ldq, k, ldk, v, ldv, o, ldo, dout, lddo, lse2, delta, dq, lddq,
-                                                 L, H, Hkv, scale);
-    static bool attr = hipFuncSetAttribute((const void*)attn_train_dkdv_kernel<64>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)dkdv_smem<64>()) ==
-                       hipSuccess;
-    (void)attr;
-    attn_train_dkdv_kernel<64><<<gk, 256, dkdv_smem<64>(), s>>>(q, ldq, k, ldk, v, ldv, dout, lddo, lse2, delta, dk,
-                                                                lddk, dv, lddv, L, H, Hkv, scale);
-  } else {
+#define XOT_BWD(DHV)                                                                                                \
+  do {                                                                                                              \
+    attn_train_dq_kernel<DHV><<<gq, 256, 0, s>>>(q, ldq, k, ldk, kt, v, ldv, o, ldo, dout, lddo, Lp, lse2, delta,   \
+                                                 dq, lddq, L, H, Hkv, scale);                                       \
+    static bool attr = hipFuncSetAttribute((const void*)attn_train_dkdv_kernel<DHV>,                               \
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)dkdv_smem<DHV>()) ==    \
+                       hipSuccess;                                                                                  \
+    (void)attr;                                                                                                     \
+    attn_train_dkdv_kernel<DHV><<<gk, 256, dkdv_smem<DHV>(), s>>>(q, ldq, qt, k, ldk, v, ldv, dout, lddo, doutt, Lp, \
+                                                                  lse2, delta, dk, lddk, dv, lddv, L, H, Hkv,       \
+                                                                  scale);                                           \
+  } while (0)
+  if (Dh == 128)
+    XOT_BWD(128);
+  else if (Dh == 64)
+    XOT_BWD(64);
+  else
     return -1;
-  }
+#undef XOT_BWD
   return 0;
 }
 

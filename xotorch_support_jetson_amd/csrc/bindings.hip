@@ -426,29 +426,48 @@ static void check_rows(const at::Tensor& t, int64_t rows, int64_t cols, const ch
          "attn_train: bad ", what, " view");
 }
 
-void attn_train_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, at::Tensor& o, at::Tensor& lse2,
-                    int64_t B, int64_t L, int64_t H, int64_t Hkv, int64_t Dh, double scale) {
+static void check_trans(const at::Tensor& t, int64_t B, int64_t n, int64_t Dh, int64_t Lp, const char* what) {
+  CHECK_BF16(t);
+  XCHECK(t.is_contiguous() && t.numel() == B * n * Dh * Lp, "attn_train: bad transposed ", what, " [B, n, Dh, Lp]");
+}
+
+// [B*L, n*Dh] token-major view -> [B, n, Dh, Lp] (tokens contiguous, zero past L)
+void attn_train_transpose(const at::Tensor& x, at::Tensor& xt, int64_t B, int64_t L, int64_t Lp, int64_t n,
+                          int64_t Dh) {
+  check_rows(x, B * L, n * Dh, "x");
+  check_trans(xt, B, n, Dh, Lp, "xt");
+  const int rc = xot::launch_attn_train_transpose(bf(x), x.stride(0), bf(xt), (int)B, (int)L, (int)Lp, (int)n,
+                                                  (int)Dh, cur_stream());
+  XCHECK(rc == 0, "attn_train_transpose: unsupported Dh=", Dh, " Lp=", Lp);
+}
+
+void attn_train_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& vt, at::Tensor& o, at::Tensor& lse2,
+                    int64_t B, int64_t L, int64_t Lp, int64_t H, int64_t Hkv, int64_t Dh, double scale) {
   check_rows(q, B * L, H * Dh, "q");
   check_rows(k, B * L, Hkv * Dh, "k");
-  check_rows(v, B * L, Hkv * Dh, "v");
+  check_trans(vt, B, Hkv, Dh, Lp, "vt");
   check_rows(o, B * L, H * Dh, "o");
   CHECK_GPU(lse2);
   CHECK_DT(lse2, at::kFloat);
   XCHECK(lse2.is_contiguous() && lse2.numel() == B * H * L, "attn_train_fwd: lse2 [B, H, L]");
-  const int rc = xot::launch_attn_train_fwd(bf(q), q.stride(0), bf(k), k.stride(0), bf(v), v.stride(0), bf(o),
+  const int rc = xot::launch_attn_train_fwd(bf(q), q.stride(0), bf(k), k.stride(0), bf(vt), (int)Lp, bf(o),
                                             o.stride(0), lse2.data_ptr<float>(), (int)B, (int)L, (int)H, (int)Hkv,
                                             (int)Dh, (float)scale, cur_stream());
   XCHECK(rc == 0, "attn_train_fwd: unsupported H=", H, " Hkv=", Hkv, " Dh=", Dh);
 }
 
-void attn_train_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, const at::Tensor& o,
-                    const at::Tensor& dout, const at::Tensor& lse2, at::Tensor& delta, at::Tensor& dq, at::Tensor& dk,
-                    at::Tensor& dv, int64_t B, int64_t L, int64_t H, int64_t Hkv, int64_t Dh, double scale) {
+void attn_train_bwd(const at::Tensor& q, const at::Tensor& qt, const at::Tensor& k, const at::Tensor& kt,
+                    const at::Tensor& v, const at::Tensor& o, const at::Tensor& dout, const at::Tensor& doutt,
+                    const at::Tensor& lse2, at::Tensor& delta, at::Tensor& dq, at::Tensor& dk, at::Tensor& dv,
+                    int64_t B, int64_t L, int64_t Lp, int64_t H, int64_t Hkv, int64_t Dh, double scale) {
   check_rows(q, B * L, H * Dh, "q");
+  check_trans(qt, B, H, Dh, Lp, "qt");
   check_rows(k, B * L, Hkv * Dh, "k");
+  check_trans(kt, B, Hkv, Dh, Lp, "kt");
   check_rows(v, B * L, Hkv * Dh, "v");
   check_rows(o, B * L, H * Dh, "o");
   check_rows(dout, B * L, H * Dh, "dout");
+  check_trans(doutt, B, H, Dh, Lp, "doutt");
   check_rows(dq, B * L, H * Dh, "dq");
   check_rows(dk, B * L, Hkv * Dh, "dk");
   check_rows(dv, B * L, Hkv * Dh, "dv");
@@ -456,11 +475,11 @@ void attn_train_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& 
   CHECK_DT(delta, at::kFloat);
   XCHECK(lse2.is_contiguous() && delta.is_contiguous() && lse2.numel() == B * H * L && delta.numel() == B * H * L,
          "attn_train_bwd: lse2 / delta [B, H, L]");
-  const int rc = xot::launch_attn_train_bwd(bf(q), q.stride(0), bf(k), k.stride(0), bf(v), v.stride(0), bf(o),
-                                            o.stride(0), bf(dout), dout.stride(0), lse2.data_ptr<float>(),
-                                            delta.data_ptr<float>(), bf(dq), dq.stride(0), bf(dk), dk.stride(0),
-                                            bf(dv), dv.stride(0), (int)B, (int)L, (int)H, (int)Hkv, (int)Dh,
-                                            (float)scale, cur_stream());
+  const int rc = xot::launch_attn_train_bwd(
+      bf(q), q.stride(0), bf(qt), bf(k), k.stride(0), bf(kt), bf(v), v.stride(0), bf(o), o.stride(0), bf(dout),
+      dout.stride(0), bf(doutt), (int)Lp, lse2.data_ptr<float>(), delta.data_ptr<float>(), bf(dq), dq.stride(0),
+      bf(dk), dk.stride(0), bf(dv), dv.stride(0), (int)B, (int)L, (int)H, (int)Hkv, (int)Dh, (float)scale,
+      cur_stream());
   XCHECK(rc == 0, "attn_train_bwd: unsupported H=", H, " Hkv=", Hkv, " Dh=", Dh);
 }
 
@@ -582,6 +601,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("ctx_lens"), py::arg("out"), py::arg("ws_o"), py::arg("ws_ml"), py::arg("pages_per_part"),
         py::arg("nparts"), py::arg("scale"), py::arg("algo") = 2);
   m.def("attn_prefill", &attn_prefill);
+  m.def("attn_train_transpose", &attn_train_transpose);
   m.def("attn_train_fwd", &attn_train_fwd);
   m.def("attn_train_bwd", &attn_train_bwd);
   m.def("sample", &sample);

@@ -60,12 +60,16 @@ int launch_attn_prefill(const uint16_t* q, const uint16_t* kc, const uint16_t* v
                         int max_blocks, const int32_t* cu_q, const int32_t* ctx_lens, uint16_t* out, int B,
                         int max_qlen, int H, int Hkv, int Dh, float scale, int num_pages, hipStream_t s);
 
-// causal self-attention for training (token-major Q / K / V slices, GQA); lse2 [B, H, L] fp32 (log2 domain)
-int launch_attn_train_fwd(const uint16_t* q, long ldq, const uint16_t* k, long ldk, const uint16_t* v, long ldv,
+// causal self-attention for training (token-major Q / K / V slices, GQA); lse2 [B, H, L] fp32 (log2 domain);
+// *t arguments are [B, heads, Dh, Lp] transposed images from launch_attn_train_transpose (zero past L)
+int launch_attn_train_transpose(const uint16_t* x, long ldx, uint16_t* xt, int B, int L, int Lp, int n, int Dh,
+                                hipStream_t s);
+int launch_attn_train_fwd(const uint16_t* q, long ldq, const uint16_t* k, long ldk, const uint16_t* vt, int Lp,
                           uint16_t* o, long ldo, float* lse2, int B, int L, int H, int Hkv, int Dh, float scale,
                           hipStream_t s);
-int launch_attn_train_bwd(const uint16_t* q, long ldq, const uint16_t* k, long ldk, const uint16_t* v, long ldv,
-                          const uint16_t* o, long ldo, const uint16_t* dout, long lddo, const float* lse2,
+int launch_attn_train_bwd(const uint16_t* q, long ldq, const uint16_t* qt, const uint16_t* k, long ldk,
+                          const uint16_t* kt, const uint16_t* v, long ldv, const uint16_t* o, long ldo,
+                          const uint16_t* dout, long lddo, const uint16_t* doutt, int Lp, const float* lse2,
                           float* delta, uint16_t* dq, long lddq, uint16_t* dk, long lddk, uint16_t* dv, long lddv,
                           int B, int L, int H, int Hkv, int Dh, float scale, hipStream_t s);
 

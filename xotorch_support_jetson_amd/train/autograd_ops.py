@@ -134,11 +134,14 @@ class AttentionFn(torch.autograd.Function):
   @staticmethod
   def forward(ctx, q, k, v, B, L, H, Hkv, Dh):
     scale = Dh ** -0.5
-    ctx.dims = (B, L, H, Hkv, Dh, scale)
+    Lp = -(-L // 64) * 64
+    ctx.dims = (B, L, Lp, H, Hkv, Dh, scale)
     if _gpu(q):
+      C = require()
       o = torch.empty(B * L, H * Dh, dtype=q.dtype, device=q.device)
       lse2 = torch.empty(B * H * L, dtype=torch.float32, device=q.device)
-      require().attn_train_fwd(q, k, v, o, lse2, B, L, H, Hkv, Dh, scale)
+      vt = _transposed(C, v, B, L, Lp, Hkv, Dh)
+      C.attn_train_fwd(q, k, vt, o, lse2, B, L, Lp, H, Hkv, Dh, scale)
       ctx.save_for_backward(q, k, v, o, lse2)
       return o
     ctx.save_for_backward(q, k, v)
@@ -146,15 +149,19 @@ class AttentionFn(torch.autograd.Function):
 
   @staticmethod
   def backward(ctx, do):
-    B, L, H, Hkv, Dh, scale = ctx.dims
+    B, L, Lp, H, Hkv, Dh, scale = ctx.dims
     if _gpu(do):
+      C = require()
       q, k, v, o, lse2 = ctx.saved_tensors
+      do = do.contiguous().to(q.dtype)
+      qt = _transposed(C, q, B, L, Lp, H, Dh)
+      kt = _transposed(C, k, B, L, Lp, Hkv, Dh)
+      dot = _transposed(C, do, B, L, Lp, H, Dh)
       dq = torch.empty(B * L, H * Dh, dtype=q.dtype, device=q.device)
       dk = torch.empty(B * L, Hkv * Dh, dtype=q.dtype, device=q.device)
       dv = torch.empty_like(dk)
       delta = torch.empty_like(lse2)
-      require().attn_train_bwd(q, k, v, o, do.contiguous().to(q.dtype), lse2, delta, dq, dk, dv, B, L, H, Hkv, Dh,
-                               scale)
+      C.attn_train_bwd(q, qt, k, kt, v, o, do, dot, lse2, delta, dq, dk, dv, B, L, Lp, H, Hkv, Dh, scale)
       return dq, dk, dv, None, None, None, None, None
     q, k, v = ctx.saved_tensors
     with torch.enable_grad():
@@ -162,6 +169,13 @@ class AttentionFn(torch.autograd.Function):
       y = _attn_ref(qr, kr, vr, B, L, H, Hkv, Dh)
       y.backward(do.float())
     return qr.grad.to(q.dtype), kr.grad.to(k.dtype), vr.grad.to(v.dtype), None, None, None, None, None
+
+
+def _transposed(C, x, B, L, Lp, n, Dh):
+  """[B*L, n*Dh] token-major -> [B, n, Dh, Lp] (the operand MFMA reads by column), zero past L."""
+  xt = torch.empty(B, n, Dh, Lp, dtype=x.dtype, device=x.device)
+  C.attn_train_transpose(x, xt, B, L, Lp, n, Dh)
+  return xt
 
 
 def _attn_ref(q, k, v, B, L, H, Hkv, Dh):
