@@ -319,9 +319,8 @@ __global__ __launch_bounds__(256) void attn_train_dkdv_kernel(const uint16_t* __
                                                               const uint16_t* __restrict__ dOT, int Lp,
                                                               const float* __restrict__ lse2,
                                                               const float* __restrict__ delta,
-                                                              uint16_t* __restrict__ dK, long lddk,
-                                                              uint16_t* __restrict__ dV, long lddv, int L, int H,
-                                                              int Hkv, float scale) {
+                                                              float* __restrict__ wk, float* __restrict__ wv, int L,
+                                                              int H, int Hkv, float scale) {
   constexpr int KS = DH / 32, NDT = DH / 16;
   constexpr int RLD = DH + 8, TLD = TT + 8, PLD = TT + 8;
   extern __shared__ __attribute__((aligned(16))) uint16_t sm[];
@@ -331,18 +330,20 @@ __global__ __launch_bounds__(256) void attn_train_dkdv_kernel(const uint16_t* __
   uint16_t* dt_ = qt_ + DH * TLD;    // dO^T         [DH][TLD]
   uint16_t* pt = dt_ + DH * TLD;     // P^T / dS^T   [4 waves][2][16][PLD]
   float* ld_ = reinterpret_cast<float*>(pt + 4 * 2 * 16 * PLD);  // lse2[64], delta[64]
-  const int kt = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
+  // one workgroup per (query head of the group, key tile, batch); key tiles are the slowest grid
+  // dimension with the heaviest (kt = 0: every query tile) first, so the causal imbalance load-balances
   const int G = H / Hkv;
+  const int hq = blockIdx.x, kvh = hq / G, hh = hq % G, kt = blockIdx.y, b = blockIdx.z;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
   const int k0 = kt * TT, krow = k0 + 16 * wave;
   const float sl = scale * L2E;
-  const int nq = (L + TT - 1) / TT, per_head = nq - kt, iters = G * per_head;
+  const int nq = (L + TT - 1) / TT, per_head = nq - kt, iters = per_head;
 
   RowsTile<DH> qr, dr;
   TransTile<DH> qtr, dtr;
   float lsv = 0.f, dlv = 0.f;
   auto load = [&](int it) {  // (head, query tile) of iteration it into registers
-    const int h = kvh * G + it / per_head, q0 = (kt + it % per_head) * TT;
+    const int h = hq, q0 = (kt + it) * TT;
     qr.load(Q + (long)b * L * ldq + h * DH, ldq, q0, L);
     dr.load(dO + (long)b * L * lddo + h * DH, lddo, q0, L);
     qtr.load(QT + ((long)b * H + h) * DH * Lp, Lp, q0);
@@ -372,7 +373,7 @@ __global__ __launch_bounds__(256) void attn_train_dkdv_kernel(const uint16_t* __
 
   if (iters > 0) load(0);
   for (int it = 0; it < iters; ++it) {
-    const int q0 = (kt + it % per_head) * TT;
+    const int q0 = (kt + it) * TT;
     __syncthreads();
     qr.template store<RLD>(qs);
     dr.template store<RLD>(ds_);
@@ -414,17 +415,42 @@ __global__ __launch_bounds__(256) void attn_train_dkdv_kernel(const uint16_t* __
       }
     }
   }
+  // fp32 partials of this query head: slab hh of [G][B*L, Hkv*DH] (summed + scaled by the reduce kernel)
+  const long slab = (long)hh * ((long)gridDim.z * L) * (Hkv * DH);
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int key = krow + 4 * g + r;
     if (key >= L) continue;
-    uint16_t* kp = dK + ((long)b * L + key) * lddk + kvh * DH + c;
-    uint16_t* vp = dV + ((long)b * L + key) * lddv + kvh * DH + c;
+    const long off = slab + ((long)b * L + key) * (Hkv * DH) + kvh * DH + c;
 #pragma unroll
     for (int dt = 0; dt < NDT; ++dt) {
-      kp[16 * dt] = f2bf(dk[dt][r] * scale);
-      vp[16 * dt] = f2bf(dv[dt][r]);
+      wk[off + 16 * dt] = dk[dt][r];
+      wv[off + 16 * dt] = dv[dt][r];
     }
+  }
+}
+
+// dK = scale * sum_h wk[h], dV = sum_h wv[h]  ([G][rows][cols] fp32 -> bf16 row views)
+__global__ __launch_bounds__(256) void attn_train_dkdv_reduce_kernel(const float* __restrict__ wk,
+                                                                     const float* __restrict__ wv, int G, long rows,
+                                                                     int cols, float scale, uint16_t* __restrict__ dK,
+                                                                     long lddk, uint16_t* __restrict__ dV, long lddv) {
+  const long n4 = rows * cols / 4, slab = rows * cols;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f}, v = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int h = 0; h < G; ++h) {
+      a += *reinterpret_cast<const f32x4*>(wk + h * slab + 4 * i);
+      v += *reinterpret_cast<const f32x4*>(wv + h * slab + 4 * i);
+    }
+    const long row = 4 * i / cols, col = 4 * i % cols;
+    s16x4 ka, va;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      ka[e] = (short)f2bf(a[e] * scale);
+      va[e] = (short)f2bf(v[e]);
+    }
+    *reinterpret_cast<s16x4*>(dK + row * lddk + col) = ka;
+    *reinterpret_cast<s16x4*>(dV + row * lddv + col) = va;
   }
 }
 
@@ -489,10 +515,13 @@ int launch_attn_train_bwd(const uint16_t* q, long ldq, const uint16_t* qt, const
                           const uint16_t* kt, const uint16_t* v, long ldv, const uint16_t* o, long ldo,
                           const uint16_t* dout, long lddo, const uint16_t* doutt, int Lp, const float* lse2,
                           float* delta, uint16_t* dq, long lddq, uint16_t* dk, long lddk, uint16_t* dv, long lddv,
-                          int B, int L, int H, int Hkv, int Dh, float scale, hipStream_t s) {
+                          float* ws, long ws_elems, int B, int L, int H, int Hkv, int Dh, float scale, hipStream_t s) {
   if (B <= 0 || L <= 0) return 0;
   if (H % Hkv != 0 || Lp % TT != 0 || Lp < L) return -1;
-  dim3 gq((L + TT - 1) / TT, H, B), gk((L + TT - 1) / TT, Hkv, B);
+  const long slab = (long)B * L * Hkv * Dh;
+  if (ws == nullptr || ws_elems < 2 * (long)(H / Hkv) * slab) return -1;
+  float *wk = ws, *wv = ws + (long)(H / Hkv) * slab;
+  dim3 gq((L + TT - 1) / TT, H, B), gk(H, (L + TT - 1) / TT, B);
 #define XOT_BWD(DHV)                                                                                                \
   do {                                                                                                              \
     attn_train_dq_kernel<DHV><<<gq, 256, 0, s>>>(q, ldq, k, ldk, kt, v, ldv, o, ldo, dout, lddo, Lp, lse2, delta,   \
@@ -502,8 +531,7 @@ int launch_attn_train_bwd(const uint16_t* q, long ldq, const uint16_t* qt, const
                        hipSuccess;                                                                                  \
     (void)attr;                                                                                                     \
     attn_train_dkdv_kernel<DHV><<<gk, 256, dkdv_smem<DHV>(), s>>>(q, ldq, qt, k, ldk, v, ldv, dout, lddo, doutt, Lp, \
-                                                                  lse2, delta, dk, lddk, dv, lddv, L, H, Hkv,       \
-                                                                  scale);                                           \
+                                                                  lse2, delta, wk, wv, L, H, Hkv, scale);           \
   } while (0)
   if (Dh == 128)
     XOT_BWD(128);
@@ -512,6 +540,11 @@ int launch_attn_train_bwd(const uint16_t* q, long ldq, const uint16_t* qt, const
   else
     return -1;
 #undef XOT_BWD
+  const long n4 = slab / 4;
+  int blocks = (int)((n4 + 255) / 256);
+  if (blocks > 4096) blocks = 4096;
+  attn_train_dkdv_reduce_kernel<<<blocks, 256, 0, s>>>(wk, wv, H / Hkv, (long)B * L, Hkv * Dh, scale, dk, lddk, dv,
+                                                       lddv);
   return 0;
 }
 

@@ -459,7 +459,8 @@ void attn_train_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& 
 void attn_train_bwd(const at::Tensor& q, const at::Tensor& qt, const at::Tensor& k, const at::Tensor& kt,
                     const at::Tensor& v, const at::Tensor& o, const at::Tensor& dout, const at::Tensor& doutt,
                     const at::Tensor& lse2, at::Tensor& delta, at::Tensor& dq, at::Tensor& dk, at::Tensor& dv,
-                    int64_t B, int64_t L, int64_t Lp, int64_t H, int64_t Hkv, int64_t Dh, double scale) {
+                    at::Tensor& ws, int64_t B, int64_t L, int64_t Lp, int64_t H, int64_t Hkv, int64_t Dh,
+                    double scale) {
   check_rows(q, B * L, H * Dh, "q");
   check_trans(qt, B, H, Dh, Lp, "qt");
   check_rows(k, B * L, Hkv * Dh, "k");
@@ -475,11 +476,14 @@ void attn_train_bwd(const at::Tensor& q, const at::Tensor& qt, const at::Tensor&
   CHECK_DT(delta, at::kFloat);
   XCHECK(lse2.is_contiguous() && delta.is_contiguous() && lse2.numel() == B * H * L && delta.numel() == B * H * L,
          "attn_train_bwd: lse2 / delta [B, H, L]");
+  CHECK_GPU(ws);
+  CHECK_DT(ws, at::kFloat);
+  XCHECK(ws.is_contiguous() && ws.numel() >= 2 * H * B * L * Dh, "attn_train_bwd: ws needs 2 * H * B * L * Dh floats");
   const int rc = xot::launch_attn_train_bwd(
       bf(q), q.stride(0), bf(qt), bf(k), k.stride(0), bf(kt), bf(v), v.stride(0), bf(o), o.stride(0), bf(dout),
       dout.stride(0), bf(doutt), (int)Lp, lse2.data_ptr<float>(), delta.data_ptr<float>(), bf(dq), dq.stride(0),
-      bf(dk), dk.stride(0), bf(dv), dv.stride(0), (int)B, (int)L, (int)H, (int)Hkv, (int)Dh, (float)scale,
-      cur_stream());
+      bf(dk), dk.stride(0), bf(dv), dv.stride(0), ws.data_ptr<float>(), (long)ws.numel(), (int)B, (int)L, (int)H,
+      (int)Hkv, (int)Dh, (float)scale, cur_stream());
   XCHECK(rc == 0, "attn_train_bwd: unsupported H=", H, " Hkv=", Hkv, " Dh=", Dh);
 }
 

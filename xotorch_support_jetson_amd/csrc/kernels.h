@@ -71,7 +71,7 @@ int launch_attn_train_bwd(const uint16_t* q, long ldq, const uint16_t* qt, const
                           const uint16_t* kt, const uint16_t* v, long ldv, const uint16_t* o, long ldo,
                           const uint16_t* dout, long lddo, const uint16_t* doutt, int Lp, const float* lse2,
                           float* delta, uint16_t* dq, long lddq, uint16_t* dk, long lddk, uint16_t* dv, long lddv,
-                          int B, int L, int H, int Hkv, int Dh, float scale, hipStream_t s);
+                          float* ws, long ws_elems, int B, int L, int H, int Hkv, int Dh, float scale, hipStream_t s);
 
 void launch_sample(const float* logits, long ld, int B, int V, const float* temps, int top_k,
                    const int64_t* seed_off, int32_t* out, uint32_t* cand_key, int32_t* cand_idx, hipStream_t s);

@@ -161,7 +161,8 @@ class AttentionFn(torch.autograd.Function):
       dk = torch.empty(B * L, Hkv * Dh, dtype=q.dtype, device=q.device)
       dv = torch.empty_like(dk)
       delta = torch.empty_like(lse2)
-      C.attn_train_bwd(q, qt, k, kt, v, o, do, dot, lse2, delta, dq, dk, dv, B, L, Lp, H, Hkv, Dh, scale)
+      ws = torch.empty(2 * H * B * L * Dh, dtype=torch.float32, device=q.device)  # per-query-head dK/dV partials
+      C.attn_train_bwd(q, qt, k, kt, v, o, do, dot, lse2, delta, dq, dk, dv, ws, B, L, Lp, H, Hkv, Dh, scale)
       return dq, dk, dv, None, None, None, None, None
     q, k, v = ctx.saved_tensors
     with torch.enable_grad():
