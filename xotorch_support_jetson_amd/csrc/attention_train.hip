@@ -96,7 +96,8 @@ __global__ __launch_bounds__(256) void attn_train_fwd_kernel(const uint16_t* __r
   __shared__ __attribute__((aligned(16))) uint16_t ks[TT * KLD];
   __shared__ __attribute__((aligned(16))) uint16_t vt[DH * VLD];
   __shared__ __attribute__((aligned(16))) uint16_t pl[4][16 * PLD];
-  const int qt = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  // query tiles are the slowest grid dimension, heaviest (most key tiles under the causal mask) first
+  const int h = blockIdx.x, qt = gridDim.y - 1 - blockIdx.y, b = blockIdx.z;
   const int kvh = h / (H / Hkv);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
   const int q0 = qt * TT, qrow = q0 + 16 * wave;
@@ -214,7 +215,8 @@ __global__ __launch_bounds__(256) void attn_train_dq_kernel(const uint16_t* __re
   __shared__ __attribute__((aligned(16))) uint16_t kt_[DH * TLD];  // K^T (dQ += dS.K)
   __shared__ __attribute__((aligned(16))) uint16_t pl[4][16 * PLD];
   __shared__ float dl[4][16];
-  const int qt = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  // query tiles are the slowest grid dimension, heaviest (most key tiles under the causal mask) first
+  const int h = blockIdx.x, qt = gridDim.y - 1 - blockIdx.y, b = blockIdx.z;
   const int kvh = h / (H / Hkv);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
   const int q0 = qt * TT, qrow = q0 + 16 * wave;
@@ -501,7 +503,7 @@ int launch_attn_train_fwd(const uint16_t* q, long ldq, const uint16_t* k, long l
                           hipStream_t s) {
   if (B <= 0 || L <= 0) return 0;
   if (H % Hkv != 0 || Lp % TT != 0 || Lp < L) return -1;
-  dim3 grid((L + TT - 1) / TT, H, B);
+  dim3 grid(H, (L + TT - 1) / TT, B);
   if (Dh == 128)
     attn_train_fwd_kernel<128><<<grid, 256, 0, s>>>(q, ldq, k, ldk, vt, Lp, o, ldo, lse2, L, H, Hkv, scale);
   else if (Dh == 64)
@@ -521,7 +523,7 @@ int launch_attn_train_bwd(const uint16_t* q, long ldq, const uint16_t* qt, const
   const long slab = (long)B * L * Hkv * Dh;
   if (ws == nullptr || ws_elems < 2 * (long)(H / Hkv) * slab) return -1;
   float *wk = ws, *wv = ws + (long)(H / Hkv) * slab;
-  dim3 gq((L + TT - 1) / TT, H, B), gk(H, (L + TT - 1) / TT, B);
+  dim3 gq(H, (L + TT - 1) / TT, B), gk(H, (L + TT - 1) / TT, B);
 #define XOT_BWD(DHV)                                                                                                \
   do {                                                                                                              \
     attn_train_dq_kernel<DHV><<<gq, 256, 0, s>>>(q, ldq, k, ldk, kt, v, ldv, o, ldo, dout, lddo, Lp, lse2, delta,   \
