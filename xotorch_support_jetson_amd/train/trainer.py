@@ -30,6 +30,11 @@ from ..ops.rope import build_cos_sin
 from . import autograd_ops as A
 
 
+def _resid_mm(h: torch.Tensor, x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+  """h + x @ w.T; on the GPU the residual add rides in the hipBLASLt epilogue (addmm, beta = 1)."""
+  return torch.addmm(h, x, w.t()) if h.is_cuda else h + x @ w.t()
+
+
 class ShardTrainer:
   def __init__(self, weights: ShardWeights, device, lr: float = 1e-5, betas=(0.9, 0.95), eps: float = 1e-8,
                weight_decay: float = 0.0, max_seq: int = 4096, grad_clip: float = 1.0):
@@ -91,9 +96,9 @@ class ShardTrainer:
       k = A.rope(qkv[:, H * Dh:(H + Hkv) * Dh].contiguous(), pos, self.cos_sin, Hkv, Dh)
       v = qkv[:, (H + Hkv) * Dh:]
       a = A.attention(q, k, v, B, L, H, Hkv, Dh)  # flash-style HIP kernels (fwd + dQ + dK/dV)
-      h = h + a @ P[f"{i}.o"].t()
+      h = _resid_mm(h, a, P[f"{i}.o"])
       xn = A.rmsnorm(h, P[f"{i}.ln2"], c.rms_norm_eps)
-      h = h + A.silu_mul((xn @ P[f"{i}.gu"].t()).contiguous()) @ P[f"{i}.down"].t()
+      h = _resid_mm(h, A.silu_mul((xn @ P[f"{i}.gu"].t()).contiguous()), P[f"{i}.down"])
     if not self.shard.is_last_layer():
       return h.view(B, L, D)
     xn = A.rmsnorm(h, P["norm"], c.rms_norm_eps)
