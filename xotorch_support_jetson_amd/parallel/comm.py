@@ -26,7 +26,9 @@ def env_rank() -> tuple[int, int, int]:
 
 
 def init_distributed(backend: Optional[str] = None, timeout_s: int = 1800) -> tuple[int, int, torch.device]:
-  """Init the default process group from torchrun-style env vars.  Returns (rank, world, device)."""
+  """Init the default process group from torchrun-style env vars.  Returns (rank, world, device).
+  XOT_DIST_BACKEND=gloo forces gloo on GPU hosts too (single-GPU rehearsals of the multi-rank ring;
+  P2PTransport then stages device tensors through host memory)."""
   rank, local, world = env_rank()
   if torch.cuda.is_available():
     local = local % torch.cuda.device_count()  # more ranks than GPUs only in single-GPU rehearsals
@@ -36,7 +38,7 @@ def init_distributed(backend: Optional[str] = None, timeout_s: int = 1800) -> tu
     device = torch.device("cpu")
   if world > 1 and not dist.is_initialized():
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    be = backend or ("nccl" if device.type == "cuda" else "gloo")
+    be = backend or os.environ.get("XOT_DIST_BACKEND") or ("nccl" if device.type == "cuda" else "gloo")
     kw = dict(backend=be, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
     if be == "nccl":
       kw["device_id"] = device
@@ -44,25 +46,71 @@ def init_distributed(backend: Optional[str] = None, timeout_s: int = 1800) -> tu
   return rank, world, device
 
 
+def ring_edges(world: int) -> list:
+  """Directed neighbour edges of the ring, both directions (activations forward, grads / ids back)."""
+  edges = []
+  for i in range(world):
+    for e in ((i, (i + 1) % world), ((i + 1) % world, i)):
+      if e[0] != e[1] and e not in edges:
+        edges.append(e)
+  return edges
+
+
+class _StagedRecv:
+  """irecv into a host bounce buffer (gloo cannot address device memory); wait() copies it in."""
+
+  def __init__(self, work, host: torch.Tensor, dst: torch.Tensor):
+    self.work, self.host, self.dst = work, host, dst
+
+  def wait(self):
+    self.work.wait()
+    self.dst.copy_(self.host)
+    return True
+
+  def is_completed(self):
+    return self.work.is_completed()
+
+
 class P2PTransport:
-  """Ordered tensor hand-off to/from ring neighbours over the default process group."""
+  """Ordered tensor hand-off to/from ring neighbours.
+
+  Every directed edge (src -> dst) gets its own 2-rank process group, i.e. its own RCCL communicator
+  and stream.  With one shared communicator per rank pair, a large hand-off in one direction (8 MB of
+  activations) and the opposite-direction traffic (sampled ids, or gradients in training) would be
+  serialised on one stream in issue order and can wait on each other across ranks — with one stream
+  per direction each link only ever carries a FIFO of same-direction messages, which cannot deadlock.
+  """
 
   def __init__(self, rank: int, world: int):
     self.rank, self.world = rank, world
     self._pending = []
+    self._groups = {}
+    self._staged = False
+    if world > 1 and dist.is_initialized():
+      self._staged = dist.get_backend() == "gloo"
+      for e in ring_edges(world):  # every rank creates every group, in the same order
+        self._groups[e] = dist.new_group(ranks=sorted(e))
+
+  def _group(self, src: int, dst: int):
+    return self._groups.get((src, dst))
 
   def isend(self, t: torch.Tensor, dst: int):
-    w = dist.isend(t, dst)
+    if self._staged and t.is_cuda:
+      t = t.to("cpu")
+    w = dist.isend(t, dst, group=self._group(self.rank, dst))
     self._pending.append((w, t))  # keep the tensor alive until the send completes
     if len(self._pending) > 64:
       self.reap()
     return w
 
   def irecv(self, t: torch.Tensor, src: int):
-    return dist.irecv(t, src)
+    if self._staged and t.is_cuda:
+      host = torch.empty(t.shape, dtype=t.dtype)
+      return _StagedRecv(dist.irecv(host, src, group=self._group(src, self.rank)), host, t)
+    return dist.irecv(t, src, group=self._group(src, self.rank))
 
   def recv(self, t: torch.Tensor, src: int) -> torch.Tensor:
-    dist.irecv(t, src).wait()
+    self.irecv(t, src).wait()
     return t
 
   def reap(self):
