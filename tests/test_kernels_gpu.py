@@ -195,6 +195,29 @@ def test_sample_split_path_matches_single_block(gpu):
     assert torch.equal(a.cpu(), b[:6].cpu()), (temp, k)
 
 
+@pytest.mark.parametrize("algo", [1, 2])
+def test_sample_algos_match_single_block(gpu, algo):
+  """Chunk candidates + merge (1) and the two-pass candidate filter (2) must pick exactly the tokens of
+  the 5-pass one-workgroup-per-row path (0), including rows whose ties overflow the candidate list."""
+  from xotorch_support_jetson_amd.ops._ext import require
+  C = require()
+  torch.manual_seed(2)
+  V = 128256
+  lg = torch.randn(70, V, device=gpu) * 3
+  lg[3] = 0.0  # every logit tied: filter overflows -> exact fallback
+  lg[4] = torch.randint(0, 3, (V,), device=gpu).float()  # heavy ties at the cut
+  for temp, k in ((0.0, 35), (0.7, 35), (1.0, 64), (0.5, 7), (0.9, 1)):
+    temps = torch.full((70,), temp, device=gpu)
+    so = torch.tensor([99, 5], device=gpu, dtype=torch.int64)
+    a = torch.empty(70, dtype=torch.int32, device=gpu)
+    b = torch.empty_like(a)
+    C.sample(lg, temps, k, so, a, 0)
+    C.sample(lg, temps, k, so, b, algo)
+    rows = torch.arange(70) if algo == 2 or temp == 0.0 or k == 1 else torch.tensor([r for r in range(70) if r not in (3, 4)])
+    # (the chunk path keeps at most k tied candidates per chunk, so it may differ on rows tied at the cut)
+    assert torch.equal(a.cpu()[rows], b.cpu()[rows]), (temp, k)
+
+
 def test_sample_split_distribution(gpu):
   base = torch.full((128256,), -30.0, device=gpu)
   base[[10, 70000, 128000]] = torch.tensor([2.0, 1.0, 0.5], device=gpu)

@@ -514,7 +514,7 @@ void attn_prefill(const at::Tensor& q, const at::Tensor& k_cache, const at::Tens
 }
 
 void sample(const at::Tensor& logits, const at::Tensor& temps, int64_t top_k, const at::Tensor& seed_off,
-            at::Tensor& out) {
+            at::Tensor& out, int64_t algo) {
   CHECK_GPU(logits);
   CHECK_DT(logits, at::kFloat);
   CHECK_DT(temps, at::kFloat);
@@ -528,7 +528,7 @@ void sample(const at::Tensor& logits, const at::Tensor& temps, int64_t top_k, co
   auto ci = at::empty({B * xot::SAMPLE_CAND_PER_ROW}, logits.options().dtype(at::kInt));
   xot::launch_sample(logits.data_ptr<float>(), logits.stride(0), (int)B, (int)V, temps.data_ptr<float>(), (int)top_k,
                      seed_off.data_ptr<int64_t>(), out.data_ptr<int32_t>(),
-                     reinterpret_cast<uint32_t*>(ck.data_ptr<int>()), ci.data_ptr<int>(), cur_stream());
+                     reinterpret_cast<uint32_t*>(ck.data_ptr<int>()), ci.data_ptr<int>(), cur_stream(), (int)algo);
 }
 
 void ce_fwd(const at::Tensor& x, const at::Tensor& tgt, at::Tensor& loss, at::Tensor& lse) {
@@ -608,7 +608,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_train_transpose", &attn_train_transpose);
   m.def("attn_train_fwd", &attn_train_fwd);
   m.def("attn_train_bwd", &attn_train_bwd);
-  m.def("sample", &sample);
+  m.def("sample", &sample, py::arg("logits"), py::arg("temps"), py::arg("top_k"), py::arg("seed_off"), py::arg("out"),
+        py::arg("algo") = -1);
   m.def("ce_fwd", &ce_fwd);
   m.def("ce_bwd", &ce_bwd);
   m.def("adamw", &adamw);

@@ -74,7 +74,7 @@ int launch_attn_train_bwd(const uint16_t* q, long ldq, const uint16_t* qt, const
                           float* ws, long ws_elems, int B, int L, int H, int Hkv, int Dh, float scale, hipStream_t s);
 
 void launch_sample(const float* logits, long ld, int B, int V, const float* temps, int top_k,
-                   const int64_t* seed_off, int32_t* out, uint32_t* cand_key, int32_t* cand_idx, hipStream_t s);
+                   const int64_t* seed_off, int32_t* out, uint32_t* cand_key, int32_t* cand_idx, hipStream_t s, int algo = -1);
 constexpr int SAMPLE_CAND_PER_ROW = 64 * 64;  // split path scratch: chunks x max top-k
 
 void launch_ce_fwd(const void* x, bool x_f32, long ld, int T, int V, const int32_t* tgt, float* loss, float* lse,
