@@ -218,6 +218,23 @@ def test_sample_algos_match_single_block(gpu, algo):
     assert torch.equal(a.cpu()[rows], b.cpu()[rows]), (temp, k)
 
 
+def test_topk_cand(gpu):
+  """Per-row top-k (value, index) candidates of a vocab slice (split LM head) == torch.topk's set."""
+  torch.manual_seed(3)
+  B, V, k, kc = 37, 64000, 35, 64
+  lg = torch.randn(B, V, device=gpu) * 3
+  lg[5] = 0.0  # all tied: the exact fallback path, any k of them
+  vals, idx = K.topk_cand(lg, k, kc)
+  ref_v, _ = torch.topk(lg, k, dim=-1)
+  assert torch.equal(idx[:, k:].cpu(), torch.full((B, kc - k), -1, dtype=torch.int32))
+  assert bool(torch.isinf(vals[:, k:]).all())
+  got_v = torch.sort(vals[:, :k], dim=-1, descending=True).values
+  assert torch.equal(got_v, ref_v)
+  # values are the logits at the returned indices, indices distinct
+  assert torch.equal(lg.gather(1, idx[:, :k].long()), vals[:, :k])
+  assert all(len(set(r)) == k for r in idx[:, :k].tolist())
+
+
 def test_sample_split_distribution(gpu):
   base = torch.full((128256,), -30.0, device=gpu)
   base[[10, 70000, 128000]] = torch.tensor([2.0, 1.0, 0.5], device=gpu)

@@ -1,6 +1,6 @@
 """Ring pipeline across processes (gloo on CPU; the same code runs RCCL p2p on MI355X): 2 ranks, each
 holding half of the layers, M=2 micro-batches in flight; greedy tokens must equal a single-process
-full-model run."""
+full-model run, with the LM head on the last stage or split between the last and the first stage."""
 import os
 import socket
 
@@ -29,24 +29,25 @@ def _run(stage, n_mb):
   mbs = [MicroBatch([f"m{m}r{b}" for b in range(B)], prompt=_prompts(m), temps=torch.zeros(B)) for m in range(n_mb)]
   first = [stage.prefill(mb) for mb in mbs]
   for mb, t in zip(mbs, first):
-    if t is not None:
+    if t is not None and not stage.split:  # split head: the prefill token is drawn by the first stage
       mb.tokens.append(t.tolist())
   run_decode_steps(stage, mbs, STEPS, first_tokens=first if stage.last else None, record=True)
   return [mb.tokens for mb in mbs]
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, split):
   os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
   dist.init_process_group("gloo", rank=rank, world_size=world)
   try:
     c = PRESETS[MODEL]
     shard = equal_layer_shards(MODEL, c.num_layers, world)[rank]
     runner = ShardRunner(c, shard, "cpu", max_batch=8, max_ctx=64)
-    stage = RingStage(runner, rank, world, P2PTransport(rank, world))
+    stage = RingStage(runner, rank, world, P2PTransport(rank, world), split_head=split)
+    assert stage.split == split
     toks = _run(stage, 2)
     stage.t.drain()
     dist.barrier()
-    if stage.last:
+    if stage.samples:
       q.put(toks)
   finally:
     dist.destroy_process_group()
@@ -58,7 +59,8 @@ def _free_port():
     return s.getsockname()[1]
 
 
-def test_two_rank_ring_matches_single_process():
+@pytest.mark.parametrize("split", [False, True])
+def test_two_rank_ring_matches_single_process(split):
   c = PRESETS[MODEL]
   full = ShardRunner(c, Shard(MODEL, 0, c.num_layers - 1, c.num_layers), "cpu", max_batch=8, max_ctx=64)
   from xotorch_support_jetson_amd.parallel.comm import LoopbackTransport
@@ -66,7 +68,7 @@ def test_two_rank_ring_matches_single_process():
   ctx = mp.get_context("spawn")
   q = ctx.Queue()
   port = _free_port()
-  procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+  procs = [ctx.Process(target=_worker, args=(r, 2, port, q, split)) for r in range(2)]
   for p in procs:
     p.start()
   try:
@@ -77,5 +79,8 @@ def test_two_rank_ring_matches_single_process():
       if p.is_alive():
         p.kill()
   assert all(p.exitcode == 0 for p in procs)
-  assert got == ref
   assert len(ref[0]) == STEPS + 1
+  if split:  # a round's tokens are drawn at the start of the next round: STEPS tokens, prefill's included
+    assert got == [r[:STEPS] for r in ref]
+  else:
+    assert got == ref

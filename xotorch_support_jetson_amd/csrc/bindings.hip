@@ -531,6 +531,20 @@ void sample(const at::Tensor& logits, const at::Tensor& temps, int64_t top_k, co
                      reinterpret_cast<uint32_t*>(ck.data_ptr<int>()), ci.data_ptr<int>(), cur_stream(), (int)algo);
 }
 
+void topk_cand(const at::Tensor& logits, int64_t top_k, at::Tensor& vals, at::Tensor& idx) {
+  CHECK_GPU(logits);
+  CHECK_DT(logits, at::kFloat);
+  CHECK_DT(vals, at::kFloat);
+  CHECK_DT(idx, at::kInt);
+  XCHECK(logits.dim() == 2 && logits.stride(1) == 1, "topk_cand: logits must be [B, V] with contiguous rows");
+  const int64_t B = logits.size(0), V = logits.size(1);
+  XCHECK(vals.dim() == 2 && vals.is_contiguous() && vals.size(0) == B && idx.sizes() == vals.sizes() &&
+             idx.is_contiguous(), "topk_cand: vals / idx must be contiguous [B, kc]");
+  const int rc = xot::launch_topk_cand(logits.data_ptr<float>(), logits.stride(0), (int)B, (int)V, (int)top_k,
+                                       vals.data_ptr<float>(), idx.data_ptr<int32_t>(), (int)vals.size(1), cur_stream());
+  XCHECK(rc == 0, "topk_cand: unsupported top_k=", top_k, " V=", V, " kc=", vals.size(1));
+}
+
 void ce_fwd(const at::Tensor& x, const at::Tensor& tgt, at::Tensor& loss, at::Tensor& lse) {
   CHECK_GPU(x);
   XCHECK(x.dim() == 2 && x.stride(1) == 1, "ce_fwd: x must be [T, V]");
@@ -608,6 +622,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_train_transpose", &attn_train_transpose);
   m.def("attn_train_fwd", &attn_train_fwd);
   m.def("attn_train_bwd", &attn_train_bwd);
+  m.def("topk_cand", &topk_cand);
   m.def("sample", &sample, py::arg("logits"), py::arg("temps"), py::arg("top_k"), py::arg("seed_off"), py::arg("out"),
         py::arg("algo") = -1);
   m.def("ce_fwd", &ce_fwd);

@@ -75,6 +75,8 @@ int launch_attn_train_bwd(const uint16_t* q, long ldq, const uint16_t* qt, const
 
 void launch_sample(const float* logits, long ld, int B, int V, const float* temps, int top_k,
                    const int64_t* seed_off, int32_t* out, uint32_t* cand_key, int32_t* cand_idx, hipStream_t s, int algo = -1);
+int launch_topk_cand(const float* logits, long ld, int B, int V, int top_k, float* cval, int32_t* cidx, int kc,
+                     hipStream_t s);
 constexpr int SAMPLE_CAND_PER_ROW = 64 * 64;  // split path scratch: chunks x max top-k
 
 void launch_ce_fwd(const void* x, bool x_f32, long ld, int T, int V, const int32_t* tgt, float* loss, float* lse,

@@ -311,10 +311,15 @@ __global__ __launch_bounds__(256) void sample_stage2_kernel(const float* __restr
 // (seed, offset).  Candidate overflow (massive ties) falls back to the exact 4-pass radix over the row.
 constexpr int FCAP = 4096;
 
+// CAND: instead of sampling, write each row's top_k (value, index) candidates to cval / cidx_o [B][kc]
+// (ties at the cut trimmed to top_k; unused slots -inf / -1) -- one vocab slice's share of a sampler
+// that runs elsewhere (parallel/pipeline.py: LM head split between the last and the first ring stage).
+template <bool CAND>
 __global__ __launch_bounds__(1024) void sample_fast_kernel(const float* __restrict__ logits, long ld, int V,
                                                            const float* __restrict__ temps, int top_k,
                                                            const int64_t* __restrict__ seed_off,
-                                                           int32_t* __restrict__ out) {
+                                                           int32_t* __restrict__ out, float* __restrict__ cval,
+                                                           int32_t* __restrict__ cidx_o, int kc) {
   __shared__ uint32_t ckey[FCAP];
   __shared__ int cidx[FCAP];
   __shared__ uint32_t mkeys[1024];
@@ -327,9 +332,9 @@ __global__ __launch_bounds__(1024) void sample_fast_kernel(const float* __restri
   const float* x = logits + (size_t)row * ld;
   const float4* x4 = reinterpret_cast<const float4*>(x);
   const int V4 = V >> 2;
-  const float temp = temps[row];
-  const bool greedy = temp <= 1e-5f || top_k == 1;
-  const bool filter = !greedy && top_k > 0 && top_k < V;
+  const float temp = CAND ? 1.f : temps[row];
+  const bool greedy = !CAND && (temp <= 1e-5f || top_k == 1);
+  const bool filter = CAND || (!greedy && top_k > 0 && top_k < V);
 
   // pass 1: per-thread max (and first argmax for greedy rows)
   float best = -INFINITY;
@@ -414,6 +419,38 @@ __global__ __launch_bounds__(1024) void sample_fast_kernel(const float* __restri
     }
   }
 
+  if constexpr (CAND) {
+    __shared__ int ecnt;
+    if (tid == 0) ecnt = 0;
+    __syncthreads();
+    float* cv = cval + (size_t)row * kc;
+    int32_t* ci = cidx_o + (size_t)row * kc;
+    auto emit = [&](uint32_t k, int i, bool tie) {
+      const int p = atomicAdd(&ecnt, 1);
+      if (!tie || p < top_k) {
+        cv[p] = __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
+        ci[p] = i;
+      }
+    };
+    for (int tie = 0; tie < 2; ++tie) {  // keys above the cut (fewer than top_k), then ties at the cut
+      if (use_cand) {
+        for (int p = tid; p < n; p += 1024)
+          if (tie ? ckey[p] == th : ckey[p] > th) emit(ckey[p], cidx[p], tie);
+      } else {
+        for (int i = tid; i < V; i += 1024) {
+          const uint32_t k = fkey(x[i]);
+          if (tie ? k == th : k > th) emit(k, i, tie);
+        }
+      }
+      __syncthreads();
+    }
+    for (int p = min(ecnt, top_k) + tid; p < kc; p += 1024) {
+      cv[p] = -INFINITY;
+      ci[p] = -1;
+    }
+    return;
+  }
+
   const float invt = 1.f / fmaxf(temp, 1e-5f);
   const uint64_t seed = (uint64_t)seed_off[0], off = (uint64_t)seed_off[1];
   const uint64_t base = splitmix64(seed ^ splitmix64(off * 0x632be59bd9b4e019ull + (uint64_t)row));
@@ -452,7 +489,7 @@ void launch_sample(const float* logits, long ld, int B, int V, const float* temp
                     top_k <= 1024;
   const bool split = !fast && can && (algo == 1 || (algo < 0 && B < 64));
   if (fast) {  // tools/bench_sample.py: B = 512 297 -> 79 us, B = 1 33 -> 31 us (128k vocab, top-k 35)
-    sample_fast_kernel<<<B, 1024, 0, s>>>(logits, ld, V, temps, top_k, seed_off, out);
+    sample_fast_kernel<false><<<B, 1024, 0, s>>>(logits, ld, V, temps, top_k, seed_off, out, nullptr, nullptr, 0);
     return;
   }
   if (split) {
@@ -461,6 +498,14 @@ void launch_sample(const float* logits, long ld, int B, int V, const float* temp
     return;
   }
   sample_kernel<<<B, 1024, 0, s>>>(logits, ld, V, temps, top_k, seed_off, out);
+}
+
+int launch_topk_cand(const float* logits, long ld, int B, int V, int top_k, float* cval, int32_t* cidx, int kc,
+                     hipStream_t s) {
+  if (B <= 0) return 0;
+  if (top_k < 1 || top_k > kc || top_k >= V || V % 4 != 0 || ld % 4 != 0 || ((uintptr_t)logits & 15) != 0) return -1;
+  sample_fast_kernel<true><<<B, 1024, 0, s>>>(logits, ld, V, nullptr, top_k, nullptr, nullptr, cval, cidx, kc);
+  return 0;
 }
 
 }  // namespace xot

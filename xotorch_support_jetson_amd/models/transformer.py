@@ -92,6 +92,10 @@ class ShardModel:
     self.ws = None
     if self.device.type == "cuda":
       self.ws = K.DecodeWorkspace(max_batch, c.num_heads, c.head_dim, max_ctx, self.device)
+    # last shard with the LM head split across two ring stages: logits of vocab rows [0, head_rows) only,
+    # and forward returns (logits, normed hidden)
+    self.head_rows: Optional[int] = None
+    self._head_cache = None
 
   # ------------------------------------------------------------------ helpers
   def _attention(self, q: torch.Tensor, li: int, inp: StepInputs) -> torch.Tensor:
@@ -206,7 +210,21 @@ class ShardModel:
     if not inp.decode or n == 0:
       hl = h.index_select(0, inp.last_idx) if not inp.decode else h
       xn, _ = K.rmsnorm(hl, w.norm, c.rms_norm_eps)
-    return linear(xn, w.lm_head, out_dtype=torch.float32)
+    if self.head_rows is None:
+      return linear(xn, w.lm_head, out_dtype=torch.float32)
+    # LM head split with another stage (parallel/pipeline.py): logits of vocab rows [0, head_rows) and
+    # the normed hidden state the other stage applies the remaining rows to
+    return linear(xn, self._head_slice(), out_dtype=torch.float32), xn
+
+  def _head_slice(self) -> torch.Tensor:
+    w = self.w.lm_head
+    if self._head_cache is None or self._head_cache[0] != self.head_rows:
+      # rows [0, r) of the pre-shuffled layout (16-row groups) are a storage prefix: a view, no copy
+      hs = w[: self.head_rows]
+      if layout_of(w) != "rowmajor":
+        hs.xot_layout = layout_of(w)
+      self._head_cache = (self.head_rows, hs)
+    return self._head_cache[1]
 
 
 def make_step_inputs(seqs: List[tuple], device, block_width: Optional[int] = None) -> StepInputs:

@@ -263,6 +263,17 @@ def random_weights(c: ModelConfig, shard: Shard, device: torch.device | str = "c
   return sw
 
 
+def random_head_rows(c: ModelConfig, rows_from: int, device: torch.device | str = "cpu", dtype=torch.bfloat16,
+                     seed: int = 0, std: float = 0.02) -> torch.Tensor:
+  """Rows [rows_from, V) of the LM head random_weights gives the last shard (same generator stream, so
+  a stage holding only these rows computes exactly the full head's logits for them)."""
+  dev = torch.device(device)
+  g = torch.Generator(device=dev)
+  g.manual_seed(seed * 1_000_003 + (1 if c.tie_word_embeddings else 3))
+  full = torch.empty((c.vocab_size, c.hidden_size), device=dev, dtype=dtype).normal_(0.0, std, generator=g)
+  return full[rows_from:].clone()
+
+
 # -------------------------------------------------------------------- HF safetensors
 def _weight_map(model_dir: Path) -> Dict[str, str]:
   idx = model_dir / "model.safetensors.index.json"

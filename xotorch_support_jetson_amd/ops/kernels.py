@@ -263,3 +263,20 @@ def sample(logits: torch.Tensor, temps: torch.Tensor, top_k: int, seed_off: torc
   out = torch.empty(logits.shape[0], dtype=torch.int32, device=logits.device) if out is None else out
   require().sample(logits, temps, int(top_k), seed_off, out)
   return out
+
+
+def topk_cand(logits: torch.Tensor, top_k: int, kc: int = 64) -> tuple:
+  """Each row's top_k (value, index) candidates in [B, kc] buffers (unused slots -inf / -1): one vocab
+  slice's contribution to a sampler that runs on another stage."""
+  B = logits.shape[0]
+  if not _gpu(logits):
+    v, i = torch.topk(logits.float(), top_k, dim=-1)
+    vals = torch.full((B, kc), float("-inf"))
+    idx = torch.full((B, kc), -1, dtype=torch.int32)
+    vals[:, :top_k] = v
+    idx[:, :top_k] = i.int()
+    return vals, idx
+  vals = torch.empty(B, kc, dtype=torch.float32, device=logits.device)
+  idx = torch.empty(B, kc, dtype=torch.int32, device=logits.device)
+  require().topk_cand(logits, int(top_k), vals, idx)
+  return vals, idx

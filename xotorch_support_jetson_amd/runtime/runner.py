@@ -47,6 +47,7 @@ class ShardRunner:
     self.device = torch.device(device)
     if self.device.type == "cuda":
       torch.cuda.set_device(self.device)
+    self._random_weights, self._seed = weights is None, seed
     self.weights = weights if weights is not None else random_weights(config, shard, self.device, seed=seed)
     if self.device.type == "cuda" and os.environ.get("XOT_SHUFFLE", "1") == "1":
       # projection weights -> pre-shuffled MFMA-fragment layout (gemm_stream for decode-shaped M,
@@ -185,7 +186,33 @@ class ShardRunner:
     else:
       g["x"][:B].copy_(x)
     g["graph"].replay()
-    return g["out"][:B]
+    out = g["out"]
+    return tuple(t[:B] for t in out) if isinstance(out, tuple) else out[:B]
+
+  # ------------------------------------------------------------------ split LM head
+  def head_tail(self, rows_from: int) -> Optional[torch.Tensor]:
+    """LM-head rows [rows_from, V) in the device layout, for a first stage that applies them to the
+    normed hidden state the last stage sends (parallel/pipeline.py).  None when they cannot be derived
+    here (externally loaded weights without the head on this shard)."""
+    from ..models.weights import random_head_rows
+    w = self.weights
+    c = self.config
+    if w.lm_head is not None:
+      full = w.lm_head
+    elif c.tie_word_embeddings and w.embed is not None:
+      full = w.embed
+    elif self._random_weights:
+      full = None
+    else:
+      return None
+    if full is not None:
+      t = full[rows_from:]
+      if linear_mod.layout_of(full) == "stream":  # rows [r, V) of the shuffled layout: a storage suffix
+        t.xot_layout = "stream"
+        return t
+      return linear_mod.to_stream_layout(t.contiguous())
+    t = random_head_rows(c, rows_from, self.device, seed=self._seed)
+    return linear_mod.to_stream_layout(t)
 
   def _capture(self, Bp: int) -> dict:
     dev = self.device
