@@ -123,6 +123,31 @@ def test_rope_kv_write(gpu, H, Hkv, Dh):
   assert torch.equal(vc, vr)
 
 
+@pytest.mark.parametrize("H,Hkv,Dh,bias", [(64, 8, 128, False), (14, 2, 64, True)])
+def test_splitk_rope_kv_write(gpu, H, Hkv, Dh, bias):
+  """QKV split-K slabs -> RoPE + paged KV write in one kernel == bf16 reduce, then rope_kv_write."""
+  from xotorch_support_jetson_amd.ops._ext import require
+  C = require()
+  torch.manual_seed(0)
+  T, S = 19, 3
+  N = (H + 2 * Hkv) * Dh
+  cs = build_cos_sin(Dh, 4096, 500000.0, None, device=gpu)
+  ws = torch.randn(S, T, N, device=gpu)
+  b = torch.randn(N, device=gpu).to(torch.bfloat16) if bias else None
+  qkv = (ws[0] + ws[1] + ws[2] + (b.float() if bias else 0.0)).to(torch.bfloat16)
+  pos = torch.randint(0, 4000, (T,), device=gpu, dtype=torch.int32)
+  slots = torch.randperm(10 * 64, device=gpu)[:T].to(torch.int64)
+  slots[3] = -1
+  caches = [(torch.zeros(10, Hkv, 64, Dh, device=gpu, dtype=torch.bfloat16),
+             torch.zeros(10, Hkv, Dh, 64, device=gpu, dtype=torch.bfloat16)) for _ in range(2)]
+  q1 = K.rope_kv_write(qkv, pos, cs, slots, caches[0][0], caches[0][1], H, Hkv)
+  q2 = torch.empty(T, H, Dh, device=gpu, dtype=torch.bfloat16)
+  C.splitk_rope_kv_write(ws, S, b, pos, cs, slots, q2, caches[1][0], caches[1][1], H, Hkv)
+  assert rel_err(q2, q1) < 1e-2
+  assert rel_err(caches[1][0], caches[0][0]) < 1e-2
+  assert rel_err(caches[1][1], caches[0][1]) < 1e-2
+
+
 @pytest.mark.parametrize("H,Hkv,Dh", [(64, 8, 128), (32, 8, 64), (14, 2, 64), (32, 4, 128)])
 @pytest.mark.parametrize("ctx", [[1, 64, 65, 700], [2100, 5, 1300, 64]])
 def test_attn_decode(gpu, H, Hkv, Dh, ctx):
@@ -140,8 +165,16 @@ def test_attn_decode(gpu, H, Hkv, Dh, ctx):
       if algo == 0 and ppp in (1, 3):
         continue
       ws = K.DecodeWorkspace(B, H, Dh, maxb * 64, gpu, pages_per_part=ppp, algo=algo)
+      assert ws.tickets is not None  # partitions merged in-kernel by the last arriver
       out = K.attn_decode(q, kc, vc, bt, cl, scale, ws)
       assert rel_err(out, ref) < 2e-2, (algo, ppp)
+      # the tickets are back at zero, so the next call merges again; the separate reduce agrees
+      assert int(ws.tickets.abs().sum()) == 0, (algo, ppp)
+      again = K.attn_decode(q, kc, vc, bt, cl, scale, ws)
+      tk, ws.tickets = ws.tickets, None
+      red = K.attn_decode(q, kc, vc, bt, cl, scale, ws)
+      ws.tickets = tk
+      assert torch.equal(again, out) and rel_err(red, out) < 1e-3, (algo, ppp)
 
 
 @pytest.mark.parametrize("H,Hkv,Dh", [(32, 8, 64), (64, 8, 128), (14, 2, 64)])

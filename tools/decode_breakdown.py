@@ -20,7 +20,7 @@ def main():
   path = a.trace or sorted(glob.glob("gpurun_out/prof/**/*kernel_trace.csv", recursive=True))[-1]
   rows = list(csv.DictReader(open(path)))
   ends = sorted(int(r["End_Timestamp"]) for r in rows
-                if "sample_kernel" in r["Kernel_Name"] or "sample_stage2" in r["Kernel_Name"])
+                if any(k in r["Kernel_Name"] for k in ("sample_kernel", "sample_stage2", "sample_fast_kernel")))
   lo, hi = ends[-(a.steps + 1)], ends[-1]
   dec = [r for r in rows if lo < int(r["Start_Timestamp"]) <= hi]
   agg = collections.defaultdict(lambda: [0, 0])

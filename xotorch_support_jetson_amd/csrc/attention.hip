@@ -31,12 +31,49 @@ __device__ __forceinline__ void wave_lds_sync() {
 }
 
 // ============================================================================ decode
+// Merge the nparts partial (o, m, l) of the G query heads of KV head kvh of sequence b (log-sum-exp).
+// Every address depends on the thread's element, so the partials come in by vector loads (the scalar
+// cache would bypass the acquire that makes other workgroups' partials visible).
+template <int DH>
+__device__ __forceinline__ void combine_parts(const float* ws_o, const float* ws_ml, uint16_t* __restrict__ out,
+                                              int b, int kvh, int G, int H, int nparts, int tid, int nthr) {
+  for (int e = tid; e < G * DH; e += nthr) {
+    const int row = e / DH, d = e % DH, h = kvh * G + row;
+    const size_t base = ((size_t)b * H + h) * nparts;
+    float M = NEG_BIG;
+    for (int p = 0; p < nparts; ++p) M = fmaxf(M, ws_ml[(base + p) * 2]);
+    float L = 0.f, O = 0.f;
+    for (int p = 0; p < nparts; ++p) {
+      const float f = exp2f(ws_ml[(base + p) * 2] - M);
+      L += ws_ml[(base + p) * 2 + 1] * f;
+      O += ws_o[(base + p) * DH + d] * f;
+    }
+    out[((size_t)b * H + h) * DH + d] = f2bf(L > 0.f ? O / L : 0.f);
+  }
+}
+
+// Last-arriver hand-off of a partition's partials (cdna_hip_programming.md Guideline 16 recipe): the
+// caller's stores are drained, one lane releases at agent scope, drains again, adds to the (sequence,
+// KV head) ticket; the last of the nparts arrivals acquires and resets the ticket for the next launch.
+__device__ __forceinline__ bool partition_arrive_last(int* tickets, int slot, int nparts) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const int prev = __hip_atomic_fetch_add(tickets + slot, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const bool last = prev == nparts - 1;
+  if (last) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(tickets + slot, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  return last;
+}
+
 template <int DH>
 __global__ __launch_bounds__(256) void attn_decode_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
     const int32_t* __restrict__ block_tables, int max_blocks, const int32_t* __restrict__ ctx_lens,
     uint16_t* __restrict__ out, float* __restrict__ ws_o, float* __restrict__ ws_ml, int H, int Hkv,
-    int pages_per_part, int nparts, float scale_log2, int num_pages) {
+    int pages_per_part, int nparts, float scale_log2, int num_pages, int* __restrict__ tickets) {
   constexpr int KS = DH / 32;   // MFMA k-steps over the head dim
   constexpr int NDT = DH / 16;  // 16-wide d tiles of the output
   constexpr int PLD = PAGE + 8;
@@ -182,6 +219,14 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
       }
     }
   }
+  if (nparts > 1 && tickets != nullptr) {  // the last partition of this (sequence, KV head) merges them all
+    __shared__ int last_s;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) last_s = partition_arrive_last(tickets, b * Hkv + kvh, nparts);
+    __syncthreads();
+    if (last_s) combine_parts<DH>(ws_o, ws_ml, out, b, kvh, G, H, nparts, threadIdx.x, 256);
+  }
 }
 
 template <int DH>
@@ -221,7 +266,7 @@ __global__ __launch_bounds__(256) void attn_decode_wave_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
     const int32_t* __restrict__ block_tables, int max_blocks, const int32_t* __restrict__ ctx_lens,
     uint16_t* __restrict__ out, float* __restrict__ ws_o, float* __restrict__ ws_ml, int B, int H, int Hkv,
-    int pages_per_part, int nparts, float scale_log2, int num_pages) {
+    int pages_per_part, int nparts, float scale_log2, int num_pages, int* __restrict__ tickets) {
   constexpr int KS = DH / 32;   // k-steps of S^T over the head dim
   constexpr int NDT = DH / 16;  // 16-row d tiles of O^T
   const int lane = threadIdx.x & 63;
@@ -337,9 +382,9 @@ __global__ __launch_bounds__(256) void attn_decode_wave_kernel(
   // lane (g, c): head c, d rows 16dt + 4g + r
   l += __shfl_xor(l, 16, 64);
   l += __shfl_xor(l, 32, 64);
-  if (c >= G) return;
   const int h = kvh * G + c;
   if (nparts == 1) {
+    if (c >= G) return;
     const float inv = l > 0.f ? 1.f / l : 0.f;
     uint16_t* op = out + ((size_t)b * H + h) * DH + 4 * g;
 #pragma unroll
@@ -349,7 +394,9 @@ __global__ __launch_bounds__(256) void attn_decode_wave_kernel(
       for (int r = 0; r < 4; ++r) v[r] = (short)f2bf(o[dt][r] * inv);
       *reinterpret_cast<s16x4*>(op + 16 * dt) = v;
     }
-  } else {
+    return;
+  }
+  if (c < G) {
     const size_t idx = ((size_t)b * H + h) * nparts + part;
     float* wo = ws_o + idx * DH + 4 * g;
 #pragma unroll
@@ -359,12 +406,22 @@ __global__ __launch_bounds__(256) void attn_decode_wave_kernel(
       ws_ml[idx * 2 + 1] = l;
     }
   }
+  if (tickets != nullptr) {  // the last partition of this (sequence, KV head) merges them all
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int last = 0;
+    if (lane == 0) last = partition_arrive_last(tickets, b * Hkv + kvh, nparts);
+    last = __shfl(last, 0, 64);
+    // (lane 0's acquire precedes the other lanes' loads: one wave, program order)
+    if (last) combine_parts<DH>(ws_o, ws_ml, out, b, kvh, G, H, nparts, lane, 64);
+  }
 }
 
 int launch_attn_decode(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, const int32_t* block_tables,
                        int max_blocks, const int32_t* ctx_lens, uint16_t* out, float* ws_o, float* ws_ml, int B,
                        int H, int Hkv, int Dh, int pages_per_part, int nparts, float scale, int num_pages, int algo,
-                       hipStream_t s) {
+                       int* tickets, hipStream_t s) {
+  // tickets ([B * Hkv] int32, zero at rest): the last partition merges in-kernel, no reduce launch
+  const bool reduce = nparts > 1 && tickets == nullptr;
   if (B <= 0) return 0;
   if (H % Hkv != 0 || H / Hkv > 16) return -1;
   dim3 grid(nparts, Hkv, B);
@@ -373,13 +430,13 @@ int launch_attn_decode(const uint16_t* q, const uint16_t* kc, const uint16_t* vc
     const int units = B * Hkv * nparts, wgs = (units + 3) / 4;
 #define XOT_WAVE(DHV, PFV)                                                                                       \
   attn_decode_wave_kernel<DHV, PFV><<<wgs, 256, 0, s>>>(q, kc, vc, block_tables, max_blocks, ctx_lens, out, ws_o, \
-                                                        ws_ml, B, H, Hkv, pages_per_part, nparts, sl, num_pages)
+                                                        ws_ml, B, H, Hkv, pages_per_part, nparts, sl, num_pages, tickets)
     if (Dh == 128) {
       if (algo == 2) XOT_WAVE(128, true); else XOT_WAVE(128, false);
-      if (nparts > 1) attn_decode_reduce_kernel<128><<<B * H, 128, 0, s>>>(ws_o, ws_ml, ctx_lens, out, H, nparts, pages_per_part);
+      if (reduce) attn_decode_reduce_kernel<128><<<B * H, 128, 0, s>>>(ws_o, ws_ml, ctx_lens, out, H, nparts, pages_per_part);
     } else if (Dh == 64) {
       if (algo == 2) XOT_WAVE(64, true); else XOT_WAVE(64, false);
-      if (nparts > 1) attn_decode_reduce_kernel<64><<<B * H, 64, 0, s>>>(ws_o, ws_ml, ctx_lens, out, H, nparts, pages_per_part);
+      if (reduce) attn_decode_reduce_kernel<64><<<B * H, 64, 0, s>>>(ws_o, ws_ml, ctx_lens, out, H, nparts, pages_per_part);
     } else {
       return -1;
     }
@@ -388,12 +445,12 @@ int launch_attn_decode(const uint16_t* q, const uint16_t* kc, const uint16_t* vc
   }
   if (Dh == 128) {
     attn_decode_kernel<128><<<grid, 256, 0, s>>>(q, kc, vc, block_tables, max_blocks, ctx_lens, out, ws_o, ws_ml,
-                                                 H, Hkv, pages_per_part, nparts, sl, num_pages);
-    if (nparts > 1) attn_decode_reduce_kernel<128><<<B * H, 128, 0, s>>>(ws_o, ws_ml, ctx_lens, out, H, nparts, pages_per_part);
+                                                 H, Hkv, pages_per_part, nparts, sl, num_pages, tickets);
+    if (reduce) attn_decode_reduce_kernel<128><<<B * H, 128, 0, s>>>(ws_o, ws_ml, ctx_lens, out, H, nparts, pages_per_part);
   } else if (Dh == 64) {
     attn_decode_kernel<64><<<grid, 256, 0, s>>>(q, kc, vc, block_tables, max_blocks, ctx_lens, out, ws_o, ws_ml, H,
-                                                Hkv, pages_per_part, nparts, sl, num_pages);
-    if (nparts > 1) attn_decode_reduce_kernel<64><<<B * H, 64, 0, s>>>(ws_o, ws_ml, ctx_lens, out, H, nparts, pages_per_part);
+                                                Hkv, pages_per_part, nparts, sl, num_pages, tickets);
+    if (reduce) attn_decode_reduce_kernel<64><<<B * H, 64, 0, s>>>(ws_o, ws_ml, ctx_lens, out, H, nparts, pages_per_part);
   } else {
     return -1;
   }

@@ -134,6 +134,38 @@ void rope_kv_write(const at::Tensor& qkv, const at::Tensor& pos, const at::Tenso
                             (int)cos_sin.size(0), (long)(nb * BS), cur_stream());
 }
 
+void splitk_rope_kv_write(const at::Tensor& ws, int64_t S, const c10::optional<at::Tensor>& bias,
+                          const at::Tensor& pos, const at::Tensor& cos_sin, const at::Tensor& slots, at::Tensor& q_out,
+                          at::Tensor& k_cache, at::Tensor& v_cache, int64_t H, int64_t Hkv) {
+  CHECK_DT(ws, at::kFloat);
+  CHECK_BF16(q_out);
+  CHECK_BF16(k_cache);
+  CHECK_BF16(v_cache);
+  CHECK_DT(pos, at::kInt);
+  CHECK_DT(slots, at::kLong);
+  CHECK_DT(cos_sin, at::kFloat);
+  XCHECK(all_contig_gpu(ws, pos, cos_sin, slots, q_out), "splitk_rope_kv_write: non-contiguous");
+  XCHECK(k_cache.is_contiguous() && v_cache.is_contiguous() && k_cache.dim() == 4 && v_cache.dim() == 4,
+         "splitk_rope_kv_write: caches must be contiguous 4-D");
+  const int64_t T = pos.numel(), Dh = k_cache.size(3), BS = k_cache.size(2), nb = k_cache.size(0);
+  XCHECK(k_cache.size(1) == Hkv && v_cache.size(0) == nb && v_cache.size(1) == Hkv && v_cache.size(2) == Dh &&
+             v_cache.size(3) == BS,
+         "splitk_rope_kv_write: cache layout must be K[nb,Hkv,BS,Dh], V[nb,Hkv,Dh,BS]");
+  const int64_t N = (H + 2 * Hkv) * Dh;
+  XCHECK(Dh % 8 == 0 && S >= 1 && ws.numel() >= S * T * N, "splitk_rope_kv_write: slabs must hold S x T x N");
+  XCHECK(q_out.numel() == T * H * Dh && slots.numel() == T, "splitk_rope_kv_write: q_out/slots shape mismatch");
+  XCHECK(cos_sin.dim() == 2 && cos_sin.size(1) == Dh, "splitk_rope_kv_write: cos_sin must be [max_pos, Dh]");
+  const uint16_t* bp = nullptr;
+  if (bias.has_value()) {
+    CHECK_BF16((*bias));
+    XCHECK(bias->is_contiguous() && bias->numel() == N, "splitk_rope_kv_write: bias shape");
+    bp = bf(*bias);
+  }
+  xot::launch_splitk_rope_kv_write(ws.data_ptr<float>(), (int)S, bp, pos.data_ptr<int32_t>(), cos_sin.data_ptr<float>(),
+                                   slots.data_ptr<int64_t>(), bf(q_out), bf(k_cache), bf(v_cache), (int)T, (int)H,
+                                   (int)Hkv, (int)Dh, (int)BS, (int)cos_sin.size(0), (long)(nb * BS), cur_stream());
+}
+
 void rope_apply(const at::Tensor& x, at::Tensor& y, const at::Tensor& pos, const at::Tensor& cos_sin, int64_t nh,
                 int64_t Dh, bool inverse) {
   CHECK_BF16(x);
@@ -389,7 +421,8 @@ void moe_combine(const at::Tensor& y, const at::Tensor& slot_of, const at::Tenso
 
 void attn_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
                  const at::Tensor& block_tables, const at::Tensor& ctx_lens, at::Tensor& out, at::Tensor& ws_o,
-                 at::Tensor& ws_ml, int64_t pages_per_part, int64_t nparts, double scale, int64_t algo) {
+                 at::Tensor& ws_ml, int64_t pages_per_part, int64_t nparts, double scale, int64_t algo,
+                 const c10::optional<at::Tensor>& tickets) {
   CHECK_BF16(q);
   CHECK_BF16(k_cache);
   CHECK_BF16(v_cache);
@@ -410,11 +443,18 @@ void attn_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tenso
   XCHECK(pages_per_part >= 1 && nparts >= 1, "attn_decode: bad partitioning");
   if (nparts > 1)
     XCHECK(ws_o.numel() >= B * H * nparts * Dh && ws_ml.numel() >= B * H * nparts * 2, "attn_decode: workspace small");
+  int* tk = nullptr;
+  if (tickets.has_value() && nparts > 1) {
+    CHECK_DT((*tickets), at::kInt);
+    XCHECK(tickets->is_contiguous() && tickets->numel() >= B * Hkv && tickets->device() == q.device(),
+           "attn_decode: tickets must hold B * Hkv zeroed int32");
+    tk = tickets->data_ptr<int32_t>();
+  }
   const int rc = xot::launch_attn_decode(bf(q), bf(k_cache), bf(v_cache), block_tables.data_ptr<int32_t>(),
                                          (int)block_tables.size(1), ctx_lens.data_ptr<int32_t>(), bf(out),
                                          ws_o.data_ptr<float>(), ws_ml.data_ptr<float>(), (int)B, (int)H, (int)Hkv,
                                          (int)Dh, (int)pages_per_part, (int)nparts, (float)scale, (int)nb, (int)algo,
-                                         cur_stream());
+                                         tk, cur_stream());
   XCHECK(rc == 0, "attn_decode: unsupported H=", H, " Hkv=", Hkv, " Dh=", Dh);
 }
 
@@ -617,8 +657,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("splits") = 1);
   m.def("attn_decode", &attn_decode, py::arg("q"), py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"),
         py::arg("ctx_lens"), py::arg("out"), py::arg("ws_o"), py::arg("ws_ml"), py::arg("pages_per_part"),
-        py::arg("nparts"), py::arg("scale"), py::arg("algo") = 2);
+        py::arg("nparts"), py::arg("scale"), py::arg("algo") = 2, py::arg("tickets") = py::none());
   m.def("attn_prefill", &attn_prefill);
+  m.def("splitk_rope_kv_write", &splitk_rope_kv_write);
   m.def("attn_train_transpose", &attn_train_transpose);
   m.def("attn_train_fwd", &attn_train_fwd);
   m.def("attn_train_bwd", &attn_train_bwd);

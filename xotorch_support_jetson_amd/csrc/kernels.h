@@ -16,6 +16,10 @@ void launch_embedding(const int32_t* ids, const uint16_t* table, uint16_t* out, 
 void launch_silu_mul(const uint16_t* gu, uint16_t* out, int T, int F, hipStream_t s);
 void launch_silu_mul_il(const uint16_t* gu, uint16_t* out, int T, int F, hipStream_t s);
 void launch_silu_mul_bwd(const uint16_t* gu, const uint16_t* dout, uint16_t* dgu, int T, int F, hipStream_t s);
+void launch_splitk_rope_kv_write(const float* ws, int S, const uint16_t* bias, const int32_t* pos,
+                                 const float* cos_sin, const int64_t* slots, uint16_t* q_out, uint16_t* kc,
+                                 uint16_t* vc, int T, int H, int Hkv, int Dh, int BS, int max_pos, long nslots,
+                                 hipStream_t s);
 void launch_rope_kv_write(const uint16_t* qkv, const int32_t* pos, const float* cos_sin, const int64_t* slots,
                           uint16_t* q_out, uint16_t* kc, uint16_t* vc, int T, int H, int Hkv, int Dh, int BS,
                           int max_pos, long nslots, hipStream_t s);
@@ -55,7 +59,7 @@ int launch_gemm_tiled(const uint16_t* X, int ldx, const uint16_t* W, int ldw, co
 int launch_attn_decode(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, const int32_t* block_tables,
                        int max_blocks, const int32_t* ctx_lens, uint16_t* out, float* ws_o, float* ws_ml, int B,
                        int H, int Hkv, int Dh, int pages_per_part, int nparts, float scale, int num_pages, int algo,
-                       hipStream_t s);
+                       int* tickets, hipStream_t s);
 int launch_attn_prefill(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, const int32_t* block_tables,
                         int max_blocks, const int32_t* cu_q, const int32_t* ctx_lens, uint16_t* out, int B,
                         int max_qlen, int H, int Hkv, int Dh, float scale, int num_pages, hipStream_t s);

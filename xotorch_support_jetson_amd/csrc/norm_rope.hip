@@ -79,7 +79,9 @@ void launch_rmsnorm(const uint16_t* x, const uint16_t* res, const uint16_t* w, u
 // ---------------------------------------------------------------- split-K reduce + residual + RMSNorm
 // One workgroup per row: h = bf16(h + bias + sum_s ws[s][row]) (in place), out = rmsnorm(h) * w.  Replaces
 // the split-K reduce kernel of a residual projection (o_proj / down_proj) and the RMSNorm that follows it.
-template <int MAXC>
+// SS > 0: exactly SS slabs, loads unrolled and issued together (a runtime slab loop waits for each load
+// in turn: one row at decode batch 1 took 6.9 us); SS = 0: any S.
+template <int MAXC, int SS>
 __global__ __launch_bounds__(256) void splitk_resid_rmsnorm_kernel(const float* __restrict__ ws, int S,
                                                                    size_t sstride, const uint16_t* __restrict__ bias,
                                                                    uint16_t* __restrict__ h,
@@ -104,12 +106,28 @@ __global__ __launch_bounds__(256) void splitk_resid_rmsnorm_kernel(const float* 
         for (int j = 0; j < 8; ++j) acc[j] += bf2f(bv[j]);
       }
       const float* sp = ws + base + c * 8;
-      for (int sl = 0; sl < S; ++sl, sp += sstride) {
-        const f32x4 p0 = *reinterpret_cast<const f32x4*>(sp), p1 = *reinterpret_cast<const f32x4*>(sp + 4);
+      if constexpr (SS > 0) {
+        f32x4 p[SS][2];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          acc[j] += p0[j];
-          acc[4 + j] += p1[j];
+        for (int sl = 0; sl < SS; ++sl) {
+          p[sl][0] = *reinterpret_cast<const f32x4*>(sp + sl * sstride);
+          p[sl][1] = *reinterpret_cast<const f32x4*>(sp + sl * sstride + 4);
+        }
+#pragma unroll
+        for (int sl = 0; sl < SS; ++sl)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            acc[j] += p[sl][0][j];
+            acc[4 + j] += p[sl][1][j];
+          }
+      } else {
+        for (int sl = 0; sl < S; ++sl, sp += sstride) {
+          const f32x4 p0 = *reinterpret_cast<const f32x4*>(sp), p1 = *reinterpret_cast<const f32x4*>(sp + 4);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            acc[j] += p0[j];
+            acc[4 + j] += p1[j];
+          }
         }
       }
       s16x8 hv;
@@ -144,14 +162,28 @@ void launch_splitk_resid_rmsnorm(const float* ws, int S, const uint16_t* bias, u
   if (rows <= 0) return;
   const int nchunk = D / 8;
   const size_t ss = (size_t)rows * D;
+  auto go = [&](auto maxc) {
+    constexpr int MC = decltype(maxc)::value;
+#define XOT_SRR(SV) splitk_resid_rmsnorm_kernel<MC, SV><<<rows, 256, 0, s>>>(ws, S, ss, bias, h, w, out, D, eps)
+    switch (S) {
+      case 1: XOT_SRR(1); break;
+      case 2: XOT_SRR(2); break;
+      case 3: XOT_SRR(3); break;
+      case 4: XOT_SRR(4); break;
+      case 6: XOT_SRR(6); break;
+      case 8: XOT_SRR(8); break;
+      default: XOT_SRR(0); break;
+    }
+#undef XOT_SRR
+  };
   if (nchunk <= 256)
-    splitk_resid_rmsnorm_kernel<1><<<rows, 256, 0, s>>>(ws, S, ss, bias, h, w, out, D, eps);
+    go(std::integral_constant<int, 1>());
   else if (nchunk <= 512)
-    splitk_resid_rmsnorm_kernel<2><<<rows, 256, 0, s>>>(ws, S, ss, bias, h, w, out, D, eps);
+    go(std::integral_constant<int, 2>());
   else if (nchunk <= 1024)
-    splitk_resid_rmsnorm_kernel<4><<<rows, 256, 0, s>>>(ws, S, ss, bias, h, w, out, D, eps);
+    go(std::integral_constant<int, 4>());
   else
-    splitk_resid_rmsnorm_kernel<8><<<rows, 256, 0, s>>>(ws, S, ss, bias, h, w, out, D, eps);
+    go(std::integral_constant<int, 8>());
 }
 
 // ---------------------------------------------------------------- RMSNorm bwd
@@ -395,6 +427,111 @@ __global__ __launch_bounds__(256) void rope_kv_write_kernel(const uint16_t* __re
     const int kh = w / Dh, d = w % Dh;
     vc[(((size_t)blk * Hkv + kh) * Dh + d) * BS + off] = vsrc[w];
   }
+}
+
+// Same, straight from the split-K fp32 slabs of the QKV projection (ws [S][T][N], N = (H + 2*Hkv)*Dh):
+// sum the slabs (+ bias), round to bf16 exactly as the separate reduce would, rotate, write -- one
+// pass instead of reduce (write bf16 qkv) + rope (read it back), and one launch less per layer.
+// Grid (T, item blocks): one thread per work item (a rotated 4+4 pair of q / k, or 4 values of v), the
+// slab loads of an item issued together (SS > 0: exactly SS slabs), so a decode step of one token is
+// a single round trip, not S dependent ones.
+template <int SS>
+__device__ __forceinline__ f32x4 slab_sum4(const float* __restrict__ ws, int S, size_t sstride,
+                                           const uint16_t* __restrict__ bias, int col) {
+  f32x4 a;
+  if constexpr (SS > 0) {
+    f32x4 p[SS];
+#pragma unroll
+    for (int k = 0; k < SS; ++k) p[k] = *reinterpret_cast<const f32x4*>(ws + k * sstride + col);
+    a = p[0];
+#pragma unroll
+    for (int k = 1; k < SS; ++k) a += p[k];
+  } else {
+    a = *reinterpret_cast<const f32x4*>(ws + col);
+    for (int k = 1; k < S; ++k) a += *reinterpret_cast<const f32x4*>(ws + k * sstride + col);
+  }
+  if (bias != nullptr) {
+    const s16x4 b = *reinterpret_cast<const s16x4*>(bias + col);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) a[j] += bf2f(b[j]);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) a[j] = bf2f(f2bf(a[j]));
+  return a;
+}
+
+template <int SS>
+__global__ __launch_bounds__(256) void splitk_rope_kv_write_kernel(
+    const float* __restrict__ ws, int S, long sstride, const uint16_t* __restrict__ bias,
+    const int32_t* __restrict__ pos, const float* __restrict__ cos_sin, const int64_t* __restrict__ slots,
+    uint16_t* __restrict__ q_out, uint16_t* __restrict__ kc, uint16_t* __restrict__ vc, int H, int Hkv, int Dh, int BS,
+    int max_pos, long nslots) {
+  const int t = blockIdx.x;
+  const int w = blockIdx.y * 256 + threadIdx.x;
+  const int half = Dh >> 1, qpr = half >> 2;
+  const int N = (H + 2 * Hkv) * Dh;
+  const int nrot = (H + Hkv) * qpr, nv4 = Hkv * Dh / 4;
+  if (w >= nrot + nv4) return;
+  const float* row = ws + (size_t)t * N;
+  const int64_t slot = slots[t] < nslots ? slots[t] : -1;
+  const long blk = slot >= 0 ? slot / BS : 0;
+  const int off = slot >= 0 ? (int)(slot % BS) : 0;
+  if (w < nrot) {
+    const int h = w / qpr, i = (w % qpr) * 4;
+    uint16_t* dst;
+    if (h < H) {
+      dst = q_out + ((size_t)t * H + h) * Dh;
+    } else if (slot >= 0) {
+      dst = kc + (((size_t)blk * Hkv + (h - H)) * BS + off) * Dh;
+    } else {
+      return;
+    }
+    int p = pos[t];
+    p = p < 0 ? 0 : (p >= max_pos ? max_pos - 1 : p);
+    const float* cs = cos_sin + (size_t)p * Dh;
+    const f32x4 a = slab_sum4<SS>(row, S, sstride, bias, h * Dh + i);
+    const f32x4 b = slab_sum4<SS>(row, S, sstride, bias, h * Dh + i + half);
+    const f32x4 c = *reinterpret_cast<const f32x4*>(cs + i);
+    const f32x4 sn = *reinterpret_cast<const f32x4*>(cs + half + i);
+    s16x4 oa, ob;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      oa[j] = (short)f2bf(a[j] * c[j] - b[j] * sn[j]);
+      ob[j] = (short)f2bf(b[j] * c[j] + a[j] * sn[j]);
+    }
+    *reinterpret_cast<s16x4*>(dst + i) = oa;
+    *reinterpret_cast<s16x4*>(dst + i + half) = ob;
+    return;
+  }
+  if (slot < 0) return;
+  const int e = 4 * (w - nrot), kh = e / Dh, d = e % Dh;
+  const f32x4 v = slab_sum4<SS>(row, S, sstride, bias, (H + Hkv) * Dh + e);
+  uint16_t* dst = vc + (((size_t)blk * Hkv + kh) * Dh + d) * BS + off;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) dst[(size_t)j * BS] = f2bf(v[j]);
+}
+
+void launch_splitk_rope_kv_write(const float* ws, int S, const uint16_t* bias, const int32_t* pos,
+                                 const float* cos_sin, const int64_t* slots, uint16_t* q_out, uint16_t* kc,
+                                 uint16_t* vc, int T, int H, int Hkv, int Dh, int BS, int max_pos, long nslots,
+                                 hipStream_t s) {
+  if (T <= 0) return;
+  const long sstride = (long)T * (H + 2 * Hkv) * Dh;
+  const int items = (H + Hkv) * (Dh / 8) + Hkv * Dh / 4;
+  const dim3 grid(T, (items + 255) / 256);
+#define XOT_SRK(SV)                                                                                            \
+  splitk_rope_kv_write_kernel<SV><<<grid, 256, 0, s>>>(ws, S, sstride, bias, pos, cos_sin, slots, q_out, kc, vc, H, \
+                                                       Hkv, Dh, BS, max_pos, nslots)
+  switch (S) {
+    case 1: XOT_SRK(1); break;
+    case 2: XOT_SRK(2); break;
+    case 3: XOT_SRK(3); break;
+    case 4: XOT_SRK(4); break;
+    case 6: XOT_SRK(6); break;
+    case 8: XOT_SRK(8); break;
+    default: XOT_SRK(0); break;
+  }
+#undef XOT_SRK
 }
 
 void launch_rope_kv_write(const uint16_t* qkv, const int32_t* pos, const float* cos_sin, const int64_t* slots,

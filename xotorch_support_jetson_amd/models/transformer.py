@@ -28,7 +28,7 @@ import torch
 from ..inference.shard import Shard
 from ..ops import kernels as K
 from ..ops._ext import require
-from ..ops.linear import layout_of, linear, linear_resid_norm
+from ..ops.linear import layout_of, linear, linear_resid_norm, linear_rope_kv
 from ..ops.rope import build_cos_sin
 from .config import ModelConfig
 from .weights import ShardWeights, expert
@@ -195,9 +195,9 @@ class ShardModel:
     xn, _ = K.rmsnorm(h, w.layers[self.layer_ids[0]].ln1, c.rms_norm_eps) if n else (None, None)
     for j, li in enumerate(self.layer_ids):
       lw = w.layers[li]
-      qkv = linear(xn, lw.qkv_w, bias=lw.qkv_b)
-      q = K.rope_kv_write(qkv, inp.positions, self.cos_sin, inp.slots, self.kv.k[j], self.kv.v[j], c.num_heads,
-                          c.num_kv_heads)
+      # QKV projection + RoPE + paged KV write (split-K slabs reduced inside the RoPE kernel)
+      q = linear_rope_kv(xn, lw.qkv_w, lw.qkv_b, inp.positions, self.cos_sin, inp.slots, self.kv.k[j], self.kv.v[j],
+                         c.num_heads, c.num_kv_heads)
       a = self._attention(q, j, inp).view(h.shape[0], c.num_heads * c.head_dim)
       # o_proj + residual + post-attention norm (one fused pass when the projection runs split-K)
       xn = linear_resid_norm(a, lw.o_w, h, lw.ln2, c.rms_norm_eps)

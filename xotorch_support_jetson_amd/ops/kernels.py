@@ -192,6 +192,10 @@ class DecodeWorkspace:
     self.units = worst  # max over batch of batch * nparts
     self.o = torch.empty(worst * H * Dh, dtype=torch.float32, device=device)
     self.ml = torch.empty(worst * H * 2, dtype=torch.float32, device=device)
+    # per-(sequence, KV head) arrival tickets: the last partition merges in-kernel (no reduce launch);
+    # zero at rest, reset by each last arriver (XOT_ATTN_TICKETS=0: separate reduce kernel)
+    self.tickets = (torch.zeros(max_batch * H, dtype=torch.int32, device=device)
+                    if os.environ.get("XOT_ATTN_TICKETS", "1") == "1" else None)
 
   def partition(self, batch: int, Hkv: int, width_pages: int):
     """(pages per partition, partitions, kernel) for this call."""
@@ -217,8 +221,9 @@ def attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale: float, ws: D
     ws = DecodeWorkspace(B, H, Dh, width * PAGE, q.device)
   ppp, nparts, algo = ws.partition(B, k_cache.shape[1], width)
   out = torch.empty_like(q) if out is None else out
+  tk = ws.tickets if ws.tickets is not None and ws.tickets.numel() >= B * k_cache.shape[1] else None
   require().attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, out, ws.o, ws.ml, ppp, nparts, float(scale),
-                        algo)
+                        algo, tk)
   return out
 
 

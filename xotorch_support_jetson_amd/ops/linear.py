@@ -383,3 +383,35 @@ def linear_resid_norm(x: torch.Tensor, w: torch.Tensor, h: torch.Tensor, ln_w: t
   linear(x, w, bias=bias, residual=h, epi="resid", out=h)
   return K.rmsnorm(h, ln_w, eps, out=out)[0]
 
+
+# XOT_FUSE_ROPE=0: keep the QKV split-K reduce and the RoPE / KV-cache write as separate kernels
+FUSE_ROPE = os.environ.get("XOT_FUSE_ROPE", "1") == "1"
+
+
+def linear_rope_kv(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None, pos: torch.Tensor,
+                   cos_sin: torch.Tensor, slots: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, H: int,
+                   Hkv: int) -> torch.Tensor:
+  """qkv = x @ w.T (+ bias); returns rope(q) [T, H, Dh] and writes rope(k), v into the paged caches.
+
+  When the QKV projection runs split-K on the pre-shuffled layout, its fp32 slabs go straight to one
+  kernel that sums them, rotates and writes q / the caches (no bf16 qkv round trip, one launch less)."""
+  if FUSE_ROPE and x.is_cuda and layout_of(w) == "stream":
+    if x.stride(1) != 1 or x.stride(0) % 8:
+      x = x.contiguous()
+    M, N = x.shape[0], w.shape[0]
+    cfg = policy.shuffled_cfg(x, w, bias, None, "none", x.dtype)
+    if cfg[0] in ("stream", "big") and cfg[2] > 1:
+      S = cfg[2]
+      ws = scratch.splitk(x.device, S * M * N)
+      y = torch.empty(M, N, dtype=x.dtype, device=x.device)  # shape carrier only: the slabs are not reduced
+      C = require()
+      if cfg[0] == "stream":
+        C.gemm_stream(x, w, y, None, None, ws, K.EPI["none"], cfg[1], S, True, None, False)
+      else:
+        C.gemm_big(x, w, y, None, None, ws, K.EPI["none"], cfg[1], S, False)
+      Dh = k_cache.shape[-1]
+      q = torch.empty(M, H, Dh, dtype=x.dtype, device=x.device)
+      C.splitk_rope_kv_write(ws, S, bias, pos, cos_sin, slots, q, k_cache, v_cache, int(H), int(Hkv))
+      return q
+  qkv = linear(x, w, bias=bias)
+  return K.rope_kv_write(qkv, pos, cos_sin, slots, k_cache, v_cache, H, Hkv)
