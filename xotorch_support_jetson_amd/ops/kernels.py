@@ -168,8 +168,10 @@ def choose_pages_per_part(batch: int, Hkv: int, max_ctx: int, algo: int | None =
       if batch * Hkv * -(-pages // ppp) >= 1024:
         return ppp
     return 4
-  # one wave per unit: >= 2048 waves in flight (8 per CU), partitions of >= 2 pages
-  nparts = max(1, min(max(pages // 2, 1), -(-2048 // max(batch * Hkv, 1))))
+  # one wave per unit: ~1024 waves (4 per CU), partitions of 2..32 pages (tools/bench_attn_small.py,
+  # profiles/bench_attn_small_r1.json: 2048 waves of shorter partitions lose to the extra merge work)
+  nparts = max(1, min(max(pages // 2, 1), -(-1024 // max(batch * Hkv, 1))))
+  nparts = max(nparts, -(-pages // 32))
   return -(-pages // nparts)
 
 
@@ -192,10 +194,12 @@ class DecodeWorkspace:
     self.units = worst  # max over batch of batch * nparts
     self.o = torch.empty(worst * H * Dh, dtype=torch.float32, device=device)
     self.ml = torch.empty(worst * H * 2, dtype=torch.float32, device=device)
-    # per-(sequence, KV head) arrival tickets: the last partition merges in-kernel (no reduce launch);
-    # zero at rest, reset by each last arriver (XOT_ATTN_TICKETS=0: separate reduce kernel)
+    # XOT_ATTN_TICKETS=1: per-(sequence, KV head) arrival tickets, the last partition merges in-kernel
+    # instead of a reduce launch.  Off by default: measured slower in every configuration
+    # (profiles/bench_attn_small_r1.json, "_t" vs "_r": one workgroup or wave merging all partitions
+    # serially, behind an agent-scope fence, costs more than the parallel reduce kernel's launch).
     self.tickets = (torch.zeros(max_batch * H, dtype=torch.int32, device=device)
-                    if os.environ.get("XOT_ATTN_TICKETS", "1") == "1" else None)
+                    if os.environ.get("XOT_ATTN_TICKETS", "0") == "1" else None)
 
   def partition(self, batch: int, Hkv: int, width_pages: int):
     """(pages per partition, partitions, kernel) for this call."""
