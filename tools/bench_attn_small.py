@@ -39,10 +39,31 @@ def graph_us(fn, reps=20):
   return best
 
 
+def pmc_run(B, ctx, H=64, Hkv=8, Dh=128):
+  dev = torch.device("cuda:0")
+  pages = -(-ctx // 64)
+  npool = B * pages + 4
+  kc = torch.randn(npool, Hkv, 64, Dh, device=dev).to(torch.bfloat16)
+  vc = torch.randn(npool, Hkv, Dh, 64, device=dev).to(torch.bfloat16)
+  bt = torch.randperm(npool, device=dev)[:B * pages].view(B, pages).to(torch.int32).contiguous()
+  cl = torch.full((B,), ctx, device=dev, dtype=torch.int32)
+  q = torch.randn(B, H, Dh, device=dev).to(torch.bfloat16)
+  out = torch.empty_like(q)
+  ws = K.DecodeWorkspace(B, H, Dh, pages * 64, dev)
+  for _ in range(20):
+    K.attn_decode(q, kc, vc, bt, cl, 1 / math.sqrt(Dh), ws, out)
+  torch.cuda.synchronize()
+  print("cfg", ws.partition(B, Hkv, pages), "KV bytes", 2 * B * Hkv * ctx * Dh * 2)
+
+
 def main():
   ap = argparse.ArgumentParser()
   ap.add_argument("--json", default=None)
+  ap.add_argument("--pmc", default=None, help="B,ctx: only the auto config, 20 direct calls (for rocprofv3 --pmc)")
   args = ap.parse_args()
+  if args.pmc:
+    B, ctx = (int(v) for v in args.pmc.split(","))
+    return pmc_run(B, ctx)
   dev = torch.device("cuda:0")
   H, Hkv, Dh = 64, 8, 128
   rows = []
