@@ -5,7 +5,7 @@
   torchrun --nproc-per-node N tools/bench_train.py --gpus N
 
 Each rank holds 32/N layers as a ShardTrainer (HIP RMSNorm/SiLU/RoPE/cross-entropy fwd+bwd kernels,
-fused AdamW on fp32 master weights, hipBLASLt GEMMs, SDPA attention); activations go forward and
+fused AdamW on fp32 master weights, hipBLASLt GEMMs, flash-style HIP attention fwd/bwd); activations go forward and
 gradients backward over RCCL p2p in a GPipe schedule (parallel/pipeline_train.py).  Synthetic token
 data, random-init weights of the exact architecture.  Prints one JSON line: trained tokens/s of the
 whole job (max step time over ranks), plus the loss curve.
