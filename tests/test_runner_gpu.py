@@ -58,3 +58,42 @@ def test_gpu_matches_cpu_reference(gpu):
     lg = gr.forward(["a", "b"], [1, 1], tok).cpu()
     assert ((lc - lg).norm() / lc.norm()).item() < 3e-2
     tok = lc.argmax(-1).int()
+
+
+def test_split_head_ring_matches_full_gpu(gpu):
+  """Two ring stages in one process (loopback transport) with the LM head split between the last and
+  the first stage: greedy tokens == the unsplit single-stage model (GPU kernels, decode graphs)."""
+  from xotorch_support_jetson_amd.parallel.comm import LoopbackTransport
+  from xotorch_support_jetson_amd.parallel.pipeline import MicroBatch, RingStage, run_decode_steps
+  name = "tiny-llama-d64"
+  c = preset(name)
+  L = c.num_layers
+  B, P, steps = 3, 12, 6
+  prompt = torch.randint(0, c.vocab_size, (B, P), generator=torch.Generator().manual_seed(5), dtype=torch.int32)
+
+  def mb():
+    return MicroBatch(["r0", "r1", "r2"], prompt=prompt, temps=torch.zeros(B, device=gpu))
+
+  LoopbackTransport._queues.clear()
+  full = RingStage(ShardRunner(c, Shard(name, 0, L - 1, L), gpu, max_batch=4, max_ctx=256), 0, 1,
+                   LoopbackTransport(0, 1))
+  ref_mb = mb()
+  first = full.prefill(ref_mb)
+  ref_mb.tokens.append(first.tolist())
+  run_decode_steps(full, [ref_mb], steps, first_tokens=[first], record=True)
+
+  s0 = RingStage(ShardRunner(c, Shard(name, 0, L // 2 - 1, L), gpu, max_batch=4, max_ctx=256), 0, 2,
+                 LoopbackTransport(0, 2), split_head=True)
+  s1 = RingStage(ShardRunner(c, Shard(name, L // 2, L - 1, L), gpu, max_batch=4, max_ctx=256), 1, 2,
+                 LoopbackTransport(1, 2), split_head=True)
+  assert s0.split and s1.split and s0.samples and not s1.samples
+  m = mb()
+  assert s0.prefill(m) is None
+  item = s1.prefill(m)
+  s1._send_item(item)
+  got = []
+  for _ in range(steps):
+    sampled, _ = s0.decode_tick(m)  # receives the hand-off, finishes the head, samples, runs its layers
+    got.append(sampled.tolist())
+    _, item = s1.decode_tick(m)  # its layers + half head + candidates -> hand-off to stage 0
+  assert got == ref_mb.tokens[:steps]
