@@ -2,7 +2,7 @@
 """BASELINE config 5: Llama-3-8B fine-tune pipeline-sharded across N peers (one per GPU).
 
   python tools/bench_train.py [--model llama-3-8b] [--seq 2048] [--mb 1] [--microbatches M]
-  torchrun --nproc-per-node N tools/bench_train.py --gpus N
+  torchrun --nproc-per-node N tools/bench_train.py --gpus N [--parallel pp|dp]
 
 Each rank holds 32/N layers as a ShardTrainer (HIP RMSNorm/SiLU/RoPE/cross-entropy fwd+bwd kernels,
 fused AdamW on fp32 master weights, hipBLASLt GEMMs, flash-style HIP attention fwd/bwd); activations go forward and
@@ -36,6 +36,9 @@ def main():
   ap.add_argument("--steps", type=int, default=4)
   ap.add_argument("--warmup", type=int, default=1)
   ap.add_argument("--lr", type=float, default=1e-5)
+  ap.add_argument("--parallel", choices=("pp", "dp"), default="pp",
+                  help="pp: layer pipeline (the reference's strategy); dp: full replica per GPU, bucketed "
+                       "all-reduce overlapped with backward (parallel/data_parallel.py)")
   args = ap.parse_args()
 
   import torch.distributed as dist
@@ -50,11 +53,18 @@ def main():
   if world != args.gpus:
     raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
   cfg = preset(args.model)
-  shard = equal_layer_shards(args.model, cfg.num_layers, world)[rank]
-  M = args.microbatches or max(8, 4 * world)
+  dp = args.parallel == "dp"
+  if dp:
+    from xotorch_support_jetson_amd.inference.shard import Shard
+    from xotorch_support_jetson_amd.parallel.data_parallel import DataParallelTrainer
+    shard = Shard(args.model, 0, cfg.num_layers - 1, cfg.num_layers)
+    M = args.microbatches or 8  # per rank
+  else:
+    shard = equal_layer_shards(args.model, cfg.num_layers, world)[rank]
+    M = args.microbatches or max(8, 4 * world)
   t0 = time.time()
   tr = ShardTrainer(random_weights(cfg, shard, dev, seed=0), dev, lr=args.lr, max_seq=args.seq)
-  pt = PipelineTrainer(tr, rank, world, P2PTransport(rank, world))
+  pt = DataParallelTrainer(tr, rank, world) if dp else PipelineTrainer(tr, rank, world, P2PTransport(rank, world))
   sync()
   print(f"[rank {rank}] layers {shard.start_layer}-{shard.end_layer} init {time.time() - t0:.1f}s", file=sys.stderr)
 
@@ -85,16 +95,19 @@ def main():
     e = torch.tensor([el], dtype=torch.float64, device=dev)
     dist.all_reduce(e, op=dist.ReduceOp.MAX)
     el = float(e)
-  tokens = args.steps * M * args.mb * args.seq
+  tokens = args.steps * M * args.mb * args.seq * (world if dp else 1)
   if rank == 0:
     print(json.dumps({
-      "metric": f"training tokens/sec (whole node) {args.model} pipeline-sharded across {world} MI355X",
+      "metric": (f"training tokens/sec (whole node) {args.model} data-parallel across {world} MI355X" if dp else
+                 f"training tokens/sec (whole node) {args.model} pipeline-sharded across {world} MI355X"),
       "value": round(tokens / el, 1), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
       "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 1), "higher_is_better": True,
       "scaling": "weak" if args.microbatches == 0 else "strong", "dtype": "bf16 (fp32 master + AdamW)",
       "data": "synthetic tokens, random-init weights", "losses": [round(l, 4) for l in losses],
       "config": {"model": args.model, "seq_len": args.seq, "micro_batch": args.mb, "micro_batches": M,
-                 "global_batch_tokens": M * args.mb * args.seq, "parallelism": f"pp{world} (GPipe, RCCL p2p)"},
+                 "global_batch_tokens": M * args.mb * args.seq * (world if dp else 1),
+                 "parallelism": (f"dp{world} (bucketed all-reduce overlapped with backward)" if dp else
+                                 f"pp{world} (GPipe, RCCL p2p)")},
     }), flush=True)
   if world > 1:
     dist.barrier()

@@ -159,11 +159,12 @@ class ShardTrainer:
       out.backward(grad_out.to(out.dtype).view_as(out))
     return loss, (leaf.grad if leaf is not None else None)
 
-  def apply(self, grad_norm_sq_reduce=None, norm_exclude=()) -> None:
+  def apply(self, grad_norm_sq_reduce=None, norm_exclude=(), grads: Optional[Dict[str, torch.Tensor]] = None) -> None:
     """One AdamW step on the accumulated grads.  `grad_norm_sq_reduce(t)` (e.g. an all-reduce over
     the pipeline stages) turns the local squared grad norm into the global one for clipping;
-    `norm_exclude` names parameters counted by another stage (a tied head copy)."""
-    self._optimizer_step(grad_norm_sq_reduce, norm_exclude)
+    `norm_exclude` names parameters counted by another stage (a tied head copy); `grads` overrides
+    the parameters' .grad (e.g. fp32 all-reduced buckets of data parallelism)."""
+    self._optimizer_step(grad_norm_sq_reduce, norm_exclude, grads)
 
   def step(self, request_id, example, target, length, train: bool = True, evaluate: bool = False,
            loss: str = "length_masked_ce"):
@@ -193,9 +194,10 @@ class ShardTrainer:
     grad_in = x.grad.detach().cpu() if need_in_grad and x.grad is not None else None
     return loss_out, grad_in
 
-  def _optimizer_step(self, grad_norm_sq_reduce=None, norm_exclude=()):
+  def _optimizer_step(self, grad_norm_sq_reduce=None, norm_exclude=(), grads=None):
     self.step_count += 1
-    grads = {k: p.grad for k, p in self.params.items() if p.grad is not None}
+    if grads is None:
+      grads = {k: p.grad for k, p in self.params.items() if p.grad is not None}
     counted = [g for k, g in grads.items() if k not in norm_exclude]
     sq = sum((g.float() ** 2).sum() for g in counted) if counted else torch.zeros((), device=self.device)
     if grad_norm_sq_reduce is not None:
