@@ -40,6 +40,28 @@ def test_ring_train_eval_resume(tmp_path):
   assert "resumed tiny-llama from iteration 2" in ev and "eval | loss=" in ev
 
 
+def test_ring_train_data_parallel(tmp_path):
+  """`--parallel dp`: two full replicas, every other micro-batch each, gradients all-reduced; rank 0
+  writes one full-model checkpoint that a data-parallel eval resumes from."""
+  ds = tmp_path / "ds"
+  ds.mkdir()
+  for split, n in (("train", 12), ("valid", 4), ("test", 4)):
+    with open(ds / f"{split}.jsonl", "w") as f:
+      for i in range(n):
+        f.write(json.dumps({"text": f"Q: select a from t{i}? A: SELECT a FROM t{i}"}) + "\n")
+  ck = tmp_path / "ck"
+  out = _xot(["train", "tiny-llama", "--ring", "--gpus", "2", "--parallel", "dp", "--iters", "2", "--batch-size", "4",
+              "--micro-batch", "1", "--save-every", "2", "--save-checkpoint-dir", str(ck), "--data", str(ds),
+              "--lr", "1e-3"], tmp_path)
+  losses = [float(l.split("loss:")[1].split(",")[0]) for l in out.splitlines() if l.startswith("epoch")]
+  assert len(losses) == 2 and losses[1] < losses[0]
+  files = sorted(p.name for p in (ck / "tiny-llama").iterdir())
+  assert files == ["000-003-of-004-000002.optim.safetensors", "000-003-of-004-000002.safetensors"]
+  ev = _xot(["eval", "tiny-llama", "--ring", "--gpus", "2", "--parallel", "dp", "--batch-size", "4", "--data",
+             str(ds), "--resume-checkpoint", str(ck)], tmp_path)
+  assert "resumed tiny-llama from iteration 2" in ev and "eval | loss=" in ev
+
+
 @pytest.mark.gpu
 def test_ring_train_gpu_single(gpu, tmp_path):
   """The same CLI on one MI355X (world 1: the HIP training kernels + fused AdamW)."""

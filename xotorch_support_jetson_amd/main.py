@@ -72,6 +72,8 @@ def build_parser() -> argparse.ArgumentParser:
   p.add_argument("--ring", action="store_true",
                  help="train/eval: run the pipeline stages on the local GPUs over RCCL (no gRPC hops)")
   p.add_argument("--micro-batch", type=int, default=1, help="--ring: sequences per pipeline micro-batch")
+  p.add_argument("--parallel", choices=("pp", "dp"), default="pp",
+                 help="--ring: pp = layer pipeline over the GPUs; dp = a full replica per GPU, gradients all-reduced")
   p.add_argument("--no-api", action="store_true", help="Do not start the ChatGPT API on this peer")
   return p
 

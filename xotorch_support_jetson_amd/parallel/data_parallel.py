@@ -127,8 +127,8 @@ class DataParallelTrainer:
       if b.work is not None:
         b.work.wait()
     tr.apply(grads={n: b.views[n] for b in self.buckets for n in b.names})
-    loss = torch.stack(losses).sum().reshape(1).float()
+    loss = torch.stack(losses).sum().reshape(1).float() if losses else torch.zeros(1, device=self.dev)
     if self.world > 1:
-      loss = loss.to(self.dev) if dist.get_backend(self.group) == "nccl" else loss
+      loss = loss.to(self.dev) if dist.get_backend(self.group) == "nccl" else loss.cpu()
       dist.all_reduce(loss, group=self.group)
     return float(loss)

@@ -1,5 +1,6 @@
-"""`xot train|eval <model> --gpus N --ring`: training / evaluation with the pipeline shards on the local
-GPUs talking RCCL over xGMI (parallel/pipeline_train.py) instead of gRPC SendExample hops.
+"""`xot train|eval <model> --gpus N --ring [--parallel pp|dp]`: training / evaluation on the local GPUs
+over RCCL / xGMI instead of gRPC SendExample hops: the layer pipeline (parallel/pipeline_train.py) or
+data-parallel replicas (parallel/data_parallel.py; each rank takes every world-th micro-batch).
 
 Same data (`--data` JSONL dir, `batch_with_lengths`), same checkpoint files as the Node path
 (`train/checkpoint.py` names, HF tensor names, optimizer sidecars) so a ring-trained checkpoint
@@ -50,7 +51,12 @@ def _worker(rank: int, world: int, port: int, a: dict) -> None:
   model = a["model"]
   mdir = _model_dir(model)
   cfg = load_config(mdir) if mdir is not None else preset(model)
-  shard = equal_layer_shards(model, cfg.num_layers, world)[rank]
+  dp = a.get("parallel") == "dp"
+  if dp:
+    from ..inference.shard import Shard
+    shard = Shard(model, 0, cfg.num_layers - 1, cfg.num_layers)
+  else:
+    shard = equal_layer_shards(model, cfg.num_layers, world)[rank]
   if mdir is not None and any(mdir.glob("*.safetensors")):
     w = load_hf_weights(mdir, cfg, shard, dev)
   else:
@@ -73,7 +79,11 @@ def _worker(rank: int, world: int, port: int, a: dict) -> None:
       if side.exists():
         from safetensors.torch import load_file
         tr.load_state_dict({k: v.to(dev) for k, v in load_file(str(side)).items()})
-  pt = PipelineTrainer(tr, rank, world, P2PTransport(rank, world))
+  if dp:
+    from ..parallel.data_parallel import DataParallelTrainer
+    pt = DataParallelTrainer(tr, rank, world)
+  else:
+    pt = PipelineTrainer(tr, rank, world, P2PTransport(rank, world))
   tok = _resolve_tokenizer(mdir if mdir is not None else (registry.get_repo(model, "ShardedInferenceEngine") or "byte"),
                            cfg.vocab_size)
   train, valid, test = load_dataset(a["data"] or DEFAULT_DATA, lambda s: tok.encode(s))
@@ -85,7 +95,7 @@ def _worker(rank: int, world: int, port: int, a: dict) -> None:
     for i in range(0, x.shape[0], mb):
       out.append(TrainBatch(torch.from_numpy(x[i:i + mb]), torch.from_numpy(y[i:i + mb]),
                             torch.from_numpy(ln[i:i + mb])))
-    return out
+    return out[rank::world] if dp else out  # data parallel: every world-th micro-batch
 
   class _Shim:  # save_shard_checkpoint wants engine.runner.weights / engine.trainer
     pass
@@ -94,7 +104,7 @@ def _worker(rank: int, world: int, port: int, a: dict) -> None:
     tot, n = 0.0, 0
     for batch in iterate_batches(test, bs):
       micro = to_micro(batch)
-      loss = _eval(pt, micro)
+      loss = _eval_dp(pt, micro) if dp else _eval(pt, micro)
       tot += loss * float(batch[2].sum())
       n += int(batch[2].sum())
     if rank == 0:
@@ -110,7 +120,7 @@ def _worker(rank: int, world: int, port: int, a: dict) -> None:
         step += 1
       if rank == 0:
         print(f"epoch {epoch + 1}/{a['iters']}\t| loss: {tot / max(n, 1):.4f}, tokens: {n}", flush=True)
-      if a["save_every"] > 0 and (epoch + 1) % a["save_every"] == 0 and a["save_dir"]:
+      if a["save_every"] > 0 and (epoch + 1) % a["save_every"] == 0 and a["save_dir"] and (rank == 0 or not dp):
         tr.sync_to_inference()
         shim = _Shim()
         shim.runner = type("R", (), {"weights": w})()
@@ -149,6 +159,23 @@ def _eval(pt, micro) -> float:
   return float(total)
 
 
+@torch.no_grad()
+def _eval_dp(pt, micro) -> float:
+  """Data-parallel evaluation: each rank its micro-batches, token-weighted losses summed over ranks."""
+  import torch.distributed as dist
+  tr = pt.tr
+  denom = pt._global_tokens(micro)
+  total = torch.zeros(1, device=pt.dev)
+  for b in micro:
+    out = tr.forward(b.x.to(pt.dev))
+    loss, _ = tr.loss_of(out, b.y, b.lengths, denom)
+    total += loss.float()
+  if pt.world > 1:
+    total = total if dist.get_backend() == "nccl" else total.cpu()
+    dist.all_reduce(total)
+  return float(total)
+
+
 def run_ring(args) -> int:
   """Spawn one training process per GPU (torch.multiprocessing, RCCL process group)."""
   import torch.multiprocessing as mp
@@ -156,7 +183,7 @@ def run_ring(args) -> int:
   a = {"model": args.model_name or args.default_model, "command": args.command, "data": args.data,
        "batch_size": args.batch_size, "micro_batch": getattr(args, "micro_batch", 1), "iters": args.iters,
        "save_every": args.save_every, "save_dir": args.save_checkpoint_dir, "resume": args.resume_checkpoint,
-       "lr": args.lr}
+       "lr": args.lr, "parallel": getattr(args, "parallel", "pp")}
   if not a["model"]:
     print("Error: model name is required")
     return 1
