@@ -97,3 +97,34 @@ def test_split_head_ring_matches_full_gpu(gpu):
     got.append(sampled.tolist())
     _, item = s1.decode_tick(m)  # its layers + half head + candidates -> hand-off to stage 0
   assert got == ref_mb.tokens[:steps]
+
+
+def test_fused_grad_accumulation_matches_autograd(gpu):
+  """Projection weights accumulating dW inside the backward GEMM (A.LinearFn, beta = 1 after the first
+  micro-batch) take the same optimizer step as plain autograd accumulation into .grad."""
+  from xotorch_support_jetson_amd.parallel.comm import LoopbackTransport
+  from xotorch_support_jetson_amd.parallel.pipeline_train import PipelineTrainer, TrainBatch
+  from xotorch_support_jetson_amd.train.trainer import ShardTrainer
+  name = "tiny-llama-d64"
+  c = preset(name)
+  sh = Shard(name, 0, c.num_layers - 1, c.num_layers)
+  g = torch.Generator().manual_seed(9)
+  batches = []
+  for _ in range(3):
+    x = torch.randint(0, c.vocab_size, (2, 64), generator=g)
+    batches.append(TrainBatch(x, torch.roll(x, -1, 1), torch.tensor([64, 50])))
+  res = []
+  for fused in (True, False):
+    tr = ShardTrainer(random_weights(c, sh, gpu, seed=4), gpu, lr=1e-3, max_seq=256)
+    assert len(tr.acc) == 4 * c.num_layers
+    if not fused:
+      tr.acc = {}
+    pt = PipelineTrainer(tr, 0, 1, LoopbackTransport(0, 1))
+    init = {k: v.clone() for k, v in tr.master.items()}
+    losses = [pt.step(batches) for _ in range(2)]
+    res.append((losses, {k: tr.master[k] - init[k] for k in init}))
+  (lf, df), (lr, dr) = res
+  assert all(abs(a - b) < 2e-3 * max(1.0, abs(b)) for a, b in zip(lf, lr)), (lf, lr)
+  for k in dr:
+    rel = ((df[k] - dr[k]).abs().mean() / (dr[k].abs().mean() + 1e-12)).item()
+    assert rel < 0.05, (k, rel)

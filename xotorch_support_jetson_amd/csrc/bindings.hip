@@ -62,7 +62,10 @@ void rmsnorm_bwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& dy,
   XCHECK(D % 8 == 0 && D <= 16384, "rmsnorm_bwd: bad D");
   XCHECK(dy.numel() == x.numel() && dx.numel() == x.numel() && dw.numel() == D && w.numel() == D,
          "rmsnorm_bwd: shape mismatch");
-  xot::launch_rmsnorm_bwd(bf(x), bf(w), bf(dy), bf(dx), dw.data_ptr<float>(), (int)rows, (int)D, (float)eps,
+  const int64_t nblk = (rows + xot::rmsnorm_bwd_part_rows() - 1) / xot::rmsnorm_bwd_part_rows();
+  auto part = at::empty({nblk * D}, x.options().dtype(at::kFloat));  // per-block dw partials
+  xot::launch_rmsnorm_bwd(bf(x), bf(w), bf(dy), bf(dx), dw.data_ptr<float>(), part.data_ptr<float>(), (int)rows,
+                          (int)D, (float)eps,
                           cur_stream());
 }
 

@@ -9,8 +9,9 @@ namespace xot {
 
 void launch_rmsnorm(const uint16_t* x, const uint16_t* res, const uint16_t* w, uint16_t* out, uint16_t* res_out,
                     int rows, int D, float eps, hipStream_t s);
-void launch_rmsnorm_bwd(const uint16_t* x, const uint16_t* w, const uint16_t* dy, uint16_t* dx, float* dw, int rows,
-                        int D, float eps, hipStream_t s);
+void launch_rmsnorm_bwd(const uint16_t* x, const uint16_t* w, const uint16_t* dy, uint16_t* dx, float* dw,
+                        float* dw_part, int rows, int D, float eps, hipStream_t s);
+int rmsnorm_bwd_part_rows();
 void launch_embedding(const int32_t* ids, const uint16_t* table, uint16_t* out, int T, int D, int vocab,
                       hipStream_t s);
 void launch_silu_mul(const uint16_t* gu, uint16_t* out, int T, int F, hipStream_t s);

@@ -8,8 +8,9 @@ model on its own micro-batches and the only traffic is one all-reduce of the gra
 
 Schedule of one optimizer step (each rank its own micro-batches, loss normalised by the GLOBAL target
 token count so the summed gradients equal one big batch's):
-  forward + backward of micro-batches 0..M-2       gradients accumulate in the bf16 .grad leaves
-  backward of the last micro-batch                 post-accumulate-grad hooks copy each finished
+  forward + backward of micro-batches 0..M-2       gradients accumulate in bf16 (projections inside
+                                                   their backward GEMM, the rest in .grad)
+  backward of the last micro-batch                 accumulation hooks copy each finished
                                                    gradient into its fp32 bucket; a full bucket starts
                                                    an async all-reduce (RCCL's stream) while autograd
                                                    keeps computing the earlier layers' gradients
@@ -70,18 +71,32 @@ class DataParallelTrainer:
         cur.append(n)
         size += numel
     self._armed = False
-    self._hooks = [p.register_post_accumulate_grad_hook(self._hook(n)) for n, p in trainer.params.items()]
+    # autograd-accumulated parameters signal through post-accumulate-grad hooks, projections with fused
+    # accumulation (trainer.acc, A.LinearFn) through their GradAcc callback
+    self._hooks = [p.register_post_accumulate_grad_hook(self._hook(n)) for n, p in trainer.params.items()
+                   if n not in trainer.acc]
+    for n, a in trainer.acc.items():
+      a.cb = self._acc_cb(n)
+
+  def _ready(self, name: str, g: torch.Tensor) -> None:
+    b = self.buckets[self.bucket_of[name]]
+    b.views[name].copy_(g)
+    b.done.add(name)
+    if len(b.done) == len(b.names):
+      self._launch(b)
 
   def _hook(self, name: str):
     def fn(p: torch.Tensor):
       if not self._armed or p.grad is None:
         return
-      b = self.buckets[self.bucket_of[name]]
-      b.views[name].copy_(p.grad)
+      self._ready(name, p.grad)
       p.grad = None
-      b.done.add(name)
-      if len(b.done) == len(b.names):
-        self._launch(b)
+    return fn
+
+  def _acc_cb(self, name: str):
+    def fn():
+      if self._armed:
+        self._ready(name, self.tr.acc[name].buf)
     return fn
 
   def _launch(self, b: _Bucket) -> None:
@@ -115,8 +130,10 @@ class DataParallelTrainer:
         for n in b.names:
           if n in b.done:
             continue
-          p = tr.params[n]
-          if p.grad is not None:
+          p, a = tr.params[n], tr.acc.get(n)
+          if a is not None and not a.fresh:
+            b.views[n].copy_(a.buf)
+          elif p.grad is not None:
             b.views[n].copy_(p.grad)
             p.grad = None
           else:

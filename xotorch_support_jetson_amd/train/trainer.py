@@ -67,6 +67,12 @@ class ShardTrainer:
       self._add("norm", weights.norm)
       if not self.c.tie_word_embeddings or "embed" not in self.params:
         self._add("lm_head", _rowmajor(weights.lm_head))
+    # projection weights accumulate their gradients inside the backward GEMM (A.LinearFn) on the GPU
+    self.acc: Dict[str, A.GradAcc] = {}
+    if self.device.type == "cuda":
+      for k in self.params:
+        if k.split(".")[-1] in ("qkv", "o", "gu", "down"):
+          self.acc[k] = A.GradAcc(k, self.params[k])
     self.master = {k: p.detach().float().clone() for k, p in self.params.items()}
     self.m = {k: torch.zeros_like(v) for k, v in self.master.items()}
     self.v = {k: torch.zeros_like(v) for k, v in self.master.items()}
@@ -89,21 +95,37 @@ class ShardTrainer:
     h = h.reshape(B * L, D)
     for i in self.shard.layers():
       xn = A.rmsnorm(h, P[f"{i}.ln1"], c.rms_norm_eps)
-      qkv = xn @ P[f"{i}.qkv"].t()
+      qkv = self._mm(xn, f"{i}.qkv")
       if f"{i}.qkv_b" in P:
         qkv = qkv + P[f"{i}.qkv_b"]
       q = A.rope(qkv[:, :H * Dh].contiguous(), pos, self.cos_sin, H, Dh)
       k = A.rope(qkv[:, H * Dh:(H + Hkv) * Dh].contiguous(), pos, self.cos_sin, Hkv, Dh)
       v = qkv[:, (H + Hkv) * Dh:]
       a = A.attention(q, k, v, B, L, H, Hkv, Dh)  # flash-style HIP kernels (fwd + dQ + dK/dV)
-      h = _resid_mm(h, a, P[f"{i}.o"])
+      h = self._mm(a, f"{i}.o", h)
       xn = A.rmsnorm(h, P[f"{i}.ln2"], c.rms_norm_eps)
-      h = _resid_mm(h, A.silu_mul((xn @ P[f"{i}.gu"].t()).contiguous()), P[f"{i}.down"])
+      h = self._mm(A.silu_mul(self._mm(xn, f"{i}.gu").contiguous()), f"{i}.down", h)
     if not self.shard.is_last_layer():
       return h.view(B, L, D)
     xn = A.rmsnorm(h, P["norm"], c.rms_norm_eps)
     head = P["lm_head"] if "lm_head" in P else P["embed"]
     return (xn @ head.t()).view(B, L, -1)
+
+  def _mm(self, x: torch.Tensor, name: str, h: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """x @ W.T (+ h) for projection `name`: fused gradient accumulation on the GPU while training."""
+    w = self.params[name]
+    acc = self.acc.get(name)
+    if acc is not None and torch.is_grad_enabled():
+      return A.linear_acc(x, w, acc, h)
+    return _resid_mm(h, x, w) if h is not None else x @ w.t()
+
+  def grads(self) -> Dict[str, torch.Tensor]:
+    """The accumulated gradients of this step: fused buffers and .grad of the other parameters."""
+    out = {k: a.buf for k, a in self.acc.items() if not a.fresh}
+    for k, p in self.params.items():
+      if k not in out and p.grad is not None:
+        out[k] = p.grad
+    return out
 
   # ------------------------------------------------------------------ steps
   def _to(self, a, dtype=None):
@@ -136,6 +158,8 @@ class ShardTrainer:
   def zero_grad(self) -> None:
     for p in self.params.values():
       p.grad = None
+    for a in self.acc.values():
+      a.fresh = True
 
   def forward_train(self, x) -> Tuple[Optional[torch.Tensor], torch.Tensor]:
     """Forward with autograd: returns (input leaf or None for token ids, output)."""
@@ -179,8 +203,7 @@ class ShardTrainer:
           l, _ = self.loss_of(out, target, length)
           return float(l)
         return 0.0
-    for p in self.params.values():
-      p.grad = None
+    self.zero_grad()
     out = self.forward(x)
     if self.shard.is_last_layer() and loss != "back_gradient":
       lval, _ = self.loss_of(out, target, length)
@@ -197,9 +220,11 @@ class ShardTrainer:
   def _optimizer_step(self, grad_norm_sq_reduce=None, norm_exclude=(), grads=None):
     self.step_count += 1
     if grads is None:
-      grads = {k: p.grad for k, p in self.params.items() if p.grad is not None}
+      grads = self.grads()
     counted = [g for k, g in grads.items() if k not in norm_exclude]
-    sq = sum((g.float() ** 2).sum() for g in counted) if counted else torch.zeros((), device=self.device)
+    # one fp32-accumulating norm kernel per tensor (no fp32 copies of the bf16 gradients)
+    sq = (torch.stack([torch.linalg.vector_norm(g, dtype=torch.float32) for g in counted]).square().sum()
+          if counted else torch.zeros((), device=self.device))
     if grad_norm_sq_reduce is not None:
       sq = grad_norm_sq_reduce(sq.reshape(1).float()).reshape(())
     gnorm = torch.sqrt(sq)
