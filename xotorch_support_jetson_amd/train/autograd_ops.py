@@ -251,3 +251,24 @@ class LinearFn(torch.autograd.Function):
 
 def linear_acc(x, w, acc, h=None):
   return LinearFn.apply(x, w, h, acc)
+
+
+class QKVSplitFn(torch.autograd.Function):
+  """Fused-QKV projection output [T, (H + 2 Hkv) Dh] -> q, k (contiguous copies) and v (a row-strided view).
+  The backward concatenates dq | dk | dv once; autograd's slice backwards would zero-fill three full-size
+  gradients, copy each slice in and add them (3 fills + 3 copies + 2 adds per layer and micro-batch)."""
+
+  @staticmethod
+  def forward(ctx, qkv, nq, nk):
+    ctx.widths = (nq, nk, qkv.shape[1] - nq - nk)
+    return qkv[:, :nq].contiguous(), qkv[:, nq:nq + nk].contiguous(), qkv[:, nq + nk:]
+
+  @staticmethod
+  def backward(ctx, dq, dk, dv):
+    ref = next(g for g in (dq, dk, dv) if g is not None)
+    parts = [g if g is not None else ref.new_zeros(ref.shape[0], w) for g, w in zip((dq, dk, dv), ctx.widths)]
+    return torch.cat(parts, dim=1), None, None
+
+
+def qkv_split(qkv, nq, nk):
+  return QKVSplitFn.apply(qkv, nq, nk)
