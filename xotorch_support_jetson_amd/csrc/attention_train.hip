@@ -41,14 +41,15 @@ __device__ __forceinline__ void wave_sync_lds() {
 // (in flight under the current tile's math), store() writes them to LDS after the barrier.
 //   rows tile:  [64 tokens][DH] of a token-major source (ld elements per token), tokens clamped to L-1
 //   trans tile: [DH][64 tokens] of a pre-transposed [.., DH, Lp] image (zero past L)
-template <int DH>
+template <int DH, int NT = 256>
 struct RowsTile {
-  static constexpr int N = TT * DH / 8 / 256;  // chunks per thread
+  static constexpr int N = TT * DH / 8 / NT;  // chunks per thread
+  static_assert(N >= 1 && TT * DH / 8 % NT == 0, "tile / thread count");
   s16x8 v[N];
   __device__ __forceinline__ void load(const uint16_t* __restrict__ src, long ld, int row0, int L) {
 #pragma unroll
     for (int i = 0; i < N; ++i) {
-      const int q = threadIdx.x + 256 * i, r = q / (DH / 8), cc = q % (DH / 8);
+      const int q = threadIdx.x + NT * i, r = q / (DH / 8), cc = q % (DH / 8);
       v[i] = ld16(src + (long)min(row0 + r, L - 1) * ld + cc * 8);
     }
   }
@@ -56,19 +57,20 @@ struct RowsTile {
   __device__ __forceinline__ void store(uint16_t* dst) const {
 #pragma unroll
     for (int i = 0; i < N; ++i) {
-      const int q = threadIdx.x + 256 * i, r = q / (DH / 8), cc = q % (DH / 8);
+      const int q = threadIdx.x + NT * i, r = q / (DH / 8), cc = q % (DH / 8);
       st16(dst + r * RLD + cc * 8, v[i]);
     }
   }
 };
-template <int DH>
+template <int DH, int NT = 256>
 struct TransTile {
-  static constexpr int N = DH * TT / 8 / 256;
+  static constexpr int N = DH * TT / 8 / NT;
+  static_assert(N >= 1 && DH * TT / 8 % NT == 0, "tile / thread count");
   s16x8 v[N];
   __device__ __forceinline__ void load(const uint16_t* __restrict__ srcT, int Lp, int tok0) {
 #pragma unroll
     for (int i = 0; i < N; ++i) {
-      const int q = threadIdx.x + 256 * i, d = q / (TT / 8), cc = q % (TT / 8);
+      const int q = threadIdx.x + NT * i, d = q / (TT / 8), cc = q % (TT / 8);
       v[i] = ld16(srcT + (long)d * Lp + tok0 + cc * 8);
     }
   }
@@ -76,7 +78,7 @@ struct TransTile {
   __device__ __forceinline__ void store(uint16_t* dst) const {
 #pragma unroll
     for (int i = 0; i < N; ++i) {
-      const int q = threadIdx.x + 256 * i, d = q / (TT / 8), cc = q % (TT / 8);
+      const int q = threadIdx.x + NT * i, d = q / (TT / 8), cc = q % (TT / 8);
       st16(dst + d * TLD + cc * 8, v[i]);
     }
   }
@@ -312,8 +314,11 @@ __global__ __launch_bounds__(256) void attn_train_dq_kernel(const uint16_t* __re
 }
 
 // ---------------------------------------------------------------------------------------- dK, dV
+// DKW = 8 waves: 128 keys per workgroup share each staged query tile (2 waves per SIMD, so one wave's
+// LDS reads and exp2 hide under the other's MFMAs; with 4 waves the LDS footprint left one wave per SIMD)
+constexpr int DKW = 8, DKT = 16 * DKW;
 template <int DH>
-__global__ __launch_bounds__(256) void attn_train_dkdv_kernel(const uint16_t* __restrict__ Q, long ldq,
+__global__ __launch_bounds__(64 * DKW) void attn_train_dkdv_kernel(const uint16_t* __restrict__ Q, long ldq,
                                                               const uint16_t* __restrict__ QT,
                                                               const uint16_t* __restrict__ K, long ldk,
                                                               const uint16_t* __restrict__ V, long ldv,
@@ -330,22 +335,23 @@ __global__ __launch_bounds__(256) void attn_train_dkdv_kernel(const uint16_t* __
   uint16_t* ds_ = qs + TT * RLD;     // dO rows      [64][RLD]
   uint16_t* qt_ = ds_ + TT * RLD;    // Q^T          [DH][TLD]
   uint16_t* dt_ = qt_ + DH * TLD;    // dO^T         [DH][TLD]
-  uint16_t* pt = dt_ + DH * TLD;     // P^T / dS^T   [4 waves][2][16][PLD]
-  float* ld_ = reinterpret_cast<float*>(pt + 4 * 2 * 16 * PLD);  // lse2[64], delta[64]
+  uint16_t* pt = dt_ + DH * TLD;     // P^T / dS^T   [DKW waves][2][16][PLD]
+  float* ld_ = reinterpret_cast<float*>(pt + DKW * 2 * 16 * PLD);  // lse2[64], delta[64]
   // one workgroup per (query head of the group, key tile, batch); key tiles are the slowest grid
   // dimension with the heaviest (kt = 0: every query tile) first, so the causal imbalance load-balances
   const int G = H / Hkv;
   const int hq = blockIdx.x, kvh = hq / G, hh = hq % G, kt = blockIdx.y, b = blockIdx.z;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
-  const int k0 = kt * TT, krow = k0 + 16 * wave;
+  const int k0 = kt * DKT, krow = k0 + 16 * wave;
   const float sl = scale * L2E;
-  const int nq = (L + TT - 1) / TT, per_head = nq - kt, iters = per_head;
+  const int qt0 = k0 / TT;  // first query tile with a query >= a key of this workgroup
+  const int nq = (L + TT - 1) / TT, iters = nq - qt0;
 
-  RowsTile<DH> qr, dr;
-  TransTile<DH> qtr, dtr;
+  RowsTile<DH, 64 * DKW> qr, dr;
+  TransTile<DH, 64 * DKW> qtr, dtr;
   float lsv = 0.f, dlv = 0.f;
   auto load = [&](int it) {  // (head, query tile) of iteration it into registers
-    const int h = hq, q0 = (kt + it) * TT;
+    const int h = hq, q0 = (qt0 + it) * TT;
     qr.load(Q + (long)b * L * ldq + h * DH, ldq, q0, L);
     dr.load(dO + (long)b * L * lddo + h * DH, lddo, q0, L);
     qtr.load(QT + ((long)b * H + h) * DH * Lp, Lp, q0);
@@ -375,7 +381,7 @@ __global__ __launch_bounds__(256) void attn_train_dkdv_kernel(const uint16_t* __
 
   if (iters > 0) load(0);
   for (int it = 0; it < iters; ++it) {
-    const int q0 = (kt + it) * TT;
+    const int q0 = (qt0 + it) * TT;
     __syncthreads();
     qr.template store<RLD>(qs);
     dr.template store<RLD>(ds_);
@@ -481,7 +487,7 @@ __global__ __launch_bounds__(256) void attn_train_transpose_kernel(const uint16_
 
 template <int DH>
 static size_t dkdv_smem() {
-  return (size_t)(2 * TT * (DH + 8) + 2 * DH * (TT + 8) + 4 * 2 * 16 * (TT + 8)) * 2 + 2 * TT * sizeof(float);
+  return (size_t)(2 * TT * (DH + 8) + 2 * DH * (TT + 8) + DKW * 2 * 16 * (TT + 8)) * 2 + 2 * TT * sizeof(float);
 }
 
 int launch_attn_train_transpose(const uint16_t* x, long ldx, uint16_t* xt, int B, int L, int Lp, int n, int Dh,
@@ -523,7 +529,7 @@ int launch_attn_train_bwd(const uint16_t* q, long ldq, const uint16_t* qt, const
   const long slab = (long)B * L * Hkv * Dh;
   if (ws == nullptr || ws_elems < 2 * (long)(H / Hkv) * slab) return -1;
   float *wk = ws, *wv = ws + (long)(H / Hkv) * slab;
-  dim3 gq(H, (L + TT - 1) / TT, B), gk(H, (L + TT - 1) / TT, B);
+  dim3 gq(H, (L + TT - 1) / TT, B), gk(H, (L + DKT - 1) / DKT, B);
 #define XOT_BWD(DHV)                                                                                                \
   do {                                                                                                              \
     attn_train_dq_kernel<DHV><<<gq, 256, 0, s>>>(q, ldq, k, ldk, kt, v, ldv, o, ldo, dout, lddo, Lp, lse2, delta,   \
@@ -532,7 +538,7 @@ int launch_attn_train_bwd(const uint16_t* q, long ldq, const uint16_t* qt, const
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)dkdv_smem<DHV>()) ==    \
                        hipSuccess;                                                                                  \
     (void)attr;                                                                                                     \
-    attn_train_dkdv_kernel<DHV><<<gk, 256, dkdv_smem<DHV>(), s>>>(q, ldq, qt, k, ldk, v, ldv, dout, lddo, doutt, Lp, \
+    attn_train_dkdv_kernel<DHV><<<gk, 64 * DKW, dkdv_smem<DHV>(), s>>>(q, ldq, qt, k, ldk, v, ldv, dout, lddo, doutt, Lp, \
                                                                   lse2, delta, wk, wv, L, H, Hkv, scale);           \
   } while (0)
   if (Dh == 128)
