@@ -495,3 +495,15 @@ def test_attention_train_fwd_bwd(gpu, B, L, H, Hkv, Dh):
   assert rel_err(o, ref) < 2e-2
   for name, sl in (("dq", slice(0, H * Dh)), ("dk", slice(H * Dh, (H + Hkv) * Dh)), ("dv", slice((H + Hkv) * Dh, None))):
     assert rel_err(g[:, sl], x.grad[:, sl]) < 3e-2, name
+
+
+@pytest.mark.parametrize("T,E,D", [(1, 8, 4096), (37, 8, 4096), (512, 8, 1024), (5, 4, 256), (9, 16, 512)])
+def test_router_logits(gpu, T, E, D):
+  from xotorch_support_jetson_amd.ops._ext import require
+  torch.manual_seed(0)
+  x = torch.randn(T, D, device=gpu, dtype=torch.bfloat16)
+  w = (torch.randn(E, D, device=gpu) * 0.05).to(torch.bfloat16)
+  out = torch.empty(T, E, device=gpu, dtype=torch.float32)
+  require().router_logits(x, w, out)
+  ref = x.float() @ w.float().t()
+  assert rel_err(out, ref) < 1e-5

@@ -390,6 +390,17 @@ void gemm_moe(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const at:
   XCHECK(rc == 0, "gemm_moe: unsupported shape N=", N, " K=", K, " epi=", epi, " splits=", splits);
 }
 
+void router_logits(const at::Tensor& x, const at::Tensor& w, at::Tensor& out) {
+  CHECK_BF16(x);
+  CHECK_BF16(w);
+  CHECK_DT(out, at::kFloat);
+  XCHECK(all_contig_gpu(x, w, out) && x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "router_logits: 2-D contiguous");
+  const int64_t T = x.size(0), D = x.size(1), E = w.size(0);
+  XCHECK(w.size(1) == D && out.size(0) == T && out.size(1) == E, "router_logits: shape mismatch");
+  const int rc = xot::launch_router_logits(bf(x), bf(w), out.data_ptr<float>(), (int)T, (int)E, (int)D, cur_stream());
+  XCHECK(rc == 0, "router_logits: unsupported E=", E, " D=", D);
+}
+
 void moe_route(const at::Tensor& logits, int64_t k, at::Tensor& topw, at::Tensor& topi, at::Tensor& slot_of,
                at::Tensor& sorted_tok, at::Tensor& off) {
   CHECK_GPU(logits);
@@ -662,6 +673,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("ctx_lens"), py::arg("out"), py::arg("ws_o"), py::arg("ws_ml"), py::arg("pages_per_part"),
         py::arg("nparts"), py::arg("scale"), py::arg("algo") = 2, py::arg("tickets") = py::none());
   m.def("attn_prefill", &attn_prefill);
+  m.def("router_logits", &router_logits);
   m.def("splitk_rope_kv_write", &splitk_rope_kv_write);
   m.def("attn_train_transpose", &attn_train_transpose);
   m.def("attn_train_fwd", &attn_train_fwd);

@@ -112,6 +112,52 @@ __global__ __launch_bounds__(256) void moe_combine_kernel(const float* __restric
   }
 }
 
+// Router logits in fp32: out[t][e] = x[t] . W[e] (x [T, D] bf16, W [E, D] bf16), one 256-thread workgroup per
+// token; W (64 KB for Mixtral) stays in L2 across the workgroups.  Replaces a bf16-output library GEMM plus
+// an fp32 cast (two launches, bf16-rounded logits) in front of moe_route.
+template <int E>
+__global__ __launch_bounds__(256) void router_logits_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
+                                                            float* __restrict__ out, int D) {
+  __shared__ float red[4][E];
+  const int t = blockIdx.x, tid = threadIdx.x;
+  float acc[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) acc[e] = 0.f;
+  const uint16_t* xr = x + (size_t)t * D;
+  for (int c = tid; c < D / 8; c += 256) {
+    const s16x8 xv = ld16(xr + c * 8);
+    float xf[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) xf[j] = bf2f(xv[j]);
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const s16x8 wv = ld16(w + (size_t)e * D + c * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[e] += xf[j] * bf2f(wv[j]);
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    float v = acc[e];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if ((tid & 63) == 0) red[tid >> 6][e] = v;
+  }
+  __syncthreads();
+  if (tid < E) out[(size_t)t * E + tid] = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
+}
+
+int launch_router_logits(const uint16_t* x, const uint16_t* w, float* out, int T, int E, int D, hipStream_t s) {
+  if (T <= 0) return 0;
+  if (D % 8 != 0) return -1;
+  switch (E) {
+    case 8: router_logits_kernel<8><<<T, 256, 0, s>>>(x, w, out, D); return 0;
+    case 16: router_logits_kernel<16><<<T, 256, 0, s>>>(x, w, out, D); return 0;
+    case 4: router_logits_kernel<4><<<T, 256, 0, s>>>(x, w, out, D); return 0;
+    default: return -1;
+  }
+}
+
 void launch_moe_route(const float* logits, int T, int E, int k, float* topw, int32_t* topi, int32_t* slot_of,
                       int32_t* sorted_tok, int32_t* off, hipStream_t s) {
   moe_route_kernel<<<1, 1024, 0, s>>>(logits, T, E, k, topw, topi, slot_of, sorted_tok, off);

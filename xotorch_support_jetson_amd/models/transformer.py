@@ -120,7 +120,12 @@ class ShardModel:
     """Mixtral sparse MoE: softmax top-k routing, tokens grouped per expert, expert GEMMs on the
     kernel library (gate/up with fused SiLU epilogue), weighted scatter-add back into h."""
     c = self.c
-    logits = linear(xn, lw.router, out_dtype=torch.float32)  # [T, E]
+    if xn.is_cuda and c.num_experts in (4, 8, 16) and layout_of(lw.router) == "rowmajor":
+      # fp32 router logits, one small kernel (instead of a bf16 library GEMM + cast)
+      logits = torch.empty(xn.shape[0], c.num_experts, dtype=torch.float32, device=xn.device)
+      require().router_logits(xn.contiguous(), lw.router.contiguous(), logits)
+    else:
+      logits = linear(xn, lw.router, out_dtype=torch.float32)  # [T, E]
     if xn.is_cuda:
       return self._moe_gpu(xn, lw, h, logits)
     probs = torch.softmax(logits, dim=-1)
