@@ -461,6 +461,12 @@ def test_moe_layer(gpu, T, E, k, shuffled):
     out = h.clone()
     C.moe_combine(y, slot_of, topw, out, S)
     assert rel_err(out.float() - h.float(), ref - h.float()) < 3e-2, S  # the MoE contribution itself
+    # combine fused with the following RMSNorm: same residual stream, normed output == rmsnorm(stream)
+    lnw = torch.randn(D, device=gpu).to(torch.bfloat16)
+    h2, normed = h.clone(), torch.empty_like(h)
+    C.moe_combine_norm(y, slot_of, topw, h2, S, lnw, normed, 1e-5)
+    assert torch.equal(h2, out), S
+    assert rel_err(normed, R.rmsnorm(out, lnw, 1e-5)[0]) < 1e-2, S
   if shuffled:  # the same block on gemm_big tiles (128-, 192- and 256-row tiles per expert)
     for bm in (128, 192, 256):
       act2 = torch.empty_like(act)

@@ -433,6 +433,23 @@ void moe_combine(const at::Tensor& y, const at::Tensor& slot_of, const at::Tenso
                           (int)D, (int)splits, (long)(T * k * D), cur_stream());
 }
 
+void moe_combine_norm(const at::Tensor& y, const at::Tensor& slot_of, const at::Tensor& topw, at::Tensor& h,
+                      int64_t splits, const at::Tensor& ln_w, at::Tensor& out, double eps) {
+  CHECK_DT(y, at::kFloat);
+  CHECK_BF16(h);
+  CHECK_BF16(ln_w);
+  CHECK_BF16(out);
+  XCHECK(all_contig_gpu(y, slot_of, topw, h, ln_w, out), "moe_combine_norm: tensors must be contiguous GPU");
+  const int64_t T = h.size(0), D = h.size(1), k = slot_of.numel() / T;
+  XCHECK(splits >= 1 && D % 8 == 0 && y.size(1) == D && y.size(0) == splits * T * k && topw.numel() == T * k &&
+             ln_w.numel() == D && out.sizes() == h.sizes(),
+         "moe_combine_norm: shapes");
+  const int rc = xot::launch_moe_combine_norm(y.data_ptr<float>(), slot_of.data_ptr<int>(), topw.data_ptr<float>(),
+                                              bf(h), bf(ln_w), bf(out), (int)T, (int)k, (int)D, (int)splits,
+                                              (long)(T * k * D), (float)eps, cur_stream());
+  XCHECK(rc == 0, "moe_combine_norm: unsupported D=", D);
+}
+
 void attn_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
                  const at::Tensor& block_tables, const at::Tensor& ctx_lens, at::Tensor& out, at::Tensor& ws_o,
                  at::Tensor& ws_ml, int64_t pages_per_part, int64_t nparts, double scale, int64_t algo,
@@ -674,6 +691,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("nparts"), py::arg("scale"), py::arg("algo") = 2, py::arg("tickets") = py::none());
   m.def("attn_prefill", &attn_prefill);
   m.def("router_logits", &router_logits);
+  m.def("moe_combine_norm", &moe_combine_norm);
   m.def("splitk_rope_kv_write", &splitk_rope_kv_write);
   m.def("attn_train_transpose", &attn_train_transpose);
   m.def("attn_train_fwd", &attn_train_fwd);

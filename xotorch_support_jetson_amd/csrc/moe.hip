@@ -112,6 +112,82 @@ __global__ __launch_bounds__(256) void moe_combine_kernel(const float* __restric
   }
 }
 
+// combine + the RMSNorm that follows the MoE block (next layer's input norm / final norm), one
+// workgroup per token: h[t] += sum_j w_j y[slot(t, j)] in place, out[t] = rmsnorm(h[t]) * ln_w.  Saves the
+// separate norm launch and its re-read of h (a decode step of one token otherwise pays two ~5 us launches).
+template <int MAXC>
+__global__ __launch_bounds__(256) void moe_combine_norm_kernel(const float* __restrict__ y,
+                                                               const int32_t* __restrict__ slot_of,
+                                                               const float* __restrict__ topw, uint16_t* __restrict__ h,
+                                                               const uint16_t* __restrict__ lnw,
+                                                               uint16_t* __restrict__ out, int k, int D, int S,
+                                                               long ysplit, float eps) {
+  __shared__ float red[4];
+  const int t = blockIdx.x, tid = threadIdx.x, nchunk = D >> 3;
+  float v[MAXC][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXC; ++i) {
+    const int c = tid + i * 256;
+    if (c >= nchunk) continue;
+    const int d = c * 8;
+    const s16x8 hv = ld16(h + (size_t)t * D + d);
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = bf2f(hv[e]);
+    for (int j = 0; j < k; ++j) {
+      const float w = topw[(size_t)t * k + j];
+      const float* yr = y + (size_t)slot_of[(size_t)t * k + j] * D + d;
+      for (int sl = 0; sl < S; ++sl, yr += ysplit) {
+        const f32x4 a = *reinterpret_cast<const f32x4*>(yr);
+        const f32x4 b = *reinterpret_cast<const f32x4*>(yr + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          acc[e] += w * a[e];
+          acc[4 + e] += w * b[e];
+        }
+      }
+    }
+    s16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      o[e] = (short)f2bf(acc[e]);
+      v[i][e] = bf2f(o[e]);  // normalise the stored (bf16) stream, as the unfused path does
+      ss += v[i][e] * v[i][e];
+    }
+    st16(h + (size_t)t * D + d, o);
+  }
+  ss = wave_sum(ss);
+  if ((tid & 63) == 0) red[tid >> 6] = ss;
+  __syncthreads();
+  const float inv = rsqrtf((red[0] + red[1] + red[2] + red[3]) / (float)D + eps);
+#pragma unroll
+  for (int i = 0; i < MAXC; ++i) {
+    const int c = tid + i * 256;
+    if (c >= nchunk) continue;
+    const s16x8 wv = ld16(lnw + c * 8);
+    s16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (short)f2bf(v[i][e] * inv * bf2f(wv[e]));
+    st16(out + (size_t)t * D + c * 8, o);
+  }
+}
+
+int launch_moe_combine_norm(const float* y, const int32_t* slot_of, const float* topw, uint16_t* h,
+                            const uint16_t* lnw, uint16_t* out, int T, int k, int D, int S, long ysplit, float eps,
+                            hipStream_t s) {
+  if (T <= 0) return 0;
+  const int nchunk = D / 8;
+  if (D % 8 != 0 || nchunk > 8 * 256) return -1;
+#define XOT_MCN(MC) moe_combine_norm_kernel<MC><<<T, 256, 0, s>>>(y, slot_of, topw, h, lnw, out, k, D, S, ysplit, eps)
+  if (nchunk <= 256) XOT_MCN(1);
+  else if (nchunk <= 512) XOT_MCN(2);
+  else if (nchunk <= 1024) XOT_MCN(4);
+  else XOT_MCN(8);
+#undef XOT_MCN
+  return 0;
+}
+
 // Router logits in fp32: out[t][e] = x[t] . W[e] (x [T, D] bf16, W [E, D] bf16), one 256-thread workgroup per
 // token; W (64 KB for Mixtral) stays in L2 across the workgroups.  Replaces a bf16-output library GEMM plus
 // an fp32 cast (two launches, bf16-rounded logits) in front of moe_route.

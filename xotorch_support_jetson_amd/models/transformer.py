@@ -113,10 +113,12 @@ class ShardModel:
         return linear_resid_norm(act, lw.down_w, h, next_norm, c.rms_norm_eps)
       linear(act, lw.down_w, residual=h, epi="resid", out=h)
       return None
-    self._moe(xn, lw, h)
+    out = self._moe(xn, lw, h, next_norm)
+    if out is not None:  # the combine kernel also applied the following RMSNorm
+      return out
     return K.rmsnorm(h, next_norm, c.rms_norm_eps)[0] if next_norm is not None else None
 
-  def _moe(self, xn: torch.Tensor, lw, h: torch.Tensor) -> torch.Tensor:
+  def _moe(self, xn: torch.Tensor, lw, h: torch.Tensor, next_norm: Optional[torch.Tensor] = None):
     """Mixtral sparse MoE: softmax top-k routing, tokens grouped per expert, expert GEMMs on the
     kernel library (gate/up with fused SiLU epilogue), weighted scatter-add back into h."""
     c = self.c
@@ -127,7 +129,7 @@ class ShardModel:
     else:
       logits = linear(xn, lw.router, out_dtype=torch.float32)  # [T, E]
     if xn.is_cuda:
-      return self._moe_gpu(xn, lw, h, logits)
+      return self._moe_gpu(xn, lw, h, logits, next_norm)
     probs = torch.softmax(logits, dim=-1)
     topw, topi = torch.topk(probs, c.num_experts_per_tok, dim=-1)
     topw = topw / topw.sum(-1, keepdim=True)
@@ -149,9 +151,10 @@ class ShardModel:
       out.index_add_(0, idx, ye * wflat[start:start + n, None])
       start += n
     h += out.to(h.dtype)
-    return h
+    return None
 
-  def _moe_gpu(self, xn: torch.Tensor, lw, h: torch.Tensor, logits: torch.Tensor) -> torch.Tensor:
+  def _moe_gpu(self, xn: torch.Tensor, lw, h: torch.Tensor, logits: torch.Tensor,
+               next_norm: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
     """Device-only MoE (graph-capturable): routing kernel (softmax top-k, per-expert slot order),
     grouped gate/up GEMM gathering token rows with the SiLU*mul epilogue, grouped down GEMM into fp32
     slots, combine kernel adding sum_j w_j * y_slot(j) into the residual stream."""
@@ -182,8 +185,12 @@ class ShardModel:
       S = 1
     y = torch.empty(S * T * k, D, dtype=torch.float32, device=dev)
     C.gemm_moe(act, lw.down_w, y, off, None, K.EPI["none"], T, layout_of(lw.down_w) == "stream", S, bm)
+    if next_norm is not None:  # combine + the following RMSNorm in one kernel
+      out = torch.empty_like(h)
+      C.moe_combine_norm(y, slot_of, topw, h, S, next_norm, out, float(c.rms_norm_eps))
+      return out
     C.moe_combine(y, slot_of, topw, h, S)
-    return h
+    return None
 
   # ------------------------------------------------------------------ forward
   @torch.inference_mode()
