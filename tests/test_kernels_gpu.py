@@ -513,3 +513,30 @@ def test_router_logits(gpu, T, E, D):
   require().router_logits(x, w, out)
   ref = x.float() @ w.float().t()
   assert rel_err(out, ref) < 1e-5
+
+
+@pytest.mark.parametrize("T", [1, 5])
+@pytest.mark.parametrize("shuffled", [False, True])
+def test_moe_gate_up_split_k(gpu, T, shuffled):
+  """Decode-sized MoE batches: grouped gate/up split over K into fp32 slabs + SiLU slab reduce == the
+  fused SiLU-epilogue grouped GEMM."""
+  from xotorch_support_jetson_amd.ops._ext import require
+  from xotorch_support_jetson_amd.ops.weights_layout import shuffle_for_stream
+  torch.manual_seed(T)
+  C = require()
+  E, k, D, F, S = 8, 2, 1024, 512, 4
+  x = torch.randn(T, D, device=gpu).to(torch.bfloat16)
+  gu = (torch.randn(E, 2 * F, D, device=gpu) / math.sqrt(D)).to(torch.bfloat16)
+  gw = torch.stack([shuffle_for_stream(gu[e]) for e in range(E)]) if shuffled else gu
+  topw = torch.empty(T * k, device=gpu)
+  topi = torch.empty(T * k, dtype=torch.int32, device=gpu)
+  slot_of, sorted_tok = torch.empty_like(topi), torch.empty_like(topi)
+  off = torch.empty(E + 1, dtype=torch.int32, device=gpu)
+  C.moe_route(torch.randn(T, E, device=gpu), k, topw, topi, slot_of, sorted_tok, off)
+  act = torch.empty(T * k, F, dtype=torch.bfloat16, device=gpu)
+  C.gemm_moe(x, gw, act, off, sorted_tok, 2, T, shuffled)
+  ys = torch.empty(S * T * k, 2 * F, dtype=torch.float32, device=gpu)
+  C.gemm_moe(x, gw, ys, off, sorted_tok, 0, T, shuffled, S)
+  act2 = torch.empty_like(act)
+  C.splitk_silu(ys, S, act2)
+  assert rel_err(act2, act) < 1e-2

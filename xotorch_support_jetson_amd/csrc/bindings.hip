@@ -433,6 +433,15 @@ void moe_combine(const at::Tensor& y, const at::Tensor& slot_of, const at::Tenso
                           (int)D, (int)splits, (long)(T * k * D), cur_stream());
 }
 
+void splitk_silu(const at::Tensor& ws, int64_t S, at::Tensor& y) {
+  CHECK_DT(ws, at::kFloat);
+  CHECK_BF16(y);
+  XCHECK(all_contig_gpu(ws, y) && y.dim() == 2, "splitk_silu: contiguous GPU tensors, y 2-D");
+  const int64_t M = y.size(0), N = 2 * y.size(1);
+  XCHECK(S >= 1 && N % 32 == 0 && ws.numel() >= S * M * N, "splitk_silu: slabs must hold S x M x 2*cols");
+  xot::launch_splitk_silu(ws.data_ptr<float>(), (int)S, (int)M, (int)N, bf(y), cur_stream());
+}
+
 void moe_combine_norm(const at::Tensor& y, const at::Tensor& slot_of, const at::Tensor& topw, at::Tensor& h,
                       int64_t splits, const at::Tensor& ln_w, at::Tensor& out, double eps) {
   CHECK_DT(y, at::kFloat);
@@ -692,6 +701,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_prefill", &attn_prefill);
   m.def("router_logits", &router_logits);
   m.def("moe_combine_norm", &moe_combine_norm);
+  m.def("splitk_silu", &splitk_silu);
   m.def("splitk_rope_kv_write", &splitk_rope_kv_write);
   m.def("attn_train_transpose", &attn_train_transpose);
   m.def("attn_train_fwd", &attn_train_fwd);

@@ -432,6 +432,15 @@ int launch_gemm_big(const uint16_t* X, int ldx, const uint16_t* W, const uint16_
                  : big_dispatch<EPI_NONE, false>(X, ldx, W, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, bn, S, reduce, s);
 }
 
+// S fp32 slabs [S][M][N] of a 16-row interleaved gate/up product -> silu(gate) * up [M, N/2] bf16
+void launch_splitk_silu(const float* ws, int S, int M, int N, uint16_t* y, hipStream_t s) {
+  if (M <= 0) return;
+  const long chunks = (long)M * (N / 2 / 8);
+  int blocks = (int)((chunks + 255) / 256);
+  if (blocks > 2048) blocks = 2048;
+  splitk_reduce_kernel<EPI_SILU, false><<<blocks, 256, 0, s>>>(ws, S, M, N, nullptr, nullptr, 0, y, N / 2);
+}
+
 // ------------------------------------------------------------------------------------ grouped (MoE)
 template <int BM, int EPI, bool F32, int MOE>
 static void big_moe_launch(const uint16_t* X, int ldx, const uint16_t* W, void* Y, int ldy, const int* off,

@@ -49,6 +49,7 @@ int launch_gemm_moe_big(const uint16_t* X, int ldx, const uint16_t* W, void* Y, 
 int launch_gemm_moe(const uint16_t* X, int ldx, const uint16_t* W, void* Y, int ldy, bool out_f32, int epi,
                     const int* off, const int* gather, int E, int max_rows, int N, int K, bool wshuf, int S,
                     long ysplit, hipStream_t s);
+void launch_splitk_silu(const float* ws, int S, int M, int N, uint16_t* y, hipStream_t s);
 int launch_moe_combine_norm(const float* y, const int32_t* slot_of, const float* topw, uint16_t* h,
                             const uint16_t* lnw, uint16_t* out, int T, int k, int D, int S, long ysplit, float eps,
                             hipStream_t s);

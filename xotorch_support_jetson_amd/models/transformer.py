@@ -35,6 +35,8 @@ from .weights import ShardWeights, expert
 
 # average rows per expert above which the grouped expert GEMMs run on gemm_big tiles
 MOE_BIG_MIN_ROWS = float(os.environ.get("XOT_MOE_BIG_MIN_ROWS", "24"))
+# K splits of the grouped gate/up GEMM for decode-sized batches (1: fused SiLU epilogue, no slabs)
+MOE_GU_SPLITS = int(os.environ.get("XOT_MOE_GU_SPLITS", "4"))
 PAGE = 64
 
 
@@ -177,7 +179,16 @@ class ShardModel:
     # ~100-160 rows, 256 otherwise (a tile's rows past the expert's count are masked MFMA work)
     bm = 0 if not shuffled or rows < MOE_BIG_MIN_ROWS else (192 if 96 < rows <= 160 else 256)
     act = torch.empty(T * k, F, dtype=torch.bfloat16, device=dev)
-    C.gemm_moe(xn, lw.gu_w, act, off, sorted_tok, K.EPI["silu"], T, layout_of(lw.gu_w) == "stream", 1, bm)
+    Sg = MOE_GU_SPLITS if (bm == 0 and T * k <= 32 and D % (256 * MOE_GU_SPLITS) == 0) else 1
+    if Sg > 1:
+      # decode-sized groups: the weight-streaming gate/up split over K into fp32 slabs (k experts x N/128
+      # column blocks alone leave the last wave of workgroups short, e.g. 448 on 512 slots at batch 1),
+      # SiLU*mul applied by the slab reduce
+      ys = torch.empty(Sg * T * k, 2 * F, dtype=torch.float32, device=dev)
+      C.gemm_moe(xn, lw.gu_w, ys, off, sorted_tok, K.EPI["none"], T, layout_of(lw.gu_w) == "stream", Sg, 0)
+      C.splitk_silu(ys, Sg, act)
+    else:
+      C.gemm_moe(xn, lw.gu_w, act, off, sorted_tok, K.EPI["silu"], T, layout_of(lw.gu_w) == "stream", 1, bm)
     # down projection split over K (fp32 partial slabs summed by the combine): the grouped GEMM only has
     # (experts hit) x N/tile workgroups with work, too few to stream the expert weights at full HBM rate
     S = (4 if T * k <= 64 else 2) if bm == 0 else (4 if bm == 192 else 2)
