@@ -86,6 +86,10 @@ struct TransTile {
 }  // namespace
 
 // ---------------------------------------------------------------------------------------- forward
+// Each wave owns FRB blocks of 16 query rows (4 waves x FRB x 16 = the workgroup's query tile): every K /
+// V^T fragment read from LDS feeds FRB MFMAs.  FRB = 2 halves the LDS reads per MFMA but also halves the
+// grid (512 workgroups for 32 heads at L = 2048, under two per CU), which measured slower (116 vs 103 us).
+constexpr int FRB = 1, FQT = 64 * FRB;  // FRB = 2 measured slower at L = 2048 (half the workgroups)
 template <int DH>
 __global__ __launch_bounds__(256) void attn_train_fwd_kernel(const uint16_t* __restrict__ Q, long ldq,
                                                              const uint16_t* __restrict__ K, long ldk,
@@ -97,106 +101,127 @@ __global__ __launch_bounds__(256) void attn_train_fwd_kernel(const uint16_t* __r
   constexpr int KLD = DH + 8, VLD = TT + 8, PLD = TT + 8;
   __shared__ __attribute__((aligned(16))) uint16_t ks[TT * KLD];
   __shared__ __attribute__((aligned(16))) uint16_t vt[DH * VLD];
-  __shared__ __attribute__((aligned(16))) uint16_t pl[4][16 * PLD];
+  __shared__ __attribute__((aligned(16))) uint16_t pl[4][FRB][16 * PLD];
   // query tiles are the slowest grid dimension, heaviest (most key tiles under the causal mask) first
   const int h = blockIdx.x, qt = gridDim.y - 1 - blockIdx.y, b = blockIdx.z;
   const int kvh = h / (H / Hkv);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
-  const int q0 = qt * TT, qrow = q0 + 16 * wave;
+  const int q0 = qt * FQT, qrow = q0 + 16 * FRB * wave;  // row block rb: rows qrow + 16 rb ..
+  const int ktl = min((L + TT - 1) / TT, (q0 + FQT + TT - 1) / TT) - 1;  // last key tile under the mask
   const uint16_t* Kb = K + (long)b * L * ldk + kvh * DH;
   const uint16_t* VTb = VT + ((long)b * Hkv + kvh) * DH * Lp;
   const float sl = scale * L2E;
 
-  s16x8 qf[KS];
-  {
-    const uint16_t* qp = Q + ((long)b * L + min(qrow + c, L - 1)) * ldq + h * DH + 8 * g;
+  s16x8 qf[FRB][KS];
 #pragma unroll
-    for (int s = 0; s < KS; ++s) qf[s] = ld16(qp + 32 * s);
+  for (int rb = 0; rb < FRB; ++rb) {
+    const uint16_t* qp = Q + ((long)b * L + min(qrow + 16 * rb + c, L - 1)) * ldq + h * DH + 8 * g;
+#pragma unroll
+    for (int s2 = 0; s2 < KS; ++s2) qf[rb][s2] = ld16(qp + 32 * s2);
   }
-  float m[4], l[4];
-  f32x4 o[NDT];
+  float m[FRB][4], l[FRB][4];
+  f32x4 o[FRB][NDT];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    m[r] = NEG;
-    l[r] = 0.f;
+  for (int rb = 0; rb < FRB; ++rb) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      m[rb][r] = NEG;
+      l[rb][r] = 0.f;
+    }
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) o[rb][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
-#pragma unroll
-  for (int dt = 0; dt < NDT; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  uint16_t* pw = pl[wave];
 
   RowsTile<DH> kr;
   TransTile<DH> vr;
   kr.load(Kb, ldk, 0, L);
   vr.load(VTb, Lp, 0);
-  for (int kt = 0; kt <= qt; ++kt) {
+  for (int kt = 0; kt <= ktl; ++kt) {
     const int k0 = kt * TT;
     __syncthreads();  // every wave is done with the previous tile
     kr.template store<KLD>(ks);
     vr.template store<VLD>(vt);
     __syncthreads();
-    if (kt < qt) {  // next tile in flight under this tile's math
+    if (kt < ktl) {  // next tile in flight under this tile's math
       kr.load(Kb, ldk, k0 + TT, L);
       vr.load(VTb, Lp, k0 + TT);
     }
-    f32x4 sc[4];
+    f32x4 sc[FRB][4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      sc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int s = 0; s < KS; ++s) sc[t] = mfma16(qf[s], ld16(ks + (16 * t + c) * KLD + 32 * s + 8 * g), sc[t]);
-    }
-    float mt[4];
+      for (int rb = 0; rb < FRB; ++rb) sc[rb][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int r = 0; r < 4; ++r) mt[r] = NEG;
+      for (int s2 = 0; s2 < KS; ++s2) {
+        const s16x8 kb = ld16(ks + (16 * t + c) * KLD + 32 * s2 + 8 * g);
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = k0 + 16 * t + c, qi = qrow + 4 * g + r;
-        const float v = (key <= qi && key < L) ? sc[t][r] * sl : -INFINITY;
-        sc[t][r] = v;
-        mt[r] = fmaxf(mt[r], v);
+        for (int rb = 0; rb < FRB; ++rb) sc[rb][t] = mfma16(qf[rb][s2], kb, sc[rb][t]);
       }
-    float alpha[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      mt[r] = group16_max(mt[r]);
-      const float mn = fmaxf(m[r], mt[r]);
-      alpha[r] = exp2f(m[r] - mn);
-      m[r] = mn;
-      l[r] *= alpha[r];
     }
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+    for (int rb = 0; rb < FRB; ++rb) {
+      float mt[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) mt[r] = NEG;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = k0 + 16 * t + c, qi = qrow + 16 * rb + 4 * g + r;
+          const float v = (key <= qi && key < L) ? sc[rb][t][r] * sl : -INFINITY;
+          sc[rb][t][r] = v;
+          mt[r] = fmaxf(mt[r], v);
+        }
+      float alpha[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float p = exp2f(sc[t][r] - m[r]);
-        l[r] += p;
-        pw[(4 * g + r) * PLD + 16 * t + c] = f2bf(p);
+        mt[r] = group16_max(mt[r]);
+        const float mn = fmaxf(m[rb][r], mt[r]);
+        alpha[r] = exp2f(m[rb][r] - mn);
+        m[rb][r] = mn;
+        l[rb][r] *= alpha[r];
       }
+      uint16_t* pw = pl[wave][rb];
 #pragma unroll
-    for (int dt = 0; dt < NDT; ++dt)
+      for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) o[dt][r] *= alpha[r];
+        for (int r = 0; r < 4; ++r) {
+          const float p = exp2f(sc[rb][t][r] - m[rb][r]);
+          l[rb][r] += p;
+          pw[(4 * g + r) * PLD + 16 * t + c] = f2bf(p);
+        }
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[rb][dt][r] *= alpha[r];
+    }
     wave_sync_lds();
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      const s16x8 pa = ld16(pw + c * PLD + 32 * kk + 8 * g);
+      s16x8 pa[FRB];
 #pragma unroll
-      for (int dt = 0; dt < NDT; ++dt) o[dt] = mfma16(pa, ld16(vt + (16 * dt + c) * VLD + 32 * kk + 8 * g), o[dt]);
+      for (int rb = 0; rb < FRB; ++rb) pa[rb] = ld16(pl[wave][rb] + c * PLD + 32 * kk + 8 * g);
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) {
+        const s16x8 vb = ld16(vt + (16 * dt + c) * VLD + 32 * kk + 8 * g);
+#pragma unroll
+        for (int rb = 0; rb < FRB; ++rb) o[rb][dt] = mfma16(pa[rb], vb, o[rb][dt]);
+      }
     }
   }
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    l[r] = group16_sum(l[r]);
-    const int qi = qrow + 4 * g + r;
-    if (qi >= L) continue;
-    const float inv = l[r] > 0.f ? 1.f / l[r] : 0.f;
-    uint16_t* op = O + ((long)b * L + qi) * ldo + h * DH + c;
+  for (int rb = 0; rb < FRB; ++rb)
 #pragma unroll
-    for (int dt = 0; dt < NDT; ++dt) op[16 * dt] = f2bf(o[dt][r] * inv);
-    if (c == 0) lse2[((long)b * H + h) * L + qi] = m[r] + log2f(l[r]);
-  }
+    for (int r = 0; r < 4; ++r) {
+      const float ls = group16_sum(l[rb][r]);
+      const int qi = qrow + 16 * rb + 4 * g + r;
+      if (qi >= L) continue;
+      const float inv = ls > 0.f ? 1.f / ls : 0.f;
+      uint16_t* op = O + ((long)b * L + qi) * ldo + h * DH + c;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) op[16 * dt] = f2bf(o[rb][dt][r] * inv);
+      if (c == 0) lse2[((long)b * H + h) * L + qi] = m[rb][r] + log2f(ls);
+    }
 }
 
 // ---------------------------------------------------------------------------------------- dQ (+ delta)
@@ -509,7 +534,7 @@ int launch_attn_train_fwd(const uint16_t* q, long ldq, const uint16_t* k, long l
                           hipStream_t s) {
   if (B <= 0 || L <= 0) return 0;
   if (H % Hkv != 0 || Lp % TT != 0 || Lp < L) return -1;
-  dim3 grid(H, (L + TT - 1) / TT, B);
+  dim3 grid(H, (L + FQT - 1) / FQT, B);
   if (Dh == 128)
     attn_train_fwd_kernel<128><<<grid, 256, 0, s>>>(q, ldq, k, ldk, vt, Lp, o, ldo, lse2, L, H, Hkv, scale);
   else if (Dh == 64)
