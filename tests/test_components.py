@@ -41,6 +41,13 @@ def test_presets_match_hf_shapes():
          (80, 8192, 64, 8, 28672, 128256)
   for name, cfg in PRESETS.items():
     assert cfg.hidden_size == cfg.num_heads * cfg.head_dim or cfg.head_dim in (64, 128), name
+  # every model card with a preset agrees on the layer count; parameter totals of the big dense cards
+  for name, card in R.model_cards.items():
+    if name in PRESETS:
+      assert PRESETS[name].num_layers == card["layers"], name
+  for name, billions in (("llama-3.1-405b", 405.9), ("qwen-2.5-72b", 72.7), ("mistral-large", 122.6),
+                         ("qwen-2.5-32b", 32.8), ("llama-3-8b", 8.0)):
+    assert abs(PRESETS[name].num_params() / 1e9 - billions) < 0.15, name
 
 
 def test_config_from_hf_dict():

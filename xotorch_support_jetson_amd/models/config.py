@@ -112,6 +112,17 @@ PRESETS: dict[str, ModelConfig] = {
                                bos_token_id=151643, eos_token_ids=(151645, 151643)),
   "qwen-2.5-7b": ModelConfig("qwen2", 152064, 3584, 18944, 28, 28, 4, 128, 1e-6, 1000000.0, None, 32768, False, True,
                              bos_token_id=151643, eos_token_ids=(151645, 151643)),
+  "qwen-2.5-3b": ModelConfig("qwen2", 151936, 2048, 11008, 36, 16, 2, 128, 1e-6, 1000000.0, None, 32768, True, True,
+                             bos_token_id=151643, eos_token_ids=(151645, 151643)),
+  "qwen-2.5-14b": ModelConfig("qwen2", 152064, 5120, 13824, 48, 40, 8, 128, 1e-5, 1000000.0, None, 32768, False, True,
+                              bos_token_id=151643, eos_token_ids=(151645, 151643)),
+  "qwen-2.5-32b": ModelConfig("qwen2", 152064, 5120, 27648, 64, 40, 8, 128, 1e-5, 1000000.0, None, 32768, False, True,
+                              bos_token_id=151643, eos_token_ids=(151645, 151643)),
+  "qwen-2.5-72b": ModelConfig("qwen2", 152064, 8192, 29568, 80, 64, 8, 128, 1e-5, 1000000.0, None, 32768, False, True,
+                              bos_token_id=151643, eos_token_ids=(151645, 151643)),
+  "llama-3.1-405b": ModelConfig("llama", 128256, 16384, 53248, 126, 128, 8, 128, 1e-5, 500000.0, _L31, 131072, False),
+  "mistral-large": ModelConfig("mistral", 32768, 12288, 28672, 88, 96, 8, 128, 1e-5, 1000000.0, None, 131072, False,
+                               bos_token_id=1, eos_token_ids=(2,)),
   "mistral-7b": ModelConfig("mistral", 32768, 4096, 14336, 32, 32, 8, 128, 1e-5, 1000000.0, None, 32768, False,
                             bos_token_id=1, eos_token_ids=(2,)),
   "mixtral-8x7b": ModelConfig("mixtral", 32000, 4096, 14336, 32, 32, 8, 128, 1e-5, 1000000.0, None, 32768, False,
@@ -133,7 +144,10 @@ for _alias, _base in {"llama-3.1-70b-bf16": "llama-3.1-70b", "nemotron-70b": "ll
                       "deepseek-r1-distill-llama-70b": "llama-3.1-70b", "deepseek-r1-distill-llama-8b": "llama-3.1-8b",
                       "qwen-2.5-coder-1.5b": "qwen-2.5-1.5b", "qwen-2.5-coder-7b": "qwen-2.5-7b",
                       "qwen-2.5-math-7b": "qwen-2.5-7b", "deepseek-r1-distill-qwen-1.5b": "qwen-2.5-1.5b",
-                      "deepseek-r1-distill-qwen-7b": "qwen-2.5-7b"}.items():
+                      "deepseek-r1-distill-qwen-7b": "qwen-2.5-7b", "qwen-2.5-coder-3b": "qwen-2.5-3b",
+                      "qwen-2.5-coder-14b": "qwen-2.5-14b", "deepseek-r1-distill-qwen-14b": "qwen-2.5-14b",
+                      "qwen-2.5-coder-32b": "qwen-2.5-32b", "deepseek-r1-distill-qwen-32b": "qwen-2.5-32b",
+                      "qwen-2.5-math-72b": "qwen-2.5-72b", "llama-3.1-405b-8bit": "llama-3.1-405b"}.items():
   PRESETS.setdefault(_alias, PRESETS[_base])
 
 
