@@ -20,6 +20,8 @@ from typing import Optional
 import torch
 import torch.distributed as dist
 
+from .health import FaultInjector, HealthMonitor, wait_work
+
 
 def env_rank() -> tuple[int, int, int]:
   return int(os.environ.get("RANK", 0)), int(os.environ.get("LOCAL_RANK", 0)), int(os.environ.get("WORLD_SIZE", 1))
@@ -62,8 +64,8 @@ class _StagedRecv:
   def __init__(self, work, host: torch.Tensor, dst: torch.Tensor):
     self.work, self.host, self.dst = work, host, dst
 
-  def wait(self):
-    self.work.wait()
+  def wait(self, monitor=None):
+    wait_work(self.work, monitor)
     self.dst.copy_(self.host)
     return True
 
@@ -81,8 +83,11 @@ class P2PTransport:
   per direction each link only ever carries a FIFO of same-direction messages, which cannot deadlock.
   """
 
-  def __init__(self, rank: int, world: int):
+  def __init__(self, rank: int, world: int, monitor: Optional[HealthMonitor] = None,
+               injector: Optional[FaultInjector] = None):
     self.rank, self.world = rank, world
+    self.monitor = monitor  # parallel/health.py: host waits raise PeerFailure instead of hanging
+    self.injector = injector if injector is not None else FaultInjector.from_env(rank, monitor)
     self._pending = []
     self._groups = {}
     self._staged = False
@@ -95,6 +100,10 @@ class P2PTransport:
     return self._groups.get((src, dst))
 
   def isend(self, t: torch.Tensor, dst: int):
+    if self.monitor is not None:
+      self.monitor.check()
+    if self.injector is not None:
+      self.injector.before_send()
     if self._staged and t.is_cuda:
       t = t.to("cpu")
     w = dist.isend(t, dst, group=self._group(self.rank, dst))
@@ -110,8 +119,20 @@ class P2PTransport:
     return dist.irecv(t, src, group=self._group(src, self.rank))
 
   def recv(self, t: torch.Tensor, src: int) -> torch.Tensor:
-    self.irecv(t, src).wait()
+    self.wait(self.irecv(t, src))
     return t
+
+  def wait(self, work) -> None:
+    """Host wait on a recv.  gloo (and staged) waits block the host, so with a monitor they poll it and
+    raise PeerFailure; an RCCL wait only orders the compute stream after the comm stream and returns at
+    once (polling it would serialise host and GPU), so a dead peer there is handled by the monitor's
+    communicator abort."""
+    if isinstance(work, _StagedRecv):
+      work.wait(self.monitor)
+    elif self._staged or dist.is_initialized() and dist.get_backend() == "gloo":
+      wait_work(work, self.monitor)
+    else:
+      work.wait()
 
   def reap(self):
     keep = []
@@ -152,6 +173,9 @@ class LoopbackTransport:
 
   def recv(self, t: torch.Tensor, src: int) -> torch.Tensor:
     return self.irecv(t, src) and t
+
+  def wait(self, work) -> None:
+    work.wait()
 
   def reap(self):
     pass

@@ -111,7 +111,7 @@ class RingStage:
     idx = torch.empty(B, KC, dtype=torch.int32, device=dev)
     works = [self.t.irecv(xn, self.prev), self.t.irecv(vals, self.prev), self.t.irecv(idx, self.prev)]
     for w in works:
-      w.wait()
+      self.t.wait(w)
     return self._finish_head(xn, vals, idx, mb.temps)
 
   # ---------------------------------------------------------------- one micro-batch through this stage
@@ -164,10 +164,10 @@ class RingStage:
         x = sampled = self._recv_and_sample(mb)
       else:
         x = torch.empty(B, dtype=torch.int32, device=dev)
-        self.t.irecv(x, self.prev).wait()
+        self.t.wait(self.t.irecv(x, self.prev))
     else:
       x = torch.empty(B, self.D, dtype=torch.bfloat16, device=dev)
-      self.t.irecv(x, self.prev).wait()
+      self.t.wait(self.t.irecv(x, self.prev))
     y = self.r.forward(mb.rids, [1] * B, x)
     if not self.last:
       # y is the decode graph's static output buffer: the next replay overwrites it, so hand RCCL a copy

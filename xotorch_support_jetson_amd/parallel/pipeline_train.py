@@ -72,7 +72,7 @@ class PipelineTrainer:
         inp = b.x.to(self.dev)
       else:
         inp = torch.empty(mb, L, self.D, dtype=torch.bfloat16, device=self.dev)
-        self.t.irecv(inp, self.prev).wait()
+        self.t.wait(self.t.irecv(inp, self.prev))
       leaf, out = tr.forward_train(inp)
       if not self.last:
         self.t.isend(out.detach().contiguous(), self.next)
@@ -84,7 +84,7 @@ class PipelineTrainer:
         losses.append(loss)
       else:
         g = torch.empty_like(out, dtype=torch.bfloat16)
-        self.t.irecv(g, self.next).wait()
+        self.t.wait(self.t.irecv(g, self.next))
         _, gin = tr.backward_accumulate(leaf, out, grad_out=g)
       if not self.first:
         self.t.isend(gin.to(torch.bfloat16).contiguous(), self.prev)

@@ -83,7 +83,11 @@ def _worker(rank: int, world: int, port: int, a: dict) -> None:
     from ..parallel.data_parallel import DataParallelTrainer
     pt = DataParallelTrainer(tr, rank, world)
   else:
-    pt = PipelineTrainer(tr, rank, world, P2PTransport(rank, world))
+    mon = None
+    if world > 1 and os.environ.get("XOT_HEARTBEAT", "1") == "1":  # parallel/health.py
+      from ..parallel.health import HealthMonitor
+      mon = HealthMonitor(rank, world, timeout=float(os.environ.get("XOT_HEARTBEAT_TIMEOUT", "30"))).start()
+    pt = PipelineTrainer(tr, rank, world, P2PTransport(rank, world, monitor=mon))
   tok = _resolve_tokenizer(mdir if mdir is not None else (registry.get_repo(model, "ShardedInferenceEngine") or "byte"),
                            cfg.vocab_size)
   train, valid, test = load_dataset(a["data"] or DEFAULT_DATA, lambda s: tok.encode(s))
@@ -110,6 +114,28 @@ def _worker(rank: int, world: int, port: int, a: dict) -> None:
     if rank == 0:
       print(f"eval | loss={tot / max(n, 1):.4f} tokens={n}", flush=True)
   else:
+    try:
+      _train_epochs(a, pt, tr, w, shard, rank, world, dp, train, bs, to_micro, _Shim)
+    except Exception as e:
+      from ..parallel.health import PeerFailure
+      if not isinstance(e, PeerFailure):
+        raise
+      # a ring peer died or wedged: its layers (and the in-flight step) are gone.  Exit without the
+      # closing barrier; `xot train --resume-checkpoint DIR` re-partitions the last saved iteration
+      # (HF key names, any layer split) over the peers that are left.
+      print(f"[rank {rank}] {e}; stopping, resume from the last checkpoint", flush=True)
+      os._exit(75)
+  if world > 1:
+    if not dp and pt.t.monitor is not None:
+      pt.t.monitor.stop()  # orderly exit: peers must not flag it
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _train_epochs(a, pt, tr, w, shard, rank, world, dp, train, bs, to_micro, _Shim):
+  from ..train import checkpoint as ck
+  from ..train.dataset import iterate_batches
+  if True:
     step = 0
     for epoch in range(a["iters"]):
       tot, n = 0.0, 0
@@ -128,9 +154,6 @@ def _worker(rank: int, world: int, port: int, a: dict) -> None:
         path = ck.checkpoint_path(a["save_dir"], shard, epoch + 1)
         ck.save_shard_checkpoint(shim, shard, path)
         print(f"[rank {rank}] saved {path}", flush=True)
-  if world > 1:
-    dist.barrier()
-    dist.destroy_process_group()
 
 
 @torch.no_grad()
