@@ -70,7 +70,7 @@ def build_parser() -> argparse.ArgumentParser:
   p.add_argument("--system-prompt", type=str, default=None, help="System prompt for the ChatGPT API")
   p.add_argument("--gpus", type=int, default=0, help="Spawn one peer process per local GPU (0 = single process)")
   p.add_argument("--ring", action="store_true",
-                 help="train/eval: run the pipeline stages on the local GPUs over RCCL (no gRPC hops)")
+                 help="serve/run/train/eval over the local GPUs as one RCCL ring (one process per GPU, no gRPC hops)")
   p.add_argument("--micro-batch", type=int, default=1, help="--ring: sequences per pipeline micro-batch")
   p.add_argument("--parallel", choices=("pp", "dp"), default="pp",
                  help="--ring: pp = layer pipeline over the GPUs; dp = a full replica per GPU, gradients all-reduced")
@@ -361,6 +361,9 @@ def run(argv=None):
   if args.ring and args.command in ("train", "eval"):
     from .train.ring_train import run_ring
     sys.exit(run_ring(args))
+  if args.ring:  # serve / run over the local GPU ring: continuous batching, RCCL activation hand-off
+    from .parallel.ring_serve import serve_ring
+    sys.exit(serve_ring(args))
   if args.gpus and args.gpus > 1 and "XOT_PEER_RANK" not in os.environ:
     sys.exit(spawn_gpu_peers(args, argv))
   if DEBUG >= 0 and not args.no_api and os.environ.get("XOT_PEER_RANK", "0") == "0":
