@@ -5,6 +5,7 @@ import os
 import socket
 import threading
 
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -24,10 +25,10 @@ def _prompt(rid, n):
   return torch.randint(0, PRESETS[MODEL].vocab_size, (n,), generator=g).tolist()
 
 
-def _serve(rank, world, ctl):
+def _serve(rank, world, ctl, device="cpu"):
   c = PRESETS[MODEL]
   shard = equal_layer_shards(MODEL, c.num_layers, world)[rank]
-  runner = ShardRunner(c, shard, "cpu", max_batch=8, max_ctx=64)
+  runner = ShardRunner(c, shard, device, max_batch=8, max_ctx=64)
   srv = RingServer(runner, rank, world, P2PTransport(rank, world), ctl)
   out = {}
   if rank == 0:
@@ -134,3 +135,15 @@ def test_chatgpt_api_over_ring_server():
     await api._runner.cleanup()
 
   asyncio.run(asyncio.wait_for(main(), 120))
+
+
+@pytest.mark.gpu
+def test_ring_server_on_gpu():
+  """The serving round loop on cuda:0 (HIP kernels, paged KV, decode graphs for the running batch):
+  staggered admissions all finish with their token budgets and free their pages."""
+  from xotorch_support_jetson_amd.ops._ext import require
+  require()
+  out, live = _serve(0, 1, None, device="cuda:0")
+  assert {r: len(v) for r, v in out.items()} == {rid: mt for rid, _, mt in REQS}
+  assert all(0 <= t < PRESETS[MODEL].vocab_size for v in out.values() for t in v)
+  assert len(live) <= 1
