@@ -128,3 +128,37 @@ def test_fused_grad_accumulation_matches_autograd(gpu):
   for k in dr:
     rel = ((df[k] - dr[k]).abs().mean() / (dr[k].abs().mean() + 1e-12)).item()
     assert rel < 0.05, (k, rel)
+
+
+def test_moe_training_gpu(gpu):
+  """Mixtral-style fine-tuning on the GPU: the first AdamW step matches the CPU trainer on the same
+  weights, loss falls, and weights trained from a decode-layout shard (pre-shuffled expert stacks) are
+  written back so the serving runner reproduces the trainer's logits."""
+  from xotorch_support_jetson_amd.train.trainer import ShardTrainer
+  name = "tiny-mixtral"
+  c = preset(name)
+  sh = Shard(name, 0, c.num_layers - 1, c.num_layers)
+  g = torch.Generator().manual_seed(3)
+  x = torch.randint(0, c.vocab_size, (2, 48), generator=g)
+  y, ln = torch.roll(x, -1, 1), torch.tensor([48, 40])
+  w = random_weights(c, sh, gpu, seed=4)  # both trainers copy their parameters from these
+  trs = [ShardTrainer(w, d, lr=1e-3, max_seq=256) for d in (torch.device("cpu"), gpu)]
+  init = [{k: v.detach().cpu().clone() for k, v in t.master.items()} for t in trs]
+  for k in init[0]:
+    assert torch.allclose(init[0][k], init[1][k]), k
+  losses = [t.step("m", x, y, ln)[0] for t in trs]
+  assert abs(losses[0] - losses[1]) < 2e-2 * max(1.0, abs(losses[0])), losses
+  for k in init[0]:
+    d0, d1 = trs[0].master[k].cpu() - init[0][k], trs[1].master[k].cpu() - init[1][k]
+    rel = ((d0 - d1).abs().mean() / (d0.abs().mean() + 1e-12)).item()
+    assert rel < 0.25, (k, rel)
+
+  runner = ShardRunner(c, sh, gpu, max_batch=4, max_ctx=256)
+  tr = ShardTrainer(runner.weights, gpu, lr=3e-3, max_seq=256)
+  ls = [tr.step("r", x, y, ln)[0] for _ in range(8)]
+  assert ls[-1] < ls[0] * 0.9, ls
+  tr.sync_to_inference()
+  out = runner.forward(["a"], [48], x[0].to(gpu, torch.int32)).float().reshape(-1)
+  with torch.no_grad():
+    ref = tr.forward(x[:1].to(gpu)).float()[0, -1]
+  assert torch.corrcoef(torch.stack([out, ref]))[0, 1] > 0.99

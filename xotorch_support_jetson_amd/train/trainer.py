@@ -47,18 +47,21 @@ class ShardTrainer:
     self.step_count = 0
     self.dirty = False
     self.cos_sin = build_cos_sin(self.c.head_dim, max_seq, self.c.rope_theta, self.c.rope_scaling, self.device)
-    if self.c.is_moe:
-      raise NotImplementedError("MoE fine-tuning is not implemented yet (dense Llama/Qwen/Mistral only)")
     # training parameters (row-major, gate|up halves), bf16 leaves + fp32 master + moments
     self.params: Dict[str, torch.Tensor] = {}
     for i, lw in weights.layers.items():
-      g, u = split_gate_up(_rowmajor(lw.gu_w))
+      g, u = split_gate_up(_rowmajor(lw.gu_w))  # [F, D] each, or [E, F, D] expert stacks
       self._add(f"{i}.qkv", _rowmajor(lw.qkv_w))
       if lw.qkv_b is not None:
         self._add(f"{i}.qkv_b", lw.qkv_b)
       self._add(f"{i}.o", _rowmajor(lw.o_w))
-      self._add(f"{i}.gu", torch.cat([g, u], 0))
-      self._add(f"{i}.down", _rowmajor(lw.down_w))
+      if self.c.is_moe:  # Mixtral: router [E, D], experts' gate|up [E, 2F, D], down [E, D, F]
+        self._add(f"{i}.router", _rowmajor(lw.router))
+        self._add(f"{i}.egu", torch.cat([g, u], 1))
+        self._add(f"{i}.edown", _rowmajor(lw.down_w))
+      else:
+        self._add(f"{i}.gu", torch.cat([g, u], 0))
+        self._add(f"{i}.down", _rowmajor(lw.down_w))
       self._add(f"{i}.ln1", lw.ln1)
       self._add(f"{i}.ln2", lw.ln2)
     if weights.embed is not None and self.shard.is_first_layer():
@@ -104,12 +107,34 @@ class ShardTrainer:
       a = A.attention(q, k, v, B, L, H, Hkv, Dh)  # flash-style HIP kernels (fwd + dQ + dK/dV)
       h = self._mm(a, f"{i}.o", h)
       xn = A.rmsnorm(h, P[f"{i}.ln2"], c.rms_norm_eps)
-      h = self._mm(A.silu_mul(self._mm(xn, f"{i}.gu").contiguous()), f"{i}.down", h)
+      if c.is_moe:
+        h = h + self._moe(xn, i)
+      else:
+        h = self._mm(A.silu_mul(self._mm(xn, f"{i}.gu").contiguous()), f"{i}.down", h)
     if not self.shard.is_last_layer():
       return h.view(B, L, D)
     xn = A.rmsnorm(h, P["norm"], c.rms_norm_eps)
     head = P["lm_head"] if "lm_head" in P else P["embed"]
     return (xn @ head.t()).view(B, L, -1)
+
+  def _moe(self, xn: torch.Tensor, i: int) -> torch.Tensor:
+    """Mixtral sparse MLP with autograd: fp32 router softmax, top-k renormalised weights (the router
+    learns through them), each expert's gate/up -> SiLU*mul -> down on the rows routed to it, weighted
+    fp32 scatter-add.  Same routing as the inference path (models/transformer.py `_moe`)."""
+    c, P = self.c, self.params
+    logits = xn.float() @ P[f"{i}.router"].float().t()  # [T, E]
+    topw, topi = torch.topk(torch.softmax(logits, dim=-1), c.num_experts_per_tok, dim=-1)
+    topw = topw / topw.sum(-1, keepdim=True)
+    egu, edown = P[f"{i}.egu"], P[f"{i}.edown"]
+    out = torch.zeros(xn.shape[0], c.hidden_size, device=xn.device, dtype=torch.float32)
+    for e in range(c.num_experts):
+      tok, slot = (topi == e).nonzero(as_tuple=True)
+      if tok.numel() == 0:
+        continue
+      act = A.silu_mul((xn.index_select(0, tok) @ egu[e].t()).contiguous())
+      ye = act @ edown[e].t()
+      out = out.index_add(0, tok, ye.float() * topw[tok, slot].unsqueeze(1))
+    return out.to(xn.dtype)
 
   def _mm(self, x: torch.Tensor, name: str, h: Optional[torch.Tensor] = None) -> torch.Tensor:
     """x @ W.T (+ h) for projection `name`: fused gradient accumulation on the GPU while training."""
@@ -253,13 +278,20 @@ class ShardTrainer:
     P = self.params
     Fd = self.c.intermediate_size
     for i, lw in self.w.layers.items():
-      gu = P[f"{i}.gu"].detach()
       assign_weight(lw.qkv_w, P[f"{i}.qkv"].detach())
       if f"{i}.qkv_b" in P:
         assign_weight(lw.qkv_b, P[f"{i}.qkv_b"].detach())
       assign_weight(lw.o_w, P[f"{i}.o"].detach())
-      assign_weight(lw.gu_w, interleave_gate_up(gu[:Fd].contiguous(), gu[Fd:].contiguous()))
-      assign_weight(lw.down_w, P[f"{i}.down"].detach())
+      if self.c.is_moe:
+        egu = P[f"{i}.egu"].detach()
+        assign_weight(lw.gu_w, torch.stack([interleave_gate_up(egu[e, :Fd].contiguous(), egu[e, Fd:].contiguous())
+                                            for e in range(egu.shape[0])]))
+        assign_weight(lw.down_w, P[f"{i}.edown"].detach())
+        assign_weight(lw.router, P[f"{i}.router"].detach())
+      else:
+        gu = P[f"{i}.gu"].detach()
+        assign_weight(lw.gu_w, interleave_gate_up(gu[:Fd].contiguous(), gu[Fd:].contiguous()))
+        assign_weight(lw.down_w, P[f"{i}.down"].detach())
       assign_weight(lw.ln1, P[f"{i}.ln1"].detach())
       assign_weight(lw.ln2, P[f"{i}.ln2"].detach())
     if "embed" in P:
