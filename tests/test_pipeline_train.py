@@ -29,19 +29,19 @@ def _batches(step):
   return out
 
 
-def _run(trainer, rank, world, transport):
-  pt = PipelineTrainer(trainer, rank, world, transport)
+def _run(trainer, rank, world, transport, schedule="gpipe"):
+  pt = PipelineTrainer(trainer, rank, world, transport, schedule=schedule)
   return [pt.step(_batches(s)) for s in range(2)]
 
 
-def _worker(rank, world, port, q, MODEL):
+def _worker(rank, world, port, q, MODEL, schedule):
   os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
   dist.init_process_group("gloo", rank=rank, world_size=world)
   try:
     c = PRESETS[MODEL]
     shard = equal_layer_shards(MODEL, c.num_layers, world)[rank]
     tr = ShardTrainer(random_weights(c, shard, "cpu", seed=3), "cpu", lr=1e-3)
-    losses = _run(tr, rank, world, P2PTransport(rank, world))
+    losses = _run(tr, rank, world, P2PTransport(rank, world), schedule)
     # numpy, not torch tensors: a queued tensor is an fd into this process, gone once it exits
     q.put((rank, losses, {k: v.detach().float().numpy().copy() for k, v in tr.master.items()}))
     dist.barrier()
@@ -55,8 +55,10 @@ def _port():
     return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("MODEL", ["tiny-llama", "tiny-llama-d64"])  # untied / tied embeddings
-def test_pipeline_training_two_ranks_matches_single(MODEL):
+# untied / tied embeddings; 1F1B over 3 ranks (warm-up forwards 2 / 1 / 0)
+@pytest.mark.parametrize("MODEL,world,schedule", [("tiny-llama", 2, "gpipe"), ("tiny-llama-d64", 2, "gpipe"),
+                                                  ("tiny-llama", 3, "1f1b")])
+def test_pipeline_training_two_ranks_matches_single(MODEL, world, schedule):
   c = PRESETS[MODEL]
   full = ShardTrainer(random_weights(c, Shard(MODEL, 0, c.num_layers - 1, c.num_layers), "cpu", seed=3), "cpu",
                       lr=1e-3)
@@ -65,12 +67,12 @@ def test_pipeline_training_two_ranks_matches_single(MODEL):
   ctx = mp.get_context("spawn")
   q = ctx.Queue()
   port = _port()
-  procs = [ctx.Process(target=_worker, args=(r, 2, port, q, MODEL)) for r in range(2)]
+  procs = [ctx.Process(target=_worker, args=(r, world, port, q, MODEL, schedule)) for r in range(world)]
   for p in procs:
     p.start()
   try:
     res = {}
-    for _ in range(2):
+    for _ in range(world):
       r, losses, master = q.get(timeout=240)
       res[r] = (losses, master)
   finally:
@@ -82,10 +84,10 @@ def test_pipeline_training_two_ranks_matches_single(MODEL):
   # tied embeddings: one bf16 grad summed by autograd vs two bf16 grads summed in fp32 -> rounding-level
   # grad differences, which early Adam steps (update ~ lr * sign(g)) can turn into <= 2 lr per element
   tol = 1e-3 if c.tie_word_embeddings else 1e-4
-  for r in (0, 1):
+  for r in range(world):
     for a, b in zip(res[r][0], ref_losses):
       assert abs(a - b) < tol, (r, res[r][0], ref_losses)
-  merged = {k: torch.from_numpy(v) for k, v in {**res[0][1], **res[1][1]}.items()}
+  merged = {k: torch.from_numpy(v) for r in range(world) for k, v in res[r][1].items()}
   for k, v in full.master.items():
     assert torch.allclose(v, merged[k], atol=1e-6 if tol < 1e-3 else 2e-3, rtol=1e-5), k
   if c.tie_word_embeddings:  # the last stage's head copy took the same update as the embedding

@@ -39,6 +39,7 @@ def main():
   ap.add_argument("--parallel", choices=("pp", "dp"), default="pp",
                   help="pp: layer pipeline (the reference's strategy); dp: full replica per GPU, bucketed "
                        "all-reduce overlapped with backward (parallel/data_parallel.py)")
+  ap.add_argument("--schedule", choices=("gpipe", "1f1b"), default="gpipe", help="pp micro-batch order")
   args = ap.parse_args()
 
   import torch.distributed as dist
@@ -64,7 +65,8 @@ def main():
     M = args.microbatches or max(8, 4 * world)
   t0 = time.time()
   tr = ShardTrainer(random_weights(cfg, shard, dev, seed=0), dev, lr=args.lr, max_seq=args.seq)
-  pt = DataParallelTrainer(tr, rank, world) if dp else PipelineTrainer(tr, rank, world, P2PTransport(rank, world))
+  pt = DataParallelTrainer(tr, rank, world) if dp else PipelineTrainer(tr, rank, world, P2PTransport(rank, world),
+                                                                      schedule=args.schedule)
   sync()
   print(f"[rank {rank}] layers {shard.start_layer}-{shard.end_layer} init {time.time() - t0:.1f}s", file=sys.stderr)
 
@@ -107,7 +109,7 @@ def main():
       "config": {"model": args.model, "seq_len": args.seq, "micro_batch": args.mb, "micro_batches": M,
                  "global_batch_tokens": M * args.mb * args.seq * (world if dp else 1),
                  "parallelism": (f"dp{world} (bucketed all-reduce overlapped with backward)" if dp else
-                                 f"pp{world} (GPipe, RCCL p2p)")},
+                                 f"pp{world} ({args.schedule}, RCCL p2p)")},
     }), flush=True)
   if world > 1:
     dist.barrier()

@@ -74,6 +74,8 @@ def build_parser() -> argparse.ArgumentParser:
   p.add_argument("--micro-batch", type=int, default=1, help="--ring: sequences per pipeline micro-batch")
   p.add_argument("--parallel", choices=("pp", "dp"), default="pp",
                  help="--ring: pp = layer pipeline over the GPUs; dp = a full replica per GPU, gradients all-reduced")
+  p.add_argument("--schedule", choices=("gpipe", "1f1b"), default="gpipe",
+                 help="--ring --parallel pp: micro-batch order (1f1b keeps at most N - rank activations alive)")
   p.add_argument("--no-api", action="store_true", help="Do not start the ChatGPT API on this peer")
   return p
 

@@ -11,6 +11,13 @@ One optimizer step = GPipe schedule over M micro-batches:
                                    -> send d act_i to r-1
   step            global grad-norm (all-reduce of squared norms) -> AdamW on every stage
 
+or (schedule="1f1b") the one-forward-one-backward order: rank r runs min(M, world - r - 1) warm-up
+forwards, then alternates F(i + warm-up) / B(i), then drains the remaining backwards.  Same gradients
+and the same bubble as GPipe, but at most world - r micro-batches' autograd graphs are alive on rank r
+instead of M, so long sequences / many micro-batches fit.  Upstream ranks always run further ahead,
+so a rank never blocks on a gradient whose producer is waiting for an activation it has not sent
+(activations and gradients travel on separate per-direction communicators, see comm.P2PTransport).
+
 Every rank issues its p2p operations in the same micro-batch order, so the per-communicator FIFO of
 RCCL never blocks a send behind a receive its peer has not posted.  Activations and gradients are
 bf16 [mb, L, D]; the loss is normalised by the global number of target tokens, so accumulated
@@ -35,7 +42,9 @@ class TrainBatch:
 
 
 class PipelineTrainer:
-  def __init__(self, trainer: ShardTrainer, rank: int, world: int, transport):
+  def __init__(self, trainer: ShardTrainer, rank: int, world: int, transport, schedule: str = "gpipe"):
+    assert schedule in ("gpipe", "1f1b"), schedule
+    self.schedule = schedule
     self.tr = trainer
     self.rank, self.world = rank, world
     self.t = transport
@@ -57,38 +66,56 @@ class PipelineTrainer:
       dist.all_reduce(t)
     return t
 
+  def _fwd(self, b: TrainBatch):
+    """Forward of one micro-batch (autograd graph kept); hands the activation to the next stage."""
+    mb, L = b.x.shape
+    if self.first:
+      inp = b.x.to(self.dev)
+    else:
+      inp = torch.empty(mb, L, self.D, dtype=torch.bfloat16, device=self.dev)
+      self.t.wait(self.t.irecv(inp, self.prev))
+    leaf, out = self.tr.forward_train(inp)
+    if not self.last:
+      self.t.isend(out.detach().contiguous(), self.next)
+    return leaf, out
+
+  def _bwd(self, b: TrainBatch, saved, denom: float, losses: list) -> None:
+    """Backward of one micro-batch (loss on the last stage, else the gradient from the next stage);
+    hands d(input) to the previous stage."""
+    leaf, out = saved
+    if self.last:
+      loss, gin = self.tr.backward_accumulate(leaf, out, target=b.y, length=b.lengths, denom=denom)
+      losses.append(loss)
+    else:
+      g = torch.empty_like(out, dtype=torch.bfloat16)
+      self.t.wait(self.t.irecv(g, self.next))
+      _, gin = self.tr.backward_accumulate(leaf, out, grad_out=g)
+    if not self.first:
+      self.t.isend(gin.to(torch.bfloat16).contiguous(), self.prev)
+
   def step(self, batches: List[TrainBatch]) -> Optional[float]:
     """One optimizer step over the micro-batches; returns the mean loss on the last stage (None
     elsewhere; also broadcast to rank 0 when world > 1)."""
     tr = self.tr
     tr.zero_grad()
     denom = float(sum(int(b.lengths.sum()) for b in batches))
-    saved = []
+    saved = {}
     losses = []
-    # ---- forward phase
-    for b in batches:
-      mb, L = b.x.shape
-      if self.first:
-        inp = b.x.to(self.dev)
-      else:
-        inp = torch.empty(mb, L, self.D, dtype=torch.bfloat16, device=self.dev)
-        self.t.wait(self.t.irecv(inp, self.prev))
-      leaf, out = tr.forward_train(inp)
-      if not self.last:
-        self.t.isend(out.detach().contiguous(), self.next)
-      saved.append((leaf, out))
-    # ---- backward phase
-    for b, (leaf, out) in zip(batches, saved):
-      if self.last:
-        loss, gin = tr.backward_accumulate(leaf, out, target=b.y, length=b.lengths, denom=denom)
-        losses.append(loss)
-      else:
-        g = torch.empty_like(out, dtype=torch.bfloat16)
-        self.t.wait(self.t.irecv(g, self.next))
-        _, gin = tr.backward_accumulate(leaf, out, grad_out=g)
-      if not self.first:
-        self.t.isend(gin.to(torch.bfloat16).contiguous(), self.prev)
-    saved.clear()
+    M = len(batches)
+    if self.schedule == "1f1b":
+      warm = min(M, self.world - self.rank - 1)
+      for i in range(warm):
+        saved[i] = self._fwd(batches[i])
+      for i in range(M - warm):
+        saved[i + warm] = self._fwd(batches[i + warm])
+        self._bwd(batches[i], saved.pop(i), denom, losses)
+      for i in range(M - warm, M):
+        self._bwd(batches[i], saved.pop(i), denom, losses)
+    else:
+      for i, b in enumerate(batches):
+        saved[i] = self._fwd(b)
+      for i, b in enumerate(batches):
+        self._bwd(b, saved.pop(i), denom, losses)
     self.t.drain()
     if self.tied_group is not None and self.tied_name is not None:
       p = tr.params[self.tied_name]

@@ -87,7 +87,7 @@ def _worker(rank: int, world: int, port: int, a: dict) -> None:
     if world > 1 and os.environ.get("XOT_HEARTBEAT", "1") == "1":  # parallel/health.py
       from ..parallel.health import HealthMonitor
       mon = HealthMonitor(rank, world, timeout=float(os.environ.get("XOT_HEARTBEAT_TIMEOUT", "30"))).start()
-    pt = PipelineTrainer(tr, rank, world, P2PTransport(rank, world, monitor=mon))
+    pt = PipelineTrainer(tr, rank, world, P2PTransport(rank, world, monitor=mon), schedule=a.get("schedule", "gpipe"))
   tok = _resolve_tokenizer(mdir if mdir is not None else (registry.get_repo(model, "ShardedInferenceEngine") or "byte"),
                            cfg.vocab_size)
   train, valid, test = load_dataset(a["data"] or DEFAULT_DATA, lambda s: tok.encode(s))
@@ -206,7 +206,7 @@ def run_ring(args) -> int:
   a = {"model": args.model_name or args.default_model, "command": args.command, "data": args.data,
        "batch_size": args.batch_size, "micro_batch": getattr(args, "micro_batch", 1), "iters": args.iters,
        "save_every": args.save_every, "save_dir": args.save_checkpoint_dir, "resume": args.resume_checkpoint,
-       "lr": args.lr, "parallel": getattr(args, "parallel", "pp")}
+       "lr": args.lr, "parallel": getattr(args, "parallel", "pp"), "schedule": getattr(args, "schedule", "gpipe")}
   if not a["model"]:
     print("Error: model name is required")
     return 1
