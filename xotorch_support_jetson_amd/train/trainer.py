@@ -126,14 +126,19 @@ class ShardTrainer:
     topw, topi = torch.topk(torch.softmax(logits, dim=-1), c.num_experts_per_tok, dim=-1)
     topw = topw / topw.sum(-1, keepdim=True)
     egu, edown = P[f"{i}.egu"], P[f"{i}.edown"]
-    out = torch.zeros(xn.shape[0], c.hidden_size, device=xn.device, dtype=torch.float32)
-    for e in range(c.num_experts):
-      tok, slot = (topi == e).nonzero(as_tuple=True)
-      if tok.numel() == 0:
-        continue
-      act = A.silu_mul((xn.index_select(0, tok) @ egu[e].t()).contiguous())
-      ye = act @ edown[e].t()
-      out = out.index_add(0, tok, ye.float() * topw[tok, slot].unsqueeze(1))
+    # group the (token, slot) pairs by expert: one gather, one host sync for the group sizes
+    flat = topi.reshape(-1)
+    order = torch.argsort(flat, stable=True)
+    tok = order // c.num_experts_per_tok
+    counts = torch.bincount(flat, minlength=c.num_experts).tolist()
+    xs = xn.index_select(0, tok)
+    ys, start = [], 0
+    for e, n in enumerate(counts):
+      if n:
+        ys.append(A.silu_mul((xs[start:start + n] @ egu[e].t()).contiguous()) @ edown[e].t())
+      start += n
+    y = torch.cat(ys).float() * topw.reshape(-1)[order].unsqueeze(1)
+    out = torch.zeros(xn.shape[0], c.hidden_size, device=xn.device, dtype=torch.float32).index_add(0, tok, y)
     return out.to(xn.dtype)
 
   def _mm(self, x: torch.Tensor, name: str, h: Optional[torch.Tensor] = None) -> torch.Tensor:
