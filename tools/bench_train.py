@@ -30,6 +30,8 @@ def main():
   ap = argparse.ArgumentParser()
   ap.add_argument("--gpus", type=int, default=1)
   ap.add_argument("--model", default="llama-3-8b")
+  ap.add_argument("--layers", type=int, default=0,
+                  help="stage-sized run: only this many layers (e.g. one pp8 stage's share); labelled in the output")
   ap.add_argument("--seq", type=int, default=2048)
   ap.add_argument("--mb", type=int, default=1, help="sequences per micro-batch")
   ap.add_argument("--microbatches", type=int, default=0, help="micro-batches per step (default max(8, 4N))")
@@ -54,6 +56,8 @@ def main():
   if world != args.gpus:
     raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
   cfg = preset(args.model)
+  if args.layers:
+    cfg = cfg.with_layers(args.layers)
   dp = args.parallel == "dp"
   if dp:
     from xotorch_support_jetson_amd.inference.shard import Shard
@@ -106,7 +110,7 @@ def main():
       "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 1), "higher_is_better": True,
       "scaling": "weak" if args.microbatches == 0 else "strong", "dtype": "bf16 (fp32 master + AdamW)",
       "data": "synthetic tokens, random-init weights", "losses": [round(l, 4) for l in losses],
-      "config": {"model": args.model, "seq_len": args.seq, "micro_batch": args.mb, "micro_batches": M,
+      "config": {"model": args.model + (f" ({args.layers} of {preset(args.model).num_layers} layers)" if args.layers else ""), "seq_len": args.seq, "micro_batch": args.mb, "micro_batches": M,
                  "global_batch_tokens": M * args.mb * args.seq * (world if dp else 1),
                  "parallelism": (f"dp{world} (bucketed all-reduce overlapped with backward)" if dp else
                                  f"pp{world} ({args.schedule}, RCCL p2p)")},

@@ -125,7 +125,9 @@ class ShardTrainer:
     logits = xn.float() @ P[f"{i}.router"].float().t()  # [T, E]
     topw, topi = torch.topk(torch.softmax(logits, dim=-1), c.num_experts_per_tok, dim=-1)
     topw = topw / topw.sum(-1, keepdim=True)
-    egu, edown = P[f"{i}.egu"], P[f"{i}.edown"]
+    # unbind once: its backward stacks the per-expert grads in one write (indexing egu[e] per expert would
+    # zero-fill and add a full [E, 2F, D] gradient for every expert)
+    egu, edown = P[f"{i}.egu"].unbind(0), P[f"{i}.edown"].unbind(0)
     # group the (token, slot) pairs by expert: one gather, one host sync for the group sizes
     flat = topi.reshape(-1)
     order = torch.argsort(flat, stable=True)
