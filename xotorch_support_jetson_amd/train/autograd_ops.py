@@ -220,6 +220,36 @@ class GradAcc:
     self.cb = None
 
 
+class StackAccFn(torch.autograd.Function):
+  """Per-expert views of an expert stack [E, R, C] whose backward adds each routed expert's gradient
+  straight into the stack's GradAcc buffer (zeroed once per step) and returns no gradient for the stack:
+  plain unbind would stack a full [E, R, C] gradient (zeros for idle experts) per micro-batch and
+  then add it into .grad."""
+
+  @staticmethod
+  def forward(ctx, w, acc):
+    ctx.acc = acc
+    ctx.set_materialize_grads(False)
+    return tuple(w[e] for e in range(w.shape[0]))
+
+  @staticmethod
+  def backward(ctx, *gs):
+    acc = ctx.acc
+    if acc.fresh:
+      acc.buf.zero_()
+      acc.fresh = False
+    for e, g in enumerate(gs):
+      if g is not None:
+        acc.buf[e].add_(g)
+    if acc.cb is not None:
+      acc.cb()
+    return None, None
+
+
+def unbind_acc(w, acc):
+  return StackAccFn.apply(w, acc)
+
+
 class LinearFn(torch.autograd.Function):
   """y = x @ W^T (+ h).  The backward accumulates dW = dy^T x straight into the weight's GradAcc buffer
   (the GEMM's beta = 1 after the first micro-batch) and returns no gradient for W, instead of

@@ -74,7 +74,7 @@ class ShardTrainer:
     self.acc: Dict[str, A.GradAcc] = {}
     if self.device.type == "cuda":
       for k in self.params:
-        if k.split(".")[-1] in ("qkv", "o", "gu", "down"):
+        if k.split(".")[-1] in ("qkv", "o", "gu", "down", "egu", "edown"):
           self.acc[k] = A.GradAcc(k, self.params[k])
     self.master = {k: p.detach().float().clone() for k, p in self.params.items()}
     self.m = {k: torch.zeros_like(v) for k, v in self.master.items()}
@@ -125,9 +125,14 @@ class ShardTrainer:
     logits = xn.float() @ P[f"{i}.router"].float().t()  # [T, E]
     topw, topi = torch.topk(torch.softmax(logits, dim=-1), c.num_experts_per_tok, dim=-1)
     topw = topw / topw.sum(-1, keepdim=True)
-    # unbind once: its backward stacks the per-expert grads in one write (indexing egu[e] per expert would
-    # zero-fill and add a full [E, 2F, D] gradient for every expert)
-    egu, edown = P[f"{i}.egu"].unbind(0), P[f"{i}.edown"].unbind(0)
+    # per-expert views, taken once per layer: indexing egu[e] per expert would zero-fill and add a full
+    # [E, 2F, D] gradient for every expert; on the GPU the routed experts' grads go straight into the
+    # stack's accumulation buffer (A.StackAccFn)
+    ea, da = self.acc.get(f"{i}.egu"), self.acc.get(f"{i}.edown")
+    if ea is not None and torch.is_grad_enabled():
+      egu, edown = A.unbind_acc(P[f"{i}.egu"], ea), A.unbind_acc(P[f"{i}.edown"], da)
+    else:
+      egu, edown = P[f"{i}.egu"].unbind(0), P[f"{i}.edown"].unbind(0)
     # group the (token, slot) pairs by expert: one gather, one host sync for the group sizes
     flat = topi.reshape(-1)
     order = torch.argsort(flat, stable=True)
