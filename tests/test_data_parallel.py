@@ -4,6 +4,7 @@ micro-batches (loss normalised by the global token count, so the summed gradient
 import os
 import socket
 
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -34,7 +35,7 @@ def _trainer():
   return ShardTrainer(random_weights(c, sh, "cpu", seed=3), "cpu", lr=LR)
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, split=(2, 2)):
   os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
   dist.init_process_group("gloo", rank=rank, world_size=world)
   try:
@@ -42,8 +43,9 @@ def _worker(rank, world, port, q):
     tr = _trainer()
     dp = DataParallelTrainer(tr, rank, world, bucket_mb=0.25)  # small buckets: several all-reduces
     assert len(dp.buckets) > 2
-    allb = _batches(4, 7)
-    losses = [dp.step(allb[2 * rank:2 * rank + 2]) for _ in range(2)]
+    allb = _batches(sum(split), 7)
+    lo = sum(split[:rank])
+    losses = [dp.step(allb[lo:lo + split[rank]]) for _ in range(2)]
     if rank == 0:
       q.put((losses, {k: v.clone().numpy() for k, v in tr.master.items()}))
   finally:
@@ -56,16 +58,19 @@ def _free_port():
     return s.getsockname()[1]
 
 
-def test_data_parallel_matches_single_process():
+@pytest.mark.parametrize("split", [(2, 2), (3, 1), (1, 0), (0, 2)])
+def test_data_parallel_matches_single_process(split):
+  """Even and uneven micro-batch counts per rank, including a rank with none (buckets fill in
+  a different order on a rank with no backward, so launches must follow the bucket list, not readiness)."""
   ref = _trainer()
   from xotorch_support_jetson_amd.parallel.comm import LoopbackTransport
   pt = PipelineTrainer(ref, 0, 1, LoopbackTransport(0, 1))
-  allb = _batches(4, 7)
+  allb = _batches(sum(split), 7)
   ref_losses = [pt.step(allb) for _ in range(2)]
   ctx = mp.get_context("spawn")
   q = ctx.Queue()
   port = _free_port()
-  procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+  procs = [ctx.Process(target=_worker, args=(r, 2, port, q, split)) for r in range(2)]
   for p in procs:
     p.start()
   try:

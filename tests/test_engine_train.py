@@ -123,6 +123,31 @@ def test_checkpoint_resharding(tmp_path):
   run(main())
 
 
+def test_checkpoint_selection_rejects_mixed_partitions(tmp_path):
+  """Files of one iteration from two runs with different layer splits overlap: loading must refuse
+  instead of letting sort order decide which copy of the shared layers wins; one complete
+  partition loads, a gap in the requested layers is reported."""
+  from xotorch_support_jetson_amd.train.checkpoint import select_checkpoint_files
+  d = tmp_path / MODEL
+  d.mkdir()
+
+  def touch(*names):
+    for n in names:
+      (d / n).write_bytes(b"")
+
+  touch(f"000-001-of-{N:03d}-000004.safetensors", f"002-{N - 1:03d}-of-{N:03d}-000004.safetensors",
+        f"000-{N - 1:03d}-of-{N:03d}-000002.safetensors")
+  it, files = select_checkpoint_files(tmp_path, Shard(MODEL, 1, 2, N))
+  assert it == 4 and [f.name[:7] for f in files] == ["000-001", f"002-{N - 1:03d}"]
+  touch(f"000-002-of-{N:03d}-000004.safetensors")  # a 3-layer first stage from another run
+  with pytest.raises(ValueError, match="overlap"):
+    select_checkpoint_files(tmp_path, Shard(MODEL, 0, N - 1, N))
+  (d / f"000-002-of-{N:03d}-000004.safetensors").unlink()
+  (d / f"002-{N - 1:03d}-of-{N:03d}-000004.safetensors").unlink()
+  with pytest.raises(FileNotFoundError, match="no file for layers"):
+    select_checkpoint_files(tmp_path, Shard(MODEL, 0, N - 1, N))
+
+
 def test_concurrent_requests_are_batched():
   """Concurrent requests on one peer run as one batched forward (mixed prefill lengths, then
   decode) and give the same logits as one-at-a-time execution."""

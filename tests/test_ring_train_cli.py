@@ -62,6 +62,23 @@ def test_ring_train_data_parallel(tmp_path):
   assert "resumed tiny-llama from iteration 2" in ev and "eval | loss=" in ev
 
 
+def test_ring_train_data_parallel_defaults_one_row_batches(tmp_path):
+  """The CLI defaults (--batch-size 1 --micro-batch 1) under `--parallel dp --gpus 2`: every batch leaves
+  one rank without rows; it must still join every bucket all-reduce in the same order."""
+  ds = tmp_path / "ds"
+  ds.mkdir()
+  for split, n in (("train", 5), ("valid", 2), ("test", 3)):
+    with open(ds / f"{split}.jsonl", "w") as f:
+      for i in range(n):
+        f.write(json.dumps({"text": f"Q: select b from u{i}? A: SELECT b FROM u{i}"}) + "\n")
+  out = _xot(["train", "tiny-llama", "--ring", "--gpus", "2", "--parallel", "dp", "--iters", "2", "--data", str(ds),
+              "--lr", "1e-3"], tmp_path)
+  losses = [float(l.split("loss:")[1].split(",")[0]) for l in out.splitlines() if l.startswith("epoch")]
+  assert len(losses) == 2 and losses[1] < losses[0]
+  ev = _xot(["eval", "tiny-llama", "--ring", "--gpus", "2", "--parallel", "dp", "--data", str(ds)], tmp_path)
+  assert "eval | loss=" in ev
+
+
 @pytest.mark.gpu
 def test_ring_train_gpu_single(gpu, tmp_path):
   """The same CLI on one MI355X (world 1: the HIP training kernels + fused AdamW)."""

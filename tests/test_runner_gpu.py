@@ -130,6 +130,43 @@ def test_fused_grad_accumulation_matches_autograd(gpu):
     assert rel < 0.05, (k, rel)
 
 
+@pytest.mark.parametrize("name", ["tiny-llama-d64", "tiny-mixtral"])
+def test_fused_grad_accumulation_values(gpu, name):
+  """The accumulated gradients themselves (not AdamW deltas, which barely react to a scaled gradient)
+  after 3 micro-batches: fused accumulation (LinearFn's beta = 1 GEMM; for the Mixtral expert stacks
+  StackAccFn's zero-once-then-add per routed expert) == plain autograd accumulation into .grad.  A
+  doubled or dropped micro-batch / expert gradient moves the ratio by >= 1/3."""
+  from xotorch_support_jetson_amd.train.trainer import ShardTrainer
+  c = preset(name)
+  sh = Shard(name, 0, c.num_layers - 1, c.num_layers)
+  g = torch.Generator().manual_seed(11)
+  batches = []
+  for _ in range(3):
+    x = torch.randint(0, c.vocab_size, (2, 48), generator=g)
+    batches.append((x, torch.roll(x, -1, 1), torch.tensor([48, 37])))
+  denom = float(sum(int(b[2].sum()) for b in batches))
+  w = random_weights(c, sh, gpu, seed=5)
+  grads = []
+  for fused in (True, False):
+    tr = ShardTrainer(w, gpu, lr=1e-3, max_seq=256)
+    if c.is_moe:
+      assert {f"0.egu", f"0.edown"} <= set(tr.acc)
+    if not fused:
+      tr.acc = {}
+    tr.zero_grad()
+    for x, y, ln in batches:
+      leaf, out = tr.forward_train(x)
+      tr.backward_accumulate(leaf, out, target=y, length=ln, denom=denom)
+    grads.append({k: v.detach().float().clone() for k, v in tr.grads().items()})
+  gf, gr = grads
+  assert set(gf) == set(gr), (set(gf) ^ set(gr))
+  for k in gr:
+    ref = gr[k]
+    rel = ((gf[k] - ref).norm() / (ref.norm() + 1e-12)).item()
+    scale = (gf[k].norm() / (ref.norm() + 1e-12)).item()
+    assert rel < 0.03 and abs(scale - 1) < 0.02, (k, rel, scale)
+
+
 def test_moe_training_gpu(gpu):
   """Mixtral-style fine-tuning on the GPU: the first AdamW step matches the CPU trainer on the same
   weights, loss falls, and weights trained from a decode-layout shard (pre-shuffled expert stacks) are

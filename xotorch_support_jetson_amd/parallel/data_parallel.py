@@ -18,6 +18,12 @@ token count so the summed gradients equal one big batch's):
                                                    reading the fp32 buckets directly
 Buckets follow reverse parameter order (the order backward produces them) and hold ~256 MB: xGMI
 all-reduce rings are per-link bandwidth bound, so a few large messages beat many small ones.
+
+Collective order.  Every rank must issue the bucket all-reduces in the same order, or RCCL pairs up
+unrelated buffers (gloo aborts with a size mismatch).  The order in which buckets *fill* depends on the
+rank's work (backward finishes the embedding last, a rank with no micro-batch fills nothing until the
+flush), so a full bucket is only marked ready; the launcher starts buckets strictly in list order,
+each as soon as it and every earlier bucket are ready.
 """
 from __future__ import annotations
 
@@ -38,6 +44,7 @@ class _Bucket:
   views: Dict[str, torch.Tensor] = field(default_factory=dict)
   done: set = field(default_factory=set)
   work: Optional[object] = None
+  ready: bool = False
 
 
 class DataParallelTrainer:
@@ -71,6 +78,7 @@ class DataParallelTrainer:
         cur.append(n)
         size += numel
     self._armed = False
+    self._next = 0  # first bucket not yet launched (launch order == list order on every rank)
     # autograd-accumulated parameters signal through post-accumulate-grad hooks, projections with fused
     # accumulation (trainer.acc, A.LinearFn) through their GradAcc callback
     self._hooks = [p.register_post_accumulate_grad_hook(self._hook(n)) for n, p in trainer.params.items()
@@ -83,7 +91,8 @@ class DataParallelTrainer:
     b.views[name].copy_(g)
     b.done.add(name)
     if len(b.done) == len(b.names):
-      self._launch(b)
+      b.ready = True
+      self._launch_ready()
 
   def _hook(self, name: str):
     def fn(p: torch.Tensor):
@@ -99,9 +108,13 @@ class DataParallelTrainer:
         self._ready(name, self.tr.acc[name].buf)
     return fn
 
-  def _launch(self, b: _Bucket) -> None:
-    if self.world > 1:
-      b.work = dist.all_reduce(b.flat, group=self.group, async_op=True)
+  def _launch_ready(self) -> None:
+    """Start every ready bucket whose predecessors have all started (same order on every rank)."""
+    while self._next < len(self.buckets) and self.buckets[self._next].ready:
+      b = self.buckets[self._next]
+      if self.world > 1:
+        b.work = dist.all_reduce(b.flat, group=self.group, async_op=True)
+      self._next += 1
 
   def _global_tokens(self, batches: List[TrainBatch]) -> float:
     n = torch.tensor([float(sum(int(b.lengths.sum()) for b in batches))], dtype=torch.float64)
@@ -111,12 +124,14 @@ class DataParallelTrainer:
     return float(n)
 
   def step(self, batches: List[TrainBatch]) -> float:
-    """One optimizer step over this rank's micro-batches; returns the global mean loss (every rank)."""
+    """One optimizer step over this rank's micro-batches (possibly none: the rank then contributes zero
+    gradients to every bucket); returns the global mean loss (every rank)."""
     tr = self.tr
     tr.zero_grad()
     denom = self._global_tokens(batches)
     for b in self.buckets:
-      b.done, b.work = set(), None
+      b.done, b.work, b.ready = set(), None, False
+    self._next = 0
     losses = []
     for i, mb in enumerate(batches):
       self._armed = i == len(batches) - 1
@@ -139,7 +154,9 @@ class DataParallelTrainer:
           else:
             b.views[n].zero_()
           b.done.add(n)
-        self._launch(b)
+        b.ready = True
+    self._launch_ready()
+    assert self._next == len(self.buckets)
     for b in self.buckets:
       if b.work is not None:
         b.work.wait()

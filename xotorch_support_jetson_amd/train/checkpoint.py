@@ -2,7 +2,10 @@
 
 File: {dir}/{model_id}/{start:03d}-{end:03d}-of-{n:03d}-{iteration:06d}.safetensors with HF tensor names
 (un-shuffled, gate/up split), so a checkpoint written by one partition can be loaded by any other:
-loading picks every tensor of the requested layer range from all shard files of the newest iteration.
+loading picks every tensor of the requested layer range from the shard files of the newest iteration.
+Those files must form ONE partition of the model (disjoint layer ranges, same layer count): files of
+the same iteration left by an earlier run with a different layer split would otherwise override each
+other's overlapping layers in sort order, so an overlap is an error, as is a gap in the requested layers.
 Optimizer state (fp32 master weights + AdamW moments + step) goes to a `.optim.safetensors` sidecar.
 `--resume-checkpoint DIR` (parsed but never read by the reference) resumes from the newest iteration.
 """
@@ -34,6 +37,28 @@ def list_checkpoints(directory: str | Path, model_id: str) -> List[Tuple[int, in
         s, e, n, it = map(int, m.groups())
         out.append((it, s, e, n, p))
   return sorted(out)
+
+
+def select_checkpoint_files(directory: str | Path, shard: Shard) -> Tuple[int, List[Path]]:
+  """(iteration, files) of the newest saved iteration for `shard.model_id`: one partition of the model
+  whose layer ranges are pairwise disjoint and cover the shard's layers."""
+  cks = list_checkpoints(directory, shard.model_id)
+  if not cks:
+    raise FileNotFoundError(f"no checkpoints for {shard.model_id} under {directory}")
+  it = cks[-1][0]
+  parts = sorted((s, e, n, p) for i, s, e, n, p in cks if i == it)
+  ns = {n for _, _, n, _ in parts}
+  if len(ns) != 1:
+    raise ValueError(f"iteration {it} of {shard.model_id} mixes models of {sorted(ns)} layers: {[p.name for *_, p in parts]}")
+  for (s0, e0, _, p0), (s1, e1, _, p1) in zip(parts, parts[1:]):
+    if s1 <= e0:
+      raise ValueError(f"iteration {it} of {shard.model_id}: {p0.name} and {p1.name} overlap (layers {s1}-{min(e0, e1)}); "
+                       "they come from runs with different layer splits -- keep one partition's files")
+  have = {l for s, e, _, _ in parts for l in range(s, e + 1)}
+  missing = [l for l in shard.layers() if l not in have]
+  if missing:
+    raise FileNotFoundError(f"iteration {it} of {shard.model_id} has no file for layers {missing[0]}..{missing[-1]}")
+  return it, [p for *_, p in parts]
 
 
 def save_shard_checkpoint(engine, shard: Shard, path: str | Path) -> Path:
@@ -73,11 +98,7 @@ def load_shard_checkpoint(engine, shard: Shard, path: str | Path) -> None:
   path = Path(path)
   cfg = engine.runner.config
   if path.is_dir():
-    cks = list_checkpoints(path, shard.model_id)
-    if not cks:
-      raise FileNotFoundError(f"no checkpoints for {shard.model_id} under {path}")
-    latest = cks[-1][0]
-    files = [p for it, s, e, n, p in cks if it == latest]
+    _, files = select_checkpoint_files(path, shard)
   else:
     files = [path]
   sd = _gather_tensors(files, shard, cfg.tie_word_embeddings)

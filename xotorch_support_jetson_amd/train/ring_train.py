@@ -61,15 +61,13 @@ def _worker(rank: int, world: int, port: int, a: dict) -> None:
     w = load_hf_weights(mdir, cfg, shard, dev)
   else:
     w = random_weights(cfg, shard, dev, seed=0)
-  if a.get("resume"):
-    files = ck.list_checkpoints(a["resume"], model)
-    if files:
-      latest = files[-1][0]
-      sd = ck._gather_tensors([p for it, s, e, n, p in files if it == latest], shard, cfg.tie_word_embeddings)
-      from ..models.weights import copy_weights_into, from_hf_state_dict
-      copy_weights_into(w, from_hf_state_dict(sd, cfg, shard, device=dev))
-      if rank == 0:
-        print(f"resumed {model} from iteration {latest}", flush=True)
+  if a.get("resume") and ck.list_checkpoints(a["resume"], model):
+    latest, files = ck.select_checkpoint_files(a["resume"], shard)  # one partition, no overlapping files
+    sd = ck._gather_tensors(files, shard, cfg.tie_word_embeddings)
+    from ..models.weights import copy_weights_into, from_hf_state_dict
+    copy_weights_into(w, from_hf_state_dict(sd, cfg, shard, device=dev))
+    if rank == 0:
+      print(f"resumed {model} from iteration {latest}", flush=True)
   tr = ShardTrainer(w, dev, lr=a["lr"], max_seq=4096)
   if a.get("resume"):  # optimizer state of this exact shard, when the partitioning is unchanged
     files = ck.list_checkpoints(a["resume"], model)
@@ -95,11 +93,16 @@ def _worker(rank: int, world: int, port: int, a: dict) -> None:
 
   def to_micro(batch):
     x, y, ln = batch
+    lo, hi = 0, x.shape[0]
+    if dp:  # data parallel: this rank's contiguous share of the rows (sizes differ by at most one; a
+      # batch with fewer rows than ranks leaves some ranks without work -- they still join every
+      # all-reduce, in the same order, with zero gradients: parallel/data_parallel.py)
+      lo, hi = rank * x.shape[0] // world, (rank + 1) * x.shape[0] // world
     out = []
-    for i in range(0, x.shape[0], mb):
-      out.append(TrainBatch(torch.from_numpy(x[i:i + mb]), torch.from_numpy(y[i:i + mb]),
-                            torch.from_numpy(ln[i:i + mb])))
-    return out[rank::world] if dp else out  # data parallel: every world-th micro-batch
+    for i in range(lo, hi, mb):
+      j = min(i + mb, hi)
+      out.append(TrainBatch(torch.from_numpy(x[i:j]), torch.from_numpy(y[i:j]), torch.from_numpy(ln[i:j])))
+    return out
 
   class _Shim:  # save_shard_checkpoint wants engine.runner.weights / engine.trainer
     pass
@@ -135,25 +138,22 @@ def _worker(rank: int, world: int, port: int, a: dict) -> None:
 def _train_epochs(a, pt, tr, w, shard, rank, world, dp, train, bs, to_micro, _Shim):
   from ..train import checkpoint as ck
   from ..train.dataset import iterate_batches
-  if True:
-    step = 0
-    for epoch in range(a["iters"]):
-      tot, n = 0.0, 0
-      for batch in iterate_batches(train, bs, train=True, seed=epoch):
-        loss = pt.step(to_micro(batch))
-        tot += loss * float(batch[2].sum())
-        n += int(batch[2].sum())
-        step += 1
-      if rank == 0:
-        print(f"epoch {epoch + 1}/{a['iters']}\t| loss: {tot / max(n, 1):.4f}, tokens: {n}", flush=True)
-      if a["save_every"] > 0 and (epoch + 1) % a["save_every"] == 0 and a["save_dir"] and (rank == 0 or not dp):
-        tr.sync_to_inference()
-        shim = _Shim()
-        shim.runner = type("R", (), {"weights": w})()
-        shim.trainer = tr
-        path = ck.checkpoint_path(a["save_dir"], shard, epoch + 1)
-        ck.save_shard_checkpoint(shim, shard, path)
-        print(f"[rank {rank}] saved {path}", flush=True)
+  for epoch in range(a["iters"]):
+    tot, n = 0.0, 0
+    for batch in iterate_batches(train, bs, train=True, seed=epoch):
+      loss = pt.step(to_micro(batch))
+      tot += loss * float(batch[2].sum())
+      n += int(batch[2].sum())
+    if rank == 0:
+      print(f"epoch {epoch + 1}/{a['iters']}\t| loss: {tot / max(n, 1):.4f}, tokens: {n}", flush=True)
+    if a["save_every"] > 0 and (epoch + 1) % a["save_every"] == 0 and a["save_dir"] and (rank == 0 or not dp):
+      tr.sync_to_inference()
+      shim = _Shim()
+      shim.runner = type("R", (), {"weights": w})()
+      shim.trainer = tr
+      path = ck.checkpoint_path(a["save_dir"], shard, epoch + 1)
+      ck.save_shard_checkpoint(shim, shard, path)
+      print(f"[rank {rank}] saved {path}", flush=True)
 
 
 @torch.no_grad()
