@@ -26,6 +26,15 @@ def _hf_model(kind, tmp_path):
   elif kind == "qwen2":
     cfg = transformers.Qwen2Config(**common, rope_theta=1000000.0, tie_word_embeddings=False)
     m = transformers.Qwen2ForCausalLM(cfg)
+  elif kind.startswith("phi3"):
+    # partial rotary (48 of 64 dims), LongRoPE: past an 8-token window the sequence uses the long factors;
+    # phi3-short stays inside a 64-token window (short factors)
+    cfg = transformers.Phi3Config(**common, tie_word_embeddings=True, partial_rotary_factor=0.75, pad_token_id=0,
+                                  bos_token_id=1, eos_token_id=2,
+                                  original_max_position_embeddings=8 if kind == "phi3" else 64,
+                                  rope_scaling={"type": "longrope", "short_factor": [1.0 + 0.1 * i for i in range(24)],
+                                                "long_factor": [3.0 + 0.2 * i for i in range(24)]})
+    m = transformers.Phi3ForCausalLM(cfg)
   else:
     cfg = transformers.MixtralConfig(**common, num_local_experts=4, num_experts_per_tok=2, rope_theta=1e6)
     m = transformers.MixtralForCausalLM(cfg)
@@ -36,12 +45,27 @@ def _hf_model(kind, tmp_path):
         p.uniform_(0.5, 1.5)
       elif "bias" in n:
         p.normal_(0, 0.1)
+      elif "q_proj" in n or "qkv_proj" in n:
+        p.mul_(6.0)  # peaked attention, so positions (RoPE) visibly change the logits
   d = tmp_path / kind
   m.save_pretrained(str(d), safe_serialization=True)
   return m, d
 
 
-@pytest.mark.parametrize("kind", ["llama", "qwen2", "mixtral"])
+def test_phi3_checkpoint_roundtrip(tmp_path):
+  """Fused HF names and the partial-rotary q/k row permutation survive to_hf_state_dict -> load."""
+  hf, d = _hf_model("phi3", tmp_path)
+  c = load_config(d)
+  sw = load_hf_weights(d, c, Shard("phi3", 0, 2, 3), dtype=torch.float32)
+  sd = sw.to_hf_state_dict()
+  ref = {k: v for k, v in hf.state_dict().items()}
+  for k, v in sd.items():
+    assert k in ref, k
+    torch.testing.assert_close(v, ref[k].float(), rtol=0, atol=0)
+  assert "model.layers.0.self_attn.qkv_proj.weight" in sd and "model.layers.0.mlp.gate_up_proj.weight" in sd
+
+
+@pytest.mark.parametrize("kind", ["llama", "qwen2", "mixtral", "phi3", "phi3-short"])
 def test_hf_parity(kind, tmp_path):
   hf, d = _hf_model(kind, tmp_path)
   c = load_config(d)

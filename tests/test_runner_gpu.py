@@ -11,7 +11,7 @@ from xotorch_support_jetson_amd.runtime.runner import ShardRunner
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("name", ["tiny-llama-d64", "tiny-qwen", "tiny-mixtral"])
+@pytest.mark.parametrize("name", ["tiny-llama-d64", "tiny-qwen", "tiny-mixtral", "tiny-phi3"])
 def test_split_equals_full_gpu(gpu, name):
   c = preset(name)
   L = c.num_layers

@@ -33,10 +33,16 @@ class ModelConfig:
   num_experts_per_tok: int = 0
   bos_token_id: int = 128000
   eos_token_ids: tuple = (128001, 128009)
+  partial_rotary_factor: float = 1.0  # Phi-3: RoPE on the first 75 % of each head's dims
 
   @property
   def qkv_size(self) -> int:
     return (self.num_heads + 2 * self.num_kv_heads) * self.head_dim
+
+  @property
+  def rotary_dim(self) -> int:
+    r = int(self.head_dim * self.partial_rotary_factor)
+    return r - (r % 2)
 
   @property
   def is_moe(self) -> bool:
@@ -61,12 +67,37 @@ class ModelConfig:
     return replace(self, num_layers=n)
 
 
+def _rope_fields(cfg: dict) -> tuple:
+  """(theta, scaling dict or None, partial_rotary_factor) from either config.json flavour: the hub's
+  top-level `rope_theta` + `rope_scaling`, or transformers-5's `rope_parameters` (theta inside)."""
+  rp = cfg.get("rope_parameters") or {}
+  theta = float(cfg.get("rope_theta", rp.get("rope_theta", 10000.0)))
+  partial = float(cfg.get("partial_rotary_factor", rp.get("partial_rotary_factor", 1.0)) or 1.0)
+  scaling = cfg.get("rope_scaling")
+  if not scaling and rp:
+    scaling = {k: v for k, v in rp.items() if k not in ("rope_theta", "partial_rotary_factor")}
+  if scaling:
+    kind = scaling.get("rope_type", scaling.get("type", "default"))
+    if kind in ("su", "longrope"):  # Phi-3 LongRoPE: needs the pretraining window and the extended one
+      scaling = dict(scaling, rope_type="longrope",
+                     original_max_position_embeddings=int(scaling.get("original_max_position_embeddings")
+                                                          or cfg.get("original_max_position_embeddings", 4096)),
+                     max_position_embeddings=int(cfg.get("max_position_embeddings", 131072)))
+    elif kind in ("default", None):
+      scaling = None
+  return theta, (scaling or None), partial
+
+
 def from_hf_config(cfg: dict) -> ModelConfig:
   mt = cfg.get("model_type", "llama")
   H = int(cfg["num_attention_heads"])
   D = int(cfg["hidden_size"])
   eos = cfg.get("eos_token_id")
   eos_ids = tuple(eos) if isinstance(eos, (list, tuple)) else ((int(eos),) if eos is not None else (2,))
+  theta, scaling, partial = _rope_fields(cfg)
+  if cfg.get("sliding_window") and mt == "phi3":
+    import warnings
+    warnings.warn(f"phi3 sliding_window={cfg['sliding_window']} is not applied (full causal attention)")
   return ModelConfig(
     model_type=mt,
     vocab_size=int(cfg["vocab_size"]),
@@ -77,8 +108,8 @@ def from_hf_config(cfg: dict) -> ModelConfig:
     num_kv_heads=int(cfg.get("num_key_value_heads", H)),
     head_dim=int(cfg.get("head_dim") or D // H),
     rms_norm_eps=float(cfg.get("rms_norm_eps", 1e-5)),
-    rope_theta=float(cfg.get("rope_theta", 10000.0)),
-    rope_scaling=cfg.get("rope_scaling"),
+    rope_theta=theta,
+    rope_scaling=scaling,
     max_position_embeddings=int(cfg.get("max_position_embeddings", 8192)),
     tie_word_embeddings=bool(cfg.get("tie_word_embeddings", False)),
     attention_bias=bool(cfg.get("attention_bias", mt == "qwen2")),
@@ -86,6 +117,7 @@ def from_hf_config(cfg: dict) -> ModelConfig:
     num_experts_per_tok=int(cfg.get("num_experts_per_tok", 0)),
     bos_token_id=int(cfg.get("bos_token_id", 1) or 1),
     eos_token_ids=eos_ids,
+    partial_rotary_factor=partial,
   )
 
 
@@ -129,6 +161,15 @@ PRESETS: dict[str, ModelConfig] = {
                               num_experts=8, num_experts_per_tok=2, bos_token_id=1, eos_token_ids=(2,)),
   "mistral-nemo": ModelConfig("mistral", 131072, 5120, 14336, 40, 32, 8, 128, 1e-5, 1000000.0, None, 131072, False,
                               bos_token_id=1, eos_token_ids=(2,)),
+  # Phi-4-mini (HF Phi3ForCausalLM): fused qkv / gate_up checkpoints, RoPE on 96 of 128 head dims, LongRoPE.
+  # The hub config's 48 short / long LongRoPE factors are not available offline: the preset uses unit
+  # factors (plain RoPE inside the 4k pretraining window, same attention factor); a downloaded config.json
+  # carries the real ones.
+  "phi-4-mini-instruct": ModelConfig("phi3", 200064, 3072, 8192, 32, 24, 8, 128, 1e-5, 10000.0,
+                                     dict(rope_type="longrope", short_factor=[1.0] * 48, long_factor=[1.0] * 48,
+                                          original_max_position_embeddings=4096, max_position_embeddings=131072),
+                                     131072, True, bos_token_id=199999, eos_token_ids=(199999, 200020),
+                                     partial_rotary_factor=0.75),
   # small shapes for tests / CPU plumbing
   "tiny-llama": ModelConfig("llama", 512, 256, 512, 4, 4, 2, 64, 1e-5, 10000.0, None, 2048, False,
                             bos_token_id=1, eos_token_ids=(2,)),
@@ -138,6 +179,11 @@ PRESETS: dict[str, ModelConfig] = {
                            bos_token_id=1, eos_token_ids=(2,)),
   "tiny-mixtral": ModelConfig("mixtral", 512, 256, 512, 4, 4, 2, 64, 1e-5, 10000.0, None, 2048, False,
                               num_experts=4, num_experts_per_tok=2, bos_token_id=1, eos_token_ids=(2,)),
+  "tiny-phi3": ModelConfig("phi3", 512, 256, 512, 4, 2, 1, 128, 1e-5, 10000.0,
+                           dict(rope_type="longrope", short_factor=[1.0 + 0.05 * i for i in range(48)],
+                                long_factor=[2.0 + 0.1 * i for i in range(48)], original_max_position_embeddings=64,
+                                max_position_embeddings=2048), 2048, True, bos_token_id=1, eos_token_ids=(2,),
+                           partial_rotary_factor=0.75),
 }
 # aliases of the reference's model cards that share an architecture
 for _alias, _base in {"llama-3.1-70b-bf16": "llama-3.1-70b", "nemotron-70b": "llama-3.1-70b",

@@ -61,6 +61,7 @@ _CARDS: List[tuple] = [
   ("tiny-llama-d64", 6, "synthetic/tiny-llama-d64", "Tiny Llama d64 (synthetic)"),
   ("tiny-qwen", 4, "synthetic/tiny-qwen", "Tiny Qwen (synthetic)"),
   ("tiny-mixtral", 4, "synthetic/tiny-mixtral", "Tiny Mixtral (synthetic)"),
+  ("tiny-phi3", 4, "synthetic/tiny-phi3", "Tiny Phi-3 (synthetic)"),
 ]
 
 model_cards: Dict[str, dict] = {mid: {"layers": n, "repo": {ENGINE: repo}} for mid, n, repo, _ in _CARDS}

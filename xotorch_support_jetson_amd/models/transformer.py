@@ -29,7 +29,7 @@ from ..inference.shard import Shard
 from ..ops import kernels as K
 from ..ops._ext import require
 from ..ops.linear import layout_of, linear, linear_resid_norm, linear_rope_kv
-from ..ops.rope import build_cos_sin
+from ..ops.rope import longrope_window, rope_shift, rope_table
 from .config import ModelConfig
 from .weights import ShardWeights, expert
 
@@ -87,7 +87,8 @@ class ShardModel:
     c = self.c
     self.scale = 1.0 / math.sqrt(c.head_dim)
     max_pos = max(max_ctx, 16)
-    self.cos_sin = build_cos_sin(c.head_dim, max_pos, c.rope_theta, c.rope_scaling, self.device)
+    self.cos_sin = rope_table(c, max_pos, self.device)
+    self.rope_rows, self.rope_window = max_pos, longrope_window(c)
     self.layer_ids: List[int] = list(self.shard.layers())
     self.max_batch = max_batch
     self.max_ctx = max_ctx
@@ -98,6 +99,12 @@ class ShardModel:
     # and forward returns (logits, normed hidden)
     self.head_rows: Optional[int] = None
     self._head_cache = None
+
+  def rope_pos(self, start: int, n: int) -> range:
+    """RoPE table rows of a step's n new tokens at positions start.. (LongRoPE: the long-factor half
+    once the sequence outgrows the pretraining window; positions only feed the RoPE kernels)."""
+    o = rope_shift(self.rope_window, self.rope_rows, start + n)
+    return range(start + o, start + n + o)
 
   # ------------------------------------------------------------------ helpers
   def _attention(self, q: torch.Tensor, li: int, inp: StepInputs) -> torch.Tensor:

@@ -87,12 +87,19 @@ class ShardWeights:
     c = self.config
     H, Hkv, Dh = c.num_heads, c.num_kv_heads, c.head_dim
     sd: Dict[str, torch.Tensor] = {}
+    from ..ops.rope import permute_qk_rows
+    fused = c.model_type == "phi3"  # Phi-3 checkpoints keep qkv_proj / gate_up_proj fused
     for i, lw in self.layers.items():
       p = f"model.layers.{i}."
-      q, k, v = _rowmajor(lw.qkv_w).split([H * Dh, Hkv * Dh, Hkv * Dh], 0)
-      sd[p + "self_attn.q_proj.weight"], sd[p + "self_attn.k_proj.weight"], sd[p + "self_attn.v_proj.weight"] = q, k, v
+      qkv_w = permute_qk_rows(_rowmajor(lw.qkv_w), H, Hkv, Dh, c.rotary_dim, inverse=True)
+      if fused:
+        sd[p + "self_attn.qkv_proj.weight"] = qkv_w
+      else:
+        q, k, v = qkv_w.split([H * Dh, Hkv * Dh, Hkv * Dh], 0)
+        sd[p + "self_attn.q_proj.weight"], sd[p + "self_attn.k_proj.weight"], sd[p + "self_attn.v_proj.weight"] = q, k, v
       if lw.qkv_b is not None:
-        qb, kb, vb = lw.qkv_b.split([H * Dh, Hkv * Dh, Hkv * Dh], 0)
+        qkv_b = permute_qk_rows(lw.qkv_b, H, Hkv, Dh, c.rotary_dim, inverse=True)
+        qb, kb, vb = qkv_b.split([H * Dh, Hkv * Dh, Hkv * Dh], 0)
         sd[p + "self_attn.q_proj.bias"], sd[p + "self_attn.k_proj.bias"], sd[p + "self_attn.v_proj.bias"] = qb, kb, vb
       sd[p + "self_attn.o_proj.weight"] = _rowmajor(lw.o_w)
       sd[p + "input_layernorm.weight"] = lw.ln1
@@ -107,7 +114,10 @@ class ShardWeights:
           sd[p + f"block_sparse_moe.experts.{e}.w2.weight"] = down[e]
       else:
         g, u = split_gate_up(gu)
-        sd[p + "mlp.gate_proj.weight"], sd[p + "mlp.up_proj.weight"] = g, u
+        if fused:
+          sd[p + "mlp.gate_up_proj.weight"] = torch.cat([g, u], 0)
+        else:
+          sd[p + "mlp.gate_proj.weight"], sd[p + "mlp.up_proj.weight"] = g, u
         sd[p + "mlp.down_proj.weight"] = down
     if self.embed is not None:
       sd["model.embed_tokens.weight"] = self.embed
@@ -322,13 +332,19 @@ def load_hf_weights(model_dir: str | Path, c: ModelConfig, shard: Shard, device=
   def has(name: str) -> bool:
     return name in wm
 
+  from ..ops.rope import permute_qk_rows
+  H, Hkv, Dh, R = c.num_heads, c.num_kv_heads, c.head_dim, c.rotary_dim
   sw = ShardWeights(c, shard)
   for i in shard.layers():
     p = f"model.layers.{i}."
-    qkv = torch.cat([get(p + f"self_attn.{n}_proj.weight") for n in "qkv"], 0)
+    if has(p + "self_attn.qkv_proj.weight"):  # Phi-3: fused [q; k; v]
+      qkv = get(p + "self_attn.qkv_proj.weight")
+    else:
+      qkv = torch.cat([get(p + f"self_attn.{n}_proj.weight") for n in "qkv"], 0)
+    qkv = permute_qk_rows(qkv, H, Hkv, Dh, R)  # partial rotary: HF dim order -> the kernels' pair order
     qkv_b = None
     if has(p + "self_attn.q_proj.bias"):
-      qkv_b = torch.cat([get(p + f"self_attn.{n}_proj.bias") for n in "qkv"], 0)
+      qkv_b = permute_qk_rows(torch.cat([get(p + f"self_attn.{n}_proj.bias") for n in "qkv"], 0), H, Hkv, Dh, R)
     if c.is_moe:
       pm = p + "block_sparse_moe."
       gu = torch.stack([interleave_gate_up(get(pm + f"experts.{e}.w1.weight"), get(pm + f"experts.{e}.w3.weight"))
@@ -336,7 +352,11 @@ def load_hf_weights(model_dir: str | Path, c: ModelConfig, shard: Shard, device=
       down = torch.stack([get(pm + f"experts.{e}.w2.weight") for e in range(c.num_experts)])
       router = get(pm + "gate.weight")
     else:
-      gu = interleave_gate_up(get(p + "mlp.gate_proj.weight"), get(p + "mlp.up_proj.weight"))
+      if has(p + "mlp.gate_up_proj.weight"):  # Phi-3: fused [gate; up]
+        gate, up = get(p + "mlp.gate_up_proj.weight").chunk(2, 0)
+      else:
+        gate, up = get(p + "mlp.gate_proj.weight"), get(p + "mlp.up_proj.weight")
+      gu = interleave_gate_up(gate, up)
       down = get(p + "mlp.down_proj.weight")
       router = None
     sw.layers[i] = LayerWeights(qkv.contiguous(), get(p + "self_attn.o_proj.weight"), gu.contiguous(), down,

@@ -1,14 +1,22 @@
 """Rotary-embedding tables (host-built once per model, consumed by the RoPE kernels).
 
 Supports plain RoPE (Qwen2/Mistral/Llama-3 without scaling), Llama-3.1/3.2 "llama3" frequency
-scaling and linear scaling.  The reference picks torchtune RoPE classes by model-id substring and
-reads the wrong config key ("rope_factor") for Llama scaling (xotorch/inference/torch/models/
-general_mha.py:33-63, llm_utils.py:68-69); here the HF `rope_scaling` dict is honoured as written and
-a missing dict means no scaling (so Llama-3-8B/70B build; the reference KeyErrors on them).
+scaling, linear scaling and Phi-3 LongRoPE with partial rotary dims.  The reference picks torchtune
+RoPE classes by model-id substring and reads the wrong config key ("rope_factor") for Llama scaling
+(xotorch/inference/torch/models/general_mha.py:33-63, llm_utils.py:68-69); here the HF `rope_scaling`
+dict is honoured as written and a missing dict means no scaling (so Llama-3-8B/70B build; the reference
+KeyErrors on them).
+
+Partial rotary (Phi-3: the first R = 0.75 Dh dims of a head rotate as pairs (j, j + R/2), the rest pass
+through) needs no kernel variant: the q / k projection rows of every head are permuted at load time
+(`rope_perm`) so that HF dim pairs (j, j + R/2) land on the kernels' pairs (p, p + Dh/2), and the table
+holds cos = 1, sin = 0 on the pass-through pairs.  q . k is invariant under the same permutation of both,
+V is untouched, so attention outputs are exactly HF's; checkpoints are written back in HF order.
 """
 from __future__ import annotations
 
 import math
+from typing import Optional
 
 import torch
 
@@ -36,9 +44,84 @@ def inv_frequencies(head_dim: int, theta: float, scaling: dict | None) -> torch.
 
 
 def build_cos_sin(head_dim: int, max_pos: int, theta: float = 10000.0, scaling: dict | None = None,
-                  device: torch.device | str = "cpu") -> torch.Tensor:
-  """[max_pos, head_dim] fp32 table, row p = [cos(p*f_0..f_{h-1}) | sin(p*f_0..f_{h-1})]."""
-  inv = inv_frequencies(head_dim, theta, scaling)
+                  device: torch.device | str = "cpu", rotary_dim: Optional[int] = None) -> torch.Tensor:
+  """[max_pos, head_dim] fp32 table, row p = [cos(p*f_0..f_{h-1}) | sin(p*f_0..f_{h-1})], h = head_dim / 2.
+  With rotary_dim R < head_dim only the first R/2 frequency slots rotate (the rest are cos 1 / sin 0)."""
+  R = rotary_dim or head_dim
   pos = torch.arange(max_pos, dtype=torch.float64)
-  ang = torch.outer(pos, inv)
-  return torch.cat([ang.cos(), ang.sin()], dim=1).to(torch.float32).to(device).contiguous()
+  kind = (scaling or {}).get("rope_type", (scaling or {}).get("type", "default"))
+  if kind == "longrope":
+    # HF _compute_longrope_parameters: short_factor while the sequence fits the pretraining window,
+    # long_factor beyond it (which one a step uses: rope_shift); cos / sin carry the attention factor
+    orig = int(scaling["original_max_position_embeddings"])
+    factor = scaling.get("factor") or float(scaling.get("max_position_embeddings", orig)) / orig
+    attn = scaling.get("attention_factor")
+    if attn is None:
+      attn = 1.0 if factor <= 1.0 else math.sqrt(1 + math.log(factor) / math.log(orig))
+    base = theta ** (torch.arange(0, R, 2, dtype=torch.float64) / R)
+    inv_s = 1.0 / (torch.tensor(scaling["short_factor"], dtype=torch.float64) * base)
+    inv_l = 1.0 / (torch.tensor(scaling["long_factor"], dtype=torch.float64) * base)
+    # rows [0, max_pos): short factors; rows [max_pos, 2 max_pos): long factors (rope_shift picks)
+    ang = torch.cat([torch.outer(pos, inv_s), torch.outer(pos, inv_l)], 0)
+    cos, sin = ang.cos() * attn, ang.sin() * attn
+  else:
+    ang = torch.outer(pos, inv_frequencies(R, theta, scaling))
+    cos, sin = ang.cos(), ang.sin()
+  if R < head_dim:
+    pad = head_dim // 2 - R // 2
+    cos = torch.cat([cos, torch.ones(cos.shape[0], pad, dtype=cos.dtype)], 1)
+    sin = torch.cat([sin, torch.zeros(sin.shape[0], pad, dtype=sin.dtype)], 1)
+  return torch.cat([cos, sin], dim=1).to(torch.float32).to(device).contiguous()
+
+
+def rope_table(c, max_pos: int, device: torch.device | str = "cpu") -> torch.Tensor:
+  """The table for a ModelConfig (rotary dims, scaling and theta from the config).  LongRoPE tables
+  hold 2 max_pos rows: the short-factor rows, then the long-factor rows (see rope_shift)."""
+  return build_cos_sin(c.head_dim, max_pos, c.rope_theta, c.rope_scaling, device, rotary_dim=c.rotary_dim)
+
+
+def longrope_window(c) -> Optional[int]:
+  s = c.rope_scaling or {}
+  if s.get("rope_type") == "longrope":
+    return int(s["original_max_position_embeddings"])
+  return None
+
+
+def rope_shift(window: Optional[int], max_pos: int, total_len: int) -> int:
+  """Row offset into a LongRoPE table for a step that leaves a sequence `total_len` tokens long.
+  HF Phi-3 rotates a whole forward with the long factors once its sequence exceeds the pretraining
+  window (Phi3ForCausalLM.prepare_inputs_for_generation even recomputes the cache at the switch); here a
+  step's new tokens follow the same rule, so a prompt longer than the window prefills entirely with the
+  long factors (= HF).  Deviation: the keys cached before a sequence crosses the window mid-generation
+  keep their short-factor rotation (HF re-runs the prefix at that single token)."""
+  return max_pos if window is not None and total_len > window else 0
+
+
+def rope_perm(head_dim: int, rotary_dim: int) -> Optional[torch.Tensor]:
+  """Kernel-order dim p of a head <- HF dim perm[p] (None when every dim rotates)."""
+  Dh, R = head_dim, rotary_dim
+  if R >= Dh:
+    return None
+  h, r = Dh // 2, R // 2
+  perm = []
+  for p in range(Dh):
+    q = p if p < h else p - h
+    if q < r:
+      perm.append(q + (0 if p < h else r))
+    else:
+      perm.append(R + (q - r) + (0 if p < h else h - r))
+  return torch.tensor(perm, dtype=torch.long)
+
+
+def permute_qk_rows(qkv: torch.Tensor, H: int, Hkv: int, Dh: int, R: int, inverse: bool = False) -> torch.Tensor:
+  """Apply rope_perm to the q and k rows of a fused [(H + 2 Hkv) Dh, ...] projection weight / bias."""
+  perm = rope_perm(Dh, R)
+  if perm is None:
+    return qkv
+  if inverse:
+    perm = torch.argsort(perm)
+  nqk = (H + Hkv) * Dh
+  idx = (torch.arange(H + Hkv)[:, None] * Dh + perm[None, :]).reshape(-1).to(qkv.device)
+  out = qkv.clone()
+  out[:nqk] = qkv[:nqk].index_select(0, idx)
+  return out

@@ -125,7 +125,7 @@ class ShardRunner:
       if start + n > self.max_ctx:
         raise ValueError(f"request {rid}: context {start + n} exceeds max_ctx {self.max_ctx}")
       slots += self.bm.append(rid, n)
-      pos += range(start, start + n)
+      pos += self.model.rope_pos(start, n)
       cu.append(cu[-1] + n)
     B = len(rids)
     self.bm.fill_batch(list(rids), self._tables_host[:B].numpy(), self._ctx_host[:B].numpy())
@@ -170,7 +170,7 @@ class ShardRunner:
       if start + 1 > self.max_ctx:
         raise ValueError(f"request {rid}: context exceeds max_ctx {self.max_ctx}")
       slots += self.bm.append(rid, 1)
-      pos.append(start)
+      pos += self.model.rope_pos(start, 1)
     self.bm.fill_batch(list(rids), self._tables_host[:B].numpy(), self._ctx_host[:B].numpy())
     pad = Bp - B
     g["pos"].copy_(torch.tensor(pos + [0] * pad, dtype=torch.int32), non_blocking=True)

@@ -26,7 +26,7 @@ import torch.nn.functional as F
 from ..models.config import ModelConfig
 from ..models.weights import ShardWeights, _rowmajor, interleave_gate_up, split_gate_up
 from ..ops._ext import require
-from ..ops.rope import build_cos_sin
+from ..ops.rope import longrope_window, rope_shift, rope_table
 from . import autograd_ops as A
 
 
@@ -46,7 +46,8 @@ class ShardTrainer:
     self.grad_clip = grad_clip
     self.step_count = 0
     self.dirty = False
-    self.cos_sin = build_cos_sin(self.c.head_dim, max_seq, self.c.rope_theta, self.c.rope_scaling, self.device)
+    self.cos_sin = rope_table(self.c, max_seq, self.device)
+    self.max_seq = max_seq
     # training parameters (row-major, gate|up halves), bf16 leaves + fp32 master + moments
     self.params: Dict[str, torch.Tensor] = {}
     for i, lw in weights.layers.items():
@@ -94,7 +95,9 @@ class ShardTrainer:
     else:
       h = x.to(torch.bfloat16)
     B, L = h.shape[0], h.shape[1]
-    pos = torch.arange(L, device=self.device, dtype=torch.int32).repeat(B)
+    # (LongRoPE: a training sequence longer than the pretraining window rotates with the long factors, as HF)
+    shift = rope_shift(longrope_window(self.c), self.max_seq, L)
+    pos = (torch.arange(L, device=self.device, dtype=torch.int32) + shift).repeat(B)
     h = h.reshape(B * L, D)
     for i in self.shard.layers():
       xn = A.rmsnorm(h, P[f"{i}.ln1"], c.rms_norm_eps)
