@@ -21,7 +21,7 @@ def test_hf_parity_gpu(gpu, tmp_path):
   from xotorch_support_jetson_amd.models.config import load_config
   from xotorch_support_jetson_amd.models.weights import load_hf_weights
   from xotorch_support_jetson_amd.runtime.runner import ShardRunner
-  for kind in ("llama", "qwen2", "phi3"):
+  for kind in ("llama", "qwen2", "phi3", "deepseek_v2", "deepseek_v3"):
     hf, d = _hf_model(kind, tmp_path)
     c = load_config(d)
     L = 40

@@ -35,6 +35,27 @@ def _hf_model(kind, tmp_path):
                                   rope_scaling={"type": "longrope", "short_factor": [1.0 + 0.1 * i for i in range(24)],
                                                 "long_factor": [3.0 + 0.2 * i for i in range(24)]})
     m = transformers.Phi3ForCausalLM(cfg)
+  elif kind == "deepseek_v2":
+    # MLA without q_lora, dense first layer, 8 routed experts in 4 groups (group-limited greedy), 2 shared
+    cfg = transformers.DeepseekV2Config(**dict(common, num_key_value_heads=4), moe_intermediate_size=256,
+                                        n_routed_experts=8, n_shared_experts=2, num_experts_per_tok=2,
+                                        first_k_dense_replace=1, kv_lora_rank=256, q_lora_rank=None,
+                                        qk_nope_head_dim=64, qk_rope_head_dim=64, v_head_dim=64,
+                                        topk_method="group_limited_greedy", n_group=4, topk_group=2,
+                                        routed_scaling_factor=1.5, pad_token_id=0, bos_token_id=1, eos_token_id=2)
+    m = transformers.DeepseekV2ForCausalLM(cfg)
+  elif kind == "deepseek_v3":
+    # MLA with q_lora, sigmoid scores + selection bias, top-2-sum groups, renormalised x 2.5, YaRN rope
+    cfg = transformers.DeepseekV3Config(**dict(common, num_key_value_heads=4), moe_intermediate_size=256,
+                                        n_routed_experts=16, n_shared_experts=1, num_experts_per_tok=4,
+                                        first_k_dense_replace=1, kv_lora_rank=256, q_lora_rank=128,
+                                        qk_nope_head_dim=64, qk_rope_head_dim=64, v_head_dim=64, n_group=4,
+                                        topk_group=2, routed_scaling_factor=2.5, norm_topk_prob=True,
+                                        rope_scaling={"type": "yarn", "factor": 4.0, "original_max_position_embeddings": 16,
+                                                      "beta_fast": 32, "beta_slow": 1, "mscale": 0.707,
+                                                      "mscale_all_dim": 1.0},
+                                        pad_token_id=0, bos_token_id=1, eos_token_id=2)
+    m = transformers.DeepseekV3ForCausalLM(cfg)
   else:
     cfg = transformers.MixtralConfig(**common, num_local_experts=4, num_experts_per_tok=2, rope_theta=1e6)
     m = transformers.MixtralForCausalLM(cfg)
@@ -45,27 +66,38 @@ def _hf_model(kind, tmp_path):
         p.uniform_(0.5, 1.5)
       elif "bias" in n:
         p.normal_(0, 0.1)
-      elif "q_proj" in n or "qkv_proj" in n:
+      elif "q_proj" in n or "qkv_proj" in n or "q_b_proj" in n:
         p.mul_(6.0)  # peaked attention, so positions (RoPE) visibly change the logits
+    for n, b in m.named_buffers():
+      if "e_score_correction_bias" in n:
+        b.normal_(0, 0.05)
   d = tmp_path / kind
   m.save_pretrained(str(d), safe_serialization=True)
   return m, d
 
 
-def test_phi3_checkpoint_roundtrip(tmp_path):
-  """Fused HF names and the partial-rotary q/k row permutation survive to_hf_state_dict -> load."""
-  hf, d = _hf_model("phi3", tmp_path)
+@pytest.mark.parametrize("kind", ["phi3", "deepseek_v2", "deepseek_v3"])
+def test_checkpoint_roundtrip(kind, tmp_path):
+  """HF names survive to_hf_state_dict -> load exactly: Phi-3's fused qkv / gate_up and partial-rotary q/k
+  row permutation, DeepSeek's MLA row reorders (nope | de-interleaved rope), expert and shared-expert stacks."""
+  hf, d = _hf_model(kind, tmp_path)
   c = load_config(d)
-  sw = load_hf_weights(d, c, Shard("phi3", 0, 2, 3), dtype=torch.float32)
+  sw = load_hf_weights(d, c, Shard(kind, 0, 2, 3), dtype=torch.float32)
   sd = sw.to_hf_state_dict()
-  ref = {k: v for k, v in hf.state_dict().items()}
+  from safetensors.torch import load_file  # the hub-format names save_pretrained wrote
+  ref = {}
+  for f in sorted(d.glob("*.safetensors")):
+    ref.update(load_file(str(f)))
   for k, v in sd.items():
     assert k in ref, k
     torch.testing.assert_close(v, ref[k].float(), rtol=0, atol=0)
-  assert "model.layers.0.self_attn.qkv_proj.weight" in sd and "model.layers.0.mlp.gate_up_proj.weight" in sd
+  missing = [k for k in ref if k not in sd and "rotary" not in k and "lm_head" not in k]
+  assert not missing, missing
+  if kind == "phi3":
+    assert "model.layers.0.self_attn.qkv_proj.weight" in sd and "model.layers.0.mlp.gate_up_proj.weight" in sd
 
 
-@pytest.mark.parametrize("kind", ["llama", "qwen2", "mixtral", "phi3", "phi3-short"])
+@pytest.mark.parametrize("kind", ["llama", "qwen2", "mixtral", "phi3", "phi3-short", "deepseek_v2", "deepseek_v3"])
 def test_hf_parity(kind, tmp_path):
   hf, d = _hf_model(kind, tmp_path)
   c = load_config(d)

@@ -540,3 +540,90 @@ def test_moe_gate_up_split_k(gpu, T, shuffled):
   act2 = torch.empty_like(act)
   C.splitk_silu(ys, S, act2)
   assert rel_err(act2, act) < 1e-2
+
+
+# ---------------------------------------------------------------------------- DeepSeek MLA / routing
+def _mla_cache(num_pages, DL, DR, dev, seed=0):
+  g = torch.Generator(device=dev).manual_seed(seed)
+  return torch.randn(num_pages, 64, DL + DR, device=dev, dtype=torch.bfloat16, generator=g)
+
+
+@pytest.mark.parametrize("DL", [512, 256])
+@pytest.mark.parametrize("H", [16, 4, 128])
+@pytest.mark.parametrize("ctxs", [[1, 64, 65, 300], [1000]])
+def test_mla_attn_decode(gpu, DL, H, ctxs):
+  torch.manual_seed(0)
+  DR, B = 64, len(ctxs)
+  width = max(-(-c // 64) for c in ctxs)
+  num_pages = B * width + 3
+  cache = _mla_cache(num_pages, DL, DR, gpu)
+  perm = torch.randperm(num_pages - 3)[:B * width].view(B, width).int()
+  bt = perm.to(gpu)
+  ctx = torch.tensor(ctxs, dtype=torch.int32, device=gpu)
+  cu = torch.arange(B + 1, dtype=torch.int32, device=gpu)
+  q_lat = torch.randn(H, B, DL, device=gpu, dtype=torch.bfloat16)
+  q_pe = torch.randn(B, H * DR + 8, device=gpu, dtype=torch.bfloat16)[:, :H * DR]  # strided rows
+  scale = 0.1
+  ref = R.mla_attn(q_lat.cpu(), q_pe.cpu(), cache.cpu(), bt.cpu(), cu.cpu(), ctx.cpu(), scale)
+  for ws in (None, K.MLAWorkspace(B, H, DL, width * 64, gpu)):  # one partition / split-KV + combine
+    out = K.mla_attn(q_lat, q_pe, cache, bt, cu, ctx, scale, ws)
+    assert rel_err(out.cpu(), ref) < 2e-2, (DL, H, ctxs)
+
+
+@pytest.mark.parametrize("DL", [512, 256])
+def test_mla_attn_prefill_causal(gpu, DL):
+  torch.manual_seed(1)
+  DR, H = 64, 16
+  qlens, ctxs = [37, 1, 130], [37, 70, 200]  # second / third: chunked prefill on top of a cached prefix
+  B = len(qlens)
+  width = max(-(-c // 64) for c in ctxs)
+  cache = _mla_cache(B * width + 1, DL, DR, gpu, seed=1)
+  bt = torch.arange(B * width, dtype=torch.int32, device=gpu).view(B, width)
+  cu = torch.tensor([0] + list(torch.tensor(qlens).cumsum(0)), dtype=torch.int32, device=gpu)
+  T = int(cu[-1])
+  ctx = torch.tensor(ctxs, dtype=torch.int32, device=gpu)
+  q_lat = torch.randn(H, T, DL, device=gpu, dtype=torch.bfloat16)
+  q_pe = torch.randn(T, H * DR, device=gpu, dtype=torch.bfloat16)
+  ref = R.mla_attn(q_lat.cpu(), q_pe.cpu(), cache.cpu(), bt.cpu(), cu.cpu(), ctx.cpu(), 0.08)
+  out = K.mla_attn(q_lat, q_pe, cache, bt, cu, ctx, 0.08, K.MLAWorkspace(T, H, DL, width * 64, gpu))
+  assert rel_err(out.cpu(), ref) < 2e-2
+
+
+def test_mla_prep(gpu):
+  torch.manual_seed(2)
+  T, H, DL, DR = 9, 16, 512, 64
+  ckv_full = torch.randn(T, 128 + DL + DR, device=gpu, dtype=torch.bfloat16)
+  ckv = ckv_full[:, 128:]  # strided rows, as sliced out of the fused A projection
+  kv_ln = torch.randn(DL, device=gpu, dtype=torch.bfloat16)
+  q = torch.randn(T, H * 192, device=gpu, dtype=torch.bfloat16)
+  pos = torch.arange(5, 5 + T, dtype=torch.int32, device=gpu)
+  cs = build_cos_sin(DR, 64, 10000.0, None, device=gpu)
+  slots = torch.tensor([3, 70, -1, 5, 6, 7, 8, 9, 100], dtype=torch.int64, device=gpu)
+  cache = torch.zeros(4, 64, DL + DR, device=gpu, dtype=torch.bfloat16)
+  q2, cache2 = q.clone().cpu(), cache.clone().cpu()
+  K.mla_prep(ckv, kv_ln, q, H * 128, H, pos, cs, slots, cache, 1e-6)
+  R.mla_prep(ckv.cpu(), kv_ln.cpu(), q2, H * 128, H, pos.cpu(), cs.cpu(), slots.cpu(), cache2, 1e-6)
+  assert rel_err(q.cpu(), q2) < 1e-2
+  assert rel_err(cache.cpu(), cache2) < 1e-2
+
+
+@pytest.mark.parametrize("E,k,ng,tg,method,sig,norm", [(64, 6, 1, 1, 0, False, False), (8, 2, 4, 2, 1, False, False),
+                                                        (256, 8, 8, 4, 2, True, True), (16, 4, 4, 2, 2, True, True)])
+def test_moe_route_ds(gpu, E, k, ng, tg, method, sig, norm):
+  torch.manual_seed(3)
+  T = 300
+  logits = torch.randn(T, E, device=gpu) * 2
+  bias = torch.randn(E, device=gpu) * 0.05 if sig else None
+  topw, topi, slot_of, sorted_tok, off = K.moe_route_ds(logits, bias, k, ng, tg, method, sig, norm, 2.5)
+  rw, ri = R.moe_route_ds(logits.cpu(), bias.cpu() if bias is not None else None, k, ng, tg, method, sig, norm, 2.5)
+  got_i, order = topi.view(T, k).cpu().long().sort(-1)
+  exp_i, eorder = ri.sort(-1)
+  assert torch.equal(got_i, exp_i)
+  torch.testing.assert_close(topw.view(T, k).cpu().gather(1, order), rw.gather(1, eorder), rtol=1e-4, atol=1e-5)
+  # slot bookkeeping: every (token, j) slot points back at its token inside its expert's range
+  off_c, st = off.cpu(), sorted_tok.cpu()
+  so = slot_of.view(T, k).cpu()
+  for t in range(0, T, 37):
+    for j in range(k):
+      e = int(topi.view(T, k)[t, j])
+      assert off_c[e] <= so[t, j] < off_c[e + 1] and int(st[so[t, j]]) == t

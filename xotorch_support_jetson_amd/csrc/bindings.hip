@@ -420,6 +420,85 @@ void moe_route(const at::Tensor& logits, int64_t k, at::Tensor& topw, at::Tensor
                         slot_of.data_ptr<int>(), sorted_tok.data_ptr<int>(), off.data_ptr<int>(), cur_stream());
 }
 
+void moe_route_ds(const at::Tensor& logits, const c10::optional<at::Tensor>& bias, int64_t k, int64_t n_group,
+                  int64_t topk_group, int64_t method, bool sigmoid, bool norm, double scale, at::Tensor& topw,
+                  at::Tensor& topi, at::Tensor& slot_of, at::Tensor& sorted_tok, at::Tensor& off) {
+  CHECK_GPU(logits);
+  CHECK_DT(logits, at::kFloat);
+  XCHECK(all_contig_gpu(logits, topw, topi, slot_of, sorted_tok, off), "moe_route_ds: tensors must be contiguous GPU");
+  const int64_t T = logits.size(0), E = logits.size(1);
+  if (bias.has_value()) {
+    CHECK_DT((*bias), at::kFloat);
+    XCHECK(bias->is_cuda() && bias->is_contiguous() && bias->numel() == E, "moe_route_ds: bias [E] fp32");
+  }
+  CHECK_DT(topw, at::kFloat);
+  CHECK_DT(topi, at::kInt);
+  CHECK_DT(slot_of, at::kInt);
+  CHECK_DT(sorted_tok, at::kInt);
+  CHECK_DT(off, at::kInt);
+  XCHECK(topw.numel() == T * k && topi.numel() == T * k && slot_of.numel() == T * k && sorted_tok.numel() == T * k &&
+             off.numel() == E + 1,
+         "moe_route_ds: output sizes");
+  const int rc = xot::launch_moe_route_ds(logits.data_ptr<float>(), bias.has_value() ? bias->data_ptr<float>() : nullptr,
+                                          (int)T, (int)E, (int)k, (int)n_group, (int)topk_group, (int)method, sigmoid,
+                                          norm, (float)scale, topw.data_ptr<float>(), topi.data_ptr<int>(),
+                                          slot_of.data_ptr<int>(), sorted_tok.data_ptr<int>(), off.data_ptr<int>(),
+                                          cur_stream());
+  XCHECK(rc == 0, "moe_route_ds: unsupported E=", E, " k=", k, " groups=", n_group, "/", topk_group);
+}
+
+// ckv [T, >= DL + DR] (row stride ldc), q [T, ldq] with q_pe of head h at qpe_off + h * DR (rotated in place)
+void mla_prep(const at::Tensor& ckv, const at::Tensor& kv_ln, at::Tensor& q, int64_t qpe_off, int64_t H,
+              const at::Tensor& pos, const at::Tensor& cos_sin, const at::Tensor& slots, at::Tensor& cache, double eps) {
+  CHECK_BF16(ckv);
+  CHECK_BF16(kv_ln);
+  CHECK_BF16(q);
+  CHECK_BF16(cache);
+  CHECK_DT(pos, at::kInt);
+  CHECK_DT(cos_sin, at::kFloat);
+  CHECK_DT(slots, at::kLong);
+  XCHECK(all_contig_gpu(kv_ln, pos, cos_sin, slots, cache), "mla_prep: contiguous GPU tensors");
+  XCHECK(ckv.dim() == 2 && ckv.stride(1) == 1 && q.dim() == 2 && q.stride(1) == 1, "mla_prep: row-major 2-D ckv / q");
+  const int64_t T = ckv.size(0), DL = kv_ln.numel(), DR = cos_sin.size(1);
+  XCHECK(cache.dim() == 3 && cache.size(1) == 64 && cache.size(2) == DL + DR, "mla_prep: cache [pages, 64, DL + DR]");
+  XCHECK(DL % 8 == 0 && DL <= 2048 && DR % 2 == 0 && ckv.size(1) >= DL + DR, "mla_prep: latent / rope dims");
+  XCHECK(q.size(0) == T && pos.numel() == T && slots.numel() == T && qpe_off + H * DR <= q.size(1), "mla_prep: shapes");
+  xot::launch_mla_prep(bf(ckv), (long)ckv.stride(0), bf(kv_ln), bf(q), (long)q.stride(0), (long)qpe_off,
+                       pos.data_ptr<int>(), cos_sin.data_ptr<float>(), slots.data_ptr<int64_t>(), bf(cache), (int)T,
+                       (int)H, (int)DL, (int)DR, (int)cos_sin.size(0), (long)(cache.size(0) * 64), (float)eps,
+                       cur_stream());
+}
+
+// q_lat / out [H, T, DL]; q_pe rows of q (row stride ldqpe = q_pe.stride(0)) as [T, H * DR]
+void mla_attn(const at::Tensor& q_lat, const at::Tensor& q_pe, const at::Tensor& cache, const at::Tensor& block_tables,
+              const at::Tensor& cu_q, const at::Tensor& ctx_lens, at::Tensor& out, at::Tensor& ws_o, at::Tensor& ws_ml,
+              int64_t pages_per_part, int64_t nparts, double scale) {
+  CHECK_BF16(q_lat);
+  CHECK_BF16(q_pe);
+  CHECK_BF16(cache);
+  CHECK_BF16(out);
+  CHECK_DT(block_tables, at::kInt);
+  CHECK_DT(cu_q, at::kInt);
+  CHECK_DT(ctx_lens, at::kInt);
+  CHECK_DT(ws_o, at::kFloat);
+  CHECK_DT(ws_ml, at::kFloat);
+  XCHECK(all_contig_gpu(q_lat, cache, block_tables, cu_q, ctx_lens, out, ws_o, ws_ml), "mla_attn: contiguous GPU");
+  XCHECK(q_pe.is_cuda() && q_pe.dim() == 2 && q_pe.stride(1) == 1 && q_pe.stride(0) % 8 == 0, "mla_attn: q_pe rows");
+  XCHECK(q_lat.dim() == 3 && cache.dim() == 3 && cache.size(1) == 64, "mla_attn: q_lat [H, T, DL], cache [pages, 64, DL+DR]");
+  const int64_t H = q_lat.size(0), T = q_lat.size(1), DL = q_lat.size(2), DR = cache.size(2) - DL;
+  const int64_t B = ctx_lens.numel();
+  XCHECK(q_pe.size(0) == T && q_pe.size(1) >= H * DR && out.sizes() == q_lat.sizes(), "mla_attn: shapes");
+  XCHECK(cu_q.numel() == B + 1 && block_tables.dim() == 2 && block_tables.size(0) == B, "mla_attn: batch tensors");
+  XCHECK(nparts == 1 || (ws_o.numel() >= T * H * nparts * DL && ws_ml.numel() >= T * H * nparts * 2),
+         "mla_attn: split-KV workspace too small");
+  const int rc = xot::launch_mla_attn(bf(q_lat), bf(q_pe), (long)q_pe.stride(0), bf(cache),
+                                      block_tables.data_ptr<int>(), (int)block_tables.size(1), cu_q.data_ptr<int>(),
+                                      ctx_lens.data_ptr<int>(), (int)B, (int)T, (int)H, (int)DL, (int)DR, bf(out),
+                                      ws_o.data_ptr<float>(), ws_ml.data_ptr<float>(), (int)pages_per_part,
+                                      (int)nparts, (float)scale, (int)cache.size(0), cur_stream());
+  XCHECK(rc == 0, "mla_attn: unsupported DL=", DL, " DR=", DR);
+}
+
 void moe_combine(const at::Tensor& y, const at::Tensor& slot_of, const at::Tensor& topw, at::Tensor& h,
                  int64_t splits) {
   CHECK_GPU(y);
@@ -693,6 +772,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_moe", &gemm_moe, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("off"), py::arg("gather"),
         py::arg("epi"), py::arg("max_rows"), py::arg("wshuf"), py::arg("splits") = 1, py::arg("big_bm") = 0);
   m.def("moe_route", &moe_route);
+  m.def("moe_route_ds", &moe_route_ds);
+  m.def("mla_prep", &mla_prep);
+  m.def("mla_attn", &mla_attn);
   m.def("moe_combine", &moe_combine, py::arg("y"), py::arg("slot_of"), py::arg("topw"), py::arg("h"),
         py::arg("splits") = 1);
   m.def("attn_decode", &attn_decode, py::arg("q"), py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"),

@@ -58,6 +58,18 @@ void launch_moe_route(const float* logits, int T, int E, int k, float* topw, int
                       int32_t* sorted_tok, int32_t* off, hipStream_t s);
 void launch_moe_combine(const float* y, const int32_t* slot_of, const float* topw, uint16_t* h, int T, int k, int D,
                         int S, long ysplit, hipStream_t s);
+// DeepSeekMoE routing: method 0 greedy, 1 group max (V2 group_limited_greedy), 2 group top-2 sum (V3 noaux_tc)
+int launch_moe_route_ds(const float* logits, const float* bias, int T, int E, int k, int n_group, int topk_group,
+                        int method, bool sigmoid, bool norm, float scale, float* topw, int32_t* topi, int32_t* slot_of,
+                        int32_t* sorted_tok, int32_t* off, hipStream_t s);
+// DeepSeek MLA: latent norm + rope + latent cache write (q_pe rotated in place), and the absorbed attention
+void launch_mla_prep(const uint16_t* ckv, long ldc, const uint16_t* kv_ln, uint16_t* q, long ldq, long qpe_off,
+                     const int32_t* pos, const float* cos_sin, const int64_t* slots, uint16_t* cache, int T, int H,
+                     int DL, int DR, int max_pos, long nslots, float eps, hipStream_t s);
+int launch_mla_attn(const uint16_t* q_lat, const uint16_t* q_pe, long ldqpe, const uint16_t* cache,
+                    const int32_t* block_tables, int max_blocks, const int32_t* cu_q, const int32_t* ctx_lens, int B,
+                    int T, int H, int DL, int DR, uint16_t* out, float* ws_o, float* ws_ml, int pages_per_part,
+                    int nparts, float scale, int num_pages, hipStream_t s);
 int launch_gemm_tiled(const uint16_t* X, int ldx, const uint16_t* W, int ldw, const uint16_t* bias,
                       const uint16_t* R, int ldr, void* Y, int ldy, bool out_f32, int epi, int M, int N, int K,
                       hipStream_t s);

@@ -79,6 +79,127 @@ __global__ __launch_bounds__(1024) void moe_route_kernel(const float* __restrict
   }
 }
 
+// DeepSeekMoE routing (HF DeepseekV2TopkRouter / DeepseekV3TopkRouter), one workgroup, one thread per token:
+//   score = softmax(logits) (V2) or sigmoid(logits) (V3); choice = score + bias (V3 selection bias)
+//   groups: experts in n_group equal groups; keep the topk_group groups ranked by max(choice) (V2
+//   group_limited_greedy) or the sum of their two best choices (V3 noaux_tc); top-k experts by choice among
+//   the kept groups; weight = score (not choice), optionally renormalised, times routed_scaling_factor.
+// Then the same per-expert slot order as moe_route_kernel.
+constexpr int MOE_DS_MAX_E = 256;
+constexpr int MOE_DS_MAX_G = 16;
+__global__ __launch_bounds__(1024) void moe_route_ds_kernel(const float* __restrict__ logits,
+                                                            const float* __restrict__ bias, int T, int E, int k,
+                                                            int n_group, int topk_group, int method, int sigmoid,
+                                                            int norm, float scale, float* __restrict__ topw,
+                                                            int32_t* __restrict__ topi, int32_t* __restrict__ slot_of,
+                                                            int32_t* __restrict__ sorted_tok, int32_t* __restrict__ off) {
+  __shared__ int cnt[MOE_DS_MAX_E];
+  __shared__ int base[MOE_DS_MAX_E + 1];
+  const int tid = threadIdx.x;
+  for (int e = tid; e < MOE_DS_MAX_E; e += blockDim.x) cnt[e] = 0;
+  __syncthreads();
+  const int per = E / n_group;
+  for (int t = tid; t < T; t += blockDim.x) {
+    const float* lg = logits + (size_t)t * E;
+    float mx = -INFINITY, den = 0.f;
+    if (!sigmoid) {
+      for (int e = 0; e < E; ++e) mx = fmaxf(mx, lg[e]);
+      for (int e = 0; e < E; ++e) den += __expf(lg[e] - mx);
+    }
+    auto score = [&](int e) { return sigmoid ? 1.f / (1.f + __expf(-lg[e])) : __expf(lg[e] - mx) / den; };
+    auto choice = [&](int e) { return score(e) + (bias != nullptr ? bias[e] : 0.f); };
+    // group selection (bitmask of kept groups)
+    unsigned keep = 0xffffffffu;
+    if (n_group > 1 && topk_group < n_group) {
+      float gs[MOE_DS_MAX_G];
+      for (int gi = 0; gi < n_group; ++gi) {
+        float a = -INFINITY, b2 = -INFINITY;
+        for (int e = gi * per; e < (gi + 1) * per; ++e) {
+          const float v = choice(e);
+          if (v > a) {
+            b2 = a;
+            a = v;
+          } else if (v > b2) {
+            b2 = v;
+          }
+        }
+        gs[gi] = method == 2 ? a + b2 : a;
+      }
+      keep = 0;
+      for (int j = 0; j < topk_group; ++j) {
+        int best = -1;
+        for (int gi = 0; gi < n_group; ++gi)
+          if (!(keep >> gi & 1u) && (best < 0 || gs[gi] > gs[best])) best = gi;
+        keep |= 1u << best;
+      }
+    }
+    float sel_v[MOE_MAX_K];
+    int sel_i[MOE_MAX_K];
+    for (int j = 0; j < k; ++j) {
+      sel_v[j] = -INFINITY;
+      sel_i[j] = 0;
+    }
+    for (int e = 0; e < E; ++e) {
+      if (!(keep >> (e / per) & 1u)) continue;
+      float v = choice(e);
+      int id = e;
+      for (int j = 0; j < k; ++j) {
+        if (v > sel_v[j]) {
+          const float tv = sel_v[j];
+          const int ti = sel_i[j];
+          sel_v[j] = v;
+          sel_i[j] = id;
+          v = tv;
+          id = ti;
+        }
+      }
+    }
+    float w[MOE_MAX_K], sum = 0.f;
+    for (int j = 0; j < k; ++j) {
+      w[j] = score(sel_i[j]);
+      sum += w[j];
+    }
+    const float f = norm ? scale / (sum + 1e-20f) : scale;
+    for (int j = 0; j < k; ++j) {
+      topw[(size_t)t * k + j] = w[j] * f;
+      topi[(size_t)t * k + j] = sel_i[j];
+      atomicAdd(&cnt[sel_i[j]], 1);
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int acc = 0;
+    for (int e = 0; e < E; ++e) {
+      base[e] = acc;
+      off[e] = acc;
+      acc += cnt[e];
+    }
+    off[E] = acc;
+  }
+  __syncthreads();
+  for (int e = tid; e < E; e += blockDim.x) cnt[e] = 0;
+  __syncthreads();
+  for (int t = tid; t < T; t += blockDim.x) {
+    for (int j = 0; j < k; ++j) {
+      const int e = topi[(size_t)t * k + j];
+      const int pos = base[e] + atomicAdd(&cnt[e], 1);
+      slot_of[(size_t)t * k + j] = pos;
+      sorted_tok[pos] = t;
+    }
+  }
+}
+
+int launch_moe_route_ds(const float* logits, const float* bias, int T, int E, int k, int n_group, int topk_group,
+                        int method, bool sigmoid, bool norm, float scale, float* topw, int32_t* topi, int32_t* slot_of,
+                        int32_t* sorted_tok, int32_t* off, hipStream_t s) {
+  if (E < 1 || E > MOE_DS_MAX_E || k < 1 || k > MOE_MAX_K || n_group < 1 || n_group > MOE_DS_MAX_G ||
+      E % n_group != 0 || topk_group < 1 || topk_group > n_group || k > (E / n_group) * topk_group)
+    return -1;
+  moe_route_ds_kernel<<<1, 1024, 0, s>>>(logits, bias, T, E, k, n_group, topk_group, method, sigmoid ? 1 : 0,
+                                         norm ? 1 : 0, scale, topw, topi, slot_of, sorted_tok, off);
+  return 0;
+}
+
 // one thread per 8 hidden columns of one token
 __global__ __launch_bounds__(256) void moe_combine_kernel(const float* __restrict__ y,
                                                           const int32_t* __restrict__ slot_of,

@@ -34,29 +34,95 @@ class ModelConfig:
   bos_token_id: int = 128000
   eos_token_ids: tuple = (128001, 128009)
   partial_rotary_factor: float = 1.0  # Phi-3: RoPE on the first 75 % of each head's dims
+  # DeepSeek-V2/V3 multi-head latent attention (kv_lora_rank > 0): per token the cache holds one
+  # normalised latent [kv_lora_rank] + one shared rotated key [qk_rope_head_dim]
+  q_lora_rank: int = 0  # 0: plain q_proj
+  kv_lora_rank: int = 0
+  qk_nope_head_dim: int = 0
+  qk_rope_head_dim: int = 0
+  v_head_dim: int = 0
+  # MoE routing (Mixtral: softmax top-k renormalised; DeepSeek: shared experts, dense first layers,
+  # group-limited selection, sigmoid scores with a selection bias (V3), scaled weights)
+  moe_intermediate_size: int = 0  # 0: intermediate_size
+  n_shared_experts: int = 0
+  first_k_dense_replace: int = 0
+  moe_layer_freq: int = 1
+  routed_scaling_factor: float = 1.0
+  topk_method: str = "greedy"  # greedy | group_limited_greedy (V2) | noaux_tc (V3)
+  n_group: int = 1
+  topk_group: int = 1
+  norm_topk_prob: bool = True
+  scoring_func: str = "softmax"  # softmax | sigmoid
 
   @property
   def qkv_size(self) -> int:
+    if self.is_mla:  # fused A projection: [q_a (or the full q) | kv_a latent | shared rope key]
+      q = self.q_lora_rank or self.num_heads * (self.qk_nope_head_dim + self.qk_rope_head_dim)
+      return q + self.kv_lora_rank + self.qk_rope_head_dim
     return (self.num_heads + 2 * self.num_kv_heads) * self.head_dim
 
   @property
+  def is_mla(self) -> bool:
+    return self.kv_lora_rank > 0
+
+  @property
+  def mla_dim(self) -> int:
+    """Latent cache row: normalised kv latent + rotated shared key."""
+    return self.kv_lora_rank + self.qk_rope_head_dim
+
+  @property
+  def rope_dim(self) -> int:
+    return self.qk_rope_head_dim if self.is_mla else self.head_dim
+
+  @property
   def rotary_dim(self) -> int:
-    r = int(self.head_dim * self.partial_rotary_factor)
+    r = int(self.rope_dim * self.partial_rotary_factor)
     return r - (r % 2)
 
   @property
   def is_moe(self) -> bool:
     return self.num_experts > 0
 
-  def params_per_layer(self) -> int:
+  @property
+  def expert_dim(self) -> int:
+    return self.moe_intermediate_size or self.intermediate_size
+
+  def moe_layer(self, i: int) -> bool:
+    """Layer i has a routed-expert MLP (HF DeepseekV3DecoderLayer's rule; every layer for Mixtral)."""
+    return self.is_moe and i >= self.first_k_dense_replace and i % max(1, self.moe_layer_freq) == 0
+
+  def attn_scale(self) -> float:
+    """Softmax scale: 1/sqrt(q.k dim); DeepSeek YaRN multiplies by mscale(factor, mscale_all_dim)^2."""
+    import math
+    dq = self.qk_nope_head_dim + self.qk_rope_head_dim if self.is_mla else self.head_dim
+    s = dq ** -0.5
+    sc = self.rope_scaling or {}
+    if sc.get("rope_type") == "yarn" and sc.get("mscale_all_dim"):
+      f = float(sc.get("factor", 1.0))
+      m = 1.0 if f <= 1 else 0.1 * float(sc["mscale_all_dim"]) * math.log(f) + 1.0
+      s *= m * m
+    return s
+
+  def params_per_layer(self, i: int = -1) -> int:
     D, F = self.hidden_size, self.intermediate_size
-    attn = D * self.qkv_size + self.num_heads * self.head_dim * D
-    mlp = 3 * D * F * max(1, self.num_experts) + (D * self.num_experts if self.is_moe else 0)
+    if self.is_mla:
+      H, dn, dr, dv = self.num_heads, self.qk_nope_head_dim, self.qk_rope_head_dim, self.v_head_dim
+      attn = D * self.qkv_size + (self.q_lora_rank * H * (dn + dr) if self.q_lora_rank else 0)
+      attn += self.kv_lora_rank * H * (dn + dv) + H * dv * D
+    else:
+      attn = D * self.qkv_size + self.num_heads * self.head_dim * D
+    moe = self.moe_layer(i) if i >= 0 else self.is_moe
+    if moe:
+      Fe = self.expert_dim
+      mlp = 3 * D * Fe * (self.num_experts + self.n_shared_experts) + D * self.num_experts
+    else:
+      mlp = 3 * D * F
     return attn + mlp + 2 * D
 
   def num_params(self) -> int:
     emb = self.vocab_size * self.hidden_size
-    return self.num_layers * self.params_per_layer() + emb * (1 if self.tie_word_embeddings else 2) + self.hidden_size
+    layers = sum(self.params_per_layer(i) for i in range(self.num_layers))
+    return layers + emb * (1 if self.tie_word_embeddings else 2) + self.hidden_size
 
   def to_dict(self) -> dict:
     d = asdict(self)
@@ -83,6 +149,10 @@ def _rope_fields(cfg: dict) -> tuple:
                      original_max_position_embeddings=int(scaling.get("original_max_position_embeddings")
                                                           or cfg.get("original_max_position_embeddings", 4096)),
                      max_position_embeddings=int(cfg.get("max_position_embeddings", 131072)))
+    elif kind == "yarn":
+      scaling = dict(scaling, rope_type="yarn",
+                     original_max_position_embeddings=int(scaling.get("original_max_position_embeddings")
+                                                          or cfg.get("original_max_position_embeddings", 4096)))
     elif kind in ("default", None):
       scaling = None
   return theta, (scaling or None), partial
@@ -98,6 +168,8 @@ def from_hf_config(cfg: dict) -> ModelConfig:
   if cfg.get("sliding_window") and mt == "phi3":
     import warnings
     warnings.warn(f"phi3 sliding_window={cfg['sliding_window']} is not applied (full causal attention)")
+  if mt in ("deepseek_v2", "deepseek_v3"):
+    return _deepseek_config(cfg, mt, theta, scaling, eos_ids)
   return ModelConfig(
     model_type=mt,
     vocab_size=int(cfg["vocab_size"]),
@@ -121,6 +193,48 @@ def from_hf_config(cfg: dict) -> ModelConfig:
   )
 
 
+def _deepseek_config(cfg: dict, mt: str, theta: float, scaling, eos_ids) -> ModelConfig:
+  """DeepSeek-V2 / V3 (and R1): MLA attention, DeepSeekMoE with shared experts."""
+  H = int(cfg["num_attention_heads"])
+  v3 = mt == "deepseek_v3"
+  return ModelConfig(
+    model_type=mt,
+    vocab_size=int(cfg["vocab_size"]),
+    hidden_size=int(cfg["hidden_size"]),
+    intermediate_size=int(cfg["intermediate_size"]),
+    num_layers=int(cfg["num_hidden_layers"]),
+    num_heads=H,
+    num_kv_heads=1,  # one shared latent per token
+    head_dim=int(cfg["qk_nope_head_dim"]) + int(cfg["qk_rope_head_dim"]),
+    rms_norm_eps=float(cfg.get("rms_norm_eps", 1e-6)),
+    rope_theta=theta,
+    rope_scaling=scaling,
+    max_position_embeddings=int(cfg.get("max_position_embeddings", 4096)),
+    tie_word_embeddings=bool(cfg.get("tie_word_embeddings", False)),
+    attention_bias=bool(cfg.get("attention_bias", False)),
+    num_experts=int(cfg.get("n_routed_experts") or 0),
+    num_experts_per_tok=int(cfg.get("num_experts_per_tok") or 0),
+    bos_token_id=int(cfg.get("bos_token_id", 0) or 0),
+    eos_token_ids=eos_ids,
+    q_lora_rank=int(cfg.get("q_lora_rank") or 0),
+    kv_lora_rank=int(cfg["kv_lora_rank"]),
+    qk_nope_head_dim=int(cfg["qk_nope_head_dim"]),
+    qk_rope_head_dim=int(cfg["qk_rope_head_dim"]),
+    v_head_dim=int(cfg["v_head_dim"]),
+    moe_intermediate_size=int(cfg.get("moe_intermediate_size") or 0),
+    n_shared_experts=int(cfg.get("n_shared_experts") or 0),
+    first_k_dense_replace=int(cfg.get("first_k_dense_replace") or 0),
+    moe_layer_freq=int(cfg.get("moe_layer_freq") or 1),
+    routed_scaling_factor=float(cfg.get("routed_scaling_factor") or 1.0),
+    topk_method="noaux_tc" if v3 else str(cfg.get("topk_method") or "greedy"),
+    n_group=int(cfg.get("n_group") or 1),
+    topk_group=int(cfg.get("topk_group") or 1),
+    # HF's V2 router never renormalises (norm_topk_prob is ignored there); V3 follows the flag
+    norm_topk_prob=bool(cfg.get("norm_topk_prob", True)) if v3 else False,
+    scoring_func="sigmoid" if v3 else "softmax",
+  )
+
+
 def load_config(model_dir: str | Path) -> ModelConfig:
   with open(Path(model_dir) / "config.json") as f:
     return from_hf_config(json.load(f))
@@ -129,6 +243,9 @@ def load_config(model_dir: str | Path) -> ModelConfig:
 _L3 = dict(rope_type="llama3", factor=32.0, low_freq_factor=1.0, high_freq_factor=4.0,
            original_max_position_embeddings=8192)
 _L31 = dict(_L3, factor=8.0)
+_DS_YARN = dict(rope_type="yarn", factor=40.0, original_max_position_embeddings=4096, beta_fast=32, beta_slow=1,
+                mscale=1.0, mscale_all_dim=1.0)  # DeepSeek-V3 / R1
+_DS2_YARN = dict(_DS_YARN, mscale=0.707, mscale_all_dim=0.707)  # DeepSeek-V2(-Lite)
 
 PRESETS: dict[str, ModelConfig] = {
   "llama-3.2-1b": ModelConfig("llama", 128256, 2048, 8192, 16, 32, 8, 64, 1e-5, 500000.0, _L3, 131072, True),
@@ -170,6 +287,19 @@ PRESETS: dict[str, ModelConfig] = {
                                           original_max_position_embeddings=4096, max_position_embeddings=131072),
                                      131072, True, bos_token_id=199999, eos_token_ids=(199999, 200020),
                                      partial_rotary_factor=0.75),
+  # DeepSeek (HF DeepseekV2/V3ForCausalLM): MLA (latent 512 + rope 64), DeepSeekMoE with shared experts
+  "deepseek-coder-v2-lite": ModelConfig("deepseek_v2", 102400, 2048, 10944, 27, 16, 1, 192, 1e-6, 10000.0,
+                                        _DS2_YARN, 163840, False, num_experts=64, num_experts_per_tok=6,
+                                        bos_token_id=100000, eos_token_ids=(100001,), kv_lora_rank=512,
+                                        qk_nope_head_dim=128, qk_rope_head_dim=64, v_head_dim=128,
+                                        moe_intermediate_size=1408, n_shared_experts=2, first_k_dense_replace=1,
+                                        norm_topk_prob=False),
+  "deepseek-v3": ModelConfig("deepseek_v3", 129280, 7168, 18432, 61, 128, 1, 192, 1e-6, 10000.0, _DS_YARN, 163840,
+                             False, num_experts=256, num_experts_per_tok=8, bos_token_id=0, eos_token_ids=(1,),
+                             q_lora_rank=1536, kv_lora_rank=512, qk_nope_head_dim=128, qk_rope_head_dim=64,
+                             v_head_dim=128, moe_intermediate_size=2048, n_shared_experts=1, first_k_dense_replace=3,
+                             routed_scaling_factor=2.5, topk_method="noaux_tc", n_group=8, topk_group=4,
+                             norm_topk_prob=True, scoring_func="sigmoid"),
   # small shapes for tests / CPU plumbing
   "tiny-llama": ModelConfig("llama", 512, 256, 512, 4, 4, 2, 64, 1e-5, 10000.0, None, 2048, False,
                             bos_token_id=1, eos_token_ids=(2,)),
@@ -184,6 +314,19 @@ PRESETS: dict[str, ModelConfig] = {
                                 long_factor=[2.0 + 0.1 * i for i in range(48)], original_max_position_embeddings=64,
                                 max_position_embeddings=2048), 2048, True, bos_token_id=1, eos_token_ids=(2,),
                            partial_rotary_factor=0.75),
+  "tiny-deepseek-v2": ModelConfig("deepseek_v2", 512, 256, 512, 3, 4, 1, 192, 1e-6, 10000.0, None, 2048, False,
+                                  num_experts=8, num_experts_per_tok=2, bos_token_id=1, eos_token_ids=(2,),
+                                  kv_lora_rank=256, qk_nope_head_dim=128, qk_rope_head_dim=64, v_head_dim=128,
+                                  moe_intermediate_size=256, n_shared_experts=2, first_k_dense_replace=1,
+                                  topk_method="group_limited_greedy", n_group=4, topk_group=2, norm_topk_prob=False,
+                                  routed_scaling_factor=1.5),
+  "tiny-deepseek-v3": ModelConfig("deepseek_v3", 512, 256, 512, 3, 16, 1, 192, 1e-6, 10000.0,
+                                  dict(_DS_YARN, original_max_position_embeddings=64), 2048, False, num_experts=16,
+                                  num_experts_per_tok=4, bos_token_id=1, eos_token_ids=(2,), q_lora_rank=256,
+                                  kv_lora_rank=256, qk_nope_head_dim=128, qk_rope_head_dim=64, v_head_dim=128,
+                                  moe_intermediate_size=256, n_shared_experts=1, first_k_dense_replace=1,
+                                  routed_scaling_factor=2.5, topk_method="noaux_tc", n_group=4, topk_group=2,
+                                  norm_topk_prob=True, scoring_func="sigmoid"),
 }
 # aliases of the reference's model cards that share an architecture
 for _alias, _base in {"llama-3.1-70b-bf16": "llama-3.1-70b", "nemotron-70b": "llama-3.1-70b",
@@ -193,7 +336,8 @@ for _alias, _base in {"llama-3.1-70b-bf16": "llama-3.1-70b", "nemotron-70b": "ll
                       "deepseek-r1-distill-qwen-7b": "qwen-2.5-7b", "qwen-2.5-coder-3b": "qwen-2.5-3b",
                       "qwen-2.5-coder-14b": "qwen-2.5-14b", "deepseek-r1-distill-qwen-14b": "qwen-2.5-14b",
                       "qwen-2.5-coder-32b": "qwen-2.5-32b", "deepseek-r1-distill-qwen-32b": "qwen-2.5-32b",
-                      "qwen-2.5-math-72b": "qwen-2.5-72b", "llama-3.1-405b-8bit": "llama-3.1-405b"}.items():
+                      "qwen-2.5-math-72b": "qwen-2.5-72b", "llama-3.1-405b-8bit": "llama-3.1-405b",
+                      "deepseek-r1": "deepseek-v3"}.items():
   PRESETS.setdefault(_alias, PRESETS[_base])
 
 

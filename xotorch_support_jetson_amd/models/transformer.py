@@ -62,19 +62,26 @@ class StepInputs:
 
 
 class KVCache:
-  """Per-shard paged KV pool: K [L, pages, Hkv, 64, Dh] and V [L, pages, Hkv, Dh, 64] (V page-transposed)."""
+  """Per-shard paged KV pool: K [L, pages, Hkv, 64, Dh] and V [L, pages, Hkv, Dh, 64] (V page-transposed).
+  MLA models (DeepSeek) keep one latent row per token instead: k = C [L, pages, 64, kv_lora + rope], v None."""
 
   def __init__(self, c: ModelConfig, n_layers: int, num_pages: int, device, dtype=torch.bfloat16):
     self.num_pages = num_pages
+    if c.is_mla:
+      self.k = torch.zeros(n_layers, num_pages, PAGE, c.mla_dim, device=device, dtype=dtype)
+      self.v = None
+      return
     self.k = torch.zeros(n_layers, num_pages, c.num_kv_heads, PAGE, c.head_dim, device=device, dtype=dtype)
     self.v = torch.zeros(n_layers, num_pages, c.num_kv_heads, c.head_dim, PAGE, device=device, dtype=dtype)
 
   @staticmethod
   def bytes_per_page(c: ModelConfig, n_layers: int) -> int:
+    if c.is_mla:
+      return n_layers * PAGE * c.mla_dim * 2
     return 2 * n_layers * c.num_kv_heads * PAGE * c.head_dim * 2
 
   def nbytes(self) -> int:
-    return 2 * self.k.numel() * self.k.element_size()
+    return sum(t.numel() * t.element_size() for t in (self.k, self.v) if t is not None)
 
 
 class ShardModel:
@@ -94,7 +101,12 @@ class ShardModel:
     self.max_ctx = max_ctx
     self.ws = None
     if self.device.type == "cuda":
-      self.ws = K.DecodeWorkspace(max_batch, c.num_heads, c.head_dim, max_ctx, self.device)
+      if c.is_mla:
+        self.ws = K.MLAWorkspace(max_batch, c.num_heads, c.kv_lora_rank, max_ctx, self.device)
+      else:
+        self.ws = K.DecodeWorkspace(max_batch, c.num_heads, c.head_dim, max_ctx, self.device)
+    if c.is_mla:
+      self.scale = c.attn_scale()
     # last shard with the LM head split across two ring stages: logits of vocab rows [0, head_rows) only,
     # and forward returns (logits, normed hidden)
     self.head_rows: Optional[int] = None
@@ -113,10 +125,42 @@ class ShardModel:
       return K.attn_decode(q, kc, vc, inp.block_tables, inp.ctx_lens, self.scale, self.ws)
     return K.attn_prefill(q, kc, vc, inp.block_tables, inp.cu_q, inp.ctx_lens, inp.max_qlen, self.scale)
 
-  def _mlp(self, xn: torch.Tensor, lw, h: torch.Tensor, next_norm: Optional[torch.Tensor]):
+  def _mla(self, xn: torch.Tensor, lw, li: int, inp: StepInputs) -> torch.Tensor:
+    """DeepSeek multi-head latent attention -> [T, H * v_head_dim] (before o_proj).
+    A = xn @ [q_a | kv_a]^T; q = rmsnorm(q_a) @ q_b^T (or A's q part); latent norm + rope + cache write;
+    absorbed query q_lat = q_nope . W_UK per head; attention over the latent cache (csrc/mla.hip);
+    o = o_lat . W_UV^T per head."""
+    c = self.c
+    T = xn.shape[0]
+    H, dn, dr, dv, L = c.num_heads, c.qk_nope_head_dim, c.qk_rope_head_dim, c.v_head_dim, c.kv_lora_rank
+    A = linear(xn, lw.qkv_w)
+    nq = c.q_lora_rank or H * (dn + dr)
+    if c.q_lora_rank:
+      qa, _ = K.rmsnorm(A[:, :nq].contiguous(), lw.q_ln, c.rms_norm_eps)
+      q = linear(qa, lw.qb_w)  # [T, H dn | H dr]
+    else:
+      q = A  # q = A[:, :nq], rows of stride A.shape[1]
+    ckv = A[:, nq:]
+    cache = self.kv.k[li]
+    K.mla_prep(ckv, lw.kv_ln, q, H * dn, H, inp.positions, self.cos_sin, inp.slots, cache, c.rms_norm_eps)
+    q_nope = q[:, :H * dn].view(T, H, dn).transpose(0, 1)  # [H, T, dn]
+    dt = q.dtype
+    if xn.is_cuda:
+      q_lat = torch.bmm(q_nope, lw.wuk)  # [H, T, L] (hipBLASLt batched GEMM)
+    else:  # CPU reference path: fp32 math whatever the shard's storage dtypes
+      q_lat = torch.bmm(q_nope.float(), lw.wuk.float()).to(dt)
+    q_pe = q[:, H * dn:]
+    o_lat = K.mla_attn(q_lat, q_pe, cache, inp.block_tables, inp.cu_q, inp.ctx_lens, self.scale, self.ws)
+    if xn.is_cuda:
+      o = torch.bmm(o_lat, lw.wuv.transpose(1, 2))  # [H, T, dv]
+    else:
+      o = torch.bmm(o_lat.float(), lw.wuv.float().transpose(1, 2)).to(dt)
+    return o.transpose(0, 1).reshape(T, H * dv)
+
+  def _mlp(self, xn: torch.Tensor, lw, h: torch.Tensor, next_norm: Optional[torch.Tensor], li: int = -1):
     """h += MLP(xn) in place; returns rmsnorm(h) * next_norm (None if there is no following norm)."""
     c = self.c
-    if not c.is_moe:
+    if lw.router is None:
       act = linear(xn, lw.gu_w, epi="silu")
       if next_norm is not None:
         return linear_resid_norm(act, lw.down_w, h, next_norm, c.rms_norm_eps)
@@ -127,10 +171,26 @@ class ShardModel:
       return out
     return K.rmsnorm(h, next_norm, c.rms_norm_eps)[0] if next_norm is not None else None
 
-  def _moe(self, xn: torch.Tensor, lw, h: torch.Tensor, next_norm: Optional[torch.Tensor] = None):
-    """Mixtral sparse MoE: softmax top-k routing, tokens grouped per expert, expert GEMMs on the
-    kernel library (gate/up with fused SiLU epilogue), weighted scatter-add back into h."""
+  @property
+  def _ds_route(self) -> bool:
+    """DeepSeekMoE routing (groups / sigmoid / bias / unnormalised scaled weights) vs Mixtral's."""
     c = self.c
+    return not (c.topk_method == "greedy" and c.scoring_func == "softmax" and c.norm_topk_prob
+                and c.routed_scaling_factor == 1.0)
+
+  def _route_args(self):
+    c = self.c
+    method = {"greedy": 0, "group_limited_greedy": 1, "noaux_tc": 2}[c.topk_method]
+    return (c.num_experts_per_tok, c.n_group if method else 1, c.topk_group if method else 1, method,
+            c.scoring_func == "sigmoid", c.norm_topk_prob, c.routed_scaling_factor)
+
+  def _moe(self, xn: torch.Tensor, lw, h: torch.Tensor, next_norm: Optional[torch.Tensor] = None):
+    """Sparse MoE: top-k routing (Mixtral softmax, or DeepSeek's grouped / sigmoid-with-bias rules), shared
+    experts (DeepSeek) added as a dense SwiGLU, tokens grouped per expert, expert GEMMs on the kernel library
+    (gate/up with fused SiLU epilogue), weighted scatter-add back into h."""
+    c = self.c
+    if lw.sh_gu_w is not None:  # shared experts: h += down(silu(gate) * up) of every token
+      linear(linear(xn, lw.sh_gu_w, epi="silu"), lw.sh_down_w, residual=h, epi="resid", out=h)
     if xn.is_cuda and c.num_experts in (4, 8, 16) and layout_of(lw.router) == "rowmajor":
       # fp32 router logits, one small kernel (instead of a bf16 library GEMM + cast)
       logits = torch.empty(xn.shape[0], c.num_experts, dtype=torch.float32, device=xn.device)
@@ -139,9 +199,12 @@ class ShardModel:
       logits = linear(xn, lw.router, out_dtype=torch.float32)  # [T, E]
     if xn.is_cuda:
       return self._moe_gpu(xn, lw, h, logits, next_norm)
-    probs = torch.softmax(logits, dim=-1)
-    topw, topi = torch.topk(probs, c.num_experts_per_tok, dim=-1)
-    topw = topw / topw.sum(-1, keepdim=True)
+    if self._ds_route:
+      topw, topi = K.moe_route_ds(logits, lw.router_bias, *self._route_args())
+    else:
+      probs = torch.softmax(logits, dim=-1)
+      topw, topi = torch.topk(probs, c.num_experts_per_tok, dim=-1)
+      topw = topw / topw.sum(-1, keepdim=True)
     T = xn.shape[0]
     flat_e = topi.reshape(-1)
     order = torch.argsort(flat_e, stable=True)
@@ -154,7 +217,7 @@ class ShardModel:
       if n == 0:
         continue
       idx = tok[start:start + n]
-      xe = xn.index_select(0, idx)
+      xe = xn.index_select(0, idx)  # (expert weights of Fe = c.expert_dim rows)
       act = linear(xe, expert(lw.gu_w, e), epi="silu")
       ye = linear(act, expert(lw.down_w, e), out_dtype=torch.float32)
       out.index_add_(0, idx, ye * wflat[start:start + n, None])
@@ -169,7 +232,7 @@ class ShardModel:
     slots, combine kernel adding sum_j w_j * y_slot(j) into the residual stream."""
     c = self.c
     T, D = xn.shape
-    k, E, F = c.num_experts_per_tok, c.num_experts, c.intermediate_size
+    k, E, F = c.num_experts_per_tok, c.num_experts, c.expert_dim
     dev = xn.device
     C = require()
     topw = torch.empty(T * k, dtype=torch.float32, device=dev)
@@ -177,7 +240,10 @@ class ShardModel:
     slot_of = torch.empty(T * k, dtype=torch.int32, device=dev)
     sorted_tok = torch.empty(T * k, dtype=torch.int32, device=dev)
     off = torch.empty(E + 1, dtype=torch.int32, device=dev)
-    C.moe_route(logits.contiguous(), k, topw, topi, slot_of, sorted_tok, off)
+    if self._ds_route:
+      K.moe_route_ds(logits, lw.router_bias, *self._route_args(), outs=(topw, topi, slot_of, sorted_tok, off))
+    else:
+      C.moe_route(logits.contiguous(), k, topw, topi, slot_of, sorted_tok, off)
     shuffled = layout_of(lw.gu_w) == "stream" and layout_of(lw.down_w) == "stream"
     # rows per expert decide the kernel: the weight-streaming GEMM for decode-sized groups, gemm_big
     # tiles (128 or 256 rows) once the groups are compute-bound
@@ -225,16 +291,19 @@ class ShardModel:
     xn, _ = K.rmsnorm(h, w.layers[self.layer_ids[0]].ln1, c.rms_norm_eps) if n else (None, None)
     for j, li in enumerate(self.layer_ids):
       lw = w.layers[li]
-      # QKV projection + RoPE + paged KV write (split-K slabs reduced inside the RoPE kernel)
-      q = linear_rope_kv(xn, lw.qkv_w, lw.qkv_b, inp.positions, self.cos_sin, inp.slots, self.kv.k[j], self.kv.v[j],
-                         c.num_heads, c.num_kv_heads)
-      a = self._attention(q, j, inp).view(h.shape[0], c.num_heads * c.head_dim)
+      if c.is_mla:
+        a = self._mla(xn, lw, j, inp)
+      else:
+        # QKV projection + RoPE + paged KV write (split-K slabs reduced inside the RoPE kernel)
+        q = linear_rope_kv(xn, lw.qkv_w, lw.qkv_b, inp.positions, self.cos_sin, inp.slots, self.kv.k[j],
+                           self.kv.v[j], c.num_heads, c.num_kv_heads)
+        a = self._attention(q, j, inp).view(h.shape[0], c.num_heads * c.head_dim)
       # o_proj + residual + post-attention norm (one fused pass when the projection runs split-K)
       xn = linear_resid_norm(a, lw.o_w, h, lw.ln2, c.rms_norm_eps)
       # the norm that follows this layer: the next layer's input norm, or the final norm (decode: every row
       # is a sequence's last token) -- fused into the down projection's reduce the same way
       nxt = w.layers[self.layer_ids[j + 1]].ln1 if j + 1 < n else (w.norm if last and inp.decode else None)
-      xn = self._mlp(xn, lw, h, nxt)
+      xn = self._mlp(xn, lw, h, nxt, li)
     if not last:
       return h
     if not inp.decode or n == 0:

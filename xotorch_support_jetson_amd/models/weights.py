@@ -53,6 +53,16 @@ class LayerWeights:
   ln2: torch.Tensor
   qkv_b: Optional[torch.Tensor] = None
   router: Optional[torch.Tensor] = None  # MoE
+  # DeepSeek MLA: qkv_w is the fused A projection [q_a (or q) | kv latent | shared rope key]
+  q_ln: Optional[torch.Tensor] = None  # [q_lora_rank]
+  kv_ln: Optional[torch.Tensor] = None  # [kv_lora_rank]
+  qb_w: Optional[torch.Tensor] = None  # [H (dn + dr), q_lora_rank], rows [all heads' nope | all heads' rope]
+  wuk: Optional[torch.Tensor] = None  # [H, dn, kv_lora_rank]  (kv_b_proj's key rows, absorbed into q)
+  wuv: Optional[torch.Tensor] = None  # [H, dv, kv_lora_rank]  (kv_b_proj's value rows)
+  # DeepSeekMoE
+  router_bias: Optional[torch.Tensor] = None  # [E] fp32 selection bias (V3 e_score_correction_bias)
+  sh_gu_w: Optional[torch.Tensor] = None  # shared experts, gate/up interleaved [2 Fs, D]
+  sh_down_w: Optional[torch.Tensor] = None  # [D, Fs]
 
   def tensors(self) -> Dict[str, torch.Tensor]:
     return {k: v for k, v in self.__dict__.items() if isinstance(v, torch.Tensor)}
@@ -91,6 +101,9 @@ class ShardWeights:
     fused = c.model_type == "phi3"  # Phi-3 checkpoints keep qkv_proj / gate_up_proj fused
     for i, lw in self.layers.items():
       p = f"model.layers.{i}."
+      if c.is_mla:
+        _mla_to_hf(c, lw, p, sd)
+        continue
       qkv_w = permute_qk_rows(_rowmajor(lw.qkv_w), H, Hkv, Dh, c.rotary_dim, inverse=True)
       if fused:
         sd[p + "self_attn.qkv_proj.weight"] = qkv_w
@@ -128,6 +141,86 @@ class ShardWeights:
     elif self.lm_head is not None and self.embed is None:
       sd["model.embed_tokens.weight"] = _rowmajor(self.lm_head)  # tied head on a shard without the embedding
     return {k: v.contiguous() for k, v in sd.items()}
+
+
+def _mla_q_order(c: ModelConfig) -> torch.Tensor:
+  """Device row r of the q projection <- HF row: all heads' nope dims, then all heads' rope dims with the
+  interleaved pairs de-interleaved (ops.rope.interleave_perm)."""
+  from ..ops.rope import interleave_perm
+  H, dn, dr = c.num_heads, c.qk_nope_head_dim, c.qk_rope_head_dim
+  hd = dn + dr
+  nope = (torch.arange(H)[:, None] * hd + torch.arange(dn)[None, :]).reshape(-1)
+  rope = (torch.arange(H)[:, None] * hd + dn + interleave_perm(dr)[None, :]).reshape(-1)
+  return torch.cat([nope, rope])
+
+
+def _mla_kv_order(c: ModelConfig) -> torch.Tensor:
+  from ..ops.rope import interleave_perm
+  L = c.kv_lora_rank
+  return torch.cat([torch.arange(L), L + interleave_perm(c.qk_rope_head_dim)])
+
+
+def _mla_from_hf(c: ModelConfig, get, has, p: str) -> dict:
+  """HF DeepSeek attention tensors -> device layout fields of LayerWeights."""
+  a = p + "self_attn."
+  qo = _mla_q_order(c)
+  kv_a = get(a + "kv_a_proj_with_mqa.weight")
+  kv_a = kv_a.index_select(0, _mla_kv_order(c).to(kv_a.device))
+  out = {}
+  if c.q_lora_rank:
+    q_a = get(a + "q_a_proj.weight")
+    out["q_ln"] = get(a + "q_a_layernorm.weight")
+    qb = get(a + "q_b_proj.weight")
+    out["qb_w"] = qb.index_select(0, qo.to(qb.device)).contiguous()
+  else:
+    q = get(a + "q_proj.weight")
+    q_a = q.index_select(0, qo.to(q.device))
+  out["qkv_w"] = torch.cat([q_a, kv_a], 0).contiguous()
+  out["kv_ln"] = get(a + "kv_a_layernorm.weight")
+  kvb = get(a + "kv_b_proj.weight").view(c.num_heads, c.qk_nope_head_dim + c.v_head_dim, c.kv_lora_rank)
+  out["wuk"] = kvb[:, :c.qk_nope_head_dim].contiguous()
+  out["wuv"] = kvb[:, c.qk_nope_head_dim:].contiguous()
+  out["o_w"] = get(a + "o_proj.weight")
+  return out
+
+
+def _mla_to_hf(c: ModelConfig, lw: "LayerWeights", p: str, sd: Dict[str, torch.Tensor]) -> None:
+  a = p + "self_attn."
+  qo = torch.argsort(_mla_q_order(c))
+  ko = torch.argsort(_mla_kv_order(c))
+  A = _rowmajor(lw.qkv_w)
+  nq = c.q_lora_rank or c.num_heads * (c.qk_nope_head_dim + c.qk_rope_head_dim)
+  q_a, kv_a = A[:nq], A[nq:]
+  sd[a + "kv_a_proj_with_mqa.weight"] = kv_a.index_select(0, ko.to(kv_a.device))
+  if c.q_lora_rank:
+    sd[a + "q_a_proj.weight"] = q_a
+    sd[a + "q_a_layernorm.weight"] = lw.q_ln
+    qb = _rowmajor(lw.qb_w)
+    sd[a + "q_b_proj.weight"] = qb.index_select(0, qo.to(qb.device))
+  else:
+    sd[a + "q_proj.weight"] = q_a.index_select(0, qo.to(q_a.device))
+  sd[a + "kv_a_layernorm.weight"] = lw.kv_ln
+  sd[a + "kv_b_proj.weight"] = torch.cat([lw.wuk, lw.wuv], 1).reshape(-1, c.kv_lora_rank)
+  sd[a + "o_proj.weight"] = _rowmajor(lw.o_w)
+  sd[p + "input_layernorm.weight"] = lw.ln1
+  sd[p + "post_attention_layernorm.weight"] = lw.ln2
+  gu, down = _rowmajor(lw.gu_w), _rowmajor(lw.down_w)
+  g, u = split_gate_up(gu)
+  if lw.router is not None:
+    m = p + "mlp."
+    sd[m + "gate.weight"] = lw.router
+    if lw.router_bias is not None:
+      sd[m + "gate.e_score_correction_bias"] = lw.router_bias
+    for e in range(c.num_experts):
+      sd[m + f"experts.{e}.gate_proj.weight"], sd[m + f"experts.{e}.up_proj.weight"] = g[e], u[e]
+      sd[m + f"experts.{e}.down_proj.weight"] = down[e]
+    if lw.sh_gu_w is not None:
+      sg, su = split_gate_up(_rowmajor(lw.sh_gu_w))
+      sd[m + "shared_experts.gate_proj.weight"], sd[m + "shared_experts.up_proj.weight"] = sg, su
+      sd[m + "shared_experts.down_proj.weight"] = _rowmajor(lw.sh_down_w)
+  else:
+    sd[p + "mlp.gate_proj.weight"], sd[p + "mlp.up_proj.weight"] = g, u
+    sd[p + "mlp.down_proj.weight"] = down
 
 
 def _rowmajor(t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
@@ -178,6 +271,7 @@ def prepare_for_decode(sw: "ShardWeights", keep_rowmajor: Iterable[str] = ()) ->
     return out
 
   for lw in sw.layers.values():
+    lw.qb_w, lw.sh_gu_w, lw.sh_down_w = conv(lw.qb_w), conv(lw.sh_gu_w), conv(lw.sh_down_w)
     if "qkv" not in keep:
       lw.qkv_w = conv(lw.qkv_w)
     if "o" not in keep:
@@ -214,7 +308,8 @@ def copy_weights_into(dst: "ShardWeights", src: "ShardWeights") -> None:
   """Copy every tensor of the row-major `src` shard into the live inference shard `dst` in place."""
   for i, lw in dst.layers.items():
     s = src.layers[i]
-    for name in ("qkv_w", "o_w", "gu_w", "down_w", "ln1", "ln2", "qkv_b", "router"):
+    for name in ("qkv_w", "o_w", "gu_w", "down_w", "ln1", "ln2", "qkv_b", "router", "q_ln", "kv_ln", "qb_w", "wuk",
+                 "wuv", "router_bias", "sh_gu_w", "sh_down_w"):
       if getattr(lw, name) is not None and getattr(s, name) is not None:
         assign_weight(getattr(lw, name), getattr(s, name))
   if dst.embed is not None and src.embed is not None:
@@ -250,20 +345,40 @@ def random_weights(c: ModelConfig, shard: Shard, device: torch.device | str = "c
   def norm_w(g):
     return (1.0 + torch.empty(D, device=dev, dtype=torch.float32).normal_(0.0, 0.05, generator=g)).to(dtype)
 
+  def vec(n, g):
+    return (1.0 + torch.empty(n, device=dev, dtype=torch.float32).normal_(0.0, 0.05, generator=g)).to(dtype)
+
   sw = ShardWeights(c, shard)
   for i in shard.layers():
     g = gen(1000 + i)
     out_std = std / (2 * c.num_layers) ** 0.5  # GPT-2 style residual-branch scaling keeps deep stacks stable
+    moe = c.moe_layer(i)
+    Fl = c.expert_dim if moe else Fd
+    El = E if moe else 0
     lw = LayerWeights(
       qkv_w=normal((c.qkv_size, D), g),
-      o_w=normal((D, c.num_heads * c.head_dim), g, out_std),
-      gu_w=normal((E, 2 * Fd, D) if E else (2 * Fd, D), g),
-      down_w=normal((E, D, Fd) if E else (D, Fd), g, out_std),
+      o_w=normal((D, c.num_heads * (c.v_head_dim if c.is_mla else c.head_dim)), g, out_std),
+      gu_w=normal((El, 2 * Fl, D) if El else (2 * Fl, D), g),
+      down_w=normal((El, D, Fl) if El else (D, Fl), g, out_std),
       ln1=norm_w(g),
       ln2=norm_w(g),
-      qkv_b=normal((c.qkv_size,), g) if c.attention_bias else None,
-      router=normal((E, D), g, 0.1) if E else None,
+      qkv_b=normal((c.qkv_size,), g) if c.attention_bias and not c.is_mla else None,
+      router=normal((El, D), g, 0.1) if El else None,
     )
+    if c.is_mla:
+      H, L = c.num_heads, c.kv_lora_rank
+      if c.q_lora_rank:
+        lw.q_ln = vec(c.q_lora_rank, g)
+        lw.qb_w = normal((H * (c.qk_nope_head_dim + c.qk_rope_head_dim), c.q_lora_rank), g)
+      lw.kv_ln = vec(L, g)
+      lw.wuk = normal((H, c.qk_nope_head_dim, L), g)
+      lw.wuv = normal((H, c.v_head_dim, L), g)
+    if moe and c.scoring_func == "sigmoid":
+      lw.router_bias = torch.empty(El, device=dev, dtype=torch.float32).normal_(0.0, 0.01, generator=g)
+    if moe and c.n_shared_experts:
+      Fs = c.n_shared_experts * c.expert_dim
+      lw.sh_gu_w = normal((2 * Fs, D), g)
+      lw.sh_down_w = normal((D, Fs), g, out_std)
     sw.layers[i] = lw
   if _needs_embed(c, shard):
     sw.embed = normal((c.vocab_size, D), gen(1))
@@ -323,11 +438,11 @@ def load_hf_weights(model_dir: str | Path, c: ModelConfig, shard: Shard, device=
   wm = _weight_map(model_dir)
   handles = {}
 
-  def get(name: str) -> torch.Tensor:
+  def get(name: str, dt: Optional[torch.dtype] = None) -> torch.Tensor:
     fname = wm[name]
     if fname not in handles:
       handles[fname] = safe_open(str(model_dir / fname), framework="pt")
-    return handles[fname].get_tensor(name).to(device=device, dtype=dtype)
+    return handles[fname].get_tensor(name).to(device=device, dtype=dt or dtype)
 
   def has(name: str) -> bool:
     return name in wm
@@ -337,6 +452,9 @@ def load_hf_weights(model_dir: str | Path, c: ModelConfig, shard: Shard, device=
   sw = ShardWeights(c, shard)
   for i in shard.layers():
     p = f"model.layers.{i}."
+    if c.is_mla:
+      sw.layers[i] = _load_deepseek_layer(c, i, p, get, has)
+      continue
     if has(p + "self_attn.qkv_proj.weight"):  # Phi-3: fused [q; k; v]
       qkv = get(p + "self_attn.qkv_proj.weight")
     else:
@@ -371,6 +489,31 @@ def load_hf_weights(model_dir: str | Path, c: ModelConfig, shard: Shard, device=
     else:
       sw.lm_head = sw.embed
   return sw
+
+
+def _load_deepseek_layer(c: ModelConfig, i: int, p: str, get, has) -> LayerWeights:
+  f = _mla_from_hf(c, get, has, p)
+  m = p + "mlp."
+  lw = LayerWeights(f["qkv_w"], f["o_w"], None, None, get(p + "input_layernorm.weight"),
+                    get(p + "post_attention_layernorm.weight"), None, None, f.get("q_ln"), f["kv_ln"], f.get("qb_w"),
+                    f["wuk"], f["wuv"])
+  if c.moe_layer(i):
+    lw.gu_w = torch.stack([interleave_gate_up(get(m + f"experts.{e}.gate_proj.weight"),
+                                              get(m + f"experts.{e}.up_proj.weight")) for e in range(c.num_experts)])
+    lw.down_w = torch.stack([get(m + f"experts.{e}.down_proj.weight") for e in range(c.num_experts)])
+    lw.router = get(m + "gate.weight")
+    if has(m + "gate.e_score_correction_bias"):
+      lw.router_bias = get(m + "gate.e_score_correction_bias", torch.float32)
+    elif c.scoring_func == "sigmoid":
+      lw.router_bias = torch.zeros(c.num_experts, dtype=torch.float32, device=lw.router.device)
+    if c.n_shared_experts:
+      lw.sh_gu_w = interleave_gate_up(get(m + "shared_experts.gate_proj.weight"),
+                                      get(m + "shared_experts.up_proj.weight")).contiguous()
+      lw.sh_down_w = get(m + "shared_experts.down_proj.weight")
+  else:
+    lw.gu_w = interleave_gate_up(get(m + "gate_proj.weight"), get(m + "up_proj.weight")).contiguous()
+    lw.down_w = get(m + "down_proj.weight")
+  return lw
 
 
 def from_hf_state_dict(sd: Dict[str, torch.Tensor], c: ModelConfig, shard: Shard, device="cpu",

@@ -289,3 +289,73 @@ def topk_cand(logits: torch.Tensor, top_k: int, kc: int = 64) -> tuple:
   idx = torch.empty(B, kc, dtype=torch.int32, device=logits.device)
   require().topk_cand(logits, int(top_k), vals, idx)
   return vals, idx
+
+
+# ------------------------------------------------------------------ DeepSeek MLA
+def mla_prep(ckv, kv_ln, q, qpe_off: int, H: int, pos, cos_sin, slots, cache, eps: float) -> None:
+  """ckv [T, >= DL+DR] (rows may be strided), q [T, ldq]: latent norm + rope + cache write, q_pe rotated
+  in place."""
+  if not _gpu(ckv):
+    ref.mla_prep(ckv, kv_ln, q, qpe_off, H, pos, cos_sin, slots, cache, eps)
+    return
+  require().mla_prep(ckv, kv_ln, q, int(qpe_off), int(H), pos, cos_sin, slots, cache, float(eps))
+
+
+class MLAWorkspace:
+  """Split-KV scratch of the MLA attention kernel."""
+
+  def __init__(self, max_tokens: int, H: int, DL: int, max_ctx: int, device):
+    self.max_tokens, self.H, self.DL = max_tokens, H, DL
+    self.pages = max(1, -(-max_ctx // PAGE))
+    self.max_parts = self.partition(1, self.pages)[1]
+    units = max(max_tokens * self.max_parts, 1)
+    self.o = torch.empty(units * H * DL, dtype=torch.float32, device=device)
+    self.ml = torch.empty(units * H * 2, dtype=torch.float32, device=device)
+
+  def partition(self, T: int, width_pages: int):
+    """(pages per partition, partitions): enough workgroups for 256 CUs (one per CU: the kernel holds two
+    73 KB pages in LDS), partitions of at least 2 pages."""
+    nhb = -(-self.H // 16)
+    want = max(1, -(-256 // max(T * nhb, 1)))
+    nparts = max(1, min(want, width_pages // 2 if width_pages >= 2 else 1))
+    ppp = -(-width_pages // nparts)
+    return ppp, -(-width_pages // ppp)
+
+
+def mla_attn(q_lat, q_pe, cache, block_tables, cu_q, ctx_lens, scale: float, ws: MLAWorkspace | None = None,
+             out: torch.Tensor | None = None) -> torch.Tensor:
+  """q_lat [H, T, DL], q_pe [T, >= H*DR] (row-major, strided rows ok) -> o_lat [H, T, DL]."""
+  if not _gpu(q_lat):
+    y = ref.mla_attn(q_lat, q_pe, cache, block_tables, cu_q, ctx_lens, scale)
+    if out is not None:
+      out.copy_(y)
+      return out
+    return y
+  H, T, DL = q_lat.shape
+  width = block_tables.shape[1]
+  if ws is None:
+    ws = MLAWorkspace(T, H, DL, width * PAGE, q_lat.device)
+  ppp, nparts = ws.partition(T, width)
+  if T * nparts > ws.max_tokens * ws.max_parts:
+    ppp, nparts = width, 1
+  out = torch.empty_like(q_lat) if out is None else out
+  require().mla_attn(q_lat, q_pe, cache, block_tables, cu_q, ctx_lens, out, ws.o, ws.ml, int(ppp), int(nparts),
+                     float(scale))
+  return out
+
+
+def moe_route_ds(logits, bias, k: int, n_group: int, topk_group: int, method: int, sigmoid: bool, norm: bool,
+                 scale: float, outs: tuple | None = None):
+  """DeepSeekMoE routing.  GPU: (topw, topi, slot_of, sorted_tok, off) device tensors (graph-capturable);
+  CPU: (topw [T, k], topi [T, k])."""
+  if not _gpu(logits):
+    return ref.moe_route_ds(logits, bias, k, n_group, topk_group, method, sigmoid, norm, scale)
+  T, E = logits.shape
+  dev = logits.device
+  if outs is None:
+    outs = (torch.empty(T * k, dtype=torch.float32, device=dev), torch.empty(T * k, dtype=torch.int32, device=dev),
+            torch.empty(T * k, dtype=torch.int32, device=dev), torch.empty(T * k, dtype=torch.int32, device=dev),
+            torch.empty(E + 1, dtype=torch.int32, device=dev))
+  require().moe_route_ds(logits.contiguous(), bias, int(k), int(n_group), int(topk_group), int(method), bool(sigmoid),
+                         bool(norm), float(scale), *outs)
+  return outs

@@ -128,3 +128,62 @@ def cross_entropy(logits: torch.Tensor, targets: torch.Tensor):
   picked = lf.gather(1, tgt[:, None])[:, 0]
   loss = torch.where(valid, lse - picked, torch.zeros_like(lse))
   return loss, lse
+
+
+# ------------------------------------------------------------------ DeepSeek MLA / MoE routing
+def mla_prep(ckv, kv_ln, q, qpe_off: int, H: int, pos, cos_sin, slots, cache, eps: float):
+  """Latent rmsnorm (HF DeepseekV2RMSNorm rounding: normalise, cast, times weight) + rope of the shared
+  key -> cache[slot] = [c | k_pe]; q_pe of every head rotated in place.  cache [pages, 64, DL + DR]."""
+  DL = kv_ln.numel()
+  DR = cos_sin.shape[1]
+  T = ckv.shape[0]
+  x = ckv[:, :DL].float()
+  c = (x * torch.rsqrt(x.pow(2).mean(-1, keepdim=True) + eps)).to(ckv.dtype).float() * kv_ln.float()
+  kpe = rope(ckv[:, DL:DL + DR].reshape(T, 1, DR), pos, cos_sin)[:, 0]
+  qpe = q[:, qpe_off:qpe_off + H * DR].reshape(T, H, DR)
+  q[:, qpe_off:qpe_off + H * DR] = rope(qpe, pos, cos_sin).reshape(T, H * DR)
+  ok = slots >= 0
+  flat = cache.view(-1, cache.shape[-1])
+  row = torch.cat([c.to(cache.dtype), kpe.to(cache.dtype)], 1)
+  flat[slots[ok].long()] = row[ok]
+
+
+def mla_attn(q_lat, q_pe, cache, block_tables, cu_q, ctx_lens, scale: float):
+  """q_lat [H, T, DL], q_pe [T, >= H*DR] -> o_lat [H, T, DL]: causal multi-query attention over the latent."""
+  H, T, DL = q_lat.shape
+  DR = cache.shape[-1] - DL
+  out = torch.zeros_like(q_lat)
+  for b in range(ctx_lens.numel()):
+    q0, q1 = int(cu_q[b]), int(cu_q[b + 1])
+    n = int(ctx_lens[b])
+    if q1 <= q0 or n <= 0:
+      continue
+    npg = -(-n // PAGE)
+    lat = cache[block_tables[b, :npg].long()].reshape(npg * PAGE, -1)[:n].float()  # [n, DL + DR]
+    qf = torch.cat([q_lat[:, q0:q1].float(), q_pe[q0:q1, :H * DR].reshape(q1 - q0, H, DR).permute(1, 0, 2).float()], 2)
+    s = torch.einsum("hsd,td->hst", qf, lat) * scale
+    qpos = torch.arange(q1 - q0)[:, None] + (n - (q1 - q0))
+    s = s.masked_fill(torch.arange(n)[None, :] > qpos, float("-inf"))
+    p = torch.softmax(s, -1)
+    out[:, q0:q1] = torch.einsum("hst,td->hsd", p, lat[:, :DL]).to(out.dtype)
+  return out
+
+
+def moe_route_ds(logits, bias, k: int, n_group: int, topk_group: int, method: int, sigmoid: bool, norm: bool,
+                 scale: float):
+  """HF DeepseekV2TopkRouter / DeepseekV3TopkRouter -> (topw [T, k], topi [T, k])."""
+  lf = logits.float()
+  scores = torch.sigmoid(lf) if sigmoid else torch.softmax(lf, -1)
+  choice = scores + bias.float() if bias is not None else scores
+  T, E = lf.shape
+  if n_group > 1 and topk_group < n_group:
+    g = choice.view(T, n_group, E // n_group)
+    gs = g.topk(2, -1).values.sum(-1) if method == 2 else g.max(-1).values
+    keep = torch.zeros_like(gs).scatter_(1, gs.topk(topk_group, -1).indices, 1.0)
+    mask = keep[:, :, None].expand(T, n_group, E // n_group).reshape(T, E).bool()
+    choice = choice.masked_fill(~mask, float("-inf"))
+  topi = choice.topk(k, -1).indices
+  topw = scores.gather(1, topi)
+  if norm:
+    topw = topw / (topw.sum(-1, keepdim=True) + 1e-20)
+  return topw * scale, topi

@@ -40,7 +40,41 @@ def inv_frequencies(head_dim: int, theta: float, scaling: dict | None) -> torch.
     return torch.where(medium, smoothed, scaled)
   if kind == "linear":
     return inv / float(scaling.get("factor", 1.0))
+  if kind == "yarn":  # HF _compute_yarn_parameters (DeepSeek-V2/V3)
+    dim, base = head_dim, theta
+    factor = float(scaling["factor"])
+    orig = float(scaling["original_max_position_embeddings"])
+    beta_fast, beta_slow = float(scaling.get("beta_fast") or 32), float(scaling.get("beta_slow") or 1)
+
+    def corr(rot):
+      return (dim * math.log(orig / (rot * 2 * math.pi))) / (2 * math.log(base))
+    lo, hi = corr(beta_fast), corr(beta_slow)
+    if scaling.get("truncate", True):
+      lo, hi = math.floor(lo), math.ceil(hi)
+    lo, hi = max(lo, 0), min(hi, dim - 1)
+    if lo == hi:
+      hi += 0.001
+    ramp = ((torch.arange(dim // 2, dtype=torch.float64) - lo) / (hi - lo)).clamp(0, 1)
+    extrap = 1.0 - ramp
+    pos_freqs = base ** (torch.arange(0, dim, 2, dtype=torch.float64) / dim)
+    return (1.0 / (factor * pos_freqs)) * (1 - extrap) + (1.0 / pos_freqs) * extrap
   return inv
+
+
+def yarn_attention_factor(scaling: dict | None) -> float:
+  """The factor HF YaRN multiplies cos / sin by (1 for DeepSeek, whose mscale == mscale_all_dim)."""
+  if not scaling or scaling.get("rope_type") != "yarn":
+    return 1.0
+  if scaling.get("attention_factor") is not None:
+    return float(scaling["attention_factor"])
+  f = float(scaling["factor"])
+
+  def ms(scale, m=1.0):
+    return 1.0 if scale <= 1 else 0.1 * m * math.log(scale) + 1.0
+  m, mad = scaling.get("mscale"), scaling.get("mscale_all_dim")
+  if m and mad:
+    return ms(f, float(m)) / ms(f, float(mad))
+  return ms(f)
 
 
 def build_cos_sin(head_dim: int, max_pos: int, theta: float = 10000.0, scaling: dict | None = None,
@@ -66,7 +100,8 @@ def build_cos_sin(head_dim: int, max_pos: int, theta: float = 10000.0, scaling: 
     cos, sin = ang.cos() * attn, ang.sin() * attn
   else:
     ang = torch.outer(pos, inv_frequencies(R, theta, scaling))
-    cos, sin = ang.cos(), ang.sin()
+    af = yarn_attention_factor(scaling)
+    cos, sin = ang.cos() * af, ang.sin() * af
   if R < head_dim:
     pad = head_dim // 2 - R // 2
     cos = torch.cat([cos, torch.ones(cos.shape[0], pad, dtype=cos.dtype)], 1)
@@ -75,9 +110,16 @@ def build_cos_sin(head_dim: int, max_pos: int, theta: float = 10000.0, scaling: 
 
 
 def rope_table(c, max_pos: int, device: torch.device | str = "cpu") -> torch.Tensor:
-  """The table for a ModelConfig (rotary dims, scaling and theta from the config).  LongRoPE tables
-  hold 2 max_pos rows: the short-factor rows, then the long-factor rows (see rope_shift)."""
-  return build_cos_sin(c.head_dim, max_pos, c.rope_theta, c.rope_scaling, device, rotary_dim=c.rotary_dim)
+  """The table for a ModelConfig (rotary dims, scaling and theta from the config; MLA models rotate
+  their qk_rope_head_dim slice).  LongRoPE tables hold 2 max_pos rows: the short-factor rows, then the
+  long-factor rows (see rope_shift)."""
+  return build_cos_sin(c.rope_dim, max_pos, c.rope_theta, c.rope_scaling, device, rotary_dim=c.rotary_dim)
+
+
+def interleave_perm(d: int) -> torch.Tensor:
+  """DeepSeek rotates interleaved pairs (2j, 2j+1): kernel dim p <- HF dim perm[p] = evens, then odds,
+  so the pairs become the kernels' rotate-half pairs (j, j + d/2)."""
+  return torch.cat([torch.arange(0, d, 2), torch.arange(1, d, 2)])
 
 
 def longrope_window(c) -> Optional[int]:

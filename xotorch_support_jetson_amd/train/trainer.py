@@ -40,6 +40,9 @@ class ShardTrainer:
                weight_decay: float = 0.0, max_seq: int = 4096, grad_clip: float = 1.0):
     self.w = weights
     self.c: ModelConfig = weights.config
+    if self.c.is_mla:
+      raise NotImplementedError(f"{self.c.model_type}: fine-tuning of MLA (DeepSeek) shards is not implemented; "
+                                "they serve (inference) only")
     self.shard = weights.shard
     self.device = torch.device(device)
     self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
