@@ -367,6 +367,29 @@ def test_gemm_stream(gpu, M, epi, ntw, splits):
     assert rel_err(y2, ref) < 1e-2
 
 
+@pytest.mark.parametrize("M", [1, 33, 200])
+@pytest.mark.parametrize("Kd", [128, 384, 1408])
+@pytest.mark.parametrize("epi", ["none", "silu"])
+def test_gemm_stream_odd_chunks(gpu, M, Kd, epi):
+  """An odd number of 128-deep k-chunks (single-chunk tail; e.g. DeepSeek-V2-Lite's 1408-wide experts)."""
+  from xotorch_support_jetson_amd.ops._ext import require
+  from xotorch_support_jetson_amd.ops.weights_layout import shuffle_for_stream
+  torch.manual_seed(Kd + M)
+  N = 512
+  x = torch.randn(M, Kd, device=gpu, dtype=torch.bfloat16)
+  w = torch.randn(N, Kd, device=gpu, dtype=torch.bfloat16) / math.sqrt(Kd)
+  full = R.linear(x, w, None)
+  if epi == "silu":
+    f = full.view(M, N // 32, 2, 16)
+    ref = (torch.nn.functional.silu(f[:, :, 0]) * f[:, :, 1]).reshape(M, N // 2)
+  else:
+    ref = full
+  for shuf in (False, True):
+    y = torch.empty(M, N // 2 if epi == "silu" else N, device=gpu, dtype=torch.bfloat16)
+    require().gemm_stream(x, shuffle_for_stream(w) if shuf else w, y, None, None, None, K.EPI[epi], 2, 1, shuf)
+    assert rel_err(y, ref) < 1e-2, shuf
+
+
 @pytest.mark.parametrize("M", [1, 77, 256, 300, 512, 700])
 @pytest.mark.parametrize("epi,bn,splits", [("none", 256, 1), ("none", 128, 1), ("resid", 256, 1), ("silu", 256, 1),
                                            ("silu", 128, 1), ("none", 256, 3), ("resid", 128, 2), ("silu", 256, 5),
@@ -417,16 +440,18 @@ def test_gemm_big_exact_layout(gpu):
 
 
 # ------------------------------------------------------------------ mixture of experts
-@pytest.mark.parametrize("T,E,k", [(1, 8, 2), (7, 8, 2), (100, 8, 2), (300, 4, 2), (64, 16, 4)])
+@pytest.mark.parametrize("T,E,k,F", [(1, 8, 2, 512), (7, 8, 2, 512), (100, 8, 2, 512), (300, 4, 2, 512),
+                                     (64, 16, 4, 512), (64, 16, 4, 384), (1, 8, 2, 384)])
 @pytest.mark.parametrize("shuffled", [False, True])
-def test_moe_layer(gpu, T, E, k, shuffled):
+def test_moe_layer(gpu, T, E, k, F, shuffled):
   """route -> grouped gate/up (gathered rows, SiLU*mul) -> grouped down -> combine, vs an fp32
-  per-expert reference of the same Mixtral MoE block."""
+  per-expert reference of the same Mixtral MoE block (F = 384: an odd count of 128-deep k-chunks in the
+  down projection, as DeepSeek-V2-Lite's 1408)."""
   from xotorch_support_jetson_amd.ops._ext import require
   from xotorch_support_jetson_amd.ops.weights_layout import shuffle_for_stream
   torch.manual_seed(T + E)
   C = require()
-  D, F = 256, 512
+  D = 256
   x = torch.randn(T, D, device=gpu).to(torch.bfloat16)
   h = torch.randn(T, D, device=gpu).to(torch.bfloat16)
   router = torch.randn(T, E, device=gpu, dtype=torch.float32)
@@ -455,7 +480,8 @@ def test_moe_layer(gpu, T, E, k, shuffled):
   dw = torch.stack([shuffle_for_stream(down[e]) for e in range(E)]) if shuffled else down
   act = torch.empty(T * k, F, dtype=torch.bfloat16, device=gpu)
   C.gemm_moe(x, gw, act, off, sorted_tok, 2, T, shuffled)
-  for S in (1, 2):  # down projection whole, and split over K into two fp32 slabs summed by the combine
+  Ss = (1, 2) if F % 256 == 0 else (1, 3)
+  for S in Ss:  # down projection whole, and split over K into fp32 slabs summed by the combine
     y = torch.empty(S * T * k, D, dtype=torch.float32, device=gpu)
     C.gemm_moe(act, dw, y, off, None, 0, T, shuffled, S)
     out = h.clone()
@@ -472,7 +498,7 @@ def test_moe_layer(gpu, T, E, k, shuffled):
       act2 = torch.empty_like(act)
       C.gemm_moe(x, gw, act2, off, sorted_tok, 2, T, True, 1, bm)
       assert rel_err(act2, act) < 1e-2, bm
-      for S in (1, 2):
+      for S in Ss:
         y = torch.empty(S * T * k, D, dtype=torch.float32, device=gpu)
         C.gemm_moe(act2, dw, y, off, None, 0, T, True, S, bm)
         out = h.clone()

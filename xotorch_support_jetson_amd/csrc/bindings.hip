@@ -421,11 +421,13 @@ void moe_route(const at::Tensor& logits, int64_t k, at::Tensor& topw, at::Tensor
 }
 
 void moe_route_ds(const at::Tensor& logits, const c10::optional<at::Tensor>& bias, int64_t k, int64_t n_group,
-                  int64_t topk_group, int64_t method, bool sigmoid, bool norm, double scale, at::Tensor& topw,
-                  at::Tensor& topi, at::Tensor& slot_of, at::Tensor& sorted_tok, at::Tensor& off) {
+                  int64_t topk_group, int64_t method, bool sigmoid, bool norm, double scale, at::Tensor& cnt,
+                  at::Tensor& topw, at::Tensor& topi, at::Tensor& slot_of, at::Tensor& sorted_tok, at::Tensor& off) {
   CHECK_GPU(logits);
   CHECK_DT(logits, at::kFloat);
-  XCHECK(all_contig_gpu(logits, topw, topi, slot_of, sorted_tok, off), "moe_route_ds: tensors must be contiguous GPU");
+  CHECK_DT(cnt, at::kInt);
+  XCHECK(all_contig_gpu(logits, cnt, topw, topi, slot_of, sorted_tok, off), "moe_route_ds: tensors must be contiguous GPU");
+  XCHECK(cnt.numel() >= logits.size(1), "moe_route_ds: cnt needs one (zeroed) counter per expert");
   const int64_t T = logits.size(0), E = logits.size(1);
   if (bias.has_value()) {
     CHECK_DT((*bias), at::kFloat);
@@ -441,7 +443,7 @@ void moe_route_ds(const at::Tensor& logits, const c10::optional<at::Tensor>& bia
          "moe_route_ds: output sizes");
   const int rc = xot::launch_moe_route_ds(logits.data_ptr<float>(), bias.has_value() ? bias->data_ptr<float>() : nullptr,
                                           (int)T, (int)E, (int)k, (int)n_group, (int)topk_group, (int)method, sigmoid,
-                                          norm, (float)scale, topw.data_ptr<float>(), topi.data_ptr<int>(),
+                                          norm, (float)scale, cnt.data_ptr<int>(), topw.data_ptr<float>(), topi.data_ptr<int>(),
                                           slot_of.data_ptr<int>(), sorted_tok.data_ptr<int>(), off.data_ptr<int>(),
                                           cur_stream());
   XCHECK(rc == 0, "moe_route_ds: unsupported E=", E, " k=", k, " groups=", n_group, "/", topk_group);

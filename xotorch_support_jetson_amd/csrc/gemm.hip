@@ -316,14 +316,17 @@ __global__ __launch_bounds__(256, OCC) void gemm_stream_kernel(const uint16_t* _
 #pragma unroll
     for (int j = 0; j < NTW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // nch is even and >= 2 (checked by the dispatcher): prologue loads chunks 0 and 1
+  // nch >= 1: prologue loads chunks 0 and 1.  An odd chunk count (grouped GEMMs over K = 128 * odd, e.g.
+  // DeepSeek-V2-Lite's 1408-wide experts) re-loads the last chunk where a pair would run past it (the
+  // loads stay unconditional) and finishes with a single-chunk tail.
+  const int last = nch - 1;
   s16x8 xr[XPT];
   s16x8 wa[NTW][KS], wb[NTW][KS];
   xload(xr, 0);
   wload(wa, 0);
   xstore(xr, 0);
-  xload(xr, 1);
-  wload(wb, 1);
+  xload(xr, min(1, last));
+  wload(wb, min(1, last));
   __syncthreads();
 
   // A fragments are software-pipelined LDPF reads ahead of their MFMAs; the scheduling fences keep
@@ -364,14 +367,18 @@ __global__ __launch_bounds__(256, OCC) void gemm_stream_kernel(const uint16_t* _
     compute(wb, 1);
     xstore(xr, 0);
     __syncthreads();
-    xload(xr, ch + 3);
-    wload(wb, ch + 3);
+    xload(xr, min(ch + 3, last));
+    wload(wb, min(ch + 3, last));
   }
-  // tail: chunks nch-2 (wa, buf 0) and nch-1 (wb / xr)
-  compute(wa, 0);
-  xstore(xr, 1);
-  __syncthreads();
-  compute(wb, 1);
+  if (nch & 1) {
+    compute(wa, 0);  // tail: chunk nch-1 (wa, buf 0)
+  } else {
+    // tail: chunks nch-2 (wa, buf 0) and nch-1 (wb / xr)
+    compute(wa, 0);
+    xstore(xr, 1);
+    __syncthreads();
+    compute(wb, 1);
+  }
 
   if constexpr (SPLIT) {
     float* slab = ws + ((size_t)blockIdx.y * Mtot + m_base) * N;
@@ -513,7 +520,7 @@ static int stream_dispatch(const uint16_t* X, int ldx, const uint16_t* W, int ld
   if (ntw == 4 && mt <= 2) ntw = 2;
   if (N % (64 * ntw) != 0 || S < 1) return -1;
   const int KS = 4;
-  if (K % (S * 64 * KS) != 0) return -1;  // an even number (>= 2) of k-chunks per workgroup
+  if (K % (S * 32 * KS) != 0) return -1;  // whole 128-deep k-chunks per workgroup (odd counts: single tail)
   if (S > 1 && (ws == nullptr || ws_elems < (long)S * M * N)) return -1;
   // in-launch split-K combine needs one ticket per (column tile, 128-row block)
   if (S == 1 || !reduce || tickets_n < (long)(N / (64 * ntw)) * ((M + 127) / 128)) tickets = nullptr;
@@ -576,7 +583,7 @@ int launch_gemm_moe(const uint16_t* X, int ldx, const uint16_t* W, void* Y, int 
                     const int* off, const int* gather, int E, int max_rows, int N, int K, bool wshuf, int S,
                     long ysplit, hipStream_t s) {
   if (max_rows <= 0) return 0;
-  if (N % 128 != 0 || S < 1 || K % (256 * S) != 0) return -1;
+  if (N % 128 != 0 || S < 1 || K % (128 * S) != 0) return -1;
   if (epi != EPI_NONE && epi != EPI_SILU) return -1;
   if (epi == EPI_SILU && out_f32) return -1;
   if (S > 1 && (epi != EPI_NONE || !out_f32)) return -1;  // K slices write fp32 partial slabs

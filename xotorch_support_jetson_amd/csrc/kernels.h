@@ -59,9 +59,10 @@ void launch_moe_route(const float* logits, int T, int E, int k, float* topw, int
 void launch_moe_combine(const float* y, const int32_t* slot_of, const float* topw, uint16_t* h, int T, int k, int D,
                         int S, long ysplit, hipStream_t s);
 // DeepSeekMoE routing: method 0 greedy, 1 group max (V2 group_limited_greedy), 2 group top-2 sum (V3 noaux_tc)
+// cnt: [E] int32 counters, zero on entry and left zero on exit
 int launch_moe_route_ds(const float* logits, const float* bias, int T, int E, int k, int n_group, int topk_group,
-                        int method, bool sigmoid, bool norm, float scale, float* topw, int32_t* topi, int32_t* slot_of,
-                        int32_t* sorted_tok, int32_t* off, hipStream_t s);
+                        int method, bool sigmoid, bool norm, float scale, int* cnt, float* topw, int32_t* topi,
+                        int32_t* slot_of, int32_t* sorted_tok, int32_t* off, hipStream_t s);
 // DeepSeek MLA: latent norm + rope + latent cache write (q_pe rotated in place), and the absorbed attention
 void launch_mla_prep(const uint16_t* ckv, long ldc, const uint16_t* kv_ln, uint16_t* q, long ldq, long qpe_off,
                      const int32_t* pos, const float* cos_sin, const int64_t* slots, uint16_t* cache, int T, int H,

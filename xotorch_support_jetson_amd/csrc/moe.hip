@@ -79,94 +79,151 @@ __global__ __launch_bounds__(1024) void moe_route_kernel(const float* __restrict
   }
 }
 
-// DeepSeekMoE routing (HF DeepseekV2TopkRouter / DeepseekV3TopkRouter), one workgroup, one thread per token:
+// DeepSeekMoE routing (HF DeepseekV2TopkRouter / DeepseekV3TopkRouter):
 //   score = softmax(logits) (V2) or sigmoid(logits) (V3); choice = score + bias (V3 selection bias)
 //   groups: experts in n_group equal groups; keep the topk_group groups ranked by max(choice) (V2
 //   group_limited_greedy) or the sum of their two best choices (V3 noaux_tc); top-k experts by choice among
 //   the kept groups; weight = score (not choice), optionally renormalised, times routed_scaling_factor.
-// Then the same per-expert slot order as moe_route_kernel.
+// Kernel 1: one wave per token (lane l holds experts l, l+64, ..); group statistics from an LDS copy of the
+// token's choices; k rounds of a wave argmax; per-expert counts by global atomics.  Kernel 2 (one workgroup):
+// exclusive scan of the counts -> expert offsets, slot per (token, j), and the counters reset to zero for
+// the next launch (so the graph-captured sequence needs no memset).
 constexpr int MOE_DS_MAX_E = 256;
 constexpr int MOE_DS_MAX_G = 16;
-__global__ __launch_bounds__(1024) void moe_route_ds_kernel(const float* __restrict__ logits,
-                                                            const float* __restrict__ bias, int T, int E, int k,
-                                                            int n_group, int topk_group, int method, int sigmoid,
-                                                            int norm, float scale, float* __restrict__ topw,
-                                                            int32_t* __restrict__ topi, int32_t* __restrict__ slot_of,
-                                                            int32_t* __restrict__ sorted_tok, int32_t* __restrict__ off) {
-  __shared__ int cnt[MOE_DS_MAX_E];
-  __shared__ int base[MOE_DS_MAX_E + 1];
-  const int tid = threadIdx.x;
-  for (int e = tid; e < MOE_DS_MAX_E; e += blockDim.x) cnt[e] = 0;
-  __syncthreads();
+constexpr int MOE_DS_EPL = MOE_DS_MAX_E / 64;  // experts per lane
+
+__global__ __launch_bounds__(256) void moe_topk_ds_kernel(const float* __restrict__ logits,
+                                                          const float* __restrict__ bias, int T, int E, int k,
+                                                          int n_group, int topk_group, int method, int sigmoid,
+                                                          int norm, float scale, float* __restrict__ topw,
+                                                          int32_t* __restrict__ topi, int* __restrict__ cnt) {
+  __shared__ float ch_lds[4][MOE_DS_MAX_E];
+  __shared__ unsigned keep_lds[4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int t = blockIdx.x * 4 + wave;
+  if (t >= T) return;  // wave-uniform; no workgroup barrier below
+  const float* lg = logits + (size_t)t * E;
+  float sc[MOE_DS_EPL], chv[MOE_DS_EPL];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < MOE_DS_EPL; ++i) {
+    const int e = lane + 64 * i;
+    sc[i] = e < E ? lg[e] : -INFINITY;
+    mx = fmaxf(mx, sc[i]);
+  }
+  if (!sigmoid) {
+    mx = wave_max(mx);
+    float den = 0.f;
+#pragma unroll
+    for (int i = 0; i < MOE_DS_EPL; ++i) {
+      sc[i] = lane + 64 * i < E ? __expf(sc[i] - mx) : 0.f;
+      den += sc[i];
+    }
+    den = wave_sum(den);
+#pragma unroll
+    for (int i = 0; i < MOE_DS_EPL; ++i) sc[i] /= den;
+  } else {
+#pragma unroll
+    for (int i = 0; i < MOE_DS_EPL; ++i) sc[i] = lane + 64 * i < E ? 1.f / (1.f + __expf(-sc[i])) : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < MOE_DS_EPL; ++i) {
+    const int e = lane + 64 * i;
+    chv[i] = e < E ? sc[i] + (bias != nullptr ? bias[e] : 0.f) : -INFINITY;
+    if (e < E) ch_lds[wave][e] = chv[i];
+  }
   const int per = E / n_group;
-  for (int t = tid; t < T; t += blockDim.x) {
-    const float* lg = logits + (size_t)t * E;
-    float mx = -INFINITY, den = 0.f;
-    if (!sigmoid) {
-      for (int e = 0; e < E; ++e) mx = fmaxf(mx, lg[e]);
-      for (int e = 0; e < E; ++e) den += __expf(lg[e] - mx);
-    }
-    auto score = [&](int e) { return sigmoid ? 1.f / (1.f + __expf(-lg[e])) : __expf(lg[e] - mx) / den; };
-    auto choice = [&](int e) { return score(e) + (bias != nullptr ? bias[e] : 0.f); };
-    // group selection (bitmask of kept groups)
-    unsigned keep = 0xffffffffu;
-    if (n_group > 1 && topk_group < n_group) {
-      float gs[MOE_DS_MAX_G];
-      for (int gi = 0; gi < n_group; ++gi) {
-        float a = -INFINITY, b2 = -INFINITY;
-        for (int e = gi * per; e < (gi + 1) * per; ++e) {
-          const float v = choice(e);
-          if (v > a) {
-            b2 = a;
-            a = v;
-          } else if (v > b2) {
-            b2 = v;
-          }
-        }
-        gs[gi] = method == 2 ? a + b2 : a;
-      }
-      keep = 0;
-      for (int j = 0; j < topk_group; ++j) {
-        int best = -1;
-        for (int gi = 0; gi < n_group; ++gi)
-          if (!(keep >> gi & 1u) && (best < 0 || gs[gi] > gs[best])) best = gi;
-        keep |= 1u << best;
-      }
-    }
-    float sel_v[MOE_MAX_K];
-    int sel_i[MOE_MAX_K];
-    for (int j = 0; j < k; ++j) {
-      sel_v[j] = -INFINITY;
-      sel_i[j] = 0;
-    }
-    for (int e = 0; e < E; ++e) {
-      if (!(keep >> (e / per) & 1u)) continue;
-      float v = choice(e);
-      int id = e;
-      for (int j = 0; j < k; ++j) {
-        if (v > sel_v[j]) {
-          const float tv = sel_v[j];
-          const int ti = sel_i[j];
-          sel_v[j] = v;
-          sel_i[j] = id;
-          v = tv;
-          id = ti;
+  unsigned keep = 0xffffffffu;
+  if (n_group > 1 && topk_group < n_group) {
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    // lane g < n_group: its group's best (V2) or best-two sum (V3) over the LDS copy
+    float gsc = -INFINITY;
+    if (lane < n_group) {
+      float a = -INFINITY, b2 = -INFINITY;
+      for (int e = lane * per; e < (lane + 1) * per; ++e) {
+        const float v = ch_lds[wave][e];
+        if (v > a) {
+          b2 = a;
+          a = v;
+        } else if (v > b2) {
+          b2 = v;
         }
       }
+      gsc = method == 2 ? a + b2 : a;
     }
-    float w[MOE_MAX_K], sum = 0.f;
-    for (int j = 0; j < k; ++j) {
-      w[j] = score(sel_i[j]);
-      sum += w[j];
-    }
-    const float f = norm ? scale / (sum + 1e-20f) : scale;
-    for (int j = 0; j < k; ++j) {
-      topw[(size_t)t * k + j] = w[j] * f;
-      topi[(size_t)t * k + j] = sel_i[j];
-      atomicAdd(&cnt[sel_i[j]], 1);
+    keep = 0;
+    for (int j = 0; j < topk_group; ++j) {  // wave argmax over the groups (ties: lower group id)
+      float v = (lane < n_group && !(keep >> lane & 1u)) ? gsc : -INFINITY;
+      int id = lane;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const float ov = __shfl_xor(v, o, 64);
+        const int oi = __shfl_xor(id, o, 64);
+        if (ov > v || (ov == v && oi < id)) {
+          v = ov;
+          id = oi;
+        }
+      }
+      keep |= 1u << id;
     }
   }
-  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < MOE_DS_EPL; ++i) {
+    const int e = lane + 64 * i;
+    if (e >= E || !(keep >> (e / per) & 1u)) chv[i] = -INFINITY;
+  }
+  float wsum = 0.f, wj_mine = 0.f;
+  int ej_mine = 0;
+  for (int j = 0; j < k; ++j) {  // k rounds of a wave argmax over the kept experts (ties: lower expert id)
+    float v = -INFINITY;
+    int id = 0x7fffffff;
+#pragma unroll
+    for (int i = 0; i < MOE_DS_EPL; ++i) {
+      const int e = lane + 64 * i;
+      if (chv[i] > v) {
+        v = chv[i];
+        id = e;
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(v, o, 64);
+      const int oi = __shfl_xor(id, o, 64);
+      if (ov > v || (ov == v && oi < id)) {
+        v = ov;
+        id = oi;
+      }
+    }
+    // the owner lane retires the winner and contributes its score
+    float wv = 0.f;
+#pragma unroll
+    for (int i = 0; i < MOE_DS_EPL; ++i)
+      if (lane + 64 * i == id) {
+        chv[i] = -INFINITY;
+        wv = sc[i];
+      }
+    wv = wave_sum(wv);
+    wsum += wv;
+    if (lane == j) {
+      wj_mine = wv;
+      ej_mine = id;
+    }
+  }
+  const float f = norm ? scale / (wsum + 1e-20f) : scale;
+  if (lane < k) {
+    topw[(size_t)t * k + lane] = wj_mine * f;
+    topi[(size_t)t * k + lane] = ej_mine;
+    atomicAdd(cnt + ej_mine, 1);
+  }
+}
+
+__global__ __launch_bounds__(1024) void moe_slots_kernel(const int32_t* __restrict__ topi, int T, int E, int k,
+                                                         int* __restrict__ cnt, int32_t* __restrict__ slot_of,
+                                                         int32_t* __restrict__ sorted_tok, int32_t* __restrict__ off) {
+  __shared__ int base[MOE_DS_MAX_E + 1];
+  __shared__ int cur[MOE_DS_MAX_E];
+  const int tid = threadIdx.x;
   if (tid == 0) {
     int acc = 0;
     for (int e = 0; e < E; ++e) {
@@ -176,27 +233,27 @@ __global__ __launch_bounds__(1024) void moe_route_ds_kernel(const float* __restr
     }
     off[E] = acc;
   }
+  for (int e = tid; e < E; e += blockDim.x) cur[e] = 0;
   __syncthreads();
-  for (int e = tid; e < E; e += blockDim.x) cnt[e] = 0;
-  __syncthreads();
-  for (int t = tid; t < T; t += blockDim.x) {
-    for (int j = 0; j < k; ++j) {
-      const int e = topi[(size_t)t * k + j];
-      const int pos = base[e] + atomicAdd(&cnt[e], 1);
-      slot_of[(size_t)t * k + j] = pos;
-      sorted_tok[pos] = t;
-    }
+  for (int e = tid; e < E; e += blockDim.x) cnt[e] = 0;  // ready for the next launch
+  for (int q = tid; q < T * k; q += blockDim.x) {
+    const int e = topi[q];
+    const int pos = base[e] + atomicAdd(&cur[e], 1);
+    slot_of[q] = pos;
+    sorted_tok[pos] = q / k;
   }
 }
 
 int launch_moe_route_ds(const float* logits, const float* bias, int T, int E, int k, int n_group, int topk_group,
-                        int method, bool sigmoid, bool norm, float scale, float* topw, int32_t* topi, int32_t* slot_of,
-                        int32_t* sorted_tok, int32_t* off, hipStream_t s) {
-  if (E < 1 || E > MOE_DS_MAX_E || k < 1 || k > MOE_MAX_K || n_group < 1 || n_group > MOE_DS_MAX_G ||
-      E % n_group != 0 || topk_group < 1 || topk_group > n_group || k > (E / n_group) * topk_group)
+                        int method, bool sigmoid, bool norm, float scale, int* cnt, float* topw, int32_t* topi,
+                        int32_t* slot_of, int32_t* sorted_tok, int32_t* off, hipStream_t s) {
+  if (E < 1 || E > MOE_DS_MAX_E || k < 1 || k > 64 || n_group < 1 || n_group > MOE_DS_MAX_G || E % n_group != 0 ||
+      topk_group < 1 || topk_group > n_group || k > (E / n_group) * topk_group)
     return -1;
-  moe_route_ds_kernel<<<1, 1024, 0, s>>>(logits, bias, T, E, k, n_group, topk_group, method, sigmoid ? 1 : 0,
-                                         norm ? 1 : 0, scale, topw, topi, slot_of, sorted_tok, off);
+  if (T <= 0) return 0;
+  moe_topk_ds_kernel<<<(T + 3) / 4, 256, 0, s>>>(logits, bias, T, E, k, n_group, topk_group, method, sigmoid ? 1 : 0,
+                                                 norm ? 1 : 0, scale, topw, topi, cnt);
+  moe_slots_kernel<<<1, 1024, 0, s>>>(topi, T, E, k, cnt, slot_of, sorted_tok, off);
   return 0;
 }
 

@@ -344,10 +344,21 @@ def mla_attn(q_lat, q_pe, cache, block_tables, cu_q, ctx_lens, scale: float, ws:
   return out
 
 
+_ROUTE_CNT = {}
+
+
+def _route_counters(device) -> torch.Tensor:
+  """Per-device expert counters of moe_route_ds: zero between launches (the kernel resets them)."""
+  key = str(device)
+  if key not in _ROUTE_CNT:
+    _ROUTE_CNT[key] = torch.zeros(256, dtype=torch.int32, device=device)
+  return _ROUTE_CNT[key]
+
+
 def moe_route_ds(logits, bias, k: int, n_group: int, topk_group: int, method: int, sigmoid: bool, norm: bool,
                  scale: float, outs: tuple | None = None):
-  """DeepSeekMoE routing.  GPU: (topw, topi, slot_of, sorted_tok, off) device tensors (graph-capturable);
-  CPU: (topw [T, k], topi [T, k])."""
+  """DeepSeekMoE routing.  GPU: (topw, topi, slot_of, sorted_tok, off) device tensors (graph-capturable;
+  launches on one stream reuse the per-device counters in order); CPU: (topw [T, k], topi [T, k])."""
   if not _gpu(logits):
     return ref.moe_route_ds(logits, bias, k, n_group, topk_group, method, sigmoid, norm, scale)
   T, E = logits.shape
@@ -357,5 +368,5 @@ def moe_route_ds(logits, bias, k: int, n_group: int, topk_group: int, method: in
             torch.empty(T * k, dtype=torch.int32, device=dev), torch.empty(T * k, dtype=torch.int32, device=dev),
             torch.empty(E + 1, dtype=torch.int32, device=dev))
   require().moe_route_ds(logits.contiguous(), bias, int(k), int(n_group), int(topk_group), int(method), bool(sigmoid),
-                         bool(norm), float(scale), *outs)
+                         bool(norm), float(scale), _route_counters(dev), *outs)
   return outs

@@ -187,7 +187,7 @@ class GemmPolicy:
       if N % (64 * ntw) or (ntw == 4 and M <= 32):
         continue
       for S in (1, 2, 4, 8):
-        if Kd % (S * 256) == 0 and (N // (64 * ntw)) * S <= 4096:
+        if Kd % (S * 128) == 0 and (N // (64 * ntw)) * S <= 4096:
           cands.append((ntw, S))
     return cands
 

@@ -14,8 +14,8 @@ import torch
 
 
 def can_shuffle(w: torch.Tensor) -> bool:
-  # the stream GEMM consumes an even number of 128-wide k-chunks per workgroup
-  return w.dim() == 2 and w.shape[0] % 64 == 0 and w.shape[1] % 256 == 0
+  # tiles of 16 rows x 128 k (the stream GEMM takes any whole number of 128-wide k-chunks per workgroup)
+  return w.dim() == 2 and w.shape[0] % 64 == 0 and w.shape[1] % 128 == 0
 
 
 def shuffle_for_stream(w: torch.Tensor) -> torch.Tensor:
