@@ -40,13 +40,14 @@ def test_presets_match_hf_shapes():
   assert (c.num_layers, c.hidden_size, c.num_heads, c.num_kv_heads, c.intermediate_size, c.vocab_size) == \
          (80, 8192, 64, 8, 28672, 128256)
   for name, cfg in PRESETS.items():
-    assert cfg.hidden_size == cfg.num_heads * cfg.head_dim or cfg.head_dim in (64, 128), name
+    assert cfg.is_mla or cfg.hidden_size == cfg.num_heads * cfg.head_dim or cfg.head_dim in (64, 128), name
   # every model card with a preset agrees on the layer count; parameter totals of the big dense cards
   for name, card in R.model_cards.items():
     if name in PRESETS:
       assert PRESETS[name].num_layers == card["layers"], name
   for name, billions in (("llama-3.1-405b", 405.9), ("qwen-2.5-72b", 72.7), ("mistral-large", 122.6),
-                         ("qwen-2.5-32b", 32.8), ("llama-3-8b", 8.0)):
+                         ("qwen-2.5-32b", 32.8), ("llama-3-8b", 8.0), ("deepseek-v3", 671.0),
+                         ("deepseek-coder-v2-lite", 15.7), ("phi-4-mini-instruct", 3.84), ("llava-1.5-7b-hf", 6.76)):
     assert abs(PRESETS[name].num_params() / 1e9 - billions) < 0.15, name
 
 

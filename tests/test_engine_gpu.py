@@ -94,3 +94,34 @@ def test_training_gpu_matches_cpu(gpu):
 def test_graft_smoke(gpu):
   import __graft_entry__ as g
   g.smoke()
+
+
+def test_llava_parity_gpu(gpu, tmp_path):
+  """LLaVA through the GPU path (vision tower GEMMs on the kernel library, spliced image rows, HIP-graph
+  decode) vs HF LlavaForConditionalGeneration in fp32."""
+  pytest.importorskip("transformers")
+  from tests.test_hf_parity import _hf_llava
+  from xotorch_support_jetson_amd.models.config import load_config
+  from xotorch_support_jetson_amd.models.vision import num_image_tokens
+  from xotorch_support_jetson_amd.models.weights import load_hf_weights
+  from xotorch_support_jetson_amd.runtime.runner import ShardRunner
+  hf, d = _hf_llava(tmp_path)
+  c = load_config(d)
+  n_img = num_image_tokens(c)
+  g = torch.Generator().manual_seed(0)
+  ids = torch.cat([torch.tensor([1, 5, 6]), torch.full((n_img,), c.image_token_id), torch.randint(3, 298, (9,), generator=g)])
+  pixels = torch.randn(1, 3, 56, 56, generator=g)
+  L = ids.numel()
+  with torch.no_grad():
+    ref = hf(input_ids=ids[None], pixel_values=pixels).logits[0].float()
+  s = Shard("llava", 0, c.num_layers - 1, c.num_layers)
+  r = ShardRunner(c, s, gpu, weights=load_hf_weights(d, c, s, device=gpu), max_batch=4, max_ctx=128)
+  feats = r.image_features(pixels)
+  got = [r.forward(["q"], [L - 3], ids[:L - 3].to(torch.int32), image_embeds=feats).float().view(-1).cpu()]
+  for t in range(L - 3, L):
+    got.append(r.forward(["q"], [1], ids[t:t + 1].to(torch.int32)).float().view(-1).cpu())
+  for k, gk in enumerate(got):
+    rr = ref[L - 4 + k]
+    cos = torch.nn.functional.cosine_similarity(gk, rr, dim=0).item()
+    err = (gk - rr).abs().max().item() / rr.abs().max().item()
+    assert cos > 0.999 and err < 6e-2, (k, cos, err)

@@ -127,3 +127,85 @@ def test_hf_parity(kind, tmp_path):
       err = (g - r).abs().max().item() / r.abs().max().item()
       cos = torch.nn.functional.cosine_similarity(g, r, dim=0).item()
       assert err < 6e-2 and cos > 0.999, (kind, len(split), k, err, cos)
+
+
+def _hf_llava(tmp_path):
+  torch.manual_seed(0)
+  tc = transformers.LlamaConfig(vocab_size=300, hidden_size=256, intermediate_size=384, num_hidden_layers=3,
+                                num_attention_heads=4, num_key_value_heads=2, max_position_embeddings=512,
+                                pad_token_id=0, bos_token_id=1, eos_token_id=2)
+  vc = transformers.CLIPVisionConfig(hidden_size=128, intermediate_size=256, num_hidden_layers=3, num_attention_heads=4,
+                                     patch_size=14, image_size=56)
+  m = transformers.LlavaForConditionalGeneration(transformers.LlavaConfig(text_config=tc, vision_config=vc,
+                                                                          image_token_index=299)).float().eval()
+  with torch.no_grad():
+    for n, p in m.named_parameters():
+      if "norm" in n and n.endswith("weight"):
+        p.uniform_(0.5, 1.5)
+      elif n.endswith("bias"):
+        p.normal_(0, 0.05)
+  d = tmp_path / "llava"
+  m.save_pretrained(str(d), safe_serialization=True)
+  return m, d
+
+
+def test_llava_parity(tmp_path):
+  """LLaVA: CLIP tower (feature layer -2, CLS dropped) + projector features spliced into the image-token
+  rows, then the Llama decoder, prefill + decode, vs HF LlavaForConditionalGeneration."""
+  from xotorch_support_jetson_amd.models.vision import num_image_tokens
+  hf, d = _hf_llava(tmp_path)
+  c = load_config(d)
+  assert c.model_type == "llava" and c.image_token_id == 299 and num_image_tokens(c) == 16
+  n_img = num_image_tokens(c)
+  ids = torch.cat([torch.tensor([1, 5, 6]), torch.full((n_img,), 299), torch.randint(3, 298, (7,))])
+  pixels = torch.randn(1, 3, 56, 56)
+  L = ids.numel()
+  with torch.no_grad():
+    ref = hf(input_ids=ids[None], pixel_values=pixels).logits[0].float()
+  for split in ([Shard("llava", 0, 2, 3)], [Shard("llava", 0, 0, 3), Shard("llava", 1, 2, 3)]):
+    runners = [ShardRunner(c, s, "cpu", weights=load_hf_weights(d, c, s, dtype=torch.float32), max_batch=2,
+                           max_ctx=64) for s in split]
+    assert runners[0].weights.vision is not None and (len(runners) == 1 or runners[1].weights.vision is None)
+    feats = runners[0].image_features(pixels)
+    x = runners[0].forward(["q"], [L - 2], ids[:L - 2].to(torch.int32), image_embeds=feats)
+    for r in runners[1:]:
+      x = r.forward(["q"], [L - 2], x)
+    got = [x.float().view(-1)]
+    for t in range(L - 2, L):
+      x = ids[t:t + 1].to(torch.int32)
+      for r in runners:
+        x = r.forward(["q"], [1], x)
+      got.append(x.float().view(-1))
+    for k, g in enumerate(got):
+      rr = ref[L - 3 + k]
+      err = (g - rr).abs().max().item() / rr.abs().max().item()
+      cos = torch.nn.functional.cosine_similarity(g, rr, dim=0).item()
+      assert err < 6e-2 and cos > 0.999, (len(split), k, err, cos)
+
+
+def test_llava_preprocess_matches_clip_processor():
+  from PIL import Image
+  from xotorch_support_jetson_amd.models.vision import preprocess
+  g = torch.Generator().manual_seed(0)
+  arr = torch.randint(0, 256, (45, 70, 3), generator=g, dtype=torch.uint8).numpy()
+  img = Image.fromarray(arr)
+  proc = transformers.CLIPImageProcessor(size={"shortest_edge": 56}, crop_size={"height": 56, "width": 56})
+  ref = torch.as_tensor(proc(images=img, return_tensors="np")["pixel_values"][0])
+  got = preprocess(img, 56)
+  assert got.shape == ref.shape
+  assert (got - ref).abs().max().item() < 0.05  # resampling implementations differ by a few grey levels
+
+
+def test_checkpoint_roundtrip_llava(tmp_path):
+  hf, d = _hf_llava(tmp_path)
+  c = load_config(d)
+  sw = load_hf_weights(d, c, Shard("llava", 0, 2, 3), dtype=torch.float32)
+  sd = sw.to_hf_state_dict()
+  from safetensors.torch import load_file
+  from xotorch_support_jetson_amd.models.weights import canonical_name
+  ref = {}
+  for f in sorted(d.glob("*.safetensors")):
+    ref.update({canonical_name(k): v for k, v in load_file(str(f)).items()})
+  for k, v in sd.items():
+    torch.testing.assert_close(v, ref[k].float(), rtol=0, atol=0)
+  assert not [k for k in ref if k not in sd], [k for k in ref if k not in sd]

@@ -1,0 +1,67 @@
+"""LLaVA plumbing on the CPU: API image parts -> in-prompt marker -> first-shard engine expands it into image
+tokens and splices the vision tower's features at prefill (model numerics vs HF: test_hf_parity.py)."""
+import asyncio
+import base64
+import io
+
+import numpy as np
+import torch
+
+from xotorch_support_jetson_amd.api.chatgpt_api import IMAGE_PLACEHOLDER, Message, build_prompt
+from xotorch_support_jetson_amd.download.shard_download import NoopShardDownloader
+from xotorch_support_jetson_amd.inference.shard import Shard
+from xotorch_support_jetson_amd.inference.sharded_engine import ShardedInferenceEngine
+from xotorch_support_jetson_amd.inference.tokenizers import ByteTokenizer
+from xotorch_support_jetson_amd.models.config import preset
+from xotorch_support_jetson_amd.models.registry import is_vision_model
+from xotorch_support_jetson_amd.models.vision import IMAGE_MARK, num_image_tokens, split_image_marks
+
+
+def _png_data_url(seed=0, size=(40, 30)):
+  from PIL import Image
+  arr = np.random.default_rng(seed).integers(0, 256, (size[1], size[0], 3), dtype=np.uint8)
+  buf = io.BytesIO()
+  Image.fromarray(arr).save(buf, format="PNG")
+  return "data:image/png;base64," + base64.b64encode(buf.getvalue()).decode()
+
+
+def test_prompt_keeps_last_image_for_vision_models():
+  url1, url2 = _png_data_url(1), _png_data_url(2)
+  msgs = [Message("user", [{"type": "image_url", "image_url": {"url": url1}}, {"type": "text", "text": "first"}]),
+          Message("assistant", "ok"),
+          Message("user", [{"type": "text", "text": "and this?"}, {"type": "image_url", "image_url": {"url": url2}}])]
+  tok = ByteTokenizer()
+  p = build_prompt(tok, msgs, vision=True)
+  pieces, urls = split_image_marks(p)
+  assert urls == [url2] and IMAGE_PLACEHOLDER in p  # earlier images become placeholders (reference rule)
+  p2 = build_prompt(tok, msgs, vision=False)
+  assert not split_image_marks(p2)[1] and IMAGE_MARK.format(url2) not in p2
+  assert is_vision_model("llava-1.5-7b-hf") and is_vision_model("tiny-llava") and not is_vision_model("llama-3-8b")
+
+
+def test_engine_expands_image_and_prefills():
+  async def main():
+    c = preset("tiny-llava")
+    n = c.num_layers
+    e = ShardedInferenceEngine(NoopShardDownloader(), device=torch.device("cpu"))
+    shard = Shard("tiny-llava", 0, n - 1, n)
+    url = _png_data_url(3)
+    prompt = "USER: " + IMAGE_MARK.format(url) + "\nwhat is this? ASSISTANT:"
+    logits, _ = await e.infer_prompt("r1", shard, prompt)
+    n_text = len(e.tokenizer.encode("USER: ")) + len(e.tokenizer.encode("\nwhat is this? ASSISTANT:", add_special_tokens=False))
+    assert e.runner.num_tokens("r1") == n_text + num_image_tokens(c)
+    assert "r1" not in e._images  # consumed by the prefill
+    # the image changes the output: same text with another image
+    logits2, _ = await e.infer_prompt("r2", shard, prompt.replace(url, _png_data_url(4)))
+    assert not torch.allclose(torch.as_tensor(logits).float(), torch.as_tensor(logits2).float())
+    # decode continues from the spliced prefix
+    tok = np.asarray([[7]])
+    out, _ = await e.infer_tensor("r1", shard, tok)
+    assert e.runner.num_tokens("r1") == n_text + num_image_tokens(c) + 1 and out is not None
+    # a text-only model reads the marker as a placeholder
+    c2 = preset("tiny-llama")
+    e2 = ShardedInferenceEngine(NoopShardDownloader(), device=torch.device("cpu"))
+    s2 = Shard("tiny-llama", 0, c2.num_layers - 1, c2.num_layers)
+    await e2.infer_prompt("t", s2, prompt)
+    assert e2.runner.num_tokens("t") == len(e2.tokenizer.encode("USER: [image]\nwhat is this? ASSISTANT:"))
+  asyncio.run(main())

@@ -23,7 +23,9 @@ from aiohttp import web
 from ..helpers import DEBUG, VERSION, shutdown
 from ..inference.tokenizers import resolve_tokenizer
 from ..models import registry
-from ..models.registry import build_base_shard, build_full_shard, get_pretty_name, get_repo, get_supported_models
+from ..models.registry import (build_base_shard, build_full_shard, get_pretty_name, get_repo, get_supported_models,
+                               is_vision_model)
+from ..models.vision import IMAGE_MARK
 from ..orchestration.tracing import tracer
 from ..utils import metrics
 
@@ -102,8 +104,18 @@ def remap_messages(messages: List[Message]) -> List[Message]:
   return out
 
 
-def build_prompt(tokenizer, messages: List[Message], tools: Optional[List[dict]] = None) -> str:
+def build_prompt(tokenizer, messages: List[Message], tools: Optional[List[dict]] = None, vision: bool = False) -> str:
+  """Chat-template prompt.  For a vision model (LLaVA) the kept image becomes an in-prompt
+  `<|xot_image:URL|>` marker that the first shard's engine expands into image tokens (models/vision.py),
+  so the image travels with the prompt to whichever peer holds the first shard."""
   msgs = [m.to_dict() for m in remap_messages(messages)]
+  for m in msgs:
+    if isinstance(m["content"], list):
+      for i, c in enumerate(m["content"]):
+        if isinstance(c, dict) and c.get("type") == "image":
+          m["content"][i] = {"type": "text", "text": IMAGE_MARK.format(c["image"]) if vision else IMAGE_PLACEHOLDER}
+      if all(isinstance(c, dict) and c.get("type") == "text" for c in m["content"]):
+        m["content"] = "".join(c["text"] for c in m["content"])
   kw = {"tokenize": False, "add_generation_prompt": True}
   if tools:
     kw["tools"] = tools
@@ -275,7 +287,7 @@ class ChatGPTAPI:
     model = self._resolve_model(data.get("model"))
     tok = await self._tokenizer(model)
     messages = [parse_message(m) for m in data.get("messages", [])]
-    prompt = build_prompt(tok, messages, data.get("tools"))
+    prompt = build_prompt(tok, messages, data.get("tools"), vision=is_vision_model(model))
     ids = tok.encode(prompt)
     return web.json_response({"length": len(prompt), "num_tokens": len(ids), "encoded_tokens": list(map(int, ids)),
                               "encoded_prompt": prompt})
@@ -305,7 +317,7 @@ class ChatGPTAPI:
     tok = await self._tokenizer(req.model)
     if self.system_prompt and not any(m.role == "system" for m in req.messages):
       req.messages.insert(0, Message("system", self.system_prompt))
-    prompt = build_prompt(tok, req.messages, req.tools)
+    prompt = build_prompt(tok, req.messages, req.tools, vision=is_vision_model(req.model))
     request_id = str(uuid.uuid4())
     tracer.extract(request_id, dict(request.headers))
     if self.on_chat_completion_request:

@@ -59,6 +59,7 @@ class ShardedInferenceEngine(InferenceEngine):
     self.lr = float(os.environ.get("XOT_LR", "1e-5"))  # `xot train --lr` sets this
     self._queue: list = []  # (request id, shard, input, future) waiting for the next batched step
     self._draining = False
+    self._images: dict = {}  # request id -> [N, 3, S, S] pixels awaiting that request's prefill (LLaVA)
 
   # ------------------------------------------------------------------ helpers
   async def _run(self, fn, *args):
@@ -85,6 +86,33 @@ class ShardedInferenceEngine(InferenceEngine):
       return tok.cpu().numpy().astype(np.int64)
 
     return await self._run(_sample)
+
+  # ------------------------------------------------------------------ prompts with images (LLaVA)
+  async def infer_prompt(self, request_id: str, shard: Shard, prompt: str,
+                         inference_state: Optional[dict] = None) -> Tuple[object, Optional[dict]]:
+    """Prompts may carry `<|xot_image:URL|>` markers (api/chatgpt_api.py keeps the chat's last image that
+    way).  A vision model's first shard expands each into its image-token run and keeps the preprocessed
+    pixels for the request's prefill; any other model reads the marker as a placeholder text."""
+    from ..models.vision import load_image, num_image_tokens, preprocess, split_image_marks
+    pieces, urls = split_image_marks(prompt)
+    if not urls:
+      return await super().infer_prompt(request_id, shard, prompt, inference_state)
+    await self.ensure_shard(shard)
+    c = self.config
+    if c.vision is None or not shard.is_first_layer():
+      text = "".join(p + ("[image]" if i < len(urls) else "") for i, p in enumerate(pieces))
+      return await super().infer_prompt(request_id, shard, text, inference_state)
+    n_img = num_image_tokens(c)
+    ids: list = []
+    for i, piece in enumerate(pieces):
+      ids += list(self.tokenizer.encode(piece, add_special_tokens=(i == 0)))
+      if i < len(urls):
+        ids += [c.image_token_id] * n_img
+    size = c.vision["image_size"]
+    pixels = await self._run(lambda: torch.stack([preprocess(load_image(u), size) for u in urls]))
+    self._images[request_id] = pixels
+    return await self.infer_tensor(request_id, shard, np.asarray(ids, dtype=np.int64).reshape(1, -1),
+                                   inference_state)
 
   # ------------------------------------------------------------------ forward (continuously batched)
   async def infer_tensor(self, request_id: str, shard: Shard, input_data,
@@ -138,8 +166,12 @@ class ShardedInferenceEngine(InferenceEngine):
         L = xs[-1].numel()
       rids.append(rid)
       qlens.append(L)
+    image_embeds = None
+    if self._images and self.shard.is_first_layer():
+      feats = [self.runner.image_features(self._images.pop(rid)) for rid in rids if rid in self._images]
+      image_embeds = torch.cat(feats) if feats else None
     try:
-      out = self.runner.forward(rids, qlens, torch.cat(xs))
+      out = self.runner.forward(rids, qlens, torch.cat(xs), image_embeds=image_embeds)
     except torch.cuda.OutOfMemoryError:
       self.clear_model()
       raise
@@ -157,6 +189,7 @@ class ShardedInferenceEngine(InferenceEngine):
     return res
 
   async def finish_request(self, request_id: str) -> None:
+    self._images.pop(request_id, None)
     if self.runner is not None:
       await self._run(self.runner.free, request_id)
 

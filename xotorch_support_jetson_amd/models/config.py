@@ -53,6 +53,12 @@ class ModelConfig:
   topk_group: int = 1
   norm_topk_prob: bool = True
   scoring_func: str = "softmax"  # softmax | sigmoid
+  # LLaVA: CLIP vision tower + projector on the first shard (HF vision_config keys), image token id
+  vision: Optional[dict] = None
+  image_token_id: int = -1
+  vision_feature_layer: int = -2
+  vision_select: str = "default"  # default: drop the CLS feature | full
+  projector_act: str = "gelu"
 
   @property
   def qkv_size(self) -> int:
@@ -160,6 +166,8 @@ def _rope_fields(cfg: dict) -> tuple:
 
 def from_hf_config(cfg: dict) -> ModelConfig:
   mt = cfg.get("model_type", "llama")
+  if mt == "llava":
+    return _llava_config(cfg)
   H = int(cfg["num_attention_heads"])
   D = int(cfg["hidden_size"])
   eos = cfg.get("eos_token_id")
@@ -235,6 +243,32 @@ def _deepseek_config(cfg: dict, mt: str, theta: float, scaling, eos_ids) -> Mode
   )
 
 
+_VISION_KEYS = ("hidden_size", "intermediate_size", "num_hidden_layers", "num_attention_heads", "patch_size",
+                "image_size", "layer_norm_eps", "hidden_act", "num_channels")
+
+
+def _llava_config(cfg: dict) -> ModelConfig:
+  """HF LlavaConfig: a Llama text model + CLIP vision tower (vision_config) + projector."""
+  text = dict(cfg.get("text_config") or {})
+  text.setdefault("model_type", "llama")
+  for k in ("bos_token_id", "eos_token_id", "pad_token_id"):
+    if k not in text and k in cfg:
+      text[k] = cfg[k]
+  lm = from_hf_config(text)
+  vc = cfg.get("vision_config") or {}
+  vision = {k: vc[k] for k in _VISION_KEYS if k in vc}
+  vision.setdefault("num_channels", 3)
+  vision.setdefault("hidden_act", "quick_gelu")
+  vision.setdefault("layer_norm_eps", 1e-5)
+  fl = cfg.get("vision_feature_layer", -2)
+  if isinstance(fl, (list, tuple)):
+    raise ValueError("multi-layer vision features are not supported")
+  return replace(lm, model_type="llava", vision=vision,
+                 image_token_id=int(cfg.get("image_token_index", cfg.get("image_token_id", 32000))),
+                 vision_feature_layer=int(fl), vision_select=str(cfg.get("vision_feature_select_strategy", "default")),
+                 projector_act=str(cfg.get("projector_hidden_act", "gelu")))
+
+
 def load_config(model_dir: str | Path) -> ModelConfig:
   with open(Path(model_dir) / "config.json") as f:
     return from_hf_config(json.load(f))
@@ -300,6 +334,12 @@ PRESETS: dict[str, ModelConfig] = {
                              v_head_dim=128, moe_intermediate_size=2048, n_shared_experts=1, first_k_dense_replace=3,
                              routed_scaling_factor=2.5, topk_method="noaux_tc", n_group=8, topk_group=4,
                              norm_topk_prob=True, scoring_func="sigmoid"),
+  # LLaVA-1.5-7B (HF LlavaForConditionalGeneration): Vicuna-7B text model + CLIP ViT-L/14-336 + MLP projector
+  "llava-1.5-7b-hf": ModelConfig("llava", 32064, 4096, 11008, 32, 32, 32, 128, 1e-5, 10000.0, None, 4096, False,
+                                 bos_token_id=1, eos_token_ids=(2,), image_token_id=32000,
+                                 vision=dict(hidden_size=1024, intermediate_size=4096, num_hidden_layers=24,
+                                             num_attention_heads=16, patch_size=14, image_size=336,
+                                             layer_norm_eps=1e-5, hidden_act="quick_gelu", num_channels=3)),
   # small shapes for tests / CPU plumbing
   "tiny-llama": ModelConfig("llama", 512, 256, 512, 4, 4, 2, 64, 1e-5, 10000.0, None, 2048, False,
                             bos_token_id=1, eos_token_ids=(2,)),
@@ -314,6 +354,11 @@ PRESETS: dict[str, ModelConfig] = {
                                 long_factor=[2.0 + 0.1 * i for i in range(48)], original_max_position_embeddings=64,
                                 max_position_embeddings=2048), 2048, True, bos_token_id=1, eos_token_ids=(2,),
                            partial_rotary_factor=0.75),
+  "tiny-llava": ModelConfig("llava", 512, 256, 512, 4, 4, 2, 64, 1e-5, 10000.0, None, 2048, False, bos_token_id=1,
+                            eos_token_ids=(2,), image_token_id=500,
+                            vision=dict(hidden_size=128, intermediate_size=256, num_hidden_layers=3, num_attention_heads=4,
+                                        patch_size=14, image_size=56, layer_norm_eps=1e-5, hidden_act="quick_gelu",
+                                        num_channels=3)),
   "tiny-deepseek-v2": ModelConfig("deepseek_v2", 512, 256, 512, 3, 4, 1, 192, 1e-6, 10000.0, None, 2048, False,
                                   num_experts=8, num_experts_per_tok=2, bos_token_id=1, eos_token_ids=(2,),
                                   kv_lora_rank=256, qk_nope_head_dim=128, qk_rope_head_dim=64, v_head_dim=128,

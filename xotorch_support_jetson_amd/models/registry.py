@@ -62,6 +62,9 @@ _CARDS: List[tuple] = [
   ("tiny-qwen", 4, "synthetic/tiny-qwen", "Tiny Qwen (synthetic)"),
   ("tiny-mixtral", 4, "synthetic/tiny-mixtral", "Tiny Mixtral (synthetic)"),
   ("tiny-phi3", 4, "synthetic/tiny-phi3", "Tiny Phi-3 (synthetic)"),
+  ("tiny-deepseek-v2", 3, "synthetic/tiny-deepseek-v2", "Tiny DeepSeek-V2 (synthetic)"),
+  ("tiny-deepseek-v3", 3, "synthetic/tiny-deepseek-v3", "Tiny DeepSeek-V3 (synthetic)"),
+  ("tiny-llava", 4, "synthetic/tiny-llava", "Tiny LLaVA (synthetic)"),
 ]
 
 model_cards: Dict[str, dict] = {mid: {"layers": n, "repo": {ENGINE: repo}} for mid, n, repo, _ in _CARDS}
@@ -107,3 +110,10 @@ def validate_layers(model_id: str, config_layers: int) -> int:
     import warnings
     warnings.warn(f"model card {model_id} says {card} layers but config.json has {config_layers}; using config.json")
   return config_layers
+
+
+def is_vision_model(model_id: str) -> bool:
+  """Cards whose architecture has an image tower (LLaVA): the API keeps their images."""
+  from .config import PRESETS
+  c = PRESETS.get(model_id)
+  return bool(c is not None and c.vision) or "llava" in model_id

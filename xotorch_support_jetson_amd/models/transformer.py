@@ -51,6 +51,7 @@ class StepInputs:
   last_idx: torch.Tensor  # [B] int64 row of each sequence's last new token
   max_qlen: int
   decode: bool  # every sequence has exactly one new token
+  image_embeds: Optional[torch.Tensor] = None  # LLaVA: [n image-token rows, D], in token order (first shard)
 
   @property
   def num_tokens(self) -> int:
@@ -284,6 +285,11 @@ class ShardModel:
     c, w = self.c, self.w
     if self.shard.is_first_layer():
       h = K.embedding(x, w.embed)
+      if inp.image_embeds is not None:  # LLaVA: projected image features replace the image-token rows
+        rows = (x.view(-1) == c.image_token_id).nonzero().view(-1)
+        if rows.numel() != inp.image_embeds.shape[0]:
+          raise ValueError(f"{rows.numel()} image tokens but {inp.image_embeds.shape[0]} image feature rows")
+        h.index_copy_(0, rows, inp.image_embeds.to(h.dtype))
     else:
       h = x.contiguous().clone() if x.dtype == torch.bfloat16 else x.to(torch.bfloat16).contiguous()
     last = self.shard.is_last_layer()

@@ -76,6 +76,7 @@ class ShardWeights:
   embed: Optional[torch.Tensor] = None  # first shard (and last, when tied)
   norm: Optional[torch.Tensor] = None  # last shard
   lm_head: Optional[torch.Tensor] = None  # last shard (aliases embed when tied)
+  vision: Optional[Dict[str, torch.Tensor]] = None  # LLaVA tower + projector (first shard), HF names
 
   def nbytes(self) -> int:
     seen, total = set(), 0
@@ -91,6 +92,8 @@ class ShardWeights:
     for t in (self.embed, self.norm, self.lm_head):
       if t is not None:
         yield t
+    if self.vision:
+      yield from self.vision.values()
 
   # ---------------------------------------------------------------- HF naming (checkpoints)
   def to_hf_state_dict(self) -> Dict[str, torch.Tensor]:
@@ -140,6 +143,8 @@ class ShardWeights:
       sd["lm_head.weight"] = _rowmajor(self.lm_head)
     elif self.lm_head is not None and self.embed is None:
       sd["model.embed_tokens.weight"] = _rowmajor(self.lm_head)  # tied head on a shard without the embedding
+    if self.vision:
+      sd.update(self.vision)
     return {k: v.contiguous() for k, v in sd.items()}
 
 
@@ -385,6 +390,9 @@ def random_weights(c: ModelConfig, shard: Shard, device: torch.device | str = "c
   if shard.is_last_layer():
     sw.norm = norm_w(gen(2))
     sw.lm_head = sw.embed if c.tie_word_embeddings else normal((c.vocab_size, D), gen(3))
+  if c.vision and shard.is_first_layer():
+    from .vision import random_vision
+    sw.vision = random_vision(c, dev, dtype, seed=seed)
   return sw
 
 
@@ -416,12 +424,32 @@ def _weight_map(model_dir: Path) -> Dict[str, str]:
   return wm
 
 
+_PREFIXES = (("language_model.model.", "model."), ("language_model.lm_head.", "lm_head."),
+             ("model.language_model.", "model."), ("model.vision_tower.", "vision_tower."),
+             ("model.multi_modal_projector.", "multi_modal_projector."), ("vision_tower.vision_model.", "vision_tower."))
+
+
+def canonical_name(k: str) -> str:
+  """One name per tensor across checkpoint flavours: LLaVA's `language_model.model.*` (hub) /
+  `model.language_model.*` (transformers 5) read as the plain LM's `model.*`, the hub's
+  `vision_tower.vision_model.*` as `vision_tower.*`."""
+  changed = True
+  while changed:
+    changed = False
+    for a, b in _PREFIXES:
+      if k.startswith(a):
+        k, changed = b + k[len(a):], True
+  return k
+
+
 def needed_files(model_dir: Path, c: ModelConfig, shard: Shard) -> set:
   """Safetensors files that hold this shard's tensors (for the downloader's allow patterns too)."""
-  wm = _weight_map(model_dir)
+  wm = {canonical_name(k): v for k, v in _weight_map(model_dir).items()}
   want = set()
   for name, fname in wm.items():
-    if name.startswith("model.layers."):
+    if (name.startswith("vision_tower.") or name.startswith("multi_modal_projector.")) and shard.is_first_layer():
+      want.add(fname)
+    elif name.startswith("model.layers."):
       if int(name.split(".")[2]) in shard.layers():
         want.add(fname)
     elif name.startswith("model.embed_tokens") and _needs_embed(c, shard):
@@ -435,14 +463,15 @@ def load_hf_weights(model_dir: str | Path, c: ModelConfig, shard: Shard, device=
   """Read only this shard's tensors (mmap'd safetensors, one tensor at a time) into the fused layout."""
   from safetensors import safe_open
   model_dir = Path(model_dir)
-  wm = _weight_map(model_dir)
+  raw = _weight_map(model_dir)
+  wm = {canonical_name(k): (k, f) for k, f in raw.items()}
   handles = {}
 
   def get(name: str, dt: Optional[torch.dtype] = None) -> torch.Tensor:
-    fname = wm[name]
+    key, fname = wm[name]
     if fname not in handles:
       handles[fname] = safe_open(str(model_dir / fname), framework="pt")
-    return handles[fname].get_tensor(name).to(device=device, dtype=dt or dtype)
+    return handles[fname].get_tensor(key).to(device=device, dtype=dt or dtype)
 
   def has(name: str) -> bool:
     return name in wm
@@ -488,6 +517,9 @@ def load_hf_weights(model_dir: str | Path, c: ModelConfig, shard: Shard, device=
       sw.lm_head = get("lm_head.weight")
     else:
       sw.lm_head = sw.embed
+  if c.vision and shard.is_first_layer():
+    from .vision import vision_names
+    sw.vision = {n: get(n) for n in vision_names(c.vision)}
   return sw
 
 

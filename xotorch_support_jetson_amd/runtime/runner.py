@@ -145,15 +145,27 @@ class ShardRunner:
     return inp
 
   # ------------------------------------------------------------------ forward
-  def forward(self, rids: Sequence[str], qlens: Sequence[int], x: torch.Tensor) -> torch.Tensor:
+  def forward(self, rids: Sequence[str], qlens: Sequence[int], x: torch.Tensor,
+              image_embeds: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Run this shard for the given requests.  x = token ids [sum(qlens)] (first shard) or hidden
     [sum(qlens), D].  Allocates KV slots for the new tokens.  Returns hidden [T, D] or, on the last
-    shard, fp32 logits [len(rids), V] of each request's last token."""
+    shard, fp32 logits [len(rids), V] of each request's last token.  image_embeds (LLaVA, first shard):
+    projected image features for the image-token rows of x, in order."""
     x = x.to(self.device, non_blocking=True)
-    if self.use_graphs and all(q == 1 for q in qlens) and len(rids) <= self.max_batch:
+    if self.use_graphs and image_embeds is None and all(q == 1 for q in qlens) and len(rids) <= self.max_batch:
       return self._decode_graph(rids, x)
     inp = self._prepare(rids, qlens)
+    if image_embeds is not None:
+      inp.image_embeds = image_embeds.to(self.device)
     return self.model.forward(x, inp)
+
+  def image_features(self, pixels: torch.Tensor) -> torch.Tensor:
+    """LLaVA first shard: [N, 3, S, S] pixel batch -> [N * image tokens, D] projected features."""
+    from ..models.vision import image_features
+    if self.weights.vision is None:
+      raise ValueError(f"{self.shard.model_id}: this shard has no vision tower")
+    with torch.inference_mode():
+      return image_features(self.config, self.weights.vision, pixels.to(self.device))
 
   # ------------------------------------------------------------------ graphs
   def _decode_graph(self, rids: Sequence[str], x: torch.Tensor) -> torch.Tensor:
