@@ -171,7 +171,9 @@ class ShardedInferenceEngine(InferenceEngine):
       feats = [self.runner.image_features(self._images.pop(rid)) for rid in rids if rid in self._images]
       image_embeds = torch.cat(feats) if feats else None
     try:
-      out = self.runner.forward(rids, qlens, torch.cat(xs), image_embeds=image_embeds)
+      x = torch.cat(xs)
+      out = (self.runner.forward(rids, qlens, x) if image_embeds is None
+             else self.runner.forward(rids, qlens, x, image_embeds=image_embeds))
     except torch.cuda.OutOfMemoryError:
       self.clear_model()
       raise
