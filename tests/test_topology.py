@@ -102,3 +102,31 @@ def test_device_capabilities_cpu_and_table():
   mi = [v for k, v in CHIP_FLOPS.items() if "MI355X" in k][0]
   assert 2000 < mi.fp16 < 2600
   assert UNKNOWN_DEVICE_CAPABILITIES.memory == 0
+
+
+def test_device_probes_without_torch_gpu(tmp_path):
+  """Jetson (device-tree model + unified MemTotal), macOS system_profiler and amd-smi / rocm-smi JSON
+  probes, with fake inputs (the reference mocks subprocess the same way, test_device_capabilities.py)."""
+  import json
+  from xotorch_support_jetson_amd.topology.device_capabilities import (_lookup_flops, amd_smi_capabilities,
+                                                                       jetson_capabilities, mac_capabilities)
+  model = tmp_path / "model"
+  model.write_bytes(b"NVIDIA Jetson AGX Orin 32GB\x00")
+  mem = tmp_path / "meminfo"
+  mem.write_text("MemTotal:       31011968 kB\nMemFree:        1000 kB\n")
+  j = jetson_capabilities(str(model), str(mem))
+  assert j.memory == 31011968 // 1024 and j.flops.fp16 == 35.3
+  model.write_bytes(b"Raspberry Pi 5\x00")
+  assert jetson_capabilities(str(model), str(mem)) is None
+  prof = ("Hardware:\n\n    Hardware Overview:\n\n      Model Name: MacBook Pro\n      Model Identifier: Mac15,9\n"
+          "      Chip: Apple M3 Max\n      Memory: 128 GB\n")
+  m = mac_capabilities(lambda cmd: prof)
+  assert (m.model, m.chip, m.memory) == ("MacBook Pro", "Apple M3 Max", 128 * 1024) and m.flops.fp16 == 28.4
+  amd = [{"gpu": 0, "asic": {"market_name": "AMD Instinct MI355X"}, "vram": {"size": {"value": 294896, "unit": "MB"}}},
+         {"gpu": 1, "asic": {"market_name": "AMD Instinct MI355X"}, "vram": {"size": {"value": 294896, "unit": "MB"}}}]
+  caps = amd_smi_capabilities(lambda cmd: json.dumps(amd) if cmd[0] == "amd-smi" else None)
+  assert len(caps) == 2 and caps[1].memory == 294896 and caps[0].flops.fp16 > 2000
+  rsmi = {"card0": {"Card Series": "AMD Instinct MI300X", "VRAM Total Memory (B)": str(192 << 30)}}
+  caps = amd_smi_capabilities(lambda cmd: json.dumps(rsmi) if cmd[0] == "rocm-smi" else None)
+  assert caps[0].memory == 192 << 10 and caps[0].flops.fp16 > 1000
+  assert _lookup_flops("Apple M1 Max").fp32 == 10.6 and _lookup_flops("Apple M1").fp32 == 2.29
