@@ -125,3 +125,31 @@ def test_llava_parity_gpu(gpu, tmp_path):
     cos = torch.nn.functional.cosine_similarity(gk, rr, dim=0).item()
     err = (gk - rr).abs().max().item() / rr.abs().max().item()
     assert cos > 0.999 and err < 6e-2, (k, cos, err)
+
+
+def test_engine_concurrent_serving_gpu():
+  """Many concurrent requests of mixed prompt lengths on the GPU engine (token-budgeted steps, chunked long
+  prefill, several decode-graph buckets): greedy continuations equal one-at-a-time runs."""
+  from xotorch_support_jetson_amd.inference.sharded_engine import ShardedInferenceEngine
+
+  async def main():
+    s = Shard(MODEL, 0, N - 1, N)
+    rng = np.random.default_rng(9)
+    prompts = [rng.integers(0, 500, size=(1, int(L))) for L in rng.integers(3, 300, size=24)]
+
+    async def gen(e, rid, p, steps=5):
+      out, _ = await e.infer_tensor(rid, s, p)
+      toks = []
+      for _ in range(steps):
+        t = int(np.argmax(np.asarray(out.float().cpu() if hasattr(out, "float") else out)))
+        toks.append(t)
+        out, _ = await e.infer_tensor(rid, s, np.array([[t]]))
+      return toks
+
+    solo = ShardedInferenceEngine(NoopShardDownloader(), device=torch.device("cuda:0"))
+    ref = [await gen(solo, f"s{i}", p) for i, p in enumerate(prompts)]
+    both = ShardedInferenceEngine(NoopShardDownloader(), device=torch.device("cuda:0"))
+    got = await asyncio.gather(*(gen(both, f"c{i}", p) for i, p in enumerate(prompts)))
+    same = sum(a == b for a, b in zip(ref, got))
+    assert same >= len(prompts) - 2, (same, ref, got)  # bf16 batch-composition rounding may flip a near-tie
+  asyncio.run(main())

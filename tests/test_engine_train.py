@@ -233,3 +233,30 @@ def test_moe_training_matches_inference_and_pipeline():
     assert not torch.allclose(ref, ref2, atol=1e-3)
 
   run(main())
+
+
+def test_step_token_budget_and_chunked_prefill(monkeypatch):
+  """A step takes at most MAX_STEP_TOKENS new tokens; a longer prompt prefills alone in chunks with the
+  same logits as one pass (chunked prefill reads the cached prefix)."""
+  import xotorch_support_jetson_amd.inference.sharded_engine as SE
+
+  async def main():
+    s = Shard(MODEL, 0, N - 1, N)
+    rng = np.random.default_rng(7)
+    long_p = rng.integers(0, 500, size=(1, 45))
+    ref_e = eng()
+    ref, _ = await ref_e.infer_tensor("r", s, long_p)
+    monkeypatch.setattr(SE, "MAX_STEP_TOKENS", 16)
+    e = eng()
+    await e.ensure_shard(s)
+    calls = []
+    orig = e.runner.forward
+    e.runner.forward = lambda rids, qlens, x: (calls.append(sum(qlens)), orig(rids, qlens, x))[1]
+    out, _ = await e.infer_tensor("r", s, long_p)
+    assert calls == [16, 16, 13]
+    assert np.allclose(np.asarray(ref), np.asarray(out), atol=5e-3)
+    calls.clear()
+    prompts = [rng.integers(0, 500, size=(1, L)) for L in (10, 5, 9, 3)]
+    await asyncio.gather(*(e.infer_tensor(f"b{i}", s, p) for i, p in enumerate(prompts)))
+    assert max(calls) <= 16 and sum(calls) == 27
+  run(main())

@@ -228,3 +228,31 @@ def test_deepseek_gpu_matches_cpu_reference(gpu, name):
     lg = gr.forward(["a", "b"], [1, 1], tok).cpu()  # HIP graph replay
     assert ((lc - lg).norm() / lc.norm()).item() < 8e-2
     tok = lc.argmax(-1).int()
+
+
+def test_graph_buckets_survive_workspace_growth(gpu):
+  """Serving pattern: a decode graph captured for a small batch bucket keeps replaying correctly after a
+  larger bucket's capture grew the shared split-K workspace (captured graphs keep the old buffer's
+  address; it must stay alive), with prefills of several lengths in between."""
+  name = "tiny-llama-d64"
+  c = preset(name)
+  L = c.num_layers
+  sh = Shard(name, 0, L - 1, L)
+  g = ShardRunner(c, sh, gpu, max_batch=64, max_ctx=512, use_graphs=True)
+  e = ShardRunner(c, sh, gpu, max_batch=64, max_ctx=512, use_graphs=False)
+  ids = torch.randint(0, c.vocab_size, (20,), generator=torch.Generator().manual_seed(3), dtype=torch.int32)
+  for r in (g, e):
+    r.forward(["solo"], [20], ids)
+  tok = torch.tensor([5], dtype=torch.int32)
+  assert torch.allclose(g.forward(["solo"], [1], tok), e.forward(["solo"], [1], tok), atol=2e-2, rtol=2e-2)  # bucket 1
+  rids = [f"b{i}" for i in range(48)]
+  ids = torch.randint(0, c.vocab_size, (48 * 7,), generator=torch.Generator().manual_seed(4), dtype=torch.int32)
+  for r in (g, e):
+    r.forward(rids, [7] * 48, ids)
+  toks = torch.randint(0, c.vocab_size, (48,), generator=torch.Generator().manual_seed(5), dtype=torch.int32)
+  for _ in range(2):  # bucket 48: its capture may grow the workspace
+    a, b = g.forward(rids, [1] * 48, toks), e.forward(rids, [1] * 48, toks)
+    assert torch.allclose(a, b, atol=2e-2, rtol=2e-2)
+  for _ in range(3):  # bucket 1 again, captured before the growth
+    a, b = g.forward(["solo"], [1], tok), e.forward(["solo"], [1], tok)
+    assert torch.allclose(a, b, atol=2e-2, rtol=2e-2)

@@ -42,6 +42,11 @@ def default_device() -> torch.device:
   return torch.device("cpu")
 
 
+# new tokens per batched forward (prefill chunks + decode tokens): bounds the step's activations and keeps a
+# burst of long prompts from stalling every decoding request for one huge step (vLLM's max_num_batched_tokens)
+MAX_STEP_TOKENS = int(os.environ.get("XOT_MAX_STEP_TOKENS", "8192"))
+
+
 class ShardedInferenceEngine(InferenceEngine):
   def __init__(self, shard_downloader=None, device: Optional[torch.device] = None, seed: int = 1234):
     self.shard: Optional[Shard] = None
@@ -129,11 +134,30 @@ class ShardedInferenceEngine(InferenceEngine):
       asyncio.create_task(self._drain())
     return await fut
 
+  @staticmethod
+  def _qlen(inp) -> int:
+    shape = inp.shape if hasattr(inp, "shape") else np.asarray(inp).shape
+    return int(shape[1]) if len(shape) >= 2 else int(np.prod(shape))
+
+  def _take_batch(self) -> list:
+    """Next step's requests: up to max_batch of them and MAX_STEP_TOKENS new tokens in all (decode
+    tokens and prefill prompts mix; a prompt longer than the budget runs alone, chunked)."""
+    cap = self.runner.max_batch if self.runner is not None else 1
+    batch, rest, tokens = [], [], 0
+    for it in self._queue:
+      n = self._qlen(it[2])
+      if len(batch) < cap and (not batch or tokens + n <= MAX_STEP_TOKENS):
+        batch.append(it)
+        tokens += n
+      else:
+        rest.append(it)
+    self._queue = rest
+    return batch
+
   async def _drain(self):
     try:
       while self._queue:
-        cap = self.runner.max_batch if self.runner is not None else 1
-        batch, self._queue = self._queue[:cap], self._queue[cap:]
+        batch = self._take_batch()
         ok = [it for it in batch if it[1] == self.shard]
         for it in batch:
           if it[1] != self.shard and not it[3].done():
@@ -172,14 +196,20 @@ class ShardedInferenceEngine(InferenceEngine):
       image_embeds = torch.cat(feats) if feats else None
     try:
       x = torch.cat(xs)
-      out = (self.runner.forward(rids, qlens, x) if image_embeds is None
-             else self.runner.forward(rids, qlens, x, image_embeds=image_embeds))
+      if sum(qlens) > MAX_STEP_TOKENS and len(rids) == 1:
+        out = self._forward_chunked(rids[0], x, image_embeds)
+      else:
+        out = (self.runner.forward(rids, qlens, x) if image_embeds is None
+               else self.runner.forward(rids, qlens, x, image_embeds=image_embeds))
     except torch.cuda.OutOfMemoryError:
       self.clear_model()
       raise
     res = []
     if self.shard.is_last_layer():
-      # [B, V] fp32 logits of each request's last token; they stay on the device for the sampler
+      # [B, V] fp32 logits of each request's last token; they stay on the device for the sampler.  A copy:
+      # a decode step's logits live in its HIP graph's static buffer, which the next step of the same batch
+      # bucket overwrites, possibly before every request of this step has sampled
+      out = out.clone()
       for i, rid in enumerate(rids):
         res.append((out[i:i + 1], {"n_past": self.runner.num_tokens(rid)}))
       return res
@@ -189,6 +219,23 @@ class ShardedInferenceEngine(InferenceEngine):
       res.append((outc[off:off + L].reshape(1, L, -1), {"n_past": self.runner.num_tokens(rid)}))
       off += L
     return res
+
+  def _forward_chunked(self, rid: str, x: torch.Tensor, image_embeds: Optional[torch.Tensor]):
+    """Chunked prefill of one long prompt: MAX_STEP_TOKENS-token pieces appended to its KV in turn.
+    Returns the last piece's logits (last shard) or every piece's hidden states (other shards)."""
+    outs, used = [], 0
+    img_id = self.config.image_token_id
+    for lo in range(0, x.shape[0], MAX_STEP_TOKENS):
+      xc = x[lo:lo + MAX_STEP_TOKENS]
+      emb = None
+      if image_embeds is not None:
+        n = int((xc == img_id).sum()) if xc.dim() == 1 else 0
+        emb = image_embeds[used:used + n] if n else None
+        used += n
+      y = (self.runner.forward([rid], [xc.shape[0]], xc) if emb is None
+           else self.runner.forward([rid], [xc.shape[0]], xc, image_embeds=emb))
+      outs.append(y if self.shard.is_last_layer() else y.clone())
+    return outs[-1] if self.shard.is_last_layer() else torch.cat(outs)
 
   async def finish_request(self, request_id: str) -> None:
     self._images.pop(request_id, None)

@@ -67,10 +67,17 @@ def to_rowmajor(w: torch.Tensor) -> torch.Tensor:
 
 # ------------------------------------------------------------------ per-device scratch
 class _Scratch:
+  """Per-device split-K slabs and tile tickets shared by every GEMM call.  A buffer that has to grow is
+  replaced, but the old one is kept alive: HIP graphs captured earlier (decode graphs of other batch
+  buckets) hold its address, and replaying them into a freed block would corrupt whatever the caching
+  allocator put there next (a serving run that captured bucket 1, then grew the slabs for bucket 64,
+  faulted exactly that way)."""
+
   def __init__(self):
     self.ws: Dict[int, torch.Tensor] = {}
     self.dense: Dict[int, torch.Tensor] = {}
     self.tk: Dict[int, torch.Tensor] = {}
+    self.retired: list = []
 
   def splitk(self, device, n: int) -> torch.Tensor:
     idx = device.index or 0
@@ -78,7 +85,9 @@ class _Scratch:
     if t is None or t.numel() < n:
       if torch.cuda.is_current_stream_capturing():
         raise RuntimeError("split-K workspace must be sized before graph capture")
-      t = torch.empty(max(n, 1 << 20), dtype=torch.float32, device=device)
+      if t is not None:
+        self.retired.append(t)
+      t = torch.empty(max(n, 1 << 20, 2 * (t.numel() if t is not None else 0)), dtype=torch.float32, device=device)
       self.ws[idx] = t
     return t
 
@@ -90,6 +99,8 @@ class _Scratch:
     if t is None or t.numel() < n:
       if torch.cuda.is_current_stream_capturing():
         raise RuntimeError("split-K tickets must be sized before graph capture")
+      if t is not None:
+        self.retired.append(t)
       t = torch.zeros(max(n, 1 << 16), dtype=torch.int32, device=device)
       self.tk[idx] = t
     return t
