@@ -100,8 +100,13 @@ async def main(a):
          "data": "random-init weights, byte tokenizer, synthetic prompts", "dtype": "bf16",
          "device": caps.chip}
   print(json.dumps(out), flush=True)
+  if os.environ.get("XOT_PROFILE"):
+    import pstats
+    PROF.disable()
+    pstats.Stats(PROF).sort_stats("tottime").print_stats(25)
   await server.close()
   await node.stop()
+  sys.stdout.flush()
   os._exit(0)  # engine executor threads / gRPC server: leave without waiting on them
 
 
@@ -112,4 +117,8 @@ if __name__ == "__main__":
   ap.add_argument("--max-tokens", type=int, default=128)
   ap.add_argument("--prompt-words", type=int, default=200)
   ap.add_argument("--temperature", type=float, default=0.6)
+  if os.environ.get("XOT_PROFILE"):  # host-side hot spots of the serving loop
+    import cProfile
+    PROF = cProfile.Profile()
+    PROF.enable()
   asyncio.run(main(ap.parse_args()))

@@ -65,6 +65,8 @@ class ShardedInferenceEngine(InferenceEngine):
     self._queue: list = []  # (request id, shard, input, future) waiting for the next batched step
     self._draining = False
     self._images: dict = {}  # request id -> [N, 3, S, S] pixels awaiting that request's prefill (LLaVA)
+    self._sample_q: list = []  # (logits, temperature, top_k, future) drawn together by _drain_samples
+    self._sampling = False
 
   # ------------------------------------------------------------------ helpers
   async def _run(self, fn, *args):
@@ -80,17 +82,52 @@ class ShardedInferenceEngine(InferenceEngine):
     return self.tokenizer.decode(np.asarray(tokens).reshape(-1).tolist())
 
   async def sample(self, x, temp: float = TEMPERATURE, top_k: int = TOP_K) -> np.ndarray:
-    def _sample():
-      from ..ops import kernels as K
-      logits = torch.as_tensor(x) if not isinstance(x, torch.Tensor) else x
-      logits = logits.reshape(-1, logits.shape[-1]).to(self.device, torch.float32).contiguous()
-      temps = torch.full((logits.shape[0],), float(temp), dtype=torch.float32, device=self.device)
-      so = self.seed_off.to(self.device)
-      tok = K.sample(logits, temps, int(top_k), so)
-      self.seed_off[1] += 1
-      return tok.cpu().numpy().astype(np.int64)
+    """Sample one request's next token.  Concurrent calls (the requests of one batched step) are drawn
+    together: one sampler launch over their stacked logits and one device-to-host copy, instead of a
+    launch + synchronisation per request."""
+    fut = asyncio.get_running_loop().create_future()
+    self._sample_q.append((x, float(temp), int(top_k), fut))
+    if not self._sampling:
+      self._sampling = True
+      asyncio.create_task(self._drain_samples())
+    return await fut
 
-    return await self._run(_sample)
+  async def _drain_samples(self):
+    try:
+      while self._sample_q:
+        batch, self._sample_q = self._sample_q, []
+        try:
+          res = await self._run(self._sample_batch, [(x, t, k) for x, t, k, _ in batch])
+          for (_, _, _, fut), r in zip(batch, res):
+            if not fut.done():
+              fut.set_result(r)
+        except Exception as e:  # noqa: BLE001 - delivered to every waiter
+          for *_, fut in batch:
+            if not fut.done():
+              fut.set_exception(e)
+    finally:
+      self._sampling = False
+
+  def _sample_batch(self, items):
+    from ..ops import kernels as K
+    rows, out = [], [None] * len(items)
+    for x, _, _ in items:
+      t = torch.as_tensor(x) if not isinstance(x, torch.Tensor) else x
+      rows.append(t.reshape(-1, t.shape[-1]))
+    for k in sorted({k for _, _, k in items}):  # one launch per distinct top_k (usually one)
+      idx = [i for i, it in enumerate(items) if it[2] == k]
+      logits = torch.cat([rows[i].to(self.device, torch.float32) for i in idx]).contiguous()
+      temps = torch.tensor([items[i][1] for i in idx for _ in range(rows[i].shape[0])], dtype=torch.float32,
+                           device=self.device)
+      so = self.seed_off.to(self.device)
+      tok = K.sample(logits, temps, k, so).cpu().numpy().astype(np.int64)
+      self.seed_off[1] += 1
+      off = 0
+      for i in idx:
+        n = rows[i].shape[0]
+        out[i] = tok[off:off + n]
+        off += n
+    return out
 
   # ------------------------------------------------------------------ prompts with images (LLaVA)
   async def infer_prompt(self, request_id: str, shard: Shard, prompt: str,

@@ -421,7 +421,16 @@ class Node:
     raise ValueError(f"Peer for {node_id} not found")
 
   def _partitions(self) -> List[Partition]:
-    return self.partitioning_strategy.partition(self.topology)
+    """Partitions of the current topology, memoised per topology content: every generated token asks
+    several times (shard of this peer, next hop), and the topology only changes on gossip."""
+    topo = self.topology
+    key = (id(topo), tuple(sorted((nid, caps.memory) for nid, caps in topo.nodes.items())))
+    cached = getattr(self, "_parts_cache", None)
+    if cached is not None and cached[0] == key:
+      return cached[1]
+    parts = self.partitioning_strategy.partition(topo)
+    self._parts_cache = (key, parts)
+    return parts
 
   def _partition_node(self, index: int) -> str:
     parts = self._partitions()
