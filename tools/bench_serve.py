@@ -88,8 +88,11 @@ async def main(a):
       await asyncio.gather(*(one(session, -2 - j, 4) for j in range(b)))
     warm = time.perf_counter() - t0
     t0 = time.perf_counter()
+    s0 = dict(eng.stats)
     res = await asyncio.gather(*(one(session, i, a.max_tokens) for i in range(a.concurrency)))
     wall = time.perf_counter() - t0
+    steps = eng.stats["steps"] - s0["steps"]
+    reqs = eng.stats["requests"] - s0["requests"]
   toks = sum(r[1] for r in res)
   ttfts = sorted(r[0] for r in res)
   out = {"metric": "API streaming output tokens/sec (one peer)", "model": a.model, "concurrency": a.concurrency,
@@ -97,6 +100,8 @@ async def main(a):
          "value": round(toks / wall, 2), "unit": "tokens/s", "wall_s": round(wall, 2), "warmup_s": round(warm, 1),
          "ttft_s": {"p50": round(ttfts[len(ttfts) // 2], 3), "max": round(ttfts[-1], 3)},
          "per_request_tok_s_p50": round(sorted(r[1] / r[2] for r in res)[len(res) // 2], 2),
+         "engine_steps": steps, "mean_requests_per_step": round(reqs / max(steps, 1), 1),
+         "ms_per_step": round(wall * 1e3 / max(steps, 1), 2),
          "data": "random-init weights, byte tokenizer, synthetic prompts", "dtype": "bf16",
          "device": caps.chip}
   print(json.dumps(out), flush=True)

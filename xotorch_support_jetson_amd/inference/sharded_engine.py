@@ -67,6 +67,7 @@ class ShardedInferenceEngine(InferenceEngine):
     self._images: dict = {}  # request id -> [N, 3, S, S] pixels awaiting that request's prefill (LLaVA)
     self._sample_q: list = []  # (logits, temperature, top_k, future) drawn together by _drain_samples
     self._sampling = False
+    self.stats = {"steps": 0, "requests": 0, "tokens": 0}  # batched forward steps (serving diagnostics)
 
   # ------------------------------------------------------------------ helpers
   async def _run(self, fn, *args):
@@ -191,9 +192,24 @@ class ShardedInferenceEngine(InferenceEngine):
     self._queue = rest
     return batch
 
+  async def _settle(self):
+    """Let the requests that are about to queue do so before a step is cut: after a batched step each
+    request's next input arrives through a chain of a few tasks (sample -> result handling -> forward),
+    and cutting the step at the first arrival would split one decode round into several forward passes,
+    each re-reading every weight."""
+    prev, stable = -1, 0
+    for _ in range(32):
+      n = len(self._queue)
+      stable = stable + 1 if n == prev else 0
+      if stable >= 3:
+        return
+      prev = n
+      await asyncio.sleep(0)
+
   async def _drain(self):
     try:
       while self._queue:
+        await self._settle()
         batch = self._take_batch()
         ok = [it for it in batch if it[1] == self.shard]
         for it in batch:
@@ -214,6 +230,8 @@ class ShardedInferenceEngine(InferenceEngine):
       self._draining = False
 
   def _infer_batch(self, items):
+    self.stats["steps"] += 1
+    self.stats["requests"] += len(items)
     if self.trainer is not None and self.trainer.dirty:
       self.trainer.sync_to_inference()  # serve the weights training just produced
     rids, qlens, xs = [], [], []
