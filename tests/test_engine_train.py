@@ -260,3 +260,24 @@ def test_step_token_budget_and_chunked_prefill(monkeypatch):
     await asyncio.gather(*(e.infer_tensor(f"b{i}", s, p) for i, p in enumerate(prompts)))
     assert max(calls) <= 16 and sum(calls) == 27
   run(main())
+
+
+def test_presampled_tokens_match_greedy():
+  """With the sampling parameters in the step's state, the last shard draws each token with the forward;
+  sample() returns it (greedy here: the argmax) without another executor trip."""
+  async def main():
+    s = Shard(MODEL, 0, N - 1, N)
+    e = eng()
+    rng = np.random.default_rng(11)
+    prompts = [rng.integers(0, 500, size=(1, L)) for L in (6, 4, 9)]
+    st = {"temperature": 0.0, "top_k": 35}
+    outs = await asyncio.gather(*(e.infer_tensor(f"p{i}", s, p, st) for i, p in enumerate(prompts)))
+    toks = await asyncio.gather(*(e.sample(o, temp=0.0, top_k=35) for o, _ in outs))
+    for (o, _), t in zip(outs, toks):
+      assert int(t[0]) == int(np.argmax(np.asarray(o)))
+    assert e.stats.get("presampled", 0) == 3
+    # a different temperature than the state's falls back to a real draw
+    out, _ = await e.infer_tensor("q", s, prompts[0], st)
+    t = await e.sample(out, temp=0.0, top_k=1)
+    assert int(t[0]) == int(np.argmax(np.asarray(out))) and e.stats["presampled"] == 3
+  run(main())

@@ -102,6 +102,7 @@ async def main(a):
          "per_request_tok_s_p50": round(sorted(r[1] / r[2] for r in res)[len(res) // 2], 2),
          "engine_steps": steps, "mean_requests_per_step": round(reqs / max(steps, 1), 1),
          "ms_per_step": round(wall * 1e3 / max(steps, 1), 2),
+         "presampled_tokens": eng.stats.get("presampled", 0) - s0.get("presampled", 0),
          "data": "random-init weights, byte tokenizer, synthetic prompts", "dtype": "bf16",
          "device": caps.chip}
   print(json.dumps(out), flush=True)

@@ -45,6 +45,7 @@ def default_device() -> torch.device:
 # new tokens per batched forward (prefill chunks + decode tokens): bounds the step's activations and keeps a
 # burst of long prompts from stalling every decoding request for one huge step (vLLM's max_num_batched_tokens)
 MAX_STEP_TOKENS = int(os.environ.get("XOT_MAX_STEP_TOKENS", "8192"))
+PRESAMPLE = os.environ.get("XOT_PRESAMPLE", "1") == "1"
 
 
 class ShardedInferenceEngine(InferenceEngine):
@@ -68,6 +69,7 @@ class ShardedInferenceEngine(InferenceEngine):
     self._sample_q: list = []  # (logits, temperature, top_k, future) drawn together by _drain_samples
     self._sampling = False
     self.stats = {"steps": 0, "requests": 0, "tokens": 0}  # batched forward steps (serving diagnostics)
+    self._presampled: dict = {}  # (logits ptr, row) -> (temperature, top_k, token) drawn with the forward
 
   # ------------------------------------------------------------------ helpers
   async def _run(self, fn, *args):
@@ -82,16 +84,53 @@ class ShardedInferenceEngine(InferenceEngine):
     await self.ensure_shard(shard)
     return self.tokenizer.decode(np.asarray(tokens).reshape(-1).tolist())
 
+  def _presample(self, logits: torch.Tensor, states: list) -> None:
+    """Last shard: draw the step's tokens right after its forward, in the same executor call (one
+    sampler launch, one device-to-host copy), for requests whose state carries their sampling
+    parameters (the Node forwards temperature / top_k with every step).  sample() then returns the
+    stored token without another trip through the executor."""
+    # tokens of the previous step nobody asked for (finished requests) go: a lagging request still holds its
+    # logits view, so no new tensor can reuse that base address and collide with a fresh key
+    self._presampled.clear()
+    if not PRESAMPLE or not states or any("temperature" not in st for st in states):
+      return
+    from ..ops import kernels as K
+    groups = {}
+    for i, st in enumerate(states):
+      groups.setdefault(int(st.get("top_k") or TOP_K), []).append(i)
+    for k, idx in groups.items():
+      sel = logits if len(idx) == logits.shape[0] else logits[torch.tensor(idx, device=logits.device)]
+      temps = torch.tensor([float(states[i]["temperature"]) for i in idx], dtype=torch.float32, device=logits.device)
+      tok = K.sample(sel.contiguous(), temps, k, self.seed_off.to(logits.device)).cpu().numpy().astype(np.int64)
+      self.seed_off[1] += 1
+      for j, i in enumerate(idx):
+        self._presampled[(logits.data_ptr(), i)] = (float(states[i]["temperature"]), k, tok[j:j + 1])
+
   async def sample(self, x, temp: float = TEMPERATURE, top_k: int = TOP_K) -> np.ndarray:
-    """Sample one request's next token.  Concurrent calls (the requests of one batched step) are drawn
+    """Sample one request's next token.  A token drawn with the forward (_presample, same parameters)
+    is returned at once; otherwise concurrent calls (the requests of one batched step) are drawn
     together: one sampler launch over their stacked logits and one device-to-host copy, instead of a
     launch + synchronisation per request."""
+    if isinstance(x, torch.Tensor) and x.dim() == 2 and x.shape[0] == 1 and self._presampled:
+      key = self._presample_key(x)
+      hit = self._presampled.pop(key, None) if key is not None else None
+      if hit is not None and hit[0] == float(temp) and hit[1] == int(top_k):
+        self.stats["presampled"] = self.stats.get("presampled", 0) + 1
+        return hit[2]
     fut = asyncio.get_running_loop().create_future()
     self._sample_q.append((x, float(temp), int(top_k), fut))
     if not self._sampling:
       self._sampling = True
       asyncio.create_task(self._drain_samples())
     return await fut
+
+  @staticmethod
+  def _presample_key(x: torch.Tensor):
+    """(data pointer of the step's logits tensor, row) of a [1, V] row view of it."""
+    if x._base is None or x._base.dim() != 2:
+      return None
+    row = (x.data_ptr() - x._base.data_ptr()) // (x.element_size() * x._base.stride(0))
+    return (x._base.data_ptr(), int(row))
 
   async def _drain_samples(self):
     try:
@@ -166,7 +205,7 @@ class ShardedInferenceEngine(InferenceEngine):
     time, through a single global KV cache (sharded_inference_engine.py:230-370)."""
     await self.ensure_shard(shard)
     fut = asyncio.get_running_loop().create_future()
-    self._queue.append((request_id, shard, input_data, fut))
+    self._queue.append((request_id, shard, input_data, fut, inference_state or {}))
     if not self._draining:
       self._draining = True
       asyncio.create_task(self._drain())
@@ -218,14 +257,14 @@ class ShardedInferenceEngine(InferenceEngine):
         if not ok:
           continue
         try:
-          results = await self._run(self._infer_batch, [(rid, x) for rid, _, x, _ in ok])
-          for (_, _, _, fut), r in zip(ok, results):
-            if not fut.done():
-              fut.set_result(r)
+          results = await self._run(self._infer_batch, [(it[0], it[2], it[4]) for it in ok])
+          for it, r in zip(ok, results):
+            if not it[3].done():
+              it[3].set_result(r)
         except Exception as e:  # noqa: BLE001 - delivered to every waiter of the batch
-          for _, _, _, fut in ok:
-            if not fut.done():
-              fut.set_exception(e)
+          for it in ok:
+            if not it[3].done():
+              it[3].set_exception(e)
     finally:
       self._draining = False
 
@@ -235,7 +274,7 @@ class ShardedInferenceEngine(InferenceEngine):
     if self.trainer is not None and self.trainer.dirty:
       self.trainer.sync_to_inference()  # serve the weights training just produced
     rids, qlens, xs = [], [], []
-    for rid, inp in items:
+    for rid, inp, *_ in items:
       x = inp if isinstance(inp, torch.Tensor) else torch.as_tensor(np.asarray(inp))
       if x.dim() == 3:  # hidden [1, L, D]
         L = x.shape[1]
@@ -265,6 +304,7 @@ class ShardedInferenceEngine(InferenceEngine):
       # a decode step's logits live in its HIP graph's static buffer, which the next step of the same batch
       # bucket overwrites, possibly before every request of this step has sampled
       out = out.clone()
+      self._presample(out, [it[2] if len(it) > 2 else {} for it in items])
       for i, rid in enumerate(rids):
         res.append((out[i:i + 1], {"n_past": self.runner.num_tokens(rid)}))
       return res
