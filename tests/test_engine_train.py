@@ -281,3 +281,62 @@ def test_presampled_tokens_match_greedy():
     t = await e.sample(out, temp=0.0, top_k=1)
     assert int(t[0]) == int(np.argmax(np.asarray(out))) and e.stats["presampled"] == 3
   run(main())
+
+
+@pytest.mark.parametrize("model", ["tiny-deepseek-v2", "tiny-deepseek-v3"])
+def test_deepseek_training_matches_inference_and_pipeline(model):
+  """DeepSeek fine-tuning (MLA in its expanded form + DeepSeekMoE with shared experts, group-limited /
+  noaux_tc routing): the trainer's forward reproduces the serving path's (absorbed MLA) logits, a two-stage
+  pipeline step equals the single-stage step, loss falls, and the trained latent projections (kv_b split
+  back into W_UK / W_UV), shared experts and router reach the inference shard."""
+  n = 3
+
+  async def main():
+    rng = np.random.default_rng(7)
+    x = rng.integers(0, 64, size=(2, 10))
+    y = np.roll(x, -1, 1)
+    ln = np.array([10, 7])
+    full = eng()
+    fs = Shard(model, 0, n - 1, n)
+    out_inf, _ = await full.infer_tensor("q", fs, x[:1])
+    tr = full._get_trainer()
+    with torch.no_grad():
+      logits = tr.forward(torch.as_tensor(x[:1])).float()[0, -1]
+    ref = torch.as_tensor(np.asarray(out_inf)).float().reshape(-1)
+    assert torch.corrcoef(torch.stack([logits, ref]))[0, 1] > 0.99
+    li = next(i for i in range(n) if tr.c.moe_layer(i))
+    torch.manual_seed(0)
+    xn = torch.randn(16, tr.c.hidden_size).bfloat16()
+    h = torch.zeros(16, tr.c.hidden_size, dtype=torch.bfloat16)
+    full.runner.model._moe(xn, full.runner.weights.layers[li], h)
+    with torch.no_grad():
+      mine = tr._moe(xn, li).float()
+    assert torch.allclose(mine, h.float(), atol=2e-3, rtol=2e-2), (mine - h.float()).abs().max()
+
+    l_full, _ = await full.train("t", fs, x, y, ln)
+    s0, s1 = eng(), eng()
+    a, b = Shard(model, 0, 0, n), Shard(model, 1, n - 1, n)
+    hh = await s0.train_forward("t", a, x)
+    l_split, g = await s1.train("t", b, hh, y, ln)
+    await s0.train("t", a, x, g, ln, loss="back_gradient")
+    assert abs(l_full - l_split) < 1e-3
+    tf, t0, t1 = full.trainer, s0.trainer, s1.trainer
+    for k in ("0.qkv", "0.kvb", "0.kv_ln", "0.gu", "embed"):
+      assert torch.allclose(tf.master[k], t0.master[k], atol=2e-6), k
+    for k in ("1.router", "1.egu", "1.sh_gu", "2.kvb", "2.o", "norm"):
+      assert torch.allclose(tf.master[k], t1.master[k], atol=2e-6), k
+    if tr.c.q_lora_rank:
+      assert torch.allclose(tf.master["1.qb"], t1.master["1.qb"], atol=2e-6)
+
+    full.lr = 3e-3
+    tf.lr = 3e-3
+    losses = [(await full.train("t", fs, x, y, ln))[0] for _ in range(10)]
+    assert losses[-1] < losses[0] * 0.9, losses
+    out2, _ = await full.infer_tensor("q2", fs, x[:1])  # syncs the trained weights into the shard
+    with torch.no_grad():
+      logits2 = tf.forward(torch.as_tensor(x[:1])).float()[0, -1]
+    ref2 = torch.as_tensor(np.asarray(out2)).float().reshape(-1)
+    assert torch.corrcoef(torch.stack([logits2, ref2]))[0, 1] > 0.99
+    assert not torch.allclose(ref, ref2, atol=1e-3)
+
+  run(main())

@@ -131,7 +131,7 @@ def test_fused_grad_accumulation_matches_autograd(gpu):
     assert rel < 0.05, (k, rel)
 
 
-@pytest.mark.parametrize("name", ["tiny-llama-d64", "tiny-mixtral"])
+@pytest.mark.parametrize("name", ["tiny-llama-d64", "tiny-mixtral", "tiny-deepseek-v3"])
 def test_fused_grad_accumulation_values(gpu, name):
   """The accumulated gradients themselves (not AdamW deltas, which barely react to a scaled gradient)
   after 3 micro-batches: fused accumulation (LinearFn's beta = 1 GEMM; for the Mixtral expert stacks
@@ -151,7 +151,8 @@ def test_fused_grad_accumulation_values(gpu, name):
   for fused in (True, False):
     tr = ShardTrainer(w, gpu, lr=1e-3, max_seq=256)
     if c.is_moe:
-      assert {f"0.egu", f"0.edown"} <= set(tr.acc)
+      li = next(i for i in range(c.num_layers) if c.moe_layer(i))
+      assert {f"{li}.egu", f"{li}.edown"} <= set(tr.acc)
     if not fused:
       tr.acc = {}
     tr.zero_grad()
@@ -168,12 +169,13 @@ def test_fused_grad_accumulation_values(gpu, name):
     assert rel < 0.03 and abs(scale - 1) < 0.02, (k, rel, scale)
 
 
-def test_moe_training_gpu(gpu):
-  """Mixtral-style fine-tuning on the GPU: the first AdamW step matches the CPU trainer on the same
-  weights, loss falls, and weights trained from a decode-layout shard (pre-shuffled expert stacks) are
-  written back so the serving runner reproduces the trainer's logits."""
+@pytest.mark.parametrize("name", ["tiny-mixtral", "tiny-deepseek-v2", "tiny-deepseek-v3"])
+def test_moe_training_gpu(gpu, name):
+  """MoE fine-tuning on the GPU (Mixtral; DeepSeek with MLA, shared experts and grouped routing): the first
+  AdamW step matches the CPU trainer on the same weights, loss falls, and weights trained from a
+  decode-layout shard (pre-shuffled expert stacks) are written back so the serving runner (absorbed MLA
+  kernels for DeepSeek) reproduces the trainer's logits."""
   from xotorch_support_jetson_amd.train.trainer import ShardTrainer
-  name = "tiny-mixtral"
   c = preset(name)
   sh = Shard(name, 0, c.num_layers - 1, c.num_layers)
   g = torch.Generator().manual_seed(3)

@@ -40,9 +40,6 @@ class ShardTrainer:
                weight_decay: float = 0.0, max_seq: int = 4096, grad_clip: float = 1.0):
     self.w = weights
     self.c: ModelConfig = weights.config
-    if self.c.is_mla:
-      raise NotImplementedError(f"{self.c.model_type}: fine-tuning of MLA (DeepSeek) shards is not implemented; "
-                                "they serve (inference) only")
     self.shard = weights.shard
     self.device = torch.device(device)
     self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
@@ -53,16 +50,31 @@ class ShardTrainer:
     self.max_seq = max_seq
     # training parameters (row-major, gate|up halves), bf16 leaves + fp32 master + moments
     self.params: Dict[str, torch.Tensor] = {}
+    self.router_bias: Dict[int, torch.Tensor] = {}  # DeepSeek-V3 selection bias: a buffer, not trained
+    c = self.c
     for i, lw in weights.layers.items():
       g, u = split_gate_up(_rowmajor(lw.gu_w))  # [F, D] each, or [E, F, D] expert stacks
-      self._add(f"{i}.qkv", _rowmajor(lw.qkv_w))
+      self._add(f"{i}.qkv", _rowmajor(lw.qkv_w))  # MLA: the fused A projection [q_a | kv latent | rope key]
       if lw.qkv_b is not None:
         self._add(f"{i}.qkv_b", lw.qkv_b)
       self._add(f"{i}.o", _rowmajor(lw.o_w))
-      if self.c.is_moe:  # Mixtral: router [E, D], experts' gate|up [E, 2F, D], down [E, D, F]
+      if c.is_mla:
+        if c.q_lora_rank:
+          self._add(f"{i}.q_ln", lw.q_ln)
+          self._add(f"{i}.qb", _rowmajor(lw.qb_w))
+        self._add(f"{i}.kv_ln", lw.kv_ln)
+        # kv_b_proj as one [H (dn + dv), kv_lora] projection (HF layout; the serving path splits it)
+        self._add(f"{i}.kvb", torch.cat([lw.wuk, lw.wuv], 1).reshape(-1, c.kv_lora_rank))
+      if lw.router is not None:  # MoE: router [E, D], experts' gate|up [E, 2F, D], down [E, D, F]
         self._add(f"{i}.router", _rowmajor(lw.router))
         self._add(f"{i}.egu", torch.cat([g, u], 1))
         self._add(f"{i}.edown", _rowmajor(lw.down_w))
+        if lw.router_bias is not None:
+          self.router_bias[i] = lw.router_bias.detach().to(self.device, torch.float32)
+        if lw.sh_gu_w is not None:  # DeepSeek shared experts: a dense SwiGLU
+          sg, su = split_gate_up(_rowmajor(lw.sh_gu_w))
+          self._add(f"{i}.sh_gu", torch.cat([sg, su], 0))
+          self._add(f"{i}.sh_down", _rowmajor(lw.sh_down_w))
       else:
         self._add(f"{i}.gu", torch.cat([g, u], 0))
         self._add(f"{i}.down", _rowmajor(lw.down_w))
@@ -78,7 +90,7 @@ class ShardTrainer:
     self.acc: Dict[str, A.GradAcc] = {}
     if self.device.type == "cuda":
       for k in self.params:
-        if k.split(".")[-1] in ("qkv", "o", "gu", "down", "egu", "edown"):
+        if k.split(".")[-1] in ("qkv", "o", "gu", "down", "egu", "edown", "qb", "kvb", "sh_gu", "sh_down"):
           self.acc[k] = A.GradAcc(k, self.params[k])
     self.master = {k: p.detach().float().clone() for k, p in self.params.items()}
     self.m = {k: torch.zeros_like(v) for k, v in self.master.items()}
@@ -104,16 +116,19 @@ class ShardTrainer:
     h = h.reshape(B * L, D)
     for i in self.shard.layers():
       xn = A.rmsnorm(h, P[f"{i}.ln1"], c.rms_norm_eps)
-      qkv = self._mm(xn, f"{i}.qkv")
-      if f"{i}.qkv_b" in P:
-        qkv = qkv + P[f"{i}.qkv_b"]
-      q, k, v = A.qkv_split(qkv, H * Dh, Hkv * Dh)
-      q = A.rope(q, pos, self.cos_sin, H, Dh)
-      k = A.rope(k, pos, self.cos_sin, Hkv, Dh)
-      a = A.attention(q, k, v, B, L, H, Hkv, Dh)  # flash-style HIP kernels (fwd + dQ + dK/dV)
+      if c.is_mla:
+        a = self._mla(xn, i, pos, B, L)
+      else:
+        qkv = self._mm(xn, f"{i}.qkv")
+        if f"{i}.qkv_b" in P:
+          qkv = qkv + P[f"{i}.qkv_b"]
+        q, k, v = A.qkv_split(qkv, H * Dh, Hkv * Dh)
+        q = A.rope(q, pos, self.cos_sin, H, Dh)
+        k = A.rope(k, pos, self.cos_sin, Hkv, Dh)
+        a = A.attention(q, k, v, B, L, H, Hkv, Dh)  # flash-style HIP kernels (fwd + dQ + dK/dV)
       h = self._mm(a, f"{i}.o", h)
       xn = A.rmsnorm(h, P[f"{i}.ln2"], c.rms_norm_eps)
-      if c.is_moe:
+      if f"{i}.router" in P:
         h = h + self._moe(xn, i)
       else:
         h = self._mm(A.silu_mul(self._mm(xn, f"{i}.gu").contiguous()), f"{i}.down", h)
@@ -123,14 +138,62 @@ class ShardTrainer:
     head = P["lm_head"] if "lm_head" in P else P["embed"]
     return (xn @ head.t()).view(B, L, -1)
 
+  def _mla(self, xn: torch.Tensor, i: int, pos: torch.Tensor, B: int, L: int) -> torch.Tensor:
+    """DeepSeek multi-head latent attention with autograd, in HF's expanded form (training sees whole
+    sequences, so the key / value up-projection runs once per token): A = xn . [q_a | kv_a]^T,
+    q = rmsnorm(q_a) . q_b^T, latent c = rmsnorm(kv_a), k_pe = rope(shared key), [k_nope | v] = c . kv_b^T,
+    causal attention over [q_nope | q_pe] . [k_nope | k_pe] (fused SDPA; 192-wide q/k, 128-wide v)."""
+    c, P = self.c, self.params
+    T = xn.shape[0]
+    H, dn, dr, dv, Lr = c.num_heads, c.qk_nope_head_dim, c.qk_rope_head_dim, c.v_head_dim, c.kv_lora_rank
+    nq = c.q_lora_rank or H * (dn + dr)
+    a = self._mm(xn, f"{i}.qkv")
+    if c.q_lora_rank:
+      q = self._mm(A.rmsnorm(a[:, :nq].contiguous(), P[f"{i}.q_ln"], c.rms_norm_eps), f"{i}.qb")
+    else:
+      q = a[:, :nq]
+    cn = A.rmsnorm(a[:, nq:nq + Lr].contiguous(), P[f"{i}.kv_ln"], c.rms_norm_eps)
+    kpe = A.rope(a[:, nq + Lr:].contiguous(), pos, self.cos_sin, 1, dr)
+    qpe = A.rope(q[:, H * dn:].contiguous(), pos, self.cos_sin, H, dr)
+    kv = self._mm(cn, f"{i}.kvb").view(T, H, dn + dv)
+    qf = torch.cat([q[:, :H * dn].reshape(T, H, dn), qpe.view(T, H, dr)], -1)
+    kf = torch.cat([kv[..., :dn], kpe.view(T, 1, dr).expand(T, H, dr)], -1)
+    vf = kv[..., dn:]
+
+    def heads(t):
+      return t.reshape(B, L, H, -1).transpose(1, 2)
+    o = F.scaled_dot_product_attention(heads(qf), heads(kf), heads(vf), is_causal=True, scale=c.attn_scale())
+    return o.transpose(1, 2).reshape(T, H * dv)
+
+  def _route(self, logits: torch.Tensor, i: int):
+    """(weights [T, k] with autograd to the router, expert ids [T, k]): Mixtral softmax top-k renormalised,
+    or DeepSeek's rule (ops.reference.moe_route_ds: groups, sigmoid scores + selection bias, scale)."""
+    c = self.c
+    ds = not (c.topk_method == "greedy" and c.scoring_func == "softmax" and c.norm_topk_prob
+              and c.routed_scaling_factor == 1.0)
+    if not ds:
+      topw, topi = torch.topk(torch.softmax(logits, dim=-1), c.num_experts_per_tok, dim=-1)
+      return topw / topw.sum(-1, keepdim=True), topi
+    from ..ops.reference import moe_route_ds
+    method = {"greedy": 0, "group_limited_greedy": 1, "noaux_tc": 2}[c.topk_method]
+    with torch.no_grad():  # the selection itself is not differentiable
+      _, topi = moe_route_ds(logits.detach(), self.router_bias.get(i), c.num_experts_per_tok,
+                             c.n_group if method else 1, c.topk_group if method else 1, method,
+                             c.scoring_func == "sigmoid", c.norm_topk_prob, c.routed_scaling_factor)
+    scores = torch.sigmoid(logits) if c.scoring_func == "sigmoid" else torch.softmax(logits, dim=-1)
+    topw = scores.gather(1, topi)
+    if c.norm_topk_prob:
+      topw = topw / (topw.sum(-1, keepdim=True) + 1e-20)
+    return topw * c.routed_scaling_factor, topi
+
   def _moe(self, xn: torch.Tensor, i: int) -> torch.Tensor:
-    """Mixtral sparse MLP with autograd: fp32 router softmax, top-k renormalised weights (the router
-    learns through them), each expert's gate/up -> SiLU*mul -> down on the rows routed to it, weighted
-    fp32 scatter-add.  Same routing as the inference path (models/transformer.py `_moe`)."""
+    """Sparse MLP with autograd: fp32 router scores, top-k weights (the router learns through them; Mixtral
+    renormalised softmax or DeepSeek's routing), each expert's gate/up -> SiLU*mul -> down on the rows
+    routed to it, weighted fp32 scatter-add, plus DeepSeek's shared experts.  Same routing as the
+    inference path (models/transformer.py `_moe`)."""
     c, P = self.c, self.params
     logits = xn.float() @ P[f"{i}.router"].float().t()  # [T, E]
-    topw, topi = torch.topk(torch.softmax(logits, dim=-1), c.num_experts_per_tok, dim=-1)
-    topw = topw / topw.sum(-1, keepdim=True)
+    topw, topi = self._route(logits, i)
     # per-expert views, taken once per layer: indexing egu[e] per expert would zero-fill and add a full
     # [E, 2F, D] gradient for every expert; on the GPU the routed experts' grads go straight into the
     # stack's accumulation buffer (A.StackAccFn)
@@ -152,6 +215,8 @@ class ShardTrainer:
       start += n
     y = torch.cat(ys).float() * topw.reshape(-1)[order].unsqueeze(1)
     out = torch.zeros(xn.shape[0], c.hidden_size, device=xn.device, dtype=torch.float32).index_add(0, tok, y)
+    if f"{i}.sh_gu" in P:
+      out = out + self._mm(A.silu_mul(self._mm(xn, f"{i}.sh_gu").contiguous()), f"{i}.sh_down").float()
     return out.to(xn.dtype)
 
   def _mm(self, x: torch.Tensor, name: str, h: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -294,18 +359,33 @@ class ShardTrainer:
       return
     from ..models.weights import assign_weight
     P = self.params
-    Fd = self.c.intermediate_size
+    c = self.c
+    Fd = c.intermediate_size
     for i, lw in self.w.layers.items():
       assign_weight(lw.qkv_w, P[f"{i}.qkv"].detach())
       if f"{i}.qkv_b" in P:
         assign_weight(lw.qkv_b, P[f"{i}.qkv_b"].detach())
       assign_weight(lw.o_w, P[f"{i}.o"].detach())
-      if self.c.is_moe:
+      if c.is_mla:
+        if c.q_lora_rank:
+          assign_weight(lw.q_ln, P[f"{i}.q_ln"].detach())
+          assign_weight(lw.qb_w, P[f"{i}.qb"].detach())
+        assign_weight(lw.kv_ln, P[f"{i}.kv_ln"].detach())
+        kvb = P[f"{i}.kvb"].detach().view(c.num_heads, c.qk_nope_head_dim + c.v_head_dim, c.kv_lora_rank)
+        assign_weight(lw.wuk, kvb[:, :c.qk_nope_head_dim].contiguous())
+        assign_weight(lw.wuv, kvb[:, c.qk_nope_head_dim:].contiguous())
+      if f"{i}.router" in P:
+        Fe = c.expert_dim
         egu = P[f"{i}.egu"].detach()
-        assign_weight(lw.gu_w, torch.stack([interleave_gate_up(egu[e, :Fd].contiguous(), egu[e, Fd:].contiguous())
+        assign_weight(lw.gu_w, torch.stack([interleave_gate_up(egu[e, :Fe].contiguous(), egu[e, Fe:].contiguous())
                                             for e in range(egu.shape[0])]))
         assign_weight(lw.down_w, P[f"{i}.edown"].detach())
         assign_weight(lw.router, P[f"{i}.router"].detach())
+        if f"{i}.sh_gu" in P:
+          sgu = P[f"{i}.sh_gu"].detach()
+          Fs = sgu.shape[0] // 2
+          assign_weight(lw.sh_gu_w, interleave_gate_up(sgu[:Fs].contiguous(), sgu[Fs:].contiguous()))
+          assign_weight(lw.sh_down_w, P[f"{i}.sh_down"].detach())
       else:
         gu = P[f"{i}.gu"].detach()
         assign_weight(lw.gu_w, interleave_gate_up(gu[:Fd].contiguous(), gu[Fd:].contiguous()))
