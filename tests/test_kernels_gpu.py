@@ -574,10 +574,14 @@ def _mla_cache(num_pages, DL, DR, dev, seed=0):
   return torch.randn(num_pages, 64, DL + DR, device=dev, dtype=torch.bfloat16, generator=g)
 
 
+@pytest.mark.parametrize("wide", ["0", "1"])
 @pytest.mark.parametrize("DL", [512, 256])
-@pytest.mark.parametrize("H", [16, 4, 128])
+@pytest.mark.parametrize("H", [16, 4, 40, 128, 200])
 @pytest.mark.parametrize("ctxs", [[1, 64, 65, 300], [1000]])
-def test_mla_attn_decode(gpu, DL, H, ctxs):
+def test_mla_attn_decode(gpu, DL, H, ctxs, wide, monkeypatch):
+  """Narrow (16 heads per workgroup) and many-head (up to 128 heads per workgroup, 1 to 8 waves, several
+  head groups past 128) kernels, one partition and split-KV + combine."""
+  monkeypatch.setenv("XOT_MLA_WIDE", wide)
   torch.manual_seed(0)
   DR, B = 64, len(ctxs)
   width = max(-(-c // 64) for c in ctxs)
@@ -596,10 +600,12 @@ def test_mla_attn_decode(gpu, DL, H, ctxs):
     assert rel_err(out.cpu(), ref) < 2e-2, (DL, H, ctxs)
 
 
+@pytest.mark.parametrize("wide,H", [("0", 16), ("1", 16), ("1", 128)])
 @pytest.mark.parametrize("DL", [512, 256])
-def test_mla_attn_prefill_causal(gpu, DL):
+def test_mla_attn_prefill_causal(gpu, DL, wide, H, monkeypatch):
+  monkeypatch.setenv("XOT_MLA_WIDE", wide)
   torch.manual_seed(1)
-  DR, H = 64, 16
+  DR = 64
   qlens, ctxs = [37, 1, 130], [37, 70, 200]  # second / third: chunked prefill on top of a cached prefix
   B = len(qlens)
   width = max(-(-c // 64) for c in ctxs)

@@ -474,7 +474,7 @@ void mla_prep(const at::Tensor& ckv, const at::Tensor& kv_ln, at::Tensor& q, int
 // q_lat / out [H, T, DL]; q_pe rows of q (row stride ldqpe = q_pe.stride(0)) as [T, H * DR]
 void mla_attn(const at::Tensor& q_lat, const at::Tensor& q_pe, const at::Tensor& cache, const at::Tensor& block_tables,
               const at::Tensor& cu_q, const at::Tensor& ctx_lens, at::Tensor& out, at::Tensor& ws_o, at::Tensor& ws_ml,
-              int64_t pages_per_part, int64_t nparts, double scale) {
+              int64_t pages_per_part, int64_t nparts, double scale, int64_t wide) {
   CHECK_BF16(q_lat);
   CHECK_BF16(q_pe);
   CHECK_BF16(cache);
@@ -497,7 +497,7 @@ void mla_attn(const at::Tensor& q_lat, const at::Tensor& q_pe, const at::Tensor&
                                       block_tables.data_ptr<int>(), (int)block_tables.size(1), cu_q.data_ptr<int>(),
                                       ctx_lens.data_ptr<int>(), (int)B, (int)T, (int)H, (int)DL, (int)DR, bf(out),
                                       ws_o.data_ptr<float>(), ws_ml.data_ptr<float>(), (int)pages_per_part,
-                                      (int)nparts, (float)scale, (int)cache.size(0), cur_stream());
+                                      (int)nparts, (float)scale, (int)cache.size(0), (int)wide, cur_stream());
   XCHECK(rc == 0, "mla_attn: unsupported DL=", DL, " DR=", DR);
 }
 
@@ -776,7 +776,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("moe_route", &moe_route);
   m.def("moe_route_ds", &moe_route_ds);
   m.def("mla_prep", &mla_prep);
-  m.def("mla_attn", &mla_attn);
+  m.def("mla_attn", &mla_attn, py::arg("q_lat"), py::arg("q_pe"), py::arg("cache"), py::arg("block_tables"),
+        py::arg("cu_q"), py::arg("ctx_lens"), py::arg("out"), py::arg("ws_o"), py::arg("ws_ml"), py::arg("pages_per_part"),
+        py::arg("nparts"), py::arg("scale"), py::arg("wide") = 0);
   m.def("moe_combine", &moe_combine, py::arg("y"), py::arg("slot_of"), py::arg("topw"), py::arg("h"),
         py::arg("splits") = 1);
   m.def("attn_decode", &attn_decode, py::arg("q"), py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"),

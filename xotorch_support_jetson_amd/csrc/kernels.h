@@ -70,7 +70,7 @@ void launch_mla_prep(const uint16_t* ckv, long ldc, const uint16_t* kv_ln, uint1
 int launch_mla_attn(const uint16_t* q_lat, const uint16_t* q_pe, long ldqpe, const uint16_t* cache,
                     const int32_t* block_tables, int max_blocks, const int32_t* cu_q, const int32_t* ctx_lens, int B,
                     int T, int H, int DL, int DR, uint16_t* out, float* ws_o, float* ws_ml, int pages_per_part,
-                    int nparts, float scale, int num_pages, hipStream_t s);
+                    int nparts, float scale, int num_pages, int wide, hipStream_t s);
 int launch_gemm_tiled(const uint16_t* X, int ldx, const uint16_t* W, int ldw, const uint16_t* bias,
                       const uint16_t* R, int ldr, void* Y, int ldy, bool out_f32, int epi, int M, int N, int K,
                       hipStream_t s);

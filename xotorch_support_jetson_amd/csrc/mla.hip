@@ -12,7 +12,7 @@
 //   o[h]     = o_lat[h] . W_UV[h]^T                      (host side: batched GEMM)
 // so attention is multi-query over one 576-wide key / 512-wide value shared by every head.
 //
-// Kernel: one workgroup (4 waves) per (query token, 16-head block, KV partition).  Each 64-key page is
+// Kernel: one workgroup (4 waves) per (query token, 16-head block, KV partition), XCD-aware order.  Each 64-key page is
 // copied HBM -> LDS once by LDS-DMA (double-buffered: page p+1 is in flight while page p is consumed) and
 // used twice: as K (S^T = K . Q^T, A operand rows = keys read by ds_read_b128, one 16-key tile per wave)
 // and as V (O^T += V^T . P^T, A operand = V^T read straight from the row-major image by the gfx950
@@ -141,7 +141,20 @@ __global__ __launch_bounds__(256, 1) void mla_attn_kernel(
   uint16_t* pbuf = smem + 2 * PAGE * ROW;        // [16 heads][PLD] bf16
   float* red = reinterpret_cast<float*>(pbuf + 16 * PLD);  // [4 waves][16 heads]
 
-  const int part = blockIdx.x, hb = blockIdx.y, t = blockIdx.z;
+  // XCD-aware order: the head blocks of one (token, partition) read the same latent pages, so they get
+  // consecutive logical ids that round-robin dispatch places on ONE XCD (one HBM read, the rest from
+  // that XCD's L2) instead of spreading them over all 8 L2s (measured 8x the cache bytes from HBM).
+  int part, hb, t;
+  {
+    const int nwg = gridDim.x * gridDim.y * gridDim.z;
+    int b = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    const int xcd = b & 7, q = nwg >> 3, r = nwg & 7;
+    b = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+    hb = b % gridDim.y;
+    b /= gridDim.y;
+    part = b % gridDim.x;
+    t = b / gridDim.x;
+  }
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, c = lane & 15;
   const int h = hb * 16 + c;
@@ -281,6 +294,188 @@ __global__ __launch_bounds__(256, 1) void mla_attn_kernel(
   }
 }
 
+// Many-head variant (DeepSeek-V3 / R1: 128 heads): one workgroup of NW <= 8 waves per (query token, KV
+// partition, 16 NW heads).  Every wave owns one 16-head block and does all the page's work for it (S^T of
+// all 64 keys, O^T of all DL dims), so a 72 KB page goes HBM -> LDS once for 128 heads instead of once per
+// 16-head workgroup (the narrow kernel above: 8x the load traffic, one latency-bound workgroup per CU).
+// The four S^T tiles take their K rows in the order key(tile 2kk + hf, row 4g' + r) = 32kk + 8g' + 4hf + r,
+// so lane (c, g) ends up with keys 32kk + 8g .. +7 of head c: exactly its P^T B-operand fragment for
+// O^T += V^T . P^T -- no LDS exchange, no cross-wave reduction; the page max is two lane shuffles.
+template <int DL>
+__global__ __launch_bounds__(512, 1) void mla_attn_wide_kernel(
+    const uint16_t* __restrict__ q_lat, const uint16_t* __restrict__ q_pe, long ldqpe,
+    const uint16_t* __restrict__ cache, const int32_t* __restrict__ block_tables, int max_blocks,
+    const int32_t* __restrict__ cu_q, const int32_t* __restrict__ ctx_lens, int B, int T, int H,
+    uint16_t* __restrict__ out, float* __restrict__ ws_o, float* __restrict__ ws_ml, int pages_per_part, int nparts,
+    float scale_log2, int num_pages) {
+  constexpr int DR = 64;
+  constexpr int ROW = DL + DR;
+  constexpr int KS = ROW / 32;
+  constexpr int NCH = PAGE * ROW * 2 / 1024;  // 1 KB LDS-DMA chunks per page
+  constexpr int NDT = DL / 16;
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+
+  const int nw = blockDim.x >> 6;
+  int part, hg, t;
+  {  // XCD-aware order (as the narrow kernel): the partitions of one token stay on one XCD
+    const int nwg = gridDim.x * gridDim.y * gridDim.z;
+    int b = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    const int xcd = b & 7, q = nwg >> 3, r = nwg & 7;
+    b = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+    part = b % gridDim.x;
+    b /= gridDim.x;
+    hg = b % gridDim.y;
+    t = b / gridDim.y;
+  }
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, c = lane & 15;
+  const int h = (hg * nw + wave) * 16 + c;
+  const bool hv = h < H;
+
+  int lo = 0, hi = B - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (cu_q[mid] <= t) lo = mid;
+    else hi = mid - 1;
+  }
+  const int b = lo;
+  const int nkeys = min(ctx_lens[b] - (cu_q[b + 1] - 1 - t), max_blocks * PAGE);
+  const int npages = nkeys > 0 ? (nkeys + PAGE - 1) / PAGE : 0;
+  const int p_begin = part * pages_per_part;
+  const int p_end = min(npages, p_begin + pages_per_part);
+  const int np = max(0, p_end - p_begin);
+
+  s16x8 qf[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const int d = 32 * s + 8 * g;
+    s16x8 x = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    if (hv) x = d < DL ? ld16(q_lat + ((size_t)h * T + t) * DL + d) : ld16(q_pe + (size_t)t * ldqpe + (size_t)h * DR + (d - DL));
+    qf[s] = x;
+  }
+  float m = NEG_BIG, l = 0.f;
+  f32x4 o[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int32_t* bt = block_tables + (size_t)b * max_blocks;
+  // LDS image of a page: row r keeps its 16-byte granule j at slot j ^ swz(r) (within its group of 8).  The
+  // row stride (ROW * 2 bytes) is an odd multiple of 128 bytes, so the bank half follows the row parity and
+  // swz spreads the rest: the 16 rows of a K read (rows 8a + b, one granule) and the 16 rows x 4 lanes of a
+  // transposed V read (8g + q4) hit disjoint banks (the plain layout put 8 lanes on each bank).  LDS-DMA
+  // writes linearly, so the permutation is applied through each lane's source address.
+  auto swz = [](int r) { return ((r >> 4) & 1) | (((r >> 3) & 1) << 1) | (((r >> 1) & 1) << 2); };
+  constexpr int GPR = ROW / 8;  // granules per row
+  auto issue = [&](int pi, int buf) {
+    const long page = min(max(bt[p_begin + pi], 0), num_pages - 1);
+    const uint16_t* src = cache + (size_t)page * PAGE * ROW;
+    uint16_t* dst = smem + buf * PAGE * ROW;
+    for (int ch = wave; ch < NCH; ch += nw) {
+      const int P = ch * 64 + lane, r = P / GPR, j = (P - r * GPR) ^ swz(r);
+      glds16(src + (r * GPR + j) * 8, dst + ch * 512);
+    }
+  };
+  // K row of S^T tile j (= 2 kk + hf) for MFMA row c: key 32 kk + 8 (c / 4) + 4 hf + c % 4; its k-step s
+  // granule 4 s + g sits at slot (4 s + g) ^ swz = 4 (s ^ xb) + xl with x = g ^ swz
+  int kb[4][2];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int r = 32 * (j >> 1) + 8 * (c >> 2) + 4 * (j & 1) + (c & 3);
+    const int x = g ^ swz(r), xb = x >> 2, xl = x & 3;
+    kb[j][0] = r * ROW + 8 * xl + 32 * xb;  // even s: s ^ xb = s + xb
+    kb[j][1] = r * ROW + 8 * xl - 32 * xb;  // odd s: s ^ xb = s - xb
+  }
+  // V^T transposed reads: lane 4 q4 + p4 of group g reads row 32 kk + 8 g + q4 (+4), dims 16 dt + 4 p4 .. +3,
+  // i.e. granule 2 dt + p4 / 2 at slot 2 dt ^ y (y = p4 / 2 ^ swz), element 4 (p4 & 1) inside it
+  const int q4 = c >> 2, p4 = c & 3;
+  int vb[4];
+  {
+    const int r = 8 * g + q4, y = (p4 >> 1) ^ swz(r), y1 = y >> 1;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) vb[v] = r * ROW + 16 * (v ^ y1) + 8 * (y & 1) + 4 * (p4 & 1);
+  }
+
+  if (np > 0) issue(0, 0);
+  for (int pi = 0; pi < np; ++pi) {
+    const int buf = pi & 1;
+    wait_vm<0>();   // this wave's share of page pi has landed
+    lds_barrier();  // ... everyone's, and every wave is done with page pi - 1 (the buffer refilled next)
+    if (pi + 1 < np) issue(pi + 1, buf ^ 1);
+    const uint16_t* Ks = smem + buf * PAGE * ROW;
+
+    f32x4 st[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) st[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) st[j] = mfma16(ld16(Ks + kb[j][s & 1] + 32 * s), qf[s], st[j]);
+    const int kbase = (p_begin + pi) * PAGE + 8 * g;
+    float mt = NEG_BIG;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = kbase + 32 * (j >> 1) + 4 * (j & 1) + r;
+        st[j][r] = key < nkeys ? st[j][r] * scale_log2 : -INFINITY;
+        mt = fmaxf(mt, st[j][r]);
+      }
+    mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    const float mn = fmaxf(m, mt);
+    const float alpha = exp2f(m - mn);
+    m = mn;
+    s16x8 pf[2];
+    float ls = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const uint16_t pb = f2bf(exp2f(st[2 * kk + (e >> 2)][e & 3] - m));
+        pf[kk][e] = (short)pb;
+        ls += bf2f(pb);
+      }
+    ls += __shfl_xor(ls, 16, 64);
+    ls += __shfl_xor(ls, 32, 64);
+    l = l * alpha + ls;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[dt][r] *= alpha;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const uint16_t* base = Ks + vb[dt & 3] + 32 * kk * ROW + 64 * (dt >> 2);
+        const s16x4 lo4 = tr_read(base), hi4 = tr_read(base + 4 * ROW);
+        const s16x8 vf = s16x8{lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
+        o[dt] = mfma16(vf, pf[kk], o[dt]);
+      }
+    }
+  }
+
+  // o[dt][r] = O[head c][dim 16 dt + 4 g + r]
+  if (!hv) return;
+  if (nparts == 1) {
+    const float il = l > 0.f ? 1.f / l : 0.f;
+    uint16_t* op = out + ((size_t)h * T + t) * DL + 4 * g;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) {
+      s16x4 v;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = (short)f2bf(o[dt][r] * il);
+      *reinterpret_cast<s16x4*>(op + 16 * dt) = v;
+    }
+  } else {
+    const size_t idx = ((size_t)t * H + h) * nparts + part;
+    float* op = ws_o + idx * DL + 4 * g;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) *reinterpret_cast<f32x4*>(op + 16 * dt) = o[dt];
+    if (g == 0) {
+      ws_ml[idx * 2] = m;
+      ws_ml[idx * 2 + 1] = l;
+    }
+  }
+}
+
 // merge the split-KV partials of (token, head): out[h][t][:] = sum_p O_p 2^(m_p - M) / sum_p l_p 2^(m_p - M)
 __global__ __launch_bounds__(256) void mla_combine_kernel(const float* __restrict__ ws_o, const float* __restrict__ ws_ml,
                                                           uint16_t* __restrict__ out, int T, int H, int DL, int nparts) {
@@ -302,32 +497,46 @@ template <int DL>
 static void mla_launch(const uint16_t* q_lat, const uint16_t* q_pe, long ldqpe, const uint16_t* cache,
                        const int32_t* bt, int max_blocks, const int32_t* cu_q, const int32_t* ctx, int B, int T, int H,
                        uint16_t* out, float* ws_o, float* ws_ml, int ppp, int nparts, float scale, int num_pages,
-                       hipStream_t s) {
+                       int wide, hipStream_t s) {
   constexpr int ROW = DL + 64;
-  constexpr int SMEM = 2 * PAGE * ROW * 2 + 16 * (PAGE + 8) * 2 + 4 * 16 * 4;
-  static_assert(SMEM <= 160 * 1024, "LDS");
-  auto kern = mla_attn_kernel<DL>;
-  static bool attr = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM) ==
-                     hipSuccess;
-  (void)attr;
-  const dim3 grid(nparts, (H + 15) / 16, T);
-  kern<<<grid, 256, SMEM, s>>>(q_lat, q_pe, ldqpe, cache, bt, max_blocks, cu_q, ctx, B, T, H, out, ws_o, ws_ml, ppp,
-                               nparts, scale * LOG2E, num_pages);
+  const int nhb = (H + 15) / 16;
+  if (wide) {
+    constexpr int SMEM = 2 * PAGE * ROW * 2;
+    static_assert(SMEM <= 160 * 1024, "LDS");
+    auto kern = mla_attn_wide_kernel<DL>;
+    static bool attr = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM) ==
+                       hipSuccess;
+    (void)attr;
+    const int nw = nhb < 8 ? nhb : 8;
+    const dim3 grid(nparts, (nhb + nw - 1) / nw, T);
+    kern<<<grid, 64 * nw, SMEM, s>>>(q_lat, q_pe, ldqpe, cache, bt, max_blocks, cu_q, ctx, B, T, H, out, ws_o, ws_ml,
+                                     ppp, nparts, scale * LOG2E, num_pages);
+  } else {
+    constexpr int SMEM = 2 * PAGE * ROW * 2 + 16 * (PAGE + 8) * 2 + 4 * 16 * 4;
+    static_assert(SMEM <= 160 * 1024, "LDS");
+    auto kern = mla_attn_kernel<DL>;
+    static bool attr = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM) ==
+                       hipSuccess;
+    (void)attr;
+    const dim3 grid(nparts, nhb, T);
+    kern<<<grid, 256, SMEM, s>>>(q_lat, q_pe, ldqpe, cache, bt, max_blocks, cu_q, ctx, B, T, H, out, ws_o, ws_ml, ppp,
+                                 nparts, scale * LOG2E, num_pages);
+  }
   if (nparts > 1) mla_combine_kernel<<<T * H, 256, 0, s>>>(ws_o, ws_ml, out, T, H, DL, nparts);
 }
 
 int launch_mla_attn(const uint16_t* q_lat, const uint16_t* q_pe, long ldqpe, const uint16_t* cache,
                     const int32_t* block_tables, int max_blocks, const int32_t* cu_q, const int32_t* ctx_lens, int B,
                     int T, int H, int DL, int DR, uint16_t* out, float* ws_o, float* ws_ml, int pages_per_part,
-                    int nparts, float scale, int num_pages, hipStream_t s) {
+                    int nparts, float scale, int num_pages, int wide, hipStream_t s) {
   if (T <= 0) return 0;
   if (DR != 64 || B < 1 || pages_per_part < 1 || nparts < 1) return -1;
   if (nparts > 1 && (ws_o == nullptr || ws_ml == nullptr)) return -1;
   switch (DL) {
     case 512: mla_launch<512>(q_lat, q_pe, ldqpe, cache, block_tables, max_blocks, cu_q, ctx_lens, B, T, H, out, ws_o,
-                              ws_ml, pages_per_part, nparts, scale, num_pages, s); return 0;
+                              ws_ml, pages_per_part, nparts, scale, num_pages, wide, s); return 0;
     case 256: mla_launch<256>(q_lat, q_pe, ldqpe, cache, block_tables, max_blocks, cu_q, ctx_lens, B, T, H, out, ws_o,
-                              ws_ml, pages_per_part, nparts, scale, num_pages, s); return 0;
+                              ws_ml, pages_per_part, nparts, scale, num_pages, wide, s); return 0;
     default: return -1;
   }
 }

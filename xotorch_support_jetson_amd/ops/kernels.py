@@ -307,19 +307,31 @@ class MLAWorkspace:
   def __init__(self, max_tokens: int, H: int, DL: int, max_ctx: int, device):
     self.max_tokens, self.H, self.DL = max_tokens, H, DL
     self.pages = max(1, -(-max_ctx // PAGE))
-    self.max_parts = self.partition(1, self.pages)[1]
+    self.max_parts = max(self.partition(1, self.pages)[1], self.partition(8, self.pages)[1])
     units = max(max_tokens * self.max_parts, 1)
     self.o = torch.empty(units * H * DL, dtype=torch.float32, device=device)
     self.ml = torch.empty(units * H * 2, dtype=torch.float32, device=device)
 
+  def wide(self, T: int) -> bool:
+    """Many-head kernel (one workgroup covers up to 128 heads, each page loaded once for all of them) for
+    >= 64 heads at batch sizes that fill the chip; the narrow kernel (a workgroup per 16 heads) keeps more
+    workgroups in flight for a handful of tokens.  XOT_MLA_WIDE=0/1 forces either."""
+    force = os.environ.get("XOT_MLA_WIDE")
+    if force in ("0", "1"):
+      return force == "1"
+    return self.H >= 64 and T >= 8
+
   def partition(self, T: int, width_pages: int):
-    """(pages per partition, partitions): enough workgroups for 256 CUs (one per CU: the kernel holds two
-    73 KB pages in LDS), partitions of at least 2 pages."""
+    """(pages per partition, partitions, wide): enough workgroups for 256 CUs (one per CU: the kernels
+    hold two 73 KB pages in LDS); narrow-kernel partitions of at least 2 pages."""
     nhb = -(-self.H // 16)
-    want = max(1, -(-256 // max(T * nhb, 1)))
-    nparts = max(1, min(want, width_pages // 2 if width_pages >= 2 else 1))
+    wide = self.wide(T)
+    units = T * -(-nhb // 8) if wide else T * nhb
+    want = max(1, -(-256 // max(units, 1)))
+    cap = width_pages if wide else (width_pages // 2 if width_pages >= 2 else 1)
+    nparts = max(1, min(want, cap))
     ppp = -(-width_pages // nparts)
-    return ppp, -(-width_pages // ppp)
+    return ppp, -(-width_pages // ppp), wide
 
 
 def mla_attn(q_lat, q_pe, cache, block_tables, cu_q, ctx_lens, scale: float, ws: MLAWorkspace | None = None,
@@ -335,12 +347,12 @@ def mla_attn(q_lat, q_pe, cache, block_tables, cu_q, ctx_lens, scale: float, ws:
   width = block_tables.shape[1]
   if ws is None:
     ws = MLAWorkspace(T, H, DL, width * PAGE, q_lat.device)
-  ppp, nparts = ws.partition(T, width)
+  ppp, nparts, wide = ws.partition(T, width)
   if T * nparts > ws.max_tokens * ws.max_parts:
     ppp, nparts = width, 1
   out = torch.empty_like(q_lat) if out is None else out
   require().mla_attn(q_lat, q_pe, cache, block_tables, cu_q, ctx_lens, out, ws.o, ws.ml, int(ppp), int(nparts),
-                     float(scale))
+                     float(scale), int(wide))
   return out
 
 
