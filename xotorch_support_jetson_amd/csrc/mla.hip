@@ -361,10 +361,12 @@ __global__ __launch_bounds__(512, 1) void mla_attn_wide_kernel(
   const int32_t* bt = block_tables + (size_t)b * max_blocks;
   // LDS image of a page: row r keeps its 16-byte granule j at slot j ^ swz(r) (within its group of 8).  The
   // row stride (ROW * 2 bytes) is an odd multiple of 128 bytes, so the bank half follows the row parity and
-  // swz spreads the rest: the 16 rows of a K read (rows 8a + b, one granule) and the 16 rows x 4 lanes of a
-  // transposed V read (8g + q4) hit disjoint banks (the plain layout put 8 lanes on each bank).  LDS-DMA
-  // writes linearly, so the permutation is applied through each lane's source address.
-  auto swz = [](int r) { return ((r >> 4) & 1) | (((r >> 3) & 1) << 1) | (((r >> 1) & 1) << 2); };
+  // swz spreads the rest.  swz was found by exhaustive search over XOR maps of the row bits against the
+  // ds_read_b128 lane groups ({0-3,12-15,20-27}, {4-11,16-19,28-31}, ...) and the two 32-lane halves of
+  // ds_read_b64_tr_b16: both the K row reads (4 LDS cycles) and the transposed V reads (2) are
+  // conflict-free (the plain layout: 16 and 8).  LDS-DMA writes linearly, so the permutation is applied
+  // through each lane's source address.
+  auto swz = [](int r) { return (((r >> 1) & 1) << 1) | (((r >> 3) & 1) << 2); };
   constexpr int GPR = ROW / 8;  // granules per row
   auto issue = [&](int pi, int buf) {
     const long page = min(max(bt[p_begin + pi], 0), num_pages - 1);
