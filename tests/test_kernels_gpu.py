@@ -177,12 +177,17 @@ def test_attn_decode(gpu, H, Hkv, Dh, ctx):
       assert torch.equal(again, out) and rel_err(red, out) < 1e-3, (algo, ppp)
 
 
-@pytest.mark.parametrize("H,Hkv,Dh", [(32, 8, 64), (64, 8, 128), (14, 2, 64)])
-def test_attn_prefill(gpu, H, Hkv, Dh):
+@pytest.mark.parametrize("algo", [1, 2])
+@pytest.mark.parametrize("H,Hkv,Dh", [(32, 8, 64), (64, 8, 128), (14, 2, 64), (8, 8, 128), (32, 8, 128)])
+@pytest.mark.parametrize("lens", [([5, 130, 1, 77], [5, 200, 64, 77]), ([300, 1000, 64], [300, 1100, 1000])])
+def test_attn_prefill(gpu, H, Hkv, Dh, lens, algo, monkeypatch):
+  """Causal varlen prefill from the paged cache, fresh prompts and chunks on top of a cached prefix; the
+  second case spans several 256-row tiles per sequence (heaviest-first order, waves past the causal edge)."""
+  monkeypatch.setattr(K, "PREFILL_ALGO", algo)
   torch.manual_seed(0)
-  qlens, ctxs = [5, 130, 1, 77], [5, 200, 64, 77]
+  qlens, ctxs = lens
   B = len(qlens)
-  maxb = 8
+  maxb = max(-(-c // 64) for c in ctxs) + 1
   kc, vc = _make_cache(B * maxb, Hkv, Dh, gpu)
   bt = torch.randperm(B * maxb, device=gpu).view(B, maxb).to(torch.int32).contiguous()
   cu = torch.tensor([0] + list(torch.tensor(qlens).cumsum(0)), device=gpu, dtype=torch.int32)

@@ -615,14 +615,290 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------- prefill v2
+// One workgroup = 8 waves = 256 rows (token, head-in-group) of one (sequence, KV head); each wave owns two
+// 16-row blocks, so every K / V^T fragment read from LDS feeds two MFMAs.  Transposed formulation as the
+// decode wave kernel: S^T = K . Q^T (A = 16 keys of the page, B = Q^T held in registers), so a lane's
+// accumulator column is one query row and the online softmax is lane-local except for the two lane-group
+// shuffles of the page max; the S^T tile rows take keys in the order 32 kk + 8 (c / 4) + 4 hf + c % 4, so
+// the probabilities come out already in the B-operand layout of O^T += V^T . P^T (no LDS round trip for P).
+// K and V^T pages (16 KB each at Dh 128) arrive by LDS-DMA into a 2-deep ring, XOR-swizzled per row
+// through the per-lane source address (swizzles found by exhaustive search against the ds_read_b128 lane
+// groups: every fragment read is conflict-free).  Waves skip the math of pages past their last row's
+// position (causal); workgroups are dispatched heaviest tile first, the tiles of one (sequence, KV head)
+// kept on one XCD.
+template <int DH>
+__device__ __forceinline__ int pf_kswz(int r) {
+  return DH == 128 ? (3 * (r & 1)) | (((r >> 1) & 1) << 2) | (((r >> 3) & 1) << 3)
+                   : (r & 1) | (((r >> 1) & 1) << 1) | (((r >> 3) & 1) << 2);
+}
+
+template <int DH>
+__global__ __launch_bounds__(512, 1) void attn_prefill_v2_kernel(
+    const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
+    const int32_t* __restrict__ block_tables, int max_blocks, const int32_t* __restrict__ cu_q,
+    const int32_t* __restrict__ ctx_lens, uint16_t* __restrict__ out, int H, int Hkv, float scale_log2,
+    int num_pages) {
+  constexpr int KS = DH / 32, NDT = DH / 16;
+  constexpr int KGPR = DH / 8;                 // 16-B granules per K row
+  constexpr int PAGE_EL = PAGE * DH;           // elements of one K (or V^T) page
+  constexpr int NCH = 2 * PAGE_EL / 512;       // 1 KB LDS-DMA chunks per page (K then V^T)
+  static_assert(NCH % 8 == 0, "chunks split over 8 waves");
+  constexpr int CPW = NCH / 8;
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];  // [3][K page | V^T page]
+
+  int tile, kvh, b;
+  {
+    const int nwg = gridDim.x * gridDim.y * gridDim.z;
+    int lin = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    const int xcd = lin & 7, qq = nwg >> 3, rr = nwg & 7;
+    lin = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (lin >> 3);
+    tile = gridDim.x - 1 - lin % gridDim.x;  // heaviest (latest rows) first
+    lin /= gridDim.x;
+    kvh = lin % gridDim.y;
+    b = lin / gridDim.y;
+  }
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, c = lane & 15;
+  const int G = H / Hkv;
+  const int q0 = cu_q[b], qlen = cu_q[b + 1] - q0;
+  const int nrows = qlen * G;
+  const int row0 = tile * 256;
+  if (row0 >= nrows) return;  // whole workgroup exits together
+  const int ctx = min(ctx_lens[b], max_blocks * PAGE);
+  const int pos0 = ctx - qlen;
+
+  // Q^T fragments (B operand: k = dims, n = rows): lane (g, c) holds row c of block blk, dims 32 s + 8 g .. +8
+  s16x8 qf[2][KS];
+  int qpos[2];
+#pragma unroll
+  for (int blk = 0; blk < 2; ++blk) {
+    const int row = row0 + 32 * wave + 16 * blk + c;
+    const bool ok = row < nrows;
+    const int ti = ok ? row / G : 0, hi = ok ? row % G : 0;
+    qpos[blk] = ok ? pos0 + ti : -1;
+    const uint16_t* qp = q + ((size_t)(q0 + ti) * H + kvh * G + hi) * DH + 8 * g;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const s16x8 v = ld16(qp + 32 * s);
+      qf[blk][s] = ok ? v : s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  }
+  const int last_row = min(nrows, row0 + 256) - 1;
+  const int npages = min((pos0 + last_row / G) / PAGE + 1, max_blocks);
+  const int wlast = min(nrows - 1, row0 + 32 * wave + 31);
+  const int wmax = wlast >= row0 + 32 * wave ? pos0 + wlast / G : -1;  // this wave's last key (causal)
+  const int wmin = pos0 + (row0 + 32 * wave) / G;                          // ... and its first row's
+
+  float m[2] = {NEG_BIG, NEG_BIG}, l[2] = {0.f, 0.f};
+  f32x4 o[2][NDT];
+#pragma unroll
+  for (int blk = 0; blk < 2; ++blk)
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) o[blk][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int32_t* bt = block_tables + (size_t)b * max_blocks;
+  auto issue = [&](int p, int buf) {
+    const long page = min(max(bt[p], 0), num_pages - 1);
+    const uint16_t* kb = kc + ((size_t)page * Hkv + kvh) * PAGE_EL;
+    const uint16_t* vb = vc + ((size_t)page * Hkv + kvh) * PAGE_EL;
+    uint16_t* dst = smem + buf * 2 * PAGE_EL;
+#pragma unroll
+    for (int i = 0; i < CPW; ++i) {
+      const int ch = wave * CPW + i;
+      int P = (ch % (NCH / 2)) * 64 + lane;  // granule of the K or V^T image
+      const uint16_t* src;
+      if (ch < NCH / 2) {
+        const int r = P / KGPR, j = (P % KGPR) ^ pf_kswz<DH>(r);
+        src = kb + (r * KGPR + j) * 8;
+      } else {
+        const int r = P >> 3, j = (P & 7) ^ (r & 7);  // V^T rows: 64 keys = 8 granules
+        src = vb + (r * 8 + j) * 8;
+      }
+      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)(dst + ch * 512), 16, 0, 0);
+    }
+  };
+  // fragment addresses (elements inside a page image), fixed per lane
+  int kofs[4][KS];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int r = 32 * (j >> 1) + 8 * (c >> 2) + 4 * (j & 1) + (c & 3);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) kofs[j][s] = r * DH + 8 * ((4 * s + g) ^ pf_kswz<DH>(r));
+  }
+  int vofs[2];
+  {
+    const int r = c;  // V^T row 16 dt + c: (16 dt + c) & 7 == c & 7
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) vofs[kk] = r * PAGE + 8 * ((4 * kk + g) ^ (r & 7));
+  }
+
+  // S^T, masking and the online softmax of one page -> P^T fragments and the rescale factors
+  auto score = [&](const uint16_t* Ks, int key0, s16x8 (&pf)[2][2], float (&alpha)[2]) {
+    f32x4 st[2][4];
+#pragma unroll
+    for (int blk = 0; blk < 2; ++blk)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) st[blk][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // K fragments KPF steps ahead of their MFMAs
+    constexpr int KPF = 4, NKS = 4 * KS;
+    s16x8 ka[KPF];
+#pragma unroll
+    for (int t = 0; t < KPF - 1; ++t) ka[t] = ld16(Ks + kofs[t & 3][t >> 2]);
+#pragma unroll
+    for (int t = 0; t < NKS; ++t) {
+      if (t + KPF - 1 < NKS) ka[(t + KPF - 1) % KPF] = ld16(Ks + kofs[(t + KPF - 1) & 3][(t + KPF - 1) >> 2]);
+      const int j = t & 3, s = t >> 2;
+      st[0][j] = mfma16(ka[t % KPF], qf[0][s], st[0][j]);
+      st[1][j] = mfma16(ka[t % KPF], qf[1][s], st[1][j]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // softmax on the raw scores: max first (scale > 0 commutes with it), then one fma per score,
+    // the bare v_exp_f32 (no denormal range fix-up: the probabilities are rounded to bf16 anyway) and
+    // packed bf16 conversions
+    const bool need_mask = key0 + PAGE - 1 > wmin;  // wave-uniform
+#pragma unroll
+    for (int blk = 0; blk < 2; ++blk) {
+      if (need_mask) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int key = key0 + 32 * (j >> 1) + 8 * g + 4 * (j & 1) + r;
+            st[blk][j][r] = key <= qpos[blk] ? st[blk][j][r] : -INFINITY;
+          }
+      }
+      float mt = NEG_BIG;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) mt = fmaxf(mt, st[blk][j][r]);
+      mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
+      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+      const float mn = fmaxf(m[blk], mt * scale_log2);
+      alpha[blk] = __builtin_amdgcn_exp2f(m[blk] - mn);
+      m[blk] = mn;
+      float ls = 0.f;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        u32x4 pw;
+#pragma unroll
+        for (int e = 0; e < 8; e += 2) {
+          const float p0 = __builtin_amdgcn_exp2f(fmaf(st[blk][2 * kk + (e >> 2)][e & 3], scale_log2, -mn));
+          const float p1 = __builtin_amdgcn_exp2f(fmaf(st[blk][2 * kk + (e >> 2)][(e & 3) + 1], scale_log2, -mn));
+          pw[e >> 1] = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t{p0, p1}), bf16x2_t));
+          ls += p0 + p1;
+        }
+        pf[blk][kk] = __builtin_bit_cast(s16x8, pw);
+      }
+      l[blk] = l[blk] * alpha[blk] + ls;
+    }
+  };
+  // O^T = alpha O^T + V^T . P^T for one page
+  auto accumulate = [&](const uint16_t* Vs, const s16x8 (&pf)[2][2], const float (&alpha)[2]) {
+    // the running max of a row stops moving after its first pages: skip the rescale when no row of the
+    // wave moved (wave-uniform branch)
+    if (__ballot(alpha[0] != 1.f || alpha[1] != 1.f)) {
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          o[0][dt][r] *= alpha[0];
+          o[1][dt][r] *= alpha[1];
+        }
+    }
+    // V^T fragments VPF dim tiles ahead of their MFMAs (the LDS latency exceeds one tile's 4 MFMAs)
+    constexpr int VPF = 3;
+    s16x8 va[VPF][2];
+#pragma unroll
+    for (int t = 0; t < VPF - 1; ++t)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) va[t][kk] = ld16(Vs + vofs[kk] + 16 * t * PAGE);
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) {
+      if (dt + VPF - 1 < NDT) {
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) va[(dt + VPF - 1) % VPF][kk] = ld16(Vs + vofs[kk] + 16 * (dt + VPF - 1) * PAGE);
+      }
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        o[0][dt] = mfma16(va[dt % VPF][kk], pf[0][kk], o[0][dt]);
+        o[1][dt] = mfma16(va[dt % VPF][kk], pf[1][kk], o[1][dt]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  // (Tried: waves 4-7 one page behind on the P.V half, to put one wave's softmax beside its SIMD partner's
+  // MFMAs, with a three-page ring -- no faster.)
+  // three-page ring, two pages in flight: page p + 2 is issued once every wave is past page p - 1
+  if (npages > 0) issue(0, 0);
+  if (npages > 1) issue(1, 1);
+  for (int p = 0; p < npages; ++p) {
+    const int buf = p % 3;
+    if (p + 1 < npages)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(CPW) : "memory");  // this wave's share of page p landed
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (p + 2 < npages) issue(p + 2, (p + 2) % 3);
+    const int key0 = p * PAGE;
+    if (key0 > wmax) continue;  // wave-uniform: every row of this wave is before the page (causal)
+    const uint16_t* Ks = smem + buf * 2 * PAGE_EL;
+    s16x8 pf[2][2];
+    float alpha[2];
+    score(Ks, key0, pf, alpha);
+    accumulate(Ks + PAGE_EL, pf, alpha);
+  }
+
+  // o[blk][dt][r] = O[row c of block blk][dim 16 dt + 4 g + r]
+#pragma unroll
+  for (int blk = 0; blk < 2; ++blk) {
+    float L = l[blk];
+    L += __shfl_xor(L, 16, 64);
+    L += __shfl_xor(L, 32, 64);
+    const int row = row0 + 32 * wave + 16 * blk + c;
+    if (row < nrows) {
+      const int ti = row / G, hi = row % G;
+      uint16_t* op = out + ((size_t)(q0 + ti) * H + kvh * G + hi) * DH + 4 * g;
+      const float inv = L > 0.f ? 1.f / L : 0.f;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) {
+        s16x4 v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = (short)f2bf(o[blk][dt][r] * inv);
+        *reinterpret_cast<s16x4*>(op + 16 * dt) = v;
+      }
+    }
+  }
+}
+
 int launch_attn_prefill(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, const int32_t* block_tables,
                         int max_blocks, const int32_t* cu_q, const int32_t* ctx_lens, uint16_t* out, int B,
-                        int max_qlen, int H, int Hkv, int Dh, float scale, int num_pages, hipStream_t s) {
+                        int max_qlen, int H, int Hkv, int Dh, float scale, int num_pages, int algo, hipStream_t s) {
   if (B <= 0 || max_qlen <= 0) return 0;
   if (H % Hkv != 0) return -1;
   const int G = H / Hkv;
-  dim3 grid((max_qlen * G + 63) / 64, Hkv, B);
   const float sl = scale * LOG2E;
+  if (algo == 2 && (Dh == 128 || Dh == 64)) {
+    const dim3 grid2((max_qlen * G + 255) / 256, Hkv, B);
+    const size_t lds = (size_t)3 * 2 * 64 * Dh * 2;
+    if (Dh == 128) {
+      static bool attr = hipFuncSetAttribute((const void*)attn_prefill_v2_kernel<128>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess;
+      (void)attr;
+      hipLaunchKernelGGL(attn_prefill_v2_kernel<128>, grid2, dim3(512), lds, s, q, kc, vc, block_tables, max_blocks,
+                         cu_q, ctx_lens, out, H, Hkv, sl, num_pages);
+    } else {
+      hipLaunchKernelGGL(attn_prefill_v2_kernel<64>, grid2, dim3(512), lds, s, q, kc, vc, block_tables, max_blocks,
+                         cu_q, ctx_lens, out, H, Hkv, sl, num_pages);
+    }
+    return 0;
+  }
+  dim3 grid((max_qlen * G + 63) / 64, Hkv, B);
   if (Dh == 128) {
     const size_t lds = (size_t)(PAGE * (128 + 8) + 128 * (PAGE + 8) + 4 * 16 * (PAGE + 8)) * 2;
     hipLaunchKernelGGL(attn_prefill_kernel<128>, grid, dim3(256), lds, s, q, kc, vc, block_tables, max_blocks, cu_q,

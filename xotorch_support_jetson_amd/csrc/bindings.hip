@@ -650,7 +650,7 @@ void attn_train_bwd(const at::Tensor& q, const at::Tensor& qt, const at::Tensor&
 
 void attn_prefill(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
                   const at::Tensor& block_tables, const at::Tensor& cu_q, const at::Tensor& ctx_lens, at::Tensor& out,
-                  int64_t max_qlen, double scale) {
+                  int64_t max_qlen, double scale, int64_t algo) {
   CHECK_BF16(q);
   CHECK_BF16(k_cache);
   CHECK_BF16(v_cache);
@@ -670,7 +670,7 @@ void attn_prefill(const at::Tensor& q, const at::Tensor& k_cache, const at::Tens
   const int rc = xot::launch_attn_prefill(bf(q), bf(k_cache), bf(v_cache), block_tables.data_ptr<int32_t>(),
                                           (int)block_tables.size(1), cu_q.data_ptr<int32_t>(),
                                           ctx_lens.data_ptr<int32_t>(), bf(out), (int)B, (int)max_qlen, (int)H,
-                                          (int)Hkv, (int)Dh, (float)scale, (int)nb, cur_stream());
+                                          (int)Hkv, (int)Dh, (float)scale, (int)nb, (int)algo, cur_stream());
   XCHECK(rc == 0, "attn_prefill: unsupported H=", H, " Hkv=", Hkv, " Dh=", Dh);
 }
 
@@ -784,7 +784,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_decode", &attn_decode, py::arg("q"), py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"),
         py::arg("ctx_lens"), py::arg("out"), py::arg("ws_o"), py::arg("ws_ml"), py::arg("pages_per_part"),
         py::arg("nparts"), py::arg("scale"), py::arg("algo") = 2, py::arg("tickets") = py::none());
-  m.def("attn_prefill", &attn_prefill);
+  m.def("attn_prefill", &attn_prefill, py::arg("q"), py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"),
+        py::arg("cu_q"), py::arg("ctx_lens"), py::arg("out"), py::arg("max_qlen"), py::arg("scale"), py::arg("algo") = 2);
   m.def("router_logits", &router_logits);
   m.def("moe_combine_norm", &moe_combine_norm);
   m.def("splitk_silu", &splitk_silu);

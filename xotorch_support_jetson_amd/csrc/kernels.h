@@ -81,7 +81,7 @@ int launch_attn_decode(const uint16_t* q, const uint16_t* kc, const uint16_t* vc
                        int* tickets, hipStream_t s);
 int launch_attn_prefill(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, const int32_t* block_tables,
                         int max_blocks, const int32_t* cu_q, const int32_t* ctx_lens, uint16_t* out, int B,
-                        int max_qlen, int H, int Hkv, int Dh, float scale, int num_pages, hipStream_t s);
+                        int max_qlen, int H, int Hkv, int Dh, float scale, int num_pages, int algo, hipStream_t s);
 
 // causal self-attention for training (token-major Q / K / V slices, GQA); lse2 [B, H, L] fp32 (log2 domain);
 // *t arguments are [B, heads, Dh, Lp] transposed images from launch_attn_train_transpose (zero past L)

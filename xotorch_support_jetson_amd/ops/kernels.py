@@ -231,6 +231,11 @@ def attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale: float, ws: D
   return out
 
 
+# XOT_PREFILL_ATTN: 2 = 256-row workgroups, LDS-DMA page ring, in-register softmax (default); 1 = the
+# first 64-row kernel (register-staged pages, P through LDS)
+PREFILL_ALGO = int(os.environ.get("XOT_PREFILL_ATTN", "2"))
+
+
 def attn_prefill(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, max_qlen: int, scale: float,
                  out: torch.Tensor | None = None) -> torch.Tensor:
   if not _gpu(q):
@@ -240,7 +245,8 @@ def attn_prefill(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, max_qlen: in
       return out
     return y
   out = torch.empty_like(q) if out is None else out
-  require().attn_prefill(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, out, int(max_qlen), float(scale))
+  require().attn_prefill(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, out, int(max_qlen), float(scale),
+                         PREFILL_ALGO)
   return out
 
 
