@@ -153,3 +153,33 @@ def test_engine_concurrent_serving_gpu():
     same = sum(a == b for a, b in zip(ref, got))
     assert same >= len(prompts) - 2, (same, ref, got)  # bf16 batch-composition rounding may flip a near-tie
   asyncio.run(main())
+
+
+@pytest.mark.parametrize("model", ["tiny-llama", "tiny-deepseek-v2"])
+def test_prefix_cache_gpu(gpu, model):
+  """Prompt-prefix reuse on the HIP path (forked pages read by the prefill kernels, graph decode after):
+  the reusing prompt's logits and its next decode step match a fresh engine's (MHA and MLA caches)."""
+  from tests.test_prefix_cache import greedy, host, prompts
+
+  async def main():
+    a, b = prompts(2)
+    n = 4 if model == "tiny-llama" else 3
+    s = Shard(model, 0, n - 1, n)
+    e = ShardedInferenceEngine(NoopShardDownloader(), device=gpu)
+    out, st = await e.infer_tensor("A", s, a)
+    for _ in range(2):
+      out, st = await e.infer_tensor("A", s, greedy(out), st)
+    outb, _ = await e.infer_tensor("B", s, b)
+    assert e.prefix_cache.stats["hit_tokens"] == 128
+    fresh = ShardedInferenceEngine(NoopShardDownloader(), device=gpu)
+    await fresh.ensure_shard(s)
+    fresh.prefix_cache = None
+    ref, _ = await fresh.infer_tensor("B", s, b)
+    x, y = torch.as_tensor(host(outb)).view(-1), torch.as_tensor(host(ref)).view(-1)
+    assert torch.corrcoef(torch.stack([x, y]))[0, 1] > 0.999
+    o2, _ = await e.infer_tensor("B", s, greedy(outb))
+    r2, _ = await fresh.infer_tensor("B", s, greedy(ref))
+    x, y = torch.as_tensor(host(o2)).view(-1), torch.as_tensor(host(r2)).view(-1)
+    assert torch.corrcoef(torch.stack([x, y]))[0, 1] > 0.999
+
+  asyncio.run(main())

@@ -46,6 +46,9 @@ def default_device() -> torch.device:
 # burst of long prompts from stalling every decoding request for one huge step (vLLM's max_num_batched_tokens)
 MAX_STEP_TOKENS = int(os.environ.get("XOT_MAX_STEP_TOKENS", "8192"))
 PRESAMPLE = os.environ.get("XOT_PRESAMPLE", "1") == "1"
+# prompt-prefix KV reuse (inference/prefix_cache.py): on by default, at most this fraction of the KV pool
+PREFIX_CACHE = os.environ.get("XOT_PREFIX_CACHE", "1") == "1"
+PREFIX_CACHE_FRAC = float(os.environ.get("XOT_PREFIX_CACHE_FRAC", "0.25"))
 
 
 class ShardedInferenceEngine(InferenceEngine):
@@ -70,6 +73,7 @@ class ShardedInferenceEngine(InferenceEngine):
     self._sampling = False
     self.stats = {"steps": 0, "requests": 0, "tokens": 0}  # batched forward steps (serving diagnostics)
     self._presampled: dict = {}  # (logits ptr, row) -> (temperature, top_k, token) drawn with the forward
+    self.prefix_cache = None  # first shard's PrefixCache (built with the runner)
 
   # ------------------------------------------------------------------ helpers
   async def _run(self, fn, *args):
@@ -273,17 +277,42 @@ class ShardedInferenceEngine(InferenceEngine):
     self.stats["requests"] += len(items)
     if self.trainer is not None and self.trainer.dirty:
       self.trainer.sync_to_inference()  # serve the weights training just produced
-    rids, qlens, xs = [], [], []
-    for rid, inp, *_ in items:
+    rids, qlens, xs, pc_ops = [], [], [], []
+    pc = self.prefix_cache
+    for rid, inp, *rest in items:
+      state = rest[0] if rest else {}
+      ops = None
       x = inp if isinstance(inp, torch.Tensor) else torch.as_tensor(np.asarray(inp))
       if x.dim() == 3:  # hidden [1, L, D]
+        from .prefix_cache import apply_ops
+        apply_ops(self.runner.bm, rid, (state or {}).get("pc"))  # the first shard's prefix-cache operations
         L = x.shape[1]
         xs.append(x.reshape(L, x.shape[2]).to(torch.bfloat16))
       else:  # token ids [1, L]
-        xs.append(x.reshape(-1).to(torch.int32))
-        L = xs[-1].numel()
+        ids = x.reshape(-1).to(torch.int32)
+        if pc is not None and rid not in self._images:
+          ops = {}
+          if not self.runner.has(rid) and ids.numel() > 1:
+            n, eid = pc.on_prompt(rid, ids.tolist())
+            if n:
+              ids = ids[n:]
+              ops["fork"] = [eid, n]
+          elif self.runner.has(rid) and ids.numel() == 1:
+            save = pc.on_decode(rid)
+            if save is not None:
+              ops["save"] = save
+          drops = pc.outgoing_drops(rid)
+          if drops:
+            ops["drop"] = drops
+        xs.append(ids)
+        L = ids.numel()
       rids.append(rid)
       qlens.append(L)
+      pc_ops.append(ops or None)
+    if pc is not None:
+      need = sum(self.runner.bm.blocks_needed(r, q) for r, q in zip(rids, qlens))
+      if need > self.runner.bm.num_free:
+        pc.evict(need)
     image_embeds = None
     if self._images and self.shard.is_first_layer():
       feats = [self.runner.image_features(self._images.pop(rid)) for rid in rids if rid in self._images]
@@ -310,8 +339,11 @@ class ShardedInferenceEngine(InferenceEngine):
       return res
     off = 0
     outc = out.cpu()
-    for rid, L in zip(rids, qlens):
-      res.append((outc[off:off + L].reshape(1, L, -1), {"n_past": self.runner.num_tokens(rid)}))
+    for rid, L, ops in zip(rids, qlens, pc_ops):
+      st = {"n_past": self.runner.num_tokens(rid)}
+      if self.shard.is_first_layer():
+        st["pc"] = ops  # replaces the previous step's operations in the state that travels the ring
+      res.append((outc[off:off + L].reshape(1, L, -1), st))
       off += L
     return res
 
@@ -335,7 +367,13 @@ class ShardedInferenceEngine(InferenceEngine):
   async def finish_request(self, request_id: str) -> None:
     self._images.pop(request_id, None)
     if self.runner is not None:
-      await self._run(self.runner.free, request_id)
+      pc = self.prefix_cache
+
+      def fin():
+        if pc is not None:
+          pc.on_finish(request_id)
+        self.runner.free(request_id)
+      await self._run(fin)
 
   # ------------------------------------------------------------------ shard lifecycle
   def _model_dir(self, shard: Shard) -> Optional[Path]:
@@ -384,6 +422,12 @@ class ShardedInferenceEngine(InferenceEngine):
                               max_ctx=max_ctx, seed=0)
     self.config = cfg
     self.model_path = model_dir
+    self.prefix_cache = None
+    longrope = (cfg.rope_scaling or {}).get("rope_type") == "longrope"  # the prefix's rotation depends on the total length
+    if PREFIX_CACHE and shard.is_first_layer() and not longrope:
+      from .prefix_cache import PrefixCache
+      self.prefix_cache = PrefixCache(self.runner.bm, int(self.runner.bm.num_blocks * PREFIX_CACHE_FRAC),
+                                      single_shard=shard.is_last_layer())
     self.tokenizer = _resolve_tokenizer(model_dir if model_dir is not None else
                                         (registry.get_repo(shard.model_id, "ShardedInferenceEngine") or "byte"),
                                         cfg.vocab_size)
