@@ -64,8 +64,9 @@ async def main(a):
   words = " ".join(f"w{i % 97}" for i in range(a.prompt_words))
 
   async def one(session, i, max_tokens):
+    text = f"{words} (request {i})" if a.shared_prefix else f"request {i}: {words}"
     body = {"model": a.model, "stream": True, "max_tokens": max_tokens, "temperature": a.temperature,
-            "messages": [{"role": "user", "content": f"request {i}: {words}"}]}
+            "messages": [{"role": "user", "content": text}]}
     t0 = time.perf_counter()
     ttft, n = None, 0
     async with session.post(url, json=body) as r:
@@ -103,6 +104,8 @@ async def main(a):
          "engine_steps": steps, "mean_requests_per_step": round(reqs / max(steps, 1), 1),
          "ms_per_step": round(wall * 1e3 / max(steps, 1), 2),
          "presampled_tokens": eng.stats.get("presampled", 0) - s0.get("presampled", 0),
+         "shared_prefix": a.shared_prefix,
+         "prefix_cache": dict(eng.prefix_cache.stats) if eng.prefix_cache is not None else None,
          "data": "random-init weights, byte tokenizer, synthetic prompts", "dtype": "bf16",
          "device": caps.chip}
   print(json.dumps(out), flush=True)
@@ -123,6 +126,9 @@ if __name__ == "__main__":
   ap.add_argument("--max-tokens", type=int, default=128)
   ap.add_argument("--prompt-words", type=int, default=200)
   ap.add_argument("--temperature", type=float, default=0.6)
+  ap.add_argument("--shared-prefix", action="store_true",
+                  help="every prompt starts with the same words (a system prompt / earlier turns) and ends with "
+                       "the request index, so prompt-prefix KV reuse applies")
   if os.environ.get("XOT_PROFILE"):  # host-side hot spots of the serving loop
     import cProfile
     PROF = cProfile.Profile()
