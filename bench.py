@@ -43,7 +43,11 @@ def main():
   ap.add_argument("--prompt-len", type=int, default=512)
   ap.add_argument("--temperature", type=float, default=0.6)
   ap.add_argument("--layers", type=int, default=0, help="debug only: truncate the model (result marked invalid)")
+  ap.add_argument("--weight-dtype", default="bf16", choices=["bf16", "fp8"],
+                  help="fp8: weight-only e4m3 projections (a separate, reduced-precision measurement; the headline "
+                       "is bf16)")
   args = ap.parse_args()
+  os.environ["XOT_WEIGHT_DTYPE"] = args.weight_dtype
 
   from xotorch_support_jetson_amd.models.config import preset
   from xotorch_support_jetson_amd.parallel.comm import P2PTransport, init_distributed
@@ -131,7 +135,7 @@ def main():
       "higher_is_better": True,
       "scaling": "weak",
       "vs_baseline": None,
-      "dtype": "bf16",
+      "dtype": "bf16" if args.weight_dtype == "bf16" else "bf16 activations, fp8-e4m3 weights (NOT the headline)",
       "data": "synthetic prompts, random-init weights (exact Llama-3-70B architecture)",
       "config": {
         "model": args.model if not args.layers else f"{args.model}-TRUNCATED-{args.layers}L-INVALID",
@@ -141,6 +145,7 @@ def main():
         "batch_per_gpu": B,
         "decode_context": f"{args.prompt_len + args.warmup}..{args.prompt_len + args.warmup + args.steps}",
         "sampling": f"temperature {args.temperature}, top-k 35 (on-device)",
+        "weight_dtype": args.weight_dtype,
       },
       "extra": {"prefill_s": round(t_prefill, 2), "init_s": round(t_init, 2),
                 "tokens_per_s_per_gpu": round(tps / world, 2),

@@ -372,6 +372,63 @@ def test_gemm_stream(gpu, M, epi, ntw, splits):
     assert rel_err(y2, ref) < 1e-2
 
 
+def test_fp8_layout_roundtrip(gpu):
+  from xotorch_support_jetson_amd.ops.weights_layout import (dequant_stream8, quantize_fp8_rows, shuffle_for_stream8,
+                                                             unshuffle_from_stream8)
+  w = torch.randn(256, 512, device=gpu) / 20
+  q, sc = quantize_fp8_rows(w)
+  assert torch.equal(unshuffle_from_stream8(shuffle_for_stream8(q)), q)
+  deq = dequant_stream8(shuffle_for_stream8(q), sc, torch.float32)
+  assert rel_err(deq, w) < 0.04  # e4m3: 3 mantissa bits
+  assert float((q.view(torch.float8_e4m3fn).float().abs().amax(1) - 448).abs().max()) == 0  # row absmax -> 448
+
+
+@pytest.mark.parametrize("M", [1, 5, 16, 33, 100, 128, 200])
+@pytest.mark.parametrize("epi,ntw,splits", [("none", 1, 1), ("none", 2, 4), ("resid", 1, 2), ("silu", 2, 1),
+                                            ("silu", 4, 2), ("none", 4, 1), ("resid", 2, 8)])
+def test_gemm_stream8(gpu, M, epi, ntw, splits):
+  """Weight-only FP8 stream GEMM against the fp32 product with the dequantised weight (the kernel widens
+  e4m3 to bf16 exactly, so only accumulation order and the bf16 output differ)."""
+  from xotorch_support_jetson_amd.ops._ext import require
+  from xotorch_support_jetson_amd.ops.weights_layout import dequant_stream8, quantize_fp8_rows, shuffle_for_stream8
+  torch.manual_seed(0)
+  N, Kd = 1024, 2048
+  x = torch.randn(M, Kd, device=gpu, dtype=torch.bfloat16)
+  w = torch.randn(N, Kd, device=gpu, dtype=torch.bfloat16) / math.sqrt(Kd)
+  q, sc = quantize_fp8_rows(w)
+  w8 = shuffle_for_stream8(q)
+  b = torch.randn(N, device=gpu, dtype=torch.bfloat16)
+  r = torch.randn(M, N, device=gpu, dtype=torch.bfloat16)
+  ws = torch.empty(splits * M * N, device=gpu, dtype=torch.float32)
+  full = x.float() @ dequant_stream8(w8, sc, torch.float32).t() + b.float()
+  if epi == "silu":
+    f = full.view(M, N // 32, 2, 16)
+    ref = (torch.nn.functional.silu(f[:, :, 0]) * f[:, :, 1]).reshape(M, N // 2)
+    y = torch.empty(M, N // 2, device=gpu, dtype=torch.bfloat16)
+  elif epi == "resid":
+    ref = full + r.float()
+    y = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+  else:
+    ref = full
+    y = torch.empty(M, N, device=gpu, dtype=torch.float32)
+  require().gemm_stream8(x, w8, sc, y, b, r if epi == "resid" else None, ws, K.EPI[epi], ntw, splits)
+  assert rel_err(y, ref) < 1e-2
+
+
+def test_linear_fp8_dispatch(gpu):
+  """ops.linear on a "stream8" weight: FP8 stream GEMM for decode-shaped M, widened bf16 GEMM above."""
+  from xotorch_support_jetson_amd.ops.linear import linear, to_rowmajor, to_stream8_layout
+  torch.manual_seed(1)
+  w = torch.randn(512, 1024, device=gpu, dtype=torch.bfloat16) / 32
+  w8 = to_stream8_layout(w)
+  assert w8.dtype == torch.uint8 and w8.xot_layout == "stream8"
+  wd = to_rowmajor(w8)
+  for M in (1, 64, 600):
+    x = torch.randn(M, 1024, device=gpu, dtype=torch.bfloat16)
+    assert rel_err(linear(x, w8), x.float() @ wd.float().t()) < 1e-2
+    assert rel_err(linear(x, w8), x.float() @ w.float().t()) < 5e-2  # quantisation error
+
+
 @pytest.mark.parametrize("M", [1, 33, 200])
 @pytest.mark.parametrize("Kd", [128, 384, 1408])
 @pytest.mark.parametrize("epi", ["none", "silu"])

@@ -258,3 +258,26 @@ def test_graph_buckets_survive_workspace_growth(gpu):
   for _ in range(3):  # bucket 1 again, captured before the growth
     a, b = g.forward(["solo"], [1], tok), e.forward(["solo"], [1], tok)
     assert torch.allclose(a, b, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("name", ["tiny-llama-d64", "tiny-qwen", "tiny-mixtral"])
+def test_fp8_weights_runner(gpu, name, monkeypatch):
+  """XOT_WEIGHT_DTYPE=fp8: the dense projections run as weight-only e4m3 (prefill through the widened bf16
+  GEMM or the FP8 stream kernel, decode graphs on the FP8 stream kernel); logits stay close to bf16."""
+  c = preset(name)
+  sh = Shard(name, 0, c.num_layers - 1, c.num_layers)
+  g = torch.Generator().manual_seed(5)
+  ids = torch.randint(0, c.vocab_size, (40,), generator=g).to(torch.int32)
+  outs = []
+  for dt in ("bf16", "fp8"):
+    monkeypatch.setenv("XOT_WEIGHT_DTYPE", dt)
+    r = ShardRunner(c, sh, gpu, max_batch=4, max_ctx=128, seed=3)
+    if dt == "fp8":
+      lw = r.weights.layers[0]
+      assert lw.qkv_w.dtype == torch.uint8 and lw.o_w.xot_layout == "stream8"
+    seq = [r.forward(["a"], [40], ids.to(gpu)).float().view(-1)]
+    for t in range(3):
+      seq.append(r.forward(["a"], [1], ids[t:t + 1].to(gpu)).float().view(-1))
+    outs.append(torch.stack(seq))
+  for a, b in zip(*outs):
+    assert torch.corrcoef(torch.stack([a, b]))[0, 1] > 0.98

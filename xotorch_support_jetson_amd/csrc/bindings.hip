@@ -12,8 +12,10 @@ namespace {
 #define CHECK_CONTIG(x) XCHECK((x).is_contiguous(), #x " must be contiguous")
 #define CHECK_DT(x, dt) XCHECK((x).scalar_type() == (dt), #x " must be " #dt)
 #define CHECK_BF16(x) \
-  CHECK_GPU(x);       \
-  CHECK_DT(x, at::kBFloat16)
+  do {                \
+    CHECK_GPU(x);     \
+    CHECK_DT(x, at::kBFloat16); \
+  } while (0)
 
 template <typename... Ts>
 bool all_contig_gpu(const Ts&... ts) {
@@ -275,6 +277,47 @@ void gemm_stream(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const 
                                          (int)epi, wsp, ws_elems, (int)M, (int)N, (int)K, (int)ntw, (int)splits,
                                          wshuf, tk, tk_n, reduce, cur_stream());
   XCHECK(rc == 0, "gemm_stream: unsupported shape M=", M, " N=", N, " K=", K, " epi=", epi, " ntw=", ntw,
+         " splits=", splits);
+}
+
+// Decode GEMM on FP8 (e4m3) pre-shuffled weights w8 [N, K] uint8 with per-row fp32 scales (y = x . (w8 * s)^T).
+void gemm_stream8(const at::Tensor& x, const at::Tensor& w8, const at::Tensor& wscale, at::Tensor& y,
+                  const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& res,
+                  const c10::optional<at::Tensor>& ws, int64_t epi, int64_t ntw, int64_t splits, bool reduce) {
+  CHECK_BF16(x);
+  CHECK_GPU(w8);
+  CHECK_DT(w8, at::kByte);
+  CHECK_GPU(wscale);
+  CHECK_DT(wscale, at::kFloat);
+  CHECK_GPU(y);
+  XCHECK(x.dim() == 2 && w8.dim() == 2 && y.dim() == 2, "gemm_stream8: x, w8, y must be 2-D");
+  XCHECK(x.stride(1) == 1 && x.stride(0) % 8 == 0 && w8.is_contiguous() && y.stride(1) == 1 && wscale.is_contiguous(),
+         "gemm_stream8: layouts");
+  const int64_t M = x.size(0), K = x.size(1), N = w8.size(0);
+  XCHECK(w8.size(1) == K && wscale.numel() == N, "gemm_stream8: shapes");
+  const bool f32 = y.scalar_type() == at::kFloat;
+  XCHECK(f32 || y.scalar_type() == at::kBFloat16, "gemm_stream8: y must be bf16 or fp32");
+  XCHECK(y.size(0) == M && y.size(1) == (epi == 2 ? N / 2 : N), "gemm_stream8: y shape");
+  if (bias.has_value()) CHECK_BF16((*bias));
+  int64_t ldr = 0;
+  if (epi == 1) {
+    XCHECK(res.has_value(), "gemm_stream8: residual epilogue needs res");
+    CHECK_BF16((*res));
+    ldr = res->stride(0);
+  }
+  float* wsp = nullptr;
+  long ws_elems = 0;
+  if (ws.has_value()) {
+    CHECK_GPU((*ws));
+    CHECK_DT((*ws), at::kFloat);
+    wsp = ws->data_ptr<float>();
+    ws_elems = ws->numel();
+  }
+  const int rc = xot::launch_gemm_stream8(bf(x), (int)x.stride(0), w8.data_ptr<uint8_t>(), wscale.data_ptr<float>(),
+                                          bf_opt(bias), epi == 1 ? bf(*res) : nullptr, (int)ldr, y.data_ptr(),
+                                          (int)y.stride(0), f32, (int)epi, wsp, ws_elems, (int)M, (int)N, (int)K,
+                                          (int)ntw, (int)splits, reduce, cur_stream());
+  XCHECK(rc == 0, "gemm_stream8: unsupported shape M=", M, " N=", N, " K=", K, " epi=", epi, " ntw=", ntw,
          " splits=", splits);
 }
 
@@ -768,6 +811,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_stream", &gemm_stream, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("bias"), py::arg("res"),
         py::arg("ws"), py::arg("epi"), py::arg("ntw"), py::arg("splits"), py::arg("wshuf"),
         py::arg("tickets") = py::none(), py::arg("reduce") = true);
+  m.def("gemm_stream8", &gemm_stream8, py::arg("x"), py::arg("w8"), py::arg("wscale"), py::arg("y"), py::arg("bias"),
+        py::arg("res"), py::arg("ws"), py::arg("epi"), py::arg("ntw"), py::arg("splits"), py::arg("reduce") = true);
   m.def("gemm_big", &gemm_big, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("bias"), py::arg("res"),
         py::arg("ws"), py::arg("epi"), py::arg("bn"), py::arg("splits"), py::arg("reduce") = true);
   m.def("splitk_resid_rmsnorm", &splitk_resid_rmsnorm);

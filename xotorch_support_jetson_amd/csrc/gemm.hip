@@ -196,7 +196,12 @@ int launch_gemm_skinny(const uint16_t* X, int ldx, const uint16_t* W, int ldw, c
 // order; MOE = 1 reads A in slot order, MOE = 2 gathers A row moe_gather[slot] (token rows).  Output
 // rows are slots.  Row blocks past an expert's count exit at once, so the grid can be sized for the
 // worst case on the host and the launch stays graph-capturable (no host sync on the routing).
-template <int MT, int NTW, int KS, int EPI, bool OUT_F32, bool SPLIT, bool WSHUF, int OCC, int MOE>
+// W8: weight-only FP8 (OCP e4m3, per-output-row fp32 scale `wscale`): pre-shuffled tiles of 16 rows x 128 k
+// as [N/16][K/128][2][lane][16 B], the 16 bytes of lane (g, c) in half h being row c, k 64 h + 8 g .. +8
+// (bytes 0-7) and 64 h + 32 + 8 g .. +8 (bytes 8-15): one 1 KB wave load carries two MFMA k-steps, half
+// the bytes of the bf16 layout.  v_cvt_scalef32_pk_bf16_fp8 widens each fragment just before its MFMAs;
+// the row scale is applied to the fp32 accumulators (so split-K slabs are already scaled).
+template <int MT, int NTW, int KS, int EPI, bool OUT_F32, bool SPLIT, bool WSHUF, int OCC, int MOE, bool W8 = false>
 __global__ __launch_bounds__(256, OCC) void gemm_stream_kernel(const uint16_t* __restrict__ X, int ldx,
                                                              const uint16_t* __restrict__ W, int ldw,
                                                              const uint16_t* __restrict__ bias,
@@ -205,8 +210,10 @@ __global__ __launch_bounds__(256, OCC) void gemm_stream_kernel(const uint16_t* _
                                                              float* __restrict__ ws, int M, int N, int kper,
                                                              int mblocks, const int* __restrict__ moe_off,
                                                              const int* __restrict__ moe_gather,
-                                                             int* __restrict__ tickets, long ysplit) {
+                                                             int* __restrict__ tickets, long ysplit,
+                                                             const float* __restrict__ wscale) {
   constexpr int KC = 32 * KS;
+  static_assert(!W8 || (WSHUF && KS == 4 && MOE == 0), "FP8 weights: pre-shuffled 128-deep chunks, dense GEMM");
   constexpr int CPR = KC / 8;  // 16-B chunks per row per k-chunk
   constexpr int NTH = 256;
   constexpr int ROWS = 16 * MT;
@@ -267,7 +274,10 @@ __global__ __launch_bounds__(256, OCC) void gemm_stream_kernel(const uint16_t* _
   constexpr int WSTEP = WSHUF ? 16 * KC : KC;  // elements between consecutive chunks of one lane
 #pragma unroll
   for (int j = 0; j < NTW; ++j) {
-    if constexpr (WSHUF)
+    if constexpr (W8)  // byte pointer carried as uint16_t*: chunks are 2 KB = 1024 "elements" apart
+      wp[j] = reinterpret_cast<const uint16_t*>(reinterpret_cast<const uint8_t*>(W) +
+                                                ((size_t)((n0 >> 4) + j) * (ldw / KC) + kb / KC) * (16 * KC) + lane * 16);
+    else if constexpr (WSHUF)
       wp[j] = W + ((size_t)((n0 >> 4) + j) * (ldw / KC) + kb / KC) * (16 * KC) + lane * 8;
     else
       wp[j] = W + (size_t)(n0 + 16 * j + c) * ldw + kb + g * 8 * KS;
@@ -305,9 +315,24 @@ __global__ __launch_bounds__(256, OCC) void gemm_stream_kernel(const uint16_t* _
 #pragma unroll
     for (int j = 0; j < NTW; ++j)
 #pragma unroll
-      for (int s = 0; s < KS; ++s)
-        wr[j][s] = __builtin_nontemporal_load(
-            reinterpret_cast<const s16x8*>(wp[j] + ch * WSTEP + (WSHUF ? 512 * s : 8 * s)));
+      for (int s = 0; s < (W8 ? 2 : KS); ++s)
+        wr[j][s] = __builtin_nontemporal_load(reinterpret_cast<const s16x8*>(
+            W8 ? wp[j] + ch * (8 * KC) + 512 * s : wp[j] + ch * WSTEP + (WSHUF ? 512 * s : 8 * s)));
+  };
+  // B fragment of k-step s for column tile j (W8: widen 8 e4m3 values of the raw 16-byte load)
+  auto bfrag = [&](const s16x8 (&wr)[NTW][KS], int j, int s) -> s16x8 {
+    if constexpr (W8) {
+      const u32x4 raw = __builtin_bit_cast(u32x4, wr[j][s >> 1]);
+      const uint32_t lo = raw[(s & 1) * 2], hi = raw[(s & 1) * 2 + 1];
+      u32x4 o;
+      o[0] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(lo, 1.0f, false));
+      o[1] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(lo, 1.0f, true));
+      o[2] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(hi, 1.0f, false));
+      o[3] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(hi, 1.0f, true));
+      return __builtin_bit_cast(s16x8, o);
+    } else {
+      return wr[j][s];
+    }
   };
 
   f32x4 acc[MT][NTW];
@@ -350,7 +375,7 @@ __global__ __launch_bounds__(256, OCC) void gemm_stream_kernel(const uint16_t* _
       const s16x8 cur = a[t % LDPF];
       if (t + LDPF < KS * MT) a[t % LDPF] = afrag(t + LDPF);
 #pragma unroll
-      for (int j = 0; j < NTW; ++j) acc[i][j] = mfma16(cur, wr[j][s], acc[i][j]);
+      for (int j = 0; j < NTW; ++j) acc[i][j] = mfma16(cur, bfrag(wr, j, s), acc[i][j]);
       __builtin_amdgcn_sched_barrier(0);
     }
   };
@@ -378,6 +403,17 @@ __global__ __launch_bounds__(256, OCC) void gemm_stream_kernel(const uint16_t* _
     xstore(xr, 1);
     __syncthreads();
     compute(wb, 1);
+  }
+
+  if constexpr (W8) {
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+      const float sc = wscale[n0 + 16 * j + c];
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] *= sc;
+    }
   }
 
   if constexpr (SPLIT) {
@@ -472,34 +508,35 @@ __global__ __launch_bounds__(256, OCC) void gemm_stream_kernel(const uint16_t* _
   }
 }
 
-template <int MT, int NTW, int KS, int EPI, bool F32, bool WSH>
+template <int MT, int NTW, int KS, int EPI, bool F32, bool WSH, bool W8 = false>
 static void stream_launch(const uint16_t* X, int ldx, const uint16_t* W, int ldw, const uint16_t* bias,
                           const uint16_t* R, int ldr, void* Y, int ldy, float* ws, int M, int N, int K, int S,
-                          int* tickets, bool reduce, hipStream_t st) {
-  // occupancy request: 2 workgroups/CU while the register budget allows it
-  constexpr int OCC = (MT * NTW >= 32) ? 1 : 2;
+                          int* tickets, bool reduce, hipStream_t st, const float* wscale = nullptr) {
+  // occupancy request: 2 workgroups/CU while the register budget allows it (FP8 weights need a few more
+  // registers for the widened fragments)
+  constexpr int OCC = (MT * NTW >= (W8 ? 16 : 32)) ? 1 : 2;
   constexpr int SMEM = 2 * 16 * MT * 32 * KS * 2;
   const int mblocks = (M + 16 * MT - 1) / (16 * MT);
   dim3 grid(N / (64 * NTW) * mblocks, S);
   const int kper = K / S;
   if (S == 1) {
-    auto kern = gemm_stream_kernel<MT, NTW, KS, EPI, F32, false, WSH, OCC, 0>;
+    auto kern = gemm_stream_kernel<MT, NTW, KS, EPI, F32, false, WSH, OCC, 0, W8>;
     if constexpr (SMEM > 65536) {
       static bool attr = (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM) ==
                           hipSuccess);
       (void)attr;
     }
     kern<<<grid, 256, SMEM, st>>>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, nullptr, M, N, kper, mblocks, nullptr, nullptr,
-                                  nullptr, 0L);
+                                  nullptr, 0L, wscale);
   } else {
-    auto kern = gemm_stream_kernel<MT, NTW, KS, EPI, F32, true, WSH, OCC, 0>;
+    auto kern = gemm_stream_kernel<MT, NTW, KS, EPI, F32, true, WSH, OCC, 0, W8>;
     if constexpr (SMEM > 65536) {
       static bool attr = (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM) ==
                           hipSuccess);
       (void)attr;
     }
     kern<<<grid, 256, SMEM, st>>>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, M, N, kper, mblocks, nullptr, nullptr,
-                                  tickets, 0L);
+                                  tickets, 0L, wscale);
     if (tickets != nullptr || !reduce) return;  // combined in-launch / slabs left for the consumer
     const int ncol = EPI == EPI_SILU ? N / 2 : N;
     long chunks = (long)M * (ncol / 8);
@@ -565,7 +602,7 @@ static void moe_launch(const uint16_t* X, int ldx, const uint16_t* W, void* Y, i
   dim3 grid(N / (64 * NTW) * mblocks, S, E);
   gemm_stream_kernel<MT, NTW, KS, EPI, F32, false, WSH, OCC, MOE><<<grid, 256, SMEM, st>>>(
       X, ldx, W, K, nullptr, nullptr, 0, Y, ldy, nullptr, max_rows, N, K / S, mblocks, off, gather, nullptr,
-      S > 1 ? ysplit : 0L);
+      S > 1 ? ysplit : 0L, nullptr);
 }
 
 template <int EPI, bool F32, bool WSH, int MOE>
@@ -602,6 +639,49 @@ int launch_gemm_moe(const uint16_t* X, int ldx, const uint16_t* W, void* Y, int 
   if (out_f32) XOT_MOE(EPI_NONE, true);
   XOT_MOE(EPI_NONE, false);
 #undef XOT_MOE
+}
+
+template <int EPI, bool F32>
+static int stream8_dispatch(const uint16_t* X, int ldx, const uint8_t* W8p, const float* wscale, int K,
+                            const uint16_t* bias, const uint16_t* R, int ldr, void* Y, int ldy, float* ws,
+                            long ws_elems, int M, int N, int ntw, int S, bool reduce, hipStream_t st) {
+  const uint16_t* W = reinterpret_cast<const uint16_t*>(W8p);
+  if (EPI == EPI_SILU && ntw == 1) ntw = 2;
+  if (ntw != 1 && ntw != 2 && ntw != 4) return -1;
+  const int mt = (M + 15) / 16;
+  if (ntw == 4 && mt <= 2) ntw = 2;
+  if (N % (64 * ntw) != 0 || S < 1 || K % (S * 128) != 0) return -1;
+  if (S > 1 && (ws == nullptr || ws_elems < (long)S * M * N)) return -1;
+#define XOT_S8(MTV)                                                                                               \
+  do {                                                                                                            \
+    if (ntw == 1 && EPI != EPI_SILU)                                                                              \
+      stream_launch<MTV, 1, 4, EPI, F32, true, true>(X, ldx, W, K, bias, R, ldr, Y, ldy, ws, M, N, K, S, nullptr,  \
+                                                     reduce, st, wscale);                                          \
+    else if (ntw == 4 && MTV >= 4)                                                                                \
+      stream_launch<MTV, 4, 4, EPI, F32, true, true>(X, ldx, W, K, bias, R, ldr, Y, ldy, ws, M, N, K, S, nullptr,  \
+                                                     reduce, st, wscale);                                          \
+    else                                                                                                          \
+      stream_launch<MTV, 2, 4, EPI, F32, true, true>(X, ldx, W, K, bias, R, ldr, Y, ldy, ws, M, N, K, S, nullptr,  \
+                                                     reduce, st, wscale);                                          \
+    return 0;                                                                                                     \
+  } while (0)
+  if (mt <= 1) XOT_S8(1);
+  if (mt <= 2) XOT_S8(2);
+  if (mt <= 4) XOT_S8(4);
+  XOT_S8(8);  // M > 128: 128-row blocks (see stream_dispatch)
+#undef XOT_S8
+}
+
+int launch_gemm_stream8(const uint16_t* X, int ldx, const uint8_t* W, const float* wscale, const uint16_t* bias,
+                        const uint16_t* R, int ldr, void* Y, int ldy, bool out_f32, int epi, float* ws, long ws_elems,
+                        int M, int N, int K, int ntw, int S, bool reduce, hipStream_t s) {
+  if (M <= 0) return 0;
+  if (epi == EPI_SILU)
+    return out_f32 ? -1 : stream8_dispatch<EPI_SILU, false>(X, ldx, W, wscale, K, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, ntw, S, reduce, s);
+  if (epi == EPI_RESID)
+    return out_f32 ? -1 : stream8_dispatch<EPI_RESID, false>(X, ldx, W, wscale, K, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, ntw, S, reduce, s);
+  return out_f32 ? stream8_dispatch<EPI_NONE, true>(X, ldx, W, wscale, K, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, ntw, S, reduce, s)
+                 : stream8_dispatch<EPI_NONE, false>(X, ldx, W, wscale, K, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, ntw, S, reduce, s);
 }
 
 int launch_gemm_stream(const uint16_t* X, int ldx, const uint16_t* W, int ldw, const uint16_t* bias,

@@ -34,6 +34,10 @@ int launch_gemm_stream(const uint16_t* X, int ldx, const uint16_t* W, int ldw, c
                        const uint16_t* R, int ldr, void* Y, int ldy, bool out_f32, int epi, float* ws, long ws_elems,
                        int M, int N, int K, int ntw, int S, bool wshuf, int* tickets, long tickets_n, bool reduce,
                        hipStream_t s);
+// decode GEMM with weight-only FP8 (e4m3 pre-shuffled tiles + per-row fp32 scale), bf16 activations
+int launch_gemm_stream8(const uint16_t* X, int ldx, const uint8_t* W, const float* wscale, const uint16_t* bias,
+                        const uint16_t* R, int ldr, void* Y, int ldy, bool out_f32, int epi, float* ws, long ws_elems,
+                        int M, int N, int K, int ntw, int S, bool reduce, hipStream_t s);
 // large-M GEMM on the pre-shuffled layout (256 x bn x 64 LDS-DMA tiles, 8 waves; split-K via ws)
 int launch_gemm_big(const uint16_t* X, int ldx, const uint16_t* W, const uint16_t* bias, const uint16_t* R, int ldr,
                     void* Y, int ldy, bool out_f32, int epi, float* ws, long ws_elems, int M, int N, int K, int bn,

@@ -230,6 +230,9 @@ def _mla_to_hf(c: ModelConfig, lw: "LayerWeights", p: str, sd: Dict[str, torch.T
 
 def _rowmajor(t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
   """Row-major view of a possibly pre-shuffled device weight (2-D, or 3-D expert stacks)."""
+  if t is not None and getattr(t, "xot_layout", "rowmajor") == "stream8":
+    from ..ops.weights_layout import dequant_stream8
+    return dequant_stream8(t, t.xot_scale)
   if t is None or getattr(t, "xot_layout", "rowmajor") != "stream":
     return t
   from ..ops.weights_layout import unshuffle_from_stream
@@ -246,7 +249,7 @@ def expert(t: torch.Tensor, e: int) -> torch.Tensor:
   return v
 
 
-def prepare_for_decode(sw: "ShardWeights", keep_rowmajor: Iterable[str] = ()) -> "ShardWeights":
+def prepare_for_decode(sw: "ShardWeights", keep_rowmajor: Iterable[str] = (), fp8: bool = False) -> "ShardWeights":
   """Convert the projection weights of a GPU shard to the pre-shuffled stream layout (in place).
   The embedding stays row-major (it is gathered); a tied LM head gets its own shuffled copy.
   `keep_rowmajor` names projections ("qkv", "o", "gu", "down") left row-major: at decode batches of
@@ -254,6 +257,7 @@ def prepare_for_decode(sw: "ShardWeights", keep_rowmajor: Iterable[str] = ()) ->
   keeps winning on o / down (tools/bench_gemm_m.py, profiles/bench_gemm_m_*.json)."""
   keep = set(keep_rowmajor)
   from ..ops.weights_layout import can_shuffle, shuffle_for_stream
+  from ..ops.linear import to_stream8_layout
   if sw.embed is not None and not sw.embed.is_cuda:
     return sw
   if sw.lm_head is None and not sw.layers:
@@ -275,16 +279,22 @@ def prepare_for_decode(sw: "ShardWeights", keep_rowmajor: Iterable[str] = ()) ->
     out.xot_layout = "stream"
     return out
 
+  def conv8(t):  # fp8=True: the dense projections become weight-only FP8 (experts, latent and LM head stay bf16)
+    if t is None or not t.is_cuda or t.dim() != 2 or getattr(t, "xot_layout", "rowmajor") != "rowmajor":
+      return conv(t)
+    return to_stream8_layout(t) if can_shuffle(t) else t
+
+  proj = conv8 if fp8 else conv
   for lw in sw.layers.values():
     lw.qb_w, lw.sh_gu_w, lw.sh_down_w = conv(lw.qb_w), conv(lw.sh_gu_w), conv(lw.sh_down_w)
-    if "qkv" not in keep:
-      lw.qkv_w = conv(lw.qkv_w)
-    if "o" not in keep:
-      lw.o_w = conv(lw.o_w)
-    if "gu" not in keep:
-      lw.gu_w = conv(lw.gu_w)
-    if "down" not in keep:
-      lw.down_w = conv(lw.down_w)
+    if "qkv" not in keep or fp8:
+      lw.qkv_w = proj(lw.qkv_w)
+    if "o" not in keep or fp8:
+      lw.o_w = proj(lw.o_w)
+    if "gu" not in keep or fp8:
+      lw.gu_w = proj(lw.gu_w)
+    if "down" not in keep or fp8:
+      lw.down_w = proj(lw.down_w)
   if sw.lm_head is not None:
     sw.lm_head = conv(sw.lm_head)  # a tied head becomes a separate shuffled copy; embed stays row-major
   return sw
@@ -295,6 +305,12 @@ def assign_weight(dst: Optional[torch.Tensor], src: torch.Tensor) -> None:
   """Write a row-major `src` into `dst` IN PLACE, honouring dst's storage layout (pre-shuffled or
   not).  In-place matters: captured HIP graphs hold the addresses of the inference weights."""
   if dst is None:
+    return
+  if getattr(dst, "xot_layout", "rowmajor") == "stream8":  # re-quantize (new row scales, same storage)
+    from ..ops.weights_layout import quantize_fp8_rows, shuffle_for_stream8
+    q, sc = quantize_fp8_rows(src.to(dst.device))
+    dst.copy_(shuffle_for_stream8(q))
+    dst.xot_scale.copy_(sc)
     return
   src = src.to(device=dst.device, dtype=dst.dtype)
   if getattr(dst, "xot_layout", "rowmajor") == "stream":

@@ -26,7 +26,8 @@ import torch
 
 from . import kernels as K
 from ._ext import require
-from .weights_layout import can_shuffle, shuffle_for_stream, unshuffle_from_stream
+from .weights_layout import (can_shuffle, dequant_stream8, quantize_fp8_rows, shuffle_for_stream, shuffle_for_stream8,
+                             unshuffle_from_stream)
 
 
 # XOT_SPLITK_IN_LAUNCH=1: split-K partial sums combined by the last-arriving workgroup of each tile
@@ -61,7 +62,21 @@ def to_stream_layout(w: torch.Tensor) -> torch.Tensor:
   return s
 
 
+def to_stream8_layout(w: torch.Tensor) -> torch.Tensor:
+  """Weight-only FP8 copy of a row-major [N, K] GPU weight: shuffled e4m3 bytes tagged "stream8", the
+  per-row fp32 scales in `.xot_scale`."""
+  if not (w.is_cuda and can_shuffle(w)):
+    return w
+  q, sc = quantize_fp8_rows(w)
+  s = shuffle_for_stream8(q)
+  s.xot_layout = "stream8"
+  s.xot_scale = sc
+  return s
+
+
 def to_rowmajor(w: torch.Tensor) -> torch.Tensor:
+  if layout_of(w) == "stream8":
+    return dequant_stream8(w, w.xot_scale)
   return unshuffle_from_stream(w) if layout_of(w) == "stream" else w
 
 
@@ -158,6 +173,31 @@ class GemmPolicy:
       times.append(st.elapsed_time(en))
     times.sort()
     return times[1]
+
+  def stream8_cfg(self, x, w, bias, residual, epi, out_dtype) -> Tuple:
+    """(ntw, split-K) of the FP8-weight stream GEMM at this M bucket (cold-cache timed once)."""
+    M, Kd = x.shape
+    N = w.shape[0]
+    key = ("s8", _m_bucket(M), N, Kd, epi, bias is not None, str(out_dtype))
+    got = self.table.get(key)
+    if got is not None:
+      return got
+    cands = self._stream_cands(M, N, Kd, epi)
+    if not cands:
+      raise RuntimeError(f"no FP8 stream GEMM configuration for N={N} K={Kd}")
+    if self._no_tuning():
+      return self._heuristic(M, N, [("stream",) + c for c in cands])[1:]
+    scratch.splitk(x.device, max(c[1] * M * N for c in cands))
+    y = torch.empty(M, N // 2 if epi == "silu" else N, dtype=out_dtype, device=x.device)
+    times = {}
+    for cfg in cands:
+      try:
+        times[cfg] = self._time(lambda: _stream8_call(x, w, bias, residual, epi, y, cfg))
+      except RuntimeError:
+        pass
+    got = min(times, key=times.get) if times else cands[0]
+    self.table[key] = got
+    return got
 
   def _no_tuning(self) -> bool:
     return self.capturing or torch.cuda.is_current_stream_capturing()
@@ -289,6 +329,29 @@ def _stream_call(x, w, bias, residual, epi, out, cfg, shuffled: bool = True):
   return out
 
 
+def _stream8_call(x, w, bias, residual, epi, out, cfg):
+  ntw, S = cfg
+  M, N = x.shape[0], w.shape[0]
+  ws = scratch.splitk(x.device, S * M * N) if S > 1 else None
+  require().gemm_stream8(x, w, w.xot_scale, out, bias, residual, ws, K.EPI[epi], ntw, S)
+  return out
+
+
+# FP8 weights: largest M for the FP8 stream GEMM; above it the weight is widened to a bf16 scratch copy
+STREAM8_MAX_M = int(os.environ.get("XOT_STREAM8_MAX_M", "256"))
+
+
+def _linear8(x, w, bias, residual, epi, out, dt):
+  M, N = x.shape[0], w.shape[0]
+  if M > STREAM8_MAX_M:  # compute-bound: widen once per call, then the bf16 library GEMM
+    return _blas(x, dequant_stream8(w, w.xot_scale), bias, residual, epi, out, dt)
+  if out is None:
+    out = torch.empty(M, N // 2 if epi == "silu" else N, dtype=dt, device=x.device)
+  if x.stride(1) != 1 or x.stride(0) % 8:
+    x = x.contiguous()
+  return _stream8_call(x, w, bias, residual, epi, out, policy.stream8_cfg(x, w, bias, residual, epi, dt))
+
+
 def _shuffled_call(x, w, bias, residual, epi, out, cfg):
   if cfg[0] == "blas":
     return _blas(x, scratch.dense_weight(w), bias, residual, epi, out, out.dtype if out is not None else None)
@@ -353,6 +416,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, r
     return K.gemm(x, to_rowmajor(w), bias=bias, residual=residual, epi=epi, out=out, out_dtype=out_dtype)
   dt = out_dtype or (out.dtype if out is not None else x.dtype)
   M, N = x.shape[0], w.shape[0]
+  if layout_of(w) == "stream8":
+    return _linear8(x, w, bias, residual, epi, out, dt)
   if layout_of(w) != "stream":
     impl = policy.choose(x, w, bias, residual, epi, dt)
     return _run_rowmajor(impl, x, w, bias, residual, epi, out, out_dtype)

@@ -7,6 +7,11 @@ i.e. block s is exactly the MFMA 16x16x32 B-operand fragment set of k [32s, 32s+
 wave-instruction (64 lanes x 16 B) then reads 1 KB of contiguous memory, instead of sixteen 64-byte row
 pieces, and a 64-deep k stage of a 16-row group is 2 KB of contiguous memory (one LDS-DMA copy).
 The logical shape stays [N, K]; only the storage order changes.
+
+`shuffle_for_stream8`: the weight-only FP8 variant (OCP e4m3 bytes + one fp32 scale per output row,
+`quantize_fp8_rows`): tiles of 16 rows x 128 k laid out [N/16][K/128][2][lane][16 B], lane (g, c)'s 16
+bytes in half h holding row c, k 64h + 8g .. +8 and 64h + 32 + 8g .. +8 -- two MFMA k-steps per 1 KB wave
+load (gemm_stream with W8, csrc/gemm.hip).
 """
 from __future__ import annotations
 
@@ -28,3 +33,32 @@ def unshuffle_from_stream(ws: torch.Tensor) -> torch.Tensor:
   N, K = ws.shape
   v = ws.reshape(N // 16, K // 128, 4, 4, 16, 8)  # nt, kc, s, g, c, e
   return v.permute(0, 4, 1, 2, 3, 5).contiguous().reshape(N, K)
+
+
+E4M3_MAX = 448.0
+
+
+def quantize_fp8_rows(w: torch.Tensor):
+  """[N, K] -> (e4m3 bits as uint8 [N, K], fp32 scale [N]) with w ~= q * scale[:, None] (row absmax -> 448)."""
+  wf = w.float()
+  scale = (wf.abs().amax(1) / E4M3_MAX).clamp_min(1e-12)
+  q = (wf / scale[:, None]).clamp(-E4M3_MAX, E4M3_MAX).to(torch.float8_e4m3fn)
+  return q.view(torch.uint8), scale
+
+
+def shuffle_for_stream8(q: torch.Tensor) -> torch.Tensor:
+  N, K = q.shape
+  v = q.reshape(N // 16, 16, K // 128, 2, 2, 4, 8)  # nt, c, kc, s', h, g, e  (k = 128kc + 64s' + 32h + 8g + e)
+  return v.permute(0, 2, 3, 5, 1, 4, 6).contiguous().reshape(N, K)
+
+
+def unshuffle_from_stream8(qs: torch.Tensor) -> torch.Tensor:
+  N, K = qs.shape
+  v = qs.reshape(N // 16, K // 128, 2, 4, 16, 2, 8)  # nt, kc, s', g, c, h, e
+  return v.permute(0, 4, 1, 2, 5, 3, 6).contiguous().reshape(N, K)
+
+
+def dequant_stream8(qs: torch.Tensor, scale: torch.Tensor, dtype=torch.bfloat16) -> torch.Tensor:
+  """Row-major [N, K] `dtype` copy of a shuffled FP8 weight."""
+  q = unshuffle_from_stream8(qs).view(torch.float8_e4m3fn)
+  return (q.float() * scale.float()[:, None]).to(dtype)

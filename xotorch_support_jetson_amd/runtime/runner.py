@@ -56,7 +56,10 @@ class ShardRunner:
       env = os.environ.get("XOT_ROWMAJOR_PROJ")
       keep = [p for p in env.split(",") if p] if env is not None else (
           ["gu"] if max_batch > 128 and not config.is_moe else [])  # grouped expert GEMMs want the shuffled layout
-      prepare_for_decode(self.weights, keep_rowmajor=keep)
+      # XOT_WEIGHT_DTYPE=fp8: weight-only e4m3 projections (half the bytes per decode step; opt-in, the
+      # serving default and every benchmark headline stay bf16)
+      self.weight_dtype = os.environ.get("XOT_WEIGHT_DTYPE", "bf16")
+      prepare_for_decode(self.weights, keep_rowmajor=keep, fp8=self.weight_dtype == "fp8")
     n_layers = shard.get_layer_count()
     per_page = KVCache.bytes_per_page(config, n_layers)
     if num_pages is None:
