@@ -77,6 +77,8 @@ def build_parser() -> argparse.ArgumentParser:
   p.add_argument("--schedule", choices=("gpipe", "1f1b"), default="gpipe",
                  help="--ring --parallel pp: micro-batch order (1f1b keeps at most N - rank activations alive)")
   p.add_argument("--no-api", action="store_true", help="Do not start the ChatGPT API on this peer")
+  p.add_argument("--weight-dtype", choices=("bf16", "fp8"), default=None,
+                 help="fp8: weight-only e4m3 dense projections (half the weight bytes per decode step)")
   return p
 
 
@@ -360,6 +362,8 @@ async def async_main(args):
 def run(argv=None):
   argv = list(sys.argv[1:] if argv is None else argv)
   args = build_parser().parse_args(argv)
+  if args.weight_dtype:  # read by every ShardRunner this process (and its spawned peers) builds
+    os.environ["XOT_WEIGHT_DTYPE"] = args.weight_dtype
   if args.ring and args.command in ("train", "eval"):
     from .train.ring_train import run_ring
     sys.exit(run_ring(args))
