@@ -213,7 +213,8 @@ __global__ __launch_bounds__(256, OCC) void gemm_stream_kernel(const uint16_t* _
                                                              int* __restrict__ tickets, long ysplit,
                                                              const float* __restrict__ wscale) {
   constexpr int KC = 32 * KS;
-  static_assert(!W8 || (WSHUF && KS == 4 && MOE == 0), "FP8 weights: pre-shuffled 128-deep chunks, dense GEMM");
+  static_assert(!W8 || (WSHUF && (KS == 4 || KS == 8) && MOE == 0),
+                "FP8 weights: pre-shuffled 128- or 256-deep chunks, dense GEMM");
   constexpr int CPR = KC / 8;  // 16-B chunks per row per k-chunk
   constexpr int NTH = 256;
   constexpr int ROWS = 16 * MT;
@@ -315,7 +316,7 @@ __global__ __launch_bounds__(256, OCC) void gemm_stream_kernel(const uint16_t* _
 #pragma unroll
     for (int j = 0; j < NTW; ++j)
 #pragma unroll
-      for (int s = 0; s < (W8 ? 2 : KS); ++s)
+      for (int s = 0; s < (W8 ? KS / 2 : KS); ++s)
         wr[j][s] = __builtin_nontemporal_load(reinterpret_cast<const s16x8*>(
             W8 ? wp[j] + ch * (8 * KC) + 512 * s : wp[j] + ch * WSTEP + (WSHUF ? 512 * s : 8 * s)));
   };
@@ -652,23 +653,24 @@ static int stream8_dispatch(const uint16_t* X, int ldx, const uint8_t* W8p, cons
   if (ntw == 4 && mt <= 2) ntw = 2;
   if (N % (64 * ntw) != 0 || S < 1 || K % (S * 128) != 0) return -1;
   if (S > 1 && (ws == nullptr || ws_elems < (long)S * M * N)) return -1;
-#define XOT_S8(MTV)                                                                                               \
-  do {                                                                                                            \
-    if (ntw == 1 && EPI != EPI_SILU)                                                                              \
-      stream_launch<MTV, 1, 4, EPI, F32, true, true>(X, ldx, W, K, bias, R, ldr, Y, ldy, ws, M, N, K, S, nullptr,  \
-                                                     reduce, st, wscale);                                          \
-    else if (ntw == 4 && MTV >= 4)                                                                                \
-      stream_launch<MTV, 4, 4, EPI, F32, true, true>(X, ldx, W, K, bias, R, ldr, Y, ldy, ws, M, N, K, S, nullptr,  \
-                                                     reduce, st, wscale);                                          \
-    else                                                                                                          \
-      stream_launch<MTV, 2, 4, EPI, F32, true, true>(X, ldx, W, K, bias, R, ldr, Y, ldy, ws, M, N, K, S, nullptr,  \
-                                                     reduce, st, wscale);                                          \
-    return 0;                                                                                                     \
+#define XOT_S8(MTV, KSV)                                                                                            \
+  do {                                                                                                              \
+    if (ntw == 1 && EPI != EPI_SILU)                                                                                \
+      stream_launch<MTV, 1, KSV, EPI, F32, true, true>(X, ldx, W, K, bias, R, ldr, Y, ldy, ws, M, N, K, S, nullptr,  \
+                                                       reduce, st, wscale);                                          \
+    else if (ntw == 4 && MTV >= 4)                                                                                  \
+      stream_launch<MTV, 4, KSV, EPI, F32, true, true>(X, ldx, W, K, bias, R, ldr, Y, ldy, ws, M, N, K, S, nullptr,  \
+                                                       reduce, st, wscale);                                          \
+    else                                                                                                            \
+      stream_launch<MTV, 2, KSV, EPI, F32, true, true>(X, ldx, W, K, bias, R, ldr, Y, ldy, ws, M, N, K, S, nullptr,  \
+                                                       reduce, st, wscale);                                          \
+    return 0;                                                                                                       \
   } while (0)
-  if (mt <= 1) XOT_S8(1);
-  if (mt <= 2) XOT_S8(2);
-  if (mt <= 4) XOT_S8(4);
-  XOT_S8(8);  // M > 128: 128-row blocks (see stream_dispatch)
+  // (256-deep k-chunks for small M -- the bf16 kernel's bytes in flight per chunk -- measured no faster)
+  if (mt <= 1) XOT_S8(1, 4);
+  if (mt <= 2) XOT_S8(2, 4);
+  if (mt <= 4) XOT_S8(4, 4);
+  XOT_S8(8, 4);  // M > 128: 128-row blocks (see stream_dispatch)
 #undef XOT_S8
 }
 
