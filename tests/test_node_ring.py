@@ -280,3 +280,46 @@ def test_api_concurrent_requests_real_engine(tmp_path):
       await stop_all(nodes)
 
   run(main())
+
+
+def test_engine_decode_loop_matches_node_path(tmp_path, monkeypatch):
+  """A single peer holding the whole model decodes in the engine's loop (continue_locally): same greedy
+  tokens as the per-token Node path, per-request max_tokens honoured, nothing left registered."""
+  import torch
+
+  from xotorch_support_jetson_amd.inference import sharded_engine as se
+
+  async def gen(loop_on):
+    monkeypatch.setattr(se, "ENGINE_LOOP", loop_on)
+    eng = se.ShardedInferenceEngine(NoopShardDownloader(), device=torch.device("cpu"))
+    d = tmp_path / str(loop_on)
+    d.mkdir()
+    nodes = await make_ring(d, ["solo4"], engines=[eng])
+    node = nodes[0]
+    done = {}
+    ev = asyncio.Event()
+
+    def on_token(rid, toks, fin):
+      if fin:
+        done[rid] = list(node.buffered_token_output[rid][0])
+        if len(done) == 4:
+          ev.set()
+    node.on_token.register("t").on_next(on_token)
+    try:
+      base = Shard("tiny-llama", 0, 0, 4)
+      for i in range(4):
+        await node.process_prompt(base, f"prompt number {i} " * (i + 1), request_id=f"q{i}",
+                                  inference_state={"temperature": 0.0, "max_tokens": 4 + i})
+      await asyncio.wait_for(ev.wait(), 60)
+      assert not eng._loops
+      return done, eng.stats
+    finally:
+      await stop_all(nodes)
+
+  on, st_on = run(gen(True))
+  off, _ = run(gen(False))
+  assert on == off
+  for i in range(4):
+    assert len(on[f"q{i}"]) <= 4 + i
+  assert st_on.get("loop_tokens", 0) == sum(len(v) for v in on.values()) - 4  # all but each first token
+  assert st_on.get("presampled", 0) >= st_on["loop_tokens"]  # drawn with their forward

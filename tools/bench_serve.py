@@ -21,15 +21,61 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+PROF = None
+
+
 def free_port():
   with socket.socket() as s:
     s.bind(("127.0.0.1", 0))
     return s.getsockname()[1]
 
 
+async def one(session, url, a, i, max_tokens):
+  words = " ".join(f"w{j % 97}" for j in range(a.prompt_words))
+  text = f"{words} (request {i})" if a.shared_prefix else f"request {i}: {words}"
+  body = {"model": a.model, "stream": True, "max_tokens": max_tokens, "temperature": a.temperature,
+          "messages": [{"role": "user", "content": text}]}
+  t0 = time.perf_counter()
+  ttft, n = None, 0
+  async with session.post(url, json=body) as r:
+    assert r.status == 200, await r.text()
+    async for raw in r.content:
+      line = raw.decode().strip()
+      if not line.startswith("data: ") or line == "data: [DONE]":
+        continue
+      d = json.loads(line[6:])
+      if d["choices"][0].get("delta", {}).get("content") is not None:
+        n += 1
+        if ttft is None:
+          ttft = time.perf_counter() - t0
+  return ttft or 0.0, n, time.perf_counter() - t0
+
+
+async def client_warmup(session, url, a):
+  await one(session, url, a, -1, 4)  # shard load, prefill / decode graph capture, GEMM policy
+  # the measured concurrency once (its batch bucket's graph)
+  await asyncio.gather(*(one(session, url, a, -2 - j, 4) for j in range(a.concurrency)))
+
+
+async def client_main(a):
+  """--client URL: the load generator in its own process (see main)."""
+  from aiohttp import ClientSession
+  loop = asyncio.get_running_loop()
+  async with ClientSession() as session:
+    t0 = time.perf_counter()
+    await client_warmup(session, a.client, a)
+    print("READY", flush=True)
+    print(json.dumps({"warmup_s": time.perf_counter() - t0}), flush=True)
+    await loop.run_in_executor(None, sys.stdin.readline)
+    t0 = time.perf_counter()
+    res = await asyncio.gather(*(one(session, a.client, a, i, a.max_tokens) for i in range(a.concurrency)))
+    wall = time.perf_counter() - t0
+  print(json.dumps({"results": res, "wall_s": wall}), flush=True)
+
+
 async def main(a):
   import torch
-  from aiohttp import ClientSession
+  from aiohttp import ClientSession  # noqa: F401  (in-process clients)
   from aiohttp.test_utils import TestServer
 
   from xotorch_support_jetson_amd.api.chatgpt_api import ChatGPTAPI
@@ -61,39 +107,42 @@ async def main(a):
   server = TestServer(api.app, host="127.0.0.1", port=free_port())
   await server.start_server()
   url = f"http://127.0.0.1:{server.port}/v1/chat/completions"
-  words = " ".join(f"w{i % 97}" for i in range(a.prompt_words))
-
-  async def one(session, i, max_tokens):
-    text = f"{words} (request {i})" if a.shared_prefix else f"request {i}: {words}"
-    body = {"model": a.model, "stream": True, "max_tokens": max_tokens, "temperature": a.temperature,
-            "messages": [{"role": "user", "content": text}]}
-    t0 = time.perf_counter()
-    ttft, n = None, 0
-    async with session.post(url, json=body) as r:
-      assert r.status == 200, await r.text()
-      async for raw in r.content:
-        line = raw.decode().strip()
-        if not line.startswith("data: ") or line == "data: [DONE]":
-          continue
-        d = json.loads(line[6:])
-        if d["choices"][0].get("delta", {}).get("content") is not None:
-          n += 1
-          if ttft is None:
-            ttft = time.perf_counter() - t0
-    return ttft or 0.0, n, time.perf_counter() - t0
-
-  async with ClientSession() as session:
-    t0 = time.perf_counter()
-    await one(session, -1, 4)  # warm-up: shard load, prefill / decode graph capture, GEMM policy
-    for b in (a.concurrency,):  # second warm-up at the measured concurrency (its batch bucket's graph)
-      await asyncio.gather(*(one(session, -2 - j, 4) for j in range(b)))
-    warm = time.perf_counter() - t0
-    t0 = time.perf_counter()
+  if a.client_proc:
+    # the clients run in a child process, as real ones would: parsing 64 SSE streams is no part of the
+    # server's host time.  The child warms up, says READY, waits for GO, runs the measured phase.
+    child = await asyncio.create_subprocess_exec(
+      sys.executable, os.path.abspath(__file__), "--client", url, "--model", a.model, "--concurrency",
+      str(a.concurrency), "--max-tokens", str(a.max_tokens), "--prompt-words", str(a.prompt_words),
+      "--temperature", str(a.temperature), *(["--shared-prefix"] if a.shared_prefix else []),
+      stdin=asyncio.subprocess.PIPE, stdout=asyncio.subprocess.PIPE)
+    line = await child.stdout.readline()
+    assert line.strip() == b"READY", line
+    warm = float(json.loads((await child.stdout.readline()).decode())["warmup_s"])
     s0 = dict(eng.stats)
-    res = await asyncio.gather(*(one(session, i, a.max_tokens) for i in range(a.concurrency)))
-    wall = time.perf_counter() - t0
-    steps = eng.stats["steps"] - s0["steps"]
-    reqs = eng.stats["requests"] - s0["requests"]
+    if PROF is not None:
+      PROF.enable()
+    child.stdin.write(b"GO\n")
+    await child.stdin.drain()
+    d = json.loads((await child.stdout.readline()).decode())
+    if PROF is not None:
+      PROF.disable()
+    await child.wait()
+    res, wall = [tuple(r) for r in d["results"]], d["wall_s"]
+  else:
+    async with ClientSession() as session:
+      t0 = time.perf_counter()
+      await client_warmup(session, url, a)
+      warm = time.perf_counter() - t0
+      s0 = dict(eng.stats)
+      if PROF is not None:  # host-side profile of the measured phase only
+        PROF.enable()
+      t0 = time.perf_counter()
+      res = await asyncio.gather(*(one(session, url, a, i, a.max_tokens) for i in range(a.concurrency)))
+      wall = time.perf_counter() - t0
+      if PROF is not None:
+        PROF.disable()
+  steps = eng.stats["steps"] - s0["steps"]
+  reqs = eng.stats["requests"] - s0["requests"]
   toks = sum(r[1] for r in res)
   ttfts = sorted(r[0] for r in res)
   out = {"metric": "API streaming output tokens/sec (one peer)", "model": a.model, "concurrency": a.concurrency,
@@ -104,15 +153,16 @@ async def main(a):
          "engine_steps": steps, "mean_requests_per_step": round(reqs / max(steps, 1), 1),
          "ms_per_step": round(wall * 1e3 / max(steps, 1), 2),
          "presampled_tokens": eng.stats.get("presampled", 0) - s0.get("presampled", 0),
+         "engine_loop_tokens": eng.stats.get("loop_tokens", 0) - s0.get("loop_tokens", 0),
          "shared_prefix": a.shared_prefix,
          "prefix_cache": dict(eng.prefix_cache.stats) if eng.prefix_cache is not None else None,
          "data": "random-init weights, byte tokenizer, synthetic prompts", "dtype": "bf16",
          "device": caps.chip}
   print(json.dumps(out), flush=True)
-  if os.environ.get("XOT_PROFILE"):
+  if PROF is not None:
     import pstats
-    PROF.disable()
-    pstats.Stats(PROF).sort_stats("tottime").print_stats(25)
+    pstats.Stats(PROF).sort_stats("tottime").print_stats(30)
+    pstats.Stats(PROF).sort_stats("cumulative").print_stats(40)
   await server.close()
   await node.stop()
   sys.stdout.flush()
@@ -129,8 +179,11 @@ if __name__ == "__main__":
   ap.add_argument("--shared-prefix", action="store_true",
                   help="every prompt starts with the same words (a system prompt / earlier turns) and ends with "
                        "the request index, so prompt-prefix KV reuse applies")
-  if os.environ.get("XOT_PROFILE"):  # host-side hot spots of the serving loop
+  ap.add_argument("--in-process-clients", dest="client_proc", action="store_false",
+                  help="run the HTTP clients on the server's event loop (their SSE parsing then counts as server time)")
+  ap.add_argument("--client", default=None, help=argparse.SUPPRESS)  # internal: load-generator child mode
+  if os.environ.get("XOT_PROFILE"):  # host-side hot spots of the serving loop (main thread)
     import cProfile
     PROF = cProfile.Profile()
-    PROF.enable()
-  asyncio.run(main(ap.parse_args()))
+  args = ap.parse_args()
+  asyncio.run(client_main(args) if args.client else main(args))

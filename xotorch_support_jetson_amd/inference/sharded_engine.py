@@ -49,6 +49,8 @@ PRESAMPLE = os.environ.get("XOT_PRESAMPLE", "1") == "1"
 # prompt-prefix KV reuse (inference/prefix_cache.py): on by default, at most this fraction of the KV pool
 PREFIX_CACHE = os.environ.get("XOT_PREFIX_CACHE", "1") == "1"
 PREFIX_CACHE_FRAC = float(os.environ.get("XOT_PREFIX_CACHE_FRAC", "0.25"))
+# single-peer requests decode in the engine's own loop (continue_locally); 0 = one Node round trip per token
+ENGINE_LOOP = os.environ.get("XOT_ENGINE_LOOP", "1") == "1"
 
 
 class ShardedInferenceEngine(InferenceEngine):
@@ -74,6 +76,7 @@ class ShardedInferenceEngine(InferenceEngine):
     self.stats = {"steps": 0, "requests": 0, "tokens": 0}  # batched forward steps (serving diagnostics)
     self._presampled: dict = {}  # (logits ptr, row) -> (temperature, top_k, token) drawn with the forward
     self.prefix_cache = None  # first shard's PrefixCache (built with the runner)
+    self._loops: dict = {}  # request id -> (emit, fail) of requests decoding in the engine loop
 
   # ------------------------------------------------------------------ helpers
   async def _run(self, fn, *args):
@@ -173,6 +176,57 @@ class ShardedInferenceEngine(InferenceEngine):
         off += n
     return out
 
+  # ------------------------------------------------------------------ engine-driven decode loop
+  def continue_locally(self, request_id: str, shard: Shard, token: int, state: dict, emit, fail=None) -> bool:
+    """Take over a request whose every layer is on this peer: its next steps are queued right after each
+    batched forward with the token drawn there (_presample), and `emit(request_id, token) -> finished` is
+    called once per token on the event loop -- instead of a chain of Node coroutines (sample, result
+    handling, forward_tensor, infer_tensor) per request per token, which at 64 concurrent streams cost more
+    host time than the GPU step itself.  Returns False when the engine cannot (then the Node forwards the
+    token as usual)."""
+    if not (ENGINE_LOOP and PRESAMPLE and self.runner is not None and shard == self.shard
+            and shard.is_first_layer() and shard.is_last_layer() and "temperature" in state):
+      return False
+    self._loops[request_id] = (emit, fail)
+    self._queue.append((request_id, shard, np.asarray([[token]], dtype=np.int64), None, state))
+    if not self._draining:
+      self._draining = True
+      asyncio.create_task(self._drain())
+    return True
+
+  async def _loop_results(self, items, results) -> None:
+    """Tokens of the engine-loop requests of one step: report each, queue the next step of the others."""
+    for it, (logits, _) in zip(items, results):
+      rid, shard, _, _, state = it
+      cb = self._loops.get(rid)
+      if cb is None:
+        continue
+      key = self._presample_key(logits) if isinstance(logits, torch.Tensor) else None
+      hit = self._presampled.pop(key, None) if key is not None else None
+      if hit is not None:
+        self.stats["presampled"] = self.stats.get("presampled", 0) + 1
+        tok = int(hit[2].reshape(-1)[0])
+      else:  # not drawn with the forward (should not happen): draw it now
+        tok = int(np.asarray(await self.sample(logits, float(state.get("temperature", TEMPERATURE)),
+                                               int(state.get("top_k") or TOP_K))).reshape(-1)[0])
+      self.stats["loop_tokens"] = self.stats.get("loop_tokens", 0) + 1
+      try:
+        finished = cb[0](rid, tok)
+      except Exception:  # noqa: BLE001 - a failing consumer ends its request, not the loop
+        finished = True
+      if finished:
+        self._loops.pop(rid, None)
+      else:
+        self._queue.append((rid, shard, np.asarray([[tok]], dtype=np.int64), None, state))
+
+  def _loop_failed(self, items, err) -> None:
+    for it in items:
+      cb = self._loops.pop(it[0], None)
+      if cb is not None and cb[1] is not None:
+        if DEBUG >= 1:
+          print(f"[engine] request {it[0]} failed in the decode loop: {err}")
+        cb[1](it[0])
+
   # ------------------------------------------------------------------ prompts with images (LLaVA)
   async def infer_prompt(self, request_id: str, shard: Shard, prompt: str,
                          inference_state: Optional[dict] = None) -> Tuple[object, Optional[dict]]:
@@ -256,19 +310,28 @@ class ShardedInferenceEngine(InferenceEngine):
         batch = self._take_batch()
         ok = [it for it in batch if it[1] == self.shard]
         for it in batch:
-          if it[1] != self.shard and not it[3].done():
-            it[3].set_exception(RuntimeError(f"shard {it[1]} is not loaded on this peer (have {self.shard})"))
+          if it[1] != self.shard:
+            err = RuntimeError(f"shard {it[1]} is not loaded on this peer (have {self.shard})")
+            if it[3] is None:
+              self._loop_failed([it], err)
+            elif not it[3].done():
+              it[3].set_exception(err)
         if not ok:
           continue
+        looped = [it for it in ok if it[3] is None]  # engine-loop steps (continue_locally)
         try:
           results = await self._run(self._infer_batch, [(it[0], it[2], it[4]) for it in ok])
           for it, r in zip(ok, results):
-            if not it[3].done():
+            if it[3] is not None and not it[3].done():
               it[3].set_result(r)
+          if looped:
+            await self._loop_results([it for it in ok if it[3] is None],
+                                     [r for it, r in zip(ok, results) if it[3] is None])
         except Exception as e:  # noqa: BLE001 - delivered to every waiter of the batch
           for it in ok:
-            if not it[3].done():
+            if it[3] is not None and not it[3].done():
               it[3].set_exception(e)
+          self._loop_failed(looped, e)
     finally:
       self._draining = False
 
@@ -366,6 +429,7 @@ class ShardedInferenceEngine(InferenceEngine):
 
   async def finish_request(self, request_id: str) -> None:
     self._images.pop(request_id, None)
+    self._loops.pop(request_id, None)
     if self.runner is not None:
       pc = self.prefix_cache
 

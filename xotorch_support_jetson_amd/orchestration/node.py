@@ -153,39 +153,72 @@ class Node:
       self.request_params[request_id] = p
     return p
 
+  def _max_tokens(self, params: dict) -> int:
+    return min(int(params.get("max_tokens") or self.max_generate_tokens), self.max_generate_tokens)
+
+  def _eos_ids(self) -> set:
+    eos = set(getattr(self.inference_engine, "eos_token_ids", ()) or ())
+    tk = getattr(self.inference_engine, "tokenizer", None)
+    if tk is not None and getattr(tk, "eos_token_id", None) is not None:
+      eos.add(int(tk.eos_token_id))
+    return eos
+
+  def _emit_token(self, request_id: str, tok: int, max_tokens: int, eos: set) -> bool:
+    """Record one sampled token of a request on its last shard: buffer, token callbacks, result broadcast,
+    and the end of the request.  Returns whether the request is finished."""
+    buf = self.buffered_token_output.setdefault(request_id, ([], False))
+    buf[0].append(tok)
+    is_finished = tok in eos or len(buf[0]) >= max_tokens
+    if DEBUG >= 2:
+      print(f"[{request_id}] token {tok} finished={is_finished} n={len(buf[0])}")
+    self.trigger_on_token_callbacks(request_id, [tok], is_finished)
+    if self.peers:
+      asyncio.create_task(self.broadcast_result(request_id, [tok], is_finished))
+    if is_finished:
+      self._finish(request_id)
+    return is_finished
+
+  def _finish(self, request_id: str) -> None:
+    buf = self.buffered_token_output.setdefault(request_id, ([], False))
+    self.buffered_token_output[request_id] = (buf[0], True)
+    self.outstanding_requests.pop(request_id, None)
+    asyncio.create_task(self.broadcast_opaque_status(request_id, json.dumps(
+      {"type": "node_status", "node_id": self.id, "status": "request_finished", "request_id": request_id})))
+
   async def process_inference_result(self, shard: Shard, result, request_id: Optional[str] = None,
                                      inference_state: Optional[dict] = None):
     params = self._params(request_id, inference_state)
-    max_tokens = int(params.get("max_tokens") or self.max_generate_tokens)
-    max_tokens = min(max_tokens, self.max_generate_tokens)
+    max_tokens = self._max_tokens(params)
     buf = self.buffered_token_output.setdefault(request_id, ([], False))
     is_finished = len(buf[0]) >= max_tokens
     forward = result
-    intermediate: List[int] = []
     if shard.is_last_layer() and not is_finished:
       temp = params.get("temperature")
       temp = self.default_sample_temperature if temp is None else float(temp)
       token = await self.inference_engine.sample(result, temp=temp, top_k=int(params.get("top_k") or 35))
       tok = int(np.asarray(token).reshape(-1)[0])
-      buf[0].append(tok)
-      eos = set(getattr(self.inference_engine, "eos_token_ids", ()) or ())
-      tk = getattr(self.inference_engine, "tokenizer", None)
-      if tk is not None and getattr(tk, "eos_token_id", None) is not None:
-        eos.add(int(tk.eos_token_id))
-      is_finished = tok in eos or len(buf[0]) >= max_tokens
+      eos = self._eos_ids()
+      is_finished = self._emit_token(request_id, tok, max_tokens, eos)
       forward = np.asarray([[tok]], dtype=np.int64)
-      intermediate = [tok]
-      if DEBUG >= 2:
-        print(f"[{request_id}] token {tok} finished={is_finished} n={len(buf[0])}")
-    if shard.is_last_layer():
-      self.trigger_on_token_callbacks(request_id, intermediate, is_finished)
-      asyncio.create_task(self.broadcast_result(request_id, intermediate, is_finished))
+      if not is_finished and shard.is_first_layer():
+        # this peer holds the whole model: hand the request to the engine's decode loop, which runs its next
+        # steps back to back and reports each token here (no per-token coroutine chain through the Node)
+        loop = getattr(self.inference_engine, "continue_locally", None)
+        state = dict(inference_state or {})
+        state.update(params)
+        state.setdefault("temperature", temp)
+        if loop is not None and loop(request_id, shard, tok, state,
+                                     lambda rid, t: self._emit_token(rid, t, max_tokens, eos), self._finish):
+          self.outstanding_requests[request_id] = "processing"
+          return np.array(buf[0])
+    elif shard.is_last_layer():  # already at max_tokens
+      self.trigger_on_token_callbacks(request_id, [], True)
+      if self.peers:
+        asyncio.create_task(self.broadcast_result(request_id, [], True))
+      self._finish(request_id)
     if is_finished:
       self.buffered_token_output[request_id] = (buf[0], True)
       self.outstanding_requests.pop(request_id, None)
-      if shard.is_last_layer():
-        asyncio.create_task(self.broadcast_opaque_status(request_id, json.dumps(
-          {"type": "node_status", "node_id": self.id, "status": "request_finished", "request_id": request_id})))
     else:
       self.outstanding_requests[request_id] = "waiting"
       state = dict(inference_state or {})
