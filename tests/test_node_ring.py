@@ -323,3 +323,50 @@ def test_engine_decode_loop_matches_node_path(tmp_path, monkeypatch):
     assert len(on[f"q{i}"]) <= 4 + i
   assert st_on.get("loop_tokens", 0) == sum(len(v) for v in on.values()) - 4  # all but each first token
   assert st_on.get("presampled", 0) >= st_on["loop_tokens"]  # drawn with their forward
+
+
+def test_engine_loop_consumer_ends_request_early():
+  """Pipelined engine loop: the next step is queued before a token is emitted (on the `stop` prediction).
+  When the consumer ends a request the prediction did not (a cancelled stream), the queued step is dropped,
+  at most the one already running computes for it, and nothing stays registered."""
+  import torch
+
+  from xotorch_support_jetson_amd.inference import sharded_engine as se
+
+  async def main():
+    eng = se.ShardedInferenceEngine(NoopShardDownloader(), device=torch.device("cpu"))
+    shard = Shard("tiny-llama", 0, 3, 4)
+    await eng.ensure_shard(shard)
+    got = {"a": [], "b": []}
+    ended = asyncio.Event()
+    steps_after_end = []
+
+    def emit(rid, tok):
+      got[rid].append(tok)
+      if rid == "a" and len(got["a"]) == 3:  # consumer stops "a" early; the prediction said go on
+        steps_after_end.append(eng.stats["steps"])
+        return True
+      if rid == "b" and len(got["b"]) == 8:
+        ended.set()
+        return True
+      return False
+
+    state = {"temperature": 0.0, "top_k": 35}
+    for rid in ("a", "b"):
+      logits, _ = await eng.infer_tensor(rid, shard, np.asarray([[1, 2, 3, 4]], dtype=np.int64), state)
+      tok = int(np.asarray(await eng.sample(logits, 0.0, 35)).reshape(-1)[0])
+      assert eng.continue_locally(rid, shard, tok, dict(state), emit, stop=lambda r, t: False)
+    await asyncio.wait_for(ended.wait(), 60)
+    for _ in range(50):
+      if not eng._draining:
+        break
+      await asyncio.sleep(0.01)
+    assert not eng._loops and not eng._queue
+    assert len(got["a"]) == 3 and len(got["b"]) == 8
+    # "a" ran its emitted steps plus at most the one in flight when it ended
+    assert eng.runner.num_tokens("a") <= 4 + 3 + 1
+    await eng.finish_request("a")
+    await eng.finish_request("b")
+    assert not eng.runner.has("a") and not eng.runner.has("b")
+
+  run(main())

@@ -59,9 +59,11 @@ async def client_warmup(session, url, a):
 
 async def client_main(a):
   """--client URL: the load generator in its own process (see main)."""
-  from aiohttp import ClientSession
+  from aiohttp import ClientSession, TCPConnector
   loop = asyncio.get_running_loop()
-  async with ClientSession() as session:
+  # limit=0: aiohttp's default connector caps a session at 100 open connections, which silently
+  # turned every concurrency above 100 into 100 streams
+  async with ClientSession(connector=TCPConnector(limit=0)) as session:
     t0 = time.perf_counter()
     await client_warmup(session, a.client, a)
     print("READY", flush=True)
@@ -75,7 +77,7 @@ async def client_main(a):
 
 async def main(a):
   import torch
-  from aiohttp import ClientSession  # noqa: F401  (in-process clients)
+  from aiohttp import ClientSession, TCPConnector  # noqa: F401  (in-process clients)
   from aiohttp.test_utils import TestServer
 
   from xotorch_support_jetson_amd.api.chatgpt_api import ChatGPTAPI
@@ -129,7 +131,7 @@ async def main(a):
     await child.wait()
     res, wall = [tuple(r) for r in d["results"]], d["wall_s"]
   else:
-    async with ClientSession() as session:
+    async with ClientSession(connector=TCPConnector(limit=0)) as session:
       t0 = time.perf_counter()
       await client_warmup(session, url, a)
       warm = time.perf_counter() - t0

@@ -344,7 +344,7 @@ class ChatGPTAPI:
         first = True
         try:
           while True:
-            tokens, finished = await asyncio.wait_for(self.token_queues[request_id].get(), timeout=self.response_timeout)
+            tokens, finished = await self._next_tokens(self.token_queues[request_id])
             if first and tokens:
               first = False
               metrics.AVAILABLE and metrics.TTFT.labels(req.model).observe(time.perf_counter() - t_start)
@@ -364,7 +364,7 @@ class ChatGPTAPI:
           return web.json_response({"detail": "Response generation timed out"}, status=408)
       tokens: List[int] = []
       while True:
-        new, finished = await asyncio.wait_for(self.token_queues[request_id].get(), timeout=self.response_timeout)
+        new, finished = await self._next_tokens(self.token_queues[request_id])
         tokens.extend(new)
         if finished:
           break
@@ -429,11 +429,25 @@ class ChatGPTAPI:
     return web.json_response(tracer.export(int(request.query.get("limit", 1000))))
 
   # ------------------------------------------------------------------ token fan-in
-  async def handle_tokens(self, request_id: str, tokens: List[int], is_finished: bool):
+  def handle_tokens(self, request_id: str, tokens: List[int], is_finished: bool):
+    """Token callback (plain function: runs inside the emitter's call, no task per token)."""
     q = self.token_queues.get(request_id)
     if q is not None:
       tracer.on_token(request_id, len(tokens))
-      await q.put((list(tokens), is_finished))
+      q.put_nowait((list(tokens), is_finished))
+
+  async def _next_tokens(self, q: asyncio.Queue):
+    """Every token chunk queued for a request, merged: (tokens, finished).  Waits (with the response
+    timeout) only when nothing is queued, so a stream that fell behind catches up in one write."""
+    try:
+      toks, fin = q.get_nowait()
+    except asyncio.QueueEmpty:
+      toks, fin = await asyncio.wait_for(q.get(), timeout=self.response_timeout)
+    toks = list(toks)
+    while not fin and not q.empty():
+      more, fin = q.get_nowait()
+      toks.extend(more)
+    return toks, fin
 
   async def run(self, host: str = "0.0.0.0", port: int = 52415):
     runner = web.AppRunner(self.app)

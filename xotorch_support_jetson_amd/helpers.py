@@ -48,11 +48,17 @@ class AsyncCallback(Generic[T]):
     self._cond = asyncio.Condition()
     self.result: Optional[Tuple[T, ...]] = None
     self.observers: List[Callable[..., Any]] = []
+    self._waiters = 0  # coroutines inside wait(): set() schedules a notify only for them
 
   async def wait(self, predicate: Callable[..., bool], timeout: Optional[float] = None) -> Tuple[T, ...]:
-    async with self._cond:
-      await asyncio.wait_for(self._cond.wait_for(lambda: self.result is not None and predicate(*self.result)), timeout)
-      return self.result  # type: ignore[return-value]
+    self._waiters += 1
+    try:
+      async with self._cond:
+        await asyncio.wait_for(self._cond.wait_for(lambda: self.result is not None and predicate(*self.result)),
+                               timeout)
+        return self.result  # type: ignore[return-value]
+    finally:
+      self._waiters -= 1
 
   def on_next(self, fn: Callable[..., Any]) -> None:
     self.observers.append(fn)
@@ -63,6 +69,8 @@ class AsyncCallback(Generic[T]):
       out = fn(*args)
       if asyncio.iscoroutine(out):  # async observers are scheduled on the running loop
         asyncio.get_running_loop().create_task(out)
+    if not self._waiters:
+      return  # nobody in wait(): no notify task (set() runs once per generated token)
     try:
       asyncio.get_running_loop().create_task(self._notify())
     except RuntimeError:

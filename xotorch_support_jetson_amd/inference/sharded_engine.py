@@ -75,6 +75,7 @@ class ShardedInferenceEngine(InferenceEngine):
     self._sampling = False
     self.stats = {"steps": 0, "requests": 0, "tokens": 0}  # batched forward steps (serving diagnostics)
     self._presampled: dict = {}  # (logits ptr, row) -> (temperature, top_k, token) drawn with the forward
+    self._presampled_prev: dict = {}  # the step before's (the next step may start before its readers sample)
     self.prefix_cache = None  # first shard's PrefixCache (built with the runner)
     self._loops: dict = {}  # request id -> (emit, fail) of requests decoding in the engine loop
 
@@ -96,9 +97,11 @@ class ShardedInferenceEngine(InferenceEngine):
     sampler launch, one device-to-host copy), for requests whose state carries their sampling
     parameters (the Node forwards temperature / top_k with every step).  sample() then returns the
     stored token without another trip through the executor."""
-    # tokens of the previous step nobody asked for (finished requests) go: a lagging request still holds its
-    # logits view, so no new tensor can reuse that base address and collide with a fresh key
-    self._presampled.clear()
+    # tokens of the step before last nobody asked for (finished requests) go; the last step's stay one more
+    # step, since with the pipelined engine loop this step may have started before that step's Node-path
+    # readers sampled.  A lagging request still holds its logits view, so no new tensor can reuse that base
+    # address and collide with a fresh key
+    self._presampled_prev, self._presampled = self._presampled, {}
     if not PRESAMPLE or not states or any("temperature" not in st for st in states):
       return
     from ..ops import kernels as K
@@ -118,9 +121,13 @@ class ShardedInferenceEngine(InferenceEngine):
     is returned at once; otherwise concurrent calls (the requests of one batched step) are drawn
     together: one sampler launch over their stacked logits and one device-to-host copy, instead of a
     launch + synchronisation per request."""
-    if isinstance(x, torch.Tensor) and x.dim() == 2 and x.shape[0] == 1 and self._presampled:
+    if isinstance(x, torch.Tensor) and x.dim() == 2 and x.shape[0] == 1 and (self._presampled or self._presampled_prev):
       key = self._presample_key(x)
-      hit = self._presampled.pop(key, None) if key is not None else None
+      hit = None
+      if key is not None:
+        hit = self._presampled.pop(key, None)
+        if hit is None:
+          hit = self._presampled_prev.pop(key, None)
       if hit is not None and hit[0] == float(temp) and hit[1] == int(top_k):
         self.stats["presampled"] = self.stats.get("presampled", 0) + 1
         return hit[2]
@@ -177,25 +184,30 @@ class ShardedInferenceEngine(InferenceEngine):
     return out
 
   # ------------------------------------------------------------------ engine-driven decode loop
-  def continue_locally(self, request_id: str, shard: Shard, token: int, state: dict, emit, fail=None) -> bool:
+  def continue_locally(self, request_id: str, shard: Shard, token: int, state: dict, emit, fail=None,
+                       stop=None) -> bool:
     """Take over a request whose every layer is on this peer: its next steps are queued right after each
     batched forward with the token drawn there (_presample), and `emit(request_id, token) -> finished` is
     called once per token on the event loop -- instead of a chain of Node coroutines (sample, result
     handling, forward_tensor, infer_tensor) per request per token, which at 64 concurrent streams cost more
-    host time than the GPU step itself.  Returns False when the engine cannot (then the Node forwards the
-    token as usual)."""
+    host time than the GPU step itself.  `stop(request_id, token) -> bool` predicts emit's answer without
+    side effects; with it the next step is queued and launched BEFORE the step's tokens are emitted, so the
+    token callbacks (SSE writes of every stream) run while the GPU computes the next step.  Returns False
+    when the engine cannot (then the Node forwards the token as usual)."""
     if not (ENGINE_LOOP and PRESAMPLE and self.runner is not None and shard == self.shard
             and shard.is_first_layer() and shard.is_last_layer() and "temperature" in state):
       return False
-    self._loops[request_id] = (emit, fail)
+    self._loops[request_id] = (emit, fail, stop)
     self._queue.append((request_id, shard, np.asarray([[token]], dtype=np.int64), None, state))
     if not self._draining:
       self._draining = True
       asyncio.create_task(self._drain())
     return True
 
-  async def _loop_results(self, items, results) -> None:
-    """Tokens of the engine-loop requests of one step: report each, queue the next step of the others."""
+  async def _loop_next(self, items, results) -> list:
+    """Tokens of the engine-loop requests of one step.  Requests whose `stop` predicts they go on are queued
+    for the next step at once; returns the (request, token, queued) emissions to make."""
+    out = []
     for it, (logits, _) in zip(items, results):
       rid, shard, _, _, state = it
       cb = self._loops.get(rid)
@@ -210,14 +222,34 @@ class ShardedInferenceEngine(InferenceEngine):
         tok = int(np.asarray(await self.sample(logits, float(state.get("temperature", TEMPERATURE)),
                                                int(state.get("top_k") or TOP_K))).reshape(-1)[0])
       self.stats["loop_tokens"] = self.stats.get("loop_tokens", 0) + 1
+      queued = False
+      if cb[2] is not None:
+        try:
+          queued = not cb[2](rid, tok)
+        except Exception:  # noqa: BLE001 - no prediction: emit first, queue after
+          queued = False
+        if queued:
+          self._queue.append((rid, shard, np.asarray([[tok]], dtype=np.int64), None, state))
+      out.append((it, tok, queued))
+    return out
+
+  def _emit(self, emissions) -> None:
+    """Report the tokens of one step (see _loop_next); reconcile requests the consumer ended differently."""
+    for it, tok, queued in emissions:
+      rid = it[0]
+      cb = self._loops.get(rid)
+      if cb is None:
+        continue
       try:
         finished = cb[0](rid, tok)
       except Exception:  # noqa: BLE001 - a failing consumer ends its request, not the loop
         finished = True
       if finished:
         self._loops.pop(rid, None)
-      else:
-        self._queue.append((rid, shard, np.asarray([[tok]], dtype=np.int64), None, state))
+        if queued:  # still waiting in the queue: drop it (one already cut into a step is skipped by rid)
+          self._queue = [q for q in self._queue if not (q[0] == rid and q[3] is None)]
+      elif not queued:
+        self._queue.append((rid, it[1], np.asarray([[tok]], dtype=np.int64), None, it[4]))
 
   def _loop_failed(self, items, err) -> None:
     for it in items:
@@ -303,37 +335,70 @@ class ShardedInferenceEngine(InferenceEngine):
       prev = n
       await asyncio.sleep(0)
 
+  def _launch(self):
+    """Cut the next step from the queue and start it on the executor: (future, items, engine-loop items),
+    or None when nothing in the cut can run."""
+    batch = self._take_batch()
+    ok = []
+    for it in batch:
+      if it[3] is None and it[0] not in self._loops:
+        continue  # an engine-loop request that ended after its step was queued
+      if it[1] != self.shard:
+        err = RuntimeError(f"shard {it[1]} is not loaded on this peer (have {self.shard})")
+        if it[3] is None:
+          self._loop_failed([it], err)
+        elif not it[3].done():
+          it[3].set_exception(err)
+        continue
+      ok.append(it)
+    if not ok:
+      return None
+    fut = asyncio.get_running_loop().run_in_executor(self.executor, self._infer_batch,
+                                                     [(it[0], it[2], it[4]) for it in ok])
+    return fut, ok, [it for it in ok if it[3] is None]
+
   async def _drain(self):
+    """Step loop.  While only engine-loop requests are waiting, step N+1 is launched before step N's
+    tokens are emitted (host work overlaps the GPU); a step that carried Node-path requests first lets
+    their follow-ups queue (_settle), so one decode round stays one forward pass."""
+    pending = None
     try:
-      while self._queue:
-        await self._settle()
-        batch = self._take_batch()
-        ok = [it for it in batch if it[1] == self.shard]
-        for it in batch:
-          if it[1] != self.shard:
-            err = RuntimeError(f"shard {it[1]} is not loaded on this peer (have {self.shard})")
-            if it[3] is None:
-              self._loop_failed([it], err)
-            elif not it[3].done():
-              it[3].set_exception(err)
-        if not ok:
-          continue
-        looped = [it for it in ok if it[3] is None]  # engine-loop steps (continue_locally)
+      while self._queue or pending is not None:
+        if pending is None:
+          await self._settle()
+          pending = self._launch()
+          if pending is None:
+            continue
+        fut, ok, looped = pending
+        pending = None
         try:
-          results = await self._run(self._infer_batch, [(it[0], it[2], it[4]) for it in ok])
-          for it, r in zip(ok, results):
-            if it[3] is not None and not it[3].done():
-              it[3].set_result(r)
-          if looped:
-            await self._loop_results([it for it in ok if it[3] is None],
-                                     [r for it, r in zip(ok, results) if it[3] is None])
+          results = await fut
         except Exception as e:  # noqa: BLE001 - delivered to every waiter of the batch
           for it in ok:
             if it[3] is not None and not it[3].done():
               it[3].set_exception(e)
           self._loop_failed(looped, e)
+          continue
+        node_path = False
+        for it, r in zip(ok, results):
+          if it[3] is not None:
+            node_path = True
+            if not it[3].done():
+              it[3].set_result(r)
+        emissions = []
+        if looped:
+          emissions = await self._loop_next(looped, [r for it, r in zip(ok, results) if it[3] is None])
+        if self._queue and not node_path:
+          pending = self._launch()
+        self._emit(emissions)
     finally:
       self._draining = False
+      if pending is not None:  # left abnormally with a step in flight: its waiters get an error, not a hang
+        err = RuntimeError("engine step loop stopped")
+        for it in pending[1]:
+          if it[3] is not None and not it[3].done():
+            it[3].set_exception(err)
+        self._loop_failed(pending[2], err)
 
   def _infer_batch(self, items):
     self.stats["steps"] += 1

@@ -207,8 +207,11 @@ class Node:
         state = dict(inference_state or {})
         state.update(params)
         state.setdefault("temperature", temp)
+        def stop(rid: str, t: int) -> bool:  # would _emit_token(rid, t) end the request? (no side effects)
+          return t in eos or len(self.buffered_token_output.get(rid, ((),))[0]) + 1 >= max_tokens
         if loop is not None and loop(request_id, shard, tok, state,
-                                     lambda rid, t: self._emit_token(rid, t, max_tokens, eos), self._finish):
+                                     lambda rid, t: self._emit_token(rid, t, max_tokens, eos), self._finish,
+                                     stop=stop):
           self.outstanding_requests[request_id] = "processing"
           return np.array(buf[0])
     elif shard.is_last_layer():  # already at max_tokens
