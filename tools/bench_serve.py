@@ -154,6 +154,10 @@ async def main(a):
          "per_request_tok_s_p50": round(sorted(r[1] / r[2] for r in res)[len(res) // 2], 2),
          "engine_steps": steps, "mean_requests_per_step": round(reqs / max(steps, 1), 1),
          "ms_per_step": round(wall * 1e3 / max(steps, 1), 2),
+         # time inside the engine's step call (host prep + GPU + token copy), vs. ms_per_step of wall time
+         "engine_ms_per_step": round((eng.stats.get("step_s", 0.0) - s0.get("step_s", 0.0)) * 1e3 / max(steps, 1), 2),
+         **{f"engine_{k}_ms_per_step": round((eng.stats.get(f"{k}_s", 0.0) - s0.get(f"{k}_s", 0.0)) * 1e3 / max(steps, 1), 2)
+            for k in ("launch", "wait")},
          "presampled_tokens": eng.stats.get("presampled", 0) - s0.get("presampled", 0),
          "engine_loop_tokens": eng.stats.get("loop_tokens", 0) - s0.get("loop_tokens", 0),
          "shared_prefix": a.shared_prefix,
@@ -188,4 +192,6 @@ if __name__ == "__main__":
     import cProfile
     PROF = cProfile.Profile()
   args = ap.parse_args()
+  if os.environ.get("XOT_SWITCH_INTERVAL_US"):  # diagnostic: CPython's GIL hand-off interval (default 5000 us)
+    sys.setswitchinterval(float(os.environ["XOT_SWITCH_INTERVAL_US"]) * 1e-6)
   asyncio.run(client_main(args) if args.client else main(args))

@@ -437,12 +437,13 @@ class ChatGPTAPI:
       q.put_nowait((list(tokens), is_finished))
 
   async def _next_tokens(self, q: asyncio.Queue):
-    """Every token chunk queued for a request, merged: (tokens, finished).  Waits (with the response
-    timeout) only when nothing is queued, so a stream that fell behind catches up in one write."""
+    """Every token chunk queued for a request, merged: (tokens, finished), so a stream that fell behind
+    catches up in one write.  No per-token wait_for (a task per token): timeout_middleware already bounds
+    the whole request by the response timeout."""
     try:
       toks, fin = q.get_nowait()
     except asyncio.QueueEmpty:
-      toks, fin = await asyncio.wait_for(q.get(), timeout=self.response_timeout)
+      toks, fin = await q.get()
     toks = list(toks)
     while not fin and not q.empty():
       more, fin = q.get_nowait()

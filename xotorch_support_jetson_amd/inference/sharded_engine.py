@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import asyncio
 import os
+import time
 from concurrent.futures import ThreadPoolExecutor
 from pathlib import Path
 from typing import Optional, Tuple
@@ -77,7 +78,7 @@ class ShardedInferenceEngine(InferenceEngine):
     self._presampled: dict = {}  # (logits ptr, row) -> (temperature, top_k, token) drawn with the forward
     self._presampled_prev: dict = {}  # the step before's (the next step may start before its readers sample)
     self.prefix_cache = None  # first shard's PrefixCache (built with the runner)
-    self._loops: dict = {}  # request id -> (emit, fail) of requests decoding in the engine loop
+    self._loops: dict = {}  # request id -> (emit, fail, stop) of requests decoding in the engine loop
 
   # ------------------------------------------------------------------ helpers
   async def _run(self, fn, *args):
@@ -91,6 +92,30 @@ class ShardedInferenceEngine(InferenceEngine):
   async def decode(self, shard: Shard, tokens: np.ndarray) -> str:
     await self.ensure_shard(shard)
     return self.tokenizer.decode(np.asarray(tokens).reshape(-1).tolist())
+
+  def _seed(self, dev: torch.device) -> torch.Tensor:
+    """[seed, offset] for the sampler on `dev`, advanced after each use by _advance_seed.  On a GPU it lives
+    on the device (advanced by a tiny kernel), so a sampler launch never waits on a host-to-device copy."""
+    if dev.type != "cuda":
+      return self.seed_off
+    t = getattr(self, "_seed_dev", None)
+    if t is None or t.device != dev:
+      t = self._seed_dev = self.seed_off.to(dev)
+    return t
+
+  def _advance_seed(self, dev: torch.device) -> None:
+    self.seed_off[1] += 1
+    if dev.type == "cuda":
+      self._seed(dev)[1:].add_(1)
+
+  @staticmethod
+  def _temps(values: list, dev: torch.device) -> torch.Tensor:
+    """Per-row temperatures on `dev` without a blocking copy (one fill kernel when they are all equal)."""
+    if dev.type != "cuda":
+      return torch.tensor(values, dtype=torch.float32)
+    if all(v == values[0] for v in values):
+      return torch.full((len(values),), values[0], dtype=torch.float32, device=dev)
+    return torch.tensor(values, dtype=torch.float32).pin_memory().to(dev, non_blocking=True)
 
   def _presample(self, logits: torch.Tensor, states: list) -> None:
     """Last shard: draw the step's tokens right after its forward, in the same executor call (one
@@ -109,10 +134,12 @@ class ShardedInferenceEngine(InferenceEngine):
     for i, st in enumerate(states):
       groups.setdefault(int(st.get("top_k") or TOP_K), []).append(i)
     for k, idx in groups.items():
-      sel = logits if len(idx) == logits.shape[0] else logits[torch.tensor(idx, device=logits.device)]
-      temps = torch.tensor([float(states[i]["temperature"]) for i in idx], dtype=torch.float32, device=logits.device)
-      tok = K.sample(sel.contiguous(), temps, k, self.seed_off.to(logits.device)).cpu().numpy().astype(np.int64)
-      self.seed_off[1] += 1
+      dev = logits.device
+      sel = logits if len(idx) == logits.shape[0] else logits[torch.tensor(idx).to(dev, non_blocking=True)]
+      temps = self._temps([float(states[i]["temperature"]) for i in idx], dev)
+      tok = K.sample(sel.contiguous(), temps, k, self._seed(dev))
+      self._advance_seed(dev)
+      tok = tok.cpu().numpy().astype(np.int64)  # the step's one blocking point
       for j, i in enumerate(idx):
         self._presampled[(logits.data_ptr(), i)] = (float(states[i]["temperature"]), k, tok[j:j + 1])
 
@@ -171,11 +198,10 @@ class ShardedInferenceEngine(InferenceEngine):
     for k in sorted({k for _, _, k in items}):  # one launch per distinct top_k (usually one)
       idx = [i for i, it in enumerate(items) if it[2] == k]
       logits = torch.cat([rows[i].to(self.device, torch.float32) for i in idx]).contiguous()
-      temps = torch.tensor([items[i][1] for i in idx for _ in range(rows[i].shape[0])], dtype=torch.float32,
-                           device=self.device)
-      so = self.seed_off.to(self.device)
-      tok = K.sample(logits, temps, k, so).cpu().numpy().astype(np.int64)
-      self.seed_off[1] += 1
+      temps = self._temps([items[i][1] for i in idx for _ in range(rows[i].shape[0])], self.device)
+      tok = K.sample(logits, temps, k, self._seed(self.device))
+      self._advance_seed(self.device)
+      tok = tok.cpu().numpy().astype(np.int64)
       off = 0
       for i in idx:
         n = rows[i].shape[0]
@@ -208,18 +234,17 @@ class ShardedInferenceEngine(InferenceEngine):
     """Tokens of the engine-loop requests of one step.  Requests whose `stop` predicts they go on are queued
     for the next step at once; returns the (request, token, queued) emissions to make."""
     out = []
-    for it, (logits, _) in zip(items, results):
+    for it, (logits, row) in zip(items, results):  # (step logits [B, V], this request's row)
       rid, shard, _, _, state = it
       cb = self._loops.get(rid)
       if cb is None:
         continue
-      key = self._presample_key(logits) if isinstance(logits, torch.Tensor) else None
-      hit = self._presampled.pop(key, None) if key is not None else None
+      hit = self._presampled.pop((logits.data_ptr(), row), None)
       if hit is not None:
         self.stats["presampled"] = self.stats.get("presampled", 0) + 1
-        tok = int(hit[2].reshape(-1)[0])
+        tok = int(hit[2][0])
       else:  # not drawn with the forward (should not happen): draw it now
-        tok = int(np.asarray(await self.sample(logits, float(state.get("temperature", TEMPERATURE)),
+        tok = int(np.asarray(await self.sample(logits[row:row + 1], float(state.get("temperature", TEMPERATURE)),
                                                int(state.get("top_k") or TOP_K))).reshape(-1)[0])
       self.stats["loop_tokens"] = self.stats.get("loop_tokens", 0) + 1
       queued = False
@@ -354,7 +379,7 @@ class ShardedInferenceEngine(InferenceEngine):
     if not ok:
       return None
     fut = asyncio.get_running_loop().run_in_executor(self.executor, self._infer_batch,
-                                                     [(it[0], it[2], it[4]) for it in ok])
+                                                     [(it[0], it[2], it[4], it[3] is None) for it in ok])
     return fut, ok, [it for it in ok if it[3] is None]
 
   async def _drain(self):
@@ -401,6 +426,13 @@ class ShardedInferenceEngine(InferenceEngine):
         self._loop_failed(pending[2], err)
 
   def _infer_batch(self, items):
+    t0 = time.perf_counter()
+    try:
+      return self._infer_batch_impl(items)
+    finally:
+      self.stats["step_s"] = self.stats.get("step_s", 0.0) + time.perf_counter() - t0
+
+  def _infer_batch_impl(self, items):
     self.stats["steps"] += 1
     self.stats["requests"] += len(items)
     if self.trainer is not None and self.trainer.dirty:
@@ -408,24 +440,24 @@ class ShardedInferenceEngine(InferenceEngine):
     rids, qlens, xs, pc_ops = [], [], [], []
     pc = self.prefix_cache
     for rid, inp, *rest in items:
-      state = rest[0] if rest else {}
+      state = (rest[0] if rest else None) or {}
       ops = None
-      x = inp if isinstance(inp, torch.Tensor) else torch.as_tensor(np.asarray(inp))
-      if x.dim() == 3:  # hidden [1, L, D]
+      if (inp.dim() if isinstance(inp, torch.Tensor) else np.ndim(inp)) == 3:  # hidden [1, L, D]
         from .prefix_cache import apply_ops
-        apply_ops(self.runner.bm, rid, (state or {}).get("pc"))  # the first shard's prefix-cache operations
+        apply_ops(self.runner.bm, rid, state.get("pc"))  # the first shard's prefix-cache operations
+        x = inp if isinstance(inp, torch.Tensor) else torch.as_tensor(np.asarray(inp))
         L = x.shape[1]
         xs.append(x.reshape(L, x.shape[2]).to(torch.bfloat16))
-      else:  # token ids [1, L]
-        ids = x.reshape(-1).to(torch.int32)
+      else:  # token ids [1, L]: numpy on the host (no per-request tensor ops; one tensor for the step)
+        ids = (inp.detach().cpu().numpy() if isinstance(inp, torch.Tensor) else np.asarray(inp)).reshape(-1)
         if pc is not None and rid not in self._images:
           ops = {}
-          if not self.runner.has(rid) and ids.numel() > 1:
+          if ids.size > 1 and not self.runner.has(rid):
             n, eid = pc.on_prompt(rid, ids.tolist())
             if n:
               ids = ids[n:]
               ops["fork"] = [eid, n]
-          elif self.runner.has(rid) and ids.numel() == 1:
+          elif ids.size == 1 and self.runner.has(rid):
             save = pc.on_decode(rid)
             if save is not None:
               ops["save"] = save
@@ -433,7 +465,7 @@ class ShardedInferenceEngine(InferenceEngine):
           if drops:
             ops["drop"] = drops
         xs.append(ids)
-        L = ids.numel()
+        L = int(ids.size)
       rids.append(rid)
       qlens.append(L)
       pc_ops.append(ops or None)
@@ -445,8 +477,12 @@ class ShardedInferenceEngine(InferenceEngine):
     if self._images and self.shard.is_first_layer():
       feats = [self.runner.image_features(self._images.pop(rid)) for rid in rids if rid in self._images]
       image_embeds = torch.cat(feats) if feats else None
+    t_prep = time.perf_counter()
     try:
-      x = torch.cat(xs)
+      if all(isinstance(t, np.ndarray) for t in xs):
+        x = torch.from_numpy(np.concatenate(xs).astype(np.int32, copy=False))
+      else:
+        x = torch.cat([torch.from_numpy(t.astype(np.int32)) if isinstance(t, np.ndarray) else t for t in xs])
       if sum(qlens) > MAX_STEP_TOKENS and len(rids) == 1:
         out = self._forward_chunked(rids[0], x, image_embeds)
       else:
@@ -461,9 +497,16 @@ class ShardedInferenceEngine(InferenceEngine):
       # a decode step's logits live in its HIP graph's static buffer, which the next step of the same batch
       # bucket overwrites, possibly before every request of this step has sampled
       out = out.clone()
+      t_launched = time.perf_counter()
       self._presample(out, [it[2] if len(it) > 2 else {} for it in items])
-      for i, rid in enumerate(rids):
-        res.append((out[i:i + 1], {"n_past": self.runner.num_tokens(rid)}))
+      st = self.stats
+      st["launch_s"] = st.get("launch_s", 0.0) + t_launched - t_prep  # host prep + kernel / graph launch
+      st["wait_s"] = st.get("wait_s", 0.0) + time.perf_counter() - t_launched  # sampler + the token copy
+      for i, (rid, it) in enumerate(zip(rids, items)):
+        if len(it) > 3 and it[3]:  # engine-loop request: (logits, row) -- no view, no state to ship
+          res.append((out, i))
+        else:
+          res.append((out[i:i + 1], {"n_past": self.runner.num_tokens(rid)}))
       return res
     off = 0
     outc = out.cpu()
