@@ -322,7 +322,9 @@ def test_engine_decode_loop_matches_node_path(tmp_path, monkeypatch):
   for i in range(4):
     assert len(on[f"q{i}"]) <= 4 + i
   assert st_on.get("loop_tokens", 0) == sum(len(v) for v in on.values()) - 4  # all but each first token
-  assert st_on.get("presampled", 0) >= st_on["loop_tokens"]  # drawn with their forward
+  # drawn with their forward: in a chained step (ids handed to the next step on the device) or presampled
+  assert st_on.get("presampled", 0) + st_on.get("chained_tokens", 0) >= st_on["loop_tokens"]
+  assert st_on.get("chained", 0) > 0
 
 
 def test_engine_loop_consumer_ends_request_early():

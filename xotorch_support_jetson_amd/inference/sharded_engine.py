@@ -52,6 +52,9 @@ PREFIX_CACHE = os.environ.get("XOT_PREFIX_CACHE", "1") == "1"
 PREFIX_CACHE_FRAC = float(os.environ.get("XOT_PREFIX_CACHE_FRAC", "0.25"))
 # single-peer requests decode in the engine's own loop (continue_locally); 0 = one Node round trip per token
 ENGINE_LOOP = os.environ.get("XOT_ENGINE_LOOP", "1") == "1"
+# engine-loop decode steps chained on the device: step N+1 takes step N's sampled ids straight from device
+# memory and is queued before step N's tokens reach the host (no GPU idle gap between decode steps)
+CHAIN = os.environ.get("XOT_CHAIN", "1") == "1"
 
 
 class ShardedInferenceEngine(InferenceEngine):
@@ -276,6 +279,123 @@ class ShardedInferenceEngine(InferenceEngine):
       elif not queued:
         self._queue.append((rid, it[1], np.asarray([[tok]], dtype=np.int64), None, it[4]))
 
+  # ------------------------------------------------------------------ chained engine-loop steps
+  def _chainable(self) -> bool:
+    """The waiting work is engine-loop decode steps only (one token each, one sampler top_k)."""
+    if not (CHAIN and self.runner is not None and self._queue):
+      return False
+    ks = set()
+    for it in self._queue:
+      if it[3] is not None or it[1] != self.shard or self._qlen(it[2]) != 1:
+        return False
+      ks.add(int(it[4].get("top_k") or TOP_K))
+    return len(ks) == 1
+
+  def _plan(self, chain) -> tuple:
+    """Next chained step: rows of the running step whose requests go on (by the count-only prediction:
+    a request that will have hit its token limit with the running step's token is left out), then queued
+    engine-loop requests (host tokens), up to max_batch.  An EOS in the running step is only seen after
+    the next step is queued: that request's extra step is discarded."""
+    cont = []
+    if chain is not None:
+      for row, rid in enumerate(chain["rids"]):
+        cb = self._loops.get(rid)
+        if cb is None:
+          continue
+        try:
+          last = cb[2](rid, -1) if cb[2] is not None else False
+        except Exception:  # noqa: BLE001
+          last = True
+        if not last:
+          cont.append((rid, row))
+    k = int(chain["states"][0].get("top_k") or TOP_K) if chain is not None and chain["rids"] else None
+    room = self.runner.max_batch - len(cont)
+    new, rest = [], []
+    seen = {rid for rid, _ in cont}
+    for it in self._queue:
+      ok = (it[3] is None and it[0] in self._loops and it[0] not in seen and self._qlen(it[2]) == 1
+            and (k is None or int(it[4].get("top_k") or TOP_K) == k))
+      if ok and len(new) < room:
+        new.append(it)
+        seen.add(it[0])
+      elif it[3] is not None or it[0] in self._loops:
+        rest.append(it)
+    self._queue = rest
+    return cont, new
+
+  def _chain_step(self, chain, cont, new):
+    """Executor: queue one engine-loop decode step whose inputs are the running step's sampled ids (rows
+    `cont`, gathered on the device) and the host tokens of `new`; queue its sampler; then read the running
+    step's tokens on the host, which overlaps the new step's GPU work.  Returns (the running step's tokens
+    as int64 numpy or None, the new running step or None)."""
+    t0 = time.perf_counter()
+    nxt = None
+    try:
+      if cont or new:
+        dev = self.runner.device
+        rids = [r for r, _ in cont] + [it[0] for it in new]
+        states = [chain["states"][row] for _, row in cont] + [it[4] for it in new]
+        parts = []
+        if cont:
+          rows = [row for _, row in cont]
+          if rows == list(range(len(chain["rids"]))):
+            parts.append(chain["tok"])
+          else:
+            idx = torch.tensor(rows, dtype=torch.int64)
+            parts.append(chain["tok"].index_select(0, (idx.pin_memory() if dev.type == "cuda" else idx)
+                                                   .to(dev, non_blocking=True)))
+        if new:
+          ids = torch.tensor([int(np.asarray(it[2]).reshape(-1)[0]) for it in new], dtype=torch.int32)
+          parts.append((ids.pin_memory() if dev.type == "cuda" else ids).to(dev, non_blocking=True))
+        x = parts[0] if len(parts) == 1 else torch.cat(parts)
+        pc = self.prefix_cache
+        if pc is not None:
+          for rid in rids:
+            pc.on_decode(rid)
+            pc.outgoing_drops(rid)
+          need = sum(self.runner.bm.blocks_needed(r, 1) for r in rids)
+          if need > self.runner.bm.num_free:
+            pc.evict(need)
+        if self.trainer is not None and self.trainer.dirty:
+          self.trainer.sync_to_inference()
+        from ..ops import kernels as K
+        logits = self.runner.forward(rids, [1] * len(rids), x)
+        temps = self._temps([float(st["temperature"]) for st in states], dev)
+        tok = K.sample(logits, temps, int(states[0].get("top_k") or TOP_K), self._seed(dev))
+        self._advance_seed(dev)
+        nxt = {"rids": rids, "states": states, "tok": tok}
+        self.stats["steps"] += 1
+        self.stats["requests"] += len(rids)
+        self.stats["chained"] = self.stats.get("chained", 0) + 1
+      prev = chain["tok"].cpu().numpy().astype(np.int64) if chain is not None else None
+      return prev, nxt
+    finally:
+      self.stats["step_s"] = self.stats.get("step_s", 0.0) + time.perf_counter() - t0
+
+  def _emit_chain(self, chain, toks) -> None:
+    """Report a finished chained step's tokens.  A request the prediction left out of the next step but
+    the consumer did not end goes back to the queue with its host token."""
+    nxt_rows = None
+    for row, rid in enumerate(chain["rids"]):
+      cb = self._loops.get(rid)
+      if cb is None:
+        continue
+      tok = int(toks[row])
+      self.stats["loop_tokens"] = self.stats.get("loop_tokens", 0) + 1
+      self.stats["chained_tokens"] = self.stats.get("chained_tokens", 0) + 1
+      try:
+        finished = cb[0](rid, tok)
+      except Exception:  # noqa: BLE001 - a failing consumer ends its request, not the loop
+        finished = True
+      if finished:
+        self._loops.pop(rid, None)
+        self._queue = [q for q in self._queue if not (q[0] == rid and q[3] is None)]
+      else:
+        if nxt_rows is None:
+          nxt_rows = chain.get("next_rids", set())
+        if rid not in nxt_rows:
+          self._queue.append((rid, self.shard, np.asarray([[tok]], dtype=np.int64), None, chain["states"][row]))
+
   def _loop_failed(self, items, err) -> None:
     for it in items:
       cb = self._loops.pop(it[0], None)
@@ -387,8 +507,28 @@ class ShardedInferenceEngine(InferenceEngine):
     tokens are emitted (host work overlaps the GPU); a step that carried Node-path requests first lets
     their follow-ups queue (_settle), so one decode round stays one forward pass."""
     pending = None
+    chain = None  # chained engine-loop step running on the device (see _chain_step)
+    loop = asyncio.get_running_loop()
     try:
-      while self._queue or pending is not None:
+      while self._queue or pending is not None or chain is not None:
+        if pending is None and (chain is not None or self._chainable()):
+          if chain is None or not self._queue or self._chainable():
+            cont, new = self._plan(chain)
+            if chain is None and not new:
+              continue
+          else:  # Node-path work is waiting: finish the running chained step, then step normally
+            cont, new = [], []
+          running = chain
+          try:
+            toks, chain = await loop.run_in_executor(self.executor, self._chain_step, running, cont, new)
+          except Exception as e:  # noqa: BLE001
+            self._loop_failed([(r,) for r in (running["rids"] if running else [])] + new, e)
+            chain = None
+            continue
+          if running is not None:
+            running["next_rids"] = set(chain["rids"]) if chain is not None else set()
+            self._emit_chain(running, toks)
+          continue
         if pending is None:
           await self._settle()
           pending = self._launch()
@@ -413,11 +553,13 @@ class ShardedInferenceEngine(InferenceEngine):
         emissions = []
         if looped:
           emissions = await self._loop_next(looped, [r for it, r in zip(ok, results) if it[3] is None])
-        if self._queue and not node_path:
+        if self._queue and not node_path and not self._chainable():
           pending = self._launch()
         self._emit(emissions)
     finally:
       self._draining = False
+      if chain is not None:
+        self._loop_failed([(r,) for r in chain["rids"]], RuntimeError("engine step loop stopped"))
       if pending is not None:  # left abnormally with a step in flight: its waiters get an error, not a hang
         err = RuntimeError("engine step loop stopped")
         for it in pending[1]:

@@ -83,10 +83,17 @@ class ShardRunner:
     self._graphs: Dict[int, dict] = {}
     self._tables_host = torch.zeros(max_batch, self.width, dtype=torch.int32)
     self._ctx_host = torch.zeros(max_batch, dtype=torch.int32)
+    bmax = _bucket(max_batch)
+    self._pos_host = torch.zeros(bmax, dtype=torch.int32)  # decode-step positions / slots (graph inputs)
+    self._slots_host = torch.zeros(bmax, dtype=torch.int64)
     self._staged = None  # event marking completion of the last async H2D copy out of the pinned buffers
     if self.device.type == "cuda":
+      # pinned: an async copy out of pageable memory may wait for the stream to drain, i.e. for the step
+      # already running, which would forbid queueing the next decode step behind it
       self._tables_host = self._tables_host.pin_memory()
       self._ctx_host = self._ctx_host.pin_memory()
+      self._pos_host = self._pos_host.pin_memory()
+      self._slots_host = self._slots_host.pin_memory()
 
   def _reuse_staging(self) -> None:
     """The pinned staging buffers may still be read by an in-flight async copy: wait for it."""
@@ -188,8 +195,10 @@ class ShardRunner:
       pos += self.model.rope_pos(start, 1)
     self.bm.fill_batch(list(rids), self._tables_host[:B].numpy(), self._ctx_host[:B].numpy())
     pad = Bp - B
-    g["pos"].copy_(torch.tensor(pos + [0] * pad, dtype=torch.int32), non_blocking=True)
-    g["slots"].copy_(torch.tensor(slots + [-1] * pad, dtype=torch.int64), non_blocking=True)
+    self._pos_host[:Bp] = torch.tensor(pos + [0] * pad, dtype=torch.int32)
+    self._slots_host[:Bp] = torch.tensor(slots + [-1] * pad, dtype=torch.int64)
+    g["pos"].copy_(self._pos_host[:Bp], non_blocking=True)
+    g["slots"].copy_(self._slots_host[:Bp], non_blocking=True)
     self._ctx_host[B:Bp] = 0
     g["tables"].copy_(self._tables_host[:Bp], non_blocking=True)
     g["ctx"].copy_(self._ctx_host[:Bp], non_blocking=True)
