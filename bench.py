@@ -28,6 +28,10 @@ def log(*a):
   print(*a, file=sys.stderr, flush=True)
 
 
+def cfg_name(model: str) -> str:
+  return {"llama-3-70b": "Llama-3-70B"}.get(model, model)
+
+
 def sync():
   if torch.cuda.is_available():
     torch.cuda.synchronize()
@@ -136,7 +140,7 @@ def main():
       "scaling": "weak",
       "vs_baseline": None,
       "dtype": "bf16" if args.weight_dtype == "bf16" else "bf16 activations, fp8-e4m3 weights (NOT the headline)",
-      "data": "synthetic prompts, random-init weights (exact Llama-3-70B architecture)",
+      "data": f"synthetic prompts, random-init weights (exact {cfg_name(args.model)} architecture)",
       "config": {
         "model": args.model if not args.layers else f"{args.model}-TRUNCATED-{args.layers}L-INVALID",
         "global_batch": M * B,
