@@ -372,3 +372,45 @@ def test_engine_loop_consumer_ends_request_early():
     assert not eng.runner.has("a") and not eng.runner.has("b")
 
   run(main())
+
+
+def test_engine_loop_mixed_top_k_all_finish():
+  """Chained engine-loop steps share one sampler top_k: a request with another top_k waiting in the queue
+  makes the running chain finish so the queue is served normally -- every request completes."""
+  import torch
+
+  from xotorch_support_jetson_amd.inference import sharded_engine as se
+
+  async def main():
+    eng = se.ShardedInferenceEngine(NoopShardDownloader(), device=torch.device("cpu"))
+    shard = Shard("tiny-llama", 0, 3, 4)
+    await eng.ensure_shard(shard)
+    want = {"a": 12, "b": 5, "c": 7}
+    got = {r: [] for r in want}
+    done = asyncio.Event()
+
+    def emit(rid, tok):
+      got[rid].append(tok)
+      fin = len(got[rid]) >= want[rid]
+      if all(len(got[r]) >= want[r] for r in want):
+        done.set()
+      return fin
+
+    def stop(rid, tok):
+      return len(got[rid]) + 1 >= want[rid]
+
+    for rid, k in (("a", 35), ("b", 1), ("c", 35)):
+      state = {"temperature": 0.7, "top_k": k}
+      logits, _ = await eng.infer_tensor(rid, shard, np.asarray([[3, 1, 4, 1, 5]], dtype=np.int64), state)
+      tok = int(np.asarray(await eng.sample(logits, 0.7, k)).reshape(-1)[0])
+      assert eng.continue_locally(rid, shard, tok, dict(state), emit, stop=stop)
+      await asyncio.sleep(0)
+    await asyncio.wait_for(done.wait(), 60)
+    for _ in range(50):
+      if not eng._draining:
+        break
+      await asyncio.sleep(0.01)
+    assert {r: len(v) for r, v in got.items()} == want
+    assert not eng._loops and not eng._queue
+
+  run(main())

@@ -280,11 +280,12 @@ class ShardedInferenceEngine(InferenceEngine):
         self._queue.append((rid, it[1], np.asarray([[tok]], dtype=np.int64), None, it[4]))
 
   # ------------------------------------------------------------------ chained engine-loop steps
-  def _chainable(self) -> bool:
-    """The waiting work is engine-loop decode steps only (one token each, one sampler top_k)."""
+  def _chainable(self, k: Optional[int] = None) -> bool:
+    """The waiting work is engine-loop decode steps only (one token each) sharing one sampler top_k (the
+    running chained step's, when given)."""
     if not (CHAIN and self.runner is not None and self._queue):
       return False
-    ks = set()
+    ks = set() if k is None else {k}
     for it in self._queue:
       if it[3] is not None or it[1] != self.shard or self._qlen(it[2]) != 1:
         return False
@@ -512,11 +513,12 @@ class ShardedInferenceEngine(InferenceEngine):
     try:
       while self._queue or pending is not None or chain is not None:
         if pending is None and (chain is not None or self._chainable()):
-          if chain is None or not self._queue or self._chainable():
+          k = int(chain["states"][0].get("top_k") or TOP_K) if chain is not None else None
+          if not self._queue or self._chainable(k):
             cont, new = self._plan(chain)
             if chain is None and not new:
               continue
-          else:  # Node-path work is waiting: finish the running chained step, then step normally
+          else:  # other work is waiting (Node-path steps, another top_k): finish the chained step first
             cont, new = [], []
           running = chain
           try:
