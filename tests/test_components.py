@@ -192,3 +192,22 @@ def test_network_topology_config(tmp_path):
     NetworkTopology.from_path(str(missing))
   with pytest.raises(FileNotFoundError):
     NetworkTopology.from_path(str(tmp_path / "nope.json"))
+
+
+def test_stream_chunks_match_generate_completion():
+  """The streaming fast path encodes chunks byte-identical to json.dumps(generate_completion(...))."""
+  import json as _json
+  from unittest import mock
+
+  from xotorch_support_jetson_amd.api.chatgpt_api import (ChatCompletionRequest, Message, StreamChunks,
+                                                           generate_completion)
+  from xotorch_support_jetson_amd.inference.tokenizers import _resolve_tokenizer
+
+  tok = _resolve_tokenizer("byte", 512)
+  req = ChatCompletionRequest("llama-3.2-1b", [Message("user", "hi")], 0.6)
+  enc = StreamChunks(req, tok, "rid-1")
+  with mock.patch("time.time", return_value=1700000000.5):
+    for toks, fr in (([72, 105], None), ([], "length"), ([34, 92, 10], "stop"), ([0xe4, 0xbd, 0xa0], None)):
+      want = "data: " + _json.dumps(generate_completion(req, tok, "p", "rid-1", toks, True, fr,
+                                                        "chat.completion.chunk")) + "\n\n"
+      assert enc.line(toks, fr) == want.encode()

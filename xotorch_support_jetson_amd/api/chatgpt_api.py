@@ -151,6 +151,25 @@ def generate_completion(req: ChatCompletionRequest, tokenizer, prompt: str, requ
   return comp
 
 
+class StreamChunks:
+  """SSE `data:` lines of one streaming chat completion, byte-identical to json.dumps of
+  generate_completion(..., stream=True, object_type="chat.completion.chunk"): the request's constant JSON is
+  encoded once and only the token text (and finish reason) is escaped per chunk -- this runs once per
+  generated token per stream."""
+
+  def __init__(self, req: ChatCompletionRequest, tokenizer, request_id: str):
+    self.tokenizer = tokenizer
+    self.head = '{"id": ' + json.dumps(f"chatcmpl-{request_id}") + ', "object": "chat.completion.chunk", "created": '
+    self.mid = (', "model": ' + json.dumps(req.model) + ', "system_fingerprint": ' + json.dumps(f"xot_{VERSION}")
+                + ', "choices": [{"index": 0, "logprobs": null, "finish_reason": ')
+
+  def line(self, tokens: List[int], finish_reason: Optional[str]) -> bytes:
+    text = self.tokenizer.decode(tokens)
+    fr = "null" if finish_reason is None else json.dumps(finish_reason)
+    return ("data: " + self.head + str(int(time.time())) + self.mid + fr
+            + ', "delta": {"role": "assistant", "content": ' + json.dumps(text) + "}}]}\n\n").encode()
+
+
 class ChatGPTAPI:
   def __init__(self, node, inference_engine_classname: str, response_timeout: int = 900,
                on_chat_completion_request=None, default_model: Optional[str] = None,
@@ -342,19 +361,21 @@ class ChatGPTAPI:
                                                                    "Access-Control-Allow-Origin": "*"})
         await resp.prepare(request)
         first = True
+        chunks = StreamChunks(req, tok, request_id)
+        counter = metrics.TOKENS.labels(req.model) if metrics.AVAILABLE else None
+        q = self.token_queues[request_id]
         try:
           while True:
-            tokens, finished = await self._next_tokens(self.token_queues[request_id])
+            tokens, finished = await self._next_tokens(q)
             if first and tokens:
               first = False
               metrics.AVAILABLE and metrics.TTFT.labels(req.model).observe(time.perf_counter() - t_start)
-            metrics.AVAILABLE and metrics.TOKENS.labels(req.model).inc(len(tokens))
+            if counter is not None:
+              counter.inc(len(tokens))
             eos_hit = finished and tokens and tokens[-1] in eos
             emit = tokens[:-1] if eos_hit else tokens
             finish_reason = ("stop" if eos_hit else "length") if finished else None
-            chunk = generate_completion(req, tok, prompt, request_id, list(emit), True, finish_reason,
-                                        "chat.completion.chunk")
-            await resp.write(f"data: {json.dumps(chunk)}\n\n".encode())
+            await resp.write(chunks.line(list(emit), finish_reason))
             if finished:
               break
           await resp.write(b"data: [DONE]\n\n")
