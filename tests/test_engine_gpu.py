@@ -183,3 +183,66 @@ def test_prefix_cache_gpu(gpu, model):
     assert torch.corrcoef(torch.stack([x, y]))[0, 1] > 0.999
 
   asyncio.run(main())
+
+
+def test_engine_loop_chained_gpu(gpu):
+  """Engine-driven decode loop on the GPU -- device-chained steps (sampled ids handed to the next step in
+  device memory, graph replay), requests joining a running chain and ending at different steps: greedy
+  tokens equal the step-by-step path of a fresh engine."""
+  from xotorch_support_jetson_amd.inference import sharded_engine as se
+
+  async def main():
+    s = Shard(MODEL, 0, N - 1, N)
+    rng = np.random.default_rng(5)
+    lens, want = (5, 40, 130, 9, 64, 300), (6, 11, 3, 17, 8, 12)
+    prompts = [rng.integers(0, 500, size=(1, L)) for L in lens]
+
+    ref_e = ShardedInferenceEngine(NoopShardDownloader(), device=gpu)
+    ref = []
+    for i, p in enumerate(prompts):
+      out, _ = await ref_e.infer_tensor(f"r{i}", s, p)
+      t = int(torch.as_tensor(out).float().argmax())
+      toks = []
+      for _ in range(want[i]):
+        out, _ = await ref_e.infer_tensor(f"r{i}", s, np.array([[t]]))
+        t = int(torch.as_tensor(out).float().argmax())
+        toks.append(t)
+      ref.append(toks)
+
+    e = ShardedInferenceEngine(NoopShardDownloader(), device=gpu)
+    got = {i: [] for i in range(len(prompts))}
+    done = asyncio.Event()
+
+    def emit(rid, tok):
+      i = int(rid[1:])
+      got[i].append(tok)
+      if all(len(got[j]) >= want[j] for j in got):
+        done.set()
+      return len(got[i]) >= want[i]
+
+    def stop(rid, tok):
+      i = int(rid[1:])
+      return len(got[i]) + 1 >= want[i]
+
+    async def start(i):
+      state = {"temperature": 0.0, "top_k": 35}
+      logits, _ = await e.infer_tensor(f"c{i}", s, prompts[i], state)
+      t = int(np.asarray(await e.sample(logits, 0.0, 35)).reshape(-1)[0])
+      assert e.continue_locally(f"c{i}", s, t, dict(state), emit, stop=stop)
+
+    await start(0)
+    await start(1)
+    await asyncio.sleep(0.05)  # the others join while a chain is running
+    await asyncio.gather(*(start(i) for i in range(2, len(prompts))))
+    await asyncio.wait_for(done.wait(), 120)
+    assert e.stats.get("chained", 0) > 0
+    same = sum(got[i] == ref[i] for i in range(len(prompts)))
+    assert same >= len(prompts) - 1, (same, ref, got)  # bf16 batch-composition rounding may flip a near-tie
+    for _ in range(100):
+      if not e._draining:
+        break
+      await asyncio.sleep(0.01)
+    assert not e._loops and not e._queue
+    assert se.CHAIN
+
+  asyncio.run(main())
