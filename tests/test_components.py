@@ -211,3 +211,48 @@ def test_stream_chunks_match_generate_completion():
       want = "data: " + _json.dumps(generate_completion(req, tok, "p", "rid-1", toks, True, fr,
                                                         "chat.completion.chunk")) + "\n\n"
       assert enc.line(toks, fr) == want.encode()
+
+
+def test_direct_sse_framing_and_fallback():
+  """Direct SSE writes: each token's chunk is HTTP/1.1-chunk framed onto the transport; a slow reader (full
+  socket buffer) sends the stream back to the queue path without losing or reordering tokens."""
+  import asyncio as _asyncio
+
+  from xotorch_support_jetson_amd.api import chatgpt_api as ca
+  from xotorch_support_jetson_amd.inference.tokenizers import _resolve_tokenizer
+
+  class FakeTransport:
+    def __init__(self):
+      self.out, self.buffered = [], 0
+
+    def write(self, b):
+      self.out.append(b)
+
+    def is_closing(self):
+      return False
+
+    def get_write_buffer_size(self):
+      return self.buffered
+
+  async def main():
+    tok = _resolve_tokenizer("byte", 512)
+    req = ca.ChatCompletionRequest("m", [ca.Message("user", "x")], 0.0)
+    chunks = ca.StreamChunks(req, tok, "r")
+    api = ca.ChatGPTAPI.__new__(ca.ChatGPTAPI)  # only the token fan-in state
+    api.token_queues, api._direct = {"r": _asyncio.Queue()}, {}
+    t = FakeTransport()
+    d = ca._DirectStream(t, chunks, {2}, None, lambda: None)
+    api._direct["r"] = d
+    api.handle_tokens("r", [72], False)
+    api.handle_tokens("r", [105], False)
+    line = chunks.line([72], None)
+    assert t.out[0] == b"%x\r\n" % len(line) + line + b"\r\n"
+    assert len(t.out) == 2 and api.token_queues["r"].empty()
+    t.buffered = ca.DIRECT_SSE_MAX_BUFFER + 1  # the reader stalls
+    api.handle_tokens("r", [33], False)
+    api.handle_tokens("r", [2], True)
+    assert d.fallback and d.done.done() and "r" not in api._direct and len(t.out) == 2
+    q = api.token_queues["r"]
+    assert [q.get_nowait(), q.get_nowait()] == [([33], False), ([2], True)]
+
+  _asyncio.run(main())

@@ -170,6 +170,42 @@ class StreamChunks:
             + ', "delta": {"role": "assistant", "content": ' + json.dumps(text) + "}}]}\n\n").encode()
 
 
+# XOT_DIRECT_SSE=0: every streamed token goes through the request's queue and wakes its handler task
+DIRECT_SSE = os.environ.get("XOT_DIRECT_SSE", "1") == "1"
+# above this many bytes waiting in a stream's socket buffer (a slow reader) its tokens go back to the queue path
+DIRECT_SSE_MAX_BUFFER = 1 << 20
+
+
+class _DirectStream:
+  """One streaming response fed straight from the token callback: each token's SSE chunk is framed (HTTP/1.1
+  chunked encoding, which the response was prepared with) and handed to the connection's transport inside
+  the emitter's call -- no queue hop and no handler-task wake-up per token, which at hundreds of streams was
+  the serving loop's largest host cost.  The handler task only waits for `done`."""
+
+  def __init__(self, transport, chunks: "StreamChunks", eos: set, counter, on_first):
+    self.transport, self.chunks, self.eos, self.counter, self.on_first = transport, chunks, eos, counter, on_first
+    self.done = asyncio.get_running_loop().create_future()
+    self.first = True
+    self.fallback = False  # set when the stream went back to the queue path
+
+  def usable(self) -> bool:
+    t = self.transport
+    return not t.is_closing() and t.get_write_buffer_size() <= DIRECT_SSE_MAX_BUFFER
+
+  def feed(self, tokens: List[int], finished: bool) -> None:
+    if self.first and tokens:
+      self.first = False
+      self.on_first()
+    if self.counter is not None:
+      self.counter.inc(len(tokens))
+    eos_hit = finished and tokens and tokens[-1] in self.eos
+    emit = tokens[:-1] if eos_hit else tokens
+    line = self.chunks.line(list(emit), ("stop" if eos_hit else "length") if finished else None)
+    self.transport.write(b"%x\r\n%s\r\n" % (len(line), line))
+    if finished and not self.done.done():
+      self.done.set_result(None)
+
+
 class ChatGPTAPI:
   def __init__(self, node, inference_engine_classname: str, response_timeout: int = 900,
                on_chat_completion_request=None, default_model: Optional[str] = None,
@@ -181,6 +217,7 @@ class ChatGPTAPI:
     self.default_model = default_model or "llama-3.2-1b"
     self.system_prompt = system_prompt
     self.token_queues: Dict[str, asyncio.Queue] = {}
+    self._direct: Dict[str, _DirectStream] = {}  # streaming requests fed straight from the token callback
     self.prompts: Dict[str, dict] = {}
     self.app = web.Application(client_max_size=100 * 1024 * 1024, middlewares=[self.timeout_middleware,
                                                                                self.log_request, self.cors_middleware])
@@ -359,12 +396,34 @@ class ChatGPTAPI:
         resp = web.StreamResponse(status=200, reason="OK", headers={"Content-Type": "text/event-stream",
                                                                    "Cache-Control": "no-cache",
                                                                    "Access-Control-Allow-Origin": "*"})
+        resp.enable_chunked_encoding()
         await resp.prepare(request)
         first = True
         chunks = StreamChunks(req, tok, request_id)
         counter = metrics.TOKENS.labels(req.model) if metrics.AVAILABLE else None
         q = self.token_queues[request_id]
-        try:
+        transport = request.transport
+        if DIRECT_SSE and transport is not None and getattr(resp, "chunked", False):
+          def on_first():
+            metrics.AVAILABLE and metrics.TTFT.labels(req.model).observe(time.perf_counter() - t_start)
+          d = _DirectStream(transport, chunks, eos, counter, on_first)
+          finished = False
+          while not q.empty() and not finished:  # tokens that arrived before this point, in order
+            toks, finished = q.get_nowait()
+            d.feed(toks, finished)
+          if not finished:
+            self._direct[request_id] = d
+            try:
+              await d.done
+            finally:
+              self._direct.pop(request_id, None)
+            finished = not d.fallback
+          first = d.first
+          if finished:
+            await resp.write(b"data: [DONE]\n\n")
+            await resp.write_eof()
+            return resp
+        try:  # queue path (also where a direct stream continues after a fallback)
           while True:
             tokens, finished = await self._next_tokens(q)
             if first and tokens:
@@ -452,9 +511,21 @@ class ChatGPTAPI:
   # ------------------------------------------------------------------ token fan-in
   def handle_tokens(self, request_id: str, tokens: List[int], is_finished: bool):
     """Token callback (plain function: runs inside the emitter's call, no task per token)."""
+    d = self._direct.get(request_id)
+    if d is not None:
+      tracer.on_token(request_id, len(tokens))
+      if d.usable():
+        d.feed(tokens, is_finished)
+        return
+      # slow reader or closing connection: back to the queue path (the handler's direct wait ends)
+      self._direct.pop(request_id, None)
+      d.fallback = True
+      if not d.done.done():
+        d.done.set_result(None)
     q = self.token_queues.get(request_id)
     if q is not None:
-      tracer.on_token(request_id, len(tokens))
+      if d is None:
+        tracer.on_token(request_id, len(tokens))
       q.put_nowait((list(tokens), is_finished))
 
   async def _next_tokens(self, q: asyncio.Queue):
