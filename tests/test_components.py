@@ -256,3 +256,25 @@ def test_direct_sse_framing_and_fallback():
     assert [q.get_nowait(), q.get_nowait()] == [([33], False), ([2], True)]
 
   _asyncio.run(main())
+
+
+def test_gemm_policy_table_persists(tmp_path, monkeypatch):
+  """Tuned GEMM choices round-trip through the on-disk table (tuples restored, atomic writes), and a new
+  policy object starts from it instead of re-timing."""
+  from xotorch_support_jetson_amd.ops import linear as L
+
+  path = tmp_path / "g" / "table.json"
+  monkeypatch.setenv("XOT_GEMM_TABLE", str(path))
+  p = L.GemmPolicy()
+  key = ("sh", 512, 8192, 8192, "resid", False, "torch.bfloat16")
+  assert p._lookup(key) is None
+  p._store(key, ("big", 128, 2))
+  p._store(("rm", 1, 64, 64, "none", False), "blas")
+  assert path.exists() and not list(path.parent.glob("*.tmp"))
+  q = L.GemmPolicy()
+  assert q._lookup(key) == ("big", 128, 2)
+  assert q._lookup(("rm", 1, 64, 64, "none", False)) == "blas"
+  path.write_text("{not json")
+  assert L.GemmPolicy()._lookup(key) is None  # a corrupt table is ignored
+  monkeypatch.setenv("XOT_GEMM_TABLE", "off")
+  assert L._default_table_path() is None

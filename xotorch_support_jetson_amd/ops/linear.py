@@ -137,20 +137,72 @@ class _Scratch:
 scratch = _Scratch()
 
 
+def _default_table_path():
+  """Where tuned GEMM choices persist: per GPU model and kernel-library build (a rebuilt library may rank
+  the kernels differently), under XOT_HOME.  XOT_GEMM_TABLE overrides; XOT_GEMM_TABLE=off disables."""
+  env = os.environ.get("XOT_GEMM_TABLE")
+  if env:
+    return None if env == "off" else env
+  try:
+    if not torch.cuda.is_available():
+      return None
+    from .. import _C
+    st = os.stat(_C.__file__)
+    dev = torch.cuda.get_device_name(0).replace(" ", "_").replace("/", "_")
+    from ..helpers import xot_home
+    return str(xot_home() / "gemm" / f"{dev}-{st.st_size:x}-{int(st.st_mtime):x}.json")
+  except Exception:  # noqa: BLE001 - no table then; tuning still works in memory
+    return None
+
+
 class GemmPolicy:
+  """GEMM implementation choice per (layout, M bucket, N, K, epilogue, ...), cold-cache timed on first use.
+  Choices persist in a JSON table (see _default_table_path), so a serving process does not stall its first
+  requests on tuning every prefill / decode bucket again on a machine that has served before."""
+
   def __init__(self):
     self.mode = os.environ.get("XOT_GEMM", "auto")
     self.table: Dict[Tuple, object] = {}
-    path = os.environ.get("XOT_GEMM_TABLE")
-    if path and os.path.exists(path):
-      with open(path) as f:
-        for k, v in json.load(f).items():
-          self.table[tuple(json.loads(k))] = tuple(v) if isinstance(v, list) else v
+    self.path = None
+    self._path_resolved = False
     self.capturing = False
 
+  def _load(self, path: str) -> None:
+    try:
+      with open(path) as f:
+        for k, v in json.load(f).items():
+          self.table.setdefault(tuple(json.loads(k)), tuple(v) if isinstance(v, list) else v)
+    except (OSError, ValueError):
+      pass  # a corrupt or unreadable table is only a cache
+
+  def _table_path(self):
+    """Resolved lazily (needs the device): loads the persisted table the first time a choice is needed."""
+    if not self._path_resolved:
+      self._path_resolved = True
+      self.path = _default_table_path()
+      if self.path and os.path.exists(self.path):
+        self._load(self.path)
+    return self.path
+
+  def _lookup(self, key):
+    self._table_path()
+    return self.table.get(key)
+
+  def _store(self, key, got):
+    self.table[key] = got
+    path = self._table_path()
+    if path:
+      try:
+        self.dump(path)
+      except OSError:
+        pass
+
   def dump(self, path: str):
-    with open(path, "w") as f:
+    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+    tmp = f"{path}.{os.getpid()}.tmp"
+    with open(tmp, "w") as f:
       json.dump({json.dumps(list(k)): v for k, v in self.table.items()}, f, indent=1)
+    os.replace(tmp, path)  # atomic: concurrent processes never read a half-written table
 
   _flush_buf = None
 
@@ -179,7 +231,7 @@ class GemmPolicy:
     M, Kd = x.shape
     N = w.shape[0]
     key = ("s8", _m_bucket(M), N, Kd, epi, bias is not None, str(out_dtype))
-    got = self.table.get(key)
+    got = self._lookup(key)
     if got is not None:
       return got
     cands = self._stream_cands(M, N, Kd, epi)
@@ -196,7 +248,7 @@ class GemmPolicy:
       except RuntimeError:
         pass
     got = min(times, key=times.get) if times else cands[0]
-    self.table[key] = got
+    self._store(key, got)
     return got
 
   def _no_tuning(self) -> bool:
@@ -211,7 +263,7 @@ class GemmPolicy:
     M, Kd = x.shape
     N = w.shape[0]
     key = ("rm", _m_bucket(M), N, Kd, epi, bias is not None)
-    got = self.table.get(key)
+    got = self._lookup(key)
     if got is not None:
       return got
     if self._no_tuning():
@@ -228,7 +280,7 @@ class GemmPolicy:
       except RuntimeError:
         times[impl] = float("inf")
     got = min(times, key=times.get)
-    self.table[key] = got
+    self._store(key, got)
     return got
 
   @staticmethod
@@ -262,7 +314,7 @@ class GemmPolicy:
     M, Kd = x.shape
     N = w.shape[0]
     key = ("sh", _m_bucket(M), N, Kd, epi, bias is not None, str(out_dtype))
-    got = self.table.get(key)
+    got = self._lookup(key)
     if got is not None:
       return got
     cands = []
@@ -285,7 +337,7 @@ class GemmPolicy:
       except RuntimeError:
         pass
     got = min(times, key=times.get) if times else cands[0]
-    self.table[key] = got
+    self._store(key, got)
     return got
 
   @staticmethod
