@@ -157,7 +157,9 @@ async def main(a):
          # time inside the engine's step call (host prep + GPU + token copy), vs. ms_per_step of wall time
          "engine_ms_per_step": round((eng.stats.get("step_s", 0.0) - s0.get("step_s", 0.0)) * 1e3 / max(steps, 1), 2),
          **{f"engine_{k}_ms_per_step": round((eng.stats.get(f"{k}_s", 0.0) - s0.get(f"{k}_s", 0.0)) * 1e3 / max(steps, 1), 2)
-            for k in ("launch", "wait")},
+            for k in ("launch", "wait", "gpu_step")},
+         "gpu_gap_ms_mean": round((eng.stats.get("gpu_gap_s", 0.0) - s0.get("gpu_gap_s", 0.0)) * 1e3
+                                  / max(eng.stats.get("gpu_gaps", 0) - s0.get("gpu_gaps", 0), 1), 3),
          "presampled_tokens": eng.stats.get("presampled", 0) - s0.get("presampled", 0),
          "engine_loop_tokens": eng.stats.get("loop_tokens", 0) - s0.get("loop_tokens", 0),
          "shared_prefix": a.shared_prefix,

@@ -55,6 +55,8 @@ ENGINE_LOOP = os.environ.get("XOT_ENGINE_LOOP", "1") == "1"
 # engine-loop decode steps chained on the device: step N+1 takes step N's sampled ids straight from device
 # memory and is queued before step N's tokens reach the host (no GPU idle gap between decode steps)
 CHAIN = os.environ.get("XOT_CHAIN", "1") == "1"
+# diagnostics: time chained steps on the GPU with events (stats gpu_step_s / gpu_gap_s)
+STEP_EVENTS = os.environ.get("XOT_STEP_EVENTS", "0") == "1"
 
 
 class ShardedInferenceEngine(InferenceEngine):
@@ -360,15 +362,48 @@ class ShardedInferenceEngine(InferenceEngine):
         if self.trainer is not None and self.trainer.dirty:
           self.trainer.sync_to_inference()
         from ..ops import kernels as K
+        ev = STEP_EVENTS and dev.type == "cuda"
+        if ev:
+          e0 = torch.cuda.Event(enable_timing=True)
+          e0.record()
         logits = self.runner.forward(rids, [1] * len(rids), x)
         temps = self._temps([float(st["temperature"]) for st in states], dev)
         tok = K.sample(logits, temps, int(states[0].get("top_k") or TOP_K), self._seed(dev))
         self._advance_seed(dev)
         nxt = {"rids": rids, "states": states, "tok": tok}
+        if dev.type == "cuda":
+          # the ids go to the host right behind this step's sampler: a plain .cpu() in the NEXT call would be
+          # ordered after the step queued there, i.e. wait for it, and leave the GPU idle between steps
+          host = torch.empty(tok.shape, dtype=tok.dtype, pin_memory=True)
+          host.copy_(tok, non_blocking=True)
+          done = torch.cuda.Event()
+          done.record()
+          nxt["host"], nxt["done"] = host, done
+        if ev:
+          e1 = torch.cuda.Event(enable_timing=True)
+          e1.record()
+          nxt["events"] = (e0, e1)
         self.stats["steps"] += 1
         self.stats["requests"] += len(rids)
         self.stats["chained"] = self.stats.get("chained", 0) + 1
-      prev = chain["tok"].cpu().numpy().astype(np.int64) if chain is not None else None
+      t1 = time.perf_counter()
+      prev = None
+      if chain is not None:
+        if "done" in chain:
+          chain["done"].synchronize()
+          prev = chain["host"].numpy().astype(np.int64)
+        else:
+          prev = chain["tok"].cpu().numpy().astype(np.int64)
+      if chain is not None and "events" in chain:  # GPU time of the running step and the idle gap before it
+        e0, e1 = chain["events"]
+        self.stats["gpu_step_s"] = self.stats.get("gpu_step_s", 0.0) + e0.elapsed_time(e1) * 1e-3
+        last = getattr(self, "_last_end_ev", None)
+        if last is not None:
+          self.stats["gpu_gap_s"] = self.stats.get("gpu_gap_s", 0.0) + last.elapsed_time(e0) * 1e-3
+          self.stats["gpu_gaps"] = self.stats.get("gpu_gaps", 0) + 1
+        self._last_end_ev = e1
+      self.stats["launch_s"] = self.stats.get("launch_s", 0.0) + t1 - t0  # host prep + graph launch
+      self.stats["wait_s"] = self.stats.get("wait_s", 0.0) + time.perf_counter() - t1  # the running step's ids
       return prev, nxt
     finally:
       self.stats["step_s"] = self.stats.get("step_s", 0.0) + time.perf_counter() - t0
