@@ -414,3 +414,46 @@ def test_engine_loop_mixed_top_k_all_finish():
     assert not eng._loops and not eng._queue
 
   run(main())
+
+
+def test_api_stream_ends_when_engine_loop_fails(tmp_path, monkeypatch):
+  """A decode-loop step that raises ends the affected requests' streams (finish chunk, [DONE]) instead of
+  leaving the HTTP clients waiting for a token that never comes."""
+  import torch
+  from aiohttp.test_utils import TestClient, TestServer
+
+  from xotorch_support_jetson_amd.api.chatgpt_api import ChatGPTAPI
+  from xotorch_support_jetson_amd.inference.sharded_engine import ShardedInferenceEngine
+
+  async def main():
+    eng = ShardedInferenceEngine(NoopShardDownloader(), device=torch.device("cpu"))
+    calls = {"n": 0}
+    real = eng._chain_step
+
+    def flaky(*a):
+      calls["n"] += 1
+      if calls["n"] == 3:
+        raise RuntimeError("injected step failure")
+      return real(*a)
+    monkeypatch.setattr(eng, "_chain_step", flaky)
+    nodes = await make_ring(tmp_path, ["solo5"], engines=[eng])
+    api = ChatGPTAPI(nodes[0], "ShardedInferenceEngine", response_timeout=60, default_model="tiny-llama")
+    client = TestClient(TestServer(api.app))
+    await client.start_server()
+    try:
+      async def ask(i):
+        r = await client.post("/v1/chat/completions", json={
+          "model": "tiny-llama", "messages": [{"role": "user", "content": f"hi {i}"}], "max_tokens": 40,
+          "temperature": 0.0, "stream": True})
+        return await r.text()
+      outs = await asyncio.wait_for(asyncio.gather(*(ask(i) for i in range(3))), 30)
+      for text in outs:
+        lines = [l for l in text.split("\n") if l.startswith("data: ")]
+        assert lines[-1] == "data: [DONE]"
+        assert json.loads(lines[-2][6:])["choices"][0]["finish_reason"] is not None
+      assert calls["n"] >= 3
+    finally:
+      await client.close()
+      await stop_all(nodes)
+
+  run(main())

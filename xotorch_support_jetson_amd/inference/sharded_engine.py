@@ -396,6 +396,7 @@ class ShardedInferenceEngine(InferenceEngine):
           prev = chain["tok"].cpu().numpy().astype(np.int64)
       if chain is not None and "events" in chain:  # GPU time of the running step and the idle gap before it
         e0, e1 = chain["events"]
+        e1.synchronize()
         self.stats["gpu_step_s"] = self.stats.get("gpu_step_s", 0.0) + e0.elapsed_time(e1) * 1e-3
         last = getattr(self, "_last_end_ev", None)
         if last is not None:

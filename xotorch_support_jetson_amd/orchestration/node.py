@@ -185,6 +185,14 @@ class Node:
     asyncio.create_task(self.broadcast_opaque_status(request_id, json.dumps(
       {"type": "node_status", "node_id": self.id, "status": "request_finished", "request_id": request_id})))
 
+  def _abort(self, request_id: str) -> None:
+    """A request the engine's decode loop could not continue: its consumers (API streams, CLI) get the end
+    of the request now -- with only _finish they would wait for a token that never comes."""
+    self.trigger_on_token_callbacks(request_id, [], True)
+    if self.peers:
+      asyncio.create_task(self.broadcast_result(request_id, [], True))
+    self._finish(request_id)
+
   async def process_inference_result(self, shard: Shard, result, request_id: Optional[str] = None,
                                      inference_state: Optional[dict] = None):
     params = self._params(request_id, inference_state)
@@ -210,7 +218,7 @@ class Node:
         def stop(rid: str, t: int) -> bool:  # would _emit_token(rid, t) end the request? (no side effects)
           return t in eos or len(self.buffered_token_output.get(rid, ((),))[0]) + 1 >= max_tokens
         if loop is not None and loop(request_id, shard, tok, state,
-                                     lambda rid, t: self._emit_token(rid, t, max_tokens, eos), self._finish,
+                                     lambda rid, t: self._emit_token(rid, t, max_tokens, eos), self._abort,
                                      stop=stop):
           self.outstanding_requests[request_id] = "processing"
           return np.array(buf[0])
