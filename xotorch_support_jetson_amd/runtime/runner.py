@@ -80,7 +80,14 @@ class ShardRunner:
       # MoE routing runs on the device too (moe_route + grouped GEMMs), so every model is capturable
       use_graphs = self.device.type == "cuda" and os.environ.get("XOT_GRAPHS", "1") == "1"
     self.use_graphs = use_graphs
-    self._graphs: Dict[int, dict] = {}
+    self._graphs: Dict[tuple, dict] = {}
+    # decode graphs per (batch bucket, block-table width class): a step whose longest context fits a narrower
+    # table replays a graph captured with it, so the split-KV partitioning (chosen from the table width,
+    # static per graph) follows the contexts actually served instead of max_ctx -- at max_ctx 8192 and
+    # contexts of a few hundred tokens the full width split every sequence into 4 mostly empty partitions
+    # plus a merge pass
+    self._widths = sorted({w for w in (8, 32) if w < self.width} | {self.width})
+    self._tables_cls = {}
     self._tables_host = torch.zeros(max_batch, self.width, dtype=torch.int32)
     self._ctx_host = torch.zeros(max_batch, dtype=torch.int32)
     bmax = _bucket(max_batch)
@@ -178,29 +185,45 @@ class ShardRunner:
       return image_features(self.config, self.weights.vision, pixels.to(self.device))
 
   # ------------------------------------------------------------------ graphs
+  def _tables_staging(self, w: int) -> torch.Tensor:
+    if w == self.width:
+      return self._tables_host
+    t = self._tables_cls.get(w)
+    if t is None:
+      t = torch.zeros(self.max_batch, w, dtype=torch.int32)
+      if self.device.type == "cuda":
+        t = t.pin_memory()
+      self._tables_cls[w] = t
+    return t
+
   def _decode_graph(self, rids: Sequence[str], x: torch.Tensor) -> torch.Tensor:
     B = len(rids)
     Bp = min(_bucket(B), self.max_batch)
-    g = self._graphs.get(Bp)
-    if g is None:
-      g = self._capture(Bp)
     # host bookkeeping -> static buffers
     self._reuse_staging()
     pos, slots = [], []
+    most = 0
     for rid in rids:
       start = self.num_tokens(rid)
       if start + 1 > self.max_ctx:
         raise ValueError(f"request {rid}: context exceeds max_ctx {self.max_ctx}")
       slots += self.bm.append(rid, 1)
       pos += self.model.rope_pos(start, 1)
-    self.bm.fill_batch(list(rids), self._tables_host[:B].numpy(), self._ctx_host[:B].numpy())
+      most = max(most, start + 1)
+    need = -(-most // PAGE)
+    w = next(c for c in self._widths if c >= need)
+    g = self._graphs.get((Bp, w))
+    if g is None:
+      g = self._capture(Bp, w)
+    tables = self._tables_staging(w)
+    self.bm.fill_batch(list(rids), tables[:B].numpy(), self._ctx_host[:B].numpy())
     pad = Bp - B
     self._pos_host[:Bp] = torch.tensor(pos + [0] * pad, dtype=torch.int32)
     self._slots_host[:Bp] = torch.tensor(slots + [-1] * pad, dtype=torch.int64)
     g["pos"].copy_(self._pos_host[:Bp], non_blocking=True)
     g["slots"].copy_(self._slots_host[:Bp], non_blocking=True)
     self._ctx_host[B:Bp] = 0
-    g["tables"].copy_(self._tables_host[:Bp], non_blocking=True)
+    g["tables"].copy_(tables[:Bp], non_blocking=True)
     g["ctx"].copy_(self._ctx_host[:Bp], non_blocking=True)
     self._mark_staged()
     if self.shard.is_first_layer():
@@ -238,13 +261,14 @@ class ShardRunner:
     t = random_head_rows(c, rows_from, self.device, seed=self._seed)
     return linear_mod.to_stream_layout(t)
 
-  def _capture(self, Bp: int) -> dict:
+  def _capture(self, Bp: int, w: Optional[int] = None) -> dict:
     dev = self.device
     c = self.config
+    w = w or self.width
     g = {
       "pos": torch.zeros(Bp, dtype=torch.int32, device=dev),
       "slots": torch.full((Bp,), -1, dtype=torch.int64, device=dev),
-      "tables": torch.zeros(Bp, self.width, dtype=torch.int32, device=dev),
+      "tables": torch.zeros(Bp, w, dtype=torch.int32, device=dev),
       "ctx": torch.zeros(Bp, dtype=torch.int32, device=dev),
       "cu": torch.arange(Bp + 1, dtype=torch.int32, device=dev),
       "last": torch.arange(Bp, dtype=torch.int64, device=dev),
@@ -271,5 +295,5 @@ class ShardRunner:
     finally:
       linear_mod.policy.capturing = False
     g["graph"] = graph
-    self._graphs[Bp] = g
+    self._graphs[(Bp, w)] = g
     return g
