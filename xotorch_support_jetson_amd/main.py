@@ -77,6 +77,10 @@ def build_parser() -> argparse.ArgumentParser:
   p.add_argument("--schedule", choices=("gpipe", "1f1b"), default="gpipe",
                  help="--ring --parallel pp: micro-batch order (1f1b keeps at most N - rank activations alive)")
   p.add_argument("--no-api", action="store_true", help="Do not start the ChatGPT API on this peer")
+  p.add_argument("--max-batch", type=int, default=None,
+                 help="Serving: most sequences per batched decode step on a peer (XOT_MAX_BATCH, default 64)")
+  p.add_argument("--max-ctx", type=int, default=None,
+                 help="Serving: longest context (prompt + generated tokens) per request (XOT_MAX_CTX, default 8192)")
   p.add_argument("--weight-dtype", choices=("bf16", "fp8"), default=None,
                  help="fp8: weight-only e4m3 dense projections (half the weight bytes per decode step)")
   return p
@@ -364,6 +368,10 @@ def run(argv=None):
   args = build_parser().parse_args(argv)
   if args.weight_dtype:  # read by every ShardRunner this process (and its spawned peers) builds
     os.environ["XOT_WEIGHT_DTYPE"] = args.weight_dtype
+  if args.max_batch:
+    os.environ["XOT_MAX_BATCH"] = str(args.max_batch)
+  if args.max_ctx:
+    os.environ["XOT_MAX_CTX"] = str(args.max_ctx)
   if args.ring and args.command in ("train", "eval"):
     from .train.ring_train import run_ring
     sys.exit(run_ring(args))
