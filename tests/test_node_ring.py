@@ -457,3 +457,52 @@ def test_api_stream_ends_when_engine_loop_fails(tmp_path, monkeypatch):
       await stop_all(nodes)
 
   run(main())
+
+
+def test_engine_loop_kv_pressure_ends_youngest():
+  """When the KV pool cannot take a chained step's new pages, the youngest requests are ended (their
+  consumers get the end of the request) and the others keep decoding -- the step does not fail for all."""
+  import torch
+
+  from xotorch_support_jetson_amd.inference import sharded_engine as se
+  from xotorch_support_jetson_amd.runtime.runner import _block_manager
+
+  async def main():
+    eng = se.ShardedInferenceEngine(NoopShardDownloader(), device=torch.device("cpu"))
+    shard = Shard("tiny-llama", 0, 3, 4)
+    await eng.ensure_shard(shard)
+    eng.runner.bm = _block_manager(7)  # 7 pages of 64 tokens for everyone
+    eng.prefix_cache = None
+    want = 40
+    got = {r: [] for r in ("a", "b", "c")}
+    ended = {}
+    done = asyncio.Event()
+
+    def emit(rid, tok):
+      got[rid].append(tok)
+      fin = len(got[rid]) >= want
+      if fin:
+        ended[rid] = "done"
+        if len(ended) == 3:
+          done.set()
+      return fin
+
+    def fail(rid):
+      ended[rid] = "kv"
+      if len(ended) == 3:
+        done.set()
+
+    for rid in ("a", "b", "c"):  # 100-token prompts: 2 pages each, crossing into a third at token 128
+      state = {"temperature": 0.0, "top_k": 35}
+      logits, _ = await eng.infer_tensor(rid, shard, np.arange(100, dtype=np.int64).reshape(1, -1) % 200, state)
+      tok = int(np.asarray(await eng.sample(logits, 0.0, 35)).reshape(-1)[0])
+      assert eng.continue_locally(rid, shard, tok, dict(state), emit, fail, stop=lambda r, t: len(got[r]) + 1 >= want)
+    await asyncio.wait_for(done.wait(), 60)
+    assert ended["a"] == "done" and ended["b"] == "done", ended  # 6 pages for a and b fit
+    assert ended["c"] == "kv" and len(got["c"]) < want  # the youngest went at the page boundary
+    assert eng.stats.get("kv_evicted_requests", 0) == 1
+    for rid in ("a", "b", "c"):
+      await eng.finish_request(rid)
+    assert eng.runner.bm.num_free == 7 and eng.runner.bm.check()
+
+  run(main())

@@ -330,10 +330,27 @@ class ShardedInferenceEngine(InferenceEngine):
     """Executor: queue one engine-loop decode step whose inputs are the running step's sampled ids (rows
     `cont`, gathered on the device) and the host tokens of `new`; queue its sampler; then read the running
     step's tokens on the host, which overlaps the new step's GPU work.  Returns (the running step's tokens
-    as int64 numpy or None, the new running step or None)."""
+    as int64 numpy or None, the new running step or None, requests left out for lack of KV pages).
+
+    KV pressure: when the step's new pages exceed the free pool even after prefix-cache eviction, the
+    youngest requests (queued joiners first, then the running rows from the back) give their pages back here
+    until the rest fit, and are reported so the event loop ends them ("length") -- instead of the whole step
+    failing for every request."""
     t0 = time.perf_counter()
     nxt = None
+    victims = []
     try:
+      bm = self.runner.bm
+      if cont or new:
+        need = [bm.blocks_needed(r, 1) for r, _ in cont] + [bm.blocks_needed(it[0], 1) for it in new]
+        if sum(need) > bm.num_free:
+          if self.prefix_cache is not None:
+            self.prefix_cache.evict(sum(need))
+          while (cont or new) and sum(need) > bm.num_free:
+            v = new.pop()[0] if new else cont.pop()[0]
+            need.pop()
+            victims.append(v)
+            self.runner.free(v)  # its pages (those not shared with a cached prefix) return to the pool now
       if cont or new:
         dev = self.runner.device
         rids = [r for r, _ in cont] + [it[0] for it in new]
@@ -405,7 +422,7 @@ class ShardedInferenceEngine(InferenceEngine):
         self._last_end_ev = e1
       self.stats["launch_s"] = self.stats.get("launch_s", 0.0) + t1 - t0  # host prep + graph launch
       self.stats["wait_s"] = self.stats.get("wait_s", 0.0) + time.perf_counter() - t1  # the running step's ids
-      return prev, nxt
+      return prev, nxt, victims
     finally:
       self.stats["step_s"] = self.stats.get("step_s", 0.0) + time.perf_counter() - t0
 
@@ -558,14 +575,19 @@ class ShardedInferenceEngine(InferenceEngine):
             cont, new = [], []
           running = chain
           try:
-            toks, chain = await loop.run_in_executor(self.executor, self._chain_step, running, cont, new)
+            toks, chain, victims = await loop.run_in_executor(self.executor, self._chain_step, running, cont, new)
           except Exception as e:  # noqa: BLE001
             self._loop_failed([(r,) for r in (running["rids"] if running else [])] + new, e)
             chain = None
             continue
           if running is not None:
-            running["next_rids"] = set(chain["rids"]) if chain is not None else set()
+            # a victim gets the running step's token, then ends (not re-queued)
+            running["next_rids"] = (set(chain["rids"]) if chain is not None else set()) | set(victims)
             self._emit_chain(running, toks)
+          if victims:
+            self.stats["kv_evicted_requests"] = self.stats.get("kv_evicted_requests", 0) + len(victims)
+            self._queue = [q for q in self._queue if not (q[3] is None and q[0] in victims)]
+            self._loop_failed([(r,) for r in victims], RuntimeError("KV cache full"))
           continue
         if pending is None:
           await self._settle()
