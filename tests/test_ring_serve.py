@@ -73,10 +73,11 @@ def _free_port():
     return s.getsockname()[1]
 
 
-def test_ring_serve_matches_single_process():
+@pytest.mark.parametrize("world", [2, 3])
+def test_ring_serve_matches_single_process(world):
+  """world 2 and 3: requests spread over `world` lanes circulating the ring concurrently."""
   ref, live1 = _serve(0, 1, None)
   assert {r: len(v) for r, v in ref.items()} == {rid: mt for rid, _, mt in REQS}
-  world = 2
   ctx = mp.get_context("spawn")
   q = ctx.Queue()
   port = _free_port()
@@ -90,8 +91,8 @@ def test_ring_serve_matches_single_process():
   for p in ps:
     p.join(30)
   assert res[0][0] == ref
-  # every request finished: all but the last round's finishers were freed on every rank
-  assert len(res[0][1]) <= 1 and len(res[1][1]) <= 1
+  # every request finished and was freed on every rank (the stop header carries the last frees)
+  assert all(not res[r][1] for r in range(world))
 
 
 def test_chatgpt_api_over_ring_server():

@@ -2,21 +2,25 @@
 
 The reference serves one request at a time, moving every hop through gRPC with the JSON state
 (xotorch/orchestration/node.py:109-147, 403-443; grpc_peer_handle.py:117-136).  Here the GPUs of one
-host are the ring peers (one process each) and the data plane is RCCL p2p over xGMI:
+host are the ring peers (one process each) and the data plane is RCCL p2p over xGMI.
 
-  control plane  rank 0 (API, tokenizer, scheduler) broadcasts one small message per round over a gloo
-                 group: the requests admitted this round (rid, prompt ids), the order of the running
-                 batch, and the requests to free.  Every rank therefore knows every tensor shape it
-                 will receive, so the data plane carries bare activations: no headers, no state.
-  data plane     per round: one prefill pass for the admitted prompts (if any), then one decode pass for
-                 the running batch.  Stage r receives [T, D] bf16 from r-1, runs its layers, sends to
-                 r+1; the last stage samples on device (temperature / top-k 35) and sends the ids [B]
-                 int32 back to rank 0 (P2PTransport: one communicator per directed edge).
+  lanes          rank 0 (API, tokenizer, scheduler) splits the running requests into `world` lanes and
+                 cycles through them: a lane's next step starts as soon as its previous step's tokens are
+                 back, while the other lanes' steps are on the other GPUs -- so the ring stays full, as
+                 in bench.py, instead of filling and draining once per round.
+  control        each lane step travels the ring ahead of its data as a small header (float64 tensor on the
+                 same p2p edges): the step's requests (integer ids) with their new-token counts and
+                 temperatures, requests to free, and a stop flag.  Every rank thus knows every shape it
+                 will receive; no collective, so no rank waits for the whole ring to drain.
+  data plane     stage r receives [T, D] bf16 from r-1, runs its layers, sends to r+1; the last stage
+                 samples on device (temperature / top-k 35) and sends the ids [B] int32 back to rank 0
+                 (P2PTransport: one communicator per directed edge, so these never queue behind the
+                 forward traffic).  Rank 0 receives lane steps' ids in launch order (FIFO per edge).
   KV             each rank holds the paged KV of its own layers for every running request; a finished
-                 request is freed on every rank in the next round's message.
+                 request is freed on every rank when the next header passes.
 
 `RingServer.submit()` is thread-safe (the asyncio API calls it); tokens come back through `on_token`
-callbacks (request_id, [token], is_finished) — the reference's token callback contract.
+callbacks (request_id, [token], is_finished) -- the reference's token callback contract.
 """
 from __future__ import annotations
 
@@ -38,22 +42,30 @@ class _Req:
   temp: float
   max_tokens: int
   out: List[int] = field(default_factory=list)
+  key: int = -1  # integer id on the wire
+  lane: int = 0
 
 
 class RingServer:
   def __init__(self, runner, rank: int, world: int, transport, ctl_group=None, eos_ids: Sequence[int] = (),
                top_k: int = 35, seed: int = 1234, max_batch: Optional[int] = None):
     self.r, self.rank, self.world, self.t = runner, rank, world, transport
-    self.ctl = ctl_group
+    self.ctl = ctl_group  # (unused: the control messages travel with the data)
     self.first, self.last = runner.shard.is_first_layer(), runner.shard.is_last_layer()
     self.prev, self.next = (rank - 1) % world, (rank + 1) % world
     self.D = runner.config.hidden_size
+    self.dev = runner.device
     self.eos = set(int(e) for e in eos_ids)
     self.top_k = top_k
     self.seed_off = torch.tensor([seed, 0], dtype=torch.int64, device=runner.device)
     self.max_batch = max_batch or runner.max_batch
+    self.lanes = max(1, world)
     self._inbox: "queue.Queue[_Req]" = queue.Queue()
     self._running: Dict[str, _Req] = {}
+    self._by_key: Dict[int, _Req] = {}
+    self._next_key = 0
+    self._free: List[int] = []  # keys to free on every rank (carried by the next header)
+    self._inflight: List[Optional[list]] = [None] * self.lanes  # per lane: the step's requests awaiting ids
     self._callbacks: List[Callable[[str, List[int], bool], None]] = []
     self._stop = False
     self._wake = threading.Event()
@@ -73,120 +85,169 @@ class RingServer:
   def idle(self) -> bool:
     return not self._running and self._inbox.empty()
 
-  # ------------------------------------------------------------------ one round
-  def _plan(self, free: List[str]) -> dict:
-    """Rank 0: admit queued requests that fit, and fix this round's batch order."""
-    new = []
+  def _emit(self, rid: str, toks: List[int], fin: bool) -> None:
+    for cb in self._callbacks:
+      cb(rid, toks, fin)
+
+  # ------------------------------------------------------------------ wire format
+  @staticmethod
+  def _header(items, free, stop: bool) -> torch.Tensor:
+    """[n_items, n_free, stop, (key, qlen, temp) * n_items, key * n_free] as float64 (exact for ids < 2^53)."""
+    vals = [float(len(items)), float(len(free)), 1.0 if stop else 0.0]
+    for key, qlen, temp in items:
+      vals += [float(key), float(qlen), float(temp)]
+    vals += [float(k) for k in free]
+    return torch.tensor(vals, dtype=torch.float64)
+
+  @staticmethod
+  def _parse(h: torch.Tensor):
+    v = h.tolist()
+    n, nf, stop = int(v[0]), int(v[1]), v[2] != 0.0
+    items = [(int(v[3 + 3 * i]), int(v[4 + 3 * i]), v[5 + 3 * i]) for i in range(n)]
+    free = [int(x) for x in v[3 + 3 * n:3 + 3 * n + nf]]
+    return items, free, stop
+
+  def _send_header(self, h: torch.Tensor) -> None:
+    # headers go host-staged over the transport (a CUDA copy on RCCL): size first, then the body
+    dev = self.dev
+    self.t.isend(torch.tensor([float(h.numel())], dtype=torch.float64, device=dev), self.next)
+    self.t.isend(h.to(dev), self.next)
+
+  def _recv_header(self) -> torch.Tensor:
+    dev = self.dev
+    n = torch.empty(1, dtype=torch.float64, device=dev)
+    self.t.recv(n, self.prev)
+    h = torch.empty(int(n.item()), dtype=torch.float64, device=dev)
+    self.t.recv(h, self.prev)
+    return h.cpu()
+
+  # ------------------------------------------------------------------ one lane step on this rank
+  def _stage(self, items, x0: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+    """Run this rank's layers for a lane step; the last rank returns the sampled ids [B] int32 (device)."""
+    rids = [str(k) for k, _, _ in items]
+    qlens = [q for _, q, _ in items]
+    if self.first:
+      x = x0.to(self.dev)
+    else:
+      x = torch.empty(sum(qlens), self.D, dtype=torch.bfloat16, device=self.dev)
+      self.t.wait(self.t.irecv(x, self.prev))
+    y = self.r.forward(rids, qlens, x)
+    if not self.last:
+      self.t.isend(y.clone(), self.next)  # y may be a decode graph's static buffer
+      return None
+    temps = torch.tensor([t for _, _, t in items], dtype=torch.float32).to(self.dev)
+    tok = K.sample(y, temps, self.top_k, self.seed_off)
+    self.seed_off[1] += 1
+    if self.world > 1:
+      self.t.isend(tok, 0)
+    return tok
+
+  def _apply_free(self, free: List[int]) -> None:
+    for k in free:
+      self.r.free(str(k))
+
+  # ------------------------------------------------------------------ rank 0: scheduler + first stage
+  def _admit(self) -> None:
     room = self.max_batch - len(self._running)
     while room > 0:
       try:
         req = self._inbox.get_nowait()
       except queue.Empty:
-        break
-      if not self.r.can_admit(req.rid, len(req.ids) + req.max_tokens):
+        return
+      req.key = self._next_key
+      self._next_key += 1
+      if not self.r.can_admit(str(req.key), len(req.ids) + req.max_tokens):
         self._emit(req.rid, [], True)  # cannot fit its context on this shard: finish it empty
         continue
-      new.append(req)
-      room -= 1
-    for req in new:
+      loads = [0] * self.lanes
+      for q in self._running.values():
+        loads[q.lane] += 1
+      req.lane = loads.index(min(loads))
       self._running[req.rid] = req
-    decode = [rid for rid in self._running if self._running[rid].out]
-    return {"new": [(q.rid, q.ids, q.temp) for q in new], "decode": decode,
-            "temps": [self._running[r].temp for r in decode], "free": list(free), "stop": self._stop}
+      self._by_key[req.key] = req
+      room -= 1
 
-  def _broadcast(self, msg: Optional[dict]) -> dict:
-    if self.world == 1:
-      return msg
-    box = [msg]
-    dist.broadcast_object_list(box, src=0, group=self.ctl)
-    return box[0]
-
-  def _pass(self, groups) -> Optional[List[List[int]]]:
-    """One pipeline pass of a round's micro-batches through this rank.  groups: [(rids, qlens, x0, temps)].
-    Micro-batch m+1 enters this stage while m is on the next one (sends are async), so with M >= world
-    micro-batches every GPU of the ring works at once.  Returns the sampled ids per group on rank 0."""
-    dev = self.r.device
-    local = []
-    for rids, qlens, x0, temps in groups:
-      if self.first:
-        x = x0
-      else:
-        x = torch.empty(sum(qlens), self.D, dtype=torch.bfloat16, device=dev)
-        self.t.wait(self.t.irecv(x, self.prev))
-      y = self.r.forward(rids, qlens, x)
-      if not self.last:
-        self.t.isend(y.clone(), self.next)  # y may be a decode graph's static buffer
-        continue
-      tok = K.sample(y, temps.to(dev), self.top_k, self.seed_off)
-      self.seed_off[1] += 1
-      if self.world > 1:
-        self.t.isend(tok, 0)
-      local.append(tok)
-    if self.rank != 0:
-      return None
-    res = []
-    for g, (rids, _, _, _) in enumerate(groups):
-      if self.last:
-        tok = local[g]
-      else:
-        tok = torch.empty(len(rids), dtype=torch.int32, device=dev)
-        self.t.wait(self.t.irecv(tok, self.world - 1))
-      res.append(tok.tolist())
-    return res
-
-  def _emit(self, rid: str, toks: List[int], fin: bool) -> None:
-    for cb in self._callbacks:
-      cb(rid, toks, fin)
-
-  def _collect(self, rids: List[str], toks: List[int], free: List[str]) -> None:
-    for rid, t in zip(rids, toks):
-      req = self._running[rid]
-      req.out.append(t)
+  def _collect(self, lane: int) -> None:
+    """Rank 0: the ids of this lane's step in flight (the oldest step in flight: lanes run in a cycle)."""
+    step = self._inflight[lane]
+    if step is None:
+      return
+    self._inflight[lane] = None
+    reqs, tok = step
+    if tok is None:  # sampled on another rank
+      tok = torch.empty(len(reqs), dtype=torch.int32, device=self.dev)
+      self.t.wait(self.t.irecv(tok, self.world - 1))
+    for req, t in zip(reqs, tok.tolist()):
+      req.out.append(int(t))
       fin = t in self.eos or len(req.out) >= req.max_tokens
-      self._emit(rid, [t], fin)
+      self._emit(req.rid, [int(t)], fin)
       if fin:
-        del self._running[rid]
-        free.append(rid)
+        del self._running[req.rid]
+        del self._by_key[req.key]
+        self.r.free(str(req.key))
+        self._free.append(req.key)
 
-  def step(self, free: List[str]) -> bool:
-    """One round on every rank (rank 0 plans; the others follow its message).  Returns False at stop."""
-    msg = self._broadcast(self._plan(free) if self.rank == 0 else None)
-    for rid in msg["free"]:
-      if self.r.has(rid):
-        self.r.free(rid)
-    free.clear()
-    if msg["new"]:
-      rids = [rid for rid, _, _ in msg["new"]]
-      lens = [len(ids) for _, ids, _ in msg["new"]]
-      x0 = torch.tensor([i for _, ids, _ in msg["new"] for i in ids], dtype=torch.int32) if self.first else None
-      temps = torch.tensor([t for _, _, t in msg["new"]], dtype=torch.float32)
-      toks = self._pass([(rids, lens, x0, temps)])
-      if self.rank == 0:
-        self._collect(rids, toks[0], free)
-    if msg["decode"]:
-      rids, temps = msg["decode"], msg["temps"]
-      M = min(self.world, len(rids))  # micro-batches in flight: one per stage fills the ring
-      per = -(-len(rids) // M)
-      groups = []
-      for lo in range(0, len(rids), per):
-        g = rids[lo:lo + per]
-        x0 = torch.tensor([self._running[r].out[-1] for r in g], dtype=torch.int32) if self.first else None
-        groups.append((g, [1] * len(g), x0, torch.tensor(temps[lo:lo + per], dtype=torch.float32)))
-      toks = self._pass(groups)
-      if self.rank == 0:
-        for (g, _, _, _), tk in zip(groups, toks):
-          self._collect(g, tk, free)
-    return not msg["stop"]
+  def _launch(self, lane: int, stop: bool = False) -> bool:
+    """Rank 0: start this lane's next step (prompts admitted to it, then its decoding requests).
+    Returns whether anything was sent."""
+    reqs = [q for q in self._running.values() if q.lane == lane] if not stop else []
+    if not reqs and not (stop or (self._free and self.world > 1 and self._idle_lanes())):
+      return False
+    items, ids = [], []
+    for q in reqs:
+      if q.out:
+        items.append((q.key, 1, q.temp))
+        ids.append(q.out[-1])
+      else:
+        items.append((q.key, len(q.ids), q.temp))
+        ids += q.ids
+    free, self._free = self._free, []
+    if self.world > 1:
+      self._send_header(self._header(items, free, stop))
+    if items:
+      tok = self._stage(items, torch.tensor(ids, dtype=torch.int32))
+      self._inflight[lane] = (reqs, tok)
+    return True
+
+  def _idle_lanes(self) -> bool:
+    return all(s is None for s in self._inflight)
 
   def serve_forever(self, idle_wait: float = 0.5) -> None:
-    """Round loop (every rank).  Rank 0 waits up to idle_wait for work when nothing is running, then
-    runs a round anyway (an empty message keeps the followers' control-plane waits short)."""
-    free: List[str] = []
+    """Rank 0 cycles through the lanes: collect a lane's ids, admit, launch its next step.  Other ranks
+    follow the headers.  Rank 0 waits up to idle_wait for work when nothing is running."""
+    if self.rank != 0:
+      self._follow()
+      return
+    lane = 0
     while True:
-      if self.rank == 0 and self.idle() and not free and not self._stop:
+      self._collect(lane)
+      if self._stop:
+        if all(s is None for s in self._inflight):
+          break
+        lane = (lane + 1) % self.lanes
+        continue
+      self._admit()
+      launched = self._launch(lane)
+      if not launched and self.idle() and all(s is None for s in self._inflight):
         self._wake.wait(idle_wait)
         self._wake.clear()
-      if not self.step(free):
+      lane = (lane + 1) % self.lanes
+    if self.world > 1:  # stop (with the last frees) travels the ring; followers exit on it
+      free, self._free = self._free, []
+      self._send_header(self._header([], free, True))
+    self.t.drain()
+
+  # ------------------------------------------------------------------ ranks 1..N-1
+  def _follow(self) -> None:
+    while True:
+      h = self._recv_header()
+      items, free, stop = self._parse(h)
+      if not self.last:
+        self._send_header(h)
+      self._apply_free(free)
+      if items:
+        self._stage(items, None)
+      if stop:
         break
     self.t.drain()
 
