@@ -135,7 +135,10 @@ class RingServer:
     if not self.last:
       self.t.isend(y.clone(), self.next)  # y may be a decode graph's static buffer
       return None
-    temps = torch.tensor([t for _, _, t in items], dtype=torch.float32).to(self.dev)
+    temps = torch.tensor([t for _, _, t in items], dtype=torch.float32)
+    if self.dev.type == "cuda":  # pinned + async: a pageable copy would wait here for the forward to finish
+      temps = temps.pin_memory()
+    temps = temps.to(self.dev, non_blocking=True)
     tok = K.sample(y, temps, self.top_k, self.seed_off)
     self.seed_off[1] += 1
     if self.world > 1:
