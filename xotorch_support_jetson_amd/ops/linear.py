@@ -150,7 +150,9 @@ def _default_table_path():
     st = os.stat(_C.__file__)
     dev = torch.cuda.get_device_name(0).replace(" ", "_").replace("/", "_")
     from ..helpers import xot_home
-    return str(xot_home() / "gemm" / f"{dev}-{st.st_size:x}-{int(st.st_mtime):x}.json")
+    # settings that change the candidate sets are part of the name, so a table never answers for another
+    tag = f"{os.environ.get('XOT_GEMM', 'auto')}-{STREAM_MAX_M}-{BIG_MIN_M}"
+    return str(xot_home() / "gemm" / f"{dev}-{st.st_size:x}-{int(st.st_mtime):x}-{tag}.json")
   except Exception:  # noqa: BLE001 - no table then; tuning still works in memory
     return None
 
