@@ -148,7 +148,7 @@ def _default_table_path():
       return None
     from .. import _C
     st = os.stat(_C.__file__)
-    dev = torch.cuda.get_device_name(0).replace(" ", "_").replace("/", "_")
+    dev = torch.cuda.get_device_name(torch.cuda.current_device()).replace(" ", "_").replace("/", "_")
     from ..helpers import xot_home
     # settings that change the candidate sets are part of the name, so a table never answers for another
     tag = f"{os.environ.get('XOT_GEMM', 'auto')}-{STREAM_MAX_M}-{BIG_MIN_M}"
