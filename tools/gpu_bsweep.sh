@@ -1,7 +1,7 @@
 #!/bin/bash
 # batch-per-gpu sweep of the headline bench (one GPU); stops at the first failure
 mkdir -p gpurun_out
-for b in 640 704; do
+for b in 448 576 512; do
   timeout -k 10 400 python -u bench.py --batch-per-gpu $b > gpurun_out/bsweep_$b.log 2>&1
-  rc=$?; echo "b=$b rc=$rc"; tail -1 gpurun_out/bsweep_$b.log | cut -c1-260; [ $rc -eq 0 ] || exit $rc
+  rc=$?; echo "b=$b rc=$rc"; grep '"metric"' gpurun_out/bsweep_$b.log | cut -c1-230; [ $rc -eq 0 ] || exit $rc
 done
