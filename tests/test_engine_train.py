@@ -140,10 +140,19 @@ def test_checkpoint_selection_rejects_mixed_partitions(tmp_path):
   it, files = select_checkpoint_files(tmp_path, Shard(MODEL, 1, 2, N))
   assert it == 4 and [f.name[:7] for f in files] == ["000-001", f"002-{N - 1:03d}"]
   touch(f"000-002-of-{N:03d}-000004.safetensors")  # a 3-layer first stage from another run
-  with pytest.raises(ValueError, match="overlap"):
+  it, files = select_checkpoint_files(tmp_path, Shard(MODEL, 0, N - 1, N))  # iteration 4 overlaps: skipped
+  assert it == 2 and [f.name[:7] for f in files] == [f"000-{N - 1:03d}"]
+  (d / f"000-{N - 1:03d}-of-{N:03d}-000002.safetensors").rename(d / f"000-{N - 1:03d}-of-{N:03d}-000002.bak")
+  with pytest.raises(ValueError, match="overlap"):  # no complete iteration left: the newest one's error
     select_checkpoint_files(tmp_path, Shard(MODEL, 0, N - 1, N))
+  (d / f"000-{N - 1:03d}-of-{N:03d}-000002.bak").rename(d / f"000-{N - 1:03d}-of-{N:03d}-000002.safetensors")
   (d / f"000-002-of-{N:03d}-000004.safetensors").unlink()
   (d / f"002-{N - 1:03d}-of-{N:03d}-000004.safetensors").unlink()
+  # iteration 4 now lacks layers 2..N-1 (one peer's save failed): the complete iteration 2 loads
+  it, _ = select_checkpoint_files(tmp_path, Shard(MODEL, 0, N - 1, N))
+  assert it == 2
+  assert select_checkpoint_files(tmp_path, Shard(MODEL, 0, 1, N))[0] == 4  # ... which covers a first stage
+  (d / f"000-{N - 1:03d}-of-{N:03d}-000002.safetensors").unlink()
   with pytest.raises(FileNotFoundError, match="no file for layers"):
     select_checkpoint_files(tmp_path, Shard(MODEL, 0, N - 1, N))
 

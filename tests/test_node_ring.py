@@ -282,6 +282,42 @@ def test_api_concurrent_requests_real_engine(tmp_path):
   run(main())
 
 
+@pytest.mark.parametrize("loop_on", [True, False])
+def test_api_request_without_temperature(tmp_path, monkeypatch, loop_on):
+  """Clients that leave out `temperature` (and top_k / max_tokens): the API forwards them as None, the Node
+  fills in its defaults, and every request -- also when batched with requests that did set one -- completes,
+  in the engine's decode loop and on the per-token Node path."""
+  import torch
+  from aiohttp.test_utils import TestClient, TestServer
+
+  from xotorch_support_jetson_amd.api.chatgpt_api import ChatGPTAPI
+  from xotorch_support_jetson_amd.inference import sharded_engine as se
+
+  async def main():
+    monkeypatch.setattr(se, "ENGINE_LOOP", loop_on)
+    eng = se.ShardedInferenceEngine(NoopShardDownloader(), device=torch.device("cpu"))
+    nodes = await make_ring(tmp_path, [f"solo_t{int(loop_on)}"], engines=[eng])
+    api = ChatGPTAPI(nodes[0], "ShardedInferenceEngine", response_timeout=60, default_model="tiny-llama")
+    client = TestClient(TestServer(api.app))
+    await client.start_server()
+    try:
+      async def ask(i):
+        body = {"model": "tiny-llama", "messages": [{"role": "user", "content": f"hello {i}"}]}
+        if i % 2:
+          body.update(temperature=0.0, max_tokens=4)
+        r = await client.post("/v1/chat/completions", json=body)
+        assert r.status == 200, await r.text()
+        return await r.json()
+      outs = await asyncio.wait_for(asyncio.gather(*(ask(i) for i in range(4))), 60)
+      for d in outs:
+        assert d["usage"]["completion_tokens"] >= 1
+    finally:
+      await client.close()
+      await stop_all(nodes)
+
+  run(main())
+
+
 def test_engine_decode_loop_matches_node_path(tmp_path, monkeypatch):
   """A single peer holding the whole model decodes in the engine's loop (continue_locally): same greedy
   tokens as the per-token Node path, per-request max_tokens honoured, nothing left registered."""

@@ -133,3 +133,73 @@ def test_policy_confirmation_and_cap():
   pc.reqs["D"].steps = 0
   assert pc.on_decode("D") == [1, 256] and 0 not in pc.entries and list(pc.drop_q) == [0]
   assert not hasattr(bm, "check") or bm.check()
+
+
+def test_failed_request_drops_its_unconfirmed_save():
+  """A request that fails part-way (a hop to a dead peer, an aborted decode loop) gives no guarantee that
+  its save reached the downstream shards: its unconfirmed entry is dropped, never forked by a later prompt;
+  a normal finish confirms it as before."""
+  bm = _block_manager(64)
+  pc = PrefixCache(bm, cap_pages=8, single_shard=False)
+  toks = list(range(3, 3 + 300))
+  pc.on_prompt("A", toks)
+  bm.append("A", 300)
+  assert pc.on_decode("A") == [0, 256]
+  pc.on_finish("A", ok=False)
+  assert 0 not in pc.entries and not bm.has(holder(0)) and list(pc.drop_q) == [0]
+  assert pc.on_prompt("B", toks[:200] + [7] * 50) == (0, None)  # a miss, not a fork of a missing holder
+  # the same sequence with a normal finish confirms the entry and serves the next prompt
+  pc.on_prompt("C", toks)
+  bm.append("C", 300)
+  save = pc.on_decode("C")
+  pc.on_finish("C")
+  assert pc.entries[save[0]].confirmed
+  assert pc.on_prompt("D", toks[:200] + [7] * 50) == (192, save[0])
+  # a failed request that forked: its pending fork is released so the entry can be evicted later
+  pc.on_finish("D", ok=False)
+  assert pc.entries[save[0]].pending == 0
+
+
+def test_node_failure_finishes_with_ok_false(tmp_path):
+  """Node._abort / _fail_request announce request_finished with failed=True; the engine then gets
+  finish_request(ok=False)."""
+  from xotorch_support_jetson_amd.inference.dummy_inference_engine import DummyInferenceEngine
+  from xotorch_support_jetson_amd.orchestration.node import Node
+  from xotorch_support_jetson_amd.topology.ring_memory_weighted_partitioning_strategy import \
+      RingMemoryWeightedPartitioningStrategy
+
+  calls = []
+
+  class Eng(DummyInferenceEngine):
+    async def finish_request(self, request_id, ok=True):
+      calls.append((request_id, ok))
+
+  async def main():
+    node = Node("n", None, Eng(), None, None, RingMemoryWeightedPartitioningStrategy())
+    node._abort("r1")
+    node._finish("r2")
+    for _ in range(20):
+      await asyncio.sleep(0.01)
+    return calls
+
+  got = run(main())
+  assert ("r1", False) in got and ("r2", True) in got
+
+
+def test_cap_follows_smallest_pool_on_the_ring():
+  """Downstream shards report their KV pool size in the step state; the first shard caps its cached pages
+  at the fraction of the SMALLEST pool, since downstream shards never evict holders on their own."""
+  async def main():
+    a, _ = prompts(2)
+    sa, sb = Shard(MODEL, 0, 1, N), Shard(MODEL, 2, N - 1, N)
+    ea, eb = eng(), eng()
+    h, st = await ea.infer_tensor("A", sa, a)
+    await eb.ensure_shard(sb)
+    eb.runner.bm = _block_manager(40)  # a much smaller pool downstream
+    out, st2 = await eb.infer_tensor("A", sb, h, st)
+    assert st2["kv_min"] == 40
+    cap0 = ea.prefix_cache.cap
+    await ea.infer_tensor("A", sa, greedy(out), {**st, **st2})
+    from xotorch_support_jetson_amd.inference.sharded_engine import PREFIX_CACHE_FRAC
+    assert ea.prefix_cache.cap == min(cap0, int(40 * PREFIX_CACHE_FRAC))
+  run(main())

@@ -25,7 +25,7 @@ from ..inference.tokenizers import resolve_tokenizer
 from ..models import registry
 from ..models.registry import (build_base_shard, build_full_shard, get_pretty_name, get_repo, get_supported_models,
                                is_vision_model)
-from ..models.vision import IMAGE_MARK
+from ..models.vision import IMAGE_MARK, escape_marks
 from ..orchestration.tracing import tracer
 from ..utils import metrics
 
@@ -109,6 +109,13 @@ def build_prompt(tokenizer, messages: List[Message], tools: Optional[List[dict]]
   `<|xot_image:URL|>` marker that the first shard's engine expands into image tokens (models/vision.py),
   so the image travels with the prompt to whichever peer holds the first shard."""
   msgs = [m.to_dict() for m in remap_messages(messages)]
+  for m in msgs:  # user text cannot forge an image marker (only the kept image part below becomes one)
+    if isinstance(m["content"], str):
+      m["content"] = escape_marks(m["content"])
+    elif isinstance(m["content"], list):
+      m["content"] = [dict(c, text=escape_marks(c["text"]))
+                      if isinstance(c, dict) and c.get("type") == "text" and isinstance(c.get("text"), str) else c
+                      for c in m["content"]]
   for m in msgs:
     if isinstance(m["content"], list):
       for i, c in enumerate(m["content"]):

@@ -49,8 +49,9 @@ class InferenceEngine(ABC):
   async def evaluate(self, request_id: str, shard: Shard, example, target, length, loss: str = "length_masked_ce"):
     raise NotImplementedError(f"{type(self).__name__} does not evaluate")
 
-  async def finish_request(self, request_id: str) -> None:
-    """Release per-request state (KV pages).  Called when a generation ends."""
+  async def finish_request(self, request_id: str, ok: bool = True) -> None:
+    """Release per-request state (KV pages).  Called when a generation ends; ok=False when it failed or
+    was aborted part-way (its steps may not have reached every shard)."""
 
   async def save_session(self, key, value):
     self.session[key] = value

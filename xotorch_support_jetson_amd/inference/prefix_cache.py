@@ -14,7 +14,8 @@ reach it:
   drop  [ids]       free holders
 The protocol never lets an operation overtake the one it depends on:
   * an entry is used for a fork only once it is confirmed: the saving request came back to the first
-    shard for another step (so every shard applied the save), or finished (likewise);
+    shard for another step (so every shard applied the save), or finished normally (likewise; a request
+    that failed part-way drops its unconfirmed entry instead);
   * an entry is dropped only when no fork of it is pending: each fork is confirmed by the forking
     request's next step or its end;
   * drop ids ride on every outgoing state until a request that carried them comes back.
@@ -200,14 +201,29 @@ class PrefixCache:
       info.drops = tuple(ids)
     return ids
 
-  def on_finish(self, rid: str) -> None:
+  def on_finish(self, rid: str, ok: bool = True) -> None:
+    """ok: the request ended normally (announced by the last shard), so every step it sent went through
+    every shard.  A failed or aborted request gives no such guarantee: the save it carried may never have
+    reached the downstream shards, so its unconfirmed entry is dropped instead of confirmed (a later fork
+    of it would find no holder there), and the drops it carried stay queued for the next carrier."""
     info = self.reqs.pop(rid, None)
     if info is None:
       return
-    # the request's end was announced by the last shard: its steps went through every shard
-    self._confirm(info)
-    for d in info.drops:
-      self.drop_q.pop(d, None)
+    if ok:
+      self._confirm(info)
+      for d in info.drops:
+        self.drop_q.pop(d, None)
+      return
+    if info.fork is not None:  # nothing else can confirm this fork any more
+      e = self.entries.get(info.fork)
+      if e is not None:
+        e.pending = max(0, e.pending - 1)
+      info.fork = None
+    if info.saved is not None:
+      e = self.entries.get(info.saved)
+      if e is not None and not e.confirmed:
+        self._drop(e)  # frees the holder here; downstream holders (if any) go with the queued drop
+      info.saved = None
 
 
 def apply_ops(bm, rid: str, ops: Optional[dict]) -> None:

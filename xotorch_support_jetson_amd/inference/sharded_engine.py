@@ -34,6 +34,12 @@ TEMPERATURE = 0.6
 TOP_K = 35
 
 
+def _temp_of(state: dict) -> float:
+  """A request's sampling temperature; a key present as None (the API's "not given") means the default."""
+  t = state.get("temperature")
+  return TEMPERATURE if t is None else float(t)
+
+
 def default_device() -> torch.device:
   env = os.environ.get("TORCH_DEVICE") or os.environ.get("XOT_DEVICE")
   if env:
@@ -132,7 +138,7 @@ class ShardedInferenceEngine(InferenceEngine):
     # readers sampled.  A lagging request still holds its logits view, so no new tensor can reuse that base
     # address and collide with a fresh key
     self._presampled_prev, self._presampled = self._presampled, {}
-    if not PRESAMPLE or not states or any("temperature" not in st for st in states):
+    if not PRESAMPLE or not states or any(st.get("temperature") is None for st in states):
       return
     from ..ops import kernels as K
     groups = {}
@@ -141,12 +147,12 @@ class ShardedInferenceEngine(InferenceEngine):
     for k, idx in groups.items():
       dev = logits.device
       sel = logits if len(idx) == logits.shape[0] else logits[torch.tensor(idx).to(dev, non_blocking=True)]
-      temps = self._temps([float(states[i]["temperature"]) for i in idx], dev)
+      temps = self._temps([_temp_of(states[i]) for i in idx], dev)
       tok = K.sample(sel.contiguous(), temps, k, self._seed(dev))
       self._advance_seed(dev)
       tok = tok.cpu().numpy().astype(np.int64)  # the step's one blocking point
       for j, i in enumerate(idx):
-        self._presampled[(logits.data_ptr(), i)] = (float(states[i]["temperature"]), k, tok[j:j + 1])
+        self._presampled[(logits.data_ptr(), i)] = (_temp_of(states[i]), k, tok[j:j + 1])
 
   async def sample(self, x, temp: float = TEMPERATURE, top_k: int = TOP_K) -> np.ndarray:
     """Sample one request's next token.  A token drawn with the forward (_presample, same parameters)
@@ -226,7 +232,7 @@ class ShardedInferenceEngine(InferenceEngine):
     token callbacks (SSE writes of every stream) run while the GPU computes the next step.  Returns False
     when the engine cannot (then the Node forwards the token as usual)."""
     if not (ENGINE_LOOP and PRESAMPLE and self.runner is not None and shard == self.shard
-            and shard.is_first_layer() and shard.is_last_layer() and "temperature" in state):
+            and shard.is_first_layer() and shard.is_last_layer() and state.get("temperature") is not None):
       return False
     self._loops[request_id] = (emit, fail, stop)
     self._queue.append((request_id, shard, np.asarray([[token]], dtype=np.int64), None, state))
@@ -249,7 +255,7 @@ class ShardedInferenceEngine(InferenceEngine):
         self.stats["presampled"] = self.stats.get("presampled", 0) + 1
         tok = int(hit[2][0])
       else:  # not drawn with the forward (should not happen): draw it now
-        tok = int(np.asarray(await self.sample(logits[row:row + 1], float(state.get("temperature", TEMPERATURE)),
+        tok = int(np.asarray(await self.sample(logits[row:row + 1], _temp_of(state),
                                                int(state.get("top_k") or TOP_K))).reshape(-1)[0])
       self.stats["loop_tokens"] = self.stats.get("loop_tokens", 0) + 1
       queued = False
@@ -384,7 +390,7 @@ class ShardedInferenceEngine(InferenceEngine):
           e0 = torch.cuda.Event(enable_timing=True)
           e0.record()
         logits = self.runner.forward(rids, [1] * len(rids), x)
-        temps = self._temps([float(st["temperature"]) for st in states], dev)
+        temps = self._temps([_temp_of(st) for st in states], dev)
         tok = K.sample(logits, temps, int(states[0].get("top_k") or TOP_K), self._seed(dev))
         self._advance_seed(dev)
         nxt = {"rids": rids, "states": states, "tok": tok}
@@ -652,6 +658,10 @@ class ShardedInferenceEngine(InferenceEngine):
         xs.append(x.reshape(L, x.shape[2]).to(torch.bfloat16))
       else:  # token ids [1, L]: numpy on the host (no per-request tensor ops; one tensor for the step)
         ids = (inp.detach().cpu().numpy() if isinstance(inp, torch.Tensor) else np.asarray(inp)).reshape(-1)
+        if pc is not None and state.get("kv_min"):
+          # the smallest KV pool on the ring (reported by every downstream shard): downstream shards never
+          # evict holders themselves, so the cap must fit the smallest pool, not just this one
+          pc.cap = min(pc.cap, int(int(state["kv_min"]) * PREFIX_CACHE_FRAC))
         if pc is not None and rid not in self._images:
           ops = {}
           if ids.size > 1 and not self.runner.has(rid):
@@ -704,18 +714,27 @@ class ShardedInferenceEngine(InferenceEngine):
       st = self.stats
       st["launch_s"] = st.get("launch_s", 0.0) + t_launched - t_prep  # host prep + kernel / graph launch
       st["wait_s"] = st.get("wait_s", 0.0) + time.perf_counter() - t_launched  # sampler + the token copy
+      kv_min = self.runner.bm.num_blocks
       for i, (rid, it) in enumerate(zip(rids, items)):
         if len(it) > 3 and it[3]:  # engine-loop request: (logits, row) -- no view, no state to ship
           res.append((out, i))
         else:
-          res.append((out[i:i + 1], {"n_past": self.runner.num_tokens(rid)}))
+          st = {"n_past": self.runner.num_tokens(rid)}
+          if not self.shard.is_first_layer():  # smallest KV pool of the ring, for the first shard's cache cap
+            prev = ((it[2] if len(it) > 2 else None) or {}).get("kv_min")
+            st["kv_min"] = min(kv_min, int(prev)) if prev else kv_min
+          res.append((out[i:i + 1], st))
       return res
     off = 0
     outc = out.cpu()
-    for rid, L, ops in zip(rids, qlens, pc_ops):
+    kv_min = self.runner.bm.num_blocks
+    for (rid, _, *rest), L, ops in zip(items, qlens, pc_ops):
       st = {"n_past": self.runner.num_tokens(rid)}
       if self.shard.is_first_layer():
         st["pc"] = ops  # replaces the previous step's operations in the state that travels the ring
+      else:
+        prev = ((rest[0] if rest else None) or {}).get("kv_min")
+        st["kv_min"] = min(kv_min, int(prev)) if prev else kv_min
       res.append((outc[off:off + L].reshape(1, L, -1), st))
       off += L
     return res
@@ -737,7 +756,7 @@ class ShardedInferenceEngine(InferenceEngine):
       outs.append(y if self.shard.is_last_layer() else y.clone())
     return outs[-1] if self.shard.is_last_layer() else torch.cat(outs)
 
-  async def finish_request(self, request_id: str) -> None:
+  async def finish_request(self, request_id: str, ok: bool = True) -> None:
     self._images.pop(request_id, None)
     self._loops.pop(request_id, None)
     if self.runner is not None:
@@ -745,7 +764,7 @@ class ShardedInferenceEngine(InferenceEngine):
 
       def fin():
         if pc is not None:
-          pc.on_finish(request_id)
+          pc.on_finish(request_id, ok=ok)
         self.runner.free(request_id)
       await self._run(fin)
 

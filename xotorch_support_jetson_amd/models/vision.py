@@ -9,8 +9,8 @@ std).  The tower runs once per image at prefill: its GEMMs go through the kernel
 (pre-shuffled stream / big-tile GEMMs or hipBLASLt), attention through fused SDPA (bidirectional, 577
 tokens), LayerNorm in torch.
 
-Images travel inside the prompt string as `<|xot_image:URL|>` markers (URL = data: base64 or a local
-path; there is no network), so a prompt forwarded to the first shard over gRPC keeps its image; the first
+Images travel inside the prompt string as `<|xot_image:URL|>` markers (URL = data: base64 or a file inside
+image_dir(); there is no network), so a prompt forwarded to the first shard over gRPC keeps its image; the first
 shard's engine turns each marker into `num_image_tokens` copies of the image token id.
 """
 from __future__ import annotations
@@ -40,14 +40,38 @@ def split_image_marks(prompt: str) -> Tuple[List[str], List[str]]:
   return pieces, urls
 
 
+def escape_marks(text: str) -> str:
+  """User text must not be able to produce an image marker: only markers build_prompt writes for the
+  chat's image part survive (a literal `<|xot_image:/etc/...|>` typed into a message stays text)."""
+  return text.replace("<|xot_image:", "<| xot_image:")
+
+
+def image_dir():
+  """The one directory local image paths may point into (XOT_IMAGE_DIR, default $XOT_HOME/images)."""
+  import os
+  from pathlib import Path
+  env = os.environ.get("XOT_IMAGE_DIR")
+  if env:
+    return Path(env).resolve()
+  from ..helpers import get_xot_images_dir
+  return get_xot_images_dir().resolve()
+
+
 def load_image(url: str):
+  """data: URLs, or files inside image_dir() -- never an arbitrary server path named by a client."""
+  from pathlib import Path
+
   from PIL import Image
   if url.startswith("data:"):
     data = base64.b64decode(url.split(",", 1)[1])
     return Image.open(io.BytesIO(data)).convert("RGB")
   if url.startswith("http://") or url.startswith("https://"):
     raise ValueError("image URLs are not fetched (offline runtime): send the image as a data: URL")
-  return Image.open(url).convert("RGB")
+  root = image_dir()
+  path = (root / url).resolve() if not Path(url).is_absolute() else Path(url).resolve()
+  if root != path and root not in path.parents:
+    raise ValueError(f"image path outside {root} refused: send the image as a data: URL")
+  return Image.open(path).convert("RGB")
 
 
 def preprocess(img, size: int) -> torch.Tensor:

@@ -105,7 +105,7 @@ class Node:
             self.current_topology.active_node_id = None
         elif st == "request_finished":
           rid = status.get("request_id")
-          asyncio.get_running_loop().create_task(self._release_request(rid))
+          asyncio.get_running_loop().create_task(self._release_request(rid, ok=not status.get("failed")))
       elif kind == "save_checkpoint" and status.get("node_id") != self.id:
         asyncio.get_running_loop().create_task(self.coordinate_save(
           Shard.from_dict(status["base_shard"]), int(status["iteration"]), status["destination"], broadcast=False))
@@ -119,13 +119,16 @@ class Node:
         print(f"Error on_node_status: {e}")
         traceback.print_exc()
 
-  async def _release_request(self, request_id: Optional[str]) -> None:
+  async def _release_request(self, request_id: Optional[str], ok: bool = True) -> None:
+    """Free a finished request's engine state.  ok=False: it was aborted or failed part-way (a hop to a dead
+    peer, a failed decode step), so its steps may not have reached every shard -- the engine must not
+    treat what it started for the request (a prefix-cache save) as applied ring-wide."""
     if not request_id:
       return
     self.request_params.pop(request_id, None)
     self.outstanding_requests.pop(request_id, None)
     try:
-      await self.inference_engine.finish_request(request_id)
+      await self.inference_engine.finish_request(request_id, ok=ok)
     except Exception:
       if DEBUG >= 2:
         traceback.print_exc()
@@ -153,6 +156,17 @@ class Node:
       self.request_params[request_id] = p
     return p
 
+  def _norm_sampling(self, state: dict) -> dict:
+    """Sampling keys the API sends as None when the client leaves them out (chatgpt_api.py) are filled
+    with the node defaults here, once, before the state reaches any engine or peer: the engines read
+    `state["temperature"]` as a number."""
+    if "temperature" in state and state["temperature"] is None:
+      state["temperature"] = self.default_sample_temperature
+    for k in ("top_k", "max_tokens"):
+      if k in state and state[k] is None:
+        del state[k]
+    return state
+
   def _max_tokens(self, params: dict) -> int:
     return min(int(params.get("max_tokens") or self.max_generate_tokens), self.max_generate_tokens)
 
@@ -178,12 +192,14 @@ class Node:
       self._finish(request_id)
     return is_finished
 
-  def _finish(self, request_id: str) -> None:
+  def _finish(self, request_id: str, failed: bool = False) -> None:
     buf = self.buffered_token_output.setdefault(request_id, ([], False))
     self.buffered_token_output[request_id] = (buf[0], True)
     self.outstanding_requests.pop(request_id, None)
-    asyncio.create_task(self.broadcast_opaque_status(request_id, json.dumps(
-      {"type": "node_status", "node_id": self.id, "status": "request_finished", "request_id": request_id})))
+    status = {"type": "node_status", "node_id": self.id, "status": "request_finished", "request_id": request_id}
+    if failed:
+      status["failed"] = True
+    asyncio.create_task(self.broadcast_opaque_status(request_id, json.dumps(status)))
 
   def _abort(self, request_id: str) -> None:
     """A request the engine's decode loop could not continue: its consumers (API streams, CLI) get the end
@@ -191,7 +207,7 @@ class Node:
     self.trigger_on_token_callbacks(request_id, [], True)
     if self.peers:
       asyncio.create_task(self.broadcast_result(request_id, [], True))
-    self._finish(request_id)
+    self._finish(request_id, failed=True)
 
   async def process_inference_result(self, shard: Shard, result, request_id: Optional[str] = None,
                                      inference_state: Optional[dict] = None):
@@ -214,7 +230,8 @@ class Node:
         loop = getattr(self.inference_engine, "continue_locally", None)
         state = dict(inference_state or {})
         state.update(params)
-        state.setdefault("temperature", temp)
+        if state.get("temperature") is None:
+          state["temperature"] = temp
         def stop(rid: str, t: int) -> bool:  # would _emit_token(rid, t) end the request? (no side effects)
           return t in eos or len(self.buffered_token_output.get(rid, ((),))[0]) + 1 >= max_tokens
         if loop is not None and loop(request_id, shard, tok, state,
@@ -244,7 +261,7 @@ class Node:
     shard = self.get_current_shard(base_shard)
     origin = (inference_state or {}).get("origin") or self.id
     self.request_origin.setdefault(request_id, origin)
-    state = dict(inference_state or {})
+    state = self._norm_sampling(dict(inference_state or {}))
     state["origin"] = origin
     self._params(request_id, state)
     asyncio.create_task(self.broadcast_opaque_status(request_id, json.dumps({
@@ -456,7 +473,8 @@ class Node:
     except Exception:
       pass
     asyncio.create_task(self.broadcast_opaque_status(request_id, json.dumps(
-      {"type": "node_status", "node_id": self.id, "status": "request_finished", "request_id": request_id})))
+      {"type": "node_status", "node_id": self.id, "status": "request_finished", "request_id": request_id,
+       "failed": True})))
 
   def _peer(self, node_id: str) -> PeerHandle:
     for p in self.peers:

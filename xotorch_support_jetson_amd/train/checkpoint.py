@@ -2,7 +2,7 @@
 
 File: {dir}/{model_id}/{start:03d}-{end:03d}-of-{n:03d}-{iteration:06d}.safetensors with HF tensor names
 (un-shuffled, gate/up split), so a checkpoint written by one partition can be loaded by any other:
-loading picks every tensor of the requested layer range from the shard files of the newest iteration.
+loading picks every tensor of the requested layer range from the shard files of the newest complete\niteration.
 Those files must form ONE partition of the model (disjoint layer ranges, same layer count): files of
 the same iteration left by an earlier run with a different layer split would otherwise override each
 other's overlapping layers in sort order, so an overlap is an error, as is a gap in the requested layers.
@@ -39,13 +39,9 @@ def list_checkpoints(directory: str | Path, model_id: str) -> List[Tuple[int, in
   return sorted(out)
 
 
-def select_checkpoint_files(directory: str | Path, shard: Shard) -> Tuple[int, List[Path]]:
-  """(iteration, files) of the newest saved iteration for `shard.model_id`: one partition of the model
-  whose layer ranges are pairwise disjoint and cover the shard's layers."""
-  cks = list_checkpoints(directory, shard.model_id)
-  if not cks:
-    raise FileNotFoundError(f"no checkpoints for {shard.model_id} under {directory}")
-  it = cks[-1][0]
+def _check_iteration(cks, it: int, shard: Shard) -> List[Path]:
+  """Files of iteration `it` if they form ONE partition (disjoint layer ranges of one model size) covering
+  the shard's layers; else ValueError (mixed / overlapping) or FileNotFoundError (a gap)."""
   parts = sorted((s, e, n, p) for i, s, e, n, p in cks if i == it)
   ns = {n for _, _, n, _ in parts}
   if len(ns) != 1:
@@ -58,7 +54,27 @@ def select_checkpoint_files(directory: str | Path, shard: Shard) -> Tuple[int, L
   missing = [l for l in shard.layers() if l not in have]
   if missing:
     raise FileNotFoundError(f"iteration {it} of {shard.model_id} has no file for layers {missing[0]}..{missing[-1]}")
-  return it, [p for *_, p in parts]
+  return [p for *_, p in parts]
+
+
+def select_checkpoint_files(directory: str | Path, shard: Shard) -> Tuple[int, List[Path]]:
+  """(iteration, files) of the newest COMPLETE saved iteration for `shard.model_id`: one partition of the
+  model whose layer ranges are pairwise disjoint and cover the shard's layers.  A newer iteration that is
+  not (one peer's save of a multi-node checkpoint failed, or a re-split run left overlapping files) is
+  skipped with a warning; if no iteration qualifies, the newest one's error is raised."""
+  cks = list_checkpoints(directory, shard.model_id)
+  if not cks:
+    raise FileNotFoundError(f"no checkpoints for {shard.model_id} under {directory}")
+  first_err = None
+  for it in sorted({c[0] for c in cks}, reverse=True):
+    try:
+      files = _check_iteration(cks, it, shard)
+    except (ValueError, FileNotFoundError) as e:
+      first_err = first_err or e
+      print(f"checkpoint: skipping incomplete iteration {it}: {e}")
+      continue
+    return it, files
+  raise first_err
 
 
 def save_shard_checkpoint(engine, shard: Shard, path: str | Path) -> Path:
