@@ -13,7 +13,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from xotorch_support_jetson_amd.ops import linear as L  # noqa: E402
-from xotorch_support_jetson_amd.ops.weights_layout import shuffle_for_stream  # noqa: E402
+from xotorch_support_jetson_amd.ops.weights_layout import shuffle_for_stream, unshuffle_from_stream  # noqa: E402
 
 SHAPES = {"qkv": (10240, 8192, "none"), "o": (8192, 8192, "resid"), "gate_up": (57344, 8192, "silu"),
           "down": (8192, 28672, "resid")}
@@ -67,7 +67,7 @@ def main():
       L._shuffled_call(x, ws, None, res, epi, out, cfg)
       err = ((out.float() - ref.float()).abs().max() / ref.float().abs().max()).item()
       us_blas = t_us(lambda i: L._blas(x, wl[i], None, res, epi, None, torch.bfloat16), nc)
-      us_unshuf = t_us(lambda i: L.scratch.dense_weight(wsl[i]), nc)
+      us_unshuf = t_us(lambda i: unshuffle_from_stream(wsl[i]), nc)
       gb = (N * K * 2) / 1e9
       row = dict(op=name, M=M, N=N, K=K, cfg=list(cfg), us_stream=round(us_stream, 1), us_hipblaslt=round(us_blas, 1),
                  us_unshuffle_copy=round(us_unshuf, 1), tbps_stream=round(gb / us_stream * 1e3, 2), tbps_blas=round(gb / us_blas * 1e3, 2),

@@ -1,0 +1,94 @@
+// Standalone GEMM lab (no torch): gemm_big_kernel variants on RANDOM bf16 operands with the weights rotated
+// through >= 1 GB (HBM-cold per call, as in a forward pass), timed interleaved in one process.
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/lab/gemm_lab2.hip -o tools/lab/gemm_lab2
+//   ./tools/lab/gemm_lab2 M N K [variant]        variant -1 = all (interleaved rounds), else one (profiling)
+#include "../../xotorch_support_jetson_amd/csrc/gemm_big.hip"
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+using namespace xot;
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
+
+__global__ void fill_rand(uint16_t* p, size_t n, uint32_t seed, float scale) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    uint32_t h = (uint32_t)i * 2654435761u ^ seed;
+    h ^= h >> 15; h *= 2246822519u; h ^= h >> 13; h *= 3266489917u; h ^= h >> 16;
+    const float u = ((h & 0xffffff) / 16777216.0f) * 2.f - 1.f;  // uniform [-1, 1)
+    p[i] = f2bf(u * scale);
+  }
+}
+
+struct Ctx {
+  const uint16_t* X; const uint16_t* W; uint16_t* Y; float* ws; int M, N, K; size_t wstride; int nc;
+};
+
+typedef void (*LaunchFn)(const Ctx&, const uint16_t* W, hipStream_t);
+
+template <int BN, int WM, int BK, int NBUF, int AUXA, int AUXB, bool PRIO, bool PP, int EPI>
+void launch_v(const Ctx& c, const uint16_t* W, hipStream_t st) {
+  constexpr int WN = 8 / WM;
+  constexpr int SMEM = NBUF * (256 + BN) * BK * 2;
+  auto k = gemm_big_kernel<256, BN, WM, WN, BK, NBUF, EPI, false, false, 0, 0, AUXA, AUXB, PRIO, PP>;
+  static bool attr = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM) == hipSuccess;
+  (void)attr;
+  const int nwg = ((c.M + 255) / 256) * (c.N / BN);
+  k<<<nwg, 512, SMEM, st>>>(c.X, c.K, W, nullptr, nullptr, 0, c.Y, EPI == EPI_SILU ? c.N / 2 : c.N, nullptr, c.M, c.N,
+                            c.K, 1, nullptr, nullptr, 0L);
+}
+
+struct Variant { const char* name; LaunchFn fn; };
+
+int main(int argc, char** argv) {
+  const int M = atoi(argv[1]), N = atoi(argv[2]), K = atoi(argv[3]);
+  const int only = argc > 4 ? atoi(argv[4]) : -1;
+  const int epi = argc > 5 ? atoi(argv[5]) : EPI_SILU;
+  const size_t wsz = (size_t)N * K;
+  const int nc = (int)std::max<size_t>(2, (1ull << 30) / (wsz * 2) + 1);
+  uint16_t *X, *W, *Y;
+  CK(hipMalloc(&X, (size_t)M * K * 2));
+  CK(hipMalloc(&W, wsz * 2 * nc));
+  CK(hipMalloc(&Y, (size_t)M * N * 4));
+  fill_rand<<<4096, 256>>>(X, (size_t)M * K, 17u, 1.0f);
+  fill_rand<<<4096, 256>>>(W, wsz * nc, 91u, 0.02f);
+  CK(hipDeviceSynchronize());
+  Ctx c{X, W, Y, nullptr, M, N, K, wsz, nc};
+  std::vector<Variant> vs;
+  if (epi == EPI_SILU) {
+    vs.push_back({"pp nt(B)     ", launch_v<256, 2, 64, 2, 0, 3, false, true, EPI_SILU>});
+    vs.push_back({"pp plain(B)  ", launch_v<256, 2, 64, 2, 0, 0, false, true, EPI_SILU>});
+    vs.push_back({"base nt(B)   ", launch_v<256, 2, 64, 2, 0, 3, false, false, EPI_SILU>});
+    vs.push_back({"base plain(B)", launch_v<256, 2, 64, 2, 0, 0, false, false, EPI_SILU>});
+  } else {
+    vs.push_back({"pp nt(B)     ", launch_v<256, 2, 64, 2, 0, 3, false, true, EPI_NONE>});
+    vs.push_back({"pp plain(B)  ", launch_v<256, 2, 64, 2, 0, 0, false, true, EPI_NONE>});
+  }
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  const double flop = 2.0 * M * N * K;
+  const int rounds = only >= 0 ? 3 : 5, iters = 10;
+  std::vector<std::vector<float>> t(vs.size());
+  int call = 0;
+  for (int r = 0; r < rounds; ++r)
+    for (size_t v = 0; v < vs.size(); ++v) {
+      if (only >= 0 && (int)v != only) continue;
+      for (int w = 0; w < 2; ++w) vs[v].fn(c, W + (size_t)((call++) % nc) * wsz, 0);
+      CK(hipEventRecord(a));
+      for (int i = 0; i < iters; ++i) vs[v].fn(c, W + (size_t)((call++) % nc) * wsz, 0);
+      CK(hipEventRecord(b));
+      CK(hipEventSynchronize(b));
+      float ms;
+      CK(hipEventElapsedTime(&ms, a, b));
+      t[v].push_back(ms * 1e3f / iters);
+    }
+  for (size_t v = 0; v < vs.size(); ++v) {
+    if (t[v].empty()) continue;
+    std::sort(t[v].begin(), t[v].end());
+    printf("M=%d N=%d K=%d %s median %8.1f us (%6.0f TF/s)  min %8.1f us\n", M, N, K, vs[v].name,
+           t[v][t[v].size() / 2], flop / t[v][t[v].size() / 2] / 1e6, t[v][0]);
+  }
+  return 0;
+}

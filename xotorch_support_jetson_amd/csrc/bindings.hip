@@ -365,6 +365,49 @@ void gemm_big(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const c10
          " splits=", splits);
 }
 
+// Stream-K large-M GEMM on the pre-shuffled weight layout (csrc/gemm_sk.hip): `cus` persistent workgroups;
+// part: fp32 [>= gemm_sk_part_elems()], sync: int32 [>= gemm_sk_sync_words(M, N)] zeroed once.
+void gemm_sk(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const c10::optional<at::Tensor>& bias,
+             const c10::optional<at::Tensor>& res, const at::Tensor& part, const at::Tensor& sync, int64_t epi,
+             int64_t cus) {
+  CHECK_BF16(x);
+  CHECK_BF16(w);
+  CHECK_GPU(y);
+  XCHECK(x.dim() == 2 && w.dim() == 2 && y.dim() == 2, "gemm_sk: x, w, y must be 2-D");
+  XCHECK(x.stride(1) == 1 && x.stride(0) % 8 == 0 && w.is_contiguous() && y.stride(1) == 1,
+         "gemm_sk: rows must be contiguous and 16-B aligned");
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
+  XCHECK(w.size(1) == K, "gemm_sk: K mismatch");
+  const bool f32 = y.scalar_type() == at::kFloat;
+  XCHECK(f32 || y.scalar_type() == at::kBFloat16, "gemm_sk: y must be bf16 or fp32");
+  XCHECK(y.size(0) == M && y.size(1) == (epi == 2 ? N / 2 : N), "gemm_sk: y shape mismatch");
+  XCHECK(M <= (1 << 24) && M * std::max(y.stride(0), x.stride(0)) < (1LL << 31), "gemm_sk: M too large");
+  if (bias.has_value()) {
+    CHECK_BF16((*bias));
+    XCHECK(bias->numel() == N && bias->is_contiguous(), "gemm_sk: bias shape mismatch");
+  }
+  int64_t ldr = 0;
+  if (epi == 1) {
+    XCHECK(res.has_value(), "gemm_sk: residual epilogue needs res");
+    CHECK_BF16((*res));
+    XCHECK(res->dim() == 2 && res->size(0) == M && res->size(1) == N && res->stride(1) == 1, "gemm_sk: res shape");
+    ldr = res->stride(0);
+  }
+  CHECK_GPU(part);
+  CHECK_DT(part, at::kFloat);
+  CHECK_GPU(sync);
+  CHECK_DT(sync, at::kInt);
+  XCHECK(part.is_contiguous() && part.numel() >= xot::gemm_sk_part_elems(), "gemm_sk: part workspace too small");
+  XCHECK(sync.is_contiguous() && sync.numel() >= xot::gemm_sk_sync_words((int)M, (int)N), "gemm_sk: sync words too small");
+  const int rc = xot::launch_gemm_sk(bf(x), (int)x.stride(0), bf(w), bf_opt(bias), epi == 1 ? bf(*res) : nullptr,
+                                     (int)ldr, y.data_ptr(), (int)y.stride(0), f32, (int)epi, part.data_ptr<float>(),
+                                     sync.data_ptr<int>(), (int)M, (int)N, (int)K, (int)cus, cur_stream());
+  XCHECK(rc == 0, "gemm_sk: unsupported shape M=", M, " N=", N, " K=", K, " epi=", epi, " cus=", cus);
+}
+
+int64_t gemm_sk_part_elems() { return xot::gemm_sk_part_elems(); }
+int64_t gemm_sk_sync_words(int64_t M, int64_t N) { return xot::gemm_sk_sync_words((int)M, (int)N); }
+
 // h [rows, D] += bias + sum_s ws[s] (the split-K slabs of a residual projection, fp32 [S][rows][D]);
 // out = rmsnorm(h) * w: the projection's reduce, the residual add and the next RMSNorm in one pass.
 void splitk_resid_rmsnorm(const at::Tensor& ws, int64_t splits, const c10::optional<at::Tensor>& bias, at::Tensor& h,
@@ -813,6 +856,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("tickets") = py::none(), py::arg("reduce") = true);
   m.def("gemm_stream8", &gemm_stream8, py::arg("x"), py::arg("w8"), py::arg("wscale"), py::arg("y"), py::arg("bias"),
         py::arg("res"), py::arg("ws"), py::arg("epi"), py::arg("ntw"), py::arg("splits"), py::arg("reduce") = true);
+  m.def("gemm_sk", &gemm_sk, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("bias"), py::arg("res"), py::arg("part"),
+        py::arg("sync"), py::arg("epi"), py::arg("cus") = 256);
+  m.def("gemm_sk_part_elems", &gemm_sk_part_elems);
+  m.def("gemm_sk_sync_words", &gemm_sk_sync_words);
   m.def("gemm_big", &gemm_big, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("bias"), py::arg("res"),
         py::arg("ws"), py::arg("epi"), py::arg("bn"), py::arg("splits"), py::arg("reduce") = true);
   m.def("splitk_resid_rmsnorm", &splitk_resid_rmsnorm);

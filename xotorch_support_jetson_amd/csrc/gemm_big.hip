@@ -27,20 +27,6 @@
 
 namespace xot {
 
-typedef __attribute__((address_space(3))) void* lds_ptr_t;
-typedef __attribute__((address_space(1))) void* glb_ptr_t;
-
-// one LDS-DMA wave instruction: lane l copies 16 B from its own global address to lds_base + 16*l
-template <int AUX = 0>
-__device__ __forceinline__ void glds16(const void* g, void* lds_base) {
-  __builtin_amdgcn_global_load_lds((glb_ptr_t)g, (lds_ptr_t)lds_base, 16, 0, AUX);
-}
-
-
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
 
 // ABL (tools/lab only): 1 = k loop without MFMAs, 2 = without stage loads, 3 = stage loads not overlapped
 // AUXA / AUXB: cache-policy bits of the X / W LDS-DMA loads (sc0 = 1, nt = 2, sc1 = 16)

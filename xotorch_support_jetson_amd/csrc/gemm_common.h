@@ -6,6 +6,21 @@ namespace xot {
 
 enum { EPI_NONE = 0, EPI_RESID = 1, EPI_SILU = 2 };
 
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef __attribute__((address_space(1))) void* glb_ptr_t;
+
+// one LDS-DMA wave instruction: lane l copies 16 B from its own global address to lds_base + 16*l
+template <int AUX = 0>
+__device__ __forceinline__ void glds16(const void* g, void* lds_base) {
+  __builtin_amdgcn_global_load_lds((glb_ptr_t)g, (lds_ptr_t)lds_base, 16, 0, AUX);
+}
+
+// wait until at most N of this wave's vector-memory operations (loads, LDS-DMA, stores) are in flight
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
 // Sum the S fp32 slabs of one output row at 8 output columns [o, o+8) and apply the epilogue.
 // wsrow = slab 0 of this row (slabs are sstride floats apart); rrow / yrow = this row of R / Y.
 template <int EPI, bool OUT_F32>

@@ -42,6 +42,14 @@ int launch_gemm_stream8(const uint16_t* X, int ldx, const uint8_t* W, const floa
 int launch_gemm_big(const uint16_t* X, int ldx, const uint16_t* W, const uint16_t* bias, const uint16_t* R, int ldr,
                     void* Y, int ldy, bool out_f32, int epi, float* ws, long ws_elems, int M, int N, int K, int bn,
                     int S, bool reduce, hipStream_t s);
+// stream-K large-M GEMM on the pre-shuffled layout: one persistent 256 x 256 x 64 workgroup per CU (cus of
+// them), split column tiles finished by their last-arriving part; part = gemm_sk_part_elems() fp32,
+// sync = gemm_sk_sync_words(M, N) int32, zero-initialised once (kept zeroed by the kernel)
+int launch_gemm_sk(const uint16_t* X, int ldx, const uint16_t* W, const uint16_t* bias, const uint16_t* R, int ldr,
+                   void* Y, int ldy, bool out_f32, int epi, float* part, int* sync, int M, int N, int K, int cus,
+                   hipStream_t s);
+long gemm_sk_part_elems();
+long gemm_sk_sync_words(int M, int N);
 // h += bias + sum of S fp32 split-K slabs [S][rows][D] (in place, bf16), out = rmsnorm(h) * w
 void launch_splitk_resid_rmsnorm(const float* ws, int S, const uint16_t* bias, uint16_t* h, const uint16_t* w,
                                  uint16_t* out, int rows, int D, float eps, hipStream_t s);

@@ -8,8 +8,8 @@ consume that layout, both with the epilogue fused (bias / residual add / SiLU*mu
                instruction straight to registers, X shared through swizzled LDS, optional split-K).
   gemm_big     compute-bound M (large decode batches, prefill chunks): 256 x {256,128} x 64 tiles,
                both operands staged by LDS-DMA, 8 waves, XCD-aware tile order, optional split-K.
-  ("blas")     long prefill chunks may instead copy the weight back to row-major scratch and run
-               hipBLASLt when that measures faster (copy included in the timing).
+No vendor GEMM runs on a shuffled weight: at prefill sizes gemm_big matches hipBLASLt once the weight
+copy the library would need is counted (profiles/r3/bench_gemm_sk.json), so there is no un-shuffle path.
 
 The configuration ((kernel, ntw|bn, split-K) per M bucket and shape) is chosen by cold-cache timing on
 first use; inside a HIP-graph capture a heuristic stands in (the runner warms every captured shape up
@@ -26,8 +26,8 @@ import torch
 
 from . import kernels as K
 from ._ext import require
-from .weights_layout import (can_shuffle, dequant_stream8, quantize_fp8_rows, shuffle_for_stream, shuffle_for_stream8,
-                             unshuffle_from_stream)
+from .weights_layout import (can_shuffle, dequant_stream8, dequant_stream8_to_stream, quantize_fp8_rows,
+                             shuffle_for_stream, shuffle_for_stream8, unshuffle_from_stream)
 
 
 # XOT_SPLITK_IN_LAUNCH=1: split-K partial sums combined by the last-arriving workgroup of each tile
@@ -90,7 +90,6 @@ class _Scratch:
 
   def __init__(self):
     self.ws: Dict[int, torch.Tensor] = {}
-    self.dense: Dict[int, torch.Tensor] = {}
     self.tk: Dict[int, torch.Tensor] = {}
     self.retired: list = []
 
@@ -120,18 +119,6 @@ class _Scratch:
       self.tk[idx] = t
     return t
 
-  def dense_weight(self, w: torch.Tensor) -> torch.Tensor:
-    """Row-major copy of a shuffled weight in a reusable buffer (prefill path)."""
-    idx = w.device.index or 0
-    n = w.numel()
-    t = self.dense.get(idx)
-    if t is None or t.numel() < n:
-      t = torch.empty(n, dtype=w.dtype, device=w.device)
-      self.dense[idx] = t
-    N, Kd = w.shape
-    v = t[:n].view(N // 16, 16, Kd // 128, 4, 4, 8)
-    v.copy_(w.view(N // 16, Kd // 128, 4, 4, 16, 8).permute(0, 4, 1, 2, 3, 5))
-    return t[:n].view(N, Kd)
 
 
 scratch = _Scratch()
@@ -324,8 +311,6 @@ class GemmPolicy:
       cands += [("stream",) + c for c in self._stream_cands(M, N, Kd, epi)]
     if M >= BIG_MIN_M and Kd % 128 == 0:
       cands += self._big_cands(M, N, Kd)
-    if M > STREAM_MAX_M and self.mode != "hip":
-      cands.append(("blas",))  # long prefill chunks: un-shuffled scratch copy + hipBLASLt
     if not cands:
       raise RuntimeError(f"no GEMM configuration for pre-shuffled N={N} K={Kd} M={M}")
     if self._no_tuning():
@@ -397,8 +382,10 @@ STREAM8_MAX_M = int(os.environ.get("XOT_STREAM8_MAX_M", "256"))
 
 def _linear8(x, w, bias, residual, epi, out, dt):
   M, N = x.shape[0], w.shape[0]
-  if M > STREAM8_MAX_M:  # compute-bound: widen once per call, then the bf16 library GEMM
-    return _blas(x, dequant_stream8(w, w.xot_scale), bias, residual, epi, out, dt)
+  if M > STREAM8_MAX_M:  # compute-bound: widen once per call (straight into the bf16 tile layout), then gemm_big
+    wb = dequant_stream8_to_stream(w, w.xot_scale)
+    wb.xot_layout = "stream"
+    return linear(x, wb, bias=bias, residual=residual, epi=epi, out=out, out_dtype=dt)
   if out is None:
     out = torch.empty(M, N // 2 if epi == "silu" else N, dtype=dt, device=x.device)
   if x.stride(1) != 1 or x.stride(0) % 8:
@@ -407,8 +394,6 @@ def _linear8(x, w, bias, residual, epi, out, dt):
 
 
 def _shuffled_call(x, w, bias, residual, epi, out, cfg):
-  if cfg[0] == "blas":
-    return _blas(x, scratch.dense_weight(w), bias, residual, epi, out, out.dtype if out is not None else None)
   if cfg[0] == "stream":
     return _stream_call(x, w, bias, residual, epi, out, cfg[1:])
   _, bn, S = cfg

@@ -58,6 +58,16 @@ def unshuffle_from_stream8(qs: torch.Tensor) -> torch.Tensor:
   return v.permute(0, 4, 1, 2, 5, 3, 6).contiguous().reshape(N, K)
 
 
+def dequant_stream8_to_stream(qs: torch.Tensor, scale: torch.Tensor) -> torch.Tensor:
+  """bf16 copy of a shuffled FP8 weight directly in the bf16 shuffled layout (no row-major round trip):
+  the 16 bytes of lane (g, c) in half h hold k 64h + 8g and 64h + 32 + 8g, which are lane (g, c) of the
+  bf16 blocks s = 2h and 2h + 1."""
+  N, K = qs.shape
+  q = qs.view(torch.float8_e4m3fn).view(N // 16, K // 128, 2, 64, 2, 8).float()  # nt, kc, h, lane, part, e
+  sc = scale.float().view(N // 16, 1, 1, 1, 16).expand(N // 16, 1, 1, 4, 16).reshape(N // 16, 1, 1, 64, 1, 1)
+  return (q * sc).to(torch.bfloat16).permute(0, 1, 2, 4, 3, 5).reshape(N, K)
+
+
 def dequant_stream8(qs: torch.Tensor, scale: torch.Tensor, dtype=torch.bfloat16) -> torch.Tensor:
   """Row-major [N, K] `dtype` copy of a shuffled FP8 weight."""
   q = unshuffle_from_stream8(qs).view(torch.float8_e4m3fn)

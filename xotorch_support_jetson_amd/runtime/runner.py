@@ -50,12 +50,12 @@ class ShardRunner:
     self._random_weights, self._seed = weights is None, seed
     self.weights = weights if weights is not None else random_weights(config, shard, self.device, seed=seed)
     if self.device.type == "cuda" and os.environ.get("XOT_SHUFFLE", "1") == "1":
-      # projection weights -> pre-shuffled MFMA-fragment layout (gemm_stream for decode-shaped M,
-      # gemm_big for large batches); with decode batches above 128 rows the gate/up projection stays
-      # row-major, where hipBLASLt measures faster (ops/linear.py; XOT_ROWMAJOR_PROJ overrides)
+      # projection weights -> pre-shuffled MFMA-fragment layout: gemm_stream for decode-shaped M, gemm_big
+      # (256 x 256 LDS-DMA tiles, fused SiLU / residual epilogues) for large decode batches and prefill
+      # chunks -- every projection runs on the library's own kernels (XOT_ROWMAJOR_PROJ=gu,... keeps the
+      # named projections row-major for A/B runs against the vendor GEMM)
       env = os.environ.get("XOT_ROWMAJOR_PROJ")
-      keep = [p for p in env.split(",") if p] if env is not None else (
-          ["gu"] if max_batch > 128 and not config.is_moe else [])  # grouped expert GEMMs want the shuffled layout
+      keep = [p for p in env.split(",") if p] if env is not None else []
       # XOT_WEIGHT_DTYPE=fp8: weight-only e4m3 projections (half the bytes per decode step; opt-in, the
       # serving default and every benchmark headline stay bf16)
       self.weight_dtype = os.environ.get("XOT_WEIGHT_DTYPE", "bf16")
