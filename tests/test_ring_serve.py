@@ -148,3 +148,113 @@ def test_ring_server_on_gpu():
   assert {r: len(v) for r, v in out.items()} == {rid: mt for rid, _, mt in REQS}
   assert all(0 <= t < PRESETS[MODEL].vocab_size for v in out.values() for t in v)
   assert len(live) <= 1
+
+
+# ---------------------------------------------------------------------------- chunked prefill, KV pressure,
+# failure recovery
+LONG = [("p", 150, 5), ("q", 40, 12), ("r", 90, 8), ("s", 20, 10)]  # prompts longer than a step's token budget
+
+
+def _ref_tokens(reqs):
+  """Single process, ample pool, whole prompts: the tokens every configuration below must reproduce."""
+  c = PRESETS[MODEL]
+  from xotorch_support_jetson_amd.inference.shard import Shard
+  runner = ShardRunner(c, Shard(MODEL, 0, c.num_layers - 1, c.num_layers), "cpu", max_batch=8, max_ctx=256)
+  srv = RingServer(runner, 0, 1, P2PTransport(0, 1), step_tokens=4096)
+  return _run_rank0(srv, reqs)
+
+
+def _run_rank0(srv, reqs, timeout=150):
+  out, done = {}, threading.Event()
+  budget = {rid: mt for rid, _, mt in reqs}
+
+  def on_tok(rid, toks, fin):
+    out.setdefault(rid, []).extend(toks)
+    if fin and all(len(out.get(r, ())) >= budget[r] for r in budget):
+      done.set()
+  srv.on_token(on_tok)
+  for rid, n, mt in reqs:
+    srv.submit(rid, _prompt(rid, n), 0.0, mt)
+  th = threading.Thread(target=srv.serve_forever, kwargs=dict(idle_wait=0.05))
+  th.start()
+  ok = done.wait(timeout)
+  srv.stop()
+  th.join(60)
+  assert ok, out
+  return out
+
+
+def _worker2(rank, world, port, q, pages, fault):
+  import datetime
+  from xotorch_support_jetson_amd.parallel.health import HealthMonitor
+  from xotorch_support_jetson_amd.parallel.ring_serve import control_group, min_pool_pages, ring_shards
+  os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+  if fault:
+    os.environ["XOT_FAULT"] = fault
+  dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=60))
+  c = PRESETS[MODEL]
+
+  def make_runner(r, w, ctl):
+    shard = ring_shards(MODEL, c.num_layers, w, ctl)[r]
+    # rank-dependent pool sizes: the ring plans with the smallest one
+    runner = ShardRunner(c, shard, "cpu", max_batch=8, max_ctx=256, num_pages=pages + 3 * r)
+    return runner, min_pool_pages(runner, w, ctl)
+
+  ctl = control_group()
+  runner, pool = make_runner(rank, world, ctl)
+  mon = HealthMonitor(rank, world, interval=0.1, timeout=1.5).start() if fault else None
+  srv = RingServer(runner, rank, world, P2PTransport(rank, world, monitor=mon), ctl, step_tokens=32, monitor=mon,
+                   make_runner=make_runner, pool_pages=pool)
+  res = None
+  if rank == 0:
+    res = _run_rank0(srv, LONG)
+  else:
+    srv.serve_forever()
+  q.put((rank, res, dict(srv.stats), srv.pool_pages, srv.r.bm.num_free == srv.r.bm.num_blocks))
+  q.close()
+  q.join_thread()
+  os._exit(0)
+
+
+def _launch2(world, pages, fault=""):
+  ctx = mp.get_context("spawn")
+  q = ctx.Queue()
+  port = _free_port()
+  ps = [ctx.Process(target=_worker2, args=(r, world, port, q, pages, fault)) for r in range(world)]
+  for p in ps:
+    p.start()
+  want = world - (1 if fault.startswith("kill") else 0)
+  res = {}
+  for _ in range(want):
+    rank, out, stats, pool, clean = q.get(timeout=240)
+    res[rank] = (out, stats, pool, clean)
+  for p in ps:
+    p.join(30)
+  return res
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_ring_serve_chunked_prefill_and_kv_pressure(world):
+  """Prompts longer than the 32-token step budget go through in chunks; a pool of 5 pages (64 tokens
+  each) cannot hold every request at once, so the youngest are preempted and later re-prefilled from
+  prompt + tokens so far.  Tokens equal the single-process reference; every rank plans with the smallest
+  pool; all pages come back."""
+  ref = _ref_tokens(LONG)
+  res = _launch2(world, pages=5)
+  out, stats, pool, _ = res[0]
+  assert out == ref
+  assert stats["chunks"] > 0 and stats["preempted"] > 0, stats
+  assert all(res[r][2] == 5 for r in res)  # min over ranks (rank r has 5 + 3r pages)
+  assert all(res[r][3] for r in res)  # every rank's pool is empty again
+
+
+def test_ring_serve_recovers_from_a_dead_peer():
+  """3 ranks; rank 1 dies mid-stream (XOT_FAULT=kill).  The survivors detect it by heartbeat, re-form a
+  2-rank ring, re-partition the layers over it and rank 0 re-admits the running requests: every request
+  completes with the tokens of the single-process reference."""
+  ref = _ref_tokens(LONG)
+  res = _launch2(3, pages=64, fault="kill:rank=1:after=12")
+  assert set(res) == {0, 2}
+  out, stats, _, _ = res[0]
+  assert stats["recoveries"] == 1
+  assert out == ref

@@ -3,7 +3,9 @@
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/lab/gemm_lab2.hip -o tools/lab/gemm_lab2
 //   ./tools/lab/gemm_lab2 M N K [variant]        variant -1 = all (interleaved rounds), else one (profiling)
 #include "../../xotorch_support_jetson_amd/csrc/gemm_big.hip"
+#include "../../xotorch_support_jetson_amd/csrc/gemm_sk.hip"
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -27,7 +29,7 @@ struct Ctx {
 
 typedef void (*LaunchFn)(const Ctx&, const uint16_t* W, hipStream_t);
 
-template <int BN, int WM, int BK, int NBUF, int AUXA, int AUXB, bool PRIO, bool PP, int EPI>
+template <int BN, int WM, int BK, int NBUF, int AUXA, int AUXB, bool PRIO, int PP, int EPI>
 void launch_v(const Ctx& c, const uint16_t* W, hipStream_t st) {
   constexpr int WN = 8 / WM;
   constexpr int SMEM = NBUF * (256 + BN) * BK * 2;
@@ -37,6 +39,14 @@ void launch_v(const Ctx& c, const uint16_t* W, hipStream_t st) {
   const int nwg = ((c.M + 255) / 256) * (c.N / BN);
   k<<<nwg, 512, SMEM, st>>>(c.X, c.K, W, nullptr, nullptr, 0, c.Y, EPI == EPI_SILU ? c.N / 2 : c.N, nullptr, c.M, c.N,
                             c.K, 1, nullptr, nullptr, 0L);
+}
+
+static float* g_part = nullptr;
+static int* g_sync = nullptr;
+template <int EPI>
+void launch_sk(const Ctx& c, const uint16_t* W, hipStream_t st) {
+  launch_gemm_sk(c.X, c.K, W, nullptr, nullptr, 0, c.Y, EPI == EPI_SILU ? c.N / 2 : c.N, false, EPI, g_part, g_sync, c.M,
+                 c.N, c.K, 256, st);
 }
 
 struct Variant { const char* name; LaunchFn fn; };
@@ -55,15 +65,38 @@ int main(int argc, char** argv) {
   fill_rand<<<4096, 256>>>(W, wsz * nc, 91u, 0.02f);
   CK(hipDeviceSynchronize());
   Ctx c{X, W, Y, nullptr, M, N, K, wsz, nc};
+  CK(hipMalloc(&g_part, gemm_sk_part_elems() * 4));
+  CK(hipMalloc(&g_sync, 1 << 20));
+  CK(hipMemset(g_sync, 0, 1 << 20));
   std::vector<Variant> vs;
   if (epi == EPI_SILU) {
-    vs.push_back({"pp nt(B)     ", launch_v<256, 2, 64, 2, 0, 3, false, true, EPI_SILU>});
-    vs.push_back({"pp plain(B)  ", launch_v<256, 2, 64, 2, 0, 0, false, true, EPI_SILU>});
-    vs.push_back({"base nt(B)   ", launch_v<256, 2, 64, 2, 0, 3, false, false, EPI_SILU>});
-    vs.push_back({"base plain(B)", launch_v<256, 2, 64, 2, 0, 0, false, false, EPI_SILU>});
+    vs.push_back({"pp nt(B)     ", launch_v<256, 2, 64, 2, 0, 3, false, 1, EPI_SILU>});
+    vs.push_back({"8ph nt(B)    ", launch_v<256, 2, 64, 2, 0, 3, false, 2, EPI_SILU>});
+    vs.push_back({"8ph plain(B) ", launch_v<256, 2, 64, 2, 0, 0, false, 2, EPI_SILU>});
+    vs.push_back({"base nt(B)   ", launch_v<256, 2, 64, 2, 0, 3, false, 0, EPI_SILU>});
+    vs.push_back({"stream-K     ", launch_sk<EPI_SILU>});
   } else {
-    vs.push_back({"pp nt(B)     ", launch_v<256, 2, 64, 2, 0, 3, false, true, EPI_NONE>});
-    vs.push_back({"pp plain(B)  ", launch_v<256, 2, 64, 2, 0, 0, false, true, EPI_NONE>});
+    vs.push_back({"pp nt(B)     ", launch_v<256, 2, 64, 2, 0, 3, false, 1, EPI_NONE>});
+    vs.push_back({"8ph nt(B)    ", launch_v<256, 2, 64, 2, 0, 3, false, 2, EPI_NONE>});
+    vs.push_back({"stream-K     ", launch_sk<EPI_NONE>});
+  }
+  {  // every variant must produce the first variant's output (same tile math; k order identical)
+    std::vector<uint16_t> ref((size_t)M * N), got((size_t)M * N);
+    const size_t ny = (size_t)M * (epi == EPI_SILU ? N / 2 : N);
+    for (size_t v = 0; v < vs.size(); ++v) {
+      CK(hipMemset(Y, 0, (size_t)M * N * 4));
+      vs[v].fn(c, W, 0);
+      CK(hipDeviceSynchronize());
+      CK(hipMemcpy(v == 0 ? ref.data() : got.data(), Y, ny * 2, hipMemcpyDeviceToHost));
+      if (v == 0) continue;
+      double maxd = 0, maxr = 0;
+      for (size_t i = 0; i < ny; ++i) {
+        const float r = __builtin_bit_cast(float, (uint32_t)ref[i] << 16), g = __builtin_bit_cast(float, (uint32_t)got[i] << 16);
+        maxd = std::max(maxd, (double)std::fabs(r - g));
+        maxr = std::max(maxr, (double)std::fabs(r));
+      }
+      printf("check %s vs %s: max |diff| %.3g (max |ref| %.3g)\n", vs[v].name, vs[0].name, maxd, maxr);
+    }
   }
   hipEvent_t a, b;
   CK(hipEventCreate(&a));

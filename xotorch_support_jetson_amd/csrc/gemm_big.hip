@@ -41,7 +41,7 @@ namespace xot {
 // halves in 0 and 1), so in phase 3 the stage two ahead is issued into the buffer being finished, and
 // the stage one ahead is retired by a counted vmcnt (LDS-DMA stays in flight across the barriers).
 template <int BM, int BN, int WM, int WN, int BK, int NBUF, int EPI, bool OUT_F32, bool SPLIT, int MOE = 0, int ABL = 0,
-          int AUXA = 0, int AUXB = 3, bool PRIO = false, bool PP = false>
+          int AUXA = 0, int AUXB = 3, bool PRIO = false, int PP = 0>
 __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __restrict__ X, int ldx,
                                                           const uint16_t* __restrict__ W,
                                                           const uint16_t* __restrict__ bias,
@@ -197,7 +197,140 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
     else wait_vm<0>();
   };
 
-  if constexpr (PP) {
+  if constexpr (PP == 2) {
+    // 8-phase interleave: the same four 16-MFMA quadrant phases per stage as PP == 1, but the LDS image is
+    // managed per operand HALF (A0 = the qm = 0 row tiles of both row halves, A1 = qm = 1; B0 = the qn = 0
+    // column tiles of every wave column, B1 = qn = 1; 16 KB each, 2 LDS-DMA instructions per wave), and
+    // each half is refilled with the stage two ahead as soon as every wave is two phases past its last read:
+    //   phase 0: read A0 B0 | issue A1(t+1)      phase 1: read B1
+    //   phase 2: read A1    | issue A0 B0(t+2)   phase 3: (registers only) | issue B1(t+2)
+    // so at most 2 DMA instructions issue beside each MFMA segment and every half lands 6 phases ahead of
+    // its first read; counted vmcnt(8) at the end of phases 0, 2 and 3 retires A1(t), A0 B0(t+1), B1(t+1)
+    // one phase before the barrier that precedes their reads (one barrier more than needed: the two row
+    // halves run one barrier apart).  Tail stages (t + 2 >= T) drain with vmcnt(0).
+    static_assert(BM == 256 && BN == 256 && WM == 2 && WN == 4 && BK == 64 && NBUF == 2 && ABL == 0, "PP geometry");
+    auto bar = []() {
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    };
+    // per-lane source / LDS destination of this wave's 2 instructions of each half
+    const uint16_t* a_src[2][2];
+    int a_dst[2][2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int rp = 16 * wave + 8 * i;                      // row of the half's 128-row set
+        const int R = (rp & 63) + ((rp >> 6) << 7) + 64 * h;  // first tile row of the instruction
+        const int row = R + lane / 8;
+        const int slot = (lane % 8) ^ aswz(row);
+        const int grow = min(m0 + row, Mv - 1);
+        a_src[h][i] = X + (size_t)grow * ldx + slot * 8;
+        a_dst[h][i] = R * BK;
+      }
+    const uint16_t* b_src[2];
+    int b_dst[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int grp = 4 * (wave >> 1) + (wave & 1) + 2 * h;  // 16-column group of this wave in half h
+      b_src[h] = W + ((size_t)((n0 >> 4) + grp) * kchunks) * 2048 + lane * 8;
+      b_dst[h] = A_ELEMS + grp * KS * 512;
+    }
+    auto issue_a = [&](int t, int h) {
+      uint16_t* base = smem + (t & 1) * STAGE;
+      const int k0 = (t_beg + t) * BK;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) glds16<AUXA>(a_src[h][i] + k0, base + a_dst[h][i]);
+    };
+    auto issue_b = [&](int t, int h) {
+      uint16_t* base = smem + (t & 1) * STAGE;
+      const int k0 = (t_beg + t) * BK;
+      const size_t woff = (size_t)(k0 >> 7) * 2048 + ((k0 & 127) >> 5) * 512;
+#pragma unroll
+      for (int s2 = 0; s2 < KS; ++s2) glds16<AUXB>(b_src[h] + woff + s2 * 512, base + b_dst[h] + s2 * 512);
+    };
+    s16x8 af[4][2], bq[2][2][2];
+    auto read_a = [&](int buf, int qm) {
+      const uint16_t* As = smem + buf * STAGE;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) af[i][s2] = ld16(As + aoff[4 * qm + i][s2]);
+    };
+    auto read_b = [&](int buf, int qn) {
+      const uint16_t* Bs = smem + buf * STAGE + A_ELEMS;
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) bq[qn][j][s2] = ld16(Bs + boff + ((2 * qn + j) * KS + s2) * 512);
+    };
+    auto quad = [&](int qm, int qn) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[4 * qm + i][2 * qn + j] = mfma16(af[i][s2], bq[qn][j][s2], acc[4 * qm + i][2 * qn + j]);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    if (T > 0) {
+      // prologue: stage 0 whole, stage 1 except A1 (issued in stage 0's phase 0)
+      issue_a(0, 0);
+      issue_b(0, 0);
+      issue_b(0, 1);
+      issue_a(0, 1);
+      if (T > 1) {
+        issue_a(1, 0);
+        issue_b(1, 0);
+        issue_b(1, 1);
+        wait_vm<8>();  // A0 B0 B1 of stage 0 landed (B1 is read before the row halves' phase-0 waits)
+      } else {
+        wait_vm<0>();
+      }
+      bar();
+      const int half = __builtin_amdgcn_readfirstlane(wm);
+      if (half == 1) bar();  // row-half 1 runs one barrier behind
+      for (int t = 0; t < T; ++t) {
+        const int buf = t & 1;
+        const bool steady = t + 2 < T;
+        // phase 0
+        read_a(buf, 0);
+        read_b(buf, 0);
+        if (t + 1 < T) issue_a(t + 1, 1);
+        bar();
+        quad(0, 0);
+        if (steady) wait_vm<8>(); else wait_vm<0>();  // A1(t) landed
+        bar();
+        // phase 1
+        read_b(buf, 1);
+        bar();
+        quad(0, 1);
+        bar();
+        // phase 2
+        read_a(buf, 1);
+        if (steady) {
+          issue_a(t + 2, 0);
+          issue_b(t + 2, 0);
+        }
+        bar();
+        quad(1, 1);
+        if (steady) wait_vm<8>(); else wait_vm<0>();  // A0 B0(t+1) landed
+        bar();
+        // phase 3
+        if (steady) issue_b(t + 2, 1);
+        bar();
+        quad(1, 0);
+        if (steady) wait_vm<8>(); else wait_vm<0>();  // B1(t+1) landed
+        bar();
+      }
+      if (half == 0) bar();  // balance the barrier count
+    }
+  } else if constexpr (PP == 1) {
     static_assert(BM == 256 && BN == 256 && WM == 2 && WN == 4 && BK == 64 && NBUF == 2 && ABL == 0, "PP geometry");
     auto bar = []() {  // raw barrier (no vmcnt / lgkmcnt drain); the asm statements are compiler fences
       asm volatile("" ::: "memory");
@@ -358,7 +491,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
   }
 }
 
-template <int BM, int BN, int WM, int WN, int BK, int NBUF, int EPI, bool F32, bool PP = false>
+template <int BM, int BN, int WM, int WN, int BK, int NBUF, int EPI, bool F32, int PP = 0>
 static void big_launch(const uint16_t* X, int ldx, const uint16_t* W, const uint16_t* bias, const uint16_t* R,
                        int ldr, void* Y, int ldy, float* ws, int M, int N, int K, int S, bool reduce,
                        hipStream_t st) {
@@ -393,7 +526,9 @@ static int big_dispatch(const uint16_t* X, int ldx, const uint16_t* W, const uin
   if (bn == 256)
     big_launch<256, 256, 2, 4, 64, 2, EPI, F32>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, S, reduce, st);
   else if (bn == 1256)  // ping-pong schedule of the 256 x 256 tile
-    big_launch<256, 256, 2, 4, 64, 2, EPI, F32, true>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, S, reduce, st);
+    big_launch<256, 256, 2, 4, 64, 2, EPI, F32, 1>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, S, reduce, st);
+  else if (bn == 2256)  // 8-phase interleave of the 256 x 256 tile (per-half LDS refills)
+    big_launch<256, 256, 2, 4, 64, 2, EPI, F32, 2>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, S, reduce, st);
   else if (bn == 128)
     big_launch<256, 128, 4, 2, 64, 3, EPI, F32>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, S, reduce, st);
   else
@@ -405,8 +540,8 @@ int launch_gemm_big(const uint16_t* X, int ldx, const uint16_t* W, const uint16_
                     void* Y, int ldy, bool out_f32, int epi, float* ws, long ws_elems, int M, int N, int K, int bn,
                     int S, bool reduce, hipStream_t s) {
   if (M <= 0) return 0;
-  const int tile_n = bn == 1256 ? 256 : bn;
-  if ((bn != 128 && bn != 256 && bn != 1256) || N % tile_n != 0 || K % 128 != 0 || S < 1 || S > K / 64) return -1;
+  const int tile_n = bn % 1000;
+  if ((bn != 128 && bn != 256 && bn != 1256 && bn != 2256) || N % tile_n != 0 || K % 128 != 0 || S < 1 || S > K / 64) return -1;
   if (S > 1 && (ws == nullptr || ws_elems < (long)S * M * N)) return -1;
   if (epi == EPI_SILU && N % 32 != 0) return -1;
   if (epi == EPI_SILU)

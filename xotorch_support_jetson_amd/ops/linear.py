@@ -36,6 +36,8 @@ from .weights_layout import (can_shuffle, dequant_stream8, dequant_stream8_to_st
 # workgroup is a serial tail on one CU).
 SPLITK_IN_LAUNCH = os.environ.get("XOT_SPLITK_IN_LAUNCH", "0") == "1"
 
+# XOT_GEMM_SK=0: leave the stream-K GEMM out of the timed candidates
+SK = os.environ.get("XOT_GEMM_SK", "1") == "1"
 # largest M for which the stream GEMM is a candidate (above it only gemm_big is timed)
 STREAM_MAX_M = int(os.environ.get("XOT_STREAM_MAX_M", "512"))
 # smallest M for which gemm_big is a candidate
@@ -91,6 +93,7 @@ class _Scratch:
   def __init__(self):
     self.ws: Dict[int, torch.Tensor] = {}
     self.tk: Dict[int, torch.Tensor] = {}
+    self.sk: Dict[int, tuple] = {}
     self.retired: list = []
 
   def splitk(self, device, n: int) -> torch.Tensor:
@@ -104,6 +107,20 @@ class _Scratch:
       t = torch.empty(max(n, 1 << 20, 2 * (t.numel() if t is not None else 0)), dtype=torch.float32, device=device)
       self.ws[idx] = t
     return t
+
+  def stream_k(self, device):
+    """(fp32 partial-tile slots, zeroed int32 tickets / flags) of the stream-K GEMM: fixed sizes, allocated
+    once per device (the kernel leaves the sync words zeroed, so graph replays can share them)."""
+    idx = device.index or 0
+    got = self.sk.get(idx)
+    if got is None:
+      if torch.cuda.is_current_stream_capturing():
+        raise RuntimeError("stream-K workspace must be allocated before graph capture")
+      C = require()
+      got = (torch.empty(C.gemm_sk_part_elems(), dtype=torch.float32, device=device),
+             torch.zeros(1 << 20, dtype=torch.int32, device=device))
+      self.sk[idx] = got
+    return got
 
   def tickets(self, device, n: int) -> torch.Tensor:
     """Zero-initialised int32 tile counters of the in-launch split-K combine (the last arriver of a
@@ -296,6 +313,10 @@ class GemmPolicy:
         if S > 1 and (tiles >= 256 or tiles * S > 1024 or Kd // 64 < 2 * S):
           continue
         cands.append(("big", bn, S))
+    # stream-K: one persistent 256 x 256 workgroup per CU, the k steps of all tiles dealt out evenly (wins when
+    # the tile count leaves the last round of plain tiles partly empty)
+    if SK and M >= 256 and N % 256 == 0 and (N // 256) * (Kd // 64) >= 256 and -(-M // 256) <= 8 and M * N < (1 << 31):
+      cands.append(("sk", 256, 1))
     return cands
 
   def shuffled_cfg(self, x, w, bias, residual, epi, out_dtype) -> Tuple:
@@ -353,7 +374,7 @@ class GemmPolicy:
 
 
 def _ws_elems(cfg, M, N) -> int:
-  return cfg[2] * M * N if len(cfg) == 3 and cfg[2] > 1 else 0
+  return cfg[2] * M * N if len(cfg) == 3 and cfg[0] != "sk" and cfg[2] > 1 else 0
 
 
 policy = GemmPolicy()
@@ -396,6 +417,10 @@ def _linear8(x, w, bias, residual, epi, out, dt):
 def _shuffled_call(x, w, bias, residual, epi, out, cfg):
   if cfg[0] == "stream":
     return _stream_call(x, w, bias, residual, epi, out, cfg[1:])
+  if cfg[0] == "sk":
+    part, sync = scratch.stream_k(x.device)
+    require().gemm_sk(x, w, out, bias, residual, part, sync, K.EPI[epi], cfg[1])
+    return out
   _, bn, S = cfg
   M, N = x.shape[0], w.shape[0]
   ws = scratch.splitk(x.device, S * M * N) if S > 1 else None

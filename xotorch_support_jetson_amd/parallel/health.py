@@ -52,20 +52,25 @@ def abort_communicators() -> None:
       pass
 
 
-def _own_store_client(timeout_s: float = 10.0):
+def store_port(generation: int = 0) -> int:
+  """TCPStore port of ring generation `generation` (0 = the launch rendezvous, n = the n-th re-formed ring)."""
+  base = int(os.environ.get("MASTER_PORT", "29500"))
+  return base if generation == 0 else base + 1 + generation
+
+
+def _own_store_client(timeout_s: float = 10.0, generation: int = 0):
   host = os.environ.get("MASTER_ADDR", "127.0.0.1")
-  port = int(os.environ.get("MASTER_PORT", "29500"))
-  return dist.TCPStore(host, port, is_master=False, wait_for_workers=False,
+  return dist.TCPStore(host, store_port(generation), is_master=False, wait_for_workers=False,
                        timeout=datetime.timedelta(seconds=timeout_s))
 
 
 class HealthMonitor:
   def __init__(self, rank: int, world: int, store=None, interval: float = 0.25, timeout: float = 3.0,
-               abort_on_failure: bool = True, prefix: str = "xot"):
+               abort_on_failure: bool = True, prefix: str = "xot", generation: int = 0):
     self.rank, self.world = rank, world
     # a connection of its own: a TCPStore client is not safe to share with the main thread's
     # rendezvous / new_group traffic
-    self.store = store if store is not None else _own_store_client()
+    self.store = store if store is not None else _own_store_client(generation=generation)
     self.interval, self.timeout = interval, timeout
     self.abort_on_failure = abort_on_failure
     self.prefix = prefix
@@ -224,7 +229,7 @@ class FaultInjector:
 def reform_ring(alive: List[int], rank: int, generation: int, backend: Optional[str] = None,
                 timeout_s: int = 60) -> tuple:
   """Re-rendezvous the surviving ranks as a new, dense world (new rank = index in `alive`) on a
-  fresh TCPStore at MASTER_PORT + 1 + generation.  The old default group must already be aborted.
+  fresh TCPStore at store_port(generation) = MASTER_PORT + 1 + generation (generation >= 1).  The old default group must already be aborted.
   Returns (new_rank, new_world)."""
   if rank not in alive:
     raise ValueError(f"rank {rank} is not among the survivors {alive}")
@@ -235,7 +240,7 @@ def reform_ring(alive: List[int], rank: int, generation: int, backend: Optional[
     pass
   new_rank, new_world = alive.index(rank), len(alive)
   host = os.environ.get("MASTER_ADDR", "127.0.0.1")
-  port = int(os.environ.get("MASTER_PORT", "29500")) + 1 + generation
+  port = store_port(generation)
   store = dist.TCPStore(host, port, new_world, is_master=new_rank == 0,
                         timeout=datetime.timedelta(seconds=timeout_s))
   dist.init_process_group(be, store=store, rank=new_rank, world_size=new_world,

@@ -2,28 +2,46 @@
 
 The reference serves one request at a time, moving every hop through gRPC with the JSON state
 (xotorch/orchestration/node.py:109-147, 403-443; grpc_peer_handle.py:117-136).  Here the GPUs of one
-host are the ring peers (one process each) and the data plane is RCCL p2p over xGMI.
+host are the ring peers (one process each, `xot --gpus N`) and the data plane is RCCL p2p over xGMI.
 
   lanes          rank 0 (API, tokenizer, scheduler) splits the running requests into `world` lanes and
                  cycles through them: a lane's next step starts as soon as its previous step's tokens are
-                 back, while the other lanes' steps are on the other GPUs -- so the ring stays full, as
-                 in bench.py, instead of filling and draining once per round.
-  control        each lane step travels the ring ahead of its data as a small header (float64 tensor on the
-                 same p2p edges): the step's requests (integer ids) with their new-token counts and
-                 temperatures, requests to free, and a stop flag.  Every rank thus knows every shape it
-                 will receive; no collective, so no rank waits for the whole ring to drain.
+                 back, while the other lanes' steps are on the other GPUs -- the ring stays full, as in
+                 bench.py, instead of filling and draining once per round.
+  control plane  each lane step is announced ahead of its data by a fixed-size header (float64: the step's
+                 requests as (wire id, new tokens, temperature), requests to free, a stop flag) sent over a
+                 gloo group, i.e. host to host: a follower reads it without touching its GPU stream, so it
+                 queues the step's receive + forward while its previous step is still running (a header on
+                 the RCCL stream would be readable only after that stream drained).
   data plane     stage r receives [T, D] bf16 from r-1, runs its layers, sends to r+1; the last stage
                  samples on device (temperature / top-k 35) and sends the ids [B] int32 back to rank 0
-                 (P2PTransport: one communicator per directed edge, so these never queue behind the
-                 forward traffic).  Rank 0 receives lane steps' ids in launch order (FIFO per edge).
-  KV             each rank holds the paged KV of its own layers for every running request; a finished
-                 request is freed on every rank when the next header passes.
+                 (P2PTransport: one communicator per directed edge).  Rank 0 receives lane steps' ids in
+                 launch order (FIFO per edge).
+  prefill        prompts go through in chunks: a lane step carries at most `step_tokens` new tokens
+                 (XOT_MAX_STEP_TOKENS), so a long prompt never stalls the other requests of its lane for a
+                 whole-prompt forward; only the final chunk's sampled token is kept.
+  KV             each rank holds the paged KV of its own layers for every running request.  All ranks size
+                 their pools to the SMALLEST pool on the ring (min over ranks at start-up), so rank 0's
+                 BlockManager -- which sees the same appends in the same order as every other rank's --
+                 accounts for every rank exactly.  When a step would not fit, rank 0 preempts the youngest
+                 requests of that lane: their pages are freed on every rank (the next header carries the
+                 frees) and they are re-admitted later by re-prefilling prompt + tokens so far; their
+                 streams continue where they stopped.  (Admission never rejects a request that fits
+                 max_ctx; the old design refused any request whose whole budget did not fit at once.)
+  failures       every rank runs a HealthMonitor (parallel/health.py: store heartbeats, communicator abort).
+                 On a peer failure the survivors re-form a dense ring (reform_ring), re-partition the
+                 layers over the live GPUs (memory-weighted, ring order), rebuild their shards, and rank 0
+                 re-admits every running request with a re-prefill -- the reference re-partitions on the
+                 next request after a peer drops (node.py:455-460, udp_discovery.py:204-246) but loses
+                 the requests in flight.  The API owner (rank 0) itself cannot be replaced.
 
 `RingServer.submit()` is thread-safe (the asyncio API calls it); tokens come back through `on_token`
 callbacks (request_id, [token], is_finished) -- the reference's token callback contract.
 """
 from __future__ import annotations
 
+import collections
+import os
 import queue
 import threading
 from dataclasses import dataclass, field
@@ -33,6 +51,10 @@ import torch
 import torch.distributed as dist
 
 from ..ops import kernels as K
+from .health import FaultInjector, HealthMonitor, PeerFailure, reform_ring, wait_work
+
+STEP_TOKENS = int(os.environ.get("XOT_MAX_STEP_TOKENS", "8192"))
+FREE_CAP = 256  # frees per header (more wait for the next one)
 
 
 @dataclass
@@ -42,33 +64,57 @@ class _Req:
   temp: float
   max_tokens: int
   out: List[int] = field(default_factory=list)
-  key: int = -1  # integer id on the wire
-  lane: int = 0
+  key: int = -1  # integer id on the wire (a new one per admission)
+  lane: int = -1
+  fed: int = 0  # tokens of ids + out already in the KV cache
+  order: int = 0  # admission order: the largest is the youngest
+
+  def todo(self) -> int:
+    """Tokens still to feed before the next sampled token is a real output (1 while decoding)."""
+    return len(self.ids) + len(self.out) - self.fed
 
 
 class RingServer:
   def __init__(self, runner, rank: int, world: int, transport, ctl_group=None, eos_ids: Sequence[int] = (),
-               top_k: int = 35, seed: int = 1234, max_batch: Optional[int] = None):
+               top_k: int = 35, seed: int = 1234, max_batch: Optional[int] = None, step_tokens: Optional[int] = None,
+               monitor: Optional[HealthMonitor] = None, make_runner: Optional[Callable] = None,
+               pool_pages: Optional[int] = None):
     self.r, self.rank, self.world, self.t = runner, rank, world, transport
-    self.ctl = ctl_group  # (unused: the control messages travel with the data)
+    self.ctl = ctl_group  # gloo group of the control plane (headers); None with world 1
+    self.eos = set(int(e) for e in eos_ids)
+    self.top_k = top_k
+    self.seed = seed
+    self.max_batch = max_batch or runner.max_batch
+    self.step_tokens = max(1, step_tokens or STEP_TOKENS)
+    self.monitor = monitor
+    self.make_runner = make_runner  # (shard) -> ShardRunner: rebuilds this rank's shard after a re-partition
+    self.generation = 0
+    self.backend = dist.get_backend() if dist.is_initialized() else "gloo"
+    self._set_topology(runner, rank, world, pool_pages)
+    self._inbox: "queue.Queue[_Req]" = queue.Queue()
+    self._waiting: "collections.deque[_Req]" = collections.deque()  # preempted (front) and new requests
+    self._running: Dict[str, _Req] = {}
+    self._next_key = 0
+    self._next_order = 0
+    self._free: List[int] = []  # keys to free on every rank (carried by the next headers)
+    self._callbacks: List[Callable[[str, List[int], bool], None]] = []
+    self._stop = False
+    self._wake = threading.Event()
+    self._pending_ctl: list = []
+    self.stats = {"steps": 0, "preempted": 0, "chunks": 0, "recoveries": 0}
+
+  def _set_topology(self, runner, rank: int, world: int, pool_pages: Optional[int]) -> None:
+    self.r, self.rank, self.world = runner, rank, world
     self.first, self.last = runner.shard.is_first_layer(), runner.shard.is_last_layer()
     self.prev, self.next = (rank - 1) % world, (rank + 1) % world
     self.D = runner.config.hidden_size
     self.dev = runner.device
-    self.eos = set(int(e) for e in eos_ids)
-    self.top_k = top_k
-    self.seed_off = torch.tensor([seed, 0], dtype=torch.int64, device=runner.device)
-    self.max_batch = max_batch or runner.max_batch
+    self.seed_off = torch.tensor([self.seed, 0], dtype=torch.int64, device=runner.device)
     self.lanes = max(1, world)
-    self._inbox: "queue.Queue[_Req]" = queue.Queue()
-    self._running: Dict[str, _Req] = {}
-    self._by_key: Dict[int, _Req] = {}
-    self._next_key = 0
-    self._free: List[int] = []  # keys to free on every rank (carried by the next header)
-    self._inflight: List[Optional[list]] = [None] * self.lanes  # per lane: the step's requests awaiting ids
-    self._callbacks: List[Callable[[str, List[int], bool], None]] = []
-    self._stop = False
-    self._wake = threading.Event()
+    self._inflight: List[Optional[list]] = [None] * self.lanes  # per lane: the step's (req, n) awaiting ids
+    # rank 0 plans with the smallest pool of the ring (exact for every rank: same appends everywhere)
+    self.pool_pages = min(pool_pages or runner.bm.num_blocks, runner.bm.num_blocks)
+    self.hcap = 4 + 3 * self.max_batch + FREE_CAP
 
   # ------------------------------------------------------------------ rank-0 API side
   def submit(self, rid: str, ids: Sequence[int], temp: float = 0.0, max_tokens: int = 256) -> None:
@@ -83,43 +129,42 @@ class RingServer:
     self._wake.set()
 
   def idle(self) -> bool:
-    return not self._running and self._inbox.empty()
+    return not self._running and not self._waiting and self._inbox.empty()
 
   def _emit(self, rid: str, toks: List[int], fin: bool) -> None:
     for cb in self._callbacks:
       cb(rid, toks, fin)
 
-  # ------------------------------------------------------------------ wire format
-  @staticmethod
-  def _header(items, free, stop: bool) -> torch.Tensor:
-    """[n_items, n_free, stop, (key, qlen, temp) * n_items, key * n_free] as float64 (exact for ids < 2^53)."""
-    vals = [float(len(items)), float(len(free)), 1.0 if stop else 0.0]
+  # ------------------------------------------------------------------ control plane (gloo, host to host)
+  def _header(self, items, free, stop: bool) -> torch.Tensor:
+    """[n_items, n_free, stop, generation, (key, qlen, temp) * n_items, key * n_free, 0 ...] float64 of fixed
+    size hcap (exact for ids < 2^53)."""
+    h = torch.zeros(self.hcap, dtype=torch.float64)
+    vals = [float(len(items)), float(len(free)), 1.0 if stop else 0.0, float(self.generation)]
     for key, qlen, temp in items:
       vals += [float(key), float(qlen), float(temp)]
     vals += [float(k) for k in free]
-    return torch.tensor(vals, dtype=torch.float64)
+    h[:len(vals)] = torch.tensor(vals, dtype=torch.float64)
+    return h
 
   @staticmethod
   def _parse(h: torch.Tensor):
     v = h.tolist()
     n, nf, stop = int(v[0]), int(v[1]), v[2] != 0.0
-    items = [(int(v[3 + 3 * i]), int(v[4 + 3 * i]), v[5 + 3 * i]) for i in range(n)]
-    free = [int(x) for x in v[3 + 3 * n:3 + 3 * n + nf]]
+    items = [(int(v[4 + 3 * i]), int(v[5 + 3 * i]), v[6 + 3 * i]) for i in range(n)]
+    free = [int(x) for x in v[4 + 3 * n:4 + 3 * n + nf]]
     return items, free, stop
 
   def _send_header(self, h: torch.Tensor) -> None:
-    # headers go host-staged over the transport (a CUDA copy on RCCL): size first, then the body
-    dev = self.dev
-    self.t.isend(torch.tensor([float(h.numel())], dtype=torch.float64, device=dev), self.next)
-    self.t.isend(h.to(dev), self.next)
+    if self.monitor is not None:
+      self.monitor.check()
+    self._pending_ctl.append((dist.isend(h, self.next, group=self.ctl), h))
+    self._pending_ctl = [(w, t) for w, t in self._pending_ctl if not w.is_completed()]
 
   def _recv_header(self) -> torch.Tensor:
-    dev = self.dev
-    n = torch.empty(1, dtype=torch.float64, device=dev)
-    self.t.recv(n, self.prev)
-    h = torch.empty(int(n.item()), dtype=torch.float64, device=dev)
-    self.t.recv(h, self.prev)
-    return h.cpu()
+    h = torch.empty(self.hcap, dtype=torch.float64)
+    wait_work(dist.irecv(h, self.prev, group=self.ctl), self.monitor)
+    return h
 
   # ------------------------------------------------------------------ one lane step on this rank
   def _stage(self, items, x0: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
@@ -150,25 +195,74 @@ class RingServer:
       self.r.free(str(k))
 
   # ------------------------------------------------------------------ rank 0: scheduler + first stage
+  def _free_pages(self) -> int:
+    bm = self.r.bm
+    return bm.num_free - (bm.num_blocks - self.pool_pages)
+
+  def _pages(self, q: _Req, n: int) -> int:
+    return self.r.bm.blocks_needed(str(q.key), n) if self.r.has(str(q.key)) else -(-n // 64)
+
+  def _release(self, q: _Req) -> None:
+    """Drop a request's pages here and (via the next headers) on every other rank."""
+    if self.r.has(str(q.key)):
+      self.r.free(str(q.key))
+    self._free.append(q.key)
+
   def _admit(self) -> None:
-    room = self.max_batch - len(self._running)
-    while room > 0:
+    while True:
       try:
-        req = self._inbox.get_nowait()
+        self._waiting.append(self._inbox.get_nowait())
       except queue.Empty:
-        return
-      req.key = self._next_key
-      self._next_key += 1
-      if not self.r.can_admit(str(req.key), len(req.ids) + req.max_tokens):
-        self._emit(req.rid, [], True)  # cannot fit its context on this shard: finish it empty
+        break
+    reserve = sum(1 for q in self._running.values() if q.todo() <= 1)  # one page of growth per decoder
+    while self._waiting and len(self._running) < self.max_batch:
+      q = self._waiting[0]
+      total = len(q.ids) + len(q.out)
+      if total + 1 > self.r.max_ctx or -(-(total + 1) // 64) > self.pool_pages:
+        self._waiting.popleft()  # can never fit on this ring: finish it (length)
+        self._emit(q.rid, [], True)
         continue
+      first = min(total, self.step_tokens)
+      if self._running and self._free_pages() - -(-first // 64) < reserve:
+        break  # wait for pages (an empty ring always admits: preemption makes the room)
+      self._waiting.popleft()
+      q.key, self._next_key = self._next_key, self._next_key + 1
+      q.order, self._next_order = self._next_order, self._next_order + 1
+      q.fed = 0
       loads = [0] * self.lanes
-      for q in self._running.values():
-        loads[q.lane] += 1
-      req.lane = loads.index(min(loads))
-      self._running[req.rid] = req
-      self._by_key[req.key] = req
-      room -= 1
+      for o in self._running.values():
+        loads[o.lane] += 1
+      q.lane = loads.index(min(loads))
+      self._running[q.rid] = q
+      reserve += 1
+
+  def _preempt(self, q: _Req) -> None:
+    self._release(q)
+    del self._running[q.rid]
+    q.lane, q.fed = -1, 0
+    self._waiting.appendleft(q)
+    self.stats["preempted"] += 1
+
+  def _plan(self, lane: int):
+    """(req, new tokens) of this lane's next step: decoders first, then prompt chunks in admission order
+    within the step's token budget; the youngest are preempted while the step's pages do not fit."""
+    reqs = sorted((q for q in self._running.values() if q.lane == lane), key=lambda q: (q.todo() > 1, q.order))
+    while True:
+      plan, budget = [], self.step_tokens
+      for q in reqs:
+        n = q.todo()
+        if n > 1:
+          n = min(n, budget)
+        if n <= 0 or budget <= 0:
+          continue
+        budget -= n
+        plan.append((q, n))
+      need = sum(self._pages(q, n) for q, n in plan)
+      if need <= self._free_pages() or not plan:
+        return plan
+      victim = max(reqs, key=lambda q: q.order)
+      reqs.remove(victim)
+      self._preempt(victim)
 
   def _collect(self, lane: int) -> None:
     """Rank 0: the ids of this lane's step in flight (the oldest step in flight: lanes run in a cycle)."""
@@ -176,40 +270,45 @@ class RingServer:
     if step is None:
       return
     self._inflight[lane] = None
-    reqs, tok = step
+    plan, tok = step
     if tok is None:  # sampled on another rank
-      tok = torch.empty(len(reqs), dtype=torch.int32, device=self.dev)
+      tok = torch.empty(len(plan), dtype=torch.int32, device=self.dev)
       self.t.wait(self.t.irecv(tok, self.world - 1))
-    for req, t in zip(reqs, tok.tolist()):
-      req.out.append(int(t))
-      fin = t in self.eos or len(req.out) >= req.max_tokens
-      self._emit(req.rid, [int(t)], fin)
+    toks = tok.tolist()
+    if self.monitor is not None:
+      self.monitor.check()  # an aborted transfer delivers garbage: never emit it
+    for (q, n), t in zip(plan, toks):
+      q.fed += n
+      if q.rid not in self._running or self._running[q.rid] is not q:
+        continue
+      if q.todo() > 0:  # a prompt chunk that was not the last one: its sample is not an output
+        continue
+      q.out.append(int(t))
+      fin = (t in self.eos or len(q.out) >= q.max_tokens or len(q.ids) + len(q.out) + 1 > self.r.max_ctx)
+      self._emit(q.rid, [int(t)], fin)
       if fin:
-        del self._running[req.rid]
-        del self._by_key[req.key]
-        self.r.free(str(req.key))
-        self._free.append(req.key)
+        del self._running[q.rid]
+        self._release(q)
 
   def _launch(self, lane: int, stop: bool = False) -> bool:
-    """Rank 0: start this lane's next step (prompts admitted to it, then its decoding requests).
-    Returns whether anything was sent."""
-    reqs = [q for q in self._running.values() if q.lane == lane] if not stop else []
-    if not reqs and not (stop or (self._free and self.world > 1 and self._idle_lanes())):
+    """Rank 0: start this lane's next step.  Returns whether anything was sent."""
+    plan = self._plan(lane) if not stop else []
+    if not plan and not (stop or (self._free and self.world > 1 and self._idle_lanes())):
       return False
     items, ids = [], []
-    for q in reqs:
-      if q.out:
-        items.append((q.key, 1, q.temp))
-        ids.append(q.out[-1])
-      else:
-        items.append((q.key, len(q.ids), q.temp))
-        ids += q.ids
-    free, self._free = self._free, []
+    for q, n in plan:
+      items.append((q.key, n, q.temp))
+      seq = q.ids + q.out
+      ids += seq[q.fed:q.fed + n]
+      if n > 1:
+        self.stats["chunks"] += 1
+    free, self._free = self._free[:FREE_CAP], self._free[FREE_CAP:]
     if self.world > 1:
       self._send_header(self._header(items, free, stop))
     if items:
       tok = self._stage(items, torch.tensor(ids, dtype=torch.int32))
-      self._inflight[lane] = (reqs, tok)
+      self._inflight[lane] = (plan, tok)
+      self.stats["steps"] += 1
     return True
 
   def _idle_lanes(self) -> bool:
@@ -217,10 +316,23 @@ class RingServer:
 
   def serve_forever(self, idle_wait: float = 0.5) -> None:
     """Rank 0 cycles through the lanes: collect a lane's ids, admit, launch its next step.  Other ranks
-    follow the headers.  Rank 0 waits up to idle_wait for work when nothing is running."""
-    if self.rank != 0:
-      self._follow()
-      return
+    follow the headers.  Rank 0 waits up to idle_wait for work when nothing is running.  A peer failure
+    re-forms the ring over the survivors and serving continues (see the module docstring)."""
+    while True:
+      try:
+        if self.rank != 0:
+          self._follow()
+        else:
+          self._lead(idle_wait)
+        return
+      except PeerFailure as e:
+        self._recover(e.dead)
+      except RuntimeError:
+        if self.monitor is None or not self.monitor.failed.is_set():
+          raise
+        self._recover(self.monitor.dead)
+
+  def _lead(self, idle_wait: float) -> None:
     lane = 0
     while True:
       self._collect(lane)
@@ -236,9 +348,15 @@ class RingServer:
         self._wake.clear()
       lane = (lane + 1) % self.lanes
     if self.world > 1:  # stop (with the last frees) travels the ring; followers exit on it
+      while len(self._free) > FREE_CAP:
+        self._send_header(self._header([], self._free[:FREE_CAP], False))
+        self._free = self._free[FREE_CAP:]
       free, self._free = self._free, []
       self._send_header(self._header([], free, True))
     self.t.drain()
+    self._drain_ctl()
+    if self.monitor is not None:
+      self.monitor.stop()
 
   # ------------------------------------------------------------------ ranks 1..N-1
   def _follow(self) -> None:
@@ -253,6 +371,55 @@ class RingServer:
       if stop:
         break
     self.t.drain()
+    self._drain_ctl()
+    if self.monitor is not None:
+      self.monitor.stop()
+
+  def _drain_ctl(self) -> None:
+    for w, _ in self._pending_ctl:
+      try:
+        w.wait()
+      except Exception:
+        pass
+    self._pending_ctl = []
+
+  # ------------------------------------------------------------------ failure recovery
+  def _recover(self, dead: Sequence[int]) -> None:
+    """Survivors: re-form a dense ring, re-partition the layers over it, rebuild this rank's shard; rank 0
+    re-admits every running request (re-prefill of prompt + tokens so far)."""
+    alive = [r for r in range(self.world) if r not in set(dead)]
+    if 0 not in alive or self.make_runner is None or self.rank not in alive:
+      raise PeerFailure(dead, "the API rank is gone or this server cannot rebuild its shard")
+    if self.monitor is not None:
+      self.monitor.stop()  # it would otherwise keep watching the old ring and abort the new groups
+    self.generation += 1
+    self.stats["recoveries"] += 1
+    print(f"[ring {self.rank}] peer(s) {sorted(dead)} failed: re-forming the ring over {alive} "
+          f"(generation {self.generation})", flush=True)
+    self._pending_ctl = []
+    new_rank, new_world = reform_ring(alive, self.rank, self.generation, backend=self.backend)
+    from .comm import P2PTransport
+    ctl = control_group() if new_world > 1 else None
+    monitor = None
+    if self.monitor is not None:
+      monitor = HealthMonitor(new_rank, new_world, interval=self.monitor.interval, timeout=self.monitor.timeout,
+                              generation=self.generation).start()
+    # the fault injector (tests) stays with the original rank numbering: none after a re-form
+    transport = P2PTransport(new_rank, new_world, monitor=monitor, injector=FaultInjector("", new_rank))
+    old = self.r
+    self.r = None
+    del old  # free this GPU's old shard before building the new one
+    if torch.cuda.is_available():
+      torch.cuda.empty_cache()
+    runner, pool = self.make_runner(new_rank, new_world, ctl)
+    self.ctl, self.t, self.monitor = ctl, transport, monitor
+    self._set_topology(runner, new_rank, new_world, pool)
+    if self.rank == 0:
+      for q in sorted(self._running.values(), key=lambda q: q.order, reverse=True):
+        q.lane, q.fed = -1, 0
+        self._waiting.appendleft(q)  # oldest ends up first
+      self._running.clear()
+      self._free = []
 
 
 # ---------------------------------------------------------------------- API adapter + process spawner
@@ -297,9 +464,39 @@ class RingNode:
     self.srv.submit(request_id, ids, self.default_temp if temp is None else float(temp), int(mt))
 
 
+def control_group():
+  """The gloo group that carries the headers: host to host, and with a week-long timeout (followers wait in
+  a header receive for as long as the API has nothing to serve)."""
+  import datetime
+  return dist.new_group(backend="gloo", timeout=datetime.timedelta(days=7))
+
+
+def ring_shards(model: str, num_layers: int, world: int, ctl=None):
+  """Layer ranges of the ring's ranks, memory-weighted in ring order (every rank's total GPU memory,
+  exchanged over the control group)."""
+  from ..topology.ring_memory_weighted_partitioning_strategy import memory_weighted_layer_shards
+  mem = 1
+  if torch.cuda.is_available():
+    mem = torch.cuda.get_device_properties(torch.cuda.current_device()).total_memory >> 20
+  mems = [mem]
+  if world > 1:
+    t = torch.tensor([mem], dtype=torch.int64)
+    out = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(out, t, group=ctl)
+    mems = [int(x[0]) for x in out]
+  return memory_weighted_layer_shards(model, num_layers, mems)
+
+
+def min_pool_pages(runner, world: int, ctl=None) -> int:
+  """The smallest KV pool (pages) of the ring: every rank sizes its plan to it."""
+  n = torch.tensor([runner.bm.num_blocks], dtype=torch.int64)
+  if world > 1:
+    dist.all_reduce(n, op=dist.ReduceOp.MIN, group=ctl)
+  return int(n[0])
+
+
 def _serve_worker(rank: int, world: int, port: int, a: dict) -> None:
   import asyncio
-  import os
   os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
                     MASTER_PORT=str(port))
   from ..inference.shard import Shard
@@ -308,21 +505,28 @@ def _serve_worker(rank: int, world: int, port: int, a: dict) -> None:
   from ..models.config import load_config, preset
   from ..models.weights import load_hf_weights
   from ..runtime.runner import ShardRunner
-  from ..topology.ring_memory_weighted_partitioning_strategy import equal_layer_shards
   from ..train.ring_train import _model_dir
   from .comm import P2PTransport, init_distributed
 
   rank, world, dev = init_distributed()
-  ctl = dist.new_group(backend="gloo") if world > 1 else None
+  ctl = control_group() if world > 1 else None
   model = a["model"]
   mdir = _model_dir(model)
   cfg = load_config(mdir) if mdir is not None else preset(model)
-  shard = equal_layer_shards(model, cfg.num_layers, world)[rank]
-  weights = load_hf_weights(mdir, cfg, shard, dev) if mdir is not None and any(mdir.glob("*.safetensors")) else None
-  runner = ShardRunner(cfg, shard, dev, weights=weights, max_batch=a["max_batch"], max_ctx=a["max_ctx"], seed=0)
-  srv = RingServer(runner, rank, world, P2PTransport(rank, world), ctl, eos_ids=cfg.eos_token_ids)
-  print(f"[ring {rank}/{world}] {model} layers {shard.start_layer}-{shard.end_layer} on {dev}"
-        + ("" if weights is not None else " (random-init weights: no local checkpoint)"), flush=True)
+
+  def make_runner(r, w, group):
+    shard = ring_shards(model, cfg.num_layers, w, group)[r]
+    weights = (load_hf_weights(mdir, cfg, shard, dev)
+               if mdir is not None and any(mdir.glob("*.safetensors")) else None)
+    runner = ShardRunner(cfg, shard, dev, weights=weights, max_batch=a["max_batch"], max_ctx=a["max_ctx"], seed=0)
+    print(f"[ring {r}/{w}] {model} layers {shard.start_layer}-{shard.end_layer} on {dev}"
+          + ("" if weights is not None else " (random-init weights: no local checkpoint)"), flush=True)
+    return runner, min_pool_pages(runner, w, group)
+
+  runner, pool = make_runner(rank, world, ctl)
+  monitor = HealthMonitor(rank, world).start() if world > 1 and os.environ.get("XOT_RING_HEALTH", "1") == "1" else None
+  srv = RingServer(runner, rank, world, P2PTransport(rank, world, monitor=monitor), ctl, eos_ids=cfg.eos_token_ids,
+                   monitor=monitor, make_runner=make_runner, pool_pages=pool)
   if rank == 0:
     tok = _resolve_tokenizer(mdir if mdir is not None else (registry.get_repo(model, "ShardedInferenceEngine") or "byte"),
                              cfg.vocab_size)
@@ -330,7 +534,7 @@ def _serve_worker(rank: int, world: int, port: int, a: dict) -> None:
     asyncio.run(_rank0_main(srv, full, tok, cfg, a))
   else:
     srv.serve_forever()
-  if world > 1:
+  if dist.is_initialized():
     dist.destroy_process_group()
 
 
@@ -341,7 +545,7 @@ async def _rank0_main(srv: RingServer, shard, tok, cfg, a: dict) -> None:
   th = threading.Thread(target=srv.serve_forever, name="xot-ring-rounds", daemon=True)
   th.start()
   try:
-    if a.get("prompt") is not None:  # `xot run <model> --ring`: one prompt, print the answer
+    if a.get("prompt") is not None:  # `xot run <model> --gpus N`: one prompt, print the answer
       done = asyncio.Event()
       out: List[int] = []
 
@@ -368,8 +572,7 @@ async def _rank0_main(srv: RingServer, shard, tok, cfg, a: dict) -> None:
 
 
 def serve_ring(args) -> int:
-  """`xot [run] <model> --ring --gpus N`: one process per GPU, continuous-batching ring over RCCL."""
-  import os
+  """`xot [run] <model> --gpus N`: one process per GPU, continuous-batching ring over RCCL."""
   import torch.multiprocessing as mp
   from ..train.ring_train import _free_port
   n = args.gpus or max(1, torch.cuda.device_count())

@@ -36,3 +36,21 @@ def equal_layer_shards(model_id: str, num_layers: int, world: int):
                                                                  flops=DeviceFlops(fp32=0, fp16=0, int8=0)))
   parts = RingMemoryWeightedPartitioningStrategy().partition(t)
   return map_partitions_to_shards(parts, num_layers, model_id)
+
+
+def memory_weighted_layer_shards(model_id: str, num_layers: int, memories):
+  """Shards for GPU peers whose ring order is fixed (process ring: rank r sends to rank r + 1): peer i gets
+  a slice of [0, 1) proportional to memories[i], boundaries rounded to 5 decimals exactly as the strategy
+  above does, but in the given order instead of sorted by memory.  Equal memories give equal_layer_shards."""
+  from .partitioning_strategy import Partition, map_partitions_to_shards
+  total = float(sum(memories))
+  parts, start = [], 0.0
+  for i, m in enumerate(memories):
+    share = m / total if total > 0 else 1.0 / len(memories)
+    end = round(start + share, 5)
+    parts.append(Partition(f"rank{i}", start, end))
+    start = end
+  shards = map_partitions_to_shards(parts, num_layers, model_id)
+  if len(shards) != len(memories):
+    raise ValueError(f"{num_layers} layers cannot be split over {len(memories)} peers with memories {list(memories)}")
+  return shards
