@@ -47,6 +47,9 @@ def main():
   ap.add_argument("--prompt-len", type=int, default=512)
   ap.add_argument("--temperature", type=float, default=0.6)
   ap.add_argument("--layers", type=int, default=0, help="debug only: truncate the model (result marked invalid)")
+  ap.add_argument("--dump-tokens", default=None,
+                  help="tests: the sampling rank writes micro-batch 0's generated ids (JSON) to this path; the "
+                       "per-step host reads make the timing meaningless")
   ap.add_argument("--weight-dtype", default="bf16", choices=["bf16", "fp8"],
                   help="fp8: weight-only e4m3 projections (a separate, reduced-precision measurement; the headline "
                        "is bf16)")
@@ -102,7 +105,8 @@ def main():
   log(f"[rank {rank}] prefill {M * B} x {args.prompt_len} tokens in {t_prefill:.1f}s")
 
   # ---- warmup rounds (graph capture + GEMM policy tuning happen here)
-  toks = run_decode_steps(stage, mbs, args.warmup, first_tokens=first if stage.last else None)
+  rec = args.dump_tokens is not None
+  toks = run_decode_steps(stage, mbs, args.warmup, first_tokens=first if stage.last else None, record=rec)
   transport.drain()
   sync()
   log(f"[rank {rank}] warmup done")
@@ -112,7 +116,7 @@ def main():
     dist.barrier()
   sync()
   t0 = time.perf_counter()
-  toks = run_decode_steps(stage, mbs, args.steps, first_tokens=toks if stage.last else None)
+  toks = run_decode_steps(stage, mbs, args.steps, first_tokens=toks if stage.last else None, record=rec)
   transport.drain()
   sync()
   if world > 1:
@@ -123,6 +127,9 @@ def main():
     dist.all_reduce(e, op=dist.ReduceOp.MAX)
     elapsed = float(e.item())
 
+  if rec and stage.samples:
+    with open(args.dump_tokens, "w") as f:
+      json.dump(mbs[0].tokens, f)
   total_tokens = args.steps * M * B
   tps = total_tokens / elapsed
   ms_step = elapsed / args.steps * 1e3

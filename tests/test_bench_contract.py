@@ -38,3 +38,29 @@ def test_bench_json_line(n):
   assert d["n_gpus"] == n and d["steps"] == 2 and d["warmup"] == 1
   assert d["config"]["global_batch"] == 2 * n and d["value"] > 0
   assert d["scaling"] == "weak" and d["higher_is_better"] is True
+
+
+@pytest.mark.parametrize("n", [4, 8])
+def test_bench_driver_command_many_ranks(n, tmp_path):
+  """The driver's exact 8-GPU command line shape (torchrun, one rank per device) at 4 and 8 ranks over gloo:
+  one JSON line, weak scaling (global batch = ranks x batch per GPU), and micro-batch 0's greedy tokens equal
+  the single-process run's, through the split LM head (last stage: top-k candidates of vocab rows [0, Vs);
+  first stage: rows [Vs, V) + the sample)."""
+  base = ["bench.py", "--steps", "3", "--warmup", "1", "--model", "tiny-llama-8l", "--batch-per-gpu", "2",
+          "--prompt-len", "8", "--temperature", "0"]
+  env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1")
+  one = subprocess.run([sys.executable] + base + ["--gpus", "1", "--dump-tokens", str(tmp_path / "t1.json")], cwd=ROOT,
+                       env=env, capture_output=True, text=True, timeout=300)
+  assert one.returncode == 0, one.stderr[-3000:]
+  cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}", "--master-addr",
+         "127.0.0.1", "--master-port", str(_port())] + base + ["--gpus", str(n), "--dump-tokens", str(tmp_path / "tn.json")]
+  r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+  assert r.returncode == 0, r.stderr[-3000:]
+  lines = [l for l in r.stdout.splitlines() if l.strip().startswith("{")]
+  assert len(lines) == 1, r.stdout
+  d = json.loads(lines[0])
+  assert d["n_gpus"] == n and d["config"]["global_batch"] == 2 * n and d["config"]["parallelism"].startswith(f"pp{n}")
+  t1, tn = json.load(open(tmp_path / "t1.json")), json.load(open(tmp_path / "tn.json"))
+  # with the split head a round's ids are drawn at the start of the next round by the first stage, so the
+  # ring's list starts with the prefill token and the single-process list with the first decode token
+  assert tn and len(tn) == len(t1) and tn[1:] == t1[:-1]

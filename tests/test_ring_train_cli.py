@@ -92,3 +92,13 @@ def test_ring_train_gpu_single(gpu, tmp_path):
               "--lr", "1e-3"], tmp_path, cpu=False)
   losses = [float(l.split("loss:")[1].split(",")[0]) for l in out.splitlines() if l.startswith("epoch")]
   assert len(losses) == 3 and losses[-1] < losses[0]
+
+
+def test_xot_run_gpus_defaults_to_rccl_ring(tmp_path):
+  """`xot run <model> --gpus 2` (no --ring): one process per device as one ring with the p2p data plane
+  (gloo on this CPU host, RCCL on GPUs) -- the same answer as the single-process run."""
+  one = _xot(["run", "tiny-llama", "--prompt", "hello ring", "--max-generate-tokens", "6"], tmp_path)
+  two = _xot(["run", "tiny-llama", "--gpus", "2", "--prompt", "hello ring", "--max-generate-tokens", "6"], tmp_path)
+  assert "[ring 1/2]" in two and "layers 2-3" in two
+  ans = lambda out: [l for l in out.splitlines() if l.strip() and not l.startswith("[")][-1]
+  assert ans(two) == ans(one)

@@ -4,8 +4,12 @@
   xot run <model> [--prompt ...]        one prompt through the ring, print the answer
   xot eval <model> [--data DIR]         one pass over test.jsonl, print the length-weighted loss
   xot train <model> [--iters N ...]     pipeline training over the ring, checkpoint every --save-every
-  xot --gpus N ...                      spawn one peer process per local GPU (each GPU is a ring peer;
-                                        rank 0 serves the API), connected by a generated manual topology
+  xot --gpus N ...                      one process per local GPU as ONE RCCL ring (parallel/ring_serve.py:
+                                        continuous batching, activations over xGMI, rank 0 serves the API;
+                                        train / eval: parallel/pipeline_train.py)
+  xot --gpus N --grpc-peers ...         the reference's topology instead: one gRPC peer process per GPU,
+                                        connected by a generated manual-discovery file (cross-host rings
+                                        always use gRPC + discovery)
 """
 from __future__ import annotations
 
@@ -68,9 +72,12 @@ def build_parser() -> argparse.ArgumentParser:
   p.add_argument("--node-id-filter", type=str, default=None, help="Comma separated node ids to allow")
   p.add_argument("--interface-type-filter", type=str, default=None, help="Comma separated interface types to allow")
   p.add_argument("--system-prompt", type=str, default=None, help="System prompt for the ChatGPT API")
-  p.add_argument("--gpus", type=int, default=0, help="Spawn one peer process per local GPU (0 = single process)")
+  p.add_argument("--gpus", type=int, default=0,
+                 help="Serve/run/train/eval over N local GPUs as one RCCL ring, one process per GPU (0 = single process)")
   p.add_argument("--ring", action="store_true",
-                 help="serve/run/train/eval over the local GPUs as one RCCL ring (one process per GPU, no gRPC hops)")
+                 help="(default with --gpus N > 1) the local GPUs as one RCCL ring; with --gpus 0/1: every visible GPU")
+  p.add_argument("--grpc-peers", action="store_true",
+                 help="--gpus N: one gRPC peer process per GPU (the reference's per-hop RPC) instead of the RCCL ring")
   p.add_argument("--micro-batch", type=int, default=1, help="--ring: sequences per pipeline micro-batch")
   p.add_argument("--parallel", choices=("pp", "dp"), default="pp",
                  help="--ring: pp = layer pipeline over the GPUs; dp = a full replica per GPU, gradients all-reduced")
@@ -372,6 +379,8 @@ def run(argv=None):
     os.environ["XOT_MAX_BATCH"] = str(args.max_batch)
   if args.max_ctx:
     os.environ["XOT_MAX_CTX"] = str(args.max_ctx)
+  if args.gpus and args.gpus > 1 and not args.grpc_peers and "XOT_PEER_RANK" not in os.environ:
+    args.ring = True  # local GPUs are ring peers over RCCL unless the gRPC topology is asked for
   if args.ring and args.command in ("train", "eval"):
     from .train.ring_train import run_ring
     sys.exit(run_ring(args))

@@ -343,6 +343,9 @@ PRESETS: dict[str, ModelConfig] = {
   # small shapes for tests / CPU plumbing
   "tiny-llama": ModelConfig("llama", 512, 256, 512, 4, 4, 2, 64, 1e-5, 10000.0, None, 2048, False,
                             bos_token_id=1, eos_token_ids=(2,)),
+  # 8 layers: multi-rank rehearsals of the 8-GPU ring (one layer per rank)
+  "tiny-llama-8l": ModelConfig("llama", 512, 256, 512, 8, 4, 2, 64, 1e-5, 10000.0, None, 2048, False,
+                               bos_token_id=1, eos_token_ids=(2,)),
   "tiny-llama-d64": ModelConfig("llama", 1024, 256, 512, 6, 4, 2, 64, 1e-5, 10000.0, _L3, 4096, True,
                                 bos_token_id=1, eos_token_ids=(2,)),
   "tiny-qwen": ModelConfig("qwen2", 512, 256, 512, 4, 4, 2, 64, 1e-6, 1000000.0, None, 2048, True, True,

@@ -555,7 +555,10 @@ async def _rank0_main(srv: RingServer, shard, tok, cfg, a: dict) -> None:
           done.set()
 
       node.on_token.register("run").on_next(on_tok)
-      await node.process_prompt(shard, a["prompt"], request_id="run-0",
+      # the same chat-templated prompt as the single-process `xot run` (main.run_model_cli)
+      templ = tok.apply_chat_template([{"role": "user", "content": a["prompt"]}], tokenize=False,
+                                      add_generation_prompt=True)
+      await node.process_prompt(shard, templ, request_id="run-0",
                                 inference_state={"max_tokens": a["max_generate_tokens"]})
       await asyncio.wait_for(done.wait(), timeout=600)
       print(tok.decode([t for t in out if t not in set(cfg.eos_token_ids)]), flush=True)

@@ -87,31 +87,46 @@ class ShardRunner:
     # contexts of a few hundred tokens the full width split every sequence into 4 mostly empty partitions
     # plus a merge pass
     self._widths = sorted({w for w in (8, 32) if w < self.width} | {self.width})
-    self._tables_cls = {}
-    self._tables_host = torch.zeros(max_batch, self.width, dtype=torch.int32)
-    self._ctx_host = torch.zeros(max_batch, dtype=torch.int32)
+    # host staging of the step inputs, double-buffered: a step's async copies read one set while the host
+    # fills the other for the next step, so the host can queue a step behind the one still copying (with
+    # one set it had to wait for the previous step's copies before writing the next step's inputs)
     bmax = _bucket(max_batch)
-    self._pos_host = torch.zeros(bmax, dtype=torch.int32)  # decode-step positions / slots (graph inputs)
-    self._slots_host = torch.zeros(bmax, dtype=torch.int64)
-    self._staged = None  # event marking completion of the last async H2D copy out of the pinned buffers
-    if self.device.type == "cuda":
-      # pinned: an async copy out of pageable memory may wait for the stream to drain, i.e. for the step
-      # already running, which would forbid queueing the next decode step behind it
-      self._tables_host = self._tables_host.pin_memory()
-      self._ctx_host = self._ctx_host.pin_memory()
-      self._pos_host = self._pos_host.pin_memory()
-      self._slots_host = self._slots_host.pin_memory()
+    self._sets = []
+    for _ in range(2):
+      st = {"tables": torch.zeros(max_batch, self.width, dtype=torch.int32),
+            "ctx": torch.zeros(max_batch, dtype=torch.int32),
+            "pos": torch.zeros(bmax, dtype=torch.int32),  # decode-step positions / slots (graph inputs)
+            "slots": torch.zeros(bmax, dtype=torch.int64)}
+      if self.device.type == "cuda":
+        # pinned: an async copy out of pageable memory may wait for the stream to drain, i.e. for the step
+        # already running, which would forbid queueing the next decode step behind it
+        st = {k: v.pin_memory() for k, v in st.items()}
+      st["cls"] = {}  # narrower block tables per width class
+      st["event"] = None  # completion of the last async H2D copy out of this set
+      self._sets.append(st)
+    self._set_idx = 1
+    self._use_set(0)
+
+  def _use_set(self, i: int) -> None:
+    st = self._sets[i]
+    self._set_idx = i
+    self._tables_host, self._ctx_host, self._pos_host, self._slots_host = st["tables"], st["ctx"], st["pos"], st["slots"]
+    self._tables_cls = st["cls"]
 
   def _reuse_staging(self) -> None:
-    """The pinned staging buffers may still be read by an in-flight async copy: wait for it."""
-    if self._staged is not None:
-      self._staged.synchronize()
-      self._staged = None
+    """Switch to the other staging set; wait only if ITS last async copy (two steps back) is still running."""
+    i = self._set_idx ^ 1
+    ev = self._sets[i]["event"]
+    if ev is not None:
+      ev.synchronize()
+      self._sets[i]["event"] = None
+    self._use_set(i)
 
   def _mark_staged(self) -> None:
     if self.device.type == "cuda":
-      self._staged = torch.cuda.Event()
-      self._staged.record()
+      ev = torch.cuda.Event()
+      ev.record()
+      self._sets[self._set_idx]["event"] = ev
 
   # ------------------------------------------------------------------ bookkeeping
   def has(self, rid: str) -> bool:
