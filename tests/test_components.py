@@ -136,13 +136,86 @@ def test_wire_roundtrip():
   y = wire.decode_tensor(wire.encode_tensor(x))
   assert y.dtype == np.float32 and (y == x).all()
   t = torch.randn(2, 3, 5).to(torch.bfloat16)
-  msg = wire.unpack(wire.pack({"tensor": wire.encode_tensor(t), "state": {"n_past": 3}}))
-  t2 = wire.decode_tensor(msg["tensor"])
+  t2 = wire.decode_tensor(wire.M.Tensor.FromString(wire.encode_tensor(t).SerializeToString()))
   assert t2.dtype == torch.bfloat16 and torch.equal(t2, t)
-  assert msg["state"] == {"n_past": 3}
   assert wire.decode_tensor(wire.encode_tensor(None)) is None
   ids = np.array([[1, 2, 3]], dtype=np.int64)
   assert (wire.decode_tensor(wire.encode_tensor(ids)) == ids).all()
+  st = {"n_past": 3, "pc": {"save": [0, 192]}, "h": torch.ones(2, 2).to(torch.bfloat16), "l": [np.zeros(3, np.int32)],
+        "temperature": np.float32(0.5)}
+  back = wire.decode_state(wire.M.InferenceState.FromString(wire.encode_state(st).SerializeToString()))
+  assert back["n_past"] == 3 and back["pc"] == {"save": [0, 192]} and back["temperature"] == 0.5
+  assert torch.equal(back["h"], st["h"]) and (back["l"][0] == 0).all()
+
+
+def test_node_service_messages_roundtrip():
+  """Every message of the reference schema (xotorch/networking/grpc/node_service.proto:15-116) encodes and
+  decodes through the runtime-built descriptors, optional fields keep their presence."""
+  from xotorch_support_jetson_amd.networking.grpc.node_service_pb import METHODS, M, SERVICE, method_path
+  tens = M.Tensor(tensor_data=b"\x01\x02", shape=[1, 2], dtype="uint8")
+  sh = M.Shard(model_id="llama-3-70b", start_layer=10, end_layer=19, n_layers=80)
+  st = M.InferenceState(other_data_json='{"n_past": 4}')
+  st.tensor_data["x"].CopyFrom(tens)
+  st.tensor_list_data["y"].tensors.extend([tens, tens])
+  topo = M.Topology()
+  topo.nodes["a"].CopyFrom(M.DeviceCapabilities(model="MI355X", chip="gfx950", memory=288 * 1024,
+                                                flops=M.DeviceFlops(fp32=157.3, fp16=2500.0, int8=5000.0)))
+  topo.peer_graph["a"].connections.add(to_id="b", description="xGMI")
+  topo.peer_graph["a"].connections.add(to_id="c")
+  msgs = [sh, tens, st, topo, M.TensorList(tensors=[tens]),
+          M.PromptRequest(shard=sh, prompt="hi", request_id="r", inference_state=st),
+          M.TensorRequest(shard=sh, tensor=tens, request_id="r", inference_state=st),
+          M.ExampleRequest(shard=sh, example=tens, target=tens, length=tens, train=True, request_id="r"),
+          M.Loss(loss=1.5, grads=tens), M.CollectTopologyRequest(visited=["a", "b"], max_depth=4),
+          M.PeerConnection(to_id="b", description="d"), M.PeerConnections(connections=[M.PeerConnection(to_id="z")]),
+          M.DeviceFlops(fp32=1.0, fp16=2.0, int8=4.0), M.DeviceCapabilities(model="m", chip="c", memory=1),
+          M.SendResultRequest(request_id="r", result=[1, 2, 3], tensor=tens, is_finished=True),
+          M.SendOpaqueStatusRequest(request_id="r", status="{}"), M.HealthCheckRequest(),
+          M.HealthCheckResponse(is_healthy=True), M.Empty()]
+  for m in msgs:
+    assert type(m).FromString(m.SerializeToString()) == m, type(m).__name__
+  bare = M.TensorRequest.FromString(M.TensorRequest(shard=sh, tensor=tens).SerializeToString())
+  assert not bare.HasField("request_id") and not bare.HasField("inference_state")
+  assert not M.PeerConnection.FromString(M.PeerConnection(to_id="x").SerializeToString()).HasField("description")
+  assert SERVICE == "node_service.NodeService" and method_path("SendTensor") == "/node_service.NodeService/SendTensor"
+  assert set(METHODS) == {"SendPrompt", "SendTensor", "SendExample", "CollectTopology", "SendResult",
+                          "SendOpaqueStatus", "HealthCheck"}
+
+
+def test_node_service_descriptor_matches_reference():
+  """Wire compatibility: the runtime-built file descriptor equals the one the reference's generated stubs
+  register (read from node_service_pb2.py's serialized descriptor with ast -- nothing of it is executed)."""
+  import ast
+  import pathlib
+
+  from google.protobuf import descriptor_pb2
+
+  from xotorch_support_jetson_amd.networking.grpc.node_service_pb import FILE
+  ref = pathlib.Path("/root/reference/xotorch/networking/grpc/node_service_pb2.py")
+  if not ref.exists():
+    pytest.skip("reference checkout not present")
+  blob = None
+  for node in ast.walk(ast.parse(ref.read_text())):
+    if isinstance(node, ast.Call) and getattr(node.func, "attr", "") == "AddSerializedFile":
+      blob = ast.literal_eval(node.args[0])
+  assert blob is not None
+  theirs = descriptor_pb2.FileDescriptorProto.FromString(blob)
+  ours = descriptor_pb2.FileDescriptorProto()
+  FILE.CopyToProto(ours)
+  assert ours.package == theirs.package and [s.name for s in ours.service] == [s.name for s in theirs.service]
+  assert [(m.name, m.input_type, m.output_type) for m in ours.service[0].method] == \
+         [(m.name, m.input_type, m.output_type) for m in theirs.service[0].method]
+
+  def fields(fdp):
+    out = {}
+    for m in fdp.message_type:
+      for f in m.field:
+        out[(m.name, f.name)] = (f.number, f.type, f.label, f.type_name, f.proto3_optional)
+      for n in m.nested_type:
+        for f in n.field:
+          out[(m.name + "." + n.name, f.name)] = (f.number, f.type, f.label, f.type_name, n.options.map_entry)
+    return out
+  assert fields(ours) == fields(theirs)
 
 
 # ---------------------------------------------------------------- dataset

@@ -1,8 +1,9 @@
 """gRPC client side of a peer (reference: xotorch/networking/grpc/grpc_peer_handle.py:25-230).
 
-Same channel options (256 MB messages, keepalive, tcp_nodelay), no gzip by default (bf16
-activations do not compress), msgpack messages (wire.py).  `send_loss` — an RPC the reference calls
-but never defines — does not exist here; gradients come back in SendExample's reply.
+Same channel options (256 MB messages, keepalive, tcp_nodelay) and the reference's protobuf messages and
+method paths (wire.py / node_service_pb.py); gzip compression is opt-in (XOT_GRPC_GZIP=1: bf16
+activations barely compress).  `send_loss` -- an RPC the reference calls but never defines -- does not
+exist here; gradients come back in SendExample's reply (Loss.grads).
 """
 from __future__ import annotations
 
@@ -16,7 +17,8 @@ from ...inference.shard import Shard
 from ...topology.device_capabilities import DeviceCapabilities
 from ...topology.topology import Topology
 from ..peer_handle import PeerHandle
-from .wire import decode_tensor, encode_tensor, method_path, pack, unpack
+from .wire import (GZIP, METHODS, M, decode_topology, encode_state, encode_tensor, method_path, opt_tensor,
+                   shard_msg)
 
 CHANNEL_OPTIONS = [
   ("grpc.max_metadata_size", 32 * 1024 * 1024),
@@ -80,19 +82,20 @@ class GRPCPeerHandle(PeerHandle):
 
   def _call(self, name: str):
     if name not in self._calls:
-      self._calls[name] = self.channel.unary_unary(method_path(name), request_serializer=lambda b: b,
-                                                   response_deserializer=lambda b: b)
+      req, resp = METHODS[name]
+      self._calls[name] = self.channel.unary_unary(method_path(name), request_serializer=req.SerializeToString,
+                                                   response_deserializer=resp.FromString)
     return self._calls[name]
 
-  async def _rpc(self, name: str, msg: dict, timeout: Optional[float] = None):
+  async def _rpc(self, name: str, msg, timeout: Optional[float] = None):
     await self._ensure_connected()
-    resp = await self._call(name)(pack(msg), timeout=timeout)
-    return unpack(resp) if resp else None
+    kw = {"compression": grpc.Compression.Gzip} if GZIP else {}
+    return await self._call(name)(msg, timeout=timeout, **kw)
 
   async def health_check(self, timeout: float = 3.0) -> bool:
     try:
-      r = await asyncio.wait_for(self._rpc("HealthCheck", {}, timeout=timeout), timeout)
-      return bool(r and r.get("is_healthy"))
+      r = await asyncio.wait_for(self._rpc("HealthCheck", M.HealthCheckRequest(), timeout=timeout), timeout)
+      return bool(r is not None and r.is_healthy)
     except asyncio.TimeoutError:
       return False
     except Exception:
@@ -103,33 +106,44 @@ class GRPCPeerHandle(PeerHandle):
 
   async def send_prompt(self, shard: Shard, prompt: str, request_id: Optional[str] = None,
                         inference_state: Optional[dict] = None) -> None:
-    await self._rpc("SendPrompt", {"shard": shard.to_dict(), "prompt": prompt, "request_id": request_id,
-                                   "inference_state": inference_state})
+    m = M.PromptRequest(shard=shard_msg(shard), prompt=prompt)
+    if request_id is not None:
+      m.request_id = request_id
+    if inference_state is not None:
+      m.inference_state.CopyFrom(encode_state(inference_state))
+    await self._rpc("SendPrompt", m)
 
   async def send_tensor(self, shard: Shard, tensor, request_id: Optional[str] = None,
                         inference_state: Optional[dict] = None) -> None:
-    await self._rpc("SendTensor", {"shard": shard.to_dict(), "tensor": encode_tensor(tensor), "request_id": request_id,
-                                   "inference_state": inference_state})
+    m = M.TensorRequest(shard=shard_msg(shard), tensor=encode_tensor(tensor))
+    if request_id is not None:
+      m.request_id = request_id
+    if inference_state is not None:
+      m.inference_state.CopyFrom(encode_state(inference_state))
+    await self._rpc("SendTensor", m)
 
   async def send_example(self, shard: Shard, example, target, length, train: bool,
                          request_id: Optional[str] = None):
-    r = await self._rpc("SendExample", {"shard": shard.to_dict(), "example": encode_tensor(example),
-                                        "target": encode_tensor(target), "length": encode_tensor(length),
-                                        "train": bool(train), "request_id": request_id})
-    loss = r.get("loss")
-    grads = decode_tensor(r.get("grads"))
-    return (loss, grads) if train else loss
+    m = M.ExampleRequest(shard=shard_msg(shard), example=encode_tensor(example), target=encode_tensor(target),
+                         length=encode_tensor(length), train=bool(train))
+    if request_id is not None:
+      m.request_id = request_id
+    r = await self._rpc("SendExample", m)
+    grads = opt_tensor(r, "grads")
+    return (float(r.loss), grads) if train else float(r.loss)
 
   async def send_result(self, request_id: str, result, is_finished: bool) -> None:
-    tensor = None
+    m = M.SendResultRequest(request_id=request_id, is_finished=bool(is_finished))
     if hasattr(result, "shape") and getattr(result, "ndim", 1) > 1:
-      tensor, result = encode_tensor(result), []
-    await self._rpc("SendResult", {"request_id": request_id, "result": [int(x) for x in result], "tensor": tensor,
-                                   "is_finished": bool(is_finished)}, timeout=15)
+      m.tensor.CopyFrom(encode_tensor(result))
+    else:
+      m.result.extend(int(x) for x in result)
+    await self._rpc("SendResult", m, timeout=15)
 
   async def send_opaque_status(self, request_id: str, status: str) -> None:
-    await self._rpc("SendOpaqueStatus", {"request_id": request_id, "status": status}, timeout=10)
+    await self._rpc("SendOpaqueStatus", M.SendOpaqueStatusRequest(request_id=request_id, status=status), timeout=10)
 
   async def collect_topology(self, visited: set, max_depth: int) -> Topology:
-    r = await self._rpc("CollectTopology", {"visited": sorted(visited), "max_depth": int(max_depth)}, timeout=5)
-    return Topology.from_json(r or {})
+    r = await self._rpc("CollectTopology", M.CollectTopologyRequest(visited=sorted(visited), max_depth=int(max_depth)),
+                        timeout=5)
+    return Topology.from_json(decode_topology(r))
