@@ -1,0 +1,23 @@
+#!/bin/bash
+# The other BASELINE.json configs on one GPU: 8B and 70B batch-1 / batch-512 decode, Mixtral, model families,
+# weight-only FP8, long context.   bash tools/gpu/configs.sh [dense|moe|families|fp8|long]...  (default: dense moe)
+source "$(dirname "$0")/common.sh"
+for what in ${@:-dense moe}; do
+  case $what in
+    dense) step cfg/l8b_b1 600 python bench.py --model llama-3-8b --batch-per-gpu 1 --steps 32 --warmup 4
+           step cfg/l8b_b512 600 python bench.py --model llama-3-8b --batch-per-gpu 512 --steps 16 --warmup 3
+           step cfg/l70b_b1 600 python bench.py --model llama-3-70b --batch-per-gpu 1 --steps 16 --warmup 3 ;;
+    moe)   step cfg/mixtral_b1 600 python bench.py --model mixtral-8x7b --batch-per-gpu 1 --steps 32 --warmup 4
+           step cfg/mixtral_b512 600 python bench.py --model mixtral-8x7b --batch-per-gpu 512 --steps 8 --warmup 3 ;;
+    families)
+           step cfg/dsl_b256 600 python bench.py --model deepseek-coder-v2-lite --batch-per-gpu 256 --steps 16 --warmup 3
+           step cfg/dsv3_8l_b256 600 python bench.py --model deepseek-v3 --layers 8 --batch-per-gpu 256 --steps 8 --warmup 3
+           step cfg/phi4_b256 600 python bench.py --model phi-4-mini --batch-per-gpu 256 --steps 16 --warmup 3
+           step cfg/llava_b64 600 python bench.py --model llava-1.5-7b-hf --batch-per-gpu 64 --steps 16 --warmup 3 ;;
+    fp8)   for m in llama-3-70b llama-3-8b; do for b in 1 64; do
+             step cfg/fp8_${m}_b$b 600 python bench.py --model $m --batch-per-gpu $b --steps 32 --warmup 4 --weight-dtype fp8
+           done; done ;;
+    long)  for t in 8192 32768 65536; do step long/l8b_$t 600 python -u tools/bench_long_prefill.py --model llama-3.1-8b --tokens $t; done
+           step long/l70b_32768 600 python -u tools/bench_long_prefill.py --model llama-3.1-70b --tokens 32768 ;;
+  esac
+done

@@ -1,0 +1,16 @@
+#!/bin/bash
+# Headline (BASELINE config 3, Llama-3-70B, 512 sequences, one GPU) and its kernel breakdown.
+#   bash tools/gpu/headline.sh [bench|ab|prof|sweep]...      (default: bench prof)
+source "$(dirname "$0")/common.sh"
+for what in ${@:-bench prof}; do
+  case $what in
+    bench) step headline/bench 400 python -u bench.py --steps 20 --warmup 5 ;;
+    ab)    # own kernels for every projection vs gate/up row-major on hipBLASLt
+           step headline/own 400 python -u bench.py --steps 10 --warmup 3
+           XOT_ROWMAJOR_PROJ=gu step headline/gu_hipblaslt 400 python -u bench.py --steps 10 --warmup 3 ;;
+    prof)  prof headline/prof 600 python3 "$R/bench.py" --steps 6 --warmup 3
+           step headline/breakdown 60 python tools/decode_breakdown.py "$(ls "$O"/headline/prof/*/*kernel_trace.csv "$O"/headline/prof/*kernel_trace.csv 2>/dev/null | head -1)" --steps 6 --json "$O/headline/breakdown.json"
+           cat "$O/headline/breakdown.log" ;;
+    sweep) for b in 448 512 576; do step headline/b$b 400 python -u bench.py --batch-per-gpu $b --steps 10 --warmup 3; done ;;
+  esac
+done
