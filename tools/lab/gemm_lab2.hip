@@ -4,6 +4,7 @@
 //   ./tools/lab/gemm_lab2 M N K [variant]        variant -1 = all (interleaved rounds), else one (profiling)
 #include "../../xotorch_support_jetson_amd/csrc/gemm_big.hip"
 #include "../../xotorch_support_jetson_amd/csrc/gemm_sk.hip"
+#include "gemm_w4.hip"
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -49,6 +50,16 @@ void launch_sk(const Ctx& c, const uint16_t* W, hipStream_t st) {
                  c.N, c.K, 256, st);
 }
 
+template <int EPI, int DMA>
+void launch_w4(const Ctx& c, const uint16_t* W, hipStream_t st) {
+  auto k = gemm_w4_kernel<EPI, false, false, DMA>;
+  static bool attr = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, w4::SMEM) == hipSuccess;
+  (void)attr;
+  const int nwg = ((c.M + 255) / 256) * (c.N / 256);
+  k<<<nwg, 256, w4::SMEM, st>>>(c.X, c.K, W, nullptr, nullptr, 0, c.Y, EPI == EPI_SILU ? c.N / 2 : c.N, nullptr, c.M, c.N,
+                                c.K, 1);
+}
+
 struct Variant { const char* name; LaunchFn fn; };
 
 int main(int argc, char** argv) {
@@ -71,13 +82,15 @@ int main(int argc, char** argv) {
   std::vector<Variant> vs;
   if (epi == EPI_SILU) {
     vs.push_back({"pp nt(B)     ", launch_v<256, 2, 64, 2, 0, 3, false, 1, EPI_SILU>});
-    vs.push_back({"8ph nt(B)    ", launch_v<256, 2, 64, 2, 0, 3, false, 2, EPI_SILU>});
-    vs.push_back({"8ph plain(B) ", launch_v<256, 2, 64, 2, 0, 0, false, 2, EPI_SILU>});
-    vs.push_back({"base nt(B)   ", launch_v<256, 2, 64, 2, 0, 3, false, 0, EPI_SILU>});
+    vs.push_back({"w4 regs      ", launch_w4<EPI_SILU, 0>});
+    vs.push_back({"w4 W-dma     ", launch_w4<EPI_SILU, 1>});
+    vs.push_back({"w4 all-dma   ", launch_w4<EPI_SILU, 2>});
     vs.push_back({"stream-K     ", launch_sk<EPI_SILU>});
   } else {
     vs.push_back({"pp nt(B)     ", launch_v<256, 2, 64, 2, 0, 3, false, 1, EPI_NONE>});
-    vs.push_back({"8ph nt(B)    ", launch_v<256, 2, 64, 2, 0, 3, false, 2, EPI_NONE>});
+    vs.push_back({"w4 regs      ", launch_w4<EPI_NONE, 0>});
+    vs.push_back({"w4 W-dma     ", launch_w4<EPI_NONE, 1>});
+    vs.push_back({"w4 all-dma   ", launch_w4<EPI_NONE, 2>});
     vs.push_back({"stream-K     ", launch_sk<EPI_NONE>});
   }
   {  // every variant must produce the first variant's output (same tile math; k order identical)
