@@ -68,6 +68,40 @@ def test_gemm_skinny(gpu, M, N, Kd):
   assert rel_err(yf, R.linear(x, w)) < 1e-3
 
 
+@pytest.mark.parametrize("H,T", [(16, 1), (16, 37), (16, 256), (128, 200)])
+def test_gemm_batched_mla(gpu, H, T):
+  """The MLA absorbed projections on gemm_batched (per-head pre-shuffled weights) vs fp32 bmm, reading the
+  query heads in place from a strided [T, H dn | H dr] row and writing o as [T, H dv]; plus the stream_t
+  layout round trip (prepare_for_decode -> _rowmajor, assign_weight)."""
+  from xotorch_support_jetson_amd.ops._ext import require
+  from xotorch_support_jetson_amd.models.weights import _rowmajor, assign_weight
+  from xotorch_support_jetson_amd.ops.weights_layout import shuffle_for_stream
+  torch.manual_seed(0)
+  dn, dr, dv, L = 128, 64, 128, 512
+  q = torch.randn(T, H * (dn + dr), device=gpu, dtype=torch.bfloat16)
+  wuk = torch.randn(H, dn, L, device=gpu, dtype=torch.bfloat16) / math.sqrt(dn)
+  wuv = torch.randn(H, dv, L, device=gpu, dtype=torch.bfloat16) / math.sqrt(L)
+  wuk_s = torch.stack([shuffle_for_stream(wuk[h].t().contiguous()) for h in range(H)])
+  wuv_s = torch.stack([shuffle_for_stream(wuv[h]) for h in range(H)])
+  C = require()
+  q_lat = torch.empty(H, T, L, device=gpu, dtype=torch.bfloat16)
+  C.gemm_batched(q[:, :H * dn], dn, dn, wuk_s, q_lat, T * L, L, T)
+  ref = torch.bmm(q[:, :H * dn].view(T, H, dn).transpose(0, 1).float(), wuk.float())
+  assert rel_err(q_lat, ref) < 1e-2
+  o_lat = torch.randn(H, T, L, device=gpu, dtype=torch.bfloat16)
+  o = torch.empty(T, H * dv, device=gpu, dtype=torch.bfloat16)
+  C.gemm_batched(o_lat.view(H * T, L), T * L, L, wuv_s, o, dv, H * dv, T)
+  ref_o = torch.bmm(o_lat.float(), wuv.float().transpose(1, 2)).transpose(0, 1).reshape(T, H * dv)
+  assert rel_err(o, ref_o) < 1e-2
+  of = torch.empty(T, H * dv, device=gpu, dtype=torch.float32)
+  C.gemm_batched(o_lat.view(H * T, L), T * L, L, wuv_s, of, dv, H * dv, T)
+  assert rel_err(of, ref_o) < 1e-3
+  wuk_s.xot_layout = "stream_t"
+  assert torch.equal(_rowmajor(wuk_s), wuk)
+  assign_weight(wuk_s, wuk * 2)
+  assert torch.equal(_rowmajor(wuk_s), wuk * 2)
+
+
 def test_gemm_epilogues(gpu):
   torch.manual_seed(0)
   M, Kd, Fd = 24, 1024, 512
@@ -484,6 +518,34 @@ def test_gemm_big(gpu, M, epi, bn, splits):
   assert rel_err(y, ref) < 1e-2
 
 
+@pytest.mark.parametrize("N", [3648, 1088, 320])
+@pytest.mark.parametrize("epi,bn,splits", [("none", 256, 1), ("none", 128, 1), ("none", 1256, 1), ("resid", 256, 1),
+                                           ("silu", 128, 1), ("none", 256, 3), ("resid", 1256, 2)])
+def test_gemm_big_column_tail(gpu, N, epi, bn, splits):
+  """N not a multiple of the column tile (DeepSeek-V2-Lite's fused A projection is 3648 wide): the last
+  column tile re-reads the last weight row group and masks its stores -- columns past N stay untouched."""
+  from xotorch_support_jetson_amd.ops._ext import require
+  from xotorch_support_jetson_amd.ops.weights_layout import shuffle_for_stream
+  torch.manual_seed(N + bn)
+  M, Kd = 300, 1024
+  x = torch.randn(M, Kd, device=gpu, dtype=torch.bfloat16)
+  w = torch.randn(N, Kd, device=gpu, dtype=torch.bfloat16) / math.sqrt(Kd)
+  r = torch.randn(M, N, device=gpu, dtype=torch.bfloat16)
+  ws = torch.empty(splits * M * N, device=gpu, dtype=torch.float32)
+  full = R.linear(x, w)
+  Ny = N // 2 if epi == "silu" else N
+  if epi == "silu":
+    f = full.view(M, N // 32, 2, 16)
+    ref = (torch.nn.functional.silu(f[:, :, 0]) * f[:, :, 1]).reshape(M, Ny)
+  else:
+    ref = full + r.float() if epi == "resid" else full
+  buf = torch.full((M, Ny + 64), 7.0, device=gpu, dtype=torch.bfloat16)
+  y = buf[:, :Ny]
+  require().gemm_big(x, shuffle_for_stream(w), y, None, r if epi == "resid" else None, ws, K.EPI[epi], bn, splits)
+  assert rel_err(y, ref) < 1e-2
+  assert bool((buf[:, Ny:] == 7.0).all())
+
+
 def test_gemm_big_exact_layout(gpu):
   """Integer-valued operands (exact in bf16 and fp32): every output element must match bit for bit,
   which pins the fragment maps, the LDS swizzle and the shuffled-layout k order."""
@@ -591,7 +653,9 @@ def test_attention_train_fwd_bwd(gpu, B, L, H, Hkv, Dh):
     assert rel_err(g[:, sl], x.grad[:, sl]) < 3e-2, name
 
 
-@pytest.mark.parametrize("T,E,D", [(1, 8, 4096), (37, 8, 4096), (512, 8, 1024), (5, 4, 256), (9, 16, 512)])
+@pytest.mark.parametrize("T,E,D", [(1, 8, 4096), (37, 8, 4096), (512, 8, 1024), (5, 4, 256), (9, 16, 512),
+                                   (1, 64, 2048), (37, 64, 2048), (4099, 64, 2048), (300, 160, 5120), (17, 256, 7168),
+                                   (3, 32, 512), (40, 128, 4096), (16, 160, 5120)])
 def test_router_logits(gpu, T, E, D):
   from xotorch_support_jetson_amd.ops._ext import require
   torch.manual_seed(0)

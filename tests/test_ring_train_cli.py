@@ -102,3 +102,30 @@ def test_xot_run_gpus_defaults_to_rccl_ring(tmp_path):
   assert "[ring 1/2]" in two and "layers 2-3" in two
   ans = lambda out: [l for l in out.splitlines() if l.strip() and not l.startswith("[")][-1]
   assert ans(two) == ans(one)
+
+
+def test_ring_train_recovers_from_a_dead_stage(tmp_path):
+  """3 pipeline stages; stage 1 dies in epoch 2 (XOT_FAULT=kill after 16 p2p sends: 12 per epoch).  The
+  survivors detect it by heartbeat, re-form a 2-rank ring, re-partition the 4 layers over it, reload the
+  epoch-1 checkpoint in process and finish the run: epochs 2 and 3 on 2 ranks, a 2-stage final checkpoint."""
+  ds = tmp_path / "ds"
+  ds.mkdir()
+  for split, n in (("train", 12), ("valid", 4), ("test", 4)):
+    with open(ds / f"{split}.jsonl", "w") as f:
+      for i in range(n):
+        f.write(json.dumps({"text": f"Q: select a from t{i}? A: SELECT a FROM t{i}"}) + "\n")
+  ck = tmp_path / "ck"
+  env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2", XOT_HOME=str(tmp_path / "home"), CUDA_VISIBLE_DEVICES="",
+             HIP_VISIBLE_DEVICES="", XOT_FAULT="kill:rank=1:after=16", XOT_HEARTBEAT_TIMEOUT="3")
+  r = subprocess.run([sys.executable, "-m", "xotorch_support_jetson_amd.main", "train", "tiny-llama", "--ring", "--gpus",
+                      "3", "--iters", "3", "--batch-size", "4", "--micro-batch", "2", "--save-every", "1",
+                      "--save-checkpoint-dir", str(ck), "--data", str(ds), "--lr", "1e-3", "--disable-tui"],
+                     capture_output=True, text=True, timeout=300, env=env, cwd=str(tmp_path))
+  out = r.stdout
+  assert r.returncode == 0, r.stderr[-3000:] + out[-2000:]
+  assert "re-forming the training ring over [0, 2]" in out and "restarting at epoch 2 on 2 rank(s)" in out
+  assert "training rank 1 exited with code 17" in out
+  epochs = [l.split("|")[0].strip() for l in out.splitlines() if l.startswith("epoch")]
+  assert epochs == ["epoch 1/3", "epoch 2/3", "epoch 3/3"]
+  names = sorted(p.name for p in (ck / "tiny-llama").iterdir() if p.name.endswith("000003.safetensors"))
+  assert names == ["000-001-of-004-000003.safetensors", "002-003-of-004-000003.safetensors"]

@@ -306,3 +306,41 @@ def test_graph_table_width_classes(gpu):
       x, y = g.forward(rids, [1] * len(rids), tok), e.forward(rids, [1] * len(rids), tok)
       assert torch.allclose(x, y, atol=3e-2, rtol=3e-2), (step, rids, (x - y).abs().max().item())
   assert {w for _, w in g._graphs} == {8, 32, 64}
+
+
+@pytest.mark.parametrize("name", ["tiny-deepseek-v2", "tiny-llama-d64"])
+def test_padded_ffn_and_mla_batched_match_cpu(gpu, name):
+  """A dense intermediate size that is not a multiple of 128 (DeepSeek-V2-Lite's first layer: 10944) is
+  zero-padded to whole 128-deep tiles (models/weights.py:pad_ffn_for_tiles) and the MLA absorbed projections
+  run on gemm_batched: GPU logits match the CPU fp32 path on the same weights, and the row-major views
+  (training / export) come back unpadded and exact."""
+  import dataclasses
+  from xotorch_support_jetson_amd.models.weights import _rowmajor
+  c = dataclasses.replace(preset(name), intermediate_size=320)
+  L = c.num_layers
+  sh = Shard(name, 0, L - 1, L)
+  w_cpu = random_weights(c, sh, "cpu")
+  w_gpu = random_weights(c, sh, "cpu")
+  for lw in w_gpu.layers.values():
+    for k, v in lw.tensors().items():
+      setattr(lw, k, v.to(gpu))
+  w_gpu.embed, w_gpu.norm = w_gpu.embed.to(gpu), w_gpu.norm.to(gpu)
+  w_gpu.lm_head = w_gpu.embed if w_cpu.lm_head is w_cpu.embed else w_gpu.lm_head.to(gpu)
+  cpu = ShardRunner(c, sh, "cpu", weights=w_cpu, max_batch=4, max_ctx=256)
+  gr = ShardRunner(c, sh, gpu, weights=w_gpu, max_batch=4, max_ctx=256)
+  lw0 = gr.weights.layers[0]
+  assert lw0.down_w.shape[-1] == 384 and getattr(lw0.down_w, "xot_logical", None) == (c.hidden_size, 320)
+  assert torch.equal(_rowmajor(lw0.down_w).cpu(), w_cpu.layers[0].down_w)
+  assert torch.equal(_rowmajor(lw0.gu_w).cpu(), w_cpu.layers[0].gu_w)
+  if c.is_mla:
+    assert getattr(lw0.wuk, "xot_layout", "") == "stream_t"
+    assert torch.equal(_rowmajor(lw0.wuk).cpu(), w_cpu.layers[0].wuk)
+  ids = torch.randint(0, c.vocab_size, (40,), dtype=torch.int32)
+  lc = cpu.forward(["a", "b"], [25, 15], ids)
+  lg = gr.forward(["a", "b"], [25, 15], ids).cpu()
+  assert ((lc - lg).norm() / lc.norm()).item() < 3e-2
+  tok = lc.argmax(-1).int()
+  for _ in range(3):
+    lc = cpu.forward(["a", "b"], [1, 1], tok)
+    lg = gr.forward(["a", "b"], [1, 1], tok).cpu()
+    assert ((lc - lg).norm() / lc.norm()).item() < 3e-2

@@ -406,6 +406,29 @@ void gemm_sk(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const c10:
 }
 
 int64_t gemm_sk_part_elems() { return xot::gemm_sk_part_elems(); }
+
+// B independent projections (MLA's per-head absorbed q . W_UK and o . W_UV^T): y_e = x_e . w_e^T with
+// x_e = x.data + e * xbat (rows x.stride(0) apart, K columns), w = [B, N, K] pre-shuffled per problem,
+// y_e = y.data + e * ybat (rows ldy apart, N columns).
+void gemm_batched(const at::Tensor& x, int64_t xbat, int64_t K, const at::Tensor& w, at::Tensor& y, int64_t ybat,
+                  int64_t ldy, int64_t M) {
+  CHECK_BF16(x);
+  CHECK_BF16(w);
+  CHECK_GPU(y);
+  XCHECK(w.dim() == 3 && w.is_contiguous() && w.size(2) == K, "gemm_batched: w must be [B, N, K] contiguous");
+  const int64_t B = w.size(0), N = w.size(1);
+  XCHECK(x.stride(-1) == 1 && x.stride(0) % 8 == 0 && xbat % 8 == 0, "gemm_batched: x rows must be 16-B aligned");
+  // the last element read, (B-1) xbat + (M-1) ldx + K - 1, must lie inside x's extent
+  XCHECK(x.dim() == 2 && x.size(0) >= M && M >= 1 &&
+             (B - 1) * xbat + (M - 1) * x.stride(0) + K <= (x.size(0) - 1) * x.stride(0) + x.size(1),
+         "gemm_batched: x too small");
+  const bool f32 = y.scalar_type() == at::kFloat;
+  XCHECK(f32 || y.scalar_type() == at::kBFloat16, "gemm_batched: y must be bf16 or fp32");
+  XCHECK(y.is_contiguous() && (B - 1) * ybat + (M - 1) * ldy + N <= y.numel(), "gemm_batched: y too small");
+  const int rc = xot::launch_gemm_batched(bf(x), (int)x.stride(0), (long)xbat, bf(w), y.data_ptr(), (int)ldy, (long)ybat,
+                                          f32, (int)B, (int)M, (int)N, (int)K, cur_stream());
+  XCHECK(rc == 0, "gemm_batched: unsupported shape B=", B, " M=", M, " N=", N, " K=", K);
+}
 int64_t gemm_sk_sync_words(int64_t M, int64_t N) { return xot::gemm_sk_sync_words((int)M, (int)N); }
 
 // h [rows, D] += bias + sum_s ws[s] (the split-K slabs of a residual projection, fp32 [S][rows][D]);
@@ -859,6 +882,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_sk", &gemm_sk, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("bias"), py::arg("res"), py::arg("part"),
         py::arg("sync"), py::arg("epi"), py::arg("cus") = 256);
   m.def("gemm_sk_part_elems", &gemm_sk_part_elems);
+  m.def("gemm_batched", &gemm_batched, py::arg("x"), py::arg("xbat"), py::arg("K"), py::arg("w"), py::arg("y"),
+        py::arg("ybat"), py::arg("ldy"), py::arg("M"));
   m.def("gemm_sk_sync_words", &gemm_sk_sync_words);
   m.def("gemm_big", &gemm_big, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("bias"), py::arg("res"),
         py::arg("ws"), py::arg("epi"), py::arg("bn"), py::arg("splits"), py::arg("reduce") = true);

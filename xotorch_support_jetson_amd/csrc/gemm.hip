@@ -191,6 +191,8 @@ int launch_gemm_skinny(const uint16_t* X, int ldx, const uint16_t* W, int ldw, c
 // so each lane reads 16*KS contiguous bytes of its weight row per chunk.
 // SPLIT: fp32 partial slabs ws[blockIdx.y][M][N], finished by splitk_reduce_kernel or -- with tickets -- by the
 // last-arriving workgroup of each tile inside the same launch (epilogue there).
+// MOE = 3: batched GEMM (per-head projections of MLA): blockIdx.z = problem e, weight W[e], A rows X + e*xbat,
+// output Y + e*ybat (element offsets; row strides ldx / ldy shared), all M rows.
 // MOE = 1 / 2: grouped (mixture-of-experts) GEMM.  blockIdx.z = expert e with weight W[e]
 // ([E][N][K], same layout per expert) and rows moe_off[e] .. moe_off[e+1] of the expert-sorted slot
 // order; MOE = 1 reads A in slot order, MOE = 2 gathers A row moe_gather[slot] (token rows).  Output
@@ -211,7 +213,8 @@ __global__ __launch_bounds__(256, OCC) void gemm_stream_kernel(const uint16_t* _
                                                              int mblocks, const int* __restrict__ moe_off,
                                                              const int* __restrict__ moe_gather,
                                                              int* __restrict__ tickets, long ysplit,
-                                                             const float* __restrict__ wscale) {
+                                                             const float* __restrict__ wscale, long xbat,
+                                                             long ybat) {
   constexpr int KC = 32 * KS;
   static_assert(!W8 || (WSHUF && (KS == 4 || KS == 8) && MOE == 0),
                 "FP8 weights: pre-shuffled 128- or 256-deep chunks, dense GEMM");
@@ -243,7 +246,16 @@ __global__ __launch_bounds__(256, OCC) void gemm_stream_kernel(const uint16_t* _
     }
   }
   int row0 = 0;  // first output row of this launch's row range
-  if constexpr (MOE != 0) {
+  if constexpr (MOE == 3) {  // batched: problem e = blockIdx.z has W[e], X + e * xbat, Y + e * ybat
+    const int e = blockIdx.z;
+    W += (size_t)e * N * ldw;
+    X += (size_t)e * xbat;
+    if constexpr (OUT_F32)
+      Yv = reinterpret_cast<float*>(Yv) + (size_t)e * ybat;
+    else
+      Yv = reinterpret_cast<uint16_t*>(Yv) + (size_t)e * ybat;
+  }
+  if constexpr (MOE == 1 || MOE == 2) {
     const int e = blockIdx.z;
     row0 = moe_off[e];
     M = moe_off[e + 1] - row0;  // this expert's rows
@@ -252,7 +264,7 @@ __global__ __launch_bounds__(256, OCC) void gemm_stream_kernel(const uint16_t* _
   }
   // grouped GEMM split over K: K slice blockIdx.y writes its own fp32 slab of Y (ysplit elements apart),
   // summed by the consumer (moe_combine_kernel)
-  if constexpr (MOE != 0) {
+  if constexpr (MOE == 1 || MOE == 2) {
     if (ysplit != 0) Yv = reinterpret_cast<float*>(Yv) + (size_t)blockIdx.y * ysplit;
   }
   const int Mtot = M, m_base = mb * ROWS;
@@ -528,7 +540,7 @@ static void stream_launch(const uint16_t* X, int ldx, const uint16_t* W, int ldw
       (void)attr;
     }
     kern<<<grid, 256, SMEM, st>>>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, nullptr, M, N, kper, mblocks, nullptr, nullptr,
-                                  nullptr, 0L, wscale);
+                                  nullptr, 0L, wscale, 0L, 0L);
   } else {
     auto kern = gemm_stream_kernel<MT, NTW, KS, EPI, F32, true, WSH, OCC, 0, W8>;
     if constexpr (SMEM > 65536) {
@@ -537,7 +549,7 @@ static void stream_launch(const uint16_t* X, int ldx, const uint16_t* W, int ldw
       (void)attr;
     }
     kern<<<grid, 256, SMEM, st>>>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, M, N, kper, mblocks, nullptr, nullptr,
-                                  tickets, 0L, wscale);
+                                  tickets, 0L, wscale, 0L, 0L);
     if (tickets != nullptr || !reduce) return;  // combined in-launch / slabs left for the consumer
     const int ncol = EPI == EPI_SILU ? N / 2 : N;
     long chunks = (long)M * (ncol / 8);
@@ -592,6 +604,42 @@ static int stream_dispatch(const uint16_t* X, int ldx, const uint16_t* W, int ld
   return -1;
 }
 
+// ------------------------------------------------------------------------------------ batched (MLA heads)
+template <int MT, bool F32>
+static void batched_launch(const uint16_t* X, int ldx, long xbat, const uint16_t* W, void* Y, int ldy, long ybat,
+                           int B, int M, int N, int K, hipStream_t st) {
+  constexpr int NTW = 2, KS = 4;
+  constexpr int OCC = (MT * NTW >= 32) ? 1 : 2;
+  constexpr int SMEM = 2 * 16 * MT * 32 * KS * 2;
+  const int mblocks = (M + 16 * MT - 1) / (16 * MT);
+  dim3 grid(N / (64 * NTW) * mblocks, 1, B);
+  gemm_stream_kernel<MT, NTW, KS, EPI_NONE, F32, false, true, OCC, 3><<<grid, 256, SMEM, st>>>(
+      X, ldx, W, K, nullptr, nullptr, 0, Y, ldy, nullptr, M, N, K, mblocks, nullptr, nullptr, nullptr, 0L, nullptr,
+      xbat, ybat);
+}
+
+// B independent GEMMs Y_e[M, N] = X_e[M, K] . W_e[N, K]^T on pre-shuffled weights W [B][N][K]
+int launch_gemm_batched(const uint16_t* X, int ldx, long xbat, const uint16_t* W, void* Y, int ldy, long ybat,
+                        bool out_f32, int B, int M, int N, int K, hipStream_t s) {
+  if (M <= 0 || B <= 0) return 0;
+  if (N % 128 != 0 || K % 128 != 0) return -1;
+  const int mt = (M + 15) / 16;
+#define XOT_BAT(MTV)                                                                                   \
+  do {                                                                                                 \
+    if (out_f32) batched_launch<MTV, true>(X, ldx, xbat, W, Y, ldy, ybat, B, M, N, K, s);              \
+    else batched_launch<MTV, false>(X, ldx, xbat, W, Y, ldy, ybat, B, M, N, K, s);                     \
+    return 0;                                                                                          \
+  } while (0)
+  // the widest row tile that still gives the 256 CUs a workgroup each (decode: M ~ 256 rows, B heads)
+  auto wgs = [&](int m) { return (long)(N / 128) * ((M + 16 * m - 1) / (16 * m)) * B; };
+  if (mt <= 1) XOT_BAT(1);
+  if (mt <= 4) XOT_BAT(4);
+  if (wgs(8) >= 256) XOT_BAT(8);
+  if (wgs(4) >= 256) XOT_BAT(4);
+  XOT_BAT(1);
+#undef XOT_BAT
+}
+
 // ------------------------------------------------------------------------------------ grouped (MoE)
 template <int MT, int EPI, bool F32, bool WSH, int MOE>
 static void moe_launch(const uint16_t* X, int ldx, const uint16_t* W, void* Y, int ldy, const int* off,
@@ -603,7 +651,7 @@ static void moe_launch(const uint16_t* X, int ldx, const uint16_t* W, void* Y, i
   dim3 grid(N / (64 * NTW) * mblocks, S, E);
   gemm_stream_kernel<MT, NTW, KS, EPI, F32, false, WSH, OCC, MOE><<<grid, 256, SMEM, st>>>(
       X, ldx, W, K, nullptr, nullptr, 0, Y, ldy, nullptr, max_rows, N, K / S, mblocks, off, gather, nullptr,
-      S > 1 ? ysplit : 0L, nullptr);
+      S > 1 ? ysplit : 0L, nullptr, 0L, 0L);
 }
 
 template <int EPI, bool F32, bool WSH, int MOE>

@@ -72,7 +72,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
   const int wm = wave / WN, wn = wave % WN;
 
   // ---- tile of this workgroup (bijective XCD remap, then split-major / column / row order)
-  const int mtiles = (M + BM - 1) / BM, ntiles = N / BN;
+  const int mtiles = (M + BM - 1) / BM, ntiles = (N + BN - 1) / BN;  // N % BN != 0: a masked last column tile
   const int nwg = mtiles * ntiles * S;
   int b = blockIdx.x;
   {
@@ -124,7 +124,8 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
 #pragma unroll
   for (int i = 0; i < B_INSTR; ++i) {
     const int q = B_INSTR * wave + i;
-    bsrc[i] = W + ((size_t)((n0 >> 4) + q / KS) * kchunks) * 2048 + (q % KS) * 512 + lane * 8;
+    const int grp = min((n0 >> 4) + q / KS, N / 16 - 1);  // groups past N re-read the last one; outputs masked
+    bsrc[i] = W + ((size_t)grp * kchunks) * 2048 + (q % KS) * 512 + lane * 8;
   }
 
   auto issue = [&](int t, int buf) {  // stage t (absolute k step) -> LDS buffer buf
@@ -234,7 +235,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int grp = 4 * (wave >> 1) + (wave & 1) + 2 * h;  // 16-column group of this wave in half h
-      b_src[h] = W + ((size_t)((n0 >> 4) + grp) * kchunks) * 2048 + lane * 8;
+      b_src[h] = W + ((size_t)min((n0 >> 4) + grp, N / 16 - 1) * kchunks) * 2048 + lane * 8;
       b_dst[h] = A_ELEMS + grp * KS * 512;
     }
     auto issue_a = [&](int t, int h) {
@@ -442,12 +443,14 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
         const int m = rbase + 16 * i + 4 * g + r;
         if (m < Mv) {
 #pragma unroll
-          for (int j = 0; j < NT; ++j) slab[(size_t)m * N + cbase + 16 * j + c] = acc[i][j][r];
+          for (int j = 0; j < NT; ++j)
+            if (cbase + 16 * j < N) slab[(size_t)m * N + cbase + 16 * j + c] = acc[i][j][r];
         }
       }
   } else if constexpr (EPI == EPI_SILU) {
 #pragma unroll
     for (int p = 0; p < NT / 2; ++p) {  // (gate tile 2p, up tile 2p+1) -> 16 output columns
+      if (cbase + 32 * p >= N) break;
       const int col = (cbase >> 1) + 16 * p + c;
       float bg = 0.f, bu = 0.f;
       if (bias != nullptr) {
@@ -471,6 +474,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
   } else {
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
+      if (cbase + 16 * j >= N) break;
       const int col = cbase + 16 * j + c;
       const float bv = bias != nullptr ? bf2f(bias[col]) : 0.f;
 #pragma unroll
@@ -497,7 +501,7 @@ static void big_launch(const uint16_t* X, int ldx, const uint16_t* W, const uint
                        hipStream_t st) {
   constexpr int SMEM = NBUF * (BM + BN) * BK * 2;
   static_assert(SMEM <= 160 * 1024, "LDS");
-  const int nwg = ((M + BM - 1) / BM) * (N / BN) * S;
+  const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN) * S;
   if (S == 1) {
     auto kern = gemm_big_kernel<BM, BN, WM, WN, BK, NBUF, EPI, F32, false, 0, 0, 0, 3, false, PP>;
     static bool attr = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM) ==
@@ -540,8 +544,7 @@ int launch_gemm_big(const uint16_t* X, int ldx, const uint16_t* W, const uint16_
                     void* Y, int ldy, bool out_f32, int epi, float* ws, long ws_elems, int M, int N, int K, int bn,
                     int S, bool reduce, hipStream_t s) {
   if (M <= 0) return 0;
-  const int tile_n = bn % 1000;
-  if ((bn != 128 && bn != 256 && bn != 1256 && bn != 2256) || N % tile_n != 0 || K % 128 != 0 || S < 1 || S > K / 64) return -1;
+  if ((bn != 128 && bn != 256 && bn != 1256 && bn != 2256) || N % 16 != 0 || K % 128 != 0 || S < 1 || S > K / 64) return -1;
   if (S > 1 && (ws == nullptr || ws_elems < (long)S * M * N)) return -1;
   if (epi == EPI_SILU && N % 32 != 0) return -1;
   if (epi == EPI_SILU)

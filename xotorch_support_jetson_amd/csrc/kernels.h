@@ -49,6 +49,9 @@ int launch_gemm_sk(const uint16_t* X, int ldx, const uint16_t* W, const uint16_t
                    void* Y, int ldy, bool out_f32, int epi, float* part, int* sync, int M, int N, int K, int cus,
                    hipStream_t s);
 long gemm_sk_part_elems();
+// B independent GEMMs Y_e = X_e . W_e^T (pre-shuffled W [B][N][K]; X_e = X + e*xbat, Y_e = Y + e*ybat)
+int launch_gemm_batched(const uint16_t* X, int ldx, long xbat, const uint16_t* W, void* Y, int ldy, long ybat,
+                        bool out_f32, int B, int M, int N, int K, hipStream_t s);
 long gemm_sk_sync_words(int M, int N);
 // h += bias + sum of S fp32 split-K slabs [S][rows][D] (in place, bf16), out = rmsnorm(h) * w
 void launch_splitk_resid_rmsnorm(const float* ws, int S, const uint16_t* bias, uint16_t* h, const uint16_t* w,

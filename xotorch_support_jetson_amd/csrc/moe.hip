@@ -401,9 +401,82 @@ __global__ __launch_bounds__(256) void router_logits_kernel(const uint16_t* __re
   if (tid < E) out[(size_t)t * E + tid] = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
 }
 
+// The same logits on MFMA for the wide routers (DeepSeek: 64 / 160 / 256 experts).  A workgroup takes 16
+// tokens x all E = 16 ET experts; its NW waves split K into contiguous slices (decode has only T / 16
+// workgroups, so the split is what keeps each wave's dependent chain to a few k iterations).  Per 32-deep
+// k step a lane loads its token row's 8 k values (A fragment: row lane & 15, k 8 (lane >> 4)) and each
+// expert tile's row (B fragment, same map) from global / L2, U steps at a time with every load issued before
+// the MFMAs; the NW partial 16 x E tiles are summed in LDS in wave order (deterministic).  Rows past T
+// re-read row T - 1 and are not stored.  Requires D % (128 NW) == 0.
+template <int ET, int NW>
+__global__ __launch_bounds__(NW * 64) void router_logits_mfma_kernel(const uint16_t* __restrict__ x,
+                                                                     const uint16_t* __restrict__ w,
+                                                                     float* __restrict__ out, int T, int D) {
+  constexpr int E = 16 * ET;
+  constexpr int U = ET <= 4 ? 4 : (ET <= 8 ? 2 : 1);  // k steps in flight per iteration (register budget)
+  extern __shared__ float red[];                      // [NW][16][E] partial logits
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, c = lane & 15;
+  const int t0 = blockIdx.x * 16;
+  const int kq = D / NW, kb = wave * kq;
+  const uint16_t* xr = x + (size_t)min(t0 + c, T - 1) * D + kb + 8 * g;
+  const uint16_t* wr = w + (size_t)c * D + kb + 8 * g;  // + 16 j D for tile j
+  f32x4 acc[ET];
+#pragma unroll
+  for (int j = 0; j < ET; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int k0 = 0; k0 < kq; k0 += 32 * U) {
+    s16x8 a[U], b[U][ET];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      a[u] = ld16(xr + k0 + 32 * u);
+#pragma unroll
+      for (int j = 0; j < ET; ++j) b[u][j] = ld16(wr + (size_t)16 * j * D + k0 + 32 * u);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int j = 0; j < ET; ++j) acc[j] = mfma16(a[u], b[u][j], acc[j]);
+  }
+#pragma unroll
+  for (int j = 0; j < ET; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[(wave * 16 + 4 * g + r) * E + 16 * j + c] = acc[j][r];
+  __syncthreads();
+  for (int i = threadIdx.x; i < 16 * E; i += NW * 64) {
+    float v = 0.f;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) v += red[q * 16 * E + i];
+    const int t = t0 + i / E;
+    if (t < T) out[(size_t)t * E + i % E] = v;
+  }
+}
+
+template <int ET, int NW>
+static void router_mfma_launch(const uint16_t* x, const uint16_t* w, float* out, int T, int D, hipStream_t s) {
+  router_logits_mfma_kernel<ET, NW><<<(T + 15) / 16, NW * 64, NW * 16 * 16 * ET * 4, s>>>(x, w, out, T, D);
+}
+
 int launch_router_logits(const uint16_t* x, const uint16_t* w, float* out, int T, int E, int D, hipStream_t s) {
   if (T <= 0) return 0;
   if (D % 8 != 0) return -1;
+  if (E >= 32 && D % 512 == 0) {
+    const bool w8 = E <= 128 && D % 1024 == 0;  // 8 waves (LDS 8 x 16 x E x 4 B <= 64 KB) when K allows
+#define XOT_RL(ETV)                                                        \
+  do {                                                                     \
+    if (w8) router_mfma_launch<ETV, 8>(x, w, out, T, D, s);               \
+    else router_mfma_launch<ETV, 4>(x, w, out, T, D, s);                   \
+    return 0;                                                              \
+  } while (0)
+    switch (E) {
+      case 32: XOT_RL(2);
+      case 64: XOT_RL(4);
+      case 128: XOT_RL(8);
+      case 160: XOT_RL(10);
+      case 256: XOT_RL(16);
+      default: break;
+    }
+#undef XOT_RL
+  }
   switch (E) {
     case 8: router_logits_kernel<8><<<T, 256, 0, s>>>(x, w, out, D); return 0;
     case 16: router_logits_kernel<16><<<T, 256, 0, s>>>(x, w, out, D); return 0;

@@ -144,13 +144,23 @@ class ShardModel:
     ckv = A[:, nq:]
     cache = self.kv.k[li]
     K.mla_prep(ckv, lw.kv_ln, q, H * dn, H, inp.positions, self.cos_sin, inp.slots, cache, c.rms_norm_eps)
-    q_nope = q[:, :H * dn].view(T, H, dn).transpose(0, 1)  # [H, T, dn]
     dt = q.dtype
+    q_pe = q[:, H * dn:]
+    if getattr(lw.wuk, "xot_layout", "rowmajor") == "stream_t":
+      # absorbed projections on the batched stream GEMM (pre-shuffled per head, csrc/gemm.hip MOE==3 mode):
+      # head h reads q[:, h dn:(h+1) dn] in place and writes q_lat[h]; o_lat[h] . W_UV[h]^T lands in o[:, h dv:]
+      KC = require()
+      q_lat = torch.empty(H, T, L, device=q.device, dtype=dt)
+      KC.gemm_batched(q[:, :H * dn], dn, dn, lw.wuk, q_lat, T * L, L, T)
+      o_lat = K.mla_attn(q_lat, q_pe, cache, inp.block_tables, inp.cu_q, inp.ctx_lens, self.scale, self.ws)
+      o = torch.empty(T, H * dv, device=q.device, dtype=dt)
+      KC.gemm_batched(o_lat.view(H * T, L), T * L, L, lw.wuv, o, dv, H * dv, T)
+      return o
+    q_nope = q[:, :H * dn].view(T, H, dn).transpose(0, 1)  # [H, T, dn]
     if xn.is_cuda:
-      q_lat = torch.bmm(q_nope, lw.wuk)  # [H, T, L] (hipBLASLt batched GEMM)
+      q_lat = torch.bmm(q_nope, lw.wuk)  # [H, T, L] (row-major weights: shapes gemm_batched does not tile)
     else:  # CPU reference path: fp32 math whatever the shard's storage dtypes
       q_lat = torch.bmm(q_nope.float(), lw.wuk.float()).to(dt)
-    q_pe = q[:, H * dn:]
     o_lat = K.mla_attn(q_lat, q_pe, cache, inp.block_tables, inp.cu_q, inp.ctx_lens, self.scale, self.ws)
     if xn.is_cuda:
       o = torch.bmm(o_lat, lw.wuv.transpose(1, 2))  # [H, T, dv]
@@ -192,7 +202,8 @@ class ShardModel:
     c = self.c
     if lw.sh_gu_w is not None:  # shared experts: h += down(silu(gate) * up) of every token
       linear(linear(xn, lw.sh_gu_w, epi="silu"), lw.sh_down_w, residual=h, epi="resid", out=h)
-    if xn.is_cuda and c.num_experts in (4, 8, 16) and layout_of(lw.router) == "rowmajor":
+    if xn.is_cuda and (c.num_experts in (4, 8, 16) or (c.num_experts in (32, 64, 128, 160, 256)
+                                                       and c.hidden_size % 512 == 0)) and layout_of(lw.router) == "rowmajor":
       # fp32 router logits, one small kernel (instead of a bf16 library GEMM + cast)
       logits = torch.empty(xn.shape[0], c.num_experts, dtype=torch.float32, device=xn.device)
       require().router_logits(xn.contiguous(), lw.router.contiguous(), logits)

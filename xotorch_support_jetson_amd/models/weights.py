@@ -205,7 +205,7 @@ def _mla_to_hf(c: ModelConfig, lw: "LayerWeights", p: str, sd: Dict[str, torch.T
   else:
     sd[a + "q_proj.weight"] = q_a.index_select(0, qo.to(q_a.device))
   sd[a + "kv_a_layernorm.weight"] = lw.kv_ln
-  sd[a + "kv_b_proj.weight"] = torch.cat([lw.wuk, lw.wuv], 1).reshape(-1, c.kv_lora_rank)
+  sd[a + "kv_b_proj.weight"] = torch.cat([_rowmajor(lw.wuk), _rowmajor(lw.wuv)], 1).reshape(-1, c.kv_lora_rank)
   sd[a + "o_proj.weight"] = _rowmajor(lw.o_w)
   sd[p + "input_layernorm.weight"] = lw.ln1
   sd[p + "post_attention_layernorm.weight"] = lw.ln2
@@ -229,10 +229,22 @@ def _mla_to_hf(c: ModelConfig, lw: "LayerWeights", p: str, sd: Dict[str, torch.T
 
 
 def _rowmajor(t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
-  """Row-major view of a possibly pre-shuffled device weight (2-D, or 3-D expert stacks)."""
+  """Row-major view of a possibly pre-shuffled device weight (2-D, or 3-D expert stacks), without the zero
+  padding a tiled layout may carry (`xot_logical`: see pad_ffn_for_tiles)."""
+  logical = getattr(t, "xot_logical", None)
+  if logical is not None:
+    full = _rowmajor_full(t)
+    return full[:logical[0], :logical[1]].contiguous()
+  return _rowmajor_full(t)
+
+
+def _rowmajor_full(t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
   if t is not None and getattr(t, "xot_layout", "rowmajor") == "stream8":
     from ..ops.weights_layout import dequant_stream8
     return dequant_stream8(t, t.xot_scale)
+  if t is not None and getattr(t, "xot_layout", "rowmajor") == "stream_t":  # per-head shuffled W^T (MLA W_UK)
+    from ..ops.weights_layout import unshuffle_from_stream
+    return torch.stack([unshuffle_from_stream(t[h]).t() for h in range(t.shape[0])])
   if t is None or getattr(t, "xot_layout", "rowmajor") != "stream":
     return t
   from ..ops.weights_layout import unshuffle_from_stream
@@ -247,6 +259,31 @@ def expert(t: torch.Tensor, e: int) -> torch.Tensor:
   if hasattr(t, "xot_layout"):
     v.xot_layout = t.xot_layout
   return v
+
+
+def _pad_to(t: torch.Tensor, shape) -> torch.Tensor:
+  """Zero-pad the trailing rows / columns of a 2-D tensor up to `shape`."""
+  return torch.nn.functional.pad(t, (0, shape[1] - t.shape[1], 0, shape[0] - t.shape[0]))
+
+
+def pad_ffn_for_tiles(lw: "LayerWeights") -> None:
+  """A dense SwiGLU whose intermediate size F is not a multiple of 128 (DeepSeek-V2-Lite's first layer:
+  10944) cannot take the down projection (K = F) on the 128-deep pre-shuffled tiles.  Pad F to F' = 128k
+  with zero features instead: gate/up gain zero rows (interleaved groups past F, so silu(0) * 0 = 0 columns
+  in the activation) and down gains zero columns -- the same products, every GEMM on the tiled kernels.
+  `xot_logical` records the unpadded shape for _rowmajor / assign_weight (training, export)."""
+  gu, down = lw.gu_w, lw.down_w
+  if gu is None or down is None or gu.dim() != 2 or lw.router is not None or not gu.is_cuda:
+    return
+  if getattr(gu, "xot_layout", "rowmajor") != "rowmajor" or getattr(down, "xot_layout", "rowmajor") != "rowmajor":
+    return
+  F = down.shape[1]
+  if F % 128 == 0 or F % TILE or gu.shape[0] != 2 * F:
+    return
+  Fp = -(-F // 128) * 128
+  lw.gu_w = _pad_to(gu, (2 * Fp, gu.shape[1]))  # pad rows after the last interleaved (gate, up) group pair
+  lw.down_w = _pad_to(down, (down.shape[0], Fp))
+  lw.gu_w.xot_logical, lw.down_w.xot_logical = tuple(gu.shape), tuple(down.shape)
 
 
 def prepare_for_decode(sw: "ShardWeights", keep_rowmajor: Iterable[str] = (), fp8: bool = False) -> "ShardWeights":
@@ -284,9 +321,31 @@ def prepare_for_decode(sw: "ShardWeights", keep_rowmajor: Iterable[str] = (), fp
       return conv(t)
     return to_stream8_layout(t) if can_shuffle(t) else t
 
+  def conv_bat(t, transpose: bool):
+    """MLA absorbed projections for gemm_batched (N % 128 == 0): W_UV [H, dv, L] per head shuffled ("stream");
+    W_UK [H, dn, L] -> per head shuffle(W_UK[h]^T) [H, L, dn] ("stream_t"), so q_lat = q_nope . W_UK is Y = X W^T."""
+    if t is None or not t.is_cuda or getattr(t, "xot_layout", "rowmajor") != "rowmajor":
+      return t
+    ws = [t[h].t() if transpose else t[h] for h in range(t.shape[0])]
+    if not all(can_shuffle(w) and w.shape[0] % 128 == 0 for w in ws):
+      return t
+    out = torch.stack([shuffle_for_stream(w.contiguous()) for w in ws])
+    out.xot_layout = "stream_t" if transpose else "stream"
+    return out
+
   proj = conv8 if fp8 else conv
+
+  def keep_logical(new, old):  # a converted weight keeps the padded tensor's logical shape
+    if new is not old and getattr(old, "xot_logical", None) is not None:
+      new.xot_logical = old.xot_logical
+    return new
+
   for lw in sw.layers.values():
+    if ("gu" not in keep and "down" not in keep) or fp8:
+      pad_ffn_for_tiles(lw)
+    g0, d0 = lw.gu_w, lw.down_w
     lw.qb_w, lw.sh_gu_w, lw.sh_down_w = conv(lw.qb_w), conv(lw.sh_gu_w), conv(lw.sh_down_w)
+    lw.wuk, lw.wuv = conv_bat(lw.wuk, True), conv_bat(lw.wuv, False)  # the absorbed MLA projections run on gemm_batched
     if "qkv" not in keep or fp8:
       lw.qkv_w = proj(lw.qkv_w)
     if "o" not in keep or fp8:
@@ -295,6 +354,7 @@ def prepare_for_decode(sw: "ShardWeights", keep_rowmajor: Iterable[str] = (), fp
       lw.gu_w = proj(lw.gu_w)
     if "down" not in keep or fp8:
       lw.down_w = proj(lw.down_w)
+    lw.gu_w, lw.down_w = keep_logical(lw.gu_w, g0), keep_logical(lw.down_w, d0)
   if sw.lm_head is not None:
     sw.lm_head = conv(sw.lm_head)  # a tied head becomes a separate shuffled copy; embed stays row-major
   return sw
@@ -308,12 +368,20 @@ def assign_weight(dst: Optional[torch.Tensor], src: torch.Tensor) -> None:
     return
   if getattr(dst, "xot_layout", "rowmajor") == "stream8":  # re-quantize (new row scales, same storage)
     from ..ops.weights_layout import quantize_fp8_rows, shuffle_for_stream8
+    if getattr(dst, "xot_logical", None) is not None:
+      src = _pad_to(src, dst.shape)
     q, sc = quantize_fp8_rows(src.to(dst.device))
     dst.copy_(shuffle_for_stream8(q))
     dst.xot_scale.copy_(sc)
     return
   src = src.to(device=dst.device, dtype=dst.dtype)
-  if getattr(dst, "xot_layout", "rowmajor") == "stream":
+  if getattr(dst, "xot_logical", None) is not None and tuple(src.shape) != tuple(dst.shape):
+    src = _pad_to(src, dst.shape)
+  if getattr(dst, "xot_layout", "rowmajor") == "stream_t":
+    from ..ops.weights_layout import shuffle_for_stream
+    for h in range(dst.shape[0]):
+      dst[h].copy_(shuffle_for_stream(src[h].t().contiguous()))
+  elif getattr(dst, "xot_layout", "rowmajor") == "stream":
     from ..ops.weights_layout import shuffle_for_stream
     if dst.dim() == 3:
       for e in range(dst.shape[0]):

@@ -305,10 +305,12 @@ class GemmPolicy:
   def _big_cands(M, N, Kd):
     cands = []
     tiles0 = -(-M // 256)
+    if N % 16:
+      return cands
     for bn in (256, 1256, 128):  # 1256: the 256 x 256 tile on the two-group ping-pong schedule
-      if N % (bn % 1000):
+      if N % (bn % 1000) and N < bn % 1000:  # a partial last column tile is masked; skip tiles wider than N
         continue
-      tiles = tiles0 * (N // (bn % 1000))
+      tiles = tiles0 * -(-N // (bn % 1000))
       for S in (1, 2, 3, 4, 6, 8):
         if S > 1 and (tiles >= 256 or tiles * S > 1024 or Kd // 64 < 2 * S):
           continue

@@ -32,102 +32,143 @@ def _model_dir(model_id: str) -> Optional[Path]:
   return p if (p / "config.json").exists() else None
 
 
-def _worker(rank: int, world: int, port: int, a: dict) -> None:
-  os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                    LOCAL_RANK=str(rank))
-  import torch.distributed as dist
-  from ..inference.tokenizers import _resolve_tokenizer
-  from ..models import registry
-  from ..models.config import load_config, preset
-  from ..models.weights import load_hf_weights, random_weights
-  from ..parallel.comm import P2PTransport, init_distributed
-  from ..parallel.pipeline_train import PipelineTrainer, TrainBatch
-  from ..topology.ring_memory_weighted_partitioning_strategy import equal_layer_shards
+def _load_stage(a: dict, cfg, mdir, shard, dev, src_dir: Optional[str], rank: int):
+  """Weights of `shard` (HF files or random init, then the newest complete checkpoint in `src_dir` if any)
+  and its ShardTrainer (optimizer moments merged from every sidecar of that iteration: after a re-partition
+  a stage's layers come from several old stages' files).  Returns (weights, trainer, iteration or 0)."""
+  from ..models.weights import copy_weights_into, from_hf_state_dict, load_hf_weights, random_weights
   from ..train import checkpoint as ck
-  from ..train.dataset import DEFAULT_DATA, iterate_batches, load_dataset
   from ..train.trainer import ShardTrainer
-
-  rank, world, dev = init_distributed()
   model = a["model"]
-  mdir = _model_dir(model)
-  cfg = load_config(mdir) if mdir is not None else preset(model)
-  dp = a.get("parallel") == "dp"
-  if dp:
-    from ..inference.shard import Shard
-    shard = Shard(model, 0, cfg.num_layers - 1, cfg.num_layers)
-  else:
-    shard = equal_layer_shards(model, cfg.num_layers, world)[rank]
   if mdir is not None and any(mdir.glob("*.safetensors")):
     w = load_hf_weights(mdir, cfg, shard, dev)
   else:
     w = random_weights(cfg, shard, dev, seed=0)
-  if a.get("resume") and ck.list_checkpoints(a["resume"], model):
-    latest, files = ck.select_checkpoint_files(a["resume"], shard)  # one partition, no overlapping files
+  it, files = 0, []
+  if src_dir and ck.list_checkpoints(src_dir, model):
+    it, files = ck.select_checkpoint_files(src_dir, shard)  # one partition, no overlapping files
     sd = ck._gather_tensors(files, shard, cfg.tie_word_embeddings)
-    from ..models.weights import copy_weights_into, from_hf_state_dict
     copy_weights_into(w, from_hf_state_dict(sd, cfg, shard, device=dev))
     if rank == 0:
-      print(f"resumed {model} from iteration {latest}", flush=True)
+      print(f"resumed {model} from iteration {it}", flush=True)
   tr = ShardTrainer(w, dev, lr=a["lr"], max_seq=4096)
-  if a.get("resume"):  # optimizer state of this exact shard, when the partitioning is unchanged
-    files = ck.list_checkpoints(a["resume"], model)
-    if files:
-      side = ck.checkpoint_path(a["resume"], shard, files[-1][0])
-      side = side.with_name(side.name.replace(".safetensors", ".optim.safetensors"))
+  if files:
+    from safetensors.torch import load_file
+    state = {}
+    for f in files:
+      side = f.with_name(f.name.replace(".safetensors", ".optim.safetensors"))
       if side.exists():
-        from safetensors.torch import load_file
-        tr.load_state_dict({k: v.to(dev) for k, v in load_file(str(side)).items()})
-  if dp:
-    from ..parallel.data_parallel import DataParallelTrainer
-    pt = DataParallelTrainer(tr, rank, world)
-  else:
-    mon = None
-    if world > 1 and os.environ.get("XOT_HEARTBEAT", "1") == "1":  # parallel/health.py
-      from ..parallel.health import HealthMonitor
-      mon = HealthMonitor(rank, world, timeout=float(os.environ.get("XOT_HEARTBEAT_TIMEOUT", "30"))).start()
-    pt = PipelineTrainer(tr, rank, world, P2PTransport(rank, world, monitor=mon), schedule=a.get("schedule", "gpipe"))
+        state.update({k: v.to(dev) for k, v in load_file(str(side)).items()})
+    if state:
+      tr.load_state_dict(state)
+  return w, tr, it
+
+
+def _failed_peers(e: BaseException, mon) -> Optional[list]:
+  """The dead ranks behind a training exception, or None if it is not a peer failure.  A collective
+  (gloo all-reduce) on a closed peer fails with a backend error before the heartbeat times out: wait for
+  the monitor's verdict."""
+  from ..parallel.health import PeerFailure
+  if isinstance(e, PeerFailure):
+    return list(e.dead)
+  if isinstance(e, RuntimeError) and mon is not None and mon.failed.wait(mon.timeout + 4 * mon.interval + 1):
+    return sorted(mon.dead)
+  return None
+
+
+def _worker(rank: int, world: int, port: int, a: dict) -> None:
+  os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                    LOCAL_RANK=str(rank))
+  import torch.distributed as dist
+  from ..inference.shard import Shard
+  from ..inference.tokenizers import _resolve_tokenizer
+  from ..models import registry
+  from ..models.config import load_config, preset
+  from ..parallel.comm import P2PTransport, init_distributed
+  from ..parallel.health import FaultInjector, HealthMonitor, reform_ring
+  from ..parallel.pipeline_train import PipelineTrainer, TrainBatch
+  from ..parallel.ring_serve import control_group, ring_shards
+  from ..train.dataset import DEFAULT_DATA, load_dataset
+
+  rank, world, dev = init_distributed()
+  backend = dist.get_backend() if world > 1 else None
+  model = a["model"]
+  mdir = _model_dir(model)
+  cfg = load_config(mdir) if mdir is not None else preset(model)
+  dp = a.get("parallel") == "dp"
   tok = _resolve_tokenizer(mdir if mdir is not None else (registry.get_repo(model, "ShardedInferenceEngine") or "byte"),
                            cfg.vocab_size)
   train, valid, test = load_dataset(a["data"] or DEFAULT_DATA, lambda s: tok.encode(s))
   bs, mb = a["batch_size"], max(1, a["micro_batch"])
-
-  def to_micro(batch):
-    x, y, ln = batch
-    lo, hi = 0, x.shape[0]
-    if dp:  # data parallel: this rank's contiguous share of the rows (sizes differ by at most one; a
-      # batch with fewer rows than ranks leaves some ranks without work -- they still join every
-      # all-reduce, in the same order, with zero gradients: parallel/data_parallel.py)
-      lo, hi = rank * x.shape[0] // world, (rank + 1) * x.shape[0] // world
-    out = []
-    for i in range(lo, hi, mb):
-      j = min(i + mb, hi)
-      out.append(TrainBatch(torch.from_numpy(x[i:j]), torch.from_numpy(y[i:j]), torch.from_numpy(ln[i:j])))
-    return out
+  hb_timeout = float(os.environ.get("XOT_HEARTBEAT_TIMEOUT", "30"))
+  injector = None  # the environment's (tests) on the first ring; none after a re-form
+  generation, src_dir, first_epoch = 0, a.get("resume"), 0
 
   class _Shim:  # save_shard_checkpoint wants engine.runner.weights / engine.trainer
     pass
 
-  if a["command"] == "eval":
-    tot, n = 0.0, 0
-    for batch in iterate_batches(test, bs):
-      micro = to_micro(batch)
-      loss = _eval_dp(pt, micro) if dp else _eval(pt, micro)
-      tot += loss * float(batch[2].sum())
-      n += int(batch[2].sum())
-    if rank == 0:
-      print(f"eval | loss={tot / max(n, 1):.4f} tokens={n}", flush=True)
-  else:
+  while True:
+    if dp:
+      shard = Shard(model, 0, cfg.num_layers - 1, cfg.num_layers)
+    else:  # memory-weighted layer ranges in ring order (parallel/ring_serve.py:ring_shards)
+      shard = ring_shards(model, cfg.num_layers, world, control_group() if world > 1 else None)[rank]
+    w, tr, _ = _load_stage(a, cfg, mdir, shard, dev, src_dir, rank)
+    mon = None
+    if dp:
+      from ..parallel.data_parallel import DataParallelTrainer
+      pt = DataParallelTrainer(tr, rank, world)
+    else:
+      if world > 1 and os.environ.get("XOT_HEARTBEAT", "1") == "1":  # parallel/health.py
+        mon = HealthMonitor(rank, world, timeout=hb_timeout, generation=generation).start()
+      t = P2PTransport(rank, world, monitor=mon, injector=injector)
+      pt = PipelineTrainer(tr, rank, world, t, schedule=a.get("schedule", "gpipe"))
+
+    def to_micro(batch, rank=rank, world=world):
+      x, y, ln = batch
+      lo, hi = 0, x.shape[0]
+      if dp:  # data parallel: this rank's contiguous share of the rows (sizes differ by at most one; a
+        # batch with fewer rows than ranks leaves some ranks without work -- they still join every
+        # all-reduce, in the same order, with zero gradients: parallel/data_parallel.py)
+        lo, hi = rank * x.shape[0] // world, (rank + 1) * x.shape[0] // world
+      out = []
+      for i in range(lo, hi, mb):
+        j = min(i + mb, hi)
+        out.append(TrainBatch(torch.from_numpy(x[i:j]), torch.from_numpy(y[i:j]), torch.from_numpy(ln[i:j])))
+      return out
+
+    if a["command"] == "eval":
+      _run_eval(pt, test, bs, to_micro, dp, rank)
+      break
     try:
-      _train_epochs(a, pt, tr, w, shard, rank, world, dp, train, bs, to_micro, _Shim)
+      _train_epochs(a, pt, tr, w, shard, rank, world, dp, train, bs, to_micro, _Shim, first_epoch)
+      break
     except Exception as e:
-      from ..parallel.health import PeerFailure
-      if not isinstance(e, PeerFailure):
+      dead = _failed_peers(e, mon)
+      if dead is None or dp or 0 in dead or rank in dead:
         raise
-      # a ring peer died or wedged: its layers (and the in-flight step) are gone.  Exit without the
-      # closing barrier; `xot train --resume-checkpoint DIR` re-partitions the last saved iteration
-      # (HF key names, any layer split) over the peers that are left.
-      print(f"[rank {rank}] {e}; stopping, resume from the last checkpoint", flush=True)
-      os._exit(75)
+      # a ring peer died or wedged: its layers and the in-flight step are gone.  The survivors re-form a
+      # dense ring, re-partition the layers over it and reload the last complete checkpoint in place
+      # (the reference re-partitions on the next request after a peer drops: orchestration/node.py:455-460).
+      alive = [r for r in range(world) if r not in set(dead)]
+      if mon is not None:
+        mon.stop()
+      generation += 1
+      print(f"[rank {rank}] peer(s) {dead} failed: re-forming the training ring over {alive} "
+            f"(generation {generation})", flush=True)
+      del pt, tr, w
+      if torch.cuda.is_available():
+        torch.cuda.empty_cache()
+      rank, world = reform_ring(alive, rank, generation, backend=backend)
+      injector = FaultInjector("", rank)
+      from ..train import checkpoint as ck
+      save = a.get("save_dir")
+      if save and ck.list_checkpoints(save, model):
+        src_dir = save
+        first_epoch = ck.select_checkpoint_files(save, Shard(model, 0, cfg.num_layers - 1, cfg.num_layers))[0]
+      else:  # nothing saved by this run yet: restart it from its initial weights
+        first_epoch = 0
+      if rank == 0:
+        print(f"restarting at epoch {first_epoch + 1} on {world} rank(s)", flush=True)
   if world > 1:
     if not dp and pt.t.monitor is not None:
       pt.t.monitor.stop()  # orderly exit: peers must not flag it
@@ -135,10 +176,22 @@ def _worker(rank: int, world: int, port: int, a: dict) -> None:
     dist.destroy_process_group()
 
 
-def _train_epochs(a, pt, tr, w, shard, rank, world, dp, train, bs, to_micro, _Shim):
+def _run_eval(pt, test, bs, to_micro, dp, rank) -> None:
+  from ..train.dataset import iterate_batches
+  tot, n = 0.0, 0
+  for batch in iterate_batches(test, bs):
+    micro = to_micro(batch)
+    loss = _eval_dp(pt, micro) if dp else _eval(pt, micro)
+    tot += loss * float(batch[2].sum())
+    n += int(batch[2].sum())
+  if rank == 0:
+    print(f"eval | loss={tot / max(n, 1):.4f} tokens={n}", flush=True)
+
+
+def _train_epochs(a, pt, tr, w, shard, rank, world, dp, train, bs, to_micro, _Shim, first_epoch: int = 0):
   from ..train import checkpoint as ck
   from ..train.dataset import iterate_batches
-  for epoch in range(a["iters"]):
+  for epoch in range(first_epoch, a["iters"]):
     tot, n = 0.0, 0
     for batch in iterate_batches(train, bs, train=True, seed=epoch):
       loss = pt.step(to_micro(batch))
@@ -218,8 +271,9 @@ def run_ring(args) -> int:
   procs = [ctx.Process(target=_worker, args=(r, n, port, a)) for r in range(n)]
   for p in procs:
     p.start()
-  rc = 0
   for p in procs:
     p.join()
-    rc = rc or (p.exitcode or 0)
-  return rc
+  for r, p in enumerate(procs[1:], 1):
+    if p.exitcode:  # the survivors re-formed the ring without it (rank 0's own exit code says if they finished)
+      print(f"training rank {r} exited with code {p.exitcode}", flush=True)
+  return procs[0].exitcode or 0

@@ -64,7 +64,7 @@ class ShardTrainer:
           self._add(f"{i}.qb", _rowmajor(lw.qb_w))
         self._add(f"{i}.kv_ln", lw.kv_ln)
         # kv_b_proj as one [H (dn + dv), kv_lora] projection (HF layout; the serving path splits it)
-        self._add(f"{i}.kvb", torch.cat([lw.wuk, lw.wuv], 1).reshape(-1, c.kv_lora_rank))
+        self._add(f"{i}.kvb", torch.cat([_rowmajor(lw.wuk), _rowmajor(lw.wuv)], 1).reshape(-1, c.kv_lora_rank))
       if lw.router is not None:  # MoE: router [E, D], experts' gate|up [E, 2F, D], down [E, D, F]
         self._add(f"{i}.router", _rowmajor(lw.router))
         self._add(f"{i}.egu", torch.cat([g, u], 1))
