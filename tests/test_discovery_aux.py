@@ -154,3 +154,38 @@ def test_topology_viz_renders():
   c.print(v.render())
   out = c.export_text()
   assert "gpu1" in out and "hello" in out and "50.0%" in out and "GPU rich" in out
+  assert "4 Node Cluster" in out and "[0.25-0.50]" in out and "2516.6 TFLOPS" in out
+
+
+def test_topology_viz_links_layers_and_own_download():
+  """The ring panel shows each edge's link description both ways and each peer's layer range; the download
+  panel details this node's repo (files, bytes, per-file bars) and summarises the other nodes."""
+  pytest.importorskip("rich")
+  from datetime import timedelta
+
+  from rich.console import Console
+
+  from xotorch_support_jetson_amd.download.download_progress import RepoFileProgressEvent, RepoProgressEvent
+  from xotorch_support_jetson_amd.inference.shard import Shard
+  from xotorch_support_jetson_amd.topology.partitioning_strategy import Partition
+  from xotorch_support_jetson_amd.topology.topology import Topology
+  from xotorch_support_jetson_amd.viz.topology_viz import TopologyViz
+  v = TopologyViz(start=False)
+  topo = Topology()
+  for i in range(3):
+    topo.update_node(f"n{i}", DeviceCapabilities(model="MI355X", chip="AMD Instinct MI355X", memory=294912,
+                                                 flops=DeviceFlops(fp32=157.3, fp16=2516.6, int8=5033.2)))
+  topo.add_edge("n0", "n1", "xGMI")
+  topo.add_edge("n1", "n0", "RCCL")
+  parts = [Partition("n0", 0.0, 0.5), Partition("n1", 0.5, 0.75), Partition("n2", 0.75, 1.0)]
+  f = RepoFileProgressEvent("org/m", "main", "model-00001.safetensors", 30, 30, 120, 10.0, timedelta(seconds=9),
+                            "in_progress", 0.0)
+  ev = RepoProgressEvent(Shard("m", 0, 39, 80), "org/m", "main", 1, 3, 300, 300, 1200, 2048.0, timedelta(seconds=65),
+                         {"model-00001.safetensors": f}, "in_progress")
+  v.update_visualization(topo, parts, "n0", {"n0": ev, "n1": ev.to_dict()}, num_layers=80)
+  c = Console(record=True, width=140)
+  c.print(v.render())
+  out = c.export_text()
+  assert "xGMI/RCCL" in out and "layers 0-39" in out and "layers 60-79" in out
+  assert "(1/3 files)" in out and "model-00001.safetensors" in out and "25%" in out and "ETA 0:01:05" in out
+  assert "Other nodes:" in out and "[0.50-0.75]" in out

@@ -37,6 +37,7 @@ from .weights import ShardWeights, expert
 MOE_BIG_MIN_ROWS = float(os.environ.get("XOT_MOE_BIG_MIN_ROWS", "24"))
 # K splits of the grouped gate/up GEMM for decode-sized batches (1: fused SiLU epilogue, no slabs)
 MOE_GU_SPLITS = int(os.environ.get("XOT_MOE_GU_SPLITS", "4"))
+MOE_BM = int(os.environ.get("XOT_MOE_BM", "0"))  # force the grouped gemm_big row tile (128 / 192 / 256; tests, A/B)
 PAGE = 64
 
 
@@ -261,8 +262,13 @@ class ShardModel:
     # tiles (128 or 256 rows) once the groups are compute-bound
     rows = T * k / E
     # measured (tools/bench_moe.py, Mixtral shapes): 192-row tiles when one tile holds an expert's
-    # ~100-160 rows, 256 otherwise (a tile's rows past the expert's count are masked MFMA work)
-    bm = 0 if not shuffled or rows < MOE_BIG_MIN_ROWS else (192 if 96 < rows <= 160 else 256)
+    # ~100-160 rows, 256 otherwise (a tile's rows past the expert's count are masked MFMA work); 128-row
+    # tiles for small groups of few experts (Mixtral B=128, 32 rows: 20.6 vs 22.3 ms/step) but not for
+    # many experts (DeepSeek-V2-Lite B=256, 64 experts x 24 rows: 12.6 vs 11.0 ms/step with 256)
+    small = 128 if E <= 16 else 256
+    bm = 0 if not shuffled or rows < MOE_BIG_MIN_ROWS else (small if rows <= 96 else (192 if rows <= 160 else 256))
+    if MOE_BM and bm:
+      bm = MOE_BM
     act = torch.empty(T * k, F, dtype=torch.bfloat16, device=dev)
     Sg = MOE_GU_SPLITS if (bm == 0 and T * k <= 32 and D % (256 * MOE_GU_SPLITS) == 0) else 1
     if Sg > 1:

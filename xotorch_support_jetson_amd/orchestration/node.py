@@ -113,7 +113,7 @@ class Node:
         self.node_download_progress[status.get("node_id")] = status.get("progress")
       if self.topology_viz:
         self.topology_viz.update_visualization(self.topology, self.partitioning_strategy.partition(self.topology), self.id,
-                                               self.node_download_progress)
+                                               self.node_download_progress, num_layers=self._viz_layers())
     except Exception as e:
       if DEBUG >= 1:
         print(f"Error on_node_status: {e}")
@@ -579,8 +579,13 @@ class Node:
     next_topology.active_node_id = self.topology.active_node_id
     self.topology = next_topology
     if self.topology_viz:
-      self.topology_viz.update_visualization(self.topology, self._partitions(), self.id)
+      self.topology_viz.update_visualization(self.topology, self._partitions(), self.id, num_layers=self._viz_layers())
     return self.topology
+
+  def _viz_layers(self):
+    """Layer count of the model this node serves (the TUI shows each peer's layer range), if one is loaded."""
+    shard = getattr(self.inference_engine, "shard", None)
+    return getattr(shard, "n_layers", None)
 
   @property
   def current_topology(self) -> Topology:
