@@ -785,3 +785,44 @@ def test_moe_route_ds(gpu, E, k, ng, tg, method, sig, norm):
     for j in range(k):
       e = int(topi.view(T, k)[t, j])
       assert off_c[e] <= so[t, j] < off_c[e + 1] and int(st[so[t, j]]) == t
+
+
+@pytest.mark.parametrize("R,C", [(256, 384), (128, 64), (512, 1024)])
+def test_relayout_kernels(gpu, R, C):
+  """csrc/layout.hip: shuffle / shuffle of the transpose / transpose vs the torch permutations, from a
+  row-strided source."""
+  from xotorch_support_jetson_amd.ops.weights_layout import shuffle_for_stream
+  from xotorch_support_jetson_amd.train.autograd_ops import relayout
+  torch.manual_seed(0)
+  big = torch.randn(R, C + 64, device=gpu, dtype=torch.bfloat16)
+  src = big[:, :C]
+  if C % 128 == 0:
+    assert torch.equal(relayout(src, 0), shuffle_for_stream(src.contiguous()))
+  assert torch.equal(relayout(src, 1), shuffle_for_stream(src.t().contiguous()))
+  assert torch.equal(relayout(src, 2), src.t().contiguous())
+
+
+@pytest.mark.parametrize("with_h", [False, True])
+def test_own_linear_grads_match_torch(gpu, with_h):
+  """OwnLinearFn (forward, dX, dW accumulated over two micro-batches into the GradAcc buffer) on the MFMA
+  GEMMs vs fp32 torch autograd."""
+  from xotorch_support_jetson_amd.train import autograd_ops as A
+  torch.manual_seed(0)
+  T, Kd, N = 256, 384, 512
+  w = (torch.randn(N, Kd, device=gpu) / math.sqrt(Kd)).to(torch.bfloat16).requires_grad_(True)
+  tw, acc = A.TrainWeight(w), A.GradAcc("w", w)
+  assert tw.ok
+  xs = [torch.randn(T, Kd, device=gpu, dtype=torch.bfloat16) for _ in range(2)]
+  hs = [torch.randn(T, N, device=gpu, dtype=torch.bfloat16) for _ in range(2)]
+  gs = [torch.randn(T, N, device=gpu, dtype=torch.bfloat16) for _ in range(2)]
+  dw_ref = torch.zeros(N, Kd, device=gpu)
+  for x, h, g in zip(xs, hs, gs):
+    xl = x.clone().requires_grad_(True)
+    y = A.linear_own(xl, w, tw, acc, h if with_h else None)
+    yr = x.float() @ w.detach().float().t() + (h.float() if with_h else 0)
+    assert rel_err(y, yr) < 1e-2
+    y.backward(g)
+    assert rel_err(xl.grad, g.float() @ w.detach().float()) < 1e-2
+    dw_ref += g.float().t() @ x.float()
+  assert w.grad is None
+  assert rel_err(acc.buf, dw_ref) < 1e-2

@@ -166,7 +166,11 @@ def test_fused_grad_accumulation_values(gpu, name):
     ref = gr[k]
     rel = ((gf[k] - ref).norm() / (ref.norm() + 1e-12)).item()
     scale = (gf[k].norm() / (ref.norm() + 1e-12)).item()
-    assert rel < 0.03 and abs(scale - 1) < 0.02, (k, rel, scale)
+    # the fused run's projections are the own MFMA GEMMs, the plain run's torch.matmul: bf16 rounding of the
+    # activations differs, and the router gradient (softmax Jacobian: differences of near-equal terms)
+    # amplifies it; a doubled / dropped micro-batch still moves `scale` by >= 1/3
+    tol = 0.1 if k.endswith("router") else 0.05
+    assert rel < tol and abs(scale - 1) < 0.02, (k, rel, scale)
 
 
 @pytest.mark.parametrize("name", ["tiny-mixtral", "tiny-deepseek-v2", "tiny-deepseek-v3"])
@@ -344,3 +348,34 @@ def test_padded_ffn_and_mla_batched_match_cpu(gpu, name):
     lc = cpu.forward(["a", "b"], [1, 1], tok)
     lg = gr.forward(["a", "b"], [1, 1], tok).cpu()
     assert ((lc - lg).norm() / lc.norm()).item() < 3e-2
+
+
+@pytest.mark.parametrize("name", ["tiny-llama-d64", "tiny-qwen"])
+def test_fused_head_ce_matches_logits_path(gpu, name):
+  """Fused LM head + chunked CE (A.LmHeadCEFn: chunks of 128 rows, own GEMMs) vs materialised logits +
+  cross-entropy: same loss and the same gradients for the head, the final norm and the input."""
+  import xotorch_support_jetson_amd.train.trainer as T
+  from xotorch_support_jetson_amd.train.trainer import ShardTrainer
+  c = preset(name)
+  sh = Shard(name, 0, c.num_layers - 1, c.num_layers)
+  tr = ShardTrainer(random_weights(c, sh, gpu, seed=3), gpu, lr=1e-3, max_seq=512)
+  assert tr.fused_head()
+  g = torch.Generator().manual_seed(1)
+  x = torch.randint(0, c.vocab_size, (2, 192), generator=g)
+  y, ln = torch.roll(x, -1, 1), torch.tensor([192, 130])
+  old = T.CE_CHUNK
+  T.CE_CHUNK = 128
+  try:
+    hid = tr.forward(x.to(gpu), logits=False)
+    l1 = tr.head_loss(hid, y, ln, 322.0)
+    l1.backward()
+  finally:
+    T.CE_CHUNK = old
+  g1 = {k: tr.params[k].grad.float().clone() for k in (tr.head_name, "norm")}
+  tr.zero_grad()
+  l2, _ = tr.loss_of(tr.forward(x.to(gpu)), y, ln, 322.0)
+  l2.backward()
+  assert abs(float(l1) - float(l2)) < 1e-3 * max(1.0, abs(float(l2)))
+  for k, a in g1.items():
+    b = tr.params[k].grad.float()
+    assert ((a - b).norm() / (b.norm() + 1e-12)).item() < 3e-2, k

@@ -410,6 +410,21 @@ int64_t gemm_sk_part_elems() { return xot::gemm_sk_part_elems(); }
 // B independent projections (MLA's per-head absorbed q . W_UK and o . W_UV^T): y_e = x_e . w_e^T with
 // x_e = x.data + e * xbat (rows x.stride(0) apart, K columns), w = [B, N, K] pre-shuffled per problem,
 // y_e = y.data + e * ybat (rows ldy apart, N columns).
+// Layout kernels of the training GEMMs (csrc/layout.hip).  mode 0: dst = shuffle(src) ([R, C], R % 16,
+// C % 128); 1: dst = shuffle(src^T) ([C, R] shuffled; R % 128, C % 64); 2: dst = src^T row-major (same).
+void relayout(const at::Tensor& src, at::Tensor& dst, int64_t mode) {
+  CHECK_BF16(src);
+  CHECK_BF16(dst);
+  XCHECK(src.dim() == 2 && src.stride(1) == 1 && src.stride(0) % 8 == 0, "relayout: src must be 2-D with 16-B rows");
+  XCHECK(dst.is_contiguous() && dst.numel() == src.numel(), "relayout: dst must be contiguous, same size");
+  const int R = (int)src.size(0), C = (int)src.size(1);
+  int rc = -1;
+  if (mode == 0) rc = xot::launch_shuffle(bf(src), src.stride(0), bf(dst), R, C, cur_stream());
+  else if (mode == 1) rc = xot::launch_shuffle_t(bf(src), src.stride(0), bf(dst), R, C, cur_stream());
+  else if (mode == 2) rc = xot::launch_transpose(bf(src), src.stride(0), bf(dst), R, C, cur_stream());
+  XCHECK(rc == 0, "relayout: unsupported shape R=", R, " C=", C, " mode=", mode);
+}
+
 void gemm_batched(const at::Tensor& x, int64_t xbat, int64_t K, const at::Tensor& w, at::Tensor& y, int64_t ybat,
                   int64_t ldy, int64_t M) {
   CHECK_BF16(x);
@@ -882,6 +897,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_sk", &gemm_sk, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("bias"), py::arg("res"), py::arg("part"),
         py::arg("sync"), py::arg("epi"), py::arg("cus") = 256);
   m.def("gemm_sk_part_elems", &gemm_sk_part_elems);
+  m.def("relayout", &relayout);
   m.def("gemm_batched", &gemm_batched, py::arg("x"), py::arg("xbat"), py::arg("K"), py::arg("w"), py::arg("y"),
         py::arg("ybat"), py::arg("ldy"), py::arg("M"));
   m.def("gemm_sk_sync_words", &gemm_sk_sync_words);

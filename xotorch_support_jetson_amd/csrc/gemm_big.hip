@@ -477,20 +477,36 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
       if (cbase + 16 * j >= N) break;
       const int col = cbase + 16 * j + c;
       const float bv = bias != nullptr ? bf2f(bias[col]) : 0.f;
+      // residuals of this column tile loaded up front (one latency for MT x 4 loads; the per-element
+      // load-add-store chain exposed it per element: +50 % on accumulating dW GEMMs); rows past Mv
+      // re-read row Mv - 1 and are not stored.  In place (R == Y) is safe: each element is read and
+      // written by this lane only.
+      constexpr int IP = MT >= 4 ? MT / 2 : MT;  // row tiles per prefetch group (register budget)
 #pragma unroll
-      for (int i = 0; i < MT; ++i)
+      for (int i0 = 0; i0 < MT; i0 += IP) {
+      float rv[IP][4];
+      if constexpr (EPI == EPI_RESID) {
+#pragma unroll
+        for (int i = 0; i < IP; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            rv[i][r] = bf2f(R[(size_t)min(rbase + 16 * (i0 + i) + 4 * g + r, Mv - 1) * ldr + col]);
+      }
+#pragma unroll
+      for (int i = 0; i < IP; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int m = rbase + 16 * i + 4 * g + r;
+          const int m = rbase + 16 * (i0 + i) + 4 * g + r;
           if (m < Mv) {
-            float v = acc[i][j][r] + bv;
-            if constexpr (EPI == EPI_RESID) v += bf2f(R[(size_t)m * ldr + col]);
+            float v = acc[i0 + i][j][r] + bv;
+            if constexpr (EPI == EPI_RESID) v += rv[i][r];
             if constexpr (OUT_F32)
               reinterpret_cast<float*>(Yv)[(size_t)m * ldy + col] = v;
             else
               reinterpret_cast<uint16_t*>(Yv)[(size_t)m * ldy + col] = f2bf(v);
           }
         }
+      }
     }
   }
 }

@@ -50,6 +50,10 @@ int launch_gemm_sk(const uint16_t* X, int ldx, const uint16_t* W, const uint16_t
                    hipStream_t s);
 long gemm_sk_part_elems();
 // B independent GEMMs Y_e = X_e . W_e^T (pre-shuffled W [B][N][K]; X_e = X + e*xbat, Y_e = Y + e*ybat)
+// training-GEMM layouts (csrc/layout.hip): src [R, C] row-major with row stride ld
+int launch_shuffle(const uint16_t* src, long ld, uint16_t* dst, int R, int C, hipStream_t s);
+int launch_shuffle_t(const uint16_t* src, long ld, uint16_t* dst, int R, int C, hipStream_t s);
+int launch_transpose(const uint16_t* src, long ld, uint16_t* dst, int R, int C, hipStream_t s);
 int launch_gemm_batched(const uint16_t* X, int ldx, long xbat, const uint16_t* W, void* Y, int ldy, long ybat,
                         bool out_f32, int B, int M, int N, int K, hipStream_t s);
 long gemm_sk_sync_words(int M, int N);

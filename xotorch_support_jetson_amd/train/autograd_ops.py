@@ -6,7 +6,8 @@
   CrossEntropyFn  per-row loss with ignore (-100) and per-row weights; forward ce_fwd, backward ce_bwd
   AttentionFn  causal GQA self-attention: attn_train_fwd (flash-style, saves O and the row log2-sum-exp),
                backward attn_train_bwd (dQ pass with delta = rowsum(dO*O), then the dK/dV pass)
-Projections use torch.matmul (hipBLASLt).
+OwnLinearFn  projections on the MFMA GEMMs (shuffled operands from csrc/layout.hip); LinearFn (torch.matmul)
+             only for shapes the tiles do not cover.
 """
 from __future__ import annotations
 
@@ -281,6 +282,150 @@ class LinearFn(torch.autograd.Function):
 
 def linear_acc(x, w, acc, h=None):
   return LinearFn.apply(x, w, h, acc)
+
+
+# ------------------------------------------------------------------ projections on the kernel library
+def relayout(src: torch.Tensor, mode: int, out: torch.Tensor | None = None) -> torch.Tensor:
+  """csrc/layout.hip: 0 shuffle(src), 1 shuffle(src^T), 2 src^T (row-major); src [R, C] bf16 with unit column
+  stride.  The shuffled results are tagged with the "stream" layout the GEMM dispatch (ops/linear.py) reads."""
+  R, C = src.shape
+  if out is None:
+    out = torch.empty((R, C) if mode == 0 else (C, R), dtype=torch.bfloat16, device=src.device)
+  require().relayout(src, out, mode)
+  if mode != 2:
+    out.xot_layout = "stream"
+  return out
+
+
+class TrainWeight:
+  """A projection weight W [N, K] in the two operand layouts of the own GEMMs, refreshed after every optimizer
+  step (`refresh`, ~2 x 2 bytes x |W| of HBM traffic): ws = shuffle(W) for y = x W^T and wts = shuffle(W^T)
+  for dX = dY W.  `ok` is False for shapes the tiles do not cover (then the projection stays on torch)."""
+
+  def __init__(self, w: torch.Tensor):
+    self.w = w
+    N, K = w.shape
+    self.ok = w.is_cuda and w.dim() == 2 and N % 128 == 0 and K % 128 == 0
+    if self.ok:
+      self.ws = torch.empty_like(w, dtype=torch.bfloat16, requires_grad=False)
+      self.wts = torch.empty(K, N, dtype=torch.bfloat16, device=w.device)
+      self.refresh()
+
+  @torch.no_grad()
+  def refresh(self) -> None:
+    if self.ok:
+      relayout(self.w.detach(), 0, self.ws)
+      relayout(self.w.detach(), 1, self.wts)
+
+
+def _own_dw_ok(x: torch.Tensor, dy: torch.Tensor) -> bool:
+  """dW = dY^T X on the tiles: dY^T [N, T] row-major and shuffle(X^T) [K, T] need T % 128, N and K % 64."""
+  return x.shape[0] % 128 == 0 and dy.shape[1] % 64 == 0 and x.shape[1] % 64 == 0
+
+
+class OwnLinearFn(torch.autograd.Function):
+  """LinearFn on the kernel library's MFMA GEMMs (gemm_big / stream-K / weight-streaming, chosen per shape by
+  ops/linear.py's policy) instead of hipBLASLt:
+    forward   y  = x . shuffle(W)^T (+ h: the residual epilogue)
+    backward  dX = dY . shuffle(W^T)^T
+              dW = dY^T . shuffle(X^T)^T into the GradAcc buffer (plain store on the first micro-batch of a
+                   step, residual epilogue acc += ... after), with dY^T and shuffle(X^T) built per micro-batch
+                   by csrc/layout.hip (about 2 x T x (N + K) x 2 bytes each)."""
+
+  @staticmethod
+  def forward(ctx, x, w, tw, h, acc):
+    from ..ops.linear import linear
+    x = x if (x.stride(1) == 1 and x.stride(0) % 8 == 0) else x.contiguous()
+    ctx.save_for_backward(x)
+    ctx.tw, ctx.acc, ctx.has_h = tw, acc, h is not None
+    if h is not None:
+      return linear(x, tw.ws, residual=h.contiguous(), epi="resid")
+    return linear(x, tw.ws)
+
+  @staticmethod
+  def backward(ctx, dy):
+    from ..ops.linear import linear
+    (x,) = ctx.saved_tensors
+    tw, acc = ctx.tw, ctx.acc
+    dy = dy.contiguous()
+    dx = linear(dy, tw.wts)
+    if _own_dw_ok(x, dy):
+      dyt = relayout(dy, 2)  # [N, T]
+      xts = relayout(x, 1)   # shuffle(X^T) [K, T]
+      if acc.fresh:
+        linear(dyt, xts, out=acc.buf)
+        acc.fresh = False
+      else:
+        linear(dyt, xts, residual=acc.buf, epi="resid", out=acc.buf)
+    else:
+      if acc.fresh:
+        torch.mm(dy.t(), x, out=acc.buf)
+        acc.fresh = False
+      else:
+        acc.buf.addmm_(dy.t(), x)
+    if acc.cb is not None:
+      acc.cb()
+    return dx, None, None, (dy if ctx.has_h else None), None
+
+
+def linear_own(x, w, tw, acc, h=None):
+  return OwnLinearFn.apply(x, w, tw, h, acc)
+
+
+class LmHeadCEFn(torch.autograd.Function):
+  """sum_t w_t CE(xn_t . head^T, y_t) without materialising [T, V] logits: row chunks of `chunk`
+  tokens; per chunk the fp32 logits come from the own GEMM, ce_fwd / ce_bwd give the loss and dlogits (bf16),
+  and -- the loss being the last op, its upstream gradient a scalar -- dX_c = dlogits_c . head and
+  dHead += dlogits_c^T . X_c are formed right there, so the backward only scales the saved gradients.
+  Peak memory: one [chunk, V] fp32 logits block + its bf16 gradient."""
+
+  @staticmethod
+  def forward(ctx, xn, head, tw, targets, weights, chunk):
+    from ..ops.linear import linear
+    T, D = xn.shape
+    C = require()
+    dxn = torch.empty_like(xn)
+    dhead = torch.empty(head.shape, dtype=torch.bfloat16, device=xn.device)
+    total = torch.zeros((), dtype=torch.float32, device=xn.device)
+    for i, r0 in enumerate(range(0, T, chunk)):
+      r1 = min(T, r0 + chunk)
+      xc = xn[r0:r1]
+      logits = linear(xc, tw.ws, out_dtype=torch.float32)  # [c, V]
+      loss = torch.empty(r1 - r0, dtype=torch.float32, device=xn.device)
+      lse = torch.empty_like(loss)
+      tc = targets[r0:r1].contiguous()
+      C.ce_fwd(logits, tc, loss, lse)
+      wc = weights[r0:r1].float().contiguous()
+      total += (loss * wc).sum()
+      dl = torch.empty(logits.shape, dtype=torch.bfloat16, device=xn.device)
+      C.ce_bwd(logits, tc, lse, wc, dl)
+      del logits
+      linear(dl, tw.wts, out=dxn[r0:r1])
+      if (r1 - r0) % 128 == 0:
+        dlt, xts = relayout(dl, 2), relayout(xc, 1)  # dlogits^T [V, c], shuffle(X_c^T) [D, c]
+        if i == 0:
+          linear(dlt, xts, out=dhead)
+        else:
+          linear(dlt, xts, residual=dhead, epi="resid", out=dhead)
+      else:  # a ragged last chunk
+        if i == 0:
+          torch.mm(dl.t(), xc, out=dhead)
+        else:
+          dhead.addmm_(dl.t(), xc)
+    ctx.save_for_backward(dxn, dhead)
+    return total
+
+  @staticmethod
+  def backward(ctx, g):
+    dxn, dhead = ctx.saved_tensors
+    if not (isinstance(g, torch.Tensor) and g.numel() == 1 and float(g) == 1.0):
+      dxn, dhead = dxn * g.to(dxn.dtype), dhead * g.to(dhead.dtype)
+    return dxn, dhead, None, None, None, None
+
+
+def lm_head_ce(xn, head, tw, targets, weights, chunk: int = 1024):
+  """xn [T, D] bf16, head [V, D] (its TrainWeight tw), targets [T] int32 (< 0 ignored), weights [T] fp32."""
+  return LmHeadCEFn.apply(xn.contiguous(), head, tw, targets, weights, chunk)
 
 
 class QKVSplitFn(torch.autograd.Function):

@@ -17,6 +17,7 @@ library's forward/backward kernels; GEMMs on hipBLASLt.  Updated weights are wri
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, Optional, Tuple
 
 import numpy as np
@@ -28,6 +29,13 @@ from ..models.weights import ShardWeights, _rowmajor, interleave_gate_up, split_
 from ..ops._ext import require
 from ..ops.rope import longrope_window, rope_shift, rope_table
 from . import autograd_ops as A
+
+
+# XOT_TRAIN_OWN_GEMM=0: projections on torch.matmul (hipBLASLt) instead of the MFMA kernels (A/B, debugging)
+OWN_GEMM = os.environ.get("XOT_TRAIN_OWN_GEMM", "1") == "1"
+# XOT_FUSED_CE=0: materialise [T, V] logits and run the separate cross-entropy (A/B, debugging)
+FUSED_CE = os.environ.get("XOT_FUSED_CE", "1") == "1"
+CE_CHUNK = int(os.environ.get("XOT_CE_CHUNK", "1024"))
 
 
 def _resid_mm(h: torch.Tensor, x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
@@ -92,6 +100,23 @@ class ShardTrainer:
       for k in self.params:
         if k.split(".")[-1] in ("qkv", "o", "gu", "down", "egu", "edown", "qb", "kvb", "sh_gu", "sh_down"):
           self.acc[k] = A.GradAcc(k, self.params[k])
+    # own-GEMM operand layouts of the 2-D projections (refreshed after each optimizer step)
+    self.tw: Dict[str, A.TrainWeight] = {}
+    if self.device.type == "cuda" and OWN_GEMM:
+      for k in self.acc:
+        if self.params[k].dim() == 2:
+          t = A.TrainWeight(self.params[k])
+          if t.ok:
+            self.tw[k] = t
+    # fused LM head + chunked CE on the last stage (A.LmHeadCEFn): forward_train hands back the final normed
+    # hidden state and backward_accumulate computes the loss from it without [T, V] logits
+    self.head_name = None
+    if self.shard.is_last_layer():
+      self.head_name = "lm_head" if "lm_head" in self.params else "embed"
+    if self.device.type == "cuda" and OWN_GEMM and FUSED_CE and self.head_name in self.params:
+      t = A.TrainWeight(self.params[self.head_name])
+      if t.ok:
+        self.tw[self.head_name] = t
     self.master = {k: p.detach().float().clone() for k, p in self.params.items()}
     self.m = {k: torch.zeros_like(v) for k, v in self.master.items()}
     self.v = {k: torch.zeros_like(v) for k, v in self.master.items()}
@@ -100,8 +125,12 @@ class ShardTrainer:
     self.params[name] = t.detach().to(self.device, torch.bfloat16).clone().requires_grad_(True)
 
   # ------------------------------------------------------------------ model
-  def forward(self, x: torch.Tensor) -> torch.Tensor:
-    """x: ids [B, L] (first stage) or hidden [B, L, D].  Returns hidden [B, L, D] or logits [B, L, V]."""
+  def fused_head(self) -> bool:
+    return self.head_name is not None and self.head_name in self.tw
+
+  def forward(self, x: torch.Tensor, logits: bool = True) -> torch.Tensor:
+    """x: ids [B, L] (first stage) or hidden [B, L, D].  Returns hidden [B, L, D] or logits [B, L, V]
+    (logits=False on the last stage: the final normed hidden state [B, L, D], for the fused head + CE)."""
     c, P = self.c, self.params
     H, Hkv, Dh, D = c.num_heads, c.num_kv_heads, c.head_dim, c.hidden_size
     if self.shard.is_first_layer():
@@ -135,7 +164,13 @@ class ShardTrainer:
     if not self.shard.is_last_layer():
       return h.view(B, L, D)
     xn = A.rmsnorm(h, P["norm"], c.rms_norm_eps)
+    if not logits:
+      return xn.view(B, L, D)
     head = P["lm_head"] if "lm_head" in P else P["embed"]
+    tw = self.tw.get(self.head_name)
+    if tw is not None and not torch.is_grad_enabled():
+      from ..ops.linear import linear
+      return linear(xn.contiguous(), tw.ws).view(B, L, -1)
     return (xn @ head.t()).view(B, L, -1)
 
   def _mla(self, xn: torch.Tensor, i: int, pos: torch.Tensor, B: int, L: int) -> torch.Tensor:
@@ -223,6 +258,13 @@ class ShardTrainer:
     """x @ W.T (+ h) for projection `name`: fused gradient accumulation on the GPU while training."""
     w = self.params[name]
     acc = self.acc.get(name)
+    tw = self.tw.get(name)
+    if tw is not None and (acc is not None or not torch.is_grad_enabled()):
+      if torch.is_grad_enabled():
+        return A.linear_own(x, w, tw, acc, h)
+      from ..ops.linear import linear
+      x = x if (x.stride(1) == 1 and x.stride(0) % 8 == 0) else x.contiguous()
+      return linear(x, tw.ws, residual=h.contiguous(), epi="resid") if h is not None else linear(x, tw.ws)
     if acc is not None and torch.is_grad_enabled():
       return A.linear_acc(x, w, acc, h)
     return _resid_mm(h, x, w) if h is not None else x @ w.t()
@@ -260,6 +302,17 @@ class ShardTrainer:
     w = torch.full((B * L,), 1.0 / denom, device=self.device, dtype=torch.float32)
     return A.cross_entropy(logits.reshape(B * L, V), tgt, w), n
 
+  def head_loss(self, xn: torch.Tensor, target, lengths, denom: float) -> torch.Tensor:
+    """The fused LM head + chunked CE of loss_of, from the final normed hidden state [B, L, D]."""
+    B, L, D = xn.shape
+    y = self._to(target, torch.int64)
+    ln = self._to(lengths, torch.int64).view(-1)
+    mask = torch.arange(L, device=self.device)[None, :] < ln[:, None]
+    tgt = torch.where(mask, y, torch.full_like(y, -100)).view(-1).to(torch.int32)
+    w = torch.full((B * L,), 1.0 / denom, device=self.device, dtype=torch.float32)
+    name = self.head_name
+    return A.lm_head_ce(xn.reshape(B * L, D), self.params[name], self.tw[name], tgt, w, CE_CHUNK)
+
   # ------------------------------------------------------------------ accumulate / apply
   # (pipeline schedules: forward every micro-batch, backward every micro-batch, then one optimizer
   # step; see parallel/pipeline_train.py)
@@ -276,7 +329,7 @@ class ShardTrainer:
     if not self.shard.is_first_layer():
       leaf = x.to(torch.bfloat16).detach().requires_grad_(True)
       x = leaf
-    return leaf, self.forward(x)
+    return leaf, self.forward(x, logits=not self.fused_head())
 
   def backward_accumulate(self, leaf, out, grad_out=None, target=None, length=None,
                           denom: Optional[float] = None) -> Tuple[Optional[torch.Tensor], Optional[torch.Tensor]]:
@@ -284,7 +337,12 @@ class ShardTrainer:
     as a device scalar, no sync); other stages: out.backward(grad_out).  Returns (loss, grad wrt input)."""
     loss = None
     if grad_out is None:
-      loss, _ = self.loss_of(out, target, length, denom)
+      if self.fused_head():  # forward_train returned the final normed hidden state
+        if denom is None:
+          denom = float(max(int((self._to(length, torch.int64)).sum().item()), 1))
+        loss = self.head_loss(out, target, length, denom)
+      else:
+        loss, _ = self.loss_of(out, target, length, denom)
       loss.backward()
       loss = loss.detach()
     else:
@@ -349,6 +407,8 @@ class ShardTrainer:
         bc1, bc2 = 1 - b1 ** self.step_count, 1 - b2 ** self.step_count
         p.mul_(1 - self.lr * self.wd).addcdiv_(m / bc1, (v / bc2).sqrt_().add_(self.eps), value=-self.lr)
         pb.data.copy_(p.to(pb.dtype))
+    for t in self.tw.values():
+      t.refresh()
     self.dirty = True
 
   # ------------------------------------------------------------------ write-back
@@ -417,5 +477,7 @@ class ShardTrainer:
         self.m[k].copy_(sd[f"m.{k}"])
         self.v[k].copy_(sd[f"v.{k}"])
         self.params[k].data.copy_(self.master[k].to(torch.bfloat16))
+    for t in self.tw.values():
+      t.refresh()
     if "step" in sd:
       self.step_count = int(sd["step"][0])
