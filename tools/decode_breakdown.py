@@ -1,36 +1,45 @@
-"""Per-kernel time of the last K decode steps in a rocprofv3 kernel trace.  A step ends with one launch of the
-sampling kernel (--marker); the window runs from the (K+1)-th last marker launch to the last, so prefill,
-warmup and the GEMM policy's first-encounter timing runs stay outside.
-  python tools/decode_breakdown.py gpurun_out/<dir>/trace_kernel_trace.csv --steps K [--marker NAME]"""
+"""Per-kernel decode-step breakdown from a rocprofv3 kernel trace of bench.py: the window is the last
+`--steps` decode rounds, delimited by the on-device sampling kernel that ends each round (so warmup
+rounds with GEMM autotuning are excluded).
+
+  python tools/decode_breakdown.py [gpurun_out/prof/<...>_kernel_trace.csv] --steps 3
+"""
 import argparse
 import collections
 import csv
+import glob
+import json
 
 
 def main():
   ap = argparse.ArgumentParser()
-  ap.add_argument("trace")
-  ap.add_argument("--steps", type=int, required=True, help="decode steps in the traced region (warmup + timed)")
-  ap.add_argument("--marker", default="sample", help="substring of the once-per-step kernel that ends a step")
-  ap.add_argument("--top", type=int, default=25)
+  ap.add_argument("trace", nargs="?", default=None)
+  ap.add_argument("--steps", type=int, required=True, help="decode rounds in the trace (warmup + steps)")
+  ap.add_argument("--json", default=None)
   a = ap.parse_args()
-  rows = sorted(csv.DictReader(open(a.trace)), key=lambda r: int(r["Start_Timestamp"]))
-  ends = [int(r["Start_Timestamp"]) for r in rows if a.marker in r["Kernel_Name"]]
-  assert len(ends) > a.steps, f"only {len(ends)} '{a.marker}' launches for {a.steps} steps"
-  lo, hi = ends[-a.steps - 1], ends[-1]
+  path = a.trace or sorted(glob.glob("gpurun_out/prof/**/*kernel_trace.csv", recursive=True))[-1]
+  rows = list(csv.DictReader(open(path)))
+  ends = sorted(int(r["End_Timestamp"]) for r in rows
+                if any(k in r["Kernel_Name"] for k in ("sample_kernel", "sample_stage2", "sample_fast_kernel")))
+  lo, hi = ends[-(a.steps + 1)], ends[-1]
   dec = [r for r in rows if lo < int(r["Start_Timestamp"]) <= hi]
-  wall = (hi - lo) / 1e6 / a.steps
-  tot = collections.Counter()
-  calls = collections.Counter()
+  agg = collections.defaultdict(lambda: [0, 0])
   for r in dec:
-    n = r["Kernel_Name"].split("(")[0][:90]
-    tot[n] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-    calls[n] += 1
-  s = sum(tot.values())
-  print(f"last {a.steps} steps: {len(dec) / a.steps:.0f} kernels/step, {s / 1e6 / a.steps:.3f} ms/step busy, "
-        f"{wall:.3f} ms/step wall")
-  for n, t in tot.most_common(a.top):
-    print(f"{t / 1e6 / a.steps:8.3f} ms/step {100 * t / s:5.1f}%  {calls[n] / a.steps:5.1f}/step  {n}")
+    name = r["Kernel_Name"].split("(")[0][:90]
+    agg[name][0] += 1
+    agg[name][1] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+  tot = sum(v[1] for v in agg.values())
+  span = hi - lo
+  out = {"trace": path, "decode_steps": a.steps, "busy_ms_per_step": tot / a.steps / 1e6,
+         "wall_ms_per_step": span / a.steps / 1e6, "kernels": []}
+  for name, (n, t) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
+    out["kernels"].append({"kernel": name, "calls_per_step": n / a.steps, "ms_per_step": t / a.steps / 1e6,
+                           "pct": 100 * t / tot})
+  print(f"busy {out['busy_ms_per_step']:.2f} ms/step, wall {out['wall_ms_per_step']:.2f} ms/step")
+  for k in out["kernels"][:25]:
+    print(f"{k['ms_per_step']:8.3f} ms {k['pct']:5.1f}%  x{k['calls_per_step']:.0f}  {k['kernel']}")
+  if a.json:
+    json.dump(out, open(a.json, "w"), indent=1)
 
 
 if __name__ == "__main__":
