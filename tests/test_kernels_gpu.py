@@ -826,3 +826,25 @@ def test_own_linear_grads_match_torch(gpu, with_h):
     dw_ref += g.float().t() @ x.float()
   assert w.grad is None
   assert rel_err(acc.buf, dw_ref) < 1e-2
+
+
+@pytest.mark.parametrize("resid", [False, True])
+def test_gemm_kgroup(gpu, resid):
+  """K-grouped GEMM (grouped experts' weight gradients): y[e] (+)= x[:, koff[e]:koff[e+1]] . w[:, ...]^T with
+  64-aligned segments, an empty one included, vs fp32 torch per segment."""
+  from xotorch_support_jetson_amd.ops._ext import require
+  from xotorch_support_jetson_amd.ops.weights_layout import shuffle_for_stream
+  torch.manual_seed(0)
+  M, N = 320, 272
+  segs = [128, 0, 64, 384, 64]
+  K = sum(segs)
+  koff = torch.tensor([0] + list(torch.tensor(segs).cumsum(0)), dtype=torch.int32, device=gpu)
+  x = torch.randn(M, K, device=gpu, dtype=torch.bfloat16)
+  w = torch.randn(N, K, device=gpu, dtype=torch.bfloat16) / 8
+  y0 = torch.randn(len(segs), M, N, device=gpu, dtype=torch.bfloat16)
+  y = y0.clone()
+  require().gemm_kgroup(x, shuffle_for_stream(w), y, koff, resid)
+  for e in range(len(segs)):
+    a, b = int(koff[e]), int(koff[e + 1])
+    ref = x[:, a:b].float() @ w[:, a:b].float().t() + (y0[e].float() if resid else 0)
+    assert rel_err(y[e], ref) < 1e-2 if ref.norm() > 0 else y[e].abs().max() == 0

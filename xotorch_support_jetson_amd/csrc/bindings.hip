@@ -425,6 +425,23 @@ void relayout(const at::Tensor& src, at::Tensor& dst, int64_t mode) {
   XCHECK(rc == 0, "relayout: unsupported shape R=", R, " C=", C, " mode=", mode);
 }
 
+// K-grouped GEMM (grouped experts' weight gradients): y[e] (+)= x[:, koff[e]:koff[e+1]] . w[:, koff[e]:koff[e+1]]^T,
+// x [M, K] row-major bf16, w [N, K] pre-shuffled, y [E, M, N] bf16 contiguous, koff [E+1] int32 (multiples of 64)
+void gemm_kgroup(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const at::Tensor& koff, bool resid) {
+  CHECK_BF16(x);
+  CHECK_BF16(w);
+  CHECK_BF16(y);
+  CHECK_GPU(koff);
+  CHECK_DT(koff, at::kInt);
+  XCHECK(x.dim() == 2 && w.dim() == 2 && y.dim() == 3 && x.stride(1) == 1 && x.stride(0) % 8 == 0, "gemm_kgroup: x");
+  XCHECK(w.is_contiguous() && y.is_contiguous() && koff.is_contiguous(), "gemm_kgroup: layout");
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0), E = y.size(0);
+  XCHECK(w.size(1) == K && y.size(1) == M && y.size(2) == N && koff.numel() == E + 1, "gemm_kgroup: shapes");
+  const int rc = xot::launch_gemm_kgroup(bf(x), (int)x.stride(0), bf(w), bf(y), (int)N, resid, koff.data_ptr<int>(),
+                                         (int)E, (int)M, (int)N, (int)K, cur_stream());
+  XCHECK(rc == 0, "gemm_kgroup: unsupported shape M=", M, " N=", N, " K=", K);
+}
+
 void gemm_batched(const at::Tensor& x, int64_t xbat, int64_t K, const at::Tensor& w, at::Tensor& y, int64_t ybat,
                   int64_t ldy, int64_t M) {
   CHECK_BF16(x);
@@ -898,6 +915,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("sync"), py::arg("epi"), py::arg("cus") = 256);
   m.def("gemm_sk_part_elems", &gemm_sk_part_elems);
   m.def("relayout", &relayout);
+  m.def("gemm_kgroup", &gemm_kgroup);
   m.def("gemm_batched", &gemm_batched, py::arg("x"), py::arg("xbat"), py::arg("K"), py::arg("w"), py::arg("y"),
         py::arg("ybat"), py::arg("ldy"), py::arg("M"));
   m.def("gemm_sk_sync_words", &gemm_sk_sync_words);

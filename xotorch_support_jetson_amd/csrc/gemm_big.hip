@@ -34,6 +34,9 @@ namespace xot {
 // moe_off[e+1] of the expert-sorted slot order; MOE 2 gathers X row moe_gather[slot]); M is the
 // worst-case rows per expert (row tiles past an expert's count exit at once, so the grid is fixed and
 // graph-capturable).  A K split writes fp32 partial slabs ysplit elements apart (summed by the consumer).
+// MOE = 4: K-grouped GEMM (the weight gradients of grouped experts): blockIdx.y = group e multiplies the k
+// range [moe_off[e], moe_off[e+1]) (multiples of BK) of the shared operands X [M, K] and W [N, K] into
+// Y_e = Y + e M ldy (and R_e for the residual epilogue); an empty range stores bias / residual only.
 // PP: two-group ping-pong schedule (BM = BN = 256, 2 x 4 waves, BK = 64, 2 buffers): each 64-deep stage
 // is 4 phases of 16 MFMAs (one 64 x 32 quadrant of the wave's 128 x 64 tile); phase = {fragment reads ->
 // barrier -> MFMAs -> barrier}; the row-half-1 waves run one barrier behind, so on every SIMD one wave's
@@ -54,7 +57,8 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
   static_assert(WM * WN == 8, "8 waves");
   static_assert(BK == 32 || BK == 64, "k stage of 32 or 64");
   static_assert(BM == 128 || BM == 192 || BM == 256, "row tile of 128, 192 or 256");
-  static_assert(MOE == 0 || (!SPLIT && EPI != EPI_RESID), "grouped GEMM: no slab reduce, no residual");
+  static_assert(MOE == 0 || MOE == 4 || (!SPLIT && EPI != EPI_RESID), "grouped GEMM: no slab reduce, no residual");
+  static_assert(MOE != 4 || !SPLIT, "K-grouped GEMM: no K split");
   constexpr int MT = BM / (16 * WM), NT = BN / (16 * WN);
   static_assert(EPI != EPI_SILU || NT % 2 == 0, "SiLU epilogue pairs gate/up n-tiles");
   constexpr int KS = BK / 32;                          // MFMA k-steps (and 1 KB W blocks per row group) per stage
@@ -82,7 +86,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
   const int mt = b % mtiles, nt = (b / mtiles) % ntiles, split = b / (mtiles * ntiles);
   const int m0 = mt * BM, n0 = nt * BN;
   int row0 = 0, Mv = M;  // first output row (slot) and valid rows of this launch's row range
-  if constexpr (MOE != 0) {
+  if constexpr (MOE == 1 || MOE == 2) {
     const int e = blockIdx.y;
     row0 = moe_off[e];
     Mv = moe_off[e + 1] - row0;
@@ -91,7 +95,17 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
     if (ysplit != 0) Yv = reinterpret_cast<float*>(Yv) + (size_t)split * ysplit;
   }
   const int T_all = K / BK;
-  const int t_beg = (int)((long)split * T_all / S), t_end = (int)((long)(split + 1) * T_all / S);
+  int t_beg = (int)((long)split * T_all / S), t_end = (int)((long)(split + 1) * T_all / S);
+  if constexpr (MOE == 4) {
+    const int e = blockIdx.y;
+    t_beg = moe_off[e] / BK;
+    t_end = moe_off[e + 1] / BK;
+    if constexpr (OUT_F32)
+      Yv = reinterpret_cast<float*>(Yv) + (size_t)e * M * ldy;
+    else
+      Yv = reinterpret_cast<uint16_t*>(Yv) + (size_t)e * M * ldy;
+    if (R != nullptr) R += (size_t)e * M * ldr;
+  }
   const int T = t_end - t_beg;
 
   // X LDS image: rows of BK bf16, 16-B slot XOR-swizzled so the 16 lanes of each A-fragment
@@ -427,7 +441,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
 
   // ---- epilogue
   const int rbase = m0 + wm * (MT * 16);
-  if constexpr (MOE != 0) {  // output rows are slots
+  if constexpr (MOE == 1 || MOE == 2) {  // output rows are slots
     if constexpr (OUT_F32)
       Yv = reinterpret_cast<float*>(Yv) + (size_t)row0 * ldy;
     else
@@ -570,6 +584,31 @@ int launch_gemm_big(const uint16_t* X, int ldx, const uint16_t* W, const uint16_
     return out_f32 ? -1 : big_dispatch<EPI_RESID, false>(X, ldx, W, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, bn, S, reduce, s);
   return out_f32 ? big_dispatch<EPI_NONE, true>(X, ldx, W, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, bn, S, reduce, s)
                  : big_dispatch<EPI_NONE, false>(X, ldx, W, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, bn, S, reduce, s);
+}
+
+// ------------------------------------------------------------------------------------ K-grouped (expert dW)
+// Y_e [M, N] (+)= X[:, koff[e]:koff[e+1]] . W[:, koff[e]:koff[e+1]]^T for e < E; X [M, K] row-major, W [N, K]
+// pre-shuffled, koff multiples of 64 (segments padded with zero rows by the caller), resid: Y_e += (in place).
+int launch_gemm_kgroup(const uint16_t* X, int ldx, const uint16_t* W, uint16_t* Y, int ldy, bool resid,
+                       const int* koff, int E, int M, int N, int K, hipStream_t st) {
+  if (M <= 0 || E <= 0 || N <= 0) return 0;
+  if (N % 16 != 0 || K % 128 != 0) return -1;
+  constexpr int SMEM = 2 * (256 + 256) * 64 * 2;
+  const dim3 grid(((M + 255) / 256) * ((N + 255) / 256), E);
+  if (resid) {
+    auto kern = gemm_big_kernel<256, 256, 2, 4, 64, 2, EPI_RESID, false, false, 4, 0, 0, 3, false, 1>;
+    static bool attr = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM) ==
+                       hipSuccess;
+    (void)attr;
+    kern<<<grid, 512, SMEM, st>>>(X, ldx, W, nullptr, Y, ldy, Y, ldy, nullptr, M, N, K, 1, koff, nullptr, 0L);
+  } else {
+    auto kern = gemm_big_kernel<256, 256, 2, 4, 64, 2, EPI_NONE, false, false, 4, 0, 0, 3, false, 1>;
+    static bool attr = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM) ==
+                       hipSuccess;
+    (void)attr;
+    kern<<<grid, 512, SMEM, st>>>(X, ldx, W, nullptr, nullptr, 0, Y, ldy, nullptr, M, N, K, 1, koff, nullptr, 0L);
+  }
+  return 0;
 }
 
 // S fp32 slabs [S][M][N] of a 16-row interleaved gate/up product -> silu(gate) * up [M, N/2] bf16

@@ -54,6 +54,8 @@ long gemm_sk_part_elems();
 int launch_shuffle(const uint16_t* src, long ld, uint16_t* dst, int R, int C, hipStream_t s);
 int launch_shuffle_t(const uint16_t* src, long ld, uint16_t* dst, int R, int C, hipStream_t s);
 int launch_transpose(const uint16_t* src, long ld, uint16_t* dst, int R, int C, hipStream_t s);
+int launch_gemm_kgroup(const uint16_t* X, int ldx, const uint16_t* W, uint16_t* Y, int ldy, bool resid,
+                       const int* koff, int E, int M, int N, int K, hipStream_t st);
 int launch_gemm_batched(const uint16_t* X, int ldx, long xbat, const uint16_t* W, void* Y, int ldy, long ybat,
                         bool out_f32, int B, int M, int N, int K, hipStream_t s);
 long gemm_sk_sync_words(int M, int N);

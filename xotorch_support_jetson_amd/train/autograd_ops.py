@@ -372,6 +372,84 @@ def linear_own(x, w, tw, acc, h=None):
   return OwnLinearFn.apply(x, w, tw, h, acc)
 
 
+class StackWeight:
+  """An expert stack W [E, N, K] in the grouped GEMMs' operand layouts (per expert, refreshed after every
+  optimizer step): ws[e] = shuffle(W[e]) (forward), wts[e] = shuffle(W[e]^T) (input gradient)."""
+
+  def __init__(self, w: torch.Tensor):
+    self.w = w
+    E, N, K = w.shape
+    self.ok = w.is_cuda and N % 128 == 0 and K % 128 == 0
+    if self.ok:
+      self.ws = torch.empty(E, N, K, dtype=torch.bfloat16, device=w.device)
+      self.wts = torch.empty(E, K, N, dtype=torch.bfloat16, device=w.device)
+      self.ws.xot_layout = self.wts.xot_layout = "stream"
+      self.refresh()
+
+  @torch.no_grad()
+  def refresh(self) -> None:
+    if self.ok:
+      w = self.w.detach()
+      for e in range(w.shape[0]):
+        relayout(w[e], 0, self.ws[e])
+        relayout(w[e], 1, self.wts[e])
+
+
+def _grouped(x, w, off, max_rows):
+  """y[rows of expert e] = x[rows] . w[e]^T over the padded slot layout (csrc: gemm_moe; gemm_big tiles when
+  the output width allows, else the weight-streaming kernel)."""
+  E, N, K = w.shape
+  y = torch.empty(x.shape[0], N, dtype=torch.bfloat16, device=x.device)
+  bm = 256 if N % 256 == 0 else 0
+  require().gemm_moe(x, w, y, off, None, 0, max_rows, True, 1, bm)
+  return y
+
+
+class GroupedExpertsFn(torch.autograd.Function):
+  """The routed experts of one MoE layer over a padded slot layout, all on the kernel library and without
+  a host sync: xs [P, D] holds every (token, choice) row grouped by expert, expert e's segment starting
+  at poff[e] (a multiple of 64, zero rows in the padding).  Forward gate|up (gemm_moe) -> SiLU*mul ->
+  down (gemm_moe).  Backward: input gradients through the per-expert transposed weights (gemm_moe), and
+  the weight gradients dW_e = dY_e^T X_e of every expert at once by the K-grouped GEMM (gemm_kgroup over
+  the transposed / shuffled-transposed slot arrays), accumulated straight into the stacks' GradAcc
+  buffers (plain store on the first micro-batch of a step, in place after)."""
+
+  @staticmethod
+  def forward(ctx, xs, poff, max_rows, sgu, sdown, agu, adown):
+    gu = _grouped(xs, sgu.ws, poff, max_rows)  # [P, 2F]
+    act = torch.empty(xs.shape[0], gu.shape[1] // 2, dtype=torch.bfloat16, device=xs.device)
+    require().silu_mul(gu, act, False)
+    y = _grouped(act, sdown.ws, poff, max_rows)  # [P, D]
+    ctx.save_for_backward(xs, poff, gu, act)
+    ctx.max_rows, ctx.sgu, ctx.sdown, ctx.agu, ctx.adown = max_rows, sgu, sdown, agu, adown
+    return y
+
+  @staticmethod
+  def backward(ctx, dy):
+    xs, poff, gu, act = ctx.saved_tensors
+    dy = dy.contiguous()
+    C = require()
+    d_act = _grouped(dy, ctx.sdown.wts, poff, ctx.max_rows)  # [P, F]
+    _kgroup_acc(relayout(dy, 2), relayout(act, 1), ctx.adown, poff)  # dW_down[e] = dy_e^T act_e
+    d_gu = torch.empty_like(gu)
+    C.silu_mul_bwd(gu, d_act, d_gu)
+    dxs = _grouped(d_gu, ctx.sgu.wts, poff, ctx.max_rows)  # [P, D]
+    _kgroup_acc(relayout(d_gu, 2), relayout(xs, 1), ctx.agu, poff)  # dW_gu[e] = d_gu_e^T xs_e
+    return dxs, None, None, None, None, None, None
+
+
+def _kgroup_acc(at, bts, acc, poff):
+  fresh = acc.fresh
+  require().gemm_kgroup(at, bts, acc.buf, poff, not fresh)
+  acc.fresh = False
+  if acc.cb is not None:
+    acc.cb()
+
+
+def grouped_experts(xs, poff, max_rows, sgu, sdown, agu, adown):
+  return GroupedExpertsFn.apply(xs, poff, max_rows, sgu, sdown, agu, adown)
+
+
 class LmHeadCEFn(torch.autograd.Function):
   """sum_t w_t CE(xn_t . head^T, y_t) without materialising [T, V] logits: row chunks of `chunk`
   tokens; per chunk the fp32 logits come from the own GEMM, ce_fwd / ce_bwd give the loss and dlogits (bf16),

@@ -100,14 +100,13 @@ class ShardTrainer:
       for k in self.params:
         if k.split(".")[-1] in ("qkv", "o", "gu", "down", "egu", "edown", "qb", "kvb", "sh_gu", "sh_down"):
           self.acc[k] = A.GradAcc(k, self.params[k])
-    # own-GEMM operand layouts of the 2-D projections (refreshed after each optimizer step)
-    self.tw: Dict[str, A.TrainWeight] = {}
+    # own-GEMM operand layouts of the 2-D projections and expert stacks (refreshed after each optimizer step)
+    self.tw: Dict[str, object] = {}
     if self.device.type == "cuda" and OWN_GEMM:
       for k in self.acc:
-        if self.params[k].dim() == 2:
-          t = A.TrainWeight(self.params[k])
-          if t.ok:
-            self.tw[k] = t
+        t = A.TrainWeight(self.params[k]) if self.params[k].dim() == 2 else A.StackWeight(self.params[k])
+        if t.ok:
+          self.tw[k] = t
     # fused LM head + chunked CE on the last stage (A.LmHeadCEFn): forward_train hands back the final normed
     # hidden state and backward_accumulate computes the loss from it without [T, V] logits
     self.head_name = None
@@ -229,6 +228,12 @@ class ShardTrainer:
     c, P = self.c, self.params
     logits = xn.float() @ P[f"{i}.router"].float().t()  # [T, E]
     topw, topi = self._route(logits, i)
+    sgu, sdown = self.tw.get(f"{i}.egu"), self.tw.get(f"{i}.edown")
+    if sgu is not None and sdown is not None and f"{i}.egu" in self.acc and f"{i}.edown" in self.acc:
+      out = self._moe_grouped(xn, i, topw, topi, sgu, sdown)
+      if f"{i}.sh_gu" in P:
+        out = out + self._mm(A.silu_mul(self._mm(xn, f"{i}.sh_gu").contiguous()), f"{i}.sh_down").float()
+      return out.to(xn.dtype)
     # per-expert views, taken once per layer: indexing egu[e] per expert would zero-fill and add a full
     # [E, 2F, D] gradient for every expert; on the GPU the routed experts' grads go straight into the
     # stack's accumulation buffer (A.StackAccFn)
@@ -253,6 +258,31 @@ class ShardTrainer:
     if f"{i}.sh_gu" in P:
       out = out + self._mm(A.silu_mul(self._mm(xn, f"{i}.sh_gu").contiguous()), f"{i}.sh_down").float()
     return out.to(xn.dtype)
+
+  def _moe_grouped(self, xn: torch.Tensor, i: int, topw: torch.Tensor, topi: torch.Tensor, sgu, sdown) -> torch.Tensor:
+    """Routed experts on the grouped kernels with no host sync (A.GroupedExpertsFn): the (token, choice)
+    rows are scattered into a slot array where expert e's rows start at poff[e], a multiple of 64 (zero
+    rows pad each segment; the array is sized for the worst case T k + 63 E, so no count leaves the
+    device), and the weighted expert outputs are gathered back and summed per token in fp32."""
+    c = self.c
+    T, D = xn.shape
+    k, E = c.num_experts_per_tok, c.num_experts
+    dev = xn.device
+    flat = topi.reshape(-1)
+    counts = torch.bincount(flat, minlength=E)
+    start = torch.cumsum(counts, 0) - counts  # first sorted slot of each expert
+    pad = (counts + 63) // 64 * 64
+    poff = torch.zeros(E + 1, dtype=torch.int32, device=dev)
+    poff[1:] = torch.cumsum(pad, 0).to(torch.int32)
+    order = torch.argsort(flat, stable=True)
+    se = flat[order]
+    dest = poff[se].long() + torch.arange(T * k, device=dev) - start[se]
+    tok = order // k
+    P = -(-(T * k + 63 * E) // 128) * 128
+    xs = torch.zeros(P, D, dtype=xn.dtype, device=dev).index_copy(0, dest, xn.index_select(0, tok))
+    y = A.grouped_experts(xs, poff, -(-T // 64) * 64, sgu, sdown, self.acc[f"{i}.egu"], self.acc[f"{i}.edown"])
+    y = y.index_select(0, dest).float() * topw.reshape(-1)[order].unsqueeze(1)
+    return torch.zeros(T, D, device=dev, dtype=torch.float32).index_add(0, tok, y)
 
   def _mm(self, x: torch.Tensor, name: str, h: Optional[torch.Tensor] = None) -> torch.Tensor:
     """x @ W.T (+ h) for projection `name`: fused gradient accumulation on the GPU while training."""
