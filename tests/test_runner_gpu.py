@@ -168,8 +168,9 @@ def test_fused_grad_accumulation_values(gpu, name):
     scale = (gf[k].norm() / (ref.norm() + 1e-12)).item()
     # the fused run's projections are the own MFMA GEMMs, the plain run's torch.matmul: bf16 rounding of the
     # activations differs, and the router gradient (softmax Jacobian: differences of near-equal terms)
-    # amplifies it; a doubled / dropped micro-batch still moves `scale` by >= 1/3
-    tol = 0.1 if k.endswith("router") else 0.05
+    # amplifies it (index_add scatter order is not deterministic either); a doubled / dropped micro-batch still
+    # moves `scale` by >= 1/3
+    tol = 0.2 if k.endswith("router") else 0.05
     assert rel < tol and abs(scale - 1) < 0.02, (k, rel, scale)
 
 
