@@ -67,7 +67,8 @@ int main(int argc, char** argv) {
   const int only = argc > 4 ? atoi(argv[4]) : -1;
   const int epi = argc > 5 ? atoi(argv[5]) : EPI_SILU;
   const size_t wsz = (size_t)N * K;
-  const int nc = (int)std::max<size_t>(2, (1ull << 30) / (wsz * 2) + 1);
+  // weight copies rotated per call (HBM-cold); argv[6] = 1 keeps one copy (cache-resident when it fits)
+  const int nc = argc > 6 ? atoi(argv[6]) : (int)std::max<size_t>(2, (1ull << 30) / (wsz * 2) + 1);
   uint16_t *X, *W, *Y;
   CK(hipMalloc(&X, (size_t)M * K * 2));
   CK(hipMalloc(&W, wsz * 2 * nc));
@@ -82,15 +83,13 @@ int main(int argc, char** argv) {
   std::vector<Variant> vs;
   if (epi == EPI_SILU) {
     vs.push_back({"pp nt(B)     ", launch_v<256, 2, 64, 2, 0, 3, false, 1, EPI_SILU>});
-    vs.push_back({"w4 regs      ", launch_w4<EPI_SILU, 0>});
-    vs.push_back({"w4 W-dma     ", launch_w4<EPI_SILU, 1>});
-    vs.push_back({"w4 all-dma   ", launch_w4<EPI_SILU, 2>});
+    vs.push_back({"base 256     ", launch_v<256, 2, 64, 2, 0, 3, false, 0, EPI_SILU>});
+    if (N % 224 == 0) vs.push_back({"base 224     ", launch_v<224, 4, 64, 2, 0, 3, false, 0, EPI_SILU>});
     vs.push_back({"stream-K     ", launch_sk<EPI_SILU>});
   } else {
     vs.push_back({"pp nt(B)     ", launch_v<256, 2, 64, 2, 0, 3, false, 1, EPI_NONE>});
-    vs.push_back({"w4 regs      ", launch_w4<EPI_NONE, 0>});
-    vs.push_back({"w4 W-dma     ", launch_w4<EPI_NONE, 1>});
-    vs.push_back({"w4 all-dma   ", launch_w4<EPI_NONE, 2>});
+    vs.push_back({"base 256     ", launch_v<256, 2, 64, 2, 0, 3, false, 0, EPI_NONE>});
+    if (N % 224 == 0) vs.push_back({"base 224     ", launch_v<224, 4, 64, 2, 0, 3, false, 0, EPI_NONE>});
     vs.push_back({"stream-K     ", launch_sk<EPI_NONE>});
   }
   {  // every variant must produce the first variant's output (same tile math; k order identical)

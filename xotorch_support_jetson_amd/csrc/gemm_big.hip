@@ -25,6 +25,8 @@
 #include "gemm_common.h"
 #include "kernels.h"
 
+#include <type_traits>
+
 namespace xot {
 
 
@@ -60,13 +62,20 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
   static_assert(MOE == 0 || MOE == 4 || (!SPLIT && EPI != EPI_RESID), "grouped GEMM: no slab reduce, no residual");
   static_assert(MOE != 4 || !SPLIT, "K-grouped GEMM: no K split");
   constexpr int MT = BM / (16 * WM), NT = BN / (16 * WN);
-  static_assert(EPI != EPI_SILU || NT % 2 == 0, "SiLU epilogue pairs gate/up n-tiles");
+  // odd NT (BN = 224: 7 row groups per wave): the gate/up pair that straddles two waves of a row is
+  // joined through LDS in the epilogue
+  static_assert(EPI != EPI_SILU || NT % 2 == 0 || (PP == 0 && MOE == 0), "SiLU epilogue pairs gate/up n-tiles");
   constexpr int KS = BK / 32;                          // MFMA k-steps (and 1 KB W blocks per row group) per stage
   constexpr int SPR = BK / 8;                          // 16-B slots per X row in LDS
   constexpr int A_ELEMS = BM * BK, B_ELEMS = BN * BK;  // bf16 elements per stage
   constexpr int STAGE = A_ELEMS + B_ELEMS;
   constexpr int A_INSTR = A_ELEMS * 2 / 1024 / 8;      // 1 KB LDS-DMA instructions per wave per stage
-  constexpr int B_INSTR = B_ELEMS * 2 / 1024 / 8;
+  // W instructions per stage: NBI in all; with NBI % 8 != 0 (BN = 224: 28) waves below NBI % 8 issue one
+  // more than the others (instruction q = 8 i + wave), and each wave retires its own count
+  constexpr int NBI = B_ELEMS * 2 / 1024;
+  constexpr int B_INSTR = (NBI + 7) / 8;
+  constexpr bool B_UNEVEN = NBI % 8 != 0;
+  static_assert(!B_UNEVEN || PP == 0, "uneven W instruction split: base schedule only");
   constexpr int NI = A_INSTR + B_INSTR;
   constexpr int PD = NBUF - 1;                         // stages in flight ahead of the one computed
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
@@ -135,12 +144,15 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
   // W: instruction q = B_INSTR*w + i copies 1 KB block q % KS of row group q / KS for this stage.
   const size_t kchunks = K / 128;
   const uint16_t* bsrc[B_INSTR];
+  auto bq = [&](int i) { return B_UNEVEN ? 8 * i + wave : B_INSTR * wave + i; };
 #pragma unroll
   for (int i = 0; i < B_INSTR; ++i) {
-    const int q = B_INSTR * wave + i;
+    const int q = min(bq(i), NBI - 1);
     const int grp = min((n0 >> 4) + q / KS, N / 16 - 1);  // groups past N re-read the last one; outputs masked
     bsrc[i] = W + ((size_t)grp * kchunks) * 2048 + (q % KS) * 512 + lane * 8;
   }
+  // wave-uniform: does this wave issue the last (partial) round of W instructions
+  const bool b_full = !B_UNEVEN || __builtin_amdgcn_readfirstlane(wave) < NBI % 8;
 
   auto issue = [&](int t, int buf) {  // stage t (absolute k step) -> LDS buffer buf
     uint16_t* As = smem + buf * STAGE;
@@ -150,7 +162,8 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
 #pragma unroll
     for (int i = 0; i < A_INSTR; ++i) glds16<AUXA>(asrc[i] + k0, As + (A_INSTR * wave + i) * 512);
 #pragma unroll
-    for (int i = 0; i < B_INSTR; ++i) glds16<AUXB>(bsrc[i] + woff, Bs + (B_INSTR * wave + i) * 512);
+    for (int i = 0; i < B_INSTR; ++i)
+      if (i < B_INSTR - 1 || b_full) glds16<AUXB>(bsrc[i] + woff, Bs + bq(i) * 512);
   };
 
   f32x4 acc[MT][NT];
@@ -205,11 +218,16 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
     asm volatile("" ::: "memory");
   };
   // wait until at most k younger stages of this wave are still in flight
-  auto wait_stages = [](int k) {
-    if (PD >= 4 && k >= 3) wait_vm<(PD >= 4 ? 3 * NI : 0)>();
-    else if (PD >= 3 && k >= 2) wait_vm<(PD >= 3 ? 2 * NI : 0)>();
-    else if (PD >= 2 && k >= 1) wait_vm<(PD >= 2 ? NI : 0)>();
+  auto wait_stages_n = [](int k, auto ni) {
+    constexpr int n = decltype(ni)::value;
+    if (PD >= 4 && k >= 3) wait_vm<(PD >= 4 ? 3 * n : 0)>();
+    else if (PD >= 3 && k >= 2) wait_vm<(PD >= 3 ? 2 * n : 0)>();
+    else if (PD >= 2 && k >= 1) wait_vm<(PD >= 2 ? n : 0)>();
     else wait_vm<0>();
+  };
+  auto wait_stages = [&](int k) {
+    if (b_full) wait_stages_n(k, std::integral_constant<int, NI>{});
+    else wait_stages_n(k, std::integral_constant<int, (B_UNEVEN ? NI - 1 : NI)>{});
   };
 
   if constexpr (PP == 2) {
@@ -462,14 +480,14 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
         }
       }
   } else if constexpr (EPI == EPI_SILU) {
-#pragma unroll
-    for (int p = 0; p < NT / 2; ++p) {  // (gate tile 2p, up tile 2p+1) -> 16 output columns
-      if (cbase + 32 * p >= N) break;
-      const int col = (cbase >> 1) + 16 * p + c;
+    // (gate group at column gcol, up group at gcol + 16) -> 16 output columns starting at gcol / 2
+    auto store_pair = [&](int gcol, auto gate, auto up) {
+      if (gcol >= N) return;
+      const int col = (gcol >> 1) + c;
       float bg = 0.f, bu = 0.f;
       if (bias != nullptr) {
-        bg = bf2f(bias[cbase + 32 * p + c]);
-        bu = bf2f(bias[cbase + 32 * p + 16 + c]);
+        bg = bf2f(bias[gcol + c]);
+        bu = bf2f(bias[gcol + 16 + c]);
       }
 #pragma unroll
       for (int i = 0; i < MT; ++i)
@@ -477,13 +495,42 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
         for (int r = 0; r < 4; ++r) {
           const int m = rbase + 16 * i + 4 * g + r;
           if (m < Mv) {
-            const float v = silu(acc[i][2 * p][r] + bg) * (acc[i][2 * p + 1][r] + bu);
+            const float v = silu(gate(i)[r] + bg) * (up(i)[r] + bu);
             if constexpr (OUT_F32)
               reinterpret_cast<float*>(Yv)[(size_t)m * ldy + col] = v;
             else
               reinterpret_cast<uint16_t*>(Yv)[(size_t)m * ldy + col] = f2bf(v);
           }
         }
+    };
+    if constexpr (NT % 2 == 0) {
+#pragma unroll
+      for (int p = 0; p < NT / 2; ++p)  // (gate tile 2p, up tile 2p+1)
+        store_pair(cbase + 32 * p, [&](int i) { return acc[i][2 * p]; }, [&](int i) { return acc[i][2 * p + 1]; });
+    } else {
+      // odd NT, 2 wave columns: wave column 0 holds pairs (0,1) .. and the GATE of the straddling pair in
+      // its last tile; wave column 1 holds that pair's UP in its tile 0, then pairs (1,2) ..  The up tile
+      // crosses through LDS (the stage buffers are idle: the k loop ended on a drained barrier).
+      static_assert(WN == 2 && MOE == 0 && !SPLIT, "odd NT: two wave columns, plain GEMM");
+      float* xch = reinterpret_cast<float*>(smem);
+      const int wcol = __builtin_amdgcn_readfirstlane(wn);
+      if (wcol == 1) {
+#pragma unroll
+        for (int i = 0; i < MT; ++i) *reinterpret_cast<f32x4*>(xch + ((wm * MT + i) * 64 + lane) * 4) = acc[i][0];
+      }
+      barrier();
+      if (wcol == 0) {
+#pragma unroll
+        for (int p = 0; p < NT / 2; ++p)
+          store_pair(cbase + 32 * p, [&](int i) { return acc[i][2 * p]; }, [&](int i) { return acc[i][2 * p + 1]; });
+        store_pair(cbase + 16 * (NT - 1), [&](int i) { return acc[i][NT - 1]; },
+                   [&](int i) { return *reinterpret_cast<const f32x4*>(xch + ((wm * MT + i) * 64 + lane) * 4); });
+      } else {
+#pragma unroll
+        for (int p = 0; p < NT / 2; ++p)
+          store_pair(cbase + 16 + 32 * p, [&](int i) { return acc[i][1 + 2 * p]; },
+                     [&](int i) { return acc[i][2 + 2 * p]; });
+      }
     }
   } else {
 #pragma unroll
@@ -565,6 +612,8 @@ static int big_dispatch(const uint16_t* X, int ldx, const uint16_t* W, const uin
     big_launch<256, 256, 2, 4, 64, 2, EPI, F32, 2>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, S, reduce, st);
   else if (bn == 128)
     big_launch<256, 128, 4, 2, 64, 3, EPI, F32>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, S, reduce, st);
+  else if (bn == 224)  // 256 x 224 tiles: 7 row groups per wave (gate/up N = 57344 -> exactly 256 column tiles)
+    big_launch<256, 224, 4, 2, 64, 2, EPI, F32>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, S, reduce, st);
   else
     return -1;
   return 0;
@@ -574,7 +623,7 @@ int launch_gemm_big(const uint16_t* X, int ldx, const uint16_t* W, const uint16_
                     void* Y, int ldy, bool out_f32, int epi, float* ws, long ws_elems, int M, int N, int K, int bn,
                     int S, bool reduce, hipStream_t s) {
   if (M <= 0) return 0;
-  if ((bn != 128 && bn != 256 && bn != 1256 && bn != 2256) || N % 16 != 0 || K % 128 != 0 || S < 1 || S > K / 64) return -1;
+  if ((bn != 128 && bn != 224 && bn != 256 && bn != 1256 && bn != 2256) || N % 16 != 0 || K % 128 != 0 || S < 1 || S > K / 64) return -1;
   if (S > 1 && (ws == nullptr || ws_elems < (long)S * M * N)) return -1;
   if (epi == EPI_SILU && N % 32 != 0) return -1;
   if (epi == EPI_SILU)
