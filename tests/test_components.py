@@ -351,3 +351,19 @@ def test_gemm_policy_table_persists(tmp_path, monkeypatch):
   assert L.GemmPolicy()._lookup(key) is None  # a corrupt table is ignored
   monkeypatch.setenv("XOT_GEMM_TABLE", "off")
   assert L._default_table_path() is None
+
+
+def test_gemm_row_tiles_for_unaligned_batches():
+  """Decode batches between the 256-row multiples get shorter row tiles (no 32+ padding rows per tile) as
+  extra timed candidates, and their tuning keys no longer collapse onto the next power of two."""
+  from xotorch_support_jetson_amd.ops import linear as L
+  assert [L.big_row_tile(m) for m in (1, 256, 300, 320, 384, 448, 480, 512, 576, 700)] == \
+      [160, 256, 160, 160, 192, 224, 256, 256, 192, 256]
+  assert [L._m_bucket(m) for m in (1, 200, 256, 300, 448, 512, 1000, 1500, 5000)] == \
+      [1, 256, 256, 320, 448, 512, 1024, 2048, 8192]
+  cands = L.GemmPolicy._big_cands(448, 8192, 8192)
+  assert ("big", 2240256, 1) in cands and ("big", 2240128, 2) in cands
+  assert all(L.tile_rows(c[1]) == 256 for c in L.GemmPolicy._big_cands(512, 8192, 8192) if c[0] == "big")
+  assert L.tile_width(2240128) == 128 and L.tile_rows(2240128) == 224 and L.tile_rows(1256) == 256
+  h = L.GemmPolicy._heuristic(384, 57344, L.GemmPolicy._big_cands(384, 57344, 8192))
+  assert h[0] == "big", h  # (untuned fallback; the timed choice decides between 256- and 192-row tiles)

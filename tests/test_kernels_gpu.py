@@ -491,7 +491,8 @@ def test_gemm_stream_odd_chunks(gpu, M, Kd, epi):
                                            ("silu", 128, 1), ("none", 256, 3), ("resid", 128, 2), ("silu", 256, 5),
                                            ("none", 1256, 1), ("resid", 1256, 1), ("silu", 1256, 1), ("none", 1256, 3),
                                            ("resid", 1256, 4), ("none", 224, 1), ("silu", 224, 1), ("resid", 224, 2),
-                                           ("silu", 224, 3)])
+                                           ("silu", 224, 3), ("none", 2240256, 1), ("silu", 1920256, 1),
+                                           ("resid", 1600128, 2), ("silu", 2240128, 1), ("none", 1920128, 3)])
 def test_gemm_big(gpu, M, epi, bn, splits):
   """Large-M LDS-DMA GEMM on the pre-shuffled layout vs the fp32 reference: masked row tiles, both
   column tilings, uneven split-K ranges, every epilogue, fp32 and bf16 outputs."""
@@ -522,7 +523,7 @@ def test_gemm_big(gpu, M, epi, bn, splits):
 @pytest.mark.parametrize("N", [3648, 1088, 320])
 @pytest.mark.parametrize("epi,bn,splits", [("none", 256, 1), ("none", 128, 1), ("none", 1256, 1), ("resid", 256, 1),
                                            ("silu", 128, 1), ("none", 256, 3), ("resid", 1256, 2), ("silu", 224, 1),
-                                           ("none", 224, 1)])
+                                           ("none", 224, 1), ("resid", 1600256, 1), ("silu", 2240128, 2)])
 def test_gemm_big_column_tail(gpu, N, epi, bn, splits):
   """N not a multiple of the column tile (DeepSeek-V2-Lite's fused A projection is 3648 wide): the last
   column tile re-reads the last weight row group and masks its stores -- columns past N stay untouched."""
@@ -559,7 +560,8 @@ def test_gemm_big_exact_layout(gpu):
   w = torch.randint(-3, 4, (N, Kd), generator=g).to(torch.bfloat16).to(gpu)
   y = torch.empty(M, N, device=gpu, dtype=torch.float32)
   ref = x.float() @ w.float().t()
-  for bn in (256, 128, 1256, 224):  # 1256: ping-pong schedule of the 256 x 256 tile; 224: odd row groups per wave
+  # 1256: ping-pong schedule of the 256 x 256 tile; 224: odd row groups per wave; + 10000 x BM: short row tiles
+  for bn in (256, 128, 1256, 224, 2240256, 1600128, 1920256):
     y.zero_()
     require().gemm_big(x, shuffle_for_stream(w), y, None, None, None, 0, bn, 1)
     assert torch.equal(y, ref), bn

@@ -25,8 +25,6 @@
 #include "gemm_common.h"
 #include "kernels.h"
 
-#include <type_traits>
-
 namespace xot {
 
 
@@ -58,7 +56,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
                                                           long ysplit = 0) {
   static_assert(WM * WN == 8, "8 waves");
   static_assert(BK == 32 || BK == 64, "k stage of 32 or 64");
-  static_assert(BM == 128 || BM == 192 || BM == 256, "row tile of 128, 192 or 256");
+  static_assert(BM % (16 * WM) == 0 && BM >= 128 && BM <= 256, "row tile of 128 .. 256 rows");
   static_assert(MOE == 0 || MOE == 4 || (!SPLIT && EPI != EPI_RESID), "grouped GEMM: no slab reduce, no residual");
   static_assert(MOE != 4 || !SPLIT, "K-grouped GEMM: no K split");
   constexpr int MT = BM / (16 * WM), NT = BN / (16 * WN);
@@ -69,13 +67,13 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
   constexpr int SPR = BK / 8;                          // 16-B slots per X row in LDS
   constexpr int A_ELEMS = BM * BK, B_ELEMS = BN * BK;  // bf16 elements per stage
   constexpr int STAGE = A_ELEMS + B_ELEMS;
-  constexpr int A_INSTR = A_ELEMS * 2 / 1024 / 8;      // 1 KB LDS-DMA instructions per wave per stage
-  // W instructions per stage: NBI in all; with NBI % 8 != 0 (BN = 224: 28) waves below NBI % 8 issue one
-  // more than the others (instruction q = 8 i + wave), and each wave retires its own count
-  constexpr int NBI = B_ELEMS * 2 / 1024;
-  constexpr int B_INSTR = (NBI + 7) / 8;
-  constexpr bool B_UNEVEN = NBI % 8 != 0;
-  static_assert(!B_UNEVEN || PP == 0, "uneven W instruction split: base schedule only");
+  // 1 KB LDS-DMA instructions per stage: NAI (X) and NBI (W) in all, A_INSTR / B_INSTR per wave.  When a
+  // count is not a multiple of 8 (BM = 224: 28 X instructions; BN = 224: 28 W instructions) the waves below
+  // count % 8 issue one more than the others (instruction q = 8 i + wave) and each wave retires its own count.
+  constexpr int NAI = A_ELEMS * 2 / 1024, NBI = B_ELEMS * 2 / 1024;
+  constexpr int A_INSTR = (NAI + 7) / 8, B_INSTR = (NBI + 7) / 8;
+  constexpr bool A_UNEVEN = NAI % 8 != 0, B_UNEVEN = NBI % 8 != 0;
+  static_assert(!(A_UNEVEN || B_UNEVEN) || PP == 0, "uneven instruction split: base schedule only");
   constexpr int NI = A_INSTR + B_INSTR;
   constexpr int PD = NBUF - 1;                         // stages in flight ahead of the one computed
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
@@ -132,9 +130,10 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
   // X: instruction i of wave w covers rows (1024 / (2*BK)) * (A_INSTR*w + i) .. ; lane -> row +lane/SPR,
   // physical slot lane%SPR holding logical slot (lane%SPR) ^ aswz(row).
   const uint16_t* asrc[A_INSTR];
+  auto aq = [&](int i) { return A_UNEVEN ? 8 * i + wave : A_INSTR * wave + i; };
 #pragma unroll
   for (int i = 0; i < A_INSTR; ++i) {
-    const int row = (64 / SPR) * (A_INSTR * wave + i) + lane / SPR;
+    const int row = (64 / SPR) * min(aq(i), NAI - 1) + lane / SPR;
     const int slot = (lane % SPR) ^ aswz(row);
     int grow = min(m0 + row, Mv - 1);  // rows past the end load valid memory; their outputs are masked
     if constexpr (MOE == 1) grow += row0;
@@ -151,8 +150,9 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
     const int grp = min((n0 >> 4) + q / KS, N / 16 - 1);  // groups past N re-read the last one; outputs masked
     bsrc[i] = W + ((size_t)grp * kchunks) * 2048 + (q % KS) * 512 + lane * 8;
   }
-  // wave-uniform: does this wave issue the last (partial) round of W instructions
-  const bool b_full = !B_UNEVEN || __builtin_amdgcn_readfirstlane(wave) < NBI % 8;
+  // this wave's LDS-DMA instructions per stage (wave-uniform)
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  const int ni_w = NI - (A_UNEVEN && wave_u >= NAI % 8 ? 1 : 0) - (B_UNEVEN && wave_u >= NBI % 8 ? 1 : 0);
 
   auto issue = [&](int t, int buf) {  // stage t (absolute k step) -> LDS buffer buf
     uint16_t* As = smem + buf * STAGE;
@@ -160,10 +160,11 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
     const int k0 = t * BK;
     const size_t woff = (size_t)(k0 >> 7) * 2048 + ((k0 & 127) >> 5) * 512;
 #pragma unroll
-    for (int i = 0; i < A_INSTR; ++i) glds16<AUXA>(asrc[i] + k0, As + (A_INSTR * wave + i) * 512);
+    for (int i = 0; i < A_INSTR; ++i)
+      if (!A_UNEVEN || aq(i) < NAI) glds16<AUXA>(asrc[i] + k0, As + aq(i) * 512);
 #pragma unroll
     for (int i = 0; i < B_INSTR; ++i)
-      if (i < B_INSTR - 1 || b_full) glds16<AUXB>(bsrc[i] + woff, Bs + bq(i) * 512);
+      if (!B_UNEVEN || bq(i) < NBI) glds16<AUXB>(bsrc[i] + woff, Bs + bq(i) * 512);
   };
 
   f32x4 acc[MT][NT];
@@ -218,16 +219,15 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
     asm volatile("" ::: "memory");
   };
   // wait until at most k younger stages of this wave are still in flight
-  auto wait_stages_n = [](int k, auto ni) {
-    constexpr int n = decltype(ni)::value;
-    if (PD >= 4 && k >= 3) wait_vm<(PD >= 4 ? 3 * n : 0)>();
-    else if (PD >= 3 && k >= 2) wait_vm<(PD >= 3 ? 2 * n : 0)>();
-    else if (PD >= 2 && k >= 1) wait_vm<(PD >= 2 ? n : 0)>();
-    else wait_vm<0>();
-  };
   auto wait_stages = [&](int k) {
-    if (b_full) wait_stages_n(k, std::integral_constant<int, NI>{});
-    else wait_stages_n(k, std::integral_constant<int, (B_UNEVEN ? NI - 1 : NI)>{});
+    if constexpr (!A_UNEVEN && !B_UNEVEN) {
+      if (PD >= 4 && k >= 3) wait_vm<(PD >= 4 ? 3 * NI : 0)>();
+      else if (PD >= 3 && k >= 2) wait_vm<(PD >= 3 ? 2 * NI : 0)>();
+      else if (PD >= 2 && k >= 1) wait_vm<(PD >= 2 ? NI : 0)>();
+      else wait_vm<0>();
+    } else {
+      wait_vm_upto<(PD - 1) * NI>(max(0, min(k, PD - 1)) * ni_w);
+    }
   };
 
   if constexpr (PP == 2) {
@@ -604,18 +604,33 @@ template <int EPI, bool F32>
 static int big_dispatch(const uint16_t* X, int ldx, const uint16_t* W, const uint16_t* bias, const uint16_t* R,
                         int ldr, void* Y, int ldy, float* ws, long ws_elems, int M, int N, int K, int bn, int S,
                         bool reduce, hipStream_t st) {
-  if (bn == 256)
-    big_launch<256, 256, 2, 4, 64, 2, EPI, F32>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, S, reduce, st);
-  else if (bn == 1256)  // ping-pong schedule of the 256 x 256 tile
-    big_launch<256, 256, 2, 4, 64, 2, EPI, F32, 1>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, S, reduce, st);
-  else if (bn == 2256)  // 8-phase interleave of the 256 x 256 tile (per-half LDS refills)
-    big_launch<256, 256, 2, 4, 64, 2, EPI, F32, 2>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, S, reduce, st);
-  else if (bn == 128)
-    big_launch<256, 128, 4, 2, 64, 3, EPI, F32>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, S, reduce, st);
-  else if (bn == 224)  // 256 x 224 tiles: 7 row groups per wave (gate/up N = 57344 -> exactly 256 column tiles)
-    big_launch<256, 224, 4, 2, 64, 2, EPI, F32>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, S, reduce, st);
-  else
+  // bn = tile code: BN (256 / 128 / 224), 1256 / 2256 (256 x 256 on the ping-pong / 8-phase schedules), plus
+  // 10000 x BM for row tiles below 256 (160 / 192 / 224: M = 320 / 384 / 448 in two tiles without padding rows)
+  const int bm = bn / 10000 ? bn / 10000 : 256, code = bn % 10000;
+#define XOT_BIG(BM_, BN_, WM_, NBUF_, ...)                                                                        \
+  big_launch<BM_, BN_, WM_, 8 / WM_, 64, NBUF_, EPI, F32, ##__VA_ARGS__>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, \
+                                                                         S, reduce, st)
+  if (bm == 256) {
+    if (code == 256) XOT_BIG(256, 256, 2, 2);
+    else if (code == 1256) XOT_BIG(256, 256, 2, 2, 1);  // ping-pong schedule of the 256 x 256 tile
+    else if (code == 2256) XOT_BIG(256, 256, 2, 2, 2);  // 8-phase interleave (per-half LDS refills)
+    else if (code == 128) XOT_BIG(256, 128, 4, 3);
+    else if (code == 224) XOT_BIG(256, 224, 4, 2);      // 7 row groups per wave (gate/up N = 57344 -> 256 tiles)
+    else return -1;
+  } else if (code == 256) {
+    if (bm == 224) XOT_BIG(224, 256, 2, 2);
+    else if (bm == 192) XOT_BIG(192, 256, 2, 2);
+    else if (bm == 160) XOT_BIG(160, 256, 2, 2);
+    else return -1;
+  } else if (code == 128) {
+    if (bm == 224) XOT_BIG(224, 128, 2, 3);
+    else if (bm == 192) XOT_BIG(192, 128, 2, 3);
+    else if (bm == 160) XOT_BIG(160, 128, 2, 3);
+    else return -1;
+  } else {
     return -1;
+  }
+#undef XOT_BIG
   return 0;
 }
 
@@ -623,7 +638,7 @@ int launch_gemm_big(const uint16_t* X, int ldx, const uint16_t* W, const uint16_
                     void* Y, int ldy, bool out_f32, int epi, float* ws, long ws_elems, int M, int N, int K, int bn,
                     int S, bool reduce, hipStream_t s) {
   if (M <= 0) return 0;
-  if ((bn != 128 && bn != 224 && bn != 256 && bn != 1256 && bn != 2256) || N % 16 != 0 || K % 128 != 0 || S < 1 || S > K / 64) return -1;
+  if (N % 16 != 0 || K % 128 != 0 || S < 1 || S > K / 64) return -1;  // tile codes: big_dispatch
   if (S > 1 && (ws == nullptr || ws_elems < (long)S * M * N)) return -1;
   if (epi == EPI_SILU && N % 32 != 0) return -1;
   if (epi == EPI_SILU)

@@ -21,6 +21,17 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// the same for a wave-uniform runtime count 0 <= n <= N (a chain of scalar compares; n clamped to N)
+template <int N>
+__device__ __forceinline__ void wait_vm_upto(int n) {
+  if constexpr (N == 0) {
+    wait_vm<0>();
+  } else {
+    if (n >= N) wait_vm<N>();
+    else wait_vm_upto<N - 1>(n);
+  }
+}
+
 // Sum the S fp32 slabs of one output row at 8 output columns [o, o+8) and apply the epilogue.
 // wsrow = slab 0 of this row (slabs are sstride floats apart); rrow / yrow = this row of R / Y.
 template <int EPI, bool OUT_F32>

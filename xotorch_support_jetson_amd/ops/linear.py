@@ -45,10 +45,31 @@ BIG_MIN_M = int(os.environ.get("XOT_BIG_MIN_M", "65"))
 
 
 def _m_bucket(M: int) -> int:
+  """Tuning-table key of a row count: powers of two up to 256, then multiples of 64 up to 1024 (the decode
+  batch buckets 320 / 384 / 448 tile differently from 512: row tiles of 160 / 192 / 224), then powers of two."""
+  if 256 < M <= 1024:
+    return -(-M // 64) * 64
   b = 1
   while b < M:
     b *= 2
   return b
+
+
+def big_row_tile(M: int) -> int:
+  """Row tile of the large-M GEMM for M rows: 256, or -- when ceil(M / 256) tiles of 256 would carry 32 or more
+  padding rows -- the smallest multiple of 32 (>= 160) that covers M in that many tiles."""
+  n = -(-M // 256)
+  bm = max(160, -(-M // (32 * n)) * 32)
+  return bm if bm < 256 else 256
+
+
+def tile_width(code: int) -> int:
+  """Columns of a gemm_big tile code (BN, 1256 / 2256 = 256 on the ping-pong schedules, + 10000 x BM)."""
+  return code % 1000
+
+
+def tile_rows(code: int) -> int:
+  return code // 10000 or 256
 
 
 def layout_of(w: torch.Tensor) -> str:
@@ -304,13 +325,16 @@ class GemmPolicy:
   @staticmethod
   def _big_cands(M, N, Kd):
     cands = []
-    tiles0 = -(-M // 256)
     if N % 16:
       return cands
-    for bn in (256, 1256, 128):  # 1256: the 256 x 256 tile on the two-group ping-pong schedule
-      if N % (bn % 1000) and N < bn % 1000:  # a partial last column tile is masked; skip tiles wider than N
+    codes = [256, 1256, 128]  # 1256: the 256 x 256 tile on the two-group ping-pong schedule
+    bm = big_row_tile(M)
+    if bm < 256:  # rows that would leave >= 32 padding rows in 256-row tiles: shorter row tiles, base schedule
+      codes += [bm * 10000 + 256, bm * 10000 + 128]
+    for bn in codes:
+      if N % tile_width(bn) and N < tile_width(bn):  # a partial last column tile is masked; skip tiles wider than N
         continue
-      tiles = tiles0 * -(-N // (bn % 1000))
+      tiles = -(-M // tile_rows(bn)) * -(-N // tile_width(bn))
       for S in (1, 2, 3, 4, 6, 8):
         if S > 1 and (tiles >= 256 or tiles * S > 1024 or Kd // 64 < 2 * S):
           continue
@@ -368,7 +392,7 @@ class GemmPolicy:
     for c in cands:
       if c[0] != "big":
         continue
-      tiles = -(-M // 256) * (N // (c[1] % 1000)) * c[2]
+      tiles = -(-M // tile_rows(c[1])) * (N // tile_width(c[1])) * c[2]
       score = abs(tiles - 256) + (0 if c[1] == 1256 else 64)
       if best is None or score < best[0]:
         best = (score, c)

@@ -32,7 +32,7 @@ def _block_manager(num_pages: int):
 
 
 def _bucket(n: int) -> int:
-  for b in (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 160, 192, 256, 320, 384, 512):
+  for b in (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 160, 192, 256, 320, 384, 448, 512):
     if n <= b:
       return b
   return n
