@@ -65,9 +65,14 @@ def main():
       it[0] ^= 1
       return it[0]
 
-    for bm in (0, 128, 192, 256):
+    for bm in (0, 128, 192, 256, 1128, 1192, 1256):  # + 1000: deeper LDS pipeline (more weight bytes in flight)
       if bm and T * k < 16:
         continue
+      C.gemm_moe(x, gus[0], act, off, sorted_tok, 2, T, True, 1, bm)
+      if bm == 0:
+        ref = act.float().clone()
+      else:  # every tile variant reproduces the weight-streaming kernel's rows
+        r[f"gu_relerr_bm{bm}"] = float((act.float() - ref).norm() / ref.norm())
       us = t_us(lambda: C.gemm_moe(x, gus[nxt()], act, off, sorted_tok, 2, T, True, 1, bm))
       r[f"gu_us_bm{bm}"] = round(us, 1)
       r[f"gu_tbps_bm{bm}"] = round(gb_gu / us * 1e3, 2)

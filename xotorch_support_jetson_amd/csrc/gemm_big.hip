@@ -685,11 +685,12 @@ void launch_splitk_silu(const float* ws, int S, int M, int N, uint16_t* y, hipSt
 }
 
 // ------------------------------------------------------------------------------------ grouped (MoE)
-template <int BM, int EPI, bool F32, int MOE>
+template <int BM, int EPI, bool F32, int MOE, int BK = 64, int NBUF = 2>
 static void big_moe_launch(const uint16_t* X, int ldx, const uint16_t* W, void* Y, int ldy, const int* off,
                            const int* gather, int E, int max_rows, int N, int K, int S, long ysplit, hipStream_t st) {
-  constexpr int BN = 256, WM = 2, WN = 4, BK = 64, NBUF = 2;
+  constexpr int BN = 256, WM = 2, WN = 4;
   constexpr int SMEM = NBUF * (BM + BN) * BK * 2;
+  static_assert(SMEM <= 160 * 1024, "LDS");
   auto kern = gemm_big_kernel<BM, BN, WM, WN, BK, NBUF, EPI, F32, false, MOE>;
   static bool attr = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM) ==
                      hipSuccess;
@@ -699,27 +700,38 @@ static void big_moe_launch(const uint16_t* X, int ldx, const uint16_t* W, void* 
                                 S > 1 ? ysplit : 0L);
 }
 
+// bm = row tile (128 / 192 / 256) + 1000 x pipeline variant: 0 = two 64-deep LDS stages (one in flight under
+// the MFMAs); 1 = more expert-weight bytes in flight for the HBM-bound groups (BM 128: three 64-deep stages;
+// BM 192 / 256: four 32-deep stages, three in flight)
 template <int EPI, bool F32>
 static void big_moe_bm(const uint16_t* X, int ldx, const uint16_t* W, void* Y, int ldy, const int* off,
                        const int* gather, int E, int max_rows, int N, int K, int S, long ysplit, int bm,
                        hipStream_t st) {
-  if (bm == 128) {
-    if (gather) big_moe_launch<128, EPI, F32, 2>(X, ldx, W, Y, ldy, off, gather, E, max_rows, N, K, S, ysplit, st);
-    else big_moe_launch<128, EPI, F32, 1>(X, ldx, W, Y, ldy, off, gather, E, max_rows, N, K, S, ysplit, st);
-  } else if (bm == 192) {
-    if (gather) big_moe_launch<192, EPI, F32, 2>(X, ldx, W, Y, ldy, off, gather, E, max_rows, N, K, S, ysplit, st);
-    else big_moe_launch<192, EPI, F32, 1>(X, ldx, W, Y, ldy, off, gather, E, max_rows, N, K, S, ysplit, st);
-  } else {
-    if (gather) big_moe_launch<256, EPI, F32, 2>(X, ldx, W, Y, ldy, off, gather, E, max_rows, N, K, S, ysplit, st);
-    else big_moe_launch<256, EPI, F32, 1>(X, ldx, W, Y, ldy, off, gather, E, max_rows, N, K, S, ysplit, st);
+#define XOT_MOE(BM_, ...)                                                                                          \
+  do {                                                                                                            \
+    if (gather)                                                                                                   \
+      big_moe_launch<BM_, EPI, F32, 2, ##__VA_ARGS__>(X, ldx, W, Y, ldy, off, gather, E, max_rows, N, K, S, ysplit, st); \
+    else                                                                                                          \
+      big_moe_launch<BM_, EPI, F32, 1, ##__VA_ARGS__>(X, ldx, W, Y, ldy, off, gather, E, max_rows, N, K, S, ysplit, st); \
+  } while (0)
+  switch (bm) {
+    case 128: XOT_MOE(128); break;
+    case 192: XOT_MOE(192); break;
+    case 1128: XOT_MOE(128, 64, 3); break;
+    case 1192: XOT_MOE(192, 32, 4); break;
+    case 1256: XOT_MOE(256, 32, 4); break;
+    default: XOT_MOE(256); break;
   }
+#undef XOT_MOE
 }
 
 int launch_gemm_moe_big(const uint16_t* X, int ldx, const uint16_t* W, void* Y, int ldy, bool out_f32, int epi,
                         const int* off, const int* gather, int E, int max_rows, int N, int K, int S, long ysplit,
                         int bm, hipStream_t s) {
   if (max_rows <= 0) return 0;
-  if ((bm != 128 && bm != 192 && bm != 256) || N % 256 != 0 || K % 128 != 0 || S < 1 || S > K / 64) return -1;
+  if ((bm % 1000 != 128 && bm % 1000 != 192 && bm % 1000 != 256) || bm > 1256 || N % 256 != 0 || K % 128 != 0 || S < 1 ||
+      S > K / 64)
+    return -1;
   if (epi != EPI_NONE && epi != EPI_SILU) return -1;
   if (epi == EPI_SILU && out_f32) return -1;
   if (S > 1 && (epi != EPI_NONE || !out_f32)) return -1;  // K slices write fp32 partial slabs

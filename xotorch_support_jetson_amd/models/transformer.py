@@ -21,7 +21,7 @@ from __future__ import annotations
 import math
 import os
 from dataclasses import dataclass
-from typing import List, Optional
+from typing import List, Optional, Tuple
 
 import torch
 
@@ -37,8 +37,27 @@ from .weights import ShardWeights, expert
 MOE_BIG_MIN_ROWS = float(os.environ.get("XOT_MOE_BIG_MIN_ROWS", "24"))
 # K splits of the grouped gate/up GEMM for decode-sized batches (1: fused SiLU epilogue, no slabs)
 MOE_GU_SPLITS = int(os.environ.get("XOT_MOE_GU_SPLITS", "4"))
-MOE_BM = int(os.environ.get("XOT_MOE_BM", "0"))  # force the grouped gemm_big row tile (128 / 192 / 256; tests, A/B)
+MOE_BM = int(os.environ.get("XOT_MOE_BM", "0"))  # force the grouped gemm_big tile code (tests, A/B)
 PAGE = 64
+
+
+def moe_tiles(rows: float, E: int) -> Tuple[int, int, int]:
+  """(gate/up tile code, down tile code, down K split) of the grouped expert GEMMs on gemm_big tiles at `rows`
+  average rows per expert.  Tile code = row tile + 1000 for the deeper LDS pipeline (three 64-deep stages for
+  128 rows: more expert-weight bytes in flight, which is what the HBM-bound small groups need).  Measured at
+  Mixtral shapes (tools/bench_moe.py, profiles/r3/moe_tiles/): ~32 rows gate/up 315 us (1128) vs 356 (128),
+  down 144 (1128, S 2) vs 166; ~64 rows gate/up 441 (1128) vs 566 (128), down 178 (256, S 2) vs 288 (128, S 2);
+  ~128 rows 192-row tiles (gate/up 439 us, down 254 at S 4).  Many small experts (DeepSeek-V2-Lite, 64 x ~24
+  rows) keep 256-row tiles (11.0 vs 12.6 ms per step with 128)."""
+  if rows <= 96 and E > 16:
+    return 256, 256, 2
+  if rows <= 48:
+    return 1128, 1128, 2
+  if rows <= 96:
+    return 1128, 256, 2
+  if rows <= 160:
+    return 192, 192, 4
+  return 256, 256, 2
 
 
 @dataclass
@@ -261,14 +280,9 @@ class ShardModel:
     # rows per expert decide the kernel: the weight-streaming GEMM for decode-sized groups, gemm_big
     # tiles (128 or 256 rows) once the groups are compute-bound
     rows = T * k / E
-    # measured (tools/bench_moe.py, Mixtral shapes): 192-row tiles when one tile holds an expert's
-    # ~100-160 rows, 256 otherwise (a tile's rows past the expert's count are masked MFMA work); 128-row
-    # tiles for small groups of few experts (Mixtral B=128, 32 rows: 20.6 vs 22.3 ms/step) but not for
-    # many experts (DeepSeek-V2-Lite B=256, 64 experts x 24 rows: 12.6 vs 11.0 ms/step with 256)
-    small = 128 if E <= 16 else 256
-    bm = 0 if not shuffled or rows < MOE_BIG_MIN_ROWS else (small if rows <= 96 else (192 if rows <= 160 else 256))
+    bm, bm_dn, S_dn = (0, 0, 0) if not shuffled or rows < MOE_BIG_MIN_ROWS else moe_tiles(rows, E)
     if MOE_BM and bm:
-      bm = MOE_BM
+      bm = bm_dn = MOE_BM
     act = torch.empty(T * k, F, dtype=torch.bfloat16, device=dev)
     Sg = MOE_GU_SPLITS if (bm == 0 and T * k <= 32 and D % (256 * MOE_GU_SPLITS) == 0) else 1
     if Sg > 1:
@@ -282,11 +296,11 @@ class ShardModel:
       C.gemm_moe(xn, lw.gu_w, act, off, sorted_tok, K.EPI["silu"], T, layout_of(lw.gu_w) == "stream", 1, bm)
     # down projection split over K (fp32 partial slabs summed by the combine): the grouped GEMM only has
     # (experts hit) x N/tile workgroups with work, too few to stream the expert weights at full HBM rate
-    S = (4 if T * k <= 64 else 2) if bm == 0 else (4 if bm == 192 else 2)
+    S = (4 if T * k <= 64 else 2) if bm == 0 else S_dn
     if F % (256 * S):
       S = 1
     y = torch.empty(S * T * k, D, dtype=torch.float32, device=dev)
-    C.gemm_moe(act, lw.down_w, y, off, None, K.EPI["none"], T, layout_of(lw.down_w) == "stream", S, bm)
+    C.gemm_moe(act, lw.down_w, y, off, None, K.EPI["none"], T, layout_of(lw.down_w) == "stream", S, bm_dn)
     if next_norm is not None:  # combine + the following RMSNorm in one kernel
       out = torch.empty_like(h)
       C.moe_combine_norm(y, slot_of, topw, h, S, next_norm, out, float(c.rms_norm_eps))
