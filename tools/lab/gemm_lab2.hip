@@ -25,7 +25,7 @@ __global__ void fill_rand(uint16_t* p, size_t n, uint32_t seed, float scale) {
 }
 
 struct Ctx {
-  const uint16_t* X; const uint16_t* W; uint16_t* Y; float* ws; int M, N, K; size_t wstride; int nc;
+  const uint16_t* X; const uint16_t* W; uint16_t* Y; float* ws; int M, N, K; size_t wstride; int nc; int ldx;
 };
 
 typedef void (*LaunchFn)(const Ctx&, const uint16_t* W, hipStream_t);
@@ -38,7 +38,7 @@ void launch_v(const Ctx& c, const uint16_t* W, hipStream_t st) {
   static bool attr = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM) == hipSuccess;
   (void)attr;
   const int nwg = ((c.M + 255) / 256) * (c.N / BN);
-  k<<<nwg, 512, SMEM, st>>>(c.X, c.K, W, nullptr, nullptr, 0, c.Y, EPI == EPI_SILU ? c.N / 2 : c.N, nullptr, c.M, c.N,
+  k<<<nwg, 512, SMEM, st>>>(c.X, c.ldx, W, nullptr, nullptr, 0, c.Y, EPI == EPI_SILU ? c.N / 2 : c.N, nullptr, c.M, c.N,
                             c.K, 1, nullptr, nullptr, 0L);
 }
 
@@ -46,7 +46,7 @@ static float* g_part = nullptr;
 static int* g_sync = nullptr;
 template <int EPI>
 void launch_sk(const Ctx& c, const uint16_t* W, hipStream_t st) {
-  launch_gemm_sk(c.X, c.K, W, nullptr, nullptr, 0, c.Y, EPI == EPI_SILU ? c.N / 2 : c.N, false, EPI, g_part, g_sync, c.M,
+  launch_gemm_sk(c.X, c.ldx, W, nullptr, nullptr, 0, c.Y, EPI == EPI_SILU ? c.N / 2 : c.N, false, EPI, g_part, g_sync, c.M,
                  c.N, c.K, 256, st);
 }
 
@@ -56,7 +56,7 @@ void launch_w4(const Ctx& c, const uint16_t* W, hipStream_t st) {
   static bool attr = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, w4::SMEM) == hipSuccess;
   (void)attr;
   const int nwg = ((c.M + 255) / 256) * (c.N / 256);
-  k<<<nwg, 256, w4::SMEM, st>>>(c.X, c.K, W, nullptr, nullptr, 0, c.Y, EPI == EPI_SILU ? c.N / 2 : c.N, nullptr, c.M, c.N,
+  k<<<nwg, 256, w4::SMEM, st>>>(c.X, c.ldx, W, nullptr, nullptr, 0, c.Y, EPI == EPI_SILU ? c.N / 2 : c.N, nullptr, c.M, c.N,
                                 c.K, 1);
 }
 
@@ -67,16 +67,19 @@ int main(int argc, char** argv) {
   const int only = argc > 4 ? atoi(argv[4]) : -1;
   const int epi = argc > 5 ? atoi(argv[5]) : EPI_SILU;
   const size_t wsz = (size_t)N * K;
-  // weight copies rotated per call (HBM-cold); argv[6] = 1 keeps one copy (cache-resident when it fits)
-  const int nc = argc > 6 ? atoi(argv[6]) : (int)std::max<size_t>(2, (1ull << 30) / (wsz * 2) + 1);
+  // weight copies rotated per call (HBM-cold); argv[6] = 1 keeps one copy (cache-resident when it fits), 0 = default
+  const int nc_arg = argc > 6 ? atoi(argv[6]) : 0;  // <= 0: the rotating default
+  const int nc = nc_arg > 0 ? nc_arg : (int)std::max<size_t>(2, (1ull << 30) / (wsz * 2) + 1);
+  // argv[7] = X row padding in elements (row stride K + pad: rows at a non-power-of-two stride)
+  const int ldx = K + (argc > 7 ? atoi(argv[7]) : 0);
   uint16_t *X, *W, *Y;
-  CK(hipMalloc(&X, (size_t)M * K * 2));
+  CK(hipMalloc(&X, (size_t)M * ldx * 2));
   CK(hipMalloc(&W, wsz * 2 * nc));
   CK(hipMalloc(&Y, (size_t)M * N * 4));
-  fill_rand<<<4096, 256>>>(X, (size_t)M * K, 17u, 1.0f);
+  fill_rand<<<4096, 256>>>(X, (size_t)M * ldx, 17u, 1.0f);
   fill_rand<<<4096, 256>>>(W, wsz * nc, 91u, 0.02f);
   CK(hipDeviceSynchronize());
-  Ctx c{X, W, Y, nullptr, M, N, K, wsz, nc};
+  Ctx c{X, W, Y, nullptr, M, N, K, wsz, nc, ldx};
   CK(hipMalloc(&g_part, gemm_sk_part_elems() * 4));
   CK(hipMalloc(&g_sync, 1 << 20));
   CK(hipMemset(g_sync, 0, 1 << 20));
