@@ -5,6 +5,9 @@ streaming chat completions.  Reports what the reference's clients measure (tinyc
 time to first token and output tokens/s), aggregated over the requests.
 
   python tools/bench_serve.py --model llama-3-8b --concurrency 64 --max-tokens 128 --prompt-words 200
+  python tools/bench_serve.py --ring 2 ...     the same load against `xot --gpus 2` (RingServer: the layers
+                                               split over 2 ranks, RCCL hand-off; XOT_DIST_BACKEND=gloo
+                                               rehearses 2 ranks on one GPU)
 
 Random-init weights (no checkpoint on the GPU box) and the offline byte tokenizer: the prompt is
 --prompt-words synthetic words; generation runs to --max-tokens unless an EOS id is sampled.
@@ -73,6 +76,58 @@ async def client_main(a):
     res = await asyncio.gather(*(one(session, a.client, a, i, a.max_tokens) for i in range(a.concurrency)))
     wall = time.perf_counter() - t0
   print(json.dumps({"results": res, "wall_s": wall}), flush=True)
+
+
+async def ring_main(a):
+  """--ring N: start `xot --gpus N` (the RCCL ring server with the API on rank 0) as a child process group,
+  wait for its API, run the same warmup + measured load with in-process clients, stop the group."""
+  import signal
+  import subprocess
+  from aiohttp import ClientSession, TCPConnector
+  port = free_port()
+  env = dict(os.environ, XOT_MAX_BATCH=str(max(a.concurrency, 1)))
+  cmd = [sys.executable, "-m", "xotorch_support_jetson_amd.main", "--gpus", str(a.ring), "--default-model", a.model,
+         "--chatgpt-api-port", str(port), "--disable-tui", "--max-generate-tokens", str(a.max_tokens)]
+  root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+  proc = subprocess.Popen(cmd, cwd=root, env=env, start_new_session=True)
+  base = f"http://127.0.0.1:{port}"
+  try:
+    async with ClientSession(connector=TCPConnector(limit=0)) as session:
+      t0 = time.perf_counter()
+      while True:  # the ranks load their shards and start the API on rank 0
+        if proc.poll() is not None:
+          raise SystemExit(f"ring server exited with {proc.returncode} before its API came up")
+        try:
+          async with session.get(base + "/healthcheck") as r:
+            if r.status == 200:
+              break
+        except OSError:
+          pass
+        if time.perf_counter() - t0 > 600:
+          raise SystemExit("ring server API did not come up within 600 s")
+        await asyncio.sleep(1.0)
+      url = base + "/v1/chat/completions"
+      await client_warmup(session, url, a)
+      warm = time.perf_counter() - t0
+      t0 = time.perf_counter()
+      res = await asyncio.gather(*(one(session, url, a, i, a.max_tokens) for i in range(a.concurrency)))
+      wall = time.perf_counter() - t0
+  finally:
+    try:
+      os.killpg(proc.pid, signal.SIGTERM)  # the group this call started (ranks are its children)
+      proc.wait(timeout=60)
+    except (ProcessLookupError, subprocess.TimeoutExpired):
+      os.killpg(proc.pid, signal.SIGKILL)
+  toks = sum(r[1] for r in res)
+  ttfts = sorted(r[0] for r in res)
+  print(json.dumps({"metric": f"API streaming output tokens/sec (ring of {a.ring} ranks)", "model": a.model,
+                    "ring": a.ring, "dist_backend": os.environ.get("XOT_DIST_BACKEND", "nccl"),
+                    "concurrency": a.concurrency, "prompt_words": a.prompt_words, "max_tokens": a.max_tokens,
+                    "output_tokens": toks, "value": round(toks / wall, 2), "unit": "tokens/s",
+                    "wall_s": round(wall, 2), "warmup_s": round(warm, 1),
+                    "ttft_s": {"p50": round(ttfts[len(ttfts) // 2], 3), "max": round(ttfts[-1], 3)},
+                    "per_request_tok_s_p50": round(sorted(r[1] / r[2] for r in res)[len(res) // 2], 2),
+                    "data": "random-init weights, byte tokenizer, synthetic prompts", "dtype": "bf16"}), flush=True)
 
 
 async def main(a):
@@ -192,10 +247,11 @@ if __name__ == "__main__":
   ap.add_argument("--in-process-clients", dest="client_proc", action="store_false",
                   help="run the HTTP clients on the server's event loop (their SSE parsing then counts as server time)")
   ap.add_argument("--client", default=None, help=argparse.SUPPRESS)  # internal: load-generator child mode
+  ap.add_argument("--ring", type=int, default=0, help="serve from `xot --gpus N` (the RCCL ring server) instead")
   if os.environ.get("XOT_PROFILE"):  # host-side hot spots of the serving loop (main thread)
     import cProfile
     PROF = cProfile.Profile()
   args = ap.parse_args()
   if os.environ.get("XOT_SWITCH_INTERVAL_US"):  # diagnostic: CPython's GIL hand-off interval (default 5000 us)
     sys.setswitchinterval(float(os.environ["XOT_SWITCH_INTERVAL_US"]) * 1e-6)
-  asyncio.run(client_main(args) if args.client else main(args))
+  asyncio.run(client_main(args) if args.client else (ring_main(args) if args.ring else main(args)))

@@ -328,6 +328,8 @@ class GemmPolicy:
     if N % 16:
       return cands
     codes = [256, 1256, 128]  # 1256: the 256 x 256 tile on the two-group ping-pong schedule
+    if N % 224 == 0:  # 7 row groups per wave: whole rounds where 256-wide tiles leave a half round (8B gate/up)
+      codes.append(224)
     bm = big_row_tile(M)
     if bm < 256:  # rows that would leave >= 32 padding rows in 256-row tiles: shorter row tiles, base schedule
       codes += [bm * 10000 + 256, bm * 10000 + 128]
