@@ -1,6 +1,6 @@
 #!/bin/bash
 # Serving through the HTTP API (Llama-3-8B): streams 1 / 64 / 256, shared-prefix cache on / off, and the
-# RCCL ring server rehearsed on one GPU (2 ranks over gloo).   bash tools/gpu/serve.sh [api|prefix|ring]...
+# RCCL ring server rehearsed on one GPU (2 ranks over gloo).   bash tools/gpu/serve.sh [api|prefix|ring|ringload]...
 source "$(dirname "$0")/common.sh"
 for what in ${@:-api}; do
   case $what in
@@ -8,5 +8,7 @@ for what in ${@:-api}; do
     prefix) for pc in 1 0; do XOT_PREFIX_CACHE=$pc XOT_MAX_BATCH=64 step serve/prefix_pc$pc 400 python -u tools/bench_serve.py --model llama-3-8b --concurrency 64 --max-tokens 128 --prompt-words 400 --shared-prefix; done ;;
     ring)   step serve/ring_tests 300 python -u -m pytest tests/test_ring_serve.py tests/test_ring_health.py -x -v --timeout 200 --timeout-method thread
             XOT_DIST_BACKEND=gloo step serve/ring_run 300 python -u -m xotorch_support_jetson_amd.main run llama-3-8b --gpus 2 --prompt "Who are you?" --max-generate-tokens 24 --disable-tui ;;
+    ringload)  # API load against the 2-rank ring server (gloo hand-off through host memory: a rehearsal, not RCCL speed)
+            for c in 1 64; do XOT_DIST_BACKEND=gloo step serve/ring2_c$c 600 python -u tools/bench_serve.py --ring 2 --model llama-3-8b --concurrency $c --max-tokens 64 --prompt-words 16; done ;;
   esac
 done
