@@ -2,6 +2,7 @@
 manual-discovery config (reference: test/test_model_helpers.py, test/test_tokenizers.py,
 xotorch/networking/manual/test_network_topology_config.py)."""
 import json
+import os
 
 import numpy as np
 import pytest
@@ -367,3 +368,35 @@ def test_gemm_row_tiles_for_unaligned_batches():
   assert L.tile_width(2240128) == 128 and L.tile_rows(2240128) == 224 and L.tile_rows(1256) == 256
   h = L.GemmPolicy._heuristic(384, 57344, L.GemmPolicy._big_cands(384, 57344, 8192))
   assert h[0] == "big", h  # (untuned fallback; the timed choice decides between 256- and 192-row tiles)
+
+
+def test_pmc_summary_decode_window(tmp_path):
+  """tools/pmc_summary.py joins the counter passes of a pmc.sh run per (kernel, grid) over the last decode
+  steps only (delimited by the sampler), so tuning calls before them never mix into the rates."""
+  import csv
+  import subprocess
+  import sys
+  fields = ["Dispatch_Id", "Kernel_Name", "Grid_Size", "Counter_Name", "Counter_Value", "Start_Timestamp",
+            "End_Timestamp"]
+  for p, ctr, val in (("p1", "GRBM_GUI_ACTIVE", 8e6), ("p2", "SQ_VALU_MFMA_BUSY_CYCLES", 5e8)):
+    d = tmp_path / p / "host"
+    d.mkdir(parents=True)
+    with open(d / "1_p_counter_collection.csv", "w", newline="") as f:
+      w = csv.DictWriter(f, fieldnames=fields)
+      w.writeheader()
+      t = 0
+      seq = [("gemm_big_kernel<1>(int)", 999, 1.0)] * 3  # tuning calls: another grid, another rate
+      seq += [("gemm_big_kernel<1>(int)", 512, 1.0), ("attn(int)", 64, 1.0), ("sample_fast_kernel(int)", 1, 1.0)] * 3
+      for i, (k, grid, _) in enumerate(seq):
+        t += 1_000_000
+        v = val if grid != 999 else val / 10
+        w.writerow(dict(Dispatch_Id=i, Kernel_Name=k, Grid_Size=grid, Counter_Name=ctr, Counter_Value=v,
+                        Start_Timestamp=t, End_Timestamp=t + 500_000))
+  out = tmp_path / "s.json"
+  tool = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "pmc_summary.py")
+  subprocess.run([sys.executable, tool, str(tmp_path), "--window", "sample_fast_kernel", "--last", "2",
+                  "--match", "gemm_big", "--json", str(out)], check=True, capture_output=True)
+  s = json.loads(out.read_text())
+  assert list(s) == ["gemm_big_kernel<1> grid=512"]
+  r = s["gemm_big_kernel<1> grid=512"]
+  assert r["us"] == 500.0 and r["clock_ghz"] == 2.0 and r["mfma_busy_pct"] == 48.8
