@@ -202,7 +202,8 @@ def _worker2(rank, world, port, q, pages, fault):
 
   ctl = control_group()
   runner, pool = make_runner(rank, world, ctl)
-  mon = HealthMonitor(rank, world, interval=0.1, timeout=1.5).start() if fault else None
+  # 5 s: a loaded CI host (parallel test workers) must not make a live peer look dead
+  mon = HealthMonitor(rank, world, interval=0.1, timeout=5.0).start() if fault else None
   srv = RingServer(runner, rank, world, P2PTransport(rank, world, monitor=mon), ctl, step_tokens=32, monitor=mon,
                    make_runner=make_runner, pool_pages=pool)
   res = None
