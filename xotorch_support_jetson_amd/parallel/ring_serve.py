@@ -328,9 +328,12 @@ class RingServer:
       except PeerFailure as e:
         self._recover(e.dead)
       except RuntimeError:
-        if self.monitor is None or not self.monitor.failed.is_set():
+        # a send / recv on a dead peer's connection can fail before the heartbeat has declared the peer
+        # dead: give the monitor its detection window before treating the error as fatal
+        m = self.monitor
+        if m is None or not m.failed.wait(timeout=m.timeout + 4 * m.interval):
           raise
-        self._recover(self.monitor.dead)
+        self._recover(m.dead)
 
   def _lead(self, idle_wait: float) -> None:
     lane = 0
