@@ -33,7 +33,7 @@ typedef void (*LaunchFn)(const Ctx&, const uint16_t* W, hipStream_t);
 template <int BN, int WM, int BK, int NBUF, int AUXA, int AUXB, bool PRIO, int PP, int EPI>
 void launch_v(const Ctx& c, const uint16_t* W, hipStream_t st) {
   constexpr int WN = 8 / WM;
-  constexpr int SMEM = NBUF * (256 + BN) * BK * 2;
+  constexpr int SMEM = big_smem<256, BN, BK, NBUF, PP>();
   auto k = gemm_big_kernel<256, BN, WM, WN, BK, NBUF, EPI, false, false, 0, 0, AUXA, AUXB, PRIO, PP>;
   static bool attr = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM) == hipSuccess;
   (void)attr;
@@ -87,11 +87,13 @@ int main(int argc, char** argv) {
   if (epi == EPI_SILU) {
     vs.push_back({"pp nt(B)     ", launch_v<256, 2, 64, 2, 0, 3, false, 1, EPI_SILU>});
     vs.push_back({"base 256     ", launch_v<256, 2, 64, 2, 0, 3, false, 0, EPI_SILU>});
+    vs.push_back({"W 3-deep     ", launch_v<256, 2, 64, 2, 0, 3, false, 3, EPI_SILU>});
     if (N % 224 == 0) vs.push_back({"base 224     ", launch_v<224, 4, 64, 2, 0, 3, false, 0, EPI_SILU>});
     vs.push_back({"stream-K     ", launch_sk<EPI_SILU>});
   } else {
     vs.push_back({"pp nt(B)     ", launch_v<256, 2, 64, 2, 0, 3, false, 1, EPI_NONE>});
     vs.push_back({"base 256     ", launch_v<256, 2, 64, 2, 0, 3, false, 0, EPI_NONE>});
+    vs.push_back({"W 3-deep     ", launch_v<256, 2, 64, 2, 0, 3, false, 3, EPI_NONE>});
     if (N % 224 == 0) vs.push_back({"base 224     ", launch_v<224, 4, 64, 2, 0, 3, false, 0, EPI_NONE>});
     vs.push_back({"stream-K     ", launch_sk<EPI_NONE>});
   }

@@ -43,6 +43,9 @@ namespace xot {
 // MFMAs overlap the other's LDS reads.  A stage is read only in its phases 0-2 (A halves in 0 and 2, B
 // halves in 0 and 1), so in phase 3 the stage two ahead is issued into the buffer being finished, and
 // the stage one ahead is retired by a counted vmcnt (LDS-DMA stays in flight across the barriers).
+// PP 2 (8-phase per-half refills) and PP 3 (X two stages deep, W three: two weight stages in flight) are
+// lab schedules, measured slower than PP 1 (profiles/r3/lab_gemm_schedules_random.log,
+// profiles/r3/lab_s2/w_three_deep_staging.log) and not offered to the tuner.
 template <int BM, int BN, int WM, int WN, int BK, int NBUF, int EPI, bool OUT_F32, bool SPLIT, int MOE = 0, int ABL = 0,
           int AUXA = 0, int AUXB = 3, bool PRIO = false, int PP = 0>
 __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __restrict__ X, int ldx,
@@ -187,9 +190,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
   // ds_read_b128 is in flight under the MFMAs of the previous row tile (the scheduling fence keeps
   // the compiler from hoisting all reads up front, which costs registers and serialises on lgkmcnt).
   constexpr int LDPF = 3;
-  auto compute = [&](int buf) {
-    const uint16_t* As = smem + buf * STAGE;
-    const uint16_t* Bs = As + A_ELEMS;
+  auto compute_ab = [&](const uint16_t* As, const uint16_t* Bs) {
     s16x8 bf[KS][NT];
 #pragma unroll
     for (int s2 = 0; s2 < KS; ++s2)
@@ -210,6 +211,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
       __builtin_amdgcn_sched_barrier(0);
     }
   };
+  auto compute = [&](int buf) { compute_ab(smem + buf * STAGE, smem + buf * STAGE + A_ELEMS); };
 
   // Barrier without the vmcnt(0) drain __syncthreads() would add: LDS-DMA stages stay in flight.
   // The asm statements are compiler fences (no LDS access moves across the barrier).
@@ -439,6 +441,45 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
       }
       if (half == 0) bar();  // balance the barrier count
     }
+  } else if constexpr (PP == 3) {
+    // X two stages deep, W three: the LDS holds 2 X images and 3 W images (2 x 32 + 3 x 32 KB = 160 KB), so
+    // the weight stream -- the operand that misses L2 -- has two stages in flight under the MFMAs of a third
+    // while the L2-resident activations keep one.  Per iteration t: X(t+1) is issued, then W(t+2); the
+    // counted wait at the end leaves only W(t+2) in flight, which retires X(t+1) and W(t+1) (issued earlier).
+    static_assert(BM == 256 && BN == 256 && BK == 64 && NBUF == 2 && !A_UNEVEN && !B_UNEVEN && ABL == 0,
+                  "PP 3 geometry");
+    uint16_t* const Xs = smem;                // 2 x A_ELEMS
+    uint16_t* const Ws = smem + 2 * A_ELEMS;  // 3 x B_ELEMS
+    auto issue_x = [&](int t) {
+      const int k0 = (t_beg + t) * BK;
+#pragma unroll
+      for (int i = 0; i < A_INSTR; ++i) glds16<AUXA>(asrc[i] + k0, Xs + (t & 1) * A_ELEMS + aq(i) * 512);
+    };
+    auto issue_w = [&](int t) {
+      const int k0 = (t_beg + t) * BK;
+      const size_t woff = (size_t)(k0 >> 7) * 2048 + ((k0 & 127) >> 5) * 512;
+#pragma unroll
+      for (int i = 0; i < B_INSTR; ++i) glds16<AUXB>(bsrc[i] + woff, Ws + (t % 3) * B_ELEMS + bq(i) * 512);
+    };
+    if (T > 0) {
+      issue_x(0);
+      issue_w(0);
+      if (T > 1) {
+        issue_w(1);
+        wait_vm<B_INSTR>();  // X(0), W(0) landed; W(1) in flight
+      } else {
+        wait_vm<0>();
+      }
+      barrier();
+      for (int t = 0; t < T; ++t) {
+        // X buffer (t+1)&1 and W buffer (t+2)%3 were last read in iteration t-1 (every wave is past its barrier)
+        if (t + 1 < T) issue_x(t + 1);
+        if (t + 2 < T) issue_w(t + 2);
+        compute_ab(Xs + (t & 1) * A_ELEMS, Ws + (t % 3) * B_ELEMS);
+        if (t + 2 < T) wait_vm<B_INSTR>(); else wait_vm<0>();
+        barrier();
+      }
+    }
   } else if (T > 0) {
     // prologue: stages 0 .. PD-1 in flight, stage 0 landed
 #pragma unroll
@@ -572,11 +613,16 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
   }
 }
 
+template <int BM, int BN, int BK, int NBUF, int PP>
+constexpr int big_smem() {  // LDS bytes of a gemm_big configuration (PP 3: 2 X stages + 3 W stages)
+  return PP == 3 ? (2 * BM + 3 * BN) * BK * 2 : NBUF * (BM + BN) * BK * 2;
+}
+
 template <int BM, int BN, int WM, int WN, int BK, int NBUF, int EPI, bool F32, int PP = 0>
 static void big_launch(const uint16_t* X, int ldx, const uint16_t* W, const uint16_t* bias, const uint16_t* R,
                        int ldr, void* Y, int ldy, float* ws, int M, int N, int K, int S, bool reduce,
                        hipStream_t st) {
-  constexpr int SMEM = NBUF * (BM + BN) * BK * 2;
+  constexpr int SMEM = big_smem<BM, BN, BK, NBUF, PP>();
   static_assert(SMEM <= 160 * 1024, "LDS");
   const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN) * S;
   if (S == 1) {
