@@ -297,6 +297,9 @@ def test_api_request_without_temperature(tmp_path, monkeypatch, loop_on):
     monkeypatch.setattr(se, "ENGINE_LOOP", loop_on)
     eng = se.ShardedInferenceEngine(NoopShardDownloader(), device=torch.device("cpu"))
     nodes = await make_ring(tmp_path, [f"solo_t{int(loop_on)}"], engines=[eng])
+    # requests without max_tokens run to the node's cap: keep it small (1024 random-weight tokens per request
+    # on the per-token CPU path overran the timeout on a loaded host)
+    nodes[0].max_generate_tokens = 16
     api = ChatGPTAPI(nodes[0], "ShardedInferenceEngine", response_timeout=60, default_model="tiny-llama")
     client = TestClient(TestServer(api.app))
     await client.start_server()

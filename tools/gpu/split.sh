@@ -1,0 +1,15 @@
+#!/bin/bash
+# A/B of the split decode step (two half-batches on two streams, models/transformer.py:_forward_split)
+# against the single-stream step at the headline config.
+#   bash tools/gpu/split.sh [base|split|split0|prof]...
+source "$(dirname "$0")/common.sh"
+for what in ${@:-base split split0}; do
+  case $what in
+    base)   step split/base 400 python -u bench.py --steps 10 --warmup 3 ;;
+    split)  XOT_SPLIT_DECODE=256 step split/split 400 python -u bench.py --steps 10 --warmup 3 ;;
+    split0) XOT_SPLIT_DECODE=256 XOT_SPLIT_OFFSET=0 step split/split0 400 python -u bench.py --steps 10 --warmup 3 ;;
+    eager)  XOT_SPLIT_DECODE=256 XOT_GRAPHS=0 step split/split_eager 400 python -u bench.py --steps 10 --warmup 3 ;;
+    prof)   XOT_SPLIT_DECODE=256 prof split/prof 600 python3 "$R/bench.py" --steps 6 --warmup 3
+            step split/breakdown 60 python tools/decode_breakdown.py "$(ls "$O"/split/prof/*/*kernel_trace.csv "$O"/split/prof/*kernel_trace.csv 2>/dev/null | head -1)" --steps 6 --json "$O/split/breakdown.json" ;;
+  esac
+done

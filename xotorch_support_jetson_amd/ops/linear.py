@@ -109,16 +109,24 @@ class _Scratch:
   replaced, but the old one is kept alive: HIP graphs captured earlier (decode graphs of other batch
   buckets) hold its address, and replaying them into a freed block would corrupt whatever the caching
   allocator put there next (a serving run that captured bucket 1, then grew the slabs for bucket 64,
-  faulted exactly that way)."""
+  faulted exactly that way).
+
+  `lane` selects an independent set of buffers: the two half-batches of a split decode step
+  (models/transformer.py:_forward_split) run concurrently on two streams and must not share slabs,
+  stream-K partial tiles or tickets."""
 
   def __init__(self):
-    self.ws: Dict[int, torch.Tensor] = {}
-    self.tk: Dict[int, torch.Tensor] = {}
-    self.sk: Dict[int, tuple] = {}
+    self.ws: Dict[tuple, torch.Tensor] = {}
+    self.tk: Dict[tuple, torch.Tensor] = {}
+    self.sk: Dict[tuple, tuple] = {}
     self.retired: list = []
+    self.lane = 0
+
+  def _key(self, device) -> tuple:
+    return (device.index or 0, self.lane)
 
   def splitk(self, device, n: int) -> torch.Tensor:
-    idx = device.index or 0
+    idx = self._key(device)
     t = self.ws.get(idx)
     if t is None or t.numel() < n:
       if torch.cuda.is_current_stream_capturing():
@@ -131,8 +139,8 @@ class _Scratch:
 
   def stream_k(self, device):
     """(fp32 partial-tile slots, zeroed int32 tickets / flags) of the stream-K GEMM: fixed sizes, allocated
-    once per device (the kernel leaves the sync words zeroed, so graph replays can share them)."""
-    idx = device.index or 0
+    once per device and lane (the kernel leaves the sync words zeroed, so graph replays can share them)."""
+    idx = self._key(device)
     got = self.sk.get(idx)
     if got is None:
       if torch.cuda.is_current_stream_capturing():
@@ -146,7 +154,7 @@ class _Scratch:
   def tickets(self, device, n: int) -> torch.Tensor:
     """Zero-initialised int32 tile counters of the in-launch split-K combine (the last arriver of a
     tile resets its counter, so the buffer stays zeroed between launches and graph replays)."""
-    idx = device.index or 0
+    idx = self._key(device)
     t = self.tk.get(idx)
     if t is None or t.numel() < n:
       if torch.cuda.is_current_stream_capturing():
