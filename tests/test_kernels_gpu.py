@@ -194,7 +194,7 @@ def test_attn_decode(gpu, H, Hkv, Dh, ctx):
   q = torch.randn(B, H, Dh, device=gpu, dtype=torch.bfloat16)
   scale = 1 / math.sqrt(Dh)
   ref = R.attn_decode(q, kc, vc, bt, cl, scale)
-  for algo in (0, 1, 2):  # workgroup kernel; wave kernel without / with page prefetch
+  for algo in (0, 1, 2, 3):  # workgroup kernel; wave kernel without / with page prefetch, + nt loads
     for ppp in (1, 3, 4, 8, None):  # None: per-call choice from the batch
       if algo == 0 and ppp in (1, 3):
         continue

@@ -17,7 +17,13 @@ for what in ${@:-dense moe}; do
     fp8)   for m in llama-3-70b llama-3-8b; do for b in 1 64; do
              step cfg/fp8_${m}_b$b 600 python bench.py --model $m --batch-per-gpu $b --steps 32 --warmup 4 --weight-dtype fp8
            done; done ;;
+    b1prof) ;;
     long)  for t in 8192 32768 65536; do step long/l8b_$t 600 python -u tools/bench_long_prefill.py --model llama-3.1-8b --tokens $t; done
            step long/l70b_32768 600 python -u tools/bench_long_prefill.py --model llama-3.1-70b --tokens 32768 ;;
   esac
 done
+# b1prof: kernel trace of 8B batch-1 decode and its per-step breakdown
+if [ "$1" = b1prof ]; then
+  prof cfg/b1prof 300 python3 "$R/bench.py" --model llama-3-8b --batch-per-gpu 1 --steps 16 --warmup 4
+  step cfg/b1breakdown 60 python tools/decode_breakdown.py "$(ls "$O"/cfg/b1prof/*/*kernel_trace.csv "$O"/cfg/b1prof/*kernel_trace.csv 2>/dev/null | head -1)" --steps 16 --json "$O/cfg/b1breakdown.json"
+fi

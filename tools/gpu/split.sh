@@ -9,7 +9,14 @@ for what in ${@:-base split split0}; do
     split)  XOT_SPLIT_DECODE=256 step split/split 400 python -u bench.py --steps 10 --warmup 3 ;;
     split0) XOT_SPLIT_DECODE=256 XOT_SPLIT_OFFSET=0 step split/split0 400 python -u bench.py --steps 10 --warmup 3 ;;
     eager)  XOT_SPLIT_DECODE=256 XOT_GRAPHS=0 step split/split_eager 400 python -u bench.py --steps 10 --warmup 3 ;;
+    attnnt) ;;
     prof)   XOT_SPLIT_DECODE=256 prof split/prof 600 python3 "$R/bench.py" --steps 6 --warmup 3
             step split/breakdown 60 python tools/decode_breakdown.py "$(ls "$O"/split/prof/*/*kernel_trace.csv "$O"/split/prof/*kernel_trace.csv 2>/dev/null | head -1)" --steps 6 --json "$O/split/breakdown.json" ;;
   esac
 done
+# attnnt: decode attention with non-temporal K / V loads (XOT_ATTN_DECODE=3) against the default
+if [ "$1" = attnnt ]; then
+  step attnnt/test 200 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k attn_decode
+  step attnnt/base 400 python -u bench.py --steps 10 --warmup 3
+  XOT_ATTN_DECODE=3 step attnnt/nt 400 python -u bench.py --steps 10 --warmup 3
+fi

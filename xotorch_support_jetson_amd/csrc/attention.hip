@@ -261,7 +261,8 @@ __global__ __launch_bounds__(DH) void attn_decode_reduce_kernel(const float* __r
 // 32kk + 8q + 4h + r, hence lane group g of the P^T operand owns keys 32kk + 8g .. +8 and reads one
 // 16-byte run of the transposed V page.  No LDS.
 // PF: prefetch the next page's K / V into registers under the current page's math.
-template <int DH, bool PF>
+// NT: K / V pages loaded non-temporal (read once per step; algo 3)
+template <int DH, bool PF, bool NT = false>
 __global__ __launch_bounds__(256) void attn_decode_wave_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
     const int32_t* __restrict__ block_tables, int max_blocks, const int32_t* __restrict__ ctx_lens,
@@ -316,12 +317,13 @@ __global__ __launch_bounds__(256) void attn_decode_wave_kernel(
     for (int t = 0; t < 4; ++t) {
       const int r = min(32 * (t >> 1) + 4 * (t & 1) + krow, lim);
 #pragma unroll
-      for (int s = 0; s < KS; ++s) kf[t][s] = ld16(kb + r * DH + 32 * s);
+      for (int s = 0; s < KS; ++s) kf[t][s] = NT ? ld16nt(kb + r * DH + 32 * s) : ld16(kb + r * DH + 32 * s);
     }
 #pragma unroll
     for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) vf[dt][kk] = ld16(vb + 16 * dt * PAGE + 32 * kk);
+      for (int kk = 0; kk < 2; ++kk)
+        vf[dt][kk] = NT ? ld16nt(vb + 16 * dt * PAGE + 32 * kk) : ld16(vb + 16 * dt * PAGE + 32 * kk);
   };
   auto compute = [&](int p, const s16x8 (&kf)[4][KS], const s16x8 (&vf)[NDT][2]) {
     f32x4 st[4];
@@ -434,14 +436,14 @@ int launch_attn_decode(const uint16_t* q, const uint16_t* kc, const uint16_t* vc
   const float sl = scale * LOG2E;
   if (algo != 0) {  // wave per (sequence, KV head, partition)
     const int units = B * Hkv * nparts, wgs = (units + 3) / 4;
-#define XOT_WAVE(DHV, PFV)                                                                                       \
-  attn_decode_wave_kernel<DHV, PFV><<<wgs, 256, 0, s>>>(q, kc, vc, block_tables, max_blocks, ctx_lens, out, ws_o, \
+#define XOT_WAVE(DHV, PFV, NTV)                                                                                  \
+  attn_decode_wave_kernel<DHV, PFV, NTV><<<wgs, 256, 0, s>>>(q, kc, vc, block_tables, max_blocks, ctx_lens, out, ws_o, \
                                                         ws_ml, B, H, Hkv, pages_per_part, nparts, sl, num_pages, tickets)
     if (Dh == 128) {
-      if (algo == 2) XOT_WAVE(128, true); else XOT_WAVE(128, false);
+      if (algo == 3) XOT_WAVE(128, true, true); else if (algo == 2) XOT_WAVE(128, true, false); else XOT_WAVE(128, false, false);
       if (reduce) attn_decode_reduce_kernel<128><<<B * H, 128, 0, s>>>(ws_o, ws_ml, ctx_lens, out, H, nparts, pages_per_part);
     } else if (Dh == 64) {
-      if (algo == 2) XOT_WAVE(64, true); else XOT_WAVE(64, false);
+      if (algo == 3) XOT_WAVE(64, true, true); else if (algo == 2) XOT_WAVE(64, true, false); else XOT_WAVE(64, false, false);
       if (reduce) attn_decode_reduce_kernel<64><<<B * H, 64, 0, s>>>(ws_o, ws_ml, ctx_lens, out, H, nparts, pages_per_part);
     } else {
       return -1;

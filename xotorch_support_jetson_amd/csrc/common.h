@@ -61,6 +61,10 @@ __device__ __forceinline__ float group16_max(float v) {
 }
 
 __device__ __forceinline__ s16x8 ld16(const void* p) { return *reinterpret_cast<const s16x8*>(p); }
+// non-temporal 16-B load (global_load_dwordx4 ... nt): bytes read once per kernel (KV pages in decode)
+__device__ __forceinline__ s16x8 ld16nt(const void* p) {
+  return __builtin_nontemporal_load(reinterpret_cast<const s16x8*>(p));
+}
 __device__ __forceinline__ void st16(void* p, const s16x8& v) { *reinterpret_cast<s16x8*>(p) = v; }
 
 __device__ __forceinline__ float silu(float x) { return x / (1.0f + __expf(-x)); }
