@@ -194,9 +194,9 @@ def test_attn_decode(gpu, H, Hkv, Dh, ctx):
   q = torch.randn(B, H, Dh, device=gpu, dtype=torch.bfloat16)
   scale = 1 / math.sqrt(Dh)
   ref = R.attn_decode(q, kc, vc, bt, cl, scale)
-  for algo in (0, 1, 2, 3):  # workgroup kernel; wave kernel without / with page prefetch, + nt loads
+  for algo in (0, 1, 2, 3, 4):  # workgroup kernel; wave kernel without / with page prefetch, + nt loads; 8-wave
     for ppp in (1, 3, 4, 8, None):  # None: per-call choice from the batch
-      if algo == 0 and ppp in (1, 3):
+      if (algo == 0 and ppp in (1, 3)) or (algo == 4 and ppp is not None):  # 4: one partition only
         continue
       ws = K.DecodeWorkspace(B, H, Dh, maxb * 64, gpu, pages_per_part=ppp, algo=algo)
       ws.tickets = torch.zeros(B * H, dtype=torch.int32, device=gpu)  # partitions merged in-kernel by the last arriver
@@ -209,6 +209,24 @@ def test_attn_decode(gpu, H, Hkv, Dh, ctx):
       red = K.attn_decode(q, kc, vc, bt, cl, scale, ws)
       ws.tickets = tk
       assert torch.equal(again, out) and rel_err(red, out) < 1e-3, (algo, ppp)
+
+
+@pytest.mark.parametrize("H,Hkv,Dh", [(32, 8, 128), (32, 8, 64), (14, 2, 64)])
+@pytest.mark.parametrize("ctx", [[700, 65, 1, 1024], [1], [512, 3]])
+def test_attn_decode_auto_short_table(gpu, H, Hkv, Dh, ctx, monkeypatch):
+  """XOT_ATTN_WG8_PAGES=16: small batch over a block table of <= 16 pages takes the 8-wave single-partition
+  kernel."""
+  monkeypatch.setattr(K, "WG8_MAX_PAGES", 16)
+  torch.manual_seed(1)
+  B, maxb = len(ctx), 16
+  kc, vc = _make_cache(B * maxb + 3, Hkv, Dh, gpu)
+  bt = torch.randperm(B * maxb + 3, device=gpu)[:B * maxb].view(B, maxb).to(torch.int32).contiguous()
+  cl = torch.tensor(ctx, device=gpu, dtype=torch.int32)
+  q = torch.randn(B, H, Dh, device=gpu, dtype=torch.bfloat16)
+  ws = K.DecodeWorkspace(B, H, Dh, maxb * 64, gpu, algo=-1)
+  assert ws.partition(B, Hkv, maxb) == (maxb, 1, 4)
+  out = K.attn_decode(q, kc, vc, bt, cl, 1 / math.sqrt(Dh), ws)
+  assert rel_err(out, R.attn_decode(q, kc, vc, bt, cl, 1 / math.sqrt(Dh))) < 2e-2
 
 
 @pytest.mark.parametrize("algo", [1, 2])

@@ -9,7 +9,7 @@ for what in ${@:-base split split0}; do
     split)  XOT_SPLIT_DECODE=256 step split/split 400 python -u bench.py --steps 10 --warmup 3 ;;
     split0) XOT_SPLIT_DECODE=256 XOT_SPLIT_OFFSET=0 step split/split0 400 python -u bench.py --steps 10 --warmup 3 ;;
     eager)  XOT_SPLIT_DECODE=256 XOT_GRAPHS=0 step split/split_eager 400 python -u bench.py --steps 10 --warmup 3 ;;
-    attnnt) ;;
+    attnnt|wg8) ;;
     prof)   XOT_SPLIT_DECODE=256 prof split/prof 600 python3 "$R/bench.py" --steps 6 --warmup 3
             step split/breakdown 60 python tools/decode_breakdown.py "$(ls "$O"/split/prof/*/*kernel_trace.csv "$O"/split/prof/*kernel_trace.csv 2>/dev/null | head -1)" --steps 6 --json "$O/split/breakdown.json" ;;
   esac
@@ -19,4 +19,12 @@ if [ "$1" = attnnt ]; then
   step attnnt/test 200 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k attn_decode
   step attnnt/base 400 python -u bench.py --steps 10 --warmup 3
   XOT_ATTN_DECODE=3 step attnnt/nt 400 python -u bench.py --steps 10 --warmup 3
+fi
+# wg8: 8-wave single-partition decode attention at small batch vs the 4-wave split + merge (XOT_ATTN_WG8_PAGES=0)
+if [ "$1" = wg8 ]; then
+  step wg8/test 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k attn_decode tests/test_runner_gpu.py tests/test_split_decode_gpu.py
+  step wg8/b1_new 300 python -u bench.py --model llama-3-8b --batch-per-gpu 1 --steps 32 --warmup 4
+  XOT_ATTN_WG8_PAGES=0 step wg8/b1_old 300 python -u bench.py --model llama-3-8b --batch-per-gpu 1 --steps 32 --warmup 4
+  step wg8/b1_new2 300 python -u bench.py --model llama-3-8b --batch-per-gpu 1 --steps 32 --warmup 4
+  step wg8/b1_70b 400 python -u bench.py --model llama-3-70b --batch-per-gpu 1 --steps 16 --warmup 3
 fi

@@ -68,8 +68,11 @@ __device__ __forceinline__ bool partition_arrive_last(int* tickets, int slot, in
   return last;
 }
 
-template <int DH>
-__global__ __launch_bounds__(256) void attn_decode_kernel(
+// NW waves share the pages of one (sequence, KV head, partition): 4 (algo 0), or 8 for one partition
+// over a short context at small batch (algo 4: at most two pages per wave and no merge launch, where
+// each further page a wave walks costs a dependent page-table -> K / V latency of ~3.5 us)
+template <int DH, int NW = 4>
+__global__ __launch_bounds__(NW * 64) void attn_decode_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
     const int32_t* __restrict__ block_tables, int max_blocks, const int32_t* __restrict__ ctx_lens,
     uint16_t* __restrict__ out, float* __restrict__ ws_o, float* __restrict__ ws_ml, int H, int Hkv,
@@ -77,9 +80,9 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
   constexpr int KS = DH / 32;   // MFMA k-steps over the head dim
   constexpr int NDT = DH / 16;  // 16-wide d tiles of the output
   constexpr int PLD = PAGE + 8;
-  __shared__ __attribute__((aligned(16))) uint16_t p_lds[4][16 * PLD];
-  __shared__ float ml_lds[4][16][2];
-  __shared__ float o_lds[4][16][DH];
+  __shared__ __attribute__((aligned(16))) uint16_t p_lds[NW][16 * PLD];
+  __shared__ float ml_lds[NW][16][2];
+  __shared__ float o_lds[NW][16][DH];
 
   const int part = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -115,7 +118,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
 
   const int32_t* bt = block_tables + (size_t)b * max_blocks;
   uint16_t* pl = p_lds[wave];
-  for (int p = p_begin + wave; p < p_end; p += 4) {
+  for (int p = p_begin + wave; p < p_end; p += NW) {
     const long page = min(max(bt[p], 0), num_pages - 1);
     const uint16_t* kb = kc + ((size_t)page * Hkv + kvh) * PAGE * DH;
     const uint16_t* vb = vc + ((size_t)page * Hkv + kvh) * DH * PAGE;
@@ -181,7 +184,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
     wave_lds_sync();
   }
 
-  // combine the 4 waves (same rows, disjoint pages)
+  // combine the NW waves (same rows, disjoint pages)
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     l[r] = group16_sum(l[r]);
@@ -195,14 +198,14 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
 #pragma unroll
     for (int r = 0; r < 4; ++r) o_lds[wave][4 * g + r][16 * dt + c] = o[dt][r];
   __syncthreads();
-  for (int e = threadIdx.x; e < G * DH; e += 256) {
+  for (int e = threadIdx.x; e < G * DH; e += NW * 64) {
     const int row = e / DH, d = e % DH;
     float M = NEG_BIG;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) M = fmaxf(M, ml_lds[w][row][0]);
+    for (int w = 0; w < NW; ++w) M = fmaxf(M, ml_lds[w][row][0]);
     float L = 0.f, O = 0.f;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
+    for (int w = 0; w < NW; ++w) {
       const float f = exp2f(ml_lds[w][row][0] - M);
       L += ml_lds[w][row][1] * f;
       O += o_lds[w][row][d] * f;
@@ -225,7 +228,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
     __syncthreads();
     if (threadIdx.x == 0) last_s = partition_arrive_last(tickets, b * Hkv + kvh, nparts);
     __syncthreads();
-    if (last_s) combine_parts<DH>(ws_o, ws_ml, out, b, kvh, G, H, nparts, threadIdx.x, 256);
+    if (last_s) combine_parts<DH>(ws_o, ws_ml, out, b, kvh, G, H, nparts, threadIdx.x, NW * 64);
   }
 }
 
@@ -434,7 +437,7 @@ int launch_attn_decode(const uint16_t* q, const uint16_t* kc, const uint16_t* vc
   if (H % Hkv != 0 || H / Hkv > 16) return -1;
   dim3 grid(nparts, Hkv, B);
   const float sl = scale * LOG2E;
-  if (algo != 0) {  // wave per (sequence, KV head, partition)
+  if (algo != 0 && algo != 4) {  // wave per (sequence, KV head, partition)
     const int units = B * Hkv * nparts, wgs = (units + 3) / 4;
 #define XOT_WAVE(DHV, PFV, NTV)                                                                                  \
   attn_decode_wave_kernel<DHV, PFV, NTV><<<wgs, 256, 0, s>>>(q, kc, vc, block_tables, max_blocks, ctx_lens, out, ws_o, \
@@ -449,6 +452,18 @@ int launch_attn_decode(const uint16_t* q, const uint16_t* kc, const uint16_t* vc
       return -1;
     }
 #undef XOT_WAVE
+    return 0;
+  }
+  if (algo == 4) {  // 8 waves, one partition (the caller passes nparts 1)
+    if (nparts != 1) return -1;
+    if (Dh == 128)
+      attn_decode_kernel<128, 8><<<grid, 512, 0, s>>>(q, kc, vc, block_tables, max_blocks, ctx_lens, out, ws_o, ws_ml,
+                                                      H, Hkv, pages_per_part, 1, sl, num_pages, nullptr);
+    else if (Dh == 64)
+      attn_decode_kernel<64, 8><<<grid, 512, 0, s>>>(q, kc, vc, block_tables, max_blocks, ctx_lens, out, ws_o, ws_ml,
+                                                     H, Hkv, pages_per_part, 1, sl, num_pages, nullptr);
+    else
+      return -1;
     return 0;
   }
   if (Dh == 128) {

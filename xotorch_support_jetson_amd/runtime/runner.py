@@ -86,7 +86,8 @@ class ShardRunner:
     # static per graph) follows the contexts actually served instead of max_ctx -- at max_ctx 8192 and
     # contexts of a few hundred tokens the full width split every sequence into 4 mostly empty partitions
     # plus a merge pass
-    self._widths = sorted({w for w in (8, 32) if w < self.width} | {self.width})
+    # (16 pages: the widest table the 8-wave single-partition attention takes at small batch, ops/kernels.py)
+    self._widths = sorted({w for w in (8, 16, 32) if w < self.width} | {self.width})
     # host staging of the step inputs, double-buffered: a step's async copies read one set while the host
     # fills the other for the next step, so the host can queue a step behind the one still copying (with
     # one set it had to wait for the previous step's copies before writing the next step's inputs)
