@@ -9,7 +9,7 @@ for what in ${@:-base split split0}; do
     split)  XOT_SPLIT_DECODE=256 step split/split 400 python -u bench.py --steps 10 --warmup 3 ;;
     split0) XOT_SPLIT_DECODE=256 XOT_SPLIT_OFFSET=0 step split/split0 400 python -u bench.py --steps 10 --warmup 3 ;;
     eager)  XOT_SPLIT_DECODE=256 XOT_GRAPHS=0 step split/split_eager 400 python -u bench.py --steps 10 --warmup 3 ;;
-    attnnt|wg8) ;;
+    attnnt|wg8|slab) ;;
     prof)   XOT_SPLIT_DECODE=256 prof split/prof 600 python3 "$R/bench.py" --steps 6 --warmup 3
             step split/breakdown 60 python tools/decode_breakdown.py "$(ls "$O"/split/prof/*/*kernel_trace.csv "$O"/split/prof/*kernel_trace.csv 2>/dev/null | head -1)" --steps 6 --json "$O/split/breakdown.json" ;;
   esac
@@ -27,4 +27,10 @@ if [ "$1" = wg8 ]; then
   XOT_ATTN_WG8_PAGES=0 step wg8/b1_old 300 python -u bench.py --model llama-3-8b --batch-per-gpu 1 --steps 32 --warmup 4
   step wg8/b1_new2 300 python -u bench.py --model llama-3-8b --batch-per-gpu 1 --steps 32 --warmup 4
   step wg8/b1_70b 400 python -u bench.py --model llama-3-70b --batch-per-gpu 1 --steps 16 --warmup 3
+fi
+# slab: GEMM tuner charging the split-K slab read-back (default) vs GEMM time only
+if [ "$1" = slab ]; then
+  XOT_HOME=$O/slab/home_new step slab/new 400 python -u bench.py --steps 10 --warmup 3
+  XOT_SLAB_TBPS=0 XOT_HOME=$O/slab/home_old step slab/old 400 python -u bench.py --steps 10 --warmup 3
+  XOT_HOME=$O/slab/home_new step slab/new_again 400 python -u bench.py --steps 10 --warmup 3
 fi

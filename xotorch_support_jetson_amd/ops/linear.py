@@ -184,7 +184,7 @@ def _default_table_path():
     dev = torch.cuda.get_device_name(torch.cuda.current_device()).replace(" ", "_").replace("/", "_")
     from ..helpers import xot_home
     # settings that change the candidate sets are part of the name, so a table never answers for another
-    tag = f"{os.environ.get('XOT_GEMM', 'auto')}-{STREAM_MAX_M}-{BIG_MIN_M}"
+    tag = f"{os.environ.get('XOT_GEMM', 'auto')}-{STREAM_MAX_M}-{BIG_MIN_M}-{SLAB_TBPS:g}"
     return str(xot_home() / "gemm" / f"{dev}-{st.st_size:x}-{int(st.st_mtime):x}-{tag}.json")
   except Exception:  # noqa: BLE001 - no table then; tuning still works in memory
     return None
@@ -377,7 +377,7 @@ class GemmPolicy:
     times = {}
     for cfg in cands:
       try:
-        times[cfg] = self._time(lambda: _shuffled_call(x, w, bias, residual, epi, y, cfg))
+        times[cfg] = self._time(lambda: _shuffled_call(x, w, bias, residual, epi, y, cfg)) + _slab_read_ms(cfg, M, N)
       except RuntimeError:
         pass
     got = min(times, key=times.get) if times else cands[0]
@@ -411,6 +411,17 @@ class GemmPolicy:
 
 def _ws_elems(cfg, M, N) -> int:
   return cfg[2] * M * N if len(cfg) == 3 and cfg[0] != "sk" and cfg[2] > 1 else 0
+
+
+# HBM rate (TB/s) at which the consumer of split-K fp32 slabs (slab reduce, fused reduce + RoPE / + residual +
+# RMSNorm) reads them back: a K-split candidate's timed GEMM is charged that read, so the tuner ranks the
+# GEMM + reduce pair rather than the GEMM alone (XOT_SLAB_TBPS=0: GEMM time only)
+SLAB_TBPS = float(os.environ.get("XOT_SLAB_TBPS", "5.0"))
+
+
+def _slab_read_ms(cfg, M, N) -> float:
+  n = _ws_elems(cfg, M, N)
+  return n * 4 / (SLAB_TBPS * 1e9) if n and SLAB_TBPS > 0 else 0.0
 
 
 policy = GemmPolicy()
