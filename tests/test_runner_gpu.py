@@ -289,8 +289,8 @@ def test_fp8_weights_runner(gpu, name, monkeypatch):
 
 
 def test_graph_table_width_classes(gpu):
-  """Decode graphs per block-table width class (max_ctx 4096: classes of 8, 32 and 64 pages): sequences whose
-  contexts cross 512 and 2048 tokens switch graphs mid-run (split-KV partitioning follows the narrower
+  """Decode graphs per block-table width class (max_ctx 4096: classes of 8, 16, 32 and 64 pages): sequences
+  whose contexts cross 512 and 2048 tokens switch graphs mid-run (split-KV partitioning follows the narrower
   tables) and still match the eager path; a batch mixing a short and a long sequence uses the wide class."""
   name = "tiny-llama-d64"
   c = preset(name)
@@ -298,7 +298,7 @@ def test_graph_table_width_classes(gpu):
   sh = Shard(name, 0, L - 1, L)
   g = ShardRunner(c, sh, gpu, max_batch=8, max_ctx=4096, use_graphs=True)
   e = ShardRunner(c, sh, gpu, max_batch=8, max_ctx=4096, use_graphs=False)
-  assert g._widths == [8, 32, 64]
+  assert g._widths == [8, 16, 32, 64]
   gen = torch.Generator().manual_seed(11)
   lens = {"a": 508, "b": 2044, "s": 9}
   for rid, n in lens.items():
@@ -310,7 +310,7 @@ def test_graph_table_width_classes(gpu):
       tok = torch.randint(0, c.vocab_size, (len(rids),), generator=gen, dtype=torch.int32)
       x, y = g.forward(rids, [1] * len(rids), tok), e.forward(rids, [1] * len(rids), tok)
       assert torch.allclose(x, y, atol=3e-2, rtol=3e-2), (step, rids, (x - y).abs().max().item())
-  assert {w for _, w in g._graphs} == {8, 32, 64}
+  assert {w for _, w in g._graphs} == {8, 16, 32, 64}
 
 
 @pytest.mark.parametrize("name", ["tiny-deepseek-v2", "tiny-llama-d64"])
