@@ -9,7 +9,7 @@ for what in ${@:-base split split0}; do
     split)  XOT_SPLIT_DECODE=256 step split/split 400 python -u bench.py --steps 10 --warmup 3 ;;
     split0) XOT_SPLIT_DECODE=256 XOT_SPLIT_OFFSET=0 step split/split0 400 python -u bench.py --steps 10 --warmup 3 ;;
     eager)  XOT_SPLIT_DECODE=256 XOT_GRAPHS=0 step split/split_eager 400 python -u bench.py --steps 10 --warmup 3 ;;
-    attnnt|wg8|slab) ;;
+    attnnt|wg8|slab|grp) ;;
     prof)   XOT_SPLIT_DECODE=256 prof split/prof 600 python3 "$R/bench.py" --steps 6 --warmup 3
             step split/breakdown 60 python tools/decode_breakdown.py "$(ls "$O"/split/prof/*/*kernel_trace.csv "$O"/split/prof/*kernel_trace.csv 2>/dev/null | head -1)" --steps 6 --json "$O/split/breakdown.json" ;;
   esac
@@ -33,4 +33,10 @@ if [ "$1" = slab ]; then
   XOT_HOME=$O/slab/home_new step slab/new 400 python -u bench.py --steps 10 --warmup 3
   XOT_SLAB_TBPS=0 XOT_HOME=$O/slab/home_old step slab/old 400 python -u bench.py --steps 10 --warmup 3
   XOT_HOME=$O/slab/home_new step slab/new_again 400 python -u bench.py --steps 10 --warmup 3
+fi
+# grp: grouped raster of tall gemm_big grids -- kernel tests, GEMM shapes at prefill M, headline prefill time
+if [ "$1" = grp ]; then
+  step grp/test 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "gemm_big or moe"
+  step grp/gemm 500 python -u tools/bench_gemm_sk.py --ms 2048,8192 --json "$O/grp/gemm.json"
+  step grp/headline 400 python -u bench.py --steps 10 --warmup 3
 fi
