@@ -151,8 +151,15 @@ def test_checkpoint_selection_rejects_mixed_partitions(tmp_path):
   # iteration 4 now lacks layers 2..N-1 (one peer's save failed): the complete iteration 2 loads
   it, _ = select_checkpoint_files(tmp_path, Shard(MODEL, 0, N - 1, N))
   assert it == 2
-  assert select_checkpoint_files(tmp_path, Shard(MODEL, 0, 1, N))[0] == 4  # ... which covers a first stage
+  # ... and so does a first stage, although iteration 4 covers it: every stage of a ring that reloads from
+  # one directory must resume from the SAME iteration; an explicit iteration is honoured
+  assert select_checkpoint_files(tmp_path, Shard(MODEL, 0, 1, N))[0] == 2
+  assert select_checkpoint_files(tmp_path, Shard(MODEL, 0, 1, N), iteration=4)[0] == 4
+  with pytest.raises(FileNotFoundError, match="no file for layers"):
+    select_checkpoint_files(tmp_path, Shard(MODEL, 1, 3, N), iteration=4)
   (d / f"000-{N - 1:03d}-of-{N:03d}-000002.safetensors").unlink()
+  # no iteration covers the whole model (each host saved its own layers): the newest covering the shard
+  assert select_checkpoint_files(tmp_path, Shard(MODEL, 0, 1, N))[0] == 4
   with pytest.raises(FileNotFoundError, match="no file for layers"):
     select_checkpoint_files(tmp_path, Shard(MODEL, 0, N - 1, N))
 

@@ -184,7 +184,7 @@ def _run_rank0(srv, reqs, timeout=150):
   return out
 
 
-def _worker2(rank, world, port, q, pages, fault):
+def _worker2(rank, world, port, q, pages, fault, free_cap=256, slack=3, reqs=None):
   import datetime
   from xotorch_support_jetson_amd.parallel.health import HealthMonitor
   from xotorch_support_jetson_amd.parallel.ring_serve import control_group, min_pool_pages, ring_shards
@@ -197,7 +197,7 @@ def _worker2(rank, world, port, q, pages, fault):
   def make_runner(r, w, ctl):
     shard = ring_shards(MODEL, c.num_layers, w, ctl)[r]
     # rank-dependent pool sizes: the ring plans with the smallest one
-    runner = ShardRunner(c, shard, "cpu", max_batch=8, max_ctx=256, num_pages=pages + 3 * r)
+    runner = ShardRunner(c, shard, "cpu", max_batch=8, max_ctx=256, num_pages=pages + slack * r)
     return runner, min_pool_pages(runner, w, ctl)
 
   ctl = control_group()
@@ -205,10 +205,10 @@ def _worker2(rank, world, port, q, pages, fault):
   # 5 s: a loaded CI host (parallel test workers) must not make a live peer look dead
   mon = HealthMonitor(rank, world, interval=0.1, timeout=5.0).start() if fault else None
   srv = RingServer(runner, rank, world, P2PTransport(rank, world, monitor=mon), ctl, step_tokens=32, monitor=mon,
-                   make_runner=make_runner, pool_pages=pool)
+                   make_runner=make_runner, pool_pages=pool, free_cap=free_cap)
   res = None
   if rank == 0:
-    res = _run_rank0(srv, LONG)
+    res = _run_rank0(srv, reqs or LONG)
   else:
     srv.serve_forever()
   q.put((rank, res, dict(srv.stats), srv.pool_pages, srv.r.bm.num_free == srv.r.bm.num_blocks))
@@ -217,11 +217,11 @@ def _worker2(rank, world, port, q, pages, fault):
   os._exit(0)
 
 
-def _launch2(world, pages, fault=""):
+def _launch2(world, pages, fault="", **kw):
   ctx = mp.get_context("spawn")
   q = ctx.Queue()
   port = _free_port()
-  ps = [ctx.Process(target=_worker2, args=(r, world, port, q, pages, fault)) for r in range(world)]
+  ps = [ctx.Process(target=_worker2, args=(r, world, port, q, pages, fault), kwargs=kw) for r in range(world)]
   for p in ps:
     p.start()
   want = world - (1 if fault.startswith("kill") else 0)
@@ -247,6 +247,20 @@ def test_ring_serve_chunked_prefill_and_kv_pressure(world):
   assert stats["chunks"] > 0 and stats["preempted"] > 0, stats
   assert all(res[r][2] == 5 for r in res)  # min over ranks (rank r has 5 + 3r pages)
   assert all(res[r][3] for r in res)  # every rank's pool is empty again
+
+
+SHORT = [(chr(ord("A") + i), 4, 3) for i in range(8)]  # finish together, in the same lane steps
+
+
+def test_ring_serve_frees_beyond_one_header_reach_followers_first():
+  """Equal pools on every rank (no slack) and one free per header: when several requests finish at once,
+  rank 0 has already dropped their pages and plans the next step into them, so every pending free must
+  reach the followers ahead of that step (free-only headers), or a follower's pool runs dry."""
+  ref = _ref_tokens(SHORT)
+  res = _launch2(2, pages=4, free_cap=1, slack=0, reqs=SHORT)
+  out, stats, pool, _ = res[0]
+  assert out == ref
+  assert pool == 4 and all(res[r][3] for r in res)
 
 
 def test_ring_serve_recovers_from_a_dead_peer():

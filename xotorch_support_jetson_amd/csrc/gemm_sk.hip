@@ -202,8 +202,8 @@ __global__ __launch_bounds__(512, 1) void gemm_sk_kernel(const uint16_t* __restr
     __syncthreads();       // all LDS reads of this segment done (no LDS-DMA in flight: vmcnt(0) above)
 
     // ---- stream-K fixup: which groups share this column tile?
-    const int g_first = sk_group_of((long)tile * T, G, total);
-    const int g_last = sk_group_of((long)tile * T + T - 1, G, total);
+    int g_first = sk_group_of((long)tile * T, G, total);
+    int g_last = sk_group_of((long)tile * T + T - 1, G, total);
     bool last = true;
     if (g_first != g_last) {
       int* sh = reinterpret_cast<int*>(smem);
@@ -233,21 +233,34 @@ __global__ __launch_bounds__(512, 1) void gemm_sk_kernel(const uint16_t* __restr
         }
       } else {
         if (tid == 0) {
+          int stale = 0;
           for (int g = g_first; g <= g_last; ++g) {
             if (g == group) continue;
             int* f = flag_of(g);
             // bounded: a part that holds a ticket is resident and publishes within microseconds; the bound
             // (seconds) only keeps a broken invariant from hanging the GPU
-            for (int spin = 0; spin < (1 << 24) &&
-                               __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0; ++spin)
+            int spin = 0;
+            for (; spin < (1 << 24) && __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0; ++spin)
               __builtin_amdgcn_s_sleep(2);
+            stale |= spin == (1 << 24);
             __hip_atomic_store(f, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           }
           __hip_atomic_store(&tickets[tk], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          sh[1] = stale;
         }
         __syncthreads();
+        if (sh[1]) {
+          // a peer part never published (broken invariant): poison the tile with NaN so the failure shows
+          // in every consumer instead of passing a sum over stale / unwritten partials
+#pragma unroll
+          for (int i = 0; i < MT; ++i)
+#pragma unroll
+            for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __builtin_nanf("")};
+          g_last = group;  // skip the summation below
+          g_first = group;
+        }
         // sum the parts in group order (own accumulators at this group's position: deterministic output),
         // one 16-row slice of the wave's tile at a time (each part's 4 loads per lane in flight together)
 #pragma unroll

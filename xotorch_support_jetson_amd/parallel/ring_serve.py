@@ -54,7 +54,7 @@ from ..ops import kernels as K
 from .health import FaultInjector, HealthMonitor, PeerFailure, reform_ring, wait_work
 
 STEP_TOKENS = int(os.environ.get("XOT_MAX_STEP_TOKENS", "8192"))
-FREE_CAP = 256  # frees per header (more wait for the next one)
+FREE_CAP = 256  # frees per header (more go ahead of the step in free-only headers)
 
 
 @dataclass
@@ -78,8 +78,9 @@ class RingServer:
   def __init__(self, runner, rank: int, world: int, transport, ctl_group=None, eos_ids: Sequence[int] = (),
                top_k: int = 35, seed: int = 1234, max_batch: Optional[int] = None, step_tokens: Optional[int] = None,
                monitor: Optional[HealthMonitor] = None, make_runner: Optional[Callable] = None,
-               pool_pages: Optional[int] = None):
+               pool_pages: Optional[int] = None, free_cap: int = FREE_CAP):
     self.r, self.rank, self.world, self.t = runner, rank, world, transport
+    self.free_cap = max(1, free_cap)  # frees per header
     self.ctl = ctl_group  # gloo group of the control plane (headers); None with world 1
     self.eos = set(int(e) for e in eos_ids)
     self.top_k = top_k
@@ -114,7 +115,7 @@ class RingServer:
     self._inflight: List[Optional[list]] = [None] * self.lanes  # per lane: the step's (req, n) awaiting ids
     # rank 0 plans with the smallest pool of the ring (exact for every rank: same appends everywhere)
     self.pool_pages = min(pool_pages or runner.bm.num_blocks, runner.bm.num_blocks)
-    self.hcap = 4 + 3 * self.max_batch + FREE_CAP
+    self.hcap = 4 + 3 * self.max_batch + self.free_cap
 
   # ------------------------------------------------------------------ rank-0 API side
   def submit(self, rid: str, ids: Sequence[int], temp: float = 0.0, max_tokens: int = 256) -> None:
@@ -302,7 +303,10 @@ class RingServer:
       ids += seq[q.fed:q.fed + n]
       if n > 1:
         self.stats["chunks"] += 1
-    free, self._free = self._free[:FREE_CAP], self._free[FREE_CAP:]
+    # Rank 0 has already dropped these pages and planned this step into them: every free must reach the
+    # other ranks AHEAD of the step (headers arrive in order), so frees beyond one header's cap go first in
+    # free-only headers.
+    free = self._flush_frees()
     if self.world > 1:
       self._send_header(self._header(items, free, stop))
     if items:
@@ -310,6 +314,15 @@ class RingServer:
       self._inflight[lane] = (plan, tok)
       self.stats["steps"] += 1
     return True
+
+  def _flush_frees(self) -> List[int]:
+    """Send free-only headers until at most free_cap frees are pending; return (and clear) those."""
+    if self.world > 1:
+      while len(self._free) > self.free_cap:
+        self._send_header(self._header([], self._free[:self.free_cap], False))
+        self._free = self._free[self.free_cap:]
+    free, self._free = self._free, []
+    return free
 
   def _idle_lanes(self) -> bool:
     return all(s is None for s in self._inflight)
@@ -351,11 +364,7 @@ class RingServer:
         self._wake.clear()
       lane = (lane + 1) % self.lanes
     if self.world > 1:  # stop (with the last frees) travels the ring; followers exit on it
-      while len(self._free) > FREE_CAP:
-        self._send_header(self._header([], self._free[:FREE_CAP], False))
-        self._free = self._free[FREE_CAP:]
-      free, self._free = self._free, []
-      self._send_header(self._header([], free, True))
+      self._send_header(self._header([], self._flush_frees(), True))
     self.t.drain()
     self._drain_ctl()
     if self.monitor is not None:

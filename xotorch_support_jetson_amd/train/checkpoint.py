@@ -57,16 +57,28 @@ def _check_iteration(cks, it: int, shard: Shard) -> List[Path]:
   return [p for *_, p in parts]
 
 
-def select_checkpoint_files(directory: str | Path, shard: Shard) -> Tuple[int, List[Path]]:
-  """(iteration, files) of the newest COMPLETE saved iteration for `shard.model_id`: one partition of the
-  model whose layer ranges are pairwise disjoint and cover the shard's layers.  A newer iteration that is
-  not (one peer's save of a multi-node checkpoint failed, or a re-split run left overlapping files) is
-  skipped with a warning; if no iteration qualifies, the newest one's error is raised."""
+def select_checkpoint_files(directory: str | Path, shard: Shard, iteration: Optional[int] = None) -> Tuple[int, List[Path]]:
+  """(iteration, files) to load `shard` from: one partition of the model whose layer ranges are pairwise
+  disjoint.  With `iteration` given, exactly that iteration (ValueError / FileNotFoundError if it does not
+  cover the shard).  Otherwise the newest iteration that covers the WHOLE model -- so every stage of a ring
+  loading from a shared directory picks the same iteration, even when a peer died mid-save and left the
+  newest one with a gap outside this shard -- and, when no iteration covers the whole model (each host of a
+  multi-host ring saved only its own layers locally), the newest one that covers this shard.  Skipped
+  iterations are reported; if none qualifies, the newest one's error is raised."""
   cks = list_checkpoints(directory, shard.model_id)
   if not cks:
     raise FileNotFoundError(f"no checkpoints for {shard.model_id} under {directory}")
+  if iteration is not None:
+    return iteration, _check_iteration(cks, iteration, shard)
+  whole = Shard(shard.model_id, 0, shard.n_layers - 1, shard.n_layers)
+  its = sorted({c[0] for c in cks}, reverse=True)
+  for it in its:
+    try:
+      return it, _check_iteration(cks, it, whole)
+    except (ValueError, FileNotFoundError):
+      continue
   first_err = None
-  for it in sorted({c[0] for c in cks}, reverse=True):
+  for it in its:
     try:
       files = _check_iteration(cks, it, shard)
     except (ValueError, FileNotFoundError) as e:

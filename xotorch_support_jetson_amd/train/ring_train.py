@@ -32,10 +32,12 @@ def _model_dir(model_id: str) -> Optional[Path]:
   return p if (p / "config.json").exists() else None
 
 
-def _load_stage(a: dict, cfg, mdir, shard, dev, src_dir: Optional[str], rank: int):
+def _load_stage(a: dict, cfg, mdir, shard, dev, src_dir: Optional[str], rank: int, iteration: Optional[int] = None):
   """Weights of `shard` (HF files or random init, then the newest complete checkpoint in `src_dir` if any)
   and its ShardTrainer (optimizer moments merged from every sidecar of that iteration: after a re-partition
-  a stage's layers come from several old stages' files).  Returns (weights, trainer, iteration or 0)."""
+  a stage's layers come from several old stages' files).  `iteration`: the one iteration every stage loads
+  (chosen once for the whole model by the caller); None picks the newest complete one.  Returns (weights,
+  trainer, iteration or 0)."""
   from ..models.weights import copy_weights_into, from_hf_state_dict, load_hf_weights, random_weights
   from ..train import checkpoint as ck
   from ..train.trainer import ShardTrainer
@@ -46,7 +48,7 @@ def _load_stage(a: dict, cfg, mdir, shard, dev, src_dir: Optional[str], rank: in
     w = random_weights(cfg, shard, dev, seed=0)
   it, files = 0, []
   if src_dir and ck.list_checkpoints(src_dir, model):
-    it, files = ck.select_checkpoint_files(src_dir, shard)  # one partition, no overlapping files
+    it, files = ck.select_checkpoint_files(src_dir, shard, iteration)  # one partition, no overlapping files
     sd = ck._gather_tensors(files, shard, cfg.tie_word_embeddings)
     copy_weights_into(w, from_hf_state_dict(sd, cfg, shard, device=dev))
     if rank == 0:
@@ -103,6 +105,7 @@ def _worker(rank: int, world: int, port: int, a: dict) -> None:
   hb_timeout = float(os.environ.get("XOT_HEARTBEAT_TIMEOUT", "30"))
   injector = None  # the environment's (tests) on the first ring; none after a re-form
   generation, src_dir, first_epoch = 0, a.get("resume"), 0
+  src_it = None  # the iteration every stage loads after a re-form (picked once, for the whole model)
 
   class _Shim:  # save_shard_checkpoint wants engine.runner.weights / engine.trainer
     pass
@@ -112,7 +115,7 @@ def _worker(rank: int, world: int, port: int, a: dict) -> None:
       shard = Shard(model, 0, cfg.num_layers - 1, cfg.num_layers)
     else:  # memory-weighted layer ranges in ring order (parallel/ring_serve.py:ring_shards)
       shard = ring_shards(model, cfg.num_layers, world, control_group() if world > 1 else None)[rank]
-    w, tr, _ = _load_stage(a, cfg, mdir, shard, dev, src_dir, rank)
+    w, tr, _ = _load_stage(a, cfg, mdir, shard, dev, src_dir, rank, src_it)
     mon = None
     if dp:
       from ..parallel.data_parallel import DataParallelTrainer
@@ -163,10 +166,12 @@ def _worker(rank: int, world: int, port: int, a: dict) -> None:
       from ..train import checkpoint as ck
       save = a.get("save_dir")
       if save and ck.list_checkpoints(save, model):
+        # one iteration for every stage and for the epoch counter: the newest that covers the WHOLE model
+        # (a peer that died mid-save leaves the newest iteration with a gap another stage would not see)
         src_dir = save
-        first_epoch = ck.select_checkpoint_files(save, Shard(model, 0, cfg.num_layers - 1, cfg.num_layers))[0]
+        src_it = first_epoch = ck.select_checkpoint_files(save, Shard(model, 0, cfg.num_layers - 1, cfg.num_layers))[0]
       else:  # nothing saved by this run yet: restart it from its initial weights
-        first_epoch = 0
+        first_epoch, src_it = 0, None
       if rank == 0:
         print(f"restarting at epoch {first_epoch + 1} on {world} rank(s)", flush=True)
   if world > 1:
@@ -273,7 +278,19 @@ def run_ring(args) -> int:
     p.start()
   for p in procs:
     p.join()
+  rc = procs[0].exitcode or 0
   for r, p in enumerate(procs[1:], 1):
-    if p.exitcode:  # the survivors re-formed the ring without it (rank 0's own exit code says if they finished)
-      print(f"training rank {r} exited with code {p.exitcode}", flush=True)
-  return procs[0].exitcode or 0
+    if not p.exitcode:
+      continue
+    if _peer_failure_exit(p.exitcode):  # the survivors re-formed the ring without it
+      print(f"training rank {r} died (exit {p.exitcode}); the ring recovered without it", flush=True)
+    else:  # a crash (uncaught exception ...) is a failure of the run even if the survivors finished
+      print(f"training rank {r} failed with exit code {p.exitcode}", flush=True)
+      rc = rc or p.exitcode
+  return rc
+
+
+def _peer_failure_exit(code: int) -> bool:
+  """Exit codes of a rank that vanished (killed by a signal, or the test fault injector's hard exit 17:
+  parallel/health.py) -- what the ring's recovery is for -- as opposed to a rank that raised."""
+  return code < 0 or code == 17
