@@ -115,6 +115,8 @@ def main():
   if world > 1:
     dist.barrier()
   sync()
+  stage.start_timing()  # device events around each tick: stage work vs. waiting for the previous stage
+  sent0 = transport.sent_bytes
   t0 = time.perf_counter()
   toks = run_decode_steps(stage, mbs, args.steps, first_tokens=toks if stage.last else None, record=rec)
   transport.drain()
@@ -126,6 +128,15 @@ def main():
     e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     dist.all_reduce(e, op=dist.ReduceOp.MAX)
     elapsed = float(e.item())
+
+  # per-rank diagnostics (after the timed region): a multi-GPU run that under-delivers shows which stage is
+  # the slow one (stage_ms) and where the ring starves (recv_wait_ms)
+  mine = dict(rank=rank, layers=f"{shard.start_layer}-{shard.end_layer}", **stage.timing(),
+              send_mb_per_step=round((transport.sent_bytes - sent0) / args.steps / 1e6, 3))
+  per_rank = [mine]
+  if world > 1:
+    per_rank = [None] * world
+    dist.all_gather_object(per_rank, mine)
 
   if rec and stage.samples:
     with open(args.dump_tokens, "w") as f:
@@ -160,7 +171,8 @@ def main():
       },
       "extra": {"prefill_s": round(t_prefill, 2), "init_s": round(t_init, 2),
                 "tokens_per_s_per_gpu": round(tps / world, 2),
-                "reference_derived_ceiling_tok_s": 0.57 if world == 8 else (2.3 if world == 2 else None)},
+                "reference_derived_ceiling_tok_s": 0.57 if world == 8 else (2.3 if world == 2 else None),
+                "per_rank": per_rank},
     }
     print(json.dumps(out), flush=True)
   if world > 1:

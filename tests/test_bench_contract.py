@@ -60,6 +60,10 @@ def test_bench_driver_command_many_ranks(n, tmp_path):
   assert len(lines) == 1, r.stdout
   d = json.loads(lines[0])
   assert d["n_gpus"] == n and d["config"]["global_batch"] == 2 * n and d["config"]["parallelism"].startswith(f"pp{n}")
+  # per-rank diagnostics: one entry per rank with its layer range and bytes handed on per step
+  pr = d["extra"]["per_rank"]
+  assert [p["rank"] for p in pr] == list(range(n)) and all(p["send_mb_per_step"] > 0 for p in pr)
+  assert pr[0]["layers"].startswith("0-") and pr[-1]["layers"].endswith("-7")
   t1, tn = json.load(open(tmp_path / "t1.json")), json.load(open(tmp_path / "tn.json"))
   # with the split head a round's ids are drawn at the start of the next round by the first stage, so the
   # ring's list starts with the prefill token and the single-process list with the first decode token

@@ -870,3 +870,41 @@ def test_gemm_kgroup(gpu, resid):
     a, b = int(koff[e]), int(koff[e + 1])
     ref = x[:, a:b].float() @ w[:, a:b].float().t() + (y0[e].float() if resid else 0)
     assert rel_err(y[e], ref) < 1e-2 if ref.norm() > 0 else y[e].abs().max() == 0
+
+
+# ------------------------------------------------------------------ stream-K GEMM (the headline's gate/up)
+@pytest.mark.parametrize("M", [256, 300, 512, 1024, 2048])
+@pytest.mark.parametrize("N,Kd", [(2048, 4096), (7168, 8192)])  # 7168 = an eighth of 70B's 57344 gate/up
+@pytest.mark.parametrize("epi,f32", [("none", True), ("none", False), ("resid", False), ("silu", False)])
+def test_gemm_sk(gpu, M, N, Kd, epi, f32):
+  """csrc/gemm_sk.hip (persistent 256 x 256 tiles, k steps dealt evenly over the CUs, partial tiles combined by
+  the last arriver in group order) vs the fp32 reference: every epilogue, fp32 / bf16 out, masked row tiles;
+  two runs give identical bits (the fix-up order is fixed) and every ticket / flag word is zero again."""
+  from xotorch_support_jetson_amd.ops._ext import require
+  from xotorch_support_jetson_amd.ops.weights_layout import shuffle_for_stream
+  C = require()
+  torch.manual_seed(M + N + len(epi))
+  x = torch.randn(M, Kd, device=gpu, dtype=torch.bfloat16)
+  w = torch.randn(N, Kd, device=gpu, dtype=torch.bfloat16) / math.sqrt(Kd)
+  b = torch.randn(N, device=gpu, dtype=torch.bfloat16)
+  r = torch.randn(M, N, device=gpu, dtype=torch.bfloat16)
+  full = R.linear(x, w, b)
+  if epi == "silu":
+    f = full.view(M, N // 32, 2, 16)
+    ref = (torch.nn.functional.silu(f[:, :, 0]) * f[:, :, 1]).reshape(M, N // 2)
+  elif epi == "resid":
+    ref = full + r.float()
+  else:
+    ref = full
+  y = torch.empty(ref.shape, device=gpu, dtype=torch.float32 if f32 else torch.bfloat16)
+  part = torch.empty(C.gemm_sk_part_elems(), device=gpu, dtype=torch.float32)
+  sync = torch.zeros(C.gemm_sk_sync_words(M, N), device=gpu, dtype=torch.int32)
+  ws = shuffle_for_stream(w)
+  C.gemm_sk(x, ws, y, b, r if epi == "resid" else None, part, sync, K.EPI[epi], 256)
+  torch.cuda.synchronize()
+  assert rel_err(y, ref) < 1e-2
+  first = y.clone()
+  C.gemm_sk(x, ws, y, b, r if epi == "resid" else None, part, sync, K.EPI[epi], 256)
+  torch.cuda.synchronize()
+  assert torch.equal(y, first)
+  assert int(sync.abs().sum()) == 0

@@ -91,6 +91,7 @@ class P2PTransport:
     self._pending = []
     self._groups = {}
     self._staged = False
+    self.sent_bytes = 0  # payload handed to isend (bench diagnostics)
     if world > 1 and dist.is_initialized():
       self._staged = dist.get_backend() == "gloo"
       for e in ring_edges(world):  # every rank creates every group, in the same order
@@ -104,6 +105,7 @@ class P2PTransport:
       self.monitor.check()
     if self.injector is not None:
       self.injector.before_send()
+    self.sent_bytes += t.numel() * t.element_size()
     if self._staged and t.is_cuda:
       t = t.to("cpu")
     w = dist.isend(t, dst, group=self._group(self.rank, dst))
@@ -162,6 +164,7 @@ class LoopbackTransport:
 
   def __init__(self, rank: int, world: int):
     self.rank, self.world = rank, world
+    self.sent_bytes = 0
 
   def isend(self, t: torch.Tensor, dst: int):
     LoopbackTransport._queues[(self.rank, dst)].append(t.clone())

@@ -103,7 +103,8 @@ class RingStage:
     cand = idx.long().gather(1, j.clamp(max=KC - 1).unsqueeze(1)).squeeze(1)
     return torch.where(j < KC, cand, j - KC + self.vs).to(torch.int32)
 
-  def _recv_and_sample(self, mb: MicroBatch) -> torch.Tensor:
+  def _recv_item(self, mb: MicroBatch) -> tuple:
+    """First stage, split head: receive the last stage's hand-off (normed hidden, candidates)."""
     B = len(mb.rids)
     dev = self.r.device
     xn = torch.empty(B, self.D, dtype=torch.bfloat16, device=dev)
@@ -112,7 +113,35 @@ class RingStage:
     works = [self.t.irecv(xn, self.prev), self.t.irecv(vals, self.prev), self.t.irecv(idx, self.prev)]
     for w in works:
       self.t.wait(w)
-    return self._finish_head(xn, vals, idx, mb.temps)
+    return xn, vals, idx
+
+  def _recv_and_sample(self, mb: MicroBatch) -> torch.Tensor:
+    return self._finish_head(*self._recv_item(mb), mb.temps)
+
+  # ---------------------------------------------------------------- per-tick device timing (bench diagnostics)
+  def start_timing(self) -> None:
+    """Record (start, data in, done) events on the compute stream around every decode tick from now on:
+    data-in minus start is the time the stream sat waiting for the previous stage's hand-off (the recv
+    wait), done minus data-in the stage's own work (layers, head share, sampling)."""
+    self._events = []
+
+  def timing(self) -> dict:
+    """Per-tick means (ms) of the recorded ticks: {'ticks', 'stage_ms', 'recv_wait_ms'}; syncs the device."""
+    ev = getattr(self, "_events", None) or []
+    if not ev:
+      return {"ticks": 0, "stage_ms": None, "recv_wait_ms": None}
+    if self.r.device.type == "cuda":
+      torch.cuda.synchronize(self.r.device)
+    wait = sum(a.elapsed_time(b) for a, b, _ in ev) / len(ev)
+    work = sum(b.elapsed_time(c) for _, b, c in ev) / len(ev)
+    return {"ticks": len(ev), "stage_ms": round(work, 3), "recv_wait_ms": round(wait, 3)}
+
+  def _mark(self):
+    if getattr(self, "_events", None) is None or self.r.device.type != "cuda":
+      return None
+    e = torch.cuda.Event(enable_timing=True)
+    e.record()
+    return e
 
   # ---------------------------------------------------------------- one micro-batch through this stage
   def prefill(self, mb: MicroBatch, chunk_tokens: int = 8192):
@@ -157,27 +186,37 @@ class RingStage:
     B = len(mb.rids)
     dev = self.r.device
     sampled = None
+    e0 = self._mark()
     if self.first:
       if item_in is not None:
         x = item_in
+        e1 = e0
       elif self.split:
-        x = sampled = self._recv_and_sample(mb)
+        got = self._recv_item(mb)
+        e1 = self._mark()
+        x = sampled = self._finish_head(*got, mb.temps)
       else:
         x = torch.empty(B, dtype=torch.int32, device=dev)
         self.t.wait(self.t.irecv(x, self.prev))
+        e1 = self._mark()
     else:
       x = torch.empty(B, self.D, dtype=torch.bfloat16, device=dev)
       self.t.wait(self.t.irecv(x, self.prev))
+      e1 = self._mark()
     y = self.r.forward(mb.rids, [1] * B, x)
     if not self.last:
       # y is the decode graph's static output buffer: the next replay overwrites it, so hand RCCL a copy
       self.t.isend(y.clone(), self.next)
+      if e0 is not None:
+        self._events.append((e0, e1, self._mark()))
       return sampled, None
     item = self._head_part(y) if self.split else self._sample(y, mb.temps)
     if not self.split:
       sampled = item
     if self.world > 1 and send:
       self._send_item(item)
+    if e0 is not None:
+      self._events.append((e0, e1, self._mark()))
     return sampled, item
 
 
