@@ -184,7 +184,7 @@ def _run_rank0(srv, reqs, timeout=150):
   return out
 
 
-def _worker2(rank, world, port, q, pages, fault, free_cap=256, slack=3, reqs=None):
+def _worker2(rank, world, port, q, pages, fault, ops_cap=256, slack=3, reqs=None):
   import datetime
   from xotorch_support_jetson_amd.parallel.health import HealthMonitor
   from xotorch_support_jetson_amd.parallel.ring_serve import control_group, min_pool_pages, ring_shards
@@ -205,13 +205,16 @@ def _worker2(rank, world, port, q, pages, fault, free_cap=256, slack=3, reqs=Non
   # 5 s: a loaded CI host (parallel test workers) must not make a live peer look dead
   mon = HealthMonitor(rank, world, interval=0.1, timeout=5.0).start() if fault else None
   srv = RingServer(runner, rank, world, P2PTransport(rank, world, monitor=mon), ctl, step_tokens=32, monitor=mon,
-                   make_runner=make_runner, pool_pages=pool, free_cap=free_cap)
+                   make_runner=make_runner, pool_pages=pool, ops_cap=ops_cap)
   res = None
   if rank == 0:
     res = _run_rank0(srv, reqs or LONG)
   else:
     srv.serve_forever()
-  q.put((rank, res, dict(srv.stats), srv.pool_pages, srv.r.bm.num_free == srv.r.bm.num_blocks))
+  # pages still held: only the prefix cache's holders (rank 0 owns the cache; every rank mirrors its pool)
+  used = srv.r.bm.num_blocks - srv.r.bm.num_free
+  cached = srv.pc.cached_pages() if srv.pc is not None else None
+  q.put((rank, res, dict(srv.stats), srv.pool_pages, (used, cached)))
   q.close()
   q.join_thread()
   os._exit(0)
@@ -246,7 +249,8 @@ def test_ring_serve_chunked_prefill_and_kv_pressure(world):
   assert out == ref
   assert stats["chunks"] > 0 and stats["preempted"] > 0, stats
   assert all(res[r][2] == 5 for r in res)  # min over ranks (rank r has 5 + 3r pages)
-  assert all(res[r][3] for r in res)  # every rank's pool is empty again
+  cached = res[0][3][1]
+  assert all(res[r][3][0] == cached for r in res)  # every rank's pool is empty again but for the cached prefixes
 
 
 SHORT = [(chr(ord("A") + i), 4, 3) for i in range(8)]  # finish together, in the same lane steps
@@ -257,10 +261,10 @@ def test_ring_serve_frees_beyond_one_header_reach_followers_first():
   rank 0 has already dropped their pages and plans the next step into them, so every pending free must
   reach the followers ahead of that step (free-only headers), or a follower's pool runs dry."""
   ref = _ref_tokens(SHORT)
-  res = _launch2(2, pages=4, free_cap=1, slack=0, reqs=SHORT)
+  res = _launch2(2, pages=4, ops_cap=1, slack=0, reqs=SHORT)
   out, stats, pool, _ = res[0]
   assert out == ref
-  assert pool == 4 and all(res[r][3] for r in res)
+  assert pool == 4 and all(res[r][3][0] == res[0][3][1] for r in res)
 
 
 def test_ring_serve_recovers_from_a_dead_peer():
@@ -273,3 +277,141 @@ def test_ring_serve_recovers_from_a_dead_peer():
   out, stats, _, _ = res[0]
   assert stats["recoveries"] == 1
   assert out == ref
+
+
+# ---------------------------------------------------------------------------- orchestration layer over the ring
+SHARED = "You are a careful assistant. " * 12  # ~340 byte tokens: five full 64-token pages
+
+
+def _image_prompt():
+  from tests.test_vision import _png_data_url
+  from xotorch_support_jetson_amd.models.vision import IMAGE_MARK
+  return "USER: " + IMAGE_MARK.format(_png_data_url(3)) + "\nwhat is this? ASSISTANT:"
+
+
+def _worker_orch(rank, world, port, q, model, prompts, max_toks):
+  """Rank 0 serves RingNode + the ChatGPT API over the ring: /v1/topology, /metrics, then `prompts` one after
+  the other through RingNode.process_prompt (image markers, prompt-prefix reuse)."""
+  import asyncio
+  import datetime
+  from xotorch_support_jetson_amd.inference.shard import Shard
+  from xotorch_support_jetson_amd.inference.tokenizers import _resolve_tokenizer
+  from xotorch_support_jetson_amd.models import registry
+  from xotorch_support_jetson_amd.parallel.ring_serve import RingNode, control_group, ring_shards
+  os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+  dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=60))
+  c = PRESETS[model]
+  ctl = control_group()
+  shard = ring_shards(model, c.num_layers, world, ctl)[rank]
+  runner = ShardRunner(c, shard, "cpu", max_batch=8, max_ctx=1024)
+  srv = RingServer(runner, rank, world, P2PTransport(rank, world), ctl, step_tokens=128)
+  if rank != 0:
+    srv.serve_forever()
+    q.put((rank, None))
+  else:
+    import aiohttp
+    from xotorch_support_jetson_amd.api.chatgpt_api import ChatGPTAPI
+    tok = _resolve_tokenizer(registry.get_repo(model, "ShardedInferenceEngine") or "byte", c.vocab_size)
+    full = Shard(model, 0, c.num_layers - 1, c.num_layers)
+    api_port = _free_port()
+
+    async def main():
+      node = RingNode(srv, full, tok, (), 0.0, max_toks, loop=asyncio.get_running_loop(), config=c)
+      th = threading.Thread(target=srv.serve_forever, kwargs=dict(idle_wait=0.05), daemon=True)
+      th.start()
+      api = ChatGPTAPI(node, "ShardedInferenceEngine", response_timeout=60, default_model=model)
+      await api.run(host="127.0.0.1", port=api_port)
+      async with aiohttp.ClientSession() as s:
+        async with s.get(f"http://127.0.0.1:{api_port}/v1/topology") as r:
+          topo = await r.json()
+        async with s.get(f"http://127.0.0.1:{api_port}/metrics") as r:
+          metrics = await r.text()
+      outs = []
+      for i, p in enumerate(prompts):
+        done, got = asyncio.Event(), []
+
+        def on_tok(rid, toks, fin, me=f"p{i}"):
+          if rid == me:
+            got.extend(toks)
+            if fin:
+              done.set()
+        node.on_token.register(f"t{i}").on_next(on_tok)
+        await node.process_prompt(full, p, request_id=f"p{i}", inference_state={"max_tokens": max_toks})
+        await asyncio.wait_for(done.wait(), 120)
+        outs.append(got)
+      srv.stop()
+      th.join(30)
+      await api._runner.cleanup()
+      return topo, metrics, outs
+
+    topo, metrics, outs = asyncio.run(main())
+    q.put((0, dict(topo=topo, kv_gauge="xot_kv_pages_total" in metrics, outs=outs,
+                   hit_tokens=srv.pc.stats["hit_tokens"] if srv.pc is not None else 0)))
+  q.close()
+  q.join_thread()
+  os._exit(0)
+
+
+def _run_orch(world, model, prompts, max_toks):
+  ctx = mp.get_context("spawn")
+  q = ctx.Queue()
+  port = _free_port()
+  ps = [ctx.Process(target=_worker_orch, args=(r, world, port, q, model, prompts, max_toks)) for r in range(world)]
+  for p in ps:
+    p.start()
+  res = dict(q.get(timeout=300) for _ in range(world))
+  for p in ps:
+    p.join(30)
+  return res[0]
+
+
+def _engine_greedy(model, prompt, n):
+  """The single-process engine's greedy tokens for a prompt (images expanded by ShardedInferenceEngine)."""
+  import asyncio
+
+  import numpy as np
+
+  from xotorch_support_jetson_amd.download.shard_download import NoopShardDownloader
+  from xotorch_support_jetson_amd.inference.shard import Shard
+  from xotorch_support_jetson_amd.inference.sharded_engine import ShardedInferenceEngine
+
+  async def main():
+    c = PRESETS[model]
+    e = ShardedInferenceEngine(NoopShardDownloader(), device=torch.device("cpu"))
+    sh = Shard(model, 0, c.num_layers - 1, c.num_layers)
+    logits, _ = await e.infer_prompt("ref", sh, prompt)
+    out = []
+    for _ in range(n):
+      t = int(np.asarray(torch.as_tensor(logits).float()).reshape(-1, c.vocab_size)[-1].argmax())
+      out.append(t)
+      logits, _ = await e.infer_tensor("ref", sh, np.asarray([[t]]))
+    return out
+  return asyncio.run(main())
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_ring_orchestration_topology_metrics_and_prefix_reuse(world):
+  """`xot --gpus N` rank 0 is a full orchestration peer: /v1/topology lists the N GPU peers with their ring
+  edges and layer ranges (covering the model once, in ring order), /metrics carries the KV gauges of the ring's
+  pool, and a second prompt sharing a long prefix with the first reuses its cached pages -- with the tokens of
+  the single-process engine for both prompts."""
+  prompts = [SHARED + "first question?", SHARED + "second one!"]
+  got = _run_orch(world, MODEL, prompts, 6)
+  topo = got["topo"]
+  assert len(topo["nodes"]) == world and topo["active_node_id"] in topo["nodes"]
+  assert sum(len(v) for v in topo["peer_graph"].values()) == world
+  parts = topo["partitions"]
+  assert [p["node_id"] for p in parts] and parts[0]["start_layer"] == 0
+  assert parts[-1]["end_layer"] == PRESETS[MODEL].num_layers - 1
+  assert all(a["end_layer"] + 1 == b["start_layer"] for a, b in zip(parts, parts[1:]))
+  assert got["kv_gauge"]
+  assert got["hit_tokens"] >= 4 * 64  # the second prompt forked the first one's cached pages
+  assert got["outs"] == [_engine_greedy(MODEL, p, 6) for p in prompts]
+
+
+def test_ring_llava_image_prompt_matches_engine():
+  """An image prompt through RingNode on a 2-rank tiny-LLaVA ring (rank 0 = first shard splices the tower's
+  features into the image-token rows) gives the single-process engine's greedy tokens."""
+  p = _image_prompt()
+  got = _run_orch(2, "tiny-llava", [p], 5)
+  assert got["outs"] == [_engine_greedy("tiny-llava", p, 5)]

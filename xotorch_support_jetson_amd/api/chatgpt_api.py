@@ -505,7 +505,11 @@ class ChatGPTAPI:
   async def handle_get_topology(self, request):
     try:
       topo = self.node.current_topology
-      return web.json_response(topo.to_json() if topo else {})
+      d = topo.to_json() if topo else {}
+      ranges = getattr(self.node, "layer_ranges", None)
+      if topo and callable(ranges):  # which layers each peer serves (extra key; the reference shape is unchanged)
+        d["partitions"] = [{"node_id": nid, "start_layer": a, "end_layer": b} for nid, a, b in ranges()]
+      return web.json_response(d)
     except Exception as e:
       return web.json_response({"detail": f"Error getting topology: {e}"}, status=500)
 

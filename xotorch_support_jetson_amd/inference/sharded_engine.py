@@ -470,7 +470,7 @@ class ShardedInferenceEngine(InferenceEngine):
     """Prompts may carry `<|xot_image:URL|>` markers (api/chatgpt_api.py keeps the chat's last image that
     way).  A vision model's first shard expands each into its image-token run and keeps the preprocessed
     pixels for the request's prefill; any other model reads the marker as a placeholder text."""
-    from ..models.vision import load_image, num_image_tokens, preprocess, split_image_marks
+    from ..models.vision import encode_with_images, image_pixels, split_image_marks
     pieces, urls = split_image_marks(prompt)
     if not urls:
       return await super().infer_prompt(request_id, shard, prompt, inference_state)
@@ -479,14 +479,8 @@ class ShardedInferenceEngine(InferenceEngine):
     if c.vision is None or not shard.is_first_layer():
       text = "".join(p + ("[image]" if i < len(urls) else "") for i, p in enumerate(pieces))
       return await super().infer_prompt(request_id, shard, text, inference_state)
-    n_img = num_image_tokens(c)
-    ids: list = []
-    for i, piece in enumerate(pieces):
-      ids += list(self.tokenizer.encode(piece, add_special_tokens=(i == 0)))
-      if i < len(urls):
-        ids += [c.image_token_id] * n_img
-    size = c.vision["image_size"]
-    pixels = await self._run(lambda: torch.stack([preprocess(load_image(u), size) for u in urls]))
+    ids, urls = encode_with_images(self.tokenizer, c, prompt)
+    pixels = await self._run(lambda: image_pixels(c, urls))
     self._images[request_id] = pixels
     return await self.infer_tensor(request_id, shard, np.asarray(ids, dtype=np.int64).reshape(1, -1),
                                    inference_state)

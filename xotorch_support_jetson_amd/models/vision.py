@@ -40,6 +40,30 @@ def split_image_marks(prompt: str) -> Tuple[List[str], List[str]]:
   return pieces, urls
 
 
+def encode_with_images(tokenizer, c, prompt: str) -> Tuple[List[int], List[str]]:
+  """Token ids of a prompt that may carry `<|xot_image:URL|>` markers, and the image urls: for a vision model
+  each marker becomes its run of image tokens (the features replace those rows on the first shard); any other
+  model reads a marker as the text "[image]" (then no urls are returned)."""
+  pieces, urls = split_image_marks(prompt)
+  if not urls:
+    return list(tokenizer.encode(prompt)), []
+  if c.vision is None:
+    return list(tokenizer.encode("".join(p + ("[image]" if i < len(urls) else "") for i, p in enumerate(pieces)))), []
+  n_img = num_image_tokens(c)
+  ids: List[int] = []
+  for i, piece in enumerate(pieces):
+    ids += list(tokenizer.encode(piece, add_special_tokens=(i == 0)))
+    if i < len(urls):
+      ids += [c.image_token_id] * n_img
+  return ids, urls
+
+
+def image_pixels(c, urls: List[str]) -> torch.Tensor:
+  """[N, 3, S, S] preprocessed pixels of the urls (CLIP preprocessing at the tower's resolution)."""
+  size = c.vision["image_size"]
+  return torch.stack([preprocess(load_image(u), size) for u in urls])
+
+
 def escape_marks(text: str) -> str:
   """User text must not be able to produce an image marker: only markers build_prompt writes for the
   chat's image part survive (a literal `<|xot_image:/etc/...|>` typed into a message stays text)."""

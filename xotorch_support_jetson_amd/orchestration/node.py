@@ -591,6 +591,18 @@ class Node:
   def current_topology(self) -> Topology:
     return self.topology
 
+  def layer_ranges(self):
+    """[(peer id, first layer, last layer)] of the current partitioning for the loaded model (empty if none)."""
+    L = self._viz_layers()
+    if not L:
+      return []
+    from ..topology.partitioning_strategy import map_partitions_to_shards
+    parts = self._partitions()
+    shards = map_partitions_to_shards(parts, L, "m")
+    if len(shards) != len(parts):  # a peer without layers: ranges would not line up with the peers
+      return []
+    return [(p.node_id, s.start_layer, s.end_layer) for p, s in zip(parts, shards)]
+
   # ------------------------------------------------------------------ callbacks / broadcast
   @property
   def on_token(self) -> AsyncCallbackSystem[str, Tuple[str, List[int], bool]]:

@@ -43,6 +43,7 @@ from __future__ import annotations
 import collections
 import os
 import queue
+import sys
 import threading
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional, Sequence
@@ -54,7 +55,40 @@ from ..ops import kernels as K
 from .health import FaultInjector, HealthMonitor, PeerFailure, reform_ring, wait_work
 
 STEP_TOKENS = int(os.environ.get("XOT_MAX_STEP_TOKENS", "8192"))
-FREE_CAP = 256  # frees per header (more go ahead of the step in free-only headers)
+OPS_CAP = 256  # KV operations per header (more go ahead of the step in op-only headers)
+# prompt-prefix KV reuse on the ring (inference/prefix_cache.py policy on rank 0): at most this fraction of the pool
+PREFIX_CACHE = os.environ.get("XOT_PREFIX_CACHE", "1") == "1"
+PREFIX_CACHE_FRAC = float(os.environ.get("XOT_PREFIX_CACHE_FRAC", "0.25"))
+# KV operations rank 0 performs on its BlockManager and every other rank repeats, in order, from the headers:
+OP_FREE, OP_FREE_HOLDER, OP_FORK_TO_REQ, OP_FORK_TO_HOLDER = 1, 2, 3, 4  # (code, a, b, ntok)
+
+
+class _RecordingBM:
+  """Rank 0's BlockManager as the prefix cache sees it: holder forks and frees go through to the real one and
+  are recorded as header operations, so every rank's pool changes the same way at the same point."""
+
+  def __init__(self, bm, sink: list):
+    self._bm, self._sink = bm, sink
+
+  def __getattr__(self, name):
+    return getattr(self._bm, name)
+
+  @staticmethod
+  def _holder_id(name: str) -> int:
+    return int(name[3:]) if name.startswith("pc:") else -1
+
+  def fork(self, src: str, dst: str, ntok: int) -> None:
+    self._bm.fork(src, dst, ntok)
+    h = self._holder_id(src)
+    if h >= 0:
+      self._sink.append((OP_FORK_TO_REQ, h, int(dst), ntok))
+    else:
+      self._sink.append((OP_FORK_TO_HOLDER, int(src), self._holder_id(dst), ntok))
+
+  def free(self, name: str) -> None:
+    self._bm.free(name)
+    h = self._holder_id(name)
+    self._sink.append((OP_FREE_HOLDER, h, 0, 0) if h >= 0 else (OP_FREE, int(name), 0, 0))
 
 
 @dataclass
@@ -68,6 +102,8 @@ class _Req:
   lane: int = -1
   fed: int = 0  # tokens of ids + out already in the KV cache
   order: int = 0  # admission order: the largest is the youngest
+  pixels: Optional[torch.Tensor] = None  # LLaVA: preprocessed images of the prompt (rank 0 = first shard)
+  feats: Optional[torch.Tensor] = None  # their projected features [image tokens, D] (computed on first use)
 
   def todo(self) -> int:
     """Tokens still to feed before the next sampled token is a real output (1 while decoding)."""
@@ -78,9 +114,10 @@ class RingServer:
   def __init__(self, runner, rank: int, world: int, transport, ctl_group=None, eos_ids: Sequence[int] = (),
                top_k: int = 35, seed: int = 1234, max_batch: Optional[int] = None, step_tokens: Optional[int] = None,
                monitor: Optional[HealthMonitor] = None, make_runner: Optional[Callable] = None,
-               pool_pages: Optional[int] = None, free_cap: int = FREE_CAP):
+               pool_pages: Optional[int] = None, ops_cap: int = OPS_CAP, prefix_cache: Optional[bool] = None):
     self.r, self.rank, self.world, self.t = runner, rank, world, transport
-    self.free_cap = max(1, free_cap)  # frees per header
+    self.ops_cap = max(1, ops_cap)  # KV operations per header
+    self.use_prefix_cache = PREFIX_CACHE if prefix_cache is None else prefix_cache
     self.ctl = ctl_group  # gloo group of the control plane (headers); None with world 1
     self.eos = set(int(e) for e in eos_ids)
     self.top_k = top_k
@@ -92,12 +129,13 @@ class RingServer:
     self.generation = 0
     self.backend = dist.get_backend() if dist.is_initialized() else "gloo"
     self._set_topology(runner, rank, world, pool_pages)
+    self._gather_peers()
     self._inbox: "queue.Queue[_Req]" = queue.Queue()
     self._waiting: "collections.deque[_Req]" = collections.deque()  # preempted (front) and new requests
     self._running: Dict[str, _Req] = {}
     self._next_key = 0
     self._next_order = 0
-    self._free: List[int] = []  # keys to free on every rank (carried by the next headers)
+    self._ops_sink()  # KV operations for every other rank (carried by the next headers, in order)
     self._callbacks: List[Callable[[str, List[int], bool], None]] = []
     self._stop = False
     self._wake = threading.Event()
@@ -115,11 +153,61 @@ class RingServer:
     self._inflight: List[Optional[list]] = [None] * self.lanes  # per lane: the step's (req, n) awaiting ids
     # rank 0 plans with the smallest pool of the ring (exact for every rank: same appends everywhere)
     self.pool_pages = min(pool_pages or runner.bm.num_blocks, runner.bm.num_blocks)
-    self.hcap = 4 + 3 * self.max_batch + self.free_cap
+    self.hcap = 4 + 3 * self.max_batch + 4 * self.ops_cap
+    # rank 0 owns the prefix-cache policy; it runs on a recording view of its pool (every fork / free of a
+    # holder becomes a header operation).  Headers reach every rank in order, so unlike the gRPC ring no
+    # confirmation protocol is needed: an operation is applied everywhere before any step that depends on it.
+    self.pc = None
+    longrope = (runner.config.rope_scaling or {}).get("rope_type") == "longrope"
+    if rank == 0 and self.use_prefix_cache and not longrope:
+      from ..inference.prefix_cache import PrefixCache
+      self.pc = PrefixCache(_RecordingBM(runner.bm, self._ops_sink()), int(self.pool_pages * PREFIX_CACHE_FRAC),
+                            single_shard=True)
+
+  def _ops_sink(self) -> list:
+    if not hasattr(self, "_ops"):
+      self._ops = []
+    return self._ops
+
+  def _gather_peers(self) -> None:
+    """Collective over the control group (every rank, at start-up and after a re-form): each rank's device
+    capabilities and layer range.  Rank 0 keeps them as the orchestration layer's Topology -- one peer per
+    GPU, ring edges labelled with the data plane -- and the ring's partitions, so /v1/topology, tinychat's
+    topology panel and the TUI show the GPU ring like the reference shows its discovered peers
+    (orchestration/node.py:533-566)."""
+    import socket
+    from ..topology.device_capabilities import DeviceCapabilities, device_capabilities
+    from ..topology.partitioning_strategy import Partition
+    from ..topology.topology import Topology
+    dev = self.r.device
+    local = dev.index if dev.type == "cuda" and dev.index is not None else self.rank
+    mine = {"id": f"{socket.gethostname()}-gpu{local}", "caps": device_capabilities(local_gpu=local).model_dump(),
+            "layers": (self.r.shard.start_layer, self.r.shard.end_layer)}
+    peers = [mine]
+    if self.world > 1 and self.ctl is not None:
+      peers = [None] * self.world
+      dist.all_gather_object(peers, mine, group=self.ctl)
+    ids = [p["id"] for p in peers]
+    if len(set(ids)) != len(ids):  # e.g. CPU ranks of one host: fall back to ring positions
+      ids = [f"{p['id']}-r{i}" for i, p in enumerate(peers)]
+    self.node_ids = ids
+    link = "xGMI (RCCL p2p)" if self.backend == "nccl" else f"{self.backend} p2p"
+    t = Topology()
+    for nid, p in zip(ids, peers):
+      t.update_node(nid, DeviceCapabilities(**p["caps"]))
+    for i in range(self.world if self.world > 1 else 0):
+      t.add_edge(ids[i], ids[(i + 1) % self.world], link)
+    t.active_node_id = ids[0]
+    L = self.r.shard.n_layers
+    self.topology = t
+    self.partitions = [Partition(nid, p["layers"][0] / L, (p["layers"][1] + 1) / L) for nid, p in zip(ids, peers)]
+    self.layer_ranges = [(nid, p["layers"][0], p["layers"][1]) for nid, p in zip(ids, peers)]
 
   # ------------------------------------------------------------------ rank-0 API side
-  def submit(self, rid: str, ids: Sequence[int], temp: float = 0.0, max_tokens: int = 256) -> None:
-    self._inbox.put(_Req(rid, [int(i) for i in ids], float(temp), int(max_tokens)))
+  def submit(self, rid: str, ids: Sequence[int], temp: float = 0.0, max_tokens: int = 256,
+             pixels: Optional[torch.Tensor] = None) -> None:
+    """pixels: [N, 3, S, S] images whose image-token runs the ids carry (LLaVA; models/vision.py)."""
+    self._inbox.put(_Req(rid, [int(i) for i in ids], float(temp), int(max_tokens), pixels=pixels))
     self._wake.set()
 
   def on_token(self, cb: Callable[[str, List[int], bool], None]) -> None:
@@ -137,24 +225,27 @@ class RingServer:
       cb(rid, toks, fin)
 
   # ------------------------------------------------------------------ control plane (gloo, host to host)
-  def _header(self, items, free, stop: bool) -> torch.Tensor:
-    """[n_items, n_free, stop, generation, (key, qlen, temp) * n_items, key * n_free, 0 ...] float64 of fixed
-    size hcap (exact for ids < 2^53)."""
+  def _header(self, items, ops, stop: bool) -> torch.Tensor:
+    """[n_items, n_ops, stop, generation, (key, qlen, temp) * n_items, (code, a, b, ntok) * n_ops, 0 ...]
+    float64 of fixed size hcap (exact for ids < 2^53).  The ops (KV frees and prefix-cache forks) are applied
+    before the step's forward, in order."""
     h = torch.zeros(self.hcap, dtype=torch.float64)
-    vals = [float(len(items)), float(len(free)), 1.0 if stop else 0.0, float(self.generation)]
+    vals = [float(len(items)), float(len(ops)), 1.0 if stop else 0.0, float(self.generation)]
     for key, qlen, temp in items:
       vals += [float(key), float(qlen), float(temp)]
-    vals += [float(k) for k in free]
+    for op in ops:
+      vals += [float(x) for x in op]
     h[:len(vals)] = torch.tensor(vals, dtype=torch.float64)
     return h
 
   @staticmethod
   def _parse(h: torch.Tensor):
     v = h.tolist()
-    n, nf, stop = int(v[0]), int(v[1]), v[2] != 0.0
+    n, no, stop = int(v[0]), int(v[1]), v[2] != 0.0
     items = [(int(v[4 + 3 * i]), int(v[5 + 3 * i]), v[6 + 3 * i]) for i in range(n)]
-    free = [int(x) for x in v[4 + 3 * n:4 + 3 * n + nf]]
-    return items, free, stop
+    o = 4 + 3 * n
+    ops = [tuple(int(x) for x in v[o + 4 * i:o + 4 * i + 4]) for i in range(no)]
+    return items, ops, stop
 
   def _send_header(self, h: torch.Tensor) -> None:
     if self.monitor is not None:
@@ -168,7 +259,8 @@ class RingServer:
     return h
 
   # ------------------------------------------------------------------ one lane step on this rank
-  def _stage(self, items, x0: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+  def _stage(self, items, x0: Optional[torch.Tensor], image_embeds: Optional[torch.Tensor] = None
+             ) -> Optional[torch.Tensor]:
     """Run this rank's layers for a lane step; the last rank returns the sampled ids [B] int32 (device)."""
     rids = [str(k) for k, _, _ in items]
     qlens = [q for _, q, _ in items]
@@ -177,7 +269,8 @@ class RingServer:
     else:
       x = torch.empty(sum(qlens), self.D, dtype=torch.bfloat16, device=self.dev)
       self.t.wait(self.t.irecv(x, self.prev))
-    y = self.r.forward(rids, qlens, x)
+    y = (self.r.forward(rids, qlens, x) if image_embeds is None
+         else self.r.forward(rids, qlens, x, image_embeds=image_embeds))
     if not self.last:
       self.t.isend(y.clone(), self.next)  # y may be a decode graph's static buffer
       return None
@@ -191,9 +284,19 @@ class RingServer:
       self.t.isend(tok, 0)
     return tok
 
-  def _apply_free(self, free: List[int]) -> None:
-    for k in free:
-      self.r.free(str(k))
+  def _apply_ops(self, ops) -> None:
+    """Followers: repeat rank 0's KV operations on this rank's pool (same order, same point in the steps)."""
+    from ..inference.prefix_cache import holder
+    bm = self.r.bm
+    for code, a, b, ntok in ops:
+      if code == OP_FREE:
+        self.r.free(str(a))
+      elif code == OP_FREE_HOLDER:
+        bm.free(holder(a))
+      elif code == OP_FORK_TO_REQ:
+        bm.fork(holder(a), str(b), ntok)
+      elif code == OP_FORK_TO_HOLDER:
+        bm.fork(str(a), holder(b), ntok)
 
   # ------------------------------------------------------------------ rank 0: scheduler + first stage
   def _free_pages(self) -> int:
@@ -207,7 +310,9 @@ class RingServer:
     """Drop a request's pages here and (via the next headers) on every other rank."""
     if self.r.has(str(q.key)):
       self.r.free(str(q.key))
-    self._free.append(q.key)
+    self._ops.append((OP_FREE, q.key, 0, 0))
+    if self.pc is not None:
+      self.pc.on_finish(str(q.key))
 
   def _admit(self) -> None:
     while True:
@@ -248,6 +353,11 @@ class RingServer:
     """(req, new tokens) of this lane's next step: decoders first, then prompt chunks in admission order
     within the step's token budget; the youngest are preempted while the step's pages do not fit."""
     reqs = sorted((q for q in self._running.values() if q.lane == lane), key=lambda q: (q.todo() > 1, q.order))
+    if self.pc is not None:  # new prompts: fork the longest cached prefix (whole pages) and feed only the rest
+      for q in reqs:
+        if q.fed == 0 and q.pixels is None and q.todo() > 1 and not self.r.has(str(q.key)):
+          n, _ = self.pc.on_prompt(str(q.key), q.ids + q.out)
+          q.fed = n
     while True:
       plan, budget = [], self.step_tokens
       for q in reqs:
@@ -261,6 +371,10 @@ class RingServer:
       need = sum(self._pages(q, n) for q, n in plan)
       if need <= self._free_pages() or not plan:
         return plan
+      if self.pc is not None and self.pc.cached_pages():  # cached prefixes go before running requests
+        self.pc.evict(need + (self.r.bm.num_blocks - self.pool_pages))
+        if need <= self._free_pages():
+          return plan
       victim = max(reqs, key=lambda q: q.order)
       reqs.remove(victim)
       self._preempt(victim)
@@ -294,35 +408,54 @@ class RingServer:
   def _launch(self, lane: int, stop: bool = False) -> bool:
     """Rank 0: start this lane's next step.  Returns whether anything was sent."""
     plan = self._plan(lane) if not stop else []
-    if not plan and not (stop or (self._free and self.world > 1 and self._idle_lanes())):
+    if not plan and not (stop or (self._ops and self.world > 1 and self._idle_lanes())):
       return False
-    items, ids = [], []
+    items, ids, embeds = [], [], []
     for q, n in plan:
       items.append((q.key, n, q.temp))
       seq = q.ids + q.out
       ids += seq[q.fed:q.fed + n]
       if n > 1:
         self.stats["chunks"] += 1
-    # Rank 0 has already dropped these pages and planned this step into them: every free must reach the
-    # other ranks AHEAD of the step (headers arrive in order), so frees beyond one header's cap go first in
-    # free-only headers.
-    free = self._flush_frees()
+      if q.pixels is not None:
+        e = self._image_rows(q, seq, n)
+        if e is not None:
+          embeds.append(e)
+      elif self.pc is not None and n == 1 and q.todo() == 1:
+        self.pc.on_decode(str(q.key))  # its first decode step: keep the prompt's pages as a cached prefix
+    # Rank 0 has already applied these operations (frees, prefix forks) and planned this step on top of
+    # them: every one must reach the other ranks AHEAD of the step (headers arrive in order), so operations
+    # beyond one header's cap go first in op-only headers.
+    ops = self._flush_ops()
     if self.world > 1:
-      self._send_header(self._header(items, free, stop))
+      self._send_header(self._header(items, ops, stop))
     if items:
-      tok = self._stage(items, torch.tensor(ids, dtype=torch.int32))
+      tok = self._stage(items, torch.tensor(ids, dtype=torch.int32), torch.cat(embeds) if embeds else None)
       self._inflight[lane] = (plan, tok)
       self.stats["steps"] += 1
     return True
 
-  def _flush_frees(self) -> List[int]:
-    """Send free-only headers until at most free_cap frees are pending; return (and clear) those."""
+  def _image_rows(self, q: _Req, seq: List[int], n: int) -> Optional[torch.Tensor]:
+    """Rank 0 (first shard): the projected image features of the image tokens in this step's chunk
+    seq[fed:fed + n] of an image prompt, in token order (the features replace those rows)."""
+    img = self.r.config.image_token_id
+    before = sum(1 for t in seq[:q.fed] if t == img)
+    k = sum(1 for t in seq[q.fed:q.fed + n] if t == img)
+    if not k:
+      return None
+    if q.feats is None:
+      q.feats = self.r.image_features(q.pixels)
+    return q.feats[before:before + k]
+
+  def _flush_ops(self) -> List[tuple]:
+    """Send op-only headers until at most ops_cap operations are pending; return (and clear) those."""
     if self.world > 1:
-      while len(self._free) > self.free_cap:
-        self._send_header(self._header([], self._free[:self.free_cap], False))
-        self._free = self._free[self.free_cap:]
-    free, self._free = self._free, []
-    return free
+      while len(self._ops) > self.ops_cap:
+        self._send_header(self._header([], self._ops[:self.ops_cap], False))
+        del self._ops[:self.ops_cap]
+    ops = list(self._ops)
+    self._ops.clear()  # the prefix cache's recording view appends to this same list
+    return ops
 
   def _idle_lanes(self) -> bool:
     return all(s is None for s in self._inflight)
@@ -363,8 +496,8 @@ class RingServer:
         self._wake.wait(idle_wait)
         self._wake.clear()
       lane = (lane + 1) % self.lanes
-    if self.world > 1:  # stop (with the last frees) travels the ring; followers exit on it
-      self._send_header(self._header([], self._flush_frees(), True))
+    if self.world > 1:  # stop (with the last operations) travels the ring; followers exit on it
+      self._send_header(self._header([], self._flush_ops(), True))
     self.t.drain()
     self._drain_ctl()
     if self.monitor is not None:
@@ -374,10 +507,10 @@ class RingServer:
   def _follow(self) -> None:
     while True:
       h = self._recv_header()
-      items, free, stop = self._parse(h)
+      items, ops, stop = self._parse(h)
       if not self.last:
         self._send_header(h)
-      self._apply_free(free)
+      self._apply_ops(ops)
       if items:
         self._stage(items, None)
       if stop:
@@ -426,22 +559,33 @@ class RingServer:
     runner, pool = self.make_runner(new_rank, new_world, ctl)
     self.ctl, self.t, self.monitor = ctl, transport, monitor
     self._set_topology(runner, new_rank, new_world, pool)
+    self._gather_peers()
     if self.rank == 0:
       for q in sorted(self._running.values(), key=lambda q: q.order, reverse=True):
-        q.lane, q.fed = -1, 0
+        q.lane, q.fed, q.feats = -1, 0, None
         self._waiting.appendleft(q)  # oldest ends up first
       self._running.clear()
-      self._free = []
+      self._ops.clear()  # the new shards start from empty pools (and a fresh prefix cache)
 
 
 # ---------------------------------------------------------------------- API adapter + process spawner
 class _Engine:
-  """What the ChatGPT API reads from `node.inference_engine` (tokenizer, eos ids, shard)."""
+  """What the ChatGPT API and /metrics read from `node.inference_engine` (tokenizer, eos ids, shard, and rank
+  0's runner: its KV pool mirrors every rank's, so its gauges are the ring's)."""
 
-  def __init__(self, shard, tokenizer, eos_ids):
+  def __init__(self, shard, tokenizer, eos_ids, server: Optional[RingServer] = None):
     self.shard, self.tokenizer, self.eos_token_ids = shard, tokenizer, tuple(eos_ids)
+    self.srv = server
     from ..download.shard_download import NoopShardDownloader
     self.shard_downloader = NoopShardDownloader()
+
+  @property
+  def runner(self):
+    return self.srv.r if self.srv is not None else None
+
+  @property
+  def prefix_cache(self):
+    return self.srv.pc if self.srv is not None else None
 
 
 class RingNode:
@@ -450,17 +594,33 @@ class RingNode:
   (reference contract: node.py:109-147 fires on_token(request_id, [token], is_finished))."""
 
   def __init__(self, server: RingServer, shard, tokenizer, eos_ids, default_temp: float, max_generate_tokens: int,
-               loop=None, topology=None):
+               loop=None, topology=None, config=None):
     from ..helpers import AsyncCallbackSystem
     self.srv = server
-    self.inference_engine = _Engine(shard, tokenizer, eos_ids)
+    self.inference_engine = _Engine(shard, tokenizer, eos_ids, server)
+    self.config = config if config is not None else server.r.config
     self.default_temp, self.max_generate_tokens = default_temp, max_generate_tokens
     self.on_token = AsyncCallbackSystem()
     self.node_download_progress = {}
-    self.current_topology = topology
+    self._topology = topology
+    self.id = server.node_ids[0] if getattr(server, "node_ids", None) else "ring-0"
     self.server = None
     self.loop = loop
     server.on_token(self._from_server)
+
+  @property
+  def current_topology(self):
+    """The ring's GPU peers (gathered by the server at start-up and after every re-form), for /v1/topology,
+    tinychat and the TUI; an explicitly given topology wins."""
+    return self._topology if self._topology is not None else getattr(self.srv, "topology", None)
+
+  @property
+  def partitions(self):
+    return getattr(self.srv, "partitions", [])
+
+  def layer_ranges(self):
+    """[(peer id, first layer, last layer)] of the ring, in ring order."""
+    return list(getattr(self.srv, "layer_ranges", []))
 
   def _from_server(self, rid, toks, fin):
     if self.loop is not None:
@@ -472,8 +632,15 @@ class RingNode:
     st = inference_state or {}
     temp = st.get("temperature")
     mt = st.get("max_tokens") or self.max_generate_tokens
-    ids = self.inference_engine.tokenizer.encode(prompt)
-    self.srv.submit(request_id, ids, self.default_temp if temp is None else float(temp), int(mt))
+    # `<|xot_image:URL|>` markers (the API keeps the chat's last image that way): a vision model's prompt gets
+    # each image's token run and rank 0 -- the first shard -- splices the tower's features at prefill
+    from ..models.vision import encode_with_images, image_pixels
+    ids, urls = encode_with_images(self.inference_engine.tokenizer, self.config, prompt)
+    pixels = None
+    if urls:
+      import asyncio
+      pixels = await asyncio.get_running_loop().run_in_executor(None, image_pixels, self.config, urls)
+    self.srv.submit(request_id, ids, self.default_temp if temp is None else float(temp), int(mt), pixels=pixels)
 
 
 def control_group():
@@ -553,7 +720,19 @@ def _serve_worker(rank: int, world: int, port: int, a: dict) -> None:
 async def _rank0_main(srv: RingServer, shard, tok, cfg, a: dict) -> None:
   import asyncio
   loop = asyncio.get_running_loop()
-  node = RingNode(srv, shard, tok, cfg.eos_token_ids, a["default_temp"], a["max_generate_tokens"], loop=loop)
+  node = RingNode(srv, shard, tok, cfg.eos_token_ids, a["default_temp"], a["max_generate_tokens"], loop=loop,
+                  config=cfg)
+  viz = None
+  if a.get("tui"):  # the reference's topology TUI, showing the GPU ring: one peer per rank, its layers, xGMI links
+    try:
+      from ..viz.topology_viz import TopologyViz
+      viz = TopologyViz(chatgpt_api_endpoints=[f"http://localhost:{a['api_port']}/v1/chat/completions"],
+                        web_chat_urls=[f"http://localhost:{a['api_port']}"], num_layers=cfg.num_layers)
+      viz.update_visualization(node.current_topology, node.partitions, node.id, num_layers=cfg.num_layers)
+      node.on_token.register("update_topology_viz").on_next(
+        lambda rid, toks, fin: viz.update_prompt_output(rid, tok.decode(toks)))
+    except Exception:
+      viz = None
   th = threading.Thread(target=srv.serve_forever, name="xot-ring-rounds", daemon=True)
   th.start()
   try:
@@ -577,9 +756,16 @@ async def _rank0_main(srv: RingServer, shard, tok, cfg, a: dict) -> None:
       return
     from ..api.chatgpt_api import ChatGPTAPI
     api = ChatGPTAPI(node, "ShardedInferenceEngine", response_timeout=a["response_timeout"],
-                     default_model=a["model"], system_prompt=a.get("system_prompt"))
+                     default_model=a["model"], system_prompt=a.get("system_prompt"),
+                     on_chat_completion_request=(lambda rid, req, prompt: viz.update_prompt(rid, prompt)) if viz else None)
     await api.run(port=a["api_port"])
     print(f"[ring 0] ChatGPT API on :{a['api_port']} (RCCL ring of {srv.world})", flush=True)
+    if a.get("chat_tui"):
+      from types import SimpleNamespace
+      from ..viz.chat_tui import run_chat_tui
+      await run_chat_tui(SimpleNamespace(default_model=a["model"], model_name=a["model"],
+                                         chatgpt_api_response_timeout=a["response_timeout"]), api, node)
+      return
     await asyncio.Event().wait()
   finally:
     srv.stop()
@@ -597,6 +783,8 @@ def serve_ring(args) -> int:
        "default_temp": args.default_temp, "max_generate_tokens": args.max_generate_tokens,
        "api_port": args.chatgpt_api_port, "response_timeout": args.chatgpt_api_response_timeout,
        "system_prompt": getattr(args, "system_prompt", None),
+       "tui": not getattr(args, "disable_tui", True) and not getattr(args, "chat_tui", False) and sys.stdout.isatty(),
+       "chat_tui": bool(getattr(args, "chat_tui", False)),
        "prompt": args.prompt if (args.command == "run" or getattr(args, "run_model", None)) else None}
   port = _free_port()
   if n == 1:
