@@ -59,7 +59,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
                                                           long ysplit = 0) {
   static_assert(WM * WN == 8, "8 waves");
   static_assert(BK == 32 || BK == 64, "k stage of 32 or 64");
-  static_assert(BM % (16 * WM) == 0 && BM >= 128 && BM <= 256, "row tile of 128 .. 256 rows");
+  static_assert(BM % (16 * WM) == 0 && BM >= 128 && BM <= 512, "row tile of 128 .. 512 rows");
   static_assert(MOE == 0 || MOE == 4 || (!SPLIT && EPI != EPI_RESID), "grouped GEMM: no slab reduce, no residual");
   static_assert(MOE != 4 || !SPLIT, "K-grouped GEMM: no K split");
   constexpr int MT = BM / (16 * WM), NT = BN / (16 * WN);
