@@ -194,7 +194,8 @@ def test_attn_decode(gpu, H, Hkv, Dh, ctx):
   q = torch.randn(B, H, Dh, device=gpu, dtype=torch.bfloat16)
   scale = 1 / math.sqrt(Dh)
   ref = R.attn_decode(q, kc, vc, bt, cl, scale)
-  for algo in (0, 1, 2, 3, 4):  # workgroup kernel; wave kernel without / with page prefetch, + nt loads; 8-wave
+  for algo in (0, 1, 2, 3, 4, 5, 6):  # workgroup kernel; wave kernel without / with page prefetch (2 / 3: double
+    # register set, 5 / 6: one set refilled per half), + nt loads; 8-wave
     for ppp in (1, 3, 4, 8, None):  # None: per-call choice from the batch
       if (algo == 0 and ppp in (1, 3)) or (algo == 4 and ppp is not None):  # 4: one partition only
         continue
@@ -504,7 +505,7 @@ def test_gemm_stream_odd_chunks(gpu, M, Kd, epi):
     assert rel_err(y, ref) < 1e-2, shuf
 
 
-@pytest.mark.parametrize("M", [1, 77, 256, 300, 512, 700])
+@pytest.mark.parametrize("M", [1, 77, 256, 300, 512, 700, 2100, 4100])
 @pytest.mark.parametrize("epi,bn,splits", [("none", 256, 1), ("none", 128, 1), ("resid", 256, 1), ("silu", 256, 1),
                                            ("silu", 128, 1), ("none", 256, 3), ("resid", 128, 2), ("silu", 256, 5),
                                            ("none", 1256, 1), ("resid", 1256, 1), ("silu", 1256, 1), ("none", 1256, 3),

@@ -20,6 +20,8 @@ from tools.bench_attn_small import graph_us  # noqa: E402
 def main():
   ap = argparse.ArgumentParser()
   ap.add_argument("--json", default=None)
+  ap.add_argument("--algos", default="2", help="wave-kernel variants to time (csrc/attention.hip: 1 no prefetch, "
+                  "2 / 3 double register set, 5 / 6 one set refilled per half; 3 / 6 nt loads)")
   args = ap.parse_args()
   dev = torch.device("cuda:0")
   H, Hkv, Dh = 64, 8, 128
@@ -35,12 +37,18 @@ def main():
     out = torch.empty_like(q)
     kv_bytes = 2 * B * Hkv * ctx * Dh * 2
     auto = K.DecodeWorkspace(B, H, Dh, pages * 64, dev)
-    cands = [("auto", auto)] + [(f"ppp{p}", K.DecodeWorkspace(B, H, Dh, pages * 64, dev, pages_per_part=p))
-                                for p in sorted({pages, -(-pages // 2), -(-pages // 3), -(-pages // 4), 2})]
+    cands = [("auto", auto)]
+    for a in [int(x) for x in args.algos.split(",")]:
+      cands += [(f"a{a}-ppp{p}", K.DecodeWorkspace(B, H, Dh, pages * 64, dev, pages_per_part=p, algo=a))
+                for p in sorted({pages, -(-pages // 2), -(-pages // 3), 2})]
+    ref = None
     for name, ws in cands:
       us = graph_us(lambda: K.attn_decode(q, kc, vc, bt, cl, 1 / math.sqrt(Dh), ws, out))
+      if ref is None:
+        ref = out.float().clone()
+      err = ((out.float() - ref).abs().max() / ref.abs().max()).item()
       r = dict(B=B, ctx=ctx, cfg=name, part=list(ws.partition(B, Hkv, pages)), us=round(us, 1),
-               tbps=round(kv_bytes / us / 1e6, 2))
+               tbps=round(kv_bytes / us / 1e6, 2), err_vs_auto=round(err, 5))
       rows.append(r)
       print(json.dumps(r), flush=True)
     del kc, vc

@@ -32,17 +32,17 @@ typedef void (*LaunchFn)(const Ctx&, const uint16_t* W, hipStream_t);
 template <int BM, int BN, int WM, int BK, int NBUF, int PP, int AUXB, int EPI>
 void launch_v(const Ctx& c, const uint16_t* W, hipStream_t st) {
   constexpr int WN = 8 / WM;
-  constexpr int SMEM = big_smem<BM, BN, BK, NBUF, PP>();
+  constexpr int SMEM = big_smem<BM, BN, BK, NBUF>();
   static_assert(SMEM <= 160 * 1024, "LDS");
   const int nwg = ((c.M + BM - 1) / BM) * (c.N / BN) * c.S;
   if (c.S == 1) {
-    auto k = gemm_big_kernel<BM, BN, WM, WN, BK, NBUF, EPI, false, false, 0, 0, 0, AUXB, false, PP>;
+    auto k = gemm_big_kernel<BM, BN, WM, WN, BK, NBUF, EPI, false, false, 0, 0, AUXB, PP>;
     static bool attr = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM) == hipSuccess;
     (void)attr;
     k<<<nwg, 512, SMEM, st>>>(c.X, c.K, W, nullptr, nullptr, 0, c.Y, EPI == EPI_SILU ? c.N / 2 : c.N, nullptr, c.M, c.N,
                               c.K, 1, nullptr, nullptr, 0L);
   } else {
-    auto k = gemm_big_kernel<BM, BN, WM, WN, BK, NBUF, EPI_NONE, false, true, 0, 0, 0, AUXB, false, PP>;
+    auto k = gemm_big_kernel<BM, BN, WM, WN, BK, NBUF, EPI_NONE, false, true, 0, 0, AUXB, PP>;
     static bool attr = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM) == hipSuccess;
     (void)attr;
     k<<<nwg, 512, SMEM, st>>>(c.X, c.K, W, nullptr, nullptr, 0, c.Y, c.N, c.ws, c.M, c.N, c.K, c.S, nullptr, nullptr, 0L);

@@ -263,10 +263,14 @@ __global__ __launch_bounds__(DH) void attn_decode_reduce_kernel(const float* __r
 // so that this works with contiguous V^T reads: tile t = 2kk + h, row c = 4q + r holds key
 // 32kk + 8q + 4h + r, hence lane group g of the P^T operand owns keys 32kk + 8g .. +8 and reads one
 // 16-byte run of the transposed V page.  No LDS.
-// PF: prefetch the next page's K / V into registers under the current page's math.
-// NT: K / V pages loaded non-temporal (read once per step; algo 3)
-template <int DH, bool PF, bool NT = false>
-__global__ __launch_bounds__(256) void attn_decode_wave_kernel(
+// PF 1: prefetch the next page's K / V into a second register set under the current page's math (378
+//       registers: one wave per SIMD).
+// PF 2: ONE register set, each half refilled as soon as it is consumed -- the next page's K right after the
+//       S^T MFMAs, its V right after the P.V MFMAs -- so a page's loads fly under the other half's math and,
+//       at under 256 registers, two waves per SIMD keep twice the pages in flight per CU (algo 5 / 6).
+// NT: K / V pages loaded non-temporal (read once per step; algo 3 / 6)
+template <int DH, int PF, bool NT = false>
+__global__ __launch_bounds__(256, PF == 2 ? 2 : 1) void attn_decode_wave_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
     const int32_t* __restrict__ block_tables, int max_blocks, const int32_t* __restrict__ ctx_lens,
     uint16_t* __restrict__ out, float* __restrict__ ws_o, float* __restrict__ ws_ml, int B, int H, int Hkv,
@@ -308,10 +312,9 @@ __global__ __launch_bounds__(256) void attn_decode_wave_kernel(
   //   d 32s + 8g .. +8 for k-step s
   // V^T page [DH][64 keys]: d tile dt, k-step kk, lane (g, c) reads d 16dt + c, keys 32kk + 8g .. +8
   const int krow = 8 * (c >> 2) + (c & 3);
-  auto load = [&](int p, s16x8 (&kf)[4][KS], s16x8 (&vf)[NDT][2]) {
-    const long page = min(max(bt[p], 0), num_pages - 1);
+  auto page_of = [&](int p) -> long { return min(max(bt[p], 0), num_pages - 1); };
+  auto load_k = [&](int p, long page, s16x8 (&kf)[4][KS]) {
     const uint16_t* kb = kc + ((size_t)page * Hkv + kvh) * PAGE * DH + g * 8;
-    const uint16_t* vb = vc + ((size_t)page * Hkv + kvh) * DH * PAGE + c * PAGE + 8 * g;
     // K rows past the context (the tail of the last page) re-read the last valid row: same cache lines,
     // no HBM bytes (their scores are masked).  PMC: the kernel streams HBM at ~6.0 TB/s, and the unused
     // K rows of the last page were ~4 % of its bytes at 525-token contexts.
@@ -322,20 +325,30 @@ __global__ __launch_bounds__(256) void attn_decode_wave_kernel(
 #pragma unroll
       for (int s = 0; s < KS; ++s) kf[t][s] = NT ? ld16nt(kb + r * DH + 32 * s) : ld16(kb + r * DH + 32 * s);
     }
+  };
+  auto load_v = [&](long page, s16x8 (&vf)[NDT][2]) {
+    const uint16_t* vb = vc + ((size_t)page * Hkv + kvh) * DH * PAGE + c * PAGE + 8 * g;
 #pragma unroll
     for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
         vf[dt][kk] = NT ? ld16nt(vb + 16 * dt * PAGE + 32 * kk) : ld16(vb + 16 * dt * PAGE + 32 * kk);
   };
-  auto compute = [&](int p, const s16x8 (&kf)[4][KS], const s16x8 (&vf)[NDT][2]) {
-    f32x4 st[4];
+  auto load = [&](int p, s16x8 (&kf)[4][KS], s16x8 (&vf)[NDT][2]) {
+    const long page = page_of(p);
+    load_k(p, page, kf);
+    load_v(page, vf);
+  };
+  // S^T tiles of page p (consumes K); the rest of the page (softmax, P.V) is pv() below
+  auto scores = [&](const s16x8 (&kf)[4][KS], f32x4 (&st)[4]) {
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       st[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < KS; ++s) st[t] = mfma16(kf[t][s], qf[s], st[t]);
     }
+  };
+  auto pv = [&](int p, f32x4 (&st)[4], const s16x8 (&vf)[NDT][2]) {
     const int key0 = p * PAGE + 8 * g;  // + 32kk + 4h + r
     float mx = NEG_BIG;
 #pragma unroll
@@ -369,8 +382,25 @@ __global__ __launch_bounds__(256) void attn_decode_wave_kernel(
       for (int dt = 0; dt < NDT; ++dt) o[dt] = mfma16(vf[dt][kk], pf, o[dt]);
     }
   };
+  auto compute = [&](int p, const s16x8 (&kf)[4][KS], const s16x8 (&vf)[NDT][2]) {
+    f32x4 st[4];
+    scores(kf, st);
+    pv(p, st, vf);
+  };
 
-  if constexpr (PF) {
+  if constexpr (PF == 2) {
+    s16x8 kf[4][KS], vf[NDT][2];
+    if (p_begin < p_end) load(p_begin, kf, vf);
+    for (int p = p_begin; p < p_end; ++p) {
+      const bool more = p + 1 < p_end;
+      const long nxt = more ? page_of(p + 1) : 0;  // scalar block-table read, ahead of the loads that need it
+      f32x4 st[4];
+      scores(kf, st);
+      if (more) load_k(p + 1, nxt, kf);  // K registers are free once the S^T MFMAs have read them
+      pv(p, st, vf);
+      if (more) load_v(nxt, vf);
+    }
+  } else if constexpr (PF == 1) {
     s16x8 ka[4][KS], kb2[4][KS];
     s16x8 va[NDT][2], vb2[NDT][2];
     int p = p_begin;
@@ -442,11 +472,14 @@ int launch_attn_decode(const uint16_t* q, const uint16_t* kc, const uint16_t* vc
 #define XOT_WAVE(DHV, PFV, NTV)                                                                                  \
   attn_decode_wave_kernel<DHV, PFV, NTV><<<wgs, 256, 0, s>>>(q, kc, vc, block_tables, max_blocks, ctx_lens, out, ws_o, \
                                                         ws_ml, B, H, Hkv, pages_per_part, nparts, sl, num_pages, tickets)
+    // algo 1: no prefetch; 2 / 3: double register set (3: nt loads); 5 / 6: one set refilled per half (6: nt)
     if (Dh == 128) {
-      if (algo == 3) XOT_WAVE(128, true, true); else if (algo == 2) XOT_WAVE(128, true, false); else XOT_WAVE(128, false, false);
+      if (algo == 3) XOT_WAVE(128, 1, true); else if (algo == 2) XOT_WAVE(128, 1, false);
+      else if (algo == 5) XOT_WAVE(128, 2, false); else if (algo == 6) XOT_WAVE(128, 2, true); else XOT_WAVE(128, 0, false);
       if (reduce) attn_decode_reduce_kernel<128><<<B * H, 128, 0, s>>>(ws_o, ws_ml, ctx_lens, out, H, nparts, pages_per_part);
     } else if (Dh == 64) {
-      if (algo == 3) XOT_WAVE(64, true, true); else if (algo == 2) XOT_WAVE(64, true, false); else XOT_WAVE(64, false, false);
+      if (algo == 3) XOT_WAVE(64, 1, true); else if (algo == 2) XOT_WAVE(64, 1, false);
+      else if (algo == 5) XOT_WAVE(64, 2, false); else if (algo == 6) XOT_WAVE(64, 2, true); else XOT_WAVE(64, 0, false);
       if (reduce) attn_decode_reduce_kernel<64><<<B * H, 64, 0, s>>>(ws_o, ws_ml, ctx_lens, out, H, nparts, pages_per_part);
     } else {
       return -1;

@@ -28,7 +28,6 @@
 namespace xot {
 
 
-// ABL (tools/lab only): 1 = k loop without MFMAs, 2 = without stage loads, 3 = stage loads not overlapped
 // AUXA / AUXB: cache-policy bits of the X / W LDS-DMA loads (sc0 = 1, nt = 2, sc1 = 16)
 // MOE = 1 / 2: grouped GEMM over experts (blockIdx.y = expert e, weight W[e], rows moe_off[e] ..
 // moe_off[e+1] of the expert-sorted slot order; MOE 2 gathers X row moe_gather[slot]); M is the
@@ -43,11 +42,11 @@ namespace xot {
 // MFMAs overlap the other's LDS reads.  A stage is read only in its phases 0-2 (A halves in 0 and 2, B
 // halves in 0 and 1), so in phase 3 the stage two ahead is issued into the buffer being finished, and
 // the stage one ahead is retired by a counted vmcnt (LDS-DMA stays in flight across the barriers).
-// PP 2 (8-phase per-half refills) and PP 3 (X two stages deep, W three: two weight stages in flight) are
-// lab schedules, measured slower than PP 1 (profiles/r3/lab_gemm_schedules_random.log,
-// profiles/r3/lab_s2/w_three_deep_staging.log) and not offered to the tuner.
-template <int BM, int BN, int WM, int WN, int BK, int NBUF, int EPI, bool OUT_F32, bool SPLIT, int MOE = 0, int ABL = 0,
-          int AUXA = 0, int AUXB = 3, bool PRIO = false, int PP = 0>
+// (Schedules measured slower and removed: an 8-phase per-half refill and a three-deep weight pipeline,
+// profiles/r3/lab_gemm_schedules_random.log, profiles/r3/lab_s2/w_three_deep_staging.log; 512 x 128 tiles,
+// profiles/r4/lab3.)
+template <int BM, int BN, int WM, int WN, int BK, int NBUF, int EPI, bool OUT_F32, bool SPLIT, int MOE = 0, int AUXA = 0,
+          int AUXB = 3, int PP = 0>
 __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __restrict__ X, int ldx,
                                                           const uint16_t* __restrict__ W,
                                                           const uint16_t* __restrict__ bias,
@@ -60,6 +59,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
   static_assert(WM * WN == 8, "8 waves");
   static_assert(BK == 32 || BK == 64, "k stage of 32 or 64");
   static_assert(BM % (16 * WM) == 0 && BM >= 128 && BM <= 512, "row tile of 128 .. 512 rows");
+  static_assert(PP == 0 || PP == 1, "schedules: base (0), ping-pong (1)");
   static_assert(MOE == 0 || MOE == 4 || (!SPLIT && EPI != EPI_RESID), "grouped GEMM: no slab reduce, no residual");
   static_assert(MOE != 4 || !SPLIT, "K-grouped GEMM: no K split");
   constexpr int MT = BM / (16 * WM), NT = BN / (16 * WN);
@@ -85,7 +85,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
   const int g = lane >> 4, c = lane & 15;
   const int wm = wave / WN, wn = wave % WN;
 
-  // ---- tile of this workgroup (bijective XCD remap, then split-major / column / row order)
+  // ---- tile of this workgroup (bijective XCD remap, then split-major / column / row order, grouped when tall)
   const int mtiles = (M + BM - 1) / BM, ntiles = (N + BN - 1) / BN;  // N % BN != 0: a masked last column tile
   const int nwg = mtiles * ntiles * S;
   int b = blockIdx.x;
@@ -93,7 +93,26 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
     const int xcd = b & 7, q = nwg >> 3, r = nwg & 7;
     b = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
   }
-  const int mt = b % mtiles, nt = (b / mtiles) % ntiles, split = b / (mtiles * ntiles);
+  // Tall grids (prefill, training: 8+ row tiles) are rastered in groups of GROUP_M row tiles x every column tile,
+  // column-major inside a group: the ~32 workgroups an XCD runs at once then cover 4 row tiles x 8 column tiles
+  // (12 distinct operand slices per k step in its L2) instead of one column tile x 32 row tiles (33).  Short
+  // grids (decode: 1-2 row tiles) keep the plain row-fastest order, which is already that.
+  constexpr int GROUP_M = 4;
+  int mt, nt, split;
+  {
+    const int tiles = mtiles * ntiles;
+    split = b / tiles;
+    const int bt = b - split * tiles;
+    if ((MOE == 0 || MOE == 4) && mtiles >= 2 * GROUP_M) {
+      const int per = GROUP_M * ntiles, grp = bt / per, first = grp * GROUP_M;
+      const int gm = min(mtiles - first, GROUP_M), rr = bt - grp * per;
+      mt = first + rr % gm;
+      nt = rr / gm;
+    } else {
+      mt = bt % mtiles;
+      nt = bt / mtiles;
+    }
+  }
   const int m0 = mt * BM, n0 = nt * BN;
   int row0 = 0, Mv = M;  // first output row (slot) and valid rows of this launch's row range
   if constexpr (MOE == 1 || MOE == 2) {
@@ -204,10 +223,8 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
       const int s2 = u / MT, i = u % MT;
       const s16x8 cur = af[u % LDPF];
       if (u + LDPF < KS * MT) af[u % LDPF] = ld16(As + aoff[(u + LDPF) % MT][(u + LDPF) / MT]);
-      if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int j = 0; j < NT; ++j) acc[i][j] = mfma16(cur, bf[s2][j], acc[i][j]);
-      if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
     }
   };
@@ -232,141 +249,8 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
     }
   };
 
-  if constexpr (PP == 2) {
-    // 8-phase interleave: the same four 16-MFMA quadrant phases per stage as PP == 1, but the LDS image is
-    // managed per operand HALF (A0 = the qm = 0 row tiles of both row halves, A1 = qm = 1; B0 = the qn = 0
-    // column tiles of every wave column, B1 = qn = 1; 16 KB each, 2 LDS-DMA instructions per wave), and
-    // each half is refilled with the stage two ahead as soon as every wave is two phases past its last read:
-    //   phase 0: read A0 B0 | issue A1(t+1)      phase 1: read B1
-    //   phase 2: read A1    | issue A0 B0(t+2)   phase 3: (registers only) | issue B1(t+2)
-    // so at most 2 DMA instructions issue beside each MFMA segment and every half lands 6 phases ahead of
-    // its first read; counted vmcnt(8) at the end of phases 0, 2 and 3 retires A1(t), A0 B0(t+1), B1(t+1)
-    // one phase before the barrier that precedes their reads (one barrier more than needed: the two row
-    // halves run one barrier apart).  Tail stages (t + 2 >= T) drain with vmcnt(0).
-    static_assert(BM == 256 && BN == 256 && WM == 2 && WN == 4 && BK == 64 && NBUF == 2 && ABL == 0, "PP geometry");
-    auto bar = []() {
-      asm volatile("" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-    };
-    // per-lane source / LDS destination of this wave's 2 instructions of each half
-    const uint16_t* a_src[2][2];
-    int a_dst[2][2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int rp = 16 * wave + 8 * i;                      // row of the half's 128-row set
-        const int R = (rp & 63) + ((rp >> 6) << 7) + 64 * h;  // first tile row of the instruction
-        const int row = R + lane / 8;
-        const int slot = (lane % 8) ^ aswz(row);
-        const int grow = min(m0 + row, Mv - 1);
-        a_src[h][i] = X + (size_t)grow * ldx + slot * 8;
-        a_dst[h][i] = R * BK;
-      }
-    const uint16_t* b_src[2];
-    int b_dst[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int grp = 4 * (wave >> 1) + (wave & 1) + 2 * h;  // 16-column group of this wave in half h
-      b_src[h] = W + ((size_t)min((n0 >> 4) + grp, N / 16 - 1) * kchunks) * 2048 + lane * 8;
-      b_dst[h] = A_ELEMS + grp * KS * 512;
-    }
-    auto issue_a = [&](int t, int h) {
-      uint16_t* base = smem + (t & 1) * STAGE;
-      const int k0 = (t_beg + t) * BK;
-#pragma unroll
-      for (int i = 0; i < 2; ++i) glds16<AUXA>(a_src[h][i] + k0, base + a_dst[h][i]);
-    };
-    auto issue_b = [&](int t, int h) {
-      uint16_t* base = smem + (t & 1) * STAGE;
-      const int k0 = (t_beg + t) * BK;
-      const size_t woff = (size_t)(k0 >> 7) * 2048 + ((k0 & 127) >> 5) * 512;
-#pragma unroll
-      for (int s2 = 0; s2 < KS; ++s2) glds16<AUXB>(b_src[h] + woff + s2 * 512, base + b_dst[h] + s2 * 512);
-    };
-    s16x8 af[4][2], bq[2][2][2];
-    auto read_a = [&](int buf, int qm) {
-      const uint16_t* As = smem + buf * STAGE;
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) af[i][s2] = ld16(As + aoff[4 * qm + i][s2]);
-    };
-    auto read_b = [&](int buf, int qn) {
-      const uint16_t* Bs = smem + buf * STAGE + A_ELEMS;
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) bq[qn][j][s2] = ld16(Bs + boff + ((2 * qn + j) * KS + s2) * 512);
-    };
-    auto quad = [&](int qm, int qn) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-            acc[4 * qm + i][2 * qn + j] = mfma16(af[i][s2], bq[qn][j][s2], acc[4 * qm + i][2 * qn + j]);
-      __builtin_amdgcn_s_setprio(0);
-      __builtin_amdgcn_sched_barrier(0);
-    };
-    if (T > 0) {
-      // prologue: stage 0 whole, stage 1 except A1 (issued in stage 0's phase 0)
-      issue_a(0, 0);
-      issue_b(0, 0);
-      issue_b(0, 1);
-      issue_a(0, 1);
-      if (T > 1) {
-        issue_a(1, 0);
-        issue_b(1, 0);
-        issue_b(1, 1);
-        wait_vm<8>();  // A0 B0 B1 of stage 0 landed (B1 is read before the row halves' phase-0 waits)
-      } else {
-        wait_vm<0>();
-      }
-      bar();
-      const int half = __builtin_amdgcn_readfirstlane(wm);
-      if (half == 1) bar();  // row-half 1 runs one barrier behind
-      for (int t = 0; t < T; ++t) {
-        const int buf = t & 1;
-        const bool steady = t + 2 < T;
-        // phase 0
-        read_a(buf, 0);
-        read_b(buf, 0);
-        if (t + 1 < T) issue_a(t + 1, 1);
-        bar();
-        quad(0, 0);
-        if (steady) wait_vm<8>(); else wait_vm<0>();  // A1(t) landed
-        bar();
-        // phase 1
-        read_b(buf, 1);
-        bar();
-        quad(0, 1);
-        bar();
-        // phase 2
-        read_a(buf, 1);
-        if (steady) {
-          issue_a(t + 2, 0);
-          issue_b(t + 2, 0);
-        }
-        bar();
-        quad(1, 1);
-        if (steady) wait_vm<8>(); else wait_vm<0>();  // A0 B0(t+1) landed
-        bar();
-        // phase 3
-        if (steady) issue_b(t + 2, 1);
-        bar();
-        quad(1, 0);
-        if (steady) wait_vm<8>(); else wait_vm<0>();  // B1(t+1) landed
-        bar();
-      }
-      if (half == 0) bar();  // balance the barrier count
-    }
-  } else if constexpr (PP == 1) {
-    static_assert(BM == 256 && BN == 256 && WM == 2 && WN == 4 && BK == 64 && NBUF == 2 && ABL == 0, "PP geometry");
+  if constexpr (PP == 1) {
+    static_assert(BM == 256 && BN == 256 && WM == 2 && WN == 4 && BK == 64 && NBUF == 2, "PP geometry");
     auto bar = []() {  // raw barrier (no vmcnt / lgkmcnt drain); the asm statements are compiler fences
       asm volatile("" ::: "memory");
       __builtin_amdgcn_s_barrier();
@@ -441,45 +325,6 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
       }
       if (half == 0) bar();  // balance the barrier count
     }
-  } else if constexpr (PP == 3) {
-    // X two stages deep, W three: the LDS holds 2 X images and 3 W images (2 x 32 + 3 x 32 KB = 160 KB), so
-    // the weight stream -- the operand that misses L2 -- has two stages in flight under the MFMAs of a third
-    // while the L2-resident activations keep one.  Per iteration t: X(t+1) is issued, then W(t+2); the
-    // counted wait at the end leaves only W(t+2) in flight, which retires X(t+1) and W(t+1) (issued earlier).
-    static_assert(BM == 256 && BN == 256 && BK == 64 && NBUF == 2 && !A_UNEVEN && !B_UNEVEN && ABL == 0,
-                  "PP 3 geometry");
-    uint16_t* const Xs = smem;                // 2 x A_ELEMS
-    uint16_t* const Ws = smem + 2 * A_ELEMS;  // 3 x B_ELEMS
-    auto issue_x = [&](int t) {
-      const int k0 = (t_beg + t) * BK;
-#pragma unroll
-      for (int i = 0; i < A_INSTR; ++i) glds16<AUXA>(asrc[i] + k0, Xs + (t & 1) * A_ELEMS + aq(i) * 512);
-    };
-    auto issue_w = [&](int t) {
-      const int k0 = (t_beg + t) * BK;
-      const size_t woff = (size_t)(k0 >> 7) * 2048 + ((k0 & 127) >> 5) * 512;
-#pragma unroll
-      for (int i = 0; i < B_INSTR; ++i) glds16<AUXB>(bsrc[i] + woff, Ws + (t % 3) * B_ELEMS + bq(i) * 512);
-    };
-    if (T > 0) {
-      issue_x(0);
-      issue_w(0);
-      if (T > 1) {
-        issue_w(1);
-        wait_vm<B_INSTR>();  // X(0), W(0) landed; W(1) in flight
-      } else {
-        wait_vm<0>();
-      }
-      barrier();
-      for (int t = 0; t < T; ++t) {
-        // X buffer (t+1)&1 and W buffer (t+2)%3 were last read in iteration t-1 (every wave is past its barrier)
-        if (t + 1 < T) issue_x(t + 1);
-        if (t + 2 < T) issue_w(t + 2);
-        compute_ab(Xs + (t & 1) * A_ELEMS, Ws + (t % 3) * B_ELEMS);
-        if (t + 2 < T) wait_vm<B_INSTR>(); else wait_vm<0>();
-        barrier();
-      }
-    }
   } else if (T > 0) {
     // prologue: stages 0 .. PD-1 in flight, stage 0 landed
 #pragma unroll
@@ -489,9 +334,8 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
     barrier();
     for (int t = 0; t < T; ++t) {
       // refill the buffer computed in iteration t-1 (every wave is past that iteration's barrier)
-      if (ABL != 2 && t + PD < T) issue(t_beg + t + PD, (t + PD) % NBUF);
-      if constexpr (ABL == 3) wait_vm<0>();
-      if constexpr (ABL != 1) compute(t % NBUF);
+      if (t + PD < T) issue(t_beg + t + PD, (t + PD) % NBUF);
+      compute(t % NBUF);
       // stage t+1 landed for this wave; the barrier makes it landed for all
       wait_stages(min(PD - 1, T - 2 - t));
       barrier();
@@ -613,26 +457,26 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
   }
 }
 
-template <int BM, int BN, int BK, int NBUF, int PP>
-constexpr int big_smem() {  // LDS bytes of a gemm_big configuration (PP 3: 2 X stages + 3 W stages)
-  return PP == 3 ? (2 * BM + 3 * BN) * BK * 2 : NBUF * (BM + BN) * BK * 2;
+template <int BM, int BN, int BK, int NBUF>
+constexpr int big_smem() {  // LDS bytes of a gemm_big configuration
+  return NBUF * (BM + BN) * BK * 2;
 }
 
 template <int BM, int BN, int WM, int WN, int BK, int NBUF, int EPI, bool F32, int PP = 0>
 static void big_launch(const uint16_t* X, int ldx, const uint16_t* W, const uint16_t* bias, const uint16_t* R,
                        int ldr, void* Y, int ldy, float* ws, int M, int N, int K, int S, bool reduce,
                        hipStream_t st) {
-  constexpr int SMEM = big_smem<BM, BN, BK, NBUF, PP>();
+  constexpr int SMEM = big_smem<BM, BN, BK, NBUF>();
   static_assert(SMEM <= 160 * 1024, "LDS");
   const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN) * S;
   if (S == 1) {
-    auto kern = gemm_big_kernel<BM, BN, WM, WN, BK, NBUF, EPI, F32, false, 0, 0, 0, 3, false, PP>;
+    auto kern = gemm_big_kernel<BM, BN, WM, WN, BK, NBUF, EPI, F32, false, 0, 0, 3, PP>;
     static bool attr = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM) ==
                        hipSuccess;
     (void)attr;
     kern<<<nwg, 512, SMEM, st>>>(X, ldx, W, bias, R, ldr, Y, ldy, nullptr, M, N, K, 1, nullptr, nullptr, 0L);
   } else {
-    auto kern = gemm_big_kernel<BM, BN, WM, WN, BK, NBUF, EPI, false, true, 0, 0, 0, 3, false, PP>;
+    auto kern = gemm_big_kernel<BM, BN, WM, WN, BK, NBUF, EPI, false, true, 0, 0, 3, PP>;
     static bool attr = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM) ==
                        hipSuccess;
     (void)attr;
@@ -650,7 +494,7 @@ template <int EPI, bool F32>
 static int big_dispatch(const uint16_t* X, int ldx, const uint16_t* W, const uint16_t* bias, const uint16_t* R,
                         int ldr, void* Y, int ldy, float* ws, long ws_elems, int M, int N, int K, int bn, int S,
                         bool reduce, hipStream_t st) {
-  // bn = tile code: BN (256 / 128 / 224), 1256 / 2256 (256 x 256 on the ping-pong / 8-phase schedules), plus
+  // bn = tile code: BN (256 / 128 / 224), 1256 (256 x 256 on the ping-pong schedule), plus
   // 10000 x BM for row tiles below 256 (160 / 192 / 224: M = 320 / 384 / 448 in two tiles without padding rows)
   const int bm = bn / 10000 ? bn / 10000 : 256, code = bn % 10000;
 #define XOT_BIG(BM_, BN_, WM_, NBUF_, ...)                                                                        \
@@ -659,7 +503,6 @@ static int big_dispatch(const uint16_t* X, int ldx, const uint16_t* W, const uin
   if (bm == 256) {
     if (code == 256) XOT_BIG(256, 256, 2, 2);
     else if (code == 1256) XOT_BIG(256, 256, 2, 2, 1);  // ping-pong schedule of the 256 x 256 tile
-    else if (code == 2256) XOT_BIG(256, 256, 2, 2, 2);  // 8-phase interleave (per-half LDS refills)
     else if (code == 128) XOT_BIG(256, 128, 4, 3);
     else if (code == 224) XOT_BIG(256, 224, 4, 2);      // 7 row groups per wave (gate/up N = 57344 -> 256 tiles)
     else return -1;
@@ -706,13 +549,13 @@ int launch_gemm_kgroup(const uint16_t* X, int ldx, const uint16_t* W, uint16_t* 
   constexpr int SMEM = 2 * (256 + 256) * 64 * 2;
   const dim3 grid(((M + 255) / 256) * ((N + 255) / 256), E);
   if (resid) {
-    auto kern = gemm_big_kernel<256, 256, 2, 4, 64, 2, EPI_RESID, false, false, 4, 0, 0, 3, false, 1>;
+    auto kern = gemm_big_kernel<256, 256, 2, 4, 64, 2, EPI_RESID, false, false, 4, 0, 3, 1>;
     static bool attr = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM) ==
                        hipSuccess;
     (void)attr;
     kern<<<grid, 512, SMEM, st>>>(X, ldx, W, nullptr, Y, ldy, Y, ldy, nullptr, M, N, K, 1, koff, nullptr, 0L);
   } else {
-    auto kern = gemm_big_kernel<256, 256, 2, 4, 64, 2, EPI_NONE, false, false, 4, 0, 0, 3, false, 1>;
+    auto kern = gemm_big_kernel<256, 256, 2, 4, 64, 2, EPI_NONE, false, false, 4, 0, 3, 1>;
     static bool attr = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM) ==
                        hipSuccess;
     (void)attr;

@@ -64,7 +64,7 @@ def big_row_tile(M: int) -> int:
 
 
 def tile_width(code: int) -> int:
-  """Columns of a gemm_big tile code (BN, 1256 / 2256 = 256 on the ping-pong schedules, + 10000 x BM)."""
+  """Columns of a gemm_big tile code (BN, 1256 = 256 on the ping-pong schedule, + 10000 x BM)."""
   return code % 1000
 
 
