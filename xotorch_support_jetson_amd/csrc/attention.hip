@@ -15,6 +15,8 @@
 // Softmax runs in the log2 domain (scores pre-multiplied by scale*log2(e), exp2).  Positions and
 // the causal mask come from context_lens on device: no mask tensor is ever built or shipped
 // (the reference materialises and JSON-ships a [1,T,T] mask per hop, llm_utils.py:473-511).
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -269,9 +271,9 @@ __global__ __launch_bounds__(DH) void attn_decode_reduce_kernel(const float* __r
 //       S^T MFMAs, its V right after the P.V MFMAs -- so a page's loads fly under the other half's math and,
 //       at under 256 registers, two waves per SIMD keep twice the pages in flight per CU (algo 5 / 6).
 // NT: K / V pages loaded non-temporal (read once per step; algo 3 / 6)
-template <int DH, int PF, bool NT = false>
-__global__ __launch_bounds__(256, PF == 2 ? 2 : 1) void attn_decode_wave_kernel(
-    const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
+template <int DH, int PF, bool NT>
+__device__ __forceinline__ void decode_wave_unit(
+    const int unit, const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
     const int32_t* __restrict__ block_tables, int max_blocks, const int32_t* __restrict__ ctx_lens,
     uint16_t* __restrict__ out, float* __restrict__ ws_o, float* __restrict__ ws_ml, int B, int H, int Hkv,
     int pages_per_part, int nparts, float scale_log2, int num_pages, int* __restrict__ tickets) {
@@ -279,10 +281,6 @@ __global__ __launch_bounds__(256, PF == 2 ? 2 : 1) void attn_decode_wave_kernel(
   constexpr int NDT = DH / 16;  // 16-row d tiles of O^T
   const int lane = threadIdx.x & 63;
   const int g = lane >> 4, c = lane & 15;
-  // wave-uniform unit id in an SGPR: page indices and block-table reads stay scalar (s_load, counted by
-  // lgkmcnt), so they never force a vmcnt(0) drain of the K / V prefetch
-  const int unit = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
-  if (unit >= B * Hkv * nparts) return;  // whole wave
   const int part = unit % nparts, kvh = (unit / nparts) % Hkv, b = unit / (nparts * Hkv);
   const int G = H / Hkv;
   const int ctx = min(max(ctx_lens[b], 0), max_blocks * PAGE);
@@ -457,6 +455,23 @@ __global__ __launch_bounds__(256, PF == 2 ? 2 : 1) void attn_decode_wave_kernel(
   }
 }
 
+
+// Wave-uniform unit ids in an SGPR: page indices and block-table reads stay scalar (s_load, counted by lgkmcnt),
+// so they never force a vmcnt(0) drain of the K / V prefetch.  A grid smaller than the units (XOT_ATTN_CUS:
+// one workgroup per CU of a subset) walks them with a stride, leaving the other CUs to concurrent work.
+template <int DH, int PF, bool NT = false>
+__global__ __launch_bounds__(256, PF == 2 ? 2 : 1) void attn_decode_wave_kernel(
+    const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
+    const int32_t* __restrict__ block_tables, int max_blocks, const int32_t* __restrict__ ctx_lens,
+    uint16_t* __restrict__ out, float* __restrict__ ws_o, float* __restrict__ ws_ml, int B, int H, int Hkv,
+    int pages_per_part, int nparts, float scale_log2, int num_pages, int* __restrict__ tickets) {
+  const int total = B * Hkv * nparts;
+  for (int unit = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6)); unit < total;
+       unit += gridDim.x * 4)
+    decode_wave_unit<DH, PF, NT>(unit, q, kc, vc, block_tables, max_blocks, ctx_lens, out, ws_o, ws_ml, B, H, Hkv,
+                                 pages_per_part, nparts, scale_log2, num_pages, tickets);
+}
+
 int launch_attn_decode(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, const int32_t* block_tables,
                        int max_blocks, const int32_t* ctx_lens, uint16_t* out, float* ws_o, float* ws_ml, int B,
                        int H, int Hkv, int Dh, int pages_per_part, int nparts, float scale, int num_pages, int algo,
@@ -468,7 +483,12 @@ int launch_attn_decode(const uint16_t* q, const uint16_t* kc, const uint16_t* vc
   dim3 grid(nparts, Hkv, B);
   const float sl = scale * LOG2E;
   if (algo != 0 && algo != 4) {  // wave per (sequence, KV head, partition)
-    const int units = B * Hkv * nparts, wgs = (units + 3) / 4;
+    const int units = B * Hkv * nparts;
+    int wgs = (units + 3) / 4;
+    if (const char* e = getenv("XOT_ATTN_CUS")) {  // experiments: a persistent grid on a subset of the CUs
+      const int cap = atoi(e) * (algo >= 5 ? 2 : 1);
+      if (cap > 0 && cap < wgs) wgs = cap;
+    }
 #define XOT_WAVE(DHV, PFV, NTV)                                                                                  \
   attn_decode_wave_kernel<DHV, PFV, NTV><<<wgs, 256, 0, s>>>(q, kc, vc, block_tables, max_blocks, ctx_lens, out, ws_o, \
                                                         ws_ml, B, H, Hkv, pages_per_part, nparts, sl, num_pages, tickets)
