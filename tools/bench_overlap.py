@@ -109,7 +109,7 @@ def main():
   res = {"gemms_ms": graph_ms([[qkv, oproj]])}
   for al in (2, 5):
     algo[0] = al
-    for cus in (0, 192, 128, 96, 64):
+    for cus in ((0, 128, 96) if al == 2 else (0, 160, 128, 112, 96)):
       os.environ["XOT_ATTN_CUS"] = str(cus)
       t_a = graph_ms([[attn]])
       t_s = graph_ms([[attn, qkv, oproj]])
