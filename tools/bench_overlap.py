@@ -107,10 +107,11 @@ def main():
     linear(a, wo[i], out=yo)
 
   res = {"gemms_ms": graph_ms([[qkv, oproj]])}
+  # (round 4 also capped the attention grid to a subset of the CUs -- XOT_ATTN_CUS, since removed: attention
+  # then slows in proportion, profiles/r4/overlap/)
   for al in (2, 5):
     algo[0] = al
-    for cus in ((0, 128, 96) if al == 2 else (0, 160, 128, 112, 96)):
-      os.environ["XOT_ATTN_CUS"] = str(cus)
+    for cus in (0,):
       t_a = graph_ms([[attn]])
       t_s = graph_ms([[attn, qkv, oproj]])
       t_p = graph_ms([[attn], [qkv, oproj]])
@@ -118,7 +119,6 @@ def main():
                parallel_ms=round(t_p, 4), gain_pct=round(100 * (1 - t_p / t_s), 1))
       res[f"a{al}_cus{cus or 256}"] = r
       print(json.dumps(r), flush=True)
-  os.environ.pop("XOT_ATTN_CUS", None)
   print(json.dumps(res), flush=True)
   if args.json:
     with open(args.json, "w") as f:

@@ -15,8 +15,6 @@
 // Softmax runs in the log2 domain (scores pre-multiplied by scale*log2(e), exp2).  Positions and
 // the causal mask come from context_lens on device: no mask tensor is ever built or shipped
 // (the reference materialises and JSON-ships a [1,T,T] mask per hop, llm_utils.py:473-511).
-#include <cstdlib>
-
 #include "common.h"
 #include "kernels.h"
 
@@ -456,20 +454,19 @@ __device__ __forceinline__ void decode_wave_unit(
 }
 
 
-// Wave-uniform unit ids in an SGPR: page indices and block-table reads stay scalar (s_load, counted by lgkmcnt),
-// so they never force a vmcnt(0) drain of the K / V prefetch.  A grid smaller than the units (XOT_ATTN_CUS:
-// one workgroup per CU of a subset) walks them with a stride, leaving the other CUs to concurrent work.
+// Wave-uniform unit id in an SGPR: page indices and block-table reads stay scalar (s_load, counted by lgkmcnt),
+// so they never force a vmcnt(0) drain of the K / V prefetch.  (A strided persistent grid on a subset of the CUs,
+// to leave whole CUs to concurrent GEMMs, was measured and dropped: profiles/r4/overlap/.)
 template <int DH, int PF, bool NT = false>
 __global__ __launch_bounds__(PF == 2 ? 512 : 256, PF == 2 ? 2 : 1) void attn_decode_wave_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
     const int32_t* __restrict__ block_tables, int max_blocks, const int32_t* __restrict__ ctx_lens,
     uint16_t* __restrict__ out, float* __restrict__ ws_o, float* __restrict__ ws_ml, int B, int H, int Hkv,
     int pages_per_part, int nparts, float scale_log2, int num_pages, int* __restrict__ tickets) {
-  const int total = B * Hkv * nparts, wpg = blockDim.x >> 6;
-  for (int unit = __builtin_amdgcn_readfirstlane(blockIdx.x * wpg + (threadIdx.x >> 6)); unit < total;
-       unit += gridDim.x * wpg)
-    decode_wave_unit<DH, PF, NT>(unit, q, kc, vc, block_tables, max_blocks, ctx_lens, out, ws_o, ws_ml, B, H, Hkv,
-                                 pages_per_part, nparts, scale_log2, num_pages, tickets);
+  const int unit = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+  if (unit >= B * Hkv * nparts) return;  // whole wave
+  decode_wave_unit<DH, PF, NT>(unit, q, kc, vc, block_tables, max_blocks, ctx_lens, out, ws_o, ws_ml, B, H, Hkv,
+                               pages_per_part, nparts, scale_log2, num_pages, tickets);
 }
 
 int launch_attn_decode(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, const int32_t* block_tables,
@@ -483,14 +480,9 @@ int launch_attn_decode(const uint16_t* q, const uint16_t* kc, const uint16_t* vc
   dim3 grid(nparts, Hkv, B);
   const float sl = scale * LOG2E;
   if (algo != 0 && algo != 4) {  // wave per (sequence, KV head, partition)
-    // algo 5 / 6: 8-wave workgroups (2 waves per SIMD fill a CU's register file, so a grid capped at C
-    // workgroups occupies exactly C CUs and leaves the rest whole for concurrent work)
+    // algo 5 / 6: 8-wave workgroups (two waves per SIMD)
     const int units = B * Hkv * nparts, wpg = algo >= 5 ? 8 : 4;
-    int wgs = (units + wpg - 1) / wpg;
-    if (const char* e = getenv("XOT_ATTN_CUS")) {  // experiments: a persistent grid on a subset of the CUs
-      const int cap = atoi(e);
-      if (cap > 0 && cap < wgs) wgs = cap;
-    }
+    const int wgs = (units + wpg - 1) / wpg;
 #define XOT_WAVE(DHV, PFV, NTV)                                                                                  \
   attn_decode_wave_kernel<DHV, PFV, NTV><<<wgs, 64 * wpg, 0, s>>>(q, kc, vc, block_tables, max_blocks, ctx_lens, out, ws_o, \
                                                         ws_ml, B, H, Hkv, pages_per_part, nparts, sl, num_pages, tickets)
