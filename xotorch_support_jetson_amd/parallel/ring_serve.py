@@ -265,7 +265,9 @@ class RingServer:
     rids = [str(k) for k, _, _ in items]
     qlens = [q for _, q, _ in items]
     if self.first:
-      x = x0.to(self.dev)
+      if self.dev.type == "cuda":  # pinned + async: a pageable copy would wait for everything queued before it
+        x0 = x0.pin_memory()
+      x = x0.to(self.dev, non_blocking=True)
     else:
       x = torch.empty(sum(qlens), self.D, dtype=torch.bfloat16, device=self.dev)
       self.t.wait(self.t.irecv(x, self.prev))
