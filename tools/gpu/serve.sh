@@ -1,6 +1,6 @@
 #!/bin/bash
 # Serving through the HTTP API (Llama-3-8B): streams 1 / 64 / 256, shared-prefix cache on / off, and the
-# RCCL ring server rehearsed on one GPU (2 ranks over gloo).   bash tools/gpu/serve.sh [api|prefix|ring|ringload]...
+# RCCL ring server rehearsed on one GPU (2 ranks over gloo).   bash tools/gpu/serve.sh [api|prefix|ring|ringload|ringload2]...
 source "$(dirname "$0")/common.sh"
 for what in ${@:-api}; do
   case $what in
@@ -10,5 +10,8 @@ for what in ${@:-api}; do
             XOT_DIST_BACKEND=gloo step serve/ring_run 300 python -u -m xotorch_support_jetson_amd.main run llama-3-8b --gpus 2 --prompt "Who are you?" --max-generate-tokens 24 --disable-tui ;;
     ringload)  # API load against the 2-rank ring server (gloo hand-off through host memory: a rehearsal, not RCCL speed)
             for c in 1 64; do XOT_DIST_BACKEND=gloo step serve/ring2_c$c 600 python -u tools/bench_serve.py --ring 2 --model llama-3-8b --concurrency $c --max-tokens 64 --prompt-words 16; done ;;
+    ringload2)  # longer loads (round 4): 2 and 4 ranks, 64 / 256 streams x 256 tokens, and a shared-prefix workload
+            for r in 2 4; do for c in 64 256; do XOT_MAX_BATCH=$c XOT_DIST_BACKEND=gloo step serve/ring${r}_c${c}_t256 600 python -u tools/bench_serve.py --ring $r --model llama-3-8b --concurrency $c --max-tokens 256 --prompt-words 16; done; done
+            XOT_MAX_BATCH=64 XOT_DIST_BACKEND=gloo step serve/ring2_prefix 600 python -u tools/bench_serve.py --ring 2 --model llama-3-8b --concurrency 64 --max-tokens 128 --prompt-words 400 --shared-prefix ;;
   esac
 done
