@@ -14,6 +14,8 @@ mkdir -p "$O/scale"
 for what in ${@:-stage8 rehearse8}; do
   case $what in
     stage8) step scale/stage8 600 python -u tools/bench_stage.py --world 8 --ranks 0,3,7 --json "$O/scale/stage8.json" ;;
+    headsplit) for f in 0.6 0.7; do XOT_HEAD_SPLIT=$f step scale/headsplit_$f 600 python -u tools/bench_stage.py --world 8 \
+                 --ranks 0,7 --json "$O/scale/headsplit_$f.json"; done ;;
     stage4) step scale/stage4 600 python -u tools/bench_stage.py --world 4 --ranks 0,3 --json "$O/scale/stage4.json" ;;
     stage2) step scale/stage2 600 python -u tools/bench_stage.py --world 2 --ranks 0,1 --json "$O/scale/stage2.json" ;;
     mixstage8) step scale/mixstage8 600 python -u tools/bench_stage.py --model mixtral-8x7b --world 8 --ranks 0,3,7 \

@@ -60,6 +60,7 @@ int launch_gemm_batched(const uint16_t* X, int ldx, long xbat, const uint16_t* W
                         bool out_f32, int B, int M, int N, int K, hipStream_t s);
 long gemm_sk_sync_words(int M, int N);
 // h += bias + sum of S fp32 split-K slabs [S][rows][D] (in place, bf16), out = rmsnorm(h) * w
+void launch_mall_prefetch(const void* p, size_t bytes, int wgs, uint32_t* sink, hipStream_t s);
 void launch_splitk_resid_rmsnorm(const float* ws, int S, const uint16_t* bias, uint16_t* h, const uint16_t* w,
                                  uint16_t* out, int rows, int D, float eps, hipStream_t s);
 // grouped expert GEMM on gemm_big tiles (bm = 128 or 256 rows per tile; large per-expert row counts)

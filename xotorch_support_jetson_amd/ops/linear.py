@@ -184,7 +184,7 @@ def _default_table_path():
     dev = torch.cuda.get_device_name(torch.cuda.current_device()).replace(" ", "_").replace("/", "_")
     from ..helpers import xot_home
     # settings that change the candidate sets are part of the name, so a table never answers for another
-    tag = f"{os.environ.get('XOT_GEMM', 'auto')}-{STREAM_MAX_M}-{BIG_MIN_M}-{SLAB_TBPS:g}"
+    tag = f"{os.environ.get('XOT_GEMM', 'auto')}-{STREAM_MAX_M}-{BIG_MIN_M}-{SLAB_TBPS:g}{'' if SK else '-nosk'}"
     return str(xot_home() / "gemm" / f"{dev}-{st.st_size:x}-{int(st.st_mtime):x}-{tag}.json")
   except Exception:  # noqa: BLE001 - no table then; tuning still works in memory
     return None
@@ -546,11 +546,14 @@ FUSE_NORM = os.environ.get("XOT_FUSE_NORM", "1") == "1"
 
 
 def linear_resid_norm(x: torch.Tensor, w: torch.Tensor, h: torch.Tensor, ln_w: torch.Tensor, eps: float,
-                      bias: torch.Tensor | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
+                      bias: torch.Tensor | None = None, out: torch.Tensor | None = None,
+                      after_gemm=None) -> torch.Tensor:
   """h += x @ w.T (+ bias) in place (the residual stream) and return rmsnorm(h) * ln_w.
 
   When the projection runs split-K on the pre-shuffled layout, the GEMM leaves its fp32 slabs and one
-  kernel does the slab reduce, the residual add and the RMSNorm (instead of reduce + norm kernels)."""
+  kernel does the slab reduce, the residual add and the RMSNorm (instead of reduce + norm kernels).
+  `after_gemm()` runs once the GEMM is queued, before the norm (a fork point for side-stream work)."""
+  after_gemm = after_gemm or (lambda: None)
   if FUSE_NORM and x.is_cuda and layout_of(w) == "stream":
     if x.stride(1) != 1 or x.stride(0) % 8:
       x = x.contiguous()
@@ -564,10 +567,12 @@ def linear_resid_norm(x: torch.Tensor, w: torch.Tensor, h: torch.Tensor, ln_w: t
         C.gemm_stream(x, w, h, None, h, ws, K.EPI["resid"], cfg[1], S, True, None, False)
       else:
         C.gemm_big(x, w, h, None, h, ws, K.EPI["resid"], cfg[1], S, False)
+      after_gemm()
       out = torch.empty_like(h) if out is None else out
       C.splitk_resid_rmsnorm(ws, S, bias, h, ln_w, out, float(eps))
       return out
   linear(x, w, bias=bias, residual=h, epi="resid", out=h)
+  after_gemm()
   return K.rmsnorm(h, ln_w, eps, out=out)[0]
 
 
@@ -577,11 +582,13 @@ FUSE_ROPE = os.environ.get("XOT_FUSE_ROPE", "1") == "1"
 
 def linear_rope_kv(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None, pos: torch.Tensor,
                    cos_sin: torch.Tensor, slots: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, H: int,
-                   Hkv: int) -> torch.Tensor:
+                   Hkv: int, after_gemm=None) -> torch.Tensor:
   """qkv = x @ w.T (+ bias); returns rope(q) [T, H, Dh] and writes rope(k), v into the paged caches.
 
   When the QKV projection runs split-K on the pre-shuffled layout, its fp32 slabs go straight to one
-  kernel that sums them, rotates and writes q / the caches (no bf16 qkv round trip, one launch less)."""
+  kernel that sums them, rotates and writes q / the caches (no bf16 qkv round trip, one launch less).
+  `after_gemm()` runs once the GEMM is queued, before the RoPE kernel."""
+  after_gemm = after_gemm or (lambda: None)
   if FUSE_ROPE and x.is_cuda and layout_of(w) == "stream":
     if x.stride(1) != 1 or x.stride(0) % 8:
       x = x.contiguous()
@@ -596,9 +603,11 @@ def linear_rope_kv(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None, 
         C.gemm_stream(x, w, y, None, None, ws, K.EPI["none"], cfg[1], S, True, None, False)
       else:
         C.gemm_big(x, w, y, None, None, ws, K.EPI["none"], cfg[1], S, False)
+      after_gemm()
       Dh = k_cache.shape[-1]
       q = torch.empty(M, H, Dh, dtype=x.dtype, device=x.device)
       C.splitk_rope_kv_write(ws, S, bias, pos, cos_sin, slots, q, k_cache, v_cache, int(H), int(Hkv))
       return q
   qkv = linear(x, w, bias=bias)
+  after_gemm()
   return K.rope_kv_write(qkv, pos, cos_sin, slots, k_cache, v_cache, H, Hkv)

@@ -29,6 +29,7 @@ from ..ops.linear import linear
 from ..runtime.runner import ShardRunner
 
 KC = 64  # candidate slots per row in the split-head hand-off (>= top_k)
+HEAD_SPLIT = 0.5  # default fraction of the LM-head rows on the last stage
 
 
 @dataclass
@@ -59,7 +60,11 @@ class RingStage:
     self.seed_off = torch.tensor([seed, 0], dtype=torch.int64, device=dev)
     self.D = runner.config.hidden_size
     V = runner.config.vocab_size
-    self.vs = (V // 2) // 256 * 256  # rows of the last stage's share (GEMM-tile aligned)
+    # rows of the last stage's share (GEMM-tile aligned).  XOT_HEAD_SPLIT: its fraction of the vocab -- the first
+    # stage also runs the embedding, the candidate copy and the sampler over its columns, so a share above one
+    # half evens the two ends out
+    frac = float(os.environ.get("XOT_HEAD_SPLIT", str(HEAD_SPLIT)))
+    self.vs = int(V * frac) // 256 * 256
     want = os.environ.get("XOT_SPLIT_HEAD", "1") == "1" if split_head is None else split_head
     # the decision depends only on config and arguments, so every rank takes the same one
     self.split = bool(want and world > 1 and 0 < self.vs < V and 1 <= top_k <= KC and top_k < self.vs)
