@@ -676,6 +676,35 @@ def test_attention_train_fwd_bwd(gpu, B, L, H, Hkv, Dh):
     assert rel_err(g[:, sl], x.grad[:, sl]) < 3e-2, name
 
 
+@pytest.mark.parametrize("B,L,H,Dh", [(1, 577, 16, 64), (2, 64, 4, 128), (3, 100, 8, 64), (1, 1, 2, 128)])
+def test_attention_bidir(gpu, B, L, H, Dh):
+  """Bidirectional attention (the vision tower's) on the training forward kernel with the causal mask off vs
+  fp32 softmax(q k^T) v, q / k / v as column slices of one qkv tensor."""
+  torch.manual_seed(B * L + H)
+  qkv = (torch.randn(B * L, 3 * H * Dh, device=gpu) * 0.5).to(torch.bfloat16)
+  q, k, v = qkv[:, :H * Dh], qkv[:, H * Dh:2 * H * Dh], qkv[:, 2 * H * Dh:]
+  got = K.attention_bidir(q, k, v, B, L, H, Dh, Dh ** -0.5)
+  ref = K.attention_bidir(*(t.float().cpu() for t in (q, k, v)), B, L, H, Dh, Dh ** -0.5)
+  assert rel_err(got.cpu(), ref) < 2e-2
+
+
+def test_vision_tower_gpu_matches_cpu(gpu):
+  """CLIP-L-shaped tower (1024 wide, 16 heads of 64, 336 px: 577 tokens; one layer run) + projector on the GPU
+  path -- weights shuffled into the stream layout (patch embedding K padded 588 -> 640), attention on the MFMA
+  kernel -- vs the fp32 CPU path on the same weights."""
+  import dataclasses
+  from xotorch_support_jetson_amd.models.config import preset
+  from xotorch_support_jetson_amd.models.vision import image_features, random_vision
+  c = preset("llava-1.5-7b-hf")
+  c = dataclasses.replace(c, vision=dict(c.vision, num_hidden_layers=2))
+  vw = random_vision(c, "cpu", seed=4)
+  pixels = torch.randn(2, 3, 336, 336, generator=torch.Generator().manual_seed(2))
+  ref = image_features(c, vw, pixels)
+  got = image_features(c, {k: t.to(gpu) for k, t in vw.items()}, pixels.to(gpu))
+  assert got.shape == ref.shape == (2 * 576, c.hidden_size)
+  assert rel_err(got.cpu(), ref) < 3e-2
+
+
 @pytest.mark.parametrize("T,E,D", [(1, 8, 4096), (37, 8, 4096), (512, 8, 1024), (5, 4, 256), (9, 16, 512),
                                    (1, 64, 2048), (37, 64, 2048), (4099, 64, 2048), (300, 160, 5120), (17, 256, 7168),
                                    (3, 32, 512), (40, 128, 4096), (16, 160, 5120)])

@@ -61,31 +61,6 @@ def test_gpu_matches_cpu_reference(gpu):
     tok = lc.argmax(-1).int()
 
 
-def test_prefetch_side_stream_leaves_decode_unchanged(gpu, monkeypatch):
-  """XOT_PREFETCH: the die-level cache warm-up forked onto a side stream inside the captured decode graph reads
-  weights only -- decode logits are bitwise those of the same runner without it."""
-  from xotorch_support_jetson_amd.models import transformer as T
-  name = "tiny-llama-d64"
-  c = preset(name)
-  L = c.num_layers
-  sh = Shard(name, 0, L - 1, L)
-  outs = []
-  for on in (0, 4):
-    monkeypatch.setattr(T, "PREFETCH_MAX_B", on)
-    r = ShardRunner(c, sh, gpu, max_batch=4, max_ctx=256, seed=3)
-    assert (r.model.pf_stream is not None) == bool(on)
-    ids = torch.randint(0, c.vocab_size, (20,), generator=torch.Generator().manual_seed(1), dtype=torch.int32)
-    lg = r.forward(["a", "b"], [12, 8], ids)
-    seq = [lg]
-    tok = lg.argmax(-1).int()
-    for _ in range(4):  # decode graphs (batch bucket 2)
-      lg = r.forward(["a", "b"], [1, 1], tok)
-      seq.append(lg)
-      tok = lg.argmax(-1).int()
-    outs.append(torch.stack([x.float().cpu() for x in seq]))
-  assert torch.equal(outs[0], outs[1])
-
-
 @pytest.mark.parametrize("frac", [0.5, 0.8])
 def test_split_head_ring_matches_full_gpu(gpu, frac, monkeypatch):
   """Two ring stages in one process (loopback transport) with the LM head split between the last and

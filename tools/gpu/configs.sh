@@ -1,6 +1,6 @@
 #!/bin/bash
 # The other BASELINE.json configs on one GPU: 8B and 70B batch-1 / batch-512 decode, Mixtral, model families,
-# weight-only FP8, long context.   bash tools/gpu/configs.sh [dense|moe|families|fp8|long|pf|b1prof]...  (default: dense moe)
+# weight-only FP8, long context.   bash tools/gpu/configs.sh [dense|moe|families|fp8|long|b1prof]...  (default: dense moe)
 source "$(dirname "$0")/common.sh"
 for what in ${@:-dense moe}; do
   case $what in
@@ -17,13 +17,6 @@ for what in ${@:-dense moe}; do
     fp8)   for m in llama-3-70b llama-3-8b; do for b in 1 64; do
              step cfg/fp8_${m}_b$b 600 python bench.py --model $m --batch-per-gpu $b --steps 32 --warmup 4 --weight-dtype fp8
            done; done ;;
-    pf)    # batch-1 decode with / without the die-level cache warm-up from a side stream (XOT_PREFETCH)
-           step pf/l8b_b1_off 600 python bench.py --model llama-3-8b --batch-per-gpu 1 --steps 64 --warmup 8
-           XOT_PREFETCH=1 step pf/l8b_b1_on 600 python bench.py --model llama-3-8b --batch-per-gpu 1 --steps 64 --warmup 8
-           XOT_PREFETCH=1 XOT_PREFETCH_WGS=256 step pf/l8b_b1_on256 600 python bench.py --model llama-3-8b --batch-per-gpu 1 --steps 64 --warmup 8
-           step pf/l8b_b1_off2 600 python bench.py --model llama-3-8b --batch-per-gpu 1 --steps 64 --warmup 8
-           step pf/l70b_b1_off 600 python bench.py --model llama-3-70b --batch-per-gpu 1 --steps 16 --warmup 3
-           XOT_PREFETCH=1 step pf/l70b_b1_on 600 python bench.py --model llama-3-70b --batch-per-gpu 1 --steps 16 --warmup 3 ;;
     b1prof) ;;
     long)  for t in 8192 32768 65536; do step long/l8b_$t 600 python -u tools/bench_long_prefill.py --model llama-3.1-8b --tokens $t; done
            step long/l70b_32768 600 python -u tools/bench_long_prefill.py --model llama-3.1-70b --tokens 32768 ;;

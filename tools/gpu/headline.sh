@@ -1,6 +1,6 @@
 #!/bin/bash
 # Headline (BASELINE config 3, Llama-3-70B, 512 sequences, one GPU) and its kernel breakdown.
-#   bash tools/gpu/headline.sh [bench|ab|sk|prof|sweep]...      (default: bench prof)
+#   bash tools/gpu/headline.sh [bench|ab|sk|tune|prof|sweep]...      (default: bench prof)
 source "$(dirname "$0")/common.sh"
 for what in ${@:-bench prof}; do
   case $what in
@@ -15,6 +15,10 @@ for what in ${@:-bench prof}; do
            XOT_GEMM_TABLE=$O/headline/tbl_default.json step headline/sk_on 400 python -u bench.py --steps 20 --warmup 5
            XOT_GEMM_SK=0 XOT_GEMM_TABLE=$O/headline/tbl_nosk.json step headline/sk_off 400 python -u bench.py --steps 20 --warmup 5
            XOT_GEMM_TABLE=$O/headline/tbl_default.json step headline/sk_on2 400 python -u bench.py --steps 20 --warmup 5 ;;
+    tune)  # GEMM tuner timing at the power cap (sustained, default) vs isolated cold calls (XOT_TUNE_SUSTAINED_M=0)
+           XOT_GEMM_TABLE=$O/headline/tbl_sustained.json step headline/tune_sustained 600 python -u bench.py --steps 20 --warmup 5
+           XOT_TUNE_SUSTAINED_M=0 XOT_GEMM_TABLE=$O/headline/tbl_isolated.json step headline/tune_isolated 400 python -u bench.py --steps 20 --warmup 5
+           XOT_GEMM_TABLE=$O/headline/tbl_sustained.json step headline/tune_sustained2 400 python -u bench.py --steps 20 --warmup 5 ;;
     sweep) for b in 448 512 576; do step headline/b$b 400 python -u bench.py --batch-per-gpu $b --steps 10 --warmup 3; done ;;
   esac
 done

@@ -90,7 +90,8 @@ struct TransTile {
 // V^T fragment read from LDS feeds FRB MFMAs.  FRB = 2 halves the LDS reads per MFMA but also halves the
 // grid (512 workgroups for 32 heads at L = 2048, under two per CU), which measured slower (116 vs 103 us).
 constexpr int FRB = 1, FQT = 64 * FRB;  // FRB = 2 measured slower at L = 2048 (half the workgroups)
-template <int DH>
+// CAUSAL = false: every query attends to all L keys (the bidirectional attention of the CLIP vision tower).
+template <int DH, bool CAUSAL = true>
 __global__ __launch_bounds__(256) void attn_train_fwd_kernel(const uint16_t* __restrict__ Q, long ldq,
                                                              const uint16_t* __restrict__ K, long ldk,
                                                              const uint16_t* __restrict__ VT, int Lp,
@@ -107,7 +108,8 @@ __global__ __launch_bounds__(256) void attn_train_fwd_kernel(const uint16_t* __r
   const int kvh = h / (H / Hkv);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
   const int q0 = qt * FQT, qrow = q0 + 16 * FRB * wave;  // row block rb: rows qrow + 16 rb ..
-  const int ktl = min((L + TT - 1) / TT, (q0 + FQT + TT - 1) / TT) - 1;  // last key tile under the mask
+  const int ktl = CAUSAL ? min((L + TT - 1) / TT, (q0 + FQT + TT - 1) / TT) - 1  // last key tile under the mask
+                         : (L + TT - 1) / TT - 1;
   const uint16_t* Kb = K + (long)b * L * ldk + kvh * DH;
   const uint16_t* VTb = VT + ((long)b * Hkv + kvh) * DH * Lp;
   const float sl = scale * L2E;
@@ -168,7 +170,7 @@ __global__ __launch_bounds__(256) void attn_train_fwd_kernel(const uint16_t* __r
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int key = k0 + 16 * t + c, qi = qrow + 16 * rb + 4 * g + r;
-          const float v = (key <= qi && key < L) ? sc[rb][t][r] * sl : -INFINITY;
+          const float v = ((!CAUSAL || key <= qi) && key < L) ? sc[rb][t][r] * sl : -INFINITY;
           sc[rb][t][r] = v;
           mt[r] = fmaxf(mt[r], v);
         }
@@ -531,16 +533,23 @@ int launch_attn_train_transpose(const uint16_t* x, long ldx, uint16_t* xt, int B
 
 int launch_attn_train_fwd(const uint16_t* q, long ldq, const uint16_t* k, long ldk, const uint16_t* vt, int Lp,
                           uint16_t* o, long ldo, float* lse2, int B, int L, int H, int Hkv, int Dh, float scale,
-                          hipStream_t s) {
+                          bool causal, hipStream_t s) {
   if (B <= 0 || L <= 0) return 0;
   if (H % Hkv != 0 || Lp % TT != 0 || Lp < L) return -1;
   dim3 grid(H, (L + FQT - 1) / FQT, B);
-  if (Dh == 128)
-    attn_train_fwd_kernel<128><<<grid, 256, 0, s>>>(q, ldq, k, ldk, vt, Lp, o, ldo, lse2, L, H, Hkv, scale);
+#define XOT_FWD(DHV, CV) \
+  attn_train_fwd_kernel<DHV, CV><<<grid, 256, 0, s>>>(q, ldq, k, ldk, vt, Lp, o, ldo, lse2, L, H, Hkv, scale)
+  if (Dh == 128 && causal)
+    XOT_FWD(128, true);
+  else if (Dh == 128)
+    XOT_FWD(128, false);
+  else if (Dh == 64 && causal)
+    XOT_FWD(64, true);
   else if (Dh == 64)
-    attn_train_fwd_kernel<64><<<grid, 256, 0, s>>>(q, ldq, k, ldk, vt, Lp, o, ldo, lse2, L, H, Hkv, scale);
+    XOT_FWD(64, false);
   else
     return -1;
+#undef XOT_FWD
   return 0;
 }
 

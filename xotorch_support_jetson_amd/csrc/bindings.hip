@@ -484,17 +484,6 @@ void splitk_resid_rmsnorm(const at::Tensor& ws, int64_t splits, const c10::optio
                                    (int)D, (float)eps, cur_stream());
 }
 
-// Read `t` once on the current stream so the die-level cache holds it for the GEMM that streams it next
-// (batch-1 decode: launched on a side stream while the short attention / norm kernels leave HBM idle).
-void mall_prefetch(const at::Tensor& t, at::Tensor& sink, int64_t wgs) {
-  CHECK_GPU(t);
-  CHECK_GPU(sink);
-  XCHECK(t.is_contiguous() && sink.scalar_type() == at::kInt && sink.numel() >= 256, "mall_prefetch: bad args");
-  XCHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0 && wgs >= 1, "mall_prefetch: unaligned");
-  xot::launch_mall_prefetch(t.data_ptr(), (size_t)t.numel() * t.element_size(), (int)wgs,
-                            reinterpret_cast<uint32_t*>(sink.data_ptr<int>()), cur_stream());
-}
-
 // grouped expert GEMM: y[slot] = x[gather ? gather[slot] : slot] @ w[e].T for slots of expert e
 // splits > 1 (fp32 output, no epilogue): K slice s writes rows [s*slots, (s+1)*slots) of y ([splits*slots, N]),
 // summed by moe_combine(..., splits)
@@ -755,7 +744,8 @@ void attn_train_transpose(const at::Tensor& x, at::Tensor& xt, int64_t B, int64_
 }
 
 void attn_train_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& vt, at::Tensor& o, at::Tensor& lse2,
-                    int64_t B, int64_t L, int64_t Lp, int64_t H, int64_t Hkv, int64_t Dh, double scale) {
+                    int64_t B, int64_t L, int64_t Lp, int64_t H, int64_t Hkv, int64_t Dh, double scale,
+                    bool causal) {
   check_rows(q, B * L, H * Dh, "q");
   check_rows(k, B * L, Hkv * Dh, "k");
   check_trans(vt, B, Hkv, Dh, Lp, "vt");
@@ -765,7 +755,7 @@ void attn_train_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& 
   XCHECK(lse2.is_contiguous() && lse2.numel() == B * H * L, "attn_train_fwd: lse2 [B, H, L]");
   const int rc = xot::launch_attn_train_fwd(bf(q), q.stride(0), bf(k), k.stride(0), bf(vt), (int)Lp, bf(o),
                                             o.stride(0), lse2.data_ptr<float>(), (int)B, (int)L, (int)H, (int)Hkv,
-                                            (int)Dh, (float)scale, cur_stream());
+                                            (int)Dh, (float)scale, causal, cur_stream());
   XCHECK(rc == 0, "attn_train_fwd: unsupported H=", H, " Hkv=", Hkv, " Dh=", Dh);
 }
 
@@ -933,7 +923,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_big", &gemm_big, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("bias"), py::arg("res"),
         py::arg("ws"), py::arg("epi"), py::arg("bn"), py::arg("splits"), py::arg("reduce") = true);
   m.def("splitk_resid_rmsnorm", &splitk_resid_rmsnorm);
-  m.def("mall_prefetch", &mall_prefetch);
   m.def("gemm_moe", &gemm_moe, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("off"), py::arg("gather"),
         py::arg("epi"), py::arg("max_rows"), py::arg("wshuf"), py::arg("splits") = 1, py::arg("big_bm") = 0);
   m.def("moe_route", &moe_route);

@@ -60,7 +60,6 @@ int launch_gemm_batched(const uint16_t* X, int ldx, long xbat, const uint16_t* W
                         bool out_f32, int B, int M, int N, int K, hipStream_t s);
 long gemm_sk_sync_words(int M, int N);
 // h += bias + sum of S fp32 split-K slabs [S][rows][D] (in place, bf16), out = rmsnorm(h) * w
-void launch_mall_prefetch(const void* p, size_t bytes, int wgs, uint32_t* sink, hipStream_t s);
 void launch_splitk_resid_rmsnorm(const float* ws, int S, const uint16_t* bias, uint16_t* h, const uint16_t* w,
                                  uint16_t* out, int rows, int D, float eps, hipStream_t s);
 // grouped expert GEMM on gemm_big tiles (bm = 128 or 256 rows per tile; large per-expert row counts)
@@ -111,7 +110,7 @@ int launch_attn_train_transpose(const uint16_t* x, long ldx, uint16_t* xt, int B
                                 hipStream_t s);
 int launch_attn_train_fwd(const uint16_t* q, long ldq, const uint16_t* k, long ldk, const uint16_t* vt, int Lp,
                           uint16_t* o, long ldo, float* lse2, int B, int L, int H, int Hkv, int Dh, float scale,
-                          hipStream_t s);
+                          bool causal, hipStream_t s);
 int launch_attn_train_bwd(const uint16_t* q, long ldq, const uint16_t* qt, const uint16_t* k, long ldk,
                           const uint16_t* kt, const uint16_t* v, long ldv, const uint16_t* o, long ldo,
                           const uint16_t* dout, long lddo, const uint16_t* doutt, int Lp, const float* lse2,

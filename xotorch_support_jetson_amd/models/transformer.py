@@ -43,11 +43,6 @@ PAGE = 64
 # streams, so one half's HBM-bound attention overlaps the other half's MFMA-bound GEMMs (0: off)
 SPLIT_DECODE_MIN = int(os.environ.get("XOT_SPLIT_DECODE", "0"))
 SPLIT_OFFSET = os.environ.get("XOT_SPLIT_OFFSET", "1") == "1"
-# XOT_PREFETCH=N: decode steps of at most N sequences warm the die-level cache from a side stream while the
-# short kernels leave HBM idle -- the o projection during RoPE / attention / merge, the next layer's QKV during
-# the post-MLP reduce + norm (0: off).  XOT_PREFETCH_WGS: workgroups of the warm-up kernel.
-PREFETCH_MAX_B = int(os.environ.get("XOT_PREFETCH", "0"))
-PREFETCH_WGS = int(os.environ.get("XOT_PREFETCH_WGS", "128"))
 
 
 def moe_tiles(rows: float, E: int) -> Tuple[int, int, int]:
@@ -132,10 +127,6 @@ class ShardModel:
     self.ws = None
     self.ws2 = None  # attention workspace of the second half-batch of a split decode step
     self.side = None
-    self.pf_stream = None  # side stream of the die-level cache warm-up (XOT_PREFETCH)
-    if self.device.type == "cuda" and PREFETCH_MAX_B:
-      self.pf_stream = torch.cuda.Stream(self.device)
-      self.pf_sink = torch.zeros(256, dtype=torch.int32, device=self.device)
     if self.device.type == "cuda":
       if c.is_mla:
         self.ws = K.MLAWorkspace(max_batch, c.num_heads, c.kv_lora_rank, max_ctx, self.device)
@@ -206,15 +197,13 @@ class ShardModel:
       o = torch.bmm(o_lat.float(), lw.wuv.float().transpose(1, 2)).to(dt)
     return o.transpose(0, 1).reshape(T, H * dv)
 
-  def _mlp(self, xn: torch.Tensor, lw, h: torch.Tensor, next_norm: Optional[torch.Tensor], li: int = -1,
-           after_down=None):
-    """h += MLP(xn) in place; returns rmsnorm(h) * next_norm (None if there is no following norm).
-    `after_down()` runs once the down projection is queued (dense MLP only)."""
+  def _mlp(self, xn: torch.Tensor, lw, h: torch.Tensor, next_norm: Optional[torch.Tensor], li: int = -1):
+    """h += MLP(xn) in place; returns rmsnorm(h) * next_norm (None if there is no following norm)."""
     c = self.c
     if lw.router is None:
       act = linear(xn, lw.gu_w, epi="silu")
       if next_norm is not None:
-        return linear_resid_norm(act, lw.down_w, h, next_norm, c.rms_norm_eps, after_gemm=after_down)
+        return linear_resid_norm(act, lw.down_w, h, next_norm, c.rms_norm_eps)
       linear(act, lw.down_w, residual=h, epi="resid", out=h)
       return None
     out = self._moe(xn, lw, h, next_norm)
@@ -348,7 +337,6 @@ class ShardModel:
     last = self.shard.is_last_layer()
     n = len(self.layer_ids)
     xn, _ = K.rmsnorm(h, w.layers[self.layer_ids[0]].ln1, c.rms_norm_eps) if n else (None, None)
-    pf = self._prefetcher(inp)
     for j, li in enumerate(self.layer_ids):
       lw = w.layers[li]
       if c.is_mla:
@@ -356,17 +344,14 @@ class ShardModel:
       else:
         # QKV projection + RoPE + paged KV write (split-K slabs reduced inside the RoPE kernel)
         q = linear_rope_kv(xn, lw.qkv_w, lw.qkv_b, inp.positions, self.cos_sin, inp.slots, self.kv.k[j],
-                           self.kv.v[j], c.num_heads, c.num_kv_heads, after_gemm=pf and (lambda: pf(lw.o_w)))
+                           self.kv.v[j], c.num_heads, c.num_kv_heads)
         a = self._attention(q, j, inp).view(h.shape[0], c.num_heads * c.head_dim)
       # o_proj + residual + post-attention norm (one fused pass when the projection runs split-K)
       xn = linear_resid_norm(a, lw.o_w, h, lw.ln2, c.rms_norm_eps)
       # the norm that follows this layer: the next layer's input norm, or the final norm (decode: every row
       # is a sequence's last token) -- fused into the down projection's reduce the same way
       nxt = w.layers[self.layer_ids[j + 1]].ln1 if j + 1 < n else (w.norm if last and inp.decode else None)
-      nqkv = w.layers[self.layer_ids[j + 1]].qkv_w if pf and j + 1 < n and not c.is_mla else None
-      xn = self._mlp(xn, lw, h, nxt, li, after_down=nqkv is not None and (lambda: pf(nqkv)) or None)
-    if pf:
-      torch.cuda.current_stream(self.device).wait_stream(self.pf_stream)
+      xn = self._mlp(xn, lw, h, nxt, li)
     if not last:
       return h
     if not inp.decode or n == 0:
@@ -377,19 +362,6 @@ class ShardModel:
     # LM head split with another stage (parallel/pipeline.py): logits of vocab rows [0, head_rows) and
     # the normed hidden state the other stage applies the remaining rows to
     return linear(xn, self._head_slice(), out_dtype=torch.float32), xn
-
-  def _prefetcher(self, inp: StepInputs):
-    """None, or fn(weight) that forks the side stream here and queues a die-level cache warm-up of `weight`
-    on it (XOT_PREFETCH; joined back at the end of the forward)."""
-    if self.pf_stream is None or not inp.decode or inp.batch > PREFETCH_MAX_B:
-      return None
-    C = K.require()
-
-    def pf(wt):
-      self.pf_stream.wait_stream(torch.cuda.current_stream(self.device))
-      with torch.cuda.stream(self.pf_stream):
-        C.mall_prefetch(wt, self.pf_sink, PREFETCH_WGS)
-    return pf
 
   def _split_ok(self, inp: StepInputs) -> bool:
     c = self.c

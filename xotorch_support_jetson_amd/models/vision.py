@@ -6,8 +6,8 @@ chat as an image part (chatgpt_api.py:97-128), but its torchtune engine has no v
 here follow HF LlavaForConditionalGeneration (vision_feature_layer -2, "default" select = drop CLS,
 linear_1 -> GELU -> linear_2) and CLIPImageProcessor (shortest edge 336 bicubic, center crop, CLIP mean /
 std).  The tower runs once per image at prefill: its GEMMs go through the kernel library's `linear`
-(pre-shuffled stream / big-tile GEMMs or hipBLASLt), attention through fused SDPA (bidirectional, 577
-tokens), LayerNorm in torch.
+(weights shuffled once into the stream / big-tile layout), attention through the flash-style MFMA kernel
+with the causal mask off (577 tokens, ops.kernels.attention_bidir), LayerNorm in torch.
 
 Images travel inside the prompt string as `<|xot_image:URL|>` markers (URL = data: base64 or a file inside
 image_dir(); there is no network), so a prompt forwarded to the first shard over gRPC keeps its image; the first
@@ -18,10 +18,13 @@ from __future__ import annotations
 import base64
 import io
 import re
+import weakref
 from typing import Dict, List, Tuple
 
 import torch
 import torch.nn.functional as F
+
+from ..ops import kernels as K
 
 IMAGE_MARK = "<|xot_image:{}|>"
 _MARK_RE = re.compile(r"<\|xot_image:(.*?)\|>", re.S)
@@ -171,9 +174,34 @@ def random_vision(c, device, dtype=torch.bfloat16, seed: int = 0, std: float = 0
 
 
 # ---------------------------------------------------------------------------------- forward
+# GPU copies of the tower's projection weights in the kernel library's pre-shuffled layout (made once per weight
+# tensor, on first use), so the tower runs on the same stream / big-tile GEMMs as the language model; the
+# checkpoint-facing dict keeps the HF row-major tensors
+_SHUF: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
+
+
+def _stream_weight(w: torch.Tensor) -> torch.Tensor:
+  got = _SHUF.get(w)
+  if got is None:
+    from ..ops.weights_layout import shuffle_for_stream
+    N, K = w.shape
+    wp = w if K % 128 == 0 else F.pad(w, (0, -K % 128))  # zero columns: the patch embedding's K = 3 * 14 * 14
+    got = shuffle_for_stream(wp.contiguous())
+    got.xot_layout = "stream"
+    _SHUF[w] = got
+  return got
+
+
 def _lin(x, w, b):
   from ..ops.linear import linear
-  y = linear(x.contiguous(), w)
+  x = x.contiguous()
+  if x.is_cuda and w.dim() == 2 and w.shape[0] % 16 == 0 and w.dtype == torch.bfloat16 == x.dtype:
+    ws = _stream_weight(w)
+    if ws.shape[1] != x.shape[1]:
+      x = F.pad(x, (0, ws.shape[1] - x.shape[1]))
+    y = linear(x, ws, bias=b.to(x.dtype) if b is not None else None)
+    return y
+  y = linear(x, w)
   return y + b.to(y.dtype) if b is not None else y
 
 
@@ -205,13 +233,8 @@ def image_features(c, vw: Dict[str, torch.Tensor], pixels: torch.Tensor) -> torc
     r = h
     y = F.layer_norm(h.float(), (Dv,), vw[q + "layer_norm1.weight"].float(), vw[q + "layer_norm1.bias"].float(),
                      eps).to(dt).view(N * T, Dv)
-    qkv = [_lin(y, vw[q + f"self_attn.{n}.weight"], vw[q + f"self_attn.{n}.bias"]).view(N, T, nh, Dv // nh)
-           .transpose(1, 2) for n in ("q_proj", "k_proj", "v_proj")]
-    if y.is_cuda:
-      a = F.scaled_dot_product_attention(*qkv)
-    else:
-      a = F.scaled_dot_product_attention(*(t.float() for t in qkv)).to(dt)
-    a = a.transpose(1, 2).reshape(N * T, Dv)
+    qkv = [_lin(y, vw[q + f"self_attn.{n}.weight"], vw[q + f"self_attn.{n}.bias"]) for n in ("q_proj", "k_proj", "v_proj")]
+    a = K.attention_bidir(*qkv, N, T, nh, Dv // nh, (Dv // nh) ** -0.5)  # [N*T, Dv]
     h = r + _lin(a, vw[q + "self_attn.out_proj.weight"], vw[q + "self_attn.out_proj.bias"]).view(N, T, Dv).to(dt)
     r = h
     y = F.layer_norm(h.float(), (Dv,), vw[q + "layer_norm2.weight"].float(), vw[q + "layer_norm2.bias"].float(),

@@ -260,6 +260,26 @@ def attn_prefill(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, max_qlen: in
 
 
 # ------------------------------------------------------------------ sampling
+def attention_bidir(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, B: int, L: int, H: int, Dh: int,
+                    scale: float) -> torch.Tensor:
+  """Bidirectional (unmasked) multi-head attention over B sequences of L tokens: q / k / v [B*L, H*Dh] token-major
+  (row views with unit inner stride) -> o [B*L, H*Dh].  GPU: the flash-style forward of the training kernels with
+  the causal mask off (csrc/attention_train.hip; V transposed per head first) for Dh 64 / 128; CPU and other
+  head sizes (the tiny test towers): fp32 reference."""
+  if not _gpu(q) or Dh not in (64, 128):
+    qh, kh, vh = (t.float().reshape(B, L, H, Dh).transpose(1, 2) for t in (q, k, v))
+    a = torch.softmax((qh @ kh.transpose(-1, -2)) * scale, -1) @ vh
+    return a.transpose(1, 2).reshape(B * L, H * Dh).to(q.dtype)
+  C = require()
+  Lp = -(-L // 64) * 64
+  vt = torch.empty(B, H, Dh, Lp, dtype=v.dtype, device=v.device)
+  C.attn_train_transpose(v, vt, B, L, Lp, H, Dh)
+  o = torch.empty(B * L, H * Dh, dtype=q.dtype, device=q.device)
+  lse2 = torch.empty(B * H * L, dtype=torch.float32, device=q.device)
+  C.attn_train_fwd(q, k, vt, o, lse2, B, L, Lp, H, H, Dh, float(scale), False)
+  return o
+
+
 def sample(logits: torch.Tensor, temps: torch.Tensor, top_k: int, seed_off: torch.Tensor,
            out: torch.Tensor | None = None) -> torch.Tensor:
   """Greedy when temp <= 1e-5, else top-k + exponential-race sampling (all on device)."""

@@ -36,8 +36,18 @@ from .weights_layout import (can_shuffle, dequant_stream8, dequant_stream8_to_st
 # workgroup is a serial tail on one CU).
 SPLITK_IN_LAUNCH = os.environ.get("XOT_SPLITK_IN_LAUNCH", "0") == "1"
 
-# XOT_GEMM_SK=0: leave the stream-K GEMM out of the timed candidates
-SK = os.environ.get("XOT_GEMM_SK", "1") == "1"
+# XOT_GEMM_SK=1: time the stream-K GEMM among the candidates.  Off by default: at the headline it wins the
+# isolated timing of gate/up (M = 512) but fetches ~37 % more bytes from beyond L2 than the ping-pong tile, and
+# under the board power cap a whole decode step ran 0.9 % slower with it (81.64 vs 80.95 ms, same box,
+# profiles/r4/tuner/)
+SK = os.environ.get("XOT_GEMM_SK", "0") == "1"
+# Compute-bound shapes (M >= XOT_TUNE_SUSTAINED_M; 0: never) are timed the way a forward pass runs them: back to
+# back for ~15 ms per candidate after as long a warm-up, cycling over copies of the weight so every call is
+# HBM-cold -- the chip then holds the clock it holds at its power cap, and a candidate that buys isolated speed
+# with extra energy (bytes from beyond L2, slab traffic) is no longer preferred
+SUSTAINED_M = int(os.environ.get("XOT_TUNE_SUSTAINED_M", "256"))
+# XOT_GEMM_BLAS=1: time hipBLASLt among the candidates for row-major weights (off: the kernel library only)
+BLAS_CAND = os.environ.get("XOT_GEMM_BLAS", "0") == "1"
 # largest M for which the stream GEMM is a candidate (above it only gemm_big is timed)
 STREAM_MAX_M = int(os.environ.get("XOT_STREAM_MAX_M", "512"))
 # smallest M for which gemm_big is a candidate
@@ -184,7 +194,8 @@ def _default_table_path():
     dev = torch.cuda.get_device_name(torch.cuda.current_device()).replace(" ", "_").replace("/", "_")
     from ..helpers import xot_home
     # settings that change the candidate sets are part of the name, so a table never answers for another
-    tag = f"{os.environ.get('XOT_GEMM', 'auto')}-{STREAM_MAX_M}-{BIG_MIN_M}-{SLAB_TBPS:g}{'' if SK else '-nosk'}"
+    tag = (f"{os.environ.get('XOT_GEMM', 'auto')}-{STREAM_MAX_M}-{BIG_MIN_M}-{SLAB_TBPS:g}{'-sk' if SK else ''}"
+           f"-s{SUSTAINED_M}{'-blas' if BLAS_CAND else ''}")
     return str(xot_home() / "gemm" / f"{dev}-{st.st_size:x}-{int(st.st_mtime):x}-{tag}.json")
   except Exception:  # noqa: BLE001 - no table then; tuning still works in memory
     return None
@@ -261,6 +272,40 @@ class GemmPolicy:
     times.sort()
     return times[1]
 
+  @classmethod
+  def _time_sustained(cls, fn, w, target_ms: float = 15.0):
+    """Per-call time (ms) of fn(weight) run back to back at the power cap: ~target_ms of warm-up, then ~target_ms
+    timed, cycling over copies of `w` (>= 512 MB between two reads of one copy: cold in L2 and the die-level
+    cache).  None when the copies do not fit in device memory (the caller falls back to _time)."""
+    nbytes = w.numel() * w.element_size()
+    ncp = min(4, max(2, -(-(512 << 20) // nbytes) + 1))
+    try:
+      copies = [w]
+      for _ in range(ncp - 1):
+        c = w.clone()
+        if hasattr(w, "xot_layout"):
+          c.xot_layout = w.xot_layout
+        copies.append(c)
+    except torch.OutOfMemoryError:
+      return None
+    st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for i in range(ncp):
+      fn(copies[i])
+    st.record()
+    for i in range(4):
+      fn(copies[i % ncp])
+    en.record()
+    en.synchronize()
+    n = int(min(400, max(8, target_ms / max(st.elapsed_time(en) / 4, 1e-3))))
+    for i in range(n):
+      fn(copies[i % ncp])
+    st.record()
+    for i in range(n):
+      fn(copies[i % ncp])
+    en.record()
+    en.synchronize()
+    return st.elapsed_time(en) / n
+
   def stream8_cfg(self, x, w, bias, residual, epi, out_dtype) -> Tuple:
     """(ntw, split-K) of the FP8-weight stream GEMM at this M bucket (cold-cache timed once)."""
     M, Kd = x.shape
@@ -291,8 +336,10 @@ class GemmPolicy:
 
   # ---------------------------------------------------------------- row-major weights
   def choose(self, x, w, bias, residual, epi, out_dtype):
-    """Row-major weight: hipBLASLt ("blas"), the library's skinny/tiled GEMM ("hip") or the stream
-    GEMM on the row-major layout (("stream", ntw, S)); cold-cache timed once per M bucket."""
+    """Row-major weight: the library's skinny/tiled GEMM ("hip") or the stream GEMM on the row-major layout
+    (("stream", ntw, S)); cold-cache timed once per M bucket.  hipBLASLt ("blas") only when asked for
+    (XOT_GEMM=blas, or XOT_GEMM_BLAS=1 to time it among the candidates) -- every weight the models run hot is
+    pre-shuffled, so row-major weights are the odd shapes that layout does not tile."""
     if self.mode in ("hip", "blas"):
       return self.mode
     M, Kd = x.shape
@@ -302,8 +349,8 @@ class GemmPolicy:
     if got is not None:
       return got
     if self._no_tuning():
-      return "blas" if M > 128 else "hip"
-    cands = ["hip", "blas"]
+      return "hip"
+    cands = ["hip", "blas"] if BLAS_CAND else ["hip"]
     if M <= 256:
       cands += [("stream",) + c for c in self._stream_cands(M, N, Kd, epi)]
       scratch.splitk(x.device, 8 * max(M, 128) * N)
@@ -375,9 +422,13 @@ class GemmPolicy:
     scratch.splitk(x.device, max(_ws_elems(c, M, N) for c in cands))
     y = torch.empty(M, N // 2 if epi == "silu" else N, dtype=out_dtype, device=x.device)
     times = {}
+    sustained = SUSTAINED_M > 0 and M >= SUSTAINED_M
     for cfg in cands:
       try:
-        times[cfg] = self._time(lambda: _shuffled_call(x, w, bias, residual, epi, y, cfg)) + _slab_read_ms(cfg, M, N)
+        t = self._time_sustained(lambda wc: _shuffled_call(x, wc, bias, residual, epi, y, cfg), w) if sustained else None
+        if t is None:
+          t = self._time(lambda: _shuffled_call(x, w, bias, residual, epi, y, cfg))
+        times[cfg] = t + _slab_read_ms(cfg, M, N)
       except RuntimeError:
         pass
     got = min(times, key=times.get) if times else cands[0]
@@ -546,14 +597,11 @@ FUSE_NORM = os.environ.get("XOT_FUSE_NORM", "1") == "1"
 
 
 def linear_resid_norm(x: torch.Tensor, w: torch.Tensor, h: torch.Tensor, ln_w: torch.Tensor, eps: float,
-                      bias: torch.Tensor | None = None, out: torch.Tensor | None = None,
-                      after_gemm=None) -> torch.Tensor:
+                      bias: torch.Tensor | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
   """h += x @ w.T (+ bias) in place (the residual stream) and return rmsnorm(h) * ln_w.
 
   When the projection runs split-K on the pre-shuffled layout, the GEMM leaves its fp32 slabs and one
-  kernel does the slab reduce, the residual add and the RMSNorm (instead of reduce + norm kernels).
-  `after_gemm()` runs once the GEMM is queued, before the norm (a fork point for side-stream work)."""
-  after_gemm = after_gemm or (lambda: None)
+  kernel does the slab reduce, the residual add and the RMSNorm (instead of reduce + norm kernels)."""
   if FUSE_NORM and x.is_cuda and layout_of(w) == "stream":
     if x.stride(1) != 1 or x.stride(0) % 8:
       x = x.contiguous()
@@ -567,12 +615,10 @@ def linear_resid_norm(x: torch.Tensor, w: torch.Tensor, h: torch.Tensor, ln_w: t
         C.gemm_stream(x, w, h, None, h, ws, K.EPI["resid"], cfg[1], S, True, None, False)
       else:
         C.gemm_big(x, w, h, None, h, ws, K.EPI["resid"], cfg[1], S, False)
-      after_gemm()
       out = torch.empty_like(h) if out is None else out
       C.splitk_resid_rmsnorm(ws, S, bias, h, ln_w, out, float(eps))
       return out
   linear(x, w, bias=bias, residual=h, epi="resid", out=h)
-  after_gemm()
   return K.rmsnorm(h, ln_w, eps, out=out)[0]
 
 
@@ -582,13 +628,11 @@ FUSE_ROPE = os.environ.get("XOT_FUSE_ROPE", "1") == "1"
 
 def linear_rope_kv(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None, pos: torch.Tensor,
                    cos_sin: torch.Tensor, slots: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, H: int,
-                   Hkv: int, after_gemm=None) -> torch.Tensor:
+                   Hkv: int) -> torch.Tensor:
   """qkv = x @ w.T (+ bias); returns rope(q) [T, H, Dh] and writes rope(k), v into the paged caches.
 
   When the QKV projection runs split-K on the pre-shuffled layout, its fp32 slabs go straight to one
-  kernel that sums them, rotates and writes q / the caches (no bf16 qkv round trip, one launch less).
-  `after_gemm()` runs once the GEMM is queued, before the RoPE kernel."""
-  after_gemm = after_gemm or (lambda: None)
+  kernel that sums them, rotates and writes q / the caches (no bf16 qkv round trip, one launch less)."""
   if FUSE_ROPE and x.is_cuda and layout_of(w) == "stream":
     if x.stride(1) != 1 or x.stride(0) % 8:
       x = x.contiguous()
@@ -603,11 +647,9 @@ def linear_rope_kv(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None, 
         C.gemm_stream(x, w, y, None, None, ws, K.EPI["none"], cfg[1], S, True, None, False)
       else:
         C.gemm_big(x, w, y, None, None, ws, K.EPI["none"], cfg[1], S, False)
-      after_gemm()
       Dh = k_cache.shape[-1]
       q = torch.empty(M, H, Dh, dtype=x.dtype, device=x.device)
       C.splitk_rope_kv_write(ws, S, bias, pos, cos_sin, slots, q, k_cache, v_cache, int(H), int(Hkv))
       return q
   qkv = linear(x, w, bias=bias)
-  after_gemm()
   return K.rope_kv_write(qkv, pos, cos_sin, slots, k_cache, v_cache, H, Hkv)

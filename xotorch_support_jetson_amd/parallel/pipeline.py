@@ -13,7 +13,9 @@ the head is split by vocab rows between the last and the first stage:
                state [B, D] bf16 + the candidates [B, 64] to the first stage
   first stage: logits of rows [Vs, V) into [B, 64 + V - Vs] behind the received candidates, samples
                once over that row (the global top-k lies inside it) and maps the column back to a token
-so each end of the ring carries half of the head.  Without it, the last stage samples and sends the
+so each end of the ring carries part of the head: the last stage 65 % of the rows (HEAD_SPLIT), since the first
+also embeds and samples -- at 512 sequences of Llama-3-70B that evens the two ends (10.54 / 10.95 ms per tick at
+70 %, 11.38 / 11.05 at 50 %, against 10.41 for a middle stage; profiles/r4/scale/headsplit_*.json).  Without it, the last stage samples and sends the
 ids [B] int32.  Transfers are only these tensors; positions and masks live on the devices.
 """
 from __future__ import annotations
@@ -29,7 +31,7 @@ from ..ops.linear import linear
 from ..runtime.runner import ShardRunner
 
 KC = 64  # candidate slots per row in the split-head hand-off (>= top_k)
-HEAD_SPLIT = 0.5  # default fraction of the LM-head rows on the last stage
+HEAD_SPLIT = 0.65  # default fraction of the LM-head rows on the last stage (measured balance, profiles/r4/scale/)
 
 
 @dataclass

@@ -142,7 +142,7 @@ class AttentionFn(torch.autograd.Function):
       o = torch.empty(B * L, H * Dh, dtype=q.dtype, device=q.device)
       lse2 = torch.empty(B * H * L, dtype=torch.float32, device=q.device)
       vt = _transposed(C, v, B, L, Lp, Hkv, Dh)
-      C.attn_train_fwd(q, k, vt, o, lse2, B, L, Lp, H, Hkv, Dh, scale)
+      C.attn_train_fwd(q, k, vt, o, lse2, B, L, Lp, H, Hkv, Dh, scale, True)
       ctx.save_for_backward(q, k, v, o, lse2)
       return o
     ctx.save_for_backward(q, k, v)
