@@ -654,7 +654,7 @@ def test_moe_layer(gpu, T, E, k, F, shuffled):
 
 
 @pytest.mark.parametrize("B,L,H,Hkv,Dh", [(1, 64, 4, 1, 64), (2, 100, 8, 2, 128), (1, 300, 8, 8, 64),
-                                          (2, 257, 16, 4, 128)])
+                                          (2, 257, 16, 4, 128), (1, 130, 4, 4, 192)])
 def test_attention_train_fwd_bwd(gpu, B, L, H, Hkv, Dh):
   """Training attention kernels (fwd, dQ, dK/dV) vs fp32 torch autograd of causal GQA attention, with
   q / k / v given as strided row views of one fused qkv tensor (as the trainer passes them)."""
@@ -674,6 +674,29 @@ def test_attention_train_fwd_bwd(gpu, B, L, H, Hkv, Dh):
   assert rel_err(o, ref) < 2e-2
   for name, sl in (("dq", slice(0, H * Dh)), ("dk", slice(H * Dh, (H + Hkv) * Dh)), ("dv", slice((H + Hkv) * Dh, None))):
     assert rel_err(g[:, sl], x.grad[:, sl]) < 3e-2, name
+
+
+@pytest.mark.parametrize("B,L,H", [(1, 100, 4), (2, 300, 8)])
+def test_attention_qk_v_deepseek_dims(gpu, B, L, H):
+  """DeepSeek MLA training attention (q / k heads of 192, v heads of 128, v zero-padded to 192 for the 192-wide
+  kernel, custom softmax scale) vs fp32 SDPA autograd: output and all three input gradients."""
+  import torch.nn.functional as F
+  from xotorch_support_jetson_amd.train import autograd_ops as A
+  torch.manual_seed(L + H)
+  T, dqk, dv, scale = B * L, 192, 128, 0.1
+  q, k = ((torch.randn(T, H * dqk, device=gpu) * 0.5).to(torch.bfloat16).requires_grad_() for _ in range(2))
+  v = (torch.randn(T, H * dv, device=gpu) * 0.5).to(torch.bfloat16).requires_grad_()
+  o = A.attention_qk_v(q, k, v, B, L, H, dqk, dv, scale)
+  do = torch.randn_like(o)
+  o.backward(do)
+  xs = [t.detach().float().requires_grad_() for t in (q, k, v)]
+  hd = lambda t: t.reshape(B, L, H, -1).transpose(1, 2)
+  ref = F.scaled_dot_product_attention(hd(xs[0]), hd(xs[1]), hd(xs[2]), is_causal=True, scale=scale)
+  ref = ref.transpose(1, 2).reshape(T, H * dv)
+  ref.backward(do.float())
+  assert rel_err(o, ref) < 2e-2
+  for name, t, x in zip("qkv", (q, k, v), xs):
+    assert rel_err(t.grad, x.grad) < 3e-2, name
 
 
 @pytest.mark.parametrize("B,L,H,Dh", [(1, 577, 16, 64), (2, 64, 4, 128), (3, 100, 8, 64), (1, 1, 2, 128)])

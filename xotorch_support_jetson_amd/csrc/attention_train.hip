@@ -524,6 +524,8 @@ int launch_attn_train_transpose(const uint16_t* x, long ldx, uint16_t* xt, int B
   dim3 grid(Lp / TT, n, B);
   if (Dh == 128)
     attn_train_transpose_kernel<128><<<grid, 256, 0, s>>>(x, ldx, xt, L, Lp, n);
+  else if (Dh == 192)
+    attn_train_transpose_kernel<192><<<grid, 256, 0, s>>>(x, ldx, xt, L, Lp, n);
   else if (Dh == 64)
     attn_train_transpose_kernel<64><<<grid, 256, 0, s>>>(x, ldx, xt, L, Lp, n);
   else
@@ -539,7 +541,9 @@ int launch_attn_train_fwd(const uint16_t* q, long ldq, const uint16_t* k, long l
   dim3 grid(H, (L + FQT - 1) / FQT, B);
 #define XOT_FWD(DHV, CV) \
   attn_train_fwd_kernel<DHV, CV><<<grid, 256, 0, s>>>(q, ldq, k, ldk, vt, Lp, o, ldo, lse2, L, H, Hkv, scale)
-  if (Dh == 128 && causal)
+  if (Dh == 192 && causal)
+    XOT_FWD(192, true);
+  else if (Dh == 128 && causal)
     XOT_FWD(128, true);
   else if (Dh == 128)
     XOT_FWD(128, false);
@@ -577,6 +581,8 @@ int launch_attn_train_bwd(const uint16_t* q, long ldq, const uint16_t* qt, const
   } while (0)
   if (Dh == 128)
     XOT_BWD(128);
+  else if (Dh == 192)
+    XOT_BWD(192);
   else if (Dh == 64)
     XOT_BWD(64);
   else

@@ -133,8 +133,8 @@ class AttentionFn(torch.autograd.Function):
   """q [B*L, H*Dh], k / v [B*L, Hkv*Dh] (token-major, may be strided row views) -> o [B*L, H*Dh]."""
 
   @staticmethod
-  def forward(ctx, q, k, v, B, L, H, Hkv, Dh):
-    scale = Dh ** -0.5
+  def forward(ctx, q, k, v, B, L, H, Hkv, Dh, scale=None):
+    scale = Dh ** -0.5 if scale is None else float(scale)
     Lp = -(-L // 64) * 64
     ctx.dims = (B, L, Lp, H, Hkv, Dh, scale)
     if _gpu(q):
@@ -146,7 +146,7 @@ class AttentionFn(torch.autograd.Function):
       ctx.save_for_backward(q, k, v, o, lse2)
       return o
     ctx.save_for_backward(q, k, v)
-    return _attn_ref(q, k, v, B, L, H, Hkv, Dh)
+    return _attn_ref(q, k, v, B, L, H, Hkv, Dh, scale)
 
   @staticmethod
   def backward(ctx, do):
@@ -164,13 +164,13 @@ class AttentionFn(torch.autograd.Function):
       delta = torch.empty_like(lse2)
       ws = torch.empty(2 * H * B * L * Dh, dtype=torch.float32, device=q.device)  # per-query-head dK/dV partials
       C.attn_train_bwd(q, qt, k, kt, v, o, do, dot, lse2, delta, dq, dk, dv, ws, B, L, Lp, H, Hkv, Dh, scale)
-      return dq, dk, dv, None, None, None, None, None
+      return dq, dk, dv, None, None, None, None, None, None
     q, k, v = ctx.saved_tensors
     with torch.enable_grad():
       qr, kr, vr = (t.detach().float().requires_grad_() for t in (q, k, v))
-      y = _attn_ref(qr, kr, vr, B, L, H, Hkv, Dh)
+      y = _attn_ref(qr, kr, vr, B, L, H, Hkv, Dh, scale)
       y.backward(do.float())
-    return qr.grad.to(q.dtype), kr.grad.to(k.dtype), vr.grad.to(v.dtype), None, None, None, None, None
+    return qr.grad.to(q.dtype), kr.grad.to(k.dtype), vr.grad.to(v.dtype), None, None, None, None, None, None
 
 
 def _transposed(C, x, B, L, Lp, n, Dh):
@@ -180,17 +180,30 @@ def _transposed(C, x, B, L, Lp, n, Dh):
   return xt
 
 
-def _attn_ref(q, k, v, B, L, H, Hkv, Dh):
+def _attn_ref(q, k, v, B, L, H, Hkv, Dh, scale=None):
   """fp32 causal GQA attention (reference / CPU path)."""
   qh = q.float().reshape(B, L, H, Dh).transpose(1, 2)
   kh = k.float().reshape(B, L, Hkv, Dh).transpose(1, 2).repeat_interleave(H // Hkv, dim=1)
   vh = v.float().reshape(B, L, Hkv, Dh).transpose(1, 2).repeat_interleave(H // Hkv, dim=1)
-  a = F.scaled_dot_product_attention(qh, kh, vh, is_causal=True)
+  a = F.scaled_dot_product_attention(qh, kh, vh, is_causal=True, scale=scale)
   return a.transpose(1, 2).reshape(B * L, H * Dh).to(q.dtype)
 
 
-def attention(q, k, v, B, L, H, Hkv, Dh):
-  return AttentionFn.apply(q, k, v, B, L, H, Hkv, Dh)
+def attention(q, k, v, B, L, H, Hkv, Dh, scale=None):
+  return AttentionFn.apply(q, k, v, B, L, H, Hkv, Dh, scale)
+
+
+ATTN_DH = (64, 128, 192)  # head sizes of the MFMA training attention kernels
+
+
+def attention_qk_v(q, k, v, B, L, H, dqk, dv, scale):
+  """Causal attention with q / k heads of dqk and v heads of dv <= dqk (DeepSeek MLA in its expanded form:
+  192 / 128): v is zero-padded per head to dqk so one kernel head size serves both products, and the output's
+  padding columns are dropped (their gradient never reaches v).  q, k [T, H*dqk], v [T, H*dv] -> [T, H*dv]."""
+  T = q.shape[0]
+  vp = F.pad(v.reshape(T, H, dv), (0, dqk - dv)).reshape(T, H * dqk) if dv < dqk else v
+  o = attention(q.contiguous(), k.contiguous(), vp.contiguous(), B, L, H, H, dqk, scale)
+  return o.view(T, H, dqk)[..., :dv].reshape(T, H * dv)
 
 
 def rmsnorm(x, w, eps):

@@ -176,7 +176,8 @@ class ShardTrainer:
     """DeepSeek multi-head latent attention with autograd, in HF's expanded form (training sees whole
     sequences, so the key / value up-projection runs once per token): A = xn . [q_a | kv_a]^T,
     q = rmsnorm(q_a) . q_b^T, latent c = rmsnorm(kv_a), k_pe = rope(shared key), [k_nope | v] = c . kv_b^T,
-    causal attention over [q_nope | q_pe] . [k_nope | k_pe] (fused SDPA; 192-wide q/k, 128-wide v)."""
+    causal attention over [q_nope | q_pe] . [k_nope | k_pe] (192-wide q/k, 128-wide v; on the GPU the MFMA
+    flash kernels with v zero-padded to 192)."""
     c, P = self.c, self.params
     T = xn.shape[0]
     H, dn, dr, dv, Lr = c.num_heads, c.qk_nope_head_dim, c.qk_rope_head_dim, c.v_head_dim, c.kv_lora_rank
@@ -194,7 +195,11 @@ class ShardTrainer:
     kf = torch.cat([kv[..., :dn], kpe.view(T, 1, dr).expand(T, H, dr)], -1)
     vf = kv[..., dn:]
 
-    def heads(t):
+    if xn.is_cuda and dn + dr in A.ATTN_DH and dv <= dn + dr:  # the MFMA flash kernels (v padded to 192)
+      return A.attention_qk_v(qf.reshape(T, -1), kf.reshape(T, -1), vf.reshape(T, -1), B, L, H, dn + dr, dv,
+                              c.attn_scale())
+
+    def heads(t):  # CPU reference (and head sizes the kernels do not cover: the tiny test configs)
       return t.reshape(B, L, H, -1).transpose(1, 2)
     o = F.scaled_dot_product_attention(heads(qf), heads(kf), heads(vf), is_causal=True, scale=c.attn_scale())
     return o.transpose(1, 2).reshape(T, H * dv)
