@@ -881,13 +881,12 @@ def test_relayout_kernels(gpu, R, C):
 @pytest.mark.parametrize("T,Kd,N", [(256, 384, 512), (192, 512, 768)])
 def test_own_linear_grads_match_torch(gpu, with_h, T, Kd, N):
   """OwnLinearFn (forward, dX, dW accumulated over two micro-batches into the GradAcc buffer) on the MFMA
-  GEMMs vs fp32 torch autograd; dW through the relayout path (K = 384) and the token-major TN GEMM."""
+  GEMMs vs fp32 torch autograd."""
   from xotorch_support_jetson_amd.train import autograd_ops as A
   torch.manual_seed(0)
   w = (torch.randn(N, Kd, device=gpu) / math.sqrt(Kd)).to(torch.bfloat16).requires_grad_(True)
   tw, acc = A.TrainWeight(w), A.GradAcc("w", w)
   assert tw.ok
-  assert A._tn_ok(torch.empty(T, Kd, device=gpu), torch.empty(T, N, device=gpu)) == (Kd % 256 == 0)
   xs = [torch.randn(T, Kd, device=gpu, dtype=torch.bfloat16) for _ in range(2)]
   hs = [torch.randn(T, N, device=gpu, dtype=torch.bfloat16) for _ in range(2)]
   gs = [torch.randn(T, N, device=gpu, dtype=torch.bfloat16) for _ in range(2)]
@@ -902,25 +901,6 @@ def test_own_linear_grads_match_torch(gpu, with_h, T, Kd, N):
     dw_ref += g.float().t() @ x.float()
   assert w.grad is None
   assert rel_err(acc.buf, dw_ref) < 1e-2
-
-
-@pytest.mark.parametrize("K,M,N,resid,f32,strided", [(64, 256, 256, False, False, False), (4096, 512, 768, True, False, True),
-                                                     (320, 1024, 256, False, True, False), (128, 768, 512, True, False, False)])
-def test_gemm_tn(gpu, K, M, N, resid, f32, strided):
-  """C (+)= A^T B from token-major operands (csrc/gemm_tn.hip: LDS-DMA images + transposed LDS reads) vs fp32
-  torch; b as a column slice of a wider tensor, the residual in place."""
-  C = __import__("xotorch_support_jetson_amd.ops._ext", fromlist=["require"]).require()
-  torch.manual_seed(K + M)
-  a = torch.randn(K, M, device=gpu).to(torch.bfloat16)
-  bw = torch.randn(K, N + (64 if strided else 0), device=gpu).to(torch.bfloat16)
-  b = bw[:, 32:32 + N] if strided else bw
-  ref = a.float().t() @ b.float()
-  c = torch.empty(M, N, device=gpu, dtype=torch.float32 if f32 else torch.bfloat16)
-  if resid:
-    c.copy_(torch.randn(M, N, device=gpu))
-    ref = ref + c.float()
-  C.gemm_tn(a, b, c, c if resid else None)
-  assert rel_err(c, ref) < 1e-2
 
 
 @pytest.mark.parametrize("resid", [False, True])

@@ -484,33 +484,6 @@ void splitk_resid_rmsnorm(const at::Tensor& ws, int64_t splits, const c10::optio
                                    (int)D, (float)eps, cur_stream());
 }
 
-// c [M, N] = a^T . b (+ res) with a [K, M], b [K, N] token-major row views (unit inner stride): the weight
-// gradient dY^T X of a projection straight from its activations (csrc/gemm_tn.hip)
-void gemm_tn(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, const c10::optional<at::Tensor>& res) {
-  CHECK_BF16(a);
-  CHECK_BF16(b);
-  CHECK_GPU(c);
-  XCHECK(a.dim() == 2 && b.dim() == 2 && c.dim() == 2 && a.size(0) == b.size(0), "gemm_tn: a [K, M], b [K, N]");
-  XCHECK(a.stride(1) == 1 && b.stride(1) == 1 && c.is_contiguous(), "gemm_tn: unit inner strides, contiguous c");
-  const int64_t K = a.size(0), M = a.size(1), N = b.size(1);
-  XCHECK(c.size(0) == M && c.size(1) == N, "gemm_tn: c must be [M, N]");
-  const bool f32 = c.scalar_type() == at::kFloat;
-  XCHECK(f32 || c.scalar_type() == at::kBFloat16, "gemm_tn: c bf16 or fp32");
-  const uint16_t* r = nullptr;
-  int64_t ldr = 0;
-  if (res.has_value()) {
-    CHECK_BF16((*res));
-    XCHECK(!f32 && res->dim() == 2 && res->size(0) == M && res->size(1) == N && res->stride(1) == 1,
-           "gemm_tn: residual [M, N] bf16 with bf16 c");
-    r = bf(*res);
-    ldr = res->stride(0);
-  }
-  const int rc = xot::launch_gemm_tn(bf(a), (int)a.stride(0), bf(b), (int)b.stride(0), r, (int)ldr, c.data_ptr(),
-                                     (int)N, f32, r ? 1 : 0, (int)M, (int)N, (int)K,
-                                     cur_stream());
-  XCHECK(rc == 0, "gemm_tn: unsupported shape M=", M, " N=", N, " K=", K);
-}
-
 // grouped expert GEMM: y[slot] = x[gather ? gather[slot] : slot] @ w[e].T for slots of expert e
 // splits > 1 (fp32 output, no epilogue): K slice s writes rows [s*slots, (s+1)*slots) of y ([splits*slots, N]),
 // summed by moe_combine(..., splits)
@@ -950,7 +923,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_big", &gemm_big, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("bias"), py::arg("res"),
         py::arg("ws"), py::arg("epi"), py::arg("bn"), py::arg("splits"), py::arg("reduce") = true);
   m.def("splitk_resid_rmsnorm", &splitk_resid_rmsnorm);
-  m.def("gemm_tn", &gemm_tn, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("res") = py::none());
   m.def("gemm_moe", &gemm_moe, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("off"), py::arg("gather"),
         py::arg("epi"), py::arg("max_rows"), py::arg("wshuf"), py::arg("splits") = 1, py::arg("big_bm") = 0);
   m.def("moe_route", &moe_route);

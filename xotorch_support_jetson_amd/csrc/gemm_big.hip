@@ -55,7 +55,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
                                                           int M, int N, int K, int S,
                                                           const int* __restrict__ moe_off = nullptr,
                                                           const int* __restrict__ moe_gather = nullptr,
-                                                          long ysplit = 0) {
+                                                          long ysplit = 0, int group_m = 4) {
   static_assert(WM * WN == 8, "8 waves");
   static_assert(BK == 32 || BK == 64, "k stage of 32 or 64");
   static_assert(BM % (16 * WM) == 0 && BM >= 128 && BM <= 512, "row tile of 128 .. 512 rows");
@@ -93,19 +93,19 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
     const int xcd = b & 7, q = nwg >> 3, r = nwg & 7;
     b = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
   }
-  // Tall grids (prefill, training: 8+ row tiles) are rastered in groups of GROUP_M row tiles x every column tile,
+  // Tall grids (prefill, training: 8+ row tiles) are rastered in groups of group_m row tiles x every column tile,
   // column-major inside a group: the ~32 workgroups an XCD runs at once then cover 4 row tiles x 8 column tiles
   // (12 distinct operand slices per k step in its L2) instead of one column tile x 32 row tiles (33).  Short
   // grids (decode: 1-2 row tiles) keep the plain row-fastest order, which is already that.
-  constexpr int GROUP_M = 4;
+  // (group_m: 4 by default, XOT_GEMM_GROUP_M; <= 1 keeps the row-fastest order)
   int mt, nt, split;
   {
     const int tiles = mtiles * ntiles;
     split = b / tiles;
     const int bt = b - split * tiles;
-    if ((MOE == 0 || MOE == 4) && mtiles >= 2 * GROUP_M) {
-      const int per = GROUP_M * ntiles, grp = bt / per, first = grp * GROUP_M;
-      const int gm = min(mtiles - first, GROUP_M), rr = bt - grp * per;
+    if ((MOE == 0 || MOE == 4) && group_m > 1 && mtiles >= 2 * group_m) {
+      const int per = group_m * ntiles, grp = bt / per, first = grp * group_m;
+      const int gm = min(mtiles - first, group_m), rr = bt - grp * per;
       mt = first + rr % gm;
       nt = rr / gm;
     } else {
@@ -462,6 +462,15 @@ constexpr int big_smem() {  // LDS bytes of a gemm_big configuration
   return NBUF * (BM + BN) * BK * 2;
 }
 
+// grouped raster width of tall plain grids (XOT_GEMM_GROUP_M, read once; default 4)
+static int big_group_m() {
+  static const int gm = [] {
+    const char* e = getenv("XOT_GEMM_GROUP_M");
+    return e != nullptr ? atoi(e) : 4;
+  }();
+  return gm;
+}
+
 template <int BM, int BN, int WM, int WN, int BK, int NBUF, int EPI, bool F32, int PP = 0>
 static void big_launch(const uint16_t* X, int ldx, const uint16_t* W, const uint16_t* bias, const uint16_t* R,
                        int ldr, void* Y, int ldy, float* ws, int M, int N, int K, int S, bool reduce,
@@ -474,13 +483,15 @@ static void big_launch(const uint16_t* X, int ldx, const uint16_t* W, const uint
     static bool attr = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM) ==
                        hipSuccess;
     (void)attr;
-    kern<<<nwg, 512, SMEM, st>>>(X, ldx, W, bias, R, ldr, Y, ldy, nullptr, M, N, K, 1, nullptr, nullptr, 0L);
+    kern<<<nwg, 512, SMEM, st>>>(X, ldx, W, bias, R, ldr, Y, ldy, nullptr, M, N, K, 1, nullptr, nullptr, 0L,
+                                 big_group_m());
   } else {
     auto kern = gemm_big_kernel<BM, BN, WM, WN, BK, NBUF, EPI, false, true, 0, 0, 3, PP>;
     static bool attr = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM) ==
                        hipSuccess;
     (void)attr;
-    kern<<<nwg, 512, SMEM, st>>>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, S, nullptr, nullptr, 0L);
+    kern<<<nwg, 512, SMEM, st>>>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, S, nullptr, nullptr, 0L,
+                                 big_group_m());
     if (!reduce) return;  // slabs left for the consumer (fused reduce + residual + RMSNorm)
     const int ncol = EPI == EPI_SILU ? N / 2 : N;
     const long chunks = (long)M * (ncol / 8);
@@ -553,13 +564,15 @@ int launch_gemm_kgroup(const uint16_t* X, int ldx, const uint16_t* W, uint16_t* 
     static bool attr = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM) ==
                        hipSuccess;
     (void)attr;
-    kern<<<grid, 512, SMEM, st>>>(X, ldx, W, nullptr, Y, ldy, Y, ldy, nullptr, M, N, K, 1, koff, nullptr, 0L);
+    kern<<<grid, 512, SMEM, st>>>(X, ldx, W, nullptr, Y, ldy, Y, ldy, nullptr, M, N, K, 1, koff, nullptr, 0L,
+                                  big_group_m());
   } else {
     auto kern = gemm_big_kernel<256, 256, 2, 4, 64, 2, EPI_NONE, false, false, 4, 0, 3, 1>;
     static bool attr = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM) ==
                        hipSuccess;
     (void)attr;
-    kern<<<grid, 512, SMEM, st>>>(X, ldx, W, nullptr, nullptr, 0, Y, ldy, nullptr, M, N, K, 1, koff, nullptr, 0L);
+    kern<<<grid, 512, SMEM, st>>>(X, ldx, W, nullptr, nullptr, 0, Y, ldy, nullptr, M, N, K, 1, koff, nullptr, 0L,
+                                  big_group_m());
   }
   return 0;
 }
@@ -586,7 +599,7 @@ static void big_moe_launch(const uint16_t* X, int ldx, const uint16_t* W, void* 
   (void)attr;
   dim3 grid(((max_rows + BM - 1) / BM) * (N / BN) * S, E);
   kern<<<grid, 512, SMEM, st>>>(X, ldx, W, nullptr, nullptr, 0, Y, ldy, nullptr, max_rows, N, K, S, off, gather,
-                                S > 1 ? ysplit : 0L);
+                                S > 1 ? ysplit : 0L, 4);
 }
 
 // bm = row tile (128 / 192 / 256) + 1000 x pipeline variant: 0 = two 64-deep LDS stages (one in flight under

@@ -42,10 +42,6 @@ int launch_gemm_stream8(const uint16_t* X, int ldx, const uint8_t* W, const floa
 int launch_gemm_big(const uint16_t* X, int ldx, const uint16_t* W, const uint16_t* bias, const uint16_t* R, int ldr,
                     void* Y, int ldy, bool out_f32, int epi, float* ws, long ws_elems, int M, int N, int K, int bn,
                     int S, bool reduce, hipStream_t s);
-// C[M,N] (+)= A[K,M]^T . B[K,N] from token-major operands (weight gradients dY^T X without relayouts):
-// 256 x 256 x 64 tiles, M, N % 256 == 0, K % 64 == 0; epi EPI_NONE or EPI_RESID (bf16 C += ..., R may be C)
-int launch_gemm_tn(const uint16_t* A, int lda, const uint16_t* B, int ldb, const uint16_t* R, int ldr, void* C,
-                   int ldc, bool out_f32, int epi, int M, int N, int K, hipStream_t s);
 // stream-K large-M GEMM on the pre-shuffled layout: one persistent 256 x 256 x 64 workgroup per CU (cus of
 // them), split column tiles finished by their last-arriving part; part = gemm_sk_part_elems() fp32,
 // sync = gemm_sk_sync_words(M, N) int32, zero-initialised once (kept zeroed by the kernel)

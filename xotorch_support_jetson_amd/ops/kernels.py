@@ -104,6 +104,8 @@ def gemm(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, res
     out = torch.empty(M, ncol, dtype=out_dtype or x.dtype, device=x.device)
   if nt == 0:
     nt = 2 if (N // 32) >= 1024 else 1
+  if algo == 0 and epi != "silu" and N % 16:  # the skinny kernel tiles 16 output columns; the tiled one masks
+    algo = 2
   require().gemm(x, w, out, bias, residual, EPI[epi], int(algo), int(nt))
   return out
 

@@ -41,11 +41,6 @@ SPLITK_IN_LAUNCH = os.environ.get("XOT_SPLITK_IN_LAUNCH", "0") == "1"
 # under the board power cap a whole decode step ran 0.9 % slower with it (81.64 vs 80.95 ms, same box,
 # profiles/r4/tuner/)
 SK = os.environ.get("XOT_GEMM_SK", "0") == "1"
-# Compute-bound shapes (M >= XOT_TUNE_SUSTAINED_M; 0: never) are timed the way a forward pass runs them: back to
-# back for ~15 ms per candidate after as long a warm-up, cycling over copies of the weight so every call is
-# HBM-cold -- the chip then holds the clock it holds at its power cap, and a candidate that buys isolated speed
-# with extra energy (bytes from beyond L2, slab traffic) is no longer preferred
-SUSTAINED_M = int(os.environ.get("XOT_TUNE_SUSTAINED_M", "256"))
 # XOT_GEMM_BLAS=1: time hipBLASLt among the candidates for row-major weights (off: the kernel library only)
 BLAS_CAND = os.environ.get("XOT_GEMM_BLAS", "0") == "1"
 # largest M for which the stream GEMM is a candidate (above it only gemm_big is timed)
@@ -195,7 +190,7 @@ def _default_table_path():
     from ..helpers import xot_home
     # settings that change the candidate sets are part of the name, so a table never answers for another
     tag = (f"{os.environ.get('XOT_GEMM', 'auto')}-{STREAM_MAX_M}-{BIG_MIN_M}-{SLAB_TBPS:g}{'-sk' if SK else ''}"
-           f"-s{SUSTAINED_M}{'-blas' if BLAS_CAND else ''}")
+           f"{'-blas' if BLAS_CAND else ''}")
     return str(xot_home() / "gemm" / f"{dev}-{st.st_size:x}-{int(st.st_mtime):x}-{tag}.json")
   except Exception:  # noqa: BLE001 - no table then; tuning still works in memory
     return None
@@ -272,40 +267,6 @@ class GemmPolicy:
     times.sort()
     return times[1]
 
-  @classmethod
-  def _time_sustained(cls, fn, w, target_ms: float = 15.0):
-    """Per-call time (ms) of fn(weight) run back to back at the power cap: ~target_ms of warm-up, then ~target_ms
-    timed, cycling over copies of `w` (>= 512 MB between two reads of one copy: cold in L2 and the die-level
-    cache).  None when the copies do not fit in device memory (the caller falls back to _time)."""
-    nbytes = w.numel() * w.element_size()
-    ncp = min(4, max(2, -(-(512 << 20) // nbytes) + 1))
-    try:
-      copies = [w]
-      for _ in range(ncp - 1):
-        c = w.clone()
-        if hasattr(w, "xot_layout"):
-          c.xot_layout = w.xot_layout
-        copies.append(c)
-    except torch.OutOfMemoryError:
-      return None
-    st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    for i in range(ncp):
-      fn(copies[i])
-    st.record()
-    for i in range(4):
-      fn(copies[i % ncp])
-    en.record()
-    en.synchronize()
-    n = int(min(400, max(8, target_ms / max(st.elapsed_time(en) / 4, 1e-3))))
-    for i in range(n):
-      fn(copies[i % ncp])
-    st.record()
-    for i in range(n):
-      fn(copies[i % ncp])
-    en.record()
-    en.synchronize()
-    return st.elapsed_time(en) / n
-
   def stream8_cfg(self, x, w, bias, residual, epi, out_dtype) -> Tuple:
     """(ntw, split-K) of the FP8-weight stream GEMM at this M bucket (cold-cache timed once)."""
     M, Kd = x.shape
@@ -362,6 +323,8 @@ class GemmPolicy:
       except RuntimeError:
         times[impl] = float("inf")
     got = min(times, key=times.get)
+    if times[got] == float("inf"):  # a shape none of the library's kernels tiles (e.g. a 300-row LM head)
+      got = "blas"
     self._store(key, got)
     return got
 
@@ -422,13 +385,9 @@ class GemmPolicy:
     scratch.splitk(x.device, max(_ws_elems(c, M, N) for c in cands))
     y = torch.empty(M, N // 2 if epi == "silu" else N, dtype=out_dtype, device=x.device)
     times = {}
-    sustained = SUSTAINED_M > 0 and M >= SUSTAINED_M
     for cfg in cands:
       try:
-        t = self._time_sustained(lambda wc: _shuffled_call(x, wc, bias, residual, epi, y, cfg), w) if sustained else None
-        if t is None:
-          t = self._time(lambda: _shuffled_call(x, w, bias, residual, epi, y, cfg))
-        times[cfg] = t + _slab_read_ms(cfg, M, N)
+        times[cfg] = self._time(lambda: _shuffled_call(x, w, bias, residual, epi, y, cfg)) + _slab_read_ms(cfg, M, N)
       except RuntimeError:
         pass
     got = min(times, key=times.get) if times else cands[0]

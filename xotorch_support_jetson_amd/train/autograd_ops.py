@@ -11,8 +11,6 @@ OwnLinearFn  projections on the MFMA GEMMs (shuffled operands from csrc/layout.h
 """
 from __future__ import annotations
 
-import os
-
 import torch
 import torch.nn.functional as F
 
@@ -333,17 +331,6 @@ class TrainWeight:
       relayout(self.w.detach(), 1, self.wts)
 
 
-# XOT_TRAIN_DW_TN=0: weight gradients through the relayout path (dY^T and shuffle(X^T) per micro-batch) instead of
-# the token-major TN GEMM
-DW_TN = os.environ.get("XOT_TRAIN_DW_TN", "1") == "1"
-
-
-def _tn_ok(x: torch.Tensor, dy: torch.Tensor) -> bool:
-  """dW = dY^T X on csrc/gemm_tn.hip straight from the token-major operands: N, K % 256, T % 64."""
-  return (DW_TN and x.shape[0] % 64 == 0 and dy.shape[1] % 256 == 0 and x.shape[1] % 256 == 0
-          and x.stride(1) == 1 and x.stride(0) % 8 == 0)
-
-
 def _own_dw_ok(x: torch.Tensor, dy: torch.Tensor) -> bool:
   """dW = dY^T X on the tiles: dY^T [N, T] row-major and shuffle(X^T) [K, T] need T % 128, N and K % 64."""
   return x.shape[0] % 128 == 0 and dy.shape[1] % 64 == 0 and x.shape[1] % 64 == 0
@@ -354,10 +341,11 @@ class OwnLinearFn(torch.autograd.Function):
   ops/linear.py's policy) instead of hipBLASLt:
     forward   y  = x . shuffle(W)^T (+ h: the residual epilogue)
     backward  dX = dY . shuffle(W^T)^T
-              dW = dY^T . X into the GradAcc buffer (plain store on the first micro-batch of a step, residual
-                   epilogue acc += ... after) on csrc/gemm_tn.hip, which reads both token-major operands as
-                   they are; shapes it does not tile fall back to dY^T . shuffle(X^T)^T with both relaid per
-                   micro-batch by csrc/layout.hip (about 2 x T x (N + K) x 2 bytes each)."""
+              dW = dY^T . shuffle(X^T)^T into the GradAcc buffer (plain store on the first micro-batch of a
+                   step, residual epilogue acc += ... after), with dY^T and shuffle(X^T) built per micro-batch
+                   by csrc/layout.hip (about 2 x T x (N + K) x 2 bytes each).  (A token-major TN GEMM reading dY
+                   and X as they are, with transposed LDS reads, measured 5-20 % slower than relayout + the
+                   pre-shuffled tile, profiles/r4/train/dw_gemm_tn_vs_relayout_vs_hipblaslt.json.)"""
 
   @staticmethod
   def forward(ctx, x, w, tw, h, acc):
@@ -376,10 +364,7 @@ class OwnLinearFn(torch.autograd.Function):
     tw, acc = ctx.tw, ctx.acc
     dy = dy.contiguous()
     dx = linear(dy, tw.wts)
-    if _tn_ok(x, dy):
-      require().gemm_tn(dy, x, acc.buf, None if acc.fresh else acc.buf)
-      acc.fresh = False
-    elif _own_dw_ok(x, dy):
+    if _own_dw_ok(x, dy):
       dyt = relayout(dy, 2)  # [N, T]
       xts = relayout(x, 1)   # shuffle(X^T) [K, T]
       if acc.fresh:
