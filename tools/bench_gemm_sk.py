@@ -96,6 +96,7 @@ def main():
             f2 = lambda i: C.gemm_big(x, wsl[i], out, None, res, ws_buf if S > 1 else None, K.EPI[epi], bn, S)
             f2(0)
             big[(bn, S)] = t_us(f2, nc)
+        row.update(big_all={f"{b}x{s}": round(v, 1) for (b, s), v in big.items()})
         best = min(big, key=big.get)
         row.update(big_cfg=list(best), us_big=round(big[best], 1), tflops_big=round(flop / big[best] / 1e6, 1))
       ub = t_us(lambda i: L._blas(x, wl[i], None, res, epi, None, torch.bfloat16), nc)
