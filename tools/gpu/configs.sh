@@ -12,7 +12,7 @@ for what in ${@:-dense moe}; do
     families)
            step cfg/dsl_b256 600 python bench.py --model deepseek-coder-v2-lite --batch-per-gpu 256 --steps 16 --warmup 3
            step cfg/dsv3_8l_b256 600 python bench.py --model deepseek-v3 --layers 8 --batch-per-gpu 256 --steps 8 --warmup 3
-           step cfg/phi4_b256 600 python bench.py --model phi-4-mini --batch-per-gpu 256 --steps 16 --warmup 3
+           step cfg/phi4_b256 600 python bench.py --model phi-4-mini-instruct --batch-per-gpu 256 --steps 16 --warmup 3
            step cfg/llava_b64 600 python bench.py --model llava-1.5-7b-hf --batch-per-gpu 64 --steps 16 --warmup 3 ;;
     fp8)   for m in llama-3-70b llama-3-8b; do for b in 1 64; do
              step cfg/fp8_${m}_b$b 600 python bench.py --model $m --batch-per-gpu $b --steps 32 --warmup 4 --weight-dtype fp8
