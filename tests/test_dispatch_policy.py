@@ -34,3 +34,17 @@ def test_slab_charge(monkeypatch):
   assert L._slab_read_ms(("big", 256, 2), 512, 8192) * 2 == four
   monkeypatch.setattr(L, "SLAB_TBPS", 0.0)
   assert L._slab_read_ms(("big", 256, 4), 512, 8192) == 0.0
+
+
+def test_tuner_tie_break_prefers_ping_pong(monkeypatch):
+  """Within XOT_GEMM_TIE of the fastest, a 256-row tile variant at the same K split gives way to the ping-pong
+  256 x 256 tile; other kernels and other splits keep the plain minimum."""
+  t = {("big", 224, 1): 0.400, ("big", 1256, 1): 0.408, ("big", 256, 1): 0.401, ("big", 1256, 2): 0.399}
+  assert L._tie_break(t) == ("big", 1256, 2)  # the fastest is already a ping-pong config
+  t.pop(("big", 1256, 2))
+  assert L._tie_break(t) == ("big", 1256, 1)
+  t[("big", 1256, 1)] = 0.500  # beyond the tie window: the next preference inside it
+  assert L._tie_break(t) == ("big", 256, 1)
+  assert L._tie_break({("stream", 2, 4): 0.1, ("big", 1256, 1): 0.101}) == ("stream", 2, 4)
+  monkeypatch.setattr(L, "TIE", 0.0)
+  assert L._tie_break({("big", 224, 1): 0.4, ("big", 1256, 1): 0.401}) == ("big", 224, 1)

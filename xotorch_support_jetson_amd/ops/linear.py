@@ -390,7 +390,7 @@ class GemmPolicy:
         times[cfg] = self._time(lambda: _shuffled_call(x, w, bias, residual, epi, y, cfg)) + _slab_read_ms(cfg, M, N)
       except RuntimeError:
         pass
-    got = min(times, key=times.get) if times else cands[0]
+    got = _tie_break(times) if times else cands[0]
     self._store(key, got)
     return got
 
@@ -417,6 +417,23 @@ class GemmPolicy:
       if best is None or score < best[0]:
         best = (score, c)
     return best[1]
+
+
+# Isolated timings of 256-row tile variants at the same K split land within a few percent of each other and the
+# winner changes from run to run, but inside a whole decode step (back to back, at the power cap) the ping-pong
+# 256 x 256 tile is the measured winner (a 256 x 224 gate/up or plain-256 qkv pick cost ~2 % of the headline step,
+# profiles/r4/tuner/slab_penalty/): within TIE of the fastest, prefer it.
+TIE = float(os.environ.get("XOT_GEMM_TIE", "0.03"))
+_BIG_PREF = {1256: 0, 256: 1, 224: 2, 128: 3}
+
+
+def _tie_break(times: Dict) -> Tuple:
+  best = min(times, key=times.get)
+  if best[0] != "big" or best[1] not in _BIG_PREF or TIE <= 0:
+    return best
+  close = [c for c, t in times.items()
+           if c[0] == "big" and c[2] == best[2] and c[1] in _BIG_PREF and t <= times[best] * (1 + TIE)]
+  return min(close, key=lambda c: (_BIG_PREF[c[1]], times[c]))
 
 
 def _ws_elems(cfg, M, N) -> int:
