@@ -190,7 +190,7 @@ def _default_table_path():
     from ..helpers import xot_home
     # settings that change the candidate sets are part of the name, so a table never answers for another
     tag = (f"{os.environ.get('XOT_GEMM', 'auto')}-{STREAM_MAX_M}-{BIG_MIN_M}-{SLAB_TBPS:g}{'-sk' if SK else ''}"
-           f"{'-blas' if BLAS_CAND else ''}")
+           f"{'-blas' if BLAS_CAND else ''}-t{TIE:g}")
     return str(xot_home() / "gemm" / f"{dev}-{st.st_size:x}-{int(st.st_mtime):x}-{tag}.json")
   except Exception:  # noqa: BLE001 - no table then; tuning still works in memory
     return None
