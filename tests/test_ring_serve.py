@@ -73,9 +73,11 @@ def _free_port():
     return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_ring_serve_matches_single_process(world):
-  """world 2 and 3: requests spread over `world` lanes circulating the ring concurrently."""
+@pytest.mark.parametrize("world,per_rank", [(2, 1), (3, 1), (2, 2)])
+def test_ring_serve_matches_single_process(world, per_rank, monkeypatch):
+  """world 2 and 3: requests spread over `world` lanes circulating the ring concurrently (2 x 2: two lanes per
+  rank, four steps in flight on a two-rank ring)."""
+  monkeypatch.setenv("XOT_RING_LANES_PER_RANK", str(per_rank))
   ref, live1 = _serve(0, 1, None)
   assert {r: len(v) for r, v in ref.items()} == {rid: mt for rid, _, mt in REQS}
   ctx = mp.get_context("spawn")

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Serving through the HTTP API (Llama-3-8B): streams 1 / 64 / 256, shared-prefix cache on / off, and the
-# RCCL ring server rehearsed on one GPU (2 ranks over gloo).   bash tools/gpu/serve.sh [api|prefix|ring|ringload|ringload2]...
+# RCCL ring server rehearsed on one GPU (2 ranks over gloo).   bash tools/gpu/serve.sh [api|prefix|ring|ringload|ringload2|lanes]...
 source "$(dirname "$0")/common.sh"
 for what in ${@:-api}; do
   case $what in
@@ -13,5 +13,7 @@ for what in ${@:-api}; do
     ringload2)  # longer loads (round 4): 2 and 4 ranks, 64 / 256 streams x 256 tokens, and a shared-prefix workload
             for r in 2 4; do for c in 64 256; do XOT_MAX_BATCH=$c XOT_DIST_BACKEND=gloo step serve/ring${r}_c${c}_t256 600 python -u tools/bench_serve.py --ring $r --model llama-3-8b --concurrency $c --max-tokens 256 --prompt-words 16; done; done
             XOT_MAX_BATCH=64 XOT_DIST_BACKEND=gloo step serve/ring2_prefix 600 python -u tools/bench_serve.py --ring 2 --model llama-3-8b --concurrency 64 --max-tokens 128 --prompt-words 400 --shared-prefix ;;
+    lanes)  # two lanes per rank vs one (rank 0 turns one lane's ids around while another lane's step is queued)
+            for l in 1 2; do for c in 64 256; do XOT_RING_LANES_PER_RANK=$l XOT_MAX_BATCH=$c XOT_DIST_BACKEND=gloo step serve/ring2_c${c}_lanes$l 600 python -u tools/bench_serve.py --ring 2 --model llama-3-8b --concurrency $c --max-tokens 256 --prompt-words 16; done; done ;;
   esac
 done

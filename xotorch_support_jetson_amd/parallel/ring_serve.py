@@ -4,7 +4,8 @@ The reference serves one request at a time, moving every hop through gRPC with t
 (xotorch/orchestration/node.py:109-147, 403-443; grpc_peer_handle.py:117-136).  Here the GPUs of one
 host are the ring peers (one process each, `xot --gpus N`) and the data plane is RCCL p2p over xGMI.
 
-  lanes          rank 0 (API, tokenizer, scheduler) splits the running requests into `world` lanes and
+  lanes          rank 0 (API, tokenizer, scheduler) splits the running requests into `world` lanes (times
+                 XOT_RING_LANES_PER_RANK) and
                  cycles through them: a lane's next step starts as soon as its previous step's tokens are
                  back, while the other lanes' steps are on the other GPUs -- the ring stays full, as in
                  bench.py, instead of filling and draining once per round.
@@ -114,8 +115,12 @@ class RingServer:
   def __init__(self, runner, rank: int, world: int, transport, ctl_group=None, eos_ids: Sequence[int] = (),
                top_k: int = 35, seed: int = 1234, max_batch: Optional[int] = None, step_tokens: Optional[int] = None,
                monitor: Optional[HealthMonitor] = None, make_runner: Optional[Callable] = None,
-               pool_pages: Optional[int] = None, ops_cap: int = OPS_CAP, prefix_cache: Optional[bool] = None):
+               pool_pages: Optional[int] = None, ops_cap: int = OPS_CAP, prefix_cache: Optional[bool] = None,
+               lanes_per_rank: Optional[int] = None):
     self.r, self.rank, self.world, self.t = runner, rank, world, transport
+    # lanes per ring rank (XOT_RING_LANES_PER_RANK): with more than one, rank 0 has another lane's step queued
+    # while it turns one lane's ids around on the host (collect, plan, header), at smaller steps per lane
+    self.lanes_per_rank = max(1, lanes_per_rank or int(os.environ.get("XOT_RING_LANES_PER_RANK", "1")))
     self.ops_cap = max(1, ops_cap)  # KV operations per header
     self.use_prefix_cache = PREFIX_CACHE if prefix_cache is None else prefix_cache
     self.ctl = ctl_group  # gloo group of the control plane (headers); None with world 1
@@ -149,7 +154,7 @@ class RingServer:
     self.D = runner.config.hidden_size
     self.dev = runner.device
     self.seed_off = torch.tensor([self.seed, 0], dtype=torch.int64, device=runner.device)
-    self.lanes = max(1, world)
+    self.lanes = max(1, world) * self.lanes_per_rank
     self._inflight: List[Optional[list]] = [None] * self.lanes  # per lane: the step's (req, n) awaiting ids
     # rank 0 plans with the smallest pool of the ring (exact for every rank: same appends everywhere)
     self.pool_pages = min(pool_pages or runner.bm.num_blocks, runner.bm.num_blocks)
