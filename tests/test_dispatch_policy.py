@@ -48,3 +48,12 @@ def test_tuner_tie_break_prefers_ping_pong(monkeypatch):
   assert L._tie_break({("stream", 2, 4): 0.1, ("big", 1256, 1): 0.101}) == ("stream", 2, 4)
   monkeypatch.setattr(L, "TIE", 0.0)
   assert L._tie_break({("big", 224, 1): 0.4, ("big", 1256, 1): 0.401}) == ("big", 224, 1)
+
+
+def test_tuner_offers_two_phase_ping_pong(monkeypatch):
+  """The two-phase ping-pong tile (2256) is a gemm_big candidate and the first choice inside the tie window."""
+  codes = {c[1] for c in L.GemmPolicy._big_cands(512, 57344, 8192)}
+  assert {256, 1256, 2256, 128} <= codes
+  assert L._tie_break({("big", 1256, 1): 0.40, ("big", 2256, 1): 0.41}) == ("big", 2256, 1)
+  monkeypatch.setattr(L, "PP2", False)
+  assert 2256 not in {c[1] for c in L.GemmPolicy._big_cands(512, 57344, 8192)}

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Headline (BASELINE config 3, Llama-3-70B, 512 sequences, one GPU) and its kernel breakdown.
-#   bash tools/gpu/headline.sh [bench|ab|sk|tune|prof|sweep]...      (default: bench prof)
+#   bash tools/gpu/headline.sh [bench|ab|sk|tune|pp2|prof|sweep]...      (default: bench prof)
 source "$(dirname "$0")/common.sh"
 for what in ${@:-bench prof}; do
   case $what in
@@ -19,6 +19,10 @@ for what in ${@:-bench prof}; do
            XOT_GEMM_TABLE=$O/headline/tbl_sustained.json step headline/tune_sustained 600 python -u bench.py --steps 20 --warmup 5
            XOT_TUNE_SUSTAINED_M=0 XOT_GEMM_TABLE=$O/headline/tbl_isolated.json step headline/tune_isolated 400 python -u bench.py --steps 20 --warmup 5
            XOT_GEMM_TABLE=$O/headline/tbl_sustained.json step headline/tune_sustained2 400 python -u bench.py --steps 20 --warmup 5 ;;
+    pp2)   # two-phase ping-pong tile offered (default) vs not, same box
+           XOT_GEMM_TABLE=$O/headline/tbl_pp2.json step headline/pp2_on 400 python -u bench.py --steps 20 --warmup 5
+           XOT_GEMM_PP2=0 XOT_GEMM_TABLE=$O/headline/tbl_nopp2.json step headline/pp2_off 400 python -u bench.py --steps 20 --warmup 5
+           XOT_GEMM_TABLE=$O/headline/tbl_pp2.json step headline/pp2_on2 400 python -u bench.py --steps 20 --warmup 5 ;;
     sweep) for b in 448 512 576; do step headline/b$b 400 python -u bench.py --batch-per-gpu $b --steps 10 --warmup 3; done ;;
   esac
 done

@@ -59,7 +59,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
   static_assert(WM * WN == 8, "8 waves");
   static_assert(BK == 32 || BK == 64, "k stage of 32 or 64");
   static_assert(BM % (16 * WM) == 0 && BM >= 128 && BM <= 512, "row tile of 128 .. 512 rows");
-  static_assert(PP == 0 || PP == 1, "schedules: base (0), ping-pong (1)");
+  static_assert(PP == 0 || PP == 1 || PP == 2, "schedules: base (0), ping-pong in 4 phases (1) or 2 phases (2)");
   static_assert(MOE == 0 || MOE == 4 || (!SPLIT && EPI != EPI_RESID), "grouped GEMM: no slab reduce, no residual");
   static_assert(MOE != 4 || !SPLIT, "K-grouped GEMM: no K split");
   constexpr int MT = BM / (16 * WM), NT = BN / (16 * WN);
@@ -249,7 +249,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
     }
   };
 
-  if constexpr (PP == 1) {
+  if constexpr (PP == 1 || PP == 2) {
     static_assert(BM == 256 && BN == 256 && WM == 2 && WN == 4 && BK == 64 && NBUF == 2, "PP geometry");
     auto bar = []() {  // raw barrier (no vmcnt / lgkmcnt drain); the asm statements are compiler fences
       asm volatile("" ::: "memory");
@@ -296,6 +296,32 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
       // wave-uniform branch (an EXEC-masked s_barrier would still execute)
       const int half = __builtin_amdgcn_readfirstlane(wm);
       if (half == 1) bar();  // row-half 1 runs one barrier behind
+      if constexpr (PP == 2) {
+      for (int t = 0; t < T; ++t) {
+        // two phases of 32 MFMAs: {A half 0, both B halves} -> quads (0,0), (0,1); {A half 1, refill with stage
+        // t+2, retire stage t+1} -> quads (1,1), (1,0).  Four barriers per stage instead of eight.
+        const int buf = t & 1;
+        read_a(buf, 0);
+        read_b(buf, 0);
+        read_b(buf, 1);
+        bar();
+        quad(0, 0);
+        quad(0, 1);
+        bar();
+        read_a(buf, 1);  // last read of this stage by this wave
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // ... landed before the refill's LDS writes
+        if (t + 2 < T) {
+          issue(t_beg + t + 2, buf);
+          wait_vm<NI>();
+        } else {
+          wait_vm<0>();
+        }
+        bar();
+        quad(1, 1);
+        quad(1, 0);
+        bar();
+      }
+      } else {
       for (int t = 0; t < T; ++t) {
         const int buf = t & 1;
         read_a(buf, 0);  // phase 0
@@ -322,6 +348,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
         bar();
         quad(1, 0);
         bar();
+      }
       }
       if (half == 0) bar();  // balance the barrier count
     }
@@ -505,7 +532,7 @@ template <int EPI, bool F32>
 static int big_dispatch(const uint16_t* X, int ldx, const uint16_t* W, const uint16_t* bias, const uint16_t* R,
                         int ldr, void* Y, int ldy, float* ws, long ws_elems, int M, int N, int K, int bn, int S,
                         bool reduce, hipStream_t st) {
-  // bn = tile code: BN (256 / 128 / 224), 1256 (256 x 256 on the ping-pong schedule), plus
+  // bn = tile code: BN (256 / 128 / 224), 1256 / 2256 (256 x 256 on the four- / two-phase ping-pong), plus
   // 10000 x BM for row tiles below 256 (160 / 192 / 224: M = 320 / 384 / 448 in two tiles without padding rows)
   const int bm = bn / 10000 ? bn / 10000 : 256, code = bn % 10000;
 #define XOT_BIG(BM_, BN_, WM_, NBUF_, ...)                                                                        \
@@ -514,6 +541,7 @@ static int big_dispatch(const uint16_t* X, int ldx, const uint16_t* W, const uin
   if (bm == 256) {
     if (code == 256) XOT_BIG(256, 256, 2, 2);
     else if (code == 1256) XOT_BIG(256, 256, 2, 2, 1);  // ping-pong schedule of the 256 x 256 tile
+    else if (code == 2256) XOT_BIG(256, 256, 2, 2, 2);  // the same in two phases per stage (4 barriers, not 8)
     else if (code == 128) XOT_BIG(256, 128, 4, 3);
     else if (code == 224) XOT_BIG(256, 224, 4, 2);      // 7 row groups per wave (gate/up N = 57344 -> 256 tiles)
     else return -1;

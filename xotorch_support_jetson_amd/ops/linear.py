@@ -41,6 +41,8 @@ SPLITK_IN_LAUNCH = os.environ.get("XOT_SPLITK_IN_LAUNCH", "0") == "1"
 # under the board power cap a whole decode step ran 0.9 % slower with it (81.64 vs 80.95 ms, same box,
 # profiles/r4/tuner/)
 SK = os.environ.get("XOT_GEMM_SK", "0") == "1"
+# XOT_GEMM_PP2=0: leave the two-phase ping-pong tile (code 2256) out of the candidates
+PP2 = os.environ.get("XOT_GEMM_PP2", "1") == "1"
 # XOT_GEMM_BLAS=1: time hipBLASLt among the candidates for row-major weights (off: the kernel library only)
 BLAS_CAND = os.environ.get("XOT_GEMM_BLAS", "0") == "1"
 # largest M for which the stream GEMM is a candidate (above it only gemm_big is timed)
@@ -69,7 +71,7 @@ def big_row_tile(M: int) -> int:
 
 
 def tile_width(code: int) -> int:
-  """Columns of a gemm_big tile code (BN, 1256 = 256 on the ping-pong schedule, + 10000 x BM)."""
+  """Columns of a gemm_big tile code (BN, 1256 / 2256 = 256 on the four- / two-phase ping-pong, + 10000 x BM)."""
   return code % 1000
 
 
@@ -190,7 +192,7 @@ def _default_table_path():
     from ..helpers import xot_home
     # settings that change the candidate sets are part of the name, so a table never answers for another
     tag = (f"{os.environ.get('XOT_GEMM', 'auto')}-{STREAM_MAX_M}-{BIG_MIN_M}-{SLAB_TBPS:g}{'-sk' if SK else ''}"
-           f"{'-blas' if BLAS_CAND else ''}-t{TIE:g}")
+           f"{'-blas' if BLAS_CAND else ''}-t{TIE:g}{'' if PP2 else '-nopp2'}")
     return str(xot_home() / "gemm" / f"{dev}-{st.st_size:x}-{int(st.st_mtime):x}-{tag}.json")
   except Exception:  # noqa: BLE001 - no table then; tuning still works in memory
     return None
@@ -345,7 +347,8 @@ class GemmPolicy:
     cands = []
     if N % 16:
       return cands
-    codes = [256, 1256, 128]  # 1256: the 256 x 256 tile on the two-group ping-pong schedule
+    # 1256 / 2256: the 256 x 256 tile on the two-group ping-pong schedule in four / two phases per stage
+    codes = [256, 1256, 2256, 128] if PP2 else [256, 1256, 128]
     if N % 224 == 0:  # 7 row groups per wave: whole rounds where 256-wide tiles leave a half round (8B gate/up)
       codes.append(224)
     bm = big_row_tile(M)
@@ -413,7 +416,7 @@ class GemmPolicy:
       if c[0] != "big":
         continue
       tiles = -(-M // tile_rows(c[1])) * (N // tile_width(c[1])) * c[2]
-      score = abs(tiles - 256) + (0 if c[1] == 1256 else 64)
+      score = abs(tiles - 256) + (0 if c[1] == (2256 if PP2 else 1256) else 64)
       if best is None or score < best[0]:
         best = (score, c)
     return best[1]
@@ -421,11 +424,11 @@ class GemmPolicy:
 
 # Isolated timings of 256-row tile variants at the same K split land within a few percent of each other and the
 # winner changes from run to run, but inside a whole decode step (back to back, at the power cap) the ping-pong
-# 256 x 256 tile is the measured winner (a 256 x 224 gate/up or plain-256 qkv pick cost ~2 % of the headline step,
+# 256 x 256 tile (two-phase first) is the measured winner (a 256 x 224 gate/up or plain-256 qkv pick cost ~2 % of the headline step,
 # profiles/r4/tuner/slab_penalty/, tie/: a plain-256 down pick 82.49 vs 81.91 / 81.83 ms): within TIE of the
 # fastest, prefer it.
 TIE = float(os.environ.get("XOT_GEMM_TIE", "0.05"))
-_BIG_PREF = {1256: 0, 256: 1, 224: 2, 128: 3}
+_BIG_PREF = {2256: 0, 1256: 1, 256: 2, 224: 3, 128: 4}
 
 
 def _tie_break(times: Dict) -> Tuple:
