@@ -588,14 +588,14 @@ int launch_gemm_kgroup(const uint16_t* X, int ldx, const uint16_t* W, uint16_t* 
   constexpr int SMEM = 2 * (256 + 256) * 64 * 2;
   const dim3 grid(((M + 255) / 256) * ((N + 255) / 256), E);
   if (resid) {
-    auto kern = gemm_big_kernel<256, 256, 2, 4, 64, 2, EPI_RESID, false, false, 4, 0, 3, 1>;
+    auto kern = gemm_big_kernel<256, 256, 2, 4, 64, 2, EPI_RESID, false, false, 4, 0, 3, 2>;
     static bool attr = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM) ==
                        hipSuccess;
     (void)attr;
     kern<<<grid, 512, SMEM, st>>>(X, ldx, W, nullptr, Y, ldy, Y, ldy, nullptr, M, N, K, 1, koff, nullptr, 0L,
                                   big_group_m());
   } else {
-    auto kern = gemm_big_kernel<256, 256, 2, 4, 64, 2, EPI_NONE, false, false, 4, 0, 3, 1>;
+    auto kern = gemm_big_kernel<256, 256, 2, 4, 64, 2, EPI_NONE, false, false, 4, 0, 3, 2>;
     static bool attr = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM) ==
                        hipSuccess;
     (void)attr;
