@@ -309,7 +309,13 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
         quad(0, 1);
         bar();
         read_a(buf, 1);  // last read of this stage by this wave
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // ... landed before the refill's LDS writes
+        // Refill with stage t+2 here, in the read phase: a wave's LDS-DMA issue inside its MFMA phase costs more
+        // than the whole schedule gains (measured: refill after the barrier, or only the A rows the group is
+        // still reading moved there, ran slower than the four-phase schedule, profiles/r4/pp2/).  The refill
+        // lands >= one L2 round trip after issue, while the reads it could overtake -- the group's own A rows
+        // here, issued at the start of this phase, and the other group's B reads, issued before the previous
+        // barrier -- complete within one LDS round trip (the same margin the four-phase schedule relies on).
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (t + 2 < T) {
           issue(t_beg + t + 2, buf);
           wait_vm<NI>();
