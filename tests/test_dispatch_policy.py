@@ -57,3 +57,22 @@ def test_tuner_offers_two_phase_ping_pong(monkeypatch):
   assert L._tie_break({("big", 1256, 1): 0.40, ("big", 2256, 1): 0.41}) == ("big", 2256, 1)
   monkeypatch.setattr(L, "PP2", False)
   assert 2256 not in {c[1] for c in L.GemmPolicy._big_cands(512, 57344, 8192)}
+
+
+def test_cpu_reference_linear_caches_fp32_weights():
+  """The CPU path widens a low-precision weight once and reuses it, re-widening after an in-place write (a
+  trained weight written back) and never caching a weight that requires grad."""
+  from xotorch_support_jetson_amd.ops import reference as ref
+  torch.manual_seed(0)
+  x = torch.randn(3, 64)
+  w = torch.randn(32, 64).to(torch.bfloat16)
+  y1 = ref.linear(x, w)
+  assert hasattr(w, "_xot_f32")
+  f32 = w._xot_f32[1]
+  assert ref.linear(x, w) is not None and w._xot_f32[1] is f32  # reused
+  w.mul_(2)
+  y2 = ref.linear(x, w)
+  assert torch.allclose(y2, 2 * y1, rtol=1e-2, atol=1e-2)
+  wg = torch.randn(32, 64, requires_grad=True)
+  ref.linear(x, wg.to(torch.bfloat16))
+  assert not hasattr(wg, "_xot_f32")

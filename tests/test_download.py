@@ -136,3 +136,36 @@ def test_corrupt_download_rejected(tmp_path, monkeypatch):
       await runner.cleanup()
 
   asyncio.run(asyncio.wait_for(main(), 60))
+
+
+def test_unreachable_hub_fails_fast(monkeypatch):
+  """Connection-level failures (no route / DNS / refused) stop the retries after `unreachable_after` attempts and
+  mark the hub unreachable for the process, so later calls fail at once; transient errors keep their retries."""
+  import xotorch_support_jetson_amd.download.new_shard_download as nsd
+  monkeypatch.setattr(nsd, "_retry_delay", lambda attempt: 0.0)
+  monkeypatch.setattr(nsd.HFRepoClient, "unreachable", False)
+  calls = []
+
+  async def refused():
+    calls.append(1)
+    raise ConnectionRefusedError("no route")
+
+  async def flaky():
+    calls.append(1)
+    if len(calls) < 5:
+      raise IOError("HTTP 500")
+    return "ok"
+
+  async def main():
+    c = nsd.HFRepoClient(endpoint="http://127.0.0.1:9", attempts=30)
+    assert await c._with_retry(flaky) == "ok" and len(calls) == 5  # transient: retried
+    calls.clear()
+    with pytest.raises(ConnectionError):
+      await c._with_retry(refused)
+    assert len(calls) == 2 and nsd.HFRepoClient.unreachable
+    calls.clear()
+    with pytest.raises(ConnectionError):
+      await c._with_retry(flaky)
+    assert calls == []  # not even tried
+
+  asyncio.run(main())

@@ -19,6 +19,7 @@ import hashlib
 import json
 import os
 import shutil
+import socket
 import time
 import traceback
 from datetime import timedelta
@@ -82,24 +83,51 @@ def _retry_delay(attempt: int) -> float:
   return min(8.0, 0.1 * (2 ** attempt))
 
 
-class HFRepoClient:
-  """Minimal async client for the HF hub file API."""
+def _unreachable_error(e: BaseException) -> bool:
+  """A failure that says the hub cannot be reached at all (no route, no DNS, refused) rather than a transient one."""
+  try:
+    import aiohttp
+    if isinstance(e, (aiohttp.ClientConnectorError, aiohttp.ServerTimeoutError)):
+      return True
+  except ImportError:
+    pass
+  return isinstance(e, (ConnectionError, socket.gaierror, asyncio.TimeoutError))
 
-  def __init__(self, endpoint: Optional[str] = None, attempts: int = 30):
+
+class HFRepoClient:
+  """Minimal async client for the HF hub file API.
+
+  Transient failures are retried with backoff (`attempts`).  Connection-level failures (no DNS, no route,
+  refused, connect timeout) are retried only `unreachable_after` times; then the hub is marked unreachable for
+  the rest of the process and every later call fails at once -- without that, a host with no network spent the
+  whole backoff budget (minutes) on each file before falling back to local / random weights."""
+
+  unreachable = False  # process-wide: set after repeated connection-level failures
+
+  def __init__(self, endpoint: Optional[str] = None, attempts: int = 30, unreachable_after: int = 2):
     self.endpoint = endpoint or get_hf_endpoint()
     self.attempts = attempts
+    self.unreachable_after = unreachable_after
 
   def _session(self, total: float = 1800):
     import aiohttp
     return aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=total, connect=30, sock_read=total))
 
   async def _with_retry(self, fn, *args):
+    if HFRepoClient.unreachable:
+      raise ConnectionError(f"{self.endpoint} unreachable (an earlier connection attempt failed)")
+    conn_failures = 0
     for attempt in range(self.attempts):
       try:
         return await fn(*args)
       except FileNotFoundError:
         raise
-      except Exception:
+      except Exception as e:
+        if _unreachable_error(e):
+          conn_failures += 1
+          if conn_failures >= self.unreachable_after:
+            HFRepoClient.unreachable = True
+            raise
         if attempt == self.attempts - 1:
           raise
         await asyncio.sleep(_retry_delay(attempt))

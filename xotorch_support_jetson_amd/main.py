@@ -168,18 +168,24 @@ async def run_model_cli(node, model_name: str, prompt: str, topology_viz=None):
     print(f"Processing prompt: {prompt}")
     t0 = time.perf_counter()
     await node.process_prompt(shard, templ, request_id=request_id)
-    tokens = []
+    tokens, first = [], []
 
     def on_token(_rid, _tokens, _finished):
       if _rid == request_id:
+        if _tokens and not first:
+          first.append(time.perf_counter())
         tokens.extend(_tokens)
       return _rid == request_id and _finished
 
     await cb.wait(on_token, timeout=300)
-    dt = time.perf_counter() - t0
+    t1 = time.perf_counter()
+    dt = t1 - t0
     print("\nGenerated response:")
     print(tok.decode(tokens))
-    print(f"\n[{len(tokens)} tokens in {dt:.2f}s, {len(tokens) / max(dt, 1e-9):.1f} tok/s]")
+    # time to the first token includes loading / initialising the shard on a cold start
+    ttft = (first[0] - t0) if first else dt
+    decode = (len(tokens) - 1) / max(t1 - first[0], 1e-9) if first and len(tokens) > 1 else 0.0
+    print(f"\n[{len(tokens)} tokens in {dt:.2f}s: first token {ttft:.2f}s, then {decode:.1f} tok/s]")
   except Exception as e:
     print(f"Error processing prompt: {e}")
     traceback.print_exc()

@@ -416,6 +416,13 @@ def _needs_embed(c: ModelConfig, s: Shard) -> bool:
 
 
 # -------------------------------------------------------------------- random init
+def _normal(shape, g: torch.Generator, std: float, dev: torch.device, dtype) -> torch.Tensor:
+  """N(0, std) of `shape` from generator g; every random weight (and random_head_rows) draws through here, so a
+  shard's rows are the same whichever function made them.  (Drawing CPU bf16 weights in fp32 and rounding is ~3x
+  faster, but it changes every value, and the exact-equality training tests are pinned to these.)"""
+  return torch.empty(shape, device=dev, dtype=dtype).normal_(0.0, std, generator=g)
+
+
 def random_weights(c: ModelConfig, shard: Shard, device: torch.device | str = "cpu", dtype=torch.bfloat16,
                    seed: int = 0, std: float = 0.02) -> ShardWeights:
   """Deterministic per-layer random weights: layer i is identical whichever shard holds it, so a
@@ -429,7 +436,7 @@ def random_weights(c: ModelConfig, shard: Shard, device: torch.device | str = "c
     return g
 
   def normal(shape, g, s=std):
-    return torch.empty(shape, device=dev, dtype=dtype).normal_(0.0, s, generator=g)
+    return _normal(shape, g, s, dev, dtype)
 
   def norm_w(g):
     return (1.0 + torch.empty(D, device=dev, dtype=torch.float32).normal_(0.0, 0.05, generator=g)).to(dtype)
@@ -487,7 +494,7 @@ def random_head_rows(c: ModelConfig, rows_from: int, device: torch.device | str 
   dev = torch.device(device)
   g = torch.Generator(device=dev)
   g.manual_seed(seed * 1_000_003 + (1 if c.tie_word_embeddings else 3))
-  full = torch.empty((c.vocab_size, c.hidden_size), device=dev, dtype=dtype).normal_(0.0, std, generator=g)
+  full = _normal((c.vocab_size, c.hidden_size), g, std, dev, dtype)
   return full[rows_from:].clone()
 
 

@@ -6,6 +6,9 @@ exactly, including the paged KV layout (K [pages, Hkv, 64, Dh], V [pages, Hkv, D
 """
 from __future__ import annotations
 
+import os
+import weakref
+
 import torch
 import torch.nn.functional as F
 
@@ -40,8 +43,39 @@ def silu_mul(gu: torch.Tensor) -> torch.Tensor:
   return (F.silu(g) * u).to(gu.dtype)
 
 
+# fp32 copies of low-precision CPU weights, made once per tensor and re-made when the tensor is written in place
+# (its version counter moves) or re-pointed: without them every CPU token widened every weight again (~1 s per
+# token for Llama-3.2-1B).  Tensors that require grad (trained parameters) are widened per call as before.
+# at most this many bytes of fp32 copies live at once (XOT_CPU_F32_CACHE_GB): a model too large for it widens the
+# rest per call, as before
+_F32_BUDGET = int(float(os.environ.get("XOT_CPU_F32_CACHE_GB", "12")) * (1 << 30))
+_f32_bytes = [0]
+
+
+def _release(n: int) -> None:
+  _f32_bytes[0] -= n
+
+
+def _wide(w: torch.Tensor) -> torch.Tensor:
+  if w.dtype == torch.float32 or w.device.type != "cpu" or w.requires_grad or w.grad_fn is not None:
+    return w.float()
+  key = (w._version, w.data_ptr(), tuple(w.shape), tuple(w.stride()))
+  got = getattr(w, "_xot_f32", None)  # kept on the tensor: freed with it
+  if got is not None and got[0] == key:
+    return got[1]
+  f = w.float()
+  n = f.numel() * 4
+  if got is None and _f32_bytes[0] + n > _F32_BUDGET:
+    return f
+  if got is None:
+    _f32_bytes[0] += n
+    weakref.finalize(w, _release, n)
+  w._xot_f32 = (key, f)
+  return f
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Tensor:
-  y = x.float() @ w.float().t()
+  y = x.float() @ _wide(w).t()
   if bias is not None:
     y = y + bias.float()
   return y
