@@ -621,13 +621,13 @@ void launch_splitk_silu(const float* ws, int S, int M, int N, uint16_t* y, hipSt
 }
 
 // ------------------------------------------------------------------------------------ grouped (MoE)
-template <int BM, int EPI, bool F32, int MOE, int BK = 64, int NBUF = 2>
+template <int BM, int EPI, bool F32, int MOE, int BK = 64, int NBUF = 2, int PP = 0>
 static void big_moe_launch(const uint16_t* X, int ldx, const uint16_t* W, void* Y, int ldy, const int* off,
                            const int* gather, int E, int max_rows, int N, int K, int S, long ysplit, hipStream_t st) {
   constexpr int BN = 256, WM = 2, WN = 4;
   constexpr int SMEM = NBUF * (BM + BN) * BK * 2;
   static_assert(SMEM <= 160 * 1024, "LDS");
-  auto kern = gemm_big_kernel<BM, BN, WM, WN, BK, NBUF, EPI, F32, false, MOE>;
+  auto kern = gemm_big_kernel<BM, BN, WM, WN, BK, NBUF, EPI, F32, false, MOE, 0, 3, PP>;
   static bool attr = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM) ==
                      hipSuccess;
   (void)attr;
@@ -638,7 +638,7 @@ static void big_moe_launch(const uint16_t* X, int ldx, const uint16_t* W, void* 
 
 // bm = row tile (128 / 192 / 256) + 1000 x pipeline variant: 0 = two 64-deep LDS stages (one in flight under
 // the MFMAs); 1 = more expert-weight bytes in flight for the HBM-bound groups (BM 128: three 64-deep stages;
-// BM 192 / 256: four 32-deep stages, three in flight)
+// BM 192 / 256: four 32-deep stages, three in flight); 2 (BM 256 only) = the two-phase ping-pong schedule
 template <int EPI, bool F32>
 static void big_moe_bm(const uint16_t* X, int ldx, const uint16_t* W, void* Y, int ldy, const int* off,
                        const int* gather, int E, int max_rows, int N, int K, int S, long ysplit, int bm,
@@ -656,6 +656,7 @@ static void big_moe_bm(const uint16_t* X, int ldx, const uint16_t* W, void* Y, i
     case 1128: XOT_MOE(128, 64, 3); break;
     case 1192: XOT_MOE(192, 32, 4); break;
     case 1256: XOT_MOE(256, 32, 4); break;
+    case 2256: XOT_MOE(256, 64, 2, 2); break;  // 256-row tiles on the two-phase ping-pong schedule
     default: XOT_MOE(256); break;
   }
 #undef XOT_MOE
@@ -665,7 +666,8 @@ int launch_gemm_moe_big(const uint16_t* X, int ldx, const uint16_t* W, void* Y, 
                         const int* off, const int* gather, int E, int max_rows, int N, int K, int S, long ysplit,
                         int bm, hipStream_t s) {
   if (max_rows <= 0) return 0;
-  if ((bm % 1000 != 128 && bm % 1000 != 192 && bm % 1000 != 256) || bm > 1256 || N % 256 != 0 || K % 128 != 0 || S < 1 ||
+  if ((bm % 1000 != 128 && bm % 1000 != 192 && bm % 1000 != 256) || (bm > 1256 && bm != 2256) || N % 256 != 0 ||
+      K % 128 != 0 || S < 1 ||
       S > K / 64)
     return -1;
   if (epi != EPI_NONE && epi != EPI_SILU) return -1;

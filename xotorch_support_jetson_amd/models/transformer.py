@@ -38,6 +38,7 @@ MOE_BIG_MIN_ROWS = float(os.environ.get("XOT_MOE_BIG_MIN_ROWS", "24"))
 # K splits of the grouped gate/up GEMM for decode-sized batches (1: fused SiLU epilogue, no slabs)
 MOE_GU_SPLITS = int(os.environ.get("XOT_MOE_GU_SPLITS", "4"))
 MOE_BM = int(os.environ.get("XOT_MOE_BM", "0"))  # force the grouped gemm_big tile code (tests, A/B)
+MOE_PP2 = os.environ.get("XOT_MOE_PP2", "1") == "1"  # 256-row expert tiles on the two-phase ping-pong schedule
 PAGE = 64
 # XOT_SPLIT_DECODE=N: decode batches of at least N sequences (dense models) run as two half-batches on two
 # streams, so one half's HBM-bound attention overlaps the other half's MFMA-bound GEMMs (0: off)
@@ -290,6 +291,8 @@ class ShardModel:
     # tiles (128 or 256 rows) once the groups are compute-bound
     rows = T * k / E
     bm, bm_dn, S_dn = (0, 0, 0) if not shuffled or rows < MOE_BIG_MIN_ROWS else moe_tiles(rows, E)
+    if MOE_PP2:  # 256-row expert tiles on the two-phase ping-pong schedule (csrc/gemm_big.hip tile code 2256)
+      bm, bm_dn = (2256 if b == 256 else b for b in (bm, bm_dn))
     if MOE_BM and bm:
       bm = bm_dn = MOE_BM
     act = torch.empty(T * k, F, dtype=torch.bfloat16, device=dev)
