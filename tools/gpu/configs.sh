@@ -1,6 +1,6 @@
 #!/bin/bash
 # The other BASELINE.json configs on one GPU: 8B and 70B batch-1 / batch-512 decode, Mixtral, model families,
-# weight-only FP8, long context.   bash tools/gpu/configs.sh [dense|moe|families|fp8|long|moepp2|b1prof]...  (default: dense moe)
+# weight-only FP8, long context.   bash tools/gpu/configs.sh [dense|moe|families|fp8|long|moepp2|moepp2mx|b1prof]...  (default: dense moe)
 source "$(dirname "$0")/common.sh"
 for what in ${@:-dense moe}; do
   case $what in
@@ -20,6 +20,8 @@ for what in ${@:-dense moe}; do
     moepp2) # 256-row expert tiles: two-phase ping-pong (default) vs base schedule
            for v in 1 0; do XOT_MOE_PP2=$v step cfg/dsl_b256_moepp2_$v 600 python bench.py --model deepseek-coder-v2-lite --batch-per-gpu 256 --steps 16 --warmup 3
              XOT_MOE_PP2=$v step cfg/dsv3_8l_b256_moepp2_$v 600 python bench.py --model deepseek-v3 --layers 8 --batch-per-gpu 256 --steps 8 --warmup 3; done ;;
+    moepp2mx) # 192-row expert tiles (Mixtral): two-phase ping-pong (default) vs base schedule
+           for v in 1 0 1; do XOT_MOE_PP2=$v step cfg/mixtral_b512_moepp2_$v 600 python bench.py --model mixtral-8x7b --batch-per-gpu 512 --steps 8 --warmup 3; done ;;
     b1prof) ;;
     long)  for t in 8192 32768 65536; do step long/l8b_$t 600 python -u tools/bench_long_prefill.py --model llama-3.1-8b --tokens $t; done
            step long/l70b_32768 600 python -u tools/bench_long_prefill.py --model llama-3.1-70b --tokens 32768 ;;

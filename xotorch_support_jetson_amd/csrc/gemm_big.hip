@@ -250,19 +250,20 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
   };
 
   if constexpr (PP == 1 || PP == 2) {
-    static_assert(BM == 256 && BN == 256 && WM == 2 && WN == 4 && BK == 64 && NBUF == 2, "PP geometry");
+    static_assert((BM == 256 || BM == 192) && BN == 256 && WM == 2 && WN == 4 && BK == 64 && NBUF == 2, "PP geometry");
+    constexpr int MQ = MT / 2;  // row tiles per A half of a wave (4 at BM 256, 3 at BM 192)
     auto bar = []() {  // raw barrier (no vmcnt / lgkmcnt drain); the asm statements are compiler fences
       asm volatile("" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
     };
-    s16x8 af[4][2], bq[2][2][2];
+    s16x8 af[MQ][2], bq[2][2][2];
     auto read_a = [&](int buf, int qm) {
       const uint16_t* As = smem + buf * STAGE;
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < MQ; ++i)
 #pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) af[i][s2] = ld16(As + aoff[4 * qm + i][s2]);
+        for (int s2 = 0; s2 < 2; ++s2) af[i][s2] = ld16(As + aoff[MQ * qm + i][s2]);
     };
     auto read_b = [&](int buf, int qn) {
       const uint16_t* Bs = smem + buf * STAGE + A_ELEMS;
@@ -277,10 +278,10 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < MQ; ++i)
 #pragma unroll
           for (int j = 0; j < 2; ++j)
-            acc[4 * qm + i][2 * qn + j] = mfma16(af[i][s2], bq[qn][j][s2], acc[4 * qm + i][2 * qn + j]);
+            acc[MQ * qm + i][2 * qn + j] = mfma16(af[i][s2], bq[qn][j][s2], acc[MQ * qm + i][2 * qn + j]);
       __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
     };
@@ -638,7 +639,7 @@ static void big_moe_launch(const uint16_t* X, int ldx, const uint16_t* W, void* 
 
 // bm = row tile (128 / 192 / 256) + 1000 x pipeline variant: 0 = two 64-deep LDS stages (one in flight under
 // the MFMAs); 1 = more expert-weight bytes in flight for the HBM-bound groups (BM 128: three 64-deep stages;
-// BM 192 / 256: four 32-deep stages, three in flight); 2 (BM 256 only) = the two-phase ping-pong schedule
+// BM 192 / 256: four 32-deep stages, three in flight); 2 (BM 192 / 256) = the two-phase ping-pong schedule
 template <int EPI, bool F32>
 static void big_moe_bm(const uint16_t* X, int ldx, const uint16_t* W, void* Y, int ldy, const int* off,
                        const int* gather, int E, int max_rows, int N, int K, int S, long ysplit, int bm,
@@ -656,7 +657,8 @@ static void big_moe_bm(const uint16_t* X, int ldx, const uint16_t* W, void* Y, i
     case 1128: XOT_MOE(128, 64, 3); break;
     case 1192: XOT_MOE(192, 32, 4); break;
     case 1256: XOT_MOE(256, 32, 4); break;
-    case 2256: XOT_MOE(256, 64, 2, 2); break;  // 256-row tiles on the two-phase ping-pong schedule
+    case 2256: XOT_MOE(256, 64, 2, 2); break;  // 256- / 192-row tiles on the two-phase ping-pong schedule
+    case 2192: XOT_MOE(192, 64, 2, 2); break;
     default: XOT_MOE(256); break;
   }
 #undef XOT_MOE
@@ -666,7 +668,7 @@ int launch_gemm_moe_big(const uint16_t* X, int ldx, const uint16_t* W, void* Y, 
                         const int* off, const int* gather, int E, int max_rows, int N, int K, int S, long ysplit,
                         int bm, hipStream_t s) {
   if (max_rows <= 0) return 0;
-  if ((bm % 1000 != 128 && bm % 1000 != 192 && bm % 1000 != 256) || (bm > 1256 && bm != 2256) || N % 256 != 0 ||
+  if ((bm % 1000 != 128 && bm % 1000 != 192 && bm % 1000 != 256) || (bm > 1256 && bm != 2256 && bm != 2192) || N % 256 != 0 ||
       K % 128 != 0 || S < 1 ||
       S > K / 64)
     return -1;

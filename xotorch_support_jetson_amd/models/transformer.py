@@ -291,8 +291,8 @@ class ShardModel:
     # tiles (128 or 256 rows) once the groups are compute-bound
     rows = T * k / E
     bm, bm_dn, S_dn = (0, 0, 0) if not shuffled or rows < MOE_BIG_MIN_ROWS else moe_tiles(rows, E)
-    if MOE_PP2:  # 256-row expert tiles on the two-phase ping-pong schedule (csrc/gemm_big.hip tile code 2256)
-      bm, bm_dn = (2256 if b == 256 else b for b in (bm, bm_dn))
+    if MOE_PP2:  # 256- / 192-row expert tiles on the two-phase ping-pong schedule (csrc/gemm_big.hip 2256 / 2192)
+      bm, bm_dn = ({256: 2256, 192: 2192}.get(b, b) for b in (bm, bm_dn))
     if MOE_BM and bm:
       bm = bm_dn = MOE_BM
     act = torch.empty(T * k, F, dtype=torch.bfloat16, device=dev)
