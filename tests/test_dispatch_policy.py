@@ -55,6 +55,13 @@ def test_tuner_offers_two_phase_ping_pong(monkeypatch):
   codes = {c[1] for c in L.GemmPolicy._big_cands(512, 57344, 8192)}
   assert {256, 1256, 2256, 128} <= codes
   assert L._tie_break({("big", 1256, 1): 0.40, ("big", 2256, 1): 0.41}) == ("big", 2256, 1)
+  # across K splits only the two-phase tile gets a (wider) window
+  t = {("big", 128, 2): 0.843, ("big", 2256, 4): 0.927, ("big", 256, 4): 0.90}
+  assert L._tie_break(t) == ("big", 2256, 4)
+  t[("big", 2256, 4)] = 0.95
+  assert L._tie_break(t) == ("big", 128, 2)
+  monkeypatch.setattr(L, "TIE_X", 0.0)
+  assert L._tie_break({("big", 128, 2): 0.843, ("big", 2256, 4): 0.85}) == ("big", 128, 2)
   monkeypatch.setattr(L, "PP2", False)
   assert 2256 not in {c[1] for c in L.GemmPolicy._big_cands(512, 57344, 8192)}
 

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Headline (BASELINE config 3, Llama-3-70B, 512 sequences, one GPU) and its kernel breakdown.
-#   bash tools/gpu/headline.sh [bench|ab|sk|tune|pp2|prof|sweep]...      (default: bench prof)
+#   bash tools/gpu/headline.sh [bench|ab|sk|tune|pp2|oproj|tunelog|tiex|prof|sweep]...      (default: bench prof)
 source "$(dirname "$0")/common.sh"
 for what in ${@:-bench prof}; do
   case $what in
@@ -23,6 +23,21 @@ for what in ${@:-bench prof}; do
            XOT_GEMM_TABLE=$O/headline/tbl_pp2.json step headline/pp2_on 400 python -u bench.py --steps 20 --warmup 5
            XOT_GEMM_PP2=0 XOT_GEMM_TABLE=$O/headline/tbl_nopp2.json step headline/pp2_off 400 python -u bench.py --steps 20 --warmup 5
            XOT_GEMM_TABLE=$O/headline/tbl_pp2.json step headline/pp2_on2 400 python -u bench.py --steps 20 --warmup 5 ;;
+    oproj) # o-proj (N = K = 8192) kernel choice in the step: tuned pick vs the two-phase 256 x 256 tile at S 4 / 2
+           T=$O/headline/tbl_o.json
+           XOT_GEMM_TABLE=$T step headline/o_tuned 400 python -u bench.py --steps 20 --warmup 5
+           python tools/gemm_table.py show "$T" > "$O/headline/tbl_o_tuned.txt"
+           for c in 4 2; do cp "$T" "$O/headline/tbl_o$c.json"
+             python tools/gemm_table.py set "$O/headline/tbl_o$c.json" 8192 8192 "[\"big\", 2256, $c]" 512
+             XOT_GEMM_TABLE=$O/headline/tbl_o$c.json step headline/o_2256s$c 400 python -u bench.py --steps 20 --warmup 5; done
+           XOT_GEMM_TABLE=$T step headline/o_tuned2 400 python -u bench.py --steps 20 --warmup 5 ;;
+    tunelog) # the tuner's isolated timings of every shuffled-weight candidate (70B and 8B at 512 sequences)
+           XOT_GEMM_TUNE_LOG=1 XOT_GEMM_TABLE=$O/headline/tbl_log70.json step headline/tunelog_70b 400 python -u bench.py --steps 5 --warmup 2
+           XOT_GEMM_TUNE_LOG=1 XOT_GEMM_TABLE=$O/headline/tbl_log8.json step headline/tunelog_8b 400 python -u bench.py --model llama-3-8b --batch-per-gpu 512 --steps 5 --warmup 2 ;;
+    tiex)  # the cross-split tie window for the two-phase tile (XOT_GEMM_TIE_X, default 0.10) vs none, 70B and 8B
+           for x in 0.10 0 0.10; do
+             XOT_GEMM_TUNE_LOG=1 XOT_GEMM_TIE_X=$x XOT_GEMM_TABLE=$O/headline/tbl_x$x.json step headline/tiex_70b_$x 400 python -u bench.py --steps 20 --warmup 5
+             XOT_GEMM_TUNE_LOG=1 XOT_GEMM_TIE_X=$x XOT_GEMM_TABLE=$O/headline/tbl_x${x}_8b.json step headline/tiex_8b_$x 400 python -u bench.py --model llama-3-8b --batch-per-gpu 512 --steps 20 --warmup 5; done ;;
     sweep) for b in 448 512 576; do step headline/b$b 400 python -u bench.py --batch-per-gpu $b --steps 10 --warmup 3; done ;;
   esac
 done

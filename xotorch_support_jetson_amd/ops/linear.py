@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import json
 import os
+import sys
 from typing import Dict, Tuple
 
 import torch
@@ -192,7 +193,7 @@ def _default_table_path():
     from ..helpers import xot_home
     # settings that change the candidate sets are part of the name, so a table never answers for another
     tag = (f"{os.environ.get('XOT_GEMM', 'auto')}-{STREAM_MAX_M}-{BIG_MIN_M}-{SLAB_TBPS:g}{'-sk' if SK else ''}"
-           f"{'-blas' if BLAS_CAND else ''}-t{TIE:g}{'' if PP2 else '-nopp2'}")
+           f"{'-blas' if BLAS_CAND else ''}-t{TIE:g}-x{TIE_X:g}{'' if PP2 else '-nopp2'}")
     return str(xot_home() / "gemm" / f"{dev}-{st.st_size:x}-{int(st.st_mtime):x}-{tag}.json")
   except Exception:  # noqa: BLE001 - no table then; tuning still works in memory
     return None
@@ -394,6 +395,9 @@ class GemmPolicy:
       except RuntimeError:
         pass
     got = _tie_break(times) if times else cands[0]
+    if TUNE_LOG:
+      print(f"[gemm tune] {key} -> {got}: " + ", ".join(f"{c}={t * 1e3:.1f}us" for c, t in sorted(times.items(), key=lambda i: i[1])),
+            file=sys.stderr, flush=True)
     self._store(key, got)
     return got
 
@@ -428,6 +432,12 @@ class GemmPolicy:
 # profiles/r4/tuner/slab_penalty/, tie/: a plain-256 down pick 82.49 vs 81.91 / 81.83 ms): within TIE of the
 # fastest, prefer it.
 TIE = float(os.environ.get("XOT_GEMM_TIE", "0.05"))
+# ... and across K splits, the two-phase tile within TIE_X of the fastest: the isolated timing runs below the power
+# cap, where a sparser MFMA schedule gains most from the higher clock.  Llama-3-70B o-proj at 512 rows: timed
+# 256 x 128 S 2 84.3 us vs two-phase S 4 92.7 us, but in the step the two-phase pick is 0.5 ms faster (78.30 vs
+# 78.82 / 78.86 ms, profiles/r4/tuner/oproj/)
+TIE_X = float(os.environ.get("XOT_GEMM_TIE_X", "0.10"))
+TUNE_LOG = os.environ.get("XOT_GEMM_TUNE_LOG", "0") == "1"  # print every shuffled-weight tuning's timings
 _BIG_PREF = {2256: 0, 1256: 1, 256: 2, 224: 3, 128: 4}
 
 
@@ -436,7 +446,8 @@ def _tie_break(times: Dict) -> Tuple:
   if best[0] != "big" or best[1] not in _BIG_PREF or TIE <= 0:
     return best
   close = [c for c, t in times.items()
-           if c[0] == "big" and c[2] == best[2] and c[1] in _BIG_PREF and t <= times[best] * (1 + TIE)]
+           if c[0] == "big" and c[1] in _BIG_PREF and ((c[2] == best[2] and t <= times[best] * (1 + TIE))
+                                                       or (c[1] == 2256 and t <= times[best] * (1 + TIE_X)))]
   return min(close, key=lambda c: (_BIG_PREF[c[1]], times[c]))
 
 
