@@ -1,6 +1,6 @@
 #!/bin/bash
 # The other BASELINE.json configs on one GPU: 8B and 70B batch-1 / batch-512 decode, Mixtral, model families,
-# weight-only FP8, long context.   bash tools/gpu/configs.sh [dense|moe|families|fp8|long|moepp2|moepp2mx|b1prof]...  (default: dense moe)
+# weight-only FP8, long context.   bash tools/gpu/configs.sh [dense|moe|families|fp8|long|moepp2|moepp2mx|b1prof|mxprof]...  (default: dense moe)
 source "$(dirname "$0")/common.sh"
 for what in ${@:-dense moe}; do
   case $what in
@@ -22,7 +22,7 @@ for what in ${@:-dense moe}; do
              XOT_MOE_PP2=$v step cfg/dsv3_8l_b256_moepp2_$v 600 python bench.py --model deepseek-v3 --layers 8 --batch-per-gpu 256 --steps 8 --warmup 3; done ;;
     moepp2mx) # 192-row expert tiles (Mixtral): two-phase ping-pong (default) vs base schedule
            for v in 1 0 1; do XOT_MOE_PP2=$v step cfg/mixtral_b512_moepp2_$v 600 python bench.py --model mixtral-8x7b --batch-per-gpu 512 --steps 8 --warmup 3; done ;;
-    b1prof) ;;
+    b1prof|mxprof) ;;
     long)  for t in 8192 32768 65536; do step long/l8b_$t 600 python -u tools/bench_long_prefill.py --model llama-3.1-8b --tokens $t; done
            step long/l70b_32768 600 python -u tools/bench_long_prefill.py --model llama-3.1-70b --tokens 32768 ;;
   esac
@@ -31,4 +31,9 @@ done
 if [ "$1" = b1prof ]; then
   prof cfg/b1prof 300 python3 "$R/bench.py" --model llama-3-8b --batch-per-gpu 1 --steps 16 --warmup 4
   step cfg/b1breakdown 60 python tools/decode_breakdown.py "$(ls "$O"/cfg/b1prof/*/*kernel_trace.csv "$O"/cfg/b1prof/*kernel_trace.csv 2>/dev/null | head -1)" --steps 16 --json "$O/cfg/b1breakdown.json"
+fi
+# mxprof: kernel trace of Mixtral-8x7B decode at 512 sequences and its per-step breakdown
+if [ "$1" = mxprof ]; then
+  prof cfg/mxprof 400 python3 "$R/bench.py" --model mixtral-8x7b --batch-per-gpu 512 --steps 6 --warmup 3
+  step cfg/mxbreakdown 60 python tools/decode_breakdown.py "$(ls "$O"/cfg/mxprof/*/*kernel_trace.csv "$O"/cfg/mxprof/*kernel_trace.csv 2>/dev/null | head -1)" --steps 6 --json "$O/cfg/mxbreakdown.json"
 fi
