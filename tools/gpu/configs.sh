@@ -1,6 +1,6 @@
 #!/bin/bash
 # The other BASELINE.json configs on one GPU: 8B and 70B batch-1 / batch-512 decode, Mixtral, model families,
-# weight-only FP8, long context.   bash tools/gpu/configs.sh [dense|moe|families|fp8|long|moepp2|moepp2mx|b1prof|mxprof]...  (default: dense moe)
+# weight-only FP8, long context.   bash tools/gpu/configs.sh [dense|moe|families|fp8|long|moepp2|moepp2mx|mxdown|b1prof|mxprof]...  (default: dense moe)
 source "$(dirname "$0")/common.sh"
 for what in ${@:-dense moe}; do
   case $what in
@@ -22,6 +22,9 @@ for what in ${@:-dense moe}; do
              XOT_MOE_PP2=$v step cfg/dsv3_8l_b256_moepp2_$v 600 python bench.py --model deepseek-v3 --layers 8 --batch-per-gpu 256 --steps 8 --warmup 3; done ;;
     moepp2mx) # 192-row expert tiles (Mixtral): two-phase ping-pong (default) vs base schedule
            for v in 1 0 1; do XOT_MOE_PP2=$v step cfg/mixtral_b512_moepp2_$v 600 python bench.py --model mixtral-8x7b --batch-per-gpu 512 --steps 8 --warmup 3; done ;;
+    mxdown) # Mixtral B=512: the grouped down GEMM's K split (default 4) and the 256-row tile
+           for v in 2 8 4 6; do XOT_MOE_DN_SPLITS=$v step cfg/mixtral_b512_dn$v 600 python bench.py --model mixtral-8x7b --batch-per-gpu 512 --steps 8 --warmup 3; done
+           XOT_MOE_BM=2256 step cfg/mixtral_b512_bm2256 600 python bench.py --model mixtral-8x7b --batch-per-gpu 512 --steps 8 --warmup 3 ;;
     b1prof|mxprof) ;;
     long)  for t in 8192 32768 65536; do step long/l8b_$t 600 python -u tools/bench_long_prefill.py --model llama-3.1-8b --tokens $t; done
            step long/l70b_32768 600 python -u tools/bench_long_prefill.py --model llama-3.1-70b --tokens 32768 ;;

@@ -38,6 +38,7 @@ MOE_BIG_MIN_ROWS = float(os.environ.get("XOT_MOE_BIG_MIN_ROWS", "24"))
 # K splits of the grouped gate/up GEMM for decode-sized batches (1: fused SiLU epilogue, no slabs)
 MOE_GU_SPLITS = int(os.environ.get("XOT_MOE_GU_SPLITS", "4"))
 MOE_BM = int(os.environ.get("XOT_MOE_BM", "0"))  # force the grouped gemm_big tile code (tests, A/B)
+MOE_DN_SPLITS = int(os.environ.get("XOT_MOE_DN_SPLITS", "0"))  # force the grouped down GEMM's K split on gemm_big tiles
 MOE_PP2 = os.environ.get("XOT_MOE_PP2", "1") == "1"  # 256-row expert tiles on the two-phase ping-pong schedule
 PAGE = 64
 # XOT_SPLIT_DECODE=N: decode batches of at least N sequences (dense models) run as two half-batches on two
@@ -295,6 +296,8 @@ class ShardModel:
       bm, bm_dn = ({256: 2256, 192: 2192}.get(b, b) for b in (bm, bm_dn))
     if MOE_BM and bm:
       bm = bm_dn = MOE_BM
+    if MOE_DN_SPLITS and bm:
+      S_dn = MOE_DN_SPLITS
     act = torch.empty(T * k, F, dtype=torch.bfloat16, device=dev)
     Sg = MOE_GU_SPLITS if (bm == 0 and T * k <= 32 and D % (256 * MOE_GU_SPLITS) == 0) else 1
     if Sg > 1:
