@@ -60,6 +60,9 @@ def test_tuner_offers_two_phase_ping_pong(monkeypatch):
   assert L._tie_break(t) == ("big", 2256, 4)
   t[("big", 2256, 4)] = 0.95
   assert L._tie_break(t) == ("big", 128, 2)
+  # short row tiles: the two-phase 192-row tile is offered and preferred like the 256-row one
+  assert ("big", 1922256, 1) in L.GemmPolicy._big_cands(384, 8192, 8192)
+  assert L._tie_break({("big", 1920256, 2): 0.50, ("big", 1922256, 2): 0.51}) == ("big", 1922256, 2)
   monkeypatch.setattr(L, "TIE_X", 0.0)
   assert L._tie_break({("big", 128, 2): 0.843, ("big", 2256, 4): 0.85}) == ("big", 128, 2)
   monkeypatch.setattr(L, "PP2", False)

@@ -512,7 +512,9 @@ def test_gemm_stream_odd_chunks(gpu, M, Kd, epi):
                                            ("resid", 1256, 4), ("none", 224, 1), ("silu", 224, 1), ("resid", 224, 2),
                                            ("silu", 224, 3), ("none", 2240256, 1), ("silu", 1920256, 1),
                                            ("resid", 1600128, 2), ("silu", 2240128, 1), ("none", 1920128, 3),
-                                           ("none", 2256, 1), ("silu", 2256, 1), ("resid", 2256, 3), ("none", 2256, 5)])
+                                           ("none", 2256, 1), ("silu", 2256, 1), ("resid", 2256, 3), ("none", 2256, 5),
+                                           ("none", 1922256, 1), ("silu", 1922256, 1), ("resid", 1922256, 3),
+                                           ("none", 1922256, 5)])
 def test_gemm_big(gpu, M, epi, bn, splits):
   """Large-M LDS-DMA GEMM on the pre-shuffled layout vs the fp32 reference: masked row tiles, both
   column tilings, uneven split-K ranges, every epilogue, fp32 and bf16 outputs."""

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Headline (BASELINE config 3, Llama-3-70B, 512 sequences, one GPU) and its kernel breakdown.
-#   bash tools/gpu/headline.sh [bench|ab|sk|tune|pp2|oproj|tunelog|tiex|prof|sweep]...      (default: bench prof)
+#   bash tools/gpu/headline.sh [bench|ab|sk|tune|pp2|oproj|tunelog|tiex|b384|prof|sweep]...      (default: bench prof)
 source "$(dirname "$0")/common.sh"
 for what in ${@:-bench prof}; do
   case $what in
@@ -38,6 +38,18 @@ for what in ${@:-bench prof}; do
            for x in 0.10 0 0.10; do
              XOT_GEMM_TUNE_LOG=1 XOT_GEMM_TIE_X=$x XOT_GEMM_TABLE=$O/headline/tbl_x$x.json step headline/tiex_70b_$x 400 python -u bench.py --steps 20 --warmup 5
              XOT_GEMM_TUNE_LOG=1 XOT_GEMM_TIE_X=$x XOT_GEMM_TABLE=$O/headline/tbl_x${x}_8b.json step headline/tiex_8b_$x 400 python -u bench.py --model llama-3-8b --batch-per-gpu 512 --steps 20 --warmup 5; done ;;
+    b384)  # 384 sequences: 192-row tiles (two-phase 1922256 offered), with the tuner's timings
+           XOT_GEMM_TUNE_LOG=1 XOT_GEMM_TABLE=$O/headline/tbl384.json step headline/b384 400 python -u bench.py --batch-per-gpu 384 --steps 20 --warmup 5
+           cp "$O/headline/tbl384.json" "$O/headline/tbl384_base.json"
+           python - "$O/headline/tbl384_base.json" <<'PY'
+import json, sys
+p = sys.argv[1]; t = json.load(open(p))
+for k, v in t.items():
+  if isinstance(v, list) and v[0] == "big" and v[1] == 1922256: t[k] = ["big", 1920256, v[2]]
+json.dump(t, open(p, "w"))
+PY
+           XOT_GEMM_TABLE=$O/headline/tbl384_base.json step headline/b384_base 400 python -u bench.py --batch-per-gpu 384 --steps 20 --warmup 5
+           XOT_GEMM_TABLE=$O/headline/tbl384.json step headline/b384_2 400 python -u bench.py --batch-per-gpu 384 --steps 20 --warmup 5 ;;
     sweep) for b in 448 512 576; do step headline/b$b 400 python -u bench.py --batch-per-gpu $b --steps 10 --warmup 3; done ;;
   esac
 done

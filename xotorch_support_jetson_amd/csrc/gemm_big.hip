@@ -540,7 +540,8 @@ static int big_dispatch(const uint16_t* X, int ldx, const uint16_t* W, const uin
                         int ldr, void* Y, int ldy, float* ws, long ws_elems, int M, int N, int K, int bn, int S,
                         bool reduce, hipStream_t st) {
   // bn = tile code: BN (256 / 128 / 224), 1256 / 2256 (256 x 256 on the four- / two-phase ping-pong), plus
-  // 10000 x BM for row tiles below 256 (160 / 192 / 224: M = 320 / 384 / 448 in two tiles without padding rows)
+  // 10000 x BM for row tiles below 256 (160 / 192 / 224: M = 320 / 384 / 448 in two tiles without padding rows;
+  // 2256 only with 192)
   const int bm = bn / 10000 ? bn / 10000 : 256, code = bn % 10000;
 #define XOT_BIG(BM_, BN_, WM_, NBUF_, ...)                                                                        \
   big_launch<BM_, BN_, WM_, 8 / WM_, 64, NBUF_, EPI, F32, ##__VA_ARGS__>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, \
@@ -556,6 +557,9 @@ static int big_dispatch(const uint16_t* X, int ldx, const uint16_t* W, const uin
     if (bm == 224) XOT_BIG(224, 256, 2, 2);
     else if (bm == 192) XOT_BIG(192, 256, 2, 2);
     else if (bm == 160) XOT_BIG(160, 256, 2, 2);
+    else return -1;
+  } else if (code == 2256) {
+    if (bm == 192) XOT_BIG(192, 256, 2, 2, 2);  // two-phase ping-pong on 192-row tiles (three row tiles per A half)
     else return -1;
   } else if (code == 128) {
     if (bm == 224) XOT_BIG(224, 128, 2, 3);

@@ -353,8 +353,8 @@ class GemmPolicy:
     if N % 224 == 0:  # 7 row groups per wave: whole rounds where 256-wide tiles leave a half round (8B gate/up)
       codes.append(224)
     bm = big_row_tile(M)
-    if bm < 256:  # rows that would leave >= 32 padding rows in 256-row tiles: shorter row tiles, base schedule
-      codes += [bm * 10000 + 256, bm * 10000 + 128]
+    if bm < 256:  # rows that would leave >= 32 padding rows in 256-row tiles: shorter row tiles (two-phase: 192 only)
+      codes += [bm * 10000 + 256, bm * 10000 + 128] + ([bm * 10000 + 2256] if PP2 and bm == 192 else [])
     for bn in codes:
       if N % tile_width(bn) and N < tile_width(bn):  # a partial last column tile is masked; skip tiles wider than N
         continue
@@ -443,12 +443,13 @@ _BIG_PREF = {2256: 0, 1256: 1, 256: 2, 224: 3, 128: 4}
 
 def _tie_break(times: Dict) -> Tuple:
   best = min(times, key=times.get)
-  if best[0] != "big" or best[1] not in _BIG_PREF or TIE <= 0:
+  code = lambda c: c[1] % 10000  # noqa: E731 - the schedule, whatever the row tile
+  if best[0] != "big" or code(best) not in _BIG_PREF or TIE <= 0:
     return best
   close = [c for c, t in times.items()
-           if c[0] == "big" and c[1] in _BIG_PREF and ((c[2] == best[2] and t <= times[best] * (1 + TIE))
-                                                       or (c[1] == 2256 and t <= times[best] * (1 + TIE_X)))]
-  return min(close, key=lambda c: (_BIG_PREF[c[1]], times[c]))
+           if c[0] == "big" and code(c) in _BIG_PREF and ((c[2] == best[2] and t <= times[best] * (1 + TIE))
+                                                          or (code(c) == 2256 and t <= times[best] * (1 + TIE_X)))]
+  return min(close, key=lambda c: (_BIG_PREF[code(c)], times[c]))
 
 
 def _ws_elems(cfg, M, N) -> int:
