@@ -644,7 +644,7 @@ def test_moe_layer(gpu, T, E, k, F, shuffled):
     assert torch.equal(h2, out), S
     assert rel_err(normed, R.rmsnorm(out, lnw, 1e-5)[0]) < 1e-2, S
   if shuffled:  # the same block on gemm_big tiles (128-, 192- and 256-row tiles per expert)
-    for bm in (128, 192, 256, 1128, 1192, 1256, 2256, 2192):  # + 1000: deeper LDS pipelines; 2xxx: two-phase
+    for bm in (128, 192, 256, 1128, 1192, 1256, 2256, 2192, 2128):  # + 1000: deeper LDS pipelines; 2xxx: two-phase
       act2 = torch.empty_like(act)
       C.gemm_moe(x, gw, act2, off, sorted_tok, 2, T, True, 1, bm)
       assert rel_err(act2, act) < 1e-2, bm

@@ -1,6 +1,6 @@
 #!/bin/bash
 # The other BASELINE.json configs on one GPU: 8B and 70B batch-1 / batch-512 decode, Mixtral, model families,
-# weight-only FP8, long context.   bash tools/gpu/configs.sh [dense|moe|families|fp8|long|moepp2|moepp2mx|mxdown|b1prof|mxprof]...  (default: dense moe)
+# weight-only FP8, long context.   bash tools/gpu/configs.sh [dense|moe|families|fp8|long|moepp2|moepp2mx|mxdown|moepp2s|b1prof|mxprof]...  (default: dense moe)
 source "$(dirname "$0")/common.sh"
 for what in ${@:-dense moe}; do
   case $what in
@@ -25,6 +25,9 @@ for what in ${@:-dense moe}; do
     mxdown) # Mixtral B=512: the grouped down GEMM's K split (default 4) and the 256-row tile
            for v in 2 8 4 6; do XOT_MOE_DN_SPLITS=$v step cfg/mixtral_b512_dn$v 600 python bench.py --model mixtral-8x7b --batch-per-gpu 512 --steps 8 --warmup 3; done
            XOT_MOE_BM=2256 step cfg/mixtral_b512_bm2256 600 python bench.py --model mixtral-8x7b --batch-per-gpu 512 --steps 8 --warmup 3 ;;
+    moepp2s) # Mixtral at 128 / 256 sequences: the tuned expert tiles vs all on the two-phase 128-row tile (2128)
+           for b in 256 128; do step cfg/mixtral_b${b}_tuned 600 python bench.py --model mixtral-8x7b --batch-per-gpu $b --steps 16 --warmup 3
+             XOT_MOE_BM=2128 step cfg/mixtral_b${b}_2128 600 python bench.py --model mixtral-8x7b --batch-per-gpu $b --steps 16 --warmup 3; done ;;
     b1prof|mxprof) ;;
     long)  for t in 8192 32768 65536; do step long/l8b_$t 600 python -u tools/bench_long_prefill.py --model llama-3.1-8b --tokens $t; done
            step long/l70b_32768 600 python -u tools/bench_long_prefill.py --model llama-3.1-70b --tokens 32768 ;;

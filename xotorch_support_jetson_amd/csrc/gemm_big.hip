@@ -250,7 +250,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
   };
 
   if constexpr (PP == 1 || PP == 2) {
-    static_assert((BM == 256 || BM == 192) && BN == 256 && WM == 2 && WN == 4 && BK == 64 && NBUF == 2, "PP geometry");
+    static_assert((BM == 256 || BM == 192 || BM == 128) && BN == 256 && WM == 2 && WN == 4 && BK == 64 && NBUF == 2, "PP geometry");
     constexpr int MQ = MT / 2;  // row tiles per A half of a wave (4 at BM 256, 3 at BM 192)
     auto bar = []() {  // raw barrier (no vmcnt / lgkmcnt drain); the asm statements are compiler fences
       asm volatile("" ::: "memory");
@@ -663,6 +663,7 @@ static void big_moe_bm(const uint16_t* X, int ldx, const uint16_t* W, void* Y, i
     case 1256: XOT_MOE(256, 32, 4); break;
     case 2256: XOT_MOE(256, 64, 2, 2); break;  // 256- / 192-row tiles on the two-phase ping-pong schedule
     case 2192: XOT_MOE(192, 64, 2, 2); break;
+    case 2128: XOT_MOE(128, 64, 2, 2); break;
     default: XOT_MOE(256); break;
   }
 #undef XOT_MOE
@@ -672,7 +673,7 @@ int launch_gemm_moe_big(const uint16_t* X, int ldx, const uint16_t* W, void* Y, 
                         const int* off, const int* gather, int E, int max_rows, int N, int K, int S, long ysplit,
                         int bm, hipStream_t s) {
   if (max_rows <= 0) return 0;
-  if ((bm % 1000 != 128 && bm % 1000 != 192 && bm % 1000 != 256) || (bm > 1256 && bm != 2256 && bm != 2192) || N % 256 != 0 ||
+  if ((bm % 1000 != 128 && bm % 1000 != 192 && bm % 1000 != 256) || (bm > 1256 && bm != 2256 && bm != 2192 && bm != 2128) || N % 256 != 0 ||
       K % 128 != 0 || S < 1 ||
       S > K / 64)
     return -1;
