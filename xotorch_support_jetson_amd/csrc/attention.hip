@@ -17,6 +17,7 @@
 // (the reference materialises and JSON-ships a [1,T,T] mask per hop, llm_utils.py:473-511).
 #include "common.h"
 #include "kernels.h"
+#include <cstdlib>
 
 namespace xot {
 
@@ -274,7 +275,7 @@ __device__ __forceinline__ void decode_wave_unit(
     const int unit, const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
     const int32_t* __restrict__ block_tables, int max_blocks, const int32_t* __restrict__ ctx_lens,
     uint16_t* __restrict__ out, float* __restrict__ ws_o, float* __restrict__ ws_ml, int B, int H, int Hkv,
-    int pages_per_part, int nparts, float scale_log2, int num_pages, int* __restrict__ tickets) {
+    int pages_per_part, int nparts, float scale_log2, int num_pages, int* __restrict__ tickets, bool vtail) {
   constexpr int KS = DH / 32;   // k-steps of S^T over the head dim
   constexpr int NDT = DH / 16;  // 16-row d tiles of O^T
   const int lane = threadIdx.x & 63;
@@ -322,18 +323,27 @@ __device__ __forceinline__ void decode_wave_unit(
       for (int s = 0; s < KS; ++s) kf[t][s] = NT ? ld16nt(kb + r * DH + 32 * s) : ld16(kb + r * DH + 32 * s);
     }
   };
-  auto load_v = [&](long page, s16x8 (&vf)[NDT][2]) {
+  // V^T rows hold a page's 64 keys as two 64-B halves; when the context ends in the first half of the last page
+  // (vtail), the second half is not read (zeros: its P is 0 anyway, and stale cache contents never reach O).
+  auto load_v = [&](int p, long page, s16x8 (&vf)[NDT][2]) {
     const uint16_t* vb = vc + ((size_t)page * Hkv + kvh) * DH * PAGE + c * PAGE + 8 * g;
+    const bool hi = !vtail || p * PAGE + 32 < ctx;  // wave-uniform
 #pragma unroll
     for (int dt = 0; dt < NDT; ++dt)
+      vf[dt][0] = NT ? ld16nt(vb + 16 * dt * PAGE) : ld16(vb + 16 * dt * PAGE);
+    if (hi) {
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-        vf[dt][kk] = NT ? ld16nt(vb + 16 * dt * PAGE + 32 * kk) : ld16(vb + 16 * dt * PAGE + 32 * kk);
+      for (int dt = 0; dt < NDT; ++dt)
+        vf[dt][1] = NT ? ld16nt(vb + 16 * dt * PAGE + 32) : ld16(vb + 16 * dt * PAGE + 32);
+    } else {
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) vf[dt][1] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
   };
   auto load = [&](int p, s16x8 (&kf)[4][KS], s16x8 (&vf)[NDT][2]) {
     const long page = page_of(p);
     load_k(p, page, kf);
-    load_v(page, vf);
+    load_v(p, page, vf);
   };
   // S^T tiles of page p (consumes K); the rest of the page (softmax, P.V) is pv() below
   auto scores = [&](const s16x8 (&kf)[4][KS], f32x4 (&st)[4]) {
@@ -394,7 +404,7 @@ __device__ __forceinline__ void decode_wave_unit(
       scores(kf, st);
       if (more) load_k(p + 1, nxt, kf);  // K registers are free once the S^T MFMAs have read them
       pv(p, st, vf);
-      if (more) load_v(nxt, vf);
+      if (more) load_v(p + 1, nxt, vf);
     }
   } else if constexpr (PF == 1) {
     s16x8 ka[4][KS], kb2[4][KS];
@@ -462,11 +472,19 @@ __global__ __launch_bounds__(PF == 2 ? 512 : 256, PF == 2 ? 2 : 1) void attn_dec
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
     const int32_t* __restrict__ block_tables, int max_blocks, const int32_t* __restrict__ ctx_lens,
     uint16_t* __restrict__ out, float* __restrict__ ws_o, float* __restrict__ ws_ml, int B, int H, int Hkv,
-    int pages_per_part, int nparts, float scale_log2, int num_pages, int* __restrict__ tickets) {
+    int pages_per_part, int nparts, float scale_log2, int num_pages, int* __restrict__ tickets, int vtail) {
   const int unit = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
   if (unit >= B * Hkv * nparts) return;  // whole wave
   decode_wave_unit<DH, PF, NT>(unit, q, kc, vc, block_tables, max_blocks, ctx_lens, out, ws_o, ws_ml, B, H, Hkv,
-                               pages_per_part, nparts, scale_log2, num_pages, tickets);
+                               pages_per_part, nparts, scale_log2, num_pages, tickets, vtail != 0);
+}
+
+static int attn_vtail() {  // XOT_ATTN_VTAIL=0: read the last page's whole V^T rows (A/B)
+  static const int v = [] {
+    const char* e = getenv("XOT_ATTN_VTAIL");
+    return e != nullptr ? atoi(e) : 1;
+  }();
+  return v;
 }
 
 int launch_attn_decode(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, const int32_t* block_tables,
@@ -485,7 +503,7 @@ int launch_attn_decode(const uint16_t* q, const uint16_t* kc, const uint16_t* vc
     const int wgs = (units + wpg - 1) / wpg;
 #define XOT_WAVE(DHV, PFV, NTV)                                                                                  \
   attn_decode_wave_kernel<DHV, PFV, NTV><<<wgs, 64 * wpg, 0, s>>>(q, kc, vc, block_tables, max_blocks, ctx_lens, out, ws_o, \
-                                                        ws_ml, B, H, Hkv, pages_per_part, nparts, sl, num_pages, tickets)
+                                                        ws_ml, B, H, Hkv, pages_per_part, nparts, sl, num_pages, tickets, attn_vtail())
     // algo 1: no prefetch; 2 / 3: double register set (3: nt loads); 5 / 6: one set refilled per half (6: nt)
     if (Dh == 128) {
       if (algo == 3) XOT_WAVE(128, 1, true); else if (algo == 2) XOT_WAVE(128, 1, false);
