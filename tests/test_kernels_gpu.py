@@ -964,3 +964,23 @@ def test_gemm_sk(gpu, M, N, Kd, epi, f32):
   torch.cuda.synchronize()
   assert torch.equal(y, first)
   assert int(sync.abs().sum()) == 0
+
+
+@pytest.mark.parametrize("rows,D,S", [(1, 8192, 4), (300, 8192, 4), (512, 8192, 4), (512, 8192, 3), (512, 4096, 4),
+                                      (256, 5120, 2), (512, 8192, 5)])
+def test_splitk_resid_rmsnorm(gpu, rows, D, S):
+  """Split-K slab reduce + bias + residual (in place) + RMSNorm vs fp32: the 256-thread rows and the 1024-thread
+  wide rows (D = 8192 at 256+ rows), unrolled and runtime slab counts."""
+  from xotorch_support_jetson_amd.ops._ext import require
+  torch.manual_seed(rows + D + S)
+  ws = torch.randn(S * rows * D, device=gpu, dtype=torch.float32)
+  h = torch.randn(rows, D, device=gpu, dtype=torch.bfloat16)
+  bias = torch.randn(D, device=gpu, dtype=torch.bfloat16)
+  w = (1 + 0.1 * torch.randn(D, device=gpu)).to(torch.bfloat16)
+  out = torch.empty(rows, D, device=gpu, dtype=torch.bfloat16)
+  ref_h = (h.float() + bias.float() + ws.view(S, rows, D).sum(0)).to(torch.bfloat16)
+  hf = ref_h.float()
+  ref = hf * torch.rsqrt(hf.pow(2).mean(-1, keepdim=True) + 1e-5) * w.float()
+  require().splitk_resid_rmsnorm(ws, S, bias, h, w, out, 1e-5)
+  assert rel_err(h, ref_h) < 1e-2
+  assert rel_err(out, ref) < 1e-2

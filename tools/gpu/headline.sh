@@ -1,6 +1,6 @@
 #!/bin/bash
 # Headline (BASELINE config 3, Llama-3-70B, 512 sequences, one GPU) and its kernel breakdown.
-#   bash tools/gpu/headline.sh [bench|ab|sk|tune|pp2|oproj|tunelog|tiex|b384|vtail|prof|sweep]...      (default: bench prof)
+#   bash tools/gpu/headline.sh [bench|ab|sk|tune|pp2|oproj|tunelog|tiex|b384|vtail|srr|prof|sweep]...      (default: bench prof)
 source "$(dirname "$0")/common.sh"
 for what in ${@:-bench prof}; do
   case $what in
@@ -53,6 +53,8 @@ PY
     vtail) # decode attention skipping the unused V half of the last page (default) or not: kernel alone, then the step
            for v in 1 0 1; do XOT_ATTN_VTAIL=$v step headline/vtail_attn_$v 300 python -u tools/bench_attn_layout.py; done
            for v in 1 0 1; do XOT_ATTN_VTAIL=$v XOT_GEMM_TABLE=$O/headline/tbl_vt.json step headline/vtail_step_$v 400 python -u bench.py --steps 20 --warmup 5; done ;;
+    srr)   # split-K residual RMSNorm at D = 8192: 1024 threads per row (default) vs 256
+           for v in 1 0 1; do XOT_SRR_WIDE=$v XOT_GEMM_TABLE=$O/headline/tbl_srr.json step headline/srr_$v 400 python -u bench.py --steps 20 --warmup 5; done ;;
     sweep) for b in 448 512 576; do step headline/b$b 400 python -u bench.py --batch-per-gpu $b --steps 10 --warmup 3; done ;;
   esac
 done

@@ -8,6 +8,7 @@
 // xotorch/inference/torch/models/llm_utils.py:399-435,513-522).
 // All loads/stores are 16 B per lane (8 x bf16); reductions are wave64 shuffles.
 #include "common.h"
+#include <cstdlib>
 #include "kernels.h"
 
 namespace xot {
@@ -81,20 +82,22 @@ void launch_rmsnorm(const uint16_t* x, const uint16_t* res, const uint16_t* w, u
 // the split-K reduce kernel of a residual projection (o_proj / down_proj) and the RMSNorm that follows it.
 // SS > 0: exactly SS slabs, loads unrolled and issued together (a runtime slab loop waits for each load
 // in turn: one row at decode batch 1 took 6.9 us); SS = 0: any S.
-template <int MAXC, int SS>
-__global__ __launch_bounds__(256) void splitk_resid_rmsnorm_kernel(const float* __restrict__ ws, int S,
+// NTH threads per row: 1024 for wide rows (D = 8192 at decode batch 512: 512 workgroups of 256 threads left 8 waves
+// per CU and each thread's four chunks x (h + S slabs) loads partly serialised; 16 waves per row keep one chunk each)
+template <int MAXC, int SS, int NTH = 256>
+__global__ __launch_bounds__(NTH) void splitk_resid_rmsnorm_kernel(const float* __restrict__ ws, int S,
                                                                    size_t sstride, const uint16_t* __restrict__ bias,
                                                                    uint16_t* __restrict__ h,
                                                                    const uint16_t* __restrict__ w,
                                                                    uint16_t* __restrict__ out, int D, float eps) {
-  __shared__ float red[4];
+  __shared__ float red[NTH / 64];
   const int row = blockIdx.x, tid = threadIdx.x, nchunk = D >> 3;
   const size_t base = (size_t)row * D;
   float v[MAXC][8];
   float ss = 0.f;
 #pragma unroll
   for (int i = 0; i < MAXC; ++i) {
-    const int c = tid + i * 256;
+    const int c = tid + i * NTH;
     if (c < nchunk) {
       const s16x8 a = ld16(h + base + c * 8);
       float acc[8];
@@ -143,11 +146,13 @@ __global__ __launch_bounds__(256) void splitk_resid_rmsnorm_kernel(const float* 
   ss = wave_sum(ss);
   if ((tid & 63) == 0) red[tid >> 6] = ss;
   __syncthreads();
-  ss = red[0] + red[1] + red[2] + red[3];
+  ss = 0.f;
+#pragma unroll
+  for (int k = 0; k < NTH / 64; ++k) ss += red[k];
   const float inv = rsqrtf(ss / (float)D + eps);
 #pragma unroll
   for (int i = 0; i < MAXC; ++i) {
-    const int c = tid + i * 256;
+    const int c = tid + i * NTH;
     if (c < nchunk) {
       s16x8 wv = ld16(w + c * 8), o;
 #pragma unroll
@@ -157,14 +162,22 @@ __global__ __launch_bounds__(256) void splitk_resid_rmsnorm_kernel(const float* 
   }
 }
 
+static bool srr_wide() {  // XOT_SRR_WIDE=0: 256 threads per row at every width (A/B)
+  static const bool v = [] {
+    const char* e = getenv("XOT_SRR_WIDE");
+    return e == nullptr || atoi(e) != 0;
+  }();
+  return v;
+}
+
 void launch_splitk_resid_rmsnorm(const float* ws, int S, const uint16_t* bias, uint16_t* h, const uint16_t* w,
                                  uint16_t* out, int rows, int D, float eps, hipStream_t s) {
   if (rows <= 0) return;
   const int nchunk = D / 8;
   const size_t ss = (size_t)rows * D;
-  auto go = [&](auto maxc) {
-    constexpr int MC = decltype(maxc)::value;
-#define XOT_SRR(SV) splitk_resid_rmsnorm_kernel<MC, SV><<<rows, 256, 0, s>>>(ws, S, ss, bias, h, w, out, D, eps)
+  auto go = [&](auto maxc, auto nth) {
+    constexpr int MC = decltype(maxc)::value, NT = decltype(nth)::value;
+#define XOT_SRR(SV) splitk_resid_rmsnorm_kernel<MC, SV, NT><<<rows, NT, 0, s>>>(ws, S, ss, bias, h, w, out, D, eps)
     switch (S) {
       case 1: XOT_SRR(1); break;
       case 2: XOT_SRR(2); break;
@@ -176,14 +189,17 @@ void launch_splitk_resid_rmsnorm(const float* ws, int S, const uint16_t* bias, u
     }
 #undef XOT_SRR
   };
+  using I256 = std::integral_constant<int, 256>;
   if (nchunk <= 256)
-    go(std::integral_constant<int, 1>());
+    go(std::integral_constant<int, 1>(), I256());
   else if (nchunk <= 512)
-    go(std::integral_constant<int, 2>());
+    go(std::integral_constant<int, 2>(), I256());
+  else if (nchunk <= 1024 && rows >= 256 && srr_wide())
+    go(std::integral_constant<int, 1>(), std::integral_constant<int, 1024>());
   else if (nchunk <= 1024)
-    go(std::integral_constant<int, 4>());
+    go(std::integral_constant<int, 4>(), I256());
   else
-    go(std::integral_constant<int, 8>());
+    go(std::integral_constant<int, 8>(), I256());
 }
 
 // ---------------------------------------------------------------- RMSNorm bwd
