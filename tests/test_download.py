@@ -141,6 +141,8 @@ def test_corrupt_download_rejected(tmp_path, monkeypatch):
 def test_unreachable_hub_fails_fast(monkeypatch):
   """Connection-level failures (no route / DNS / refused) stop the retries after `unreachable_after` attempts and
   mark the hub unreachable for the process, so later calls fail at once; transient errors keep their retries."""
+  import socket
+  import aiohttp
   import xotorch_support_jetson_amd.download.new_shard_download as nsd
   monkeypatch.setattr(nsd, "_retry_delay", lambda attempt: 0.0)
   monkeypatch.setattr(nsd.HFRepoClient, "unreachable", False)
@@ -159,6 +161,17 @@ def test_unreachable_hub_fails_fast(monkeypatch):
   async def main():
     c = nsd.HFRepoClient(endpoint="http://127.0.0.1:9", attempts=30)
     assert await c._with_retry(flaky) == "ok" and len(calls) == 5  # transient: retried
+    for transient in (aiohttp.SocketTimeoutError("read"), ConnectionResetError("reset"), asyncio.TimeoutError(),
+                      aiohttp.ServerDisconnectedError()):
+      calls.clear()
+
+      async def slow(exc=transient):
+        calls.append(1)
+        if len(calls) < 4:
+          raise exc
+        return "ok"
+      assert await c._with_retry(slow) == "ok" and len(calls) == 4 and not nsd.HFRepoClient.unreachable
+    assert nsd._unreachable_error(aiohttp.ConnectionTimeoutError()) and nsd._unreachable_error(socket.gaierror(-2, "x"))
     calls.clear()
     with pytest.raises(ConnectionError):
       await c._with_retry(refused)

@@ -726,9 +726,13 @@ def test_vision_tower_gpu_matches_cpu(gpu):
   vw = random_vision(c, "cpu", seed=4)
   pixels = torch.randn(2, 3, 336, 336, generator=torch.Generator().manual_seed(2))
   ref = image_features(c, vw, pixels)
-  got = image_features(c, {k: t.to(gpu) for k, t in vw.items()}, pixels.to(gpu))
+  vg = {k: t.to(gpu) for k, t in vw.items()}
+  got = image_features(c, vg, pixels.to(gpu))
   assert got.shape == ref.shape == (2 * 576, c.hidden_size)
   assert rel_err(got.cpu(), ref) < 3e-2
+  # a second image on the same weights dict reuses the shuffled copies (identity-keyed cache)
+  again = image_features(c, vg, pixels[:1].to(gpu))
+  assert rel_err(again.cpu(), ref[:576]) < 3e-2
 
 
 @pytest.mark.parametrize("T,E,D", [(1, 8, 4096), (37, 8, 4096), (512, 8, 1024), (5, 4, 256), (9, 16, 512),

@@ -87,3 +87,20 @@ def test_ui_image_message_body_is_answered_by_llava(tmp_path):
   from xotorch_support_jetson_amd.models.vision import num_image_tokens
   (n_ids, pixels), = seen
   assert isinstance(pixels, torch.Tensor) and pixels.shape[0] == 1 and n_ids > num_image_tokens(c)
+
+
+def test_failed_send_resumes_only_after_a_download_completes():
+  """A failed send is re-sent only after a download was seen in progress and then finished -- never on an empty
+  progress map (a plain server error would otherwise be re-sent every second) -- and at most 3 times."""
+  got = _js("""(() => {
+    const w = {failed: true, sawDownload: false, tries: 0}, out = [];
+    const busy = [["n", {status: "in_progress", total_bytes: 10, downloaded_bytes: 3}]];
+    const done = [["n", {status: "complete", total_bytes: 10, downloaded_bytes: 10}]];
+    out.push(t.resumeAfterDownload(w, []));        // error with no download at all: no resume
+    out.push(t.resumeAfterDownload(w, []));
+    out.push(t.resumeAfterDownload(w, busy));      // the model starts downloading
+    out.push(t.resumeAfterDownload(w, done));      // ... and finishes: resume once
+    out.push(t.resumeAfterDownload(w, done));      // not again without a new failure
+    for (let i = 0; i < 5; i++) { w.failed = true; t.resumeAfterDownload(w, busy); out.push(t.resumeAfterDownload(w, [])); }
+    return out; })()""")
+  assert got == [False, False, False, True, False, True, True, False, False, False]

@@ -88,3 +88,18 @@ def test_user_text_cannot_forge_image_marker_and_paths_are_confined(tmp_path, mo
   for bad in ("/etc/passwd", "../x.png", str(tmp_path / ".." / "x.png")):
     with pytest.raises(ValueError):
       load_image(bad)
+
+
+def test_shuffled_weight_cache_is_identity_keyed(monkeypatch):
+  """The vision tower's shuffled-weight cache is looked up once per projection per image: the second lookup of
+  the same tensor must hit (a WeakKeyDictionary keyed by tensors compared them elementwise and raised)."""
+  from xotorch_support_jetson_amd.models import vision
+  import xotorch_support_jetson_amd.ops.weights_layout as wl
+  calls = []
+  monkeypatch.setattr(wl, "shuffle_for_stream", lambda w: (calls.append(1), w.clone())[1])
+  w = torch.randn(32, 128, dtype=torch.bfloat16)
+  a = vision._stream_weight(w)
+  b = vision._stream_weight(w)
+  assert a is b and len(calls) == 1
+  w2 = w.clone()  # equal values, different tensor: its own entry
+  assert vision._stream_weight(w2) is not a and len(calls) == 2

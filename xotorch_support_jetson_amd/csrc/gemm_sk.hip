@@ -229,7 +229,13 @@ __global__ __launch_bounds__(512, 1) void gemm_sk_kernel(const uint16_t* __restr
         if (tid == 0) {
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          __hip_atomic_store(flag_of(group), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          // 0 -> 1 publishes; -1 means the last arriver gave up on this part (timed out, tile poisoned):
+          // consume that mark back to 0, so a late publish never leaves a stale 1 for the next launch (stream
+          // order guarantees this wave finishes before the next launch of the stream starts)
+          int expect = 0;
+          if (!__hip_atomic_compare_exchange_strong(flag_of(group), &expect, 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT))
+            __hip_atomic_store(flag_of(group), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
       } else {
         if (tid == 0) {
@@ -240,10 +246,18 @@ __global__ __launch_bounds__(512, 1) void gemm_sk_kernel(const uint16_t* __restr
             // bounded: a part that holds a ticket is resident and publishes within microseconds; the bound
             // (seconds) only keeps a broken invariant from hanging the GPU
             int spin = 0;
-            for (; spin < (1 << 24) && __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0; ++spin)
+            for (; spin < (1 << 24) && __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 1; ++spin)
               __builtin_amdgcn_s_sleep(2);
-            stale |= spin == (1 << 24);
-            __hip_atomic_store(f, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (spin == (1 << 24)) {
+              // timed out: mark the part abandoned (-1) unless it published in the meantime (then clear it)
+              stale = 1;
+              int expect = 0;
+              if (!__hip_atomic_compare_exchange_strong(f, &expect, -1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT))
+                __hip_atomic_store(f, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+              __hip_atomic_store(f, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
           }
           __hip_atomic_store(&tickets[tk], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");

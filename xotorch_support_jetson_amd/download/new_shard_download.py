@@ -15,6 +15,7 @@ weights of the same architecture.
 from __future__ import annotations
 
 import asyncio
+import errno
 import hashlib
 import json
 import os
@@ -84,14 +85,20 @@ def _retry_delay(attempt: int) -> float:
 
 
 def _unreachable_error(e: BaseException) -> bool:
-  """A failure that says the hub cannot be reached at all (no route, no DNS, refused) rather than a transient one."""
+  """A CONNECT-phase failure: the hub cannot be reached at all (no DNS, no route, refused, connect timeout).
+  Failures after a connection was made -- socket read timeouts, resets mid-transfer, HTTP errors -- are transient
+  and keep the normal backoff retries (a slow large file must not mark the hub unreachable for the process)."""
   try:
     import aiohttp
-    if isinstance(e, (aiohttp.ClientConnectorError, aiohttp.ServerTimeoutError)):
+    if isinstance(e, (aiohttp.ClientConnectorError, aiohttp.ConnectionTimeoutError)):
       return True
+    if isinstance(e, aiohttp.ClientError):
+      return False  # ServerDisconnectedError, SocketTimeoutError (read), ClientPayloadError, ...
   except ImportError:
     pass
-  return isinstance(e, (ConnectionError, socket.gaierror, asyncio.TimeoutError))
+  if isinstance(e, (ConnectionRefusedError, socket.gaierror)):
+    return True
+  return isinstance(e, OSError) and e.errno in (errno.ENETUNREACH, errno.EHOSTUNREACH)
 
 
 class HFRepoClient:

@@ -18,11 +18,11 @@ from __future__ import annotations
 import base64
 import io
 import re
-import weakref
 from typing import Dict, List, Tuple
 
 import torch
 import torch.nn.functional as F
+from torch.utils.weak import WeakIdKeyDictionary
 
 from ..ops import kernels as K
 
@@ -177,7 +177,8 @@ def random_vision(c, device, dtype=torch.bfloat16, seed: int = 0, std: float = 0
 # GPU copies of the tower's projection weights in the kernel library's pre-shuffled layout (made once per weight
 # tensor, on first use), so the tower runs on the same stream / big-tile GEMMs as the language model; the
 # checkpoint-facing dict keeps the HF row-major tensors
-_SHUF: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
+# keyed by tensor identity: a WeakKeyDictionary would compare tensors with the elementwise __eq__ on a hash clash
+_SHUF = WeakIdKeyDictionary()
 
 
 def _stream_weight(w: torch.Tensor) -> torch.Tensor:

@@ -104,8 +104,25 @@ function requestBody(model, messages, temperature, maxTokens) {
   return { model, stream: true, messages: apiMessages(messages), temperature, max_tokens: maxTokens };
 }
 
+// Resume decision for a failed send, called once per download-progress poll.  `w` = {failed, sawDownload,
+// tries}: `failed` is set by the failed send; the pending message is re-sent only once a download was seen in
+// progress AFTER that failure and every download has since completed (an empty progress map before any download
+// was seen is not "complete"), and at most `maxTries` times per message.  Returns true to resume now.
+function downloadComplete(d) {
+  return d.status === "complete" || Boolean(d.total_bytes && d.downloaded_bytes >= d.total_bytes);
+}
+
+function resumeAfterDownload(w, entries, maxTries = 3) {
+  if (!w.failed) return false;
+  const active = entries.filter(([, d]) => !downloadComplete(d)).length;
+  if (active > 0) { w.sawDownload = true; return false; }
+  if (!w.sawDownload || w.tries >= maxTries) return false;
+  w.failed = false; w.sawDownload = false; w.tries += 1;
+  return true;
+}
+
 if (typeof module !== "undefined" && module.exports) {
-  module.exports = { escapeHtml, highlight, renderMarkdown, apiMessages, requestBody };
+  module.exports = { escapeHtml, highlight, renderMarkdown, apiMessages, requestBody, resumeAfterDownload };
 }
 
 // ------------------------------------------------------------------ the page
@@ -119,6 +136,7 @@ const state = {
   abort: null,
   image: null,             // data URL of the attachment for the next message
   lastError: null,         // the last send failed (e.g. the model was still downloading): resume when ready
+  wait: { failed: false, sawDownload: false, tries: 0 },  // resumeAfterDownload's state for the pending message
 };
 
 function save() {
@@ -337,10 +355,13 @@ async function generate(conv) {
     ok = true;
   } catch (e) {
     if (e.name === "AbortError") ok = true;  // stopped by the user: nothing to resume
-    else { reply.content += `\n[error: ${e.message}]`; state.lastError = e.message; }
+    else {
+      reply.content += `\n[error: ${e.message}]`; state.lastError = e.message;
+      state.wait.failed = true; state.wait.sawDownload = false;
+    }
   } finally {
     state.abort = null;
-    if (ok) { setPending(null); state.lastError = null; }
+    if (ok) { setPending(null); state.lastError = null; state.wait = { failed: false, sawDownload: false, tries: 0 }; }
     $("send").hidden = false; $("stop").hidden = true;
     save(); drawMessages();
   }
@@ -396,8 +417,7 @@ async function pollDownloads() {
         `${pct.toFixed(1)}%</div><div class="bar"><div style="width:${pct}%"></div></div>`;
       box.appendChild(row);
     }
-    const complete = entries.every(([, d]) => d.status === "complete" || (d.total_bytes && d.downloaded_bytes >= d.total_bytes));
-    if (complete && state.lastError && getPending()) { state.lastError = null; resumePending(); }
+    if (getPending() && resumeAfterDownload(state.wait, entries)) { state.lastError = null; resumePending(); }
   } catch (e) { /* ignore */ }
 }
 
