@@ -5,8 +5,9 @@
   torchrun --nproc-per-node N bench.py --gpus N ...         (one rank per GPU, RCCL p2p ring)
 
 Each rank holds 80/N consecutive layers (ring memory-weighted partitioner).  The node serves
-N micro-batches of --batch-per-gpu sequences each (weak scaling: per-GPU work per step is fixed:
-80 layer-passes x batch-per-gpu tokens), so the ring is full and all GPUs work concurrently.
+N x --batch-per-gpu sequences (weak scaling: per-GPU work per step is fixed: 80 layer-passes x batch-per-gpu
+tokens) as N micro-batches (or --micro-batches K >= N of N x batch-per-gpu / K each), so the ring is full and
+all GPUs work concurrently.
 Prompts (--prompt-len tokens, synthetic ids) are prefilled through the real model, then W untimed
 decode rounds, then K timed rounds; one round = every sequence in the node generates one token
 (sampled on device with temperature / top-k 35, the reference's sampler).  Weights are random-init
@@ -44,6 +45,10 @@ def main():
   ap.add_argument("--warmup", type=int, default=3)
   ap.add_argument("--model", default="llama-3-70b")
   ap.add_argument("--batch-per-gpu", type=int, default=int(os.environ.get("XOT_BENCH_BATCH", 512)))
+  ap.add_argument("--micro-batches", type=int, default=0,
+                  help="micro-batches circulating in the ring (default: one per stage).  The node's batch stays "
+                       "gpus x batch-per-gpu; 2 x gpus micro-batches of half the size give every stage a spare "
+                       "micro-batch to run while a hand-off is in flight (hop latency / stage jitter slack)")
   ap.add_argument("--prompt-len", type=int, default=512)
   ap.add_argument("--temperature", type=float, default=0.6)
   ap.add_argument("--layers", type=int, default=0, help="debug only: truncate the model (result marked invalid)")
@@ -72,8 +77,10 @@ def main():
   shards = equal_layer_shards(args.model, cfg.num_layers, world)
   assert len(shards) == world, shards
   shard = shards[rank]
-  M = world  # micro-batches in flight = stages, so the ring is always full
-  B = args.batch_per_gpu
+  M = args.micro_batches or world  # micro-batches in flight >= stages, so the ring is always full
+  if M < world or (args.batch_per_gpu * world) % M:
+    raise SystemExit(f"--micro-batches {M}: needs >= {world} and to divide {args.batch_per_gpu * world} sequences")
+  B = args.batch_per_gpu * world // M  # sequences per micro-batch
   max_ctx = args.prompt_len + args.warmup + args.steps + 8
   pages_per_seq = -(-max_ctx // 64)
   t0 = time.time()
@@ -164,7 +171,9 @@ def main():
         "global_batch": M * B,
         "seq_len": args.prompt_len,
         "parallelism": f"pp{world} (ring, {M} micro-batches x {B})",
-        "batch_per_gpu": B,
+        "batch_per_gpu": args.batch_per_gpu,
+        "micro_batches": M,
+        "micro_batch_size": B,
         "decode_context": f"{args.prompt_len + args.warmup}..{args.prompt_len + args.warmup + args.steps}",
         "sampling": f"temperature {args.temperature}, top-k 35 (on-device)",
         "weight_dtype": args.weight_dtype,

@@ -68,3 +68,27 @@ def test_bench_driver_command_many_ranks(n, tmp_path):
   # with the split head a round's ids are drawn at the start of the next round by the first stage, so the
   # ring's list starts with the prefill token and the single-process list with the first decode token
   assert tn and len(tn) == len(t1) and tn[1:] == t1[:-1]
+
+
+def test_bench_more_micro_batches_than_stages(tmp_path):
+  """--micro-batches 2 x world (half-size micro-batches: slack for the hop latency) keeps the node's batch and
+  the tokens: sequence 0's greedy ids through a 2-rank ring of 4 one-sequence micro-batches equal the
+  single-process run's, and the config reports the micro-batching."""
+  base = ["bench.py", "--steps", "3", "--warmup", "1", "--model", "tiny-llama-8l", "--prompt-len", "8",
+          "--temperature", "0"]
+  env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1")
+  one = subprocess.run([sys.executable] + base + ["--gpus", "1", "--batch-per-gpu", "2", "--dump-tokens",
+                                                  str(tmp_path / "t1.json")],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+  assert one.returncode == 0, one.stderr[-3000:]
+  cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
+         "127.0.0.1", "--master-port", str(_port())] + base + ["--gpus", "2", "--batch-per-gpu", "2",
+                                                               "--micro-batches", "4", "--dump-tokens",
+                                                               str(tmp_path / "tn.json")]
+  r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+  assert r.returncode == 0, r.stderr[-3000:]
+  d = json.loads([l for l in r.stdout.splitlines() if l.strip().startswith("{")][-1])
+  assert d["config"]["global_batch"] == 4 and d["config"]["micro_batches"] == 4
+  assert d["config"]["micro_batch_size"] == 1 and "4 micro-batches x 1" in d["config"]["parallelism"]
+  t1, tn = json.load(open(tmp_path / "t1.json")), json.load(open(tmp_path / "tn.json"))
+  assert [s[0] for s in tn[1:]] == [s[0] for s in t1[:-1]]

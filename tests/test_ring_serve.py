@@ -417,3 +417,45 @@ def test_ring_llava_image_prompt_matches_engine():
   p = _image_prompt()
   got = _run_orch(2, "tiny-llava", [p], 5)
   assert got["outs"] == [_engine_greedy("tiny-llava", p, 5)]
+
+
+@pytest.mark.gpu
+def test_ring_server_tokens_equal_ring_stage_gpu():
+  """The served path and the benchmarked path are one code path: four requests through RingServer (world 1:
+  async lane steps, decoders fed from the device ids of the step before) draw exactly the tokens bench.py's
+  RingStage / run_decode_steps draws for the same prompts -- sampled at temperature 0.7 with the same seed, on
+  cuda:0 with the decode graphs."""
+  from xotorch_support_jetson_amd.inference.shard import Shard
+  from xotorch_support_jetson_amd.ops._ext import require
+  from xotorch_support_jetson_amd.parallel.comm import LoopbackTransport
+  from xotorch_support_jetson_amd.parallel.pipeline import MicroBatch, RingStage, run_decode_steps
+  require()
+  name, B, P, steps = "tiny-llama-d64", 4, 12, 8
+  c = PRESETS[name]
+  shard = Shard(name, 0, c.num_layers - 1, c.num_layers)
+  prompt = torch.randint(0, c.vocab_size, (B, P), generator=torch.Generator().manual_seed(8), dtype=torch.int32)
+  st = RingStage(ShardRunner(c, shard, "cuda:0", max_batch=8, max_ctx=128), 0, 1, LoopbackTransport(0, 1))
+  mb = MicroBatch([f"r{i}" for i in range(B)], prompt=prompt, temps=torch.full((B,), 0.7, device="cuda:0"))
+  first = st.prefill(mb)
+  mb.tokens.append(first.tolist())
+  run_decode_steps(st, [mb], steps - 1, first_tokens=[first], record=True)
+  ref = {f"q{i}": [s[i] for s in mb.tokens] for i in range(B)}
+
+  srv = RingServer(ShardRunner(c, shard, "cuda:0", max_batch=8, max_ctx=128), 0, 1, P2PTransport(0, 1),
+                   prefix_cache=False)
+  out, done = {}, threading.Event()
+
+  def on_tok(rid, toks, fin):
+    out.setdefault(rid, []).extend(toks)
+    if sum(len(v) for v in out.values()) == B * steps:
+      done.set()
+  srv.on_token(on_tok)
+  for i in range(B):
+    srv.submit(f"q{i}", prompt[i].tolist(), 0.7, steps)
+  th = threading.Thread(target=srv.serve_forever, kwargs=dict(idle_wait=0.05))
+  th.start()
+  ok = done.wait(120)
+  srv.stop()
+  th.join(60)
+  assert ok, out
+  assert out == ref

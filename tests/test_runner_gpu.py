@@ -429,3 +429,59 @@ def test_llama70b_layers_tuned_decode_match_cpu(gpu):
     agree = (lc.argmax(-1) == lg.argmax(-1).cpu()).float().mean().item()
     assert agree > 0.9, agree
     tok = lc.argmax(-1).int()
+
+
+def test_decode_tick_issues_no_host_sync(gpu):
+  """The decode tick never blocks the host on the device: run_decode_steps for one stage (world 1) and for the
+  split-head loopback pair under torch.cuda.set_sync_debug_mode("error") -- any .item() / .tolist(), blocking
+  copy or stream / device synchronize inside a tick raises.  (An unnoticed sync added to the tick would
+  serialise an 8-stage ring.)  Graph capture happens in the untimed warm-up, outside the mode."""
+  from xotorch_support_jetson_amd.parallel.comm import LoopbackTransport
+  from xotorch_support_jetson_amd.parallel.pipeline import MicroBatch, RingStage, run_decode_steps
+  name = "tiny-llama-d64"
+  c = preset(name)
+  L = c.num_layers
+  B, P = 3, 12
+  prompt = torch.randint(0, c.vocab_size, (B, P), generator=torch.Generator().manual_seed(2), dtype=torch.int32)
+
+  def mb(tag):
+    return MicroBatch([f"{tag}{i}" for i in range(B)], prompt=prompt, temps=torch.full((B,), 0.7, device=gpu))
+
+  torch.cuda.set_sync_debug_mode("error")
+  try:
+    with pytest.raises(RuntimeError):
+      torch.ones(1, device=gpu).item()  # the mode is live
+  finally:
+    torch.cuda.set_sync_debug_mode("default")
+
+  LoopbackTransport._queues.clear()
+  one = RingStage(ShardRunner(c, Shard(name, 0, L - 1, L), gpu, max_batch=4, max_ctx=256), 0, 1,
+                  LoopbackTransport(0, 1))
+  mbs = [mb("a"), mb("b")]
+  items = run_decode_steps(one, mbs, 2, first_tokens=[one.prefill(m) for m in mbs])  # captures the graphs
+  torch.cuda.synchronize()
+  torch.cuda.set_sync_debug_mode("error")
+  try:
+    items = run_decode_steps(one, mbs, 4, first_tokens=items)
+  finally:
+    torch.cuda.set_sync_debug_mode("default")
+
+  s0 = RingStage(ShardRunner(c, Shard(name, 0, L // 2 - 1, L), gpu, max_batch=4, max_ctx=256), 0, 2,
+                 LoopbackTransport(0, 2), split_head=True)
+  s1 = RingStage(ShardRunner(c, Shard(name, L // 2, L - 1, L), gpu, max_batch=4, max_ctx=256), 1, 2,
+                 LoopbackTransport(1, 2), split_head=True)
+  m = mb("s")
+  s0.prefill(m)
+  s1._send_item(s1.prefill(m))
+  for _ in range(2):  # capture
+    s0.decode_tick(m)
+    s1.decode_tick(m)
+  torch.cuda.synchronize()
+  torch.cuda.set_sync_debug_mode("error")
+  try:
+    for _ in range(4):
+      s0.decode_tick(m)
+      s1.decode_tick(m)
+  finally:
+    torch.cuda.set_sync_debug_mode("default")
+  torch.cuda.synchronize()

@@ -1,0 +1,105 @@
+"""`xot train` (the reference's protocol: Node -> engine.train -> ShardTrainer.step, reference
+xotorch/orchestration/node.py:299-345, main.py:301-318) runs on the kernel library only: with the reference's
+batch-size-1 ragged JSONL lengths (T not a multiple of 128) no vendor GEMM may run -- a dispatch mode that raises
+on every aten GEMM op wraps the GPU engine's executor (and autograd's device threads, which inherit it) -- and
+the losses and gradients still match the CPU path on the same weights."""
+import asyncio
+
+import numpy as np
+import pytest
+import torch
+from torch.utils._python_dispatch import TorchDispatchMode
+
+from xotorch_support_jetson_amd.download.shard_download import NoopShardDownloader
+from xotorch_support_jetson_amd.inference.shard import Shard
+from xotorch_support_jetson_amd.inference.sharded_engine import ShardedInferenceEngine
+
+pytestmark = pytest.mark.gpu
+
+GEMM_OPS = {"mm", "addmm", "bmm", "baddbmm", "addbmm", "matmul", "linear", "addmv", "mv", "dot", "_scaled_mm",
+            "_addmm_activation", "tensordot", "einsum"}
+
+
+class NoVendorGemm(TorchDispatchMode):
+  """Raises on any aten GEMM / GEMV (hipBLASLt / rocBLAS) issued while active; counts the other ops."""
+
+  def __init__(self):
+    super().__init__()
+    self.seen = []
+
+  def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+    name = func.overloadpacket.__name__
+    if name in GEMM_OPS and any(isinstance(a, torch.Tensor) and a.is_cuda for a in args):
+      raise AssertionError(f"vendor GEMM on the train path: aten.{name}")
+    self.seen.append(name)
+    return func(*args, **(kwargs or {}))
+
+
+def _guard(engine, mode):
+  """Run every engine call inside `mode` on the engine's executor thread."""
+  run = engine._run
+
+  async def guarded(fn, *args):
+    def call():
+      with mode:
+        return fn(*args)
+    return await run(call)
+  engine._run = guarded
+
+
+@pytest.mark.parametrize("model", ["tiny-llama", "tiny-mixtral"])
+def test_xot_train_ragged_no_vendor_gemm(gpu, model, monkeypatch):
+  from xotorch_support_jetson_amd.models.config import PRESETS
+  from xotorch_support_jetson_amd.models.weights import copy_weights_into, random_weights
+  c = PRESETS[model]
+  n = c.num_layers
+  rng = np.random.default_rng(3)
+  # batch size 1 with a ragged length (37 tokens), then 2 sequences padded to 53 with lengths 53 / 29
+  batches = [rng.integers(0, c.vocab_size, size=(1, 37)), rng.integers(0, c.vocab_size, size=(2, 53))]
+  lens = [np.array([37]), np.array([53, 29])]
+  a, b = Shard(model, 0, n // 2 - 1, n), Shard(model, n // 2, n - 1, n)
+
+  for fn in ("matmul", "mm", "addmm", "bmm"):  # the Python entry points too (belt and braces)
+    real = getattr(torch, fn)
+
+    def trap(*args, _real=real, _fn=fn, **kw):
+      if any(isinstance(t, torch.Tensor) and t.is_cuda for t in args):
+        raise AssertionError(f"torch.{_fn} on the train path")
+      return _real(*args, **kw)
+    monkeypatch.setattr(torch, fn, trap)
+
+  async def run(dev):
+    e, e2 = (ShardedInferenceEngine(NoopShardDownloader(), device=torch.device(dev)) for _ in range(2))
+    await e.ensure_shard(a)
+    await e2.ensure_shard(b)
+    for eng, sh in ((e, a), (e2, b)):
+      copy_weights_into(eng.runner.weights, random_weights(c, sh, "cpu", seed=0))
+      eng.lr = 1e-3
+    init = {k: v.float().cpu().clone() for k, v in e2._get_trainer().master.items()}
+    mode = NoVendorGemm()
+    if dev != "cpu":
+      _guard(e, mode)
+      _guard(e2, mode)
+    losses, grads = [], []
+    for x, ln in zip(batches * 2, lens * 2):
+      y = np.roll(x, -1, 1)
+      h = await e.train_forward("t", a, x)
+      loss, g = await e2.train("t", b, h, y, ln)
+      await e.train("t", a, x, g, ln, loss="back_gradient")
+      losses.append(loss)
+      grads.append(torch.as_tensor(g).float().reshape(-1))
+    tr = e2._get_trainer()
+    if dev != "cpu":
+      assert tr.fused_head() and "linear" not in mode.seen and len(mode.seen) > 100
+    delta = {k: tr.master[k].float().cpu() - init[k] for k in tr.master}
+    return losses, grads, delta
+
+  lc, gc, wc = asyncio.run(run("cpu"))
+  lg, gg, wg = asyncio.run(run("cuda:0"))
+  assert np.allclose(lc, lg, rtol=2e-2), (lc, lg)
+  for x, y in zip(gc, gg):  # gradient wrt the stage input (the SendExample reply)
+    cos = torch.nn.functional.cosine_similarity(x, y, dim=0).item()
+    assert cos > 0.99, cos
+  for k in wc:  # four AdamW steps from the same start: the last stage's weight updates agree
+    d = ((wc[k] - wg[k]).abs().mean() / (wc[k].abs().mean() + 1e-12)).item()
+    assert d < 0.25, (k, d)

@@ -33,13 +33,15 @@ def free_port():
     return s.getsockname()[1]
 
 
-async def one(session, url, a, i, max_tokens):
+async def one(session, url, a, i, max_tokens, base=None):
+  """One streaming request: (TTFT, tokens, seconds, [first, last] token times relative to `base`, token times)."""
   words = " ".join(f"w{j % 97}" for j in range(a.prompt_words))
   text = f"{words} (request {i})" if a.shared_prefix else f"request {i}: {words}"
   body = {"model": a.model, "stream": True, "max_tokens": max_tokens, "temperature": a.temperature,
           "messages": [{"role": "user", "content": text}]}
   t0 = time.perf_counter()
-  ttft, n = None, 0
+  base = t0 if base is None else base
+  ttft, n, stamps = None, 0, []
   async with session.post(url, json=body) as r:
     assert r.status == 200, await r.text()
     async for raw in r.content:
@@ -49,9 +51,26 @@ async def one(session, url, a, i, max_tokens):
       d = json.loads(line[6:])
       if d["choices"][0].get("delta", {}).get("content") is not None:
         n += 1
+        now = time.perf_counter()
+        stamps.append(now - base)
         if ttft is None:
-          ttft = time.perf_counter() - t0
-  return ttft or 0.0, n, time.perf_counter() - t0
+          ttft = now - t0
+  return ttft or 0.0, n, time.perf_counter() - t0, stamps
+
+
+def decode_window(res):
+  """Aggregate output tokens/s while EVERY stream is decoding: from the last first token to the first last
+  token (prefill of the later arrivals and the tail of the early finishers excluded) -- the serving
+  counterpart of bench.py's decode-step rate.  None when the window is empty."""
+  starts = [r[3][0] for r in res if r[3]]
+  ends = [r[3][-1] for r in res if r[3]]
+  if not starts:
+    return None
+  lo, hi = max(starts), min(ends)
+  if hi <= lo:
+    return None
+  n = sum(1 for r in res for t in r[3] if lo < t <= hi)
+  return {"tok_s": round(n / (hi - lo), 2), "window_s": round(hi - lo, 3), "tokens": n}
 
 
 async def client_warmup(session, url, a):
@@ -73,7 +92,7 @@ async def client_main(a):
     print(json.dumps({"warmup_s": time.perf_counter() - t0}), flush=True)
     await loop.run_in_executor(None, sys.stdin.readline)
     t0 = time.perf_counter()
-    res = await asyncio.gather(*(one(session, a.client, a, i, a.max_tokens) for i in range(a.concurrency)))
+    res = await asyncio.gather(*(one(session, a.client, a, i, a.max_tokens, t0) for i in range(a.concurrency)))
     wall = time.perf_counter() - t0
   print(json.dumps({"results": res, "wall_s": wall}), flush=True)
 
@@ -110,7 +129,7 @@ async def ring_main(a):
       await client_warmup(session, url, a)
       warm = time.perf_counter() - t0
       t0 = time.perf_counter()
-      res = await asyncio.gather(*(one(session, url, a, i, a.max_tokens) for i in range(a.concurrency)))
+      res = await asyncio.gather(*(one(session, url, a, i, a.max_tokens, t0) for i in range(a.concurrency)))
       wall = time.perf_counter() - t0
   finally:
     try:
@@ -127,6 +146,7 @@ async def ring_main(a):
                     "wall_s": round(wall, 2), "warmup_s": round(warm, 1),
                     "ttft_s": {"p50": round(ttfts[len(ttfts) // 2], 3), "max": round(ttfts[-1], 3)},
                     "per_request_tok_s_p50": round(sorted(r[1] / r[2] for r in res)[len(res) // 2], 2),
+                    "decode_window": decode_window(res),
                     "data": "random-init weights, byte tokenizer, synthetic prompts", "dtype": "bf16"}), flush=True)
 
 
@@ -194,7 +214,7 @@ async def main(a):
       if PROF is not None:  # host-side profile of the measured phase only
         PROF.enable()
       t0 = time.perf_counter()
-      res = await asyncio.gather(*(one(session, url, a, i, a.max_tokens) for i in range(a.concurrency)))
+      res = await asyncio.gather(*(one(session, url, a, i, a.max_tokens, t0) for i in range(a.concurrency)))
       wall = time.perf_counter() - t0
       if PROF is not None:
         PROF.disable()
@@ -207,6 +227,7 @@ async def main(a):
          "value": round(toks / wall, 2), "unit": "tokens/s", "wall_s": round(wall, 2), "warmup_s": round(warm, 1),
          "ttft_s": {"p50": round(ttfts[len(ttfts) // 2], 3), "max": round(ttfts[-1], 3)},
          "per_request_tok_s_p50": round(sorted(r[1] / r[2] for r in res)[len(res) // 2], 2),
+         "decode_window": decode_window(res),
          "engine_steps": steps, "mean_requests_per_step": round(reqs / max(steps, 1), 1),
          "ms_per_step": round(wall * 1e3 / max(steps, 1), 2),
          # time inside the engine's step call (host prep + GPU + token copy), vs. ms_per_step of wall time

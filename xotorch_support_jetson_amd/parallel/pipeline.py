@@ -110,9 +110,8 @@ class RingStage:
     cand = idx.long().gather(1, j.clamp(max=KC - 1).unsqueeze(1)).squeeze(1)
     return torch.where(j < KC, cand, j - KC + self.vs).to(torch.int32)
 
-  def _recv_item(self, mb: MicroBatch) -> tuple:
-    """First stage, split head: receive the last stage's hand-off (normed hidden, candidates)."""
-    B = len(mb.rids)
+  def _recv_item(self, B: int) -> tuple:
+    """First stage, split head: receive the last stage's hand-off (normed hidden, candidates) of B rows."""
     dev = self.r.device
     xn = torch.empty(B, self.D, dtype=torch.bfloat16, device=dev)
     vals = torch.empty(B, KC, dtype=torch.float32, device=dev)
@@ -123,7 +122,7 @@ class RingStage:
     return xn, vals, idx
 
   def _recv_and_sample(self, mb: MicroBatch) -> torch.Tensor:
-    return self._finish_head(*self._recv_item(mb), mb.temps)
+    return self._finish_head(*self._recv_item(len(mb.rids)), mb.temps)
 
   # ---------------------------------------------------------------- per-tick device timing (bench diagnostics)
   def start_timing(self) -> None:
@@ -199,7 +198,7 @@ class RingStage:
         x = item_in
         e1 = e0
       elif self.split:
-        got = self._recv_item(mb)
+        got = self._recv_item(B)
         e1 = self._mark()
         x = sampled = self._finish_head(*got, mb.temps)
       else:

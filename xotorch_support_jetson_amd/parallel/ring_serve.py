@@ -14,10 +14,18 @@ host are the ring peers (one process each, `xot --gpus N`) and the data plane is
                  gloo group, i.e. host to host: a follower reads it without touching its GPU stream, so it
                  queues the step's receive + forward while its previous step is still running (a header on
                  the RCCL stream would be readable only after that stream drained).
-  data plane     stage r receives [T, D] bf16 from r-1, runs its layers, sends to r+1; the last stage
-                 samples on device (temperature / top-k 35) and sends the ids [B] int32 back to rank 0
-                 (P2PTransport: one communicator per directed edge).  Rank 0 receives lane steps' ids in
-                 launch order (FIFO per edge).
+  data plane     stage r receives [T, D] bf16 from r-1, runs its layers, sends to r+1 (P2PTransport: one
+                 communicator per directed edge).  The ring ends share the LM head as in bench.py
+                 (pipeline.RingStage, the same hand-off code): the last stage computes vocab rows [0, Vs) and
+                 sends the normed hidden state + its top-k candidates to rank 0, which computes rows [Vs, V)
+                 and samples on device (temperature / top-k 35); without the split the last stage samples and
+                 sends the ids [B] int32.  Rank 0 receives lane steps' hand-offs in launch order (FIFO per edge).
+  async steps    rank 0 never waits for a lane's ids before queueing that lane's next step: the running decoders
+                 of the next step read their input ids straight from the device tensor the previous step
+                 sampled, and the host reads those ids (tokens to emit, EOS) while the next step is already
+                 on the GPU -- at world 1 the single lane keeps one step queued behind the running one.  A
+                 request that turns out to have finished (EOS) had one speculative token computed: it is
+                 discarded and the request's pages are freed as usual.
   prefill        prompts go through in chunks: a lane step carries at most `step_tokens` new tokens
                  (XOT_MAX_STEP_TOKENS), so a long prompt never stalls the other requests of its lane for a
                  whole-prompt forward; only the final chunk's sampled token is kept.
@@ -101,14 +109,19 @@ class _Req:
   out: List[int] = field(default_factory=list)
   key: int = -1  # integer id on the wire (a new one per admission)
   lane: int = -1
-  fed: int = 0  # tokens of ids + out already in the KV cache
+  fed: int = 0  # tokens of ids + out (+ pending samples) fed to the ring (in the KV cache or in a step in flight)
+  pend: int = 0  # sampled tokens of steps in flight, not read on the host yet (0, 1, or 2 briefly)
   order: int = 0  # admission order: the largest is the youngest
   pixels: Optional[torch.Tensor] = None  # LLaVA: preprocessed images of the prompt (rank 0 = first shard)
   feats: Optional[torch.Tensor] = None  # their projected features [image tokens, D] (computed on first use)
 
   def todo(self) -> int:
     """Tokens still to feed before the next sampled token is a real output (1 while decoding)."""
-    return len(self.ids) + len(self.out) - self.fed
+    return len(self.ids) + len(self.out) + self.pend - self.fed
+
+  def on_device(self) -> bool:
+    """Its next token to feed is a sample still on the device (the lane's step in flight drew it)."""
+    return self.pend > 0 and self.fed >= len(self.ids) + len(self.out)
 
 
 class RingServer:
@@ -116,8 +129,9 @@ class RingServer:
                top_k: int = 35, seed: int = 1234, max_batch: Optional[int] = None, step_tokens: Optional[int] = None,
                monitor: Optional[HealthMonitor] = None, make_runner: Optional[Callable] = None,
                pool_pages: Optional[int] = None, ops_cap: int = OPS_CAP, prefix_cache: Optional[bool] = None,
-               lanes_per_rank: Optional[int] = None):
+               lanes_per_rank: Optional[int] = None, split_head: Optional[bool] = None):
     self.r, self.rank, self.world, self.t = runner, rank, world, transport
+    self.want_split = split_head
     # lanes per ring rank (XOT_RING_LANES_PER_RANK): with more than one, rank 0 has another lane's step queued
     # while it turns one lane's ids around on the host (collect, plan, header), at smaller steps per lane
     self.lanes_per_rank = max(1, lanes_per_rank or int(os.environ.get("XOT_RING_LANES_PER_RANK", "1")))
@@ -153,9 +167,9 @@ class RingServer:
     self.prev, self.next = (rank - 1) % world, (rank + 1) % world
     self.D = runner.config.hidden_size
     self.dev = runner.device
-    self.seed_off = torch.tensor([self.seed, 0], dtype=torch.int64, device=runner.device)
+    self._make_stage(runner, rank, world)
     self.lanes = max(1, world) * self.lanes_per_rank
-    self._inflight: List[Optional[list]] = [None] * self.lanes  # per lane: the step's (req, n) awaiting ids
+    self._inflight: List[Optional[dict]] = [None] * self.lanes  # per lane: its step in flight (see _launch)
     # rank 0 plans with the smallest pool of the ring (exact for every rank: same appends everywhere)
     self.pool_pages = min(pool_pages or runner.bm.num_blocks, runner.bm.num_blocks)
     self.hcap = 4 + 3 * self.max_batch + 4 * self.ops_cap
@@ -168,6 +182,28 @@ class RingServer:
       from ..inference.prefix_cache import PrefixCache
       self.pc = PrefixCache(_RecordingBM(runner.bm, self._ops_sink()), int(self.pool_pages * PREFIX_CACHE_FRAC),
                             single_shard=True)
+
+  def _make_stage(self, runner, rank: int, world: int) -> None:
+    """The ring-stage helper shared with bench.py (pipeline.RingStage): sampler + seed, and at world > 1 the LM
+    head split between the ring ends.  Every rank must take the same split decision: the first stage cannot
+    derive its head rows for externally loaded weights without a head, so the flags are reduced (MIN) over the
+    control group and every rank falls back to the unsplit head together."""
+    from .pipeline import RingStage
+    want = (os.environ.get("XOT_SPLIT_HEAD", "1") == "1") if self.want_split is None else self.want_split
+    try:
+      st = RingStage(runner, rank, world, self.t, top_k=self.top_k, seed=self.seed, split_head=want)
+      ok = 1
+    except ValueError:
+      st, ok = None, 0
+    if world > 1 and self.ctl is not None and want:
+      flag = torch.tensor([ok], dtype=torch.int64)
+      dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.ctl)
+      ok = int(flag[0])
+    if st is None or (st.split and not ok):
+      runner.model.head_rows = None
+      st = RingStage(runner, rank, world, self.t, top_k=self.top_k, seed=self.seed, split_head=False)
+    self.ring = st
+    self.seed_off = st.seed_off
 
   def _ops_sink(self) -> list:
     if not hasattr(self, "_ops"):
@@ -264,15 +300,21 @@ class RingServer:
     return h
 
   # ------------------------------------------------------------------ one lane step on this rank
-  def _stage(self, items, x0: Optional[torch.Tensor], image_embeds: Optional[torch.Tensor] = None
-             ) -> Optional[torch.Tensor]:
-    """Run this rank's layers for a lane step; the last rank returns the sampled ids [B] int32 (device)."""
+  def _stage(self, items, x0: Optional[torch.Tensor], image_embeds: Optional[torch.Tensor] = None,
+             gather=None, temps: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+    """Run this rank's layers for a lane step.  Rank 0's input ids are x0 (host) with the rows `gather` =
+    (rows in x, device ids of the previous step, rows there) filled on the device.  The last rank samples (or,
+    with the split head, sends its head share to rank 0); returns the sampled ids [B] int32 (device) where
+    they are drawn on this rank, else None."""
     rids = [str(k) for k, _, _ in items]
     qlens = [q for _, q, _ in items]
     if self.first:
       if self.dev.type == "cuda":  # pinned + async: a pageable copy would wait for everything queued before it
         x0 = x0.pin_memory()
       x = x0.to(self.dev, non_blocking=True)
+      if gather is not None:
+        at, prev, rows = gather
+        x.index_copy_(0, at, prev.index_select(0, rows))
     else:
       x = torch.empty(sum(qlens), self.D, dtype=torch.bfloat16, device=self.dev)
       self.t.wait(self.t.irecv(x, self.prev))
@@ -281,15 +323,35 @@ class RingServer:
     if not self.last:
       self.t.isend(y.clone(), self.next)  # y may be a decode graph's static buffer
       return None
-    temps = torch.tensor([t for _, _, t in items], dtype=torch.float32)
-    if self.dev.type == "cuda":  # pinned + async: a pageable copy would wait here for the forward to finish
-      temps = temps.pin_memory()
-    temps = temps.to(self.dev, non_blocking=True)
-    tok = K.sample(y, temps, self.top_k, self.seed_off)
-    self.seed_off[1] += 1
+    if self.ring.split:  # the last stage's share of the head + its top-k candidates -> rank 0
+      self.ring._send_item(self.ring._head_part(y))
+      return None
+    if temps is None:
+      temps = self._temps(items)
+    tok = self.ring._sample(y, temps)
     if self.world > 1:
       self.t.isend(tok, 0)
     return tok
+
+  def _temps(self, items) -> torch.Tensor:
+    temps = torch.tensor([t for _, _, t in items], dtype=torch.float32)
+    if self.dev.type == "cuda":  # pinned + async: a pageable copy would wait here for the queued work
+      temps = temps.pin_memory()
+    return temps.to(self.dev, non_blocking=True)
+
+  def _resolve(self, step: dict) -> torch.Tensor:
+    """Rank 0: the device ids of its oldest step in flight.  At world 1 they were sampled by _stage; otherwise
+    the last stage's hand-off is received (a stream dependency, no host wait) and, with the split head, the
+    remaining head rows + the sampler run here.  Called in launch order (the hand-offs arrive FIFO)."""
+    if step["tok"] is None:
+      B = len(step["plan"])
+      if self.ring.split:
+        step["tok"] = self.ring._finish_head(*self.ring._recv_item(B), step["temps"])
+      else:
+        tok = torch.empty(B, dtype=torch.int32, device=self.dev)
+        self.t.wait(self.t.irecv(tok, self.world - 1))
+        step["tok"] = tok
+    return step["tok"]
 
   def _apply_ops(self, ops) -> None:
     """Followers: repeat rank 0's KV operations on this rank's pool (same order, same point in the steps)."""
@@ -352,14 +414,20 @@ class RingServer:
   def _preempt(self, q: _Req) -> None:
     self._release(q)
     del self._running[q.rid]
-    q.lane, q.fed = -1, 0
+    q.lane, q.fed, q.pend = -1, 0, 0  # a sample still in flight is dropped (re-prefill resumes from q.out)
     self._waiting.appendleft(q)
     self.stats["preempted"] += 1
 
+  def _finishes(self, q: _Req) -> bool:
+    """Known to finish once its pending samples are read (token budget or context), whatever they are."""
+    return q.pend > 0 and (len(q.out) + q.pend >= q.max_tokens or len(q.ids) + len(q.out) + q.pend + 1 > self.r.max_ctx)
+
   def _plan(self, lane: int):
     """(req, new tokens) of this lane's next step: decoders first, then prompt chunks in admission order
-    within the step's token budget; the youngest are preempted while the step's pages do not fit."""
-    reqs = sorted((q for q in self._running.values() if q.lane == lane), key=lambda q: (q.todo() > 1, q.order))
+    within the step's token budget; the youngest are preempted while the step's pages do not fit.  Requests
+    certain to finish with the samples in flight get no further step."""
+    reqs = sorted((q for q in self._running.values() if q.lane == lane and not self._finishes(q)),
+                  key=lambda q: (q.todo() > 1, q.order))
     if self.pc is not None:  # new prompts: fork the longest cached prefix (whole pages) and feed only the rest
       for q in reqs:
         if q.fed == 0 and q.pixels is None and q.todo() > 1 and not self.r.has(str(q.key)):
@@ -386,25 +454,17 @@ class RingServer:
       reqs.remove(victim)
       self._preempt(victim)
 
-  def _collect(self, lane: int) -> None:
-    """Rank 0: the ids of this lane's step in flight (the oldest step in flight: lanes run in a cycle)."""
-    step = self._inflight[lane]
-    if step is None:
-      return
-    self._inflight[lane] = None
-    plan, tok = step
-    if tok is None:  # sampled on another rank
-      tok = torch.empty(len(plan), dtype=torch.int32, device=self.dev)
-      self.t.wait(self.t.irecv(tok, self.world - 1))
-    toks = tok.tolist()
+  def _collect(self, step: dict) -> None:
+    """Rank 0: read a step's ids on the host (the next step of its lane is already queued behind it) and emit
+    the real outputs; finished requests are released (a speculative token of theirs in the next step is
+    ignored when that step is collected: the request is gone or re-admitted under another key)."""
+    toks = self._resolve(step).tolist()
     if self.monitor is not None:
       self.monitor.check()  # an aborted transfer delivers garbage: never emit it
-    for (q, n), t in zip(plan, toks):
-      q.fed += n
-      if q.rid not in self._running or self._running[q.rid] is not q:
+    for (q, n, real, key), t in zip(step["plan"], toks):
+      if not real or self._running.get(q.rid) is not q or q.key != key:
         continue
-      if q.todo() > 0:  # a prompt chunk that was not the last one: its sample is not an output
-        continue
+      q.pend -= 1
       q.out.append(int(t))
       fin = (t in self.eos or len(q.out) >= q.max_tokens or len(q.ids) + len(q.out) + 1 > self.r.max_ctx)
       self._emit(q.rid, [int(t)], fin)
@@ -412,35 +472,58 @@ class RingServer:
         del self._running[q.rid]
         self._release(q)
 
-  def _launch(self, lane: int, stop: bool = False) -> bool:
-    """Rank 0: start this lane's next step.  Returns whether anything was sent."""
+  def _launch(self, lane: int, prev: Optional[dict] = None, stop: bool = False) -> Optional[dict]:
+    """Rank 0: start this lane's next step.  `prev` is the lane's step still in flight: decoders whose next
+    input is a sample of it read that id from its device tensor.  Returns the step (None if nothing ran):
+    {plan: [(req, n, real, key)], tok: device ids or None until _resolve, temps}."""
     plan = self._plan(lane) if not stop else []
     if not plan and not (stop or (self._ops and self.world > 1 and self._idle_lanes())):
-      return False
-    items, ids, embeds = [], [], []
+      return None
+    items, ids, embeds, steps = [], [], [], []
+    at, rows = [], []
     for q, n in plan:
       items.append((q.key, n, q.temp))
-      seq = q.ids + q.out
-      ids += seq[q.fed:q.fed + n]
+      real = q.todo() == n  # this chunk completes what is known: its sample is the next output
+      if q.on_device():
+        assert n == 1 and prev is not None, "a pending sample without its step"
+        at.append(len(ids))
+        rows.append(prev["row"][q.key])
+        ids.append(0)
+      else:
+        seq = q.ids + q.out
+        ids += seq[q.fed:q.fed + n]
       if n > 1:
         self.stats["chunks"] += 1
       if q.pixels is not None:
-        e = self._image_rows(q, seq, n)
+        e = self._image_rows(q, q.ids + q.out, n)
         if e is not None:
           embeds.append(e)
       elif self.pc is not None and n == 1 and q.todo() == 1:
         self.pc.on_decode(str(q.key))  # its first decode step: keep the prompt's pages as a cached prefix
+      steps.append((q, n, real, q.key))
     # Rank 0 has already applied these operations (frees, prefix forks) and planned this step on top of
     # them: every one must reach the other ranks AHEAD of the step (headers arrive in order), so operations
     # beyond one header's cap go first in op-only headers.
     ops = self._flush_ops()
     if self.world > 1:
       self._send_header(self._header(items, ops, stop))
-    if items:
-      tok = self._stage(items, torch.tensor(ids, dtype=torch.int32), torch.cat(embeds) if embeds else None)
-      self._inflight[lane] = (plan, tok)
-      self.stats["steps"] += 1
-    return True
+    if not items:
+      return None
+    gather = None
+    if at:
+      pin = self.dev.type == "cuda"
+      mk = (lambda v: torch.tensor(v, dtype=torch.int64).pin_memory().to(self.dev, non_blocking=True)) if pin else \
+          (lambda v: torch.tensor(v, dtype=torch.int64))
+      gather = (mk(at), self._resolve(prev), mk(rows))
+    temps = self._temps(items)
+    tok = self._stage(items, torch.tensor(ids, dtype=torch.int32), torch.cat(embeds) if embeds else None,
+                      gather=gather, temps=temps)
+    for q, n, real, _ in steps:
+      q.fed += n
+      if real:
+        q.pend += 1
+    self.stats["steps"] += 1
+    return {"plan": steps, "tok": tok, "temps": temps, "row": {key: i for i, (_, _, _, key) in enumerate(steps)}}
 
   def _image_rows(self, q: _Req, seq: List[int], n: int) -> Optional[torch.Tensor]:
     """Rank 0 (first shard): the projected image features of the image tokens in this step's chunk
@@ -489,17 +572,25 @@ class RingServer:
         self._recover(m.dead)
 
   def _lead(self, idle_wait: float) -> None:
+    """Per lane: the step in flight gets its device ids (_resolve), the lane's next step is launched on top of
+    them, and only then are the previous step's ids read on the host (_collect) -- so the GPU always has the
+    lane's next step queued while the host emits tokens, plans and builds headers."""
     lane = 0
     while True:
-      self._collect(lane)
-      if self._stop:
-        if all(s is None for s in self._inflight):
-          break
-        lane = (lane + 1) % self.lanes
-        continue
-      self._admit()
-      launched = self._launch(lane)
-      if not launched and self.idle() and all(s is None for s in self._inflight):
+      prev = self._inflight[lane]
+      self._inflight[lane] = None
+      nxt = None
+      if not self._stop:
+        if prev is not None:
+          self._resolve(prev)
+        self._admit()
+        nxt = self._launch(lane, prev)
+      if prev is not None:
+        self._collect(prev)
+      self._inflight[lane] = nxt
+      if self._stop and all(s is None for s in self._inflight):
+        break
+      if nxt is None and prev is None and self.idle() and all(s is None for s in self._inflight):
         self._wake.wait(idle_wait)
         self._wake.clear()
       lane = (lane + 1) % self.lanes
@@ -569,7 +660,7 @@ class RingServer:
     self._gather_peers()
     if self.rank == 0:
       for q in sorted(self._running.values(), key=lambda q: q.order, reverse=True):
-        q.lane, q.fed, q.feats = -1, 0, None
+        q.lane, q.fed, q.pend, q.feats = -1, 0, 0, None
         self._waiting.appendleft(q)  # oldest ends up first
       self._running.clear()
       self._ops.clear()  # the new shards start from empty pools (and a fresh prefix cache)
@@ -681,6 +772,21 @@ def min_pool_pages(runner, world: int, ctl=None) -> int:
   return int(n[0])
 
 
+def default_max_batch(cfg, world: int, avg_ctx: int = 512) -> int:
+  """Running requests of the whole ring when XOT_MAX_BATCH is not set: as many as one rank's KV pool holds at
+  `avg_ctx` tokens each (paged KV: requests grow on demand, preemption handles the rest), between 64 and 512
+  per lane (512 = the batch where the decode GEMMs reach their tiles' rate, as in bench.py)."""
+  if not torch.cuda.is_available():
+    return 64
+  from ..models.transformer import KVCache
+  layers = -(-cfg.num_layers // world)
+  total = torch.cuda.get_device_properties(torch.cuda.current_device()).total_memory
+  weights = 2 * (sum(cfg.params_per_layer(i) for i in range(layers)) + 2 * cfg.vocab_size * cfg.hidden_size)
+  per_tok = KVCache.bytes_per_page(cfg, layers) / 64
+  pool_tokens = max(0.0, (total - weights - (4 << 30)) * 0.85) / per_tok
+  return int(min(512 * world, max(64, pool_tokens // avg_ctx)))
+
+
 def _serve_worker(rank: int, world: int, port: int, a: dict) -> None:
   import asyncio
   os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
@@ -699,6 +805,8 @@ def _serve_worker(rank: int, world: int, port: int, a: dict) -> None:
   model = a["model"]
   mdir = _model_dir(model)
   cfg = load_config(mdir) if mdir is not None else preset(model)
+  if not a.get("max_batch"):
+    a = dict(a, max_batch=default_max_batch(cfg, world))
 
   def make_runner(r, w, group):
     shard = ring_shards(model, cfg.num_layers, w, group)[r]
@@ -785,7 +893,7 @@ def serve_ring(args) -> int:
   from ..train.ring_train import _free_port
   n = args.gpus or max(1, torch.cuda.device_count())
   model = getattr(args, "model_name", None) or getattr(args, "run_model", None) or args.default_model
-  a = {"model": model, "max_batch": int(os.environ.get("XOT_MAX_BATCH", 64)),
+  a = {"model": model, "max_batch": int(os.environ.get("XOT_MAX_BATCH", 0)),  # 0: sized from HBM per rank
        "max_ctx": int(os.environ.get("XOT_MAX_CTX", 8192 if torch.cuda.is_available() else 2048)),
        "default_temp": args.default_temp, "max_generate_tokens": args.max_generate_tokens,
        "api_port": args.chatgpt_api_port, "response_timeout": args.chatgpt_api_response_timeout,

@@ -331,9 +331,31 @@ class TrainWeight:
       relayout(self.w.detach(), 1, self.wts)
 
 
-def _own_dw_ok(x: torch.Tensor, dy: torch.Tensor) -> bool:
-  """dW = dY^T X on the tiles: dY^T [N, T] row-major and shuffle(X^T) [K, T] need T % 128, N and K % 64."""
-  return x.shape[0] % 128 == 0 and dy.shape[1] % 64 == 0 and x.shape[1] % 64 == 0
+def pad_rows(t: torch.Tensor, mult: int = 128, value=0) -> torch.Tensor:
+  """t with its rows (dim 0) padded to a multiple of `mult` (`value` rows), or t itself when aligned.  Zero rows
+  are exact for the weight-gradient GEMMs: a zero dY (or dlogits) row adds nothing to dW = dY^T X."""
+  T = t.shape[0]
+  Tp = -(-T // mult) * mult
+  if Tp == T:
+    return t
+  out = torch.full((Tp,) + tuple(t.shape[1:]), value, dtype=t.dtype, device=t.device) if value else \
+      torch.zeros((Tp,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+  out[:T] = t
+  return out
+
+
+def own_dw(dy: torch.Tensor, x: torch.Tensor, acc: "GradAcc") -> None:
+  """acc.buf (+)= dY^T X on the own tiles: dY^T [N, T] row-major and shuffle(X^T) [K, T] need T % 128, so ragged
+  token counts (the reference's batch-size-1 JSONL lengths) are zero-padded to 128 rows first."""
+  from ..ops.linear import linear
+  dy, x = pad_rows(dy), pad_rows(x)
+  dyt = relayout(dy, 2)  # [N, T]
+  xts = relayout(x, 1)   # shuffle(X^T) [K, T]
+  if acc.fresh:
+    linear(dyt, xts, out=acc.buf)
+    acc.fresh = False
+  else:
+    linear(dyt, xts, residual=acc.buf, epi="resid", out=acc.buf)
 
 
 class OwnLinearFn(torch.autograd.Function):
@@ -364,20 +386,7 @@ class OwnLinearFn(torch.autograd.Function):
     tw, acc = ctx.tw, ctx.acc
     dy = dy.contiguous()
     dx = linear(dy, tw.wts)
-    if _own_dw_ok(x, dy):
-      dyt = relayout(dy, 2)  # [N, T]
-      xts = relayout(x, 1)   # shuffle(X^T) [K, T]
-      if acc.fresh:
-        linear(dyt, xts, out=acc.buf)
-        acc.fresh = False
-      else:
-        linear(dyt, xts, residual=acc.buf, epi="resid", out=acc.buf)
-    else:
-      if acc.fresh:
-        torch.mm(dy.t(), x, out=acc.buf)
-        acc.fresh = False
-      else:
-        acc.buf.addmm_(dy.t(), x)
+    own_dw(dy, x, acc)
     if acc.cb is not None:
       acc.cb()
     return dx, None, None, (dy if ctx.has_h else None), None
@@ -465,6 +474,49 @@ def grouped_experts(xs, poff, max_rows, sgu, sdown, agu, adown):
   return GroupedExpertsFn.apply(xs, poff, max_rows, sgu, sdown, agu, adown)
 
 
+class RouterFn(torch.autograd.Function):
+  """MoE router scores in fp32, logits [T, E] = x . W^T, on the kernel library: forward the router_logits
+  kernel (fp32 accumulation of bf16 inputs, as the serving path), backward two own GEMMs on the tiles with the
+  gradient rounded to bf16 -- dX = dL . W through K = E zero-padded to 128 (shuffle(W^T) rebuilt per call:
+  E x D is small), and dW = dL^T . X through the ragged-T padding of own_dw."""
+
+  @staticmethod
+  def forward(ctx, x, w):
+    T, E = x.shape[0], w.shape[0]
+    out = torch.empty(T, E, dtype=torch.float32, device=x.device)
+    require().router_logits(x, w, out)
+    ctx.save_for_backward(x, w)
+    return out
+
+  @staticmethod
+  def backward(ctx, dl):
+    from ..ops.linear import linear
+    x, w = ctx.saved_tensors
+    E, D = w.shape
+    Ep = -(-E // 128) * 128
+    dlb = dl.to(torch.bfloat16)
+    a = torch.zeros(dlb.shape[0], Ep, dtype=torch.bfloat16, device=x.device)
+    a[:, :E] = dlb
+    wp = torch.zeros(Ep, D, dtype=torch.bfloat16, device=x.device)
+    wp[:E] = w
+    dx = linear(a, relayout(wp, 1))  # [T, D] = dL . W
+    dw = linear(relayout(pad_rows(dlb), 2), relayout(pad_rows(x), 1))  # [E, D] = dL^T . X
+    return dx, dw.to(w.dtype)
+
+
+def router_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
+  E, D = w.shape
+  return x.is_cuda and x.dtype == w.dtype == torch.bfloat16 and D % 128 == 0 and \
+      (E in (4, 8, 16) or (E in (32, 64, 128, 160, 256) and D % 512 == 0))  # launch_router_logits' cases
+
+
+def router_logits(x, w):
+  """fp32 router logits [T, E] with autograd to x and w (RouterFn on the GPU, fp32 torch on the CPU)."""
+  if router_ok(x, w):
+    return RouterFn.apply(x.contiguous(), w)
+  return x.float() @ w.float().t()
+
+
 class LmHeadCEFn(torch.autograd.Function):
   """sum_t w_t CE(xn_t . head^T, y_t) without materialising [T, V] logits: row chunks of `chunk`
   tokens; per chunk the fp32 logits come from the own GEMM, ce_fwd / ce_bwd give the loss and dlogits (bf16),
@@ -475,6 +527,11 @@ class LmHeadCEFn(torch.autograd.Function):
   @staticmethod
   def forward(ctx, xn, head, tw, targets, weights, chunk):
     from ..ops.linear import linear
+    T0 = xn.shape[0]
+    # ragged token counts: zero rows with ignored targets (their dlogits rows are zero) up to a multiple of 128,
+    # so every chunk's dHead GEMM runs on the tiles
+    assert chunk % 128 == 0, chunk
+    xn, targets, weights = pad_rows(xn), pad_rows(targets, value=-1), pad_rows(weights)
     T, D = xn.shape
     C = require()
     dxn = torch.empty_like(xn)
@@ -494,18 +551,12 @@ class LmHeadCEFn(torch.autograd.Function):
       C.ce_bwd(logits, tc, lse, wc, dl)
       del logits
       linear(dl, tw.wts, out=dxn[r0:r1])
-      if (r1 - r0) % 128 == 0:
-        dlt, xts = relayout(dl, 2), relayout(xc, 1)  # dlogits^T [V, c], shuffle(X_c^T) [D, c]
-        if i == 0:
-          linear(dlt, xts, out=dhead)
-        else:
-          linear(dlt, xts, residual=dhead, epi="resid", out=dhead)
-      else:  # a ragged last chunk
-        if i == 0:
-          torch.mm(dl.t(), xc, out=dhead)
-        else:
-          dhead.addmm_(dl.t(), xc)
-    ctx.save_for_backward(dxn, dhead)
+      dlt, xts = relayout(dl, 2), relayout(xc, 1)  # dlogits^T [V, c], shuffle(X_c^T) [D, c]
+      if i == 0:
+        linear(dlt, xts, out=dhead)
+      else:
+        linear(dlt, xts, residual=dhead, epi="resid", out=dhead)
+    ctx.save_for_backward(dxn[:T0], dhead)
     return total
 
   @staticmethod

@@ -10,8 +10,10 @@ no activations are kept between the hops.
 
 Numerics: bf16 working weights (leaf tensors with grads), fp32 master weights + fp32 AdamW moments
 updated by the fused HIP AdamW kernel, which also refreshes the bf16 copy.  RMSNorm, SiLU*mul, RoPE,
-the causal GQA attention (flash-style fwd / dQ / dK-dV kernels) and the cross-entropy run on the kernel
-library's forward/backward kernels; GEMMs on hipBLASLt.  Updated weights are written back into the inference shard lazily
+the causal GQA attention (flash-style fwd / dQ / dK-dV kernels), the projections (OwnLinearFn: forward, dX and
+dW on the MFMA tiles, ragged token counts zero-padded to 128 rows) and the LM head + cross-entropy (LmHeadCEFn,
+chunked, no [T, V] logits) run on the kernel library; torch GEMMs remain only on the CPU and for shapes the
+tiles do not cover.  Updated weights are written back into the inference shard lazily
 (`sync_to_inference`) so `xot run` after `xot train` uses the trained model.
 """
 from __future__ import annotations
@@ -231,7 +233,7 @@ class ShardTrainer:
     routed to it, weighted fp32 scatter-add, plus DeepSeek's shared experts.  Same routing as the
     inference path (models/transformer.py `_moe`)."""
     c, P = self.c, self.params
-    logits = xn.float() @ P[f"{i}.router"].float().t()  # [T, E]
+    logits = A.router_logits(xn, P[f"{i}.router"])  # [T, E] fp32
     topw, topi = self._route(logits, i)
     sgu, sdown = self.tw.get(f"{i}.egu"), self.tw.get(f"{i}.edown")
     if sgu is not None and sdown is not None and f"{i}.egu" in self.acc and f"{i}.edown" in self.acc:
@@ -405,8 +407,16 @@ class ShardTrainer:
           return float(l)
         return 0.0
     self.zero_grad()
-    out = self.forward(x)
-    if self.shard.is_last_layer() and loss != "back_gradient":
+    head_loss = self.shard.is_last_layer() and loss != "back_gradient"
+    fused = head_loss and self.fused_head()
+    out = self.forward(x, logits=not fused)
+    if fused:  # the LM head + CE on own GEMMs, chunked: no [T, V] logits (A.LmHeadCEFn)
+      L = out.shape[1]
+      denom = float(max(int(self._to(length, torch.int64).clamp(max=L).sum()), 1))
+      lval = self.head_loss(out, target, length, denom)
+      lval.backward()
+      loss_out = float(lval.detach())
+    elif head_loss:
       lval, _ = self.loss_of(out, target, length)
       lval.backward()
       loss_out = float(lval.detach())
