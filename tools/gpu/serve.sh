@@ -1,6 +1,6 @@
 #!/bin/bash
 # Serving through the HTTP API (Llama-3-8B): streams 1 / 64 / 256, shared-prefix cache on / off, and the
-# RCCL ring server rehearsed on one GPU (2 ranks over gloo).   bash tools/gpu/serve.sh [api|prefix|ring|ringload|ringload2|lanes]...
+# RCCL ring server rehearsed on one GPU (2 ranks over gloo).   bash tools/gpu/serve.sh [api|prefix|ring|ringload|ringload2|lanes|ring70]...
 source "$(dirname "$0")/common.sh"
 for what in ${@:-api}; do
   case $what in
@@ -15,5 +15,8 @@ for what in ${@:-api}; do
             XOT_MAX_BATCH=64 XOT_DIST_BACKEND=gloo step serve/ring2_prefix 600 python -u tools/bench_serve.py --ring 2 --model llama-3-8b --concurrency 64 --max-tokens 128 --prompt-words 400 --shared-prefix ;;
     lanes)  # two lanes per rank vs one (rank 0 turns one lane's ids around while another lane's step is queued)
             for l in 1 2; do for c in 64 256; do XOT_RING_LANES_PER_RANK=$l XOT_MAX_BATCH=$c XOT_DIST_BACKEND=gloo step serve/ring2_c${c}_lanes$l 600 python -u tools/bench_serve.py --ring 2 --model llama-3-8b --concurrency $c --max-tokens 256 --prompt-words 16; done; done ;;
+    ring70) # `xot --gpus 1` (RingServer: async lane steps) at the headline operating point: Llama-3-70B, 512 streams,
+            # ~512-token prompts, 128 tokens each; compare decode_window.tok_s with bench.py
+            step serve/ring1_70b_c512 1000 python -u tools/bench_serve.py --ring 1 --model llama-3-70b --concurrency 512 --max-tokens 128 --prompt-words 124 ;;
   esac
 done

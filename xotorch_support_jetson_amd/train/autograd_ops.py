@@ -477,8 +477,8 @@ def grouped_experts(xs, poff, max_rows, sgu, sdown, agu, adown):
 class RouterFn(torch.autograd.Function):
   """MoE router scores in fp32, logits [T, E] = x . W^T, on the kernel library: forward the router_logits
   kernel (fp32 accumulation of bf16 inputs, as the serving path), backward two own GEMMs on the tiles with the
-  gradient rounded to bf16 -- dX = dL . W through K = E zero-padded to 128 (shuffle(W^T) rebuilt per call:
-  E x D is small), and dW = dL^T . X through the ragged-T padding of own_dw."""
+  gradient rounded to bf16 and E zero-padded to 128 (E x D is small): dX = dL . W (shuffle(W^T) rebuilt per
+  call) and dW = dL^T . X (T zero-padded to 128 rows as in own_dw)."""
 
   @staticmethod
   def forward(ctx, x, w):
@@ -500,7 +500,7 @@ class RouterFn(torch.autograd.Function):
     wp = torch.zeros(Ep, D, dtype=torch.bfloat16, device=x.device)
     wp[:E] = w
     dx = linear(a, relayout(wp, 1))  # [T, D] = dL . W
-    dw = linear(relayout(pad_rows(dlb), 2), relayout(pad_rows(x), 1))  # [E, D] = dL^T . X
+    dw = linear(relayout(pad_rows(a), 2), relayout(pad_rows(x), 1))[:E]  # [E, D] = dL^T . X (Ep rows, E kept)
     return dx, dw.to(w.dtype)
 
 
