@@ -571,6 +571,57 @@ def test_gemm_big_column_tail(gpu, N, epi, bn, splits):
   assert bool((buf[:, Ny:] == 7.0).all())
 
 
+@pytest.mark.parametrize("M", [256, 300, 1024, 2100])
+@pytest.mark.parametrize("epi,f32,splits", [("none", False, 1), ("none", True, 1), ("resid", False, 1),
+                                            ("silu", False, 1), ("none", True, 3), ("silu", False, 2),
+                                            ("resid", False, 4)])
+def test_gemm_w4(gpu, M, epi, f32, splits):
+  """Four-wave 256 x 256 tile (tile code 4256, csrc/gemm_w4.hip: swapped MFMA operands, permuted weight-row reads
+  for 16-B stores, branch-free k loop) vs the fp32 reference: masked row tiles, every epilogue with a bias, fp32
+  out, uneven split-K ranges (slabs reduced by the split-K reduce kernel)."""
+  from xotorch_support_jetson_amd.ops._ext import require
+  from xotorch_support_jetson_amd.ops.weights_layout import shuffle_for_stream
+  torch.manual_seed(M + splits)
+  N, Kd = 1024, 1280
+  x = torch.randn(M, Kd, device=gpu, dtype=torch.bfloat16)
+  w = torch.randn(N, Kd, device=gpu, dtype=torch.bfloat16) / math.sqrt(Kd)
+  b = torch.randn(N, device=gpu, dtype=torch.bfloat16)
+  r = torch.randn(M, N, device=gpu, dtype=torch.bfloat16)
+  ws = torch.empty(splits * M * N, device=gpu, dtype=torch.float32)
+  full = R.linear(x, w, b)
+  if epi == "silu":
+    f = full.view(M, N // 32, 2, 16)
+    ref = (torch.nn.functional.silu(f[:, :, 0]) * f[:, :, 1]).reshape(M, N // 2)
+    y = torch.empty(M, N // 2, device=gpu, dtype=torch.float32 if f32 else torch.bfloat16)
+  elif epi == "resid":
+    ref = full + r.float()
+    y = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+  else:
+    ref = full
+    y = torch.empty(M, N, device=gpu, dtype=torch.float32 if f32 else torch.bfloat16)
+  require().gemm_big(x, shuffle_for_stream(w), y, b, r if epi == "resid" else None, ws, K.EPI[epi], 4256, splits)
+  assert rel_err(y, ref) < 1e-2
+
+
+def test_gemm_w4_exact_layout(gpu):
+  """Integer-valued operands: the four-wave tile matches bit for bit (fragment maps, the permuted weight rows and
+  the XOR-4 weight image swizzle, the token-row swizzle, the shuffled k order), and in place with the residual."""
+  from xotorch_support_jetson_amd.ops._ext import require
+  from xotorch_support_jetson_amd.ops.weights_layout import shuffle_for_stream
+  g = torch.Generator(device="cpu").manual_seed(6)
+  M, N, Kd = 700, 768, 512
+  x = torch.randint(-3, 4, (M, Kd), generator=g).to(torch.bfloat16).to(gpu)
+  w = torch.randint(-3, 4, (N, Kd), generator=g).to(torch.bfloat16).to(gpu)
+  ref = x.float() @ w.float().t()
+  y = torch.zeros(M, N, device=gpu, dtype=torch.float32)
+  require().gemm_big(x, shuffle_for_stream(w), y, None, None, None, 0, 4256, 1)
+  assert torch.equal(y, ref)
+  h = torch.randint(-3, 4, (M, N), generator=g).to(torch.bfloat16).to(gpu)
+  want = (h.float() + ref).to(torch.bfloat16)
+  require().gemm_big(x, shuffle_for_stream(w), h, None, h, None, 1, 4256, 1)
+  assert torch.equal(h, want)
+
+
 def test_gemm_big_exact_layout(gpu):
   """Integer-valued operands (exact in bf16 and fp32): every output element must match bit for bit,
   which pins the fragment maps, the LDS swizzle and the shuffled-layout k order."""

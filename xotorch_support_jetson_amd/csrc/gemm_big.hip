@@ -543,6 +543,16 @@ static int big_dispatch(const uint16_t* X, int ldx, const uint16_t* W, const uin
   // 10000 x BM for row tiles below 256 (160 / 192 / 224: M = 320 / 384 / 448 in two tiles without padding rows;
   // 2256 only with 192)
   const int bm = bn / 10000 ? bn / 10000 : 256, code = bn % 10000;
+  if (code == 4256 && bm == 256) {  // four-wave 256 x 256 tile (gemm_w4.hip)
+    const int rc = launch_gemm_w4(X, ldx, W, bias, R, ldr, Y, ldy, F32, EPI, ws, M, N, K, S, big_group_m(), st);
+    if (rc != 0 || S == 1 || !reduce) return rc;
+    const int ncol = EPI == EPI_SILU ? N / 2 : N;
+    const long chunks = (long)M * (ncol / 8);
+    int blocks = (int)((chunks + 255) / 256);
+    if (blocks > 2048) blocks = 2048;
+    splitk_reduce_kernel<EPI, F32><<<blocks, 256, 0, st>>>(ws, S, M, N, bias, R, ldr, Y, ldy);
+    return 0;
+  }
 #define XOT_BIG(BM_, BN_, WM_, NBUF_, ...)                                                                        \
   big_launch<BM_, BN_, WM_, 8 / WM_, 64, NBUF_, EPI, F32, ##__VA_ARGS__>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, \
                                                                          S, reduce, st)

@@ -1,0 +1,361 @@
+// Four-wave 256 x 256 x 64 GEMM on the pre-shuffled weight layout (tile code 4256):  Y[M,N] = X[M,K] . W[N,K]^T
+//
+// The large-M shapes of prefill and training (M >= 1024: a dozen k stages or more per tile) run gemm_big's
+// eight-wave ping-pong at ~1.55 us per 64-deep k step and 18 us of fixed cost per tile; hipBLASLt's
+// MT256x256x64 kernel takes ~1.33 us and 11 us (profiles/r5/gemm_overhead/).  This kernel follows the
+// schedule that gets there (one wave per SIMD, everything of a stage in registers early):
+//   * 4 waves, each 128 x 128 of the tile: 64 accumulator tiles (256 AGPRs) and ALL 32 fragments of a
+//     64-deep stage in registers (128 VGPRs) -- 0.25 fragment reads per MFMA instead of 0.375
+//   * two LDS stage buffers (2 x 64 KB, LDS-DMA, 16 1-KB instructions per wave and stage); a stage's buffer is
+//     free as soon as every wave holds its fragments, so stage t+2 is issued a quarter into stage t and has
+//     ~1.6 stages of latency budget (the ping-pong tile's refill has ~1)
+//   * per stage: half 0's 64 MFMAs with half 1's 16 fragment reads under the first 16; lgkmcnt(0) + barrier;
+//     16 LDS-DMA issues spread over the next 80 MFMAs; vmcnt + barrier (stage t+1 landed); stage t+1's half-0
+//     fragments read under the last 20 MFMAs of half 1 -- two barriers per 128 MFMAs
+// Operand roles are swapped against gemm_big: the MFMA A operand is the weight fragment (16 output columns x 32 k),
+// B the activation fragment (32 k x 16 tokens), so a lane's accumulator holds 4 consecutive output COLUMNS of one
+// token.  With PERM (every epilogue but SiLU) the weight rows of each pair of 16-column tiles are read permuted
+// (tile 2J row m = column 32 J + 8 (m >> 2) + (m & 3) + 4 (j & 1)), so a lane ends with 8 consecutive columns and
+// the epilogue stores 16 B per instruction (gemm_big: 2 B); the weight LDS image is swizzled through the DMA
+// source addresses (rows XOR 4 in odd k quarters) so those permuted reads stay bank-conflict free.  SiLU keeps the
+// natural rows: gate tile 2J and up tile 2J + 1 meet in one lane (8-B stores).
+// Reference parity: the projections of xotorch/inference/torch/models/general_mha.py:77-120 / llm_utils.py:513-522.
+#include "common.h"
+#include "gemm_common.h"
+#include "kernels.h"
+
+#include <type_traits>
+
+namespace xot {
+
+namespace w4 {
+constexpr int BM = 256, BN = 256, BK = 64;
+constexpr int A_EL = BM * BK, STAGE = (BM + BN) * BK;  // bf16 elements per stage buffer (64 KB)
+constexpr int SMEM = 2 * STAGE * 2;                     // two stage buffers, 128 KB
+}  // namespace w4
+
+template <int EPI, bool OUT_F32, bool SPLIT>
+__global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const uint16_t* __restrict__ X, int ldx,
+                                                         const uint16_t* __restrict__ W,
+                                                         const uint16_t* __restrict__ bias,
+                                                         const uint16_t* __restrict__ R, int ldr,
+                                                         void* __restrict__ Yv, int ldy, float* __restrict__ ws,
+                                                         int M, int N, int K, int S, int group_m) {
+  using namespace w4;
+  constexpr bool PERM = EPI != EPI_SILU;
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, c = lane & 15;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  // ---- tile: bijective XCD remap, split-major, tall grids rastered in groups of group_m row tiles (gemm_big)
+  const int mtiles = (M + BM - 1) / BM, ntiles = N / BN;
+  const int nwg = mtiles * ntiles * S;
+  int b = blockIdx.x;
+  {
+    const int xcd = b & 7, q = nwg >> 3, r = nwg & 7;
+    b = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+  }
+  int mt, nt, split;
+  {
+    const int tiles = mtiles * ntiles;
+    split = b / tiles;
+    const int bt = b - split * tiles;
+    if (group_m > 1 && mtiles >= 2 * group_m) {
+      const int per = group_m * ntiles, grp = bt / per, first = grp * group_m;
+      const int gm = min(mtiles - first, group_m), rr = bt - grp * per;
+      mt = first + rr % gm;
+      nt = rr / gm;
+    } else {
+      mt = bt % mtiles;
+      nt = bt / mtiles;
+    }
+  }
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int T_all = K / BK;
+  const int t_beg = (int)((long)split * T_all / S), t_end = (int)((long)(split + 1) * T_all / S);
+  const int T = t_end - t_beg;
+
+  // ---- LDS-DMA sources (32-bit element offsets: few VGPRs beside the 128 fragment registers).  X image: 256 rows
+  // x 128 B, 16-B slot (lane % 8) of row r holds logical slot (lane % 8) ^ ((r >> 1) & 7) (gemm_big's BK = 64 map);
+  // instruction q = 8 wave + i copies rows 8q .. 8q + 7, so the swizzle of lane's row is ((lane >> 4) + 4 (i & 1)) & 7.
+  auto aswz = [](int row) -> int { return (row >> 1) & 7; };
+  const int xr0 = 64 * wave + (lane >> 3);
+  const int xslot[2] = {((lane & 7) ^ ((lane >> 4) & 7)) * 8, ((lane & 7) ^ (((lane >> 4) + 4) & 7)) * 8};
+  // W image: (16-row group, k32 block) 1-KB blocks in order (group * 2 + block); instruction q = 8 wave + i copies
+  // block q & 1 of group q >> 1.  PERM: lane l of a block loads granule (kq = l >> 4, row (l & 15) ^ 4 (kq & 1)).
+  const int wl = PERM ? (((lane >> 4) * 16 + ((lane & 15) ^ (4 * ((lane >> 4) & 1)))) * 8) : lane * 8;
+  const uint16_t* wbase = W + (size_t)((n0 >> 4) + 4 * wave) * (K / 128) * 2048 + wl;  // group 4 wave, block 0
+  auto issue = [&](int t, int buf, int d) {  // LDS-DMA instruction d (0..15) of this wave for k stage t
+    uint16_t* As = smem + buf * STAGE;
+    const int k0 = t * BK;
+    if (d < 8) {
+      const int row = min(m0 + xr0 + 8 * d, M - 1);  // rows past M re-read the last; their outputs are masked
+      glds16<0>(X + (size_t)row * ldx + k0 + xslot[d & 1], As + (8 * wave + d) * 512);
+    } else {
+      const int i = d - 8;  // group 4 wave + i / 2, block i & 1
+      glds16<3>(wbase + (size_t)(i >> 1) * (K / 128) * 2048 + (i & 1) * 512 + (size_t)(k0 >> 5) * 512,
+                As + A_EL + (8 * wave + i) * 512);
+    }
+  };
+
+  // ---- fragment offsets (elements inside a stage buffer).  Token tile i: base + 1024 i (16 rows of 64); its swizzle
+  // ((16 i + c) >> 1) & 7 = (c >> 1) & 7 does not depend on i.  Weight tile j: pair base (j & 1) + 2048 (j >> 1).
+  int xo[2], wo[2][2];
+  {
+    const int row = wm * 128 + c;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) xo[s2] = row * BK + (((4 * s2 + g) ^ aswz(row)) * 8);
+  }
+#pragma unroll
+  for (int jj = 0; jj < 2; ++jj) {
+    int grp, pos;
+    if constexpr (PERM) {
+      const int rho = 8 * (c >> 2) + (c & 3) + 4 * jj;  // row of the 32-row block of tiles (2J, 2J + 1)
+      grp = wn * 8 + (rho >> 4);
+      pos = g * 16 + ((rho & 15) ^ (4 * (g & 1)));
+    } else {
+      grp = wn * 8 + jj;
+      pos = g * 16 + c;
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) wo[jj][s2] = A_EL + (grp * 2 + s2) * 512 + pos * 8;
+  }
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  s16x8 wf[2][8], xf[2][8];
+
+  auto bar = []() {  // raw barrier: LDS-DMA stays in flight; the asm statements fence the compiler
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  // MFMA u (0..63) of k half h: weight tile j = u / 8 against token tile i = u % 8.  Inline asm with the accumulator
+  // tied to its AGPR quad: with the builtin the compiler kept moving the 256 accumulators between AGPRs and VGPRs
+  // inside the k loop (~500 v_accvgpr moves per stage).  The asm is invisible to the hazard recognizer: the
+  // epilogue waits for the last MFMAs explicitly.
+  auto mma = [&](int h, int u) {
+    const int j = u >> 3, i = u & 7;
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(wf[h][j]), "v"(xf[h][i]));
+  };
+  auto rd = [&](int buf, int h, int f) {  // fragment read f (0..15) of k half h: 8 weight, then 8 token tiles
+    const uint16_t* Ls = smem + buf * STAGE;
+    if (f < 8) wf[h][f] = ld16(Ls + wo[f & 1][h] + 2048 * (f >> 1));
+    else xf[h][f - 8] = ld16(Ls + xo[h] + 1024 * (f - 8));
+  };
+
+  {  // T >= 1 (S <= K / 64).  Prologue without branches: stage 1 (stage 0 again when T == 1) into buffer 1
+#pragma unroll
+    for (int d = 0; d < 16; ++d) issue(t_beg, 0, d);
+#pragma unroll
+    for (int d = 0; d < 16; ++d) issue(t_beg + min(1, T - 1), 1, d);
+    wait_vm<16>();
+    bar();
+#pragma unroll
+    for (int f = 0; f < 16; ++f) rd(0, 0, f);
+
+    // one 64-deep stage; LAST: no stage after it (no refill, no read-ahead).  Every other stage refills
+    // unconditionally -- past the end with stage T - 1 again, into the buffer no later stage reads -- so the k loop
+    // is straight-line code: a branch inside it made the register allocator shuffle the 256 accumulators between
+    // AGPR quads at the join.
+    auto body = [&](int t, auto last_c) {
+      constexpr bool LAST = decltype(last_c)::value;
+      const int buf = t & 1;
+      const int tr = t_beg + min(t + 2, T - 1);
+      // half 0 (64 MFMAs): half 1's fragments read under the first 16, then every wave is done with this buffer
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        mma(0, u);
+        rd(buf, 1, u);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int u = 16; u < 24; ++u) mma(0, u);
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      bar();
+      // stage t + 2 into the buffer just freed: 16 LDS-DMA instructions over the next 80 MFMAs
+#pragma unroll
+      for (int u = 24; u < 64; ++u) {
+        mma(0, u);
+        if (!LAST && (u - 24) % 5 == 4) issue(tr, buf, (u - 24) / 5);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int u = 0; u < 44; ++u) {
+        mma(1, u);
+        if (!LAST && u % 5 == 4 && u < 40) issue(tr, buf, 8 + u / 5);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if constexpr (!LAST) {
+        // stage t + 1 landed for this wave (the 16 refill instructions stay in flight), then for every wave
+        wait_vm<16>();
+        bar();
+#pragma unroll
+        for (int u = 44; u < 60; ++u) {
+          mma(1, u);
+          rd(buf ^ 1, 0, u - 44);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int u = 60; u < 64; ++u) mma(1, u);
+      } else {
+#pragma unroll
+        for (int u = 44; u < 64; ++u) mma(1, u);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    for (int t = 0; t < T - 1; ++t) body(t, std::false_type{});
+    body(T - 1, std::true_type{});
+    wait_vm<0>();  // the last refill (a re-load of stage T - 1 nobody reads) lands before the wave ends
+  }
+
+  // the last MFMAs (inline asm) retire before the epilogue reads their accumulators
+  asm volatile("s_nop 7\n s_nop 7\n s_nop 7" ::: "memory");
+
+  // ---- epilogue.  Lane (g, c): token row trow(i) = m0 + 128 wm + 16 i + c; PERM: columns 32 J + 8 g .. +8 of the
+  // wave's 128 from tiles (2J, 2J + 1); SiLU: output columns 16 J + 4 g .. +4 (gate tile 2J, up tile 2J + 1).
+  const int rbase = m0 + wm * 128 + c;
+  const int cbase = n0 + wn * 128;
+  if constexpr (SPLIT) {  // raw fp32 partial slabs, in the natural or permuted column order of the lane
+    float* slab = ws + (size_t)split * M * N;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = rbase + 16 * i;
+      if (m >= M) continue;
+      float* row = slab + (size_t)m * N + cbase;
+#pragma unroll
+      for (int J = 0; J < 4; ++J) {
+        if constexpr (PERM) {
+          *reinterpret_cast<f32x4*>(row + 32 * J + 8 * g) = acc[i][2 * J];
+          *reinterpret_cast<f32x4*>(row + 32 * J + 8 * g + 4) = acc[i][2 * J + 1];
+        } else {
+          *reinterpret_cast<f32x4*>(row + 32 * J + 4 * g) = acc[i][2 * J];
+          *reinterpret_cast<f32x4*>(row + 32 * J + 16 + 4 * g) = acc[i][2 * J + 1];
+        }
+      }
+    }
+  } else if constexpr (PERM) {
+    s16x8 bv[4];
+    if (bias != nullptr) {
+#pragma unroll
+      for (int J = 0; J < 4; ++J) bv[J] = ld16(bias + cbase + 32 * J + 8 * g);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = rbase + 16 * i;
+      s16x8 rv[4];
+      if constexpr (EPI == EPI_RESID) {
+        const int mr = min(m, M - 1);
+#pragma unroll
+        for (int J = 0; J < 4; ++J) rv[J] = ld16(R + (size_t)mr * ldr + cbase + 32 * J + 8 * g);
+      }
+      if (m < M) {
+#pragma unroll
+        for (int J = 0; J < 4; ++J) {
+          float v[8];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            v[r] = acc[i][2 * J][r];
+            v[4 + r] = acc[i][2 * J + 1][r];
+          }
+          const int col = cbase + 32 * J + 8 * g;
+          {
+            if (bias != nullptr) {
+#pragma unroll
+              for (int e = 0; e < 8; ++e) v[e] += bf2f(bv[J][e]);
+            }
+            if constexpr (EPI == EPI_RESID) {
+#pragma unroll
+              for (int e = 0; e < 8; ++e) v[e] += bf2f(rv[J][e]);
+            }
+            if constexpr (OUT_F32) {
+              float* p = reinterpret_cast<float*>(Yv) + (size_t)m * ldy + col;
+              *reinterpret_cast<f32x4*>(p) = f32x4{v[0], v[1], v[2], v[3]};
+              *reinterpret_cast<f32x4*>(p + 4) = f32x4{v[4], v[5], v[6], v[7]};
+            } else {
+              s16x8 o;
+#pragma unroll
+              for (int e = 0; e < 8; ++e) o[e] = (short)f2bf(v[e]);
+              st16(reinterpret_cast<uint16_t*>(Yv) + (size_t)m * ldy + col, o);
+            }
+          }
+        }
+      }
+    }
+  } else {  // SiLU: natural rows, gate tile 2J / up tile 2J + 1 -> 4 output columns per lane
+    const int obase = cbase / 2;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = rbase + 16 * i;
+      if (m >= M) continue;
+#pragma unroll
+      for (int J = 0; J < 4; ++J) {
+        const int gcol = cbase + 32 * J + 4 * g;  // gate rows of this lane (16-row interleaved gate / up groups)
+        float o4[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float gv = acc[i][2 * J][r], uv = acc[i][2 * J + 1][r];
+          if (bias != nullptr) {
+            gv += bf2f(bias[gcol + r]);
+            uv += bf2f(bias[gcol + 16 + r]);
+          }
+          o4[r] = silu(gv) * uv;
+        }
+        const int col = obase + 16 * J + 4 * g;
+        if constexpr (OUT_F32) {
+          *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(Yv) + (size_t)m * ldy + col) =
+              f32x4{o4[0], o4[1], o4[2], o4[3]};
+        } else {
+          typedef short s16x4_t __attribute__((ext_vector_type(4)));
+          s16x4_t o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = (short)f2bf(o4[r]);
+          *reinterpret_cast<s16x4_t*>(reinterpret_cast<uint16_t*>(Yv) + (size_t)m * ldy + col) = o;
+        }
+      }
+    }
+  }
+}
+
+template <int EPI, bool F32, bool SPLIT>
+static void w4_launch(const uint16_t* X, int ldx, const uint16_t* W, const uint16_t* bias, const uint16_t* R, int ldr,
+                      void* Y, int ldy, float* ws, int M, int N, int K, int S, int group_m, hipStream_t st) {
+  auto kern = gemm_w4_kernel<EPI, F32, SPLIT>;
+  static bool attr =
+      hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, w4::SMEM) == hipSuccess;
+  (void)attr;
+  const int nwg = ((M + 255) / 256) * (N / 256) * S;
+  kern<<<nwg, 256, w4::SMEM, st>>>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, S, group_m);
+}
+
+// Tile code 4256 of launch_gemm_big.  S > 1 writes fp32 slabs (reduced by the caller's reduce kernel).
+int launch_gemm_w4(const uint16_t* X, int ldx, const uint16_t* W, const uint16_t* bias, const uint16_t* R, int ldr,
+                   void* Y, int ldy, bool out_f32, int epi, float* ws, int M, int N, int K, int S, int group_m,
+                   hipStream_t st) {
+  if (M <= 0) return 0;
+  if (N % 256 != 0 || K % 128 != 0 || S < 1 || S > K / 64) return -1;
+  if (S > 1) {
+    if (ws == nullptr) return -1;
+    if (epi == EPI_SILU) w4_launch<EPI_SILU, true, true>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, S, group_m, st);
+    else w4_launch<EPI_NONE, true, true>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, S, group_m, st);
+    return 0;
+  }
+  if (epi == EPI_SILU) {
+    if (out_f32) w4_launch<EPI_SILU, true, false>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, 1, group_m, st);
+    else w4_launch<EPI_SILU, false, false>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, 1, group_m, st);
+  } else if (epi == EPI_RESID) {
+    if (out_f32) return -1;
+    w4_launch<EPI_RESID, false, false>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, 1, group_m, st);
+  } else {
+    if (out_f32) w4_launch<EPI_NONE, true, false>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, 1, group_m, st);
+    else w4_launch<EPI_NONE, false, false>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, 1, group_m, st);
+  }
+  return 0;
+}
+
+}  // namespace xot

@@ -39,6 +39,10 @@ int launch_gemm_stream8(const uint16_t* X, int ldx, const uint8_t* W, const floa
                         const uint16_t* R, int ldr, void* Y, int ldy, bool out_f32, int epi, float* ws, long ws_elems,
                         int M, int N, int K, int ntw, int S, bool reduce, hipStream_t s);
 // large-M GEMM on the pre-shuffled layout (256 x bn x 64 LDS-DMA tiles, 8 waves; split-K via ws)
+// four-wave 256 x 256 tile (gemm_w4.hip; tile code 4256 of launch_gemm_big): N % 256 == 0, K % 128 == 0
+int launch_gemm_w4(const uint16_t* X, int ldx, const uint16_t* W, const uint16_t* bias, const uint16_t* R, int ldr,
+                   void* Y, int ldy, bool out_f32, int epi, float* ws, int M, int N, int K, int S, int group_m,
+                   hipStream_t st);
 int launch_gemm_big(const uint16_t* X, int ldx, const uint16_t* W, const uint16_t* bias, const uint16_t* R, int ldr,
                     void* Y, int ldy, bool out_f32, int epi, float* ws, long ws_elems, int M, int N, int K, int bn,
                     int S, bool reduce, hipStream_t s);
