@@ -214,8 +214,11 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const uint16_t* __restr
     wait_vm<0>();  // the last refill (a re-load of stage T - 1 nobody reads) lands before the wave ends
   }
 
-  // the last MFMAs (inline asm) retire before the epilogue reads their accumulators
-  asm volatile("s_nop 7\n s_nop 7\n s_nop 7" ::: "memory");
+  // the last MFMAs (inline asm: the hazard recognizer does not see them) retire before the epilogue reads their
+  // accumulators; the scheduling barrier keeps those reads (no dependence on the nops) from moving above them
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 7\n s_nop 7\n s_nop 7\n s_nop 7" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
 
   // ---- epilogue.  Lane (g, c): token row trow(i) = m0 + 128 wm + 16 i + c; PERM: columns 32 J + 8 g .. +8 of the
   // wave's 128 from tiles (2J, 2J + 1); SiLU: output columns 16 J + 4 g .. +4 (gate tile 2J, up tile 2J + 1).
