@@ -142,6 +142,16 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const uint16_t* __restr
     const int j = u >> 3, i = u & 7;
     asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(wf[h][j]), "v"(xf[h][i]));
   };
+  // Keep the 16 fragments of k half h alive up to this point.  The MFMAs are inline asm, so the hazard recognizer
+  // does not know they read their A / B registers over several cycles: a VALU write to a fragment register right
+  // after the MFMA that last read it (the compiler reused dead fragment registers for address arithmetic one MFMA
+  // later) corrupted the product.  Fragment registers stay allocated for a whole phase, and the loop end pads the
+  // one boundary where a VALU may follow the last reader directly.
+  auto keep = [&](int h) {
+    asm volatile("" ::"v"(wf[h][0]), "v"(wf[h][1]), "v"(wf[h][2]), "v"(wf[h][3]), "v"(wf[h][4]), "v"(wf[h][5]),
+                 "v"(wf[h][6]), "v"(wf[h][7]), "v"(xf[h][0]), "v"(xf[h][1]), "v"(xf[h][2]), "v"(xf[h][3]),
+                 "v"(xf[h][4]), "v"(xf[h][5]), "v"(xf[h][6]), "v"(xf[h][7]));
+  };
   auto rd = [&](int buf, int h, int f) {  // fragment read f (0..15) of k half h: 8 weight, then 8 token tiles
     const uint16_t* Ls = smem + buf * STAGE;
     if (f < 8) wf[h][f] = ld16(Ls + wo[f & 1][h] + 2048 * (f >> 1));
@@ -185,6 +195,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const uint16_t* __restr
         if (!LAST && (u - 24) % 5 == 4) issue(tr, buf, (u - 24) / 5);
         __builtin_amdgcn_sched_barrier(0);
       }
+      keep(0);
 #pragma unroll
       for (int u = 0; u < 44; ++u) {
         mma(1, u);
@@ -207,6 +218,9 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const uint16_t* __restr
 #pragma unroll
         for (int u = 44; u < 64; ++u) mma(1, u);
       }
+      keep(1);
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_nop 7\n s_nop 7" ::: "memory");  // VALU after the last reader of a half-1 register (loop top)
       __builtin_amdgcn_sched_barrier(0);
     };
     for (int t = 0; t < T - 1; ++t) body(t, std::false_type{});
