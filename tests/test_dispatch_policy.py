@@ -86,3 +86,17 @@ def test_cpu_reference_linear_caches_fp32_weights():
   wg = torch.randn(32, 64, requires_grad=True)
   ref.linear(x, wg.to(torch.bfloat16))
   assert not hasattr(wg, "_xot_f32")
+
+
+def test_tuner_prefers_four_wave_tile_on_tall_gemms(monkeypatch):
+  """The four-wave 256 x 256 tile (4256) is a candidate wherever N % 256 == 0; from W4_PREF_M rows it takes the
+  ping-pong tile's place as first choice inside the tie windows, below it the ping-pong tile keeps it."""
+  assert 4256 in {c[1] for c in L.GemmPolicy._big_cands(4096, 4096, 4096)}
+  assert 4256 not in {c[1] for c in L.GemmPolicy._big_cands(4096, 4096 + 224, 4096)}
+  t = {("big", 2256, 1): 0.40, ("big", 4256, 1): 0.41}
+  assert L._tie_break(t, 4096) == ("big", 4256, 1)
+  assert L._tie_break(t, 512) == ("big", 2256, 1)
+  t = {("big", 2256, 2): 0.40, ("big", 4256, 1): 0.43}  # across K splits: the preferred tile's wider window
+  assert L._tie_break(t, 4096) == ("big", 4256, 1)
+  monkeypatch.setattr(L, "W4", False)
+  assert 4256 not in {c[1] for c in L.GemmPolicy._big_cands(4096, 4096, 4096)}

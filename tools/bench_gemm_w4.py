@@ -44,7 +44,13 @@ def main():
   ap.add_argument("--shapes", default="train8b,prefill70b")
   ap.add_argument("--codes", default="4256,2256")
   ap.add_argument("--splits", type=int, default=1)
+  ap.add_argument("--mnk", default="", help="one shape M,N,K,epi instead of --shapes (e.g. for PMC passes)")
+  ap.add_argument("--no-blas", action="store_true")
   a = ap.parse_args()
+  if a.mnk:
+    m_, n_, k_, e_ = a.mnk.split(",")
+    SHAPES["mnk"] = [(int(m_), int(n_), int(k_), e_)]
+    a.shapes = "mnk"
   from xotorch_support_jetson_amd.ops import kernels as K
   from xotorch_support_jetson_amd.ops._ext import require
   from xotorch_support_jetson_amd.ops.weights_layout import shuffle_for_stream
@@ -63,13 +69,16 @@ def main():
       slab = torch.empty(S * M * N, device=dev, dtype=torch.float32) if S > 1 else None
       fl = 2.0 * M * N * Kd
       out = {"group": group, "M": M, "N": N, "K": Kd, "epi": epi, "splits": S}
-      for code in [int(c) for c in a.codes.split(",")]:
+      for code in [int(c) for c in a.codes.split(",") if c != "none"]:
         try:
           us = t_us(lambda i: C.gemm_big(x, wsh[i], y, None, r, slab, K.EPI[epi], code, S), nc)
           out[f"c{code}_us"] = round(us, 1)
           out[f"c{code}_pflops"] = round(fl / us / 1e9, 3)
         except RuntimeError as e:
           out[f"c{code}_err"] = str(e)[:80]
+      if a.no_blas:
+        print(json.dumps(out), flush=True)
+        continue
       if epi == "resid":
         blas = lambda i: torch.addmm(r, x, ws_[i].t())
       else:

@@ -152,10 +152,13 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const uint16_t* __restr
                  "v"(wf[h][6]), "v"(wf[h][7]), "v"(xf[h][0]), "v"(xf[h][1]), "v"(xf[h][2]), "v"(xf[h][3]),
                  "v"(xf[h][4]), "v"(xf[h][5]), "v"(xf[h][6]), "v"(xf[h][7]));
   };
-  auto rd = [&](int buf, int h, int f) {  // fragment read f (0..15) of k half h: 8 weight, then 8 token tiles
+  // fragment read f (0..15) of k half h, in the order the MFMAs consume them (weight tile 0, token tiles 0..7,
+  // weight tiles 1..7): the first MFMA of a half waits for 2 reads (counted lgkmcnt), not for all 16
+  auto rd = [&](int buf, int h, int f) {
     const uint16_t* Ls = smem + buf * STAGE;
-    if (f < 8) wf[h][f] = ld16(Ls + wo[f & 1][h] + 2048 * (f >> 1));
-    else xf[h][f - 8] = ld16(Ls + xo[h] + 1024 * (f - 8));
+    const int j = f == 0 ? 0 : (f <= 8 ? -1 : f - 8);
+    if (j >= 0) wf[h][j] = ld16(Ls + wo[j & 1][h] + 2048 * (j >> 1));
+    else xf[h][f - 1] = ld16(Ls + xo[h] + 1024 * (f - 1));
   };
 
   {  // T >= 1 (S <= K / 64).  Prologue without branches: stage 1 (stage 0 again when T == 1) into buffer 1
@@ -184,8 +187,10 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const uint16_t* __restr
         __builtin_amdgcn_sched_barrier(0);
       }
 #pragma unroll
-      for (int u = 16; u < 24; ++u) mma(0, u);
-      __builtin_amdgcn_sched_barrier(0);
+      for (int u = 16; u < 24; ++u) {
+        mma(0, u);
+        __builtin_amdgcn_sched_barrier(0);
+      }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       bar();
       // stage t + 2 into the buffer just freed: 16 LDS-DMA instructions over the next 80 MFMAs
@@ -213,19 +218,29 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const uint16_t* __restr
           __builtin_amdgcn_sched_barrier(0);
         }
 #pragma unroll
-        for (int u = 60; u < 64; ++u) mma(1, u);
+        for (int u = 60; u < 64; ++u) {
+          mma(1, u);
+          __builtin_amdgcn_sched_barrier(0);
+        }
       } else {
+        // (a scheduling barrier after every MFMA: the epilogue's accumulator reads must not move in among the last
+        // MFMAs, which the hazard recognizer cannot see)
 #pragma unroll
-        for (int u = 44; u < 64; ++u) mma(1, u);
+        for (int u = 44; u < 64; ++u) {
+          mma(1, u);
+          __builtin_amdgcn_sched_barrier(0);
+        }
       }
       keep(1);
       __builtin_amdgcn_sched_barrier(0);
       asm volatile("s_nop 7\n s_nop 7" ::: "memory");  // VALU after the last reader of a half-1 register (loop top)
       __builtin_amdgcn_sched_barrier(0);
     };
-    for (int t = 0; t < T - 1; ++t) body(t, std::false_type{});
-    body(T - 1, std::true_type{});
-    wait_vm<0>();  // the last refill (a re-load of stage T - 1 nobody reads) lands before the wave ends
+    // One loop body for every stage, the last included (its read-ahead reads a re-loaded stage nobody uses): a
+    // peeled last body got its own accumulator allocation, and the AGPR shuffle the allocator put between the loop
+    // and it raced the inline-asm MFMAs it cannot see.
+    for (int t = 0; t < T; ++t) body(t, std::false_type{});
+    wait_vm<0>();  // the last refills (re-loads of stage T - 1 nobody reads) land before the wave ends
   }
 
   // the last MFMAs (inline asm: the hazard recognizer does not see them) retire before the epilogue reads their

@@ -44,6 +44,12 @@ SPLITK_IN_LAUNCH = os.environ.get("XOT_SPLITK_IN_LAUNCH", "0") == "1"
 SK = os.environ.get("XOT_GEMM_SK", "0") == "1"
 # XOT_GEMM_PP2=0: leave the two-phase ping-pong tile (code 2256) out of the candidates
 PP2 = os.environ.get("XOT_GEMM_PP2", "1") == "1"
+# XOT_GEMM_W4=0: leave the four-wave 256 x 256 tile (code 4256) out of the candidates
+W4 = os.environ.get("XOT_GEMM_W4", "1") == "1"
+# rows from which the four-wave tile is preferred over the two-phase ping-pong within TIE (tall prefill / training
+# GEMMs: it reads a third less LDS per FLOP and has ~6 us less fixed cost per tile, profiles/r5/gemm_w4/); below
+# it the ping-pong tile, the measured in-step winner at the decode batches, keeps the preference
+W4_PREF_M = int(os.environ.get("XOT_GEMM_W4_PREF_M", "2048"))
 # XOT_GEMM_BLAS=1: time hipBLASLt among the candidates for row-major weights (off: the kernel library only)
 BLAS_CAND = os.environ.get("XOT_GEMM_BLAS", "0") == "1"
 # largest M for which the stream GEMM is a candidate (above it only gemm_big is timed)
@@ -350,6 +356,8 @@ class GemmPolicy:
       return cands
     # 1256 / 2256: the 256 x 256 tile on the two-group ping-pong schedule in four / two phases per stage
     codes = [256, 1256, 2256, 128] if PP2 else [256, 1256, 128]
+    if W4 and N % 256 == 0:  # four-wave 256 x 256 tile (csrc/gemm_w4.hip): 256-row tiles only
+      codes.append(4256)
     if N % 224 == 0:  # 7 row groups per wave: whole rounds where 256-wide tiles leave a half round (8B gate/up)
       codes.append(224)
     bm = big_row_tile(M)
@@ -394,7 +402,7 @@ class GemmPolicy:
         times[cfg] = self._time(lambda: _shuffled_call(x, w, bias, residual, epi, y, cfg)) + _slab_read_ms(cfg, M, N)
       except RuntimeError:
         pass
-    got = _tie_break(times) if times else cands[0]
+    got = _tie_break(times, M) if times else cands[0]
     if TUNE_LOG:
       print(f"[gemm tune] {key} -> {got}: " + ", ".join(f"{c}={t * 1e3:.1f}us" for c, t in sorted(times.items(), key=lambda i: i[1])),
             file=sys.stderr, flush=True)
@@ -438,18 +446,21 @@ TIE = float(os.environ.get("XOT_GEMM_TIE", "0.05"))
 # 78.82 / 78.86 ms, profiles/r4/tuner/oproj/)
 TIE_X = float(os.environ.get("XOT_GEMM_TIE_X", "0.10"))
 TUNE_LOG = os.environ.get("XOT_GEMM_TUNE_LOG", "0") == "1"  # print every shuffled-weight tuning's timings
-_BIG_PREF = {2256: 0, 1256: 1, 256: 2, 224: 3, 128: 4}
+_BIG_PREF = {2256: 0, 4256: 1, 1256: 2, 256: 3, 224: 4, 128: 5}
+_BIG_PREF_TALL = {4256: 0, 2256: 1, 1256: 2, 256: 3, 224: 4, 128: 5}
 
 
-def _tie_break(times: Dict) -> Tuple:
+def _tie_break(times: Dict, M: int = 0) -> Tuple:
   best = min(times, key=times.get)
   code = lambda c: c[1] % 10000  # noqa: E731 - the schedule, whatever the row tile
   if best[0] != "big" or code(best) not in _BIG_PREF or TIE <= 0:
     return best
+  pref = _BIG_PREF_TALL if M >= W4_PREF_M else _BIG_PREF
+  top = min(pref, key=pref.get)
   close = [c for c, t in times.items()
-           if c[0] == "big" and code(c) in _BIG_PREF and ((c[2] == best[2] and t <= times[best] * (1 + TIE))
-                                                          or (code(c) == 2256 and t <= times[best] * (1 + TIE_X)))]
-  return min(close, key=lambda c: (_BIG_PREF[code(c)], times[c]))
+           if c[0] == "big" and code(c) in pref and ((c[2] == best[2] and t <= times[best] * (1 + TIE))
+                                                     or (code(c) == top and t <= times[best] * (1 + TIE_X)))]
+  return min(close, key=lambda c: (pref[code(c)], times[c]))
 
 
 def _ws_elems(cfg, M, N) -> int:
