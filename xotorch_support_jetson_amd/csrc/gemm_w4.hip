@@ -8,10 +8,11 @@
 //     64-deep stage in registers (128 VGPRs) -- 0.25 fragment reads per MFMA instead of 0.375
 //   * two LDS stage buffers (2 x 64 KB, LDS-DMA, 16 1-KB instructions per wave and stage); a stage's buffer is
 //     free as soon as every wave holds its fragments, so stage t+2 is issued a quarter into stage t and has
-//     ~1.6 stages of latency budget (the ping-pong tile's refill has ~1)
-//   * per stage: half 0's 64 MFMAs with half 1's 16 fragment reads under the first 16; lgkmcnt(0) + barrier;
-//     16 LDS-DMA issues spread over the next 80 MFMAs; vmcnt + barrier (stage t+1 landed); stage t+1's half-0
-//     fragments read under the last 20 MFMAs of half 1 -- two barriers per 128 MFMAs
+//     ~1.5 stages of latency budget (the ping-pong tile's refill has ~1)
+//   * per stage: half 0's 64 MFMAs with half 1's 16 fragment reads under the first 16; lgkmcnt(0) + barrier after
+//     32; 16 LDS-DMA issues spread over the next 64 MFMAs; vmcnt + barrier (stage t+1 landed); stage t+1's half-0
+//     fragments read under MFMAs 32..47 of half 1, in the order the MFMAs consume them -- two barriers per 128
+//     MFMAs, every fragment read 16 MFMAs ahead of its first use
 // Operand roles are swapped against gemm_big: the MFMA A operand is the weight fragment (16 output columns x 32 k),
 // B the activation fragment (32 k x 16 tokens), so a lane's accumulator holds 4 consecutive output COLUMNS of one
 // token.  With PERM (every epilogue but SiLU) the weight rows of each pair of 16-column tiles are read permuted
@@ -26,9 +27,64 @@
 
 #include <type_traits>
 
+
 namespace xot {
 
+// cache-policy bits of the LDS-DMA loads (gfx950 CPol: 1 = sc0, 2 = nt, 16 = sc1), tunable by tools/lab/w4_lab.hip.
+// sc1 on both: 3.5-5 % faster than the weights' sc0 + nt streaming hint at 4096 x 4096 x 8192, 4096 x 28672 x 4096
+// and 8192^3 (profiles/r5/gemm_w4/lab_cache_bits.log); nt on both is 6-7 % slower
+#ifndef W4_XAUX
+#define W4_XAUX 16
+#endif
+#ifndef W4_WAUX
+#define W4_WAUX 16
+#endif
+// k-loop schedule positions (see body below): barrier 1 after MFMA W4_B1 - 1 of half 0, barrier 2 after MFMA
+// W4_B2 - 1 of half 1
+#ifndef W4_B1
+#define W4_B1 32
+#endif
+#ifndef W4_B2
+#define W4_B2 32
+#endif
+// refill DMA spacing in MFMAs from barrier 1 (0: spread evenly up to barrier 2)
+#ifndef W4_DGAP
+#define W4_DGAP 0
+#endif
+#ifndef W4_PROBE
+#define W4_PROBE 0
+#endif
+// lab ablations of the k loop (wrong results; timing only, tools/lab/w4_lab.hip): 1 = no refill DMA, 2 = no
+// barriers / waits, 4 = no fragment reads
+#ifndef W4_ABL
+#define W4_ABL 0
+#endif
+
+#if W4_PROBE  // lab timing probes (tools/lab/w4_lab.hip): s_memtime at 4 points of every stage, per block and wave
+__device__ unsigned long long w4_probe[4096 * 4 * 8 * 4];
+#define W4_MARK(P)                                                                                 \
+  do {                                                                                             \
+    const unsigned long long ts_ = __builtin_amdgcn_s_memtime();                                   \
+    w4_probe[((blockIdx.x * 4 + wave) * 8 + (t & 7)) * 4 + (P)] = ts_;                               \
+  } while (0)
+#else
+#define W4_MARK(P) \
+  do {             \
+  } while (0)
+#endif
+
 namespace w4 {
+template <int I, int N, class F>
+__device__ __forceinline__ void static_for_(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for_<I + 1, N>(f);
+  }
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {  // f(integral_constant<int, 0>) .. f(integral_constant<int, N - 1>)
+  static_for_<0, N>(f);
+}
 constexpr int BM = 256, BN = 256, BK = 64;
 constexpr int A_EL = BM * BK, STAGE = (BM + BN) * BK;  // bf16 elements per stage buffer (64 KB)
 constexpr int SMEM = 2 * STAGE * 2;                     // two stage buffers, 128 KB
@@ -76,26 +132,40 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const uint16_t* __restr
   const int t_beg = (int)((long)split * T_all / S), t_end = (int)((long)(split + 1) * T_all / S);
   const int T = t_end - t_beg;
 
-  // ---- LDS-DMA sources (32-bit element offsets: few VGPRs beside the 128 fragment registers).  X image: 256 rows
-  // x 128 B, 16-B slot (lane % 8) of row r holds logical slot (lane % 8) ^ ((r >> 1) & 7) (gemm_big's BK = 64 map);
-  // instruction q = 8 wave + i copies rows 8q .. 8q + 7, so the swizzle of lane's row is ((lane >> 4) + 4 (i & 1)) & 7.
+  // ---- LDS-DMA: buffer loads with the whole address in scalar registers but for constant per-lane byte offsets
+  // (9 VGPRs): the k stage goes in soffset, the LDS destination in M0 (SALU), so issuing a refill
+  // costs the MFMA stream no VALU work.  (Per-issue 64-bit address arithmetic + readfirstlane for M0 -- ~70 VALU
+  // per stage -- cost 20 % of the k loop: profiles/r5/gemm_w4/lab_ablation.log.)  Byte offsets are 32-bit: the
+  // launcher requires X and this tile's weight rows below 4 GB.
+  //   X image: 256 rows x 128 B, 16-B slot (lane % 8) of row r holds logical slot (lane % 8) ^ ((r >> 1) & 7) (gemm_big's
+  //   BK = 64 map); instruction d < 8 copies rows 8 (8 wave + d) .. +7, so the swizzle of lane's row is
+  //   ((lane >> 4) + 4 (d & 1)) & 7.  Rows past M re-read the last; their outputs are masked.
+  //   W image: (16-row group, k32 block) 1-KB blocks in order (group * 2 + block); instruction 8 + i copies block
+  //   i & 1 of group 4 wave + i / 2.  PERM: lane l of a block loads granule (kq = l >> 4, row (l & 15) ^ 4 (kq & 1)).
   auto aswz = [](int row) -> int { return (row >> 1) & 7; };
-  const int xr0 = 64 * wave + (lane >> 3);
-  const int xslot[2] = {((lane & 7) ^ ((lane >> 4) & 7)) * 8, ((lane & 7) ^ (((lane >> 4) + 4) & 7)) * 8};
-  // W image: (16-row group, k32 block) 1-KB blocks in order (group * 2 + block); instruction q = 8 wave + i copies
-  // block q & 1 of group q >> 1.  PERM: lane l of a block loads granule (kq = l >> 4, row (l & 15) ^ 4 (kq & 1)).
-  const int wl = PERM ? (((lane >> 4) * 16 + ((lane & 15) ^ (4 * ((lane >> 4) & 1)))) * 8) : lane * 8;
-  const uint16_t* wbase = W + (size_t)((n0 >> 4) + 4 * wave) * (K / 128) * 2048 + wl;  // group 4 wave, block 0
+  const int swave = __builtin_amdgcn_readfirstlane(wave);
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, -1, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(W + (size_t)((n0 >> 4) + 4 * swave) * (K / 128) * 2048), (short)0, -1, 0x00020000);
+  int xvo[8], wvo;  // per-lane byte offsets: X per instruction (row clamp), W one for all (the rest is scalar)
+  {
+    const int xr0 = 64 * wave + (lane >> 3);
+    const int xslot[2] = {((lane & 7) ^ ((lane >> 4) & 7)) * 8, ((lane & 7) ^ (((lane >> 4) + 4) & 7)) * 8};
+#pragma unroll
+    for (int d = 0; d < 8; ++d)
+      xvo[d] = (int)(((unsigned)min(m0 + xr0 + 8 * d, M - 1) * (unsigned)ldx + xslot[d & 1]) * 2u);
+    wvo = (PERM ? (((lane >> 4) * 16 + ((lane & 15) ^ (4 * ((lane >> 4) & 1)))) * 8) : lane * 8) * 2;
+  }
   auto issue = [&](int t, int buf, int d) {  // LDS-DMA instruction d (0..15) of this wave for k stage t
+    typedef __attribute__((address_space(3))) void* lds_t;
     uint16_t* As = smem + buf * STAGE;
-    const int k0 = t * BK;
     if (d < 8) {
-      const int row = min(m0 + xr0 + 8 * d, M - 1);  // rows past M re-read the last; their outputs are masked
-      glds16<0>(X + (size_t)row * ldx + k0 + xslot[d & 1], As + (8 * wave + d) * 512);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_t)(As + (8 * swave + d) * 512), 16, xvo[d], t * (BK * 2), 0,
+                                               W4_XAUX);
     } else {
       const int i = d - 8;  // group 4 wave + i / 2, block i & 1
-      glds16<3>(wbase + (size_t)(i >> 1) * (K / 128) * 2048 + (i & 1) * 512 + (size_t)(k0 >> 5) * 512,
-                As + A_EL + (8 * wave + i) * 512);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lds_t)(As + A_EL + (8 * swave + i) * 512), 16, wvo,
+                                               t * 2048 + (i >> 1) * (K / 128) * 4096 + (i & 1) * 1024, 0, W4_WAUX);
     }
   };
 
@@ -169,77 +239,61 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const uint16_t* __restr
     wait_vm<16>();
     bar();
 #pragma unroll
-    for (int f = 0; f < 16; ++f) rd(0, 0, f);
+    for (int f = 0; f < 16; ++f) {  // in consumption order, as in the loop
+      rd(0, 0, f);
+      __builtin_amdgcn_sched_barrier(0);
+    }
 
-    // one 64-deep stage; LAST: no stage after it (no refill, no read-ahead).  Every other stage refills
-    // unconditionally -- past the end with stage T - 1 again, into the buffer no later stage reads -- so the k loop
-    // is straight-line code: a branch inside it made the register allocator shuffle the 256 accumulators between
-    // AGPR quads at the join.
-    auto body = [&](int t, auto last_c) {
-      constexpr bool LAST = decltype(last_c)::value;
+    // one 64-deep stage.  Every stage refills and reads ahead unconditionally -- past the end stage T - 1 again,
+    // into a buffer no later stage reads -- so the k loop is straight-line code: a branch inside it made the
+    // register allocator shuffle the 256 accumulators between AGPR quads at the join.
+    // Global MFMA index v = 0..127 of a stage (half v / 64, MFMA v % 64).  Half 1's 16 fragment reads go under the
+    // first 16; after MFMA B1 - 1 every wave has them (lgkmcnt(0) + barrier) and this buffer is free; the 16 refill
+    // DMAs of stage t + 2 spread evenly over MFMAs B1 .. 64 + B2 - 1; after MFMA 64 + B2 - 1 stage t + 1 has landed
+    // for this wave (vmcnt(16): the refill stays in flight) and for every wave (barrier), and its half-0 fragments
+    // are read under the next 16 MFMAs, in the order the next stage consumes them.
+    constexpr int B1 = W4_B1, B2 = W4_B2, SPAN = 64 - B1 + B2, DGAP = W4_DGAP;
+    static_assert(DGAP == 0 || B1 + DGAP * 15 < 64 + B2, "refill DMAs before barrier 2");
+    static_assert(B1 >= 17 && B1 <= 64 && B2 >= 8 && B2 <= 48, "schedule positions");
+    auto body = [&](int t) {
       const int buf = t & 1;
       const int tr = t_beg + min(t + 2, T - 1);
-      // half 0 (64 MFMAs): half 1's fragments read under the first 16, then every wave is done with this buffer
-#pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        mma(0, u);
-        rd(buf, 1, u);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-#pragma unroll
-      for (int u = 16; u < 24; ++u) {
-        mma(0, u);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      bar();
-      // stage t + 2 into the buffer just freed: 16 LDS-DMA instructions over the next 80 MFMAs
-#pragma unroll
-      for (int u = 24; u < 64; ++u) {
-        mma(0, u);
-        if (!LAST && (u - 24) % 5 == 4) issue(tr, buf, (u - 24) / 5);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      keep(0);
-#pragma unroll
-      for (int u = 0; u < 44; ++u) {
-        mma(1, u);
-        if (!LAST && u % 5 == 4 && u < 40) issue(tr, buf, 8 + u / 5);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      if constexpr (!LAST) {
-        // stage t + 1 landed for this wave (the 16 refill instructions stay in flight), then for every wave
-        wait_vm<16>();
-        bar();
-#pragma unroll
-        for (int u = 44; u < 60; ++u) {
-          mma(1, u);
-          rd(buf ^ 1, 0, u - 44);
-          __builtin_amdgcn_sched_barrier(0);
+      W4_MARK(0);
+      static_for<128>([&](auto vc) {  // compile-time v: every condition below folds away
+        constexpr int v = decltype(vc)::value;
+        constexpr int h = v >> 6, u = v & 63;
+        mma(h, u);
+        if constexpr (!(W4_ABL & 4) && v < 16) rd(buf, 1, v);
+        if constexpr (!(W4_ABL & 4) && v >= 64 + B2 && v < 64 + B2 + 16) rd(buf ^ 1, 0, v - 64 - B2);
+        if constexpr (!(W4_ABL & 1) && v >= B1 && v < 64 + B2) {
+          static_for<16>([&](auto kc) {  // refill DMA k after MFMA B1 + ((k + 1) SPAN) / 16 - 1
+            constexpr int k = decltype(kc)::value;
+            if constexpr ((DGAP ? B1 + DGAP * k : B1 + ((k + 1) * SPAN) / 16 - 1) == v) issue(tr, buf, k);
+          });
         }
-#pragma unroll
-        for (int u = 60; u < 64; ++u) {
-          mma(1, u);
-          __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (!(W4_ABL & 2) && v == B1 - 1) {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          bar();
+          W4_MARK(1);
         }
-      } else {
-        // (a scheduling barrier after every MFMA: the epilogue's accumulator reads must not move in among the last
-        // MFMAs, which the hazard recognizer cannot see)
-#pragma unroll
-        for (int u = 44; u < 64; ++u) {
-          mma(1, u);
-          __builtin_amdgcn_sched_barrier(0);
+        if constexpr (!(W4_ABL & 2) && v == 64 + B2 - 1) {
+          wait_vm<(W4_ABL & 1) ? 0 : 16>();
+          bar();
+          W4_MARK(2);
         }
-      }
+        if constexpr (v == 63) keep(0);
+      });
       keep(1);
       __builtin_amdgcn_sched_barrier(0);
       asm volatile("s_nop 7\n s_nop 7" ::: "memory");  // VALU after the last reader of a half-1 register (loop top)
       __builtin_amdgcn_sched_barrier(0);
+      W4_MARK(3);
     };
     // One loop body for every stage, the last included (its read-ahead reads a re-loaded stage nobody uses): a
     // peeled last body got its own accumulator allocation, and the AGPR shuffle the allocator put between the loop
     // and it raced the inline-asm MFMAs it cannot see.
-    for (int t = 0; t < T; ++t) body(t, std::false_type{});
+    for (int t = 0; t < T; ++t) body(t);
     wait_vm<0>();  // the last refills (re-loads of stage T - 1 nobody reads) land before the wave ends
   }
 
@@ -371,6 +425,7 @@ int launch_gemm_w4(const uint16_t* X, int ldx, const uint16_t* W, const uint16_t
                    hipStream_t st) {
   if (M <= 0) return 0;
   if (N % 256 != 0 || K % 128 != 0 || S < 1 || S > K / 64) return -1;
+  if ((size_t)M * ldx * 2 >= (1ull << 32)) return -1;  // 32-bit byte offsets of the LDS-DMA buffer loads
   if (S > 1) {
     if (ws == nullptr) return -1;
     if (epi == EPI_SILU) w4_launch<EPI_SILU, true, true>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, S, group_m, st);
