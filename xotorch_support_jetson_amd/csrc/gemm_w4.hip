@@ -54,8 +54,12 @@ namespace xot {
 #ifndef W4_PROBE
 #define W4_PROBE 0
 #endif
+// fragment reads one per W4_RSP MFMAs
+#ifndef W4_RSP
+#define W4_RSP 1
+#endif
 // lab ablations of the k loop (wrong results; timing only, tools/lab/w4_lab.hip): 1 = no refill DMA, 2 = no
-// barriers / waits, 4 = no fragment reads
+// barriers / waits, 4 = no fragment reads, 8 = no loop-end nops (hazard: timing only)
 #ifndef W4_ABL
 #define W4_ABL 0
 #endif
@@ -252,7 +256,8 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const uint16_t* __restr
     // DMAs of stage t + 2 spread evenly over MFMAs B1 .. 64 + B2 - 1; after MFMA 64 + B2 - 1 stage t + 1 has landed
     // for this wave (vmcnt(16): the refill stays in flight) and for every wave (barrier), and its half-0 fragments
     // are read under the next 16 MFMAs, in the order the next stage consumes them.
-    constexpr int B1 = W4_B1, B2 = W4_B2, SPAN = 64 - B1 + B2, DGAP = W4_DGAP;
+    constexpr int B1 = W4_B1, B2 = W4_B2, SPAN = 64 - B1 + B2, DGAP = W4_DGAP, RSP = W4_RSP;
+    static_assert(16 * RSP <= B1 && B2 + 16 * RSP <= 64, "fragment reads between the barriers");
     static_assert(DGAP == 0 || B1 + DGAP * 15 < 64 + B2, "refill DMAs before barrier 2");
     static_assert(B1 >= 17 && B1 <= 64 && B2 >= 8 && B2 <= 48, "schedule positions");
     auto body = [&](int t) {
@@ -263,8 +268,9 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const uint16_t* __restr
         constexpr int v = decltype(vc)::value;
         constexpr int h = v >> 6, u = v & 63;
         mma(h, u);
-        if constexpr (!(W4_ABL & 4) && v < 16) rd(buf, 1, v);
-        if constexpr (!(W4_ABL & 4) && v >= 64 + B2 && v < 64 + B2 + 16) rd(buf ^ 1, 0, v - 64 - B2);
+        if constexpr (!(W4_ABL & 4) && v % RSP == 0 && v < 16 * RSP) rd(buf, 1, v / RSP);
+        if constexpr (!(W4_ABL & 4) && v >= 64 + B2 && (v - 64 - B2) % RSP == 0 && v < 64 + B2 + 16 * RSP)
+          rd(buf ^ 1, 0, (v - 64 - B2) / RSP);
         if constexpr (!(W4_ABL & 1) && v >= B1 && v < 64 + B2) {
           static_for<16>([&](auto kc) {  // refill DMA k after MFMA B1 + ((k + 1) SPAN) / 16 - 1
             constexpr int k = decltype(kc)::value;
@@ -286,7 +292,8 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const uint16_t* __restr
       });
       keep(1);
       __builtin_amdgcn_sched_barrier(0);
-      asm volatile("s_nop 7\n s_nop 7" ::: "memory");  // VALU after the last reader of a half-1 register (loop top)
+      if constexpr (!(W4_ABL & 8))
+        asm volatile("s_nop 7\n s_nop 7" ::: "memory");  // VALU after the last reader of a half-1 register (loop top)
       __builtin_amdgcn_sched_barrier(0);
       W4_MARK(3);
     };
