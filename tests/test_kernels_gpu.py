@@ -45,6 +45,27 @@ def test_rmsnorm_bwd(gpu):
   require().rmsnorm_bwd(x, w, dy, dx, dw, 1e-5)
   assert rel_err(dx, xr.grad) < 2e-2
   assert rel_err(dw, wr.grad) < 1e-2
+  # the residual stream's gradient joined in the same kernel (training's ResNormFn)
+  res = torch.randn_like(x)
+  dx2 = torch.empty_like(x)
+  dw2 = torch.zeros(2048, device=gpu, dtype=torch.float32)
+  require().rmsnorm_bwd(x, w, dy, dx2, dw2, 1e-5, res)
+  assert rel_err(dx2, xr.grad + res.float()) < 2e-2
+  assert torch.allclose(dw2, dw, rtol=1e-5, atol=1e-4)  # atomics: summation order varies
+
+
+def test_multi_sumsq(gpu):
+  """Gradient-clipping sum of squares over many tensors (bf16 and fp32, odd sizes, an unaligned view start):
+  the fp32 sum of the per-tensor squared norms."""
+  torch.manual_seed(0)
+  from xotorch_support_jetson_amd.ops._ext import require
+  ts = [torch.randn(n, device=gpu, dtype=torch.bfloat16) for n in (1, 7, 4096, 300_001, 2_100_000)]
+  ts += [torch.randn(n, device=gpu, dtype=torch.float32) for n in (5, 65_537)]
+  ts.append(torch.randn(1001, device=gpu, dtype=torch.bfloat16)[3:])  # data pointer not 16-byte aligned
+  ts += [torch.randn(33, device=gpu, dtype=torch.bfloat16) for _ in range(70)]  # more than one batch of 64
+  got = float(require().multi_sumsq(ts)[0])
+  want = float(sum(t.float().pow(2).sum() for t in ts))
+  assert abs(got - want) <= 1e-4 * want
 
 
 def test_embedding_and_silu(gpu):
@@ -708,7 +729,7 @@ def test_moe_layer(gpu, T, E, k, F, shuffled):
 
 
 @pytest.mark.parametrize("B,L,H,Hkv,Dh", [(1, 64, 4, 1, 64), (2, 100, 8, 2, 128), (1, 300, 8, 8, 64),
-                                          (2, 257, 16, 4, 128), (1, 130, 4, 4, 192)])
+                                          (2, 257, 16, 4, 128), (1, 130, 4, 4, 192), (1, 1024, 8, 2, 128)])
 def test_attention_train_fwd_bwd(gpu, B, L, H, Hkv, Dh):
   """Training attention kernels (fwd, dQ, dK/dV) vs fp32 torch autograd of causal GQA attention, with
   q / k / v given as strided row views of one fused qkv tensor (as the trainer passes them)."""

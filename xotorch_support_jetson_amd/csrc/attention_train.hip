@@ -226,6 +226,245 @@ __global__ __launch_bounds__(256) void attn_train_fwd_kernel(const uint16_t* __r
     }
 }
 
+// ---------------------------------------------------------------------------------------- forward, v2
+// The causal forward on the schedule of the serving prefill kernel (csrc/attention.hip attn_prefill_v2_kernel,
+// 745-932 TF/s vs ~375 for attn_train_fwd_kernel above): one workgroup = 8 waves = 256 rows (token, head-in-
+// group) of one (sequence, KV head), two 16-row blocks per wave so every K / V^T fragment read from LDS feeds
+// two MFMAs; S^T = K . Q^T with the K rows permuted so the probabilities land in the B-operand layout of
+// O^T += V^T . P^T (softmax lane-local but for two shuffles of the page max, no LDS round trip for P); K rows
+// (token-major, stride ldk) and V^T rows (the [B, Hkv, DH, Lp] image) arrive by LDS-DMA in a three-page ring,
+// XOR-swizzled through the source addresses so every fragment read is bank-conflict free.  Writes O and the
+// same per-row lse2 (log2 domain) as attn_train_fwd_kernel, so the dQ / dK dV passes are unchanged.
+template <int DH>
+__device__ __forceinline__ int tf2_kswz(int r) {  // K-row granule swizzle (the prefill kernel's searched map)
+  return DH == 128 ? (3 * (r & 1)) | (((r >> 1) & 1) << 2) | (((r >> 3) & 1) << 3)
+                   : (r & 1) | (((r >> 1) & 1) << 1) | (((r >> 3) & 1) << 2);
+}
+
+template <int DH>
+__global__ __launch_bounds__(512, 1) void attn_train_fwd_v2_kernel(const uint16_t* __restrict__ Q, long ldq,
+                                                                   const uint16_t* __restrict__ K, long ldk,
+                                                                   const uint16_t* __restrict__ VT, int Lp,
+                                                                   uint16_t* __restrict__ O, long ldo,
+                                                                   float* __restrict__ lse2, int L, int H, int Hkv,
+                                                                   float sl) {
+  constexpr int KS = DH / 32, NDT = DH / 16, KGPR = DH / 8;
+  constexpr int PAGE_EL = TT * DH;          // elements of one K (or V^T) page
+  constexpr int NCH = 2 * PAGE_EL / 512;    // 1 KB LDS-DMA chunks per page (K then V^T)
+  static_assert(NCH % 8 == 0, "chunks split over 8 waves");
+  constexpr int CPW = NCH / 8;
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];  // [3][K page | V^T page]
+
+  int tile, kvh, b;
+  {  // bijective XCD remap: the tiles of one (sequence, KV head) on one XCD; heaviest (latest rows) first
+    const int nwg = gridDim.x * gridDim.y * gridDim.z;
+    int lin = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    const int xcd = lin & 7, qq = nwg >> 3, rr = nwg & 7;
+    lin = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (lin >> 3);
+    tile = gridDim.x - 1 - lin % gridDim.x;
+    lin /= gridDim.x;
+    kvh = lin % gridDim.y;
+    b = lin / gridDim.y;
+  }
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, c = lane & 15;
+  const int G = H / Hkv, nrows = L * G, row0 = tile * 256;
+  if (row0 >= nrows) return;  // whole workgroup exits together
+
+  // Q^T fragments (B operand: k = dims, n = rows): lane (g, c) holds row c of block blk, dims 32 s + 8 g .. +8
+  s16x8 qf[2][KS];
+  int qpos[2];
+#pragma unroll
+  for (int blk = 0; blk < 2; ++blk) {
+    const int row = row0 + 32 * wave + 16 * blk + c;
+    const bool ok = row < nrows;
+    const int ti = ok ? row / G : 0, hi = ok ? row % G : 0;
+    qpos[blk] = ok ? ti : -1;
+    const uint16_t* qp = Q + ((long)b * L + ti) * ldq + (kvh * G + hi) * DH + 8 * g;
+#pragma unroll
+    for (int s2 = 0; s2 < KS; ++s2) {
+      const s16x8 v = ld16(qp + 32 * s2);
+      qf[blk][s2] = ok ? v : s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  }
+  const int last_row = min(nrows, row0 + 256) - 1;
+  const int npages = (last_row / G) / TT + 1;
+  const int wlast = min(nrows - 1, row0 + 32 * wave + 31);
+  const int wmax = wlast >= row0 + 32 * wave ? wlast / G : -1;  // this wave's last key (causal)
+  const int wmin = (row0 + 32 * wave) / G;                       // ... and its first row's
+
+  float m[2] = {NEG, NEG}, l[2] = {0.f, 0.f};
+  f32x4 o[2][NDT];
+#pragma unroll
+  for (int blk = 0; blk < 2; ++blk)
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) o[blk][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const uint16_t* Kb = K + (long)b * L * ldk + kvh * DH;
+  const uint16_t* VTb = VT + ((long)b * Hkv + kvh) * DH * Lp;
+  auto issue = [&](int p, int buf) {
+    uint16_t* dst = smem + buf * 2 * PAGE_EL;
+#pragma unroll
+    for (int i = 0; i < CPW; ++i) {
+      const int ch = wave * CPW + i;
+      const int P = (ch % (NCH / 2)) * 64 + lane;  // granule of the K or V^T page image
+      const uint16_t* src;
+      if (ch < NCH / 2) {
+        const int r = P / KGPR, j = (P % KGPR) ^ tf2_kswz<DH>(r);
+        src = Kb + (long)min(p * TT + r, L - 1) * ldk + j * 8;  // keys past L: masked (key > every row)
+      } else {
+        const int r = P >> 3, j = (P & 7) ^ (r & 7);  // V^T rows: 64 keys = 8 granules (zero past L)
+        src = VTb + (long)r * Lp + p * TT + j * 8;
+      }
+      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)(dst + ch * 512), 16, 0, 0);
+    }
+  };
+  int kofs[4][KS];  // fragment addresses (elements inside a page image), fixed per lane
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int r = 32 * (j >> 1) + 8 * (c >> 2) + 4 * (j & 1) + (c & 3);
+#pragma unroll
+    for (int s2 = 0; s2 < KS; ++s2) kofs[j][s2] = r * DH + 8 * ((4 * s2 + g) ^ tf2_kswz<DH>(r));
+  }
+  int vofs[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) vofs[kk] = c * TT + 8 * ((4 * kk + g) ^ (c & 7));
+
+  // S^T, causal mask and the online softmax of one page -> P^T fragments and the rescale factors
+  auto score = [&](const uint16_t* Ks, int key0, s16x8 (&pf)[2][2], float (&alpha)[2]) {
+    f32x4 st[2][4];
+#pragma unroll
+    for (int blk = 0; blk < 2; ++blk)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) st[blk][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    constexpr int KPF = 4, NKS = 4 * KS;  // K fragments KPF steps ahead of their MFMAs
+    s16x8 ka[KPF];
+#pragma unroll
+    for (int t = 0; t < KPF - 1; ++t) ka[t] = ld16(Ks + kofs[t & 3][t >> 2]);
+#pragma unroll
+    for (int t = 0; t < NKS; ++t) {
+      if (t + KPF - 1 < NKS) ka[(t + KPF - 1) % KPF] = ld16(Ks + kofs[(t + KPF - 1) & 3][(t + KPF - 1) >> 2]);
+      const int j = t & 3, s2 = t >> 2;
+      st[0][j] = mfma16(ka[t % KPF], qf[0][s2], st[0][j]);
+      st[1][j] = mfma16(ka[t % KPF], qf[1][s2], st[1][j]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    const bool need_mask = key0 + TT - 1 > wmin;  // wave-uniform
+#pragma unroll
+    for (int blk = 0; blk < 2; ++blk) {
+      if (need_mask) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int key = key0 + 32 * (j >> 1) + 8 * g + 4 * (j & 1) + r;
+            st[blk][j][r] = key <= qpos[blk] ? st[blk][j][r] : -INFINITY;
+          }
+      }
+      float mt = NEG;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) mt = fmaxf(mt, st[blk][j][r]);
+      mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
+      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+      const float mn = fmaxf(m[blk], mt * sl);
+      alpha[blk] = __builtin_amdgcn_exp2f(m[blk] - mn);
+      m[blk] = mn;
+      float ls = 0.f;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        u32x4 pw;
+#pragma unroll
+        for (int e = 0; e < 8; e += 2) {
+          const float p0 = __builtin_amdgcn_exp2f(fmaf(st[blk][2 * kk + (e >> 2)][e & 3], sl, -mn));
+          const float p1 = __builtin_amdgcn_exp2f(fmaf(st[blk][2 * kk + (e >> 2)][(e & 3) + 1], sl, -mn));
+          pw[e >> 1] = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t{p0, p1}), bf16x2_t));
+          ls += p0 + p1;
+        }
+        pf[blk][kk] = __builtin_bit_cast(s16x8, pw);
+      }
+      l[blk] = l[blk] * alpha[blk] + ls;
+    }
+  };
+  // O^T = alpha O^T + V^T . P^T for one page
+  auto accumulate = [&](const uint16_t* Vs, const s16x8 (&pf)[2][2], const float (&alpha)[2]) {
+    if (__ballot(alpha[0] != 1.f || alpha[1] != 1.f)) {  // no row's max moved: no rescale (wave-uniform)
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          o[0][dt][r] *= alpha[0];
+          o[1][dt][r] *= alpha[1];
+        }
+    }
+    constexpr int VPF = 3;  // V^T fragments VPF dim tiles ahead of their MFMAs
+    s16x8 va[VPF][2];
+#pragma unroll
+    for (int t = 0; t < VPF - 1; ++t)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) va[t][kk] = ld16(Vs + vofs[kk] + 16 * t * TT);
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) {
+      if (dt + VPF - 1 < NDT) {
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) va[(dt + VPF - 1) % VPF][kk] = ld16(Vs + vofs[kk] + 16 * (dt + VPF - 1) * TT);
+      }
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        o[0][dt] = mfma16(va[dt % VPF][kk], pf[0][kk], o[0][dt]);
+        o[1][dt] = mfma16(va[dt % VPF][kk], pf[1][kk], o[1][dt]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  // three-page ring, two pages in flight: page p + 2 is issued once every wave is past page p - 1
+  issue(0, 0);
+  if (npages > 1) issue(1, 1);
+  for (int p = 0; p < npages; ++p) {
+    const int buf = p % 3;
+    if (p + 1 < npages)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(CPW) : "memory");  // this wave's share of page p landed
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (p + 2 < npages) issue(p + 2, (p + 2) % 3);
+    const int key0 = p * TT;
+    if (key0 > wmax) continue;  // wave-uniform: every row of this wave is before the page (causal)
+    const uint16_t* Ks = smem + buf * 2 * PAGE_EL;
+    s16x8 pf[2][2];
+    float alpha[2];
+    score(Ks, key0, pf, alpha);
+    accumulate(Ks + PAGE_EL, pf, alpha);
+  }
+
+  // o[blk][dt][r] = O[row c of block blk][dim 16 dt + 4 g + r]
+#pragma unroll
+  for (int blk = 0; blk < 2; ++blk) {
+    float ls = l[blk];
+    ls += __shfl_xor(ls, 16, 64);
+    ls += __shfl_xor(ls, 32, 64);
+    const int row = row0 + 32 * wave + 16 * blk + c;
+    if (row < nrows) {
+      const int ti = row / G, h = kvh * G + row % G;
+      uint16_t* op = O + ((long)b * L + ti) * ldo + h * DH + 4 * g;
+      const float inv = ls > 0.f ? 1.f / ls : 0.f;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) {
+        s16x4 v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = (short)f2bf(o[blk][dt][r] * inv);
+        *reinterpret_cast<s16x4*>(op + 16 * dt) = v;
+      }
+      if (g == 0) lse2[((long)b * H + h) * L + ti] = m[blk] + log2f(ls);
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------------- dQ (+ delta)
 template <int DH>
 __global__ __launch_bounds__(256) void attn_train_dq_kernel(const uint16_t* __restrict__ Q, long ldq,
@@ -533,11 +772,34 @@ int launch_attn_train_transpose(const uint16_t* x, long ldx, uint16_t* xt, int B
   return 0;
 }
 
+// XOT_TRAIN_ATTN_V1=1: the first forward kernel for every shape (A/B)
+static bool attn_train_fwd_v2_on() {
+  static const bool on = [] {
+    const char* e = getenv("XOT_TRAIN_ATTN_V1");
+    return !(e != nullptr && e[0] == '1');
+  }();
+  return on;
+}
+
 int launch_attn_train_fwd(const uint16_t* q, long ldq, const uint16_t* k, long ldk, const uint16_t* vt, int Lp,
                           uint16_t* o, long ldo, float* lse2, int B, int L, int H, int Hkv, int Dh, float scale,
                           bool causal, hipStream_t s) {
   if (B <= 0 || L <= 0) return 0;
   if (H % Hkv != 0 || Lp % TT != 0 || Lp < L) return -1;
+  if (causal && (Dh == 128 || Dh == 64) && attn_train_fwd_v2_on()) {
+    const dim3 grid2((L * (H / Hkv) + 255) / 256, Hkv, B);
+    const size_t lds = (size_t)3 * 2 * TT * Dh * 2;
+    const float sl = scale * L2E;
+    if (Dh == 128) {
+      static bool attr = hipFuncSetAttribute((const void*)attn_train_fwd_v2_kernel<128>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess;
+      (void)attr;
+      attn_train_fwd_v2_kernel<128><<<grid2, 512, lds, s>>>(q, ldq, k, ldk, vt, Lp, o, ldo, lse2, L, H, Hkv, sl);
+    } else {
+      attn_train_fwd_v2_kernel<64><<<grid2, 512, lds, s>>>(q, ldq, k, ldk, vt, Lp, o, ldo, lse2, L, H, Hkv, sl);
+    }
+    return 0;
+  }
   dim3 grid(H, (L + FQT - 1) / FQT, B);
 #define XOT_FWD(DHV, CV) \
   attn_train_fwd_kernel<DHV, CV><<<grid, 256, 0, s>>>(q, ldq, k, ldk, vt, Lp, o, ldo, lse2, L, H, Hkv, scale)

@@ -50,7 +50,7 @@ void rmsnorm(const at::Tensor& x, const at::Tensor& w, at::Tensor& out, const c1
 }
 
 void rmsnorm_bwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& dy, at::Tensor& dx, at::Tensor& dw,
-                 double eps) {
+                 double eps, const c10::optional<at::Tensor>& res) {
   CHECK_BF16(x);
   CHECK_BF16(w);
   CHECK_BF16(dy);
@@ -64,11 +64,15 @@ void rmsnorm_bwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& dy,
   XCHECK(D % 8 == 0 && D <= 16384, "rmsnorm_bwd: bad D");
   XCHECK(dy.numel() == x.numel() && dx.numel() == x.numel() && dw.numel() == D && w.numel() == D,
          "rmsnorm_bwd: shape mismatch");
+  if (res.has_value()) {
+    CHECK_BF16(*res);
+    CHECK_CONTIG(*res);
+    XCHECK(res->numel() == x.numel(), "rmsnorm_bwd: res shape");
+  }
   const int64_t nblk = (rows + xot::rmsnorm_bwd_part_rows() - 1) / xot::rmsnorm_bwd_part_rows();
   auto part = at::empty({nblk * D}, x.options().dtype(at::kFloat));  // per-block dw partials
   xot::launch_rmsnorm_bwd(bf(x), bf(w), bf(dy), bf(dx), dw.data_ptr<float>(), part.data_ptr<float>(), (int)rows,
-                          (int)D, (float)eps,
-                          cur_stream());
+                          (int)D, (float)eps, cur_stream(), res.has_value() ? bf(*res) : nullptr);
 }
 
 void embedding(const at::Tensor& ids, const at::Tensor& table, at::Tensor& out) {
@@ -876,6 +880,32 @@ void ce_bwd(const at::Tensor& x, const at::Tensor& tgt, const at::Tensor& lse, c
                      lse.data_ptr<float>(), gscale.data_ptr<float>(), bf(dx), dx.stride(0), cur_stream());
 }
 
+// sum of squares of every tensor (bf16 or fp32, contiguous, one GPU) as a one-element fp32 tensor
+at::Tensor multi_sumsq(const std::vector<at::Tensor>& ts) {
+  XCHECK(!ts.empty(), "multi_sumsq: no tensors");
+  std::vector<xot::SumsqBatch> batches;
+  long maxn = 1;
+  for (size_t i = 0; i < ts.size(); ++i) {
+    const at::Tensor& t = ts[i];
+    XCHECK(t.is_cuda() && t.is_contiguous() && t.device() == ts[0].device(), "multi_sumsq: contiguous GPU tensors");
+    XCHECK(t.scalar_type() == at::kFloat || t.scalar_type() == at::kBFloat16, "multi_sumsq: fp32 or bf16");
+    if (i % xot::SUMSQ_MAXT == 0) batches.push_back(xot::SumsqBatch{});
+    xot::SumsqBatch& b = batches.back();
+    b.p[b.count] = t.data_ptr();
+    b.n[b.count] = t.numel();
+    b.f32[b.count] = t.scalar_type() == at::kFloat;
+    ++b.count;
+    maxn = std::max<long>(maxn, t.numel());
+  }
+  const int maxc = (int)((maxn + xot::multi_sumsq_chunk() - 1) / xot::multi_sumsq_chunk());
+  auto part = at::empty({(long)batches.size() * xot::SUMSQ_MAXT * maxc}, ts[0].options().dtype(at::kFloat));
+  auto out = at::empty({1}, ts[0].options().dtype(at::kFloat));
+  part.zero_();  // rows of a batch's unused tensor slots
+  xot::launch_multi_sumsq(batches.data(), (int)batches.size(), maxc, part.data_ptr<float>(), out.data_ptr<float>(),
+                          cur_stream());
+  return out;
+}
+
 void adamw(at::Tensor& p, const at::Tensor& g, at::Tensor& m, at::Tensor& v, const c10::optional<at::Tensor>& p_bf16,
            double lr, double b1, double b2, double eps, double wd, int64_t step, double gscale) {
   CHECK_DT(p, at::kFloat);
@@ -900,7 +930,8 @@ void adamw(at::Tensor& p, const at::Tensor& g, at::Tensor& m, at::Tensor& v, con
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "xot MI355X (gfx950) kernel library";
   m.def("rmsnorm", &rmsnorm);
-  m.def("rmsnorm_bwd", &rmsnorm_bwd);
+  m.def("rmsnorm_bwd", &rmsnorm_bwd, py::arg("x"), py::arg("w"), py::arg("dy"), py::arg("dx"), py::arg("dw"),
+        py::arg("eps"), py::arg("res") = py::none());
   m.def("embedding", &embedding);
   m.def("silu_mul", &silu_mul);
   m.def("silu_mul_bwd", &silu_mul_bwd);
@@ -951,4 +982,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ce_fwd", &ce_fwd);
   m.def("ce_bwd", &ce_bwd);
   m.def("adamw", &adamw);
+  m.def("multi_sumsq", &multi_sumsq);
 }

@@ -10,7 +10,7 @@ namespace xot {
 void launch_rmsnorm(const uint16_t* x, const uint16_t* res, const uint16_t* w, uint16_t* out, uint16_t* res_out,
                     int rows, int D, float eps, hipStream_t s);
 void launch_rmsnorm_bwd(const uint16_t* x, const uint16_t* w, const uint16_t* dy, uint16_t* dx, float* dw,
-                        float* dw_part, int rows, int D, float eps, hipStream_t s);
+                        float* dw_part, int rows, int D, float eps, hipStream_t s, const uint16_t* res = nullptr);
 int rmsnorm_bwd_part_rows();
 void launch_embedding(const int32_t* ids, const uint16_t* table, uint16_t* out, int T, int D, int vocab,
                       hipStream_t s);
@@ -131,6 +131,16 @@ void launch_ce_fwd(const void* x, bool x_f32, long ld, int T, int V, const int32
                    hipStream_t s);
 void launch_ce_bwd(const void* x, bool x_f32, long ld, int T, int V, const int32_t* tgt, const float* lse,
                    const float* gscale, uint16_t* dx, long ldd, hipStream_t s);
+// multi-tensor sum of squares (gradient clipping): batches of up to SUMSQ_MAXT tensors passed by value
+constexpr int SUMSQ_MAXT = 64;
+struct SumsqBatch {
+  const void* p[SUMSQ_MAXT];
+  long n[SUMSQ_MAXT];
+  int f32[SUMSQ_MAXT];
+  int count;
+};
+int multi_sumsq_chunk();
+void launch_multi_sumsq(const SumsqBatch* batches, int nbatch, int maxc, float* part, float* out, hipStream_t s);
 void launch_adamw(float* p, const void* g, bool g_f32, float* m, float* v, uint16_t* p_bf16, long n, float lr,
                   float b1, float b2, float eps, float wd, int step, float gscale, hipStream_t s);
 

@@ -204,7 +204,8 @@ void launch_splitk_resid_rmsnorm(const float* ws, int S, const uint16_t* bias, u
 
 // ---------------------------------------------------------------- RMSNorm bwd
 // y = x * inv * w  (inv = rsqrt(mean(x^2)+eps))
-// dx = inv * (w*dy - xhat * mean(xhat * w * dy)),  dw += sum_rows dy * xhat
+// dx = inv * (w*dy - xhat * mean(xhat * w * dy)) (+ res: the residual stream's gradient joining here, so the
+// training step needs no separate add kernel per residual join),  dw += sum_rows dy * xhat
 // ROWS rows per block so the dw partial sum is flushed once per block.
 constexpr int RMS_BWD_ROWS = 4;  // 512 workgroups at 2048 rows: the rows of a block run one after another
 template <int MAXC>
@@ -212,7 +213,8 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const uint16_t* __rest
                                                           const uint16_t* __restrict__ w,
                                                           const uint16_t* __restrict__ dy,
                                                           uint16_t* __restrict__ dx, float* __restrict__ dw,
-                                                          float* __restrict__ dw_part, int rows, int D, float eps) {
+                                                          float* __restrict__ dw_part, int rows, int D, float eps,
+                                                          const uint16_t* __restrict__ res) {
   __shared__ float red[2][4];
   const int tid = threadIdx.x, nchunk = D >> 3;
   float dwacc[MAXC][8];
@@ -257,11 +259,12 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const uint16_t* __rest
     for (int i = 0; i < MAXC; ++i) {
       const int c = tid + i * 256;
       if (c < nchunk) {
-        s16x8 wv = ld16(w + c * 8), o;
+        s16x8 wv = ld16(w + c * 8), o, rv = {};
+        if (res != nullptr) rv = ld16(res + base + c * 8);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float xhat = xv[i][j] * inv;
-          o[j] = (short)f2bf(inv * (bf2f(wv[j]) * gv[i][j] - xv[i][j] * coef));
+          o[j] = (short)f2bf(inv * (bf2f(wv[j]) * gv[i][j] - xv[i][j] * coef) + bf2f(rv[j]));
           dwacc[i][j] += gv[i][j] * xhat;
         }
         st16(dx + base + c * 8, o);
@@ -309,19 +312,19 @@ __global__ __launch_bounds__(256) void rmsnorm_dw_reduce_kernel(const float* __r
 // instead of every block's atomics on the same D words (512 blocks contending on 4096 addresses ran
 // the training step's RMSNorm backward 1.9x slower than the atomic-free form).
 void launch_rmsnorm_bwd(const uint16_t* x, const uint16_t* w, const uint16_t* dy, uint16_t* dx, float* dw,
-                        float* dw_part, int rows, int D, float eps, hipStream_t s) {
+                        float* dw_part, int rows, int D, float eps, hipStream_t s, const uint16_t* res) {
   if (rows <= 0) return;
   const int nchunk = D / 8;
   const int nblk = (rows + RMS_BWD_ROWS - 1) / RMS_BWD_ROWS;
   dim3 grid(nblk);
   if (nchunk <= 256)
-    rmsnorm_bwd_kernel<1><<<grid, 256, 0, s>>>(x, w, dy, dx, dw, dw_part, rows, D, eps);
+    rmsnorm_bwd_kernel<1><<<grid, 256, 0, s>>>(x, w, dy, dx, dw, dw_part, rows, D, eps, res);
   else if (nchunk <= 512)
-    rmsnorm_bwd_kernel<2><<<grid, 256, 0, s>>>(x, w, dy, dx, dw, dw_part, rows, D, eps);
+    rmsnorm_bwd_kernel<2><<<grid, 256, 0, s>>>(x, w, dy, dx, dw, dw_part, rows, D, eps, res);
   else if (nchunk <= 1024)
-    rmsnorm_bwd_kernel<4><<<grid, 256, 0, s>>>(x, w, dy, dx, dw, dw_part, rows, D, eps);
+    rmsnorm_bwd_kernel<4><<<grid, 256, 0, s>>>(x, w, dy, dx, dw, dw_part, rows, D, eps, res);
   else
-    rmsnorm_bwd_kernel<8><<<grid, 256, 0, s>>>(x, w, dy, dx, dw, dw_part, rows, D, eps);
+    rmsnorm_bwd_kernel<8><<<grid, 256, 0, s>>>(x, w, dy, dx, dw, dw_part, rows, D, eps, res);
   if (dw_part != nullptr)
     rmsnorm_dw_reduce_kernel<<<dim3((D + 255) / 256, RED_SPLIT), 256, 0, s>>>(dw_part, nblk, D, dw);
 }

@@ -11,6 +11,8 @@ OwnLinearFn  projections on the MFMA GEMMs (shuffled operands from csrc/layout.h
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -47,6 +49,37 @@ class RMSNormFn(torch.autograd.Function):
       y = xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + ctx.eps) * wr
       y.backward(dy.float())
     return xr.grad.to(x.dtype), wr.grad.to(w.dtype), None
+
+
+class ResNormFn(torch.autograd.Function):
+  """(h, rmsnorm(h)) for a residual stream h that is both normalised into a branch and carried on: the backward
+  joins the two gradients in the RMSNorm backward kernel (dh = dh_carried + rmsnorm'(dxn), csrc/norm_rope.hip
+  `res`) instead of autograd's separate add kernel per residual join (2 per layer and micro-batch)."""
+
+  @staticmethod
+  def forward(ctx, h, w, eps):
+    ctx.eps = eps
+    ctx.save_for_backward(h, w)
+    if _gpu(h):
+      xn = torch.empty_like(h)
+      require().rmsnorm(h.contiguous(), w, xn, None, None, float(eps))
+    else:
+      xn = ref.rmsnorm(h, w, eps)[0]
+    return h.view_as(h), xn
+
+  @staticmethod
+  def backward(ctx, dh, dxn):
+    h, w = ctx.saved_tensors
+    if dxn is None:
+      return dh, None, None
+    if _gpu(h):
+      dx = torch.empty_like(h)
+      dw = torch.zeros(w.numel(), dtype=torch.float32, device=h.device)
+      res = dh.contiguous().to(h.dtype) if dh is not None else None
+      require().rmsnorm_bwd(h.contiguous(), w, dxn.contiguous().to(h.dtype), dx, dw, float(ctx.eps), res)
+      return dx, dw.to(w.dtype), None
+    dx, dw, _ = RMSNormFn.backward(ctx, dxn)
+    return (dx if dh is None else dx + dh), dw, None
 
 
 class SiluMulFn(torch.autograd.Function):
@@ -208,6 +241,16 @@ def attention_qk_v(q, k, v, B, L, H, dqk, dv, scale):
 
 def rmsnorm(x, w, eps):
   return RMSNormFn.apply(x, w, eps)
+
+
+RESNORM = os.environ.get("XOT_RESNORM", "1") == "1"  # 0: plain RMSNorm + autograd's add per residual join (A/B)
+
+
+def res_rmsnorm(h, w, eps):
+  """(h, rmsnorm(h, w)): use the returned h downstream so the residual gradient joins in the norm's backward."""
+  if not RESNORM:
+    return h, RMSNormFn.apply(h, w, eps)
+  return ResNormFn.apply(h, w, eps)
 
 
 def silu_mul(gu):

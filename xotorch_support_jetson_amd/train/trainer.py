@@ -145,7 +145,7 @@ class ShardTrainer:
     pos = (torch.arange(L, device=self.device, dtype=torch.int32) + shift).repeat(B)
     h = h.reshape(B * L, D)
     for i in self.shard.layers():
-      xn = A.rmsnorm(h, P[f"{i}.ln1"], c.rms_norm_eps)
+      h, xn = A.res_rmsnorm(h, P[f"{i}.ln1"], c.rms_norm_eps)
       if c.is_mla:
         a = self._mla(xn, i, pos, B, L)
       else:
@@ -157,7 +157,7 @@ class ShardTrainer:
         k = A.rope(k, pos, self.cos_sin, Hkv, Dh)
         a = A.attention(q, k, v, B, L, H, Hkv, Dh)  # flash-style HIP kernels (fwd + dQ + dK/dV)
       h = self._mm(a, f"{i}.o", h)
-      xn = A.rmsnorm(h, P[f"{i}.ln2"], c.rms_norm_eps)
+      h, xn = A.res_rmsnorm(h, P[f"{i}.ln2"], c.rms_norm_eps)
       if f"{i}.router" in P:
         h = h + self._moe(xn, i)
       else:
@@ -433,9 +433,14 @@ class ShardTrainer:
     if grads is None:
       grads = self.grads()
     counted = [g for k, g in grads.items() if k not in norm_exclude]
-    # one fp32-accumulating norm kernel per tensor (no fp32 copies of the bf16 gradients)
-    sq = (torch.stack([torch.linalg.vector_norm(g, dtype=torch.float32) for g in counted]).square().sum()
-          if counted else torch.zeros((), device=self.device))
+    # GPU: one multi-tensor sum-of-squares pass (csrc/train_ops.hip multi_sumsq) over every gradient, no fp32
+    # copies; CPU: an fp32-accumulating norm per tensor
+    if counted and os.environ.get("XOT_MULTI_SUMSQ", "1") == "1" and all(g.is_cuda and g.is_contiguous() and g.dtype in (torch.bfloat16, torch.float32)
+                       for g in counted):
+      sq = require().multi_sumsq(counted).reshape(())
+    else:
+      sq = (torch.stack([torch.linalg.vector_norm(g, dtype=torch.float32) for g in counted]).square().sum()
+            if counted else torch.zeros((), device=self.device))
     if grad_norm_sq_reduce is not None:
       sq = grad_norm_sq_reduce(sq.reshape(1).float()).reshape(())
     gnorm = torch.sqrt(sq)
