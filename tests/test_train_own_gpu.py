@@ -103,3 +103,35 @@ def test_xot_train_ragged_no_vendor_gemm(gpu, model, monkeypatch):
   for k in wc:  # four AdamW steps from the same start: the last stage's weight updates agree
     d = ((wc[k] - wg[k]).abs().mean() / (wc[k].abs().mean() + 1e-12)).item()
     assert d < 0.25, (k, d)
+
+
+@pytest.mark.parametrize("N,K,gdt", [(256, 384, torch.bfloat16), (128, 1024, torch.float32)])
+def test_adamw_tiled_matches_adamw_and_relayout(N, K, gdt):
+  """The fused AdamW (csrc/train_ops.hip adamw_tiled) updates p / m / v as the plain kernel does and writes
+  exactly shuffle(W) and shuffle(W^T) of its own bf16 result (the TrainWeight operand images)."""
+  from xotorch_support_jetson_amd.ops._ext import require
+  from xotorch_support_jetson_amd.ops.weights_layout import shuffle_for_stream
+  C = require()
+  dev = torch.device("cuda:0")
+  torch.manual_seed(0)
+  p0 = torch.randn(N, K, device=dev)
+  g = (torch.randn(N, K, device=dev) * 0.1).to(gdt)
+  m0, v0 = torch.randn(N, K, device=dev) * 0.01, torch.rand(N, K, device=dev) * 1e-3
+  args = (1e-3, 0.9, 0.95, 1e-8, 0.1, 3, 0.7)
+  p1, m1, v1, pb1 = p0.clone(), m0.clone(), v0.clone(), torch.empty(N, K, device=dev, dtype=torch.bfloat16)
+  C.adamw(p1, g, m1, v1, pb1, *args)
+  p2, m2, v2, pb2 = p0.clone(), m0.clone(), v0.clone(), torch.empty(N, K, device=dev, dtype=torch.bfloat16)
+  ws = torch.empty(N, K, device=dev, dtype=torch.bfloat16)
+  wts = torch.empty(K, N, device=dev, dtype=torch.bfloat16)
+  C.adamw_tiled(p2, g, m2, v2, pb2, ws, wts, *args)
+  torch.cuda.synchronize()
+  for a, b in ((p1, p2), (m1, m2), (v1, v2)):
+    assert torch.allclose(a, b, rtol=1e-6, atol=1e-7)
+  assert (pb1.float() - pb2.float()).abs().max().item() <= 2 * (pb1.float().abs().max().item() * 2 ** -8)
+  assert torch.equal(ws, shuffle_for_stream(pb2))
+  assert torch.equal(wts, shuffle_for_stream(pb2.t().contiguous()))
+  # without the plain copy the images are the same
+  p3, m3, v3 = p0.clone(), m0.clone(), v0.clone()
+  ws3, wts3 = torch.empty_like(ws), torch.empty_like(wts)
+  C.adamw_tiled(p3, g, m3, v3, None, ws3, wts3, *args)
+  assert torch.equal(ws3, ws) and torch.equal(wts3, wts)

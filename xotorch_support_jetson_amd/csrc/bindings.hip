@@ -880,6 +880,33 @@ void ce_bwd(const at::Tensor& x, const at::Tensor& tgt, const at::Tensor& lse, c
                      lse.data_ptr<float>(), gscale.data_ptr<float>(), bf(dx), dx.stride(0), cur_stream());
 }
 
+// AdamW of a 2-D weight [N, K] fused with its shuffle(W) / shuffle(W^T) operand images (N, K % 128 == 0)
+void adamw_tiled(at::Tensor& p, const at::Tensor& g, at::Tensor& m, at::Tensor& v,
+                 const c10::optional<at::Tensor>& p_bf16, at::Tensor& ws, at::Tensor& wts, double lr, double b1,
+                 double b2, double eps, double wd, int64_t step, double gscale) {
+  CHECK_DT(p, at::kFloat);
+  CHECK_DT(m, at::kFloat);
+  CHECK_DT(v, at::kFloat);
+  CHECK_BF16(ws);
+  CHECK_BF16(wts);
+  const bool gf32 = g.scalar_type() == at::kFloat;
+  XCHECK(gf32 || g.scalar_type() == at::kBFloat16, "adamw_tiled: grad must be fp32 or bf16");
+  XCHECK(all_contig_gpu(p, g, m, v) && ws.is_contiguous() && wts.is_contiguous(), "adamw_tiled: contiguous GPU");
+  XCHECK(p.dim() == 2, "adamw_tiled: 2-D weight");
+  const int64_t N = p.size(0), K = p.size(1);
+  XCHECK(g.numel() == N * K && m.numel() == N * K && v.numel() == N * K && ws.numel() == N * K &&
+             wts.numel() == N * K, "adamw_tiled: shape mismatch");
+  if (p_bf16.has_value()) {
+    CHECK_BF16((*p_bf16));
+    XCHECK(p_bf16->numel() == N * K && p_bf16->is_contiguous(), "adamw_tiled: p_bf16 shape");
+  }
+  const int rc = xot::launch_adamw_tiled(p.data_ptr<float>(), g.data_ptr(), gf32, m.data_ptr<float>(),
+                                         v.data_ptr<float>(), bf_opt(p_bf16), bf(ws), bf(wts), (int)N, (int)K,
+                                         (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, (int)step,
+                                         (float)gscale, cur_stream());
+  XCHECK(rc == 0, "adamw_tiled: N and K must be multiples of 128");
+}
+
 // sum of squares of every tensor (bf16 or fp32, contiguous, one GPU) as a one-element fp32 tensor
 at::Tensor multi_sumsq(const std::vector<at::Tensor>& ts) {
   XCHECK(!ts.empty(), "multi_sumsq: no tensors");
@@ -983,4 +1010,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ce_bwd", &ce_bwd);
   m.def("adamw", &adamw);
   m.def("multi_sumsq", &multi_sumsq);
+  m.def("adamw_tiled", &adamw_tiled);
 }

@@ -141,6 +141,9 @@ struct SumsqBatch {
 };
 int multi_sumsq_chunk();
 void launch_multi_sumsq(const SumsqBatch* batches, int nbatch, int maxc, float* part, float* out, hipStream_t s);
+int launch_adamw_tiled(float* p, const void* g, bool g_f32, float* m, float* v, uint16_t* pb, uint16_t* ws,
+                       uint16_t* wts, int N, int K, float lr, float b1, float b2, float eps, float wd, int step,
+                       float gscale, hipStream_t s);
 void launch_adamw(float* p, const void* g, bool g_f32, float* m, float* v, uint16_t* p_bf16, long n, float lr,
                   float b1, float b2, float eps, float wd, int step, float gscale, hipStream_t s);
 

@@ -137,6 +137,103 @@ void launch_adamw(float* p, const void* g, bool g_f32, float* m, float* v, uint1
                                                 gscale);
 }
 
+// ---------------------------------------------------------------- AdamW fused with the operand-layout refresh
+// One 2-D projection weight W [N, K] (N, K multiples of 128): the AdamW update of a 128 x 128 tile, then the
+// tile's bf16 values written straight into both own-GEMM operand images -- ws = shuffle(W) and wts =
+// shuffle(W^T) (csrc/layout.hip modes 0 / 1, ops/weights_layout.py shuffle_for_stream) -- from LDS, instead
+// of writing the bf16 copy and re-reading it twice in two relayout kernels after the step (~2 x 2 B per
+// parameter of HBM traffic, ~10 ms of the Llama-3-8B step).  In both images a 16-row group x 128-column block
+// is one contiguous 2048-element run: position ((k % 128) / 8) * 16 + row % 16 holds the row's 8-element
+// granule, so every global store is a full 16 B and consecutive threads store consecutive granules.
+// pb (nullable): the plain bf16 copy, for weights something else still reads (a tied embedding).
+constexpr int AT_LD = 128 + 8;  // padded LDS rows: a 16-lane group reading 16 rows of one granule hits 64 banks
+
+template <typename G>
+__global__ __launch_bounds__(256) void adamw_tiled_kernel(float* __restrict__ p, const G* __restrict__ gr,
+                                                          float* __restrict__ m, float* __restrict__ v,
+                                                          uint16_t* __restrict__ pb, uint16_t* __restrict__ ws,
+                                                          uint16_t* __restrict__ wts, int N, int K, float lr,
+                                                          float b1, float b2, float eps, float wd, float bc1,
+                                                          float bc2, float gscale) {
+  __shared__ __attribute__((aligned(16))) uint16_t tr[128 * AT_LD];  // tile [n][k]
+  __shared__ __attribute__((aligned(16))) uint16_t tt[128 * AT_LD];  // tile [k][n]
+  const int n0 = blockIdx.y * 128, k0 = blockIdx.x * 128;
+#pragma unroll 2
+  for (int it = 0; it < 8; ++it) {
+    const int i = threadIdx.x + 256 * it, row = i >> 4, cg = i & 15;
+    const long off = (long)(n0 + row) * K + k0 + cg * 8;
+    float gv[8];
+    if constexpr (sizeof(G) == 2) {
+      const s16x8 g8 = ld16(reinterpret_cast<const uint16_t*>(gr) + off);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) gv[e] = bf2f(g8[e]);
+    } else {
+      const f32x4 ga = *reinterpret_cast<const f32x4*>(gr + off), gb = *reinterpret_cast<const f32x4*>(gr + off + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        gv[e] = ga[e];
+        gv[4 + e] = gb[e];
+      }
+    }
+    f32x4 pv[2], mv[2], vv[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      pv[h] = *reinterpret_cast<const f32x4*>(p + off + 4 * h);
+      mv[h] = *reinterpret_cast<const f32x4*>(m + off + 4 * h);
+      vv[h] = *reinterpret_cast<const f32x4*>(v + off + 4 * h);
+    }
+    s16x8 bv;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int h = e >> 2, j = e & 3;
+      const float g = gv[e] * gscale;
+      const float mi = b1 * mv[h][j] + (1.f - b1) * g;
+      const float vi = b2 * vv[h][j] + (1.f - b2) * g * g;
+      mv[h][j] = mi;
+      vv[h][j] = vi;
+      float pi = pv[h][j];
+      pi -= lr * ((mi / bc1) / (sqrtf(vi / bc2) + eps) + wd * pi);
+      pv[h][j] = pi;
+      bv[e] = (short)f2bf(pi);
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      *reinterpret_cast<f32x4*>(p + off + 4 * h) = pv[h];
+      *reinterpret_cast<f32x4*>(m + off + 4 * h) = mv[h];
+      *reinterpret_cast<f32x4*>(v + off + 4 * h) = vv[h];
+    }
+    if (pb != nullptr) st16(pb + off, bv);
+    st16(tr + row * AT_LD + cg * 8, bv);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) tt[(cg * 8 + e) * AT_LD + row] = (uint16_t)bv[e];
+  }
+  __syncthreads();
+  // 8 groups of 16 rows x 256 granules in each image
+#pragma unroll 4
+  for (int it = 0; it < 8; ++it) {
+    const int i = threadIdx.x + 256 * it, blk = i >> 8, pos = i & 255, q8 = pos >> 4, r = pos & 15;
+    st16(ws + ((long)((n0 >> 4) + blk) * (K / 128) + (k0 >> 7)) * 2048 + pos * 8,
+         ld16(tr + (blk * 16 + r) * AT_LD + q8 * 8));
+    st16(wts + ((long)((k0 >> 4) + blk) * (N / 128) + (n0 >> 7)) * 2048 + pos * 8,
+         ld16(tt + (blk * 16 + r) * AT_LD + q8 * 8));
+  }
+}
+
+int launch_adamw_tiled(float* p, const void* g, bool g_f32, float* m, float* v, uint16_t* pb, uint16_t* ws,
+                       uint16_t* wts, int N, int K, float lr, float b1, float b2, float eps, float wd, int step,
+                       float gscale, hipStream_t s) {
+  if (N % 128 || K % 128 || N <= 0 || K <= 0) return -1;
+  const float bc1 = 1.f - powf(b1, (float)step), bc2 = 1.f - powf(b2, (float)step);
+  const dim3 grid(K / 128, N / 128);
+  if (g_f32)
+    adamw_tiled_kernel<float><<<grid, 256, 0, s>>>(p, (const float*)g, m, v, pb, ws, wts, N, K, lr, b1, b2, eps, wd,
+                                                   bc1, bc2, gscale);
+  else
+    adamw_tiled_kernel<uint16_t><<<grid, 256, 0, s>>>(p, (const uint16_t*)g, m, v, pb, ws, wts, N, K, lr, b1, b2,
+                                                      eps, wd, bc1, bc2, gscale);
+  return 0;
+}
+
 // ---------------------------------------------------------------- multi-tensor sum of squares
 // Gradient-norm clipping over every parameter's gradient in two launches instead of one torch norm kernel per
 // tensor (195 for Llama-3-8B, 8.5 ms/step at ~1.9 TB/s, profiles/r5/train/trainprof_step_r5h.txt): block

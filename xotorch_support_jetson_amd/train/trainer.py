@@ -38,6 +38,8 @@ OWN_GEMM = os.environ.get("XOT_TRAIN_OWN_GEMM", "1") == "1"
 # XOT_FUSED_CE=0: materialise [T, V] logits and run the separate cross-entropy (A/B, debugging)
 FUSED_CE = os.environ.get("XOT_FUSED_CE", "1") == "1"
 CE_CHUNK = int(os.environ.get("XOT_CE_CHUNK", "1024"))
+# XOT_FUSED_ADAMW=0: plain AdamW + relayout refresh of the operand images (A/B of csrc/train_ops.hip adamw_tiled)
+FUSED_ADAMW = os.environ.get("XOT_FUSED_ADAMW", "1") == "1"
 
 
 def _resid_mm(h: torch.Tensor, x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
@@ -119,6 +121,7 @@ class ShardTrainer:
       if t.ok:
         self.tw[self.head_name] = t
     self.master = {k: p.detach().float().clone() for k, p in self.params.items()}
+    self._pb_stale: set = set()  # bf16 params the fused AdamW did not rewrite (refresh_params)
     self.m = {k: torch.zeros_like(v) for k, v in self.master.items()}
     self.v = {k: torch.zeros_like(v) for k, v in self.master.items()}
 
@@ -446,9 +449,20 @@ class ShardTrainer:
     gnorm = torch.sqrt(sq)
     scale = float(min(1.0, self.grad_clip / (float(gnorm) + 1e-6))) if self.grad_clip else 1.0
     b1, b2 = self.betas
+    fused = set()
     for k, g in grads.items():
       p, m, v, pb = self.master[k], self.m[k], self.v[k], self.params[k]
-      if p.is_cuda:
+      tw = self.tw.get(k)
+      if p.is_cuda and FUSED_ADAMW and isinstance(tw, A.TrainWeight) and p.dim() == 2:
+        # the update writes the own-GEMM operand images directly (no bf16 copy + two relayouts); the plain bf16
+        # copy only where something else reads it (a tied embedding's lookup), else it is refreshed on demand
+        keep = k == "embed"
+        require().adamw_tiled(p, g.contiguous(), m, v, pb.data if keep else None, tw.ws, tw.wts, self.lr, b1, b2,
+                              self.eps, self.wd, self.step_count, scale)
+        fused.add(k)
+        if not keep:
+          self._pb_stale.add(k)
+      elif p.is_cuda:
         require().adamw(p, g.contiguous(), m, v, pb.data, self.lr, b1, b2, self.eps, self.wd, self.step_count, scale)
       else:
         gf = g.float() * scale
@@ -457,9 +471,17 @@ class ShardTrainer:
         bc1, bc2 = 1 - b1 ** self.step_count, 1 - b2 ** self.step_count
         p.mul_(1 - self.lr * self.wd).addcdiv_(m / bc1, (v / bc2).sqrt_().add_(self.eps), value=-self.lr)
         pb.data.copy_(p.to(pb.dtype))
-    for t in self.tw.values():
-      t.refresh()
+    for k, t in self.tw.items():
+      if k not in fused:
+        t.refresh()
     self.dirty = True
+
+  @torch.no_grad()
+  def refresh_params(self) -> None:
+    """Bring the plain bf16 parameters the fused AdamW left stale back in line with the fp32 masters."""
+    for k in self._pb_stale:
+      self.params[k].data.copy_(self.master[k].to(torch.bfloat16))
+    self._pb_stale.clear()
 
   # ------------------------------------------------------------------ write-back
   @torch.no_grad()
@@ -467,6 +489,7 @@ class ShardTrainer:
     """Copy the trained weights into the inference shard (re-interleave gate/up, re-shuffle on GPU)."""
     if not self.dirty:
       return
+    self.refresh_params()
     from ..models.weights import assign_weight
     P = self.params
     c = self.c
