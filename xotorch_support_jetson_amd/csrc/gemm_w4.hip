@@ -54,12 +54,17 @@ namespace xot {
 #ifndef W4_PROBE
 #define W4_PROBE 0
 #endif
+// fragment reads as inline asm with explicit counted waits (0: compiler-visible loads)
+#ifndef W4_ASMRD
+#define W4_ASMRD 1
+#endif
 // fragment reads one per W4_RSP MFMAs
 #ifndef W4_RSP
 #define W4_RSP 1
 #endif
 // lab ablations of the k loop (wrong results; timing only, tools/lab/w4_lab.hip): 1 = no refill DMA, 2 = no
-// barriers / waits, 4 = no fragment reads, 8 = no loop-end nops (hazard: timing only)
+// barriers / waits, 4 = no fragment reads, 8 = no loop-end nops (hazard: timing only), 16 = no barrier 1,
+// 32 = no vmcnt wait before barrier 2, 64 = no barrier 2
 #ifndef W4_ABL
 #define W4_ABL 0
 #endif
@@ -203,6 +208,21 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const uint16_t* __restr
     for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   s16x8 wf[2][8], xf[2][8];
 
+  // The k loop's waits as the s_waitcnt builtin, not inline asm: the compiler's wait-count model then sees them.
+  // With an opaque asm lgkmcnt(0) it still counted half 1's 16 reads as in flight at the loop top, more than the
+  // 4-bit counter can name beside the 16 read-ahead reads, and fell back to lgkmcnt(0) before the first MFMA of
+  // every stage (waiting for the whole read-ahead) instead of the lgkmcnt(14) its two operands need.
+  // gfx950 encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt[5:4] << 14.
+  auto lgkm0 = []() {  // lgkmcnt(0)
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    asm volatile("" ::: "memory");
+  };
+  auto vm16 = []() {  // vmcnt(16): this wave's older stage landed, the 16 refill DMAs stay in flight
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_waitcnt((16 & 15) | (7 << 4) | (15 << 8) | ((16 >> 4) << 14));
+    asm volatile("" ::: "memory");
+  };
   auto bar = []() {  // raw barrier: LDS-DMA stays in flight; the asm statements fence the compiler
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -228,12 +248,46 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const uint16_t* __restr
   };
   // fragment read f (0..15) of k half h, in the order the MFMAs consume them (weight tile 0, token tiles 0..7,
   // weight tiles 1..7): the first MFMA of a half waits for 2 reads (counted lgkmcnt), not for all 16
+#if W4_ASMRD
+  // Fragment reads as inline asm with explicit counted waits (before MFMAs 0..8 and 16 of a stage): the
+  // compiler's wait-count model, merging the prologue's and the previous stage's read-ahead at the loop header,
+  // put lgkmcnt(0) before every stage's first MFMA -- the whole 16-read read-ahead exposed each stage.  Byte
+  // addresses: one base per (operand, k half) plus the stage buffer's 64 KB, tile offsets as immediates.
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint16_t*)smem;
+  auto rd = [&](int buf, int h, int f) {
+    const uint32_t bo = lds0 + (uint32_t)buf * (STAGE * 2);
+    if (f == 0 || f > 8) {
+      const int j = f == 0 ? 0 : f - 8;
+      const uint32_t a = bo + (uint32_t)wo[j & 1][h] * 2;
+      switch (j >> 1) {  // immediate offset 4096 (j / 2) bytes
+        case 0: asm volatile("ds_read_b128 %0, %1" : "=v"(wf[h][j]) : "v"(a)); break;
+        case 1: asm volatile("ds_read_b128 %0, %1 offset:4096" : "=v"(wf[h][j]) : "v"(a)); break;
+        case 2: asm volatile("ds_read_b128 %0, %1 offset:8192" : "=v"(wf[h][j]) : "v"(a)); break;
+        default: asm volatile("ds_read_b128 %0, %1 offset:12288" : "=v"(wf[h][j]) : "v"(a)); break;
+      }
+    } else {
+      const int i = f - 1;
+      const uint32_t a = bo + (uint32_t)xo[h] * 2;
+      switch (i) {  // immediate offset 2048 i bytes
+        case 0: asm volatile("ds_read_b128 %0, %1" : "=v"(xf[h][i]) : "v"(a)); break;
+        case 1: asm volatile("ds_read_b128 %0, %1 offset:2048" : "=v"(xf[h][i]) : "v"(a)); break;
+        case 2: asm volatile("ds_read_b128 %0, %1 offset:4096" : "=v"(xf[h][i]) : "v"(a)); break;
+        case 3: asm volatile("ds_read_b128 %0, %1 offset:6144" : "=v"(xf[h][i]) : "v"(a)); break;
+        case 4: asm volatile("ds_read_b128 %0, %1 offset:8192" : "=v"(xf[h][i]) : "v"(a)); break;
+        case 5: asm volatile("ds_read_b128 %0, %1 offset:10240" : "=v"(xf[h][i]) : "v"(a)); break;
+        case 6: asm volatile("ds_read_b128 %0, %1 offset:12288" : "=v"(xf[h][i]) : "v"(a)); break;
+        default: asm volatile("ds_read_b128 %0, %1 offset:14336" : "=v"(xf[h][i]) : "v"(a)); break;
+      }
+    }
+  };
+#else
   auto rd = [&](int buf, int h, int f) {
     const uint16_t* Ls = smem + buf * STAGE;
     const int j = f == 0 ? 0 : (f <= 8 ? -1 : f - 8);
     if (j >= 0) wf[h][j] = ld16(Ls + wo[j & 1][h] + 2048 * (j >> 1));
     else xf[h][f - 1] = ld16(Ls + xo[h] + 1024 * (f - 1));
   };
+#endif
 
   {  // T >= 1 (S <= K / 64).  Prologue without branches: stage 1 (stage 0 again when T == 1) into buffer 1
 #pragma unroll
@@ -260,6 +314,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const uint16_t* __restr
     static_assert(16 * RSP <= B1 && B2 + 16 * RSP <= 64, "fragment reads between the barriers");
     static_assert(DGAP == 0 || B1 + DGAP * 15 < 64 + B2, "refill DMAs before barrier 2");
     static_assert(B1 >= 17 && B1 <= 64 && B2 >= 8 && B2 <= 48, "schedule positions");
+    static_assert(!W4_ASMRD || RSP == 1, "the explicit read waits assume one read per MFMA");
     auto body = [&](int t) {
       const int buf = t & 1;
       const int tr = t_beg + min(t + 2, T - 1);
@@ -267,6 +322,13 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const uint16_t* __restr
       static_for<128>([&](auto vc) {  // compile-time v: every condition below folds away
         constexpr int v = decltype(vc)::value;
         constexpr int h = v >> 6, u = v & 63;
+#if W4_ASMRD
+        // the read-ahead (16 reads, consumption order) and the v half-1 reads issued since: MFMA v <= 8 needs
+        // read-ahead v + 1 (w0 + x_v, then w1) -> at most 14 younger reads in flight; from MFMA 16 on (w2..w7)
+        // the whole read-ahead -> 15 (stricter than needed, the counter's maximum)
+        if constexpr (v <= 8) asm volatile("s_waitcnt lgkmcnt(14)" ::: "memory");
+        if constexpr (v == 16) asm volatile("s_waitcnt lgkmcnt(15)" ::: "memory");
+#endif
         mma(h, u);
         if constexpr (!(W4_ABL & 4) && v % RSP == 0 && v < 16 * RSP) rd(buf, 1, v / RSP);
         if constexpr (!(W4_ABL & 4) && v >= 64 + B2 && (v - 64 - B2) % RSP == 0 && v < 64 + B2 + 16 * RSP)
@@ -279,13 +341,13 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const uint16_t* __restr
         }
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (!(W4_ABL & 2) && v == B1 - 1) {
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          bar();
+          lgkm0();
+          if constexpr (!(W4_ABL & 16)) bar();
           W4_MARK(1);
         }
         if constexpr (!(W4_ABL & 2) && v == 64 + B2 - 1) {
-          wait_vm<(W4_ABL & 1) ? 0 : 16>();
-          bar();
+          if constexpr (!(W4_ABL & 32)) vm16();
+          if constexpr (!(W4_ABL & 64)) bar();
           W4_MARK(2);
         }
         if constexpr (v == 63) keep(0);
@@ -302,6 +364,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const uint16_t* __restr
     // and it raced the inline-asm MFMAs it cannot see.
     for (int t = 0; t < T; ++t) body(t);
     wait_vm<0>();  // the last refills (re-loads of stage T - 1 nobody reads) land before the wave ends
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // ... and the last read-ahead, before registers are reused
   }
 
   // the last MFMAs (inline asm: the hazard recognizer does not see them) retire before the epilogue reads their
