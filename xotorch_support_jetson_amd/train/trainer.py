@@ -455,8 +455,10 @@ class ShardTrainer:
       tw = self.tw.get(k)
       if p.is_cuda and FUSED_ADAMW and isinstance(tw, A.TrainWeight) and p.dim() == 2:
         # the update writes the own-GEMM operand images directly (no bf16 copy + two relayouts); the plain bf16
-        # copy only where something else reads it (a tied embedding's lookup), else it is refreshed on demand
-        keep = k == "embed"
+        # copy only where something may still read it: a projection without a GradAcc runs torch's matmul on it,
+        # the LM head / tied embedding is read by the embedding lookup and the unfused logits path.  Projections
+        # with a GradAcc read only the images while training; refresh_params() catches their copies up on demand.
+        keep = k not in self.acc
         require().adamw_tiled(p, g.contiguous(), m, v, pb.data if keep else None, tw.ws, tw.wts, self.lr, b1, b2,
                               self.eps, self.wd, self.step_count, scale)
         fused.add(k)
