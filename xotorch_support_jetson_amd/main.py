@@ -10,6 +10,9 @@
   xot --gpus N --grpc-peers ...         the reference's topology instead: one gRPC peer process per GPU,
                                         connected by a generated manual-discovery file (cross-host rings
                                         always use gRPC + discovery)
+  xot --gpus N --federate ...           the local RCCL ring as ONE peer of the discovered cluster: rank 0 runs
+                                        the Node, the range the cluster assigns it is split over the GPUs
+                                        (parallel/ring_federation.py)
 """
 from __future__ import annotations
 
@@ -78,6 +81,9 @@ def build_parser() -> argparse.ArgumentParser:
                  help="(default with --gpus N > 1) the local GPUs as one RCCL ring; with --gpus 0/1: every visible GPU")
   p.add_argument("--grpc-peers", action="store_true",
                  help="--gpus N: one gRPC peer process per GPU (the reference's per-hop RPC) instead of the RCCL ring")
+  p.add_argument("--federate", action="store_true",
+                 help="--gpus N: join discovery as ONE cluster peer whose assigned layer range is split over the "
+                      "local GPUs over RCCL (parallel/ring_federation.py)")
   p.add_argument("--micro-batch", type=int, default=1, help="--ring: sequences per pipeline micro-batch")
   p.add_argument("--parallel", choices=("pp", "dp"), default="pp",
                  help="--ring: pp = layer pipeline over the GPUs; dp = a full replica per GPU, gradients all-reduced")
@@ -260,7 +266,7 @@ async def train_model_cli(node, model_name: str, data_dir, batch_size: int, iter
 
 
 # ------------------------------------------------------------------ assembly
-def build_node(args):
+def build_node(args, engine=None, device_caps=None):
   from .api.chatgpt_api import ChatGPTAPI
   from .download.new_shard_download import new_shard_downloader
   from .download.shard_download import NoopShardDownloader
@@ -274,7 +280,10 @@ def build_node(args):
 
   engine_name = args.inference_engine
   downloader = NoopShardDownloader() if engine_name == "dummy" else new_shard_downloader(args.max_parallel_downloads)
-  engine = get_inference_engine(engine_name, downloader)
+  if engine is None:
+    engine = get_inference_engine(engine_name, downloader)
+  else:  # --federate: the local RCCL ring's engine (its sub-ranges download through each rank's own engine)
+    engine_name = "ShardedInferenceEngine"
   if hasattr(engine, "lr"):
     engine.lr = args.lr
   print(f"Using inference engine: {type(engine).__name__} with shard downloader: {type(downloader).__name__}")
@@ -301,7 +310,7 @@ def build_node(args):
       viz = None
   node = Node(node_id, None, engine, discovery, downloader, RingMemoryWeightedPartitioningStrategy(),
               max_generate_tokens=args.max_generate_tokens, default_sample_temperature=args.default_temp,
-              topology_viz=viz)
+              topology_viz=viz, device_caps=device_caps)
   node.server = GRPCServer(node, args.node_host, port)
   api = None
   if not args.no_api:
@@ -339,11 +348,11 @@ def build_node(args):
   return node, api, engine, viz
 
 
-async def async_main(args):
+async def async_main(args, engine=None, device_caps=None):
   if args.models_seed_dir:
     from .download.new_shard_download import seed_models
     seed_models(args.models_seed_dir)
-  node, api, engine, viz = build_node(args)
+  node, api, engine, viz = build_node(args, engine=engine, device_caps=device_caps)
   loop = asyncio.get_running_loop()
   for s in (signal.SIGINT, signal.SIGTERM):
     try:
@@ -385,6 +394,9 @@ def run(argv=None):
     os.environ["XOT_MAX_BATCH"] = str(args.max_batch)
   if args.max_ctx:
     os.environ["XOT_MAX_CTX"] = str(args.max_ctx)
+  if args.federate and args.gpus and args.gpus > 1 and "XOT_PEER_RANK" not in os.environ:
+    from .parallel.ring_federation import federate_ring  # the local RCCL ring as one discovered peer
+    sys.exit(federate_ring(args, argv))
   if args.gpus and args.gpus > 1 and not args.grpc_peers and "XOT_PEER_RANK" not in os.environ:
     args.ring = True  # local GPUs are ring peers over RCCL unless the gRPC topology is asked for
   if args.ring and args.command in ("train", "eval"):
