@@ -97,3 +97,43 @@ def test_federated_ring_matches_one_engine(world, lo, hi):
   for a, b in zip(got, ref):
     assert np.allclose(a, b, atol=2e-2, rtol=2e-2), np.abs(a - b).max()
     assert int(a.argmax()) == int(b.argmax())
+
+
+def _worker_gpu(rank, world, port, q, shard_dict):
+  os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+  dist.init_process_group("gloo", rank=rank, world_size=world)
+  try:
+    groups = {"ctl": dist.new_group(backend="gloo"), "data": dist.group.WORLD}
+    dev = torch.device("cuda", 0)  # both ranks on the one GPU of the box: activations staged through the host
+    local = ShardedInferenceEngine(NoopShardDownloader(), device=dev)
+    if rank == 0:
+      eng = RingFederatedEngine(local, 0, world, groups, dev)
+      out = asyncio.run(_steps(eng, Shard.from_dict(shard_dict)))
+      eng.stop()
+      q.put((rank, out))
+    else:
+      asyncio.run(follower_loop(local, rank, world, groups, dev))
+      q.put((rank, None))
+  finally:
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_federated_ring_on_gpu():
+  """The GPU engines (batched forward, HIP kernels) behind the federation: two ranks on the box's GPU."""
+  shard = Shard(MODEL, 0, 7, 8)
+  ref = asyncio.run(_steps(ShardedInferenceEngine(NoopShardDownloader(), device=torch.device("cuda", 0)), shard))
+  ctx = mp.get_context("spawn")
+  q = ctx.Queue()
+  port = _free_port()
+  ps = [ctx.Process(target=_worker_gpu, args=(r, 2, port, q, shard.to_dict())) for r in range(2)]
+  for p in ps:
+    p.start()
+  res = {}
+  for _ in range(2):
+    rank, out = q.get(timeout=100)
+    res[rank] = out
+  for p in ps:
+    p.join(30)
+  for a, b in zip(res[0], ref):
+    assert np.allclose(a, b, atol=3e-2, rtol=3e-2), np.abs(a - b).max()
