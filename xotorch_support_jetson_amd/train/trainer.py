@@ -37,7 +37,9 @@ from . import autograd_ops as A
 OWN_GEMM = os.environ.get("XOT_TRAIN_OWN_GEMM", "1") == "1"
 # XOT_FUSED_CE=0: materialise [T, V] logits and run the separate cross-entropy (A/B, debugging)
 FUSED_CE = os.environ.get("XOT_FUSED_CE", "1") == "1"
-CE_CHUNK = int(os.environ.get("XOT_CE_CHUNK", "1024"))
+# rows per fused LM-head + CE chunk: 4096 (one [4096, V] fp32 logits block, 2.1 GB at V = 128256) ran the
+# Llama-3-8B step 1.1 % faster than 1024 (profiles/r5/train/knobs_r5s/)
+CE_CHUNK = int(os.environ.get("XOT_CE_CHUNK", "4096"))
 # XOT_FUSED_ADAMW=0: plain AdamW + relayout refresh of the operand images (A/B of csrc/train_ops.hip adamw_tiled)
 FUSED_ADAMW = os.environ.get("XOT_FUSED_ADAMW", "1") == "1"
 
