@@ -100,3 +100,16 @@ def test_tuner_prefers_four_wave_tile_on_tall_gemms(monkeypatch):
   assert L._tie_break(t, 4096) == ("big", 4256, 1)
   monkeypatch.setattr(L, "W4", False)
   assert 4256 not in {c[1] for c in L.GemmPolicy._big_cands(4096, 4096, 4096)}
+
+
+def test_tall_gemms_take_the_four_wave_tile_untimed(monkeypatch):
+  """M >= W4_PREF_M: ('big', 4256, 1) straight away (no cold-timing pass inside the first prefill chunk), except a
+  residual epilogue into fp32 (the tile has none); XOT_GEMM_TALL_TUNE=1 times them again."""
+  pol = L.GemmPolicy()
+  x, w = torch.empty(4096, 1024, dtype=torch.bfloat16), torch.empty(2048, 1024, dtype=torch.bfloat16)
+  assert pol.shuffled_cfg(x, w, None, None, "none", torch.bfloat16) == ("big", 4256, 1)
+  assert pol.shuffled_cfg(x, w, None, None, "none", torch.float32) == ("big", 4256, 1)
+  monkeypatch.setattr(L, "TALL_FIXED", False)
+  monkeypatch.setattr(L.GemmPolicy, "_no_tuning", lambda self: True)  # the heuristic instead of a GPU timing
+  pol2 = L.GemmPolicy()
+  assert pol2.shuffled_cfg(x, w, None, None, "none", torch.bfloat16)[0] == "big"

@@ -50,6 +50,8 @@ W4 = os.environ.get("XOT_GEMM_W4", "1") == "1"
 # GEMMs: it reads a third less LDS per FLOP and has ~6 us less fixed cost per tile, profiles/r5/gemm_w4/); below
 # it the ping-pong tile, the measured in-step winner at the decode batches, keeps the preference
 W4_PREF_M = int(os.environ.get("XOT_GEMM_W4_PREF_M", "2048"))
+# XOT_GEMM_TALL_TUNE=1: time the candidates for tall GEMMs too (default: the four-wave tile directly, see shuffled_cfg)
+TALL_FIXED = os.environ.get("XOT_GEMM_TALL_TUNE", "0") != "1"
 # XOT_GEMM_BLAS=1: time hipBLASLt among the candidates for row-major weights (off: the kernel library only)
 BLAS_CAND = os.environ.get("XOT_GEMM_BLAS", "0") == "1"
 # largest M for which the stream GEMM is a candidate (above it only gemm_big is timed)
@@ -384,6 +386,13 @@ class GemmPolicy:
     key = ("sh", _m_bucket(M), N, Kd, epi, bias is not None, str(out_dtype))
     got = self._lookup(key)
     if got is not None:
+      return got
+    if TALL_FIXED and W4 and M >= W4_PREF_M and N % 256 == 0 and Kd % 128 == 0 and not (epi == "resid" and out_dtype == torch.float32):
+      # tall GEMMs (prefill chunks, training): the four-wave tile at S = 1 won every tuned tall shape this round
+      # (profiles/r5/headline/bench_r5o_tunelog.log), so it is taken without the cold-timing pass, which cost
+      # ~0.5 s inside the first prefill chunk of every fresh process
+      got = ("big", 4256, 1)
+      self._store(key, got)
       return got
     cands = []
     if M <= STREAM_MAX_M:

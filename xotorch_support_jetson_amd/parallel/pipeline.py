@@ -33,6 +33,9 @@ from ..runtime.runner import ShardRunner
 KC = 64  # candidate slots per row in the split-head hand-off (>= top_k)
 HEAD_SPLIT = 0.65  # default fraction of the LM-head rows on the last stage (measured balance, profiles/r4/scale/)
 
+# tokens per prefill forward of RingStage (whole sequences): the tall GEMMs' M (XOT_PREFILL_CHUNK)
+PREFILL_CHUNK = int(os.environ.get("XOT_PREFILL_CHUNK", "8192"))
+
 
 @dataclass
 class MicroBatch:
@@ -150,12 +153,13 @@ class RingStage:
     return e
 
   # ---------------------------------------------------------------- one micro-batch through this stage
-  def prefill(self, mb: MicroBatch, chunk_tokens: int = 8192):
+  def prefill(self, mb: MicroBatch, chunk_tokens: int = 0):
     """Run the prompts of a micro-batch through this stage in chunks of whole sequences.  First stage
     reads mb.prompt; others receive hidden states.  The last stage returns the hand-off item of the
     first generated token (the sampled ids [B], or the split-head tuple); other stages None."""
     B, L = len(mb.rids), (mb.prompt.shape[1] if mb.prompt is not None else 0)
     dev = self.r.device
+    chunk_tokens = chunk_tokens or PREFILL_CHUNK
     per = max(1, chunk_tokens // max(L, 1)) if L else B
     outs = []
     for lo in range(0, B, per):
