@@ -155,19 +155,22 @@ def _make_cache(n_pages, Hkv, Dh, device):
   return kc, vc
 
 
-@pytest.mark.parametrize("H,Hkv,Dh", [(32, 8, 64), (64, 8, 128), (14, 2, 64), (32, 8, 128)])
-def test_rope_kv_write(gpu, H, Hkv, Dh):
+@pytest.mark.parametrize("H,Hkv,Dh,T,contig", [(32, 8, 64, 19, False), (64, 8, 128, 19, False), (14, 2, 64, 19, False),
+                                               (32, 8, 128, 19, False), (64, 8, 128, 300, False),
+                                               (32, 8, 128, 1000, True), (14, 2, 64, 257, True)])
+def test_rope_kv_write(gpu, H, Hkv, Dh, T, contig):
+  """T >= 256 runs the 64-token tiled kernel (V transposed through LDS), random or prefill-like contiguous slots."""
   torch.manual_seed(0)
-  T = 19
   cs = build_cos_sin(Dh, 4096, 500000.0, {"rope_type": "llama3", "factor": 32.0, "low_freq_factor": 1.0,
                                           "high_freq_factor": 4.0, "original_max_position_embeddings": 8192},
                      device=gpu)
   qkv = torch.randn(T, (H + 2 * Hkv) * Dh, device=gpu, dtype=torch.bfloat16)
   pos = torch.randint(0, 4000, (T,), device=gpu, dtype=torch.int32)
-  slots = torch.randperm(10 * 64, device=gpu)[:T].to(torch.int64)
+  pages = max(10, -(-T // 64) + 2)
+  slots = (torch.arange(T, device=gpu) + 37 if contig else torch.randperm(pages * 64, device=gpu)[:T]).to(torch.int64)
   slots[3] = -1
-  kc, vc = torch.zeros(10, Hkv, 64, Dh, device=gpu, dtype=torch.bfloat16), torch.zeros(10, Hkv, Dh, 64, device=gpu,
-                                                                                          dtype=torch.bfloat16)
+  kc = torch.zeros(pages, Hkv, 64, Dh, device=gpu, dtype=torch.bfloat16)
+  vc = torch.zeros(pages, Hkv, Dh, 64, device=gpu, dtype=torch.bfloat16)
   kr, vr = kc.clone(), vc.clone()
   q = K.rope_kv_write(qkv, pos, cs, slots, kc, vc, H, Hkv)
   x = qkv.view(T, H + 2 * Hkv, Dh)

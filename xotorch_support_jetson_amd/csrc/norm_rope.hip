@@ -453,7 +453,7 @@ __global__ __launch_bounds__(256) void rope_kv_write_kernel(const uint16_t* __re
                                                             const int64_t* __restrict__ slots,
                                                             uint16_t* __restrict__ q_out, uint16_t* __restrict__ kc,
                                                             uint16_t* __restrict__ vc, int H, int Hkv, int Dh, int BS,
-                                                            int max_pos, long nslots) {
+                                                            int max_pos, long nslots, int skip_v) {
   const int t = blockIdx.x;
   const int half = Dh >> 1, qpr = half >> 2;  // 4-wide pair-groups per head
   int p = pos[t];
@@ -474,7 +474,7 @@ __global__ __launch_bounds__(256) void rope_kv_write_kernel(const uint16_t* __re
       rope4(row + h * Dh, dst, cs, i, half, 1.f);
     }
   }
-  if (slot < 0) return;
+  if (slot < 0 || skip_v) return;
   const int nv = Hkv * Dh;
   const uint16_t* vsrc = row + (H + Hkv) * Dh;
   for (int w = threadIdx.x; w < nv; w += 256) {
@@ -588,11 +588,47 @@ void launch_splitk_rope_kv_write(const float* ws, int S, const uint16_t* bias, c
 #undef XOT_SRK
 }
 
+// V of prefill-sized T: the per-token kernel above writes a token's V as Hkv * Dh scattered 2-byte stores (V is
+// stored transposed, 128 B between a token's consecutive dims), one partial cache line per element.  Here a
+// workgroup takes 64 consecutive tokens of one KV head: the [64][Dh] block goes through LDS and leaves as rows of
+// up to 64 consecutive keys of the transposed page (one 128-B line per dim when the tokens share a page, as a
+// prefill chunk's do).  The rotations stay on the per-token kernel (skip_v).
+constexpr int RKV_TOK = 64;
+__global__ __launch_bounds__(256) void v_write_tiled_kernel(const uint16_t* __restrict__ qkv,
+                                                            const int64_t* __restrict__ slots,
+                                                            uint16_t* __restrict__ vc, int T, int H, int Hkv, int Dh,
+                                                            int BS, long nslots) {
+  extern __shared__ uint16_t vt[];  // [RKV_TOK][Dh + 2] (odd dword stride: the transposed reads hit 64 banks)
+  const int t0 = blockIdx.x * RKV_TOK, nt = min(RKV_TOK, T - t0), kh = blockIdx.y;
+  const int rowlen = (H + 2 * Hkv) * Dh, VLD = Dh + 2, cpr = Dh / 8;
+  for (int w = threadIdx.x; w < nt * cpr; w += 256) {
+    const int tt = w / cpr, cc = w % cpr;
+    const s16x8 v = ld16(qkv + (size_t)(t0 + tt) * rowlen + (H + Hkv + kh) * Dh + cc * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) vt[tt * VLD + cc * 8 + j] = (uint16_t)v[j];
+  }
+  __syncthreads();
+  for (int w = threadIdx.x; w < nt * Dh; w += 256) {
+    const int d = w / nt, tt = w % nt, t = t0 + tt;
+    const int64_t slot = slots[t] < nslots ? slots[t] : -1;
+    if (slot >= 0) vc[(((size_t)(slot / BS) * Hkv + kh) * Dh + d) * BS + slot % BS] = vt[tt * VLD + d];
+  }
+}
+
 void launch_rope_kv_write(const uint16_t* qkv, const int32_t* pos, const float* cos_sin, const int64_t* slots,
                           uint16_t* q_out, uint16_t* kc, uint16_t* vc, int T, int H, int Hkv, int Dh, int BS,
                           int max_pos, long nslots, hipStream_t s) {
   if (T <= 0) return;
-  rope_kv_write_kernel<<<T, 256, 0, s>>>(qkv, pos, cos_sin, slots, q_out, kc, vc, H, Hkv, Dh, BS, max_pos, nslots);
+  static const bool tiled = [] {  // XOT_ROPE_TILED=0: the per-token kernel for every T (A/B)
+    const char* e = getenv("XOT_ROPE_TILED");
+    return !(e != nullptr && e[0] == '0');
+  }();
+  const bool vt = tiled && T >= 4 * RKV_TOK && Dh % 8 == 0;
+  rope_kv_write_kernel<<<T, 256, 0, s>>>(qkv, pos, cos_sin, slots, q_out, kc, vc, H, Hkv, Dh, BS, max_pos, nslots,
+                                         vt ? 1 : 0);
+  if (vt)
+    v_write_tiled_kernel<<<dim3((T + RKV_TOK - 1) / RKV_TOK, Hkv), 256, (size_t)RKV_TOK * (Dh + 2) * 2, s>>>(
+        qkv, slots, vc, T, H, Hkv, Dh, BS, nslots);
 }
 
 // plain rotation of x [T, nh, Dh] (row stride ld elements between tokens) -> y (may alias x);
