@@ -925,7 +925,7 @@ at::Tensor multi_sumsq(const std::vector<at::Tensor>& ts) {
     maxn = std::max<long>(maxn, t.numel());
   }
   const int maxc = (int)((maxn + xot::multi_sumsq_chunk() - 1) / xot::multi_sumsq_chunk());
-  auto part = at::empty({(long)batches.size() * xot::SUMSQ_MAXT * maxc}, ts[0].options().dtype(at::kFloat));
+  auto part = at::empty({xot::multi_sumsq_scratch((int)batches.size(), maxc)}, ts[0].options().dtype(at::kFloat));
   auto out = at::empty({1}, ts[0].options().dtype(at::kFloat));
   part.zero_();  // rows of a batch's unused tensor slots
   xot::launch_multi_sumsq(batches.data(), (int)batches.size(), maxc, part.data_ptr<float>(), out.data_ptr<float>(),

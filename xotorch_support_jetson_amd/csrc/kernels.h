@@ -140,6 +140,7 @@ struct SumsqBatch {
   int count;
 };
 int multi_sumsq_chunk();
+long multi_sumsq_scratch(int nbatch, int maxc);  // floats of `part`
 void launch_multi_sumsq(const SumsqBatch* batches, int nbatch, int maxc, float* part, float* out, hipStream_t s);
 int launch_adamw_tiled(float* p, const void* g, bool g_f32, float* m, float* v, uint16_t* pb, uint16_t* ws,
                        uint16_t* wts, int N, int K, float lr, float b1, float b2, float eps, float wd, int step,

@@ -285,24 +285,32 @@ __global__ __launch_bounds__(256) void multi_sumsq_kernel(SumsqBatch b, float* _
   if (threadIdx.x == 0) part[(long)t * maxc + c] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
+// sum of part[0 .. n) into out[blockIdx.x] by a grid-stride over gridDim.x blocks (two launches: gridDim.x
+// partials, then one block over them -- one block over the ~10^6 per-chunk partials took 1.5 ms)
 __global__ __launch_bounds__(256) void sum_reduce_kernel(const float* __restrict__ part, long n,
                                                          float* __restrict__ out) {
   float acc = 0.f;
-  for (long i = threadIdx.x; i < n; i += 256) acc += part[i];
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) acc += part[i];
   __shared__ float red[4];
   acc = wave_sum(acc);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
   __syncthreads();
-  if (threadIdx.x == 0) out[0] = (red[0] + red[1]) + (red[2] + red[3]);
+  if (threadIdx.x == 0) out[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
 int multi_sumsq_chunk() { return SUMSQ_CHUNK; }
+constexpr int SUMSQ_RED_BLOCKS = 512;  // first reduce level (its partials live in part's first slots' tail)
 
 void launch_multi_sumsq(const SumsqBatch* batches, int nbatch, int maxc, float* part, float* out, hipStream_t s) {
   for (int i = 0; i < nbatch; ++i)
     multi_sumsq_kernel<<<dim3(maxc, batches[i].count), 256, 0, s>>>(batches[i], part + (long)i * SUMSQ_MAXT * maxc,
                                                                      maxc);
-  sum_reduce_kernel<<<1, 256, 0, s>>>(part, (long)nbatch * SUMSQ_MAXT * maxc, out);
+  const long n = (long)nbatch * SUMSQ_MAXT * maxc;
+  float* lvl = part + n;  // SUMSQ_RED_BLOCKS floats after the per-chunk partials (multi_sumsq_scratch)
+  sum_reduce_kernel<<<SUMSQ_RED_BLOCKS, 256, 0, s>>>(part, n, lvl);
+  sum_reduce_kernel<<<1, 256, 0, s>>>(lvl, SUMSQ_RED_BLOCKS, out);
 }
+
+long multi_sumsq_scratch(int nbatch, int maxc) { return (long)nbatch * SUMSQ_MAXT * maxc + SUMSQ_RED_BLOCKS; }
 
 }  // namespace xot
