@@ -33,6 +33,7 @@ from typing import Dict, List, Optional
 import torch
 import torch.distributed as dist
 
+from ..train import autograd_ops as A
 from ..train.trainer import ShardTrainer
 from .pipeline_train import TrainBatch
 
@@ -105,6 +106,7 @@ class DataParallelTrainer:
   def _acc_cb(self, name: str):
     def fn():
       if self._armed:
+        A.join_dw_stream()  # the buffer may still be written on the weight-gradient side stream
         self._ready(name, self.tr.acc[name].buf)
     return fn
 
@@ -140,6 +142,7 @@ class DataParallelTrainer:
       losses.append(loss)
       del out
     self._armed = False
+    A.join_dw_stream()
     for b in self.buckets:  # parameters that received no gradient this step count as zeros
       if len(b.done) < len(b.names):
         for n in b.names:

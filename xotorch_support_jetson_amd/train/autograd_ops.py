@@ -387,7 +387,46 @@ def pad_rows(t: torch.Tensor, mult: int = 128, value=0) -> torch.Tensor:
   return out
 
 
+# Weight gradients on a side stream (XOT_DW_STREAM=0: inline).  dW is off the backward's critical path (only the
+# optimizer step reads it), so the dW GEMMs and their relayouts run beside the dX chain: the tail rounds of one
+# GEMM (qkv dW: 384 tiles = 1.5 rounds of 256 CUs; down dX / dW: 3.5 rounds) and the chain's memory-bound kernels
+# (SiLU / RMSNorm / attention backward, relayouts) fill each other's idle CUs.  Every reader of a GradAcc buffer
+# on the main stream joins first (join_dw_stream: trainer.grads, the optimizer step, the data-parallel buckets).
+DW_STREAM = os.environ.get("XOT_DW_STREAM", "1") != "0"
+_DW_STREAMS: dict = {}
+
+
+def _dw_stream(dev: torch.device):
+  s = _DW_STREAMS.get(dev.index)
+  if s is None:
+    s = _DW_STREAMS[dev.index] = torch.cuda.Stream(device=dev)
+  return s
+
+
+def join_dw_stream() -> None:
+  """The current stream waits for every weight gradient queued on the side streams so far."""
+  for s in _DW_STREAMS.values():
+    torch.cuda.current_stream(s.device).wait_stream(s)
+
+
 def own_dw(dy: torch.Tensor, x: torch.Tensor, acc: "GradAcc") -> None:
+  """acc.buf (+)= dY^T X on the own tiles (on the side stream when DW_STREAM), then acc.cb."""
+  if not (DW_STREAM and dy.is_cuda):
+    _own_dw(dy, x, acc)
+    if acc.cb is not None:
+      acc.cb()
+    return
+  side = _dw_stream(dy.device)
+  side.wait_stream(torch.cuda.current_stream(dy.device))  # dy and x are ready
+  with torch.cuda.stream(side):
+    _own_dw(dy, x, acc)
+  dy.record_stream(side)  # allocated on the main stream, read by the side stream: no reuse before it ran
+  x.record_stream(side)
+  if acc.cb is not None:
+    acc.cb()  # on the main stream: a callback that reads acc.buf joins the side stream first
+
+
+def _own_dw(dy: torch.Tensor, x: torch.Tensor, acc: "GradAcc") -> None:
   """acc.buf (+)= dY^T X on the own tiles: dY^T [N, T] row-major and shuffle(X^T) [K, T] need T % 128, so ragged
   token counts (the reference's batch-size-1 JSONL lengths) are zero-padded to 128 rows first."""
   from ..ops.linear import linear
@@ -408,7 +447,8 @@ class OwnLinearFn(torch.autograd.Function):
     backward  dX = dY . shuffle(W^T)^T
               dW = dY^T . shuffle(X^T)^T into the GradAcc buffer (plain store on the first micro-batch of a
                    step, residual epilogue acc += ... after), with dY^T and shuffle(X^T) built per micro-batch
-                   by csrc/layout.hip (about 2 x T x (N + K) x 2 bytes each).  (A token-major TN GEMM reading dY
+                   by csrc/layout.hip (about 2 x T x (N + K) x 2 bytes each), on the weight-gradient side
+                   stream (DW_STREAM above).  (A token-major TN GEMM reading dY
                    and X as they are, with transposed LDS reads, measured 5-20 % slower than relayout + the
                    pre-shuffled tile, profiles/r4/train/dw_gemm_tn_vs_relayout_vs_hipblaslt.json.)"""
 
@@ -430,8 +470,6 @@ class OwnLinearFn(torch.autograd.Function):
     dy = dy.contiguous()
     dx = linear(dy, tw.wts)
     own_dw(dy, x, acc)
-    if acc.cb is not None:
-      acc.cb()
     return dx, None, None, (dy if ctx.has_h else None), None
 
 

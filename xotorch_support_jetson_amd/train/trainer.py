@@ -313,6 +313,7 @@ class ShardTrainer:
 
   def grads(self) -> Dict[str, torch.Tensor]:
     """The accumulated gradients of this step: fused buffers and .grad of the other parameters."""
+    A.join_dw_stream()
     out = {k: a.buf for k, a in self.acc.items() if not a.fresh}
     for k, p in self.params.items():
       if k not in out and p.grad is not None:
