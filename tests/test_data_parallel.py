@@ -91,3 +91,36 @@ def test_data_parallel_matches_single_process(split):
     # whose tiny gradient differs in sign between the two bf16 accumulation orders flip individually)
     rel = ((d_dp - d_ref).abs().mean() / (d_ref.abs().mean() + 1e-12)).item()
     assert rel < 0.05, (k, rel)
+
+
+@pytest.mark.gpu
+def test_data_parallel_gpu_side_stream_matches_pipeline(monkeypatch):
+  """On the GPU the projections' weight gradients (and the untied LM head's) accumulate on a side stream
+  (train/autograd_ops.py DW_STREAM); the data-parallel buckets copy them out in the last micro-batch's backward,
+  after joining that stream.  One rank's DataParallelTrainer == the pipeline trainer (side stream on and off)."""
+  from xotorch_support_jetson_amd.parallel.comm import LoopbackTransport
+  from xotorch_support_jetson_amd.parallel.data_parallel import DataParallelTrainer
+  import xotorch_support_jetson_amd.train.autograd_ops as A
+  dev = torch.device("cuda", 0)
+  c = PRESETS[MODEL]
+  sh = Shard(MODEL, 0, c.num_layers - 1, c.num_layers)
+
+  def run(kind, side):
+    monkeypatch.setattr(A, "DW_STREAM", side)
+    tr = ShardTrainer(random_weights(c, sh, "cpu", seed=3), dev, lr=LR)
+    assert "lm_head" in tr.acc or "lm_head" not in tr.params
+    pt = DataParallelTrainer(tr, 0, 1, bucket_mb=0.25) if kind == "dp" else PipelineTrainer(tr, 0, 1, LoopbackTransport(0, 1))
+    losses = [pt.step(_batches(3, 7)) for _ in range(2)]
+    torch.cuda.synchronize()
+    return losses, {k: v.float().cpu() for k, v in tr.master.items()}
+
+  init = _trainer().master
+  ref_l, ref_m = run("pp", False)
+  for kind, side in (("dp", True), ("pp", True), ("dp", False)):
+    got_l, got_m = run(kind, side)
+    for a, b in zip(got_l, ref_l):
+      assert abs(a - b) < 1e-3 * max(1.0, abs(b)), (kind, side, got_l, ref_l)
+    for k, v in ref_m.items():
+      d_ref, d = v - init[k], got_m[k] - init[k]
+      rel = ((d - d_ref).abs().mean() / (d_ref.abs().mean() + 1e-12)).item()
+      assert rel < 0.05, (kind, side, k, rel)

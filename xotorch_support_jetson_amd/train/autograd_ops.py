@@ -409,11 +409,11 @@ def join_dw_stream() -> None:
     torch.cuda.current_stream(s.device).wait_stream(s)
 
 
-def own_dw(dy: torch.Tensor, x: torch.Tensor, acc: "GradAcc") -> None:
-  """acc.buf (+)= dY^T X on the own tiles (on the side stream when DW_STREAM), then acc.cb."""
+def own_dw(dy: torch.Tensor, x: torch.Tensor, acc: "GradAcc", cb: bool = True) -> None:
+  """acc.buf (+)= dY^T X on the own tiles (on the side stream when DW_STREAM), then acc.cb (if `cb`)."""
   if not (DW_STREAM and dy.is_cuda):
     _own_dw(dy, x, acc)
-    if acc.cb is not None:
+    if cb and acc.cb is not None:
       acc.cb()
     return
   side = _dw_stream(dy.device)
@@ -422,7 +422,7 @@ def own_dw(dy: torch.Tensor, x: torch.Tensor, acc: "GradAcc") -> None:
     _own_dw(dy, x, acc)
   dy.record_stream(side)  # allocated on the main stream, read by the side stream: no reuse before it ran
   x.record_stream(side)
-  if acc.cb is not None:
+  if cb and acc.cb is not None:
     acc.cb()  # on the main stream: a callback that reads acc.buf joins the side stream first
 
 
@@ -603,10 +603,12 @@ class LmHeadCEFn(torch.autograd.Function):
   tokens; per chunk the fp32 logits come from the own GEMM, ce_fwd / ce_bwd give the loss and dlogits (bf16),
   and -- the loss being the last op, its upstream gradient a scalar -- dX_c = dlogits_c . head and
   dHead += dlogits_c^T . X_c are formed right there, so the backward only scales the saved gradients.
-  Peak memory: one [chunk, V] fp32 logits block + its bf16 gradient."""
+  Peak memory: one [chunk, V] fp32 logits block + its bf16 gradient.  With a GradAcc `acc` (an untied head) the
+  dHead GEMMs accumulate straight into it through own_dw -- on the weight-gradient side stream, beside the rest of
+  the backward -- and the head gets no autograd gradient (no [V, D] add per micro-batch)."""
 
   @staticmethod
-  def forward(ctx, xn, head, tw, targets, weights, chunk):
+  def forward(ctx, xn, head, tw, targets, weights, chunk, acc=None):
     from ..ops.linear import linear
     T0 = xn.shape[0]
     # ragged token counts: zero rows with ignored targets (their dlogits rows are zero) up to a multiple of 128,
@@ -616,7 +618,7 @@ class LmHeadCEFn(torch.autograd.Function):
     T, D = xn.shape
     C = require()
     dxn = torch.empty_like(xn)
-    dhead = torch.empty(head.shape, dtype=torch.bfloat16, device=xn.device)
+    dhead = torch.empty(head.shape if acc is None else (0,), dtype=torch.bfloat16, device=xn.device)
     total = torch.zeros((), dtype=torch.float32, device=xn.device)
     for i, r0 in enumerate(range(0, T, chunk)):
       r1 = min(T, r0 + chunk)
@@ -632,11 +634,17 @@ class LmHeadCEFn(torch.autograd.Function):
       C.ce_bwd(logits, tc, lse, wc, dl)
       del logits
       linear(dl, tw.wts, out=dxn[r0:r1])
+      if acc is not None:
+        own_dw(dl, xc, acc, cb=False)
+        continue
       dlt, xts = relayout(dl, 2), relayout(xc, 1)  # dlogits^T [V, c], shuffle(X_c^T) [D, c]
       if i == 0:
         linear(dlt, xts, out=dhead)
       else:
         linear(dlt, xts, residual=dhead, epi="resid", out=dhead)
+    if acc is not None and acc.cb is not None:
+      acc.cb()
+    ctx.acc = acc
     ctx.save_for_backward(dxn[:T0], dhead)
     return total
 
@@ -644,13 +652,16 @@ class LmHeadCEFn(torch.autograd.Function):
   def backward(ctx, g):
     dxn, dhead = ctx.saved_tensors
     if not (isinstance(g, torch.Tensor) and g.numel() == 1 and float(g) == 1.0):
+      if ctx.acc is not None:
+        raise RuntimeError("a scaled loss cannot reach the head gradient already accumulated in its GradAcc")
       dxn, dhead = dxn * g.to(dxn.dtype), dhead * g.to(dhead.dtype)
-    return dxn, dhead, None, None, None, None
+    return dxn, (None if ctx.acc is not None else dhead), None, None, None, None, None
 
 
-def lm_head_ce(xn, head, tw, targets, weights, chunk: int = 1024):
-  """xn [T, D] bf16, head [V, D] (its TrainWeight tw), targets [T] int32 (< 0 ignored), weights [T] fp32."""
-  return LmHeadCEFn.apply(xn.contiguous(), head, tw, targets, weights, chunk)
+def lm_head_ce(xn, head, tw, targets, weights, chunk: int = 1024, acc=None):
+  """xn [T, D] bf16, head [V, D] (its TrainWeight tw), targets [T] int32 (< 0 ignored), weights [T] fp32;
+  `acc`: the head's GradAcc (then the head gradient is accumulated there, not returned)."""
+  return LmHeadCEFn.apply(xn.contiguous(), head, tw, targets, weights, chunk, acc)
 
 
 class QKVSplitFn(torch.autograd.Function):

@@ -122,6 +122,8 @@ class ShardTrainer:
       t = A.TrainWeight(self.params[self.head_name])
       if t.ok:
         self.tw[self.head_name] = t
+        if self.head_name == "lm_head":  # untied: the fused CE accumulates dHead into a GradAcc (A.LmHeadCEFn)
+          self.acc["lm_head"] = A.GradAcc("lm_head", self.params["lm_head"])
     self.master = {k: p.detach().float().clone() for k, p in self.params.items()}
     self._pb_stale: set = set()  # bf16 params the fused AdamW did not rewrite (refresh_params)
     self.m = {k: torch.zeros_like(v) for k, v in self.master.items()}
@@ -354,7 +356,7 @@ class ShardTrainer:
     tgt = torch.where(mask, y, torch.full_like(y, -100)).view(-1).to(torch.int32)
     w = torch.full((B * L,), 1.0 / denom, device=self.device, dtype=torch.float32)
     name = self.head_name
-    return A.lm_head_ce(xn.reshape(B * L, D), self.params[name], self.tw[name], tgt, w, CE_CHUNK)
+    return A.lm_head_ce(xn.reshape(B * L, D), self.params[name], self.tw[name], tgt, w, CE_CHUNK, self.acc.get(name))
 
   # ------------------------------------------------------------------ accumulate / apply
   # (pipeline schedules: forward every micro-batch, backward every micro-batch, then one optimizer
@@ -461,7 +463,7 @@ class ShardTrainer:
         # copy only where something may still read it: a projection without a GradAcc runs torch's matmul on it,
         # the LM head / tied embedding is read by the embedding lookup and the unfused logits path.  Projections
         # with a GradAcc read only the images while training; refresh_params() catches their copies up on demand.
-        keep = k not in self.acc
+        keep = k not in self.acc or k == self.head_name
         require().adamw_tiled(p, g.contiguous(), m, v, pb.data if keep else None, tw.ws, tw.wts, self.lr, b1, b2,
                               self.eps, self.wd, self.step_count, scale)
         fused.add(k)
