@@ -751,6 +751,146 @@ __global__ __launch_bounds__(256) void attn_train_transpose_kernel(const uint16_
   }
 }
 
+// dK / dV without the P^T / dS^T round trip through LDS (v2).  S = Q.K^T and dP = dO.V^T are computed with the
+// query on the accumulator row (lane (g, c) holds queries 16 t + 4 g + r of key c), so two 16-query sub-tiles
+// give a lane the 8 values of B-operand rows 8 g .. 8 g + 7 of dV^T += dO^T . P and dK^T += Q^T . dS -- in
+// the k order "sub-tile 2 kk rows 4 g .. 4 g + 3, then sub-tile 2 kk + 1 rows 4 g .. 4 g + 3".  The transposed
+// Q^T / dO^T tiles are staged in LDS in that same permuted token order, so their A fragments stay single
+// 16-byte reads.  v1 stored 32 two-byte P^T / dS^T values per lane and query tile and read them back (about a
+// quarter of the kernel's LDS cycles); v2 drops those and 37 KB of LDS.
+__device__ __forceinline__ int dkdv_perm_pos(int cc) {  // 8-token chunk cc of a 64-token tile -> its first slot
+  const int kk = cc >> 2, w = cc & 3;                  // tokens 32 kk + 8 w .. +7: (t' = w / 2, g = 2 (w % 2) ..)
+  return 32 * kk + 8 * (2 * (w & 1)) + 4 * (w >> 1);   // low 4 tokens here, high 4 at +8
+}
+template <int DH, int NT>
+__device__ __forceinline__ void trans_store_perm(const TransTile<DH, NT>& t, uint16_t* dst, int TLD) {
+#pragma unroll
+  for (int i = 0; i < TransTile<DH, NT>::N; ++i) {
+    const int q = threadIdx.x + NT * i, d = q / (TT / 8), cc = q % (TT / 8);
+    uint16_t* p = dst + d * TLD + dkdv_perm_pos(cc);
+    const s16x8 v = t.v[i];
+    *reinterpret_cast<s16x4*>(p) = s16x4{v[0], v[1], v[2], v[3]};
+    *reinterpret_cast<s16x4*>(p + 8) = s16x4{v[4], v[5], v[6], v[7]};
+  }
+}
+
+template <int DH>
+__global__ __launch_bounds__(64 * DKW) void attn_train_dkdv_v2_kernel(const uint16_t* __restrict__ Q, long ldq,
+                                                                   const uint16_t* __restrict__ QT,
+                                                                   const uint16_t* __restrict__ K, long ldk,
+                                                                   const uint16_t* __restrict__ V, long ldv,
+                                                                   const uint16_t* __restrict__ dO, long lddo,
+                                                                   const uint16_t* __restrict__ dOT, int Lp,
+                                                                   const float* __restrict__ lse2,
+                                                                   const float* __restrict__ delta,
+                                                                   float* __restrict__ wk, float* __restrict__ wv,
+                                                                   int L, int H, int Hkv, float scale) {
+  constexpr int KS = DH / 32, NDT = DH / 16;
+  constexpr int RLD = DH + 8, TLD = TT + 8;
+  extern __shared__ __attribute__((aligned(16))) uint16_t sm[];
+  uint16_t* qs = sm;                 // Q rows       [64][RLD]
+  uint16_t* ds_ = qs + TT * RLD;     // dO rows      [64][RLD]
+  uint16_t* qt_ = ds_ + TT * RLD;    // Q^T          [DH][TLD], tokens in dkdv_perm_pos order
+  uint16_t* dt_ = qt_ + DH * TLD;    // dO^T         [DH][TLD], same order
+  float* ld_ = reinterpret_cast<float*>(dt_ + DH * TLD);  // lse2[64], delta[64]
+  const int G = H / Hkv;
+  const int hq = blockIdx.x, kvh = hq / G, hh = hq % G, kt = blockIdx.y, b = blockIdx.z;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
+  const int k0 = kt * DKT, krow = k0 + 16 * wave;
+  const float sl = scale * L2E;
+  const int qt0 = k0 / TT;
+  const int nq = (L + TT - 1) / TT, iters = nq - qt0;
+  const int key = krow + c;  // this lane's key (B-operand column of every product)
+
+  RowsTile<DH, 64 * DKW> qr, dr;
+  TransTile<DH, 64 * DKW> qtr, dtr;
+  float lsv = 0.f, dlv = 0.f;
+  auto load = [&](int it) {
+    const int h = hq, q0 = (qt0 + it) * TT;
+    qr.load(Q + (long)b * L * ldq + h * DH, ldq, q0, L);
+    dr.load(dO + (long)b * L * lddo + h * DH, lddo, q0, L);
+    qtr.load(QT + ((long)b * H + h) * DH * Lp, Lp, q0);
+    dtr.load(dOT + ((long)b * H + h) * DH * Lp, Lp, q0);
+    if (threadIdx.x < TT) {
+      const long idx = ((long)b * H + h) * L + min(q0 + (int)threadIdx.x, L - 1);
+      lsv = lse2[idx];
+      dlv = delta[idx];
+    }
+  };
+
+  s16x8 kf[KS], vf[KS];  // B operands: lane (g, c) = key c, dims 32 s + 8 g .. +7
+  {
+    const long row = (long)b * L + min(key, L - 1);
+    const uint16_t* kp = K + row * ldk + kvh * DH + 8 * g;
+    const uint16_t* vp = V + row * ldv + kvh * DH + 8 * g;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      kf[s] = ld16(kp + 32 * s);
+      vf[s] = ld16(vp + 32 * s);
+    }
+  }
+  f32x4 dkT[NDT], dvT[NDT];  // [dim 16 dt + 4 g + r][key c]
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) dkT[dt] = dvT[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (iters > 0) load(0);
+  for (int it = 0; it < iters; ++it) {
+    const int q0 = (qt0 + it) * TT;
+    __syncthreads();
+    qr.template store<RLD>(qs);
+    dr.template store<RLD>(ds_);
+    trans_store_perm(qtr, qt_, TLD);
+    trans_store_perm(dtr, dt_, TLD);
+    if (threadIdx.x < TT) {
+      ld_[threadIdx.x] = lsv;
+      ld_[TT + threadIdx.x] = dlv;
+    }
+    __syncthreads();
+    if (it + 1 < iters) load(it + 1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {  // 32 queries: sub-tiles 2 kk and 2 kk + 1
+      s16x8 pa, sa;
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt) {
+        const int t = 2 * kk + tt;
+        f32x4 st = f32x4{0.f, 0.f, 0.f, 0.f}, dpt = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          st = mfma16(ld16(qs + (16 * t + c) * RLD + 32 * s + 8 * g), kf[s], st);
+          dpt = mfma16(ld16(ds_ + (16 * t + c) * RLD + 32 * s + 8 * g), vf[s], dpt);
+        }
+        const f32x4 lq = *reinterpret_cast<const f32x4*>(ld_ + 16 * t + 4 * g);
+        const f32x4 dq = *reinterpret_cast<const f32x4*>(ld_ + TT + 16 * t + 4 * g);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int qi = q0 + 16 * t + 4 * g + r;
+          const float p = (key <= qi && qi < L) ? exp2f(st[r] * sl - lq[r]) : 0.f;
+          pa[4 * tt + r] = (short)f2bf(p);
+          sa[4 * tt + r] = (short)f2bf(p * (dpt[r] - dq[r]));
+        }
+      }
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) {
+        dvT[dt] = mfma16(ld16(dt_ + (16 * dt + c) * TLD + 32 * kk + 8 * g), pa, dvT[dt]);
+        dkT[dt] = mfma16(ld16(qt_ + (16 * dt + c) * TLD + 32 * kk + 8 * g), sa, dkT[dt]);
+      }
+    }
+  }
+  if (key >= L) return;
+  const long slab = (long)hh * ((long)gridDim.z * L) * (Hkv * DH);
+  const long off = slab + ((long)b * L + key) * (Hkv * DH) + kvh * DH + 4 * g;
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) {
+    *reinterpret_cast<f32x4*>(wk + off + 16 * dt) = dkT[dt];
+    *reinterpret_cast<f32x4*>(wv + off + 16 * dt) = dvT[dt];
+  }
+}
+
+template <int DH>
+static size_t dkdv_v2_smem() {
+  return (size_t)(2 * TT * (DH + 8) + 2 * DH * (TT + 8)) * 2 + 2 * TT * sizeof(float);
+}
+
 template <int DH>
 static size_t dkdv_smem() {
   return (size_t)(2 * TT * (DH + 8) + 2 * DH * (TT + 8) + DKW * 2 * 16 * (TT + 8)) * 2 + 2 * TT * sizeof(float);
@@ -830,16 +970,29 @@ int launch_attn_train_bwd(const uint16_t* q, long ldq, const uint16_t* qt, const
   if (ws == nullptr || ws_elems < 2 * (long)(H / Hkv) * slab) return -1;
   float *wk = ws, *wv = ws + (long)(H / Hkv) * slab;
   dim3 gq(H, (L + TT - 1) / TT, B), gk(H, (L + DKT - 1) / DKT, B);
+  static const bool dkdv_v1 = [] {  // XOT_TRAIN_DKDV_V1=1: the P^T-through-LDS kernel (A/B)
+    const char* e = getenv("XOT_TRAIN_DKDV_V1");
+    return e != nullptr && e[0] == '1';
+  }();
 #define XOT_BWD(DHV)                                                                                                \
   do {                                                                                                              \
     attn_train_dq_kernel<DHV><<<gq, 256, 0, s>>>(q, ldq, k, ldk, kt, v, ldv, o, ldo, dout, lddo, Lp, lse2, delta,   \
                                                  dq, lddq, L, H, Hkv, scale);                                       \
-    static bool attr = hipFuncSetAttribute((const void*)attn_train_dkdv_kernel<DHV>,                               \
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)dkdv_smem<DHV>()) ==    \
-                       hipSuccess;                                                                                  \
-    (void)attr;                                                                                                     \
-    attn_train_dkdv_kernel<DHV><<<gk, 64 * DKW, dkdv_smem<DHV>(), s>>>(q, ldq, qt, k, ldk, v, ldv, dout, lddo, doutt, Lp, \
-                                                                  lse2, delta, wk, wv, L, H, Hkv, scale);           \
+    if (dkdv_v1 || DHV > 128) { /* 192: v2 spills more than v1 */                                               \
+      static bool attr = hipFuncSetAttribute((const void*)attn_train_dkdv_kernel<DHV>,                             \
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)dkdv_smem<DHV>()) ==  \
+                         hipSuccess;                                                                                \
+      (void)attr;                                                                                                   \
+      attn_train_dkdv_kernel<DHV><<<gk, 64 * DKW, dkdv_smem<DHV>(), s>>>(q, ldq, qt, k, ldk, v, ldv, dout, lddo,    \
+                                                                    doutt, Lp, lse2, delta, wk, wv, L, H, Hkv, scale); \
+    } else {                                                                                                        \
+      static bool attr2 = hipFuncSetAttribute((const void*)attn_train_dkdv_v2_kernel<DHV>,                         \
+                                              hipFuncAttributeMaxDynamicSharedMemorySize,                           \
+                                              (int)dkdv_v2_smem<DHV>()) == hipSuccess;                              \
+      (void)attr2;                                                                                                  \
+      attn_train_dkdv_v2_kernel<DHV><<<gk, 64 * DKW, dkdv_v2_smem<DHV>(), s>>>(                                     \
+          q, ldq, qt, k, ldk, v, ldv, dout, lddo, doutt, Lp, lse2, delta, wk, wv, L, H, Hkv, scale);                \
+    }                                                                                                               \
   } while (0)
   if (Dh == 128)
     XOT_BWD(128);
