@@ -886,6 +886,109 @@ __global__ __launch_bounds__(64 * DKW) void attn_train_dkdv_v2_kernel(const uint
   }
 }
 
+// dQ without the dS round trip through LDS (v2, the dkdv v2 idea on the query side): S^T = K.Q^T and
+// dP^T = V.dO^T put the key on the accumulator row (lane (g, c) holds keys 16 t + 4 g + r of query c), two
+// 16-key sub-tiles give a lane the 8 B-operand values of dQ^T += K^T . dS^T, and K^T is staged in the matching
+// permuted key order.  Each lane owns one query, so lse2 / delta are lane scalars.
+template <int DH>
+__global__ __launch_bounds__(256) void attn_train_dq_v2_kernel(const uint16_t* __restrict__ Q, long ldq,
+                                                               const uint16_t* __restrict__ K, long ldk,
+                                                               const uint16_t* __restrict__ KT,
+                                                               const uint16_t* __restrict__ V, long ldv,
+                                                               const uint16_t* __restrict__ O, long ldo,
+                                                               const uint16_t* __restrict__ dO, long lddo, int Lp,
+                                                               const float* __restrict__ lse2,
+                                                               float* __restrict__ delta, uint16_t* __restrict__ dQ,
+                                                               long lddq, int L, int H, int Hkv, float scale) {
+  constexpr int KS = DH / 32, NDT = DH / 16;
+  constexpr int KLD = DH + 8, TLD = TT + 8;
+  __shared__ __attribute__((aligned(16))) uint16_t ks[TT * KLD];   // K rows
+  __shared__ __attribute__((aligned(16))) uint16_t vs[TT * KLD];   // V rows
+  __shared__ __attribute__((aligned(16))) uint16_t kt_[DH * TLD];  // K^T, keys in dkdv_perm_pos order
+  const int h = blockIdx.x, qt = gridDim.y - 1 - blockIdx.y, b = blockIdx.z;
+  const int kvh = h / (H / Hkv);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
+  const int q0 = qt * TT, qrow = q0 + 16 * wave, qi = qrow + c;  // this lane's query
+  const uint16_t* Kb = K + (long)b * L * ldk + kvh * DH;
+  const uint16_t* Vb = V + (long)b * L * ldv + kvh * DH;
+  const uint16_t* KTb = KT + ((long)b * Hkv + kvh) * DH * Lp;
+  const float sl = scale * L2E;
+
+  RowsTile<DH> kr, vr;
+  TransTile<DH> ktr;
+  kr.load(Kb, ldk, 0, L);
+  vr.load(Vb, ldv, 0, L);
+  ktr.load(KTb, Lp, 0);
+
+  s16x8 qf[KS], df[KS];  // B operands: lane (g, c) = query c, dims 32 s + 8 g .. +7
+  float dsum = 0.f;
+  {
+    const long row = (long)b * L + min(qi, L - 1);
+    const uint16_t* qp = Q + row * ldq + h * DH + 8 * g;
+    const uint16_t* dp = dO + row * lddo + h * DH + 8 * g;
+    const uint16_t* opp = O + row * ldo + h * DH + 8 * g;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      qf[s] = ld16(qp + 32 * s);
+      df[s] = ld16(dp + 32 * s);
+      const s16x8 ov = ld16(opp + 32 * s);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dsum += bf2f(df[s][e]) * bf2f(ov[e]);
+    }
+  }
+  dsum += __shfl_xor(dsum, 16, 64);  // delta of query c, in every lane group
+  dsum += __shfl_xor(dsum, 32, 64);
+  if (g == 0 && qi < L) delta[((long)b * H + h) * L + qi] = dsum;
+  const float lse = lse2[((long)b * H + h) * L + min(qi, L - 1)];
+  f32x4 dqT[NDT];  // [dim 16 dt + 4 g + r][query c]
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) dqT[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int kt = 0; kt <= qt; ++kt) {
+    const int k0 = kt * TT;
+    __syncthreads();
+    kr.template store<KLD>(ks);
+    vr.template store<KLD>(vs);
+    trans_store_perm(ktr, kt_, TLD);
+    __syncthreads();
+    if (kt < qt) {
+      kr.load(Kb, ldk, k0 + TT, L);
+      vr.load(Vb, ldv, k0 + TT, L);
+      ktr.load(KTb, Lp, k0 + TT);
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {  // 32 keys: sub-tiles 2 kk and 2 kk + 1
+      s16x8 sa;
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt) {
+        const int t = 2 * kk + tt;
+        f32x4 sc = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          sc = mfma16(ld16(ks + (16 * t + c) * KLD + 32 * s + 8 * g), qf[s], sc);
+          dp = mfma16(ld16(vs + (16 * t + c) * KLD + 32 * s + 8 * g), df[s], dp);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = k0 + 16 * t + 4 * g + r;
+          const float p = (key <= qi && key < L) ? exp2f(sc[r] * sl - lse) : 0.f;
+          sa[4 * tt + r] = (short)f2bf(p * (dp[r] - dsum));
+        }
+      }
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+        dqT[dt] = mfma16(ld16(kt_ + (16 * dt + c) * TLD + 32 * kk + 8 * g), sa, dqT[dt]);
+    }
+  }
+  if (qi >= L) return;
+  uint16_t* op = dQ + ((long)b * L + qi) * lddq + h * DH + 4 * g;
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt)
+    *reinterpret_cast<s16x4*>(op + 16 * dt) =
+        s16x4{(short)f2bf(dqT[dt][0] * scale), (short)f2bf(dqT[dt][1] * scale), (short)f2bf(dqT[dt][2] * scale),
+              (short)f2bf(dqT[dt][3] * scale)};
+}
+
 template <int DH>
 static size_t dkdv_v2_smem() {
   return (size_t)(2 * TT * (DH + 8) + 2 * DH * (TT + 8)) * 2 + 2 * TT * sizeof(float);
@@ -974,10 +1077,18 @@ int launch_attn_train_bwd(const uint16_t* q, long ldq, const uint16_t* qt, const
     const char* e = getenv("XOT_TRAIN_DKDV_V1");
     return e != nullptr && e[0] == '1';
   }();
+  static const bool dq_v1 = [] {  // XOT_TRAIN_DQ_V1=1: the dS-through-LDS kernel (A/B)
+    const char* e = getenv("XOT_TRAIN_DQ_V1");
+    return e != nullptr && e[0] == '1';
+  }();
 #define XOT_BWD(DHV)                                                                                                \
   do {                                                                                                              \
-    attn_train_dq_kernel<DHV><<<gq, 256, 0, s>>>(q, ldq, k, ldk, kt, v, ldv, o, ldo, dout, lddo, Lp, lse2, delta,   \
-                                                 dq, lddq, L, H, Hkv, scale);                                       \
+    if (dq_v1)                                                                                                     \
+      attn_train_dq_kernel<DHV><<<gq, 256, 0, s>>>(q, ldq, k, ldk, kt, v, ldv, o, ldo, dout, lddo, Lp, lse2, delta, \
+                                                   dq, lddq, L, H, Hkv, scale);                                     \
+    else                                                                                                            \
+      attn_train_dq_v2_kernel<DHV><<<gq, 256, 0, s>>>(q, ldq, k, ldk, kt, v, ldv, o, ldo, dout, lddo, Lp, lse2,     \
+                                                      delta, dq, lddq, L, H, Hkv, scale);                           \
     if (dkdv_v1 || DHV > 128) { /* 192: v2 spills more than v1 */                                               \
       static bool attr = hipFuncSetAttribute((const void*)attn_train_dkdv_kernel<DHV>,                             \
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)dkdv_smem<DHV>()) ==  \
