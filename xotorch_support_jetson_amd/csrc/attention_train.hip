@@ -4,19 +4,21 @@
 // K / V [B*L, ldk / ldv] holding Hkv heads (GQA: query head h reads KV head h / (H / Hkv)).
 // Sequences are right-padded to L; causality alone keeps valid queries off padded keys.
 //
-// Operands that MFMA reads "by column" (V for P.V, K for dS.K, Q / dO for the dK / dV products) come from
-// pre-transposed [B, heads, DH, Lp] images (attn_train_transpose_kernel), so every staging copy is 16
-// bytes wide; the next tile is loaded into registers under the current tile's math.
+// Operands that MFMA reads "by column": V for P.V comes from a pre-transposed [B, heads, DH, Lp] image
+// (attn_train_transpose_kernel); the backward's K (dS.K) and Q / dO (dK / dV products) are read transposed out of
+// the row tiles already in LDS (ds_read_b64_tr_b16, the v2 kernels; v1 staged transposed images of them too).
+// The next tile is loaded into registers under the current tile's math.
 //
 //  fwd   grid (L/64, H, B): 4 waves x 16 query rows.  Per 64-key tile: K rows and V^T staged in LDS,
 //        S = Q.K^T, online softmax in the log2 domain, P through LDS into P.V.  Writes O and the
 //        per-row log2-sum-exp (lse2 = max + log2 sum, scores pre-scaled by scale*log2(e)).
-//  dq    grid (L/64, H, B): recomputes P from lse2, dP = dO.V^T, dS = P (dP - delta); dQ += dS.K.
-//        Also computes delta = rowsum(dO * O) for its rows and stores it for the dK/dV pass.
-//  dkdv  grid (L/64, Hkv, B): 4 waves x 16 keys; sweeps the G query heads x query tiles >= its key
-//        tile: S^T = K.Q^T, dP^T = V.dO^T with the query on the lane (lse2 / delta are lane-local);
-//        P^T and dS^T go through LDS into dV += P^T.dO and dK += dS^T.Q.  dK / dV need no cross-
-//        workgroup sum (each workgroup owns its keys), dQ needs none either (separate pass).
+//  dq    grid (H, L/64, B): recomputes P from lse2, dP = dO.V^T, dS = P (dP - delta); dQ += dS.K.
+//        Also computes delta = rowsum(dO * O) for its rows and stores it for the dK/dV pass.  v2: S^T / dP^T
+//        with the key on the accumulator row, dS^T stays in registers as the B operand of dQ^T += K^T.dS^T.
+//  dkdv  grid (H, L/128, B): 8 waves x 16 keys per query head; sweeps the query tiles >= its key tile; fp32
+//        partials per query head, summed over the GQA group by attn_train_dkdv_reduce_kernel.  v1: S^T, dP^T
+//        with the query on the lane, P^T / dS^T through LDS into dV += P^T.dO, dK += dS^T.Q; v2: S, dP with
+//        the query on the accumulator row, P / dS stay in registers as the B operands of dV^T / dK^T.
 //
 // Replaces torch SDPA in the reference-parity train step (the reference never implemented training:
 // xotorch/inference/inference_engine.py:34-35; the torchtune attention it would have used is
@@ -754,25 +756,25 @@ __global__ __launch_bounds__(256) void attn_train_transpose_kernel(const uint16_
 // dK / dV without the P^T / dS^T round trip through LDS (v2).  S = Q.K^T and dP = dO.V^T are computed with the
 // query on the accumulator row (lane (g, c) holds queries 16 t + 4 g + r of key c), so two 16-query sub-tiles
 // give a lane the 8 values of B-operand rows 8 g .. 8 g + 7 of dV^T += dO^T . P and dK^T += Q^T . dS -- in
-// the k order "sub-tile 2 kk rows 4 g .. 4 g + 3, then sub-tile 2 kk + 1 rows 4 g .. 4 g + 3".  The transposed
-// Q^T / dO^T tiles are staged in LDS in that same permuted token order, so their A fragments stay single
-// 16-byte reads.  v1 stored 32 two-byte P^T / dS^T values per lane and query tile and read them back (about a
-// quarter of the kernel's LDS cycles); v2 drops those and 37 KB of LDS.
-__device__ __forceinline__ int dkdv_perm_pos(int cc) {  // 8-token chunk cc of a 64-token tile -> its first slot
-  const int kk = cc >> 2, w = cc & 3;                  // tokens 32 kk + 8 w .. +7: (t' = w / 2, g = 2 (w % 2) ..)
-  return 32 * kk + 8 * (2 * (w & 1)) + 4 * (w >> 1);   // low 4 tokens here, high 4 at +8
+// the k order "sub-tile 2 kk rows 4 g .. 4 g + 3, then sub-tile 2 kk + 1 rows 4 g .. 4 g + 3".  That is the
+// order two transposed LDS reads (tr_frag) deliver the Q^T / dO^T A fragments in, straight from the row-major
+// Q / dO tiles the S and dP products read: no transposed images in HBM or LDS.  v1 stored 32 two-byte P^T / dS^T
+// values per lane and query tile and read them back, and staged Q^T / dO^T tiles besides; v2 needs a third of
+// v1's LDS.
+typedef __attribute__((address_space(3))) s16x4* lds_s16x4_t;
+// The A operand X^T[col 16 dt + c][rows in the permuted order] of a row-major LDS tile X [64][ld]: two
+// ds_read_b64_tr_b16 (4 rows x 16 columns each, column c to lane c of the 16-lane group g): rows 32 kk + 4 g .. +3
+// (elements 0..3) and rows 32 kk + 16 + 4 g .. +3 (elements 4..7).  Lane 4 q + p of the group addresses row q,
+// columns 4 p .. 4 p + 3 of its block.  A row stride of 8 (mod 64) dwords keeps both reads conflict-free.
+__device__ __forceinline__ s16x8 tr_frag(const uint16_t* X, int ld, int kk, int dt, int g, int c) {
+  const uint16_t* p = X + (32 * kk + 4 * g + (c >> 2)) * ld + 16 * dt + 4 * (c & 3);
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t)(p));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t)(p + 16 * ld));
+  return s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
-template <int DH, int NT>
-__device__ __forceinline__ void trans_store_perm(const TransTile<DH, NT>& t, uint16_t* dst, int TLD) {
-#pragma unroll
-  for (int i = 0; i < TransTile<DH, NT>::N; ++i) {
-    const int q = threadIdx.x + NT * i, d = q / (TT / 8), cc = q % (TT / 8);
-    uint16_t* p = dst + d * TLD + dkdv_perm_pos(cc);
-    const s16x8 v = t.v[i];
-    *reinterpret_cast<s16x4*>(p) = s16x4{v[0], v[1], v[2], v[3]};
-    *reinterpret_cast<s16x4*>(p + 8) = s16x4{v[4], v[5], v[6], v[7]};
-  }
-}
+// Row stride of those tiles: DH + 16 elements = 72 dwords (DH 128) or 40 (DH 64, 192) mod 64, so the 8 rows a
+// 32-lane half reads sit on 8 distinct 8-bank groups (and the 16x16x32 row reads stay conflict-free too).
+__host__ __device__ constexpr int tr_ld(int dh) { return dh + 16; }
 
 template <int DH>
 __global__ __launch_bounds__(64 * DKW) void attn_train_dkdv_v2_kernel(const uint16_t* __restrict__ Q, long ldq,
@@ -786,13 +788,11 @@ __global__ __launch_bounds__(64 * DKW) void attn_train_dkdv_v2_kernel(const uint
                                                                    float* __restrict__ wk, float* __restrict__ wv,
                                                                    int L, int H, int Hkv, float scale) {
   constexpr int KS = DH / 32, NDT = DH / 16;
-  constexpr int RLD = DH + 8, TLD = TT + 8;
+  constexpr int RLD = tr_ld(DH);
   extern __shared__ __attribute__((aligned(16))) uint16_t sm[];
-  uint16_t* qs = sm;                 // Q rows       [64][RLD]
-  uint16_t* ds_ = qs + TT * RLD;     // dO rows      [64][RLD]
-  uint16_t* qt_ = ds_ + TT * RLD;    // Q^T          [DH][TLD], tokens in dkdv_perm_pos order
-  uint16_t* dt_ = qt_ + DH * TLD;    // dO^T         [DH][TLD], same order
-  float* ld_ = reinterpret_cast<float*>(dt_ + DH * TLD);  // lse2[64], delta[64]
+  uint16_t* qs = sm;                 // Q rows       [64][RLD] (row reads for S, transposed reads for dK)
+  uint16_t* ds_ = qs + TT * RLD;     // dO rows      [64][RLD] (row reads for dP, transposed reads for dV)
+  float* ld_ = reinterpret_cast<float*>(ds_ + TT * RLD);  // lse2[64], delta[64]
   const int G = H / Hkv;
   const int hq = blockIdx.x, kvh = hq / G, hh = hq % G, kt = blockIdx.y, b = blockIdx.z;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
@@ -803,14 +803,11 @@ __global__ __launch_bounds__(64 * DKW) void attn_train_dkdv_v2_kernel(const uint
   const int key = krow + c;  // this lane's key (B-operand column of every product)
 
   RowsTile<DH, 64 * DKW> qr, dr;
-  TransTile<DH, 64 * DKW> qtr, dtr;
   float lsv = 0.f, dlv = 0.f;
   auto load = [&](int it) {
     const int h = hq, q0 = (qt0 + it) * TT;
     qr.load(Q + (long)b * L * ldq + h * DH, ldq, q0, L);
     dr.load(dO + (long)b * L * lddo + h * DH, lddo, q0, L);
-    qtr.load(QT + ((long)b * H + h) * DH * Lp, Lp, q0);
-    dtr.load(dOT + ((long)b * H + h) * DH * Lp, Lp, q0);
     if (threadIdx.x < TT) {
       const long idx = ((long)b * H + h) * L + min(q0 + (int)threadIdx.x, L - 1);
       lsv = lse2[idx];
@@ -839,8 +836,6 @@ __global__ __launch_bounds__(64 * DKW) void attn_train_dkdv_v2_kernel(const uint
     __syncthreads();
     qr.template store<RLD>(qs);
     dr.template store<RLD>(ds_);
-    trans_store_perm(qtr, qt_, TLD);
-    trans_store_perm(dtr, dt_, TLD);
     if (threadIdx.x < TT) {
       ld_[threadIdx.x] = lsv;
       ld_[TT + threadIdx.x] = dlv;
@@ -871,8 +866,8 @@ __global__ __launch_bounds__(64 * DKW) void attn_train_dkdv_v2_kernel(const uint
       }
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt) {
-        dvT[dt] = mfma16(ld16(dt_ + (16 * dt + c) * TLD + 32 * kk + 8 * g), pa, dvT[dt]);
-        dkT[dt] = mfma16(ld16(qt_ + (16 * dt + c) * TLD + 32 * kk + 8 * g), sa, dkT[dt]);
+        dvT[dt] = mfma16(tr_frag(ds_, RLD, kk, dt, g, c), pa, dvT[dt]);
+        dkT[dt] = mfma16(tr_frag(qs, RLD, kk, dt, g, c), sa, dkT[dt]);
       }
     }
   }
@@ -901,24 +896,20 @@ __global__ __launch_bounds__(256) void attn_train_dq_v2_kernel(const uint16_t* _
                                                                float* __restrict__ delta, uint16_t* __restrict__ dQ,
                                                                long lddq, int L, int H, int Hkv, float scale) {
   constexpr int KS = DH / 32, NDT = DH / 16;
-  constexpr int KLD = DH + 8, TLD = TT + 8;
-  __shared__ __attribute__((aligned(16))) uint16_t ks[TT * KLD];   // K rows
+  constexpr int KLD = tr_ld(DH);
+  __shared__ __attribute__((aligned(16))) uint16_t ks[TT * KLD];   // K rows (row reads for S^T, transposed for dQ)
   __shared__ __attribute__((aligned(16))) uint16_t vs[TT * KLD];   // V rows
-  __shared__ __attribute__((aligned(16))) uint16_t kt_[DH * TLD];  // K^T, keys in dkdv_perm_pos order
   const int h = blockIdx.x, qt = gridDim.y - 1 - blockIdx.y, b = blockIdx.z;
   const int kvh = h / (H / Hkv);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
   const int q0 = qt * TT, qrow = q0 + 16 * wave, qi = qrow + c;  // this lane's query
   const uint16_t* Kb = K + (long)b * L * ldk + kvh * DH;
   const uint16_t* Vb = V + (long)b * L * ldv + kvh * DH;
-  const uint16_t* KTb = KT + ((long)b * Hkv + kvh) * DH * Lp;
   const float sl = scale * L2E;
 
   RowsTile<DH> kr, vr;
-  TransTile<DH> ktr;
   kr.load(Kb, ldk, 0, L);
   vr.load(Vb, ldv, 0, L);
-  ktr.load(KTb, Lp, 0);
 
   s16x8 qf[KS], df[KS];  // B operands: lane (g, c) = query c, dims 32 s + 8 g .. +7
   float dsum = 0.f;
@@ -949,12 +940,10 @@ __global__ __launch_bounds__(256) void attn_train_dq_v2_kernel(const uint16_t* _
     __syncthreads();
     kr.template store<KLD>(ks);
     vr.template store<KLD>(vs);
-    trans_store_perm(ktr, kt_, TLD);
     __syncthreads();
     if (kt < qt) {
       kr.load(Kb, ldk, k0 + TT, L);
       vr.load(Vb, ldv, k0 + TT, L);
-      ktr.load(KTb, Lp, k0 + TT);
     }
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {  // 32 keys: sub-tiles 2 kk and 2 kk + 1
@@ -977,7 +966,7 @@ __global__ __launch_bounds__(256) void attn_train_dq_v2_kernel(const uint16_t* _
       }
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt)
-        dqT[dt] = mfma16(ld16(kt_ + (16 * dt + c) * TLD + 32 * kk + 8 * g), sa, dqT[dt]);
+        dqT[dt] = mfma16(tr_frag(ks, KLD, kk, dt, g, c), sa, dqT[dt]);
     }
   }
   if (qi >= L) return;
@@ -991,7 +980,7 @@ __global__ __launch_bounds__(256) void attn_train_dq_v2_kernel(const uint16_t* _
 
 template <int DH>
 static size_t dkdv_v2_smem() {
-  return (size_t)(2 * TT * (DH + 8) + 2 * DH * (TT + 8)) * 2 + 2 * TT * sizeof(float);
+  return (size_t)(2 * TT * tr_ld(DH)) * 2 + 2 * TT * sizeof(float);
 }
 
 template <int DH>
@@ -1081,6 +1070,7 @@ int launch_attn_train_bwd(const uint16_t* q, long ldq, const uint16_t* qt, const
     const char* e = getenv("XOT_TRAIN_DQ_V1");
     return e != nullptr && e[0] == '1';
   }();
+  if ((dq_v1 && kt == nullptr) || (dkdv_v1 && (qt == nullptr || doutt == nullptr))) return -1;
 #define XOT_BWD(DHV)                                                                                                \
   do {                                                                                                              \
     if (dq_v1)                                                                                                     \
@@ -1089,7 +1079,7 @@ int launch_attn_train_bwd(const uint16_t* q, long ldq, const uint16_t* qt, const
     else                                                                                                            \
       attn_train_dq_v2_kernel<DHV><<<gq, 256, 0, s>>>(q, ldq, k, ldk, kt, v, ldv, o, ldo, dout, lddo, Lp, lse2,     \
                                                       delta, dq, lddq, L, H, Hkv, scale);                           \
-    if (dkdv_v1 || DHV > 128) { /* 192: v2 spills more than v1 */                                               \
+    if (dkdv_v1) {                                                                                              \
       static bool attr = hipFuncSetAttribute((const void*)attn_train_dkdv_kernel<DHV>,                             \
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)dkdv_smem<DHV>()) ==  \
                          hipSuccess;                                                                                \

@@ -768,14 +768,16 @@ void attn_train_bwd(const at::Tensor& q, const at::Tensor& qt, const at::Tensor&
                     const at::Tensor& lse2, at::Tensor& delta, at::Tensor& dq, at::Tensor& dk, at::Tensor& dv,
                     at::Tensor& ws, int64_t B, int64_t L, int64_t Lp, int64_t H, int64_t Hkv, int64_t Dh,
                     double scale) {
+  // qt / kt / doutt: the transposed images only the v1 kernels read (XOT_TRAIN_DQ_V1 / XOT_TRAIN_DKDV_V1); empty
+  // tensors otherwise (the v2 kernels read the transposed operands straight from their row tiles in LDS)
   check_rows(q, B * L, H * Dh, "q");
-  check_trans(qt, B, H, Dh, Lp, "qt");
+  if (qt.numel()) check_trans(qt, B, H, Dh, Lp, "qt");
   check_rows(k, B * L, Hkv * Dh, "k");
-  check_trans(kt, B, Hkv, Dh, Lp, "kt");
+  if (kt.numel()) check_trans(kt, B, Hkv, Dh, Lp, "kt");
   check_rows(v, B * L, Hkv * Dh, "v");
   check_rows(o, B * L, H * Dh, "o");
   check_rows(dout, B * L, H * Dh, "dout");
-  check_trans(doutt, B, H, Dh, Lp, "doutt");
+  if (doutt.numel()) check_trans(doutt, B, H, Dh, Lp, "doutt");
   check_rows(dq, B * L, H * Dh, "dq");
   check_rows(dk, B * L, Hkv * Dh, "dk");
   check_rows(dv, B * L, Hkv * Dh, "dv");
@@ -787,11 +789,12 @@ void attn_train_bwd(const at::Tensor& q, const at::Tensor& qt, const at::Tensor&
   CHECK_DT(ws, at::kFloat);
   XCHECK(ws.is_contiguous() && ws.numel() >= 2 * H * B * L * Dh, "attn_train_bwd: ws needs 2 * H * B * L * Dh floats");
   const int rc = xot::launch_attn_train_bwd(
-      bf(q), q.stride(0), bf(qt), bf(k), k.stride(0), bf(kt), bf(v), v.stride(0), bf(o), o.stride(0), bf(dout),
-      dout.stride(0), bf(doutt), (int)Lp, lse2.data_ptr<float>(), delta.data_ptr<float>(), bf(dq), dq.stride(0),
+      bf(q), q.stride(0), qt.numel() ? bf(qt) : nullptr, bf(k), k.stride(0), kt.numel() ? bf(kt) : nullptr, bf(v),
+      v.stride(0), bf(o), o.stride(0), bf(dout), dout.stride(0), doutt.numel() ? bf(doutt) : nullptr, (int)Lp, lse2.data_ptr<float>(), delta.data_ptr<float>(), bf(dq), dq.stride(0),
       bf(dk), dk.stride(0), bf(dv), dv.stride(0), ws.data_ptr<float>(), (long)ws.numel(), (int)B, (int)L, (int)H,
       (int)Hkv, (int)Dh, (float)scale, cur_stream());
-  XCHECK(rc == 0, "attn_train_bwd: unsupported H=", H, " Hkv=", Hkv, " Dh=", Dh);
+  XCHECK(rc == 0, "attn_train_bwd: unsupported H=", H, " Hkv=", Hkv, " Dh=", Dh,
+         " (or a transposed image the selected v1 kernel needs is missing)");
 }
 
 void attn_prefill(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,

@@ -162,6 +162,12 @@ class CrossEntropyFn(torch.autograd.Function):
     return d.to(logits.dtype), None, None
 
 
+# A/B switches of the backward kernels (read once by the library too): the v1 dQ / dK-dV kernels stage transposed
+# [B, heads, DH, Lp] images of K / Q and dO; the v2 kernels transpose in their LDS reads instead.
+_DQ_V1 = os.environ.get("XOT_TRAIN_DQ_V1", "0") == "1"
+_DKDV_V1 = os.environ.get("XOT_TRAIN_DKDV_V1", "0") == "1"
+
+
 class AttentionFn(torch.autograd.Function):
   """q [B*L, H*Dh], k / v [B*L, Hkv*Dh] (token-major, may be strided row views) -> o [B*L, H*Dh]."""
 
@@ -188,9 +194,10 @@ class AttentionFn(torch.autograd.Function):
       C = require()
       q, k, v, o, lse2 = ctx.saved_tensors
       do = do.contiguous().to(q.dtype)
-      qt = _transposed(C, q, B, L, Lp, H, Dh)
-      kt = _transposed(C, k, B, L, Lp, Hkv, Dh)
-      dot = _transposed(C, do, B, L, Lp, H, Dh)
+      none = torch.empty(0, dtype=q.dtype, device=q.device)  # the v2 kernels read no transposed image
+      qt = _transposed(C, q, B, L, Lp, H, Dh) if _DKDV_V1 else none
+      kt = _transposed(C, k, B, L, Lp, Hkv, Dh) if _DQ_V1 else none
+      dot = _transposed(C, do, B, L, Lp, H, Dh) if _DKDV_V1 else none
       dq = torch.empty(B * L, H * Dh, dtype=q.dtype, device=q.device)
       dk = torch.empty(B * L, Hkv * Dh, dtype=q.dtype, device=q.device)
       dv = torch.empty_like(dk)
