@@ -135,3 +135,44 @@ def test_adamw_tiled_matches_adamw_and_relayout(N, K, gdt):
   ws3, wts3 = torch.empty_like(ws), torch.empty_like(wts)
   C.adamw_tiled(p3, g, m3, v3, None, ws3, wts3, *args)
   assert torch.equal(ws3, ws) and torch.equal(wts3, wts)
+
+
+@pytest.mark.parametrize("T", [300, 1024])
+def test_silu_down_fused_backward_matches_fp32(T, monkeypatch):
+  """A.SiluDownFn: y = (silu(gate) * up) . W_down^T + h, its backward with the SiLU derivative in the epilogue of
+  the down projection's dA GEMM (gemm_silu_bwd, four-wave tile), against fp32 torch autograd -- dGU, dh and the
+  fused-accumulated dW_down -- and against the two-kernel path (XOT_SILU_BWD_FUSED=0)."""
+  from xotorch_support_jetson_amd.train import autograd_ops as A
+  dev = torch.device("cuda", 0)
+  D, F = 384, 512  # F % 256, D % 128: the fused tile path
+  torch.manual_seed(T)
+  gu = (torch.randn(T, 2 * F, device=dev)).to(torch.bfloat16)
+  w = (torch.randn(D, F, device=dev) / F ** 0.5).to(torch.bfloat16)
+  h = torch.randn(T, D, device=dev).to(torch.bfloat16)
+  dy = torch.randn(T, D, device=dev).to(torch.bfloat16)
+  tw = A.TrainWeight(w)
+  assert tw.ok
+
+  def run(fused):
+    monkeypatch.setattr(A, "SILU_BWD_FUSED", fused)
+    acc = A.GradAcc("down", w)
+    g, hh = gu.clone().requires_grad_(), h.clone().requires_grad_()
+    y = A.silu_down_own(g, w, tw, acc, hh)
+    y.backward(dy)
+    A.join_dw_stream()
+    torch.cuda.synchronize()
+    return y.float(), g.grad.float(), hh.grad.float(), acc.buf.float()
+
+  gf, hf = gu.float().requires_grad_(), h.float().requires_grad_()
+  wf = w.float().requires_grad_()
+  yr = (torch.nn.functional.silu(gf[:, :F]) * gf[:, F:]) @ wf.t() + hf
+  yr.backward(dy.float())
+  ref = (yr, gf.grad, hf.grad, wf.grad)
+  fused, plain = run(True), run(False)
+  for name, a, b, r in zip(("y", "dgu", "dh", "dW"), fused, plain, ref):
+    assert rel_err(a, r) < 2e-2, (name, rel_err(a, r))
+    assert rel_err(a, b) < 2e-2, (name, rel_err(a, b))
+
+
+def rel_err(a, b):
+  return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()

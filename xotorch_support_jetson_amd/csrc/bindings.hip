@@ -327,6 +327,26 @@ void gemm_stream8(const at::Tensor& x, const at::Tensor& w8, const at::Tensor& w
 
 // Large-M GEMM on the pre-shuffled weight layout (prefill chunks, decode batches > 128 rows).
 // bn: 256 or 128 output columns per workgroup; splits > 1 needs an fp32 workspace of splits*M*N.
+// dGU = silu_mul'(GU) * (dY . W): the down projection's input-gradient GEMM on the four-wave tile with the SiLU
+// backward in its epilogue.  dy [M, K] bf16, w = shuffle(W_down^T) [F, K], gu / dgu [M, 2F] ([gate | up]).
+void gemm_silu_bwd(const at::Tensor& dy, const at::Tensor& w, const at::Tensor& gu, at::Tensor& dgu) {
+  CHECK_BF16(dy);
+  CHECK_BF16(w);
+  CHECK_BF16(gu);
+  CHECK_BF16(dgu);
+  XCHECK(dy.dim() == 2 && w.dim() == 2 && gu.dim() == 2 && dgu.dim() == 2, "gemm_silu_bwd: 2-D operands");
+  XCHECK(dy.stride(1) == 1 && dy.stride(0) % 8 == 0 && w.is_contiguous() && gu.stride(1) == 1 &&
+             gu.stride(0) % 8 == 0 && dgu.stride(1) == 1 && dgu.stride(0) % 8 == 0,
+         "gemm_silu_bwd: rows must be contiguous and 16-B aligned");
+  const int64_t M = dy.size(0), K = dy.size(1), F = w.size(0);
+  XCHECK(w.size(1) == K && gu.size(0) == M && gu.size(1) == 2 * F && dgu.size(0) == M && dgu.size(1) == 2 * F,
+         "gemm_silu_bwd: shapes");
+  const int rc = xot::launch_gemm_w4(bf(dy), (int)dy.stride(0), bf(w), nullptr, bf(gu), (int)gu.stride(0),
+                                     dgu.data_ptr(), (int)dgu.stride(0), false, 3 /* EPI_SILU_BWD */, nullptr, (int)M,
+                                     (int)F, (int)K, 1, xot::gemm_big_group_m(), cur_stream());
+  XCHECK(rc == 0, "gemm_silu_bwd: unsupported shape M=", M, " F=", F, " K=", K, " (F % 256, K % 128)");
+}
+
 void gemm_big(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const c10::optional<at::Tensor>& bias,
               const c10::optional<at::Tensor>& res, const c10::optional<at::Tensor>& ws, int64_t epi, int64_t bn,
               int64_t splits, bool reduce) {
@@ -981,6 +1001,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_batched", &gemm_batched, py::arg("x"), py::arg("xbat"), py::arg("K"), py::arg("w"), py::arg("y"),
         py::arg("ybat"), py::arg("ldy"), py::arg("M"));
   m.def("gemm_sk_sync_words", &gemm_sk_sync_words);
+  m.def("gemm_silu_bwd", &gemm_silu_bwd, py::arg("dy"), py::arg("w"), py::arg("gu"), py::arg("dgu"));
   m.def("gemm_big", &gemm_big, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("bias"), py::arg("res"),
         py::arg("ws"), py::arg("epi"), py::arg("bn"), py::arg("splits"), py::arg("reduce") = true);
   m.def("splitk_resid_rmsnorm", &splitk_resid_rmsnorm);

@@ -497,7 +497,9 @@ constexpr int big_smem() {  // LDS bytes of a gemm_big configuration
 }
 
 // grouped raster width of tall plain grids (XOT_GEMM_GROUP_M, read once; default 4)
-static int big_group_m() {
+int gemm_big_group_m();
+static int big_group_m() { return gemm_big_group_m(); }
+int gemm_big_group_m() {
   static const int gm = [] {
     const char* e = getenv("XOT_GEMM_GROUP_M");
     return e != nullptr ? atoi(e) : 4;

@@ -43,6 +43,7 @@ int launch_gemm_stream8(const uint16_t* X, int ldx, const uint8_t* W, const floa
 int launch_gemm_w4(const uint16_t* X, int ldx, const uint16_t* W, const uint16_t* bias, const uint16_t* R, int ldr,
                    void* Y, int ldy, bool out_f32, int epi, float* ws, int M, int N, int K, int S, int group_m,
                    hipStream_t st);
+int gemm_big_group_m();  // grouped raster width of tall grids (XOT_GEMM_GROUP_M)
 int launch_gemm_big(const uint16_t* X, int ldx, const uint16_t* W, const uint16_t* bias, const uint16_t* R, int ldr,
                     void* Y, int ldy, bool out_f32, int epi, float* ws, long ws_elems, int M, int N, int K, int bn,
                     int S, bool reduce, hipStream_t s);

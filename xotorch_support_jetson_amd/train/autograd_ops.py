@@ -484,6 +484,52 @@ def linear_own(x, w, tw, acc, h=None):
   return OwnLinearFn.apply(x, w, tw, h, acc)
 
 
+# 1: the SiLU backward in the dA GEMM's epilogue.  Measured slower on the Llama-3-8B step (728-730 vs 721 ms,
+# profiles/r5/train/silu_bwd_fused/): the epilogue's gate / up reads and two outputs run at the tail of every tile
+# on the dX chain's critical path, where the separate silu_mul_bwd kernel streams at ~6 TB/s.  Off by default.
+SILU_BWD_FUSED = os.environ.get("XOT_SILU_BWD_FUSED", "0") == "1"
+
+
+class SiluDownFn(torch.autograd.Function):
+  """y = (silu(gate) * up) . W_down^T (+ h): SiluMulFn and the down projection's OwnLinearFn in one, so the
+  backward forms dGU in the epilogue of the down projection's input-gradient GEMM (csrc gemm_w4 EPI_SILU_BWD via
+  gemm_silu_bwd): the four-wave tile reads gate / up beside its accumulators and writes dgate / dup, instead of
+  writing dA [T, F] and re-reading it with gate / up in silu_mul_bwd (2 x T x F x 2 bytes of HBM traffic and a
+  kernel per layer and micro-batch).  Shapes the tile does not cover take the two-kernel path."""
+
+  @staticmethod
+  def forward(ctx, gu, w, tw, h, acc):
+    from ..ops.linear import linear
+    gu = gu.contiguous()
+    F = gu.shape[1] // 2
+    a = torch.empty(gu.shape[0], F, dtype=gu.dtype, device=gu.device)
+    require().silu_mul(gu, a, False)
+    ctx.save_for_backward(gu, a)
+    ctx.tw, ctx.acc, ctx.has_h = tw, acc, h is not None
+    if h is not None:
+      return linear(a, tw.ws, residual=h.contiguous(), epi="resid")
+    return linear(a, tw.ws)
+
+  @staticmethod
+  def backward(ctx, dy):
+    from ..ops.linear import linear
+    gu, a = ctx.saved_tensors
+    tw, acc = ctx.tw, ctx.acc
+    dy = dy.contiguous()
+    F, K = tw.wts.shape
+    dgu = torch.empty_like(gu)
+    if SILU_BWD_FUSED and F % 256 == 0 and K % 128 == 0 and dy.shape[0] * K * 2 < (1 << 32):
+      require().gemm_silu_bwd(dy, tw.wts, gu, dgu)
+    else:
+      require().silu_mul_bwd(gu, linear(dy, tw.wts), dgu)
+    own_dw(dy, a, acc)
+    return dgu, None, None, (dy if ctx.has_h else None), None
+
+
+def silu_down_own(gu, w, tw, acc, h=None):
+  return SiluDownFn.apply(gu, w, tw, h, acc)
+
+
 class StackWeight:
   """An expert stack W [E, N, K] in the grouped GEMMs' operand layouts (per expert, refreshed after every
   optimizer step): ws[e] = shuffle(W[e]) (forward), wts[e] = shuffle(W[e]^T) (input gradient)."""

@@ -168,7 +168,7 @@ class ShardTrainer:
       if f"{i}.router" in P:
         h = h + self._moe(xn, i)
       else:
-        h = self._mm(A.silu_mul(self._mm(xn, f"{i}.gu").contiguous()), f"{i}.down", h)
+        h = self._ffn(xn, f"{i}.gu", f"{i}.down", h)
     if not self.shard.is_last_layer():
       return h.view(B, L, D)
     xn = A.rmsnorm(h, P["norm"], c.rms_norm_eps)
@@ -297,6 +297,15 @@ class ShardTrainer:
     y = A.grouped_experts(xs, poff, -(-T // 64) * 64, sgu, sdown, self.acc[f"{i}.egu"], self.acc[f"{i}.edown"])
     y = y.index_select(0, dest).float() * topw.reshape(-1)[order].unsqueeze(1)
     return torch.zeros(T, D, device=dev, dtype=torch.float32).index_add(0, tok, y)
+
+  def _ffn(self, xn: torch.Tensor, gu: str, down: str, h: torch.Tensor) -> torch.Tensor:
+    """h + down(silu(gate) * up) of the gated MLP; while training on the own GEMMs as one A.SiluDownFn (the SiLU
+    backward runs in the down projection's input-gradient GEMM epilogue)."""
+    g = self._mm(xn, gu)
+    tw, acc = self.tw.get(down), self.acc.get(down)
+    if torch.is_grad_enabled() and isinstance(tw, A.TrainWeight) and acc is not None:
+      return A.silu_down_own(g, self.params[down], tw, acc, h)
+    return self._mm(A.silu_mul(g.contiguous()), down, h)
 
   def _mm(self, x: torch.Tensor, name: str, h: Optional[torch.Tensor] = None) -> torch.Tensor:
     """x @ W.T (+ h) for projection `name`: fused gradient accumulation on the GPU while training."""
