@@ -377,6 +377,29 @@ def test_sample_distribution(gpu):
   assert torch.allclose(counts[:3], p, atol=0.03)
 
 
+@pytest.mark.parametrize("V", [50000, 50001, 512])
+def test_cross_entropy_fp32_logits(gpu, V):
+  """fp32 logits (the fused LM head's chunks): the 16-byte vector kernels (V % 8 == 0) and the scalar fallback."""
+  from xotorch_support_jetson_amd.ops._ext import require
+  C = require()
+  torch.manual_seed(V)
+  T = 7
+  x = torch.randn(T, V, device=gpu) * 3
+  tgt = torch.randint(0, V, (T,), device=gpu, dtype=torch.int32)
+  tgt[1] = -100
+  tgt[4] = V - 1
+  loss, lse = torch.empty(T, device=gpu), torch.empty(T, device=gpu)
+  C.ce_fwd(x, tgt, loss, lse)
+  ref = torch.nn.functional.cross_entropy(x, tgt.long(), ignore_index=-100, reduction="none")
+  assert torch.allclose(loss, ref, atol=1e-3, rtol=1e-4)
+  dx = torch.empty(T, V, device=gpu, dtype=torch.bfloat16)
+  C.ce_bwd(x, tgt, lse, torch.full((T,), 0.25, device=gpu), dx)
+  xr = x.clone().requires_grad_()
+  (torch.nn.functional.cross_entropy(xr, tgt.long(), ignore_index=-100, reduction="none") * 0.25).sum().backward()
+  assert rel_err(dx, xr.grad) < 1e-2
+  assert dx[1].abs().max().item() == 0
+
+
 def test_cross_entropy_and_adamw(gpu):
   torch.manual_seed(0)
   from xotorch_support_jetson_amd.ops._ext import require

@@ -85,9 +85,63 @@ __global__ __launch_bounds__(256) void ce_bwd_kernel(const T* __restrict__ x, lo
   }
 }
 
+// fp32 logits with V % 8 == 0 and 16-byte rows (the fused LM head's chunks): 16-byte loads, one online-softmax
+// update per 4 values (the scalar forms ran at 3.3 / 4.0 TB/s on the 128k-vocab chunks)
+__global__ __launch_bounds__(256) void ce_fwd_vec_kernel(const float* __restrict__ x, long ld, int V,
+                                                        const int32_t* __restrict__ tgt, float* __restrict__ loss,
+                                                        float* __restrict__ lse) {
+  __shared__ float sm[4], ss[4];
+  const int t = blockIdx.x;
+  const f32x4* row = reinterpret_cast<const f32x4*>(x + (size_t)t * ld);
+  // finite start: a thread with no elements (V / 4 < 256) must not feed exp(-inf - -inf) = NaN into the combine
+  float m = -1e30f, s = 0.f;
+  for (int i = threadIdx.x; i < V / 4; i += 256) {
+    const f32x4 v = row[i];
+    const float m4 = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
+    if (m4 > m) {
+      s *= __expf(m - m4);
+      m = m4;
+    }
+    s += __expf(v[0] - m) + __expf(v[1] - m) + __expf(v[2] - m) + __expf(v[3] - m);
+  }
+  block_reduce_max_sum(m, s, sm, ss);
+  if (threadIdx.x == 0) {
+    const float l = m + __logf(s);
+    const int y = tgt[t];
+    lse[t] = l;
+    loss[t] = (y >= 0 && y < V) ? l - x[(size_t)t * ld + y] : 0.f;
+  }
+}
+
+__global__ __launch_bounds__(256) void ce_bwd_vec_kernel(const float* __restrict__ x, long ld, int V,
+                                                        const int32_t* __restrict__ tgt, const float* __restrict__ lse,
+                                                        const float* __restrict__ gscale, uint16_t* __restrict__ dx,
+                                                        long ldd) {
+  const int t = blockIdx.x;
+  const f32x4* row = reinterpret_cast<const f32x4*>(x + (size_t)t * ld);
+  s16x8* drow = reinterpret_cast<s16x8*>(dx + (size_t)t * ldd);
+  const int y = tgt[t];
+  const bool ign = y < 0 || y >= V;
+  const float l = lse[t], gs = ign ? 0.f : gscale[t];
+  for (int i = threadIdx.x; i < V / 8; i += 256) {
+    const f32x4 a = row[2 * i], b = row[2 * i + 1];
+    s16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float v = e < 4 ? a[e] : b[e - 4];
+      o[e] = (short)f2bf(gs * (__expf(v - l) - (8 * i + e == y ? 1.f : 0.f)));
+    }
+    drow[i] = o;
+  }
+}
+
 void launch_ce_fwd(const void* x, bool x_f32, long ld, int T, int V, const int32_t* tgt, float* loss, float* lse,
                    hipStream_t s) {
   if (T <= 0) return;
+  if (x_f32 && V % 8 == 0 && ld % 4 == 0 && ((uintptr_t)x & 15) == 0) {
+    ce_fwd_vec_kernel<<<T, 256, 0, s>>>((const float*)x, ld, V, tgt, loss, lse);
+    return;
+  }
   if (x_f32)
     ce_fwd_kernel<float><<<T, 256, 0, s>>>((const float*)x, ld, V, tgt, loss, lse);
   else
@@ -97,6 +151,10 @@ void launch_ce_fwd(const void* x, bool x_f32, long ld, int T, int V, const int32
 void launch_ce_bwd(const void* x, bool x_f32, long ld, int T, int V, const int32_t* tgt, const float* lse,
                    const float* gscale, uint16_t* dx, long ldd, hipStream_t s) {
   if (T <= 0) return;
+  if (x_f32 && V % 8 == 0 && ld % 4 == 0 && ldd % 8 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)dx & 15) == 0) {
+    ce_bwd_vec_kernel<<<T, 256, 0, s>>>((const float*)x, ld, V, tgt, lse, gscale, dx, ldd);
+    return;
+  }
   if (x_f32)
     ce_bwd_kernel<float><<<T, 256, 0, s>>>((const float*)x, ld, V, tgt, lse, gscale, dx, ldd);
   else
