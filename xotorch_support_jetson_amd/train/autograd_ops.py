@@ -736,3 +736,49 @@ class QKVSplitFn(torch.autograd.Function):
 
 def qkv_split(qkv, nq, nk):
   return QKVSplitFn.apply(qkv, nq, nk)
+
+
+class QKVRopeFn(torch.autograd.Function):
+  """Fused-QKV projection output [T, (H + 2 Hkv) Dh] -> rope(q), rope(k) (contiguous) and v (a row-strided view),
+  in two rope_apply launches that read q / k straight out of the qkv rows (QKVSplitFn + RopeFn made contiguous
+  copies first).  The backward writes the inverse rotations of dq / dk and dv straight into the slices of one
+  dqkv buffer instead of rotating into temporaries and concatenating."""
+
+  @staticmethod
+  def forward(ctx, qkv, pos, cos_sin, H, Hkv, Dh):
+    C = require()
+    T, nq, nk = qkv.shape[0], H * Dh, Hkv * Dh
+    ctx.save_for_backward(pos, cos_sin)
+    ctx.dims = (H, Hkv, Dh, qkv.shape[1])
+    q = torch.empty(T, nq, dtype=qkv.dtype, device=qkv.device)
+    k = torch.empty(T, nk, dtype=qkv.dtype, device=qkv.device)
+    C.rope_apply(qkv[:, :nq], q, pos, cos_sin, int(H), int(Dh), False)
+    C.rope_apply(qkv[:, nq:nq + nk], k, pos, cos_sin, int(Hkv), int(Dh), False)
+    return q, k, qkv[:, nq + nk:]
+
+  @staticmethod
+  def backward(ctx, dq, dk, dv):
+    C = require()
+    pos, cos_sin = ctx.saved_tensors
+    H, Hkv, Dh, W = ctx.dims
+    nq, nk = H * Dh, Hkv * Dh
+    ref_t = next(g for g in (dq, dk, dv) if g is not None)
+    dqkv = torch.empty(ref_t.shape[0], W, dtype=ref_t.dtype, device=ref_t.device)
+    for g, lo, n, nh in ((dq, 0, nq, H), (dk, nq, nk, Hkv)):
+      if g is None:
+        dqkv[:, lo:lo + n].zero_()
+      else:
+        C.rope_apply(g.contiguous(), dqkv[:, lo:lo + n], pos, cos_sin, int(nh), int(Dh), True)
+    if dv is None:
+      dqkv[:, nq + nk:].zero_()
+    else:
+      dqkv[:, nq + nk:].copy_(dv)
+    return dqkv, None, None, None, None, None
+
+
+def qkv_rope(qkv, pos, cos_sin, H, Hkv, Dh):
+  """(rope(q), rope(k), v) of a fused-QKV projection output (QKVRopeFn on the GPU)."""
+  if _gpu(qkv) and qkv.stride(1) == 1:
+    return QKVRopeFn.apply(qkv, pos, cos_sin, H, Hkv, Dh)
+  q, k, v = qkv_split(qkv, H * Dh, Hkv * Dh)
+  return rope(q, pos, cos_sin, H, Dh), rope(k, pos, cos_sin, Hkv, Dh), v

@@ -159,9 +159,7 @@ class ShardTrainer:
         qkv = self._mm(xn, f"{i}.qkv")
         if f"{i}.qkv_b" in P:
           qkv = qkv + P[f"{i}.qkv_b"]
-        q, k, v = A.qkv_split(qkv, H * Dh, Hkv * Dh)
-        q = A.rope(q, pos, self.cos_sin, H, Dh)
-        k = A.rope(k, pos, self.cos_sin, Hkv, Dh)
+        q, k, v = A.qkv_rope(qkv, pos, self.cos_sin, H, Hkv, Dh)
         a = A.attention(q, k, v, B, L, H, Hkv, Dh)  # flash-style HIP kernels (fwd + dQ + dK/dV)
       h = self._mm(a, f"{i}.o", h)
       h, xn = A.res_rmsnorm(h, P[f"{i}.ln2"], c.rms_norm_eps)
