@@ -786,26 +786,30 @@ __global__ __launch_bounds__(64 * DKW) void attn_train_dkdv_v2_kernel(const uint
                                                                    const float* __restrict__ lse2,
                                                                    const float* __restrict__ delta,
                                                                    float* __restrict__ wk, float* __restrict__ wv,
-                                                                   int L, int H, int Hkv, float scale) {
+                                                                   int L, int H, int Hkv, float scale, int hpw) {
   constexpr int KS = DH / 32, NDT = DH / 16;
   constexpr int RLD = tr_ld(DH);
   extern __shared__ __attribute__((aligned(16))) uint16_t sm[];
   uint16_t* qs = sm;                 // Q rows       [64][RLD] (row reads for S, transposed reads for dK)
   uint16_t* ds_ = qs + TT * RLD;     // dO rows      [64][RLD] (row reads for dP, transposed reads for dV)
   float* ld_ = reinterpret_cast<float*>(ds_ + TT * RLD);  // lse2[64], delta[64]
+  // hpw query heads of one GQA group per workgroup (their dK / dV sum in the accumulators): G / hpw partial
+  // slabs for the reduce kernel instead of G.  2 at G = 4 keeps 512 workgroups of 64 .. 4 query tiles, which
+  // heaviest-first scheduling still balances over 256 CUs; 4 would leave one workgroup per CU, 128 vs 8 tiles.
   const int G = H / Hkv;
-  const int hq = blockIdx.x, kvh = hq / G, hh = hq % G, kt = blockIdx.y, b = blockIdx.z;
+  const int hq = blockIdx.x * hpw, kvh = hq / G, hh = (hq % G) / hpw, kt = blockIdx.y, b = blockIdx.z;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
   const int k0 = kt * DKT, krow = k0 + 16 * wave;
   const float sl = scale * L2E;
   const int qt0 = k0 / TT;
-  const int nq = (L + TT - 1) / TT, iters = nq - qt0;
+  const int nq = (L + TT - 1) / TT, iters = (nq - qt0) * hpw;  // (head, query tile) pairs, head-major
+  const int per = nq - qt0;
   const int key = krow + c;  // this lane's key (B-operand column of every product)
 
   RowsTile<DH, 64 * DKW> qr, dr;
   float lsv = 0.f, dlv = 0.f;
   auto load = [&](int it) {
-    const int h = hq, q0 = (qt0 + it) * TT;
+    const int h = hq + it / per, q0 = (qt0 + it % per) * TT;
     qr.load(Q + (long)b * L * ldq + h * DH, ldq, q0, L);
     dr.load(dO + (long)b * L * lddo + h * DH, lddo, q0, L);
     if (threadIdx.x < TT) {
@@ -832,7 +836,7 @@ __global__ __launch_bounds__(64 * DKW) void attn_train_dkdv_v2_kernel(const uint
 
   if (iters > 0) load(0);
   for (int it = 0; it < iters; ++it) {
-    const int q0 = (qt0 + it) * TT;
+    const int q0 = (qt0 + it % per) * TT;
     __syncthreads();
     qr.template store<RLD>(qs);
     dr.template store<RLD>(ds_);
@@ -1071,6 +1075,12 @@ int launch_attn_train_bwd(const uint16_t* q, long ldq, const uint16_t* qt, const
     return e != nullptr && e[0] == '1';
   }();
   if ((dq_v1 && kt == nullptr) || (dkdv_v1 && (qt == nullptr || doutt == nullptr))) return -1;
+  static const int hpw_env = [] {  // XOT_TRAIN_DKDV_HPW: query heads per dK / dV workgroup (v2; 1 or 2)
+    const char* e = getenv("XOT_TRAIN_DKDV_HPW");
+    return e != nullptr ? atoi(e) : 2;
+  }();
+  const int G = H / Hkv, hpw = (!dkdv_v1 && hpw_env == 2 && G % 2 == 0) ? 2 : 1;
+  const dim3 gk2(H / hpw, (L + DKT - 1) / DKT, B);
 #define XOT_BWD(DHV)                                                                                                \
   do {                                                                                                              \
     if (dq_v1)                                                                                                     \
@@ -1091,8 +1101,8 @@ int launch_attn_train_bwd(const uint16_t* q, long ldq, const uint16_t* qt, const
                                               hipFuncAttributeMaxDynamicSharedMemorySize,                           \
                                               (int)dkdv_v2_smem<DHV>()) == hipSuccess;                              \
       (void)attr2;                                                                                                  \
-      attn_train_dkdv_v2_kernel<DHV><<<gk, 64 * DKW, dkdv_v2_smem<DHV>(), s>>>(                                     \
-          q, ldq, qt, k, ldk, v, ldv, dout, lddo, doutt, Lp, lse2, delta, wk, wv, L, H, Hkv, scale);                \
+      attn_train_dkdv_v2_kernel<DHV><<<gk2, 64 * DKW, dkdv_v2_smem<DHV>(), s>>>(                                    \
+          q, ldq, qt, k, ldk, v, ldv, dout, lddo, doutt, Lp, lse2, delta, wk, wv, L, H, Hkv, scale, hpw);           \
     }                                                                                                               \
   } while (0)
   if (Dh == 128)
@@ -1107,7 +1117,7 @@ int launch_attn_train_bwd(const uint16_t* q, long ldq, const uint16_t* qt, const
   const long n4 = slab / 4;
   int blocks = (int)((n4 + 255) / 256);
   if (blocks > 4096) blocks = 4096;
-  attn_train_dkdv_reduce_kernel<<<blocks, 256, 0, s>>>(wk, wv, H / Hkv, (long)B * L, Hkv * Dh, scale, dk, lddk, dv,
+  attn_train_dkdv_reduce_kernel<<<blocks, 256, 0, s>>>(wk, wv, G / hpw, (long)B * L, Hkv * Dh, scale, dk, lddk, dv,
                                                        lddv);
   return 0;
 }
