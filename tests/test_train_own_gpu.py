@@ -176,3 +176,24 @@ def test_silu_down_fused_backward_matches_fp32(T, monkeypatch):
 
 def rel_err(a, b):
   return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+def test_embed_acc_matches_autograd():
+  """A.EmbedAccFn: the embedding gradient of two micro-batches (repeated ids included) index-added into an fp32
+  GradAcc equals autograd's summed dense gradient."""
+  from xotorch_support_jetson_amd.train import autograd_ops as A
+  dev = torch.device("cuda", 0)
+  torch.manual_seed(0)
+  V, D = 1000, 256
+  w = (torch.randn(V, D, device=dev) * 0.1).to(torch.bfloat16)
+  acc = A.GradAcc("embed", w)
+  acc.buf = torch.empty(V, D, dtype=torch.float32, device=dev)
+  wr = w.clone().requires_grad_()
+  for mb in range(2):
+    ids = torch.randint(0, 50, (3, 40), device=dev)  # many repeats
+    dh = torch.randn(3, 40, D, device=dev).to(torch.bfloat16)
+    A.embed_acc(ids, w.requires_grad_(), acc).backward(dh)
+    torch.nn.functional.embedding(ids, wr).backward(dh)
+  torch.cuda.synchronize()
+  assert rel_err(acc.buf, wr.grad) < 1e-2
+  assert acc.buf[50:].abs().max().item() == 0

@@ -284,6 +284,34 @@ class GradAcc:
     self.cb = None
 
 
+class EmbedAccFn(torch.autograd.Function):
+  """h = W[ids] (an untied input embedding) whose backward adds the dh rows into its GradAcc buffer (fp32 [V, D],
+  index_add_) instead of autograd's per-micro-batch dense [V, D] gradient (a zero fill of the whole table, a
+  sort-and-scatter, then an add of the table into .grad for every micro-batch after the first)."""
+
+  @staticmethod
+  def forward(ctx, ids, w, acc):
+    ctx.save_for_backward(ids)
+    ctx.acc = acc
+    return F.embedding(ids, w)
+
+  @staticmethod
+  def backward(ctx, dh):
+    (ids,) = ctx.saved_tensors
+    acc = ctx.acc
+    if acc.fresh:
+      acc.buf.zero_()
+      acc.fresh = False
+    acc.buf.index_add_(0, ids.reshape(-1), dh.reshape(-1, dh.shape[-1]).float())
+    if acc.cb is not None:
+      acc.cb()
+    return None, None, None
+
+
+def embed_acc(ids, w, acc):
+  return EmbedAccFn.apply(ids, w, acc)
+
+
 class StackAccFn(torch.autograd.Function):
   """Per-expert views of an expert stack [E, R, C] whose backward adds each routed expert's gradient
   straight into the stack's GradAcc buffer (zeroed once per step) and returns no gradient for the stack:

@@ -40,6 +40,7 @@ FUSED_CE = os.environ.get("XOT_FUSED_CE", "1") == "1"
 # rows per fused LM-head + CE chunk: 4096 (one [4096, V] fp32 logits block, 2.1 GB at V = 128256) ran the
 # Llama-3-8B step 1.1 % faster than 1024 (profiles/r5/train/knobs_r5s/)
 CE_CHUNK = int(os.environ.get("XOT_CE_CHUNK", "4096"))
+EMBED_ACC = os.environ.get("XOT_EMBED_ACC", "1") == "1"  # 0: autograd's dense embedding gradient (A/B)
 # XOT_FUSED_ADAMW=0: plain AdamW + relayout refresh of the operand images (A/B of csrc/train_ops.hip adamw_tiled)
 FUSED_ADAMW = os.environ.get("XOT_FUSED_ADAMW", "1") == "1"
 
@@ -124,6 +125,12 @@ class ShardTrainer:
         self.tw[self.head_name] = t
         if self.head_name == "lm_head":  # untied: the fused CE accumulates dHead into a GradAcc (A.LmHeadCEFn)
           self.acc["lm_head"] = A.GradAcc("lm_head", self.params["lm_head"])
+    # untied input embedding: its gradient accumulates into an fp32 GradAcc (A.EmbedAccFn), not a dense autograd
+    # gradient per micro-batch (after the TrainWeight loop above: the table has no operand images)
+    if self.device.type == "cuda" and "embed" in self.params and self.head_name != "embed" and EMBED_ACC:
+      a = A.GradAcc("embed", self.params["embed"])
+      a.buf = torch.empty(self.params["embed"].shape, dtype=torch.float32, device=self.device)
+      self.acc["embed"] = a
     self.master = {k: p.detach().float().clone() for k, p in self.params.items()}
     self._pb_stale: set = set()  # bf16 params the fused AdamW did not rewrite (refresh_params)
     self.m = {k: torch.zeros_like(v) for k, v in self.master.items()}
@@ -143,7 +150,8 @@ class ShardTrainer:
     H, Hkv, Dh, D = c.num_heads, c.num_kv_heads, c.head_dim, c.hidden_size
     if self.shard.is_first_layer():
       ids = x.long().clamp(0, c.vocab_size - 1)
-      h = F.embedding(ids, P["embed"])
+      acc = self.acc.get("embed")
+      h = A.embed_acc(ids, P["embed"], acc) if acc is not None and torch.is_grad_enabled() else F.embedding(ids, P["embed"])
     else:
       h = x.to(torch.bfloat16)
     B, L = h.shape[0], h.shape[1]
