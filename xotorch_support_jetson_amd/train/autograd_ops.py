@@ -24,10 +24,30 @@ def _gpu(t: torch.Tensor) -> bool:
   return t.is_cuda
 
 
+def _norm_dw(w, acc, dev):
+  """The fp32 dw the RMSNorm backward kernel adds into: the norm weight's GradAcc buffer (zeroed on the step's
+  first micro-batch; the kernel's reduce accumulates with atomics), or a fresh zeroed vector."""
+  if acc is None:
+    return torch.zeros(w.numel(), dtype=torch.float32, device=dev)
+  if acc.fresh:
+    acc.buf.zero_()
+    acc.fresh = False
+  return acc.buf
+
+
+def _norm_dw_out(w, dw, acc):
+  """The weight gradient autograd sees: none when it went into the GradAcc (then its callback fires)."""
+  if acc is None:
+    return dw.to(w.dtype)
+  if acc.cb is not None:
+    acc.cb()
+  return None
+
+
 class RMSNormFn(torch.autograd.Function):
   @staticmethod
-  def forward(ctx, x, w, eps):
-    ctx.eps = eps
+  def forward(ctx, x, w, eps, acc=None):
+    ctx.eps, ctx.acc = eps, acc
     ctx.save_for_backward(x, w)
     if _gpu(x):
       out = torch.empty_like(x)
@@ -40,15 +60,15 @@ class RMSNormFn(torch.autograd.Function):
     x, w = ctx.saved_tensors
     if _gpu(x):
       dx = torch.empty_like(x)
-      dw = torch.zeros(w.numel(), dtype=torch.float32, device=x.device)
+      dw = _norm_dw(w, ctx.acc, x.device)
       require().rmsnorm_bwd(x.contiguous(), w, dy.contiguous().to(x.dtype), dx, dw, float(ctx.eps))
-      return dx, dw.to(w.dtype), None
+      return dx, _norm_dw_out(w, dw, ctx.acc), None, None
     with torch.enable_grad():
       xr = x.detach().float().requires_grad_()
       wr = w.detach().float().requires_grad_()
       y = xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + ctx.eps) * wr
       y.backward(dy.float())
-    return xr.grad.to(x.dtype), wr.grad.to(w.dtype), None
+    return xr.grad.to(x.dtype), wr.grad.to(w.dtype), None, None
 
 
 class ResNormFn(torch.autograd.Function):
@@ -57,8 +77,8 @@ class ResNormFn(torch.autograd.Function):
   `res`) instead of autograd's separate add kernel per residual join (2 per layer and micro-batch)."""
 
   @staticmethod
-  def forward(ctx, h, w, eps):
-    ctx.eps = eps
+  def forward(ctx, h, w, eps, acc=None):
+    ctx.eps, ctx.acc = eps, acc
     ctx.save_for_backward(h, w)
     if _gpu(h):
       xn = torch.empty_like(h)
@@ -71,15 +91,15 @@ class ResNormFn(torch.autograd.Function):
   def backward(ctx, dh, dxn):
     h, w = ctx.saved_tensors
     if dxn is None:
-      return dh, None, None
+      return dh, None, None, None
     if _gpu(h):
       dx = torch.empty_like(h)
-      dw = torch.zeros(w.numel(), dtype=torch.float32, device=h.device)
+      dw = _norm_dw(w, ctx.acc, h.device)
       res = dh.contiguous().to(h.dtype) if dh is not None else None
       require().rmsnorm_bwd(h.contiguous(), w, dxn.contiguous().to(h.dtype), dx, dw, float(ctx.eps), res)
-      return dx, dw.to(w.dtype), None
-    dx, dw, _ = RMSNormFn.backward(ctx, dxn)
-    return (dx if dh is None else dx + dh), dw, None
+      return dx, _norm_dw_out(w, dw, ctx.acc), None, None
+    dx, dw, _, _ = RMSNormFn.backward(ctx, dxn)
+    return (dx if dh is None else dx + dh), dw, None, None
 
 
 class SiluMulFn(torch.autograd.Function):
@@ -246,18 +266,19 @@ def attention_qk_v(q, k, v, B, L, H, dqk, dv, scale):
   return o.view(T, H, dqk)[..., :dv].reshape(T, H * dv)
 
 
-def rmsnorm(x, w, eps):
-  return RMSNormFn.apply(x, w, eps)
+def rmsnorm(x, w, eps, acc=None):
+  """acc: the weight's fp32 GradAcc (GPU: dw accumulates there across micro-batches, no autograd gradient)."""
+  return RMSNormFn.apply(x, w, eps, acc)
 
 
 RESNORM = os.environ.get("XOT_RESNORM", "1") == "1"  # 0: plain RMSNorm + autograd's add per residual join (A/B)
 
 
-def res_rmsnorm(h, w, eps):
+def res_rmsnorm(h, w, eps, acc=None):
   """(h, rmsnorm(h, w)): use the returned h downstream so the residual gradient joins in the norm's backward."""
   if not RESNORM:
-    return h, RMSNormFn.apply(h, w, eps)
-  return ResNormFn.apply(h, w, eps)
+    return h, RMSNormFn.apply(h, w, eps, acc)
+  return ResNormFn.apply(h, w, eps, acc)
 
 
 def silu_mul(gu):

@@ -41,6 +41,7 @@ FUSED_CE = os.environ.get("XOT_FUSED_CE", "1") == "1"
 # Llama-3-8B step 1.1 % faster than 1024 (profiles/r5/train/knobs_r5s/)
 CE_CHUNK = int(os.environ.get("XOT_CE_CHUNK", "4096"))
 EMBED_ACC = os.environ.get("XOT_EMBED_ACC", "1") == "1"  # 0: autograd's dense embedding gradient (A/B)
+NORM_ACC = os.environ.get("XOT_NORM_ACC", "1") == "1"  # 0: autograd-accumulated RMSNorm weight gradients (A/B)
 # XOT_FUSED_ADAMW=0: plain AdamW + relayout refresh of the operand images (A/B of csrc/train_ops.hip adamw_tiled)
 FUSED_ADAMW = os.environ.get("XOT_FUSED_ADAMW", "1") == "1"
 
@@ -125,6 +126,14 @@ class ShardTrainer:
         self.tw[self.head_name] = t
         if self.head_name == "lm_head":  # untied: the fused CE accumulates dHead into a GradAcc (A.LmHeadCEFn)
           self.acc["lm_head"] = A.GradAcc("lm_head", self.params["lm_head"])
+    # RMSNorm weights: the backward kernel's dw reduce adds into an fp32 GradAcc across micro-batches (no zeroed
+    # vector, bf16 copy and autograd accumulation add per norm and micro-batch)
+    if self.device.type == "cuda" and NORM_ACC:
+      for k in self.params:
+        if k == "norm" or k.split(".")[-1] in ("ln1", "ln2"):
+          a = A.GradAcc(k, self.params[k])
+          a.buf = torch.empty(self.params[k].shape, dtype=torch.float32, device=self.device)
+          self.acc[k] = a
     # untied input embedding: its gradient accumulates into an fp32 GradAcc (A.EmbedAccFn), not a dense autograd
     # gradient per micro-batch (after the TrainWeight loop above: the table has no operand images)
     if self.device.type == "cuda" and "embed" in self.params and self.head_name != "embed" and EMBED_ACC:
@@ -160,7 +169,7 @@ class ShardTrainer:
     pos = (torch.arange(L, device=self.device, dtype=torch.int32) + shift).repeat(B)
     h = h.reshape(B * L, D)
     for i in self.shard.layers():
-      h, xn = A.res_rmsnorm(h, P[f"{i}.ln1"], c.rms_norm_eps)
+      h, xn = A.res_rmsnorm(h, P[f"{i}.ln1"], c.rms_norm_eps, self.acc.get(f"{i}.ln1"))
       if c.is_mla:
         a = self._mla(xn, i, pos, B, L)
       else:
@@ -170,14 +179,14 @@ class ShardTrainer:
         q, k, v = A.qkv_rope(qkv, pos, self.cos_sin, H, Hkv, Dh)
         a = A.attention(q, k, v, B, L, H, Hkv, Dh)  # flash-style HIP kernels (fwd + dQ + dK/dV)
       h = self._mm(a, f"{i}.o", h)
-      h, xn = A.res_rmsnorm(h, P[f"{i}.ln2"], c.rms_norm_eps)
+      h, xn = A.res_rmsnorm(h, P[f"{i}.ln2"], c.rms_norm_eps, self.acc.get(f"{i}.ln2"))
       if f"{i}.router" in P:
         h = h + self._moe(xn, i)
       else:
         h = self._ffn(xn, f"{i}.gu", f"{i}.down", h)
     if not self.shard.is_last_layer():
       return h.view(B, L, D)
-    xn = A.rmsnorm(h, P["norm"], c.rms_norm_eps)
+    xn = A.rmsnorm(h, P["norm"], c.rms_norm_eps, self.acc.get("norm"))
     if not logits:
       return xn.view(B, L, D)
     head = P["lm_head"] if "lm_head" in P else P["embed"]
