@@ -92,3 +92,58 @@ def test_pipeline_training_two_ranks_matches_single(MODEL, world, schedule):
     assert torch.allclose(v, merged[k], atol=1e-6 if tol < 1e-3 else 2e-3, rtol=1e-5), k
   if c.tie_word_embeddings:  # the last stage's head copy took the same update as the embedding
     assert torch.allclose(merged["lm_head"], torch.from_numpy(res[0][1]["embed"]), atol=1e-7)
+
+
+def _worker_gpu(rank, world, port, q, MODEL):
+  os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+  dist.init_process_group("gloo", rank=rank, world_size=world)
+  try:
+    c = PRESETS[MODEL]
+    shard = equal_layer_shards(MODEL, c.num_layers, world)[rank]
+    dev = torch.device("cuda", 0)  # both ranks on the box's GPU, hand-offs staged through the host
+    tr = ShardTrainer(random_weights(c, shard, dev, seed=3), dev, lr=1e-3)
+    losses = _run(tr, rank, world, P2PTransport(rank, world))
+    q.put((rank, losses, {k: v.detach().float().cpu().numpy().copy() for k, v in tr.master.items()},
+           sorted(tr.acc)))
+    dist.barrier()
+  finally:
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_pipeline_tied_embedding_gpu_grad_acc():
+  """On the GPU the embedding (first stage) and its head copy (last stage) accumulate their gradients in fp32
+  GradAcc buffers (EMBED_ACC / the fused-CE dHead), not p.grad: the tied sum must read and write those, so both
+  copies take the same update and match the single-GPU run of the whole model."""
+  MODEL, world = "tiny-llama-d64", 2
+  c = PRESETS[MODEL]
+  dev = torch.device("cuda", 0)
+  full = ShardTrainer(random_weights(c, Shard(MODEL, 0, c.num_layers - 1, c.num_layers), dev, seed=3), dev, lr=1e-3)
+  init = full.master["embed"].float().cpu().clone()
+  ref_losses = _run(full, 0, 1, LoopbackTransport(0, 1))
+  ctx = mp.get_context("spawn")
+  q = ctx.Queue()
+  port = _port()
+  procs = [ctx.Process(target=_worker_gpu, args=(r, world, port, q, MODEL)) for r in range(world)]
+  for p in procs:
+    p.start()
+  try:
+    res = {}
+    for _ in range(world):
+      r, losses, master, accs = q.get(timeout=100)
+      res[r] = (losses, master, accs)
+  finally:
+    for p in procs:
+      p.join(timeout=60)
+      if p.is_alive():
+        p.kill()
+  assert "embed" in res[0][2]  # the GradAcc path is the one under test
+  assert torch.allclose(torch.from_numpy(res[1][1]["lm_head"]), torch.from_numpy(res[0][1]["embed"]), atol=1e-7)
+  for r in range(world):
+    for a, b in zip(res[r][0], ref_losses):
+      assert abs(a - b) < 2e-2, (r, res[r][0], ref_losses)
+  d_ref = full.master["embed"].float().cpu() - init
+  d_got = torch.from_numpy(res[0][1]["embed"]) - init
+  rel = float((d_got - d_ref).abs().mean() / d_ref.abs().mean())
+  print(f"tied embedding update: mean relative difference {rel:.4f}")
+  assert rel < 0.10, rel  # bf16 GEMMs on both sides: the update, not bit patterns

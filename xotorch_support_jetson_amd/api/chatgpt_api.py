@@ -559,3 +559,10 @@ class ChatGPTAPI:
     site = web.TCPSite(runner, host, port)
     await site.start()
     self._runner = runner
+
+  async def stop(self) -> None:
+    """Close the HTTP listener (its open connections get the server's shutdown)."""
+    runner = getattr(self, "_runner", None)
+    self._runner = None
+    if runner is not None:
+      await runner.cleanup()

@@ -90,7 +90,9 @@ def _unreachable_error(e: BaseException) -> bool:
   and keep the normal backoff retries (a slow large file must not mark the hub unreachable for the process)."""
   try:
     import aiohttp
-    if isinstance(e, (aiohttp.ClientConnectorError, aiohttp.ConnectionTimeoutError)):
+    # (ConnectionTimeoutError exists from aiohttp 3.10; older releases raise ServerTimeoutError for connect timeouts)
+    connect_timeout = getattr(aiohttp, "ConnectionTimeoutError", aiohttp.ServerTimeoutError)
+    if isinstance(e, (aiohttp.ClientConnectorError, connect_timeout)):
       return True
     if isinstance(e, aiohttp.ClientError):
       return False  # ServerDisconnectedError, SocketTimeoutError (read), ClientPayloadError, ...

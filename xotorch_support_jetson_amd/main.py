@@ -35,7 +35,7 @@ os.environ.setdefault("GRPC_VERBOSITY", "error")
 os.environ.setdefault("TRANSFORMERS_VERBOSITY", "error")
 os.environ.setdefault("TOKENIZERS_PARALLELISM", "true")
 
-from .helpers import DEBUG, VERSION, find_available_port, get_or_create_node_id, print_banner, shutdown, xot_home  # noqa: E402
+from .helpers import DEBUG, VERSION, find_available_port, get_or_create_node_id, print_banner, xot_home  # noqa: E402
 
 
 def build_parser() -> argparse.ArgumentParser:
@@ -354,12 +354,39 @@ async def async_main(args, engine=None, device_caps=None):
     seed_models(args.models_seed_dir)
   node, api, engine, viz = build_node(args, engine=engine, device_caps=device_caps)
   loop = asyncio.get_running_loop()
+  # SIGINT / SIGTERM end the command, then the node shuts down in order (tasks, discovery, gRPC server, API)
+  # before the loop closes -- cancelling every task from the handler instead (the reference's helpers.shutdown,
+  # xotorch/helpers.py:318-326) left the gRPC server's own shutdown to run on a closed loop
+  stop = asyncio.Event()
+
+  def on_signal(s):
+    print(f"Received exit signal {s.name}...")
+    stop.set()
+
   for s in (signal.SIGINT, signal.SIGTERM):
     try:
-      loop.add_signal_handler(s, lambda s=s: asyncio.ensure_future(shutdown(s, loop, node.server)))
+      loop.add_signal_handler(s, on_signal, s)
     except NotImplementedError:  # pragma: no cover
       pass
-  await node.start(wait_for_peers=args.wait_for_peers)
+  work = asyncio.ensure_future(_command(args, node, api, viz))
+  halt = asyncio.ensure_future(stop.wait())
+  rc = 0
+  try:
+    await node.start(wait_for_peers=args.wait_for_peers)
+    done, _ = await asyncio.wait({work, halt}, return_when=asyncio.FIRST_COMPLETED)
+    if work in done:
+      rc = work.result() or 0
+  finally:
+    for t in (work, halt):
+      t.cancel()
+    await asyncio.gather(work, halt, return_exceptions=True)
+    await node.stop()
+    if api is not None:
+      await api.stop()
+  return rc
+
+
+async def _command(args, node, api, viz) -> int:
   model_name = args.model_name or args.run_model
   if args.command == "run" or args.run_model:
     if not model_name:
@@ -381,7 +408,6 @@ async def async_main(args, engine=None, device_caps=None):
     await asyncio.Event().wait()
   if args.wait_for_peers > 0:
     await asyncio.sleep(5)  # let peers finish their side of the last request
-  await node.stop()
   return 0
 
 

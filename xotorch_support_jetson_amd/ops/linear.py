@@ -387,7 +387,10 @@ class GemmPolicy:
     got = self._lookup(key)
     if got is not None:
       return got
-    if TALL_FIXED and W4 and M >= W4_PREF_M and N % 256 == 0 and Kd % 128 == 0 and not (epi == "resid" and out_dtype == torch.float32):
+    if (TALL_FIXED and W4 and M >= W4_PREF_M and N % 256 == 0 and Kd % 128 == 0
+        and not (epi == "resid" and out_dtype == torch.float32) and M * x.stride(0) * 2 < (1 << 32)):
+      # (the last term: the tile's LDS-DMA loads take 32-bit byte offsets into X; taller / wider X take the
+      # tuned candidates below)
       # tall GEMMs (prefill chunks, training): the four-wave tile at S = 1 won every tuned tall shape this round
       # (profiles/r5/headline/bench_r5o_tunelog.log), so it is taken without the cold-timing pass, which cost
       # ~0.5 s inside the first prefill chunk of every fresh process

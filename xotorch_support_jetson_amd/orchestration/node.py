@@ -356,10 +356,12 @@ class Node:
                             request_id: Optional[str] = None):
     shard = self.get_current_shard(base_shard)
     kind = "train" if train else "eval"
+    # (a downstream stage's example is a bf16 activation tensor, which numpy cannot hold)
+    shape = [int(d) for d in (example.shape if hasattr(example, "shape") else np.asarray(example).shape)]
     asyncio.create_task(self.broadcast_opaque_status(request_id, json.dumps({
       "type": "node_status", "node_id": self.id, "status": f"start_{kind}_example", "base_shard": base_shard.to_dict(),
-      "shard": shard.to_dict(), "example_size": int(np.asarray(example).size),
-      "example_shape": list(np.asarray(example).shape), "request_id": request_id})))
+      "shard": shard.to_dict(), "example_size": int(np.prod(shape)), "example_shape": shape,
+      "request_id": request_id})))
     t0 = time.perf_counter_ns()
     resp = await self._process_example(shard, example, target, length, train, request_id)
     asyncio.create_task(self.broadcast_opaque_status(request_id, json.dumps({

@@ -84,7 +84,8 @@ class P2PTransport:
   """
 
   def __init__(self, rank: int, world: int, monitor: Optional[HealthMonitor] = None,
-               injector: Optional[FaultInjector] = None):
+               injector: Optional[FaultInjector] = None, edges: Optional[list] = None):
+    """`edges`: the directed (src, dst) pairs to give communicators (default: the ring's neighbour edges)."""
     self.rank, self.world = rank, world
     self.monitor = monitor  # parallel/health.py: host waits raise PeerFailure instead of hanging
     self.injector = injector if injector is not None else FaultInjector.from_env(rank, monitor)
@@ -94,7 +95,7 @@ class P2PTransport:
     self.sent_bytes = 0  # payload handed to isend (bench diagnostics)
     if world > 1 and dist.is_initialized():
       self._staged = dist.get_backend() == "gloo"
-      for e in ring_edges(world):  # every rank creates every group, in the same order
+      for e in (edges if edges is not None else ring_edges(world)):  # every rank creates every group, in order
         self._groups[e] = dist.new_group(ranks=sorted(e))
 
   def _group(self, src: int, dst: int):

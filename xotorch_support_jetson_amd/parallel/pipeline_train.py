@@ -118,11 +118,21 @@ class PipelineTrainer:
         self._bwd(b, saved.pop(i), denom, losses)
     self.t.drain()
     if self.tied_group is not None and self.tied_name is not None:
-      p = tr.params[self.tied_name]
-      g = p.grad if p.grad is not None else torch.zeros_like(p)
-      g = g.float()
+      # the local gradient of this stage's copy: on the GPU it sits in a GradAcc buffer (fp32 embedding
+      # index-add, fused-CE dHead), which tr.grads() prefers over p.grad -- sum THAT over the two ends and
+      # write it back where the optimizer reads it, so both copies take the same update
+      name = self.tied_name
+      p = tr.params[name]
+      g = tr.grads().get(name)
+      g = torch.zeros_like(p, dtype=torch.float32) if g is None else g.float()
       dist.all_reduce(g, group=self.tied_group)
-      p.grad = g.to(p.dtype)
+      acc = tr.acc.get(name)
+      if acc is not None:
+        acc.buf.copy_(g)
+        acc.fresh = False
+        p.grad = None
+      else:
+        p.grad = g.to(p.dtype)
     tied_copy = ("lm_head",) if (self.tied_group is not None and self.last) else ()
     tr.apply(self._reduce_sq, norm_exclude=tied_copy)
     loss = float(torch.stack(losses).sum()) if losses else None

@@ -125,8 +125,14 @@ def load_shard_checkpoint(engine, shard: Shard, path: str | Path) -> None:
   from ..models.weights import copy_weights_into, from_hf_state_dict
   path = Path(path)
   cfg = engine.runner.config
+  m = _NAME.match(path.name)
   if path.is_dir():
     _, files = select_checkpoint_files(path, shard)
+  elif m and (not path.exists() or not (int(m.group(1)) <= shard.start_layer and shard.end_layer <= int(m.group(2)))):
+    # a file name that does not cover the shard (or was never written as one file) names an iteration: take that
+    # iteration's partition from its directory (e.g. a checkpoint a federated box saved as one file per local
+    # sub-range, loaded under another split)
+    _, files = select_checkpoint_files(path.parent.parent, shard, iteration=int(m.group(4)))
   else:
     files = [path]
   sd = _gather_tensors(files, shard, cfg.tie_word_embeddings)
