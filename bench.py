@@ -38,6 +38,75 @@ def sync():
     torch.cuda.synchronize()
 
 
+class ClockSampler:
+  """Board power / shader clock of this rank's GPU over the timed rounds (rocm-smi, read-only, ~0.3 s apart): a
+  decode step is GEMM-bound at the board power cap, so a slow box shows up here (a lower sclk at the same cap)."""
+
+  def __init__(self, device_index: int, enabled: bool = True):
+    import shutil
+    import threading
+    self.idx = device_index
+    self.samples = []
+    self._stop = threading.Event()
+    on = enabled and shutil.which("rocm-smi") is not None
+    self._t = threading.Thread(target=self._run, daemon=True) if on else None
+
+  def _one(self):
+    import re
+    import subprocess
+    r = subprocess.run(["rocm-smi", "-d", str(self.idx), "--showpower", "--showclocks", "--json"],
+                       capture_output=True, text=True, timeout=10)
+    card = next(iter(json.loads(r.stdout).values()))
+    power = sclk = None
+    for k, v in card.items():
+      if "Power" in k and power is None:
+        try:
+          power = float(str(v).split()[0])
+        except ValueError:
+          pass
+      if k.startswith("sclk"):
+        m = re.search(r"(\d+)\s*Mhz", str(v), re.I)
+        sclk = float(m.group(1)) if m else None
+    return power, sclk
+
+  def _run(self):
+    while not self._stop.is_set():
+      try:
+        self.samples.append(self._one())
+      except Exception:  # noqa: BLE001 - diagnostics only
+        pass
+      self._stop.wait(0.3)
+
+  def __enter__(self):
+    if self._t is not None:
+      self._t.start()
+    return self
+
+  def __exit__(self, *exc):
+    self._stop.set()
+    if self._t is not None:
+      self._t.join(15)
+
+  def summary(self) -> dict:
+    ps = [p for p, _ in self.samples if p is not None]
+    cs = [c for _, c in self.samples if c is not None]
+    mean = lambda xs: round(sum(xs) / len(xs), 1) if xs else None  # noqa: E731
+    return {"samples": len(self.samples), "power_w_mean": mean(ps), "power_w_max": max(ps) if ps else None,
+            "sclk_mhz_mean": mean(cs), "sclk_mhz_min": min(cs) if cs else None}
+
+
+def gemm_choices(batch: int) -> dict:
+  """The GEMM configuration the warmup tuner chose for each decode projection shape of this batch (kernel, tile
+  code | n-tiles, K split): what a fresh box picked, so a slow record can be told from a different tile pick."""
+  from xotorch_support_jetson_amd.ops import linear as L
+  mb = L._m_bucket(batch)
+  out = {}
+  for k, v in L.policy.table.items():
+    if len(k) >= 5 and k[0] == "sh" and k[1] == mb:
+      out[f"N{k[2]} K{k[3]} {k[4]}"] = list(v) if isinstance(v, tuple) else v
+  return out
+
+
 def main():
   ap = argparse.ArgumentParser()
   ap.add_argument("--gpus", type=int, default=1)
@@ -124,13 +193,15 @@ def main():
   sync()
   stage.start_timing()  # device events around each tick: stage work vs. waiting for the previous stage
   sent0 = transport.sent_bytes
-  t0 = time.perf_counter()
-  toks = run_decode_steps(stage, mbs, args.steps, first_tokens=toks if stage.last else None, record=rec)
-  transport.drain()
-  sync()
-  if world > 1:
-    dist.barrier()
-  elapsed = time.perf_counter() - t0
+  clocks = ClockSampler(dev.index or 0, enabled=dev.type == "cuda")
+  with clocks:
+    t0 = time.perf_counter()
+    toks = run_decode_steps(stage, mbs, args.steps, first_tokens=toks if stage.last else None, record=rec)
+    transport.drain()
+    sync()
+    if world > 1:
+      dist.barrier()
+    elapsed = time.perf_counter() - t0
   if world > 1:
     e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     dist.all_reduce(e, op=dist.ReduceOp.MAX)
@@ -139,7 +210,8 @@ def main():
   # per-rank diagnostics (after the timed region): a multi-GPU run that under-delivers shows which stage is
   # the slow one (stage_ms) and where the ring starves (recv_wait_ms)
   mine = dict(rank=rank, layers=f"{shard.start_layer}-{shard.end_layer}", **stage.timing(),
-              send_mb_per_step=round((transport.sent_bytes - sent0) / args.steps / 1e6, 3))
+              send_mb_per_step=round((transport.sent_bytes - sent0) / args.steps / 1e6, 3),
+              gpu=clocks.summary(), gemm=gemm_choices(B))
   per_rank = [mine]
   if world > 1:
     per_rank = [None] * world

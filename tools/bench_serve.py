@@ -105,10 +105,13 @@ async def ring_main(a):
   from aiohttp import ClientSession, TCPConnector
   port = free_port()
   env = dict(os.environ, XOT_MAX_BATCH=str(max(a.concurrency, 1)))
-  cmd = [sys.executable, "-m", "xotorch_support_jetson_amd.main", "--gpus", str(a.ring), "--default-model", a.model,
-         "--chatgpt-api-port", str(port), "--disable-tui", "--max-generate-tokens", str(a.max_tokens)]
+  # --ring always: `xot --gpus 1` alone is the single-process Node path (main.run sets args.ring only for N > 1)
+  cmd = [sys.executable, "-m", "xotorch_support_jetson_amd.main", "--gpus", str(a.ring), "--ring", "--default-model",
+         a.model, "--chatgpt-api-port", str(port), "--disable-tui", "--max-generate-tokens", str(a.max_tokens)]
   root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-  proc = subprocess.Popen(cmd, cwd=root, env=env, start_new_session=True)
+  log_path = a.server_log or os.path.join(tempfile.gettempdir(), f"xot_ring_{port}.log")
+  log_f = open(log_path, "w")
+  proc = subprocess.Popen(cmd, cwd=root, env=env, start_new_session=True, stdout=log_f, stderr=subprocess.STDOUT)
   base = f"http://127.0.0.1:{port}"
   try:
     async with ClientSession(connector=TCPConnector(limit=0)) as session:
@@ -137,10 +140,15 @@ async def ring_main(a):
       proc.wait(timeout=60)
     except (ProcessLookupError, subprocess.TimeoutExpired):
       os.killpg(proc.pid, signal.SIGKILL)
+    log_f.close()
+  # which server answered: RingServer's rank 0 announces its API as "[ring 0] ChatGPT API on ..."
+  with open(log_path) as f:
+    server = "RingServer" if "[ring 0] ChatGPT API" in f.read() else "Node (single-process)"
   toks = sum(r[1] for r in res)
   ttfts = sorted(r[0] for r in res)
   print(json.dumps({"metric": f"API streaming output tokens/sec (ring of {a.ring} ranks)", "model": a.model,
-                    "ring": a.ring, "dist_backend": os.environ.get("XOT_DIST_BACKEND", "nccl"),
+                    "ring": a.ring, "server": server, "server_log": log_path,
+                    "dist_backend": os.environ.get("XOT_DIST_BACKEND", "nccl"),
                     "concurrency": a.concurrency, "prompt_words": a.prompt_words, "max_tokens": a.max_tokens,
                     "output_tokens": toks, "value": round(toks / wall, 2), "unit": "tokens/s",
                     "wall_s": round(wall, 2), "warmup_s": round(warm, 1),
@@ -268,7 +276,8 @@ if __name__ == "__main__":
   ap.add_argument("--in-process-clients", dest="client_proc", action="store_false",
                   help="run the HTTP clients on the server's event loop (their SSE parsing then counts as server time)")
   ap.add_argument("--client", default=None, help=argparse.SUPPRESS)  # internal: load-generator child mode
-  ap.add_argument("--ring", type=int, default=0, help="serve from `xot --gpus N` (the RCCL ring server) instead")
+  ap.add_argument("--ring", type=int, default=0, help="serve from `xot --gpus N --ring` (the RCCL ring server) instead")
+  ap.add_argument("--server-log", default=None, help="--ring: where the server's output goes (default: a temp file)")
   if os.environ.get("XOT_PROFILE"):  # host-side hot spots of the serving loop (main thread)
     import cProfile
     PROF = cProfile.Profile()

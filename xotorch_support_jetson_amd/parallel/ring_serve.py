@@ -881,7 +881,16 @@ async def _rank0_main(srv: RingServer, shard, tok, cfg, a: dict) -> None:
       await run_chat_tui(SimpleNamespace(default_model=a["model"], model_name=a["model"],
                                          chatgpt_api_response_timeout=a["response_timeout"]), api, node)
       return
-    await asyncio.Event().wait()
+    stop = asyncio.Event()  # SIGTERM / SIGINT: close the API, then stop the ring in order (exit code 0)
+    import signal
+    for sig in (signal.SIGINT, signal.SIGTERM):
+      try:
+        loop.add_signal_handler(sig, stop.set)
+      except (NotImplementedError, RuntimeError):  # pragma: no cover
+        pass
+    await stop.wait()
+    print("[ring 0] exit signal: shutting down", flush=True)
+    await api.stop()
   finally:
     srv.stop()
     await asyncio.get_running_loop().run_in_executor(None, th.join, 60)
