@@ -13,14 +13,12 @@ def test_decode_partition_defaults():
   # many pairs: one wave per unit with page prefetch
   ppp, nparts, algo = ws.partition(512, 8, 9)
   assert algo == 2 and ppp * nparts >= 9
-  assert K.WG8_MAX_PAGES == 0 or ws.partition(1, 8, K.WG8_MAX_PAGES)[2] == 4
 
 
-def test_decode_partition_wg8_opt_in(monkeypatch):
-  monkeypatch.setattr(K, "WG8_MAX_PAGES", 16)
+
+def test_decode_partition_small_batch():
   ws = K.DecodeWorkspace(8, 32, 128, 4096, torch.device("cpu"), algo=-1)
-  assert ws.partition(1, 8, 16) == (16, 1, 4)  # one partition, 8 waves
-  assert ws.partition(1, 8, 32)[2] == 0  # wider tables keep the split
+  assert ws.partition(1, 8, 16)[2] == 0 and ws.partition(1, 8, 32)[2] == 0  # the workgroup kernel, split
   assert ws.partition(8, 8, 8)[2] == 2  # 64 pairs: the wave kernel
   fixed = K.DecodeWorkspace(8, 32, 128, 4096, torch.device("cpu"), pages_per_part=4, algo=-1)
   assert fixed.partition(1, 8, 16)[2] == 0  # an explicit partition size is honoured
@@ -28,7 +26,6 @@ def test_decode_partition_wg8_opt_in(monkeypatch):
 
 def test_slab_charge(monkeypatch):
   assert L._slab_read_ms(("big", 256, 1), 512, 8192) == 0.0
-  assert L._slab_read_ms(("sk", 256, 1), 512, 8192) == 0.0
   four = L._slab_read_ms(("big", 256, 4), 512, 8192)
   assert abs(four - 4 * 512 * 8192 * 4 / (L.SLAB_TBPS * 1e9)) < 1e-12
   assert L._slab_read_ms(("big", 256, 2), 512, 8192) * 2 == four

@@ -218,30 +218,23 @@ def test_attn_decode(gpu, H, Hkv, Dh, ctx):
   q = torch.randn(B, H, Dh, device=gpu, dtype=torch.bfloat16)
   scale = 1 / math.sqrt(Dh)
   ref = R.attn_decode(q, kc, vc, bt, cl, scale)
-  for algo in (0, 1, 2, 3, 4, 5, 6):  # workgroup kernel; wave kernel without / with page prefetch (2 / 3: double
-    # register set, 5 / 6: one set refilled per half), + nt loads; 8-wave
+  for algo in (0, 1, 2, 3, 5, 6):  # workgroup kernel; wave kernel without / with page prefetch (2 / 3: double
+    # register set, 5 / 6: one set refilled per half), + nt loads
     for ppp in (1, 3, 4, 8, None):  # None: per-call choice from the batch
-      if (algo == 0 and ppp in (1, 3)) or (algo == 4 and ppp is not None):  # 4: one partition only
+      if algo == 0 and ppp in (1, 3):
         continue
       ws = K.DecodeWorkspace(B, H, Dh, maxb * 64, gpu, pages_per_part=ppp, algo=algo)
-      ws.tickets = torch.zeros(B * H, dtype=torch.int32, device=gpu)  # partitions merged in-kernel by the last arriver
       out = K.attn_decode(q, kc, vc, bt, cl, scale, ws)
       assert rel_err(out, ref) < 2e-2, (algo, ppp)
-      # the tickets are back at zero, so the next call merges again; the separate reduce agrees
-      assert int(ws.tickets.abs().sum()) == 0, (algo, ppp)
       again = K.attn_decode(q, kc, vc, bt, cl, scale, ws)
-      tk, ws.tickets = ws.tickets, None
-      red = K.attn_decode(q, kc, vc, bt, cl, scale, ws)
-      ws.tickets = tk
-      assert torch.equal(again, out) and rel_err(red, out) < 1e-3, (algo, ppp)
+      assert torch.equal(again, out), (algo, ppp)
 
 
 @pytest.mark.parametrize("H,Hkv,Dh", [(32, 8, 128), (32, 8, 64), (14, 2, 64)])
 @pytest.mark.parametrize("ctx", [[700, 65, 1, 1024], [1], [512, 3]])
-def test_attn_decode_auto_short_table(gpu, H, Hkv, Dh, ctx, monkeypatch):
-  """XOT_ATTN_WG8_PAGES=16: small batch over a block table of <= 16 pages takes the 8-wave single-partition
-  kernel."""
-  monkeypatch.setattr(K, "WG8_MAX_PAGES", 16)
+def test_attn_decode_auto_short_table(gpu, H, Hkv, Dh, ctx):
+  """The default choice at small batch over a short block table (the workgroup kernel below 64 (sequence, KV head)
+  pairs) against the fp32 reference."""
   torch.manual_seed(1)
   B, maxb = len(ctx), 16
   kc, vc = _make_cache(B * maxb + 3, Hkv, Dh, gpu)
@@ -249,7 +242,7 @@ def test_attn_decode_auto_short_table(gpu, H, Hkv, Dh, ctx, monkeypatch):
   cl = torch.tensor(ctx, device=gpu, dtype=torch.int32)
   q = torch.randn(B, H, Dh, device=gpu, dtype=torch.bfloat16)
   ws = K.DecodeWorkspace(B, H, Dh, maxb * 64, gpu, algo=-1)
-  assert ws.partition(B, Hkv, maxb) == (maxb, 1, 4)
+  assert ws.partition(B, Hkv, maxb)[2] in (0, 2)
   out = K.attn_decode(q, kc, vc, bt, cl, 1 / math.sqrt(Dh), ws)
   assert rel_err(out, R.attn_decode(q, kc, vc, bt, cl, 1 / math.sqrt(Dh))) < 2e-2
 
@@ -457,13 +450,6 @@ def test_gemm_stream(gpu, M, epi, ntw, splits):
     y = torch.empty(M, N, device=gpu, dtype=torch.float32)
   require().gemm_stream(x, w, y, b, r if epi == "resid" else None, ws, K.EPI[epi], ntw, splits, False)
   assert rel_err(y, ref) < 1e-2
-  if splits > 1:  # in-launch combine (tickets), twice: the counters must come back to zero
-    tk = torch.zeros(4096, dtype=torch.int32, device=gpu)
-    for _ in range(2):
-      y.zero_()
-      require().gemm_stream(x, w, y, b, r if epi == "resid" else None, ws, K.EPI[epi], ntw, splits, False, tk)
-      assert rel_err(y, ref) < 1e-2
-    assert int(tk.abs().sum()) == 0
   if True:  # pre-shuffled layout, every M (M > 128 runs the XCD-paired 128-row blocks)
     from xotorch_support_jetson_amd.ops.weights_layout import shuffle_for_stream
     y2 = torch.empty_like(y)
@@ -967,10 +953,12 @@ def test_moe_route_ds(gpu, E, k, ng, tg, method, sig, norm):
       assert off_c[e] <= so[t, j] < off_c[e + 1] and int(st[so[t, j]]) == t
 
 
-@pytest.mark.parametrize("R,C", [(256, 384), (128, 64), (512, 1024)])
+@pytest.mark.parametrize("R,C", [(256, 384), (128, 64), (512, 1024), (384, 1152), (1280, 256)])
 def test_relayout_kernels(gpu, R, C):
   """csrc/layout.hip: shuffle / shuffle of the transpose / transpose vs the torch permutations, from a
-  row-strided source."""
+  row-strided source -- the 128 x 128 transposed-LDS-read kernels (variant 2, the default where both dims are
+  multiples of 128) and the 128 x 64 staged-transpose kernels (variant 1) alike."""
+  from xotorch_support_jetson_amd.ops._ext import require
   from xotorch_support_jetson_amd.ops.weights_layout import shuffle_for_stream
   from xotorch_support_jetson_amd.train.autograd_ops import relayout
   torch.manual_seed(0)
@@ -980,6 +968,11 @@ def test_relayout_kernels(gpu, R, C):
     assert torch.equal(relayout(src, 0), shuffle_for_stream(src.contiguous()))
   assert torch.equal(relayout(src, 1), shuffle_for_stream(src.t().contiguous()))
   assert torch.equal(relayout(src, 2), src.t().contiguous())
+  for mode, want in ((1, shuffle_for_stream(src.t().contiguous())), (2, src.t().contiguous())):
+    for variant in (1, 2):
+      out = torch.full((C * R,), 7.0, device=gpu, dtype=torch.bfloat16).view(want.shape)
+      require().relayout(src, out, mode, variant)
+      assert torch.equal(out, want), (mode, variant)
 
 
 @pytest.mark.parametrize("with_h", [False, True])
@@ -1031,43 +1024,6 @@ def test_gemm_kgroup(gpu, resid):
 
 
 # ------------------------------------------------------------------ stream-K GEMM (the headline's gate/up)
-@pytest.mark.parametrize("M", [256, 300, 512, 1024, 2048])
-@pytest.mark.parametrize("N,Kd", [(2048, 4096), (7168, 8192)])  # 7168 = an eighth of 70B's 57344 gate/up
-@pytest.mark.parametrize("epi,f32", [("none", True), ("none", False), ("resid", False), ("silu", False)])
-def test_gemm_sk(gpu, M, N, Kd, epi, f32):
-  """csrc/gemm_sk.hip (persistent 256 x 256 tiles, k steps dealt evenly over the CUs, partial tiles combined by
-  the last arriver in group order) vs the fp32 reference: every epilogue, fp32 / bf16 out, masked row tiles;
-  two runs give identical bits (the fix-up order is fixed) and every ticket / flag word is zero again."""
-  from xotorch_support_jetson_amd.ops._ext import require
-  from xotorch_support_jetson_amd.ops.weights_layout import shuffle_for_stream
-  C = require()
-  torch.manual_seed(M + N + len(epi))
-  x = torch.randn(M, Kd, device=gpu, dtype=torch.bfloat16)
-  w = torch.randn(N, Kd, device=gpu, dtype=torch.bfloat16) / math.sqrt(Kd)
-  b = torch.randn(N, device=gpu, dtype=torch.bfloat16)
-  r = torch.randn(M, N, device=gpu, dtype=torch.bfloat16)
-  full = R.linear(x, w, b)
-  if epi == "silu":
-    f = full.view(M, N // 32, 2, 16)
-    ref = (torch.nn.functional.silu(f[:, :, 0]) * f[:, :, 1]).reshape(M, N // 2)
-  elif epi == "resid":
-    ref = full + r.float()
-  else:
-    ref = full
-  y = torch.empty(ref.shape, device=gpu, dtype=torch.float32 if f32 else torch.bfloat16)
-  part = torch.empty(C.gemm_sk_part_elems(), device=gpu, dtype=torch.float32)
-  sync = torch.zeros(C.gemm_sk_sync_words(M, N), device=gpu, dtype=torch.int32)
-  ws = shuffle_for_stream(w)
-  C.gemm_sk(x, ws, y, b, r if epi == "resid" else None, part, sync, K.EPI[epi], 256)
-  torch.cuda.synchronize()
-  assert rel_err(y, ref) < 1e-2
-  first = y.clone()
-  C.gemm_sk(x, ws, y, b, r if epi == "resid" else None, part, sync, K.EPI[epi], 256)
-  torch.cuda.synchronize()
-  assert torch.equal(y, first)
-  assert int(sync.abs().sum()) == 0
-
-
 @pytest.mark.parametrize("rows,D,S", [(1, 8192, 4), (300, 8192, 4), (512, 8192, 4), (512, 8192, 3), (512, 4096, 4),
                                       (256, 5120, 2), (512, 8192, 5)])
 def test_splitk_resid_rmsnorm(gpu, rows, D, S):

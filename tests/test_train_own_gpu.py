@@ -80,7 +80,7 @@ def test_xot_train_ragged_no_vendor_gemm(gpu, model, monkeypatch):
     if dev != "cpu":
       _guard(e, mode)
       _guard(e2, mode)
-    losses, grads = [], []
+    losses, grads, m1 = [], [], None
     for x, ln in zip(batches * 2, lens * 2):
       y = np.roll(x, -1, 1)
       h = await e.train_forward("t", a, x)
@@ -88,19 +88,25 @@ def test_xot_train_ragged_no_vendor_gemm(gpu, model, monkeypatch):
       await e.train("t", a, x, g, ln, loss="back_gradient")
       losses.append(loss)
       grads.append(torch.as_tensor(g).float().reshape(-1))
+      if m1 is None:  # AdamW's first moment after step 1: (1 - beta1) x the clipped gradient of every weight
+        m1 = {k: v.float().cpu().clone() for k, v in e2._get_trainer().m.items()}
     tr = e2._get_trainer()
     if dev != "cpu":
       assert tr.fused_head() and "linear" not in mode.seen and len(mode.seen) > 100
     delta = {k: tr.master[k].float().cpu() - init[k] for k in tr.master}
-    return losses, grads, delta
+    return losses, grads, delta, m1
 
-  lc, gc, wc = asyncio.run(run("cpu"))
-  lg, gg, wg = asyncio.run(run("cuda:0"))
+  lc, gc, wc, mc = asyncio.run(run("cpu"))
+  lg, gg, wg, mg = asyncio.run(run("cuda:0"))
   assert np.allclose(lc, lg, rtol=2e-2), (lc, lg)
   for x, y in zip(gc, gg):  # gradient wrt the stage input (the SendExample reply)
     cos = torch.nn.functional.cosine_similarity(x, y, dim=0).item()
     assert cos > 0.99, cos
-  for k in wc:  # four AdamW steps from the same start: the last stage's weight updates agree
+  for k in mc:  # every weight gradient of the last stage (own-kernel dW, fused CE dHead, norm dw) vs CPU fp32
+    d = ((mc[k] - mg[k]).abs().mean() / (mc[k].abs().mean() + 1e-12)).item()
+    assert d < 0.05, (k, d)
+  for k in wc:  # four AdamW steps from the same start: the updates (~ lr sign(m / sqrt(v)) early on, so elements
+    # with near-zero gradients may flip) agree in the mean
     d = ((wc[k] - wg[k]).abs().mean() / (wc[k].abs().mean() + 1e-12)).item()
     assert d < 0.25, (k, d)
 
@@ -138,13 +144,12 @@ def test_adamw_tiled_matches_adamw_and_relayout(N, K, gdt):
 
 
 @pytest.mark.parametrize("T", [300, 1024])
-def test_silu_down_fused_backward_matches_fp32(T, monkeypatch):
-  """A.SiluDownFn: y = (silu(gate) * up) . W_down^T + h, its backward with the SiLU derivative in the epilogue of
-  the down projection's dA GEMM (gemm_silu_bwd, four-wave tile), against fp32 torch autograd -- dGU, dh and the
-  fused-accumulated dW_down -- and against the two-kernel path (XOT_SILU_BWD_FUSED=0)."""
+def test_silu_down_backward_matches_fp32(T):
+  """A.SiluDownFn: y = (silu(gate) * up) . W_down^T + h and its backward (dA on the own tiles, silu_mul_bwd, the
+  fused-accumulated dW_down) against fp32 torch autograd: dGU, dh and dW."""
   from xotorch_support_jetson_amd.train import autograd_ops as A
   dev = torch.device("cuda", 0)
-  D, F = 384, 512  # F % 256, D % 128: the fused tile path
+  D, F = 384, 512
   torch.manual_seed(T)
   gu = (torch.randn(T, 2 * F, device=dev)).to(torch.bfloat16)
   w = (torch.randn(D, F, device=dev) / F ** 0.5).to(torch.bfloat16)
@@ -152,26 +157,18 @@ def test_silu_down_fused_backward_matches_fp32(T, monkeypatch):
   dy = torch.randn(T, D, device=dev).to(torch.bfloat16)
   tw = A.TrainWeight(w)
   assert tw.ok
-
-  def run(fused):
-    monkeypatch.setattr(A, "SILU_BWD_FUSED", fused)
-    acc = A.GradAcc("down", w)
-    g, hh = gu.clone().requires_grad_(), h.clone().requires_grad_()
-    y = A.silu_down_own(g, w, tw, acc, hh)
-    y.backward(dy)
-    A.join_dw_stream()
-    torch.cuda.synchronize()
-    return y.float(), g.grad.float(), hh.grad.float(), acc.buf.float()
-
+  acc = A.GradAcc("down", w)
+  g, hh = gu.clone().requires_grad_(), h.clone().requires_grad_()
+  y = A.silu_down_own(g, w, tw, acc, hh)
+  y.backward(dy)
+  A.join_dw_stream()
+  torch.cuda.synchronize()
   gf, hf = gu.float().requires_grad_(), h.float().requires_grad_()
   wf = w.float().requires_grad_()
   yr = (torch.nn.functional.silu(gf[:, :F]) * gf[:, F:]) @ wf.t() + hf
   yr.backward(dy.float())
-  ref = (yr, gf.grad, hf.grad, wf.grad)
-  fused, plain = run(True), run(False)
-  for name, a, b, r in zip(("y", "dgu", "dh", "dW"), fused, plain, ref):
+  for name, a, r in zip(("y", "dgu", "dh", "dW"), (y, g.grad, hh.grad, acc.buf), (yr, gf.grad, hf.grad, wf.grad)):
     assert rel_err(a, r) < 2e-2, (name, rel_err(a, r))
-    assert rel_err(a, b) < 2e-2, (name, rel_err(a, b))
 
 
 def rel_err(a, b):

@@ -81,8 +81,6 @@ def main():
       for algo, ppps in ((0, (4, 8, 16, 32)), (2, (2, 4, 8, 16))):
         for ppp in ppps:
           ws = K.DecodeWorkspace(B, H, Dh, pages * 64, dev, pages_per_part=ppp, algo=algo)
-          r[f"a{algo}_p{ppp}_t"] = round(graph_us(lambda: K.attn_decode(q, kc, vc, bt, cl, 1 / math.sqrt(Dh), ws, out)), 2)
-          ws.tickets = None  # separate reduce kernel
           r[f"a{algo}_p{ppp}_r"] = round(graph_us(lambda: K.attn_decode(q, kc, vc, bt, cl, 1 / math.sqrt(Dh), ws, out)), 2)
       ws = K.DecodeWorkspace(B, H, Dh, pages * 64, dev)
       r["auto"] = round(graph_us(lambda: K.attn_decode(q, kc, vc, bt, cl, 1 / math.sqrt(Dh), ws, out)), 2)

@@ -1,8 +1,7 @@
 #!/usr/bin/env python3
 """Training attention kernels in isolation at the Llama-3-8B training shape (B=2, L=2048, 32 / 8 heads of 128):
-forward, and the backward (transposes + dQ + dK/dV + reduce), median of N timed repetitions on one stream.
-The kernel variants are chosen by environment variables read once per process (XOT_TRAIN_DQ_V1,
-XOT_TRAIN_DKDV_V1, XOT_TRAIN_ATTN_V1), so an A/B runs this script once per setting.
+forward, and the backward (dQ + dK/dV + reduce), median of N timed repetitions on one stream.  (The round-5 v1
+backward kernels this used to A/B against were removed in round 6; their numbers are in profiles/r5/train/.)
 
   python tools/bench_attn_train.py [--B 2 --L 2048 --H 32 --Hkv 8 --Dh 128 --reps 20]"""
 import argparse
@@ -56,8 +55,7 @@ def main():
     torch.autograd.backward(o, do, retain_graph=True)
   t_bwd = timed(bwd)
   flops = 4 * B * H * Dh * L * L / 2  # causal: two L x L x Dh products, half the square
-  env = {k: os.environ[k] for k in ("XOT_TRAIN_DQ_V1", "XOT_TRAIN_DKDV_V1", "XOT_TRAIN_ATTN_V1") if k in os.environ}
-  print(json.dumps({"shape": [B, L, H, Hkv, Dh], "env": env, "fwd_us": round(t_fwd, 1), "bwd_us": round(t_bwd, 1),
+  print(json.dumps({"shape": [B, L, H, Hkv, Dh], "fwd_us": round(t_fwd, 1), "bwd_us": round(t_bwd, 1),
                     "fwd_tflops": round(flops / t_fwd / 1e6, 1), "bwd_tflops": round(2.5 * flops / t_bwd / 1e6, 1)}))
 
 

@@ -4,7 +4,7 @@ source "$(dirname "$0")/common.sh"
 for what in ${@:-gemm attn}; do
   case $what in
     gemm)    step kern/gemm_tests 400 python -u -m pytest tests/test_kernels_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread -k "gemm or moe"
-             step kern/gemm 600 python -u tools/bench_gemm_sk.py --ms 512,2048 --ops gate_up,down,qkv,o,gate_up_8b --json "$O/kern/gemm.json" ;;
+             step kern/gemm 600 python -u tools/bench_gemm_big.py ;;
     lab)     # standalone HIP lab (random operands, HBM-cold, variants interleaved): build it first with
              # hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/lab/gemm_lab2.hip -o tools/lab/gemm_lab2
              for a in "512 57344 8192" "2048 57344 8192" "512 8192 28672 -1 0"; do step kern/lab_${a// /_} 120 tools/lab/gemm_lab2 $a; done ;;

@@ -1,0 +1,30 @@
+#!/bin/bash
+# Round-6 headline experiments, one case per argument (each step under its own time limit, first failure ends):
+#   bash tools/gpu/r6.sh bench reduce nov prof ...
+# Every bench in one call shares one GEMM table (tuned once, by the first bench), so A/B arms run the same tiles.
+source "$(dirname "$0")/common.sh"
+T=$O/r6/gemm_table.json
+mkdir -p "$O/r6"
+for what in "$@"; do
+  case $what in
+    bench)  XOT_GEMM_TABLE=$T step r6/bench 400 python -u bench.py --steps 20 --warmup 5 ;;
+    bench2) XOT_GEMM_TABLE=$T step r6/bench2 400 python -u bench.py --steps 20 --warmup 5 ;;
+    reduce) step r6/reduce 120 python -u tools/bench_reduce.py ;;
+    nov)    XOT_EXP_NO_V=1 XOT_GEMM_TABLE=$T step r6/bench_nov 400 python -u bench.py --steps 20 --warmup 5 ;;
+    attn)   step r6/attn 200 python -u tools/bench_attn_b512.py ;;
+    prof)   XOT_GEMM_TABLE=$T prof r6/prof 600 python3 "$R/bench.py" --steps 6 --warmup 3
+            step r6/breakdown 60 python tools/decode_breakdown.py "$(ls "$O"/r6/prof/*/*kernel_trace.csv "$O"/r6/prof/*kernel_trace.csv 2>/dev/null | head -1)" --steps 6 --json "$O/r6/breakdown.json"
+            cat "$O/r6/breakdown.log" ;;
+    b1)     prof r6/prof8b1 300 python3 "$R/bench.py" --model llama-3-8b --batch-per-gpu 1 --steps 16 --warmup 4
+            step r6/breakdown8b1 60 python tools/decode_breakdown.py "$(ls "$O"/r6/prof8b1/*/*kernel_trace.csv "$O"/r6/prof8b1/*kernel_trace.csv 2>/dev/null | head -1)" --steps 16 --json "$O/r6/breakdown8b1.json" ;;
+    ring70) # RingServer (`xot --gpus 1 --ring`) at the headline operating point: Llama-3-70B, 512 streams x 128 tokens
+            step r6/ring70 1100 python -u tools/bench_serve.py --ring 1 --model llama-3-70b --concurrency 512 --max-tokens 128 --prompt-words 124 --server-log "$O/r6/ring70_server.log" ;;
+    layout) step r6/layout 120 python -u tools/bench_layout.py ;;
+    train)  step r6/train 900 python -u tools/bench_train.py --model llama-3-8b --seq 2048 --mb 2 --microbatches 4 --steps 3 --warmup 1 ;;
+    trainprof) prof r6/trainprof 900 python3 "$R/tools/bench_train.py" --mb 2 --microbatches 4 --steps 3 --warmup 1
+            step r6/trainstep 60 python tools/step_window.py "$(ls "$O"/r6/trainprof/*/*kernel_trace.csv "$O"/r6/trainprof/*kernel_trace.csv 2>/dev/null | head -1)" ;;
+    relayout_test) step r6/relayout_test 300 python -u -m pytest tests/test_kernels_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread -k relayout ;;
+    tests)  step r6/gpu_tests 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
+    *) echo "unknown case $what"; exit 2 ;;
+  esac
+done

@@ -8,7 +8,7 @@ are averaged, and the derived rates are computed:
   fetch_gb         FETCH_SIZE (KB) x 2 (gfx950 reports half the bytes of 16-B streaming reads)
   lds_conflict_pct SQ_LDS_BANK_CONFLICT / SQ_INSTS_LDS (extra cycles per LDS instruction, %)
 
-  python tools/pmc_summary.py gpurun_out/pmc/<name> --match gemm_big,gemm_sk,attn_decode --last 6 [--json out]
+  python tools/pmc_summary.py gpurun_out/pmc/<name> --match gemm_big,gemm_w4,attn_decode --last 6 [--json out]
   python tools/pmc_summary.py gpurun_out/pmc/<name> --window sample_fast_kernel --last 2   (decode steps of bench.py)
 """
 import argparse
@@ -38,7 +38,7 @@ def load_pass(d):
 def main():
   ap = argparse.ArgumentParser()
   ap.add_argument("root")
-  ap.add_argument("--match", default="gemm_big,gemm_sk,gemm_stream,attn_decode")
+  ap.add_argument("--match", default="gemm_big,gemm_w4,gemm_stream,attn_decode")
   ap.add_argument("--last", type=int, default=6)
   ap.add_argument("--json", default=None)
   ap.add_argument("--window", default=None,

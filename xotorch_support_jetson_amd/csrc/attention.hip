@@ -32,43 +32,6 @@ __device__ __forceinline__ void wave_lds_sync() {
 }
 
 // ============================================================================ decode
-// Merge the nparts partial (o, m, l) of the G query heads of KV head kvh of sequence b (log-sum-exp).
-// Every address depends on the thread's element, so the partials come in by vector loads (the scalar
-// cache would bypass the acquire that makes other workgroups' partials visible).
-template <int DH>
-__device__ __forceinline__ void combine_parts(const float* ws_o, const float* ws_ml, uint16_t* __restrict__ out,
-                                              int b, int kvh, int G, int H, int nparts, int tid, int nthr) {
-  for (int e = tid; e < G * DH; e += nthr) {
-    const int row = e / DH, d = e % DH, h = kvh * G + row;
-    const size_t base = ((size_t)b * H + h) * nparts;
-    float M = NEG_BIG;
-    for (int p = 0; p < nparts; ++p) M = fmaxf(M, ws_ml[(base + p) * 2]);
-    float L = 0.f, O = 0.f;
-    for (int p = 0; p < nparts; ++p) {
-      const float f = exp2f(ws_ml[(base + p) * 2] - M);
-      L += ws_ml[(base + p) * 2 + 1] * f;
-      O += ws_o[(base + p) * DH + d] * f;
-    }
-    out[((size_t)b * H + h) * DH + d] = f2bf(L > 0.f ? O / L : 0.f);
-  }
-}
-
-// Last-arriver hand-off of a partition's partials (cdna_hip_programming.md Guideline 16 recipe): the
-// caller's stores are drained, one lane releases at agent scope, drains again, adds to the (sequence,
-// KV head) ticket; the last of the nparts arrivals acquires and resets the ticket for the next launch.
-__device__ __forceinline__ bool partition_arrive_last(int* tickets, int slot, int nparts) {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  const int prev = __hip_atomic_fetch_add(tickets + slot, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const bool last = prev == nparts - 1;
-  if (last) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_store(tickets + slot, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  return last;
-}
-
 // NW waves share the pages of one (sequence, KV head, partition): 4 (algo 0), or 8 for one partition
 // over a short context at small batch (algo 4: at most two pages per wave and no merge launch, where
 // each further page a wave walks costs a dependent page-table -> K / V latency of ~3.5 us)
@@ -222,14 +185,6 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_kernel(
         ws_ml[idx * 2 + 1] = L;
       }
     }
-  }
-  if (nparts > 1 && tickets != nullptr) {  // the last partition of this (sequence, KV head) merges them all
-    __shared__ int last_s;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) last_s = partition_arrive_last(tickets, b * Hkv + kvh, nparts);
-    __syncthreads();
-    if (last_s) combine_parts<DH>(ws_o, ws_ml, out, b, kvh, G, H, nparts, threadIdx.x, NW * 64);
   }
 }
 
@@ -453,14 +408,6 @@ __device__ __forceinline__ void decode_wave_unit(
       ws_ml[idx * 2 + 1] = l;
     }
   }
-  if (tickets != nullptr) {  // the last partition of this (sequence, KV head) merges them all
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    int last = 0;
-    if (lane == 0) last = partition_arrive_last(tickets, b * Hkv + kvh, nparts);
-    last = __shfl(last, 0, 64);
-    // (lane 0's acquire precedes the other lanes' loads: one wave, program order)
-    if (last) combine_parts<DH>(ws_o, ws_ml, out, b, kvh, G, H, nparts, lane, 64);
-  }
 }
 
 
@@ -479,31 +426,25 @@ __global__ __launch_bounds__(PF == 2 ? 512 : 256, PF == 2 ? 2 : 1) void attn_dec
                                pages_per_part, nparts, scale_log2, num_pages, tickets, vtail != 0);
 }
 
-static int attn_vtail() {  // XOT_ATTN_VTAIL=0: read the last page's whole V^T rows (A/B)
-  static const int v = [] {
-    const char* e = getenv("XOT_ATTN_VTAIL");
-    return e != nullptr ? atoi(e) : 1;
-  }();
-  return v;
-}
-
 int launch_attn_decode(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, const int32_t* block_tables,
                        int max_blocks, const int32_t* ctx_lens, uint16_t* out, float* ws_o, float* ws_ml, int B,
                        int H, int Hkv, int Dh, int pages_per_part, int nparts, float scale, int num_pages, int algo,
-                       int* tickets, hipStream_t s) {
-  // tickets ([B * Hkv] int32, zero at rest): the last partition merges in-kernel, no reduce launch
-  const bool reduce = nparts > 1 && tickets == nullptr;
+                       hipStream_t s) {
+  // (an in-kernel merge by the last-arriving partition measured slower than the reduce launch in every
+  // configuration, profiles/bench_attn_small_r1.json, and was removed in round 6)
+  int* tickets = nullptr;
+  const bool reduce = nparts > 1;
   if (B <= 0) return 0;
   if (H % Hkv != 0 || H / Hkv > 16) return -1;
   dim3 grid(nparts, Hkv, B);
   const float sl = scale * LOG2E;
-  if (algo != 0 && algo != 4) {  // wave per (sequence, KV head, partition)
+  if (algo != 0) {  // wave per (sequence, KV head, partition)
     // algo 5 / 6: 8-wave workgroups (two waves per SIMD)
     const int units = B * Hkv * nparts, wpg = algo >= 5 ? 8 : 4;
     const int wgs = (units + wpg - 1) / wpg;
 #define XOT_WAVE(DHV, PFV, NTV)                                                                                  \
   attn_decode_wave_kernel<DHV, PFV, NTV><<<wgs, 64 * wpg, 0, s>>>(q, kc, vc, block_tables, max_blocks, ctx_lens, out, ws_o, \
-                                                        ws_ml, B, H, Hkv, pages_per_part, nparts, sl, num_pages, tickets, attn_vtail())
+                                                        ws_ml, B, H, Hkv, pages_per_part, nparts, sl, num_pages, tickets, 1)
     // algo 1: no prefetch; 2 / 3: double register set (3: nt loads); 5 / 6: one set refilled per half (6: nt)
     if (Dh == 128) {
       if (algo == 3) XOT_WAVE(128, 1, true); else if (algo == 2) XOT_WAVE(128, 1, false);
@@ -517,18 +458,6 @@ int launch_attn_decode(const uint16_t* q, const uint16_t* kc, const uint16_t* vc
       return -1;
     }
 #undef XOT_WAVE
-    return 0;
-  }
-  if (algo == 4) {  // 8 waves, one partition (the caller passes nparts 1)
-    if (nparts != 1) return -1;
-    if (Dh == 128)
-      attn_decode_kernel<128, 8><<<grid, 512, 0, s>>>(q, kc, vc, block_tables, max_blocks, ctx_lens, out, ws_o, ws_ml,
-                                                      H, Hkv, pages_per_part, 1, sl, num_pages, nullptr);
-    else if (Dh == 64)
-      attn_decode_kernel<64, 8><<<grid, 512, 0, s>>>(q, kc, vc, block_tables, max_blocks, ctx_lens, out, ws_o, ws_ml,
-                                                     H, Hkv, pages_per_part, 1, sl, num_pages, nullptr);
-    else
-      return -1;
     return 0;
   }
   if (Dh == 128) {

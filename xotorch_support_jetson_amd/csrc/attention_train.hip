@@ -467,245 +467,10 @@ __global__ __launch_bounds__(512, 1) void attn_train_fwd_v2_kernel(const uint16_
   }
 }
 
-// ---------------------------------------------------------------------------------------- dQ (+ delta)
-template <int DH>
-__global__ __launch_bounds__(256) void attn_train_dq_kernel(const uint16_t* __restrict__ Q, long ldq,
-                                                            const uint16_t* __restrict__ K, long ldk,
-                                                            const uint16_t* __restrict__ KT,
-                                                            const uint16_t* __restrict__ V, long ldv,
-                                                            const uint16_t* __restrict__ O, long ldo,
-                                                            const uint16_t* __restrict__ dO, long lddo, int Lp,
-                                                            const float* __restrict__ lse2, float* __restrict__ delta,
-                                                            uint16_t* __restrict__ dQ, long lddq, int L, int H,
-                                                            int Hkv, float scale) {
-  constexpr int KS = DH / 32, NDT = DH / 16;
-  constexpr int KLD = DH + 8, TLD = TT + 8, PLD = TT + 8;
-  __shared__ __attribute__((aligned(16))) uint16_t ks[TT * KLD];   // K rows (S = Q.K^T)
-  __shared__ __attribute__((aligned(16))) uint16_t vs[TT * KLD];   // V rows (dP = dO.V^T)
-  __shared__ __attribute__((aligned(16))) uint16_t kt_[DH * TLD];  // K^T (dQ += dS.K)
-  __shared__ __attribute__((aligned(16))) uint16_t pl[4][16 * PLD];
-  __shared__ float dl[4][16];
-  // query tiles are the slowest grid dimension, heaviest (most key tiles under the causal mask) first
-  const int h = blockIdx.x, qt = gridDim.y - 1 - blockIdx.y, b = blockIdx.z;
-  const int kvh = h / (H / Hkv);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
-  const int q0 = qt * TT, qrow = q0 + 16 * wave;
-  const uint16_t* Kb = K + (long)b * L * ldk + kvh * DH;
-  const uint16_t* Vb = V + (long)b * L * ldv + kvh * DH;
-  const uint16_t* KTb = KT + ((long)b * Hkv + kvh) * DH * Lp;
-  const float sl = scale * L2E;
-
-  RowsTile<DH> kr, vr;
-  TransTile<DH> ktr;
-  kr.load(Kb, ldk, 0, L);
-  vr.load(Vb, ldv, 0, L);
-  ktr.load(KTb, Lp, 0);
-
-  s16x8 qf[KS], df[KS];
-  float dsum = 0.f;
-  {
-    const long row = (long)b * L + min(qrow + c, L - 1);
-    const uint16_t* qp = Q + row * ldq + h * DH + 8 * g;
-    const uint16_t* dp = dO + row * lddo + h * DH + 8 * g;
-    const uint16_t* opp = O + row * ldo + h * DH + 8 * g;
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      qf[s] = ld16(qp + 32 * s);
-      df[s] = ld16(dp + 32 * s);
-      const s16x8 ov = ld16(opp + 32 * s);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) dsum += bf2f(df[s][e]) * bf2f(ov[e]);
-    }
-  }
-  // delta of row c: sum over the 4 lane groups; broadcast to the C layout (rows 4g + r) through LDS
-  dsum += __shfl_xor(dsum, 16, 64);
-  dsum += __shfl_xor(dsum, 32, 64);
-  if (g == 0) {
-    dl[wave][c] = dsum;
-    if (qrow + c < L) delta[((long)b * H + h) * L + qrow + c] = dsum;
-  }
-  wave_sync_lds();
-  float del[4], lse[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    del[r] = dl[wave][4 * g + r];
-    lse[r] = lse2[((long)b * H + h) * L + min(qrow + 4 * g + r, L - 1)];
-  }
-  f32x4 dq[NDT];
-#pragma unroll
-  for (int dt = 0; dt < NDT; ++dt) dq[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  uint16_t* pw = pl[wave];
-
-  for (int kt = 0; kt <= qt; ++kt) {
-    const int k0 = kt * TT;
-    __syncthreads();
-    kr.template store<KLD>(ks);
-    vr.template store<KLD>(vs);
-    ktr.template store<TLD>(kt_);
-    __syncthreads();
-    if (kt < qt) {
-      kr.load(Kb, ldk, k0 + TT, L);
-      vr.load(Vb, ldv, k0 + TT, L);
-      ktr.load(KTb, Lp, k0 + TT);
-    }
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      f32x4 sc = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        sc = mfma16(qf[s], ld16(ks + (16 * t + c) * KLD + 32 * s + 8 * g), sc);
-        dp = mfma16(df[s], ld16(vs + (16 * t + c) * KLD + 32 * s + 8 * g), dp);
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = k0 + 16 * t + c, qi = qrow + 4 * g + r;
-        const float p = (key <= qi && key < L) ? exp2f(sc[r] * sl - lse[r]) : 0.f;
-        pw[(4 * g + r) * PLD + 16 * t + c] = f2bf(p * (dp[r] - del[r]));
-      }
-    }
-    wave_sync_lds();
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const s16x8 da = ld16(pw + c * PLD + 32 * kk + 8 * g);
-#pragma unroll
-      for (int dt = 0; dt < NDT; ++dt) dq[dt] = mfma16(da, ld16(kt_ + (16 * dt + c) * TLD + 32 * kk + 8 * g), dq[dt]);
-    }
-  }
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int qi = qrow + 4 * g + r;
-    if (qi >= L) continue;
-    uint16_t* op = dQ + ((long)b * L + qi) * lddq + h * DH + c;
-#pragma unroll
-    for (int dt = 0; dt < NDT; ++dt) op[16 * dt] = f2bf(dq[dt][r] * scale);
-  }
-}
-
 // ---------------------------------------------------------------------------------------- dK, dV
 // DKW = 8 waves: 128 keys per workgroup share each staged query tile (2 waves per SIMD, so one wave's
 // LDS reads and exp2 hide under the other's MFMAs; with 4 waves the LDS footprint left one wave per SIMD)
 constexpr int DKW = 8, DKT = 16 * DKW;
-template <int DH>
-__global__ __launch_bounds__(64 * DKW) void attn_train_dkdv_kernel(const uint16_t* __restrict__ Q, long ldq,
-                                                              const uint16_t* __restrict__ QT,
-                                                              const uint16_t* __restrict__ K, long ldk,
-                                                              const uint16_t* __restrict__ V, long ldv,
-                                                              const uint16_t* __restrict__ dO, long lddo,
-                                                              const uint16_t* __restrict__ dOT, int Lp,
-                                                              const float* __restrict__ lse2,
-                                                              const float* __restrict__ delta,
-                                                              float* __restrict__ wk, float* __restrict__ wv, int L,
-                                                              int H, int Hkv, float scale) {
-  constexpr int KS = DH / 32, NDT = DH / 16;
-  constexpr int RLD = DH + 8, TLD = TT + 8, PLD = TT + 8;
-  extern __shared__ __attribute__((aligned(16))) uint16_t sm[];
-  uint16_t* qs = sm;                 // Q rows       [64][RLD]
-  uint16_t* ds_ = qs + TT * RLD;     // dO rows      [64][RLD]
-  uint16_t* qt_ = ds_ + TT * RLD;    // Q^T          [DH][TLD]
-  uint16_t* dt_ = qt_ + DH * TLD;    // dO^T         [DH][TLD]
-  uint16_t* pt = dt_ + DH * TLD;     // P^T / dS^T   [DKW waves][2][16][PLD]
-  float* ld_ = reinterpret_cast<float*>(pt + DKW * 2 * 16 * PLD);  // lse2[64], delta[64]
-  // one workgroup per (query head of the group, key tile, batch); key tiles are the slowest grid
-  // dimension with the heaviest (kt = 0: every query tile) first, so the causal imbalance load-balances
-  const int G = H / Hkv;
-  const int hq = blockIdx.x, kvh = hq / G, hh = hq % G, kt = blockIdx.y, b = blockIdx.z;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
-  const int k0 = kt * DKT, krow = k0 + 16 * wave;
-  const float sl = scale * L2E;
-  const int qt0 = k0 / TT;  // first query tile with a query >= a key of this workgroup
-  const int nq = (L + TT - 1) / TT, iters = nq - qt0;
-
-  RowsTile<DH, 64 * DKW> qr, dr;
-  TransTile<DH, 64 * DKW> qtr, dtr;
-  float lsv = 0.f, dlv = 0.f;
-  auto load = [&](int it) {  // (head, query tile) of iteration it into registers
-    const int h = hq, q0 = (qt0 + it) * TT;
-    qr.load(Q + (long)b * L * ldq + h * DH, ldq, q0, L);
-    dr.load(dO + (long)b * L * lddo + h * DH, lddo, q0, L);
-    qtr.load(QT + ((long)b * H + h) * DH * Lp, Lp, q0);
-    dtr.load(dOT + ((long)b * H + h) * DH * Lp, Lp, q0);
-    if (threadIdx.x < TT) {
-      const long idx = ((long)b * H + h) * L + min(q0 + (int)threadIdx.x, L - 1);
-      lsv = lse2[idx];
-      dlv = delta[idx];
-    }
-  };
-
-  s16x8 kf[KS], vf[KS];
-  {
-    const long row = (long)b * L + min(krow + c, L - 1);
-    const uint16_t* kp = K + row * ldk + kvh * DH + 8 * g;
-    const uint16_t* vp = V + row * ldv + kvh * DH + 8 * g;
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      kf[s] = ld16(kp + 32 * s);
-      vf[s] = ld16(vp + 32 * s);
-    }
-  }
-  f32x4 dk[NDT], dv[NDT];
-#pragma unroll
-  for (int dt = 0; dt < NDT; ++dt) dk[dt] = dv[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  uint16_t* pw = pt + wave * 2 * 16 * PLD;  // [0]: P^T, [1]: dS^T
-
-  if (iters > 0) load(0);
-  for (int it = 0; it < iters; ++it) {
-    const int q0 = (qt0 + it) * TT;
-    __syncthreads();
-    qr.template store<RLD>(qs);
-    dr.template store<RLD>(ds_);
-    qtr.template store<TLD>(qt_);
-    dtr.template store<TLD>(dt_);
-    if (threadIdx.x < TT) {
-      ld_[threadIdx.x] = lsv;
-      ld_[TT + threadIdx.x] = dlv;
-    }
-    __syncthreads();
-    if (it + 1 < iters) load(it + 1);
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {  // 16-query sub-tiles: query on the lane (column c)
-      f32x4 st = f32x4{0.f, 0.f, 0.f, 0.f}, dpt = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        st = mfma16(kf[s], ld16(qs + (16 * t + c) * RLD + 32 * s + 8 * g), st);
-        dpt = mfma16(vf[s], ld16(ds_ + (16 * t + c) * RLD + 32 * s + 8 * g), dpt);
-      }
-      const int qi = q0 + 16 * t + c;
-      const float lq = ld_[16 * t + c], dq = ld_[TT + 16 * t + c];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = krow + 4 * g + r;
-        const float p = (key <= qi && qi < L) ? exp2f(st[r] * sl - lq) : 0.f;
-        pw[(4 * g + r) * PLD + 16 * t + c] = f2bf(p);
-        pw[16 * PLD + (4 * g + r) * PLD + 16 * t + c] = f2bf(p * (dpt[r] - dq));
-      }
-    }
-    wave_sync_lds();
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const s16x8 pa = ld16(pw + c * PLD + 32 * kk + 8 * g);
-      const s16x8 sa = ld16(pw + 16 * PLD + c * PLD + 32 * kk + 8 * g);
-#pragma unroll
-      for (int dt = 0; dt < NDT; ++dt) {
-        dv[dt] = mfma16(pa, ld16(dt_ + (16 * dt + c) * TLD + 32 * kk + 8 * g), dv[dt]);
-        dk[dt] = mfma16(sa, ld16(qt_ + (16 * dt + c) * TLD + 32 * kk + 8 * g), dk[dt]);
-      }
-    }
-  }
-  // fp32 partials of this query head: slab hh of [G][B*L, Hkv*DH] (summed + scaled by the reduce kernel)
-  const long slab = (long)hh * ((long)gridDim.z * L) * (Hkv * DH);
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int key = krow + 4 * g + r;
-    if (key >= L) continue;
-    const long off = slab + ((long)b * L + key) * (Hkv * DH) + kvh * DH + c;
-#pragma unroll
-    for (int dt = 0; dt < NDT; ++dt) {
-      wk[off + 16 * dt] = dk[dt][r];
-      wv[off + 16 * dt] = dv[dt][r];
-    }
-  }
-}
-
 // dK = scale * sum_h wk[h], dV = sum_h wv[h]  ([G][rows][cols] fp32 -> bf16 row views)
 __global__ __launch_bounds__(256) void attn_train_dkdv_reduce_kernel(const float* __restrict__ wk,
                                                                      const float* __restrict__ wv, int G, long rows,
@@ -987,11 +752,6 @@ static size_t dkdv_v2_smem() {
   return (size_t)(2 * TT * tr_ld(DH)) * 2 + 2 * TT * sizeof(float);
 }
 
-template <int DH>
-static size_t dkdv_smem() {
-  return (size_t)(2 * TT * (DH + 8) + 2 * DH * (TT + 8) + DKW * 2 * 16 * (TT + 8)) * 2 + 2 * TT * sizeof(float);
-}
-
 int launch_attn_train_transpose(const uint16_t* x, long ldx, uint16_t* xt, int B, int L, int Lp, int n, int Dh,
                                 hipStream_t s) {
   if (B <= 0 || L <= 0) return 0;
@@ -1008,21 +768,12 @@ int launch_attn_train_transpose(const uint16_t* x, long ldx, uint16_t* xt, int B
   return 0;
 }
 
-// XOT_TRAIN_ATTN_V1=1: the first forward kernel for every shape (A/B)
-static bool attn_train_fwd_v2_on() {
-  static const bool on = [] {
-    const char* e = getenv("XOT_TRAIN_ATTN_V1");
-    return !(e != nullptr && e[0] == '1');
-  }();
-  return on;
-}
-
 int launch_attn_train_fwd(const uint16_t* q, long ldq, const uint16_t* k, long ldk, const uint16_t* vt, int Lp,
                           uint16_t* o, long ldo, float* lse2, int B, int L, int H, int Hkv, int Dh, float scale,
                           bool causal, hipStream_t s) {
   if (B <= 0 || L <= 0) return 0;
   if (H % Hkv != 0 || Lp % TT != 0 || Lp < L) return -1;
-  if (causal && (Dh == 128 || Dh == 64) && attn_train_fwd_v2_on()) {
+  if (causal && (Dh == 128 || Dh == 64)) {  // v2; the first kernel keeps Dh 192 and the bidirectional case
     const dim3 grid2((L * (H / Hkv) + 255) / 256, Hkv, B);
     const size_t lds = (size_t)3 * 2 * TT * Dh * 2;
     const float sl = scale * L2E;
@@ -1055,9 +806,8 @@ int launch_attn_train_fwd(const uint16_t* q, long ldq, const uint16_t* k, long l
   return 0;
 }
 
-int launch_attn_train_bwd(const uint16_t* q, long ldq, const uint16_t* qt, const uint16_t* k, long ldk,
-                          const uint16_t* kt, const uint16_t* v, long ldv, const uint16_t* o, long ldo,
-                          const uint16_t* dout, long lddo, const uint16_t* doutt, int Lp, const float* lse2,
+int launch_attn_train_bwd(const uint16_t* q, long ldq, const uint16_t* k, long ldk, const uint16_t* v, long ldv,
+                          const uint16_t* o, long ldo, const uint16_t* dout, long lddo, int Lp, const float* lse2,
                           float* delta, uint16_t* dq, long lddq, uint16_t* dk, long lddk, uint16_t* dv, long lddv,
                           float* ws, long ws_elems, int B, int L, int H, int Hkv, int Dh, float scale, hipStream_t s) {
   if (B <= 0 || L <= 0) return 0;
@@ -1065,45 +815,20 @@ int launch_attn_train_bwd(const uint16_t* q, long ldq, const uint16_t* qt, const
   const long slab = (long)B * L * Hkv * Dh;
   if (ws == nullptr || ws_elems < 2 * (long)(H / Hkv) * slab) return -1;
   float *wk = ws, *wv = ws + (long)(H / Hkv) * slab;
-  dim3 gq(H, (L + TT - 1) / TT, B), gk(H, (L + DKT - 1) / DKT, B);
-  static const bool dkdv_v1 = [] {  // XOT_TRAIN_DKDV_V1=1: the P^T-through-LDS kernel (A/B)
-    const char* e = getenv("XOT_TRAIN_DKDV_V1");
-    return e != nullptr && e[0] == '1';
-  }();
-  static const bool dq_v1 = [] {  // XOT_TRAIN_DQ_V1=1: the dS-through-LDS kernel (A/B)
-    const char* e = getenv("XOT_TRAIN_DQ_V1");
-    return e != nullptr && e[0] == '1';
-  }();
-  if ((dq_v1 && kt == nullptr) || (dkdv_v1 && (qt == nullptr || doutt == nullptr))) return -1;
-  static const int hpw_env = [] {  // XOT_TRAIN_DKDV_HPW: query heads per dK / dV workgroup (v2; 1 or 2)
-    const char* e = getenv("XOT_TRAIN_DKDV_HPW");
-    return e != nullptr ? atoi(e) : 2;
-  }();
-  const int G = H / Hkv, hpw = (!dkdv_v1 && hpw_env == 2 && G % 2 == 0) ? 2 : 1;
-  const dim3 gk2(H / hpw, (L + DKT - 1) / DKT, B);
+  // two query heads of a GQA group per dK / dV workgroup (half the fp32 partials; 563 vs 590 us per layer and
+  // micro-batch, profiles/r5/train/dkdv_hpw/) when the group size is even
+  const int G = H / Hkv, hpw = G % 2 == 0 ? 2 : 1;
+  const dim3 gq(H, (L + TT - 1) / TT, B), gk2(H / hpw, (L + DKT - 1) / DKT, B);
 #define XOT_BWD(DHV)                                                                                                \
   do {                                                                                                              \
-    if (dq_v1)                                                                                                     \
-      attn_train_dq_kernel<DHV><<<gq, 256, 0, s>>>(q, ldq, k, ldk, kt, v, ldv, o, ldo, dout, lddo, Lp, lse2, delta, \
-                                                   dq, lddq, L, H, Hkv, scale);                                     \
-    else                                                                                                            \
-      attn_train_dq_v2_kernel<DHV><<<gq, 256, 0, s>>>(q, ldq, k, ldk, kt, v, ldv, o, ldo, dout, lddo, Lp, lse2,     \
-                                                      delta, dq, lddq, L, H, Hkv, scale);                           \
-    if (dkdv_v1) {                                                                                              \
-      static bool attr = hipFuncSetAttribute((const void*)attn_train_dkdv_kernel<DHV>,                             \
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)dkdv_smem<DHV>()) ==  \
-                         hipSuccess;                                                                                \
-      (void)attr;                                                                                                   \
-      attn_train_dkdv_kernel<DHV><<<gk, 64 * DKW, dkdv_smem<DHV>(), s>>>(q, ldq, qt, k, ldk, v, ldv, dout, lddo,    \
-                                                                    doutt, Lp, lse2, delta, wk, wv, L, H, Hkv, scale); \
-    } else {                                                                                                        \
-      static bool attr2 = hipFuncSetAttribute((const void*)attn_train_dkdv_v2_kernel<DHV>,                         \
-                                              hipFuncAttributeMaxDynamicSharedMemorySize,                           \
-                                              (int)dkdv_v2_smem<DHV>()) == hipSuccess;                              \
-      (void)attr2;                                                                                                  \
-      attn_train_dkdv_v2_kernel<DHV><<<gk2, 64 * DKW, dkdv_v2_smem<DHV>(), s>>>(                                    \
-          q, ldq, qt, k, ldk, v, ldv, dout, lddo, doutt, Lp, lse2, delta, wk, wv, L, H, Hkv, scale, hpw);           \
-    }                                                                                                               \
+    attn_train_dq_v2_kernel<DHV><<<gq, 256, 0, s>>>(q, ldq, k, ldk, nullptr, v, ldv, o, ldo, dout, lddo, Lp, lse2,   \
+                                                    delta, dq, lddq, L, H, Hkv, scale);                             \
+    static bool attr2 = hipFuncSetAttribute((const void*)attn_train_dkdv_v2_kernel<DHV>,                           \
+                                            hipFuncAttributeMaxDynamicSharedMemorySize,                             \
+                                            (int)dkdv_v2_smem<DHV>()) == hipSuccess;                                \
+    (void)attr2;                                                                                                    \
+    attn_train_dkdv_v2_kernel<DHV><<<gk2, 64 * DKW, dkdv_v2_smem<DHV>(), s>>>(                                      \
+        q, ldq, nullptr, k, ldk, v, ldv, dout, lddo, nullptr, Lp, lse2, delta, wk, wv, L, H, Hkv, scale, hpw);      \
   } while (0)
   if (Dh == 128)
     XOT_BWD(128);

@@ -233,7 +233,7 @@ void gemm(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const c10::op
 // an fp32 workspace of >= splits*M*N floats).  ntw: 16-row n-tiles per wave (1 or 2).
 void gemm_stream(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const c10::optional<at::Tensor>& bias,
                  const c10::optional<at::Tensor>& res, const c10::optional<at::Tensor>& ws, int64_t epi, int64_t ntw,
-                 int64_t splits, bool wshuf, const c10::optional<at::Tensor>& tickets, bool reduce) {
+                 int64_t splits, bool wshuf, bool reduce) {
   CHECK_BF16(x);
   CHECK_BF16(w);
   CHECK_GPU(y);
@@ -267,19 +267,10 @@ void gemm_stream(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const 
     ws_elems = ws->numel();
   }
   if (splits > 1 && epi == 1) XCHECK(res->data_ptr() != nullptr, "gemm_stream: res");
-  int* tk = nullptr;
-  long tk_n = 0;
-  if (tickets.has_value()) {  // zero-initialised int32 counters for the in-launch split-K combine
-    CHECK_GPU((*tickets));
-    CHECK_DT((*tickets), at::kInt);
-    XCHECK(tickets->is_contiguous(), "gemm_stream: tickets must be contiguous");
-    tk = tickets->data_ptr<int>();
-    tk_n = tickets->numel();
-  }
   const int rc = xot::launch_gemm_stream(bf(x), (int)x.stride(0), bf(w), (int)K, bf_opt(bias),
                                          epi == 1 ? bf(*res) : nullptr, (int)ldr, y.data_ptr(), (int)y.stride(0), f32,
                                          (int)epi, wsp, ws_elems, (int)M, (int)N, (int)K, (int)ntw, (int)splits,
-                                         wshuf, tk, tk_n, reduce, cur_stream());
+                                         wshuf, reduce, cur_stream());
   XCHECK(rc == 0, "gemm_stream: unsupported shape M=", M, " N=", N, " K=", K, " epi=", epi, " ntw=", ntw,
          " splits=", splits);
 }
@@ -327,26 +318,6 @@ void gemm_stream8(const at::Tensor& x, const at::Tensor& w8, const at::Tensor& w
 
 // Large-M GEMM on the pre-shuffled weight layout (prefill chunks, decode batches > 128 rows).
 // bn: 256 or 128 output columns per workgroup; splits > 1 needs an fp32 workspace of splits*M*N.
-// dGU = silu_mul'(GU) * (dY . W): the down projection's input-gradient GEMM on the four-wave tile with the SiLU
-// backward in its epilogue.  dy [M, K] bf16, w = shuffle(W_down^T) [F, K], gu / dgu [M, 2F] ([gate | up]).
-void gemm_silu_bwd(const at::Tensor& dy, const at::Tensor& w, const at::Tensor& gu, at::Tensor& dgu) {
-  CHECK_BF16(dy);
-  CHECK_BF16(w);
-  CHECK_BF16(gu);
-  CHECK_BF16(dgu);
-  XCHECK(dy.dim() == 2 && w.dim() == 2 && gu.dim() == 2 && dgu.dim() == 2, "gemm_silu_bwd: 2-D operands");
-  XCHECK(dy.stride(1) == 1 && dy.stride(0) % 8 == 0 && w.is_contiguous() && gu.stride(1) == 1 &&
-             gu.stride(0) % 8 == 0 && dgu.stride(1) == 1 && dgu.stride(0) % 8 == 0,
-         "gemm_silu_bwd: rows must be contiguous and 16-B aligned");
-  const int64_t M = dy.size(0), K = dy.size(1), F = w.size(0);
-  XCHECK(w.size(1) == K && gu.size(0) == M && gu.size(1) == 2 * F && dgu.size(0) == M && dgu.size(1) == 2 * F,
-         "gemm_silu_bwd: shapes");
-  const int rc = xot::launch_gemm_w4(bf(dy), (int)dy.stride(0), bf(w), nullptr, bf(gu), (int)gu.stride(0),
-                                     dgu.data_ptr(), (int)dgu.stride(0), false, 3 /* EPI_SILU_BWD */, nullptr, (int)M,
-                                     (int)F, (int)K, 1, xot::gemm_big_group_m(), cur_stream());
-  XCHECK(rc == 0, "gemm_silu_bwd: unsupported shape M=", M, " F=", F, " K=", K, " (F % 256, K % 128)");
-}
-
 void gemm_big(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const c10::optional<at::Tensor>& bias,
               const c10::optional<at::Tensor>& res, const c10::optional<at::Tensor>& ws, int64_t epi, int64_t bn,
               int64_t splits, bool reduce) {
@@ -389,54 +360,13 @@ void gemm_big(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const c10
          " splits=", splits);
 }
 
-// Stream-K large-M GEMM on the pre-shuffled weight layout (csrc/gemm_sk.hip): `cus` persistent workgroups;
-// part: fp32 [>= gemm_sk_part_elems()], sync: int32 [>= gemm_sk_sync_words(M, N)] zeroed once.
-void gemm_sk(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const c10::optional<at::Tensor>& bias,
-             const c10::optional<at::Tensor>& res, const at::Tensor& part, const at::Tensor& sync, int64_t epi,
-             int64_t cus) {
-  CHECK_BF16(x);
-  CHECK_BF16(w);
-  CHECK_GPU(y);
-  XCHECK(x.dim() == 2 && w.dim() == 2 && y.dim() == 2, "gemm_sk: x, w, y must be 2-D");
-  XCHECK(x.stride(1) == 1 && x.stride(0) % 8 == 0 && w.is_contiguous() && y.stride(1) == 1,
-         "gemm_sk: rows must be contiguous and 16-B aligned");
-  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
-  XCHECK(w.size(1) == K, "gemm_sk: K mismatch");
-  const bool f32 = y.scalar_type() == at::kFloat;
-  XCHECK(f32 || y.scalar_type() == at::kBFloat16, "gemm_sk: y must be bf16 or fp32");
-  XCHECK(y.size(0) == M && y.size(1) == (epi == 2 ? N / 2 : N), "gemm_sk: y shape mismatch");
-  XCHECK(M <= (1 << 24) && M * std::max(y.stride(0), x.stride(0)) < (1LL << 31), "gemm_sk: M too large");
-  if (bias.has_value()) {
-    CHECK_BF16((*bias));
-    XCHECK(bias->numel() == N && bias->is_contiguous(), "gemm_sk: bias shape mismatch");
-  }
-  int64_t ldr = 0;
-  if (epi == 1) {
-    XCHECK(res.has_value(), "gemm_sk: residual epilogue needs res");
-    CHECK_BF16((*res));
-    XCHECK(res->dim() == 2 && res->size(0) == M && res->size(1) == N && res->stride(1) == 1, "gemm_sk: res shape");
-    ldr = res->stride(0);
-  }
-  CHECK_GPU(part);
-  CHECK_DT(part, at::kFloat);
-  CHECK_GPU(sync);
-  CHECK_DT(sync, at::kInt);
-  XCHECK(part.is_contiguous() && part.numel() >= xot::gemm_sk_part_elems(), "gemm_sk: part workspace too small");
-  XCHECK(sync.is_contiguous() && sync.numel() >= xot::gemm_sk_sync_words((int)M, (int)N), "gemm_sk: sync words too small");
-  const int rc = xot::launch_gemm_sk(bf(x), (int)x.stride(0), bf(w), bf_opt(bias), epi == 1 ? bf(*res) : nullptr,
-                                     (int)ldr, y.data_ptr(), (int)y.stride(0), f32, (int)epi, part.data_ptr<float>(),
-                                     sync.data_ptr<int>(), (int)M, (int)N, (int)K, (int)cus, cur_stream());
-  XCHECK(rc == 0, "gemm_sk: unsupported shape M=", M, " N=", N, " K=", K, " epi=", epi, " cus=", cus);
-}
-
-int64_t gemm_sk_part_elems() { return xot::gemm_sk_part_elems(); }
 
 // B independent projections (MLA's per-head absorbed q . W_UK and o . W_UV^T): y_e = x_e . w_e^T with
 // x_e = x.data + e * xbat (rows x.stride(0) apart, K columns), w = [B, N, K] pre-shuffled per problem,
 // y_e = y.data + e * ybat (rows ldy apart, N columns).
 // Layout kernels of the training GEMMs (csrc/layout.hip).  mode 0: dst = shuffle(src) ([R, C], R % 16,
 // C % 128); 1: dst = shuffle(src^T) ([C, R] shuffled; R % 128, C % 64); 2: dst = src^T row-major (same).
-void relayout(const at::Tensor& src, at::Tensor& dst, int64_t mode) {
+void relayout(const at::Tensor& src, at::Tensor& dst, int64_t mode, int64_t variant) {
   CHECK_BF16(src);
   CHECK_BF16(dst);
   XCHECK(src.dim() == 2 && src.stride(1) == 1 && src.stride(0) % 8 == 0, "relayout: src must be 2-D with 16-B rows");
@@ -444,8 +374,8 @@ void relayout(const at::Tensor& src, at::Tensor& dst, int64_t mode) {
   const int R = (int)src.size(0), C = (int)src.size(1);
   int rc = -1;
   if (mode == 0) rc = xot::launch_shuffle(bf(src), src.stride(0), bf(dst), R, C, cur_stream());
-  else if (mode == 1) rc = xot::launch_shuffle_t(bf(src), src.stride(0), bf(dst), R, C, cur_stream());
-  else if (mode == 2) rc = xot::launch_transpose(bf(src), src.stride(0), bf(dst), R, C, cur_stream());
+  else if (mode == 1) rc = xot::launch_shuffle_t(bf(src), src.stride(0), bf(dst), R, C, cur_stream(), (int)variant);
+  else if (mode == 2) rc = xot::launch_transpose(bf(src), src.stride(0), bf(dst), R, C, cur_stream(), (int)variant);
   XCHECK(rc == 0, "relayout: unsupported shape R=", R, " C=", C, " mode=", mode);
 }
 
@@ -485,7 +415,6 @@ void gemm_batched(const at::Tensor& x, int64_t xbat, int64_t K, const at::Tensor
                                           f32, (int)B, (int)M, (int)N, (int)K, cur_stream());
   XCHECK(rc == 0, "gemm_batched: unsupported shape B=", B, " M=", M, " N=", N, " K=", K);
 }
-int64_t gemm_sk_sync_words(int64_t M, int64_t N) { return xot::gemm_sk_sync_words((int)M, (int)N); }
 
 // h [rows, D] += bias + sum_s ws[s] (the split-K slabs of a residual projection, fp32 [S][rows][D]);
 // out = rmsnorm(h) * w: the projection's reduce, the residual add and the next RMSNorm in one pass.
@@ -707,8 +636,7 @@ void moe_combine_norm(const at::Tensor& y, const at::Tensor& slot_of, const at::
 
 void attn_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
                  const at::Tensor& block_tables, const at::Tensor& ctx_lens, at::Tensor& out, at::Tensor& ws_o,
-                 at::Tensor& ws_ml, int64_t pages_per_part, int64_t nparts, double scale, int64_t algo,
-                 const c10::optional<at::Tensor>& tickets) {
+                 at::Tensor& ws_ml, int64_t pages_per_part, int64_t nparts, double scale, int64_t algo) {
   CHECK_BF16(q);
   CHECK_BF16(k_cache);
   CHECK_BF16(v_cache);
@@ -729,18 +657,11 @@ void attn_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tenso
   XCHECK(pages_per_part >= 1 && nparts >= 1, "attn_decode: bad partitioning");
   if (nparts > 1)
     XCHECK(ws_o.numel() >= B * H * nparts * Dh && ws_ml.numel() >= B * H * nparts * 2, "attn_decode: workspace small");
-  int* tk = nullptr;
-  if (tickets.has_value() && nparts > 1) {
-    CHECK_DT((*tickets), at::kInt);
-    XCHECK(tickets->is_contiguous() && tickets->numel() >= B * Hkv && tickets->device() == q.device(),
-           "attn_decode: tickets must hold B * Hkv zeroed int32");
-    tk = tickets->data_ptr<int32_t>();
-  }
   const int rc = xot::launch_attn_decode(bf(q), bf(k_cache), bf(v_cache), block_tables.data_ptr<int32_t>(),
                                          (int)block_tables.size(1), ctx_lens.data_ptr<int32_t>(), bf(out),
                                          ws_o.data_ptr<float>(), ws_ml.data_ptr<float>(), (int)B, (int)H, (int)Hkv,
                                          (int)Dh, (int)pages_per_part, (int)nparts, (float)scale, (int)nb, (int)algo,
-                                         tk, cur_stream());
+                                         cur_stream());
   XCHECK(rc == 0, "attn_decode: unsupported H=", H, " Hkv=", Hkv, " Dh=", Dh);
 }
 
@@ -783,21 +704,16 @@ void attn_train_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& 
   XCHECK(rc == 0, "attn_train_fwd: unsupported H=", H, " Hkv=", Hkv, " Dh=", Dh);
 }
 
-void attn_train_bwd(const at::Tensor& q, const at::Tensor& qt, const at::Tensor& k, const at::Tensor& kt,
-                    const at::Tensor& v, const at::Tensor& o, const at::Tensor& dout, const at::Tensor& doutt,
-                    const at::Tensor& lse2, at::Tensor& delta, at::Tensor& dq, at::Tensor& dk, at::Tensor& dv,
-                    at::Tensor& ws, int64_t B, int64_t L, int64_t Lp, int64_t H, int64_t Hkv, int64_t Dh,
-                    double scale) {
-  // qt / kt / doutt: the transposed images only the v1 kernels read (XOT_TRAIN_DQ_V1 / XOT_TRAIN_DKDV_V1); empty
-  // tensors otherwise (the v2 kernels read the transposed operands straight from their row tiles in LDS)
+void attn_train_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, const at::Tensor& o,
+                    const at::Tensor& dout, const at::Tensor& lse2, at::Tensor& delta, at::Tensor& dq, at::Tensor& dk,
+                    at::Tensor& dv, at::Tensor& ws, int64_t B, int64_t L, int64_t Lp, int64_t H, int64_t Hkv,
+                    int64_t Dh, double scale) {
+  // the kernels read the transposed operands straight from their row tiles in LDS (ds_read_b64_tr_b16)
   check_rows(q, B * L, H * Dh, "q");
-  if (qt.numel()) check_trans(qt, B, H, Dh, Lp, "qt");
   check_rows(k, B * L, Hkv * Dh, "k");
-  if (kt.numel()) check_trans(kt, B, Hkv, Dh, Lp, "kt");
   check_rows(v, B * L, Hkv * Dh, "v");
   check_rows(o, B * L, H * Dh, "o");
   check_rows(dout, B * L, H * Dh, "dout");
-  if (doutt.numel()) check_trans(doutt, B, H, Dh, Lp, "doutt");
   check_rows(dq, B * L, H * Dh, "dq");
   check_rows(dk, B * L, Hkv * Dh, "dk");
   check_rows(dv, B * L, Hkv * Dh, "dv");
@@ -809,12 +725,11 @@ void attn_train_bwd(const at::Tensor& q, const at::Tensor& qt, const at::Tensor&
   CHECK_DT(ws, at::kFloat);
   XCHECK(ws.is_contiguous() && ws.numel() >= 2 * H * B * L * Dh, "attn_train_bwd: ws needs 2 * H * B * L * Dh floats");
   const int rc = xot::launch_attn_train_bwd(
-      bf(q), q.stride(0), qt.numel() ? bf(qt) : nullptr, bf(k), k.stride(0), kt.numel() ? bf(kt) : nullptr, bf(v),
-      v.stride(0), bf(o), o.stride(0), bf(dout), dout.stride(0), doutt.numel() ? bf(doutt) : nullptr, (int)Lp, lse2.data_ptr<float>(), delta.data_ptr<float>(), bf(dq), dq.stride(0),
-      bf(dk), dk.stride(0), bf(dv), dv.stride(0), ws.data_ptr<float>(), (long)ws.numel(), (int)B, (int)L, (int)H,
-      (int)Hkv, (int)Dh, (float)scale, cur_stream());
-  XCHECK(rc == 0, "attn_train_bwd: unsupported H=", H, " Hkv=", Hkv, " Dh=", Dh,
-         " (or a transposed image the selected v1 kernel needs is missing)");
+      bf(q), q.stride(0), bf(k), k.stride(0), bf(v), v.stride(0), bf(o), o.stride(0), bf(dout), dout.stride(0),
+      (int)Lp, lse2.data_ptr<float>(), delta.data_ptr<float>(), bf(dq), dq.stride(0), bf(dk), dk.stride(0), bf(dv),
+      dv.stride(0), ws.data_ptr<float>(), (long)ws.numel(), (int)B, (int)L, (int)H, (int)Hkv, (int)Dh, (float)scale,
+      cur_stream());
+  XCHECK(rc == 0, "attn_train_bwd: unsupported H=", H, " Hkv=", Hkv, " Dh=", Dh);
 }
 
 void attn_prefill(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
@@ -990,18 +905,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm", &gemm);
   m.def("gemm_stream", &gemm_stream, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("bias"), py::arg("res"),
         py::arg("ws"), py::arg("epi"), py::arg("ntw"), py::arg("splits"), py::arg("wshuf"),
-        py::arg("tickets") = py::none(), py::arg("reduce") = true);
+        py::arg("reduce") = true);
   m.def("gemm_stream8", &gemm_stream8, py::arg("x"), py::arg("w8"), py::arg("wscale"), py::arg("y"), py::arg("bias"),
         py::arg("res"), py::arg("ws"), py::arg("epi"), py::arg("ntw"), py::arg("splits"), py::arg("reduce") = true);
-  m.def("gemm_sk", &gemm_sk, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("bias"), py::arg("res"), py::arg("part"),
-        py::arg("sync"), py::arg("epi"), py::arg("cus") = 256);
-  m.def("gemm_sk_part_elems", &gemm_sk_part_elems);
-  m.def("relayout", &relayout);
+  m.def("relayout", &relayout, py::arg("src"), py::arg("dst"), py::arg("mode"), py::arg("variant") = 2);
   m.def("gemm_kgroup", &gemm_kgroup);
   m.def("gemm_batched", &gemm_batched, py::arg("x"), py::arg("xbat"), py::arg("K"), py::arg("w"), py::arg("y"),
         py::arg("ybat"), py::arg("ldy"), py::arg("M"));
-  m.def("gemm_sk_sync_words", &gemm_sk_sync_words);
-  m.def("gemm_silu_bwd", &gemm_silu_bwd, py::arg("dy"), py::arg("w"), py::arg("gu"), py::arg("dgu"));
   m.def("gemm_big", &gemm_big, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("bias"), py::arg("res"),
         py::arg("ws"), py::arg("epi"), py::arg("bn"), py::arg("splits"), py::arg("reduce") = true);
   m.def("splitk_resid_rmsnorm", &splitk_resid_rmsnorm);
@@ -1017,7 +927,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("splits") = 1);
   m.def("attn_decode", &attn_decode, py::arg("q"), py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"),
         py::arg("ctx_lens"), py::arg("out"), py::arg("ws_o"), py::arg("ws_ml"), py::arg("pages_per_part"),
-        py::arg("nparts"), py::arg("scale"), py::arg("algo") = 2, py::arg("tickets") = py::none());
+        py::arg("nparts"), py::arg("scale"), py::arg("algo") = 2);
   m.def("attn_prefill", &attn_prefill, py::arg("q"), py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"),
         py::arg("cu_q"), py::arg("ctx_lens"), py::arg("out"), py::arg("max_qlen"), py::arg("scale"), py::arg("algo") = 2);
   m.def("router_logits", &router_logits);

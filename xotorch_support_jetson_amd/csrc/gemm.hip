@@ -189,8 +189,8 @@ int launch_gemm_skinny(const uint16_t* X, int ldx, const uint16_t* W, int ldw, c
 //   W rows       : streamed once, straight to VGPRs, two chunks in flight (prefetch depth 2)
 // MFMA k-order is permuted per lane group (group g owns k in [8*KS*g, 8*KS*(g+1)) of the chunk)
 // so each lane reads 16*KS contiguous bytes of its weight row per chunk.
-// SPLIT: fp32 partial slabs ws[blockIdx.y][M][N], finished by splitk_reduce_kernel or -- with tickets -- by the
-// last-arriving workgroup of each tile inside the same launch (epilogue there).
+// SPLIT: fp32 partial slabs ws[blockIdx.y][M][N], finished by splitk_reduce_kernel or by the consumer's fused reduce
+// (a last-arriver combine inside the launch measured no faster at batch 1 and 3 % slower at 512: removed in round 6).
 // MOE = 3: batched GEMM (per-head projections of MLA): blockIdx.z = problem e, weight W[e], A rows X + e*xbat,
 // output Y + e*ybat (element offsets; row strides ldx / ldy shared), all M rows.
 // MOE = 1 / 2: grouped (mixture-of-experts) GEMM.  blockIdx.z = expert e with weight W[e]
@@ -440,41 +440,6 @@ __global__ __launch_bounds__(256, OCC) void gemm_stream_kernel(const uint16_t* _
           const int m = wrow + 16 * i + 4 * g + r;
           if (m < M) slab[(size_t)m * N + n0 + 16 * j + c] = acc[i][j][r];
         }
-    if (tickets != nullptr) {
-      // In-launch combine: the split that arrives last for this (column tile, row block) sums every
-      // slab of the tile and applies the epilogue (no second kernel).  Publish: stores drained,
-      // agent-scope release, relaxed ticket; reducer: agent-scope acquire before reading the slabs.
-      // The reducer resets the ticket, so the zero-initialised counters stay valid across launches
-      // and HIP-graph replays.
-      const int S = gridDim.y, tile = bt * mblocks + mb;
-      int* flag = reinterpret_cast<int*>(xs_raw);  // LDS is free again after the last compute phase
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const int t = __hip_atomic_fetch_add(&tickets[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int last = t == S - 1;
-        if (last) {
-          __hip_atomic_store(&tickets[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        *flag = last;
-      }
-      __syncthreads();
-      if (*flag == 0) return;
-      const int c0 = bt * (64 * NTW);  // first weight row (output column before SiLU pairing)
-      constexpr int OCOLS = EPI == EPI_SILU ? 32 * NTW : 64 * NTW;
-      const int oc0 = EPI == EPI_SILU ? c0 / 2 : c0;
-      for (int q = tid; q < M * (OCOLS / 8); q += NTH) {
-        const int m = q / (OCOLS / 8), o = oc0 + (q % (OCOLS / 8)) * 8;
-        void* yrow = OUT_F32 ? (void*)(reinterpret_cast<float*>(Yv) + (size_t)m * ldy)
-                             : (void*)(reinterpret_cast<uint16_t*>(Yv) + (size_t)m * ldy);
-        splitk_out8<EPI, OUT_F32>(ws + ((size_t)m_base + m) * N, (size_t)Mtot * N, S, o, bias,
-                                  EPI == EPI_RESID ? R + (size_t)m * ldr : nullptr, yrow);
-      }
-    }
   } else if constexpr (EPI == EPI_SILU && NTW >= 2) {
 #pragma unroll
     for (int p = 0; p < NTW / 2; ++p) {  // pair (gate tile 2p, up tile 2p+1) -> 16 output columns
@@ -524,7 +489,7 @@ __global__ __launch_bounds__(256, OCC) void gemm_stream_kernel(const uint16_t* _
 template <int MT, int NTW, int KS, int EPI, bool F32, bool WSH, bool W8 = false>
 static void stream_launch(const uint16_t* X, int ldx, const uint16_t* W, int ldw, const uint16_t* bias,
                           const uint16_t* R, int ldr, void* Y, int ldy, float* ws, int M, int N, int K, int S,
-                          int* tickets, bool reduce, hipStream_t st, const float* wscale = nullptr) {
+                          bool reduce, hipStream_t st, const float* wscale = nullptr) {
   // occupancy request: 2 workgroups/CU while the register budget allows it (FP8 weights need a few more
   // registers for the widened fragments)
   constexpr int OCC = (MT * NTW >= (W8 ? 16 : 32)) ? 1 : 2;
@@ -549,8 +514,8 @@ static void stream_launch(const uint16_t* X, int ldx, const uint16_t* W, int ldw
       (void)attr;
     }
     kern<<<grid, 256, SMEM, st>>>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, M, N, kper, mblocks, nullptr, nullptr,
-                                  tickets, 0L, wscale, 0L, 0L);
-    if (tickets != nullptr || !reduce) return;  // combined in-launch / slabs left for the consumer
+                                  nullptr, 0L, wscale, 0L, 0L);
+    if (!reduce) return;  // slabs left for the consumer
     const int ncol = EPI == EPI_SILU ? N / 2 : N;
     long chunks = (long)M * (ncol / 8);
     int blocks = (int)((chunks + 255) / 256);
@@ -562,8 +527,7 @@ static void stream_launch(const uint16_t* X, int ldx, const uint16_t* W, int ldw
 template <int EPI, bool F32>
 static int stream_dispatch(const uint16_t* X, int ldx, const uint16_t* W, int ldw, const uint16_t* bias,
                            const uint16_t* R, int ldr, void* Y, int ldy, float* ws, long ws_elems, int M, int N,
-                           int K, int ntw, int S, bool wshuf, int* tickets, long tickets_n, bool reduce,
-                           hipStream_t st) {
+                           int K, int ntw, int S, bool wshuf, bool reduce, hipStream_t st) {
   if (EPI == EPI_SILU && ntw == 1) ntw = 2;
   if (ntw != 1 && ntw != 2 && ntw != 4) return -1;
   const int mt = (M + 15) / 16;
@@ -572,18 +536,16 @@ static int stream_dispatch(const uint16_t* X, int ldx, const uint16_t* W, int ld
   const int KS = 4;
   if (K % (S * 32 * KS) != 0) return -1;  // whole 128-deep k-chunks per workgroup (odd counts: single tail)
   if (S > 1 && (ws == nullptr || ws_elems < (long)S * M * N)) return -1;
-  // in-launch split-K combine needs one ticket per (column tile, 128-row block)
-  if (S == 1 || !reduce || tickets_n < (long)(N / (64 * ntw)) * ((M + 127) / 128)) tickets = nullptr;
   if (EPI == EPI_SILU && N % 32 != 0) return -1;
   if (wshuf && (KS != 4 || K % 128 != 0)) return -1;
 #define XOT_ST2(MTV, KSV, WSH)                                                                              \
   do {                                                                                                      \
     if (ntw == 1 && EPI != EPI_SILU)                                                                        \
-      stream_launch<MTV, 1, KSV, EPI, F32, WSH>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, M, N, K, S, tickets, reduce, st);  \
+      stream_launch<MTV, 1, KSV, EPI, F32, WSH>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, M, N, K, S, reduce, st);  \
     else if (ntw == 4 && MTV >= 4 && MTV <= 8)                                                                    \
-      stream_launch<MTV, 4, KSV, EPI, F32, WSH>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, M, N, K, S, tickets, reduce, st);  \
+      stream_launch<MTV, 4, KSV, EPI, F32, WSH>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, M, N, K, S, reduce, st);  \
     else                                                                                                    \
-      stream_launch<MTV, 2, KSV, EPI, F32, WSH>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, M, N, K, S, tickets, reduce, st);  \
+      stream_launch<MTV, 2, KSV, EPI, F32, WSH>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, M, N, K, S, reduce, st);  \
     return 0;                                                                                               \
   } while (0)
 #define XOT_ST(MTV, KSV)                  \
@@ -704,14 +666,14 @@ static int stream8_dispatch(const uint16_t* X, int ldx, const uint8_t* W8p, cons
 #define XOT_S8(MTV, KSV)                                                                                            \
   do {                                                                                                              \
     if (ntw == 1 && EPI != EPI_SILU)                                                                                \
-      stream_launch<MTV, 1, KSV, EPI, F32, true, true>(X, ldx, W, K, bias, R, ldr, Y, ldy, ws, M, N, K, S, nullptr,  \
-                                                       reduce, st, wscale);                                          \
+      stream_launch<MTV, 1, KSV, EPI, F32, true, true>(X, ldx, W, K, bias, R, ldr, Y, ldy, ws, M, N, K, S, reduce,  \
+                                                       st, wscale);                                          \
     else if (ntw == 4 && MTV >= 4)                                                                                  \
-      stream_launch<MTV, 4, KSV, EPI, F32, true, true>(X, ldx, W, K, bias, R, ldr, Y, ldy, ws, M, N, K, S, nullptr,  \
-                                                       reduce, st, wscale);                                          \
+      stream_launch<MTV, 4, KSV, EPI, F32, true, true>(X, ldx, W, K, bias, R, ldr, Y, ldy, ws, M, N, K, S, reduce,  \
+                                                       st, wscale);                                          \
     else                                                                                                            \
-      stream_launch<MTV, 2, KSV, EPI, F32, true, true>(X, ldx, W, K, bias, R, ldr, Y, ldy, ws, M, N, K, S, nullptr,  \
-                                                       reduce, st, wscale);                                          \
+      stream_launch<MTV, 2, KSV, EPI, F32, true, true>(X, ldx, W, K, bias, R, ldr, Y, ldy, ws, M, N, K, S, reduce,  \
+                                                       st, wscale);                                          \
     return 0;                                                                                                       \
   } while (0)
   // (256-deep k-chunks for small M -- the bf16 kernel's bytes in flight per chunk -- measured no faster)
@@ -736,16 +698,16 @@ int launch_gemm_stream8(const uint16_t* X, int ldx, const uint8_t* W, const floa
 
 int launch_gemm_stream(const uint16_t* X, int ldx, const uint16_t* W, int ldw, const uint16_t* bias,
                        const uint16_t* R, int ldr, void* Y, int ldy, bool out_f32, int epi, float* ws, long ws_elems,
-                       int M, int N, int K, int ntw, int S, bool wshuf, int* tickets, long tickets_n, bool reduce,
+                       int M, int N, int K, int ntw, int S, bool wshuf, bool reduce,
                        hipStream_t s) {
   if (M <= 0) return 0;
   if (epi == EPI_SILU)
-    return out_f32 ? stream_dispatch<EPI_SILU, true>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, ntw, S, wshuf, tickets, tickets_n, reduce, s)
-                   : stream_dispatch<EPI_SILU, false>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, ntw, S, wshuf, tickets, tickets_n, reduce, s);
+    return out_f32 ? stream_dispatch<EPI_SILU, true>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, ntw, S, wshuf, reduce, s)
+                   : stream_dispatch<EPI_SILU, false>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, ntw, S, wshuf, reduce, s);
   if (epi == EPI_RESID)
-    return out_f32 ? -1 : stream_dispatch<EPI_RESID, false>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, ntw, S, wshuf, tickets, tickets_n, reduce, s);
-  return out_f32 ? stream_dispatch<EPI_NONE, true>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, ntw, S, wshuf, tickets, tickets_n, reduce, s)
-                 : stream_dispatch<EPI_NONE, false>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, ntw, S, wshuf, tickets, tickets_n, reduce, s);
+    return out_f32 ? -1 : stream_dispatch<EPI_RESID, false>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, ntw, S, wshuf, reduce, s);
+  return out_f32 ? stream_dispatch<EPI_NONE, true>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, ntw, S, wshuf, reduce, s)
+                 : stream_dispatch<EPI_NONE, false>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, ntw, S, wshuf, reduce, s);
 }
 
 // ------------------------------------------------------------------------------------ tiled

@@ -4,8 +4,7 @@
 
 namespace xot {
 
-// EPI_SILU_BWD: four-wave tile only (R = [gate | up] rows, Y = [dgate | dup]; bindings.hip gemm_silu_bwd)
-enum { EPI_NONE = 0, EPI_RESID = 1, EPI_SILU = 2, EPI_SILU_BWD = 3 };
+enum { EPI_NONE = 0, EPI_RESID = 1, EPI_SILU = 2 };
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef __attribute__((address_space(1))) void* glb_ptr_t;

@@ -404,30 +404,6 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const uint16_t* __restr
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int m = rbase + 16 * i;
-      if constexpr (EPI == EPI_SILU_BWD) {
-        // this GEMM is dA = dY . W_down for A = silu(gate) * up: R = [gate | up] [M, 2N] (ldr), Y = [dgate | dup]
-        // (ldy); dgate = dA up silu'(gate), dup = dA silu(gate), in fp32 from the accumulators
-        if (m >= M) continue;
-        const uint16_t* gr = R + (size_t)m * ldr;
-        uint16_t* yr = reinterpret_cast<uint16_t*>(Yv) + (size_t)m * ldy;
-#pragma unroll
-        for (int J = 0; J < 4; ++J) {
-          const int col = cbase + 32 * J + 8 * g;
-          const s16x8 gv = ld16(gr + col), uv = ld16(gr + N + col);
-          s16x8 dg, du;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float da = e < 4 ? acc[i][2 * J][e] : acc[i][2 * J + 1][e - 4];
-            const float gf = bf2f(gv[e]), uf = bf2f(uv[e]);
-            const float sg = 1.0f / (1.0f + __expf(-gf));
-            dg[e] = (short)f2bf(da * uf * (sg * (1.0f + gf * (1.0f - sg))));
-            du[e] = (short)f2bf(da * gf * sg);
-          }
-          st16(yr + col, dg);
-          st16(yr + N + col, du);
-        }
-        continue;
-      }
       s16x8 rv[4];
       if constexpr (EPI == EPI_RESID) {
         const int mr = min(m, M - 1);
@@ -532,9 +508,6 @@ int launch_gemm_w4(const uint16_t* X, int ldx, const uint16_t* W, const uint16_t
   } else if (epi == EPI_RESID) {
     if (out_f32) return -1;
     w4_launch<EPI_RESID, false, false>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, 1, group_m, st);
-  } else if (epi == EPI_SILU_BWD) {
-    if (out_f32 || R == nullptr || bias != nullptr) return -1;
-    w4_launch<EPI_SILU_BWD, false, false>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, 1, group_m, st);
   } else {
     if (out_f32) w4_launch<EPI_NONE, true, false>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, 1, group_m, st);
     else w4_launch<EPI_NONE, false, false>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, 1, group_m, st);

@@ -32,8 +32,7 @@ int launch_gemm_skinny(const uint16_t* X, int ldx, const uint16_t* W, int ldw, c
                        int nt, hipStream_t s);
 int launch_gemm_stream(const uint16_t* X, int ldx, const uint16_t* W, int ldw, const uint16_t* bias,
                        const uint16_t* R, int ldr, void* Y, int ldy, bool out_f32, int epi, float* ws, long ws_elems,
-                       int M, int N, int K, int ntw, int S, bool wshuf, int* tickets, long tickets_n, bool reduce,
-                       hipStream_t s);
+                       int M, int N, int K, int ntw, int S, bool wshuf, bool reduce, hipStream_t s);
 // decode GEMM with weight-only FP8 (e4m3 pre-shuffled tiles + per-row fp32 scale), bf16 activations
 int launch_gemm_stream8(const uint16_t* X, int ldx, const uint8_t* W, const float* wscale, const uint16_t* bias,
                         const uint16_t* R, int ldr, void* Y, int ldy, bool out_f32, int epi, float* ws, long ws_elems,
@@ -47,23 +46,15 @@ int gemm_big_group_m();  // grouped raster width of tall grids (XOT_GEMM_GROUP_M
 int launch_gemm_big(const uint16_t* X, int ldx, const uint16_t* W, const uint16_t* bias, const uint16_t* R, int ldr,
                     void* Y, int ldy, bool out_f32, int epi, float* ws, long ws_elems, int M, int N, int K, int bn,
                     int S, bool reduce, hipStream_t s);
-// stream-K large-M GEMM on the pre-shuffled layout: one persistent 256 x 256 x 64 workgroup per CU (cus of
-// them), split column tiles finished by their last-arriving part; part = gemm_sk_part_elems() fp32,
-// sync = gemm_sk_sync_words(M, N) int32, zero-initialised once (kept zeroed by the kernel)
-int launch_gemm_sk(const uint16_t* X, int ldx, const uint16_t* W, const uint16_t* bias, const uint16_t* R, int ldr,
-                   void* Y, int ldy, bool out_f32, int epi, float* part, int* sync, int M, int N, int K, int cus,
-                   hipStream_t s);
-long gemm_sk_part_elems();
 // B independent GEMMs Y_e = X_e . W_e^T (pre-shuffled W [B][N][K]; X_e = X + e*xbat, Y_e = Y + e*ybat)
 // training-GEMM layouts (csrc/layout.hip): src [R, C] row-major with row stride ld
 int launch_shuffle(const uint16_t* src, long ld, uint16_t* dst, int R, int C, hipStream_t s);
-int launch_shuffle_t(const uint16_t* src, long ld, uint16_t* dst, int R, int C, hipStream_t s);
-int launch_transpose(const uint16_t* src, long ld, uint16_t* dst, int R, int C, hipStream_t s);
+int launch_shuffle_t(const uint16_t* src, long ld, uint16_t* dst, int R, int C, hipStream_t s, int variant = 2);
+int launch_transpose(const uint16_t* src, long ld, uint16_t* dst, int R, int C, hipStream_t s, int variant = 2);
 int launch_gemm_kgroup(const uint16_t* X, int ldx, const uint16_t* W, uint16_t* Y, int ldy, bool resid,
                        const int* koff, int E, int M, int N, int K, hipStream_t st);
 int launch_gemm_batched(const uint16_t* X, int ldx, long xbat, const uint16_t* W, void* Y, int ldy, long ybat,
                         bool out_f32, int B, int M, int N, int K, hipStream_t s);
-long gemm_sk_sync_words(int M, int N);
 // h += bias + sum of S fp32 split-K slabs [S][rows][D] (in place, bf16), out = rmsnorm(h) * w
 void launch_splitk_resid_rmsnorm(const float* ws, int S, const uint16_t* bias, uint16_t* h, const uint16_t* w,
                                  uint16_t* out, int rows, int D, float eps, hipStream_t s);
@@ -104,7 +95,7 @@ int launch_gemm_tiled(const uint16_t* X, int ldx, const uint16_t* W, int ldw, co
 int launch_attn_decode(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, const int32_t* block_tables,
                        int max_blocks, const int32_t* ctx_lens, uint16_t* out, float* ws_o, float* ws_ml, int B,
                        int H, int Hkv, int Dh, int pages_per_part, int nparts, float scale, int num_pages, int algo,
-                       int* tickets, hipStream_t s);
+                       hipStream_t s);
 int launch_attn_prefill(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, const int32_t* block_tables,
                         int max_blocks, const int32_t* cu_q, const int32_t* ctx_lens, uint16_t* out, int B,
                         int max_qlen, int H, int Hkv, int Dh, float scale, int num_pages, int algo, hipStream_t s);
@@ -116,9 +107,8 @@ int launch_attn_train_transpose(const uint16_t* x, long ldx, uint16_t* xt, int B
 int launch_attn_train_fwd(const uint16_t* q, long ldq, const uint16_t* k, long ldk, const uint16_t* vt, int Lp,
                           uint16_t* o, long ldo, float* lse2, int B, int L, int H, int Hkv, int Dh, float scale,
                           bool causal, hipStream_t s);
-int launch_attn_train_bwd(const uint16_t* q, long ldq, const uint16_t* qt, const uint16_t* k, long ldk,
-                          const uint16_t* kt, const uint16_t* v, long ldv, const uint16_t* o, long ldo,
-                          const uint16_t* dout, long lddo, const uint16_t* doutt, int Lp, const float* lse2,
+int launch_attn_train_bwd(const uint16_t* q, long ldq, const uint16_t* k, long ldk, const uint16_t* v, long ldv,
+                          const uint16_t* o, long ldo, const uint16_t* dout, long lddo, int Lp, const float* lse2,
                           float* delta, uint16_t* dq, long lddq, uint16_t* dk, long lddk, uint16_t* dv, long lddv,
                           float* ws, long ws_elems, int B, int L, int H, int Hkv, int Dh, float scale, hipStream_t s);
 

@@ -162,14 +162,6 @@ __global__ __launch_bounds__(NTH) void splitk_resid_rmsnorm_kernel(const float* 
   }
 }
 
-static bool srr_wide() {  // XOT_SRR_WIDE=0: 256 threads per row at every width (A/B)
-  static const bool v = [] {
-    const char* e = getenv("XOT_SRR_WIDE");
-    return e == nullptr || atoi(e) != 0;
-  }();
-  return v;
-}
-
 void launch_splitk_resid_rmsnorm(const float* ws, int S, const uint16_t* bias, uint16_t* h, const uint16_t* w,
                                  uint16_t* out, int rows, int D, float eps, hipStream_t s) {
   if (rows <= 0) return;
@@ -194,7 +186,7 @@ void launch_splitk_resid_rmsnorm(const float* ws, int S, const uint16_t* bias, u
     go(std::integral_constant<int, 1>(), I256());
   else if (nchunk <= 512)
     go(std::integral_constant<int, 2>(), I256());
-  else if (nchunk <= 1024 && rows >= 256 && srr_wide())
+  else if (nchunk <= 1024 && rows >= 256)  // 1024 threads per row: 16.4 -> 14.4 us at 512 x 8192 (r4 srr_wide)
     go(std::integral_constant<int, 1>(), std::integral_constant<int, 1024>());
   else if (nchunk <= 1024)
     go(std::integral_constant<int, 4>(), I256());
@@ -541,7 +533,8 @@ __global__ __launch_bounds__(256) void splitk_rope_kv_write_kernel(
       return;
     }
     int p = pos[t];
-    p = p < 0 ? 0 : (p >= max_pos ? max_pos - 1 : p);
+    const int mp = max_pos < 0 ? -max_pos : max_pos;
+    p = p < 0 ? 0 : (p >= mp ? mp - 1 : p);
     const float* cs = cos_sin + (size_t)p * Dh;
     const f32x4 a = slab_sum4<SS>(row, S, sstride, bias, h * Dh + i);
     const f32x4 b = slab_sum4<SS>(row, S, sstride, bias, h * Dh + i + half);
@@ -557,7 +550,7 @@ __global__ __launch_bounds__(256) void splitk_rope_kv_write_kernel(
     *reinterpret_cast<s16x4*>(dst + i + half) = ob;
     return;
   }
-  if (slot < 0) return;
+  if (slot < 0 || max_pos < 0) return;  // (max_pos < 0: timing experiment without the V write, XOT_EXP_NO_V)
   const int e = 4 * (w - nrot), kh = e / Dh, d = e % Dh;
   const f32x4 v = slab_sum4<SS>(row, S, sstride, bias, (H + Hkv) * Dh + e);
   uint16_t* dst = vc + (((size_t)blk * Hkv + kh) * Dh + d) * BS + off;
@@ -570,6 +563,8 @@ void launch_splitk_rope_kv_write(const float* ws, int S, const uint16_t* bias, c
                                  uint16_t* vc, int T, int H, int Hkv, int Dh, int BS, int max_pos, long nslots,
                                  hipStream_t s) {
   if (T <= 0) return;
+  static const bool no_v = getenv("XOT_EXP_NO_V") != nullptr;  // experiment only: skip the V write (wrong output)
+  if (no_v) max_pos = -max_pos;
   const long sstride = (long)T * (H + 2 * Hkv) * Dh;
   const int items = (H + Hkv) * (Dh / 8) + Hkv * Dh / 4;
   const dim3 grid(T, (items + 255) / 256);
@@ -619,11 +614,7 @@ void launch_rope_kv_write(const uint16_t* qkv, const int32_t* pos, const float* 
                           uint16_t* q_out, uint16_t* kc, uint16_t* vc, int T, int H, int Hkv, int Dh, int BS,
                           int max_pos, long nslots, hipStream_t s) {
   if (T <= 0) return;
-  static const bool tiled = [] {  // XOT_ROPE_TILED=0: the per-token kernel for every T (A/B)
-    const char* e = getenv("XOT_ROPE_TILED");
-    return !(e != nullptr && e[0] == '0');
-  }();
-  const bool vt = tiled && T >= 4 * RKV_TOK && Dh % 8 == 0;
+  const bool vt = T >= 4 * RKV_TOK && Dh % 8 == 0;  // V through LDS tiles (prefill chunks)
   rope_kv_write_kernel<<<T, 256, 0, s>>>(qkv, pos, cos_sin, slots, q_out, kc, vc, H, Hkv, Dh, BS, max_pos, nslots,
                                          vt ? 1 : 0);
   if (vt)

@@ -368,18 +368,23 @@ async def async_main(args, engine=None, device_caps=None):
       loop.add_signal_handler(s, on_signal, s)
     except NotImplementedError:  # pragma: no cover
       pass
-  work = asyncio.ensure_future(_command(args, node, api, viz))
   halt = asyncio.ensure_future(stop.wait())
+  start = work = None
   rc = 0
   try:
-    await node.start(wait_for_peers=args.wait_for_peers)
-    done, _ = await asyncio.wait({work, halt}, return_when=asyncio.FIRST_COMPLETED)
-    if work in done:
-      rc = work.result() or 0
+    start = asyncio.ensure_future(node.start(wait_for_peers=args.wait_for_peers))
+    await asyncio.wait({start, halt}, return_when=asyncio.FIRST_COMPLETED)
+    if start.done():
+      start.result()
+      work = asyncio.ensure_future(_command(args, node, api, viz))  # the command once the node is up
+      done, _ = await asyncio.wait({work, halt}, return_when=asyncio.FIRST_COMPLETED)
+      if work in done:
+        rc = work.result() or 0
   finally:
-    for t in (work, halt):
+    pending = [t for t in (start, work, halt) if t is not None]
+    for t in pending:
       t.cancel()
-    await asyncio.gather(work, halt, return_exceptions=True)
+    await asyncio.gather(*pending, return_exceptions=True)
     await node.stop()
     if api is not None:
       await api.stop()

@@ -41,10 +41,6 @@ MOE_BM = int(os.environ.get("XOT_MOE_BM", "0"))  # force the grouped gemm_big ti
 MOE_DN_SPLITS = int(os.environ.get("XOT_MOE_DN_SPLITS", "0"))  # force the grouped down GEMM's K split on gemm_big tiles
 MOE_PP2 = os.environ.get("XOT_MOE_PP2", "1") == "1"  # 256-row expert tiles on the two-phase ping-pong schedule
 PAGE = 64
-# XOT_SPLIT_DECODE=N: decode batches of at least N sequences (dense models) run as two half-batches on two
-# streams, so one half's HBM-bound attention overlaps the other half's MFMA-bound GEMMs (0: off)
-SPLIT_DECODE_MIN = int(os.environ.get("XOT_SPLIT_DECODE", "0"))
-SPLIT_OFFSET = os.environ.get("XOT_SPLIT_OFFSET", "1") == "1"
 
 
 def moe_tiles(rows: float, E: int) -> Tuple[int, int, int]:
@@ -127,16 +123,11 @@ class ShardModel:
     self.max_batch = max_batch
     self.max_ctx = max_ctx
     self.ws = None
-    self.ws2 = None  # attention workspace of the second half-batch of a split decode step
-    self.side = None
     if self.device.type == "cuda":
       if c.is_mla:
         self.ws = K.MLAWorkspace(max_batch, c.num_heads, c.kv_lora_rank, max_ctx, self.device)
       else:
         self.ws = K.DecodeWorkspace(max_batch, c.num_heads, c.head_dim, max_ctx, self.device)
-        if SPLIT_DECODE_MIN and max_batch >= SPLIT_DECODE_MIN:
-          self.ws2 = K.DecodeWorkspace(max_batch // 2, c.num_heads, c.head_dim, max_ctx, self.device)
-          self.side = torch.cuda.Stream(self.device)
     if c.is_mla:
       self.scale = c.attn_scale()
     # last shard with the LM head split across two ring stages: logits of vocab rows [0, head_rows) only,
@@ -329,8 +320,6 @@ class ShardModel:
     """x: token ids [T] (first shard) or hidden [T, D] bf16.  Returns hidden [T, D] (non-last shard)
     or fp32 logits [B, V] of each sequence's last token (last shard)."""
     c, w = self.c, self.w
-    if self._split_ok(inp):
-      return self._forward_split(x, inp)
     if self.shard.is_first_layer():
       h = K.embedding(x, w.embed)
       if inp.image_embeds is not None:  # LLaVA: projected image features replace the image-token rows
@@ -368,70 +357,6 @@ class ShardModel:
     # LM head split with another stage (parallel/pipeline.py): logits of vocab rows [0, head_rows) and
     # the normed hidden state the other stage applies the remaining rows to
     return linear(xn, self._head_slice(), out_dtype=torch.float32), xn
-
-  def _split_ok(self, inp: StepInputs) -> bool:
-    c = self.c
-    return (self.side is not None and inp.decode and inp.batch >= SPLIT_DECODE_MIN and inp.batch % 2 == 0
-            and not c.is_mla and c.num_experts == 0 and inp.image_embeds is None and self.head_rows is None
-            and len(self.layer_ids) > 0)
-
-  def _forward_split(self, x: torch.Tensor, inp: StepInputs) -> torch.Tensor:
-    """Decode step as two independent half-batches, the second on a side stream (fork / join events, so
-    it captures into one HIP graph with two branches).  Every kernel of a half reads / writes only its
-    rows, its own split-K slabs (scratch lane 1) and attention workspace; the KV pages of the two
-    halves are disjoint.  The issue order alternates layer by layer between the halves."""
-    c, w = self.c, self.w
-    B, half = inp.batch, inp.batch // 2
-    if self.shard.is_first_layer():
-      h = K.embedding(x, w.embed)
-    else:
-      h = x.contiguous().clone() if x.dtype == torch.bfloat16 else x.to(torch.bfloat16).contiguous()
-    xn, _ = K.rmsnorm(h, w.layers[self.layer_ids[0]].ln1, c.rms_norm_eps)
-    last = self.shard.is_last_layer()
-    V = w.lm_head.shape[0]
-    logits = torch.empty(B, V, dtype=torch.float32, device=h.device) if last else None
-    cur = torch.cuda.current_stream(h.device)
-    self.side.wait_stream(cur)
-    n = len(self.layer_ids)
-
-    def half_steps(lane: int):
-      sl = slice(lane * half, (lane + 1) * half)
-      sub = StepInputs(inp.positions[sl], inp.slots[sl], inp.block_tables[sl], inp.ctx_lens[sl],
-                       inp.cu_q[:half + 1], inp.last_idx[:half], 1, True)
-      hh, xx = h[sl], xn[sl]
-      ws = self.ws if lane == 0 else self.ws2
-      for j, li in enumerate(self.layer_ids):
-        lw = w.layers[li]
-        q = linear_rope_kv(xx, lw.qkv_w, lw.qkv_b, sub.positions, self.cos_sin, sub.slots, self.kv.k[j],
-                           self.kv.v[j], c.num_heads, c.num_kv_heads)
-        a = self._attention(q, j, sub, ws).view(half, c.num_heads * c.head_dim)
-        yield
-        xx = linear_resid_norm(a, lw.o_w, hh, lw.ln2, c.rms_norm_eps)
-        nxt = w.layers[self.layer_ids[j + 1]].ln1 if j + 1 < n else (w.norm if last else None)
-        xx = self._mlp(xx, lw, hh, nxt, li)
-        yield
-      if last:
-        linear(xx, w.lm_head, out=logits[sl])
-      yield
-
-    gens = [half_steps(0), half_steps(1)]
-    streams = [cur, self.side]
-    try:
-      for k in range(2 * n + 1):
-        for lane in (0, 1):
-          scratch.lane = lane
-          with torch.cuda.stream(streams[lane]):
-            next(gens[lane])
-          if k == 0 and lane == 0 and SPLIT_OFFSET:
-            # start the second half once the first half's first attention is queued: its GEMMs then
-            # run while the first half streams KV
-            ev = torch.cuda.Event()
-            ev.record(cur)
-            self.side.wait_event(ev)
-    finally:
-      scratch.lane = 0
-    cur.wait_stream(self.side)
-    return logits if last else h
 
   def _head_slice(self) -> torch.Tensor:
     w = self.w.lm_head

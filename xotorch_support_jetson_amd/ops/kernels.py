@@ -150,13 +150,11 @@ def rope_apply(x: torch.Tensor, pos: torch.Tensor, cos_sin: torch.Tensor, nh: in
 # 1 / 2: wave per (sequence, KV head, partition), transposed S^T (lane = query head), no LDS;
 #        2 prefetches the next page under the current one
 # 3: 2 with non-temporal K / V loads (measured neutral, profiles/r3/s3/)
-# 4: workgroup of 8 waves over ONE partition (no merge launch) -- short block tables at small batch
 # -1 (default): 0 below 64 (sequence, KV head) pairs -- few long sequences, where the workgroup
-#        kernel's 4-wave page split needs fewer partitions -- (4 instead when the table is at most
-#        XOT_ATTN_WG8_PAGES pages: opt-in, 3.55 vs 3.52 ms per 8B batch-1 step, profiles/r3/s3/); else 2
-#        (measured: tools/bench_kernels.py)
+#        kernel's 4-wave page split needs fewer partitions; else 2 (measured: tools/bench_kernels.py)
+# (4, an 8-wave workgroup over one partition for short tables at small batch, measured 1 % slower at 8B batch 1 --
+#  3.55 vs 3.52 ms, profiles/r3/s3/ -- and was removed in round 6)
 DECODE_ALGO = int(os.environ.get("XOT_ATTN_DECODE", "-1"))
-WG8_MAX_PAGES = int(os.environ.get("XOT_ATTN_WG8_PAGES", "0"))  # 0: off (measured 1 % slower at 8B batch 1)
 
 
 def resolve_decode_algo(batch: int, Hkv: int, algo: int | None = None) -> int:
@@ -170,8 +168,6 @@ def choose_pages_per_part(batch: int, Hkv: int, max_ctx: int, algo: int | None =
   """KV pages per split-KV partition for a decode step of `batch` sequences."""
   algo = resolve_decode_algo(batch, Hkv, algo)
   pages = max(1, -(-max_ctx // PAGE))
-  if algo == 4:  # one partition
-    return pages
   if algo == 0:  # enough workgroups to cover 256 CUs several times, >= 4 pages (one per wave) each
     for ppp in (16, 8, 4):
       if batch * Hkv * -(-pages // ppp) >= 1024:
@@ -203,18 +199,10 @@ class DecodeWorkspace:
     self.units = worst  # max over batch of batch * nparts
     self.o = torch.empty(worst * H * Dh, dtype=torch.float32, device=device)
     self.ml = torch.empty(worst * H * 2, dtype=torch.float32, device=device)
-    # XOT_ATTN_TICKETS=1: per-(sequence, KV head) arrival tickets, the last partition merges in-kernel
-    # instead of a reduce launch.  Off by default: measured slower in every configuration
-    # (profiles/bench_attn_small_r1.json, "_t" vs "_r": one workgroup or wave merging all partitions
-    # serially, behind an agent-scope fence, costs more than the parallel reduce kernel's launch).
-    self.tickets = (torch.zeros(max_batch * H, dtype=torch.int32, device=device)
-                    if os.environ.get("XOT_ATTN_TICKETS", "0") == "1" else None)
 
   def partition(self, batch: int, Hkv: int, width_pages: int):
     """(pages per partition, partitions, kernel) for this call."""
     algo = resolve_decode_algo(batch, Hkv, self.algo)
-    if algo == 0 and self.algo < 0 and self.fixed_ppp is None and width_pages <= WG8_MAX_PAGES:
-      algo = 4  # short table, few (sequence, KV head) pairs: 8 waves, <= 2 pages each, no merge launch
     ppp = self.fixed_ppp or choose_pages_per_part(batch, Hkv, width_pages * PAGE, algo)
     nparts = max(1, -(-width_pages // ppp))
     if batch * nparts > self.units:
@@ -236,9 +224,8 @@ def attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale: float, ws: D
     ws = DecodeWorkspace(B, H, Dh, width * PAGE, q.device)
   ppp, nparts, algo = ws.partition(B, k_cache.shape[1], width)
   out = torch.empty_like(q) if out is None else out
-  tk = ws.tickets if ws.tickets is not None and ws.tickets.numel() >= B * k_cache.shape[1] else None
   require().attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, out, ws.o, ws.ml, ppp, nparts, float(scale),
-                        algo, tk)
+                        algo)
   return out
 
 

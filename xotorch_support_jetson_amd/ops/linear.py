@@ -31,17 +31,9 @@ from .weights_layout import (can_shuffle, dequant_stream8, dequant_stream8_to_st
                              shuffle_for_stream, shuffle_for_stream8, unshuffle_from_stream)
 
 
-# XOT_SPLITK_IN_LAUNCH=1: split-K partial sums combined by the last-arriving workgroup of each tile
-# (one launch instead of GEMM + reduce kernel).  Off by default: measured no faster at batch 1
-# (graph launches of the small reduce kernel are cheap) and ~3 % slower at batch 512 (the reducing
-# workgroup is a serial tail on one CU).
-SPLITK_IN_LAUNCH = os.environ.get("XOT_SPLITK_IN_LAUNCH", "0") == "1"
-
-# XOT_GEMM_SK=1: time the stream-K GEMM among the candidates.  Off by default: at the headline it wins the
-# isolated timing of gate/up (M = 512) but fetches ~37 % more bytes from beyond L2 than the ping-pong tile, and
-# under the board power cap a whole decode step ran 0.9 % slower with it (81.64 vs 80.95 ms, same box,
-# profiles/r4/tuner/)
-SK = os.environ.get("XOT_GEMM_SK", "0") == "1"
+# (A stream-K kernel -- persistent 256 x 256 workgroups, k steps dealt evenly -- won the isolated timing of gate/up
+# at M = 512 but fetched ~37 % more bytes from beyond L2 than the ping-pong tile and ran the whole decode step 0.9 %
+# slower under the board power cap, 81.64 vs 80.95 ms, profiles/r4/tuner/; removed in round 6.)
 # XOT_GEMM_PP2=0: leave the two-phase ping-pong tile (code 2256) out of the candidates
 PP2 = os.environ.get("XOT_GEMM_PP2", "1") == "1"
 # XOT_GEMM_W4=0: leave the four-wave 256 x 256 tile (code 4256) out of the candidates
@@ -50,8 +42,8 @@ W4 = os.environ.get("XOT_GEMM_W4", "1") == "1"
 # GEMMs: it reads a third less LDS per FLOP and has ~6 us less fixed cost per tile, profiles/r5/gemm_w4/); below
 # it the ping-pong tile, the measured in-step winner at the decode batches, keeps the preference
 W4_PREF_M = int(os.environ.get("XOT_GEMM_W4_PREF_M", "2048"))
-# XOT_GEMM_TALL_TUNE=1: time the candidates for tall GEMMs too (default: the four-wave tile directly, see shuffled_cfg)
-TALL_FIXED = os.environ.get("XOT_GEMM_TALL_TUNE", "0") != "1"
+# tall GEMMs take the four-wave tile without a timing pass (see shuffled_cfg; tests switch it off)
+TALL_FIXED = True
 # XOT_GEMM_BLAS=1: time hipBLASLt among the candidates for row-major weights (off: the kernel library only)
 BLAS_CAND = os.environ.get("XOT_GEMM_BLAS", "0") == "1"
 # largest M for which the stream GEMM is a candidate (above it only gemm_big is timed)
@@ -121,28 +113,17 @@ def to_rowmajor(w: torch.Tensor) -> torch.Tensor:
 
 # ------------------------------------------------------------------ per-device scratch
 class _Scratch:
-  """Per-device split-K slabs and tile tickets shared by every GEMM call.  A buffer that has to grow is
-  replaced, but the old one is kept alive: HIP graphs captured earlier (decode graphs of other batch
-  buckets) hold its address, and replaying them into a freed block would corrupt whatever the caching
-  allocator put there next (a serving run that captured bucket 1, then grew the slabs for bucket 64,
-  faulted exactly that way).
-
-  `lane` selects an independent set of buffers: the two half-batches of a split decode step
-  (models/transformer.py:_forward_split) run concurrently on two streams and must not share slabs,
-  stream-K partial tiles or tickets."""
+  """Per-device split-K slabs shared by every GEMM call.  A buffer that has to grow is replaced, but the old one is
+  kept alive: HIP graphs captured earlier (decode graphs of other batch buckets) hold its address, and replaying
+  them into a freed block would corrupt whatever the caching allocator put there next (a serving run that captured
+  bucket 1, then grew the slabs for bucket 64, faulted exactly that way)."""
 
   def __init__(self):
-    self.ws: Dict[tuple, torch.Tensor] = {}
-    self.tk: Dict[tuple, torch.Tensor] = {}
-    self.sk: Dict[tuple, tuple] = {}
+    self.ws: Dict[int, torch.Tensor] = {}
     self.retired: list = []
-    self.lane = 0
-
-  def _key(self, device) -> tuple:
-    return (device.index or 0, self.lane)
 
   def splitk(self, device, n: int) -> torch.Tensor:
-    idx = self._key(device)
+    idx = device.index or 0
     t = self.ws.get(idx)
     if t is None or t.numel() < n:
       if torch.cuda.is_current_stream_capturing():
@@ -152,35 +133,6 @@ class _Scratch:
       t = torch.empty(max(n, 1 << 20, 2 * (t.numel() if t is not None else 0)), dtype=torch.float32, device=device)
       self.ws[idx] = t
     return t
-
-  def stream_k(self, device):
-    """(fp32 partial-tile slots, zeroed int32 tickets / flags) of the stream-K GEMM: fixed sizes, allocated
-    once per device and lane (the kernel leaves the sync words zeroed, so graph replays can share them)."""
-    idx = self._key(device)
-    got = self.sk.get(idx)
-    if got is None:
-      if torch.cuda.is_current_stream_capturing():
-        raise RuntimeError("stream-K workspace must be allocated before graph capture")
-      C = require()
-      got = (torch.empty(C.gemm_sk_part_elems(), dtype=torch.float32, device=device),
-             torch.zeros(1 << 20, dtype=torch.int32, device=device))
-      self.sk[idx] = got
-    return got
-
-  def tickets(self, device, n: int) -> torch.Tensor:
-    """Zero-initialised int32 tile counters of the in-launch split-K combine (the last arriver of a
-    tile resets its counter, so the buffer stays zeroed between launches and graph replays)."""
-    idx = self._key(device)
-    t = self.tk.get(idx)
-    if t is None or t.numel() < n:
-      if torch.cuda.is_current_stream_capturing():
-        raise RuntimeError("split-K tickets must be sized before graph capture")
-      if t is not None:
-        self.retired.append(t)
-      t = torch.zeros(max(n, 1 << 16), dtype=torch.int32, device=device)
-      self.tk[idx] = t
-    return t
-
 
 
 scratch = _Scratch()
@@ -200,7 +152,7 @@ def _default_table_path():
     dev = torch.cuda.get_device_name(torch.cuda.current_device()).replace(" ", "_").replace("/", "_")
     from ..helpers import xot_home
     # settings that change the candidate sets are part of the name, so a table never answers for another
-    tag = (f"{os.environ.get('XOT_GEMM', 'auto')}-{STREAM_MAX_M}-{BIG_MIN_M}-{SLAB_TBPS:g}{'-sk' if SK else ''}"
+    tag = (f"{os.environ.get('XOT_GEMM', 'auto')}-{STREAM_MAX_M}-{BIG_MIN_M}-{SLAB_TBPS:g}"
            f"{'-blas' if BLAS_CAND else ''}-t{TIE:g}-x{TIE_X:g}{'' if PP2 else '-nopp2'}")
     return str(xot_home() / "gemm" / f"{dev}-{st.st_size:x}-{int(st.st_mtime):x}-{tag}.json")
   except Exception:  # noqa: BLE001 - no table then; tuning still works in memory
@@ -373,10 +325,6 @@ class GemmPolicy:
         if S > 1 and (tiles >= 256 or tiles * S > 1024 or Kd // 64 < 2 * S):
           continue
         cands.append(("big", bn, S))
-    # stream-K: one persistent 256 x 256 workgroup per CU, the k steps of all tiles dealt out evenly (wins when
-    # the tile count leaves the last round of plain tiles partly empty)
-    if SK and M >= 256 and N % 256 == 0 and (N // 256) * (Kd // 64) >= 256 and -(-M // 256) <= 8 and M * N < (1 << 31):
-      cands.append(("sk", 256, 1))
     return cands
 
   def shuffled_cfg(self, x, w, bias, residual, epi, out_dtype) -> Tuple:
@@ -476,7 +424,7 @@ def _tie_break(times: Dict, M: int = 0) -> Tuple:
 
 
 def _ws_elems(cfg, M, N) -> int:
-  return cfg[2] * M * N if len(cfg) == 3 and cfg[0] != "sk" and cfg[2] > 1 else 0
+  return cfg[2] * M * N if len(cfg) == 3 and cfg[2] > 1 else 0
 
 
 # HBM rate (TB/s) at which the consumer of split-K fp32 slabs (slab reduce, fused reduce + RoPE / + residual +
@@ -497,8 +445,7 @@ def _stream_call(x, w, bias, residual, epi, out, cfg, shuffled: bool = True):
   ntw, S = cfg
   M, N = x.shape[0], w.shape[0]
   ws = scratch.splitk(x.device, S * M * N) if S > 1 else None
-  tk = scratch.tickets(x.device, (N // 64) * (-(-M // 128))) if S > 1 and SPLITK_IN_LAUNCH else None
-  require().gemm_stream(x, w, out, bias, residual, ws, K.EPI[epi], ntw, S, shuffled, tk)
+  require().gemm_stream(x, w, out, bias, residual, ws, K.EPI[epi], ntw, S, shuffled)
   return out
 
 
@@ -530,10 +477,6 @@ def _linear8(x, w, bias, residual, epi, out, dt):
 def _shuffled_call(x, w, bias, residual, epi, out, cfg):
   if cfg[0] == "stream":
     return _stream_call(x, w, bias, residual, epi, out, cfg[1:])
-  if cfg[0] == "sk":
-    part, sync = scratch.stream_k(x.device)
-    require().gemm_sk(x, w, out, bias, residual, part, sync, K.EPI[epi], cfg[1])
-    return out
   _, bn, S = cfg
   M, N = x.shape[0], w.shape[0]
   ws = scratch.splitk(x.device, S * M * N) if S > 1 else None
@@ -607,8 +550,6 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, r
   return out
 
 
-# XOT_FUSE_NORM=0: keep the split-K reduce and the following RMSNorm as separate kernels
-FUSE_NORM = os.environ.get("XOT_FUSE_NORM", "1") == "1"
 
 
 def linear_resid_norm(x: torch.Tensor, w: torch.Tensor, h: torch.Tensor, ln_w: torch.Tensor, eps: float,
@@ -617,7 +558,7 @@ def linear_resid_norm(x: torch.Tensor, w: torch.Tensor, h: torch.Tensor, ln_w: t
 
   When the projection runs split-K on the pre-shuffled layout, the GEMM leaves its fp32 slabs and one
   kernel does the slab reduce, the residual add and the RMSNorm (instead of reduce + norm kernels)."""
-  if FUSE_NORM and x.is_cuda and layout_of(w) == "stream":
+  if x.is_cuda and layout_of(w) == "stream":
     if x.stride(1) != 1 or x.stride(0) % 8:
       x = x.contiguous()
     M, N = x.shape[0], w.shape[0]
@@ -627,7 +568,7 @@ def linear_resid_norm(x: torch.Tensor, w: torch.Tensor, h: torch.Tensor, ln_w: t
       ws = scratch.splitk(x.device, S * M * N)
       C = require()
       if cfg[0] == "stream":
-        C.gemm_stream(x, w, h, None, h, ws, K.EPI["resid"], cfg[1], S, True, None, False)
+        C.gemm_stream(x, w, h, None, h, ws, K.EPI["resid"], cfg[1], S, True, False)
       else:
         C.gemm_big(x, w, h, None, h, ws, K.EPI["resid"], cfg[1], S, False)
       out = torch.empty_like(h) if out is None else out
@@ -637,8 +578,6 @@ def linear_resid_norm(x: torch.Tensor, w: torch.Tensor, h: torch.Tensor, ln_w: t
   return K.rmsnorm(h, ln_w, eps, out=out)[0]
 
 
-# XOT_FUSE_ROPE=0: keep the QKV split-K reduce and the RoPE / KV-cache write as separate kernels
-FUSE_ROPE = os.environ.get("XOT_FUSE_ROPE", "1") == "1"
 
 
 def linear_rope_kv(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None, pos: torch.Tensor,
@@ -648,7 +587,7 @@ def linear_rope_kv(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None, 
 
   When the QKV projection runs split-K on the pre-shuffled layout, its fp32 slabs go straight to one
   kernel that sums them, rotates and writes q / the caches (no bf16 qkv round trip, one launch less)."""
-  if FUSE_ROPE and x.is_cuda and layout_of(w) == "stream":
+  if x.is_cuda and layout_of(w) == "stream":
     if x.stride(1) != 1 or x.stride(0) % 8:
       x = x.contiguous()
     M, N = x.shape[0], w.shape[0]
@@ -659,7 +598,7 @@ def linear_rope_kv(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None, 
       y = torch.empty(M, N, dtype=x.dtype, device=x.device)  # shape carrier only: the slabs are not reduced
       C = require()
       if cfg[0] == "stream":
-        C.gemm_stream(x, w, y, None, None, ws, K.EPI["none"], cfg[1], S, True, None, False)
+        C.gemm_stream(x, w, y, None, None, ws, K.EPI["none"], cfg[1], S, True, False)
       else:
         C.gemm_big(x, w, y, None, None, ws, K.EPI["none"], cfg[1], S, False)
       Dh = k_cache.shape[-1]

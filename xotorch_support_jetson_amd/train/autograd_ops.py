@@ -182,12 +182,6 @@ class CrossEntropyFn(torch.autograd.Function):
     return d.to(logits.dtype), None, None
 
 
-# A/B switches of the backward kernels (read once by the library too): the v1 dQ / dK-dV kernels stage transposed
-# [B, heads, DH, Lp] images of K / Q and dO; the v2 kernels transpose in their LDS reads instead.
-_DQ_V1 = os.environ.get("XOT_TRAIN_DQ_V1", "0") == "1"
-_DKDV_V1 = os.environ.get("XOT_TRAIN_DKDV_V1", "0") == "1"
-
-
 class AttentionFn(torch.autograd.Function):
   """q [B*L, H*Dh], k / v [B*L, Hkv*Dh] (token-major, may be strided row views) -> o [B*L, H*Dh]."""
 
@@ -214,16 +208,12 @@ class AttentionFn(torch.autograd.Function):
       C = require()
       q, k, v, o, lse2 = ctx.saved_tensors
       do = do.contiguous().to(q.dtype)
-      none = torch.empty(0, dtype=q.dtype, device=q.device)  # the v2 kernels read no transposed image
-      qt = _transposed(C, q, B, L, Lp, H, Dh) if _DKDV_V1 else none
-      kt = _transposed(C, k, B, L, Lp, Hkv, Dh) if _DQ_V1 else none
-      dot = _transposed(C, do, B, L, Lp, H, Dh) if _DKDV_V1 else none
       dq = torch.empty(B * L, H * Dh, dtype=q.dtype, device=q.device)
       dk = torch.empty(B * L, Hkv * Dh, dtype=q.dtype, device=q.device)
       dv = torch.empty_like(dk)
       delta = torch.empty_like(lse2)
       ws = torch.empty(2 * H * B * L * Dh, dtype=torch.float32, device=q.device)  # per-query-head dK/dV partials
-      C.attn_train_bwd(q, qt, k, kt, v, o, do, dot, lse2, delta, dq, dk, dv, ws, B, L, Lp, H, Hkv, Dh, scale)
+      C.attn_train_bwd(q, k, v, o, do, lse2, delta, dq, dk, dv, ws, B, L, Lp, H, Hkv, Dh, scale)
       return dq, dk, dv, None, None, None, None, None, None
     q, k, v = ctx.saved_tensors
     with torch.enable_grad():
@@ -271,13 +261,8 @@ def rmsnorm(x, w, eps, acc=None):
   return RMSNormFn.apply(x, w, eps, acc)
 
 
-RESNORM = os.environ.get("XOT_RESNORM", "1") == "1"  # 0: plain RMSNorm + autograd's add per residual join (A/B)
-
-
 def res_rmsnorm(h, w, eps, acc=None):
   """(h, rmsnorm(h, w)): use the returned h downstream so the residual gradient joins in the norm's backward."""
-  if not RESNORM:
-    return h, RMSNormFn.apply(h, w, eps, acc)
   return ResNormFn.apply(h, w, eps, acc)
 
 
@@ -533,18 +518,11 @@ def linear_own(x, w, tw, acc, h=None):
   return OwnLinearFn.apply(x, w, tw, h, acc)
 
 
-# 1: the SiLU backward in the dA GEMM's epilogue.  Measured slower on the Llama-3-8B step (728-730 vs 721 ms,
-# profiles/r5/train/silu_bwd_fused/): the epilogue's gate / up reads and two outputs run at the tail of every tile
-# on the dX chain's critical path, where the separate silu_mul_bwd kernel streams at ~6 TB/s.  Off by default.
-SILU_BWD_FUSED = os.environ.get("XOT_SILU_BWD_FUSED", "0") == "1"
-
-
 class SiluDownFn(torch.autograd.Function):
-  """y = (silu(gate) * up) . W_down^T (+ h): SiluMulFn and the down projection's OwnLinearFn in one, so the
-  backward forms dGU in the epilogue of the down projection's input-gradient GEMM (csrc gemm_w4 EPI_SILU_BWD via
-  gemm_silu_bwd): the four-wave tile reads gate / up beside its accumulators and writes dgate / dup, instead of
-  writing dA [T, F] and re-reading it with gate / up in silu_mul_bwd (2 x T x F x 2 bytes of HBM traffic and a
-  kernel per layer and micro-batch).  Shapes the tile does not cover take the two-kernel path."""
+  """y = (silu(gate) * up) . W_down^T (+ h): SiluMulFn and the down projection's OwnLinearFn in one autograd node
+  (the backward: dA = dY . W_down on the own tiles, then silu_mul_bwd at ~6 TB/s).  (The SiLU backward in the dA
+  GEMM's epilogue was measured slower -- 728-730 vs 721 ms per Llama-3-8B step, profiles/r5/train/silu_bwd_fused/:
+  the gate / up reads and two outputs sat at the tail of every tile on the dX chain's critical path -- and removed.)"""
 
   @staticmethod
   def forward(ctx, gu, w, tw, h, acc):
@@ -565,12 +543,8 @@ class SiluDownFn(torch.autograd.Function):
     gu, a = ctx.saved_tensors
     tw, acc = ctx.tw, ctx.acc
     dy = dy.contiguous()
-    F, K = tw.wts.shape
     dgu = torch.empty_like(gu)
-    if SILU_BWD_FUSED and F % 256 == 0 and K % 128 == 0 and dy.shape[0] * K * 2 < (1 << 32):
-      require().gemm_silu_bwd(dy, tw.wts, gu, dgu)
-    else:
-      require().silu_mul_bwd(gu, linear(dy, tw.wts), dgu)
+    require().silu_mul_bwd(gu, linear(dy, tw.wts), dgu)
     own_dw(dy, a, acc)
     return dgu, None, None, (dy if ctx.has_h else None), None
 

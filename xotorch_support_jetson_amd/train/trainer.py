@@ -40,10 +40,6 @@ FUSED_CE = os.environ.get("XOT_FUSED_CE", "1") == "1"
 # rows per fused LM-head + CE chunk: 4096 (one [4096, V] fp32 logits block, 2.1 GB at V = 128256) ran the
 # Llama-3-8B step 1.1 % faster than 1024 (profiles/r5/train/knobs_r5s/)
 CE_CHUNK = int(os.environ.get("XOT_CE_CHUNK", "4096"))
-EMBED_ACC = os.environ.get("XOT_EMBED_ACC", "1") == "1"  # 0: autograd's dense embedding gradient (A/B)
-NORM_ACC = os.environ.get("XOT_NORM_ACC", "1") == "1"  # 0: autograd-accumulated RMSNorm weight gradients (A/B)
-# XOT_FUSED_ADAMW=0: plain AdamW + relayout refresh of the operand images (A/B of csrc/train_ops.hip adamw_tiled)
-FUSED_ADAMW = os.environ.get("XOT_FUSED_ADAMW", "1") == "1"
 
 
 def _resid_mm(h: torch.Tensor, x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
@@ -128,7 +124,7 @@ class ShardTrainer:
           self.acc["lm_head"] = A.GradAcc("lm_head", self.params["lm_head"])
     # RMSNorm weights: the backward kernel's dw reduce adds into an fp32 GradAcc across micro-batches (no zeroed
     # vector, bf16 copy and autograd accumulation add per norm and micro-batch)
-    if self.device.type == "cuda" and NORM_ACC:
+    if self.device.type == "cuda":
       for k in self.params:
         if k == "norm" or k.split(".")[-1] in ("ln1", "ln2"):
           a = A.GradAcc(k, self.params[k])
@@ -136,7 +132,7 @@ class ShardTrainer:
           self.acc[k] = a
     # untied input embedding: its gradient accumulates into an fp32 GradAcc (A.EmbedAccFn), not a dense autograd
     # gradient per micro-batch (after the TrainWeight loop above: the table has no operand images)
-    if self.device.type == "cuda" and "embed" in self.params and self.head_name != "embed" and EMBED_ACC:
+    if self.device.type == "cuda" and "embed" in self.params and self.head_name != "embed":
       a = A.GradAcc("embed", self.params["embed"])
       a.buf = torch.empty(self.params["embed"].shape, dtype=torch.float32, device=self.device)
       self.acc["embed"] = a
@@ -467,7 +463,7 @@ class ShardTrainer:
     counted = [g for k, g in grads.items() if k not in norm_exclude]
     # GPU: one multi-tensor sum-of-squares pass (csrc/train_ops.hip multi_sumsq) over every gradient, no fp32
     # copies; CPU: an fp32-accumulating norm per tensor
-    if counted and os.environ.get("XOT_MULTI_SUMSQ", "1") == "1" and all(g.is_cuda and g.is_contiguous() and g.dtype in (torch.bfloat16, torch.float32)
+    if counted and all(g.is_cuda and g.is_contiguous() and g.dtype in (torch.bfloat16, torch.float32)
                        for g in counted):
       sq = require().multi_sumsq(counted).reshape(())
     else:
@@ -482,7 +478,7 @@ class ShardTrainer:
     for k, g in grads.items():
       p, m, v, pb = self.master[k], self.m[k], self.v[k], self.params[k]
       tw = self.tw.get(k)
-      if p.is_cuda and FUSED_ADAMW and isinstance(tw, A.TrainWeight) and p.dim() == 2:
+      if p.is_cuda and isinstance(tw, A.TrainWeight) and p.dim() == 2:
         # the update writes the own-GEMM operand images directly (no bf16 copy + two relayouts); the plain bf16
         # copy only where something may still read it: a projection without a GradAcc runs torch's matmul on it,
         # the LM head / tied embedding is read by the embedding lookup and the unfused logits path.  Projections
