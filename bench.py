@@ -64,7 +64,7 @@ class ClockSampler:
           power = float(str(v).split()[0])
         except ValueError:
           pass
-      if k.startswith("sclk"):
+      if "sclk" in k.lower() and sclk is None:  # ("sclk clock speed:" "(2100Mhz)"; the level key has no MHz)
         m = re.search(r"(\d+)\s*Mhz", str(v), re.I)
         sclk = float(m.group(1)) if m else None
     return power, sclk

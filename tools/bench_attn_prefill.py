@@ -58,7 +58,8 @@ def main():
                       "us": round(us, 1), "TFLOPs": round(flops / us / 1e6, 1)}), flush=True)
   # torch SDPA on the same data laid out contiguously
   kk = kc[bt.long()].permute(0, 2, 1, 3, 4).reshape(B, Hkv, pages * 64, Dh)[:, :, :L]
-  vv = vc[bt.long()].permute(0, 2, 1, 4, 3).reshape(B, Hkv, pages * 64, Dh)[:, :, :L]
+  from xotorch_support_jetson_amd.ops.reference import v_chunks
+  vv = v_chunks(vc)[bt.long()].permute(0, 2, 1, 3, 5, 4).reshape(B, Hkv, pages * 64, Dh)[:, :, :L]
   kk = kk.repeat_interleave(H // Hkv, 1).contiguous()
   vv = vv.repeat_interleave(H // Hkv, 1).contiguous()
   qq = q.view(B, L, H, Dh).transpose(1, 2).contiguous()

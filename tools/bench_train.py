@@ -42,6 +42,9 @@ def main():
                   help="pp: layer pipeline (the reference's strategy); dp: full replica per GPU, bucketed "
                        "all-reduce overlapped with backward (parallel/data_parallel.py)")
   ap.add_argument("--schedule", choices=("gpipe", "1f1b"), default="gpipe", help="pp micro-batch order")
+  ap.add_argument("--torch-prof", default="",
+                  help="after the timed steps, profile one more step with torch.profiler and write the per-op table "
+                       "(device time of the torch ops that are not own kernels, with their Python call sites) here")
   args = ap.parse_args()
 
   import torch.distributed as dist
@@ -115,6 +118,14 @@ def main():
                  "parallelism": (f"dp{world} (bucketed all-reduce overlapped with backward)" if dp else
                                  f"pp{world} ({args.schedule}, RCCL p2p)")},
     }), flush=True)
+  if args.torch_prof and rank == 0:
+    from torch.profiler import ProfilerActivity, profile
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
+      pt.step(batches())
+      sync()
+    with open(args.torch_prof, "w") as f:
+      f.write(prof.key_averages().table(sort_by="self_cuda_time_total", row_limit=60) + "\n")
+      f.write(prof.key_averages(group_by_stack_n=6).table(sort_by="self_cuda_time_total", row_limit=40) + "\n")
   if world > 1:
     dist.barrier()
     dist.destroy_process_group()

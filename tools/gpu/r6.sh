@@ -19,8 +19,10 @@ for what in "$@"; do
             step r6/breakdown8b1 60 python tools/decode_breakdown.py "$(ls "$O"/r6/prof8b1/*/*kernel_trace.csv "$O"/r6/prof8b1/*kernel_trace.csv 2>/dev/null | head -1)" --steps 16 --json "$O/r6/breakdown8b1.json" ;;
     ring70) # RingServer (`xot --gpus 1 --ring`) at the headline operating point: Llama-3-70B, 512 streams x 128 tokens
             step r6/ring70 1100 python -u tools/bench_serve.py --ring 1 --model llama-3-70b --concurrency 512 --max-tokens 128 --prompt-words 124 --server-log "$O/r6/ring70_server.log" ;;
-    layout) step r6/layout 120 python -u tools/bench_layout.py ;;
     train)  step r6/train 900 python -u tools/bench_train.py --model llama-3-8b --seq 2048 --mb 2 --microbatches 4 --steps 3 --warmup 1 ;;
+    train_norelayout) XOT_EXP_NO_RELAYOUT=1 step r6/train_norelayout 900 python -u tools/bench_train.py --model llama-3-8b --seq 2048 --mb 2 --microbatches 4 --steps 3 --warmup 1 ;;
+    train_norope) XOT_EXP_NO_ROPE=1 step r6/train_norope 900 python -u tools/bench_train.py --model llama-3-8b --seq 2048 --mb 2 --microbatches 4 --steps 3 --warmup 1 ;;
+    train_tprof) step r6/train_tprof 900 python -u tools/bench_train.py --model llama-3-8b --seq 2048 --mb 2 --microbatches 4 --steps 2 --warmup 1 --torch-prof "$O/r6/train_torch_ops.txt" ;;
     trainprof) prof r6/trainprof 900 python3 "$R/tools/bench_train.py" --mb 2 --microbatches 4 --steps 3 --warmup 1
             step r6/trainstep 60 python tools/step_window.py "$(ls "$O"/r6/trainprof/*/*kernel_trace.csv "$O"/r6/trainprof/*kernel_trace.csv 2>/dev/null | head -1)" ;;
     relayout_test) step r6/relayout_test 300 python -u -m pytest tests/test_kernels_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread -k relayout ;;

@@ -1,7 +1,10 @@
 // Paged-KV attention for CDNA4 (MFMA 16x16x32 bf16, wave64).
 //
-// KV cache (one per layer, per shard):  K [num_pages, Hkv, 64, Dh]   V [num_pages, Hkv, Dh, 64]
-// (V is stored transposed inside a page so the P.V MFMA B-operand is contiguous along keys).
+// KV cache (one per layer, per shard):  K [num_pages, Hkv, 64, Dh]   V [num_pages, Hkv, 8, Dh, 8]
+// V is stored chunk-major inside a page (kernels.h v_page_off): 8 chunks of 8 keys, each chunk [Dh][8], so the
+// P.V MFMA operand (8 consecutive keys of one dim) is one 16-B run, a lane group's 16 dims are 256 contiguous
+// bytes, and a decode step's new token touches 16 cache lines per KV head (one 16-B run of 8 dims in each)
+// instead of the 128 lines of a [Dh][64] transposed page (profiles/r6/headline/v_chunk/).
 //
 //  decode:  one query token per sequence.  The G = H/Hkv query heads that share a KV head are the
 //           16 MFMA rows (GQA packing: K/V are read once per KV head, not once per query head).
@@ -94,7 +97,7 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_kernel(
 #pragma unroll
     for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
-      for (int k2 = 0; k2 < 2; ++k2) vf[dt][k2] = ld16(vb + (16 * dt + c) * PAGE + 16 * g + 8 * k2);
+      for (int k2 = 0; k2 < 2; ++k2) vf[dt][k2] = ld16(vb + v_page_off(8 * (2 * g + k2), 16 * dt + c, DH));
 
     f32x4 sc[4];
 #pragma unroll
@@ -262,7 +265,7 @@ __device__ __forceinline__ void decode_wave_unit(
   const int32_t* bt = block_tables + (size_t)b * max_blocks;
   // K page [64 keys][DH]: score tile t = 2kk + h, lane (g, c) reads key 32kk + 8(c/4) + 4h + c%4,
   //   d 32s + 8g .. +8 for k-step s
-  // V^T page [DH][64 keys]: d tile dt, k-step kk, lane (g, c) reads d 16dt + c, keys 32kk + 8g .. +8
+  // V page (chunk-major): d tile dt, k-step kk, lane (g, c) reads d 16dt + c, keys 32kk + 8g .. +8 = chunk 4kk + g
   const int krow = 8 * (c >> 2) + (c & 3);
   auto page_of = [&](int p) -> long { return min(max(bt[p], 0), num_pages - 1); };
   auto load_k = [&](int p, long page, s16x8 (&kf)[4][KS]) {
@@ -278,21 +281,24 @@ __device__ __forceinline__ void decode_wave_unit(
       for (int s = 0; s < KS; ++s) kf[t][s] = NT ? ld16nt(kb + r * DH + 32 * s) : ld16(kb + r * DH + 32 * s);
     }
   };
-  // V^T rows hold a page's 64 keys as two 64-B halves; when the context ends in the first half of the last page
-  // (vtail), the second half is not read (zeros: its P is 0 anyway, and stale cache contents never reach O).
+  // Chunks of 8 keys that start past the context (the tail of the last page, vtail) are not read: zeros (their P
+  // is 0 anyway, and stale cache contents never reach O).  Lane group g's chunks are 4kk + g, so the skip is per
+  // 16-lane group, at 256-B granularity.
   auto load_v = [&](int p, long page, s16x8 (&vf)[NDT][2]) {
-    const uint16_t* vb = vc + ((size_t)page * Hkv + kvh) * DH * PAGE + c * PAGE + 8 * g;
-    const bool hi = !vtail || p * PAGE + 32 < ctx;  // wave-uniform
+    const uint16_t* vb = vc + ((size_t)page * Hkv + kvh) * DH * PAGE + v_page_off(8 * g, c, DH);
+    const int left = vtail ? ctx - p * PAGE : PAGE;  // keys of this page inside the context
 #pragma unroll
-    for (int dt = 0; dt < NDT; ++dt)
-      vf[dt][0] = NT ? ld16nt(vb + 16 * dt * PAGE) : ld16(vb + 16 * dt * PAGE);
-    if (hi) {
+    for (int kk = 0; kk < 2; ++kk) {
+      if (8 * (4 * kk + g) < left) {
 #pragma unroll
-      for (int dt = 0; dt < NDT; ++dt)
-        vf[dt][1] = NT ? ld16nt(vb + 16 * dt * PAGE + 32) : ld16(vb + 16 * dt * PAGE + 32);
-    } else {
+        for (int dt = 0; dt < NDT; ++dt) {
+          const uint16_t* a = vb + v_page_off(32 * kk, 16 * dt, DH);
+          vf[dt][kk] = NT ? ld16nt(a) : ld16(a);
+        }
+      } else {
 #pragma unroll
-      for (int dt = 0; dt < NDT; ++dt) vf[dt][1] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        for (int dt = 0; dt < NDT; ++dt) vf[dt][kk] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      }
     }
   };
   auto load = [&](int p, s16x8 (&kf)[4][KS], s16x8 (&vf)[NDT][2]) {
@@ -555,7 +561,7 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(
     for (int i = 0; i < NCH; ++i) {
       const int qd = tid + 256 * i;
       st16(ks + (qd / CPR) * KLD + (qd % CPR) * 8, rk[i]);
-      st16(vs + (qd / (PAGE / 8)) * VLD + (qd % (PAGE / 8)) * 8, rv[i]);
+      st16(vs + (qd % DH) * VLD + (qd / DH) * 8, rv[i]);  // granule qd = (key chunk qd / DH, dim qd % DH)
     }
     __syncthreads();
     if (p + 1 < npages) gload(p + 1);
@@ -723,8 +729,8 @@ __global__ __launch_bounds__(512, 1) void attn_prefill_v2_kernel(
         const int r = P / KGPR, j = (P % KGPR) ^ pf_kswz<DH>(r);
         src = kb + (r * KGPR + j) * 8;
       } else {
-        const int r = P >> 3, j = (P & 7) ^ (r & 7);  // V^T rows: 64 keys = 8 granules
-        src = vb + (r * 8 + j) * 8;
+        const int r = P >> 3, j = (P & 7) ^ (r & 7);  // V^T image rows: 64 keys = 8 granules (chunks)
+        src = vb + v_page_off(8 * j, r, DH);
       }
       __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
                                        (__attribute__((address_space(3))) void*)(dst + ch * 512), 16, 0, 0);

@@ -366,7 +366,7 @@ void gemm_big(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const c10
 // y_e = y.data + e * ybat (rows ldy apart, N columns).
 // Layout kernels of the training GEMMs (csrc/layout.hip).  mode 0: dst = shuffle(src) ([R, C], R % 16,
 // C % 128); 1: dst = shuffle(src^T) ([C, R] shuffled; R % 128, C % 64); 2: dst = src^T row-major (same).
-void relayout(const at::Tensor& src, at::Tensor& dst, int64_t mode, int64_t variant) {
+void relayout(const at::Tensor& src, at::Tensor& dst, int64_t mode) {
   CHECK_BF16(src);
   CHECK_BF16(dst);
   XCHECK(src.dim() == 2 && src.stride(1) == 1 && src.stride(0) % 8 == 0, "relayout: src must be 2-D with 16-B rows");
@@ -374,8 +374,8 @@ void relayout(const at::Tensor& src, at::Tensor& dst, int64_t mode, int64_t vari
   const int R = (int)src.size(0), C = (int)src.size(1);
   int rc = -1;
   if (mode == 0) rc = xot::launch_shuffle(bf(src), src.stride(0), bf(dst), R, C, cur_stream());
-  else if (mode == 1) rc = xot::launch_shuffle_t(bf(src), src.stride(0), bf(dst), R, C, cur_stream(), (int)variant);
-  else if (mode == 2) rc = xot::launch_transpose(bf(src), src.stride(0), bf(dst), R, C, cur_stream(), (int)variant);
+  else if (mode == 1) rc = xot::launch_shuffle_t(bf(src), src.stride(0), bf(dst), R, C, cur_stream());
+  else if (mode == 2) rc = xot::launch_transpose(bf(src), src.stride(0), bf(dst), R, C, cur_stream());
   XCHECK(rc == 0, "relayout: unsupported shape R=", R, " C=", C, " mode=", mode);
 }
 
@@ -908,7 +908,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("reduce") = true);
   m.def("gemm_stream8", &gemm_stream8, py::arg("x"), py::arg("w8"), py::arg("wscale"), py::arg("y"), py::arg("bias"),
         py::arg("res"), py::arg("ws"), py::arg("epi"), py::arg("ntw"), py::arg("splits"), py::arg("reduce") = true);
-  m.def("relayout", &relayout, py::arg("src"), py::arg("dst"), py::arg("mode"), py::arg("variant") = 2);
+  m.def("relayout", &relayout, py::arg("src"), py::arg("dst"), py::arg("mode"));
   m.def("gemm_kgroup", &gemm_kgroup);
   m.def("gemm_batched", &gemm_batched, py::arg("x"), py::arg("xbat"), py::arg("K"), py::arg("w"), py::arg("y"),
         py::arg("ybat"), py::arg("ldy"), py::arg("M"));

@@ -69,4 +69,9 @@ __device__ __forceinline__ void st16(void* p, const s16x8& v) { *reinterpret_cas
 
 __device__ __forceinline__ float silu(float x) { return x / (1.0f + __expf(-x)); }
 
+// Paged V cache: a 64-key page of one KV head is stored chunk-major, 8 chunks of 8 keys, each chunk [Dh][8]:
+// element offset of (key, d) inside the page.  Readers (the attention kernels) load 8 consecutive keys of one dim
+// as one 16-B run; a writer's token fills 2 B in each of Dh 16-B runs packed 8 to a 128-B line.
+__host__ __device__ __forceinline__ int v_page_off(int key, int d, int Dh) { return ((key >> 3) * Dh + d) * 8 + (key & 7); }
+
 }  // namespace xot

@@ -49,8 +49,8 @@ int launch_gemm_big(const uint16_t* X, int ldx, const uint16_t* W, const uint16_
 // B independent GEMMs Y_e = X_e . W_e^T (pre-shuffled W [B][N][K]; X_e = X + e*xbat, Y_e = Y + e*ybat)
 // training-GEMM layouts (csrc/layout.hip): src [R, C] row-major with row stride ld
 int launch_shuffle(const uint16_t* src, long ld, uint16_t* dst, int R, int C, hipStream_t s);
-int launch_shuffle_t(const uint16_t* src, long ld, uint16_t* dst, int R, int C, hipStream_t s, int variant = 2);
-int launch_transpose(const uint16_t* src, long ld, uint16_t* dst, int R, int C, hipStream_t s, int variant = 2);
+int launch_shuffle_t(const uint16_t* src, long ld, uint16_t* dst, int R, int C, hipStream_t s);
+int launch_transpose(const uint16_t* src, long ld, uint16_t* dst, int R, int C, hipStream_t s);
 int launch_gemm_kgroup(const uint16_t* X, int ldx, const uint16_t* W, uint16_t* Y, int ldy, bool resid,
                        const int* koff, int E, int M, int N, int K, hipStream_t st);
 int launch_gemm_batched(const uint16_t* X, int ldx, long xbat, const uint16_t* W, void* Y, int ldy, long ybat,

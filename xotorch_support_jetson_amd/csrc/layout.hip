@@ -84,63 +84,6 @@ __global__ __launch_bounds__(256) void transpose_kernel(const uint16_t* __restri
 }
 
 
-// ---- v2 (round 6): 128 x 128 tiles staged row-major (16-B LDS writes, 144-element pitch = 8 dwords mod 64) and read
-// back TRANSPOSED with ds_read_b64_tr_b16: a 16-lane group's two reads return, lane c, src column c of a 16-column
-// block at 8 consecutive src rows -- exactly one 8-element output chunk, so every store is 16 B and a wave's four
-// groups write 64 B (transpose) / 1 KB (shuffle_t) contiguous.  Column tiles are the fastest grid dimension: the
-// blocks in flight together read adjacent 256-B segments of the same 128 src rows (the v1 grid walked down the
-// rows of one 128-B column strip, ~1.1 TB/s on the training step's dY^T).
-typedef __attribute__((address_space(3))) s16x4* lds_s16x4_t;
-constexpr int T2 = 128, T2P = T2 + 16;
-
-__device__ __forceinline__ void stage_tile_rows(const uint16_t* __restrict__ src, long ld, int r0, int c0,
-                                                uint16_t* lt) {
-#pragma unroll
-  for (int i = 0; i < T2 * T2 / 8 / 256; ++i) {  // 2048 chunks of 8, 16 per row
-    const int q = i * 256 + threadIdx.x;
-    const int r = q >> 4, c8 = (q & 15) * 8;
-    *reinterpret_cast<s16x8*>(lt + r * T2P + c8) = ld16(src + (long)(r0 + r) * ld + c0 + c8);
-  }
-}
-
-// 8 consecutive tile rows rr .. rr+7 of tile column cc + (lane c of the 16-lane group), from the row-major LDS tile
-__device__ __forceinline__ s16x8 tr_chunk(const uint16_t* lt, int rr, int cc, int c) {
-  const uint16_t* p = lt + (rr + (c >> 2)) * T2P + cc + 4 * (c & 3);
-  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t)(p));
-  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t)(p + 4 * T2P));
-  return s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-}
-
-__global__ __launch_bounds__(256) void transpose2_kernel(const uint16_t* __restrict__ src, long ld,
-                                                         uint16_t* __restrict__ dst, int R, int C) {
-  __shared__ __attribute__((aligned(16))) uint16_t lt[T2 * T2P];
-  const int c0 = blockIdx.x * T2, r0 = blockIdx.y * T2;
-  stage_tile_rows(src, ld, r0, c0, lt);
-  __syncthreads();
-  const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15, wave = threadIdx.x >> 6;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {  // 128 groups = 8 column blocks x 16 row blocks of 8
-    const int G = i * 16 + wave * 4 + g, rb = G & 15, cb = G >> 4;
-    st16(dst + (long)(c0 + cb * 16 + c) * R + r0 + rb * 8, tr_chunk(lt, rb * 8, cb * 16, c));
-  }
-}
-
-__global__ __launch_bounds__(256) void shuffle_t2_kernel(const uint16_t* __restrict__ src, long ld,
-                                                         uint16_t* __restrict__ dst, int R, int C) {
-  __shared__ __attribute__((aligned(16))) uint16_t lt[T2 * T2P];
-  const int c0 = blockIdx.x * T2, r0 = blockIdx.y * T2;  // 8 row groups (nt) x one 128-deep k chunk (kc)
-  stage_tile_rows(src, ld, r0, c0, lt);
-  __syncthreads();
-  const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15, wave = threadIdx.x >> 6;
-  const int KC = R / 128, kc = r0 / 128;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {  // 128 groups = 8 nt x 4 k-steps (s) x 4 lane groups (g')
-    const int G = i * 16 + wave * 4 + g, gp = G & 3, st = (G >> 2) & 3, ntl = G >> 4;
-    const long nt = c0 / 16 + ntl;
-    st16(dst + (((nt * KC + kc) * 4 + st) * 64 + 16 * gp + c) * 8, tr_chunk(lt, st * 32 + gp * 8, ntl * 16, c));
-  }
-}
-
 int launch_shuffle(const uint16_t* src, long ld, uint16_t* dst, int R, int C, hipStream_t s) {
   if (R % 16 || C % 128) return -1;
   const long chunks = (long)R * C / 8;
@@ -150,24 +93,14 @@ int launch_shuffle(const uint16_t* src, long ld, uint16_t* dst, int R, int C, hi
   return 0;
 }
 
-int launch_shuffle_t(const uint16_t* src, long ld, uint16_t* dst, int R, int C, hipStream_t s, int variant) {
-  if (variant == 2 && R % T2 == 0 && C % T2 == 0) {
-    if (R == 0 || C == 0) return 0;
-    shuffle_t2_kernel<<<dim3(C / T2, R / T2), 256, 0, s>>>(src, ld, dst, R, C);
-    return 0;
-  }
+int launch_shuffle_t(const uint16_t* src, long ld, uint16_t* dst, int R, int C, hipStream_t s) {
   if (R % TR || C % TC) return -1;
   if (R == 0 || C == 0) return 0;
   shuffle_t_kernel<<<dim3(R / TR, C / TC), 256, 0, s>>>(src, ld, dst, R, C);
   return 0;
 }
 
-int launch_transpose(const uint16_t* src, long ld, uint16_t* dst, int R, int C, hipStream_t s, int variant) {
-  if (variant == 2 && R % T2 == 0 && C % T2 == 0) {
-    if (R == 0 || C == 0) return 0;
-    transpose2_kernel<<<dim3(C / T2, R / T2), 256, 0, s>>>(src, ld, dst, R, C);
-    return 0;
-  }
+int launch_transpose(const uint16_t* src, long ld, uint16_t* dst, int R, int C, hipStream_t s) {
   if (R % TR || C % TC) return -1;
   if (R == 0 || C == 0) return 0;
   transpose_kernel<<<dim3(R / TR, C / TC), 256, 0, s>>>(src, ld, dst, R, C);

@@ -437,8 +437,8 @@ __device__ __forceinline__ void rope4(const uint16_t* __restrict__ src, uint16_t
 }
 
 // qkv [T, (H + 2*Hkv) * Dh]  ->  q_out [T, H, Dh] (rotated), k -> k_cache (rotated), v -> v_cache
-// k_cache: [num_blocks, Hkv, BS, Dh]   v_cache: [num_blocks, Hkv, Dh, BS]  (V stored transposed
-// per page so the P.V MFMA B-operand is contiguous along keys)
+// k_cache: [num_blocks, Hkv, BS, Dh]   v_cache: [num_blocks, Hkv, BS / 8, Dh, 8]  (V chunk-major per page,
+// common.h v_page_off, so the P.V MFMA operand is contiguous along keys)
 __global__ __launch_bounds__(256) void rope_kv_write_kernel(const uint16_t* __restrict__ qkv,
                                                             const int32_t* __restrict__ pos,
                                                             const float* __restrict__ cos_sin,
@@ -471,7 +471,7 @@ __global__ __launch_bounds__(256) void rope_kv_write_kernel(const uint16_t* __re
   const uint16_t* vsrc = row + (H + Hkv) * Dh;
   for (int w = threadIdx.x; w < nv; w += 256) {
     const int kh = w / Dh, d = w % Dh;
-    vc[(((size_t)blk * Hkv + kh) * Dh + d) * BS + off] = vsrc[w];
+    vc[((size_t)blk * Hkv + kh) * Dh * BS + v_page_off(off, d, Dh)] = vsrc[w];
   }
 }
 
@@ -553,9 +553,9 @@ __global__ __launch_bounds__(256) void splitk_rope_kv_write_kernel(
   if (slot < 0 || max_pos < 0) return;  // (max_pos < 0: timing experiment without the V write, XOT_EXP_NO_V)
   const int e = 4 * (w - nrot), kh = e / Dh, d = e % Dh;
   const f32x4 v = slab_sum4<SS>(row, S, sstride, bias, (H + Hkv) * Dh + e);
-  uint16_t* dst = vc + (((size_t)blk * Hkv + kh) * Dh + d) * BS + off;
+  uint16_t* dst = vc + ((size_t)blk * Hkv + kh) * Dh * BS + v_page_off(off, d, Dh);
 #pragma unroll
-  for (int j = 0; j < 4; ++j) dst[(size_t)j * BS] = f2bf(v[j]);
+  for (int j = 0; j < 4; ++j) dst[8 * j] = f2bf(v[j]);  // dims d .. d+3: 16 B apart in one 64-B span
 }
 
 void launch_splitk_rope_kv_write(const float* ws, int S, const uint16_t* bias, const int32_t* pos,
@@ -583,17 +583,17 @@ void launch_splitk_rope_kv_write(const float* ws, int S, const uint16_t* bias, c
 #undef XOT_SRK
 }
 
-// V of prefill-sized T: the per-token kernel above writes a token's V as Hkv * Dh scattered 2-byte stores (V is
-// stored transposed, 128 B between a token's consecutive dims), one partial cache line per element.  Here a
-// workgroup takes 64 consecutive tokens of one KV head: the [64][Dh] block goes through LDS and leaves as rows of
-// up to 64 consecutive keys of the transposed page (one 128-B line per dim when the tokens share a page, as a
-// prefill chunk's do).  The rotations stay on the per-token kernel (skip_v).
+// V of prefill-sized T: the per-token kernel above writes a token's V as Hkv * Dh scattered 2-byte stores.  Here a
+// workgroup takes 64 consecutive tokens of one KV head through LDS: each group of 8 tokens whose slots are one
+// aligned 8-key chunk of a page (every group of a prefill chunk that starts on a page boundary) leaves as Dh
+// 16-B stores of [8 keys] runs, a wave's 64 dims 1 KB contiguous; other groups fall back to per-token stores.
 constexpr int RKV_TOK = 64;
 __global__ __launch_bounds__(256) void v_write_tiled_kernel(const uint16_t* __restrict__ qkv,
                                                             const int64_t* __restrict__ slots,
                                                             uint16_t* __restrict__ vc, int T, int H, int Hkv, int Dh,
                                                             int BS, long nslots) {
-  extern __shared__ uint16_t vt[];  // [RKV_TOK][Dh + 2] (odd dword stride: the transposed reads hit 64 banks)
+  extern __shared__ uint16_t vt[];  // [RKV_TOK][Dh + 2]
+  __shared__ long cslot[RKV_TOK / 8];  // first slot of each 8-token group when it is one aligned chunk, else -1
   const int t0 = blockIdx.x * RKV_TOK, nt = min(RKV_TOK, T - t0), kh = blockIdx.y;
   const int rowlen = (H + 2 * Hkv) * Dh, VLD = Dh + 2, cpr = Dh / 8;
   for (int w = threadIdx.x; w < nt * cpr; w += 256) {
@@ -602,11 +602,31 @@ __global__ __launch_bounds__(256) void v_write_tiled_kernel(const uint16_t* __re
 #pragma unroll
     for (int j = 0; j < 8; ++j) vt[tt * VLD + cc * 8 + j] = (uint16_t)v[j];
   }
+  if (threadIdx.x < RKV_TOK / 8) {
+    const int tt0 = threadIdx.x * 8;
+    long s0 = tt0 + 8 <= nt ? (long)slots[t0 + tt0] : -1;
+    if (s0 < 0 || s0 % 8 != 0 || s0 + 8 > nslots) s0 = -1;
+    for (int i = 1; i < 8 && s0 >= 0; ++i)
+      if ((long)slots[t0 + tt0 + i] != s0 + i) s0 = -1;
+    cslot[threadIdx.x] = s0;
+  }
   __syncthreads();
-  for (int w = threadIdx.x; w < nt * Dh; w += 256) {
-    const int d = w / nt, tt = w % nt, t = t0 + tt;
-    const int64_t slot = slots[t] < nslots ? slots[t] : -1;
-    if (slot >= 0) vc[(((size_t)(slot / BS) * Hkv + kh) * Dh + d) * BS + slot % BS] = vt[tt * VLD + d];
+  const size_t head = (size_t)kh * Dh * BS;
+  for (int w = threadIdx.x; w < ((nt + 7) / 8) * Dh; w += 256) {
+    const int cg = w / Dh, d = w % Dh, tt0 = cg * 8;
+    const long s0 = cslot[cg];
+    if (s0 >= 0) {
+      s16x8 v;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = (short)vt[(tt0 + i) * VLD + d];
+      st16(vc + (size_t)(s0 / BS) * Hkv * Dh * BS + head + v_page_off((int)(s0 % BS), d, Dh), v);
+    } else {
+      for (int i = 0; i < 8 && tt0 + i < nt; ++i) {
+        const int64_t slot = slots[t0 + tt0 + i] < nslots ? slots[t0 + tt0 + i] : -1;
+        if (slot >= 0)
+          vc[(size_t)(slot / BS) * Hkv * Dh * BS + head + v_page_off((int)(slot % BS), d, Dh)] = vt[(tt0 + i) * VLD + d];
+      }
+    }
   }
 }
 

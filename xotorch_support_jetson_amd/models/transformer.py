@@ -85,7 +85,8 @@ class StepInputs:
 
 
 class KVCache:
-  """Per-shard paged KV pool: K [L, pages, Hkv, 64, Dh] and V [L, pages, Hkv, Dh, 64] (V page-transposed).
+  """Per-shard paged KV pool: K [L, pages, Hkv, 64, Dh] and V [L, pages, Hkv, Dh, 64] (V storage: each page chunk-major,
+  [8 chunks][Dh][8 keys], ops/reference.py v_chunks).
   MLA models (DeepSeek) keep one latent row per token instead: k = C [L, pages, 64, kv_lora + rope], v None."""
 
   def __init__(self, c: ModelConfig, n_layers: int, num_pages: int, device, dtype=torch.bfloat16):

@@ -2,7 +2,8 @@
 
 These are (1) the numerical oracles the HIP kernels are tested against and (2) the compute path on
 CPU-only hosts (BASELINE config 1: Llama-3.2-1B on the CPU engine).  Semantics match the kernels
-exactly, including the paged KV layout (K [pages, Hkv, 64, Dh], V [pages, Hkv, Dh, 64]).
+exactly, including the paged KV layout (K [pages, Hkv, 64, Dh], V [pages, Hkv, Dh, 64] storage holding each page
+chunk-major, see v_chunks).
 """
 from __future__ import annotations
 
@@ -81,6 +82,13 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None) -
   return y
 
 
+def v_chunks(v_cache: torch.Tensor) -> torch.Tensor:
+  """The V pool [pages, Hkv, Dh, BS] (storage shape) as the layout the kernels use: each page of a KV head
+  chunk-major, [BS / 8 chunks][Dh][8 keys] (csrc/common.h v_page_off)."""
+  nb, Hkv, Dh, BS = v_cache.shape
+  return v_cache.view(nb, Hkv, BS // 8, Dh, 8)
+
+
 def write_kv(k: torch.Tensor, v: torch.Tensor, slots: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor):
   """k, v [T, Hkv, Dh] -> paged caches at global slots (slot < 0 skipped)."""
   BS = k_cache.shape[2]
@@ -88,7 +96,7 @@ def write_kv(k: torch.Tensor, v: torch.Tensor, slots: torch.Tensor, k_cache: tor
   s = slots[ok].long()
   blk, off = s // BS, s % BS
   k_cache[blk, :, off, :] = k[ok].to(k_cache.dtype)
-  v_cache[blk, :, :, off] = v[ok].to(v_cache.dtype)
+  v_chunks(v_cache)[blk, :, off // 8, :, off % 8] = v[ok].to(v_cache.dtype)
 
 
 def gather_kv(k_cache, v_cache, table, n):
@@ -97,7 +105,7 @@ def gather_kv(k_cache, v_cache, table, n):
   npg = (n + BS - 1) // BS
   pages = table[:npg].long()
   k = k_cache[pages].permute(0, 2, 1, 3).reshape(npg * BS, k_cache.shape[1], k_cache.shape[3])[:n]
-  v = v_cache[pages].permute(0, 3, 1, 2).reshape(npg * BS, v_cache.shape[1], v_cache.shape[2])[:n]
+  v = v_chunks(v_cache)[pages].permute(0, 2, 4, 1, 3).reshape(npg * BS, v_cache.shape[1], v_cache.shape[2])[:n]
   return k, v
 
 

@@ -117,24 +117,20 @@ class PipelineTrainer:
       for i, b in enumerate(batches):
         self._bwd(b, saved.pop(i), denom, losses)
     self.t.drain()
+    grads = None
     if self.tied_group is not None and self.tied_name is not None:
-      # the local gradient of this stage's copy: on the GPU it sits in a GradAcc buffer (fp32 embedding
-      # index-add, fused-CE dHead), which tr.grads() prefers over p.grad -- sum THAT over the two ends and
-      # write it back where the optimizer reads it, so both copies take the same update
+      # the local gradient of this stage's copy: on the GPU it may sit in a GradAcc buffer (fp32 embedding
+      # index-add, fused-CE dHead), which tr.grads() prefers over p.grad -- sum THAT over the two ends in fp32
+      # and hand the sum to the optimizer as it is (no bf16 rounding on one end only), so both copies take
+      # bit-identical updates
       name = self.tied_name
-      p = tr.params[name]
-      g = tr.grads().get(name)
-      g = torch.zeros_like(p, dtype=torch.float32) if g is None else g.float()
+      grads = tr.grads()
+      g = grads.get(name)
+      g = torch.zeros_like(tr.params[name], dtype=torch.float32) if g is None else g.float()
       dist.all_reduce(g, group=self.tied_group)
-      acc = tr.acc.get(name)
-      if acc is not None:
-        acc.buf.copy_(g)
-        acc.fresh = False
-        p.grad = None
-      else:
-        p.grad = g.to(p.dtype)
+      grads[name] = g
     tied_copy = ("lm_head",) if (self.tied_group is not None and self.last) else ()
-    tr.apply(self._reduce_sq, norm_exclude=tied_copy)
+    tr.apply(self._reduce_sq, norm_exclude=tied_copy, grads=grads)
     loss = float(torch.stack(losses).sum()) if losses else None
     if self.world > 1:
       lt = torch.tensor([loss if loss is not None else 0.0], dtype=torch.float32, device=self.dev)
