@@ -973,6 +973,52 @@ def test_relayout_kernels(gpu, R, C):
     assert torch.equal(out, want), mode
 
 
+@pytest.mark.parametrize("T,M,N", [(64, 256, 256), (192, 512, 768), (4096, 256, 512)])
+@pytest.mark.parametrize("resid", [False, True])
+def test_gemm_tn(gpu, T, M, N, resid):
+  """csrc/gemm_big.hip TN (the weight-gradient GEMM on token-major operands, fragments read transposed out of LDS):
+  y (+)= dy^T . x from a row-strided dy, against fp32 torch."""
+  from xotorch_support_jetson_amd.ops._ext import require
+  torch.manual_seed(T + M)
+  dy = (torch.randn(T, M + 64, device=gpu) * 0.5).to(torch.bfloat16)[:, :M]
+  x = torch.randn(T, N, device=gpu).to(torch.bfloat16)
+  y0 = (torch.randn(M, N, device=gpu) * 4).to(torch.bfloat16)
+  y = y0.clone()
+  require().gemm_tn(dy, x, y, resid)
+  want = dy.float().t() @ x.float() + (y0.float() if resid else 0.0)
+  err = ((y.float() - want).norm() / want.norm()).item()
+  assert err < 5e-3, err
+  if not resid:  # fp32 output
+    y32 = torch.empty(M, N, device=gpu)
+    require().gemm_tn(dy, x, y32, False)
+    assert ((y32 - dy.float().t() @ x.float()).norm() / want.norm()).item() < 1e-4
+
+
+def test_gemm_tn_exact_layout(gpu):
+  """Integer operands (exact in bf16 and fp32): every element of dy^T . x bit-exact, so a wrong swizzle, fragment
+  order or tile mapping cannot hide in the tolerance."""
+  from xotorch_support_jetson_amd.ops._ext import require
+  g = torch.Generator(device=gpu).manual_seed(1)
+  T, M, N = 128, 512, 768
+  dy = torch.randint(-1, 2, (T, M), device=gpu, generator=g).to(torch.bfloat16)
+  x = torch.randint(-1, 2, (T, N), device=gpu, generator=g).to(torch.bfloat16)
+  y = torch.full((M, N), 3.0, device=gpu, dtype=torch.bfloat16)
+  require().gemm_tn(dy, x, y, True)
+  assert torch.equal(y.float(), dy.float().t() @ x.float() + 3.0)
+
+
+def test_dw_tn_ragged_tokens(gpu):
+  """train/autograd_ops.dw_tn pads a ragged token count (37) with zero rows; the result equals the fp32 product."""
+  from xotorch_support_jetson_amd.train.autograd_ops import dw_tn
+  torch.manual_seed(0)
+  dy = torch.randn(37, 256, device=gpu).to(torch.bfloat16)
+  x = torch.randn(37, 512, device=gpu).to(torch.bfloat16)
+  out = torch.empty(256, 512, device=gpu, dtype=torch.bfloat16)
+  assert dw_tn(dy, x, out, False)
+  want = dy.float().t() @ x.float()
+  assert ((out.float() - want).norm() / want.norm()).item() < 5e-3
+
+
 @pytest.mark.parametrize("with_h", [False, True])
 @pytest.mark.parametrize("T,Kd,N", [(256, 384, 512), (192, 512, 768)])
 def test_own_linear_grads_match_torch(gpu, with_h, T, Kd, N):

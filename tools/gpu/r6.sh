@@ -21,6 +21,10 @@ for what in "$@"; do
             step r6/ring70 1100 python -u tools/bench_serve.py --ring 1 --model llama-3-70b --concurrency 512 --max-tokens 128 --prompt-words 124 --server-log "$O/r6/ring70_server.log" ;;
     train)  step r6/train 900 python -u tools/bench_train.py --model llama-3-8b --seq 2048 --mb 2 --microbatches 4 --steps 3 --warmup 1 ;;
     train_norelayout) XOT_EXP_NO_RELAYOUT=1 step r6/train_norelayout 900 python -u tools/bench_train.py --model llama-3-8b --seq 2048 --mb 2 --microbatches 4 --steps 3 --warmup 1 ;;
+    tn_test) step r6/tn_test 300 python -u -m pytest tests/test_kernels_gpu.py tests/test_train_own_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread -k "tn or train or silu_down or relayout" ;;
+    train_relayout) XOT_DW_TN=0 step r6/train_relayout 900 python -u tools/bench_train.py --model llama-3-8b --seq 2048 --mb 2 --microbatches 4 --steps 3 --warmup 1 ;;
+    dw) step r6/dw 300 python -u tools/bench_dw.py ;;
+    train_inline) XOT_DW_STREAM=0 step r6/train_inline 900 python -u tools/bench_train.py --model llama-3-8b --seq 2048 --mb 2 --microbatches 4 --steps 3 --warmup 1 ;;
     train_norope) XOT_EXP_NO_ROPE=1 step r6/train_norope 900 python -u tools/bench_train.py --model llama-3-8b --seq 2048 --mb 2 --microbatches 4 --steps 3 --warmup 1 ;;
     train_tprof) step r6/train_tprof 900 python -u tools/bench_train.py --model llama-3-8b --seq 2048 --mb 2 --microbatches 4 --steps 2 --warmup 1 --torch-prof "$O/r6/train_torch_ops.txt" ;;
     trainprof) prof r6/trainprof 900 python3 "$R/tools/bench_train.py" --mb 2 --microbatches 4 --steps 3 --warmup 1

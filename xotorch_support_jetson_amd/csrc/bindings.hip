@@ -379,6 +379,28 @@ void relayout(const at::Tensor& src, at::Tensor& dst, int64_t mode) {
   XCHECK(rc == 0, "relayout: unsupported shape R=", R, " C=", C, " mode=", mode);
 }
 
+// Weight-gradient GEMM on token-major operands: y [M, N] = dy^T . x (resid: y += dy^T . x, in place), dy [T, M]
+// and x [T, N] bf16 with unit column stride (rows may be strided), y bf16 (or fp32 without resid) contiguous.
+// M, N multiples of 256, T of 64 (the caller pads ragged token counts with zero rows).
+void gemm_tn(const at::Tensor& dy, const at::Tensor& x, at::Tensor& y, bool resid) {
+  CHECK_BF16(dy);
+  CHECK_BF16(x);
+  CHECK_GPU(y);
+  XCHECK(dy.dim() == 2 && x.dim() == 2 && y.dim() == 2, "gemm_tn: 2-D operands");
+  XCHECK(dy.stride(1) == 1 && x.stride(1) == 1 && dy.stride(0) % 8 == 0 && x.stride(0) % 8 == 0,
+         "gemm_tn: dy / x need unit column stride and 16-B rows");
+  const int64_t T = dy.size(0), M = dy.size(1), N = x.size(1);
+  XCHECK(x.size(0) == T && y.size(0) == M && y.size(1) == N && y.is_contiguous(), "gemm_tn: shapes");
+  const bool f32 = y.scalar_type() == at::kFloat;
+  XCHECK(f32 || y.scalar_type() == at::kBFloat16, "gemm_tn: y must be bf16 or fp32");
+  XCHECK(!(resid && f32), "gemm_tn: the residual epilogue writes bf16");
+  XCHECK(T * std::max(dy.stride(0), x.stride(0)) < (int64_t(1) << 31), "gemm_tn: operands too large");
+  const int rc = xot::launch_gemm_tn(bf(dy), (int)dy.stride(0), bf(x), (int)x.stride(0),
+                                     resid ? reinterpret_cast<const uint16_t*>(y.data_ptr()) : nullptr, (int)N,
+                                     y.data_ptr(), (int)N, f32, resid ? 1 : 0, (int)M, (int)N, (int)T, cur_stream());
+  XCHECK(rc == 0, "gemm_tn: unsupported shape M=", M, " N=", N, " T=", T);
+}
+
 // K-grouped GEMM (grouped experts' weight gradients): y[e] (+)= x[:, koff[e]:koff[e+1]] . w[:, koff[e]:koff[e+1]]^T,
 // x [M, K] row-major bf16, w [N, K] pre-shuffled, y [E, M, N] bf16 contiguous, koff [E+1] int32 (multiples of 64)
 void gemm_kgroup(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const at::Tensor& koff, bool resid) {
@@ -910,6 +932,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("res"), py::arg("ws"), py::arg("epi"), py::arg("ntw"), py::arg("splits"), py::arg("reduce") = true);
   m.def("relayout", &relayout, py::arg("src"), py::arg("dst"), py::arg("mode"));
   m.def("gemm_kgroup", &gemm_kgroup);
+  m.def("gemm_tn", &gemm_tn, py::arg("dy"), py::arg("x"), py::arg("y"), py::arg("resid"));
   m.def("gemm_batched", &gemm_batched, py::arg("x"), py::arg("xbat"), py::arg("K"), py::arg("w"), py::arg("y"),
         py::arg("ybat"), py::arg("ldy"), py::arg("M"));
   m.def("gemm_big", &gemm_big, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("bias"), py::arg("res"),

@@ -51,6 +51,9 @@ int launch_gemm_big(const uint16_t* X, int ldx, const uint16_t* W, const uint16_
 int launch_shuffle(const uint16_t* src, long ld, uint16_t* dst, int R, int C, hipStream_t s);
 int launch_shuffle_t(const uint16_t* src, long ld, uint16_t* dst, int R, int C, hipStream_t s);
 int launch_transpose(const uint16_t* src, long ld, uint16_t* dst, int R, int C, hipStream_t s);
+// weight-gradient GEMM on token-major operands (gemm_big.hip TN): Y [M, N] (+)= Xt^T . Wt, Xt [K, M], Wt [K, N]
+int launch_gemm_tn(const uint16_t* Xt, int ldx, const uint16_t* Wt, int ldw, const uint16_t* R, int ldr, void* Y,
+                   int ldy, bool out_f32, int epi, int M, int N, int K, hipStream_t st);
 int launch_gemm_kgroup(const uint16_t* X, int ldx, const uint16_t* W, uint16_t* Y, int ldy, bool resid,
                        const int* koff, int E, int M, int N, int K, hipStream_t st);
 int launch_gemm_batched(const uint16_t* X, int ldx, long xbat, const uint16_t* W, void* Y, int ldy, long ybat,

@@ -453,18 +453,45 @@ def join_dw_stream() -> None:
 def own_dw(dy: torch.Tensor, x: torch.Tensor, acc: "GradAcc", cb: bool = True) -> None:
   """acc.buf (+)= dY^T X on the own tiles (on the side stream when DW_STREAM), then acc.cb (if `cb`)."""
   if not (DW_STREAM and dy.is_cuda):
-    _own_dw(dy, x, acc)
+    _dw(dy, x, acc)
     if cb and acc.cb is not None:
       acc.cb()
     return
   side = _dw_stream(dy.device)
   side.wait_stream(torch.cuda.current_stream(dy.device))  # dy and x are ready
   with torch.cuda.stream(side):
-    _own_dw(dy, x, acc)
+    _dw(dy, x, acc)
   dy.record_stream(side)  # allocated on the main stream, read by the side stream: no reuse before it ran
   x.record_stream(side)
   if cb and acc.cb is not None:
     acc.cb()  # on the main stream: a callback that reads acc.buf joins the side stream first
+
+
+# Weight gradients straight from the token-major dY and X (csrc/gemm_big.hip TN: both operands staged as [64 tokens]
+# row tiles, MFMA fragments read transposed out of LDS), no dY^T / shuffle(X^T) images in HBM: the relayouts cost
+# 66 ms of a 705 ms Llama-3-8B step (profiles/r6/train/relayout_cost/).  XOT_DW_TN=0: relayouts + pre-shuffled tile.
+DW_TN = os.environ.get("XOT_DW_TN", "0") == "1"
+
+
+def dw_tn(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor, accumulate: bool) -> bool:
+  """out (+)= dY^T X on the TN tile when the shapes allow it (dY [T, M], X [T, N], M and N multiples of 256; T is
+  zero-padded to 64).  False: not taken (the caller builds the relayout images)."""
+  if not (DW_TN and dy.is_cuda and dy.shape[1] % 256 == 0 and x.shape[1] % 256 == 0):
+    return False
+  dy, x = pad_rows(dy, 64), pad_rows(x, 64)
+  if dy.stride(1) != 1 or dy.stride(0) % 8:
+    dy = dy.contiguous()
+  if x.stride(1) != 1 or x.stride(0) % 8:
+    x = x.contiguous()
+  require().gemm_tn(dy, x, out, accumulate)
+  return True
+
+
+def _dw(dy: torch.Tensor, x: torch.Tensor, acc: "GradAcc") -> None:
+  if dw_tn(dy, x, acc.buf, not acc.fresh):
+    acc.fresh = False
+  else:
+    _dw_gemm(*_dw_operands(dy, x), acc)
 
 
 # timing experiments only (wrong gradients): XOT_EXP_NO_RELAYOUT=1 skips the dW operand relayouts (the dW GEMMs read
@@ -473,18 +500,21 @@ EXP_NO_RELAYOUT = os.environ.get("XOT_EXP_NO_RELAYOUT", "0") == "1"
 EXP_NO_ROPE = os.environ.get("XOT_EXP_NO_ROPE", "0") == "1"
 
 
-def _own_dw(dy: torch.Tensor, x: torch.Tensor, acc: "GradAcc") -> None:
-  """acc.buf (+)= dY^T X on the own tiles: dY^T [N, T] row-major and shuffle(X^T) [K, T] need T % 128, so ragged
-  token counts (the reference's batch-size-1 JSONL lengths) are zero-padded to 128 rows first."""
-  from ..ops.linear import linear
+def _dw_operands(dy: torch.Tensor, x: torch.Tensor):
+  """dY^T [N, T] row-major and shuffle(X^T) [K, T] for the dW GEMM; they need T % 128, so ragged token counts (the
+  reference's batch-size-1 JSONL lengths) are zero-padded to 128 rows first."""
   dy, x = pad_rows(dy), pad_rows(x)
   if EXP_NO_RELAYOUT:
     dyt = torch.empty(dy.shape[1], dy.shape[0], dtype=torch.bfloat16, device=dy.device)
     xts = torch.empty(x.shape[1], x.shape[0], dtype=torch.bfloat16, device=x.device)
     xts.xot_layout = "stream"
-  else:
-    dyt = relayout(dy, 2)  # [N, T]
-    xts = relayout(x, 1)   # shuffle(X^T) [K, T]
+    return dyt, xts
+  return relayout(dy, 2), relayout(x, 1)
+
+
+def _dw_gemm(dyt: torch.Tensor, xts: torch.Tensor, acc: "GradAcc") -> None:
+  """acc.buf (+)= dyt . xts^T on the own tiles (plain store on the step's first micro-batch, then accumulate)."""
+  from ..ops.linear import linear
   if acc.fresh:
     linear(dyt, xts, out=acc.buf)
     acc.fresh = False
@@ -723,6 +753,8 @@ class LmHeadCEFn(torch.autograd.Function):
       linear(dl, tw.wts, out=dxn[r0:r1])
       if acc is not None:
         own_dw(dl, xc, acc, cb=False)
+        continue
+      if dw_tn(dl, xc, dhead, i > 0):
         continue
       dlt, xts = relayout(dl, 2), relayout(xc, 1)  # dlogits^T [V, c], shuffle(X_c^T) [D, c]
       if i == 0:
