@@ -976,7 +976,7 @@ def test_relayout_kernels(gpu, R, C):
 @pytest.mark.parametrize("T,M,N", [(64, 256, 256), (192, 512, 768), (4096, 256, 512)])
 @pytest.mark.parametrize("resid", [False, True])
 def test_gemm_tn(gpu, T, M, N, resid):
-  """csrc/gemm_big.hip TN (the weight-gradient GEMM on token-major operands, fragments read transposed out of LDS):
+  """csrc/gemm_w4.hip TN (the weight-gradient GEMM on token-major operands, fragments read transposed out of LDS):
   y (+)= dy^T . x from a row-strided dy, against fp32 torch."""
   from xotorch_support_jetson_amd.ops._ext import require
   torch.manual_seed(T + M)
@@ -1007,9 +1007,11 @@ def test_gemm_tn_exact_layout(gpu):
   assert torch.equal(y.float(), dy.float().t() @ x.float() + 3.0)
 
 
-def test_dw_tn_ragged_tokens(gpu):
+def test_dw_tn_ragged_tokens(gpu, monkeypatch):
   """train/autograd_ops.dw_tn pads a ragged token count (37) with zero rows; the result equals the fp32 product."""
+  from xotorch_support_jetson_amd.train import autograd_ops as A
   from xotorch_support_jetson_amd.train.autograd_ops import dw_tn
+  monkeypatch.setattr(A, "DW_TN", True)
   torch.manual_seed(0)
   dy = torch.randn(37, 256, device=gpu).to(torch.bfloat16)
   x = torch.randn(37, 512, device=gpu).to(torch.bfloat16)

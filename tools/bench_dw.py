@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Weight-gradient GEMM dW = dY^T . X of one Llama-3-8B micro-batch (T = 4096 tokens) per projection, in isolation:
 the relayout path (dY^T + shuffle(X^T) by csrc/layout.hip, then the pre-shuffled tile the tuner picks) against the
-TN tile (csrc/gemm_big.hip TN: token-major operands, transposed LDS reads).  Medians of --reps calls, us.
+TN tile (csrc/gemm_w4.hip TN: token-major operands, transposed LDS reads).  Medians of --reps calls, us.
 
   python tools/bench_dw.py [--T 4096] [--reps 20]
 """
@@ -53,7 +53,6 @@ def main():
     r["relayout_us"] = timed(lambda: (relayout(dy, 2, dyt), relayout(x, 1, xts)), a.reps)
     r["gemm_shuffled_us"] = timed(lambda: linear(dyt, xts, residual=acc, epi="resid", out=acc), a.reps)
     r["tn_us"] = timed(lambda: C.gemm_tn(dy, x, acc, True), a.reps)
-    r["pp2256_us"] = timed(lambda: C.gemm_big(dyt, xts, acc, None, acc, None, 1, 2256, 1), a.reps)
     fl = 2.0 * M * N * T
     r["tn_TFs"] = round(fl / r["tn_us"] / 1e6, 1)
     r["shuffled_TFs"] = round(fl / r["gemm_shuffled_us"] / 1e6, 1)

@@ -22,6 +22,8 @@ for what in "$@"; do
     train)  step r6/train 900 python -u tools/bench_train.py --model llama-3-8b --seq 2048 --mb 2 --microbatches 4 --steps 3 --warmup 1 ;;
     train_norelayout) XOT_EXP_NO_RELAYOUT=1 step r6/train_norelayout 900 python -u tools/bench_train.py --model llama-3-8b --seq 2048 --mb 2 --microbatches 4 --steps 3 --warmup 1 ;;
     tn_test) step r6/tn_test 300 python -u -m pytest tests/test_kernels_gpu.py tests/test_train_own_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread -k "tn or train or silu_down or relayout" ;;
+    tn_test_on) XOT_DW_TN=1 step r6/tn_test_on 300 python -u -m pytest tests/test_train_own_gpu.py tests/test_pipeline_train.py -m gpu -x -q --timeout 120 --timeout-method thread ;;
+    train_tn) XOT_DW_TN=1 step r6/train_tn 900 python -u tools/bench_train.py --model llama-3-8b --seq 2048 --mb 2 --microbatches 4 --steps 3 --warmup 1 ;;
     train_relayout) XOT_DW_TN=0 step r6/train_relayout 900 python -u tools/bench_train.py --model llama-3-8b --seq 2048 --mb 2 --microbatches 4 --steps 3 --warmup 1 ;;
     dw) step r6/dw 300 python -u tools/bench_dw.py ;;
     train_inline) XOT_DW_STREAM=0 step r6/train_inline 900 python -u tools/bench_train.py --model llama-3-8b --seq 2048 --mb 2 --microbatches 4 --steps 3 --warmup 1 ;;

@@ -382,6 +382,7 @@ void relayout(const at::Tensor& src, at::Tensor& dst, int64_t mode) {
 // Weight-gradient GEMM on token-major operands: y [M, N] = dy^T . x (resid: y += dy^T . x, in place), dy [T, M]
 // and x [T, N] bf16 with unit column stride (rows may be strided), y bf16 (or fp32 without resid) contiguous.
 // M, N multiples of 256, T of 64 (the caller pads ragged token counts with zero rows).
+// On the four-wave tile (gemm_w4.hip TN: both operands staged as [64 tokens] row tiles, fragments read transposed).
 void gemm_tn(const at::Tensor& dy, const at::Tensor& x, at::Tensor& y, bool resid) {
   CHECK_BF16(dy);
   CHECK_BF16(x);
@@ -395,9 +396,10 @@ void gemm_tn(const at::Tensor& dy, const at::Tensor& x, at::Tensor& y, bool resi
   XCHECK(f32 || y.scalar_type() == at::kBFloat16, "gemm_tn: y must be bf16 or fp32");
   XCHECK(!(resid && f32), "gemm_tn: the residual epilogue writes bf16");
   XCHECK(T * std::max(dy.stride(0), x.stride(0)) < (int64_t(1) << 31), "gemm_tn: operands too large");
-  const int rc = xot::launch_gemm_tn(bf(dy), (int)dy.stride(0), bf(x), (int)x.stride(0),
-                                     resid ? reinterpret_cast<const uint16_t*>(y.data_ptr()) : nullptr, (int)N,
-                                     y.data_ptr(), (int)N, f32, resid ? 1 : 0, (int)M, (int)N, (int)T, cur_stream());
+  const uint16_t* r = resid ? reinterpret_cast<const uint16_t*>(y.data_ptr()) : nullptr;
+  const int rc = xot::launch_gemm_w4_tn(bf(dy), (int)dy.stride(0), bf(x), (int)x.stride(0), r, (int)N, y.data_ptr(),
+                                        (int)N, f32, resid ? 1 : 0, (int)M, (int)N, (int)T, xot::gemm_big_group_m(),
+                                        cur_stream());
   XCHECK(rc == 0, "gemm_tn: unsupported shape M=", M, " N=", N, " T=", T);
 }
 

@@ -45,16 +45,8 @@ namespace xot {
 // (Schedules measured slower and removed: an 8-phase per-half refill and a three-deep weight pipeline,
 // profiles/r3/lab_gemm_schedules_random.log, profiles/r3/lab_s2/w_three_deep_staging.log; 512 x 128 tiles,
 // profiles/r4/lab3.)
-// TN: both operands token-major, as the weight-gradient GEMM dW = dY^T . X finds them -- X holds the logical
-// [M, K] operand TRANSPOSED (row k = tokens, ldx elements apart, M contiguous: dY [T, M]) and W the logical [N, K]
-// one the same way (row k, ldw apart: X [T, N]), so no dY^T / shuffle(X^T) images are built in HBM.  Each 64-deep
-// stage arrives by LDS-DMA as row-major [64 k][cols] images -- X as two [64][128] halves (each half's waves
-// refill only the rows they read: the ping-pong's other half is still reading its own), W as one [64][256] --
-// with the 16-B granules XOR-swizzled by tn_swz(k row) through the source address, and the MFMA fragments (8
-// consecutive k of one row / column) are read transposed out of them with pairs of ds_read_b64_tr_b16.
-// Two-phase ping-pong schedule only.
 template <int BM, int BN, int WM, int WN, int BK, int NBUF, int EPI, bool OUT_F32, bool SPLIT, int MOE = 0, int AUXA = 0,
-          int AUXB = 3, int PP = 0, bool TN = false>
+          int AUXB = 3, int PP = 0>
 __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __restrict__ X, int ldx,
                                                           const uint16_t* __restrict__ W,
                                                           const uint16_t* __restrict__ bias,
@@ -63,10 +55,8 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
                                                           int M, int N, int K, int S,
                                                           const int* __restrict__ moe_off = nullptr,
                                                           const int* __restrict__ moe_gather = nullptr,
-                                                          long ysplit = 0, int group_m = 4, int ldw = 0) {
+                                                          long ysplit = 0, int group_m = 4) {
   static_assert(WM * WN == 8, "8 waves");
-  static_assert(!TN || (PP == 2 && MOE == 0 && BM == 256 && BN == 256 && BK == 64 && NBUF == 2),
-                "TN: the 256 x 256 two-phase ping-pong tile");
   static_assert(BK == 32 || BK == 64, "k stage of 32 or 64");
   static_assert(BM % (16 * WM) == 0 && BM >= 128 && BM <= 512, "row tile of 128 .. 512 rows");
   static_assert(PP == 0 || PP == 1 || PP == 2, "schedules: base (0), ping-pong in 4 phases (1) or 2 phases (2)");
@@ -163,18 +153,8 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
   // physical slot lane%SPR holding logical slot (lane%SPR) ^ aswz(row).
   const uint16_t* asrc[A_INSTR];
   auto aq = [&](int i) { return A_UNEVEN ? 8 * i + wave : A_INSTR * wave + i; };
-  // TN, X: instruction q < 16 copies k rows 4q .. 4q + 3 of row half 0 (columns m0 .. m0 + 127, 256 B per k row),
-  // q >= 16 the same of half 1 -- the waves of row half h (4 h .. 4 h + 3) issue exactly their half's 16; lane l ->
-  // k row 4 (q % 16) + l / 16, physical granule l % 16 holding logical granule (l % 16) ^ tn_swz(k row).
-  // W: instruction q copies k rows 2q, 2q + 1 (512 B each); lane l -> k row 2q + l / 32, granule l % 32 likewise.
-  auto tn_swz = [](int krow) -> int { return 2 * ((krow & 3) | (((krow >> 3) & 1) << 2)); };
 #pragma unroll
   for (int i = 0; i < A_INSTR; ++i) {
-    if constexpr (TN) {
-      const int q = aq(i), kr = 4 * (q & 15) + (lane >> 4);
-      asrc[i] = X + (size_t)kr * ldx + m0 + 128 * (q >> 4) + (((lane & 15) ^ tn_swz(kr)) * 8);
-      continue;
-    }
     const int row = (64 / SPR) * min(aq(i), NAI - 1) + lane / SPR;
     const int slot = (lane % SPR) ^ aswz(row);
     int grow = min(m0 + row, Mv - 1);  // rows past the end load valid memory; their outputs are masked
@@ -188,11 +168,6 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
   auto bq = [&](int i) { return B_UNEVEN ? 8 * i + wave : B_INSTR * wave + i; };
 #pragma unroll
   for (int i = 0; i < B_INSTR; ++i) {
-    if constexpr (TN) {
-      const int kr = 2 * bq(i) + (lane >> 5);
-      bsrc[i] = W + (size_t)kr * ldw + n0 + (((lane & 31) ^ tn_swz(kr)) * 8);
-      continue;
-    }
     const int q = min(bq(i), NBI - 1);
     const int grp = min((n0 >> 4) + q / KS, N / 16 - 1);  // groups past N re-read the last one; outputs masked
     bsrc[i] = W + ((size_t)grp * kchunks) * 2048 + (q % KS) * 512 + lane * 8;
@@ -206,13 +181,12 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
     uint16_t* Bs = As + A_ELEMS;
     const int k0 = t * BK;
     const size_t woff = (size_t)(k0 >> 7) * 2048 + ((k0 & 127) >> 5) * 512;
-    const size_t aoff_k = TN ? (size_t)k0 * ldx : (size_t)k0, boff_k = TN ? (size_t)k0 * ldw : woff;
 #pragma unroll
     for (int i = 0; i < A_INSTR; ++i)
-      if (!A_UNEVEN || aq(i) < NAI) glds16<AUXA>(asrc[i] + aoff_k, As + aq(i) * 512);
+      if (!A_UNEVEN || aq(i) < NAI) glds16<AUXA>(asrc[i] + k0, As + aq(i) * 512);
 #pragma unroll
     for (int i = 0; i < B_INSTR; ++i)
-      if (!B_UNEVEN || bq(i) < NBI) glds16<AUXB>(bsrc[i] + boff_k, Bs + bq(i) * 512);
+      if (!B_UNEVEN || bq(i) < NBI) glds16<AUXB>(bsrc[i] + woff, Bs + bq(i) * 512);
   };
 
   f32x4 acc[MT][NT];
@@ -284,35 +258,19 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const uint16_t* __rest
       asm volatile("" ::: "memory");
     };
     s16x8 af[MQ][2], bq[2][2][2];
-    // TN fragment of 16 columns col0 .. col0 + 15 of a [64 k][pitch] image, k 32 s2 + 8 g .. +8: two transposed
-    // reads of 4 k rows x 16 columns (lane 4 q + p of the 16-lane group addresses k row + q, columns 4 p .. 4 p + 3;
-    // lane c receives column c).  Rows are 256 or 512 B (0 mod 64 banks); tn_swz puts the 8 rows a 32-lane half
-    // reads on 8 distinct 8-bank octets: conflict-free.
-    auto tn_frag = [&](const uint16_t* img, int pitch, int col0, int s2) -> s16x8 {
-      typedef __attribute__((address_space(3))) s16x4* lds_s16x4_t;
-      const int kr = 32 * s2 + 8 * g + (c >> 2), col = col0 + 4 * (c & 3);
-      const uint16_t* p0 = img + kr * pitch + ((((col >> 3) ^ tn_swz(kr)) << 3) | (col & 7));
-      const uint16_t* p1 = img + (kr + 4) * pitch + ((((col >> 3) ^ tn_swz(kr + 4)) << 3) | (col & 7));
-      const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t)(p0));
-      const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t)(p1));
-      return s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    };
     auto read_a = [&](int buf, int qm) {
       const uint16_t* As = smem + buf * STAGE;
 #pragma unroll
       for (int i = 0; i < MQ; ++i)
 #pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2)
-          af[i][s2] = TN ? tn_frag(As + wm * 64 * 128, 128, 16 * (MQ * qm + i), s2) : ld16(As + aoff[MQ * qm + i][s2]);
+        for (int s2 = 0; s2 < 2; ++s2) af[i][s2] = ld16(As + aoff[MQ * qm + i][s2]);
     };
     auto read_b = [&](int buf, int qn) {
       const uint16_t* Bs = smem + buf * STAGE + A_ELEMS;
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2)
-          bq[qn][j][s2] = TN ? tn_frag(Bs, 256, (wn * NT + 2 * qn + j) * 16, s2)
-                             : ld16(Bs + boff + ((2 * qn + j) * KS + s2) * 512);
+        for (int s2 = 0; s2 < 2; ++s2) bq[qn][j][s2] = ld16(Bs + boff + ((2 * qn + j) * KS + s2) * 512);
     };
     auto quad = [&](int qm, int qn) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -562,14 +520,14 @@ static void big_launch(const uint16_t* X, int ldx, const uint16_t* W, const uint
                        hipSuccess;
     (void)attr;
     kern<<<nwg, 512, SMEM, st>>>(X, ldx, W, bias, R, ldr, Y, ldy, nullptr, M, N, K, 1, nullptr, nullptr, 0L,
-                                 big_group_m(), 0);
+                                 big_group_m());
   } else {
     auto kern = gemm_big_kernel<BM, BN, WM, WN, BK, NBUF, EPI, false, true, 0, 0, 3, PP>;
     static bool attr = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM) ==
                        hipSuccess;
     (void)attr;
     kern<<<nwg, 512, SMEM, st>>>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, S, nullptr, nullptr, 0L,
-                                 big_group_m(), 0);
+                                 big_group_m());
     if (!reduce) return;  // slabs left for the consumer (fused reduce + residual + RMSNorm)
     const int ncol = EPI == EPI_SILU ? N / 2 : N;
     const long chunks = (long)M * (ncol / 8);
@@ -643,25 +601,6 @@ int launch_gemm_big(const uint16_t* X, int ldx, const uint16_t* W, const uint16_
                  : big_dispatch<EPI_NONE, false>(X, ldx, W, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, K, bn, S, reduce, s);
 }
 
-// ------------------------------------------------------------------------------------ TN (weight gradients)
-// Y [M, N] (+)= Xt^T . Wt with Xt [K, M] (ldx) and Wt [K, N] (ldw) token-major: dW = dY^T . X straight from the
-// activations and output gradients of the step (no transposed / shuffled operand images).  M, N multiples of 256,
-// K of 64; epilogues: plain (bf16 or fp32) or the residual add (bf16, in place when R == Y: the GradAcc update).
-int launch_gemm_tn(const uint16_t* Xt, int ldx, const uint16_t* Wt, int ldw, const uint16_t* R, int ldr, void* Y,
-                   int ldy, bool out_f32, int epi, int M, int N, int K, hipStream_t st) {
-  if (M <= 0 || N <= 0) return 0;
-  if (M % 256 || N % 256 || K % 64 || K <= 0 || ldx % 8 || ldw % 8) return -1;
-  if (epi != EPI_NONE && (epi != EPI_RESID || out_f32)) return -1;
-  constexpr int SMEM = big_smem<256, 256, 64, 2>();
-  const int nwg = (M / 256) * (N / 256);
-#define XOT_TN(EPIV, F32V)                                                                                              do {                                                                                                                    auto kern = gemm_big_kernel<256, 256, 2, 4, 64, 2, EPIV, F32V, false, 0, 0, 3, 2, true>;                             static bool attr = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM) ==                           hipSuccess;                                                                                        (void)attr;                                                                                                           kern<<<nwg, 512, SMEM, st>>>(Xt, ldx, Wt, nullptr, R, ldr, Y, ldy, nullptr, M, N, K, 1, nullptr, nullptr, 0L,                                     big_group_m(), ldw);                                                                   } while (0)
-  if (epi == EPI_RESID) XOT_TN(EPI_RESID, false);
-  else if (out_f32) XOT_TN(EPI_NONE, true);
-  else XOT_TN(EPI_NONE, false);
-#undef XOT_TN
-  return 0;
-}
-
 // ------------------------------------------------------------------------------------ K-grouped (expert dW)
 // Y_e [M, N] (+)= X[:, koff[e]:koff[e+1]] . W[:, koff[e]:koff[e+1]]^T for e < E; X [M, K] row-major, W [N, K]
 // pre-shuffled, koff multiples of 64 (segments padded with zero rows by the caller), resid: Y_e += (in place).
@@ -677,14 +616,14 @@ int launch_gemm_kgroup(const uint16_t* X, int ldx, const uint16_t* W, uint16_t* 
                        hipSuccess;
     (void)attr;
     kern<<<grid, 512, SMEM, st>>>(X, ldx, W, nullptr, Y, ldy, Y, ldy, nullptr, M, N, K, 1, koff, nullptr, 0L,
-                                  big_group_m(), 0);
+                                  big_group_m());
   } else {
     auto kern = gemm_big_kernel<256, 256, 2, 4, 64, 2, EPI_NONE, false, false, 4, 0, 3, 2>;
     static bool attr = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM) ==
                        hipSuccess;
     (void)attr;
     kern<<<grid, 512, SMEM, st>>>(X, ldx, W, nullptr, nullptr, 0, Y, ldy, nullptr, M, N, K, 1, koff, nullptr, 0L,
-                                  big_group_m(), 0);
+                                  big_group_m());
   }
   return 0;
 }
@@ -711,7 +650,7 @@ static void big_moe_launch(const uint16_t* X, int ldx, const uint16_t* W, void* 
   (void)attr;
   dim3 grid(((max_rows + BM - 1) / BM) * (N / BN) * S, E);
   kern<<<grid, 512, SMEM, st>>>(X, ldx, W, nullptr, nullptr, 0, Y, ldy, nullptr, max_rows, N, K, S, off, gather,
-                                S > 1 ? ysplit : 0L, 4, 0);
+                                S > 1 ? ysplit : 0L, 4);
 }
 
 // bm = row tile (128 / 192 / 256) + 1000 x pipeline variant: 0 = two 64-deep LDS stages (one in flight under

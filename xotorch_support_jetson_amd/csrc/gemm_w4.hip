@@ -99,15 +99,23 @@ constexpr int A_EL = BM * BK, STAGE = (BM + BN) * BK;  // bf16 elements per stag
 constexpr int SMEM = 2 * STAGE * 2;                     // two stage buffers, 128 KB
 }  // namespace w4
 
-template <int EPI, bool OUT_F32, bool SPLIT>
+// TN (the weight-gradient GEMM dW = dY^T . X on the step's token-major tensors, no dY^T / shuffle(X^T) images in
+// HBM): X holds the token operand transposed, Xt [K, M] (k = tokens, ldx apart), W the weight operand likewise,
+// Wt [K, N] (ldw apart).  A stage arrives by LDS-DMA as two row-major [64 k][256] images (512-B rows, 16-B granules
+// XOR-swizzled by tn_swz(k row) through the source offsets) and every fragment (8 consecutive k of one row or
+// column) is two ds_read_b64_tr_b16; the fragment rows are in natural order (no PERM), so the epilogue stores 8 B
+// per lane and tile.  The reads are compiler-visible (the explicit read waits below assume one read per fragment).
+template <int EPI, bool OUT_F32, bool SPLIT, bool TN = false>
 __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const uint16_t* __restrict__ X, int ldx,
                                                          const uint16_t* __restrict__ W,
                                                          const uint16_t* __restrict__ bias,
                                                          const uint16_t* __restrict__ R, int ldr,
                                                          void* __restrict__ Yv, int ldy, float* __restrict__ ws,
-                                                         int M, int N, int K, int S, int group_m) {
+                                                         int M, int N, int K, int S, int group_m, int ldw) {
   using namespace w4;
-  constexpr bool PERM = EPI != EPI_SILU;
+  static_assert(!TN || (!SPLIT && EPI != EPI_SILU), "TN: weight gradients (plain or residual epilogue)");
+  constexpr bool PERM = EPI != EPI_SILU && !TN;
+  constexpr bool ASMRD = W4_ASMRD && !TN;
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, c = lane & 15;
@@ -157,17 +165,42 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const uint16_t* __restr
   const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(W + (size_t)((n0 >> 4) + 4 * swave) * (K / 128) * 2048), (short)0, -1, 0x00020000);
   int xvo[8], wvo;  // per-lane byte offsets: X per instruction (row clamp), W one for all (the rest is scalar)
-  {
+  int tvo[8];       // TN: the W operand's per-instruction offsets
+  // TN: instruction q = 8 wave + d of either operand copies k rows 2q, 2q + 1 of the stage (512 B each): lane l ->
+  // k row 2q + l / 32, physical granule l % 32 holding logical granule (l % 32) ^ tn_swz(k row).  tn_swz puts the
+  // 8 rows a 32-lane half reads transposed (rows 8 g + 0..3 of two lane groups) on 8 distinct 8-bank octets.
+  auto tn_swz = [](int krow) -> int { return 2 * ((krow & 3) | (((krow >> 3) & 1) << 2)); };
+  if constexpr (TN) {
+#pragma unroll
+    for (int d = 0; d < 8; ++d) {
+      const int kr = 2 * (8 * wave + d) + (lane >> 5), lg = (lane & 31) ^ tn_swz(kr);
+      xvo[d] = (int)(((unsigned)kr * (unsigned)ldx + (unsigned)(m0 + 8 * lg)) * 2u);
+      tvo[d] = (int)(((unsigned)kr * (unsigned)ldw + (unsigned)(n0 + 8 * lg)) * 2u);
+    }
+    wvo = 0;
+  } else {
     const int xr0 = 64 * wave + (lane >> 3);
     const int xslot[2] = {((lane & 7) ^ ((lane >> 4) & 7)) * 8, ((lane & 7) ^ (((lane >> 4) + 4) & 7)) * 8};
 #pragma unroll
     for (int d = 0; d < 8; ++d)
       xvo[d] = (int)(((unsigned)min(m0 + xr0 + 8 * d, M - 1) * (unsigned)ldx + xslot[d & 1]) * 2u);
     wvo = (PERM ? (((lane >> 4) * 16 + ((lane & 15) ^ (4 * ((lane >> 4) & 1)))) * 8) : lane * 8) * 2;
+#pragma unroll
+    for (int d = 0; d < 8; ++d) tvo[d] = 0;
   }
+  const __amdgpu_buffer_rsrc_t trs = __builtin_amdgcn_make_buffer_rsrc((void*)W, (short)0, -1, 0x00020000);
   auto issue = [&](int t, int buf, int d) {  // LDS-DMA instruction d (0..15) of this wave for k stage t
     typedef __attribute__((address_space(3))) void* lds_t;
     uint16_t* As = smem + buf * STAGE;
+    if constexpr (TN) {
+      if (d < 8)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_t)(As + (8 * swave + d) * 512), 16, xvo[d], t * (BK * 2) * ldx,
+                                                 0, W4_XAUX);
+      else
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(trs, (lds_t)(As + A_EL + (8 * swave + d - 8) * 512), 16, tvo[d - 8],
+                                                 t * (BK * 2) * ldw, 0, W4_WAUX);
+      return;
+    }
     if (d < 8) {
       __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_t)(As + (8 * swave + d) * 512), 16, xvo[d], t * (BK * 2), 0,
                                                W4_XAUX);
@@ -254,7 +287,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const uint16_t* __restr
   // put lgkmcnt(0) before every stage's first MFMA -- the whole 16-read read-ahead exposed each stage.  Byte
   // addresses: one base per (operand, k half) plus the stage buffer's 64 KB, tile offsets as immediates.
   const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint16_t*)smem;
-  auto rd = [&](int buf, int h, int f) {
+  auto rd_asm = [&](int buf, int h, int f) {
     const uint32_t bo = lds0 + (uint32_t)buf * (STAGE * 2);
     if (f == 0 || f > 8) {
       const int j = f == 0 ? 0 : f - 8;
@@ -280,14 +313,55 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const uint16_t* __restr
       }
     }
   };
-#else
-  auto rd = [&](int buf, int h, int f) {
+#endif
+  auto rd_c = [&](int buf, int h, int f) {
     const uint16_t* Ls = smem + buf * STAGE;
     const int j = f == 0 ? 0 : (f <= 8 ? -1 : f - 8);
     if (j >= 0) wf[h][j] = ld16(Ls + wo[j & 1][h] + 2048 * (j >> 1));
     else xf[h][f - 1] = ld16(Ls + xo[h] + 1024 * (f - 1));
   };
+  // TN fragments: element offsets (k half 0, rows 8 g + (c >> 2)) of token tile i and weight tile j in their images;
+  // k half h is 32 rows further, the second read 4 rows (tn_swz ignores bit 2 of the row: same swizzle).  Lane
+  // 4 q + p of a 16-lane group addresses k row q of the block, columns 4 p .. 4 p + 3; lane c receives column c.
+  int ta[8], tb[8];
+  if constexpr (TN) {
+    const int kr = 8 * g + (c >> 2), sw = tn_swz(kr);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int xc = wm * 128 + 16 * i + 4 * (c & 3), wc = wn * 128 + 16 * i + 4 * (c & 3);
+      ta[i] = kr * 256 + ((((xc >> 3) ^ sw) << 3) | (xc & 7));
+      tb[i] = A_EL + kr * 256 + ((((wc >> 3) ^ sw) << 3) | (wc & 7));
+    }
+  }
+  // As inline asm: compiler-visible LDS reads after LDS-DMA issues made hipcc drain vmcnt(0) -- the whole refill in
+  // flight -- before the first read of every stage.  Waits: the k loop's s_waitcnt lgkmcnt(15) before MFMAs 0 .. 16.
+  const uint32_t tlds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint16_t*)smem;
+  auto rd_tn = [&](int buf, int h, int f) {
+    const int j = f == 0 ? 0 : (f <= 8 ? -1 : f - 8);
+    const uint32_t a = tlds0 + (uint32_t)buf * (STAGE * 2) + (uint32_t)(j >= 0 ? tb[j] : ta[f - 1]) * 2;
+    s16x4 lo, hi;
+    if (h == 0) {
+      asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(a));
+      asm volatile("ds_read_b64_tr_b16 %0, %1 offset:2048" : "=v"(hi) : "v"(a));
+    } else {
+      asm volatile("ds_read_b64_tr_b16 %0, %1 offset:16384" : "=v"(lo) : "v"(a));
+      asm volatile("ds_read_b64_tr_b16 %0, %1 offset:18432" : "=v"(hi) : "v"(a));
+    }
+    const s16x8 v = s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    if (j >= 0) wf[h][j] = v;
+    else xf[h][f - 1] = v;
+  };
+  auto rd = [&](int buf, int h, int f) {
+    if constexpr (TN) {
+      rd_tn(buf, h, f);
+    } else {
+#if W4_ASMRD
+      rd_asm(buf, h, f);
+#else
+      rd_c(buf, h, f);
 #endif
+    }
+  };
 
   {  // T >= 1 (S <= K / 64).  Prologue without branches: stage 1 (stage 0 again when T == 1) into buffer 1
 #pragma unroll
@@ -323,12 +397,19 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const uint16_t* __restr
         constexpr int v = decltype(vc)::value;
         constexpr int h = v >> 6, u = v & 63;
 #if W4_ASMRD
+        if constexpr (ASMRD) {
         // the read-ahead (16 reads, consumption order) and the v half-1 reads issued since: MFMA v <= 8 needs
         // read-ahead v + 1 (w0 + x_v, then w1) -> at most 14 younger reads in flight; from MFMA 16 on (w2..w7)
         // the whole read-ahead -> 15 (stricter than needed, the counter's maximum)
         if constexpr (v <= 8) asm volatile("s_waitcnt lgkmcnt(14)" ::: "memory");
         if constexpr (v == 16) asm volatile("s_waitcnt lgkmcnt(15)" ::: "memory");
+        }
 #endif
+        // TN: 32 read-ahead reads (two per fragment, consumption order) then two half-1 reads per MFMA from MFMA 0:
+        // before MFMA v <= 16 at most 15 reads in flight means reads 0 .. 16 + 2v are done (LDS reads retire in
+        // order), which covers fragment v + 1 (x_v, reads 2v + 2, 2v + 3) up to v = 7, w1 (reads 18, 19) at 8 .. 15
+        // and, at 16, all 32 read-ahead reads
+        if constexpr (TN && v <= 16) asm volatile("s_waitcnt lgkmcnt(15)" ::: "memory");
         mma(h, u);
         if constexpr (!(W4_ABL & 4) && v % RSP == 0 && v < 16 * RSP) rd(buf, 1, v / RSP);
         if constexpr (!(W4_ABL & 4) && v >= 64 + B2 && (v - 64 - B2) % RSP == 0 && v < 64 + B2 + 16 * RSP)
@@ -392,6 +473,33 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const uint16_t* __restr
         } else {
           *reinterpret_cast<f32x4*>(row + 32 * J + 4 * g) = acc[i][2 * J];
           *reinterpret_cast<f32x4*>(row + 32 * J + 16 + 4 * g) = acc[i][2 * J + 1];
+        }
+      }
+    }
+  } else if constexpr (TN) {  // natural column order: lane (g, c) holds columns cbase + 16 j + 4 g .. +4 of token row
+    typedef short s16x4_t __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = rbase + 16 * i;
+      if (m >= M) continue;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int col = cbase + 16 * j + 4 * g;
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r];
+        if constexpr (EPI == EPI_RESID) {
+          const s16x4_t rv = *reinterpret_cast<const s16x4_t*>(R + (size_t)m * ldr + col);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] += bf2f(rv[r]);
+        }
+        if constexpr (OUT_F32) {
+          *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(Yv) + (size_t)m * ldy + col) = f32x4{v[0], v[1], v[2], v[3]};
+        } else {
+          s16x4_t o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = (short)f2bf(v[r]);
+          *reinterpret_cast<s16x4_t*>(reinterpret_cast<uint16_t*>(Yv) + (size_t)m * ldy + col) = o;
         }
       }
     }
@@ -486,7 +594,37 @@ static void w4_launch(const uint16_t* X, int ldx, const uint16_t* W, const uint1
       hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, w4::SMEM) == hipSuccess;
   (void)attr;
   const int nwg = ((M + 255) / 256) * (N / 256) * S;
-  kern<<<nwg, 256, w4::SMEM, st>>>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, S, group_m);
+  kern<<<nwg, 256, w4::SMEM, st>>>(X, ldx, W, bias, R, ldr, Y, ldy, ws, M, N, K, S, group_m, 0);
+}
+
+template <int EPI, bool F32>
+static void w4_tn_launch(const uint16_t* Xt, int ldx, const uint16_t* Wt, int ldw, const uint16_t* R, int ldr, void* Y,
+                         int ldy, int M, int N, int K, int group_m, hipStream_t st) {
+  auto kern = gemm_w4_kernel<EPI, F32, false, true>;
+  static bool attr =
+      hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, w4::SMEM) == hipSuccess;
+  (void)attr;
+  kern<<<(M / 256) * (N / 256), 256, w4::SMEM, st>>>(Xt, ldx, Wt, nullptr, R, ldr, Y, ldy, nullptr, M, N, K, 1,
+                                                       group_m, ldw);
+}
+
+// Weight gradients on the token-major operands: Y [M, N] (+)= Xt^T . Wt, Xt [K, M] (ldx), Wt [K, N] (ldw); M, N
+// multiples of 256, K of 64; plain (bf16 / fp32) or residual (bf16, in place when R == Y) epilogue.
+int launch_gemm_w4_tn(const uint16_t* Xt, int ldx, const uint16_t* Wt, int ldw, const uint16_t* R, int ldr, void* Y,
+                      int ldy, bool out_f32, int epi, int M, int N, int K, int group_m, hipStream_t st) {
+  if (M <= 0 || N <= 0) return 0;
+  if (M % 256 || N % 256 || K % 64 || K <= 0 || ldx % 8 || ldw % 8) return -1;
+  if ((size_t)K * ldx * 2 >= (1ull << 31) || (size_t)K * ldw * 2 >= (1ull << 31)) return -1;  // 32-bit offsets
+  if (epi == EPI_RESID) {
+    if (out_f32) return -1;
+    w4_tn_launch<EPI_RESID, false>(Xt, ldx, Wt, ldw, R, ldr, Y, ldy, M, N, K, group_m, st);
+  } else if (epi == EPI_NONE) {
+    if (out_f32) w4_tn_launch<EPI_NONE, true>(Xt, ldx, Wt, ldw, R, ldr, Y, ldy, M, N, K, group_m, st);
+    else w4_tn_launch<EPI_NONE, false>(Xt, ldx, Wt, ldw, R, ldr, Y, ldy, M, N, K, group_m, st);
+  } else {
+    return -1;
+  }
+  return 0;
 }
 
 // Tile code 4256 of launch_gemm_big.  S > 1 writes fp32 slabs (reduced by the caller's reduce kernel).

@@ -42,6 +42,9 @@ int launch_gemm_stream8(const uint16_t* X, int ldx, const uint8_t* W, const floa
 int launch_gemm_w4(const uint16_t* X, int ldx, const uint16_t* W, const uint16_t* bias, const uint16_t* R, int ldr,
                    void* Y, int ldy, bool out_f32, int epi, float* ws, int M, int N, int K, int S, int group_m,
                    hipStream_t st);
+// the same tile on token-major operands (weight gradients): Y [M, N] (+)= Xt^T . Wt, Xt [K, M], Wt [K, N]
+int launch_gemm_w4_tn(const uint16_t* Xt, int ldx, const uint16_t* Wt, int ldw, const uint16_t* R, int ldr, void* Y,
+                      int ldy, bool out_f32, int epi, int M, int N, int K, int group_m, hipStream_t st);
 int gemm_big_group_m();  // grouped raster width of tall grids (XOT_GEMM_GROUP_M)
 int launch_gemm_big(const uint16_t* X, int ldx, const uint16_t* W, const uint16_t* bias, const uint16_t* R, int ldr,
                     void* Y, int ldy, bool out_f32, int epi, float* ws, long ws_elems, int M, int N, int K, int bn,
@@ -51,9 +54,6 @@ int launch_gemm_big(const uint16_t* X, int ldx, const uint16_t* W, const uint16_
 int launch_shuffle(const uint16_t* src, long ld, uint16_t* dst, int R, int C, hipStream_t s);
 int launch_shuffle_t(const uint16_t* src, long ld, uint16_t* dst, int R, int C, hipStream_t s);
 int launch_transpose(const uint16_t* src, long ld, uint16_t* dst, int R, int C, hipStream_t s);
-// weight-gradient GEMM on token-major operands (gemm_big.hip TN): Y [M, N] (+)= Xt^T . Wt, Xt [K, M], Wt [K, N]
-int launch_gemm_tn(const uint16_t* Xt, int ldx, const uint16_t* Wt, int ldw, const uint16_t* R, int ldr, void* Y,
-                   int ldy, bool out_f32, int epi, int M, int N, int K, hipStream_t st);
 int launch_gemm_kgroup(const uint16_t* X, int ldx, const uint16_t* W, uint16_t* Y, int ldy, bool resid,
                        const int* koff, int E, int M, int N, int K, hipStream_t st);
 int launch_gemm_batched(const uint16_t* X, int ldx, long xbat, const uint16_t* W, void* Y, int ldy, long ybat,

@@ -467,10 +467,12 @@ def own_dw(dy: torch.Tensor, x: torch.Tensor, acc: "GradAcc", cb: bool = True) -
     acc.cb()  # on the main stream: a callback that reads acc.buf joins the side stream first
 
 
-# Weight gradients straight from the token-major dY and X (csrc/gemm_big.hip TN: both operands staged as [64 tokens]
-# row tiles, MFMA fragments read transposed out of LDS), no dY^T / shuffle(X^T) images in HBM: the relayouts cost
-# 66 ms of a 705 ms Llama-3-8B step (profiles/r6/train/relayout_cost/).  XOT_DW_TN=0: relayouts + pre-shuffled tile.
-DW_TN = os.environ.get("XOT_DW_TN", "0") == "1"
+# Weight gradients straight from the token-major dY and X (csrc/gemm_w4.hip TN: both operands staged as [64 tokens]
+# row tiles by LDS-DMA, MFMA fragments read transposed out of LDS with ds_read_b64_tr_b16): no dY^T / shuffle(X^T)
+# images in HBM (~1.1 GB of relayout traffic per layer and 4096-token micro-batch on Llama-3-8B, and their transient
+# buffers).  The TN tile runs 5-10 % slower than the pre-shuffled one and the relayouts cost about that much: the step
+# is the same (706-708 vs 709 ms, profiles/r6/train/tn/).  XOT_DW_TN=0: relayouts + the pre-shuffled tile.
+DW_TN = os.environ.get("XOT_DW_TN", "1") != "0"
 
 
 def dw_tn(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor, accumulate: bool) -> bool:
@@ -529,10 +531,8 @@ class OwnLinearFn(torch.autograd.Function):
     backward  dX = dY . shuffle(W^T)^T
               dW = dY^T . shuffle(X^T)^T into the GradAcc buffer (plain store on the first micro-batch of a
                    step, residual epilogue acc += ... after), with dY^T and shuffle(X^T) built per micro-batch
-                   by csrc/layout.hip (about 2 x T x (N + K) x 2 bytes each), on the weight-gradient side
-                   stream (DW_STREAM above).  (A token-major TN GEMM reading dY
-                   and X as they are, with transposed LDS reads, measured 5-20 % slower than relayout + the
-                   pre-shuffled tile, profiles/r4/train/dw_gemm_tn_vs_relayout_vs_hipblaslt.json.)"""
+                   by csrc/layout.hip (about 2 x T x (N + K) x 2 bytes each) -- or, by default, straight from dY
+                   and X on the four-wave TN tile (dw_tn) -- on the weight-gradient side stream (DW_STREAM above)."""
 
   @staticmethod
   def forward(ctx, x, w, tw, h, acc):
