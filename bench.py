@@ -100,7 +100,7 @@ def gemm_choices(batch: int) -> dict:
   code | n-tiles, K split): what a fresh box picked, so a slow record can be told from a different tile pick."""
   from xotorch_support_jetson_amd.ops import linear as L
   mb = L._m_bucket(batch)
-  out = {}
+  out = {"_source": "seed table (ops/gemm_seed_mi355x.json) under the box's own" if L.policy.seeded else "tuned"}
   for k, v in L.policy.table.items():
     if len(k) >= 5 and k[0] == "sh" and k[1] == mb:
       out[f"N{k[2]} K{k[3]} {k[4]}"] = list(v) if isinstance(v, tuple) else v

@@ -110,3 +110,18 @@ def test_tall_gemms_take_the_four_wave_tile_untimed(monkeypatch):
   monkeypatch.setattr(L.GemmPolicy, "_no_tuning", lambda self: True)  # the heuristic instead of a GPU timing
   pol2 = L.GemmPolicy()
   assert pol2.shuffled_cfg(x, w, None, None, "none", torch.bfloat16)[0] == "big"
+
+
+def test_seed_table_parses_and_loads_under_the_box_table(tmp_path):
+  """ops/gemm_seed_mi355x.json: comment keys skipped, the headline decode picks load, and a key the box tuned itself
+  keeps the box's choice (the seed only fills gaps)."""
+  import json
+  from xotorch_support_jetson_amd.ops import linear as L
+  pol = L.GemmPolicy()
+  own = ("sh", 512, 10240, 8192, "none", False, "torch.bfloat16")
+  pol.table[own] = ("big", 256, 2)  # as if the box had tuned it
+  pol._load(L.SEED_TABLE)
+  assert pol.table[own] == ("big", 256, 2)
+  assert pol.table[("sh", 512, 57344, 8192, "silu", False, "torch.bfloat16")] == ("big", 2256, 1)
+  assert not any(isinstance(k, tuple) and k and str(k[0]).startswith("_") for k in pol.table)
+  assert all(k.startswith("_") or json.loads(k)[0] == "sh" for k in json.load(open(L.SEED_TABLE)))

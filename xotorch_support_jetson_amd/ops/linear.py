@@ -159,6 +159,23 @@ def _default_table_path():
     return None
 
 
+# Seed table: the headline decode step's picks (ops/gemm_seed_mi355x.json), tuned on MI355X over rounds 4-6 and
+# stable there, loaded under the box's own table so a fresh box runs them without re-timing in a noisy warmup.
+# XOT_GEMM_SEED=0 (or XOT_GEMM_TABLE=off, or another GPU): tuned in-process like every other shape.
+SEED_TABLE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_seed_mi355x.json")
+
+
+def _seed_table_path():
+  if os.environ.get("XOT_GEMM_SEED", "1") == "0" or os.environ.get("XOT_GEMM_TABLE") == "off":
+    return None
+  try:
+    if not (torch.cuda.is_available() and "MI355" in torch.cuda.get_device_name(torch.cuda.current_device())):
+      return None
+  except Exception:  # noqa: BLE001
+    return None
+  return SEED_TABLE if os.path.exists(SEED_TABLE) else None
+
+
 class GemmPolicy:
   """GEMM implementation choice per (layout, M bucket, N, K, epilogue, ...), cold-cache timed on first use.
   Choices persist in a JSON table (see _default_table_path), so a serving process does not stall its first
@@ -166,6 +183,7 @@ class GemmPolicy:
 
   def __init__(self):
     self.mode = os.environ.get("XOT_GEMM", "auto")
+    self.seeded = False
     self.table: Dict[Tuple, object] = {}
     self.path = None
     self._path_resolved = False
@@ -175,17 +193,24 @@ class GemmPolicy:
     try:
       with open(path) as f:
         for k, v in json.load(f).items():
+          if k.startswith("_"):  # comments
+            continue
           self.table.setdefault(tuple(json.loads(k)), tuple(v) if isinstance(v, list) else v)
     except (OSError, ValueError):
       pass  # a corrupt or unreadable table is only a cache
 
   def _table_path(self):
-    """Resolved lazily (needs the device): loads the persisted table the first time a choice is needed."""
+    """Resolved lazily (needs the device): loads the persisted table the first time a choice is needed, then the
+    seed table under it (keys the box has not tuned itself)."""
     if not self._path_resolved:
       self._path_resolved = True
       self.path = _default_table_path()
       if self.path and os.path.exists(self.path):
         self._load(self.path)
+      seed = _seed_table_path()
+      if seed:
+        self._load(seed)
+        self.seeded = True
     return self.path
 
   def _lookup(self, key):
