@@ -169,7 +169,11 @@ def _seed_table_path():
   if os.environ.get("XOT_GEMM_SEED", "1") == "0" or os.environ.get("XOT_GEMM_TABLE") == "off":
     return None
   try:
-    if not (torch.cuda.is_available() and "MI355" in torch.cuda.get_device_name(torch.cuda.current_device())):
+    if not torch.cuda.is_available():
+      return None
+    i = torch.cuda.current_device()
+    arch = getattr(torch.cuda.get_device_properties(i), "gcnArchName", "")
+    if not (arch.startswith("gfx950") or "MI355" in torch.cuda.get_device_name(i)):  # CDNA4 (gfx950) only
       return None
   except Exception:  # noqa: BLE001
     return None
