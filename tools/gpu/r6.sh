@@ -12,6 +12,8 @@ for what in "$@"; do
     reduce) step r6/reduce 120 python -u tools/bench_reduce.py ;;
     nov)    XOT_EXP_NO_V=1 XOT_GEMM_TABLE=$T step r6/bench_nov 400 python -u bench.py --steps 20 --warmup 5 ;;
     attn)   step r6/attn 200 python -u tools/bench_attn_b512.py ;;
+    attn_small) step r6/attn_small 300 python -u tools/bench_attn_small.py ;;
+    b1bench) step r6/b1bench 300 python -u bench.py --model llama-3-8b --batch-per-gpu 1 --steps 64 --warmup 8 ;;
     prof)   XOT_GEMM_TABLE=$T prof r6/prof 600 python3 "$R/bench.py" --steps 6 --warmup 3
             step r6/breakdown 60 python tools/decode_breakdown.py "$(ls "$O"/r6/prof/*/*kernel_trace.csv "$O"/r6/prof/*kernel_trace.csv 2>/dev/null | head -1)" --steps 6 --json "$O/r6/breakdown.json"
             cat "$O/r6/breakdown.log" ;;
@@ -26,6 +28,7 @@ for what in "$@"; do
     train_tn) XOT_DW_TN=1 step r6/train_tn 900 python -u tools/bench_train.py --model llama-3-8b --seq 2048 --mb 2 --microbatches 4 --steps 3 --warmup 1 ;;
     train_relayout) XOT_DW_TN=0 step r6/train_relayout 900 python -u tools/bench_train.py --model llama-3-8b --seq 2048 --mb 2 --microbatches 4 --steps 3 --warmup 1 ;;
     dw) step r6/dw 300 python -u tools/bench_dw.py ;;
+    train_mb) for cfg in "4 2" "8 1" "1 8"; do set -- $cfg; step r6/train_mb$1x$2 900 python -u tools/bench_train.py --model llama-3-8b --seq 2048 --mb $1 --microbatches $2 --steps 3 --warmup 1; done ;;
     train_inline) XOT_DW_STREAM=0 step r6/train_inline 900 python -u tools/bench_train.py --model llama-3-8b --seq 2048 --mb 2 --microbatches 4 --steps 3 --warmup 1 ;;
     train_norope) XOT_EXP_NO_ROPE=1 step r6/train_norope 900 python -u tools/bench_train.py --model llama-3-8b --seq 2048 --mb 2 --microbatches 4 --steps 3 --warmup 1 ;;
     train_tprof) step r6/train_tprof 900 python -u tools/bench_train.py --model llama-3-8b --seq 2048 --mb 2 --microbatches 4 --steps 2 --warmup 1 --torch-prof "$O/r6/train_torch_ops.txt" ;;
