@@ -10,7 +10,6 @@ for what in "$@"; do
     bench)  XOT_GEMM_TABLE=$T step r6/bench 400 python -u bench.py --steps 20 --warmup 5 ;;
     bench2) XOT_GEMM_TABLE=$T step r6/bench2 400 python -u bench.py --steps 20 --warmup 5 ;;
     reduce) step r6/reduce 120 python -u tools/bench_reduce.py ;;
-    nov)    XOT_EXP_NO_V=1 XOT_GEMM_TABLE=$T step r6/bench_nov 400 python -u bench.py --steps 20 --warmup 5 ;;
     attn)   step r6/attn 200 python -u tools/bench_attn_b512.py ;;
     attn_small) step r6/attn_small 300 python -u tools/bench_attn_small.py ;;
     b1bench) step r6/b1bench 300 python -u bench.py --model llama-3-8b --batch-per-gpu 1 --steps 64 --warmup 8 ;;
@@ -22,7 +21,6 @@ for what in "$@"; do
     ring70) # RingServer (`xot --gpus 1 --ring`) at the headline operating point: Llama-3-70B, 512 streams x 128 tokens
             step r6/ring70 1100 python -u tools/bench_serve.py --ring 1 --model llama-3-70b --concurrency 512 --max-tokens 128 --prompt-words 124 --server-log "$O/r6/ring70_server.log" ;;
     train)  step r6/train 900 python -u tools/bench_train.py --model llama-3-8b --seq 2048 --mb 2 --microbatches 4 --steps 3 --warmup 1 ;;
-    train_norelayout) XOT_EXP_NO_RELAYOUT=1 step r6/train_norelayout 900 python -u tools/bench_train.py --model llama-3-8b --seq 2048 --mb 2 --microbatches 4 --steps 3 --warmup 1 ;;
     tn_test) step r6/tn_test 300 python -u -m pytest tests/test_kernels_gpu.py tests/test_train_own_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread -k "tn or train or silu_down or relayout" ;;
     tn_test_on) XOT_DW_TN=1 step r6/tn_test_on 300 python -u -m pytest tests/test_train_own_gpu.py tests/test_pipeline_train.py -m gpu -x -q --timeout 120 --timeout-method thread ;;
     train_tn) XOT_DW_TN=1 step r6/train_tn 900 python -u tools/bench_train.py --model llama-3-8b --seq 2048 --mb 2 --microbatches 4 --steps 3 --warmup 1 ;;
@@ -30,7 +28,6 @@ for what in "$@"; do
     dw) step r6/dw 300 python -u tools/bench_dw.py ;;
     train_mb) for cfg in "4 2" "8 1" "1 8"; do set -- $cfg; step r6/train_mb$1x$2 900 python -u tools/bench_train.py --model llama-3-8b --seq 2048 --mb $1 --microbatches $2 --steps 3 --warmup 1; done ;;
     train_inline) XOT_DW_STREAM=0 step r6/train_inline 900 python -u tools/bench_train.py --model llama-3-8b --seq 2048 --mb 2 --microbatches 4 --steps 3 --warmup 1 ;;
-    train_norope) XOT_EXP_NO_ROPE=1 step r6/train_norope 900 python -u tools/bench_train.py --model llama-3-8b --seq 2048 --mb 2 --microbatches 4 --steps 3 --warmup 1 ;;
     train_tprof) step r6/train_tprof 900 python -u tools/bench_train.py --model llama-3-8b --seq 2048 --mb 2 --microbatches 4 --steps 2 --warmup 1 --torch-prof "$O/r6/train_torch_ops.txt" ;;
     trainprof) prof r6/trainprof 900 python3 "$R/tools/bench_train.py" --mb 2 --microbatches 4 --steps 3 --warmup 1
             step r6/trainstep 60 python tools/step_window.py "$(ls "$O"/r6/trainprof/*/*kernel_trace.csv "$O"/r6/trainprof/*kernel_trace.csv 2>/dev/null | head -1)" ;;

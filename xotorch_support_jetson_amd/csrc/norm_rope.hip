@@ -533,8 +533,7 @@ __global__ __launch_bounds__(256) void splitk_rope_kv_write_kernel(
       return;
     }
     int p = pos[t];
-    const int mp = max_pos < 0 ? -max_pos : max_pos;
-    p = p < 0 ? 0 : (p >= mp ? mp - 1 : p);
+    p = p < 0 ? 0 : (p >= max_pos ? max_pos - 1 : p);
     const float* cs = cos_sin + (size_t)p * Dh;
     const f32x4 a = slab_sum4<SS>(row, S, sstride, bias, h * Dh + i);
     const f32x4 b = slab_sum4<SS>(row, S, sstride, bias, h * Dh + i + half);
@@ -550,7 +549,7 @@ __global__ __launch_bounds__(256) void splitk_rope_kv_write_kernel(
     *reinterpret_cast<s16x4*>(dst + i + half) = ob;
     return;
   }
-  if (slot < 0 || max_pos < 0) return;  // (max_pos < 0: timing experiment without the V write, XOT_EXP_NO_V)
+  if (slot < 0) return;
   const int e = 4 * (w - nrot), kh = e / Dh, d = e % Dh;
   const f32x4 v = slab_sum4<SS>(row, S, sstride, bias, (H + Hkv) * Dh + e);
   uint16_t* dst = vc + ((size_t)blk * Hkv + kh) * Dh * BS + v_page_off(off, d, Dh);
@@ -563,8 +562,6 @@ void launch_splitk_rope_kv_write(const float* ws, int S, const uint16_t* bias, c
                                  uint16_t* vc, int T, int H, int Hkv, int Dh, int BS, int max_pos, long nslots,
                                  hipStream_t s) {
   if (T <= 0) return;
-  static const bool no_v = getenv("XOT_EXP_NO_V") != nullptr;  // experiment only: skip the V write (wrong output)
-  if (no_v) max_pos = -max_pos;
   const long sstride = (long)T * (H + 2 * Hkv) * Dh;
   const int items = (H + Hkv) * (Dh / 8) + Hkv * Dh / 4;
   const dim3 grid(T, (items + 255) / 256);

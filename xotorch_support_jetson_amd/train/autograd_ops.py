@@ -496,21 +496,10 @@ def _dw(dy: torch.Tensor, x: torch.Tensor, acc: "GradAcc") -> None:
     _dw_gemm(*_dw_operands(dy, x), acc)
 
 
-# timing experiments only (wrong gradients): XOT_EXP_NO_RELAYOUT=1 skips the dW operand relayouts (the dW GEMMs read
-# unwritten images), XOT_EXP_NO_ROPE=1 skips the training RoPE rotations -- upper bounds of what fusing them saves
-EXP_NO_RELAYOUT = os.environ.get("XOT_EXP_NO_RELAYOUT", "0") == "1"
-EXP_NO_ROPE = os.environ.get("XOT_EXP_NO_ROPE", "0") == "1"
-
-
 def _dw_operands(dy: torch.Tensor, x: torch.Tensor):
   """dY^T [N, T] row-major and shuffle(X^T) [K, T] for the dW GEMM; they need T % 128, so ragged token counts (the
   reference's batch-size-1 JSONL lengths) are zero-padded to 128 rows first."""
   dy, x = pad_rows(dy), pad_rows(x)
-  if EXP_NO_RELAYOUT:
-    dyt = torch.empty(dy.shape[1], dy.shape[0], dtype=torch.bfloat16, device=dy.device)
-    xts = torch.empty(x.shape[1], x.shape[0], dtype=torch.bfloat16, device=x.device)
-    xts.xot_layout = "stream"
-    return dyt, xts
   return relayout(dy, 2), relayout(x, 1)
 
 
@@ -816,8 +805,6 @@ class QKVRopeFn(torch.autograd.Function):
     T, nq, nk = qkv.shape[0], H * Dh, Hkv * Dh
     ctx.save_for_backward(pos, cos_sin)
     ctx.dims = (H, Hkv, Dh, qkv.shape[1])
-    if EXP_NO_ROPE:
-      return qkv[:, :nq], qkv[:, nq:nq + nk], qkv[:, nq + nk:]
     q = torch.empty(T, nq, dtype=qkv.dtype, device=qkv.device)
     k = torch.empty(T, nk, dtype=qkv.dtype, device=qkv.device)
     C.rope_apply(qkv[:, :nq], q, pos, cos_sin, int(H), int(Dh), False)
@@ -832,8 +819,6 @@ class QKVRopeFn(torch.autograd.Function):
     nq, nk = H * Dh, Hkv * Dh
     ref_t = next(g for g in (dq, dk, dv) if g is not None)
     dqkv = torch.empty(ref_t.shape[0], W, dtype=ref_t.dtype, device=ref_t.device)
-    if EXP_NO_ROPE:
-      return dqkv, None, None, None, None, None
     for g, lo, n, nh in ((dq, 0, nq, H), (dk, nq, nk, Hkv)):
       if g is None:
         dqkv[:, lo:lo + n].zero_()
