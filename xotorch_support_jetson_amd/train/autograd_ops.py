@@ -485,6 +485,8 @@ def dw_tn(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor, accumulate: bool
     dy = dy.contiguous()
   if x.stride(1) != 1 or x.stride(0) % 8:
     x = x.contiguous()
+  if dy.shape[0] * max(dy.stride(0), x.stride(0)) * 2 >= (1 << 31):  # the tile's 32-bit LDS-DMA byte offsets
+    return False
   require().gemm_tn(dy, x, out, accumulate)
   return True
 
