@@ -9,6 +9,8 @@ for what in "$@"; do
   case $what in
     bench)  XOT_GEMM_TABLE=$T step r6/bench 400 python -u bench.py --steps 20 --warmup 5 ;;
     bench2) XOT_GEMM_TABLE=$T step r6/bench2 400 python -u bench.py --steps 20 --warmup 5 ;;
+    bench_w4) cp tools/gpu/tables/decode_w4.json "$O/r6/t_w4.json" && XOT_GEMM_TABLE=$O/r6/t_w4.json step r6/bench_w4 400 python -u bench.py --steps 20 --warmup 5 ;;
+    bench_w4gu) cp tools/gpu/tables/decode_w4_gateup.json "$O/r6/t_w4gu.json" && XOT_GEMM_TABLE=$O/r6/t_w4gu.json step r6/bench_w4gu 400 python -u bench.py --steps 20 --warmup 5 ;;
     reduce) step r6/reduce 120 python -u tools/bench_reduce.py ;;
     attn)   step r6/attn 200 python -u tools/bench_attn_b512.py ;;
     attn_small) step r6/attn_small 300 python -u tools/bench_attn_small.py ;;
