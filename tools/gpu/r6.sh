@@ -34,6 +34,9 @@ for what in "$@"; do
     trainprof) prof r6/trainprof 900 python3 "$R/tools/bench_train.py" --mb 2 --microbatches 4 --steps 3 --warmup 1
             step r6/trainstep 60 python tools/step_window.py "$(ls "$O"/r6/trainprof/*/*kernel_trace.csv "$O"/r6/trainprof/*kernel_trace.csv 2>/dev/null | head -1)" ;;
     relayout_test) step r6/relayout_test 300 python -u -m pytest tests/test_kernels_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread -k relayout ;;
+    attn_train) step r6/attn_train_test 300 python -u -m pytest tests/test_kernels_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread -k "attention_train or deepseek" &&
+                step r6/attn_train 200 python -u tools/bench_attn_train.py --reps 30 &&
+                prof r6/attn_train_prof 200 python3 "$R/tools/bench_attn_train.py" --reps 10 ;;
     tests)  step r6/gpu_tests 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
     *) echo "unknown case $what"; exit 2 ;;
   esac

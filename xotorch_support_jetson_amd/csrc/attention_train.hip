@@ -599,6 +599,51 @@ __global__ __launch_bounds__(64 * DKW) void attn_train_dkdv_v2_kernel(const uint
 #pragma unroll
   for (int dt = 0; dt < NDT; ++dt) dkT[dt] = dvT[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // The row constants ride in as the accumulators' initial values (LDS: -lse2 / sl, -delta per query row), so
+  // S' = Q.K^T - lse2 / sl and dP' = dO.V^T - delta leave their MFMA chains ready: p = exp2(sl S') and
+  // dS = p dP' cost one multiply each.  Only tiles that straddle the diagonal or the sequence end are masked.
+  const float isl = 1.f / sl;
+  auto tile = [&](const int q0, auto masked) {
+    constexpr bool MASK = decltype(masked)::value;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {  // 32 queries: sub-tiles 2 kk and 2 kk + 1
+      uint32_t pw[4], sw[4];
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt) {
+        const int t = 2 * kk + tt;
+        f32x4 st = *reinterpret_cast<const f32x4*>(ld_ + 16 * t + 4 * g);
+        f32x4 dpt = *reinterpret_cast<const f32x4*>(ld_ + TT + 16 * t + 4 * g);
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          st = mfma16(ld16(qs + (16 * t + c) * RLD + 32 * s + 8 * g), kf[s], st);
+          dpt = mfma16(ld16(ds_ + (16 * t + c) * RLD + 32 * s + 8 * g), vf[s], dpt);
+        }
+        float p[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          p[r] = __builtin_amdgcn_exp2f(st[r] * sl);
+          if constexpr (MASK) {
+            const int qi = q0 + 16 * t + 4 * g + r;
+            if (!(key <= qi && qi < L)) p[r] = 0.f;
+          }
+        }
+        pw[2 * tt] = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t{p[0], p[1]}), bf16x2_t));
+        pw[2 * tt + 1] = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t{p[2], p[3]}), bf16x2_t));
+        sw[2 * tt] = __builtin_bit_cast(uint32_t,
+                                        __builtin_convertvector((f32x2_t{p[0] * dpt[0], p[1] * dpt[1]}), bf16x2_t));
+        sw[2 * tt + 1] = __builtin_bit_cast(uint32_t,
+                                            __builtin_convertvector((f32x2_t{p[2] * dpt[2], p[3] * dpt[3]}), bf16x2_t));
+      }
+      const s16x8 pa = __builtin_bit_cast(s16x8, u32x4{pw[0], pw[1], pw[2], pw[3]});
+      const s16x8 sa = __builtin_bit_cast(s16x8, u32x4{sw[0], sw[1], sw[2], sw[3]});
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) {
+        dvT[dt] = mfma16(tr_frag(ds_, RLD, kk, dt, g, c), pa, dvT[dt]);
+        dkT[dt] = mfma16(tr_frag(qs, RLD, kk, dt, g, c), sa, dkT[dt]);
+      }
+    }
+  };
+
   if (iters > 0) load(0);
   for (int it = 0; it < iters; ++it) {
     const int q0 = (qt0 + it % per) * TT;
@@ -606,39 +651,15 @@ __global__ __launch_bounds__(64 * DKW) void attn_train_dkdv_v2_kernel(const uint
     qr.template store<RLD>(qs);
     dr.template store<RLD>(ds_);
     if (threadIdx.x < TT) {
-      ld_[threadIdx.x] = lsv;
-      ld_[TT + threadIdx.x] = dlv;
+      ld_[threadIdx.x] = -lsv * isl;
+      ld_[TT + threadIdx.x] = -dlv;
     }
     __syncthreads();
     if (it + 1 < iters) load(it + 1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {  // 32 queries: sub-tiles 2 kk and 2 kk + 1
-      s16x8 pa, sa;
-#pragma unroll
-      for (int tt = 0; tt < 2; ++tt) {
-        const int t = 2 * kk + tt;
-        f32x4 st = f32x4{0.f, 0.f, 0.f, 0.f}, dpt = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s = 0; s < KS; ++s) {
-          st = mfma16(ld16(qs + (16 * t + c) * RLD + 32 * s + 8 * g), kf[s], st);
-          dpt = mfma16(ld16(ds_ + (16 * t + c) * RLD + 32 * s + 8 * g), vf[s], dpt);
-        }
-        const f32x4 lq = *reinterpret_cast<const f32x4*>(ld_ + 16 * t + 4 * g);
-        const f32x4 dq = *reinterpret_cast<const f32x4*>(ld_ + TT + 16 * t + 4 * g);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int qi = q0 + 16 * t + 4 * g + r;
-          const float p = (key <= qi && qi < L) ? exp2f(st[r] * sl - lq[r]) : 0.f;
-          pa[4 * tt + r] = (short)f2bf(p);
-          sa[4 * tt + r] = (short)f2bf(p * (dpt[r] - dq[r]));
-        }
-      }
-#pragma unroll
-      for (int dt = 0; dt < NDT; ++dt) {
-        dvT[dt] = mfma16(tr_frag(ds_, RLD, kk, dt, g, c), pa, dvT[dt]);
-        dkT[dt] = mfma16(tr_frag(qs, RLD, kk, dt, g, c), sa, dkT[dt]);
-      }
-    }
+    if (q0 >= krow + 15 && q0 + TT <= L)  // wave-uniform: every query of the tile sees all 16 keys of this wave
+      tile(q0, std::false_type{});
+    else
+      tile(q0, std::true_type{});
   }
   if (key >= L) return;
   const long slab = (long)hh * ((long)gridDim.z * L) * (Hkv * DH);
@@ -704,6 +725,44 @@ __global__ __launch_bounds__(256) void attn_train_dq_v2_kernel(const uint16_t* _
 #pragma unroll
   for (int dt = 0; dt < NDT; ++dt) dqT[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // row constants as the accumulators' initial values (the dK / dV kernel's scheme; here they are lane scalars):
+  // p = exp2(sl (S - lse2 / sl)), dS = p (dP - delta); only the diagonal tile is masked
+  const float sc0 = -lse / sl;
+  const f32x4 sinit = f32x4{sc0, sc0, sc0, sc0}, dinit = f32x4{-dsum, -dsum, -dsum, -dsum};
+  auto tile = [&](const int k0, auto masked) {
+    constexpr bool MASK = decltype(masked)::value;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {  // 32 keys: sub-tiles 2 kk and 2 kk + 1
+      uint32_t sw[4];
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt) {
+        const int t = 2 * kk + tt;
+        f32x4 sc = sinit, dp = dinit;
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          sc = mfma16(ld16(ks + (16 * t + c) * KLD + 32 * s + 8 * g), qf[s], sc);
+          dp = mfma16(ld16(vs + (16 * t + c) * KLD + 32 * s + 8 * g), df[s], dp);
+        }
+        float d[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float p = __builtin_amdgcn_exp2f(sc[r] * sl);
+          if constexpr (MASK) {
+            const int key = k0 + 16 * t + 4 * g + r;
+            if (!(key <= qi && key < L)) p = 0.f;
+          }
+          d[r] = p * dp[r];
+        }
+        sw[2 * tt] = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t{d[0], d[1]}), bf16x2_t));
+        sw[2 * tt + 1] = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t{d[2], d[3]}), bf16x2_t));
+      }
+      const s16x8 sa = __builtin_bit_cast(s16x8, u32x4{sw[0], sw[1], sw[2], sw[3]});
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+        dqT[dt] = mfma16(tr_frag(ks, KLD, kk, dt, g, c), sa, dqT[dt]);
+    }
+  };
+
   for (int kt = 0; kt <= qt; ++kt) {
     const int k0 = kt * TT;
     __syncthreads();
@@ -713,29 +772,9 @@ __global__ __launch_bounds__(256) void attn_train_dq_v2_kernel(const uint16_t* _
     if (kt < qt) {
       kr.load(Kb, ldk, k0 + TT, L);
       vr.load(Vb, ldv, k0 + TT, L);
-    }
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {  // 32 keys: sub-tiles 2 kk and 2 kk + 1
-      s16x8 sa;
-#pragma unroll
-      for (int tt = 0; tt < 2; ++tt) {
-        const int t = 2 * kk + tt;
-        f32x4 sc = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s = 0; s < KS; ++s) {
-          sc = mfma16(ld16(ks + (16 * t + c) * KLD + 32 * s + 8 * g), qf[s], sc);
-          dp = mfma16(ld16(vs + (16 * t + c) * KLD + 32 * s + 8 * g), df[s], dp);
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int key = k0 + 16 * t + 4 * g + r;
-          const float p = (key <= qi && key < L) ? exp2f(sc[r] * sl - lse) : 0.f;
-          sa[4 * tt + r] = (short)f2bf(p * (dp[r] - dsum));
-        }
-      }
-#pragma unroll
-      for (int dt = 0; dt < NDT; ++dt)
-        dqT[dt] = mfma16(tr_frag(ks, KLD, kk, dt, g, c), sa, dqT[dt]);
+      tile(k0, std::false_type{});  // every key of a tile below the diagonal precedes every query of this one
+    } else {
+      tile(k0, std::true_type{});
     }
   }
   if (qi >= L) return;
