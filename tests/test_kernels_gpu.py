@@ -458,6 +458,45 @@ def test_gemm_stream(gpu, M, epi, ntw, splits):
     assert rel_err(y2, ref) < 1e-2
 
 
+@pytest.mark.parametrize("Kd,N,epi,ntw,splits,s_in,with_bias", [
+    (2048, 1024, "none", 1, 4, 4, False), (2048, 1024, "none", 2, 2, 2, True), (4096, 2048, "silu", 2, 1, 4, False),
+    (4096, 2048, "silu", 2, 4, 1, True), (8192, 1024, "none", 2, 4, 8, False), (4096, 768, "none", 1, 1, 3, False)])
+def test_gemm_stream_norm(gpu, Kd, N, epi, ntw, splits, s_in, with_bias):
+  """Batch-1 GEMM with the RMSNorm of a pending split-K residual sum in its prologue (gemm_stream_norm) against the
+  unfused pair (splitk_resid_rmsnorm, then gemm_stream on its output): the same arithmetic in the same order, so
+  the summed residual row and the GEMM output are bitwise equal."""
+  from xotorch_support_jetson_amd.ops._ext import require
+  from xotorch_support_jetson_amd.ops.weights_layout import shuffle_for_stream
+  C = require()
+  torch.manual_seed(Kd + N + s_in)
+  h = torch.randn(1, Kd, device=gpu, dtype=torch.bfloat16)
+  ws_in = torch.randn(s_in * Kd, device=gpu, dtype=torch.float32) * 0.3
+  bias_in = torch.randn(Kd, device=gpu, dtype=torch.bfloat16) if with_bias else None
+  lnw = (1 + 0.1 * torch.randn(Kd, device=gpu)).to(torch.bfloat16)
+  w = shuffle_for_stream(torch.randn(N, Kd, device=gpu, dtype=torch.bfloat16) / math.sqrt(Kd))
+  b = torch.randn(N, device=gpu, dtype=torch.bfloat16) if with_bias else None
+  ncol = N // 2 if epi == "silu" else N
+  # unfused: slab reduce + residual + norm, then the stream GEMM on the normalised row
+  h_ref = h.clone()
+  xn = torch.empty_like(h)
+  C.splitk_resid_rmsnorm(ws_in, s_in, bias_in, h_ref, lnw, xn, 1e-5)
+  ws = torch.empty(max(splits, 1) * N, device=gpu, dtype=torch.float32)
+  y_ref = torch.empty(1, ncol, device=gpu, dtype=torch.bfloat16)
+  C.gemm_stream(xn, w, y_ref, b, None, ws, K.EPI[epi], ntw, splits, True)
+  # fused
+  hout = torch.full_like(h, 7.0)
+  y = torch.empty_like(y_ref)
+  C.gemm_stream_norm(w, y, b, torch.empty_like(ws), K.EPI[epi], ntw, splits, True, h, ws_in, s_in, bias_in, lnw, hout,
+                     1e-5)
+  assert torch.equal(hout, h_ref)
+  assert torch.equal(y, y_ref), (y.float() - y_ref.float()).abs().max().item()
+  # the residual buffer the prologue read is untouched
+  h2 = h.clone()
+  C.gemm_stream_norm(w, y, b, torch.empty_like(ws), K.EPI[epi], ntw, splits, True, h, ws_in, s_in, bias_in, lnw, hout,
+                     1e-5)
+  assert torch.equal(h, h2)
+
+
 def test_fp8_layout_roundtrip(gpu):
   from xotorch_support_jetson_amd.ops.weights_layout import (dequant_stream8, quantize_fp8_rows, shuffle_for_stream8,
                                                              unshuffle_from_stream8)

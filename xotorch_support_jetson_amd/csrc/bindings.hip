@@ -275,6 +275,59 @@ void gemm_stream(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const 
          " splits=", splits);
 }
 
+// Batch-1 decode GEMM on pre-shuffled weights whose input row is rmsnorm(bf16(h + bias_in + sum of the S_in slabs of
+// ws_in)) * lnw, computed in the GEMM's prologue; the summed residual row is stored to hout (!= h).  y = [1, N] (epi 0)
+// or [1, N / 2] (epi 2, SiLU * up); splits > 1 writes fp32 slabs into ws (!= ws_in), reduced unless reduce = false.
+void gemm_stream_norm(const at::Tensor& w, at::Tensor& y, const c10::optional<at::Tensor>& bias,
+                      const c10::optional<at::Tensor>& ws, int64_t epi, int64_t ntw, int64_t splits, bool reduce,
+                      const at::Tensor& h, const c10::optional<at::Tensor>& ws_in, int64_t s_in,
+                      const c10::optional<at::Tensor>& bias_in, const at::Tensor& lnw, at::Tensor& hout, double eps) {
+  CHECK_BF16(w);
+  CHECK_BF16(h);
+  CHECK_BF16(lnw);
+  CHECK_BF16(hout);
+  CHECK_GPU(y);
+  XCHECK(w.dim() == 2 && w.is_contiguous(), "gemm_stream_norm: w");
+  const int64_t N = w.size(0), K = w.size(1);
+  XCHECK(h.dim() == 2 && h.size(0) == 1 && h.size(1) == K && h.is_contiguous(), "gemm_stream_norm: h must be [1, K]");
+  XCHECK(hout.sizes() == h.sizes() && hout.is_contiguous() && hout.data_ptr() != h.data_ptr(),
+         "gemm_stream_norm: hout must be a distinct [1, K] buffer");
+  XCHECK(lnw.numel() == K && lnw.is_contiguous(), "gemm_stream_norm: lnw");
+  XCHECK(y.scalar_type() == at::kBFloat16 && y.dim() == 2 && y.size(0) == 1 && y.size(1) == (epi == 2 ? N / 2 : N) &&
+             y.stride(1) == 1,
+         "gemm_stream_norm: y");
+  if (bias.has_value()) {
+    CHECK_BF16((*bias));
+    XCHECK(bias->numel() == N && bias->is_contiguous(), "gemm_stream_norm: bias");
+  }
+  if (bias_in.has_value()) {
+    CHECK_BF16((*bias_in));
+    XCHECK(bias_in->numel() == K && bias_in->is_contiguous(), "gemm_stream_norm: bias_in");
+  }
+  float* wsp = nullptr;
+  long ws_elems = 0;
+  if (ws.has_value()) {
+    CHECK_GPU((*ws));
+    CHECK_DT((*ws), at::kFloat);
+    XCHECK(ws->is_contiguous(), "gemm_stream_norm: ws");
+    wsp = ws->data_ptr<float>();
+    ws_elems = ws->numel();
+  }
+  xot::NormPro np{bf(h), nullptr, K, (int)s_in, bf_opt(bias_in), bf(lnw), bf(hout), (float)eps, (int)K};
+  if (s_in > 0) {
+    XCHECK(ws_in.has_value(), "gemm_stream_norm: ws_in");
+    CHECK_GPU((*ws_in));
+    CHECK_DT((*ws_in), at::kFloat);
+    XCHECK(ws_in->is_contiguous() && ws_in->numel() >= s_in * K, "gemm_stream_norm: ws_in holds s_in slabs of K");
+    np.ws = ws_in->data_ptr<float>();
+  }
+  const int rc = xot::launch_gemm_stream_norm(bf(w), bf_opt(bias), y.data_ptr(), (int)y.stride(0), (int)epi, wsp,
+                                              ws_elems, (int)N, (int)K, (int)ntw, (int)splits, reduce, np,
+                                              cur_stream());
+  XCHECK(rc == 0, "gemm_stream_norm: unsupported N=", N, " K=", K, " epi=", epi, " ntw=", ntw, " splits=", splits,
+         " s_in=", s_in);
+}
+
 // Decode GEMM on FP8 (e4m3) pre-shuffled weights w8 [N, K] uint8 with per-row fp32 scales (y = x . (w8 * s)^T).
 void gemm_stream8(const at::Tensor& x, const at::Tensor& w8, const at::Tensor& wscale, at::Tensor& y,
                   const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& res,
@@ -930,6 +983,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_stream", &gemm_stream, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("bias"), py::arg("res"),
         py::arg("ws"), py::arg("epi"), py::arg("ntw"), py::arg("splits"), py::arg("wshuf"),
         py::arg("reduce") = true);
+  m.def("gemm_stream_norm", &gemm_stream_norm, py::arg("w"), py::arg("y"), py::arg("bias"), py::arg("ws"),
+        py::arg("epi"), py::arg("ntw"), py::arg("splits"), py::arg("reduce"), py::arg("h"), py::arg("ws_in"),
+        py::arg("s_in"), py::arg("bias_in"), py::arg("lnw"), py::arg("hout"), py::arg("eps"));
   m.def("gemm_stream8", &gemm_stream8, py::arg("x"), py::arg("w8"), py::arg("wscale"), py::arg("y"), py::arg("bias"),
         py::arg("res"), py::arg("ws"), py::arg("epi"), py::arg("ntw"), py::arg("splits"), py::arg("reduce") = true);
   m.def("relayout", &relayout, py::arg("src"), py::arg("dst"), py::arg("mode"));

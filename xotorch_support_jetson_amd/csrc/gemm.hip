@@ -203,7 +203,8 @@ int launch_gemm_skinny(const uint16_t* X, int ldx, const uint16_t* W, int ldw, c
 // (bytes 0-7) and 64 h + 32 + 8 g .. +8 (bytes 8-15): one 1 KB wave load carries two MFMA k-steps, half
 // the bytes of the bf16 layout.  v_cvt_scalef32_pk_bf16_fp8 widens each fragment just before its MFMAs;
 // the row scale is applied to the fp32 accumulators (so split-K slabs are already scaled).
-template <int MT, int NTW, int KS, int EPI, bool OUT_F32, bool SPLIT, bool WSHUF, int OCC, int MOE, bool W8 = false>
+template <int MT, int NTW, int KS, int EPI, bool OUT_F32, bool SPLIT, bool WSHUF, int OCC, int MOE, bool W8 = false,
+          bool NORM = false>
 __global__ __launch_bounds__(256, OCC) void gemm_stream_kernel(const uint16_t* __restrict__ X, int ldx,
                                                              const uint16_t* __restrict__ W, int ldw,
                                                              const uint16_t* __restrict__ bias,
@@ -214,7 +215,7 @@ __global__ __launch_bounds__(256, OCC) void gemm_stream_kernel(const uint16_t* _
                                                              const int* __restrict__ moe_gather,
                                                              int* __restrict__ tickets, long ysplit,
                                                              const float* __restrict__ wscale, long xbat,
-                                                             long ybat) {
+                                                             long ybat, NormPro np) {
   constexpr int KC = 32 * KS;
   static_assert(!W8 || (WSHUF && (KS == 4 || KS == 8) && MOE == 0),
                 "FP8 weights: pre-shuffled 128- or 256-deep chunks, dense GEMM");
@@ -358,8 +359,92 @@ __global__ __launch_bounds__(256, OCC) void gemm_stream_kernel(const uint16_t* _
   // DeepSeek-V2-Lite's 1408-wide experts) re-loads the last chunk where a pair would run past it (the
   // loads stay unconditional) and finishes with a single-chunk tail.
   const int last = nch - 1;
-  s16x8 xr[XPT];
   s16x8 wa[NTW][KS], wb[NTW][KS];
+  if constexpr (NORM) {
+    // RMSNorm prologue (one input row): the first two weight chunks are requested before it, so the HBM
+    // latency of the stream hides under the residual / slab reads (L2-resident: the producer just wrote them).
+    // Same arithmetic and reduction order as splitk_resid_rmsnorm_kernel<*, *, 256>, so the row is bitwise
+    // the one the unfused pair would give.
+    static_assert(MT == 1 && MOE == 0 && !W8 && WSHUF, "norm prologue: one row, pre-shuffled bf16 weights");
+    __shared__ float nred[NTH / 64];
+    uint16_t* x1 = xs_raw;  // this workgroup's K slice of the normalised row, [kper] bf16
+    wload(wa, 0);
+    wload(wb, min(1, last));
+    const int nchunk = np.D >> 3, c0 = kb >> 3, c1 = (kb + kper) >> 3;
+    const bool wg0 = blockIdx.x == 0 && blockIdx.y == 0;
+    float ss = 0.f;
+    for (int cc = tid; cc < nchunk; cc += NTH) {
+      const s16x8 a = ld16(np.h + cc * 8);
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = bf2f(a[j]);
+      if (np.bias != nullptr) {
+        const s16x8 bv = ld16(np.bias + cc * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] += bf2f(bv[j]);
+      }
+      f32x4 p[8][2];  // up to 8 slabs, requested together
+#pragma unroll
+      for (int sl = 0; sl < 8; ++sl)
+        if (sl < np.S) {
+          p[sl][0] = *reinterpret_cast<const f32x4*>(np.ws + sl * np.sstride + cc * 8);
+          p[sl][1] = *reinterpret_cast<const f32x4*>(np.ws + sl * np.sstride + cc * 8 + 4);
+        }
+#pragma unroll
+      for (int sl = 0; sl < 8; ++sl)
+        if (sl < np.S) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            v[j] += p[sl][0][j];
+            v[4 + j] += p[sl][1][j];
+          }
+        }
+      s16x8 hv;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        hv[j] = (short)f2bf(v[j]);
+        const float r = bf2f(hv[j]);
+        ss += r * r;
+      }
+      if (wg0) st16(np.hout + cc * 8, hv);
+      if (cc >= c0 && cc < c1) st16(x1 + (cc - c0) * 8, hv);
+    }
+    ss = wave_sum(ss);
+    if (lane == 0) nred[wave] = ss;
+    __syncthreads();
+    ss = 0.f;
+#pragma unroll
+    for (int k = 0; k < NTH / 64; ++k) ss += nred[k];
+    const float inv = rsqrtf(ss / (float)np.D + np.eps);
+    for (int cc = tid; cc < c1 - c0; cc += NTH) {
+      const s16x8 hv = ld16(x1 + cc * 8), wv = ld16(np.lnw + (c0 + cc) * 8);
+      s16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (short)f2bf(bf2f(hv[j]) * inv * bf2f(wv[j]));
+      st16(x1 + cc * 8, o);
+    }
+    __syncthreads();
+    // row 0 is the only real row: its A fragments come from the slice (natural k order of the pre-shuffled
+    // layout: lane group g holds k 32 s + 8 g .. +8), the other 15 MFMA rows are zero
+    auto compute_n = [&](const s16x8 (&wr)[NTW][KS], int ch) {
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const s16x8 a = c == 0 ? ld16(x1 + ch * KC + (4 * s + g) * 8) : s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int j = 0; j < NTW; ++j) acc[0][j] = mfma16(a, wr[j][s], acc[0][j]);
+      }
+    };
+    int ch = 0;
+    for (; ch + 2 < nch; ch += 2) {
+      compute_n(wa, ch);
+      wload(wa, ch + 2);
+      compute_n(wb, ch + 1);
+      wload(wb, min(ch + 3, last));
+    }
+    compute_n(wa, ch);
+    if (!(nch & 1)) compute_n(wb, ch + 1);
+  } else {
+  s16x8 xr[XPT];
   xload(xr, 0);
   wload(wa, 0);
   xstore(xr, 0);
@@ -417,6 +502,7 @@ __global__ __launch_bounds__(256, OCC) void gemm_stream_kernel(const uint16_t* _
     __syncthreads();
     compute(wb, 1);
   }
+  }  // !NORM
 
   if constexpr (W8) {
 #pragma unroll
@@ -505,7 +591,7 @@ static void stream_launch(const uint16_t* X, int ldx, const uint16_t* W, int ldw
       (void)attr;
     }
     kern<<<grid, 256, SMEM, st>>>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, nullptr, M, N, kper, mblocks, nullptr, nullptr,
-                                  nullptr, 0L, wscale, 0L, 0L);
+                                  nullptr, 0L, wscale, 0L, 0L, NormPro{});
   } else {
     auto kern = gemm_stream_kernel<MT, NTW, KS, EPI, F32, true, WSH, OCC, 0, W8>;
     if constexpr (SMEM > 65536) {
@@ -514,7 +600,7 @@ static void stream_launch(const uint16_t* X, int ldx, const uint16_t* W, int ldw
       (void)attr;
     }
     kern<<<grid, 256, SMEM, st>>>(X, ldx, W, ldw, bias, R, ldr, Y, ldy, ws, M, N, kper, mblocks, nullptr, nullptr,
-                                  nullptr, 0L, wscale, 0L, 0L);
+                                  nullptr, 0L, wscale, 0L, 0L, NormPro{});
     if (!reduce) return;  // slabs left for the consumer
     const int ncol = EPI == EPI_SILU ? N / 2 : N;
     long chunks = (long)M * (ncol / 8);
@@ -577,7 +663,7 @@ static void batched_launch(const uint16_t* X, int ldx, long xbat, const uint16_t
   dim3 grid(N / (64 * NTW) * mblocks, 1, B);
   gemm_stream_kernel<MT, NTW, KS, EPI_NONE, F32, false, true, OCC, 3><<<grid, 256, SMEM, st>>>(
       X, ldx, W, K, nullptr, nullptr, 0, Y, ldy, nullptr, M, N, K, mblocks, nullptr, nullptr, nullptr, 0L, nullptr,
-      xbat, ybat);
+      xbat, ybat, NormPro{});
 }
 
 // B independent GEMMs Y_e[M, N] = X_e[M, K] . W_e[N, K]^T on pre-shuffled weights W [B][N][K]
@@ -613,7 +699,7 @@ static void moe_launch(const uint16_t* X, int ldx, const uint16_t* W, void* Y, i
   dim3 grid(N / (64 * NTW) * mblocks, S, E);
   gemm_stream_kernel<MT, NTW, KS, EPI, F32, false, WSH, OCC, MOE><<<grid, 256, SMEM, st>>>(
       X, ldx, W, K, nullptr, nullptr, 0, Y, ldy, nullptr, max_rows, N, K / S, mblocks, off, gather, nullptr,
-      S > 1 ? ysplit : 0L, nullptr, 0L, 0L);
+      S > 1 ? ysplit : 0L, nullptr, 0L, 0L, NormPro{});
 }
 
 template <int EPI, bool F32, bool WSH, int MOE>
@@ -694,6 +780,46 @@ int launch_gemm_stream8(const uint16_t* X, int ldx, const uint8_t* W, const floa
     return out_f32 ? -1 : stream8_dispatch<EPI_RESID, false>(X, ldx, W, wscale, K, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, ntw, S, reduce, s);
   return out_f32 ? stream8_dispatch<EPI_NONE, true>(X, ldx, W, wscale, K, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, ntw, S, reduce, s)
                  : stream8_dispatch<EPI_NONE, false>(X, ldx, W, wscale, K, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, ntw, S, reduce, s);
+}
+
+template <int NTW, int EPI>
+static void stream_norm_launch(const uint16_t* W, const uint16_t* bias, void* Y, int ldy, float* ws, int N, int K,
+                               int S, bool reduce, const NormPro& np, hipStream_t st) {
+  const int kper = K / S;
+  const dim3 grid(N / (64 * NTW), S);
+  const size_t smem = (size_t)kper * 2;  // the normalised K slice (<= 16 KB at K = 8192)
+  if (S == 1) {
+    gemm_stream_kernel<1, NTW, 4, EPI, false, false, true, 2, 0, false, true><<<grid, 256, smem, st>>>(
+        nullptr, 0, W, K, bias, nullptr, 0, Y, ldy, nullptr, 1, N, kper, 1, nullptr, nullptr, nullptr, 0L, nullptr,
+        0L, 0L, np);
+    return;
+  }
+  gemm_stream_kernel<1, NTW, 4, EPI, false, true, true, 2, 0, false, true><<<grid, 256, smem, st>>>(
+      nullptr, 0, W, K, bias, nullptr, 0, Y, ldy, ws, 1, N, kper, 1, nullptr, nullptr, nullptr, 0L, nullptr, 0L, 0L,
+      np);
+  if (!reduce) return;
+  const int ncol = EPI == EPI_SILU ? N / 2 : N;
+  splitk_reduce_kernel<EPI, false><<<(ncol / 8 + 255) / 256, 256, 0, st>>>(ws, S, 1, N, bias, nullptr, 0, Y, ldy);
+}
+
+int launch_gemm_stream_norm(const uint16_t* W, const uint16_t* bias, void* Y, int ldy, int epi, float* ws,
+                            long ws_elems, int N, int K, int ntw, int S, bool reduce, const NormPro& np,
+                            hipStream_t s) {
+  if (epi != EPI_NONE && epi != EPI_SILU) return -1;
+  if (epi == EPI_SILU || ntw == 4) ntw = 2;  // one row: NTW 4 is never picked (stream_dispatch)
+  if (ntw != 1 && ntw != 2) return -1;
+  if (np.D != K || K % 8 != 0 || np.S < 0 || np.S > 8 || np.h == nullptr || np.lnw == nullptr || np.hout == nullptr)
+    return -1;
+  if (np.S > 0 && (np.ws == nullptr || np.sstride < K)) return -1;
+  if (S < 1 || N % (64 * ntw) != 0 || K % (S * 128) != 0 || (long)(K / S) * 2 > 65536) return -1;
+  if (S > 1 && (ws == nullptr || ws == np.ws || ws_elems < (long)S * N)) return -1;
+  if (epi == EPI_SILU)
+    stream_norm_launch<2, EPI_SILU>(W, bias, Y, ldy, ws, N, K, S, reduce, np, s);
+  else if (ntw == 1)
+    stream_norm_launch<1, EPI_NONE>(W, bias, Y, ldy, ws, N, K, S, reduce, np, s);
+  else
+    stream_norm_launch<2, EPI_NONE>(W, bias, Y, ldy, ws, N, K, S, reduce, np, s);
+  return 0;
 }
 
 int launch_gemm_stream(const uint16_t* X, int ldx, const uint16_t* W, int ldw, const uint16_t* bias,

@@ -33,6 +33,25 @@ int launch_gemm_skinny(const uint16_t* X, int ldx, const uint16_t* W, int ldw, c
 int launch_gemm_stream(const uint16_t* X, int ldx, const uint16_t* W, int ldw, const uint16_t* bias,
                        const uint16_t* R, int ldr, void* Y, int ldy, bool out_f32, int epi, float* ws, long ws_elems,
                        int M, int N, int K, int ntw, int S, bool wshuf, bool reduce, hipStream_t s);
+// Batch-1 decode GEMM whose input row is the RMSNorm of a residual projection's pending split-K sum:
+// x = rmsnorm(bf16(h + bias + sum_s ws[s])) * lnw, recomputed by every workgroup from the slabs (no separate
+// reduce + norm launch); workgroup (0, 0) stores the summed residual row to hout (never h itself: the other
+// workgroups are still reading h).  Pre-shuffled bf16 weights, epi none / silu, split-K into ws (a different
+// buffer from np.ws).
+struct NormPro {
+  const uint16_t* h;
+  const float* ws;
+  long sstride;
+  int S;
+  const uint16_t* bias;
+  const uint16_t* lnw;
+  uint16_t* hout;
+  float eps;
+  int D;
+};
+int launch_gemm_stream_norm(const uint16_t* W, const uint16_t* bias, void* Y, int ldy, int epi, float* ws,
+                            long ws_elems, int N, int K, int ntw, int S, bool reduce, const NormPro& np,
+                            hipStream_t s);
 // decode GEMM with weight-only FP8 (e4m3 pre-shuffled tiles + per-row fp32 scale), bf16 activations
 int launch_gemm_stream8(const uint16_t* X, int ldx, const uint8_t* W, const float* wscale, const uint16_t* bias,
                         const uint16_t* R, int ldr, void* Y, int ldy, bool out_f32, int epi, float* ws, long ws_elems,

@@ -28,7 +28,7 @@ import torch
 from ..inference.shard import Shard
 from ..ops import kernels as K
 from ..ops._ext import require
-from ..ops.linear import layout_of, linear, linear_resid_norm, linear_rope_kv, scratch
+from ..ops.linear import FUSE_NORM, PendingNorm, layout_of, linear, linear_resid_norm, linear_rope_kv, scratch
 from ..ops.rope import longrope_window, rope_shift, rope_table
 from .config import ModelConfig
 from .weights import ShardWeights, expert
@@ -191,15 +191,19 @@ class ShardModel:
       o = torch.bmm(o_lat.float(), lw.wuv.float().transpose(1, 2)).to(dt)
     return o.transpose(0, 1).reshape(T, H * dv)
 
-  def _mlp(self, xn: torch.Tensor, lw, h: torch.Tensor, next_norm: Optional[torch.Tensor], li: int = -1):
-    """h += MLP(xn) in place; returns rmsnorm(h) * next_norm (None if there is no following norm)."""
+  def _mlp(self, xn: torch.Tensor, lw, h: torch.Tensor, next_norm: Optional[torch.Tensor], li: int = -1,
+           defer_to: Optional[torch.Tensor] = None):
+    """h += MLP(xn) in place; returns rmsnorm(h) * next_norm (None if there is no following norm), or a
+    PendingNorm whose residual continues in defer_to (see linear_resid_norm)."""
     c = self.c
     if lw.router is None:
       act = linear(xn, lw.gu_w, epi="silu")
       if next_norm is not None:
-        return linear_resid_norm(act, lw.down_w, h, next_norm, c.rms_norm_eps)
+        return linear_resid_norm(act, lw.down_w, h, next_norm, c.rms_norm_eps, defer_to=defer_to)
       linear(act, lw.down_w, residual=h, epi="resid", out=h)
       return None
+    if isinstance(xn, PendingNorm):
+      xn = xn.materialize()
     out = self._moe(xn, lw, h, next_norm)
     if out is not None:  # the combine kernel also applied the following RMSNorm
       return out
@@ -333,6 +337,11 @@ class ShardModel:
     last = self.shard.is_last_layer()
     n = len(self.layer_ids)
     xn, _ = K.rmsnorm(h, w.layers[self.layer_ids[0]].ln1, c.rms_norm_eps) if n else (None, None)
+    # batch-1 decode: the split-K reduce + residual + RMSNorm after o_proj / down_proj is deferred into the next
+    # GEMM's prologue (ops.linear.PendingNorm); the residual stream then alternates between two row buffers
+    fuse = FUSE_NORM and h.is_cuda and h.shape[0] == 1 and not c.is_mla and n > 0
+    hb = (h, torch.empty_like(h)) if fuse else None
+    other = (lambda t: hb[1] if t is hb[0] else hb[0]) if fuse else (lambda t: None)
     for j, li in enumerate(self.layer_ids):
       lw = w.layers[li]
       if c.is_mla:
@@ -341,13 +350,18 @@ class ShardModel:
         # QKV projection + RoPE + paged KV write (split-K slabs reduced inside the RoPE kernel)
         q = linear_rope_kv(xn, lw.qkv_w, lw.qkv_b, inp.positions, self.cos_sin, inp.slots, self.kv.k[j],
                            self.kv.v[j], c.num_heads, c.num_kv_heads)
+        if isinstance(xn, PendingNorm):
+          h = xn.dst
         a = self._attention(q, j, inp).view(h.shape[0], c.num_heads * c.head_dim)
       # o_proj + residual + post-attention norm (one fused pass when the projection runs split-K)
-      xn = linear_resid_norm(a, lw.o_w, h, lw.ln2, c.rms_norm_eps)
+      xn = linear_resid_norm(a, lw.o_w, h, lw.ln2, c.rms_norm_eps,
+                             defer_to=other(h) if lw.router is None else None)
+      if isinstance(xn, PendingNorm):
+        h = xn.dst  # gate/up's prologue stores the summed residual there
       # the norm that follows this layer: the next layer's input norm, or the final norm (decode: every row
       # is a sequence's last token) -- fused into the down projection's reduce the same way
       nxt = w.layers[self.layer_ids[j + 1]].ln1 if j + 1 < n else (w.norm if last and inp.decode else None)
-      xn = self._mlp(xn, lw, h, nxt, li)
+      xn = self._mlp(xn, lw, h, nxt, li, defer_to=other(h) if j + 1 < n else None)
     if not last:
       return h
     if not inp.decode or n == 0:

@@ -122,16 +122,18 @@ class _Scratch:
     self.ws: Dict[int, torch.Tensor] = {}
     self.retired: list = []
 
-  def splitk(self, device, n: int) -> torch.Tensor:
-    idx = device.index or 0
-    t = self.ws.get(idx)
+  def splitk(self, device, n: int, slot: int = 0) -> torch.Tensor:
+    """slot 1 holds the slabs of a residual projection whose reduce is deferred into the next GEMM (PendingNorm),
+    which writes its own slabs to slot 0 while it still reads slot 1."""
+    key = (device.index or 0, slot)
+    t = self.ws.get(key)
     if t is None or t.numel() < n:
       if torch.cuda.is_current_stream_capturing():
         raise RuntimeError("split-K workspace must be sized before graph capture")
       if t is not None:
         self.retired.append(t)
       t = torch.empty(max(n, 1 << 20, 2 * (t.numel() if t is not None else 0)), dtype=torch.float32, device=device)
-      self.ws[idx] = t
+      self.ws[key] = t
     return t
 
 
@@ -559,8 +561,66 @@ def _blas(x, w, bias, residual, epi, out, out_dtype):
   return y
 
 
+# XOT_FUSE_NORM=0: batch-1 decode keeps the separate split-K reduce + residual + RMSNorm launch after o_proj /
+# down_proj (fused: the next GEMM recomputes the norm of the pending slabs in its prologue, csrc/gemm.hip NORM)
+FUSE_NORM = os.environ.get("XOT_FUSE_NORM", "1") != "0"
+
+
+class PendingNorm:
+  """rmsnorm(bf16(src + bias + sum of the S fp32 slabs in ws)) * ln_w, not computed yet.
+
+  A residual projection of a batch-1 decode step (linear_resid_norm with defer_to) leaves its split-K slabs; the
+  next GEMM (linear with epi none / silu, linear_rope_kv) folds the slab sum, the residual add and the RMSNorm into
+  its prologue (gemm_stream_norm) and stores the summed residual row into dst -- a buffer distinct from src, since
+  every workgroup of that GEMM reads src.  Any other consumer calls materialize(), the unfused kernel, which
+  leaves the same residual in dst.  After either, dst is the residual stream."""
+
+  __slots__ = ("src", "dst", "ws", "S", "bias", "ln_w", "eps")
+
+  def __init__(self, src, dst, ws, S, bias, ln_w, eps):
+    self.src, self.dst, self.ws, self.S, self.bias, self.ln_w, self.eps = src, dst, ws, S, bias, ln_w, float(eps)
+
+  @property
+  def shape(self):
+    return self.src.shape
+
+  def materialize(self) -> torch.Tensor:
+    if self.dst.data_ptr() != self.src.data_ptr():
+      self.dst.copy_(self.src)
+    out = torch.empty_like(self.dst)
+    require().splitk_resid_rmsnorm(self.ws, self.S, self.bias, self.dst, self.ln_w, out, self.eps)
+    return out
+
+  def run(self, w: torch.Tensor, y: torch.Tensor, bias, epi: str, ntw: int, S: int, reduce: bool) -> None:
+    ws = scratch.splitk(y.device, S * w.shape[0]) if S > 1 else None
+    require().gemm_stream_norm(w, y, bias, ws, K.EPI[epi], ntw, S, reduce, self.src, self.ws, self.S, self.bias,
+                               self.ln_w, self.dst, self.eps)
+
+
+def _pending_cfg(p: PendingNorm, w: torch.Tensor, bias, epi: str):
+  """The stream configuration the consumer GEMM of a pending norm runs (tuned on the unfused kernel with the
+  residual row as a stand-in input), or None when the fused kernel does not cover it."""
+  if layout_of(w) != "stream" or epi not in ("none", "silu") or w.shape[1] != p.src.shape[1]:
+    return None
+  cfg = policy.shuffled_cfg(p.src, w, bias, None, epi, torch.bfloat16)
+  if cfg[0] != "stream" or w.shape[1] % (cfg[2] * 128) or (w.shape[1] // cfg[2]) * 2 > 65536:
+    return None
+  return cfg
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, residual: torch.Tensor | None = None,
            epi: str = "none", out: torch.Tensor | None = None, out_dtype: torch.dtype | None = None) -> torch.Tensor:
+  if isinstance(x, PendingNorm):
+    cfg = None if (residual is not None or (out_dtype not in (None, torch.bfloat16))
+                   or (out is not None and out.dtype != torch.bfloat16)) else _pending_cfg(x, w, bias, epi)
+    if cfg is None:
+      x = x.materialize()
+    else:
+      if out is None:
+        out = torch.empty(1, w.shape[0] // 2 if epi == "silu" else w.shape[0], dtype=torch.bfloat16,
+                          device=x.src.device)
+      x.run(w, out, bias, epi, cfg[1], cfg[2], True)
+      return out
   if not x.is_cuda:
     return K.gemm(x, to_rowmajor(w), bias=bias, residual=residual, epi=epi, out=out, out_dtype=out_dtype)
   dt = out_dtype or (out.dtype if out is not None else x.dtype)
@@ -582,16 +642,25 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, r
 
 
 def linear_resid_norm(x: torch.Tensor, w: torch.Tensor, h: torch.Tensor, ln_w: torch.Tensor, eps: float,
-                      bias: torch.Tensor | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
+                      bias: torch.Tensor | None = None, out: torch.Tensor | None = None,
+                      defer_to: torch.Tensor | None = None):
   """h += x @ w.T (+ bias) in place (the residual stream) and return rmsnorm(h) * ln_w.
 
   When the projection runs split-K on the pre-shuffled layout, the GEMM leaves its fp32 slabs and one
-  kernel does the slab reduce, the residual add and the RMSNorm (instead of reduce + norm kernels)."""
+  kernel does the slab reduce, the residual add and the RMSNorm (instead of reduce + norm kernels).
+  defer_to (a second residual buffer, one row): return a PendingNorm instead -- the slabs stay for the next
+  GEMM's prologue, and the residual stream continues in defer_to (h is left as it was)."""
   if x.is_cuda and layout_of(w) == "stream":
     if x.stride(1) != 1 or x.stride(0) % 8:
       x = x.contiguous()
     M, N = x.shape[0], w.shape[0]
     cfg = policy.shuffled_cfg(x, w, bias, h, "resid", h.dtype)
+    if (defer_to is not None and FUSE_NORM and M == 1 and cfg[0] == "stream" and 1 < cfg[2] <= 8 and out is None
+        and h.is_contiguous() and h.dtype == torch.bfloat16):
+      S = cfg[2]
+      ws = scratch.splitk(x.device, S * M * N, slot=1)
+      require().gemm_stream(x, w, h, None, h, ws, K.EPI["resid"], cfg[1], S, True, False)
+      return PendingNorm(h, defer_to, ws, S, bias, ln_w, eps)
     if cfg[0] in ("stream", "big") and cfg[2] > 1:
       S = cfg[2]
       ws = scratch.splitk(x.device, S * M * N)
@@ -615,7 +684,21 @@ def linear_rope_kv(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None, 
   """qkv = x @ w.T (+ bias); returns rope(q) [T, H, Dh] and writes rope(k), v into the paged caches.
 
   When the QKV projection runs split-K on the pre-shuffled layout, its fp32 slabs go straight to one
-  kernel that sums them, rotates and writes q / the caches (no bf16 qkv round trip, one launch less)."""
+  kernel that sums them, rotates and writes q / the caches (no bf16 qkv round trip, one launch less).
+  x may be a PendingNorm: the projection then computes its input row in its prologue."""
+  if isinstance(x, PendingNorm):
+    cfg = _pending_cfg(x, w, bias, "none")
+    if cfg is None or cfg[2] < 2:
+      x = x.materialize()
+    else:
+      S, N = cfg[2], w.shape[0]
+      y = torch.empty(1, N, dtype=torch.bfloat16, device=x.src.device)  # shape carrier only
+      x.run(w, y, None, "none", cfg[1], S, False)
+      Dh = k_cache.shape[-1]
+      q = torch.empty(1, H, Dh, dtype=torch.bfloat16, device=y.device)
+      ws = scratch.splitk(y.device, S * N)
+      require().splitk_rope_kv_write(ws, S, bias, pos, cos_sin, slots, q, k_cache, v_cache, int(H), int(Hkv))
+      return q
   if x.is_cuda and layout_of(w) == "stream":
     if x.stride(1) != 1 or x.stride(0) % 8:
       x = x.contiguous()
