@@ -460,7 +460,8 @@ def test_gemm_stream(gpu, M, epi, ntw, splits):
 
 @pytest.mark.parametrize("Kd,N,epi,ntw,splits,s_in,with_bias", [
     (2048, 1024, "none", 1, 4, 4, False), (2048, 1024, "none", 2, 2, 2, True), (4096, 2048, "silu", 2, 1, 4, False),
-    (4096, 2048, "silu", 2, 4, 1, True), (8192, 1024, "none", 2, 4, 8, False), (4096, 768, "none", 1, 1, 3, False)])
+    (4096, 2048, "silu", 2, 4, 1, True), (8192, 1024, "none", 2, 4, 4, False), (4096, 768, "none", 1, 1, 3, False),
+    (4096, 1024, "none", 2, 4, 8, True), (8192, 2048, "silu", 2, 1, 6, False)])
 def test_gemm_stream_norm(gpu, Kd, N, epi, ntw, splits, s_in, with_bias):
   """Batch-1 GEMM with the RMSNorm of a pending split-K residual sum in its prologue (gemm_stream_norm) against the
   unfused pair (splitk_resid_rmsnorm, then gemm_stream on its output): the same arithmetic in the same order, so

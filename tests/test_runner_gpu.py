@@ -490,28 +490,38 @@ def test_decode_tick_issues_no_host_sync(gpu):
 
 def test_batch1_fused_norm_decode_matches_unfused(gpu, monkeypatch):
   """Batch-1 decode with the split-K reduce + residual + RMSNorm deferred into the next GEMM's prologue
-  (ops.linear.PendingNorm, the default) against the unfused kernels on the same weights: two Llama-3-8B layers,
-  eager and HIP-graph decode, bitwise-equal logits and final hidden state, and the fused path really ran."""
+  (ops.linear.PendingNorm) and the attention's partition merge done in o_proj's prologue (kernels.PendingMerge),
+  the defaults, against the unfused kernels on the same weights: two Llama-3-8B layers, a 600-token context (split
+  over attention partitions), eager and HIP-graph decode, bitwise-equal logits, and both fused paths really ran."""
   import xotorch_support_jetson_amd.models.transformer as TM
+  from xotorch_support_jetson_amd.ops import kernels as KK
   from xotorch_support_jetson_amd.ops import linear as L
   c = preset("llama-3-8b").with_layers(2)
   sh = Shard("llama-3-8b", 0, 1, 2)
   w = random_weights(c, sh, gpu, seed=5)
-  runs = {"n": 0}
-  orig = L.PendingNorm.run
+  runs = {"norm": 0, "merge": 0}
+  orig_run, orig_attn = L.PendingNorm.run, KK.attn_decode
 
   def counted(self, *a, **k):
-    runs["n"] += 1
-    return orig(self, *a, **k)
+    runs["norm"] += 1
+    return orig_run(self, *a, **k)
+
+  def attn(*a, **k):
+    out = orig_attn(*a, **k)
+    runs["merge"] += isinstance(out, KK.PendingMerge)
+    return out
 
   monkeypatch.setattr(L.PendingNorm, "run", counted)
-  ids = torch.randint(0, c.vocab_size, (12,), generator=torch.Generator().manual_seed(1), dtype=torch.int32)
+  monkeypatch.setattr(KK, "attn_decode", attn)
+  P = 600
+  ids = torch.randint(0, c.vocab_size, (P,), generator=torch.Generator().manual_seed(1), dtype=torch.int32)
 
   def decode(fuse: bool, graphs: bool):
-    monkeypatch.setattr(L, "FUSE_NORM", fuse)
-    monkeypatch.setattr(TM, "FUSE_NORM", fuse)
-    r = ShardRunner(c, sh, gpu, weights=w, max_batch=4, max_ctx=128, use_graphs=graphs)
-    out = [r.forward(["a"], [12], ids).clone()]  # graph replays reuse the output buffer
+    for mod in (L, TM):
+      monkeypatch.setattr(mod, "FUSE_NORM", fuse)
+      monkeypatch.setattr(mod, "FUSE_MERGE", fuse)
+    r = ShardRunner(c, sh, gpu, weights=w, max_batch=4, max_ctx=1024, use_graphs=graphs)
+    out = [r.forward(["a"], [P], ids).clone()]  # graph replays reuse the output buffer
     tok = out[0].argmax(-1).int()
     for _ in range(4):
       out.append(r.forward(["a"], [1], tok).clone())
@@ -519,9 +529,9 @@ def test_batch1_fused_norm_decode_matches_unfused(gpu, monkeypatch):
     return out
 
   ref = decode(False, False)
-  assert runs["n"] == 0
+  assert runs == {"norm": 0, "merge": 0}
   for graphs in (False, True):
     got = decode(True, graphs)
-    assert runs["n"] > 0
+    assert runs["norm"] > 0 and runs["merge"] > 0, runs
     for a, b in zip(ref, got):
       assert torch.equal(a, b), (a.float() - b.float()).abs().max().item()

@@ -38,6 +38,7 @@ for what in "$@"; do
                 step r6/attn_train 200 python -u tools/bench_attn_train.py --reps 30 &&
                 prof r6/attn_train_prof 200 python3 "$R/tools/bench_attn_train.py" --reps 10 ;;
     fnorm_test) step r6/fnorm_test 400 python -u -m pytest tests/test_kernels_gpu.py tests/test_runner_gpu.py -m gpu -x -v --timeout 300 --timeout-method thread -k "gemm_stream_norm or fused_norm or test_gemm_stream or split_equals_full or llama70b_layers" ;;
+    b1_nomerge) XOT_FUSE_MERGE=0 step r6/b1_nomerge 300 python -u bench.py --model llama-3-8b --batch-per-gpu 1 --steps 64 --warmup 8 ;;
     b1_unfused) XOT_FUSE_NORM=0 step r6/b1_unfused 300 python -u bench.py --model llama-3-8b --batch-per-gpu 1 --steps 64 --warmup 8 ;;
     b1_fused) XOT_FUSE_NORM=1 step r6/b1_fused 300 python -u bench.py --model llama-3-8b --batch-per-gpu 1 --steps 64 --warmup 8 ;;
     fnorm_diag) step r6/fnorm_diag 300 python -u tools/diag/fused_norm_diag.py ;;

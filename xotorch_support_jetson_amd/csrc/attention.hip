@@ -435,11 +435,12 @@ __global__ __launch_bounds__(PF == 2 ? 512 : 256, PF == 2 ? 2 : 1) void attn_dec
 int launch_attn_decode(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, const int32_t* block_tables,
                        int max_blocks, const int32_t* ctx_lens, uint16_t* out, float* ws_o, float* ws_ml, int B,
                        int H, int Hkv, int Dh, int pages_per_part, int nparts, float scale, int num_pages, int algo,
-                       hipStream_t s) {
+                       hipStream_t s, bool merge) {
   // (an in-kernel merge by the last-arriving partition measured slower than the reduce launch in every
-  // configuration, profiles/bench_attn_small_r1.json, and was removed in round 6)
+  // configuration, profiles/bench_attn_small_r1.json, and was removed in round 6.)  merge = false: the
+  // partitions are left in ws_o / ws_ml for the consumer (launch_gemm_stream_merge's prologue at batch 1).
   int* tickets = nullptr;
-  const bool reduce = nparts > 1;
+  const bool reduce = nparts > 1 && merge;
   if (B <= 0) return 0;
   if (H % Hkv != 0 || H / Hkv > 16) return -1;
   dim3 grid(nparts, Hkv, B);
@@ -478,6 +479,15 @@ int launch_attn_decode(const uint16_t* q, const uint16_t* kc, const uint16_t* vc
     return -1;
   }
   return 0;
+}
+
+void launch_attn_decode_merge(const float* ws_o, const float* ws_ml, const int32_t* ctx_lens, uint16_t* out, int B,
+                              int H, int Dh, int nparts, int pages_per_part, hipStream_t s) {
+  if (B <= 0) return;
+  if (Dh == 128)
+    attn_decode_reduce_kernel<128><<<B * H, 128, 0, s>>>(ws_o, ws_ml, ctx_lens, out, H, nparts, pages_per_part);
+  else if (Dh == 64)
+    attn_decode_reduce_kernel<64><<<B * H, 64, 0, s>>>(ws_o, ws_ml, ctx_lens, out, H, nparts, pages_per_part);
 }
 
 // ============================================================================ prefill

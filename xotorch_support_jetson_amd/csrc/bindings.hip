@@ -713,7 +713,8 @@ void moe_combine_norm(const at::Tensor& y, const at::Tensor& slot_of, const at::
 
 void attn_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
                  const at::Tensor& block_tables, const at::Tensor& ctx_lens, at::Tensor& out, at::Tensor& ws_o,
-                 at::Tensor& ws_ml, int64_t pages_per_part, int64_t nparts, double scale, int64_t algo) {
+                 at::Tensor& ws_ml, int64_t pages_per_part, int64_t nparts, double scale, int64_t algo,
+                 bool merge) {
   CHECK_BF16(q);
   CHECK_BF16(k_cache);
   CHECK_BF16(v_cache);
@@ -738,8 +739,50 @@ void attn_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tenso
                                          (int)block_tables.size(1), ctx_lens.data_ptr<int32_t>(), bf(out),
                                          ws_o.data_ptr<float>(), ws_ml.data_ptr<float>(), (int)B, (int)H, (int)Hkv,
                                          (int)Dh, (int)pages_per_part, (int)nparts, (float)scale, (int)nb, (int)algo,
-                                         cur_stream());
+                                         cur_stream(), merge);
   XCHECK(rc == 0, "attn_decode: unsupported H=", H, " Hkv=", Hkv, " Dh=", Dh);
+}
+
+// the partition merge attn_decode(merge = false) left out: out [B, H, Dh] from ws_o / ws_ml
+void attn_decode_merge(const at::Tensor& ws_o, const at::Tensor& ws_ml, const at::Tensor& ctx_lens, at::Tensor& out,
+                       int64_t pages_per_part, int64_t nparts) {
+  CHECK_BF16(out);
+  CHECK_DT(ws_o, at::kFloat);
+  CHECK_DT(ws_ml, at::kFloat);
+  CHECK_DT(ctx_lens, at::kInt);
+  XCHECK(all_contig_gpu(ws_o, ws_ml, ctx_lens, out) && out.dim() == 3, "attn_decode_merge: contiguous GPU, out [B,H,Dh]");
+  const int64_t B = out.size(0), H = out.size(1), Dh = out.size(2);
+  XCHECK(Dh == 128 || Dh == 64, "attn_decode_merge: Dh");
+  XCHECK(ws_o.numel() >= B * H * nparts * Dh && ws_ml.numel() >= B * H * nparts * 2 && ctx_lens.numel() >= B,
+         "attn_decode_merge: workspace");
+  xot::launch_attn_decode_merge(ws_o.data_ptr<float>(), ws_ml.data_ptr<float>(), ctx_lens.data_ptr<int32_t>(), bf(out),
+                                (int)B, (int)H, (int)Dh, (int)nparts, (int)pages_per_part, cur_stream());
+}
+
+// o_proj of a batch-1 decode step on the pre-shuffled weight w [N, H*Dh], its input row merged from the attention's
+// partitions (ws_o / ws_ml, row 0) in the prologue; writes `splits` fp32 slabs into ws (no reduce)
+void gemm_stream_merge(const at::Tensor& w, at::Tensor& ws, int64_t ntw, int64_t splits, const at::Tensor& ws_o,
+                       const at::Tensor& ws_ml, const at::Tensor& ctx_lens, int64_t pages_per_part, int64_t nparts,
+                       int64_t Dh) {
+  CHECK_BF16(w);
+  CHECK_DT(ws, at::kFloat);
+  CHECK_DT(ws_o, at::kFloat);
+  CHECK_DT(ws_ml, at::kFloat);
+  CHECK_DT(ctx_lens, at::kInt);
+  XCHECK(all_contig_gpu(w, ws, ws_o, ws_ml, ctx_lens) && w.dim() == 2, "gemm_stream_merge: contiguous GPU tensors");
+  const int64_t N = w.size(0), K = w.size(1);
+  XCHECK(Dh > 0 && K % Dh == 0 && ws_o.numel() >= (K / Dh) * nparts * Dh && ws_ml.numel() >= (K / Dh) * nparts * 2,
+         "gemm_stream_merge: attention workspace");
+  xot::NormPro np{};
+  np.mo = ws_o.data_ptr<float>();
+  np.ml = ws_ml.data_ptr<float>();
+  np.ctx = ctx_lens.data_ptr<int32_t>();
+  np.nparts = (int)nparts;
+  np.ppp = (int)pages_per_part;
+  np.dh = (int)Dh;
+  const int rc = xot::launch_gemm_stream_merge(bf(w), ws.data_ptr<float>(), ws.numel(), (int)N, (int)K, (int)ntw,
+                                               (int)splits, np, cur_stream());
+  XCHECK(rc == 0, "gemm_stream_merge: unsupported N=", N, " K=", K, " ntw=", ntw, " splits=", splits);
 }
 
 // training attention: 2-D token-major views ([B*L, n*Dh] rows, unit inner stride; row strides may differ,
@@ -1008,7 +1051,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("splits") = 1);
   m.def("attn_decode", &attn_decode, py::arg("q"), py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"),
         py::arg("ctx_lens"), py::arg("out"), py::arg("ws_o"), py::arg("ws_ml"), py::arg("pages_per_part"),
-        py::arg("nparts"), py::arg("scale"), py::arg("algo") = 2);
+        py::arg("nparts"), py::arg("scale"), py::arg("algo") = 2, py::arg("merge") = true);
+  m.def("attn_decode_merge", &attn_decode_merge, py::arg("ws_o"), py::arg("ws_ml"), py::arg("ctx_lens"), py::arg("out"),
+        py::arg("pages_per_part"), py::arg("nparts"));
+  m.def("gemm_stream_merge", &gemm_stream_merge, py::arg("w"), py::arg("ws"), py::arg("ntw"), py::arg("splits"),
+        py::arg("ws_o"), py::arg("ws_ml"), py::arg("ctx_lens"), py::arg("pages_per_part"), py::arg("nparts"),
+        py::arg("Dh"));
   m.def("attn_prefill", &attn_prefill, py::arg("q"), py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"),
         py::arg("cu_q"), py::arg("ctx_lens"), py::arg("out"), py::arg("max_qlen"), py::arg("scale"), py::arg("algo") = 2);
   m.def("router_logits", &router_logits);

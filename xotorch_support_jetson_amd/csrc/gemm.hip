@@ -204,7 +204,7 @@ int launch_gemm_skinny(const uint16_t* X, int ldx, const uint16_t* W, int ldw, c
 // the bytes of the bf16 layout.  v_cvt_scalef32_pk_bf16_fp8 widens each fragment just before its MFMAs;
 // the row scale is applied to the fp32 accumulators (so split-K slabs are already scaled).
 template <int MT, int NTW, int KS, int EPI, bool OUT_F32, bool SPLIT, bool WSHUF, int OCC, int MOE, bool W8 = false,
-          bool NORM = false>
+          int NORM = 0, bool MERGE = false>
 __global__ __launch_bounds__(256, OCC) void gemm_stream_kernel(const uint16_t* __restrict__ X, int ldx,
                                                              const uint16_t* __restrict__ W, int ldw,
                                                              const uint16_t* __restrict__ bias,
@@ -360,54 +360,105 @@ __global__ __launch_bounds__(256, OCC) void gemm_stream_kernel(const uint16_t* _
   // loads stay unconditional) and finishes with a single-chunk tail.
   const int last = nch - 1;
   s16x8 wa[NTW][KS], wb[NTW][KS];
-  if constexpr (NORM) {
-    // RMSNorm prologue (one input row): the first two weight chunks are requested before it, so the HBM
-    // latency of the stream hides under the residual / slab reads (L2-resident: the producer just wrote them).
-    // Same arithmetic and reduction order as splitk_resid_rmsnorm_kernel<*, *, 256>, so the row is bitwise
-    // the one the unfused pair would give.
-    static_assert(MT == 1 && MOE == 0 && !W8 && WSHUF, "norm prologue: one row, pre-shuffled bf16 weights");
+  if constexpr (NORM > 0 || MERGE) {
+  static_assert(MT == 1 && MOE == 0 && !W8 && WSHUF, "row prologue: one row, pre-shuffled bf16 weights");
+  uint16_t* x1 = xs_raw;  // this workgroup's K slice of the input row, [kper] bf16
+  wload(wa, 0);
+  wload(wb, min(1, last));
+  if constexpr (MERGE) {
+    // split-KV decode attention merge (attn_decode_reduce_kernel's arithmetic, in its order) for the heads of
+    // this workgroup's K slice: o = sum_p 2^(m_p - M) o_p / sum_p 2^(m_p - M) l_p over the row's partitions
+    const int npages = (max(np.ctx[0], 0) + 63) / 64;
+    int npart = (npages + np.ppp - 1) / np.ppp;
+    npart = npart < 1 ? 1 : (npart > np.nparts ? np.nparts : npart);
+    for (int e = tid; e < kper; e += NTH) {
+      const int k = kb + e, hd = k / np.dh, d = k - hd * np.dh;
+      const size_t base = (size_t)hd * np.nparts;
+      float M = -1e30f;
+      for (int q = 0; q < npart; ++q) M = fmaxf(M, np.ml[(base + q) * 2]);
+      float L = 0.f, O = 0.f;
+      for (int q = 0; q < npart; ++q) {
+        const float f = exp2f(np.ml[(base + q) * 2] - M);
+        L += np.ml[(base + q) * 2 + 1] * f;
+        O += np.mo[(base + q) * np.dh + d] * f;
+      }
+      x1[e] = f2bf(L > 0.f ? O / L : 0.f);
+    }
+  } else {
+    // RMSNorm prologue (one input row; NORM = 16-B chunks of the row per thread): the first two weight chunks,
+    // then every residual / bias / norm-weight load and the first SMAX slabs are requested before any is used,
+    // so the chain is one L2 round trip per SMAX slabs (the producer just wrote them), one wave reduction and two
+    // barriers, under the weight stream's own HBM latency.  Same arithmetic and reduction order as
+    // splitk_resid_rmsnorm_kernel<*, *, 256>: the row is bitwise the one the unfused pair gives.
+    constexpr int PM = NORM, SMAX = NORM >= 4 ? 2 : 4;  // slabs per round trip (registers: PM x SMAX x 8)
     __shared__ float nred[NTH / 64];
-    uint16_t* x1 = xs_raw;  // this workgroup's K slice of the normalised row, [kper] bf16
-    wload(wa, 0);
-    wload(wb, min(1, last));
     const int nchunk = np.D >> 3, c0 = kb >> 3, c1 = (kb + kper) >> 3;
     const bool wg0 = blockIdx.x == 0 && blockIdx.y == 0;
-    float ss = 0.f;
-    for (int cc = tid; cc < nchunk; cc += NTH) {
-      const s16x8 a = ld16(np.h + cc * 8);
-      float v[8];
+    s16x8 ha[PM], ba[PM], la[PM];
+    f32x4 p[PM][SMAX][2];
+    // slabs s0 .. s0 + SMAX - 1 of this thread's chunks (all requested before any is added)
+    auto slabs = [&](int s0) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = bf2f(a[j]);
+      for (int i = 0; i < PM; ++i) {
+        const int cc = tid + NTH * i;
+        if (cc < nchunk) {
+#pragma unroll
+          for (int sl = 0; sl < SMAX; ++sl)
+            if (s0 + sl < np.S) {
+              const float* sp = np.ws + (s0 + sl) * np.sstride + cc * 8;
+              p[i][sl][0] = *reinterpret_cast<const f32x4*>(sp);
+              p[i][sl][1] = *reinterpret_cast<const f32x4*>(sp + 4);
+            }
+        }
+      }
+    };
+#pragma unroll
+    for (int i = 0; i < PM; ++i) {
+      const int cc = tid + NTH * i;
+      if (cc < nchunk) {
+        ha[i] = ld16(np.h + cc * 8);
+        if (np.bias != nullptr) ba[i] = ld16(np.bias + cc * 8);
+        if (cc >= c0 && cc < c1) la[i] = ld16(np.lnw + cc * 8);
+      }
+    }
+    slabs(0);
+    float v[PM][8];
+#pragma unroll
+    for (int i = 0; i < PM; ++i) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[i][j] = bf2f(ha[i][j]);
       if (np.bias != nullptr) {
-        const s16x8 bv = ld16(np.bias + cc * 8);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] += bf2f(bv[j]);
+        for (int j = 0; j < 8; ++j) v[i][j] += bf2f(ba[i][j]);
       }
-      f32x4 p[8][2];  // up to 8 slabs, requested together
+    }
+    for (int s0 = 0; s0 < np.S; s0 += SMAX) {  // one L2 round trip per SMAX slabs
+      if (s0 > 0) slabs(s0);
 #pragma unroll
-      for (int sl = 0; sl < 8; ++sl)
-        if (sl < np.S) {
-          p[sl][0] = *reinterpret_cast<const f32x4*>(np.ws + sl * np.sstride + cc * 8);
-          p[sl][1] = *reinterpret_cast<const f32x4*>(np.ws + sl * np.sstride + cc * 8 + 4);
-        }
+      for (int i = 0; i < PM; ++i)
 #pragma unroll
-      for (int sl = 0; sl < 8; ++sl)
-        if (sl < np.S) {
+        for (int sl = 0; sl < SMAX; ++sl)
+          if (s0 + sl < np.S) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            v[j] += p[sl][0][j];
-            v[4 + j] += p[sl][1][j];
+            for (int j = 0; j < 4; ++j) {
+              v[i][j] += p[i][sl][0][j];
+              v[i][4 + j] += p[i][sl][1][j];
+            }
           }
-        }
-      s16x8 hv;
+    }
+    float ss = 0.f;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        hv[j] = (short)f2bf(v[j]);
-        const float r = bf2f(hv[j]);
-        ss += r * r;
+    for (int i = 0; i < PM; ++i) {
+      const int cc = tid + NTH * i;
+      if (cc < nchunk) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          ha[i][j] = (short)f2bf(v[i][j]);
+          const float r = bf2f(ha[i][j]);
+          ss += r * r;
+        }
+        if (wg0) st16(np.hout + cc * 8, ha[i]);
       }
-      if (wg0) st16(np.hout + cc * 8, hv);
-      if (cc >= c0 && cc < c1) st16(x1 + (cc - c0) * 8, hv);
     }
     ss = wave_sum(ss);
     if (lane == 0) nred[wave] = ss;
@@ -416,13 +467,17 @@ __global__ __launch_bounds__(256, OCC) void gemm_stream_kernel(const uint16_t* _
 #pragma unroll
     for (int k = 0; k < NTH / 64; ++k) ss += nred[k];
     const float inv = rsqrtf(ss / (float)np.D + np.eps);
-    for (int cc = tid; cc < c1 - c0; cc += NTH) {
-      const s16x8 hv = ld16(x1 + cc * 8), wv = ld16(np.lnw + (c0 + cc) * 8);
-      s16x8 o;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = (short)f2bf(bf2f(hv[j]) * inv * bf2f(wv[j]));
-      st16(x1 + cc * 8, o);
+    for (int i = 0; i < PM; ++i) {
+      const int cc = tid + NTH * i;
+      if (cc < nchunk && cc >= c0 && cc < c1) {
+        s16x8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = (short)f2bf(bf2f(ha[i][j]) * inv * bf2f(la[i][j]));
+        st16(x1 + (cc - c0) * 8, o);
+      }
     }
+  }
     __syncthreads();
     // row 0 is the only real row: its A fragments come from the slice (natural k order of the pre-shuffled
     // layout: lane group g holds k 32 s + 8 g .. +8), the other 15 MFMA rows are zero
@@ -782,24 +837,48 @@ int launch_gemm_stream8(const uint16_t* X, int ldx, const uint8_t* W, const floa
                  : stream8_dispatch<EPI_NONE, false>(X, ldx, W, wscale, K, bias, R, ldr, Y, ldy, ws, ws_elems, M, N, ntw, S, reduce, s);
 }
 
-template <int NTW, int EPI>
+template <int NTW, int EPI, int PM>
 static void stream_norm_launch(const uint16_t* W, const uint16_t* bias, void* Y, int ldy, float* ws, int N, int K,
                                int S, bool reduce, const NormPro& np, hipStream_t st) {
   const int kper = K / S;
   const dim3 grid(N / (64 * NTW), S);
   const size_t smem = (size_t)kper * 2;  // the normalised K slice (<= 16 KB at K = 8192)
   if (S == 1) {
-    gemm_stream_kernel<1, NTW, 4, EPI, false, false, true, 2, 0, false, true><<<grid, 256, smem, st>>>(
+    gemm_stream_kernel<1, NTW, 4, EPI, false, false, true, 2, 0, false, PM><<<grid, 256, smem, st>>>(
         nullptr, 0, W, K, bias, nullptr, 0, Y, ldy, nullptr, 1, N, kper, 1, nullptr, nullptr, nullptr, 0L, nullptr,
         0L, 0L, np);
     return;
   }
-  gemm_stream_kernel<1, NTW, 4, EPI, false, true, true, 2, 0, false, true><<<grid, 256, smem, st>>>(
+  gemm_stream_kernel<1, NTW, 4, EPI, false, true, true, 2, 0, false, PM><<<grid, 256, smem, st>>>(
       nullptr, 0, W, K, bias, nullptr, 0, Y, ldy, ws, 1, N, kper, 1, nullptr, nullptr, nullptr, 0L, nullptr, 0L, 0L,
       np);
   if (!reduce) return;
   const int ncol = EPI == EPI_SILU ? N / 2 : N;
   splitk_reduce_kernel<EPI, false><<<(ncol / 8 + 255) / 256, 256, 0, st>>>(ws, S, 1, N, bias, nullptr, 0, Y, ldy);
+}
+
+// o_proj of a batch-1 decode step with the attention's partition merge in its prologue: split-K slabs only (the
+// consumer -- splitk_resid_rmsnorm or the next GEMM's norm prologue -- adds them to the residual)
+int launch_gemm_stream_merge(const uint16_t* W, float* ws, long ws_elems, int N, int K, int ntw, int S,
+                             const NormPro& np, hipStream_t s) {
+  if (ntw == 4) ntw = 2;
+  if (ntw != 1 && ntw != 2) return -1;
+  if (S < 2 || N % (64 * ntw) != 0 || K % (S * 128) != 0 || (long)(K / S) * 2 > 65536) return -1;
+  if (ws == nullptr || ws_elems < (long)S * N || np.mo == nullptr || np.ml == nullptr || np.ctx == nullptr ||
+      np.nparts < 1 || np.ppp < 1 || np.dh <= 0 || K % np.dh != 0)
+    return -1;
+  const int kper = K / S;
+  const dim3 grid(N / (64 * ntw), S);
+  const size_t smem = (size_t)kper * 2;
+  if (ntw == 1)
+    gemm_stream_kernel<1, 1, 4, EPI_NONE, false, true, true, 2, 0, false, 0, true><<<grid, 256, smem, s>>>(
+        nullptr, 0, W, K, nullptr, nullptr, 0, nullptr, N, ws, 1, N, kper, 1, nullptr, nullptr, nullptr, 0L, nullptr,
+        0L, 0L, np);
+  else
+    gemm_stream_kernel<1, 2, 4, EPI_NONE, false, true, true, 2, 0, false, 0, true><<<grid, 256, smem, s>>>(
+        nullptr, 0, W, K, nullptr, nullptr, 0, nullptr, N, ws, 1, N, kper, 1, nullptr, nullptr, nullptr, 0L, nullptr,
+        0L, 0L, np);
+  return 0;
 }
 
 int launch_gemm_stream_norm(const uint16_t* W, const uint16_t* bias, void* Y, int ldy, int epi, float* ws,
@@ -808,17 +887,27 @@ int launch_gemm_stream_norm(const uint16_t* W, const uint16_t* bias, void* Y, in
   if (epi != EPI_NONE && epi != EPI_SILU) return -1;
   if (epi == EPI_SILU || ntw == 4) ntw = 2;  // one row: NTW 4 is never picked (stream_dispatch)
   if (ntw != 1 && ntw != 2) return -1;
-  if (np.D != K || K % 8 != 0 || np.S < 0 || np.S > 8 || np.h == nullptr || np.lnw == nullptr || np.hout == nullptr)
+  if (np.D != K || K % 8 != 0 || K > 8 * 256 * 4 || np.S < 0 || np.S > 8 || np.h == nullptr || np.lnw == nullptr || np.hout == nullptr)
     return -1;
   if (np.S > 0 && (np.ws == nullptr || np.sstride < K)) return -1;
   if (S < 1 || N % (64 * ntw) != 0 || K % (S * 128) != 0 || (long)(K / S) * 2 > 65536) return -1;
   if (S > 1 && (ws == nullptr || ws == np.ws || ws_elems < (long)S * N)) return -1;
-  if (epi == EPI_SILU)
-    stream_norm_launch<2, EPI_SILU>(W, bias, Y, ldy, ws, N, K, S, reduce, np, s);
-  else if (ntw == 1)
-    stream_norm_launch<1, EPI_NONE>(W, bias, Y, ldy, ws, N, K, S, reduce, np, s);
+  const int pm = (K / 8 + 255) / 256;  // 16-B chunks of the row per thread
+  auto go = [&](auto pmc) {
+    constexpr int PM = decltype(pmc)::value;
+    if (epi == EPI_SILU)
+      stream_norm_launch<2, EPI_SILU, PM>(W, bias, Y, ldy, ws, N, K, S, reduce, np, s);
+    else if (ntw == 1)
+      stream_norm_launch<1, EPI_NONE, PM>(W, bias, Y, ldy, ws, N, K, S, reduce, np, s);
+    else
+      stream_norm_launch<2, EPI_NONE, PM>(W, bias, Y, ldy, ws, N, K, S, reduce, np, s);
+  };
+  if (pm <= 1)
+    go(std::integral_constant<int, 1>());
+  else if (pm == 2)
+    go(std::integral_constant<int, 2>());
   else
-    stream_norm_launch<2, EPI_NONE>(W, bias, Y, ldy, ws, N, K, S, reduce, np, s);
+    go(std::integral_constant<int, 4>());
   return 0;
 }
 

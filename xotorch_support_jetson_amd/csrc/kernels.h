@@ -38,6 +38,9 @@ int launch_gemm_stream(const uint16_t* X, int ldx, const uint16_t* W, int ldw, c
 // reduce + norm launch); workgroup (0, 0) stores the summed residual row to hout (never h itself: the other
 // workgroups are still reading h).  Pre-shuffled bf16 weights, epi none / silu, split-K into ws (a different
 // buffer from np.ws).
+// The same kernel's other row prologue (launch_gemm_stream_merge): the row is the merge of a batch-1 split-KV
+// decode attention's partitions (mo [H][nparts][dh], ml [H][nparts][2], ctx_lens[0]), so the o_proj GEMM replaces
+// the attention's merge launch.
 struct NormPro {
   const uint16_t* h;
   const float* ws;
@@ -48,7 +51,15 @@ struct NormPro {
   uint16_t* hout;
   float eps;
   int D;
+  const float* mo;
+  const float* ml;
+  const int32_t* ctx;
+  int nparts, ppp, dh;
 };
+int launch_gemm_stream_merge(const uint16_t* W, float* ws, long ws_elems, int N, int K, int ntw, int S,
+                             const NormPro& np, hipStream_t s);
+void launch_attn_decode_merge(const float* ws_o, const float* ws_ml, const int32_t* ctx_lens, uint16_t* out, int B,
+                              int H, int Dh, int nparts, int pages_per_part, hipStream_t s);
 int launch_gemm_stream_norm(const uint16_t* W, const uint16_t* bias, void* Y, int ldy, int epi, float* ws,
                             long ws_elems, int N, int K, int ntw, int S, bool reduce, const NormPro& np,
                             hipStream_t s);
@@ -117,7 +128,7 @@ int launch_gemm_tiled(const uint16_t* X, int ldx, const uint16_t* W, int ldw, co
 int launch_attn_decode(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, const int32_t* block_tables,
                        int max_blocks, const int32_t* ctx_lens, uint16_t* out, float* ws_o, float* ws_ml, int B,
                        int H, int Hkv, int Dh, int pages_per_part, int nparts, float scale, int num_pages, int algo,
-                       hipStream_t s);
+                       hipStream_t s, bool merge = true);
 int launch_attn_prefill(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, const int32_t* block_tables,
                         int max_blocks, const int32_t* cu_q, const int32_t* ctx_lens, uint16_t* out, int B,
                         int max_qlen, int H, int Hkv, int Dh, float scale, int num_pages, int algo, hipStream_t s);

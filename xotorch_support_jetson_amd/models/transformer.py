@@ -28,7 +28,7 @@ import torch
 from ..inference.shard import Shard
 from ..ops import kernels as K
 from ..ops._ext import require
-from ..ops.linear import FUSE_NORM, PendingNorm, layout_of, linear, linear_resid_norm, linear_rope_kv, scratch
+from ..ops.linear import FUSE_MERGE, FUSE_NORM, PendingNorm, layout_of, linear, linear_resid_norm, linear_rope_kv, scratch
 from ..ops.rope import longrope_window, rope_shift, rope_table
 from .config import ModelConfig
 from .weights import ShardWeights, expert
@@ -143,10 +143,11 @@ class ShardModel:
     return range(start + o, start + n + o)
 
   # ------------------------------------------------------------------ helpers
-  def _attention(self, q: torch.Tensor, li: int, inp: StepInputs, ws=None) -> torch.Tensor:
+  def _attention(self, q: torch.Tensor, li: int, inp: StepInputs, ws=None, defer_merge: bool = False):
     kc, vc = self.kv.k[li], self.kv.v[li]
     if inp.decode:
-      return K.attn_decode(q, kc, vc, inp.block_tables, inp.ctx_lens, self.scale, ws or self.ws)
+      return K.attn_decode(q, kc, vc, inp.block_tables, inp.ctx_lens, self.scale, ws or self.ws,
+                           defer_merge=defer_merge)
     return K.attn_prefill(q, kc, vc, inp.block_tables, inp.cu_q, inp.ctx_lens, inp.max_qlen, self.scale)
 
   def _mla(self, xn: torch.Tensor, lw, li: int, inp: StepInputs) -> torch.Tensor:
@@ -352,7 +353,9 @@ class ShardModel:
                            self.kv.v[j], c.num_heads, c.num_kv_heads)
         if isinstance(xn, PendingNorm):
           h = xn.dst
-        a = self._attention(q, j, inp).view(h.shape[0], c.num_heads * c.head_dim)
+        a = self._attention(q, j, inp, defer_merge=fuse and FUSE_MERGE and lw.router is None)
+        if not isinstance(a, K.PendingMerge):  # (a pending merge is finished inside o_proj's prologue)
+          a = a.view(h.shape[0], c.num_heads * c.head_dim)
       # o_proj + residual + post-attention norm (one fused pass when the projection runs split-K)
       xn = linear_resid_norm(a, lw.o_w, h, lw.ln2, c.rms_norm_eps,
                              defer_to=other(h) if lw.router is None else None)

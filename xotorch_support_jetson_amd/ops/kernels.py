@@ -210,8 +210,24 @@ class DecodeWorkspace:
     return ppp, nparts, algo
 
 
+class PendingMerge:
+  """A batch-1 split-KV decode attention whose partition merge was left to its consumer: o_proj merges the
+  partitions of its K slice in its GEMM prologue (linear_resid_norm -> gemm_stream_merge), one launch less per
+  layer.  materialize() runs the merge kernel into `out` instead."""
+
+  __slots__ = ("o", "ml", "ctx_lens", "ppp", "nparts", "out")
+
+  def __init__(self, o, ml, ctx_lens, ppp, nparts, out):
+    self.o, self.ml, self.ctx_lens, self.ppp, self.nparts, self.out = o, ml, ctx_lens, ppp, nparts, out
+
+  def materialize(self) -> torch.Tensor:
+    require().attn_decode_merge(self.o, self.ml, self.ctx_lens, self.out, self.ppp, self.nparts)
+    return self.out
+
+
 def attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale: float, ws: DecodeWorkspace | None = None,
-                out: torch.Tensor | None = None) -> torch.Tensor:
+                out: torch.Tensor | None = None, defer_merge: bool = False):
+  """defer_merge (one sequence): return a PendingMerge when the context is split over partitions."""
   if not _gpu(q):
     y = ref.attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale)
     if out is not None:
@@ -224,9 +240,10 @@ def attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale: float, ws: D
     ws = DecodeWorkspace(B, H, Dh, width * PAGE, q.device)
   ppp, nparts, algo = ws.partition(B, k_cache.shape[1], width)
   out = torch.empty_like(q) if out is None else out
+  defer = defer_merge and B == 1 and nparts > 1
   require().attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, out, ws.o, ws.ml, ppp, nparts, float(scale),
-                        algo)
-  return out
+                        algo, not defer)
+  return PendingMerge(ws.o, ws.ml, ctx_lens, ppp, nparts, out) if defer else out
 
 
 # XOT_PREFILL_ATTN: 2 = 256-row workgroups, LDS-DMA page ring, in-register softmax (default); 1 = the

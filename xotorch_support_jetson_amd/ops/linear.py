@@ -564,6 +564,9 @@ def _blas(x, w, bias, residual, epi, out, out_dtype):
 # XOT_FUSE_NORM=0: batch-1 decode keeps the separate split-K reduce + residual + RMSNorm launch after o_proj /
 # down_proj (fused: the next GEMM recomputes the norm of the pending slabs in its prologue, csrc/gemm.hip NORM)
 FUSE_NORM = os.environ.get("XOT_FUSE_NORM", "1") != "0"
+# XOT_FUSE_MERGE=0: batch-1 decode keeps the attention's partition-merge launch (fused: o_proj merges the partitions
+# of its K slice in its prologue, csrc/gemm.hip MERGE; only together with the deferred norm above)
+FUSE_MERGE = os.environ.get("XOT_FUSE_MERGE", "1") != "0"
 
 
 class PendingNorm:
@@ -649,14 +652,28 @@ def linear_resid_norm(x: torch.Tensor, w: torch.Tensor, h: torch.Tensor, ln_w: t
   When the projection runs split-K on the pre-shuffled layout, the GEMM leaves its fp32 slabs and one
   kernel does the slab reduce, the residual add and the RMSNorm (instead of reduce + norm kernels).
   defer_to (a second residual buffer, one row): return a PendingNorm instead -- the slabs stay for the next
-  GEMM's prologue, and the residual stream continues in defer_to (h is left as it was)."""
+  GEMM's prologue, and the residual stream continues in defer_to (h is left as it was).
+  x may be a kernels.PendingMerge (batch-1 decode attention): with defer_to, the projection merges the attention's
+  partitions in its own prologue (gemm_stream_merge); otherwise the merge kernel runs first."""
+  if isinstance(x, K.PendingMerge):
+    xm = x.out.view(x.out.shape[0], -1)  # [1, H * Dh]; the stand-in operand of the configuration choice
+    if defer_to is not None and FUSE_NORM and layout_of(w) == "stream" and xm.shape[0] == 1:
+      N, Kd = w.shape
+      cfg = policy.shuffled_cfg(xm, w, bias, h, "resid", h.dtype)
+      if (cfg[0] == "stream" and 1 < cfg[2] <= 8 and N <= 8192 and Kd % (cfg[2] * 128) == 0
+          and (Kd // cfg[2]) * 2 <= 65536 and h.is_contiguous() and h.dtype == torch.bfloat16 and out is None):
+        S = cfg[2]
+        ws = scratch.splitk(h.device, S * N, slot=1)
+        require().gemm_stream_merge(w, ws, cfg[1], S, x.o, x.ml, x.ctx_lens, x.ppp, x.nparts, x.out.shape[-1])
+        return PendingNorm(h, defer_to, ws, S, bias, ln_w, eps)
+    x = x.materialize().view(xm.shape)
   if x.is_cuda and layout_of(w) == "stream":
     if x.stride(1) != 1 or x.stride(0) % 8:
       x = x.contiguous()
     M, N = x.shape[0], w.shape[0]
     cfg = policy.shuffled_cfg(x, w, bias, h, "resid", h.dtype)
-    if (defer_to is not None and FUSE_NORM and M == 1 and cfg[0] == "stream" and 1 < cfg[2] <= 8 and out is None
-        and h.is_contiguous() and h.dtype == torch.bfloat16):
+    if (defer_to is not None and FUSE_NORM and M == 1 and cfg[0] == "stream" and 1 < cfg[2] <= 8 and N <= 8192
+        and out is None and h.is_contiguous() and h.dtype == torch.bfloat16):
       S = cfg[2]
       ws = scratch.splitk(x.device, S * M * N, slot=1)
       require().gemm_stream(x, w, h, None, h, ws, K.EPI["resid"], cfg[1], S, True, False)
