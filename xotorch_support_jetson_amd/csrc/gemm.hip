@@ -371,18 +371,50 @@ __global__ __launch_bounds__(256, OCC) void gemm_stream_kernel(const uint16_t* _
     const int npages = (max(np.ctx[0], 0) + 63) / 64;
     int npart = (npages + np.ppp - 1) / np.ppp;
     npart = npart < 1 ? 1 : (npart > np.nparts ? np.nparts : npart);
-    for (int e = tid; e < kper; e += NTH) {
-      const int k = kb + e, hd = k / np.dh, d = k - hd * np.dh;
+    constexpr int NPM = 8;  // partitions whose loads are all requested before use (more: a second, per-element loop)
+    for (int e0 = 4 * tid; e0 < kper; e0 += 4 * NTH) {  // 4 consecutive elements of one head per thread
+      const int k = kb + e0, hd = k / np.dh, d = k - hd * np.dh;
       const size_t base = (size_t)hd * np.nparts;
-      float M = -1e30f;
-      for (int q = 0; q < npart; ++q) M = fmaxf(M, np.ml[(base + q) * 2]);
-      float L = 0.f, O = 0.f;
-      for (int q = 0; q < npart; ++q) {
-        const float f = exp2f(np.ml[(base + q) * 2] - M);
-        L += np.ml[(base + q) * 2 + 1] * f;
-        O += np.mo[(base + q) * np.dh + d] * f;
+      float o4[4];
+      if (npart <= NPM) {
+        f32x2_t mv[NPM];
+        f32x4 ov[NPM];
+#pragma unroll
+        for (int q = 0; q < NPM; ++q)
+          if (q < npart) {
+            mv[q] = *reinterpret_cast<const f32x2_t*>(np.ml + (base + q) * 2);
+            ov[q] = *reinterpret_cast<const f32x4*>(np.mo + (base + q) * np.dh + d);
+          }
+        float M = -1e30f;
+#pragma unroll
+        for (int q = 0; q < NPM; ++q)
+          if (q < npart) M = fmaxf(M, mv[q][0]);
+        float L = 0.f, O[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int q = 0; q < NPM; ++q)
+          if (q < npart) {
+            const float f = exp2f(mv[q][0] - M);
+            L += mv[q][1] * f;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) O[j] += ov[q][j] * f;
+          }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o4[j] = L > 0.f ? O[j] / L : 0.f;
+      } else {
+        float M = -1e30f;
+        for (int q = 0; q < npart; ++q) M = fmaxf(M, np.ml[(base + q) * 2]);
+        float L = 0.f, O[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int q = 0; q < npart; ++q) {
+          const float f = exp2f(np.ml[(base + q) * 2] - M);
+          L += np.ml[(base + q) * 2 + 1] * f;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) O[j] += np.mo[(base + q) * np.dh + d + j] * f;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o4[j] = L > 0.f ? O[j] / L : 0.f;
       }
-      x1[e] = f2bf(L > 0.f ? O / L : 0.f);
+      *reinterpret_cast<s16x4*>(x1 + e0) =
+          s16x4{(short)f2bf(o4[0]), (short)f2bf(o4[1]), (short)f2bf(o4[2]), (short)f2bf(o4[3])};
     }
   } else {
     // RMSNorm prologue (one input row; NORM = 16-B chunks of the row per thread): the first two weight chunks,
@@ -390,7 +422,7 @@ __global__ __launch_bounds__(256, OCC) void gemm_stream_kernel(const uint16_t* _
     // so the chain is one L2 round trip per SMAX slabs (the producer just wrote them), one wave reduction and two
     // barriers, under the weight stream's own HBM latency.  Same arithmetic and reduction order as
     // splitk_resid_rmsnorm_kernel<*, *, 256>: the row is bitwise the one the unfused pair gives.
-    constexpr int PM = NORM, SMAX = NORM >= 4 ? 2 : 4;  // slabs per round trip (registers: PM x SMAX x 8)
+    constexpr int PM = NORM, SMAX = NORM >= 4 ? 2 : 8;  // slabs per round trip (registers: PM x SMAX x 8)
     __shared__ float nred[NTH / 64];
     const int nchunk = np.D >> 3, c0 = kb >> 3, c1 = (kb + kper) >> 3;
     const bool wg0 = blockIdx.x == 0 && blockIdx.y == 0;
@@ -865,7 +897,7 @@ int launch_gemm_stream_merge(const uint16_t* W, float* ws, long ws_elems, int N,
   if (ntw != 1 && ntw != 2) return -1;
   if (S < 2 || N % (64 * ntw) != 0 || K % (S * 128) != 0 || (long)(K / S) * 2 > 65536) return -1;
   if (ws == nullptr || ws_elems < (long)S * N || np.mo == nullptr || np.ml == nullptr || np.ctx == nullptr ||
-      np.nparts < 1 || np.ppp < 1 || np.dh <= 0 || K % np.dh != 0)
+      np.nparts < 1 || np.ppp < 1 || np.dh <= 0 || np.dh % 4 != 0 || K % np.dh != 0)
     return -1;
   const int kper = K / S;
   const dim3 grid(N / (64 * ntw), S);
