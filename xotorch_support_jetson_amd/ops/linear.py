@@ -567,6 +567,9 @@ FUSE_NORM = os.environ.get("XOT_FUSE_NORM", "1") != "0"
 # XOT_FUSE_MERGE=0: batch-1 decode keeps the attention's partition-merge launch (fused: o_proj merges the partitions
 # of its K slice in its prologue, csrc/gemm.hip MERGE; only together with the deferred norm above)
 FUSE_MERGE = os.environ.get("XOT_FUSE_MERGE", "1") != "0"
+# widest residual row whose norm is deferred: every consumer workgroup re-reads the row and all its slabs, which paid
+# at 4096 (Llama-3-8B 3.50 -> 3.33 ms/token) but not at 8192 (Llama-3-70B 23.97 vs 24.07 ms, profiles/r6/headline/b1/)
+DEFER_MAX_D = 4096
 
 
 class PendingNorm:
@@ -660,19 +663,25 @@ def linear_resid_norm(x: torch.Tensor, w: torch.Tensor, h: torch.Tensor, ln_w: t
     if defer_to is not None and FUSE_NORM and layout_of(w) == "stream" and xm.shape[0] == 1:
       N, Kd = w.shape
       cfg = policy.shuffled_cfg(xm, w, bias, h, "resid", h.dtype)
-      if (cfg[0] == "stream" and 1 < cfg[2] <= 8 and N <= 8192 and Kd % (cfg[2] * 128) == 0
-          and (Kd // cfg[2]) * 2 <= 65536 and h.is_contiguous() and h.dtype == torch.bfloat16 and out is None):
+      if (cfg[0] == "stream" and 1 < cfg[2] <= 8 and Kd % (cfg[2] * 128) == 0 and (Kd // cfg[2]) * 2 <= 65536
+          and h.is_contiguous() and h.dtype == torch.bfloat16):
         S = cfg[2]
-        ws = scratch.splitk(h.device, S * N, slot=1)
+        if N <= DEFER_MAX_D and out is None:  # merge here, norm in the next GEMM's prologue
+          ws = scratch.splitk(h.device, S * N, slot=1)
+          require().gemm_stream_merge(w, ws, cfg[1], S, x.o, x.ml, x.ctx_lens, x.ppp, x.nparts, x.out.shape[-1])
+          return PendingNorm(h, defer_to, ws, S, bias, ln_w, eps)
+        ws = scratch.splitk(h.device, S * N)  # merge here, then the usual slab reduce + residual + norm
         require().gemm_stream_merge(w, ws, cfg[1], S, x.o, x.ml, x.ctx_lens, x.ppp, x.nparts, x.out.shape[-1])
-        return PendingNorm(h, defer_to, ws, S, bias, ln_w, eps)
+        out = torch.empty_like(h) if out is None else out
+        require().splitk_resid_rmsnorm(ws, S, bias, h, ln_w, out, float(eps))
+        return out
     x = x.materialize().view(xm.shape)
   if x.is_cuda and layout_of(w) == "stream":
     if x.stride(1) != 1 or x.stride(0) % 8:
       x = x.contiguous()
     M, N = x.shape[0], w.shape[0]
     cfg = policy.shuffled_cfg(x, w, bias, h, "resid", h.dtype)
-    if (defer_to is not None and FUSE_NORM and M == 1 and cfg[0] == "stream" and 1 < cfg[2] <= 8 and N <= 8192
+    if (defer_to is not None and FUSE_NORM and M == 1 and cfg[0] == "stream" and 1 < cfg[2] <= 8 and N <= DEFER_MAX_D
         and out is None and h.is_contiguous() and h.dtype == torch.bfloat16):
       S = cfg[2]
       ws = scratch.splitk(x.device, S * M * N, slot=1)
