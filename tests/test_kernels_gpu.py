@@ -803,6 +803,29 @@ def test_attention_train_fwd_bwd(gpu, B, L, H, Hkv, Dh):
     assert rel_err(g[:, sl], x.grad[:, sl]) < 3e-2, name
 
 
+@pytest.mark.parametrize("B,L,H,Hkv,Dh", [(2, 100, 8, 2, 128), (1, 257, 16, 4, 128), (1, 130, 4, 4, 64)])
+def test_qkv_attention_fused_matches_separate(gpu, B, L, H, Hkv, Dh):
+  """QKVAttentionFn (one rope launch for q and k, dv straight into dqkv) against QKVRopeFn + AttentionFn: the same
+  kernels on the same values, so output and dqkv are bitwise equal."""
+  from xotorch_support_jetson_amd.train import autograd_ops as A
+  torch.manual_seed(L)
+  ang = torch.rand(512, Dh // 2, device=gpu) * 6.28  # any table: both paths rotate with the same one
+  cos_sin = torch.cat([ang.cos(), ang.sin()], 1).contiguous()
+  pos = (torch.arange(L, device=gpu, dtype=torch.int32)).repeat(B)
+  W = (H + 2 * Hkv) * Dh
+  x = (torch.randn(B * L, W, device=gpu) * 0.5).to(torch.bfloat16)
+  do = torch.randn(B * L, H * Dh, device=gpu).to(torch.bfloat16)
+  a = x.clone().requires_grad_()
+  oa = A.qkv_attention(a, pos, cos_sin, B, L, H, Hkv, Dh)
+  oa.backward(do)
+  b = x.clone().requires_grad_()
+  q, k, v = A.qkv_rope(b, pos, cos_sin, H, Hkv, Dh)
+  ob = A.attention(q, k, v, B, L, H, Hkv, Dh)
+  ob.backward(do)
+  assert torch.equal(oa, ob)
+  assert torch.equal(a.grad, b.grad)
+
+
 @pytest.mark.parametrize("B,L,H", [(1, 100, 4), (2, 300, 8)])
 def test_attention_qk_v_deepseek_dims(gpu, B, L, H):
   """DeepSeek MLA training attention (q / k heads of 192, v heads of 128, v zero-padded to 192 for the 192-wide

@@ -38,10 +38,13 @@ for what in "$@"; do
                 step r6/attn_train 200 python -u tools/bench_attn_train.py --reps 30 &&
                 prof r6/attn_train_prof 200 python3 "$R/tools/bench_attn_train.py" --reps 10 ;;
     fnorm_test) step r6/fnorm_test 400 python -u -m pytest tests/test_kernels_gpu.py tests/test_runner_gpu.py -m gpu -x -v --timeout 300 --timeout-method thread -k "gemm_stream_norm or fused_norm or test_gemm_stream or split_equals_full or llama70b_layers" ;;
+    b1_70b) step r6/b1_70b 400 python -u bench.py --batch-per-gpu 1 --steps 32 --warmup 4 ;;
+    b1_70b_unfused) XOT_FUSE_NORM=0 step r6/b1_70b_unfused 400 python -u bench.py --batch-per-gpu 1 --steps 32 --warmup 4 ;;
     b1_nomerge) XOT_FUSE_MERGE=0 step r6/b1_nomerge 300 python -u bench.py --model llama-3-8b --batch-per-gpu 1 --steps 64 --warmup 8 ;;
     b1_unfused) XOT_FUSE_NORM=0 step r6/b1_unfused 300 python -u bench.py --model llama-3-8b --batch-per-gpu 1 --steps 64 --warmup 8 ;;
     b1_fused) XOT_FUSE_NORM=1 step r6/b1_fused 300 python -u bench.py --model llama-3-8b --batch-per-gpu 1 --steps 64 --warmup 8 ;;
     fnorm_diag) step r6/fnorm_diag 300 python -u tools/diag/fused_norm_diag.py ;;
+    qkvattn_test) step r6/qkvattn_test 400 python -u -m pytest tests/test_kernels_gpu.py tests/test_train_own_gpu.py tests/test_runner_gpu.py tests/test_engine_gpu.py -m gpu -x -q --timeout 300 --timeout-method thread -k "qkv_attention or attention_train or train or fused_grad or tied" ;;
     tests)  step r6/gpu_tests 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
     *) echo "unknown case $what"; exit 2 ;;
   esac

@@ -833,6 +833,54 @@ class QKVRopeFn(torch.autograd.Function):
     return dqkv, None, None, None, None, None
 
 
+class QKVAttentionFn(torch.autograd.Function):
+  """Fused-QKV projection output [T, (H + 2 Hkv) Dh] -> causal GQA attention of (rope(q), rope(k), v): QKVRopeFn +
+  AttentionFn in one node, so q and k rotate in ONE rope_apply launch (their heads are adjacent columns) into one
+  [T, (H + Hkv) Dh] buffer the attention reads as two strided views, and the backward writes dq / dk side by side
+  (one inverse rope_apply into the dqkv rows) and dv straight into its dqkv slice (no copy)."""
+
+  @staticmethod
+  def forward(ctx, qkv, pos, cos_sin, B, L, H, Hkv, Dh):
+    C = require()
+    scale = Dh ** -0.5
+    Lp = -(-L // 64) * 64
+    T, nq, nk = qkv.shape[0], H * Dh, Hkv * Dh
+    qk = torch.empty(T, nq + nk, dtype=qkv.dtype, device=qkv.device)
+    C.rope_apply(qkv[:, :nq + nk], qk, pos, cos_sin, int(H + Hkv), int(Dh), False)
+    q, k, v = qk[:, :nq], qk[:, nq:], qkv[:, nq + nk:]
+    o = torch.empty(T, nq, dtype=qkv.dtype, device=qkv.device)
+    lse2 = torch.empty(B * H * L, dtype=torch.float32, device=qkv.device)
+    vt = _transposed(C, v, B, L, Lp, Hkv, Dh)
+    C.attn_train_fwd(q, k, vt, o, lse2, B, L, Lp, H, Hkv, Dh, scale, True)
+    ctx.save_for_backward(qk, qkv, o, lse2, pos, cos_sin)
+    ctx.dims = (B, L, Lp, H, Hkv, Dh, scale)
+    return o
+
+  @staticmethod
+  def backward(ctx, do):
+    C = require()
+    qk, qkv, o, lse2, pos, cos_sin = ctx.saved_tensors
+    B, L, Lp, H, Hkv, Dh, scale = ctx.dims
+    T, nq, nk = qk.shape[0], H * Dh, Hkv * Dh
+    do = do.contiguous().to(qk.dtype)
+    dqkv = torch.empty(T, qkv.shape[1], dtype=qk.dtype, device=qk.device)
+    dqk = torch.empty_like(qk)
+    delta = torch.empty_like(lse2)
+    ws = torch.empty(2 * H * B * L * Dh, dtype=torch.float32, device=qk.device)  # per-query-head dK/dV partials
+    C.attn_train_bwd(qk[:, :nq], qk[:, nq:], qkv[:, nq + nk:], o, do, lse2, delta, dqk[:, :nq], dqk[:, nq:],
+                     dqkv[:, nq + nk:], ws, B, L, Lp, H, Hkv, Dh, scale)
+    C.rope_apply(dqk, dqkv[:, :nq + nk], pos, cos_sin, int(H + Hkv), int(Dh), True)
+    return dqkv, None, None, None, None, None, None, None
+
+
+def qkv_attention(qkv, pos, cos_sin, B, L, H, Hkv, Dh):
+  """Causal GQA attention of a fused-QKV projection output with RoPE on q / k (QKVAttentionFn on the GPU)."""
+  if _gpu(qkv) and qkv.stride(1) == 1 and Dh in (64, 128):
+    return QKVAttentionFn.apply(qkv, pos, cos_sin, B, L, H, Hkv, Dh)
+  q, k, v = qkv_rope(qkv, pos, cos_sin, H, Hkv, Dh)
+  return attention(q, k, v, B, L, H, Hkv, Dh)
+
+
 def qkv_rope(qkv, pos, cos_sin, H, Hkv, Dh):
   """(rope(q), rope(k), v) of a fused-QKV projection output (QKVRopeFn on the GPU)."""
   if _gpu(qkv) and qkv.stride(1) == 1:

@@ -172,8 +172,7 @@ class ShardTrainer:
         qkv = self._mm(xn, f"{i}.qkv")
         if f"{i}.qkv_b" in P:
           qkv = qkv + P[f"{i}.qkv_b"]
-        q, k, v = A.qkv_rope(qkv, pos, self.cos_sin, H, Hkv, Dh)
-        a = A.attention(q, k, v, B, L, H, Hkv, Dh)  # flash-style HIP kernels (fwd + dQ + dK/dV)
+        a = A.qkv_attention(qkv, pos, self.cos_sin, B, L, H, Hkv, Dh)  # RoPE + flash-style HIP kernels
       h = self._mm(a, f"{i}.o", h)
       h, xn = A.res_rmsnorm(h, P[f"{i}.ln2"], c.rms_norm_eps, self.acc.get(f"{i}.ln2"))
       if f"{i}.router" in P:
