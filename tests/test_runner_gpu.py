@@ -488,8 +488,9 @@ def test_decode_tick_issues_no_host_sync(gpu):
   torch.cuda.synchronize()
 
 
-@pytest.mark.parametrize("defer_max_d", [4096, 0])
-def test_batch1_fused_norm_decode_matches_unfused(gpu, monkeypatch, defer_max_d):
+@pytest.mark.parametrize("name,defer_max_d", [("llama-3-8b", 4096), ("llama-3-8b", 0), ("tiny-qwen", 4096),
+                                              ("tiny-phi3", 4096), ("tiny-mixtral", 4096)])
+def test_batch1_fused_norm_decode_matches_unfused(gpu, monkeypatch, name, defer_max_d):
   """Batch-1 decode with the split-K reduce + residual + RMSNorm deferred into the next GEMM's prologue
   (ops.linear.PendingNorm) and the attention's partition merge done in o_proj's prologue (kernels.PendingMerge),
   the defaults, against the unfused kernels on the same weights: two Llama-3-8B layers, a 600-token context (split
@@ -497,8 +498,8 @@ def test_batch1_fused_norm_decode_matches_unfused(gpu, monkeypatch, defer_max_d)
   import xotorch_support_jetson_amd.models.transformer as TM
   from xotorch_support_jetson_amd.ops import kernels as KK
   from xotorch_support_jetson_amd.ops import linear as L
-  c = preset("llama-3-8b").with_layers(2)
-  sh = Shard("llama-3-8b", 0, 1, 2)
+  c = preset(name).with_layers(2) if name == "llama-3-8b" else preset(name)
+  sh = Shard(name, 0, c.num_layers - 1, c.num_layers)
   w = random_weights(c, sh, gpu, seed=5)
   runs = {"norm": 0, "merge": 0}
   orig_run, orig_attn = L.PendingNorm.run, KK.attn_decode
@@ -534,6 +535,7 @@ def test_batch1_fused_norm_decode_matches_unfused(gpu, monkeypatch, defer_max_d)
   assert runs == {"norm": 0, "merge": 0}
   for graphs in (False, True):
     got = decode(True, graphs)
-    assert (runs["norm"] > 0) == (defer_max_d > 0) and runs["merge"] > 0, runs
+    if name == "llama-3-8b":  # (the tiny presets' projections may not split K: then nothing is deferred)
+      assert (runs["norm"] > 0) == (defer_max_d > 0) and runs["merge"] > 0, runs
     for a, b in zip(ref, got):
       assert torch.equal(a, b), (a.float() - b.float()).abs().max().item()
