@@ -12,14 +12,14 @@ def test_decode_partition_defaults():
   assert ws.partition(1, 8, 32) == (4, 8, 0)
   # many pairs: one wave per unit with page prefetch
   ppp, nparts, algo = ws.partition(512, 8, 9)
-  assert algo == 2 and ppp * nparts >= 9
+  assert algo == 3 and ppp * nparts >= 9  # one wave per unit, page prefetch, non-temporal page loads
 
 
 
 def test_decode_partition_small_batch():
   ws = K.DecodeWorkspace(8, 32, 128, 4096, torch.device("cpu"), algo=-1)
   assert ws.partition(1, 8, 16)[2] == 0 and ws.partition(1, 8, 32)[2] == 0  # the workgroup kernel, split
-  assert ws.partition(8, 8, 8)[2] == 2  # 64 pairs: the wave kernel
+  assert ws.partition(8, 8, 8)[2] == 3  # 64 pairs: the wave kernel
   fixed = K.DecodeWorkspace(8, 32, 128, 4096, torch.device("cpu"), pages_per_part=4, algo=-1)
   assert fixed.partition(1, 8, 16)[2] == 0  # an explicit partition size is honoured
 

@@ -8,11 +8,14 @@ mkdir -p "$O/r6"
 for what in "$@"; do
   case $what in
     bench)  XOT_GEMM_TABLE=$T step r6/bench 400 python -u bench.py --steps 20 --warmup 5 ;;
+    bench_a6) XOT_ATTN_DECODE=6 XOT_GEMM_TABLE=$T step r6/bench_a6 400 python -u bench.py --steps 20 --warmup 5 ;;
+    bench_a3) XOT_ATTN_DECODE=3 XOT_GEMM_TABLE=$T step r6/bench_a3 400 python -u bench.py --steps 20 --warmup 5 ;;
     bench2) XOT_GEMM_TABLE=$T step r6/bench2 400 python -u bench.py --steps 20 --warmup 5 ;;
     bench_w4) cp tools/gpu/tables/decode_w4.json "$O/r6/t_w4.json" && XOT_GEMM_TABLE=$O/r6/t_w4.json step r6/bench_w4 400 python -u bench.py --steps 20 --warmup 5 ;;
     bench_w4gu) cp tools/gpu/tables/decode_w4_gateup.json "$O/r6/t_w4gu.json" && XOT_GEMM_TABLE=$O/r6/t_w4gu.json step r6/bench_w4gu 400 python -u bench.py --steps 20 --warmup 5 ;;
     reduce) step r6/reduce 120 python -u tools/bench_reduce.py ;;
     attn)   step r6/attn 200 python -u tools/bench_attn_b512.py ;;
+    attn_algos) step r6/attn_algos 300 python -u tools/bench_attn_b512.py --algos 1,2,3,5,6 ;;
     attn_small) step r6/attn_small 300 python -u tools/bench_attn_small.py ;;
     b1bench) step r6/b1bench 300 python -u bench.py --model llama-3-8b --batch-per-gpu 1 --steps 64 --warmup 8 ;;
     prof)   XOT_GEMM_TABLE=$T prof r6/prof 600 python3 "$R/bench.py" --steps 6 --warmup 3

@@ -149,9 +149,12 @@ def rope_apply(x: torch.Tensor, pos: torch.Tensor, cos_sin: torch.Tensor, nh: in
 # 0: workgroup per (sequence, KV head, partition), waves split pages + LDS combine
 # 1 / 2: wave per (sequence, KV head, partition), transposed S^T (lane = query head), no LDS;
 #        2 prefetches the next page under the current one
-# 3: 2 with non-temporal K / V loads (measured neutral, profiles/r3/s3/)
+# 3: 2 with non-temporal K / V loads (neutral in round 3, profiles/r3/s3/; on the chunk-major V cache of round 6
+#        the KV stream runs 5-13 % faster in isolation -- B 512: 183.9 vs 193.7 us per layer, B 256 / ctx 1040:
+#        166.6 vs 185.1, B 128 / ctx 2048: 156.2 vs 177.3 -- and the 70B headline step 74.6-74.7 vs 75.4-75.7 ms,
+#        profiles/r6/headline/attn_nt/)
 # -1 (default): 0 below 64 (sequence, KV head) pairs -- few long sequences, where the workgroup
-#        kernel's 4-wave page split needs fewer partitions; else 2 (measured: tools/bench_kernels.py)
+#        kernel's 4-wave page split needs fewer partitions; else 3
 # (4, an 8-wave workgroup over one partition for short tables at small batch, measured 1 % slower at 8B batch 1 --
 #  3.55 vs 3.52 ms, profiles/r3/s3/ -- and was removed in round 6)
 DECODE_ALGO = int(os.environ.get("XOT_ATTN_DECODE", "-1"))
@@ -160,7 +163,7 @@ DECODE_ALGO = int(os.environ.get("XOT_ATTN_DECODE", "-1"))
 def resolve_decode_algo(batch: int, Hkv: int, algo: int | None = None) -> int:
   algo = DECODE_ALGO if algo is None else algo
   if algo < 0:
-    return 0 if batch * Hkv < 64 else 2
+    return 0 if batch * Hkv < 64 else 3
   return algo
 
 
