@@ -19,7 +19,8 @@ def test_decode_partition_defaults():
 def test_decode_partition_small_batch():
   ws = K.DecodeWorkspace(8, 32, 128, 4096, torch.device("cpu"), algo=-1)
   assert ws.partition(1, 8, 16)[2] == 0 and ws.partition(1, 8, 32)[2] == 0  # the workgroup kernel, split
-  assert ws.partition(8, 8, 8)[2] == 3  # 64 pairs: the wave kernel
+  assert ws.partition(8, 8, 8)[2] == 2  # 64 pairs: the wave kernel (cache-resident pages: plain loads)
+  assert K.DecodeWorkspace(64, 32, 128, 8192, torch.device("cpu"), algo=-1).partition(64, 8, 128)[2] == 3  # 2 GB: nt
   fixed = K.DecodeWorkspace(8, 32, 128, 4096, torch.device("cpu"), pages_per_part=4, algo=-1)
   assert fixed.partition(1, 8, 16)[2] == 0  # an explicit partition size is honoured
 

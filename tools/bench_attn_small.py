@@ -1,5 +1,5 @@
 """Decode attention at small batches (latency regime): workgroup kernel (algo 0) vs wave kernel
-(algo 2) over partition sizes, each timed as 20 calls replayed from one HIP graph.
+(algo 2, and 3 with non-temporal page loads) over partition sizes, each timed as 20 calls replayed from one HIP graph.
 
   python tools/bench_attn_small.py [--json out.json]
 """
@@ -78,7 +78,7 @@ def main():
       q = torch.randn(B, H, Dh, device=dev).to(torch.bfloat16)
       out = torch.empty_like(q)
       r = dict(B=B, ctx=ctx)
-      for algo, ppps in ((0, (4, 8, 16, 32)), (2, (2, 4, 8, 16))):
+      for algo, ppps in ((0, (4, 8, 16, 32)), (2, (2, 4, 8, 16)), (3, (2, 4, 8, 16))):
         for ppp in ppps:
           ws = K.DecodeWorkspace(B, H, Dh, pages * 64, dev, pages_per_part=ppp, algo=algo)
           r[f"a{algo}_p{ppp}_r"] = round(graph_us(lambda: K.attn_decode(q, kc, vc, bt, cl, 1 / math.sqrt(Dh), ws, out)), 2)

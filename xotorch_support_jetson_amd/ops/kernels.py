@@ -154,16 +154,24 @@ def rope_apply(x: torch.Tensor, pos: torch.Tensor, cos_sin: torch.Tensor, nh: in
 #        166.6 vs 185.1, B 128 / ctx 2048: 156.2 vs 177.3 -- and the 70B headline step 74.6-74.7 vs 75.4-75.7 ms,
 #        profiles/r6/headline/attn_nt/)
 # -1 (default): 0 below 64 (sequence, KV head) pairs -- few long sequences, where the workgroup
-#        kernel's 4-wave page split needs fewer partitions; else 3
+#        kernel's 4-wave page split needs fewer partitions; else 3 once a layer's K / V pages (batch x block-table
+#        width) outgrow the 256 MB last-level cache, 2 below (B 16 / ctx 530: 15.1 vs 13.5 us, B 64 / ctx 530: 29.3 vs
+#        24.8 with nt; B 16 / ctx 8192: 85.7 vs 97.1, B 64 / ctx 2048: 85.1 vs 97.2; tools/bench_attn_small.py,
+#        profiles/r6/headline/attn_nt/attn_small.log)
 # (4, an 8-wave workgroup over one partition for short tables at small batch, measured 1 % slower at 8B batch 1 --
 #  3.55 vs 3.52 ms, profiles/r3/s3/ -- and was removed in round 6)
 DECODE_ALGO = int(os.environ.get("XOT_ATTN_DECODE", "-1"))
 
 
-def resolve_decode_algo(batch: int, Hkv: int, algo: int | None = None) -> int:
+NT_MIN_KV_BYTES = 256 << 20  # K / V bytes per layer from which the page loads go non-temporal (algo 3)
+
+
+def resolve_decode_algo(batch: int, Hkv: int, algo: int | None = None, kv_bytes: int | None = None) -> int:
   algo = DECODE_ALGO if algo is None else algo
   if algo < 0:
-    return 0 if batch * Hkv < 64 else 3
+    if batch * Hkv < 64:
+      return 0
+    return 3 if kv_bytes is None or kv_bytes >= NT_MIN_KV_BYTES else 2
   return algo
 
 
@@ -192,6 +200,7 @@ class DecodeWorkspace:
     self.algo = DECODE_ALGO if algo is None else algo
     self.max_ctx = max_ctx
     self.Hkv_hint = None
+    self.Dh = Dh
     self.fixed_ppp = pages_per_part
     pages = max(1, -(-max_ctx // PAGE))
     worst = 1
@@ -205,7 +214,7 @@ class DecodeWorkspace:
 
   def partition(self, batch: int, Hkv: int, width_pages: int):
     """(pages per partition, partitions, kernel) for this call."""
-    algo = resolve_decode_algo(batch, Hkv, self.algo)
+    algo = resolve_decode_algo(batch, Hkv, self.algo, kv_bytes=batch * Hkv * width_pages * PAGE * self.Dh * 4)
     ppp = self.fixed_ppp or choose_pages_per_part(batch, Hkv, width_pages * PAGE, algo)
     nparts = max(1, -(-width_pages // ppp))
     if batch * nparts > self.units:
